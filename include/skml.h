@@ -1,0 +1,210 @@
+/*
+ * skml.h -- C ABI of the MI355X SketchML gradient codec (libskml.so, sketchml_amd/lib/).
+ *
+ * This is the drop-in boundary for the reference's `sketch` module hot path.  Every entry point
+ * takes plain pointers and sizes (no torch / no C++ types) so the reference's Java host can bind
+ * it through JNI.  Each function below names the reference interface it
+ * replaces; paths are relative to
+ *   /root/reference/sketch/src/main/java/org/dma/sketchml/sketch/
+ *
+ * Execution model: a context owns one HIP stream on one device.  Encode / decode calls enqueue
+ * device work and return without synchronising; errors detected on the device (NaN input, as
+ * HeapQuantileSketch.update throws, HeapQuantileSketch.java:75-76) are recorded in the payload
+ * header and reported by skml_dense_info() / skml_ctx_sync().
+ *
+ * RNG model: the reference draws compaction bits from an unseeded JVM-global java.util.Random
+ * (QSketchUtils.java:9,47).  Here the stream is java.util.Random(params.seed), consumed in exactly
+ * the order the sequential Java sketch would consume it, so results are reproducible and equal
+ * to the reference algorithm driven by that stream.
+ */
+#ifndef SKML_H
+#define SKML_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes; the JNI shim maps them to the reference's exceptions ---- */
+#define SKML_OK 0
+#define SKML_E_ARG 1   /* SketchMLException / QuantileSketchException (argument checks) */
+#define SKML_E_NAN 2   /* QuantileSketchException("Encounter NaN value") */
+#define SKML_E_ORDER 3 /* SketchMLException("Log for ...") on non-increasing keys */
+#define SKML_E_HIP 4
+#define SKML_E_RCCL 5
+#define SKML_E_OOM 6
+#define SKML_E_STATE 7
+
+#define SKML_DENSE_MAGIC 0x444D4B53u /* "SKMD" */
+#define SKML_MAX_BINS 65536          /* Quantizer.writeObject's short-code limit */
+
+typedef struct skml_ctx skml_ctx;
+
+/* Codec knobs (ml/conf/MLConf.scala:35-42; Quantizer.java:29; GroupedMinMaxSketch.java:35-36;
+ * MinMaxSketch.java:25).  The sketch's k is fixed at 128 (HeapQuantileSketch.java:13). */
+typedef struct skml_params {
+    int32_t bin_num;   /* requested bins, 2..65536, default 256 */
+    int32_t group_num; /* sparse: MinMax groups, default 8 */
+    int32_t row_num;   /* sparse: MinMax rows, default 2 */
+    int32_t dedup;     /* 1: QuantileQuantizer.quantize (Maths.unique); 0: parallelQuantize */
+    double col_ratio;  /* sparse: MinMax columns / group size, default 0.3 */
+    int64_t seed;      /* java.util.Random seed of the sketch's compaction stream */
+    int64_t hash_seed; /* sparse: group g's hashes are drawn from Random(hash_seed + g) */
+} skml_params;
+
+/* Device payload header (little-endian, 64 bytes) followed by double splits[req_bins-1],
+ * padded to 256 bytes, then the packed codes (code_bits per element, LSB-first). */
+typedef struct skml_dense_header {
+    uint32_t magic;
+    int32_t status;    /* SKML_OK or SKML_E_NAN */
+    int64_t n;
+    int32_t bin_num;   /* effective bins (after Maths.unique), Quantizer.binNum */
+    int32_t zero_idx;  /* Quantizer.zeroIdx */
+    int32_t code_bits; /* 1, 2, 4, 8 or 16 */
+    int32_t req_bins;  /* capacity of the splits array + 1 */
+    double min;        /* Quantizer.min (Double.MAX_VALUE-initialised quirk kept) */
+    double max;        /* Quantizer.max (Double.MIN_VALUE-initialised quirk kept) */
+    int64_t codes_offset;
+    int64_t reserved;
+} skml_dense_header;
+
+void skml_params_default(skml_params* p);
+const char* skml_last_error(void); /* thread-local message of the last failing call */
+const char* skml_version(void);
+
+/* Context: one HIP stream on one device.  `hip_stream` is an existing hipStream_t (e.g.
+ * torch.cuda.current_stream().cuda_stream; NULL is the device's default stream) or
+ * SKML_STREAM_OWN, in which case the library creates and owns a non-blocking stream. */
+#define SKML_STREAM_OWN ((void*)(intptr_t)-1)
+int skml_ctx_create(int device, void* hip_stream, skml_ctx** out);
+int skml_ctx_destroy(skml_ctx* ctx);
+int skml_ctx_sync(skml_ctx* ctx);
+int skml_ctx_set_stream(skml_ctx* ctx, void* hip_stream);
+
+/* ---- Dense path: QuantileQuantizer.quantize + Quantizer.getBins/getValues ---- */
+
+/* Bytes of a device payload able to hold n codes for `bin_num` requested bins. */
+size_t skml_dense_payload_bytes(int64_t n, int32_t bin_num);
+
+/* QuantileQuantizer.quantize(double[]) (quantization/QuantileQuantizer.java:27-50) on fp32
+ * input: k=128 quantile sketch (HeapQuantileSketch.update), getQuantiles(bin_num), Maths.unique,
+ * findZeroIdx, then bins[i] = indexOf(x[i]) (Quantizer.java:49-92), packed into the payload.
+ * params->dedup = 0 gives parallelQuantize's no-dedup split table (QuantileQuantizer.java:85).
+ * x_dev and payload_dev are device pointers.  Asynchronous. */
+int skml_dense_encode_f32(skml_ctx* ctx, const float* x_dev, int64_t n, const skml_params* params,
+                          void* payload_dev, size_t payload_cap);
+
+/* Split-injected parity mode: quantise against a caller-given split table (host doubles,
+ * sorted ascending), min and max, exactly as Quantizer.quantizeToBins would.  Asynchronous. */
+int skml_dense_encode_with_splits_f32(skml_ctx* ctx, const float* x_dev, int64_t n,
+                                      const double* splits_host, int32_t nsplits, double min,
+                                      double max, void* payload_dev, size_t payload_cap);
+
+/* DenseVectorCompressor.decompressDense (sample/DenseVectorCompressor.java:84-91):
+ * out[i] = (float) Quantizer.getValues()[bin[i]].  Asynchronous. */
+int skml_dense_decode_f32(skml_ctx* ctx, const void* payload_dev, float* out_dev, int64_t n);
+
+/* Fused decode of P payloads into one sum: out[i] = scale * sum_p values_p[bin_p[i]], the
+ * decode half of Gradient.sum + timesBy(1/P) (ml/gradient/Gradient.scala:44-49,
+ * ml/algorithm/GeneralizedLinearModel.scala:145-150).  payloads_dev points to P payloads laid
+ * out `stride` bytes apart.  Asynchronous. */
+int skml_dense_decode_sum_f32(skml_ctx* ctx, const void* payloads_dev, int32_t P, size_t stride,
+                              float* out_dev, int64_t n, double scale);
+
+/* Quantizer.getBins() (Quantizer.java:168-170): materialise int32 bins on the device. */
+int skml_dense_bins_i32(skml_ctx* ctx, const void* payload_dev, int32_t* bins_dev, int64_t n);
+
+/* Synchronise and read the header + splits (Quantizer.getBinNum/getSplits/getZeroIdx/getMin/
+ * getMax/getN).  splits_host may be NULL; otherwise it receives bin_num-1 doubles.  Returns the
+ * header's status (SKML_E_NAN if the input held a NaN). */
+int skml_dense_info(skml_ctx* ctx, const void* payload_dev, skml_dense_header* hdr_host,
+                    double* splits_host, int32_t splits_cap);
+
+/* Quantizer.timesBy (Quantizer.java:119-124): scale min, max and splits in place. */
+int skml_dense_times_by(skml_ctx* ctx, void* payload_dev, double x);
+
+/* Quantizer.writeObject field stream (Quantizer.java:184-203): big-endian binNum, n,
+ * splits[binNum-1], zeroIdx, min, max, bins.length, then bins as (bin-128) bytes / (bin-32768)
+ * shorts / ints.  Synchronising.  *written receives the byte count (also when buf is NULL). */
+int skml_dense_serialize_ref(skml_ctx* ctx, const void* payload_dev, uint8_t* buf_host,
+                             size_t cap, size_t* written);
+/* Quantizer.readObject (Quantizer.java:205-226) into a device payload.  Synchronising. */
+int skml_dense_deserialize_ref(skml_ctx* ctx, const uint8_t* buf_host, size_t len,
+                               void* payload_dev, size_t payload_cap);
+
+/* ---- Sparse path: SketchGradient.fromSparse / SparseVectorCompressor ---- */
+
+typedef struct skml_sparse skml_sparse; /* library-owned; free with skml_sparse_free */
+
+/* DenseDoubleGradient.countNNZ + toSparse (ml/gradient/DenseDoubleGradient.scala:64-89):
+ * keep |x| > 1e-8 with ascending int32 keys.  keys_dev / vals_dev need dim capacity.
+ * Synchronising (returns nnz through *nnz_out). */
+int skml_sparse_compact_f32(skml_ctx* ctx, const float* dense_dev, int64_t dim, int32_t* keys_dev,
+                            float* vals_dev, int64_t* nnz_out);
+
+/* SparseVectorCompressor.compressSparse (sample/SparseVectorCompressor.java:52-67):
+ * QuantileQuantizer.quantize(values) then GroupedMinMaxSketch.create(keys, bins)
+ * (frequency/GroupedMinMaxSketch.java:51-70): group partition, MinMax insert, DeltaAdaptive key
+ * encoding (binary/DeltaAdaptiveEncoder.java:54-112).  Synchronising. */
+int skml_sparse_encode_kv_f32(skml_ctx* ctx, const int32_t* keys_dev, const float* vals_dev,
+                              int64_t nnz, const skml_params* params, skml_sparse** out);
+/* SketchGradient.fromSparse after toAuto's compaction: compact + encode_kv. */
+int skml_sparse_encode_f32(skml_ctx* ctx, const float* dense_dev, int64_t dim,
+                           const skml_params* params, skml_sparse** out);
+/* GroupedMinMaxSketch.restore + Sort.merge (GroupedMinMaxSketch.java:123-146,
+ * util/Sort.java:362-379) and SparseVectorCompressor.decompressSparse's value lookup
+ * (SparseVectorCompressor.java:118-126).  keys/vals device buffers of nnz capacity. */
+int skml_sparse_decode_f32(skml_ctx* ctx, const skml_sparse* s, int32_t* keys_dev,
+                           float* vals_dev);
+int skml_sparse_nnz(const skml_sparse* s, int64_t* nnz);
+/* Header of the quantizer inside the sparse payload (bins, zero index, splits). */
+int skml_sparse_quant_info(const skml_sparse* s, skml_dense_header* hdr, double* splits_host,
+                           int32_t splits_cap);
+/* Per-group view for parity checks: size, colNum, hash ids, DeltaAdaptive choice and bit
+ * lengths; tables/words are copied to host buffers when non-NULL. */
+typedef struct skml_sparse_group {
+    int32_t size;
+    int32_t col_num;
+    int32_t hash_ids[8];
+    int32_t num_intervals;
+    int32_t flag_kind;
+    int64_t n_flag_bits;
+    int64_t n_delta_bits;
+} skml_sparse_group;
+int skml_sparse_group_info(skml_ctx* ctx, const skml_sparse* s, int32_t g, skml_sparse_group* info,
+                           int32_t* table_host, uint64_t* flag_words_host,
+                           uint64_t* delta_words_host);
+/* GroupedMinMaxSketch.writeObject-ordered field stream (GroupedMinMaxSketch.java:148-158),
+ * without Java object-stream framing; see DESIGN.md for the exact layout. */
+int skml_sparse_serialize(skml_ctx* ctx, const skml_sparse* s, uint8_t* buf_host, size_t cap,
+                          size_t* written);
+int skml_sparse_free(skml_sparse* s);
+
+/* ---- DeltaAdaptiveEncoder as a standalone BinaryEncoder (base/BinaryEncoder.java:6-11) ---- */
+/* encode(int[]): keys strictly increasing (keys[0] >= 0).  Outputs the choice and the two
+ * BitSet word streams (BitSet.toLongArray layout).  Synchronising. */
+int skml_delta_encode(skml_ctx* ctx, const int32_t* keys_dev, int64_t n, int32_t* num_intervals,
+                      int32_t* flag_kind, int64_t* n_flag_bits, int64_t* n_delta_bits,
+                      uint64_t* flag_words_dev, uint64_t* delta_words_dev, int64_t words_cap);
+/* decode(): keys_dev receives n keys.  Asynchronous. */
+int skml_delta_decode(skml_ctx* ctx, int64_t n, int32_t num_intervals, int32_t flag_kind,
+                      const uint64_t* flag_words_dev, int64_t n_flag_words,
+                      const uint64_t* delta_words_dev, int64_t n_delta_words, int32_t* keys_dev);
+
+/* ---- Multi-GPU: RCCL all-gather of payloads over xGMI ---- */
+typedef struct skml_comm skml_comm;
+#define SKML_UNIQUE_ID_BYTES 128
+int skml_comm_unique_id(uint8_t id_out[SKML_UNIQUE_ID_BYTES]);
+int skml_comm_init_rank(skml_ctx* ctx, const uint8_t id[SKML_UNIQUE_ID_BYTES], int32_t nranks,
+                        int32_t rank, skml_comm** out);
+int skml_comm_destroy(skml_comm* comm);
+/* ncclAllGather of `bytes` from each rank's payload into all_dev (nranks * bytes). Async. */
+int skml_allgather(skml_ctx* ctx, skml_comm* comm, const void* payload_dev, size_t bytes,
+                   void* all_dev);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SKML_H */

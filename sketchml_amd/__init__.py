@@ -1,0 +1,16 @@
+"""sketchml_amd -- MI355X-native SketchML gradient codec.
+
+The hot path (k=128 quantile sketch, bucket quantisation, packed codes, sparse key/value
+codec) runs in hand-written gfx950 HIP kernels in lib/libskml.so behind the C ABI of
+include/skml.h; this package mirrors the reference's Java surface over that ABI.
+"""
+from . import _lib
+from .compressor import DenseVectorCompressor
+from .context import Context, alloc_aligned, get_context
+from .exceptions import QuantileSketchException, SketchMLException
+from .quantization import QuantileQuantizer, QuantizationType, Quantizer
+
+__all__ = ["Context", "DenseVectorCompressor", "QuantileQuantizer", "QuantizationType", "Quantizer",
+           "QuantileSketchException", "SketchMLException", "get_context", "alloc_aligned"]
+
+LIB_PATH = _lib.LIB_PATH

@@ -1,0 +1,112 @@
+"""ctypes binding of libskml.so (the C ABI in include/skml.h).
+
+There is no CPU fallback: if the HIP library is missing or cannot be loaded, importing the
+package fails loudly.  The library is built in-tree by __graft_entry__.build()
+(sketchml_amd/csrc/Makefile -> sketchml_amd/lib/libskml.so).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libskml.so")
+
+SKML_OK = 0
+SKML_E_ARG = 1
+SKML_E_NAN = 2
+SKML_E_ORDER = 3
+SKML_E_HIP = 4
+SKML_E_RCCL = 5
+SKML_E_OOM = 6
+SKML_E_STATE = 7
+UNIQUE_ID_BYTES = 128
+SKML_MAX_BINS = 65536
+
+vp = C.c_void_p
+i32 = C.c_int32
+i64 = C.c_int64
+i64p = C.POINTER(C.c_int64)
+i32p = C.POINTER(C.c_int32)
+u8p = C.POINTER(C.c_uint8)
+dblp = C.POINTER(C.c_double)
+szp = C.POINTER(C.c_size_t)
+
+
+class Params(C.Structure):
+    _fields_ = [("bin_num", C.c_int32), ("group_num", C.c_int32), ("row_num", C.c_int32),
+                ("dedup", C.c_int32), ("col_ratio", C.c_double), ("seed", C.c_int64),
+                ("hash_seed", C.c_int64)]
+
+
+class DenseHeader(C.Structure):
+    _fields_ = [("magic", C.c_uint32), ("status", C.c_int32), ("n", C.c_int64),
+                ("bin_num", C.c_int32), ("zero_idx", C.c_int32), ("code_bits", C.c_int32),
+                ("req_bins", C.c_int32), ("min", C.c_double), ("max", C.c_double),
+                ("codes_offset", C.c_int64), ("reserved", C.c_int64)]
+
+
+class SparseGroup(C.Structure):
+    _fields_ = [("size", C.c_int32), ("col_num", C.c_int32), ("hash_ids", C.c_int32 * 8),
+                ("num_intervals", C.c_int32), ("flag_kind", C.c_int32),
+                ("n_flag_bits", C.c_int64), ("n_delta_bits", C.c_int64)]
+
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "skml_params_default": (None, [C.POINTER(Params)]),
+    "skml_last_error": (C.c_char_p, []),
+    "skml_version": (C.c_char_p, []),
+    "skml_ctx_create": (C.c_int, [C.c_int, vp, C.POINTER(vp)]),
+    "skml_ctx_destroy": (C.c_int, [vp]),
+    "skml_ctx_sync": (C.c_int, [vp]),
+    "skml_ctx_set_stream": (C.c_int, [vp, vp]),
+    "skml_dense_payload_bytes": (C.c_size_t, [i64, i32]),
+    "skml_dense_encode_f32": (C.c_int, [vp, vp, i64, C.POINTER(Params), vp, C.c_size_t]),
+    "skml_dense_encode_with_splits_f32": (C.c_int, [vp, vp, i64, dblp, i32, C.c_double, C.c_double,
+                                                    vp, C.c_size_t]),
+    "skml_dense_decode_f32": (C.c_int, [vp, vp, vp, i64]),
+    "skml_dense_decode_sum_f32": (C.c_int, [vp, vp, i32, C.c_size_t, vp, i64, C.c_double]),
+    "skml_dense_bins_i32": (C.c_int, [vp, vp, vp, i64]),
+    "skml_dense_info": (C.c_int, [vp, vp, C.POINTER(DenseHeader), dblp, i32]),
+    "skml_dense_times_by": (C.c_int, [vp, vp, C.c_double]),
+    "skml_dense_serialize_ref": (C.c_int, [vp, vp, u8p, C.c_size_t, szp]),
+    "skml_dense_deserialize_ref": (C.c_int, [vp, u8p, C.c_size_t, vp, C.c_size_t]),
+    "skml_sparse_compact_f32": (C.c_int, [vp, vp, i64, vp, vp, i64p]),
+    "skml_sparse_encode_kv_f32": (C.c_int, [vp, vp, vp, i64, C.POINTER(Params), C.POINTER(vp)]),
+    "skml_sparse_encode_f32": (C.c_int, [vp, vp, i64, C.POINTER(Params), C.POINTER(vp)]),
+    "skml_sparse_decode_f32": (C.c_int, [vp, vp, vp, vp]),
+    "skml_sparse_nnz": (C.c_int, [vp, i64p]),
+    "skml_sparse_quant_info": (C.c_int, [vp, C.POINTER(DenseHeader), dblp, i32]),
+    "skml_sparse_group_info": (C.c_int, [vp, vp, i32, C.POINTER(SparseGroup), i32p,
+                                         C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "skml_sparse_serialize": (C.c_int, [vp, vp, u8p, C.c_size_t, szp]),
+    "skml_sparse_free": (C.c_int, [vp]),
+    "skml_delta_encode": (C.c_int, [vp, vp, i64, i32p, i32p, i64p, i64p, vp, vp, i64]),
+    "skml_delta_decode": (C.c_int, [vp, i64, i32, i32, vp, i64, vp, i64, vp]),
+    "skml_comm_unique_id": (C.c_int, [u8p]),
+    "skml_comm_init_rank": (C.c_int, [vp, u8p, i32, i32, C.POINTER(vp)]),
+    "skml_comm_destroy": (C.c_int, [vp]),
+    "skml_allgather": (C.c_int, [vp, vp, vp, C.c_size_t, vp]),
+}
+
+EXPORTED = tuple(_SIGS)
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"sketchml_amd: HIP library not built ({LIB_PATH}); run "
+                          f"`python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)  # AttributeError here == ABI drift vs include/skml.h
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def last_error() -> str:
+    return (lib.skml_last_error() or b"").decode("utf-8", "replace")

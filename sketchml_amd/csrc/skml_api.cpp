@@ -1,0 +1,571 @@
+// skml_api.cpp -- host side of the C ABI (include/skml.h): contexts, workspace, launch planning
+// for the dense codec, Java-layout (de)serialisation, RCCL all-gather.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "skml_internal.h"
+#include "skml_sparse.h"
+
+using namespace skml;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                       \
+    do {                                                                                    \
+        hipError_t e_ = (expr);                                                             \
+        if (e_ != hipSuccess)                                                               \
+            return fail(SKML_E_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                        __FILE__, __LINE__);                                                \
+    } while (0)
+
+}  // namespace
+
+// =============================================================================================
+// context
+// =============================================================================================
+struct skml_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    uint64_t* jump_tab = nullptr;  // device, 4 x 256 x (A^m, C_m)
+    // dense workspace (grow-only)
+    void* ws = nullptr;
+    size_t ws_cap = 0;
+    // rank table cache for (n, bin_num): HeapQuantileSketch.getQuantiles' curFrac ranks
+    int64_t* ranks = nullptr;
+    size_t ranks_cap = 0;
+    int64_t ranks_n = -1;
+    int ranks_bins = -1;
+    // staging
+    void* stage = nullptr;
+    size_t stage_cap = 0;
+    SparseWorkspace sparse;
+};
+
+namespace {
+
+struct Workspace {
+    LeafPartial* part;
+    float* nodes6;
+    float* roots;
+    float* upA;
+    float* upB;
+    double* raw;
+};
+
+size_t ws_layout(int64_t chunks, Workspace* w, char* base) {
+    const int64_t nwg = (chunks + kLeafChunks - 1) / kLeafChunks;
+    const int64_t full = chunks / kLeafChunks;
+    const int64_t up = (full >> kMergeGroupLog) + 2 * kMaxLevels + 8;
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        size_t o = off;
+        off = align_up(off + bytes, 256);
+        return base ? (void*)(base + o) : nullptr;
+    };
+    Workspace t;
+    t.part = (LeafPartial*)take(sizeof(LeafPartial) * (size_t)(nwg + 1));
+    t.nodes6 = (float*)take(sizeof(float) * kK * (size_t)(full + 1));
+    t.roots = (float*)take(sizeof(float) * kK * kMaxLevels);
+    t.upA = (float*)take(sizeof(float) * kK * (size_t)up);
+    t.upB = (float*)take(sizeof(float) * kK * (size_t)up);
+    t.raw = (double*)take(sizeof(double) * SKML_MAX_BINS);
+    if (w) *w = t;
+    return off;
+}
+
+int ensure_ws(skml_ctx* ctx, int64_t chunks, Workspace* w) {
+    const size_t need = ws_layout(chunks, nullptr, nullptr);
+    if (need > ctx->ws_cap) {
+        if (ctx->ws) HIP_TRY(hipFree(ctx->ws));
+        ctx->ws = nullptr;
+        size_t cap = need + need / 4;
+        HIP_TRY(hipMalloc(&ctx->ws, cap));
+        ctx->ws_cap = cap;
+    }
+    ws_layout(chunks, w, (char*)ctx->ws);
+    return SKML_OK;
+}
+
+int ensure_stage(skml_ctx* ctx, size_t bytes) {
+    if (bytes <= ctx->stage_cap) return SKML_OK;
+    if (ctx->stage) HIP_TRY(hipFree(ctx->stage));
+    ctx->stage = nullptr;
+    HIP_TRY(hipMalloc(&ctx->stage, bytes));
+    ctx->stage_cap = bytes;
+    return SKML_OK;
+}
+
+// getQuantiles(int) ranks: curFrac accumulated by repeated `+= 1/B` in double
+// (HeapQuantileSketch.java:304-321); depends only on (n, B) so it is planned on the host.
+int ensure_ranks(skml_ctx* ctx, int64_t n, int bins) {
+    if (ctx->ranks_n == n && ctx->ranks_bins == bins) return SKML_OK;
+    const size_t cnt = (size_t)(bins - 1);
+    if (cnt > ctx->ranks_cap) {
+        if (ctx->ranks) HIP_TRY(hipFree(ctx->ranks));
+        ctx->ranks = nullptr;
+        HIP_TRY(hipMalloc(&ctx->ranks, sizeof(int64_t) * (cnt + 1)));
+        ctx->ranks_cap = cnt;
+    }
+    std::vector<int64_t> r(cnt + 1, 0);
+    volatile double frac = 1.0 / bins;  // volatile: keep the JVM's sequential double rounding
+    const double step = 1.0 / bins;
+    for (size_t i = 0; i < cnt; i++) {
+        int64_t rank = (int64_t)((double)n * frac);
+        if (rank > n - 1) rank = n - 1;
+        r[i] = rank;
+        frac = frac + step;
+    }
+    HIP_TRY(hipMemcpyAsync(ctx->ranks, r.data(), sizeof(int64_t) * cnt, hipMemcpyHostToDevice,
+                           ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    ctx->ranks_n = n;
+    ctx->ranks_bins = bins;
+    return SKML_OK;
+}
+
+void build_jump_table(std::vector<uint64_t>& tab) {
+    tab.assign(4 * 256 * 2, 0);
+    uint64_t base_a = kLcgMult, base_c = kLcgAdd;  // J_1
+    for (int lvl = 0; lvl < 4; lvl++) {
+        uint64_t a = 1, c = 0;  // J_0
+        for (int b = 0; b < 256; b++) {
+            tab[(lvl * 256 + b) * 2] = a;
+            tab[(lvl * 256 + b) * 2 + 1] = c;
+            // J_{(b+1) * 256^lvl} = J_base o J_{b * 256^lvl}
+            c = (base_a * c + base_c) & kLcgMask;
+            a = (base_a * a) & kLcgMask;
+        }
+        // next base = J_base^256
+        uint64_t na = 1, nc = 0;
+        for (int i = 0; i < 256; i++) {
+            nc = (base_a * nc + base_c) & kLcgMask;
+            na = (base_a * na) & kLcgMask;
+        }
+        base_a = na;
+        base_c = nc;
+    }
+}
+
+// Plan the upper merge passes for the trees of bits >= 6 of the chunk count.
+struct Tree {
+    int level;           // tree level l (bit of chunks)
+    int m;               // remaining log2 node count
+    int cur_level;       // level of its current nodes
+    int64_t src;         // first node index in the current src buffer
+    int64_t chunk_base;  // first chunk
+};
+
+bool valid_payload_ptr(const void* p) { return p && (((uintptr_t)p) % 256 == 0); }
+
+}  // namespace
+
+extern "C" {
+
+void skml_params_default(skml_params* p) {
+    p->bin_num = 256;
+    p->group_num = 8;
+    p->row_num = 2;
+    p->dedup = 1;
+    p->col_ratio = 0.3;
+    p->seed = 0;
+    p->hash_seed = 0;
+}
+
+const char* skml_last_error(void) { return g_err.c_str(); }
+const char* skml_version(void) { return "skml-mi355x 0.1 (gfx950)"; }
+
+int skml_ctx_create(int device, void* hip_stream, skml_ctx** out) {
+    if (!out) return fail(SKML_E_ARG, "out is NULL");
+    *out = nullptr;
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(SKML_E_ARG, "device %d of %d", device, ndev);
+    HIP_TRY(hipSetDevice(device));
+    skml_ctx* c = new skml_ctx();
+    c->device = device;
+    if (hip_stream != SKML_STREAM_OWN) {
+        c->stream = (hipStream_t)hip_stream;
+    } else {
+        hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+        if (e != hipSuccess) {
+            delete c;
+            return fail(SKML_E_HIP, "hipStreamCreate: %s", hipGetErrorString(e));
+        }
+        c->own_stream = true;
+    }
+    std::vector<uint64_t> tab;
+    build_jump_table(tab);
+    hipError_t e = hipMalloc(&c->jump_tab, tab.size() * sizeof(uint64_t));
+    if (e == hipSuccess)
+        e = hipMemcpy(c->jump_tab, tab.data(), tab.size() * sizeof(uint64_t), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        skml_ctx_destroy(c);
+        return fail(SKML_E_HIP, "jump table: %s", hipGetErrorString(e));
+    }
+    *out = c;
+    return SKML_OK;
+}
+
+int skml_ctx_destroy(skml_ctx* c) {
+    if (!c) return SKML_OK;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->jump_tab) (void)hipFree(c->jump_tab);
+    if (c->ws) (void)hipFree(c->ws);
+    if (c->ranks) (void)hipFree(c->ranks);
+    if (c->stage) (void)hipFree(c->stage);
+    sparse_ws_free(&c->sparse);
+    if (c->own_stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return SKML_OK;
+}
+
+int skml_ctx_sync(skml_ctx* c) {
+    if (!c) return fail(SKML_E_ARG, "ctx is NULL");
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return SKML_OK;
+}
+
+int skml_ctx_set_stream(skml_ctx* c, void* hip_stream) {
+    if (!c) return fail(SKML_E_ARG, "ctx is NULL");
+    if (c->own_stream) {
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        HIP_TRY(hipStreamDestroy(c->stream));
+        c->own_stream = false;
+    }
+    c->stream = (hipStream_t)hip_stream;
+    return SKML_OK;
+}
+
+size_t skml_dense_payload_bytes(int64_t n, int32_t bin_num) {
+    if (n < 0 || bin_num < 2 || bin_num > SKML_MAX_BINS) return 0;
+    const size_t rounded = align_up((size_t)n, 1024);
+    return dense_codes_offset(bin_num) + align_up(rounded * (size_t)code_bits_for(bin_num) / 8, 256);
+}
+
+static int check_dense_args(skml_ctx* c, const float* x, int64_t n, int bins, const void* payload,
+                            size_t cap) {
+    if (!c) return fail(SKML_E_ARG, "ctx is NULL");
+    if (n < 0 || n > 0x7FFFFFFFLL) return fail(SKML_E_ARG, "n=%lld outside Java int range", (long long)n);
+    if (bins < 2 || bins > SKML_MAX_BINS)
+        return fail(SKML_E_ARG, "Invalid partition number: %d", bins);  // QSketchUtils.java:40-43
+    if (n > 0 && (!x || ((uintptr_t)x) % 16 != 0))
+        return fail(SKML_E_ARG, "input must be a 16-byte aligned device pointer");
+    if (!valid_payload_ptr(payload)) return fail(SKML_E_ARG, "payload must be 256-byte aligned");
+    if (cap < skml_dense_payload_bytes(n, bins))
+        return fail(SKML_E_ARG, "payload capacity %zu < %zu", cap, skml_dense_payload_bytes(n, bins));
+    return SKML_OK;
+}
+
+int skml_dense_encode_f32(skml_ctx* c, const float* x, int64_t n, const skml_params* p,
+                          void* payload, size_t cap) {
+    skml_params def;
+    if (!p) {
+        skml_params_default(&def);
+        p = &def;
+    }
+    int st = check_dense_args(c, x, n, p->bin_num, payload, cap);
+    if (st) return st;
+    HIP_TRY(hipSetDevice(c->device));
+    const int64_t chunks = n / kChunk;
+    Workspace w;
+    if ((st = ensure_ws(c, chunks, &w))) return st;
+    if ((st = ensure_ranks(c, n, p->bin_num))) return st;
+    const uint64_t s0 = ((uint64_t)p->seed ^ kLcgMult) & kLcgMask;
+    const int64_t nwg = (chunks + kLeafChunks - 1) / kLeafChunks;
+
+    if (chunks > 0) {
+        HIP_TRY(launch_leaf(c->stream, x, chunks, s0, c->jump_tab, w.part, w.nodes6, w.roots));
+        // ---- upper trees: bits l >= 7 of chunks (bit 6 is a single leaf-workgroup node) ----
+        std::vector<Tree> trees;
+        for (int l = kMaxLevels - 1; l > kLeafTopLevel; l--) {
+            if (!((chunks >> l) & 1)) continue;
+            Tree t;
+            t.level = l;
+            t.m = l - kLeafTopLevel;
+            t.cur_level = kLeafTopLevel;
+            t.chunk_base = (chunks >> (l + 1)) << (l + 1);
+            t.src = t.chunk_base >> kLeafTopLevel;
+            trees.push_back(t);
+        }
+        const float* src = w.nodes6;
+        float* dst = w.upA;
+        while (true) {
+            MergePass pass;
+            std::memset(&pass, 0, sizeof(pass));
+            int64_t dst_off = 0;
+            int wg = 0;
+            for (auto& t : trees) {
+                if (t.m == 0) continue;
+                const int g = t.m < kMergeGroupLog ? t.m : kMergeGroupLog;
+                MergeJob& j = pass.job[pass.njobs];
+                j.src_node = t.src;
+                j.dst_node = dst_off;
+                j.chunk_base = t.chunk_base;
+                j.level_in = t.cur_level;
+                j.group_log = g;
+                j.groups = 1 << (t.m - g);
+                j.root_level = (t.m - g == 0) ? t.level : -1;
+                pass.wg_prefix[pass.njobs] = wg;
+                wg += j.groups;
+                pass.njobs++;
+                t.src = dst_off;
+                dst_off += j.groups;
+                t.m -= g;
+                t.cur_level += g;
+            }
+            if (pass.njobs == 0) break;
+            pass.wg_prefix[pass.njobs] = wg;
+            HIP_TRY(launch_merge_pass(c->stream, pass, src, dst, w.roots, s0, c->jump_tab));
+            src = dst;
+            dst = (dst == w.upA) ? w.upB : w.upA;
+        }
+    }
+    HIP_TRY(launch_summary(c->stream, x, n, w.part, nwg, w.roots, c->ranks, p->bin_num, p->dedup ? 1 : 0,
+                           payload, w.raw));
+    HIP_TRY(launch_quantize(c->stream, x, n, payload));
+    return SKML_OK;
+}
+
+int skml_dense_encode_with_splits_f32(skml_ctx* c, const float* x, int64_t n, const double* splits,
+                                      int32_t nsplits, double mn, double mx, void* payload,
+                                      size_t cap) {
+    int st = check_dense_args(c, x, n, nsplits + 1, payload, cap);
+    if (st) return st;
+    if (!splits) return fail(SKML_E_ARG, "splits is NULL");
+    for (int i = 1; i < nsplits; i++)
+        if (!(splits[i - 1] <= splits[i])) return fail(SKML_E_ARG, "splits must be ascending");
+    HIP_TRY(hipSetDevice(c->device));
+    if ((st = ensure_stage(c, sizeof(double) * (size_t)nsplits))) return st;
+    HIP_TRY(hipMemcpyAsync(c->stage, splits, sizeof(double) * (size_t)nsplits, hipMemcpyHostToDevice,
+                           c->stream));
+    HIP_TRY(launch_set_splits(c->stream, payload, n, (const double*)c->stage, nsplits, mn, mx, nsplits + 1));
+    HIP_TRY(launch_quantize(c->stream, x, n, payload));
+    HIP_TRY(hipStreamSynchronize(c->stream));  // the staged splits are reused by later calls
+    return SKML_OK;
+}
+
+int skml_dense_decode_f32(skml_ctx* c, const void* payload, float* out, int64_t n) {
+    if (!c || !valid_payload_ptr(payload) || (n > 0 && (!out || ((uintptr_t)out) % 16)))
+        return fail(SKML_E_ARG, "bad decode arguments");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(launch_decode(c->stream, payload, out, n));
+    return SKML_OK;
+}
+
+int skml_dense_decode_sum_f32(skml_ctx* c, const void* payloads, int32_t P, size_t stride, float* out,
+                              int64_t n, double scale) {
+    if (!c || !valid_payload_ptr(payloads) || stride % 256 || P < 1 || P > 16 ||
+        (n > 0 && (!out || ((uintptr_t)out) % 16)))
+        return fail(SKML_E_ARG, "bad decode_sum arguments (P in [1,16], 256-B aligned payloads)");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(launch_decode_sum(c->stream, payloads, P, stride, out, n, scale));
+    return SKML_OK;
+}
+
+int skml_dense_bins_i32(skml_ctx* c, const void* payload, int32_t* bins, int64_t n) {
+    if (!c || !valid_payload_ptr(payload) || (n > 0 && !bins)) return fail(SKML_E_ARG, "bad arguments");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(launch_bins(c->stream, payload, bins, n));
+    return SKML_OK;
+}
+
+int skml_dense_info(skml_ctx* c, const void* payload, skml_dense_header* hdr, double* splits,
+                    int32_t splits_cap) {
+    if (!c || !valid_payload_ptr(payload) || !hdr) return fail(SKML_E_ARG, "bad arguments");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipMemcpyAsync(hdr, payload, sizeof(*hdr), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (hdr->magic != SKML_DENSE_MAGIC) return fail(SKML_E_STATE, "not a dense payload");
+    if (splits && hdr->status == SKML_OK) {
+        const int ns = hdr->bin_num - 1;
+        if (ns > splits_cap) return fail(SKML_E_ARG, "splits capacity %d < %d", splits_cap, ns);
+        HIP_TRY(hipMemcpyAsync(splits, (const char*)payload + kHeaderBytes, sizeof(double) * ns,
+                               hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
+    if (hdr->status == SKML_E_NAN) return fail(SKML_E_NAN, "Encounter NaN value");
+    return hdr->status;
+}
+
+int skml_dense_times_by(skml_ctx* c, void* payload, double x) {
+    if (!c || !valid_payload_ptr(payload)) return fail(SKML_E_ARG, "bad arguments");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(launch_times_by(c->stream, payload, x));
+    return SKML_OK;
+}
+
+static void put_be(uint8_t* p, uint64_t v, int nb) {
+    for (int i = nb - 1; i >= 0; i--) {
+        p[i] = (uint8_t)(v & 0xFF);
+        v >>= 8;
+    }
+}
+static uint64_t get_be(const uint8_t* p, int nb) {
+    uint64_t v = 0;
+    for (int i = 0; i < nb; i++) v = (v << 8) | p[i];
+    return v;
+}
+static uint64_t dbl_bits(double d) {
+    uint64_t u;
+    std::memcpy(&u, &d, 8);
+    return u;
+}
+
+int skml_dense_serialize_ref(skml_ctx* c, const void* payload, uint8_t* buf, size_t cap, size_t* written) {
+    skml_dense_header h;
+    std::vector<double> sp(SKML_MAX_BINS);
+    int st = skml_dense_info(c, payload, &h, sp.data(), SKML_MAX_BINS);
+    if (st) return st;
+    const int B = h.bin_num, ns = B - 1;
+    const int width = B <= 256 ? 1 : (B <= 65536 ? 2 : 4);
+    const size_t head = 4 + 4 + 8 * (size_t)ns + 4 + 8 + 8 + 4;
+    const size_t total = head + (size_t)width * (size_t)h.n;
+    if (written) *written = total;
+    if (!buf) return SKML_OK;
+    if (cap < total) return fail(SKML_E_ARG, "buffer capacity %zu < %zu", cap, total);
+    uint8_t* p = buf;
+    put_be(p, (uint32_t)B, 4); p += 4;
+    put_be(p, (uint32_t)h.n, 4); p += 4;
+    for (int i = 0; i < ns; i++) { put_be(p, dbl_bits(sp[i]), 8); p += 8; }
+    put_be(p, (uint32_t)h.zero_idx, 4); p += 4;
+    put_be(p, dbl_bits(h.min), 8); p += 8;
+    put_be(p, dbl_bits(h.max), 8); p += 8;
+    put_be(p, (uint32_t)h.n, 4); p += 4;
+    if (h.n > 0) {
+        if ((st = ensure_stage(c, (size_t)width * (size_t)h.n))) return st;
+        HIP_TRY(launch_ref_body(c->stream, payload, (uint8_t*)c->stage, h.n, width));
+        HIP_TRY(hipMemcpyAsync(p, c->stage, (size_t)width * (size_t)h.n, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
+    return SKML_OK;
+}
+
+int skml_dense_deserialize_ref(skml_ctx* c, const uint8_t* buf, size_t len, void* payload, size_t cap) {
+    if (!c || !buf || !valid_payload_ptr(payload)) return fail(SKML_E_ARG, "bad arguments");
+    if (len < 8) return fail(SKML_E_ARG, "truncated stream");
+    const uint8_t* p = buf;
+    const int32_t B = (int32_t)get_be(p, 4);
+    const int32_t n = (int32_t)get_be(p + 4, 4);
+    if (B < 2 || B > SKML_MAX_BINS || n < 0) return fail(SKML_E_ARG, "bad binNum %d / n %d", B, n);
+    const int ns = B - 1;
+    const int width = B <= 256 ? 1 : (B <= 65536 ? 2 : 4);
+    const size_t head = 4 + 4 + 8 * (size_t)ns + 4 + 8 + 8 + 4;
+    if (len < head) return fail(SKML_E_ARG, "truncated stream");
+    p += 8;
+    std::vector<double> sp(ns);
+    for (int i = 0; i < ns; i++) {
+        uint64_t u = get_be(p, 8);
+        std::memcpy(&sp[i], &u, 8);
+        p += 8;
+    }
+    skml_dense_header h;
+    std::memset(&h, 0, sizeof(h));
+    h.magic = SKML_DENSE_MAGIC;
+    h.status = SKML_OK;
+    h.zero_idx = (int32_t)get_be(p, 4); p += 4;
+    uint64_t u = get_be(p, 8); std::memcpy(&h.min, &u, 8); p += 8;
+    u = get_be(p, 8); std::memcpy(&h.max, &u, 8); p += 8;
+    const int32_t nb = (int32_t)get_be(p, 4); p += 4;
+    if (nb != n || len < head + (size_t)width * (size_t)n) return fail(SKML_E_ARG, "truncated bins");
+    if (cap < skml_dense_payload_bytes(n, B)) return fail(SKML_E_ARG, "payload too small");
+    h.n = n;
+    h.bin_num = B;
+    h.code_bits = code_bits_for(B);
+    h.req_bins = B;
+    h.codes_offset = (int64_t)dense_codes_offset(B);
+    HIP_TRY(hipSetDevice(c->device));
+    int st = ensure_stage(c, (size_t)width * (size_t)n + 16);
+    if (st) return st;
+    HIP_TRY(hipMemcpyAsync(payload, &h, sizeof(h), hipMemcpyHostToDevice, c->stream));
+    if (ns) HIP_TRY(hipMemcpyAsync((char*)payload + kHeaderBytes, sp.data(), sizeof(double) * ns,
+                                   hipMemcpyHostToDevice, c->stream));
+    if (n) {
+        HIP_TRY(hipMemcpyAsync(c->stage, p, (size_t)width * (size_t)n, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(launch_pack_ref(c->stream, (const uint8_t*)c->stage, width, n, payload));
+    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return SKML_OK;
+}
+
+// =============================================================================================
+// RCCL all-gather of payloads over xGMI
+// =============================================================================================
+struct skml_comm {
+    ncclComm_t comm;
+    int nranks, rank;
+};
+
+int skml_comm_unique_id(uint8_t id_out[SKML_UNIQUE_ID_BYTES]) {
+    static_assert(sizeof(ncclUniqueId) <= SKML_UNIQUE_ID_BYTES, "unique id size");
+    ncclUniqueId id;
+    ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) return fail(SKML_E_RCCL, "ncclGetUniqueId: %s", ncclGetErrorString(r));
+    std::memset(id_out, 0, SKML_UNIQUE_ID_BYTES);
+    std::memcpy(id_out, &id, sizeof(id));
+    return SKML_OK;
+}
+
+int skml_comm_init_rank(skml_ctx* c, const uint8_t id_in[SKML_UNIQUE_ID_BYTES], int32_t nranks,
+                        int32_t rank, skml_comm** out) {
+    if (!c || !out || nranks < 1 || rank < 0 || rank >= nranks) return fail(SKML_E_ARG, "bad comm args");
+    HIP_TRY(hipSetDevice(c->device));
+    ncclUniqueId id;
+    std::memcpy(&id, id_in, sizeof(id));
+    skml_comm* cm = new skml_comm();
+    ncclResult_t r = ncclCommInitRank(&cm->comm, nranks, id, rank);
+    if (r != ncclSuccess) {
+        delete cm;
+        return fail(SKML_E_RCCL, "ncclCommInitRank: %s", ncclGetErrorString(r));
+    }
+    cm->nranks = nranks;
+    cm->rank = rank;
+    *out = cm;
+    return SKML_OK;
+}
+
+int skml_comm_destroy(skml_comm* cm) {
+    if (!cm) return SKML_OK;
+    ncclCommDestroy(cm->comm);
+    delete cm;
+    return SKML_OK;
+}
+
+int skml_allgather(skml_ctx* c, skml_comm* cm, const void* payload, size_t bytes, void* all) {
+    if (!c || !cm || !payload || !all) return fail(SKML_E_ARG, "bad allgather arguments");
+    HIP_TRY(hipSetDevice(c->device));
+    ncclResult_t r = ncclAllGather(payload, all, bytes, ncclUint8, cm->comm, c->stream);
+    if (r != ncclSuccess) return fail(SKML_E_RCCL, "ncclAllGather: %s", ncclGetErrorString(r));
+    return SKML_OK;
+}
+
+}  // extern "C"
+
+// ---- accessors used by the sparse translation unit ----
+namespace skml {
+hipStream_t ctx_stream(skml_ctx* c) { return c->stream; }
+int ctx_device(skml_ctx* c) { return c->device; }
+SparseWorkspace* ctx_sparse_ws(skml_ctx* c) { return &c->sparse; }
+int set_error(int code, const char* msg) { return fail(code, "%s", msg); }
+}  // namespace skml

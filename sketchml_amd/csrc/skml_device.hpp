@@ -1,0 +1,212 @@
+// skml_device.hpp -- device helpers shared by the CDNA4 kernels (gfx950, wave64).
+//
+// Keys: fp32 values are sorted as "total-order keys" (sign-magnitude -> unsigned), which is
+// exactly the order java.util.Arrays.sort(double[]) uses (-0.0 before 0.0; NaN never sorted:
+// HeapQuantileSketch.update rejects it, HeapQuantileSketch.java:75-76).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "skml_internal.h"
+
+namespace skml {
+
+__device__ __forceinline__ uint32_t f2key(uint32_t b) {
+    return b ^ ((uint32_t)((int32_t)b >> 31) | 0x80000000u);
+}
+__device__ __forceinline__ uint32_t key2f(uint32_t k) {
+    return k ^ ((k >> 31) ? 0x80000000u : 0xFFFFFFFFu);
+}
+__device__ __forceinline__ bool is_nan_bits(uint32_t b) { return (b & 0x7FFFFFFFu) > 0x7F800000u; }
+
+// ------------------------------------------------------------------------------------------
+// Cross-lane exchange: value held by lane ^ M.  Picks the cheapest gfx950 primitive per mask:
+// DPP quad_perm / row_mirror / row_half_mirror / row_ror:8 when the pattern stays inside a
+// 16-lane row, ds_swizzle (bit mode) inside 32 lanes, ds_bpermute otherwise.
+// ------------------------------------------------------------------------------------------
+template <int M>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t v) {
+    int x = (int)v;
+    if constexpr (M == 1) return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, true);
+    else if constexpr (M == 2) return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, true);
+    else if constexpr (M == 3) return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0x1B, 0xF, 0xF, true);
+    else if constexpr (M == 7) return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0x141, 0xF, 0xF, true);
+    else if constexpr (M == 15) return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0x140, 0xF, 0xF, true);
+    else if constexpr (M == 8) return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0x128, 0xF, 0xF, true);
+    else if constexpr (M < 32) return (uint32_t)__builtin_amdgcn_ds_swizzle(x, (M << 10) | 0x1F);
+    else {
+        int lane = (int)__lane_id();
+        return (uint32_t)__builtin_amdgcn_ds_bpermute((lane ^ M) << 2, x);
+    }
+}
+
+__device__ __forceinline__ void ce(uint32_t& a, uint32_t& b) {
+    uint32_t lo = a < b ? a : b;
+    uint32_t hi = a < b ? b : a;
+    a = lo;
+    b = hi;
+}
+
+// In-register bitonic sort of R keys, ascending, all comparators in "flip" form.
+template <int R>
+__device__ __forceinline__ void sort_regs(uint32_t (&v)[R]) {
+#pragma unroll
+    for (int k = 2; k <= R; k <<= 1) {
+#pragma unroll
+        for (int i = 0; i < R; i++) {
+            int j = i ^ (k - 1);
+            if (j > i) ce(v[i], v[j]);
+        }
+#pragma unroll
+        for (int d = k >> 2; d >= 1; d >>= 1) {
+#pragma unroll
+            for (int i = 0; i < R; i++) {
+                int j = i ^ d;
+                if (j > i) ce(v[i], v[j]);
+            }
+        }
+    }
+}
+
+template <int R>
+__device__ __forceinline__ void halfclean_regs(uint32_t (&v)[R]) {
+#pragma unroll
+    for (int d = R >> 1; d >= 1; d >>= 1) {
+#pragma unroll
+        for (int i = 0; i < R; i++) {
+            int j = i ^ d;
+            if (j > i) ce(v[i], v[j]);
+        }
+    }
+}
+
+// Flip stage across a block of (M+1) lanes: element (lane, r) meets (lane^M, R-1-r).
+template <int R, int M>
+__device__ __forceinline__ void flip_lanes(uint32_t (&v)[R], int lane) {
+    const bool lower = (lane & ((M + 1) >> 1)) == 0;
+#pragma unroll
+    for (int r = 0; r < R / 2; r++) {
+        uint32_t pa = lane_xor<M>(v[R - 1 - r]);
+        uint32_t pb = lane_xor<M>(v[r]);
+        uint32_t a = v[r], b = v[R - 1 - r];
+        v[r] = lower ? (a < pa ? a : pa) : (a < pa ? pa : a);
+        v[R - 1 - r] = lower ? (b < pb ? b : pb) : (b < pb ? pb : b);
+    }
+}
+
+template <int R, int D>
+__device__ __forceinline__ void halfclean_lanes(uint32_t (&v)[R], int lane) {
+    const bool lower = (lane & D) == 0;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        uint32_t p = lane_xor<D>(v[r]);
+        uint32_t a = v[r];
+        v[r] = lower ? (a < p ? a : p) : (a < p ? p : a);
+    }
+}
+
+template <int R, int D>
+__device__ __forceinline__ void halfclean_lanes_down(uint32_t (&v)[R], int lane) {
+    if constexpr (D >= 1) {
+        halfclean_lanes<R, D>(v, lane);
+        halfclean_lanes_down<R, D / 2>(v, lane);
+    }
+}
+
+// Bitonic merge of a group of G = 256/R lanes holding two sorted 128-runs (lower G/2 lanes and
+// upper G/2 lanes, positions lane_in_group*R + r) into one sorted 256-run.
+template <int R>
+__device__ __forceinline__ void merge_group(uint32_t (&v)[R], int lane) {
+    constexpr int G = 256 / R;
+    flip_lanes<R, G - 1>(v, lane);
+    halfclean_lanes_down<R, G / 4>(v, lane);
+    halfclean_regs<R>(v);
+}
+
+// Sort 256 keys held by a group of G = 256/R lanes (any initial placement).
+template <int R, int S>
+__device__ __forceinline__ void sort_lanes_from(uint32_t (&v)[R], int lane) {
+    if constexpr (S <= 256) {
+        constexpr int M = S / R - 1;
+        flip_lanes<R, M>(v, lane);
+        halfclean_lanes_down<R, S / R / 4>(v, lane);
+        halfclean_regs<R>(v);
+        sort_lanes_from<R, S * 2>(v, lane);
+    }
+}
+template <int R>
+__device__ __forceinline__ void sort_group256(uint32_t (&v)[R], int lane) {
+    sort_regs<R>(v);
+    sort_lanes_from<R, 2 * R>(v, lane);
+}
+
+// Keep every other sorted position: parity `odd` is the compaction RNG bit
+// (QSketchUtils.compactBuffer, QSketchUtils.java:45-51).
+template <int R>
+__device__ __forceinline__ void compact_regs(const uint32_t (&v)[R], uint32_t (&w)[R / 2], bool odd) {
+#pragma unroll
+    for (int j = 0; j < R / 2; j++) w[j] = odd ? v[2 * j + 1] : v[2 * j];
+}
+
+// ------------------------------------------------------------------------------------------
+// java.util.Random jump-ahead: state after `steps` LCG steps = A^steps * s + C_steps (mod 2^48),
+// from a 4-level byte-indexed table of (A^m, C_m) (built on the host, skml_api.cpp).
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t lcg_jump(const uint64_t* __restrict__ tab, uint64_t s,
+                                             uint64_t steps) {
+#pragma unroll
+    for (int lvl = 0; lvl < 4; lvl++) {
+        uint32_t b = (uint32_t)(steps >> (8 * lvl)) & 255u;
+        if (b) {
+            const uint64_t a = tab[(lvl * 256 + b) * 2];
+            const uint64_t c = tab[(lvl * 256 + b) * 2 + 1];
+            s = (a * s + c) & kLcgMask;
+        }
+    }
+    return s;
+}
+// next(1) of the idx-th draw (0-based) from Random(seed) whose scrambled state is s0.
+__device__ __forceinline__ uint32_t lcg_bit(const uint64_t* __restrict__ tab, uint64_t s0,
+                                            uint64_t idx) {
+    return (uint32_t)(lcg_jump(tab, s0, idx + 1) >> 47) & 1u;
+}
+// Bit-stream index of the compaction that forms the node at `level` whose last chunk is c:
+// chunk c's leaf bit is #(2c - popcount(c)), followed by its carry compactions.
+__device__ __forceinline__ uint64_t node_bit_index(uint64_t c, int level) {
+    return 2 * c - (uint64_t)__popcll(c) + (uint64_t)level;
+}
+
+// ------------------------------------------------------------------------------------------
+// Exact merge of two sorted 128-runs with the reference tie rule (QSketchUtils.mergeArrays,
+// QSketchUtils.java:53-69: IEEE `<`, a tie emits the NEWER run first) followed by compaction.
+// Task t in [0,256): element t of older (t<128) or newer.  Writes kept elements to out.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ int count_le(const float* run, float x) {  // #{run[i] <= x}
+    int lo = 0;
+#pragma unroll
+    for (int step = 64; step >= 1; step >>= 1)
+        if (run[lo + step - 1] <= x) lo += step;
+    return lo + (run[lo] <= x ? 1 : 0) * (lo == 127 ? 1 : 0);
+}
+__device__ __forceinline__ int count_lt(const float* run, float x) {  // #{run[i] < x}
+    int lo = 0;
+#pragma unroll
+    for (int step = 64; step >= 1; step >>= 1)
+        if (run[lo + step - 1] < x) lo += step;
+    return lo + (run[lo] < x ? 1 : 0) * (lo == 127 ? 1 : 0);
+}
+__device__ __forceinline__ void exact_merge_task(const float* older, const float* newer, float* out,
+                                                 int t, uint32_t odd) {
+    float v;
+    int pos;
+    if (t < 128) {
+        v = older[t];
+        pos = t + count_le(newer, v);
+    } else {
+        v = newer[t - 128];
+        pos = (t - 128) + count_lt(older, v);
+    }
+    if (((uint32_t)pos & 1u) == odd) out[pos >> 1] = v;
+}
+
+}  // namespace skml

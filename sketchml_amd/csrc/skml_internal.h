@@ -1,0 +1,79 @@
+// skml_internal.h -- constants and launch interfaces shared by skml_api.cpp and the kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/skml.h"
+
+namespace skml {
+
+constexpr uint64_t kLcgMult = 0x5DEECE66DULL;  // java.util.Random
+constexpr uint64_t kLcgAdd = 0xBULL;
+constexpr uint64_t kLcgMask = (1ULL << 48) - 1;
+
+constexpr int kK = 128;                 // HeapQuantileSketch.DEFAULT_K (HeapQuantileSketch.java:13)
+constexpr int kChunk = 2 * kK;          // base buffer size: 256 values per leaf
+constexpr int kLeafWaves = 8;           // waves per leaf workgroup
+constexpr int kChunksPerWave = 8;       // 32 keys per lane, 8 lanes per chunk
+constexpr int kLeafChunks = kLeafWaves * kChunksPerWave;  // 64 chunks -> one level-6 node
+constexpr int kLeafTopLevel = 6;
+constexpr int kMergeGroupLog = 6;       // upper merge: 64 nodes per workgroup
+constexpr int kMaxLevels = 24;     // n < 2^31 -> fewer than 2^23 chunks
+constexpr int kHeaderBytes = 64;
+
+// Per leaf workgroup partial results: min key, max key, flags (bit0 NaN, bit1 -0, bit2 +0).
+struct LeafPartial {
+    uint32_t min_key;
+    uint32_t max_key;
+    uint32_t flags;
+    uint32_t pad;
+};
+
+struct MergeJob {
+    int64_t src_node;      // first input node index (in src buffer)
+    int64_t dst_node;      // first output node index (in dst buffer), or -1 -> root slot
+    int64_t chunk_base;    // first chunk covered by the job's first input node
+    int32_t level_in;      // level of the input nodes
+    int32_t group_log;     // each workgroup merges 2^group_log consecutive nodes
+    int32_t groups;        // number of workgroups for this job
+    int32_t root_level;    // >= 0: the single output is the tree root of this level
+};
+constexpr int kMaxJobs = 24;
+struct MergePass {
+    MergeJob job[kMaxJobs];
+    int32_t njobs;
+    int32_t wg_prefix[kMaxJobs + 1];
+};
+
+__host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+// Packed code width: smallest of 1, 2, 4, 8, 16 bits holding bin_num codes.
+__host__ __device__ inline int code_bits_for(int bins) {
+    int b = 1;
+    while ((1LL << b) < bins) b <<= 1;
+    return b;
+}
+__host__ __device__ inline size_t dense_codes_offset(int req_bins) {
+    return align_up(kHeaderBytes + 8 * (size_t)(req_bins - 1), 256);
+}
+
+// ---- kernel launchers (skml_dense.hip) ----
+hipError_t launch_leaf(hipStream_t st, const float* x, int64_t chunks, uint64_t s0,
+                       const uint64_t* jump_tab, LeafPartial* part, float* nodes6, float* roots);
+hipError_t launch_merge_pass(hipStream_t st, const MergePass& pass, const float* src, float* dst,
+                             float* roots, uint64_t s0, const uint64_t* jump_tab);
+hipError_t launch_summary(hipStream_t st, const float* x, int64_t n, const LeafPartial* part,
+                          int64_t nparts, const float* roots, const int64_t* ranks, int req_bins,
+                          int dedup, void* payload, double* scratch_raw);
+hipError_t launch_set_splits(hipStream_t st, void* payload, int64_t n, const double* splits_dev,
+                             int nsplits, double mn, double mx, int req_bins);
+hipError_t launch_quantize(hipStream_t st, const float* x, int64_t n, void* payload);
+hipError_t launch_decode(hipStream_t st, const void* payload, float* out, int64_t n);
+hipError_t launch_decode_sum(hipStream_t st, const void* payloads, int P, size_t stride, float* out,
+                             int64_t n, double scale);
+hipError_t launch_bins(hipStream_t st, const void* payload, int32_t* bins, int64_t n);
+hipError_t launch_ref_body(hipStream_t st, const void* payload, uint8_t* out, int64_t n, int width);
+hipError_t launch_times_by(hipStream_t st, void* payload, double x);
+hipError_t launch_pack_ref(hipStream_t st, const uint8_t* body, int width, int64_t n, void* payload);
+
+}  // namespace skml

@@ -1,0 +1,244 @@
+"""Quantizer / QuantileQuantizer over the HIP codec.
+
+Mirrors base/Quantizer.java:18-228 and quantization/QuantileQuantizer.java:18-99: the same
+method names, argument meaning and exceptions, with the gradient held on the GPU.  The encoded
+state is one device payload (header + split table + packed codes, include/skml.h); getBins()
+materialises int32 bins on demand.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import struct
+from enum import Enum
+
+import numpy as np
+import torch
+
+from . import _lib
+from .context import alloc_aligned, as_device_f32, get_context
+from .exceptions import QuantileSketchException, SketchMLException, check
+
+
+class QuantizationType(Enum):
+    UNIFORM = "UNIFORM"
+    QUANTILE = "QUANTILE"
+
+    def __str__(self):
+        return self.value
+
+
+class Quantizer:
+    """base/Quantizer.java:18-228."""
+
+    DEFAULT_BIN_NUM = 256
+
+    def __init__(self, binNum: int = DEFAULT_BIN_NUM, seed: int = 0):
+        self.binNum = int(binNum)
+        self.seed = int(seed)
+        self.n = 0
+        self.payload = None          # torch.uint8 device tensor
+        self.device = None
+        self._hdr = None
+        self._splits = None
+        self._bins = None
+
+    # ---- abstract surface ----
+    def quantize(self, values) -> None:
+        raise NotImplementedError
+
+    def parallelQuantize(self, values) -> None:
+        raise NotImplementedError
+
+    def quantizationType(self) -> QuantizationType:
+        raise NotImplementedError
+
+    @staticmethod
+    def newQuantizer(qtype, binNum: int, seed: int = 0) -> "Quantizer":
+        """Quantizer.newQuantizer (Quantizer.java:126-136)."""
+        if str(qtype) == "QUANTILE":
+            return QuantileQuantizer(binNum, seed)
+        raise SketchMLException(f"Unrecognizable quantization type: {qtype}")
+
+    # ---- device payload plumbing ----
+    def _ctx(self):
+        return get_context(self.device)
+
+    def _load_header(self):
+        if self._hdr is None:
+            hdr = _lib.DenseHeader()
+            splits = np.zeros(_lib.SKML_MAX_BINS, dtype=np.float64)
+            st = _lib.lib.skml_dense_info(self._ctx().handle, C.c_void_p(self.payload.data_ptr()),
+                                          C.byref(hdr), splits.ctypes.data_as(_lib.dblp), len(splits))
+            check(st, "quantize")
+            self._hdr = hdr
+            self._splits = splits[: hdr.bin_num - 1].copy()
+            self.binNum = hdr.bin_num
+        return self._hdr
+
+    def _encode(self, values, dedup: bool):
+        x = as_device_f32(values, self.device)
+        self.device = x.device
+        self.n = x.numel()
+        if self.binNum <= 1:
+            raise QuantileSketchException(f"Invalid partition number: {self.binNum}")
+        nbytes = _lib.lib.skml_dense_payload_bytes(self.n, self.binNum)
+        if nbytes == 0:
+            raise SketchMLException(f"bad quantizer arguments n={self.n} binNum={self.binNum}")
+        self.payload = alloc_aligned(nbytes, x.device)
+        p = _lib.Params()
+        _lib.lib.skml_params_default(C.byref(p))
+        p.bin_num = self.binNum
+        p.seed = self.seed
+        p.dedup = 1 if dedup else 0
+        st = _lib.lib.skml_dense_encode_f32(self._ctx().handle, C.c_void_p(x.data_ptr()), self.n,
+                                            C.byref(p), C.c_void_p(self.payload.data_ptr()), nbytes)
+        check(st, "quantize")
+        self._hdr = None
+        self._bins = None
+        self._x = x  # keep the input alive until the stream has consumed it
+        self._load_header()  # surfaces NaN as QuantileSketchException, like update() throws
+        self._x = None
+
+    # ---- Quantizer getters ----
+    def getValues(self) -> np.ndarray:
+        """Quantizer.getValues (Quantizer.java:39-47): bin midpoints in double."""
+        h = self._load_header()
+        s = self._splits
+        ns = h.bin_num - 1
+        res = np.empty(h.bin_num, dtype=np.float64)
+        res[0] = 0.5 * (h.min + s[0])
+        for i in range(1, ns):
+            res[i] = 0.5 * (s[i - 1] + s[i])
+        res[ns] = 0.5 * (s[ns - 1] + h.max)
+        return res
+
+    def indexOf(self, x: float) -> int:
+        """Quantizer.indexOf (Quantizer.java:49-72) on the host (one value)."""
+        h = self._load_header()
+        s = self._splits
+        B = h.bin_num
+        if x < s[0]:
+            return 0
+        if x >= s[B - 2]:
+            return B - 1
+        lo = hi = h.zero_idx
+        if x < 0.0:
+            lo = 0
+        else:
+            hi = B - 2
+        while lo + 1 < hi:
+            mid = (lo + hi) >> 1
+            if s[mid] > x:
+                if mid == 0 or s[mid - 1] <= x:
+                    return mid
+                hi = mid
+            else:
+                lo = mid
+        mid = (lo + hi) >> 1
+        return mid + 1 if s[mid] <= x else mid
+
+    def getBins(self) -> torch.Tensor:
+        """Quantizer.getBins: int32 bins materialised on the device."""
+        if self._bins is None:
+            self._load_header()
+            b = torch.empty(self.n, dtype=torch.int32, device=self.device)
+            check(_lib.lib.skml_dense_bins_i32(self._ctx().handle, C.c_void_p(self.payload.data_ptr()),
+                                               C.c_void_p(b.data_ptr()), self.n), "getBins")
+            self._bins = b
+        return self._bins
+
+    def getBinNum(self) -> int:
+        return self._load_header().bin_num if self.payload is not None else self.binNum
+
+    def getN(self) -> int:
+        return self.n
+
+    def getSplits(self) -> np.ndarray:
+        self._load_header()
+        return self._splits.copy()
+
+    def getZeroIdx(self) -> int:
+        return self._load_header().zero_idx
+
+    def getMin(self) -> float:
+        return self._load_header().min
+
+    def getMax(self) -> float:
+        return self._load_header().max
+
+    def codeBits(self) -> int:
+        return self._load_header().code_bits
+
+    def timesBy(self, x: float) -> None:
+        """Quantizer.timesBy (Quantizer.java:119-124)."""
+        self._load_header()
+        check(_lib.lib.skml_dense_times_by(self._ctx().handle, C.c_void_p(self.payload.data_ptr()),
+                                           float(x)), "timesBy")
+        self._hdr = None
+
+    def decode(self, out: torch.Tensor = None) -> torch.Tensor:
+        """values[bins[i]] in fp32 on the device (DenseVectorCompressor.decompressDense)."""
+        self._load_header()
+        if out is None:
+            out = torch.empty(self.n, dtype=torch.float32, device=self.device)
+        check(_lib.lib.skml_dense_decode_f32(self._ctx().handle, C.c_void_p(self.payload.data_ptr()),
+                                             C.c_void_p(out.data_ptr()), self.n), "decode")
+        return out
+
+    # ---- java serialisation field stream ----
+    def writeObject(self) -> bytes:
+        """Quantizer.writeObject (Quantizer.java:184-203) field stream, big-endian."""
+        self._load_header()
+        n = C.c_size_t()
+        ctx = self._ctx().handle
+        pl = C.c_void_p(self.payload.data_ptr())
+        check(_lib.lib.skml_dense_serialize_ref(ctx, pl, None, 0, C.byref(n)), "writeObject")
+        buf = np.zeros(n.value, dtype=np.uint8)
+        check(_lib.lib.skml_dense_serialize_ref(ctx, pl, buf.ctypes.data_as(_lib.u8p), n.value,
+                                                C.byref(n)), "writeObject")
+        return buf.tobytes()
+
+    @classmethod
+    def readObject(cls, data: bytes, device=None) -> "Quantizer":
+        """Quantizer.readObject (Quantizer.java:205-226)."""
+        if len(data) < 8:
+            raise SketchMLException("truncated Quantizer stream")
+        B, n = struct.unpack(">ii", data[:8])
+        q = QuantileQuantizer(B)
+        q.device = torch.device("cuda", torch.cuda.current_device()) if device is None else device
+        q.n = n
+        nbytes = _lib.lib.skml_dense_payload_bytes(n, B)
+        if nbytes == 0:
+            raise SketchMLException(f"bad Quantizer stream binNum={B} n={n}")
+        q.payload = alloc_aligned(nbytes, q.device)
+        arr = np.frombuffer(data, dtype=np.uint8).copy()
+        check(_lib.lib.skml_dense_deserialize_ref(q._ctx().handle, arr.ctypes.data_as(_lib.u8p), len(arr),
+                                                  C.c_void_p(q.payload.data_ptr()), nbytes), "readObject")
+        q._load_header()
+        return q
+
+
+class QuantileQuantizer(Quantizer):
+    """quantization/QuantileQuantizer.java:18-99 on the GPU.
+
+    `seed` seeds the java.util.Random stream that the reference draws from its JVM-global
+    Random (QSketchUtils.java:9): same seed -> same splits and bins as the oracle.
+    """
+
+    def __init__(self, binNum: int = Quantizer.DEFAULT_BIN_NUM, seed: int = 0):
+        super().__init__(binNum, seed)
+
+    def quantize(self, values) -> None:
+        """QuantileQuantizer.quantize (QuantileQuantizer.java:27-50)."""
+        self._encode(values, dedup=True)
+
+    def parallelQuantize(self, values) -> None:
+        """QuantileQuantizer.parallelQuantize (QuantileQuantizer.java:53-92): one device sketch
+        (T = 1 merge order) and, as in the reference, no Maths.unique of the splits."""
+        self._encode(values, dedup=False)
+
+    def quantizationType(self) -> QuantizationType:
+        return QuantizationType.QUANTILE
+
+
+DEFAULT_BIN_NUM = Quantizer.DEFAULT_BIN_NUM
