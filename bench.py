@@ -1,0 +1,270 @@
+#!/usr/bin/env python
+"""Benchmark of the MI355X SketchML gradient codec (BASELINE.json metric).
+
+One step = encode one 2^26-float fp32 gradient bucket resident in HBM (k=128 quantile sketch ->
+getQuantiles(256) -> Maths.unique -> bucket quantise -> packed codes), i.e. BASELINE config 2
+(SURVEY.md C2).  With --gpus N > 1 (launched by torch.distributed.run) every rank encodes its own
+2^26 bucket (config 4, weak scaling) and the step adds the RCCL all-gather of the compressed
+payloads over xGMI.  `value` = fp32-input GB/s of the whole job.
+
+Extra fields: decode GB/s and decode L2 error (the metric's "+ decode L2 err"), per-kernel
+device times, the roofline of the dominant kernel, the CPU baseline (the C restatement of the
+reference Java algorithm, oracle/, timed on this host on a bounded sample) and the
+H2D/D2H-inclusive rate.
+"""
+import argparse
+import ctypes as C
+import glob
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, MI355X_MICROARCH.md "Chip-level parameters"
+KNAMES = {0: "k_leaf", 1: "k_merge", 2: "k_summary", 3: "k_quantize", 4: "k_decode"}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--n", type=int, default=2**26, help="floats per GPU bucket")
+    ap.add_argument("--bins", type=int, default=256)
+    ap.add_argument("--buffers", type=int, default=4,
+                    help="rotating input buckets so a step never re-reads the previous step's "
+                         "input from the 256 MB Infinity Cache")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip decode / H2D measurements")
+    return ap.parse_args()
+
+
+def kernel_stats(lib, ctx):
+    out = {}
+    for kid, name in KNAMES.items():
+        n = C.c_int64()
+        ms = C.c_double()
+        lib.skml_ctx_kernel_stats(ctx, kid, C.byref(n), C.byref(ms))
+        if n.value:
+            out[name] = {"launches": n.value, "avg_us": 1000.0 * ms.value / n.value}
+    return out
+
+
+def pmc_traffic(kernel, n):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc summary, if one exists
+    for this problem size (profiles/*pmc*.json, written by tools/pmc_summary.py)."""
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except Exception:
+            continue
+        k = d.get("kernels", {}).get(kernel)
+        if k and d.get("n") == n and "hbm_bytes_per_launch" in k:
+            best = (k["hbm_bytes_per_launch"], os.path.relpath(path, ROOT))
+    return best
+
+
+def cpu_baseline(x_host, bins, budget_s):
+    """Oracle (C restatement of QuantileQuantizer.quantize + 1-byte code write, scalar -O2,
+    double arithmetic, 1 thread) on a bounded sample of the same workload."""
+    from oracle import oracle as O
+    sample = x_host[: 2**22]
+    t, _ = O.bench_dense_encode(sample, bins, seed=1, reps=1)
+    reps = max(1, int(budget_s / max(t, 1e-3)))
+    t, _ = O.bench_dense_encode(sample, bins, seed=1, reps=reps)
+    gbs = 4.0 * len(sample) * reps / t / 1e9
+    return {"value": round(gbs, 4), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": f"first 2^22 floats of the bucket, {reps} encode(s), {t:.1f} s",
+            "cpu": _cpu_model()}
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    import sketchml_amd as sk
+    from sketchml_amd import _lib
+    lib = _lib.lib
+    ctx = sk.get_context(dev.index).handle
+
+    n, bins = args.n, args.bins
+    nb = lib.skml_dense_payload_bytes(n, bins)
+    nbuf = max(1, args.buffers)
+    gen = torch.Generator(device=dev)
+    xs = []
+    for b in range(nbuf):
+        gen.manual_seed(4 + rank + 1000 * b)  # config 4: bucket r seeded 4 + r
+        xs.append(torch.randn(n, device=dev, generator=gen))
+    payload = sk.alloc_aligned(nb, dev)
+    params = _lib.Params()
+    lib.skml_params_default(C.byref(params))
+    params.bin_num = bins
+    params.seed = 2 + rank
+
+    comm = None
+    allp = None
+    if world > 1:
+        uid = (C.c_uint8 * _lib.UNIQUE_ID_BYTES)()
+        if rank == 0:
+            assert lib.skml_comm_unique_id(uid) == 0, _lib.last_error()
+        obj = [bytes(uid)]
+        dist.broadcast_object_list(obj, src=0)
+        uid = (C.c_uint8 * _lib.UNIQUE_ID_BYTES).from_buffer_copy(obj[0])
+        comm = C.c_void_p()
+        assert lib.skml_comm_init_rank(ctx, uid, world, rank, C.byref(comm)) == 0, _lib.last_error()
+        allp = sk.alloc_aligned(nb * world, dev)
+
+    def step(i):
+        x = xs[i % nbuf]
+        st = lib.skml_dense_encode_f32(ctx, C.c_void_p(x.data_ptr()), n, C.byref(params),
+                                       C.c_void_p(payload.data_ptr()), nb)
+        if st:
+            raise RuntimeError(_lib.last_error())
+        if comm is not None:
+            st = lib.skml_allgather(ctx, comm, C.c_void_p(payload.data_ptr()), nb,
+                                    C.c_void_p(allp.data_ptr()))
+            if st:
+                raise RuntimeError(_lib.last_error())
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    lib.skml_ctx_set_timing(ctx, 1)
+    lib.skml_ctx_reset_stats(ctx)
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    torch.cuda.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    lib.skml_ctx_set_timing(ctx, 0)
+    kstats = kernel_stats(lib, ctx)
+
+    ms_per_step = 1000.0 * elapsed / args.steps
+    value = world * 4.0 * n * args.steps / elapsed / 1e9
+
+    # ---- roofline of the dominant kernel (algorithmic bytes per launch / avg duration) ----
+    hdr = _lib.DenseHeader()
+    lib.skml_dense_info(ctx, C.c_void_p(payload.data_ptr()), C.byref(hdr), None, 0)
+    code_bits = hdr.code_bits
+    alg_bytes = {"k_leaf": 4.0 * n, "k_quantize": 4.0 * n + n * code_bits / 8.0,
+                 "k_merge": 4.0 * 128 * max(1, n // 256 // 64), "k_summary": 0.0}
+    dom = max((k for k in kstats if k in alg_bytes), key=lambda k: kstats[k]["avg_us"] * kstats[k]["launches"])
+    ach = alg_bytes[dom] / (kstats[dom]["avg_us"] * 1e-6) / 1e9
+    traffic = pmc_traffic(dom, n)
+    roofline = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                "traffic": traffic[0] if traffic else None,
+                "traffic_source": traffic[1] if traffic else None,
+                "alg_bytes_per_launch": alg_bytes[dom]}
+    encode_device_us = sum(v["avg_us"] * v["launches"] for k, v in kstats.items()
+                           if k in alg_bytes) / args.steps
+    extras = {"encode_device_us": round(encode_device_us, 2),
+              "encode_roofline_frac": round((8.0 + code_bits / 8.0) * n / (encode_device_us * 1e-6)
+                                            / 1e9 / HBM_PEAK_GBS, 4),
+              "kernels": {k: {"avg_us": round(v["avg_us"], 2), "launches": v["launches"]}
+                          for k, v in kstats.items()},
+              "bin_num_effective": hdr.bin_num, "code_bits": code_bits}
+
+    # ---- decode throughput + decode L2 error (rank-local) ----
+    if not args.no_extras:
+        out = torch.empty(n, dtype=torch.float32, device=dev)
+        x = xs[(args.warmup + args.steps - 1) % nbuf]
+        lib.skml_ctx_set_timing(ctx, 1)
+        lib.skml_ctx_reset_stats(ctx)
+        for _ in range(10):
+            lib.skml_dense_decode_f32(ctx, C.c_void_p(payload.data_ptr()), C.c_void_p(out.data_ptr()), n)
+        dstats = kernel_stats(lib, ctx)
+        lib.skml_ctx_set_timing(ctx, 0)
+        dus = dstats["k_decode"]["avg_us"]
+        diff = (out.double() - x.double())
+        l2 = float(torch.linalg.vector_norm(diff).item())
+        extras["decode"] = {"gbps_fp32_out": round(4.0 * n / (dus * 1e-6) / 1e9, 1), "avg_us": round(dus, 2),
+                            "roofline_frac": round((4.0 + code_bits / 8.0) * n / (dus * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+        extras["decode_l2_err"] = l2
+        extras["decode_rmse"] = l2 / np.sqrt(n)
+        extras["decode_rel_l2"] = l2 / float(torch.linalg.vector_norm(x.double()).item())
+        # end-to-end with PCIe: pinned host fp32 -> device -> encode -> payload back to host
+        if rank == 0:
+            host = torch.empty(n, dtype=torch.float32, pin_memory=True)
+            host.copy_(x.cpu())
+            hp = torch.empty(nb, dtype=torch.uint8, pin_memory=True)
+            xd = torch.empty(n, dtype=torch.float32, device=dev)
+            reps = 5
+            torch.cuda.synchronize()
+            ta = time.perf_counter()
+            for _ in range(reps):
+                xd.copy_(host, non_blocking=True)
+                lib.skml_dense_encode_f32(ctx, C.c_void_p(xd.data_ptr()), n, C.byref(params),
+                                          C.c_void_p(payload.data_ptr()), nb)
+                hp.copy_(payload, non_blocking=True)
+            torch.cuda.synchronize()
+            tb = time.perf_counter()
+            extras["h2d_d2h_inclusive_gbps"] = round(4.0 * n * reps / (tb - ta) / 1e9, 2)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(xs[0][: 2**22].cpu().numpy(), bins, args.cpu_seconds)
+
+    if world > 1:
+        lib.skml_comm_destroy(comm)
+    if rank == 0:
+        line = {
+            "metric": "device-resident grad encode GB/s (fp32 in) + decode L2 err, 1/2/4/8 GPU",
+            "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic N(0,1), torch generator",
+            "config": {"workload": ("C2: 2^26-float dense gradient bucket per GPU, 256 requested bins, "
+                                    "encode" + (" + RCCL all-gather of payloads (C4)" if world > 1 else "")),
+                       "n_per_gpu": n, "bins": bins, "rotating_buffers": nbuf, "parallelism": f"dp{world}"},
+            "roofline": roofline, "cpu_baseline": cpu, "extras": extras,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

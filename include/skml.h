@@ -83,6 +83,21 @@ int skml_ctx_destroy(skml_ctx* ctx);
 int skml_ctx_sync(skml_ctx* ctx);
 int skml_ctx_set_stream(skml_ctx* ctx, void* hip_stream);
 
+/* Per-kernel timing with HIP events recorded on the context stream around every launch
+ * (profiling aid for bench.py's roofline; off by default). */
+#define SKML_K_LEAF 0
+#define SKML_K_MERGE 1
+#define SKML_K_SUMMARY 2
+#define SKML_K_QUANTIZE 3
+#define SKML_K_DECODE 4
+#define SKML_K_DECODE_SUM 5
+#define SKML_K_SPARSE 6
+#define SKML_K_COUNT 7
+int skml_ctx_set_timing(skml_ctx* ctx, int enable);
+/* Synchronises; total device milliseconds and launch count of kernel `kid` since the reset. */
+int skml_ctx_kernel_stats(skml_ctx* ctx, int kid, int64_t* launches, double* total_ms);
+int skml_ctx_reset_stats(skml_ctx* ctx);
+
 /* ---- Dense path: QuantileQuantizer.quantize + Quantizer.getBins/getValues ---- */
 
 /* Bytes of a device payload able to hold n codes for `bin_num` requested bins. */

@@ -60,7 +60,41 @@ struct skml_ctx {
     void* stage = nullptr;
     size_t stage_cap = 0;
     SparseWorkspace sparse;
+    // per-kernel event timing (skml_ctx_set_timing)
+    bool timing = false;
+    std::vector<hipEvent_t> ev[SKML_K_COUNT];  // start/stop pairs
+    size_t ev_used[SKML_K_COUNT] = {};
 };
+
+namespace skml {
+// Records a start event on construction and a stop event on destruction when timing is on.
+struct KernelTimer {
+    skml_ctx* c;
+    int kid;
+    bool on;
+    KernelTimer(skml_ctx* ctx, int k) : c(ctx), kid(k), on(ctx->timing) {
+        if (!on) return;
+        auto& v = c->ev[kid];
+        if (c->ev_used[kid] + 2 > v.size()) {
+            hipEvent_t a, b;
+            if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) {
+                on = false;
+                return;
+            }
+            v.push_back(a);
+            v.push_back(b);
+        }
+        (void)hipEventRecord(v[c->ev_used[kid]], c->stream);
+    }
+    ~KernelTimer() {
+        if (!on) return;
+        (void)hipEventRecord(c->ev[kid][c->ev_used[kid] + 1], c->stream);
+        c->ev_used[kid] += 2;
+    }
+};
+KernelTimer* make_timer(skml_ctx* c, int kid) { return new KernelTimer(c, kid); }
+void end_timer(KernelTimer* t) { delete t; }
+}  // namespace skml
 
 namespace {
 
@@ -235,6 +269,8 @@ int skml_ctx_destroy(skml_ctx* c) {
     if (c->ws) (void)hipFree(c->ws);
     if (c->ranks) (void)hipFree(c->ranks);
     if (c->stage) (void)hipFree(c->stage);
+    for (int k = 0; k < SKML_K_COUNT; k++)
+        for (hipEvent_t e : c->ev[k]) (void)hipEventDestroy(e);
     sparse_ws_free(&c->sparse);
     if (c->own_stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -244,6 +280,33 @@ int skml_ctx_destroy(skml_ctx* c) {
 int skml_ctx_sync(skml_ctx* c) {
     if (!c) return fail(SKML_E_ARG, "ctx is NULL");
     HIP_TRY(hipStreamSynchronize(c->stream));
+    return SKML_OK;
+}
+
+int skml_ctx_set_timing(skml_ctx* c, int enable) {
+    if (!c) return fail(SKML_E_ARG, "ctx is NULL");
+    c->timing = enable != 0;
+    return SKML_OK;
+}
+
+int skml_ctx_reset_stats(skml_ctx* c) {
+    if (!c) return fail(SKML_E_ARG, "ctx is NULL");
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    for (int k = 0; k < SKML_K_COUNT; k++) c->ev_used[k] = 0;
+    return SKML_OK;
+}
+
+int skml_ctx_kernel_stats(skml_ctx* c, int kid, int64_t* launches, double* total_ms) {
+    if (!c || kid < 0 || kid >= SKML_K_COUNT) return fail(SKML_E_ARG, "bad kernel id");
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    double tot = 0.0;
+    for (size_t i = 0; i + 1 < c->ev_used[kid]; i += 2) {
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, c->ev[kid][i], c->ev[kid][i + 1]));
+        tot += ms;
+    }
+    if (launches) *launches = (int64_t)(c->ev_used[kid] / 2);
+    if (total_ms) *total_ms = tot;
     return SKML_OK;
 }
 
@@ -296,7 +359,10 @@ int skml_dense_encode_f32(skml_ctx* c, const float* x, int64_t n, const skml_par
     const int64_t nwg = (chunks + kLeafChunks - 1) / kLeafChunks;
 
     if (chunks > 0) {
-        HIP_TRY(launch_leaf(c->stream, x, chunks, s0, c->jump_tab, w.part, w.nodes6, w.roots));
+        {
+            KernelTimer kt(c, SKML_K_LEAF);
+            HIP_TRY(launch_leaf(c->stream, x, chunks, s0, c->jump_tab, w.part, w.nodes6, w.roots));
+        }
         // ---- upper trees: bits l >= 7 of chunks (bit 6 is a single leaf-workgroup node) ----
         std::vector<Tree> trees;
         for (int l = kMaxLevels - 1; l > kLeafTopLevel; l--) {
@@ -337,14 +403,23 @@ int skml_dense_encode_f32(skml_ctx* c, const float* x, int64_t n, const skml_par
             }
             if (pass.njobs == 0) break;
             pass.wg_prefix[pass.njobs] = wg;
-            HIP_TRY(launch_merge_pass(c->stream, pass, src, dst, w.roots, s0, c->jump_tab));
+            {
+                KernelTimer kt(c, SKML_K_MERGE);
+                HIP_TRY(launch_merge_pass(c->stream, pass, src, dst, w.roots, s0, c->jump_tab));
+            }
             src = dst;
             dst = (dst == w.upA) ? w.upB : w.upA;
         }
     }
-    HIP_TRY(launch_summary(c->stream, x, n, w.part, nwg, w.roots, c->ranks, p->bin_num, p->dedup ? 1 : 0,
-                           payload, w.raw));
-    HIP_TRY(launch_quantize(c->stream, x, n, payload));
+    {
+        KernelTimer kt(c, SKML_K_SUMMARY);
+        HIP_TRY(launch_summary(c->stream, x, n, w.part, nwg, w.roots, c->ranks, p->bin_num,
+                               p->dedup ? 1 : 0, payload, w.raw));
+    }
+    {
+        KernelTimer kt(c, SKML_K_QUANTIZE);
+        HIP_TRY(launch_quantize(c->stream, x, n, payload));
+    }
     return SKML_OK;
 }
 
@@ -370,6 +445,7 @@ int skml_dense_decode_f32(skml_ctx* c, const void* payload, float* out, int64_t 
     if (!c || !valid_payload_ptr(payload) || (n > 0 && (!out || ((uintptr_t)out) % 16)))
         return fail(SKML_E_ARG, "bad decode arguments");
     HIP_TRY(hipSetDevice(c->device));
+    KernelTimer kt(c, SKML_K_DECODE);
     HIP_TRY(launch_decode(c->stream, payload, out, n));
     return SKML_OK;
 }
@@ -380,6 +456,7 @@ int skml_dense_decode_sum_f32(skml_ctx* c, const void* payloads, int32_t P, size
         (n > 0 && (!out || ((uintptr_t)out) % 16)))
         return fail(SKML_E_ARG, "bad decode_sum arguments (P in [1,16], 256-B aligned payloads)");
     HIP_TRY(hipSetDevice(c->device));
+    KernelTimer kt(c, SKML_K_DECODE_SUM);
     HIP_TRY(launch_decode_sum(c->stream, payloads, P, stride, out, n, scale));
     return SKML_OK;
 }
