@@ -97,6 +97,10 @@ int skml_ctx_set_timing(skml_ctx* ctx, int enable);
 /* Synchronises; total device milliseconds and launch count of kernel `kid` since the reset. */
 int skml_ctx_kernel_stats(skml_ctx* ctx, int kid, int64_t* launches, double* total_ms);
 int skml_ctx_reset_stats(skml_ctx* ctx);
+/* Profiling ablation of the sketch leaf kernel (stage 0 load, 1 + leaf sort, 2 + in-wave merges,
+ * 3 full): average device ms over `iters` launches on n values.  Not part of the codec. */
+int skml_debug_leaf_stage(skml_ctx* ctx, const float* x_dev, int64_t n, int stage, int iters,
+                          double* avg_ms);
 
 /* ---- Dense path: QuantileQuantizer.quantize + Quantizer.getBins/getValues ---- */
 

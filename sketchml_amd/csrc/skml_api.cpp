@@ -310,6 +310,35 @@ int skml_ctx_kernel_stats(skml_ctx* c, int kid, int64_t* launches, double* total
     return SKML_OK;
 }
 
+int skml_debug_leaf_stage(skml_ctx* c, const float* x, int64_t n, int stage, int iters,
+                          double* avg_ms) {
+    if (!c || !x || n < kChunk || iters < 1 || !avg_ms) return fail(SKML_E_ARG, "bad arguments");
+    HIP_TRY(hipSetDevice(c->device));
+    const int64_t chunks = n / kChunk;
+    Workspace w;
+    int st = ensure_ws(c, chunks, &w);
+    if (st) return st;
+    const int64_t nwg = (chunks + kLeafChunks - 1) / kLeafChunks;
+    if ((st = ensure_stage(c, sizeof(float) * 512 * (size_t)nwg))) return st;
+    hipEvent_t a, b;
+    HIP_TRY(hipEventCreate(&a));
+    HIP_TRY(hipEventCreate(&b));
+    HIP_TRY(launch_leaf_stage(c->stream, stage, x, chunks, 12345, c->jump_tab, w.part,
+                              (float*)c->stage, w.roots));
+    HIP_TRY(hipEventRecord(a, c->stream));
+    for (int i = 0; i < iters; i++)
+        HIP_TRY(launch_leaf_stage(c->stream, stage, x, chunks, 12345, c->jump_tab, w.part,
+                                  (float*)c->stage, w.roots));
+    HIP_TRY(hipEventRecord(b, c->stream));
+    HIP_TRY(hipEventSynchronize(b));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    *avg_ms = ms / iters;
+    return SKML_OK;
+}
+
 int skml_ctx_set_stream(skml_ctx* c, void* hip_stream) {
     if (!c) return fail(SKML_E_ARG, "ctx is NULL");
     if (c->own_stream) {

@@ -73,6 +73,8 @@ __device__ __forceinline__ void export_wave_root(const uint32_t (&w)[R], int lan
     for (int r = 0; r < R; r++) dst[li * R + r] = __uint_as_float(key2f(w[r]));
 }
 
+// STAGE < 3 are truncated variants used only by skml_debug_leaf (profiling ablation).
+template <int STAGE>
 __global__ __launch_bounds__(512) void k_leaf(const float* __restrict__ x, int64_t chunks,
                                               uint64_t s0, const uint64_t* __restrict__ tab,
                                               LeafPartial* __restrict__ part,
@@ -132,6 +134,13 @@ __global__ __launch_bounds__(512) void k_leaf(const float* __restrict__ x, int64
         sh.mask[wave] = mask;
         sh.start[wave] = start;
     }
+    if constexpr (STAGE == 0) {
+        uint32_t acc = mn ^ mx ^ fl ^ (uint32_t)mask;
+#pragma unroll
+        for (int r = 0; r < 32; r++) acc ^= v[r];
+        nodes6[(size_t)blockIdx.x * 512 + tid] = __uint_as_float(acc);
+        return;
+    }
 
     // ---- leaf: sort the chunk (Arrays.sort total order) and keep every other sample ----
     sort_group256<32>(v, lane);
@@ -141,6 +150,13 @@ __global__ __launch_bounds__(512) void k_leaf(const float* __restrict__ x, int64
         compact_regs<32>(v, w1, odd);
     }
     export_wave_root<16>(w1, lane, 0, wave_c0, wg_c0, rem, roots);
+    if constexpr (STAGE == 1) {
+        uint32_t acc = mn ^ mx ^ fl;
+#pragma unroll
+        for (int r = 0; r < 16; r++) acc ^= w1[r];
+        nodes6[(size_t)blockIdx.x * 512 + tid] = __uint_as_float(acc);
+        return;
+    }
 
     // In-register bitonic merges equal the reference merge (IEEE `<`, ties -> newer run) unless
     // the wave's values contain both -0.0 and +0.0; then take the exact LDS path.
@@ -180,6 +196,10 @@ __global__ __launch_bounds__(512) void k_leaf(const float* __restrict__ x, int64
         } else {
             wave_exact_level<4>(w3, w4, lane, odd, fb);
         }
+    }
+    if constexpr (STAGE == 2) {
+        nodes6[(size_t)blockIdx.x * 512 + tid] = __uint_as_float(w4[0] ^ w4[1] ^ mn ^ mx ^ fl);
+        return;
     }
     sh.wn[wave][lane * 2] = __uint_as_float(key2f(w4[0]));
     sh.wn[wave][lane * 2 + 1] = __uint_as_float(key2f(w4[1]));
@@ -241,8 +261,24 @@ hipError_t launch_leaf(hipStream_t st, const float* x, int64_t chunks, uint64_t 
                        const uint64_t* jump_tab, LeafPartial* part, float* nodes6, float* roots) {
     const int64_t nwg = (chunks + kLeafChunks - 1) / kLeafChunks;
     if (nwg <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_leaf, dim3((unsigned)nwg), dim3(512), 0, st, x, chunks, s0, jump_tab, part,
-                       nodes6, roots);
+    hipLaunchKernelGGL(k_leaf<3>, dim3((unsigned)nwg), dim3(512), 0, st, x, chunks, s0, jump_tab,
+                       part, nodes6, roots);
+    return hipGetLastError();
+}
+
+// Profiling ablation: stage 0 = load + keys, 1 = + leaf sort/compaction, 2 = + in-wave merges,
+// 3 = full kernel.  `scratch` must hold nwg * 512 floats.
+hipError_t launch_leaf_stage(hipStream_t st, int stage, const float* x, int64_t chunks, uint64_t s0,
+                             const uint64_t* jump_tab, LeafPartial* part, float* scratch, float* roots) {
+    const int64_t nwg = (chunks + kLeafChunks - 1) / kLeafChunks;
+    if (nwg <= 0) return hipSuccess;
+    dim3 g((unsigned)nwg), b(512);
+    switch (stage) {
+        case 0: hipLaunchKernelGGL(k_leaf<0>, g, b, 0, st, x, chunks, s0, jump_tab, part, scratch, roots); break;
+        case 1: hipLaunchKernelGGL(k_leaf<1>, g, b, 0, st, x, chunks, s0, jump_tab, part, scratch, roots); break;
+        case 2: hipLaunchKernelGGL(k_leaf<2>, g, b, 0, st, x, chunks, s0, jump_tab, part, scratch, roots); break;
+        default: hipLaunchKernelGGL(k_leaf<3>, g, b, 0, st, x, chunks, s0, jump_tab, part, scratch, roots); break;
+    }
     return hipGetLastError();
 }
 

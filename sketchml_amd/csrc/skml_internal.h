@@ -60,6 +60,8 @@ __host__ __device__ inline size_t dense_codes_offset(int req_bins) {
 // ---- kernel launchers (skml_dense.hip) ----
 hipError_t launch_leaf(hipStream_t st, const float* x, int64_t chunks, uint64_t s0,
                        const uint64_t* jump_tab, LeafPartial* part, float* nodes6, float* roots);
+hipError_t launch_leaf_stage(hipStream_t st, int stage, const float* x, int64_t chunks, uint64_t s0,
+                             const uint64_t* jump_tab, LeafPartial* part, float* scratch, float* roots);
 hipError_t launch_merge_pass(hipStream_t st, const MergePass& pass, const float* src, float* dst,
                              float* roots, uint64_t s0, const uint64_t* jump_tab);
 hipError_t launch_summary(hipStream_t st, const float* x, int64_t n, const LeafPartial* part,
