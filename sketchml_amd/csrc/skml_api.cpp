@@ -99,6 +99,7 @@ void end_timer(KernelTimer* t) { delete t; }
 namespace {
 
 struct Workspace {
+    unsigned* done;  // arrival counter of the fused summary (always at offset 0, self-resetting)
     LeafPartial* part;
     float* nodes6;
     float* roots;
@@ -118,6 +119,7 @@ size_t ws_layout(int64_t chunks, Workspace* w, char* base) {
         return base ? (void*)(base + o) : nullptr;
     };
     Workspace t;
+    t.done = (unsigned*)take(256);
     t.part = (LeafPartial*)take(sizeof(LeafPartial) * (size_t)(nwg + 1));
     t.nodes6 = (float*)take(sizeof(float) * kK * (size_t)(full + 1));
     t.roots = (float*)take(sizeof(float) * kK * kMaxLevels);
@@ -135,6 +137,7 @@ int ensure_ws(skml_ctx* ctx, int64_t chunks, Workspace* w) {
         ctx->ws = nullptr;
         size_t cap = need + need / 4;
         HIP_TRY(hipMalloc(&ctx->ws, cap));
+        HIP_TRY(hipMemset(ctx->ws, 0, 256));
         ctx->ws_cap = cap;
     }
     ws_layout(chunks, w, (char*)ctx->ws);
@@ -387,6 +390,7 @@ int skml_dense_encode_f32(skml_ctx* c, const float* x, int64_t n, const skml_par
     const uint64_t s0 = ((uint64_t)p->seed ^ kLcgMult) & kLcgMask;
     const int64_t nwg = (chunks + kLeafChunks - 1) / kLeafChunks;
 
+    bool fused = false;
     if (chunks > 0) {
         {
             KernelTimer kt(c, SKML_K_LEAF);
@@ -404,8 +408,7 @@ int skml_dense_encode_f32(skml_ctx* c, const float* x, int64_t n, const skml_par
             t.src = t.chunk_base >> kLeafTopLevel;
             trees.push_back(t);
         }
-        const float* src = w.nodes6;
-        float* dst = w.upA;
+        std::vector<MergePass> passes;
         while (true) {
             MergePass pass;
             std::memset(&pass, 0, sizeof(pass));
@@ -432,15 +435,22 @@ int skml_dense_encode_f32(skml_ctx* c, const float* x, int64_t n, const skml_par
             }
             if (pass.njobs == 0) break;
             pass.wg_prefix[pass.njobs] = wg;
-            {
-                KernelTimer kt(c, SKML_K_MERGE);
-                HIP_TRY(launch_merge_pass(c->stream, pass, src, dst, w.roots, s0, c->jump_tab));
-            }
+            passes.push_back(pass);
+        }
+        if (!passes.empty()) passes.back().fuse_summary = 1;
+        const float* src = w.nodes6;
+        float* dst = w.upA;
+        for (const MergePass& pass : passes) {
+            KernelTimer kt(c, SKML_K_MERGE);
+            HIP_TRY(launch_merge_pass(c->stream, pass, src, dst, w.roots, s0, c->jump_tab, w.done, x, n,
+                                      w.part, nwg, c->ranks, p->bin_num, p->dedup ? 1 : 0, payload,
+                                      w.raw));
             src = dst;
             dst = (dst == w.upA) ? w.upB : w.upA;
         }
+        fused = !passes.empty();
     }
-    {
+    if (!fused) {
         KernelTimer kt(c, SKML_K_SUMMARY);
         HIP_TRY(launch_summary(c->stream, x, n, w.part, nwg, w.roots, c->ranks, p->bin_num,
                                p->dedup ? 1 : 0, payload, w.raw));

@@ -142,10 +142,13 @@ __device__ __forceinline__ void sort_group256(uint32_t (&v)[R], int lane) {
 
 // Keep every other sorted position: parity `odd` is the compaction RNG bit
 // (QSketchUtils.compactBuffer, QSketchUtils.java:45-51).
+// (Written as a bit-select: `odd ? v[2j+1] : v[2j]` is turned into a dynamically indexed
+// private array -- i.e. scratch memory -- by hipcc.)
 template <int R>
 __device__ __forceinline__ void compact_regs(const uint32_t (&v)[R], uint32_t (&w)[R / 2], bool odd) {
+    const uint32_t m = odd ? 0xFFFFFFFFu : 0u;
 #pragma unroll
-    for (int j = 0; j < R / 2; j++) w[j] = odd ? v[2 * j + 1] : v[2 * j];
+    for (int j = 0; j < R / 2; j++) w[j] = (v[2 * j + 1] & m) | (v[2 * j] & ~m);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -43,6 +43,7 @@ constexpr int kMaxJobs = 24;
 struct MergePass {
     MergeJob job[kMaxJobs];
     int32_t njobs;
+    int32_t fuse_summary;  // last pass: its last workgroup also runs the summary
     int32_t wg_prefix[kMaxJobs + 1];
 };
 
@@ -57,13 +58,17 @@ __host__ __device__ inline size_t dense_codes_offset(int req_bins) {
     return align_up(kHeaderBytes + 8 * (size_t)(req_bins - 1), 256);
 }
 
-// ---- kernel launchers (skml_dense.hip) ----
+// ---- kernel launchers (skml_sketch.hip) ----
 hipError_t launch_leaf(hipStream_t st, const float* x, int64_t chunks, uint64_t s0,
                        const uint64_t* jump_tab, LeafPartial* part, float* nodes6, float* roots);
 hipError_t launch_leaf_stage(hipStream_t st, int stage, const float* x, int64_t chunks, uint64_t s0,
                              const uint64_t* jump_tab, LeafPartial* part, float* scratch, float* roots);
 hipError_t launch_merge_pass(hipStream_t st, const MergePass& pass, const float* src, float* dst,
-                             float* roots, uint64_t s0, const uint64_t* jump_tab);
+                             float* roots, uint64_t s0, const uint64_t* jump_tab, unsigned* done,
+                             const float* x, int64_t n, const LeafPartial* part, int64_t nparts,
+                             const int64_t* ranks, int req_bins, int dedup, void* payload,
+                             double* scratch_raw);
+// ---- kernel launchers (skml_dense.hip) ----
 hipError_t launch_summary(hipStream_t st, const float* x, int64_t n, const LeafPartial* part,
                           int64_t nparts, const float* roots, const int64_t* ranks, int req_bins,
                           int dedup, void* payload, double* scratch_raw);

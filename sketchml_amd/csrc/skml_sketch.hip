@@ -1,0 +1,786 @@
+// skml_sketch.hip -- CDNA4 (gfx950) kernels building the k=128 quantile sketch of an fp32 bucket.
+//
+// The reference sketch (HeapQuantileSketch.java) is a fixed binary merge tree over 256-value
+// chunks: each chunk is sorted (Arrays.sort total order) and compacted to 128 samples with one
+// RNG bit (fullBaseBufferPropagation, HeapQuantileSketch.java:107-124; compactBuffer,
+// QSketchUtils.java:45-51); node (level L+1) = compact(merge(older level-L node, newer one))
+// (levelwisePropagation / mergeArrays, QSketchUtils.java:53-82).  The bit used by the node at
+// `level` whose last chunk is c is draw #(2c - popcount(c) + level) of java.util.Random(seed).
+//
+//   k_leaf    one pass over the bucket.  512 threads = 8 waves; wave w owns 8 chunks as 32 keys
+//             per lane (8 lanes per chunk).  In registers: bitonic sort of every chunk +
+//             compaction, then tree levels 1..3 (bitonic merges, DPP / swizzle exchanges); levels
+//             4..6 across waves via LDS.  Output: one level-6 node per 64 chunks.
+//   k_merge   64 nodes of level L -> one node of level L+6 with the same machinery; the last
+//             workgroup of the last pass also runs the summary (makeSummary + getQuantiles +
+//             Maths.unique + findZeroIdx, HeapQuantileSketch.java:126-174,293-323,
+//             Maths.java:51-67, Quantizer.java:74-85) and writes the payload header.
+//   k_summary the summary alone (buckets with < 128 chunks).
+//
+// Bitonic merges sort by total-order key; they equal the reference merge (IEEE `<`, ties emit
+// the newer run) unless a merge sees both -0.0 and +0.0, in which case that workgroup takes the
+// exact LDS path (count-based merge positions with the reference tie rule).
+#include "skml_device.hpp"
+
+namespace skml {
+
+// =============================================================================================
+// shared memory
+// =============================================================================================
+struct TileShared {
+    float fb[kLeafWaves][1024];  // per-wave exact-merge area (mixed +/-0 only)
+    float wn[kLeafWaves][kK];    // level L0+3 node of each wave
+    float l4[4][kK];
+    float l5[2][kK];
+    float l6[kK];
+    uint64_t mask[kLeafWaves];   // leaf: RNG draws [start, start+64) of each wave's chunks
+    uint64_t start[kLeafWaves];
+    uint32_t wgbits;             // bits of the 7 cross-wave merges
+    uint32_t min_key, max_key, flags;
+    int is_last;
+};
+
+constexpr int kSumMaxRaw = 1024;  // raw splits kept in LDS up to this many
+constexpr int kMaxSamples = kMaxLevels * kK + kChunk;
+struct SummaryShared {
+    float smp[kMaxSamples];      // gathered runs
+    float sorted[kMaxSamples];   // samplesArr after blockyMergeSort
+    int64_t w[kMaxSamples + 1];  // weightsArr -> cut points
+    double raw[kSumMaxRaw];      // getQuantiles output before Maths.unique
+    int64_t wsum[16];
+    int run_off[kMaxLevels + 2];
+    int run_lvl[kMaxLevels + 2];
+    int nruns;
+    uint32_t min_key, max_key, flags;
+    int zero;
+    int64_t total;
+};
+
+union MergeShared {
+    TileShared t;
+    SummaryShared s;
+};
+
+// =============================================================================================
+// in-wave tree levels (input: 8 nodes of 128 keys, 8 lanes x 16 keys per node)
+// =============================================================================================
+
+// Exact path for one in-wave merge level (R keys / lane, G = 256/R lanes per merge group).
+template <int R>
+__device__ __forceinline__ void wave_exact_level(uint32_t (&v)[R], uint32_t (&w)[R / 2], int lane,
+                                                 uint32_t odd, float* fb) {
+    constexpr int G = 256 / R;
+    const int grp = lane / G, li = lane % G;
+    float* run = fb + grp * 256;
+#pragma unroll
+    for (int r = 0; r < R; r++) run[li * R + r] = __uint_as_float(key2f(v[r]));
+    int pos[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const int p = li * R + r;
+        const float x = __uint_as_float(key2f(v[r]));
+        pos[r] = p < 128 ? p + count_le(run + 128, x) : (p - 128) + count_lt(run, x);
+    }
+    float* out = fb + grp * 128;  // in place: every read of this wave precedes every write
+#pragma unroll
+    for (int r = 0; r < R; r++)
+        if (((uint32_t)pos[r] & 1u) == odd) out[pos[r] >> 1] = __uint_as_float(key2f(v[r]));
+#pragma unroll
+    for (int j = 0; j < R / 2; j++) w[j] = f2key(__float_as_uint(out[li * (R / 2) + j]));
+}
+
+template <int R>
+__device__ __forceinline__ void wave_level(uint32_t (&v)[R], uint32_t (&w)[R / 2], int lane,
+                                           uint32_t odd, bool exact, float* fb) {
+    if (!exact) {
+        merge_group<R>(v, lane);
+        compact_regs<R>(v, w, odd);
+    } else {
+        wave_exact_level<R>(v, w, lane, odd, fb);
+    }
+}
+
+// Write the node held by lanes [g*G, g*G+G) (R keys per lane) as 128 floats.
+template <int R>
+__device__ __forceinline__ void store_node(const uint32_t (&w)[R], int lane, float* dst) {
+    constexpr int G = kK / R;
+    const int li = lane % G;
+#pragma unroll
+    for (int r = 0; r < R; r++) dst[li * R + r] = __uint_as_float(key2f(w[r]));
+}
+
+// Levels +1..+3 inside a wave.  bits: 0..3 -> level+1 nodes, 4..5 -> level+2, 6 -> level+3.
+// Exp(level_offset, node_in_wave, regs...) is called after each level for root exports.
+template <class Exp>
+__device__ __forceinline__ void inwave_levels(uint32_t (&w1)[16], uint32_t (&w4)[2], int lane,
+                                              uint32_t bits, bool exact, float* fb, Exp&& exp) {
+    uint32_t w2[8], w3[4];
+    wave_level<16>(w1, w2, lane, (bits >> (lane >> 4)) & 1u, exact, fb);
+    exp.template at<8>(1, lane >> 4, w2);
+    wave_level<8>(w2, w3, lane, (bits >> (4 + (lane >> 5))) & 1u, exact, fb);
+    exp.template at<4>(2, lane >> 5, w3);
+    wave_level<4>(w3, w4, lane, (bits >> 6) & 1u, exact, fb);
+    exp.template at<2>(3, 0, w4);
+}
+
+// One wave merges two 128-float nodes from LDS into `out` (bitonic, 64 lanes x 4 keys).
+__device__ __forceinline__ void wave_pair_merge(const float* A, const float* B, float* out, int lane,
+                                                uint32_t odd) {
+    const float4 f = lane < 32 ? reinterpret_cast<const float4*>(A)[lane]
+                               : reinterpret_cast<const float4*>(B)[lane - 32];
+    uint32_t v[4] = {f2key(__float_as_uint(f.x)), f2key(__float_as_uint(f.y)),
+                     f2key(__float_as_uint(f.z)), f2key(__float_as_uint(f.w))};
+    merge_group<4>(v, lane);
+    uint32_t o[2];
+    compact_regs<4>(v, o, odd);
+    reinterpret_cast<float2*>(out)[lane] = make_float2(__uint_as_float(key2f(o[0])), __uint_as_float(key2f(o[1])));
+}
+
+// Levels +4..+6 across the 8 waves.  bits: 0..3 level+4, 4..5 level+5, 6 level+6.
+__device__ __forceinline__ void crosswave_levels(TileShared& sh, int tid, uint32_t bits, bool exact) {
+    const int wave = tid >> 6, lane = tid & 63;
+    if (!exact) {
+        if (wave < 4) wave_pair_merge(sh.wn[2 * wave], sh.wn[2 * wave + 1], sh.l4[wave], lane, (bits >> wave) & 1u);
+    } else {
+        for (int task = tid; task < 4 * 256; task += 512) {
+            const int m = task >> 8;
+            exact_merge_task(sh.wn[2 * m], sh.wn[2 * m + 1], sh.l4[m], task & 255, (bits >> m) & 1u);
+        }
+    }
+    __syncthreads();
+    if (!exact) {
+        if (wave < 2) wave_pair_merge(sh.l4[2 * wave], sh.l4[2 * wave + 1], sh.l5[wave], lane, (bits >> (4 + wave)) & 1u);
+    } else {
+        const int m = tid >> 8;
+        exact_merge_task(sh.l4[2 * m], sh.l4[2 * m + 1], sh.l5[m], tid & 255, (bits >> (4 + m)) & 1u);
+    }
+    __syncthreads();
+    if (!exact) {
+        if (wave == 0) wave_pair_merge(sh.l5[0], sh.l5[1], sh.l6, lane, (bits >> 6) & 1u);
+    } else if (tid < 256) {
+        exact_merge_task(sh.l5[0], sh.l5[1], sh.l6, tid, (bits >> 6) & 1u);
+    }
+    __syncthreads();
+}
+
+// =============================================================================================
+// Leaf kernel
+// =============================================================================================
+struct NoExport {
+    template <int R>
+    __device__ void at(int, int, const uint32_t (&)[R]) const {}
+};
+
+// Roots of the small trees (chunks mod 64) in the last, partial leaf workgroup.
+struct LeafExport {
+    int lane, rem;
+    int64_t wave_off;  // first chunk of the wave, relative to the workgroup
+    float* roots;
+    template <int R>
+    __device__ __forceinline__ void at(int level, int node, const uint32_t (&w)[R]) const {
+        if (!rem || !((rem >> level) & 1)) return;
+        const int64_t cs = ((int64_t)rem >> (level + 1)) << (level + 1);
+        if (wave_off + ((int64_t)node << level) != cs) return;
+        store_node<R>(w, lane, roots + (size_t)level * kK);
+    }
+};
+
+template <int STAGE, int MINW = 1>
+__global__ __launch_bounds__(512, MINW) void k_leaf(const float* __restrict__ x, int64_t chunks,
+                                              uint64_t s0, const uint64_t* __restrict__ tab,
+                                              LeafPartial* __restrict__ part,
+                                              float* __restrict__ nodes6,
+                                              float* __restrict__ roots) {
+    __shared__ TileShared sh;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int64_t wg_c0 = (int64_t)blockIdx.x * kLeafChunks;
+    const int64_t wave_c0 = wg_c0 + wave * kChunksPerWave;
+    const int64_t chunk = wave_c0 + (lane >> 3);
+    const int rem = (wg_c0 + kLeafChunks > chunks) ? (int)(chunks - wg_c0) : 0;
+    const bool valid = chunk < chunks;
+
+    if (tid == 0) {
+        sh.min_key = 0xFFFFFFFFu;
+        sh.max_key = 0u;
+        sh.flags = 0u;
+    }
+    __syncthreads();
+
+    // ---- load 32 values: 8 x float4, each 8-lane group reads a full 128-B line per load ----
+    uint32_t v[32];
+    uint32_t mn = 0xFFFFFFFFu, mx = 0u, fl = 0u;
+    {
+        const float4* src = reinterpret_cast<const float4*>(x + (valid ? chunk : 0) * kChunk);
+        float4 f[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) f[j] = src[j * 8 + (lane & 7)];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint32_t b[4] = {__float_as_uint(f[j].x), __float_as_uint(f[j].y),
+                                   __float_as_uint(f[j].z), __float_as_uint(f[j].w)};
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                fl |= is_nan_bits(b[e]) ? 1u : 0u;
+                fl |= (b[e] == 0x80000000u) ? 2u : 0u;
+                fl |= (b[e] == 0u) ? 4u : 0u;
+                const uint32_t k = f2key(b[e]);
+                mn = k < mn ? k : mn;
+                mx = k > mx ? k : mx;
+                v[j * 4 + e] = k;
+            }
+        }
+        if (!valid) fl = 0u;
+    }
+
+    // ---- compaction bits for the wave's chunks: lane l computes draw #(start + l) ----
+    const uint64_t start = node_bit_index((uint64_t)wave_c0, 0);
+    uint64_t mask;
+    {
+        const uint64_t s_start = lcg_jump(tab, s0, start + 1);
+        const uint64_t a = tab[lane * 2], c = tab[lane * 2 + 1];  // level-0 table: A^lane, C_lane
+        const uint64_t s = (lane == 0) ? s_start : ((a * s_start + c) & kLcgMask);
+        mask = __ballot((s >> 47) & 1ull);
+    }
+    if (lane == 0) {
+        sh.mask[wave] = mask;
+        sh.start[wave] = start;
+    }
+    if constexpr (STAGE == 0) {
+        uint32_t acc = mn ^ mx ^ fl ^ (uint32_t)mask;
+#pragma unroll
+        for (int r = 0; r < 32; r++) acc ^= v[r];
+        nodes6[(size_t)blockIdx.x * 512 + tid] = __uint_as_float(acc);
+        return;
+    }
+
+    // ---- leaf: sort the chunk (Arrays.sort total order) and keep every other sample ----
+    sort_group256<32>(v, lane);
+    uint32_t w1[16];
+    compact_regs<32>(v, w1, (uint32_t)(mask >> (node_bit_index((uint64_t)chunk, 0) - start)) & 1u);
+    const LeafExport exp{lane, rem, wave * kChunksPerWave, roots};
+    exp.at<16>(0, lane >> 3, w1);
+    if constexpr (STAGE == 1) {
+        uint32_t acc = mn ^ mx ^ fl;
+#pragma unroll
+        for (int r = 0; r < 16; r++) acc ^= w1[r];
+        nodes6[(size_t)blockIdx.x * 512 + tid] = __uint_as_float(acc);
+        return;
+    }
+
+    // ---- tree levels 1..3 in the wave ----
+    uint32_t ibits = 0;
+    {
+        auto bit = [&](int level, int node) -> uint32_t {
+            const uint64_t c = (uint64_t)wave_c0 + ((uint64_t)(node + 1) << level) - 1;
+            return (uint32_t)(mask >> (node_bit_index(c, level) - start)) & 1u;
+        };
+        for (int j = 0; j < 4; j++) ibits |= bit(1, j) << j;
+        ibits |= bit(2, 0) << 4 | bit(2, 1) << 5 | bit(3, 0) << 6;
+    }
+    const bool wexact = (__ballot((fl & 2u) != 0) != 0) && (__ballot((fl & 4u) != 0) != 0);
+    uint32_t w4[2];
+    inwave_levels(w1, w4, lane, ibits, wexact, sh.fb[wave], exp);
+    if constexpr (STAGE == 2) {
+        nodes6[(size_t)blockIdx.x * 512 + tid] = __uint_as_float(w4[0] ^ w4[1] ^ mn ^ mx ^ fl);
+        return;
+    }
+    store_node<2>(w4, lane, sh.wn[wave]);
+    if (valid) {
+        atomicMin(&sh.min_key, mn);
+        atomicMax(&sh.max_key, mx);
+        if (fl) atomicOr(&sh.flags, fl);
+    }
+    __syncthreads();
+
+    // ---- tree levels 4..6 across waves ----
+    uint32_t wbits = 0;
+    {
+        auto bit = [&](int level, int node) -> uint32_t {
+            const int64_t last = wg_c0 + ((int64_t)(node + 1) << level) - 1;
+            const int wv = (int)((last - wg_c0) >> 3);
+            return (uint32_t)(sh.mask[wv] >> (node_bit_index((uint64_t)last, level) - sh.start[wv])) & 1u;
+        };
+        for (int m = 0; m < 4; m++) wbits |= bit(4, m) << m;
+        wbits |= bit(5, 0) << 4 | bit(5, 1) << 5 | bit(6, 0) << 6;
+    }
+    const bool gexact = (sh.flags & 6u) == 6u;
+    crosswave_levels(sh, tid, wbits, gexact);
+
+    if (!rem) {
+        if (tid < kK) {
+            nodes6[(size_t)blockIdx.x * kK + tid] = sh.l6[tid];
+            // a level-6 tree (bit 6 of the chunk count) is this single node
+            if (((chunks >> 6) & 1) && (int64_t)blockIdx.x == ((chunks >> 7) << 1))
+                roots[(size_t)6 * kK + tid] = sh.l6[tid];
+        }
+    } else if (tid < kK) {
+        for (int level = 4; level <= 5; level++) {  // roots of levels 4..5 live in LDS
+            if (!((rem >> level) & 1)) continue;
+            const int cs = (rem >> (level + 1)) << (level + 1);
+            const float* src = level == 4 ? sh.l4[cs >> 4] : sh.l5[cs >> 5];
+            roots[(size_t)level * kK + tid] = src[tid];
+        }
+    }
+    if (tid == 0) {
+        LeafPartial p;
+        p.min_key = sh.min_key;
+        p.max_key = sh.max_key;
+        p.flags = sh.flags;
+        p.pad = 0;
+        part[blockIdx.x] = p;
+    }
+}
+
+hipError_t launch_leaf(hipStream_t st, const float* x, int64_t chunks, uint64_t s0,
+                       const uint64_t* jump_tab, LeafPartial* part, float* nodes6, float* roots) {
+    const int64_t nwg = (chunks + kLeafChunks - 1) / kLeafChunks;
+    if (nwg <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_leaf<3>, dim3((unsigned)nwg), dim3(512), 0, st, x, chunks, s0, jump_tab,
+                       part, nodes6, roots);
+    return hipGetLastError();
+}
+
+// Profiling ablation: stage 0 = load + keys, 1 = + leaf sort/compaction, 2 = + in-wave merges,
+// 3 = full kernel.  `scratch` must hold nwg * 512 floats.
+hipError_t launch_leaf_stage(hipStream_t st, int stage, const float* x, int64_t chunks, uint64_t s0,
+                             const uint64_t* jump_tab, LeafPartial* part, float* scratch, float* roots) {
+    const int64_t nwg = (chunks + kLeafChunks - 1) / kLeafChunks;
+    if (nwg <= 0) return hipSuccess;
+    dim3 g((unsigned)nwg), b(512);
+    switch (stage) {
+        case 0: hipLaunchKernelGGL(k_leaf<0>, g, b, 0, st, x, chunks, s0, jump_tab, part, scratch, roots); break;
+        case 1: hipLaunchKernelGGL(k_leaf<1>, g, b, 0, st, x, chunks, s0, jump_tab, part, scratch, roots); break;
+        case 2: hipLaunchKernelGGL(k_leaf<2>, g, b, 0, st, x, chunks, s0, jump_tab, part, scratch, roots); break;
+        case 3: hipLaunchKernelGGL(k_leaf<3>, g, b, 0, st, x, chunks, s0, jump_tab, part, scratch, roots); break;
+        // occupancy variants: 10 + stage with >= 6 waves / SIMD (<= 80 VGPRs)
+        case 11: hipLaunchKernelGGL((k_leaf<1, 6>), g, b, 0, st, x, chunks, s0, jump_tab, part, scratch, roots); break;
+        case 13: hipLaunchKernelGGL((k_leaf<3, 6>), g, b, 0, st, x, chunks, s0, jump_tab, part, scratch, roots); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// =============================================================================================
+// Summary (one workgroup, any multiple of 64 threads up to 1024)
+// =============================================================================================
+__device__ __forceinline__ int run_count_le(const float* r, int len, float x) {
+    int lo = 0, hi = len;
+    while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        if (r[mid] <= x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+__device__ __forceinline__ int run_count_lt(const float* r, int len, float x) {
+    int lo = 0, hi = len;
+    while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        if (r[mid] < x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// Exclusive block scan of one int64 per thread (wave shuffles + one LDS round).
+__device__ int64_t block_scan_excl(int64_t v, int64_t* wsum, int64_t* total) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, nw = blockDim.x >> 6;
+    int64_t x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int64_t y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    if (w == 0) {
+        int64_t s = lane < nw ? wsum[lane] : 0;
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+            const int64_t y = __shfl_up(s, off, 64);
+            if (lane >= off) s += y;
+        }
+        if (lane < nw) wsum[lane] = s;
+    }
+    __syncthreads();
+    const int64_t base = w > 0 ? wsum[w - 1] : 0;
+    *total = wsum[nw - 1];
+    __syncthreads();
+    return base + x - v;
+}
+
+struct SummaryArgs {
+    const float* x;
+    int64_t n;
+    const LeafPartial* part;
+    int64_t nparts;
+    const float* roots;
+    const int64_t* ranks;
+    uint8_t* payload;
+    double* g_raw;
+    int req_bins;
+    int dedup;
+};
+
+__device__ void summary_block(const SummaryArgs& a, SummaryShared& S) {
+    const int t = threadIdx.x, T = blockDim.x;
+    skml_dense_header* hdr = reinterpret_cast<skml_dense_header*>(a.payload);
+    double* splits = reinterpret_cast<double*>(a.payload + kHeaderBytes);
+    const int64_t n = a.n;
+    const int64_t chunks = n / kChunk;
+    const int tail = (int)(n - chunks * kChunk);
+    const float* xt = a.x + chunks * kChunk;
+    const int req_bins = a.req_bins;
+
+    if (t == 0) {
+        S.min_key = 0xFFFFFFFFu;
+        S.max_key = 0u;
+        S.flags = 0u;
+        S.zero = 0x7FFFFFFF;
+        int nr = 0, off = 0;
+        for (int l = 0; l < kMaxLevels; l++)
+            if ((chunks >> l) & 1) {  // copyBuf2Arr: lowest level first (HeapQuantileSketch.java:151-161)
+                S.run_off[nr] = off;
+                S.run_lvl[nr] = l;
+                nr++;
+                off += kK;
+            }
+        S.run_off[nr] = off;  // tail = base buffer (weight 1)
+        S.run_lvl[nr] = -1;
+        S.run_off[nr + 1] = off + tail;
+        S.nruns = nr + 1;
+    }
+    __syncthreads();
+    // ---- min / max / NaN ----
+    {
+        uint32_t mn = 0xFFFFFFFFu, mx = 0u, fl = 0u;
+        for (int64_t i = t; i < a.nparts; i += T) {
+            const LeafPartial p = a.part[i];
+            mn = p.min_key < mn ? p.min_key : mn;
+            mx = p.max_key > mx ? p.max_key : mx;
+            fl |= p.flags;
+        }
+        for (int i = t; i < tail; i += T) {
+            const uint32_t b = __float_as_uint(xt[i]);
+            fl |= is_nan_bits(b) ? 1u : 0u;
+            const uint32_t k = f2key(b);
+            mn = k < mn ? k : mn;
+            mx = k > mx ? k : mx;
+        }
+        atomicMin(&S.min_key, mn);
+        atomicMax(&S.max_key, mx);
+        if (fl) atomicOr(&S.flags, fl);
+    }
+    // ---- gather runs; the tail is sorted in Arrays.sort total order by rank counting ----
+    const int nruns = S.nruns;
+    const int ns = S.run_off[nruns];
+    for (int r = 0; r + 1 < nruns; r++) {
+        const float* src = a.roots + (size_t)S.run_lvl[r] * kK;
+        for (int i = t; i < kK; i += T) S.smp[S.run_off[r] + i] = src[i];
+    }
+    {
+        const int toff = S.run_off[nruns - 1];
+        for (int i = t; i < tail; i += T) {
+            const uint32_t ki = f2key(__float_as_uint(xt[i]));
+            int rank = 0;
+            for (int j = 0; j < tail; j++) {
+                const uint32_t kj = f2key(__float_as_uint(xt[j]));
+                rank += (kj < ki) || (kj == ki && j < i);
+            }
+            S.smp[toff + rank] = xt[i];
+        }
+    }
+    __syncthreads();
+
+    double vmin = 1.7976931348623157e308, vmax = 4.9e-324;  // HeapQuantileSketch.java:67-68
+    if (n > 0) {
+        const double fmin = (double)__uint_as_float(key2f(S.min_key));
+        const double fmax = (double)__uint_as_float(key2f(S.max_key));
+        if (fmin <= vmin) vmin = fmin;  // Math.min(Double.MAX_VALUE, x)
+        if (fmax > vmax) vmax = fmax;   // Math.max(Double.MIN_VALUE, x)
+    }
+    if (S.flags & 1u) {  // NaN: QuantileSketchException("Encounter NaN value")
+        if (t == 0) {
+            hdr->magic = SKML_DENSE_MAGIC;
+            hdr->status = SKML_E_NAN;
+            hdr->n = n;
+            hdr->bin_num = req_bins;
+            hdr->zero_idx = 0;
+            hdr->code_bits = code_bits_for(req_bins);
+            hdr->req_bins = req_bins;
+            hdr->min = vmin;
+            hdr->max = vmax;
+            hdr->codes_offset = (int64_t)dense_codes_offset(req_bins);
+            hdr->reserved = 0;
+        }
+        return;
+    }
+
+    // ---- blockyMergeSort == stable sort under IEEE `<=` (left run wins ties): rank across runs ----
+    for (int i = t; i < ns; i += T) {
+        int r = 0;
+        while (S.run_off[r + 1] <= i) r++;
+        const float v = S.smp[i];
+        int rank = i - S.run_off[r];
+        for (int q = 0; q < nruns; q++) {
+            if (q == r) continue;
+            const float* run = S.smp + S.run_off[q];
+            const int len = S.run_off[q + 1] - S.run_off[q];
+            rank += q < r ? run_count_le(run, len, v) : run_count_lt(run, len, v);
+        }
+        S.sorted[rank] = v;
+        S.w[rank] = S.run_lvl[r] < 0 ? 1 : ((int64_t)2 << S.run_lvl[r]);
+    }
+    __syncthreads();
+
+    // ---- exclusive prefix of weights (HeapQuantileSketch.java:137-142) ----
+    {
+        const int per = (ns + T - 1) / T;
+        const int b0 = min(ns, t * per), b1 = min(ns, b0 + per);
+        int64_t loc = 0;
+        for (int i = b0; i < b1; i++) loc += S.w[i];
+        const int64_t base = block_scan_excl(loc, S.wsum, &S.total);
+        int64_t acc = base;
+        for (int i = b0; i < b1; i++) {
+            const int64_t wv = S.w[i];
+            S.w[i] = acc;
+            acc += wv;
+        }
+        if (t == 0) S.w[ns] = S.total;
+    }
+    __syncthreads();
+
+    // ---- getQuantiles(int): split_i = samples[max idx with cut[idx] <= rank_i] ----
+    const int nsplit_req = req_bins - 1;
+    const bool lds_raw = nsplit_req <= kSumMaxRaw;
+    double* raw = lds_raw ? S.raw : a.g_raw;
+    for (int i = t; i < nsplit_req; i += T) {
+        double sp;
+        if (ns == 0) {
+            sp = __longlong_as_double(0x7FF8000000000000LL);  // NaN (HeapQuantileSketch.java:299-301)
+        } else {
+            const int64_t rank = a.ranks[i];
+            int lo = 0, hi = ns;
+            while (lo + 1 < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (S.w[mid] <= rank) lo = mid;
+                else hi = mid;
+            }
+            sp = (double)S.sorted[lo];
+        }
+        raw[i] = sp;
+    }
+    if (!lds_raw) __threadfence();
+    __syncthreads();
+
+    // ---- Maths.unique (IEEE !=, keep first) + findZeroIdx ----
+    int bin_num;
+    {
+        const int per = (nsplit_req + T - 1) / T;
+        const int b0 = min(nsplit_req, t * per), b1 = min(nsplit_req, b0 + per);
+        int64_t loc = 0;
+        for (int i = b0; i < b1; i++) loc += (!a.dedup || i == 0 || raw[i] != raw[i - 1]) ? 1 : 0;
+        const int64_t base = block_scan_excl(loc, S.wsum, &S.total);
+        int64_t o = base;
+        for (int i = b0; i < b1; i++) {
+            if (!a.dedup || i == 0 || raw[i] != raw[i - 1]) {
+                const double sp = raw[i];
+                splits[o] = sp;
+                if (!(sp < 0.0)) atomicMin(&S.zero, (int)o);
+                o++;
+            }
+        }
+        bin_num = (int)S.total + 1;
+    }
+    __syncthreads();
+    if (t == 0) {
+        int zero;
+        if (vmin > 0.0) zero = 0;
+        else if (vmax < 0.0) zero = bin_num - 1;
+        else zero = S.zero < bin_num - 1 ? S.zero : bin_num - 1;
+        hdr->magic = SKML_DENSE_MAGIC;
+        hdr->status = SKML_OK;
+        hdr->n = n;
+        hdr->bin_num = bin_num;
+        hdr->zero_idx = zero;
+        hdr->code_bits = code_bits_for(bin_num);
+        hdr->req_bins = req_bins;
+        hdr->min = vmin;
+        hdr->max = vmax;
+        hdr->codes_offset = (int64_t)dense_codes_offset(req_bins);
+        hdr->reserved = 0;
+    }
+}
+
+__global__ __launch_bounds__(512) void k_summary(SummaryArgs a) {
+    __shared__ SummaryShared S;
+    summary_block(a, S);
+}
+
+hipError_t launch_summary(hipStream_t st, const float* x, int64_t n, const LeafPartial* part,
+                          int64_t nparts, const float* roots, const int64_t* ranks, int req_bins,
+                          int dedup, void* payload, double* scratch_raw) {
+    SummaryArgs a{x, n, part, nparts, roots, ranks, reinterpret_cast<uint8_t*>(payload), scratch_raw,
+                  req_bins, dedup};
+    hipLaunchKernelGGL(k_summary, dim3(1), dim3(512), 0, st, a);
+    return hipGetLastError();
+}
+
+// =============================================================================================
+// Upper merge levels: each workgroup merges 2^g (g <= 6) consecutive level-L nodes of one tree.
+// Input nodes are placed like leaf chunks (8 per wave, 8 lanes x 16 keys per node); missing
+// nodes (g < 6) are padding whose merges are never exported.
+// =============================================================================================
+struct MergeExport {
+    int lane, wave, g;
+    float* out;
+    template <int R>
+    __device__ __forceinline__ void at(int level, int node, const uint32_t (&w)[R]) const {
+        if (level == g && wave == 0 && node == 0) store_node<R>(w, lane, out);
+    }
+};
+
+__global__ __launch_bounds__(512) void k_merge(MergePass pass, const float* __restrict__ src,
+                                               float* __restrict__ dst, float* __restrict__ roots,
+                                               uint64_t s0, const uint64_t* __restrict__ tab,
+                                               unsigned* __restrict__ done, SummaryArgs sa) {
+    __shared__ MergeShared U;
+    TileShared& sh = U.t;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    int j = 0;
+    while (j + 1 < pass.njobs && (int)blockIdx.x >= pass.wg_prefix[j + 1]) j++;
+    const MergeJob job = pass.job[j];
+    const int grp = (int)blockIdx.x - pass.wg_prefix[j];
+    const int g = job.group_log, L = job.level_in;
+    const int nodes = 1 << g;
+    const int64_t node0 = job.src_node + ((int64_t)grp << g);
+    const int64_t chunk0 = job.chunk_base + ((int64_t)grp << (g + L));
+    float* out = job.root_level >= 0 ? roots + (size_t)job.root_level * kK
+                                     : dst + (size_t)(job.dst_node + grp) * kK;
+    if (tid == 0) sh.flags = 0u;
+    __syncthreads();
+
+    // ---- load: node nd = 8*wave + lane/8, 16 floats per lane ----
+    const int nd = wave * 8 + (lane >> 3);
+    const bool valid = nd < nodes;
+    uint32_t w1[16];
+    uint32_t fl = 0;
+    {
+        const float4* p = reinterpret_cast<const float4*>(src + (size_t)(node0 + (valid ? nd : 0)) * kK) +
+                          (lane & 7) * 4;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const float4 f = p[q];
+            const uint32_t b[4] = {__float_as_uint(f.x), __float_as_uint(f.y), __float_as_uint(f.z),
+                                   __float_as_uint(f.w)};
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                fl |= (b[e] == 0x80000000u) ? 2u : 0u;
+                fl |= (b[e] == 0u) ? 4u : 0u;
+                w1[q * 4 + e] = valid ? f2key(b[e]) : 0xFFFFFFFFu;
+            }
+        }
+        if (!valid) fl = 0;
+    }
+    // ---- RNG bits: lane k < 7 computes one in-wave merge bit; wave 0 also the 7 cross-wave ones ----
+    auto node_bit = [&](int level_off, int last_node) -> uint32_t {
+        const uint64_t c = (uint64_t)chunk0 + ((uint64_t)(last_node + 1) << L) - 1;
+        return lcg_bit(tab, s0, node_bit_index(c, L + level_off));
+    };
+    uint32_t ibits;
+    {
+        uint32_t b = 0;
+        if (lane < 4) b = node_bit(1, wave * 8 + 2 * lane + 1);
+        else if (lane < 6) b = node_bit(2, wave * 8 + 4 * (lane - 4) + 3);
+        else if (lane == 6) b = node_bit(3, wave * 8 + 7);
+        else if (wave == 0 && lane >= 8 && lane < 12) b = node_bit(4, 16 * (lane - 8) + 15);
+        else if (wave == 0 && lane >= 12 && lane < 14) b = node_bit(5, 32 * (lane - 12) + 31);
+        else if (wave == 0 && lane == 14) b = node_bit(6, 63);
+        const uint64_t m = __ballot(b != 0);
+        ibits = (uint32_t)m & 0x7Fu;
+        if (wave == 0 && lane == 0) sh.wgbits = (uint32_t)(m >> 8) & 0x7Fu;
+    }
+    if (fl) atomicOr(&sh.flags, fl);
+    const bool wexact = (__ballot((fl & 2u) != 0) != 0) && (__ballot((fl & 4u) != 0) != 0);
+    const MergeExport exp{lane, wave, g, out};
+    uint32_t w4[2];
+    inwave_levels(w1, w4, lane, ibits, wexact, sh.fb[wave], exp);
+    store_node<2>(w4, lane, sh.wn[wave]);
+    __syncthreads();
+    if (g >= 4) {
+        crosswave_levels(sh, tid, sh.wgbits, (sh.flags & 6u) == 6u);
+        if (tid < kK) out[tid] = g == 4 ? sh.l4[0][tid] : (g == 5 ? sh.l5[0][tid] : sh.l6[tid]);
+    }
+    if (!pass.fuse_summary) return;
+
+    // ---- last workgroup of the last pass: summary (release/acquire per Guideline 16) ----
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned old = atomicAdd(done, 1u);
+        const int last = old == (unsigned)(pass.wg_prefix[pass.njobs] - 1);
+        if (last) {
+            *done = 0u;  // reset for the next encode
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        sh.is_last = last;
+    }
+    __syncthreads();
+    if (!sh.is_last) return;
+    __syncthreads();
+    summary_block(sa, U.s);
+}
+
+hipError_t launch_merge_pass(hipStream_t st, const MergePass& pass, const float* src, float* dst,
+                             float* roots, uint64_t s0, const uint64_t* jump_tab, unsigned* done,
+                             const float* x, int64_t n, const LeafPartial* part, int64_t nparts,
+                             const int64_t* ranks, int req_bins, int dedup, void* payload,
+                             double* scratch_raw) {
+    const int nwg = pass.wg_prefix[pass.njobs];
+    if (nwg <= 0) return hipSuccess;
+    SummaryArgs a{x, n, part, nparts, roots, ranks, reinterpret_cast<uint8_t*>(payload), scratch_raw,
+                  req_bins, dedup};
+    hipLaunchKernelGGL(k_merge, dim3(nwg), dim3(512), 0, st, pass, src, dst, roots, s0, jump_tab, done, a);
+    return hipGetLastError();
+}
+
+// Split-injected parity mode: header from caller splits (Quantizer.findZeroIdx rule).
+__global__ void k_set_splits(uint8_t* payload, int64_t n, const double* __restrict__ sp, int nsplits,
+                             double mn, double mx, int req_bins) {
+    skml_dense_header* hdr = reinterpret_cast<skml_dense_header*>(payload);
+    double* splits = reinterpret_cast<double*>(payload + kHeaderBytes);
+    __shared__ int s_zero;
+    if (threadIdx.x == 0) s_zero = 0x7FFFFFFF;
+    __syncthreads();
+    for (int i = threadIdx.x; i < nsplits; i += blockDim.x) {
+        splits[i] = sp[i];
+        if (!(sp[i] < 0.0)) atomicMin(&s_zero, i);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int bins = nsplits + 1;
+        hdr->magic = SKML_DENSE_MAGIC;
+        hdr->status = SKML_OK;
+        hdr->n = n;
+        hdr->bin_num = bins;
+        hdr->zero_idx = mn > 0.0 ? 0 : (mx < 0.0 ? bins - 1 : (s_zero < bins - 1 ? s_zero : bins - 1));
+        hdr->code_bits = code_bits_for(bins);
+        hdr->req_bins = req_bins;
+        hdr->min = mn;
+        hdr->max = mx;
+        hdr->codes_offset = (int64_t)dense_codes_offset(req_bins);
+        hdr->reserved = 0;
+    }
+}
+
+hipError_t launch_set_splits(hipStream_t st, void* payload, int64_t n, const double* splits_dev,
+                             int nsplits, double mn, double mx, int req_bins) {
+    hipLaunchKernelGGL(k_set_splits, dim3(1), dim3(256), 0, st, reinterpret_cast<uint8_t*>(payload),
+                       n, splits_dev, nsplits, mn, mx, req_bins);
+    return hipGetLastError();
+}
+
+}  // namespace skml
