@@ -80,28 +80,35 @@ __device__ __forceinline__ void halfclean_regs(uint32_t (&v)[R]) {
     }
 }
 
+// Cross-lane compare-exchange in one VALU op: the lower lane of a pair keeps min(a, b), the
+// upper lane max(a, b), i.e. med3(a, b, sel) with sel = 0 (lower) or ~0 (upper).  The pattern
+// below compiles to a single v_med3_u32.
+__device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
+    return min(max(a, b), max(min(a, b), c));
+}
+
 // Flip stage across a block of (M+1) lanes: element (lane, r) meets (lane^M, R-1-r).
 template <int R, int M>
 __device__ __forceinline__ void flip_lanes(uint32_t (&v)[R], int lane) {
-    const bool lower = (lane & ((M + 1) >> 1)) == 0;
+    const uint32_t sel = (lane & ((M + 1) >> 1)) ? 0xFFFFFFFFu : 0u;
 #pragma unroll
     for (int r = 0; r < R / 2; r++) {
-        uint32_t pa = lane_xor<M>(v[R - 1 - r]);
-        uint32_t pb = lane_xor<M>(v[r]);
-        uint32_t a = v[r], b = v[R - 1 - r];
-        v[r] = lower ? (a < pa ? a : pa) : (a < pa ? pa : a);
-        v[R - 1 - r] = lower ? (b < pb ? b : pb) : (b < pb ? pb : b);
+        const uint32_t pa = lane_xor<M>(v[R - 1 - r]);
+        const uint32_t pb = lane_xor<M>(v[r]);
+        v[r] = umed3(v[r], pa, sel);
+        v[R - 1 - r] = umed3(v[R - 1 - r], pb, sel);
+        // keep the scheduler from hoisting every exchange of the stage (register pressure)
+        if ((r & 3) == 3) __builtin_amdgcn_sched_barrier(0);
     }
 }
 
 template <int R, int D>
 __device__ __forceinline__ void halfclean_lanes(uint32_t (&v)[R], int lane) {
-    const bool lower = (lane & D) == 0;
+    const uint32_t sel = (lane & D) ? 0xFFFFFFFFu : 0u;
 #pragma unroll
     for (int r = 0; r < R; r++) {
-        uint32_t p = lane_xor<D>(v[r]);
-        uint32_t a = v[r];
-        v[r] = lower ? (a < p ? a : p) : (a < p ? p : a);
+        v[r] = umed3(v[r], lane_xor<D>(v[r]), sel);
+        if ((r & 7) == 7) __builtin_amdgcn_sched_barrier(0);
     }
 }
 

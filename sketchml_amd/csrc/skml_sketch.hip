@@ -27,8 +27,9 @@ namespace skml {
 // =============================================================================================
 // shared memory
 // =============================================================================================
+constexpr int kWaveFb = 1536;  // per-wave exact-merge area, floats
 struct TileShared {
-    float fb[kLeafWaves][1024];  // per-wave exact-merge area (mixed +/-0 only)
+    float fb[kLeafWaves][kWaveFb];  // per-wave exact-merge area (mixed +/-0 only)
     float wn[kLeafWaves][kK];    // level L0+3 node of each wave
     float l4[4][kK];
     float l5[2][kK];
@@ -66,25 +67,24 @@ union MergeShared {
 // =============================================================================================
 
 // Exact path for one in-wave merge level (R keys / lane, G = 256/R lanes per merge group).
+// fb holds 1536 floats: runs in [0, 1024), merged nodes in [1024, 1536).  The element loop is
+// kept rolled and reads back from LDS so this rare path adds no register pressure.
 template <int R>
 __device__ __forceinline__ void wave_exact_level(uint32_t (&v)[R], uint32_t (&w)[R / 2], int lane,
                                                  uint32_t odd, float* fb) {
     constexpr int G = 256 / R;
     const int grp = lane / G, li = lane % G;
     float* run = fb + grp * 256;
+    float* out = fb + 1024 + grp * 128;
 #pragma unroll
     for (int r = 0; r < R; r++) run[li * R + r] = __uint_as_float(key2f(v[r]));
-    int pos[R];
-#pragma unroll
+#pragma unroll 1
     for (int r = 0; r < R; r++) {
         const int p = li * R + r;
-        const float x = __uint_as_float(key2f(v[r]));
-        pos[r] = p < 128 ? p + count_le(run + 128, x) : (p - 128) + count_lt(run, x);
+        const float x = run[p];
+        const int pos = p < 128 ? p + count_le(run + 128, x) : (p - 128) + count_lt(run, x);
+        if (((uint32_t)pos & 1u) == odd) out[pos >> 1] = x;
     }
-    float* out = fb + grp * 128;  // in place: every read of this wave precedes every write
-#pragma unroll
-    for (int r = 0; r < R; r++)
-        if (((uint32_t)pos[r] & 1u) == odd) out[pos[r] >> 1] = __uint_as_float(key2f(v[r]));
 #pragma unroll
     for (int j = 0; j < R / 2; j++) w[j] = f2key(__float_as_uint(out[li * (R / 2) + j]));
 }
@@ -105,8 +105,16 @@ template <int R>
 __device__ __forceinline__ void store_node(const uint32_t (&w)[R], int lane, float* dst) {
     constexpr int G = kK / R;
     const int li = lane % G;
+    if constexpr (R >= 4) {  // vector stores: few address registers
+        float4* d = reinterpret_cast<float4*>(dst + li * R);
 #pragma unroll
-    for (int r = 0; r < R; r++) dst[li * R + r] = __uint_as_float(key2f(w[r]));
+        for (int q = 0; q < R / 4; q++)
+            d[q] = make_float4(__uint_as_float(key2f(w[4 * q])), __uint_as_float(key2f(w[4 * q + 1])),
+                               __uint_as_float(key2f(w[4 * q + 2])), __uint_as_float(key2f(w[4 * q + 3])));
+    } else {
+        reinterpret_cast<float2*>(dst + li * R)[0] =
+            make_float2(__uint_as_float(key2f(w[0])), __uint_as_float(key2f(w[1])));
+    }
 }
 
 // Levels +1..+3 inside a wave.  bits: 0..3 -> level+1 nodes, 4..5 -> level+2, 6 -> level+3.
@@ -185,6 +193,203 @@ struct LeafExport {
     }
 };
 
+// ---------------------------------------------------------------------------------------------
+// Wave-persistent leaf: every wave owns 64 consecutive chunks (one level-6 node) and walks them in
+// 8 rounds of 8 chunks.  Round nodes (level 3) are carried through a register stack of levels
+// 3..5 exactly like HeapQuantileSketch's binary counter (inPlacePropagationUpdate,
+// HeapQuantileSketch.java:116-124), so no workgroup barrier is ever needed.
+// ---------------------------------------------------------------------------------------------
+constexpr int kLeafWaveChunks = 64;
+constexpr int kLeaf2Waves = 4;
+
+// Merge two register-resident nodes (64 lanes x 2 keys, positions lane*2 + r): older A, newer B.
+__device__ __forceinline__ void wave_node_merge(const uint32_t (&A)[2], const uint32_t (&B)[2],
+                                                uint32_t (&out)[2], int lane, uint32_t odd, bool exact,
+                                                float* buf) {
+    float* a = buf;
+    float* b = buf + kK;
+    float* o = buf + 2 * kK;
+    reinterpret_cast<float2*>(a)[lane] = make_float2(__uint_as_float(key2f(A[0])), __uint_as_float(key2f(A[1])));
+    reinterpret_cast<float2*>(b)[lane] = make_float2(__uint_as_float(key2f(B[0])), __uint_as_float(key2f(B[1])));
+    if (!exact) {
+        wave_pair_merge(a, b, o, lane, odd);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; k++) exact_merge_task(a, b, o, lane + 64 * k, odd);
+    }
+    const float2 r = reinterpret_cast<const float2*>(o)[lane];
+    out[0] = f2key(__float_as_uint(r.x));
+    out[1] = f2key(__float_as_uint(r.y));
+}
+
+// Roots of the small trees inside the partial 64-chunk tile (compiled only into the PARTIAL
+// variant: a divergent export in the hot kernel costs ~50 VGPRs).
+template <bool PARTIAL>
+struct WaveExport {
+    int lane, rem;
+    int64_t round_off;  // first chunk of the round relative to the tile
+    float* roots;
+    template <int R>
+    __device__ __forceinline__ void at(int level, int node, const uint32_t (&w)[R]) const {
+        if constexpr (PARTIAL) {
+            if (!((rem >> level) & 1)) return;
+            const int64_t cs = ((int64_t)rem >> (level + 1)) << (level + 1);
+            if (round_off + ((int64_t)node << level) != cs) return;
+            store_node<R>(w, lane, roots + (size_t)level * kK);
+        }
+    }
+};
+
+template <int STAGE, bool PARTIAL = false>
+__global__ __launch_bounds__(256, 4) void k_leaf2(const float* __restrict__ x, int64_t chunks,
+                                               uint64_t s0, const uint64_t* __restrict__ tab,
+                                               LeafPartial* __restrict__ part,
+                                               float* __restrict__ nodes6,
+                                               float* __restrict__ roots, int64_t tile0) {
+    __shared__ float fb[kLeaf2Waves][kWaveFb];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t tile = tile0 + (int64_t)blockIdx.x * kLeaf2Waves + wave;
+    const int64_t c_tile = tile * kLeafWaveChunks;
+    if (c_tile >= chunks) return;  // wave-uniform; no block barriers in this kernel
+    const int64_t left = chunks - c_tile;
+    const int rem = left < kLeafWaveChunks ? (int)left : 0;
+    const int nrounds = rem ? (rem + kChunksPerWave - 1) / kChunksPerWave : kLeafWaveChunks / kChunksPerWave;
+    float* wfb = fb[wave];
+    const uint64_t ta = tab[lane * 2], tc = tab[lane * 2 + 1];  // A^lane, C_lane
+
+    uint32_t mn = 0xFFFFFFFFu, mx = 0u, fl = 0u;
+    bool neg_any = false, pos_any = false;
+    uint32_t st3[2], st4[2], st5[2], top[2];
+    uint32_t acc = 0;
+#pragma unroll 1
+    for (int round = 0; round < nrounds; round++) {
+        const int64_t c0 = c_tile + round * kChunksPerWave;
+        const int64_t chunk = c0 + (lane >> 3);
+        const bool valid = chunk < chunks;
+        uint32_t v[32];
+        uint32_t rfl = 0;
+        {
+            const float4* src = reinterpret_cast<const float4*>(x + (valid ? chunk : c0) * kChunk);
+            float4 f[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) f[j] = src[j * 8 + (lane & 7)];
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const uint32_t b[4] = {__float_as_uint(f[j].x), __float_as_uint(f[j].y),
+                                       __float_as_uint(f[j].z), __float_as_uint(f[j].w)};
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    rfl |= is_nan_bits(b[e]) ? 1u : 0u;
+                    rfl |= (b[e] == 0x80000000u) ? 2u : 0u;
+                    rfl |= (b[e] == 0u) ? 4u : 0u;
+                    const uint32_t k = f2key(b[e]);
+                    if (valid) {
+                        mn = k < mn ? k : mn;
+                        mx = k > mx ? k : mx;
+                    }
+                    v[j * 4 + e] = k;
+                }
+            }
+            if (!valid) rfl = 0u;
+            fl |= rfl;
+        }
+        // compaction bits of this round's chunks (and their carries): draws [start, start+64)
+        const uint64_t start = node_bit_index((uint64_t)c0, 0);
+        uint64_t mask;
+        {
+            const uint64_t s_start = lcg_jump(tab, s0, start + 1);
+            const uint64_t s = lane == 0 ? s_start : ((ta * s_start + tc) & kLcgMask);
+            mask = __ballot((s >> 47) & 1ull);
+        }
+        if constexpr (STAGE == 0) {
+#pragma unroll
+            for (int r = 0; r < 32; r++) acc ^= v[r];
+            acc ^= (uint32_t)mask;
+            continue;
+        }
+        neg_any = neg_any || (__ballot((rfl & 2u) != 0) != 0);
+        pos_any = pos_any || (__ballot((rfl & 4u) != 0) != 0);
+        const bool exact = STAGE == 2 ? false : (neg_any && pos_any);
+        auto bit = [&](int level, int64_t last_chunk) -> uint32_t {
+            return (uint32_t)(mask >> (node_bit_index((uint64_t)last_chunk, level) - start)) & 1u;
+        };
+
+        sort_group256<32>(v, lane);
+        uint32_t w1[16];
+        compact_regs<32>(v, w1, bit(0, chunk));
+        const WaveExport<PARTIAL> exp{lane, rem, round * kChunksPerWave, roots};
+        exp.template at<16>(0, lane >> 3, w1);
+        if constexpr (STAGE == 1) {
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc ^= w1[r];
+            continue;
+        }
+        uint32_t ibits = 0;
+        for (int j = 0; j < 4; j++) ibits |= bit(1, c0 + 2 * j + 1) << j;
+        ibits |= bit(2, c0 + 3) << 4 | bit(2, c0 + 7) << 5 | bit(3, c0 + 7) << 6;
+        uint32_t node[2];
+        inwave_levels(w1, node, lane, ibits, exact, wfb, exp);
+        if constexpr (STAGE == 2) {
+            acc ^= node[0] ^ node[1];
+            continue;
+        }
+
+        // carry through the stack (older node first), levels 4..6
+        if (!(round & 1)) {
+            st3[0] = node[0];
+            st3[1] = node[1];
+            continue;
+        }
+        uint32_t n4[2];
+        wave_node_merge(st3, node, n4, lane, bit(4, c0 + 7), exact, wfb);
+        if constexpr (PARTIAL)
+            if (((rem >> 4) & 1) && (int64_t)(round - 1) * kChunksPerWave == ((int64_t)(rem >> 5) << 5))
+                store_node<2>(n4, lane, roots + (size_t)4 * kK);
+        if (!(round & 2)) {
+            st4[0] = n4[0];
+            st4[1] = n4[1];
+            continue;
+        }
+        uint32_t n5[2];
+        wave_node_merge(st4, n4, n5, lane, bit(5, c0 + 7), exact, wfb);
+        if constexpr (PARTIAL)
+            if (((rem >> 5) & 1) && round == 3) store_node<2>(n5, lane, roots + (size_t)5 * kK);
+        if (!(round & 4)) {
+            st5[0] = n5[0];
+            st5[1] = n5[1];
+            continue;
+        }
+        wave_node_merge(st5, n5, top, lane, bit(6, c0 + 7), exact, wfb);
+    }
+    if constexpr (STAGE <= 2) {
+        nodes6[(size_t)tile * 64 + lane] = __uint_as_float(acc ^ mn ^ mx ^ fl);
+        return;
+    }
+    if constexpr (!PARTIAL) {
+        store_node<2>(top, lane, nodes6 + (size_t)tile * kK);
+        // a level-6 tree (bit 6 of the chunk count) is this single node
+        if (((chunks >> 6) & 1) && tile == ((chunks >> 7) << 1)) store_node<2>(top, lane, roots + (size_t)6 * kK);
+    }
+    // per-wave partial: min / max / flags
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const uint32_t omn = (uint32_t)__shfl_xor((int)mn, off, 64);
+        const uint32_t omx = (uint32_t)__shfl_xor((int)mx, off, 64);
+        const uint32_t ofl = (uint32_t)__shfl_xor((int)fl, off, 64);
+        mn = omn < mn ? omn : mn;
+        mx = omx > mx ? omx : mx;
+        fl |= ofl;
+    }
+    if (lane == 0) {
+        LeafPartial p;
+        p.min_key = mn;
+        p.max_key = mx;
+        p.flags = fl;
+        p.pad = 0;
+        part[tile] = p;
+    }
+}
+
 template <int STAGE, int MINW = 1>
 __global__ __launch_bounds__(512, MINW) void k_leaf(const float* __restrict__ x, int64_t chunks,
                                               uint64_t s0, const uint64_t* __restrict__ tab,
@@ -212,8 +417,18 @@ __global__ __launch_bounds__(512, MINW) void k_leaf(const float* __restrict__ x,
     {
         const float4* src = reinterpret_cast<const float4*>(x + (valid ? chunk : 0) * kChunk);
         float4 f[8];
+        if constexpr (STAGE == 4) {  // ablation: no HBM traffic, synthetic values
+            uint32_t h = (uint32_t)(blockIdx.x * 512 + tid) * 2654435761u;
 #pragma unroll
-        for (int j = 0; j < 8; j++) f[j] = src[j * 8 + (lane & 7)];
+            for (int j = 0; j < 8; j++) {
+                h ^= h << 13; h ^= h >> 17; h ^= h << 5;
+                f[j] = make_float4(__uint_as_float(h & 0xBF7FFFFFu), __uint_as_float((h * 3u) & 0xBF7FFFFFu),
+                                   __uint_as_float((h * 5u) & 0xBF7FFFFFu), __uint_as_float((h * 7u) & 0xBF7FFFFFu));
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; j++) f[j] = src[j * 8 + (lane & 7)];
+        }
 #pragma unroll
         for (int j = 0; j < 8; j++) {
             const uint32_t b[4] = {__float_as_uint(f[j].x), __float_as_uint(f[j].y),
@@ -254,12 +469,20 @@ __global__ __launch_bounds__(512, MINW) void k_leaf(const float* __restrict__ x,
     }
 
     // ---- leaf: sort the chunk (Arrays.sort total order) and keep every other sample ----
+    if constexpr (STAGE == 5) {  // ablation: in-register stages only
+        sort_regs<32>(v);
+        uint32_t acc = mn ^ mx ^ fl;
+#pragma unroll
+        for (int r = 0; r < 32; r++) acc ^= v[r] * (r + 1);
+        nodes6[(size_t)blockIdx.x * 512 + tid] = __uint_as_float(acc);
+        return;
+    }
     sort_group256<32>(v, lane);
     uint32_t w1[16];
     compact_regs<32>(v, w1, (uint32_t)(mask >> (node_bit_index((uint64_t)chunk, 0) - start)) & 1u);
     const LeafExport exp{lane, rem, wave * kChunksPerWave, roots};
     exp.at<16>(0, lane >> 3, w1);
-    if constexpr (STAGE == 1) {
+    if constexpr (STAGE == 1 || STAGE == 4) {
         uint32_t acc = mn ^ mx ^ fl;
 #pragma unroll
         for (int r = 0; r < 16; r++) acc ^= w1[r];
@@ -333,10 +556,14 @@ __global__ __launch_bounds__(512, MINW) void k_leaf(const float* __restrict__ x,
 
 hipError_t launch_leaf(hipStream_t st, const float* x, int64_t chunks, uint64_t s0,
                        const uint64_t* jump_tab, LeafPartial* part, float* nodes6, float* roots) {
-    const int64_t nwg = (chunks + kLeafChunks - 1) / kLeafChunks;
-    if (nwg <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_leaf<3>, dim3((unsigned)nwg), dim3(512), 0, st, x, chunks, s0, jump_tab,
-                       part, nodes6, roots);
+    const int64_t full = chunks / kLeafWaveChunks;
+    if (full > 0)
+        hipLaunchKernelGGL((k_leaf2<3, false>), dim3((unsigned)((full + kLeaf2Waves - 1) / kLeaf2Waves)),
+                           dim3(64 * kLeaf2Waves), 0, st, x, full * kLeafWaveChunks, s0, jump_tab, part,
+                           nodes6, roots, (int64_t)0);
+    if (chunks % kLeafWaveChunks)  // the small trees of the last chunks: one wave
+        hipLaunchKernelGGL((k_leaf2<3, true>), dim3(1), dim3(64), 0, st, x, chunks, s0, jump_tab, part,
+                           nodes6, roots, full);
     return hipGetLastError();
 }
 
@@ -352,6 +579,19 @@ hipError_t launch_leaf_stage(hipStream_t st, int stage, const float* x, int64_t 
         case 1: hipLaunchKernelGGL(k_leaf<1>, g, b, 0, st, x, chunks, s0, jump_tab, part, scratch, roots); break;
         case 2: hipLaunchKernelGGL(k_leaf<2>, g, b, 0, st, x, chunks, s0, jump_tab, part, scratch, roots); break;
         case 3: hipLaunchKernelGGL(k_leaf<3>, g, b, 0, st, x, chunks, s0, jump_tab, part, scratch, roots); break;
+        case 4: hipLaunchKernelGGL(k_leaf<4>, g, b, 0, st, x, chunks, s0, jump_tab, part, scratch, roots); break;
+        // wave-persistent leaf: 20 = load only, 21 = + leaf sort, 23 = full
+        case 20: case 21: case 22: case 23: {
+            const int64_t tiles = (chunks + kLeafWaveChunks - 1) / kLeafWaveChunks;
+            dim3 g2((unsigned)((tiles + kLeaf2Waves - 1) / kLeaf2Waves)), b2(64 * kLeaf2Waves);
+            const int64_t z = 0;
+            if (stage == 20) hipLaunchKernelGGL((k_leaf2<0>), g2, b2, 0, st, x, chunks, s0, jump_tab, part, scratch, roots, z);
+            else if (stage == 21) hipLaunchKernelGGL((k_leaf2<1>), g2, b2, 0, st, x, chunks, s0, jump_tab, part, scratch, roots, z);
+            else if (stage == 22) hipLaunchKernelGGL((k_leaf2<2>), g2, b2, 0, st, x, chunks, s0, jump_tab, part, scratch, roots, z);
+            else hipLaunchKernelGGL((k_leaf2<3>), g2, b2, 0, st, x, chunks, s0, jump_tab, part, scratch, roots, z);
+            break;
+        }
+        case 5: hipLaunchKernelGGL(k_leaf<5>, g, b, 0, st, x, chunks, s0, jump_tab, part, scratch, roots); break;
         // occupancy variants: 10 + stage with >= 6 waves / SIMD (<= 80 VGPRs)
         case 11: hipLaunchKernelGGL((k_leaf<1, 6>), g, b, 0, st, x, chunks, s0, jump_tab, part, scratch, roots); break;
         case 13: hipLaunchKernelGGL((k_leaf<3, 6>), g, b, 0, st, x, chunks, s0, jump_tab, part, scratch, roots); break;
