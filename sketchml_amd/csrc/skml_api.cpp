@@ -106,6 +106,7 @@ struct Workspace {
     float* upA;
     float* upB;
     double* raw;
+    QuantLut* lut;  // quantize bucket LUT, written by the summary / set-splits kernel
 };
 
 size_t ws_layout(int64_t chunks, Workspace* w, char* base) {
@@ -126,6 +127,7 @@ size_t ws_layout(int64_t chunks, Workspace* w, char* base) {
     t.upA = (float*)take(sizeof(float) * kK * (size_t)up);
     t.upB = (float*)take(sizeof(float) * kK * (size_t)up);
     t.raw = (double*)take(sizeof(double) * SKML_MAX_BINS);
+    t.lut = (QuantLut*)take(sizeof(QuantLut));
     if (w) *w = t;
     return off;
 }
@@ -444,7 +446,7 @@ int skml_dense_encode_f32(skml_ctx* c, const float* x, int64_t n, const skml_par
             KernelTimer kt(c, SKML_K_MERGE);
             HIP_TRY(launch_merge_pass(c->stream, pass, src, dst, w.roots, s0, c->jump_tab, w.done, x, n,
                                       w.part, nwg, c->ranks, p->bin_num, p->dedup ? 1 : 0, payload,
-                                      w.raw));
+                                      w.raw, w.lut));
             src = dst;
             dst = (dst == w.upA) ? w.upB : w.upA;
         }
@@ -453,11 +455,11 @@ int skml_dense_encode_f32(skml_ctx* c, const float* x, int64_t n, const skml_par
     if (!fused) {
         KernelTimer kt(c, SKML_K_SUMMARY);
         HIP_TRY(launch_summary(c->stream, x, n, w.part, nwg, w.roots, c->ranks, p->bin_num,
-                               p->dedup ? 1 : 0, payload, w.raw));
+                               p->dedup ? 1 : 0, payload, w.raw, w.lut));
     }
     {
         KernelTimer kt(c, SKML_K_QUANTIZE);
-        HIP_TRY(launch_quantize(c->stream, x, n, payload));
+        HIP_TRY(launch_quantize(c->stream, x, n, payload, w.lut, p->bin_num));
     }
     return SKML_OK;
 }
@@ -474,8 +476,11 @@ int skml_dense_encode_with_splits_f32(skml_ctx* c, const float* x, int64_t n, co
     if ((st = ensure_stage(c, sizeof(double) * (size_t)nsplits))) return st;
     HIP_TRY(hipMemcpyAsync(c->stage, splits, sizeof(double) * (size_t)nsplits, hipMemcpyHostToDevice,
                            c->stream));
-    HIP_TRY(launch_set_splits(c->stream, payload, n, (const double*)c->stage, nsplits, mn, mx, nsplits + 1));
-    HIP_TRY(launch_quantize(c->stream, x, n, payload));
+    Workspace w;
+    if ((st = ensure_ws(c, 0, &w))) return st;
+    HIP_TRY(launch_set_splits(c->stream, payload, n, (const double*)c->stage, nsplits, mn, mx, nsplits + 1,
+                              w.lut));
+    HIP_TRY(launch_quantize(c->stream, x, n, payload, w.lut, nsplits + 1));
     HIP_TRY(hipStreamSynchronize(c->stream));  // the staged splits are reused by later calls
     return SKML_OK;
 }

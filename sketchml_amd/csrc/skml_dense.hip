@@ -4,6 +4,8 @@
 //   k_decode     values[bins[i]] (DenseVectorCompressor.java:84-91), LUT in LDS; k_decode_sum,
 //                k_bins, k_ref_body / k_pack_ref (Quantizer.writeObject/readObject), k_times_by.
 // The sketch build (leaf / merge / summary) lives in skml_sketch.hip.
+#include <algorithm>
+
 #include "skml_device.hpp"
 
 namespace skml {
@@ -39,69 +41,63 @@ __device__ __forceinline__ void store_codes4(uint8_t* codes, int64_t e0, uint32_
     }
 }
 
-__device__ __forceinline__ uint32_t eytz_bin(const float* E, int levels, uint32_t P, float xv) {
-    uint32_t i = 1;
-    for (int s = 0; s < levels; s++) i = 2 * i + (E[i] <= xv ? 1u : 0u);
-    return i - P;
-}
+// Search modes of the quantize pass, chosen per launch from the header and the bucket LUT:
+//   kModeLut<S>  bin = base[key >> 18] then S bisection steps over the LDS split table
+//   kModeEytz    branchless Eytzinger descent over the LDS split table (cmax too large)
+//   kModeGlobal  binary search over the payload's double splits (> 4095 splits)
+// All compare the float value against splits rounded toward +inf, which is exact (see
+// build_quant_lut); NaN values take Quantizer.indexOf's NaN bin.
+constexpr int kModeEytz = 8, kModeGlobal = 9;
 
-__device__ __forceinline__ uint32_t global_bin(const double* sp, int nsplit, float xv) {
-    int lo = 0, hi = nsplit;
-    const double xd = (double)xv;
-    while (lo < hi) {
-        int mid = (lo + hi) >> 1;
-        if (sp[mid] <= xd) lo = mid + 1;
-        else hi = mid;
-    }
-    return (uint32_t)lo;
-}
+struct QuantTables {
+    const uint16_t* base;  // LDS bucket bases
+    const float* S;        // LDS splits (+NaN padding), or Eytzinger array
+    const double* sp;      // payload splits (global mode)
+    int nsplit, levels;
+    uint32_t P, nan_bin;
+};
 
-__global__ __launch_bounds__(kQThreads) void k_quantize(const float* __restrict__ x, int64_t n,
-                                                        uint8_t* __restrict__ payload) {
-    __shared__ float E[kEytzMax];
-    const skml_dense_header* hdr = reinterpret_cast<const skml_dense_header*>(payload);
-    if (hdr->status != SKML_OK) return;
-    const int bins = hdr->bin_num, bits = hdr->code_bits, nsplit = bins - 1;
-    const double* sp = reinterpret_cast<const double*>(payload + kHeaderBytes);
-    uint8_t* codes = payload + hdr->codes_offset;
-    uint32_t P = 1;
-    int levels = 0;
-    while (P < (uint32_t)bins) {
-        P <<= 1;
-        levels++;
-    }
-    const bool lds = P <= kEytzMax;
-    if (lds) {
-        for (uint32_t i = threadIdx.x + 1; i < P; i += kQThreads) {
-            const int d = 31 - __clz(i);
-            const uint32_t idx = ((2u * (i - (1u << d)) + 1u) << (levels - 1 - d)) - 1u;
-            E[i] = idx < (uint32_t)nsplit ? (float)sp[idx] : __uint_as_float(0x7FC00000u);
+template <int MODE>
+__device__ __forceinline__ uint32_t quant_bin(const QuantTables& q, float xv) {
+    uint32_t bin;
+    if constexpr (MODE <= 4) {
+        bin = q.base[f2key(__float_as_uint(xv)) >> (32 - kLutBits)];
+#pragma unroll
+        for (int h = (1 << MODE) >> 1; h > 0; h >>= 1) bin += q.S[bin + h - 1] <= xv ? (uint32_t)h : 0u;
+    } else if constexpr (MODE == kModeEytz) {
+        uint32_t i = 1;
+        for (int s = 0; s < q.levels; s++) i = 2 * i + (q.S[i] <= xv ? 1u : 0u);
+        bin = i - q.P;
+    } else {
+        int lo = 0, hi = q.nsplit;
+        const double xd = (double)xv;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (q.sp[mid] <= xd) lo = mid + 1;
+            else hi = mid;
         }
-        __syncthreads();
+        bin = (uint32_t)lo;
     }
+    return xv == xv ? bin : q.nan_bin;
+}
+
+template <int MODE>
+__device__ __forceinline__ void quant_tiles(const QuantTables& q, const float* __restrict__ x, int64_t n,
+                                            uint8_t* __restrict__ codes, int bits) {
     const int lane = threadIdx.x & 63;
     const int64_t nwaves_total = (int64_t)gridDim.x * (kQThreads / 64);
     const int64_t wave_id = (int64_t)blockIdx.x * (kQThreads / 64) + (threadIdx.x >> 6);
     const int64_t full_tiles = n / 1024;
     for (int64_t tile = wave_id; tile < full_tiles; tile += nwaves_total) {
-        const float4* src = reinterpret_cast<const float4*>(x + tile * 1024);
-        float4 f[4];
+        typedef float f32x4 __attribute__((ext_vector_type(4)));
+        const f32x4* src = reinterpret_cast<const f32x4*>(x + tile * 1024);
+        f32x4 f[4];
 #pragma unroll
-        for (int j = 0; j < 4; j++) f[j] = src[j * 64 + lane];
+        for (int j = 0; j < 4; j++) f[j] = __builtin_nontemporal_load(src + j * 64 + lane);
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            uint32_t c0, c1, c2, c3;
-            if (lds) {
-                c0 = eytz_bin(E, levels, P, f[j].x);
-                c1 = eytz_bin(E, levels, P, f[j].y);
-                c2 = eytz_bin(E, levels, P, f[j].z);
-                c3 = eytz_bin(E, levels, P, f[j].w);
-            } else {
-                c0 = global_bin(sp, nsplit, f[j].x);
-                c1 = global_bin(sp, nsplit, f[j].y);
-                c2 = global_bin(sp, nsplit, f[j].z);
-                c3 = global_bin(sp, nsplit, f[j].w);
-            }
+            const uint32_t c0 = quant_bin<MODE>(q, f[j].x), c1 = quant_bin<MODE>(q, f[j].y);
+            const uint32_t c2 = quant_bin<MODE>(q, f[j].z), c3 = quant_bin<MODE>(q, f[j].w);
             store_codes4(codes, tile * 1024 + j * 256 + lane * 4, c0, c1, c2, c3, bits, lane);
         }
     }
@@ -113,20 +109,74 @@ __global__ __launch_bounds__(kQThreads) void k_quantize(const float* __restrict_
             const int64_t e0 = base + j * 256 + lane * 4;
             uint32_t c[4] = {0, 0, 0, 0};
             for (int e = 0; e < 4; e++)
-                if (e0 + e < n) {
-                    const float xv = x[e0 + e];
-                    c[e] = lds ? eytz_bin(E, levels, P, xv) : global_bin(sp, nsplit, xv);
-                }
-            const bool any = e0 < n;
+                if (e0 + e < n) c[e] = quant_bin<MODE>(q, x[e0 + e]);
             if (bits == 1) {
                 const int64_t pair0 = base + j * 256 + (lane & ~1) * 4;
                 const uint32_t nib = c[0] | (c[1] << 1) | (c[2] << 2) | (c[3] << 3);
                 const uint32_t other = lane_xor<1>(nib);
                 if ((lane & 1) == 0 && pair0 < n) codes[pair0 / 8] = (uint8_t)(nib | (other << 4));
-            } else if (any) {
+            } else if (e0 < n) {
                 store_codes4(codes, e0, c[0], c[1], c[2], c[3], bits, lane);
             }
         }
+    }
+}
+
+// Dynamic LDS: [0, 32 KB) bucket bases, then `lds_splits` floats (LUT mode); Eytzinger mode
+// reuses the start of the same buffer (P <= 4096 floats).
+__global__ __launch_bounds__(kQThreads) void k_quantize(const float* __restrict__ x, int64_t n,
+                                                        uint8_t* __restrict__ payload,
+                                                        const QuantLut* __restrict__ lut, int lds_splits) {
+    extern __shared__ __align__(16) uint8_t qsm[];
+    const skml_dense_header* hdr = reinterpret_cast<const skml_dense_header*>(payload);
+    if (hdr->status != SKML_OK) return;
+    const int bins = hdr->bin_num, bits = hdr->code_bits, nsplit = bins - 1;
+    const double* sp = reinterpret_cast<const double*>(payload + kHeaderBytes);
+    uint8_t* codes = payload + hdr->codes_offset;
+    QuantTables q;
+    q.sp = sp;
+    q.nsplit = nsplit;
+    q.nan_bin = (uint32_t)nan_bin_for(bins, hdr->zero_idx);
+    q.P = 1;
+    q.levels = 0;
+    while (q.P < (uint32_t)bins) {
+        q.P <<= 1;
+        q.levels++;
+    }
+    const int cmax = lut ? lut->cmax : -1;
+    int mode;
+    if (cmax >= 0 && nsplit + kLutPad <= lds_splits) {
+        mode = cmax == 0 ? 0 : 32 - __clz((uint32_t)cmax);  // bisection steps: ceil(log2(cmax+1))
+        uint16_t* base = reinterpret_cast<uint16_t*>(qsm);
+        float* S = reinterpret_cast<float*>(qsm + sizeof(lut->base));
+        const uint4* src = reinterpret_cast<const uint4*>(lut->base);
+        for (int i = threadIdx.x; i < (int)(sizeof(lut->base) / 16); i += kQThreads)
+            reinterpret_cast<uint4*>(base)[i] = src[i];
+        for (int i = threadIdx.x; i < nsplit + kLutPad; i += kQThreads)
+            S[i] = i < nsplit ? __double2float_ru(sp[i]) : __uint_as_float(0x7FC00000u);
+        q.base = base;
+        q.S = S;
+    } else if (q.P <= kEytzMax) {
+        mode = kModeEytz;
+        float* E = reinterpret_cast<float*>(qsm);
+        for (uint32_t i = threadIdx.x + 1; i < q.P; i += kQThreads) {
+            const int d = 31 - __clz(i);
+            const uint32_t idx = ((2u * (i - (1u << d)) + 1u) << (q.levels - 1 - d)) - 1u;
+            E[i] = idx < (uint32_t)nsplit ? __double2float_ru(sp[idx]) : __uint_as_float(0x7FC00000u);
+        }
+        q.S = E;
+    } else {
+        mode = kModeGlobal;
+    }
+    __syncthreads();
+    switch (mode) {
+        case 0: quant_tiles<0>(q, x, n, codes, bits); break;
+        case 1: quant_tiles<1>(q, x, n, codes, bits); break;
+        case 2: quant_tiles<2>(q, x, n, codes, bits); break;
+        case 3: quant_tiles<3>(q, x, n, codes, bits); break;
+        case 4: quant_tiles<4>(q, x, n, codes, bits); break;
+        case kModeEytz: quant_tiles<kModeEytz>(q, x, n, codes, bits); break;
+        default: quant_tiles<kModeGlobal>(q, x, n, codes, bits); break;
     }
 }
 
@@ -138,10 +188,16 @@ static int quant_grid(int64_t n) {
     return (int)wg;
 }
 
-hipError_t launch_quantize(hipStream_t st, const float* x, int64_t n, void* payload) {
+hipError_t launch_quantize(hipStream_t st, const float* x, int64_t n, void* payload, const QuantLut* lut,
+                           int req_bins) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_quantize, dim3(quant_grid(n)), dim3(kQThreads), 0, st, x, n,
-                       reinterpret_cast<uint8_t*>(payload));
+    // LDS sized for this request's split table; persistent-style grid (the LUT is loaded once per WG)
+    const int lds_splits = std::min(std::max(req_bins - 1, 1), kLutMaxSplits) + kLutPad;
+    const size_t lds = sizeof(QuantLut::base) + (size_t)lds_splits * sizeof(float);
+    const int64_t tiles = (n + 1023) / 1024;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((tiles + 3) / 4, 1024));
+    hipLaunchKernelGGL(k_quantize, dim3(grid), dim3(kQThreads), lds, st, x, n,
+                       reinterpret_cast<uint8_t*>(payload), lut, lds_splits);
     return hipGetLastError();
 }
 

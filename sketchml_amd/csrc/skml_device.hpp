@@ -219,4 +219,57 @@ __device__ __forceinline__ void exact_merge_task(const float* older, const float
     if (((uint32_t)pos & 1u) == odd) out[pos >> 1] = v;
 }
 
+// ------------------------------------------------------------------------------------------
+// Bucket LUT for the quantize pass (built by one workgroup; `sp` = splits in LDS as floats
+// rounded toward +inf, IEEE-sorted; `lut` in global memory).  For a non-NaN float x and a
+// double split s, s <= x  <=>  RU(s) <= x, so the float table gives the exact indexOf.
+// base[b] = #{s < vmin(b)} (IEEE), where vmin/vmax are the smallest / largest non-NaN values
+// whose key has prefix b (NaN-only buckets clamp to +-inf); need(b) = #{s <= vmax(b)} - base[b];
+// cmax = max need.  Each thread sweeps a contiguous bucket range with two pointers.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ float lut_bucket_value(uint32_t key) {
+    constexpr uint32_t kNegInf = 0x007FFFFFu, kPosInf = 0xFF800000u;  // f2key(-inf), f2key(+inf)
+    key = key < kNegInf ? kNegInf : (key > kPosInf ? kPosInf : key);
+    return __uint_as_float(key2f(key));
+}
+
+__device__ __forceinline__ void build_quant_lut(const float* sp, int nsplit, QuantLut* lut, int* s_cmax) {
+    const int T = blockDim.x, t = threadIdx.x;
+    if (t == 0) *s_cmax = 0;
+    __syncthreads();
+    const int per = (kLutSize + T - 1) / T;
+    const int b0 = t * per, b1 = min(kLutSize, b0 + per);
+    int need_max = 0;
+    if (b0 < b1) {
+        const float v0 = lut_bucket_value((uint32_t)b0 << (32 - kLutBits));
+        int lo = 0, hi = nsplit;  // p = #{s < v0}
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (sp[mid] < v0) lo = mid + 1;
+            else hi = mid;
+        }
+        int p = lo, q = lo;
+        for (int b = b0; b < b1; b++) {
+            const float vmin = lut_bucket_value((uint32_t)b << (32 - kLutBits));
+            const float vmax = lut_bucket_value(((uint32_t)(b + 1) << (32 - kLutBits)) - 1u);
+            while (p < nsplit && sp[p] < vmin) p++;
+            if (q < p) q = p;
+            while (q < nsplit && sp[q] <= vmax) q++;
+            lut->base[b] = (uint16_t)p;
+            need_max = max(need_max, q - p);
+        }
+    }
+    atomicMax(s_cmax, need_max);
+    __syncthreads();
+    if (t == 0) lut->cmax = (*s_cmax <= kLutMaxNeed && nsplit <= kLutMaxSplits) ? *s_cmax : -1;
+}
+
+// Quantizer.indexOf (Quantizer.java:49-92) on a NaN value: the probe never succeeds, so the
+// search runs from zeroIdx up to the last split and returns its final midpoint.
+__host__ __device__ inline int nan_bin_for(int bin_num, int zero_idx) {
+    const int last = bin_num - 2;
+    if (last < 0) return 0;
+    return zero_idx + 1 < last ? last - 1 : (zero_idx + last) >> 1;
+}
+
 }  // namespace skml

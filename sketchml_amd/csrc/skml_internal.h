@@ -21,6 +21,18 @@ constexpr int kLeafTopLevel = 6;
 constexpr int kMergeGroupLog = 6;       // upper merge: 64 nodes per workgroup
 constexpr int kMaxLevels = 24;     // n < 2^31 -> fewer than 2^23 chunks
 constexpr int kHeaderBytes = 64;
+// Quantize bucket LUT: the top kLutBits of a value's total-order key select a bucket whose entry
+// is the number of splits below the bucket; at most `cmax` splits fall inside any bucket.
+constexpr int kLutBits = 14;
+constexpr int kLutSize = 1 << kLutBits;
+constexpr int kLutMaxNeed = 15;    // <= 4 bisection steps after the lookup; else Eytzinger
+constexpr int kLutMaxSplits = 4096;  // split table must fit the quantize kernel's LDS
+constexpr int kLutPad = 16;          // NaN padding after the last split (2^4 bisection reach)
+struct QuantLut {
+    uint16_t base[kLutSize];
+    int32_t cmax;  // -1: LUT unusable (too many splits per bucket)
+    int32_t pad[15];
+};
 
 // Per leaf workgroup partial results: min key, max key, flags (bit0 NaN, bit1 -0, bit2 +0).
 struct LeafPartial {
@@ -67,14 +79,16 @@ hipError_t launch_merge_pass(hipStream_t st, const MergePass& pass, const float*
                              float* roots, uint64_t s0, const uint64_t* jump_tab, unsigned* done,
                              const float* x, int64_t n, const LeafPartial* part, int64_t nparts,
                              const int64_t* ranks, int req_bins, int dedup, void* payload,
-                             double* scratch_raw);
-// ---- kernel launchers (skml_dense.hip) ----
+                             double* scratch_raw, QuantLut* lut);
 hipError_t launch_summary(hipStream_t st, const float* x, int64_t n, const LeafPartial* part,
                           int64_t nparts, const float* roots, const int64_t* ranks, int req_bins,
-                          int dedup, void* payload, double* scratch_raw);
+                          int dedup, void* payload, double* scratch_raw, QuantLut* lut);
 hipError_t launch_set_splits(hipStream_t st, void* payload, int64_t n, const double* splits_dev,
-                             int nsplits, double mn, double mx, int req_bins);
-hipError_t launch_quantize(hipStream_t st, const float* x, int64_t n, void* payload);
+                             int nsplits, double mn, double mx, int req_bins, QuantLut* lut);
+// ---- kernel launchers (skml_dense.hip) ----
+// `lut` may be null (Eytzinger / global search); req_bins sizes the kernel's LDS split table.
+hipError_t launch_quantize(hipStream_t st, const float* x, int64_t n, void* payload, const QuantLut* lut,
+                           int req_bins);
 hipError_t launch_decode(hipStream_t st, const void* payload, float* out, int64_t n);
 hipError_t launch_decode_sum(hipStream_t st, const void* payloads, int P, size_t stride, float* out,
                              int64_t n, double scale);

@@ -658,6 +658,7 @@ struct SummaryArgs {
     const int64_t* ranks;
     uint8_t* payload;
     double* g_raw;
+    QuantLut* lut;
     int req_bins;
     int dedup;
 };
@@ -850,6 +851,16 @@ __device__ void summary_block(const SummaryArgs& a, SummaryShared& S) {
         hdr->codes_offset = (int64_t)dense_codes_offset(req_bins);
         hdr->reserved = 0;
     }
+    // ---- quantize bucket LUT over the final split table ----
+    const int nsplit = bin_num - 1;
+    if (nsplit <= kMaxSamples && nsplit <= kLutMaxSplits && n > 0) {
+        __threadfence_block();
+        for (int i = t; i < nsplit; i += T) S.smp[i] = (float)splits[i];
+        __syncthreads();
+        build_quant_lut(S.smp, nsplit, a.lut, &S.zero);
+    } else if (t == 0) {
+        a.lut->cmax = -1;
+    }
 }
 
 __global__ __launch_bounds__(512) void k_summary(SummaryArgs a) {
@@ -859,9 +870,9 @@ __global__ __launch_bounds__(512) void k_summary(SummaryArgs a) {
 
 hipError_t launch_summary(hipStream_t st, const float* x, int64_t n, const LeafPartial* part,
                           int64_t nparts, const float* roots, const int64_t* ranks, int req_bins,
-                          int dedup, void* payload, double* scratch_raw) {
+                          int dedup, void* payload, double* scratch_raw, QuantLut* lut) {
     SummaryArgs a{x, n, part, nparts, roots, ranks, reinterpret_cast<uint8_t*>(payload), scratch_raw,
-                  req_bins, dedup};
+                  lut, req_bins, dedup};
     hipLaunchKernelGGL(k_summary, dim3(1), dim3(512), 0, st, a);
     return hipGetLastError();
 }
@@ -978,28 +989,33 @@ hipError_t launch_merge_pass(hipStream_t st, const MergePass& pass, const float*
                              float* roots, uint64_t s0, const uint64_t* jump_tab, unsigned* done,
                              const float* x, int64_t n, const LeafPartial* part, int64_t nparts,
                              const int64_t* ranks, int req_bins, int dedup, void* payload,
-                             double* scratch_raw) {
+                             double* scratch_raw, QuantLut* lut) {
     const int nwg = pass.wg_prefix[pass.njobs];
     if (nwg <= 0) return hipSuccess;
     SummaryArgs a{x, n, part, nparts, roots, ranks, reinterpret_cast<uint8_t*>(payload), scratch_raw,
-                  req_bins, dedup};
+                  lut, req_bins, dedup};
     hipLaunchKernelGGL(k_merge, dim3(nwg), dim3(512), 0, st, pass, src, dst, roots, s0, jump_tab, done, a);
     return hipGetLastError();
 }
 
 // Split-injected parity mode: header from caller splits (Quantizer.findZeroIdx rule).
-__global__ void k_set_splits(uint8_t* payload, int64_t n, const double* __restrict__ sp, int nsplits,
-                             double mn, double mx, int req_bins) {
+__global__ __launch_bounds__(256) void k_set_splits(uint8_t* payload, int64_t n, const double* __restrict__ sp,
+                                                    int nsplits, double mn, double mx, int req_bins,
+                                                    QuantLut* lut) {
     skml_dense_header* hdr = reinterpret_cast<skml_dense_header*>(payload);
     double* splits = reinterpret_cast<double*>(payload + kHeaderBytes);
-    __shared__ int s_zero;
+    __shared__ int s_zero, s_cmax;
+    __shared__ float s_sp[kLutMaxSplits];
     if (threadIdx.x == 0) s_zero = 0x7FFFFFFF;
     __syncthreads();
     for (int i = threadIdx.x; i < nsplits; i += blockDim.x) {
         splits[i] = sp[i];
+        if (i < kLutMaxSplits) s_sp[i] = __double2float_ru(sp[i]);
         if (!(sp[i] < 0.0)) atomicMin(&s_zero, i);
     }
     __syncthreads();
+    if (nsplits <= kLutMaxSplits) build_quant_lut(s_sp, nsplits, lut, &s_cmax);
+    else if (threadIdx.x == 0) lut->cmax = -1;
     if (threadIdx.x == 0) {
         const int bins = nsplits + 1;
         hdr->magic = SKML_DENSE_MAGIC;
@@ -1017,9 +1033,9 @@ __global__ void k_set_splits(uint8_t* payload, int64_t n, const double* __restri
 }
 
 hipError_t launch_set_splits(hipStream_t st, void* payload, int64_t n, const double* splits_dev,
-                             int nsplits, double mn, double mx, int req_bins) {
+                             int nsplits, double mn, double mx, int req_bins, QuantLut* lut) {
     hipLaunchKernelGGL(k_set_splits, dim3(1), dim3(256), 0, st, reinterpret_cast<uint8_t*>(payload),
-                       n, splits_dev, nsplits, mn, mx, req_bins);
+                       n, splits_dev, nsplits, mn, mx, req_bins, lut);
     return hipGetLastError();
 }
 

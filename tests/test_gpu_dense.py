@@ -219,6 +219,69 @@ def test_split_injected_mode(gpu):
     assert np.array_equal(bins.cpu().numpy(), want)
 
 
+def _encode_with_splits(gpu, x, splits, mn, mx):
+    from sketchml_amd import _lib
+    n = x.numel()
+    nb = _lib.lib.skml_dense_payload_bytes(n, len(splits) + 1)
+    pl = gpu.alloc_aligned(nb, "cuda")
+    ctx = gpu.get_context()
+    sp = np.ascontiguousarray(splits, dtype=np.float64)
+    st = _lib.lib.skml_dense_encode_with_splits_f32(ctx.handle, C.c_void_p(x.data_ptr()), n,
+                                                    sp.ctypes.data_as(_lib.dblp), len(sp), mn, mx,
+                                                    C.c_void_p(pl.data_ptr()), nb)
+    assert st == 0
+    bins = torch.empty(n, dtype=torch.int32, device="cuda")
+    assert _lib.lib.skml_dense_bins_i32(ctx.handle, C.c_void_p(pl.data_ptr()), C.c_void_p(bins.data_ptr()), n) == 0
+    torch.cuda.synchronize()
+    return bins.cpu().numpy()
+
+
+def _oracle_index_of(splits, mn, mx, xs):
+    """Quantizer.indexOf per value (oracle restatement, Quantizer.java:49-72)."""
+    h = O.QuantHeader()
+    h.bin_num = len(splits) + 1
+    h.min, h.max = mn, mx
+    for i, s in enumerate(splits):
+        h.splits[i] = float(s)
+    if mn > 0.0:
+        h.zero_idx = 0
+    elif mx < 0.0:
+        h.zero_idx = h.bin_num - 1
+    else:
+        h.zero_idx = int(np.sum(np.asarray(splits) < 0.0))
+    f = O.lib().orc_index_of
+    return np.array([f(C.byref(h), float(v)) for v in xs], dtype=np.int32)
+
+
+@pytest.mark.parametrize("case", ["irrational", "dense_bucket", "two_bins", "wide", "zeros"])
+def test_split_injected_exact_compare(gpu, case):
+    """Double splits that fp32 cannot represent: the LUT / Eytzinger tables hold RU(split) and
+    must still give indexOf's answer for every float, including values adjacent to a split,
+    +-0, +-inf, denormals and NaN (indexOf's NaN bin)."""
+    rng = np.random.default_rng(len(case) * 7919)
+    if case == "irrational":
+        splits = np.sort(rng.standard_normal(255)) * np.pi
+    elif case == "dense_bucket":  # > 15 splits inside one LUT bucket -> Eytzinger fallback
+        splits = 1.0 + np.arange(300) * 3e-7 + 1e-9
+    elif case == "two_bins":
+        splits = np.array([0.1])
+    elif case == "wide":
+        splits = np.sort(np.concatenate([-np.logspace(-40, 38, 60), np.logspace(-40, 38, 60),
+                                         [-1e300, 1e300, -1e-300, 1e-300]]))
+    else:
+        splits = np.array([-1e-45, -0.0, 0.0, 0.0, 1e-45, 1.0])
+    s32 = splits.astype(np.float32)
+    near = np.concatenate([s32, np.nextafter(s32, np.float32(np.inf)), np.nextafter(s32, np.float32(-np.inf))])
+    special = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, -np.nan, 1e-45, -1e-45, 3.4e38, -3.4e38],
+                       dtype=np.float32)
+    body = (rng.standard_normal(40000) * (np.abs(splits).max() if case != "wide" else 1.0)).astype(np.float32)
+    x = np.concatenate([near, special, body, near]).astype(np.float32)
+    mn, mx = -10.0, 10.0
+    got = _encode_with_splits(gpu, torch.from_numpy(x).cuda(), splits, mn, mx)
+    want = _oracle_index_of(splits, mn, mx, x.astype(np.float64))
+    assert np.array_equal(got, want)
+
+
 def test_decode_sum(gpu):
     from sketchml_amd import _lib
     n, P = 100003, 3
