@@ -178,6 +178,11 @@ int skml_sparse_encode_f32(skml_ctx* ctx, const float* dense_dev, int64_t dim,
 int skml_sparse_decode_f32(skml_ctx* ctx, const skml_sparse* s, int32_t* keys_dev,
                            float* vals_dev);
 int skml_sparse_nnz(const skml_sparse* s, int64_t* nnz);
+/* SparseVectorCompressor.timesBy (sample/SparseVectorCompressor.java:128-134): scales the
+ * double quantValues table in place (the scaled values are what decode returns, as fp32). */
+int skml_sparse_times_by(skml_sparse* s, double x);
+/* quantValues (Quantizer.getValues times every timesBy factor): min(bin_num, cap) doubles. */
+int skml_sparse_values(const skml_sparse* s, double* out, int32_t cap);
 /* Header of the quantizer inside the sparse payload (bins, zero index, splits). */
 int skml_sparse_quant_info(const skml_sparse* s, skml_dense_header* hdr, double* splits_host,
                            int32_t splits_cap);

@@ -9,8 +9,11 @@ from .compressor import DenseVectorCompressor
 from .context import Context, alloc_aligned, get_context
 from .exceptions import QuantileSketchException, SketchMLException
 from .quantization import QuantileQuantizer, QuantizationType, Quantizer
+from .sparse import (DeltaAdaptiveEncoder, GroupedMinMaxSketch, SparseVectorCompressor, encode_dense_as_sparse,
+                     encode_sparse, to_sparse)
 
-__all__ = ["Context", "DenseVectorCompressor", "QuantileQuantizer", "QuantizationType", "Quantizer",
+__all__ = ["Context", "DeltaAdaptiveEncoder", "DenseVectorCompressor", "GroupedMinMaxSketch",
+           "SparseVectorCompressor", "encode_dense_as_sparse", "encode_sparse", "to_sparse", "QuantileQuantizer", "QuantizationType", "Quantizer",
            "QuantileSketchException", "SketchMLException", "get_context", "alloc_aligned"]
 
 LIB_PATH = _lib.LIB_PATH

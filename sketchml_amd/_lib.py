@@ -81,6 +81,8 @@ _SIGS = {
     "skml_sparse_encode_f32": (C.c_int, [vp, vp, i64, C.POINTER(Params), C.POINTER(vp)]),
     "skml_sparse_decode_f32": (C.c_int, [vp, vp, vp, vp]),
     "skml_sparse_nnz": (C.c_int, [vp, i64p]),
+    "skml_sparse_times_by": (C.c_int, [vp, C.c_double]),
+    "skml_sparse_values": (C.c_int, [vp, dblp, i32]),
     "skml_sparse_quant_info": (C.c_int, [vp, C.POINTER(DenseHeader), dblp, i32]),
     "skml_sparse_group_info": (C.c_int, [vp, vp, i32, C.POINTER(SparseGroup), i32p,
                                          C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),

@@ -59,7 +59,11 @@ struct skml_ctx {
     // staging
     void* stage = nullptr;
     size_t stage_cap = 0;
-    SparseWorkspace sparse;
+    // sparse path: grow-only device scratch slots and pinned host staging
+    void* scratch[kScratchSlots] = {};
+    size_t scratch_cap[kScratchSlots] = {};
+    void* pinned = nullptr;
+    size_t pinned_cap = 0;
     // per-kernel event timing (skml_ctx_set_timing)
     bool timing = false;
     std::vector<hipEvent_t> ev[SKML_K_COUNT];  // start/stop pairs
@@ -276,7 +280,9 @@ int skml_ctx_destroy(skml_ctx* c) {
     if (c->stage) (void)hipFree(c->stage);
     for (int k = 0; k < SKML_K_COUNT; k++)
         for (hipEvent_t e : c->ev[k]) (void)hipEventDestroy(e);
-    sparse_ws_free(&c->sparse);
+    for (int i = 0; i < kScratchSlots; i++)
+        if (c->scratch[i]) (void)hipFree(c->scratch[i]);
+    if (c->pinned) (void)hipHostFree(c->pinned);
     if (c->own_stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return SKML_OK;
@@ -687,6 +693,36 @@ int skml_allgather(skml_ctx* c, skml_comm* cm, const void* payload, size_t bytes
 namespace skml {
 hipStream_t ctx_stream(skml_ctx* c) { return c->stream; }
 int ctx_device(skml_ctx* c) { return c->device; }
-SparseWorkspace* ctx_sparse_ws(skml_ctx* c) { return &c->sparse; }
 int set_error(int code, const char* msg) { return fail(code, "%s", msg); }
+bool ctx_timing(skml_ctx* c) { return c->timing; }
+void* ctx_scratch(skml_ctx* c, int slot, size_t bytes) {
+    if (slot < 0 || slot >= kScratchSlots) return nullptr;
+    if (bytes == 0) bytes = 256;
+    if (bytes > c->scratch_cap[slot]) {
+        if (c->scratch[slot]) {
+            (void)hipStreamSynchronize(c->stream);
+            (void)hipFree(c->scratch[slot]);
+        }
+        c->scratch[slot] = nullptr;
+        c->scratch_cap[slot] = 0;
+        const size_t cap = align_up(bytes + bytes / 8, 256);
+        if (hipMalloc(&c->scratch[slot], cap) != hipSuccess) return nullptr;
+        c->scratch_cap[slot] = cap;
+    }
+    return c->scratch[slot];
+}
+void* ctx_pinned(skml_ctx* c, size_t bytes) {
+    if (bytes > c->pinned_cap) {
+        if (c->pinned) {
+            (void)hipStreamSynchronize(c->stream);
+            (void)hipHostFree(c->pinned);
+        }
+        c->pinned = nullptr;
+        c->pinned_cap = 0;
+        const size_t cap = align_up(bytes + bytes / 8 + 4096, 4096);
+        if (hipHostMalloc(&c->pinned, cap, hipHostMallocDefault) != hipSuccess) return nullptr;
+        c->pinned_cap = cap;
+    }
+    return c->pinned;
+}
 }  // namespace skml

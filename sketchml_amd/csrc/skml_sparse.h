@@ -1,4 +1,5 @@
-// skml_sparse.h -- sparse-path workspace shared between skml_api.cpp and skml_sparse.hip.
+// skml_sparse.h -- sparse-path device structures and launchers shared by skml_sparse_api.cpp and
+// skml_sparse.hip (SparseVectorCompressor / GroupedMinMaxSketch / DeltaAdaptiveEncoder).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stddef.h>
@@ -8,16 +9,91 @@
 
 namespace skml {
 
-struct SparseWorkspace {
-    void* buf = nullptr;
-    size_t cap = 0;
-};
-void sparse_ws_free(SparseWorkspace* w);
+constexpr int kMaxGroups = 64;  // GroupedMinMaxSketch groups (Java: any int; 8 by default)
+constexpr int kMaxRows = 8;     // MinMaxSketch rows <= the 8 hash functions (HashFactory.java:24-27)
 
-// accessors into the opaque context (skml_api.cpp)
+// Group table in device memory, filled by the host between the partition and the encode passes.
+// Group g holds grouped elements [gstart[g], gstart[g+1]).
+struct SpGroups {
+    int32_t G, rows, zero, bin_num;
+    int32_t fill;  // MinMaxSketch table sentinel (MinMaxSketch.java:30-33)
+    int32_t pad0;
+    int32_t edges[kMaxGroups];  // FSketchUtils.calGroupEdges
+    int64_t gstart[kMaxGroups + 1];
+    int32_t cols[kMaxGroups];
+    int64_t tab_off[kMaxGroups];  // first cell of group g's rows*cols table
+    int32_t hash_ids[kMaxGroups][kMaxRows];
+    int32_t m[kMaxGroups];     // DeltaAdaptiveEncoder.numIntervals
+    int32_t kind[kMaxGroups];  // DeltaAdaptiveEncoder.flagKind (0 fixed, 1 unary)
+    int64_t fb[kMaxGroups + 1];  // first flag bit of group g in the concatenated flag stream
+    int64_t db[kMaxGroups + 1];  // first delta bit of group g in the concatenated delta stream
+    int32_t kind1_before[kMaxGroups];  // elements of unary-flag groups before g (decode select)
+};
+
+constexpr int kSpThreads = 256;
+constexpr int kSpTile = 2048;             // elements per workgroup tile (8 per thread)
+constexpr int kCompactTile = 4096;        // dense elements per compaction tile (16 per thread)
+constexpr int kDeltaHist = 33;            // bitsNeeded in 1..32
+
+inline int64_t sp_tiles(int64_t n, int64_t tile) { return (n + tile - 1) / tile; }
+
+// ---- launchers (skml_sparse.hip) ----
+// DenseDoubleGradient.toSparse: keys/vals of |x| > 1e-8 in index order.  status/ticket zeroed.
+hipError_t launch_compact(hipStream_t st, const float* x, int64_t dim, int32_t* keys, float* vals,
+                          uint64_t* status, unsigned* ticket, int64_t* nnz_out);
+// Exclusive scan, in place, of each of K columns of a [tiles][K] u64 table; totals -> row `tiles`.
+hipError_t launch_scan_cols(hipStream_t st, uint64_t* sums, int64_t tiles, int K);
+// FSketchUtils.partition: per-tile group counts, then the stable scatter into group order.
+hipError_t launch_part_count(hipStream_t st, const void* qpayload, int64_t n, const SpGroups* gp,
+                             uint64_t* tile_counts);
+hipError_t launch_part_scatter(hipStream_t st, const int32_t* keys, const void* qpayload, int64_t n,
+                               const SpGroups* gp, const uint64_t* tile_base, int32_t* gkeys,
+                               int32_t* gbins);
+// Deltas, bitsNeeded histogram, order check and MinMaxSketch.insert (u64 cells, pre-filled ~0).
+hipError_t launch_group_prep(hipStream_t st, const int32_t* gkeys, const int32_t* gbins, int64_t n,
+                             const SpGroups* gp, uint8_t* need, uint32_t* hist, uint32_t* err,
+                             uint64_t* cells);
+hipError_t launch_minmax_finalize(hipStream_t st, const uint64_t* cells, int64_t ncells, int32_t fill,
+                                  int32_t* table);
+// DeltaAdaptiveEncoder bit streams: tile sums of (flag bits, delta bits), then the writer.
+hipError_t launch_delta_lens(hipStream_t st, const uint8_t* need, int64_t n, const SpGroups* gp,
+                             uint64_t* tile_sums);
+hipError_t launch_delta_write(hipStream_t st, const int32_t* gkeys, const uint8_t* need, int64_t n,
+                              SpGroups* gp, const uint64_t* tile_base, uint64_t* flag_words,
+                              uint64_t* delta_words);
+// ---- decode (GroupedMinMaxSketch.restore) ----
+hipError_t launch_unary_count(hipStream_t st, const uint64_t* flag_words, int64_t nwords,
+                              const SpGroups* gp, uint64_t* tile_sums);
+hipError_t launch_unary_select(hipStream_t st, const uint64_t* flag_words, int64_t nwords,
+                               const SpGroups* gp, const uint64_t* tile_base, int64_t* end_pos);
+hipError_t launch_dec_lens(hipStream_t st, const uint64_t* flag_words, int64_t n_flag_words,
+                           const int64_t* end_pos, int64_t n, const SpGroups* gp, uint8_t* dlen,
+                           uint64_t* tile_sums);
+hipError_t launch_dec_deltas(hipStream_t st, const uint64_t* delta_words, int64_t n_delta_words,
+                             const uint8_t* dlen, int64_t n, const SpGroups* gp,
+                             const uint64_t* tile_base, uint32_t* delta, uint64_t* tile_sums);
+hipError_t launch_group_prefix(hipStream_t st, const uint32_t* delta, int64_t n, const SpGroups* gp, int G,
+                               const uint64_t* tile_base, uint64_t* gpre);
+hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, const SpGroups* gp,
+                           const uint64_t* tile_base, const uint64_t* gpre, const int32_t* table,
+                           int32_t* gkeys, int32_t* gbins);
+// One round of pairwise stable merges of sorted runs (Sort.merge order: lower run first on ties).
+// run_start: nruns + 1 device offsets; total = run_start[nruns].
+hipError_t launch_merge_round(hipStream_t st, const int32_t* kin, const int32_t* bin_in, int32_t* kout,
+                              int32_t* bout, const int64_t* run_start, int nruns, int64_t total);
+// values[bins[i]] from the double quantValues LUT (SparseVectorCompressor.java:118-126).
+hipError_t launch_bin_values(hipStream_t st, const int32_t* bins, int64_t n, const double* qvalues, int B,
+                             float* vals);
+
+// ---- context services (skml_api.cpp) ----
 hipStream_t ctx_stream(skml_ctx* c);
 int ctx_device(skml_ctx* c);
-SparseWorkspace* ctx_sparse_ws(skml_ctx* c);
+// grow-only device scratch buffer `slot` (< kScratchSlots) of at least `bytes`; null on failure
+constexpr int kScratchSlots = 16;
+void* ctx_scratch(skml_ctx* c, int slot, size_t bytes);
+// pinned host staging of at least `bytes`
+void* ctx_pinned(skml_ctx* c, size_t bytes);
 int set_error(int code, const char* msg);
+bool ctx_timing(skml_ctx* c);
 
 }  // namespace skml

@@ -1,25 +1,955 @@
-// skml_sparse.hip -- sparse path (placeholder until the device implementation lands).
+// skml_sparse.hip -- CDNA4 (gfx950) kernels of the sparse codec (SketchGradient.fromSparse /
+// SparseVectorCompressor.compressSparse and restore):
+//   k_compact        DenseDoubleGradient.toSparse (ml/gradient/DenseDoubleGradient.scala:64-89):
+//                    single-pass stream compaction with decoupled look-back (ticketed tiles).
+//   k_part_*         FSketchUtils.partition (frequency/FSketchUtils.java:30-47): stable counting
+//                    sort of (key, bin) by group, group = #{edges <= bin}.
+//   k_group_prep     DeltaAdaptiveEncoder.encode step 1 (binary/DeltaAdaptiveEncoder.java:54-71)
+//                    and MinMaxSketch.insert (frequency/MinMaxSketch.java:48-55) as a 64-bit
+//                    atomicMin on (|bin-zero|, key, bin): the smaller distance wins, ties keep the
+//                    earlier (= smaller key, keys ascend within a group) insert.
+//   k_delta_*        DeltaAdaptiveEncoder.encode step 3 (:72-109): per-element bit lengths, a
+//                    tile scan, and a writer that packs MSB-first fields (BinaryUtils.setBits) into
+//                    an LDS window of 64-bit BitSet words, flushing boundary words atomically.
+//   k_unary_* / k_dec_*  DeltaAdaptiveEncoder.decode (:114-146) in parallel: unary flags are
+//                    resolved by selecting zero bits, delta offsets and keys by scans.
+//   k_merge_round    Sort.merge (util/Sort.java:362-379) as rounds of stable merge-path merges.
+#include <algorithm>
+
+#include "skml_device.hpp"
 #include "skml_sparse.h"
 
 namespace skml {
-void sparse_ws_free(SparseWorkspace* w) {
-    if (w->buf) (void)hipFree(w->buf);
-    w->buf = nullptr;
-    w->cap = 0;
-}
-}  // namespace skml
 
-extern "C" {
-static int nyi() { return skml::set_error(SKML_E_STATE, "sparse path not built yet"); }
-int skml_sparse_compact_f32(skml_ctx*, const float*, int64_t, int32_t*, float*, int64_t*) { return nyi(); }
-int skml_sparse_encode_kv_f32(skml_ctx*, const int32_t*, const float*, int64_t, const skml_params*, skml_sparse**) { return nyi(); }
-int skml_sparse_encode_f32(skml_ctx*, const float*, int64_t, const skml_params*, skml_sparse**) { return nyi(); }
-int skml_sparse_decode_f32(skml_ctx*, const skml_sparse*, int32_t*, float*) { return nyi(); }
-int skml_sparse_nnz(const skml_sparse*, int64_t*) { return nyi(); }
-int skml_sparse_quant_info(const skml_sparse*, skml_dense_header*, double*, int32_t) { return nyi(); }
-int skml_sparse_group_info(skml_ctx*, const skml_sparse*, int32_t, skml_sparse_group*, int32_t*, uint64_t*, uint64_t*) { return nyi(); }
-int skml_sparse_serialize(skml_ctx*, const skml_sparse*, uint8_t*, size_t, size_t*) { return nyi(); }
-int skml_sparse_free(skml_sparse*) { return SKML_OK; }
-int skml_delta_encode(skml_ctx*, const int32_t*, int64_t, int32_t*, int32_t*, int64_t*, int64_t*, uint64_t*, uint64_t*, int64_t) { return nyi(); }
-int skml_delta_decode(skml_ctx*, int64_t, int32_t, int32_t, const uint64_t*, int64_t, const uint64_t*, int64_t, int32_t*) { return nyi(); }
+constexpr uint64_t kStAgg = 1ULL << 62, kStPre = 2ULL << 62, kStMask = (1ULL << 62) - 1;
+
+// ---------------------------------------------------------------------------------------------
+// block scan helpers (256 threads)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t wave_incl_u64(uint64_t v, int lane) {
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint64_t y = __shfl_up(v, off, 64);
+        if (lane >= off) v += y;
+    }
+    return v;
 }
+
+// v[k] -> exclusive prefix over the block; total[k] = block sum.  sh: 4*K u64 of LDS.
+template <int K>
+__device__ __forceinline__ void block_excl_scan(uint64_t (&v)[K], uint64_t (&total)[K], uint64_t* sh) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    uint64_t inc[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        inc[k] = wave_incl_u64(v[k], lane);
+        if (lane == 63) sh[w * K + k] = inc[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        uint64_t base = 0, tot = 0;
+#pragma unroll
+        for (int j = 0; j < kSpThreads / 64; j++) {
+            const uint64_t s = sh[j * K + k];
+            base += j < w ? s : 0;
+            tot += s;
+        }
+        v[k] = base + inc[k] - v[k];
+        total[k] = tot;
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ uint64_t ld_acquire(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_release(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// packed code of element e (LSB-first codes, code_bits in {1,2,4,8,16})
+__device__ __forceinline__ int32_t code_at(const uint8_t* codes, int64_t e, int bits) {
+    switch (bits) {
+        case 8: return codes[e];
+        case 16: return reinterpret_cast<const uint16_t*>(codes)[e];
+        case 4: return (codes[e >> 1] >> ((e & 1) * 4)) & 15;
+        case 2: return (codes[e >> 2] >> ((e & 3) * 2)) & 3;
+        default: return (codes[e >> 3] >> (e & 7)) & 1;
+    }
+}
+
+// #{edges[j] <= bin} over a sorted 64-entry LDS table padded with INT32_MAX
+__device__ __forceinline__ int group_of_bin(const int32_t* E, int32_t bin) {
+    int g = 0;
+#pragma unroll
+    for (int step = 32; step >= 1; step >>= 1)
+        if (E[g + step - 1] <= bin) g += step;
+    return g;
+}
+// group g with gstart[g] <= i < gstart[g+1] (S: G+1 offsets in LDS, padded to 65 with INT64_MAX)
+__device__ __forceinline__ int group_of_elem(const int64_t* S, int64_t i) {
+    int g = 0;
+#pragma unroll
+    for (int step = 32; step >= 1; step >>= 1)
+        if (S[g + step] <= i) g += step;
+    return g;
+}
+
+__device__ __forceinline__ void load_edges(const SpGroups* gp, int32_t* E) {
+    for (int j = threadIdx.x; j < kMaxGroups; j += blockDim.x) E[j] = j < gp->G ? gp->edges[j] : INT32_MAX;
+}
+__device__ __forceinline__ void load_starts(const SpGroups* gp, int64_t* S) {
+    for (int j = threadIdx.x; j <= kMaxGroups; j += blockDim.x) S[j] = j <= gp->G ? gp->gstart[j] : INT64_MAX;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Java Int2IntHash family (hash/BJHash.java:10-20, Mix64Hash.java:10-21, TWHash.java:10-20,
+// BKDRHash.java:13-21), int32 wrap-around arithmetic; code % size folded non-negative.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t sar(uint32_t c, int s) { return (uint32_t)((int32_t)c >> s); }
+
+__device__ __forceinline__ int32_t java_hash(int id, int32_t key, int32_t size) {
+    uint32_t c = (uint32_t)key;
+    if (id == 0) {
+        c = (c + 0x7ed55d16u) + (c << 12);
+        c = (c ^ 0xc761c23cu) ^ sar(c, 19);
+        c = (c + 0x165667b1u) + (c << 5);
+        c = (c + 0xd3a2646cu) ^ (c << 9);
+        c = (c + 0xfd7046c5u) + (c << 3);
+        c = (c ^ 0xb55a4f09u) ^ sar(c, 16);
+    } else if (id == 1) {
+        c = ~c + (c << 21);
+        c = c ^ sar(c, 24);
+        c = (c + (c << 3)) + (c << 8);
+        c = c ^ sar(c, 14);
+        c = (c + (c << 2)) + (c << 4);
+        c = c ^ sar(c, 28);
+        c = c + (c << 31);
+    } else if (id == 2) {
+        c = ~c + (c << 15);
+        c = c ^ sar(c, 12);
+        c = c + (c << 2);
+        c = c ^ sar(c, 4);
+        c = c * 2057u;
+        c = c ^ sar(c, 16);
+    } else {
+        const uint32_t seed = id == 3 ? 31u : id == 4 ? 131u : id == 5 ? 267u : id == 6 ? 1313u : 13131u;
+        int32_t k = key;
+        c = 0;
+        while (k != 0) {
+            c = seed * c + (uint32_t)(k % 10);
+            k /= 10;
+        }
+    }
+    int32_t r = (int32_t)c % size;
+    return r >= 0 ? r : r + size;
+}
+
+// |v - zero| with Java int wrap (MinMaxSketch.compare, MinMaxSketch.java:80-86)
+__device__ __forceinline__ int32_t mm_dist(int32_t v, int32_t zero) {
+    const int32_t d = (int32_t)((uint32_t)v - (uint32_t)zero);
+    return d < 0 ? (int32_t)(0u - (uint32_t)d) : d;
+}
+
+// =============================================================================================
+// Compaction (decoupled look-back)
+// =============================================================================================
+__global__ __launch_bounds__(kSpThreads) void k_compact(const float* __restrict__ x, int64_t dim,
+                                                        int32_t* __restrict__ keys, float* __restrict__ vals,
+                                                        uint64_t* status, unsigned* ticket, int64_t ntiles,
+                                                        int64_t* nnz_out) {
+    __shared__ float4 sx[kCompactTile / 4];
+    __shared__ uint64_t sh[8];
+    __shared__ int64_t s_tile;
+    __shared__ uint64_t s_excl;
+    const int t = threadIdx.x;
+    if (t == 0) s_tile = (int64_t)atomicAdd(ticket, 1u);
+    __syncthreads();
+    const int64_t tile = s_tile;
+    const int64_t base = tile * kCompactTile;
+    const int64_t lim = dim - base;
+    if (lim >= kCompactTile && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+        typedef float f32x4 __attribute__((ext_vector_type(4)));
+        const f32x4* src = reinterpret_cast<const f32x4*>(x + base);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const f32x4 f = __builtin_nontemporal_load(src + j * kSpThreads + t);
+            sx[j * kSpThreads + t] = make_float4(f.x, f.y, f.z, f.w);
+        }
+    } else {
+        float* s = reinterpret_cast<float*>(sx);
+        for (int i = t; i < kCompactTile; i += kSpThreads) s[i] = i < lim ? x[base + i] : 0.0f;
+    }
+    __syncthreads();
+    float v[16];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const float4 f = sx[t * 4 + q];
+        v[4 * q] = f.x;
+        v[4 * q + 1] = f.y;
+        v[4 * q + 2] = f.z;
+        v[4 * q + 3] = f.w;
+    }
+    uint32_t keep = 0;
+#pragma unroll
+    for (int j = 0; j < 16; j++) keep |= (fabs((double)v[j]) > 1e-8) ? (1u << j) : 0u;  // Maths.scala:8 EPS
+    uint64_t c[1] = {(uint64_t)__popc(keep)}, tot[1];
+    block_excl_scan<1>(c, tot, sh);
+    if (t == 0) {
+        uint64_t excl = 0;
+        if (tile == 0) {
+            st_release(&status[0], kStPre | tot[0]);
+        } else {
+            st_release(&status[tile], kStAgg | tot[0]);
+            int64_t p = tile - 1;
+            while (true) {
+                const uint64_t s = ld_acquire(&status[p]);
+                const uint64_t f = s & ~kStMask;
+                if (f == 0) {
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                excl += s & kStMask;
+                if (f == kStPre) break;
+                p--;
+            }
+            st_release(&status[tile], kStPre | (excl + tot[0]));
+        }
+        s_excl = excl;
+        if (tile == ntiles - 1) *nnz_out = (int64_t)(excl + tot[0]);
+    }
+    __syncthreads();
+    int64_t pos = (int64_t)(s_excl + c[0]);
+    const int64_t e0 = base + t * 16;
+#pragma unroll
+    for (int j = 0; j < 16; j++)
+        if (keep & (1u << j)) {
+            keys[pos] = (int32_t)(e0 + j);
+            vals[pos] = v[j];
+            pos++;
+        }
+}
+
+hipError_t launch_compact(hipStream_t st, const float* x, int64_t dim, int32_t* keys, float* vals,
+                          uint64_t* status, unsigned* ticket, int64_t* nnz_out) {
+    const int64_t tiles = sp_tiles(dim, kCompactTile);
+    if (tiles <= 0) return hipMemsetAsync(nnz_out, 0, sizeof(int64_t), st);
+    hipLaunchKernelGGL(k_compact, dim3((unsigned)tiles), dim3(kSpThreads), 0, st, x, dim, keys, vals, status,
+                       ticket, tiles, nnz_out);
+    return hipGetLastError();
+}
+
+// =============================================================================================
+// Column scan of [tiles][K] u64 tile sums (one workgroup per column)
+// =============================================================================================
+__global__ __launch_bounds__(kSpThreads) void k_scan_cols(uint64_t* sums, int64_t tiles, int K) {
+    __shared__ uint64_t sh[4];
+    const int k = blockIdx.x, t = threadIdx.x;
+    uint64_t carry = 0;
+    for (int64_t c0 = 0; c0 < tiles; c0 += kSpThreads * 8) {
+        uint64_t loc[8], s = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int64_t i = c0 + t * 8 + j;
+            loc[j] = i < tiles ? sums[i * K + k] : 0;
+            s += loc[j];
+        }
+        uint64_t v[1] = {s}, tot[1];
+        block_excl_scan<1>(v, tot, sh);
+        uint64_t run = carry + v[0];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int64_t i = c0 + t * 8 + j;
+            if (i < tiles) sums[i * K + k] = run;
+            run += loc[j];
+        }
+        carry += tot[0];
+    }
+    if (t == 0) sums[tiles * K + k] = carry;
+}
+
+hipError_t launch_scan_cols(hipStream_t st, uint64_t* sums, int64_t tiles, int K) {
+    hipLaunchKernelGGL(k_scan_cols, dim3(K), dim3(kSpThreads), 0, st, sums, tiles, K);
+    return hipGetLastError();
+}
+
+// =============================================================================================
+// Partition by group (stable)
+// =============================================================================================
+__global__ __launch_bounds__(kSpThreads) void k_part_count(const uint8_t* __restrict__ qpayload, int64_t n,
+                                                           const SpGroups* __restrict__ gp,
+                                                           uint64_t* __restrict__ tile_counts) {
+    __shared__ int32_t E[kMaxGroups];
+    __shared__ uint32_t cnt[kMaxGroups];
+    const skml_dense_header* h = reinterpret_cast<const skml_dense_header*>(qpayload);
+    const uint8_t* codes = qpayload + h->codes_offset;
+    const int bits = h->code_bits, G = gp->G;
+    load_edges(gp, E);
+    for (int j = threadIdx.x; j < kMaxGroups; j += kSpThreads) cnt[j] = 0;
+    __syncthreads();
+    const int64_t base = (int64_t)blockIdx.x * kSpTile;
+    for (int j = threadIdx.x; j < kSpTile; j += kSpThreads) {
+        const int64_t i = base + j;
+        if (i < n) atomicAdd(&cnt[group_of_bin(E, code_at(codes, i, bits))], 1u);
+    }
+    __syncthreads();
+    for (int g = threadIdx.x; g < G; g += kSpThreads) tile_counts[(int64_t)blockIdx.x * G + g] = cnt[g];
+}
+
+hipError_t launch_part_count(hipStream_t st, const void* qpayload, int64_t n, const SpGroups* gp,
+                             uint64_t* tile_counts) {
+    const int64_t tiles = sp_tiles(n, kSpTile);
+    if (tiles <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_part_count, dim3((unsigned)tiles), dim3(kSpThreads), 0, st,
+                       reinterpret_cast<const uint8_t*>(qpayload), n, gp, tile_counts);
+    return hipGetLastError();
+}
+
+// Wave w of the tile owns elements [w*512, (w+1)*512), 64 per step in order; lanes with the same
+// group are ranked by lane (peer mask from log2(G) ballots), so the scatter is stable.
+__global__ __launch_bounds__(kSpThreads) void k_part_scatter(const int32_t* __restrict__ keys,
+                                                             const uint8_t* __restrict__ qpayload, int64_t n,
+                                                             const SpGroups* __restrict__ gp,
+                                                             const uint64_t* __restrict__ tile_base,
+                                                             int32_t* __restrict__ gkeys, int32_t* __restrict__ gbins) {
+    constexpr int kWaves = kSpThreads / 64, kSteps = kSpTile / kSpThreads;
+    __shared__ int32_t E[kMaxGroups];
+    __shared__ int64_t wb[kWaves][kMaxGroups];  // running output position per (wave, group)
+    const skml_dense_header* h = reinterpret_cast<const skml_dense_header*>(qpayload);
+    const uint8_t* codes = qpayload + h->codes_offset;
+    const int bits = h->code_bits, G = gp->G;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    load_edges(gp, E);
+    for (int j = t; j < kWaves * kMaxGroups; j += kSpThreads) wb[j / kMaxGroups][j % kMaxGroups] = 0;
+    __syncthreads();
+    const int64_t base = (int64_t)blockIdx.x * kSpTile + (int64_t)w * (kSpTile / kWaves);
+    int32_t kk[kSteps], gg[kSteps], bb[kSteps];
+#pragma unroll
+    for (int s = 0; s < kSteps; s++) {
+        const int64_t i = base + s * 64 + lane;
+        gg[s] = -1;
+        if (i < n) {
+            kk[s] = keys[i];
+            bb[s] = code_at(codes, i, bits);
+            gg[s] = group_of_bin(E, bb[s]);
+            atomicAdd(reinterpret_cast<unsigned long long*>(&wb[w][gg[s]]), 1ull);
+        }
+    }
+    __syncthreads();
+    if (t < G) {  // wave-exclusive offsets per group, plus the group's start and tile base
+        int64_t run = gp->gstart[t] + (int64_t)tile_base[(int64_t)blockIdx.x * G + t];
+        for (int j = 0; j < kWaves; j++) {
+            const int64_t c = wb[j][t];
+            wb[j][t] = run;
+            run += c;
+        }
+    }
+    __syncthreads();
+    int nb = 0;
+    while ((1 << nb) < G) nb++;
+    const uint64_t lt = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int s = 0; s < kSteps; s++) {
+        const bool valid = gg[s] >= 0;
+        uint64_t peers = __ballot(valid);
+        for (int b = 0; b < nb; b++) {
+            const uint64_t bal = __ballot(valid && ((gg[s] >> b) & 1));
+            peers &= ((gg[s] >> b) & 1) ? bal : ~bal;
+        }
+        if (valid) {
+            const int64_t dst = wb[w][gg[s]] + __popcll(peers & lt);
+            gkeys[dst] = kk[s];
+            gbins[dst] = bb[s];
+        }
+        // every lane has read its base; the leader of each peer set advances it
+        __builtin_amdgcn_wave_barrier();
+        if (valid && (peers & lt) == 0) wb[w][gg[s]] += __popcll(peers);
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+hipError_t launch_part_scatter(hipStream_t st, const int32_t* keys, const void* qpayload, int64_t n,
+                               const SpGroups* gp, const uint64_t* tile_base, int32_t* gkeys,
+                               int32_t* gbins) {
+    const int64_t tiles = sp_tiles(n, kSpTile);
+    if (tiles <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_part_scatter, dim3((unsigned)tiles), dim3(kSpThreads), 0, st, keys,
+                       reinterpret_cast<const uint8_t*>(qpayload), n, gp, tile_base, gkeys, gbins);
+    return hipGetLastError();
+}
+
+// =============================================================================================
+// Group prep: deltas / bitsNeeded / order check / MinMax insert
+// =============================================================================================
+__global__ __launch_bounds__(kSpThreads) void k_group_prep(const int32_t* __restrict__ gkeys,
+                                                           const int32_t* __restrict__ gbins, int64_t n,
+                                                           const SpGroups* __restrict__ gp,
+                                                           uint8_t* __restrict__ need, uint32_t* __restrict__ hist,
+                                                           uint32_t* __restrict__ err, uint64_t* __restrict__ cells) {
+    __shared__ int64_t S[kMaxGroups + 1];
+    __shared__ uint32_t H[kMaxGroups * kDeltaHist];
+    const int G = gp->G, rows = gp->rows, zero = gp->zero;
+    load_starts(gp, S);
+    for (int j = threadIdx.x; j < G * kDeltaHist; j += kSpThreads) H[j] = 0;
+    __syncthreads();
+    uint32_t bad = 0;
+    for (int64_t i = (int64_t)blockIdx.x * kSpThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kSpThreads) {
+        const int g = group_of_elem(S, i);
+        const int32_t key = gkeys[i], bin = gbins[i];
+        const bool first = i == S[g];
+        const int32_t d = first ? key : (int32_t)((uint32_t)key - (uint32_t)gkeys[i - 1]);
+        int nb;
+        if (first && d == 0) nb = 1;
+        else {
+            if (d <= 0) bad = 1;  // Maths.log2nlz: "Log for <d>" (util/Maths.java:16-21)
+            nb = d > 0 ? 32 - __clz(d) : 1;
+        }
+        need[i] = (uint8_t)nb;
+        atomicAdd(&H[g * kDeltaHist + nb], 1u);
+        const int32_t cols = gp->cols[g];
+        const uint64_t cell = ((uint64_t)mm_dist(bin, zero) << 47) | ((uint64_t)(uint32_t)key << 16) |
+                              (uint64_t)(uint32_t)bin;
+        for (int r = 0; r < rows; r++) {
+            const int64_t idx = gp->tab_off[g] + (int64_t)r * cols + java_hash(gp->hash_ids[g][r], key, cols);
+            atomicMin(reinterpret_cast<unsigned long long*>(&cells[idx]), (unsigned long long)cell);
+        }
+    }
+    if (bad) atomicOr(err, 1u);
+    __syncthreads();
+    for (int j = threadIdx.x; j < G * kDeltaHist; j += kSpThreads)
+        if (H[j]) atomicAdd(&hist[j], H[j]);
+}
+
+hipError_t launch_group_prep(hipStream_t st, const int32_t* gkeys, const int32_t* gbins, int64_t n,
+                             const SpGroups* gp, uint8_t* need, uint32_t* hist, uint32_t* err,
+                             uint64_t* cells) {
+    if (n <= 0) return hipSuccess;
+    const int64_t grid = std::min<int64_t>(sp_tiles(n, kSpThreads * 4), 2048);
+    hipLaunchKernelGGL(k_group_prep, dim3((unsigned)grid), dim3(kSpThreads), 0, st, gkeys, gbins, n, gp, need,
+                       hist, err, cells);
+    return hipGetLastError();
+}
+
+__global__ void k_minmax_finalize(const uint64_t* __restrict__ cells, int64_t ncells, int32_t fill,
+                                  int32_t* __restrict__ table) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ncells; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t c = cells[i];
+        table[i] = c == ~0ull ? fill : (int32_t)(c & 0xFFFFu);
+    }
+}
+
+hipError_t launch_minmax_finalize(hipStream_t st, const uint64_t* cells, int64_t ncells, int32_t fill,
+                                  int32_t* table) {
+    if (ncells <= 0) return hipSuccess;
+    const int64_t grid = std::min<int64_t>(sp_tiles(ncells, kSpThreads), 4096);
+    hipLaunchKernelGGL(k_minmax_finalize, dim3((unsigned)grid), dim3(kSpThreads), 0, st, cells, ncells, fill, table);
+    return hipGetLastError();
+}
+
+// =============================================================================================
+// DeltaAdaptive bit streams
+// =============================================================================================
+struct DeltaShape {
+    int bpi, shift, nf, kind;
+};
+__device__ __forceinline__ DeltaShape delta_shape(const SpGroups* gp, int g) {
+    DeltaShape s;
+    const int m = gp->m[g];
+    s.bpi = 32 / m;
+    s.shift = 31 - __clz(s.bpi);
+    s.nf = 31 - __clz(m);
+    s.kind = gp->kind[g];
+    return s;
+}
+// interval count, flag length, delta length of one element
+__device__ __forceinline__ void delta_lens(const DeltaShape& s, int nb, int& iv, int& fl, int& dl) {
+    iv = (nb + s.bpi - 1) >> s.shift;
+    fl = s.kind ? iv + 1 : s.nf;
+    dl = s.bpi * iv;
+}
+
+__global__ __launch_bounds__(kSpThreads) void k_delta_lens(const uint8_t* __restrict__ need, int64_t n,
+                                                           const SpGroups* __restrict__ gp,
+                                                           uint64_t* __restrict__ tile_sums) {
+    __shared__ int64_t S[kMaxGroups + 1];
+    __shared__ uint64_t sh[8];
+    load_starts(gp, S);
+    __syncthreads();
+    const int64_t i0 = (int64_t)blockIdx.x * kSpTile + threadIdx.x * 8;
+    uint64_t fsum = 0, dsum = 0;
+    if (i0 < n) {
+        int g = group_of_elem(S, i0);
+        DeltaShape s = delta_shape(gp, g);
+        for (int j = 0; j < 8 && i0 + j < n; j++) {
+            const int64_t i = i0 + j;
+            while (i >= S[g + 1]) s = delta_shape(gp, ++g);
+            int iv, fl, dl;
+            delta_lens(s, need[i], iv, fl, dl);
+            fsum += fl;
+            dsum += dl;
+        }
+    }
+    uint64_t v[2] = {fsum, dsum}, tot[2];
+    block_excl_scan<2>(v, tot, sh);
+    if (threadIdx.x == 0) {
+        tile_sums[blockIdx.x * 2] = tot[0];
+        tile_sums[blockIdx.x * 2 + 1] = tot[1];
+    }
+}
+
+hipError_t launch_delta_lens(hipStream_t st, const uint8_t* need, int64_t n, const SpGroups* gp,
+                             uint64_t* tile_sums) {
+    const int64_t tiles = sp_tiles(n, kSpTile);
+    if (tiles <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_delta_lens, dim3((unsigned)tiles), dim3(kSpThreads), 0, st, need, n, gp, tile_sums);
+    return hipGetLastError();
+}
+
+// BinaryUtils.setBits (binary/BinaryUtils.java:6-14): value's MSB at the lowest bit position.
+__device__ __forceinline__ void lds_put_bits(uint64_t* win, int64_t rel, uint32_t value, int nbits) {
+    if (nbits <= 0) return;
+    const uint64_t rev = (uint64_t)(__brev(value) >> (32 - nbits));
+    const int64_t w = rel >> 6;
+    const int sh = (int)(rel & 63);
+    atomicOr(reinterpret_cast<unsigned long long*>(&win[w]), (unsigned long long)(rev << sh));
+    if (sh + nbits > 64) atomicOr(reinterpret_cast<unsigned long long*>(&win[w + 1]), (unsigned long long)(rev >> (64 - sh)));
+}
+
+constexpr int kFlagWin = (kSpTile * 17 + 63) / 64 + 2;
+constexpr int kDeltaWin = (kSpTile * 32 + 63) / 64 + 2;
+
+__device__ __forceinline__ void flush_window(const uint64_t* win, int64_t bit0, uint64_t nbits, uint64_t* out) {
+    if (nbits == 0) return;
+    const int64_t w0 = bit0 >> 6, w1 = (bit0 + (int64_t)nbits - 1) >> 6;
+    for (int64_t w = w0 + threadIdx.x; w <= w1; w += kSpThreads) {
+        const uint64_t v = win[w - w0];
+        if (w == w0 || w == w1) {
+            if (v) atomicOr(reinterpret_cast<unsigned long long*>(&out[w]), (unsigned long long)v);
+        } else {
+            out[w] = v;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kSpThreads) void k_delta_write(const int32_t* __restrict__ gkeys,
+                                                            const uint8_t* __restrict__ need, int64_t n,
+                                                            SpGroups* __restrict__ gp,
+                                                            const uint64_t* __restrict__ tile_base,
+                                                            uint64_t* __restrict__ flag_words,
+                                                            uint64_t* __restrict__ delta_words) {
+    __shared__ int64_t S[kMaxGroups + 1];
+    __shared__ uint64_t sh[8];
+    __shared__ uint64_t fwin[kFlagWin];
+    __shared__ uint64_t dwin[kDeltaWin];
+    load_starts(gp, S);
+    for (int j = threadIdx.x; j < kFlagWin; j += kSpThreads) fwin[j] = 0;
+    for (int j = threadIdx.x; j < kDeltaWin; j += kSpThreads) dwin[j] = 0;
+    __syncthreads();
+    const int64_t i0 = (int64_t)blockIdx.x * kSpTile + threadIdx.x * 8;
+    int32_t key[8];
+    uint8_t nb[8];
+    uint64_t fsum = 0, dsum = 0;
+    int g0 = 0;
+    if (i0 < n) {
+        g0 = group_of_elem(S, i0);
+        int g = g0;
+        DeltaShape s = delta_shape(gp, g);
+        for (int j = 0; j < 8; j++) {
+            const int64_t i = i0 + j;
+            if (i >= n) break;
+            while (i >= S[g + 1]) s = delta_shape(gp, ++g);
+            key[j] = gkeys[i];
+            nb[j] = need[i];
+            int iv, fl, dl;
+            delta_lens(s, nb[j], iv, fl, dl);
+            fsum += fl;
+            dsum += dl;
+        }
+    }
+    uint64_t v[2] = {fsum, dsum}, tot[2];
+    block_excl_scan<2>(v, tot, sh);
+    const uint64_t fbase = tile_base[blockIdx.x * 2], dbase = tile_base[blockIdx.x * 2 + 1];
+    const int64_t fw0 = (int64_t)(fbase >> 6) << 6, dw0 = (int64_t)(dbase >> 6) << 6;
+    if (i0 < n) {
+        int g = g0;
+        DeltaShape s = delta_shape(gp, g);
+        uint64_t fo = fbase + v[0], dof = dbase + v[1];
+        int32_t prev = i0 > S[g] ? gkeys[i0 - 1] : 0;
+        for (int j = 0; j < 8; j++) {
+            const int64_t i = i0 + j;
+            if (i >= n) break;
+            while (i >= S[g + 1]) s = delta_shape(gp, ++g);
+            const bool first = i == S[g];
+            if (first) {
+                gp->fb[g] = (int64_t)fo;
+                gp->db[g] = (int64_t)dof;
+            }
+            const uint32_t d = first ? (uint32_t)key[j] : (uint32_t)key[j] - (uint32_t)prev;
+            prev = key[j];
+            int iv, fl, dl;
+            delta_lens(s, nb[j], iv, fl, dl);
+            const uint32_t fv = s.kind ? (uint32_t)((1u << (iv + 1)) - 2u) : (uint32_t)(iv - 1);
+            lds_put_bits(fwin, (int64_t)fo - fw0, fv, fl);
+            // bitsPerInterval * intervalNeeded <= 32; a 32-bit field holds d itself
+            lds_put_bits(dwin, (int64_t)dof - dw0, d, dl);
+            fo += fl;
+            dof += dl;
+        }
+    }
+    __syncthreads();
+    flush_window(fwin, (int64_t)fbase, tot[0], flag_words);
+    flush_window(dwin, (int64_t)dbase, tot[1], delta_words);
+}
+
+hipError_t launch_delta_write(hipStream_t st, const int32_t* gkeys, const uint8_t* need, int64_t n,
+                              SpGroups* gp, const uint64_t* tile_base, uint64_t* flag_words,
+                              uint64_t* delta_words) {
+    const int64_t tiles = sp_tiles(n, kSpTile);
+    if (tiles <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_delta_write, dim3((unsigned)tiles), dim3(kSpThreads), 0, st, gkeys, need, n, gp,
+                       tile_base, flag_words, delta_words);
+    return hipGetLastError();
+}
+
+// =============================================================================================
+// Decode
+// =============================================================================================
+// Mask of the bits of word w that lie in unary-flag groups' flag ranges.
+__device__ __forceinline__ uint64_t unary_mask(const SpGroups* gp, int64_t w) {
+    const int64_t lo = w * 64, hi = lo + 64;
+    uint64_t m = 0;
+    for (int g = 0; g < gp->G; g++) {
+        if (!gp->kind[g]) continue;
+        const int64_t a = std::max(lo, gp->fb[g]), b = std::min(hi, gp->fb[g + 1]);
+        if (a >= b) continue;
+        const int la = (int)(a - lo), lb = (int)(b - lo);
+        const uint64_t upto_b = lb >= 64 ? ~0ull : ((1ull << lb) - 1ull);
+        m |= upto_b & ~((1ull << la) - 1ull);
+    }
+    return m;
+}
+
+__global__ __launch_bounds__(kSpThreads) void k_unary_count(const uint64_t* __restrict__ words, int64_t nwords,
+                                                            const SpGroups* __restrict__ gp,
+                                                            uint64_t* __restrict__ tile_sums) {
+    __shared__ uint64_t sh[4];
+    const int64_t w0 = (int64_t)blockIdx.x * kSpTile + threadIdx.x * 8;
+    uint64_t c = 0;
+    for (int j = 0; j < 8; j++) {
+        const int64_t w = w0 + j;
+        if (w < nwords) c += __popcll(~words[w] & unary_mask(gp, w));
+    }
+    uint64_t v[1] = {c}, tot[1];
+    block_excl_scan<1>(v, tot, sh);
+    if (threadIdx.x == 0) tile_sums[blockIdx.x] = tot[0];
+}
+
+hipError_t launch_unary_count(hipStream_t st, const uint64_t* flag_words, int64_t nwords,
+                              const SpGroups* gp, uint64_t* tile_sums) {
+    const int64_t tiles = sp_tiles(nwords, kSpTile);
+    if (tiles <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_unary_count, dim3((unsigned)tiles), dim3(kSpThreads), 0, st, flag_words, nwords, gp,
+                       tile_sums);
+    return hipGetLastError();
+}
+
+// Zero bit #r (over unary groups, in stream order) ends the flag of element
+// gstart[g] + r - kind1_before[g]; its position is recorded in end_pos.
+__global__ __launch_bounds__(kSpThreads) void k_unary_select(const uint64_t* __restrict__ words, int64_t nwords,
+                                                             const SpGroups* __restrict__ gp,
+                                                             const uint64_t* __restrict__ tile_base,
+                                                             int64_t* __restrict__ end_pos) {
+    __shared__ uint64_t sh[4];
+    const int64_t w0 = (int64_t)blockIdx.x * kSpTile + threadIdx.x * 8;
+    uint64_t z[8], c = 0;
+    for (int j = 0; j < 8; j++) {
+        const int64_t w = w0 + j;
+        z[j] = w < nwords ? (~words[w] & unary_mask(gp, w)) : 0;
+        c += __popcll(z[j]);
+    }
+    uint64_t v[1] = {c}, tot[1];
+    block_excl_scan<1>(v, tot, sh);
+    uint64_t r = tile_base[blockIdx.x] + v[0];
+    int g = 0;
+    for (int j = 0; j < 8; j++) {
+        uint64_t m = z[j];
+        while (m) {
+            const int b = __ffsll((unsigned long long)m) - 1;
+            m &= m - 1;
+            const int64_t p = (w0 + j) * 64 + b;
+            while (g + 1 < gp->G && gp->fb[g + 1] <= p) g++;
+            const int64_t e = gp->gstart[g] + (int64_t)r - gp->kind1_before[g];
+            if (e < gp->gstart[g + 1]) end_pos[e] = p;  // zeros past the last flag are padding
+            r++;
+        }
+    }
+}
+
+hipError_t launch_unary_select(hipStream_t st, const uint64_t* flag_words, int64_t nwords,
+                               const SpGroups* gp, const uint64_t* tile_base, int64_t* end_pos) {
+    const int64_t tiles = sp_tiles(nwords, kSpTile);
+    if (tiles <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_unary_select, dim3((unsigned)tiles), dim3(kSpThreads), 0, st, flag_words, nwords, gp,
+                       tile_base, end_pos);
+    return hipGetLastError();
+}
+
+// BinaryUtils.getBits (binary/BinaryUtils.java:16-25): nbits (<= 32) read MSB-first.
+__device__ __forceinline__ uint32_t get_bits(const uint64_t* words, int64_t nwords, int64_t off, int nbits) {
+    if (nbits <= 0) return 0;
+    const int64_t w = off >> 6;
+    const int sh = (int)(off & 63);
+    uint64_t lo = w < nwords ? words[w] : 0;
+    uint64_t v = lo >> sh;
+    if (sh + nbits > 64) {
+        const uint64_t hi = (w + 1) < nwords ? words[w + 1] : 0;
+        v |= hi << (64 - sh);
+    }
+    const uint32_t field = (uint32_t)(v & (nbits == 64 ? ~0ull : ((1ull << nbits) - 1ull)));
+    return __brev(field) >> (32 - nbits);
+}
+
+__global__ __launch_bounds__(kSpThreads) void k_dec_lens(const uint64_t* __restrict__ fw, int64_t nfw,
+                                                         const int64_t* __restrict__ end_pos, int64_t n,
+                                                         const SpGroups* __restrict__ gp, uint8_t* __restrict__ dlen,
+                                                         uint64_t* __restrict__ tile_sums) {
+    __shared__ int64_t S[kMaxGroups + 1];
+    __shared__ uint64_t sh[4];
+    load_starts(gp, S);
+    __syncthreads();
+    const int64_t i0 = (int64_t)blockIdx.x * kSpTile + threadIdx.x * 8;
+    uint64_t sum = 0;
+    if (i0 < n) {
+        int g = group_of_elem(S, i0);
+        DeltaShape s = delta_shape(gp, g);
+        for (int j = 0; j < 8; j++) {
+            const int64_t i = i0 + j;
+            if (i >= n) break;
+            while (i >= S[g + 1]) s = delta_shape(gp, ++g);
+            int iv;
+            if (!s.kind) {
+                iv = (int)get_bits(fw, nfw, gp->fb[g] + (i - S[g]) * s.nf, s.nf) + 1;
+            } else {
+                const int64_t start = i == S[g] ? gp->fb[g] : end_pos[i - 1] + 1;
+                iv = (int)(end_pos[i] - start);
+            }
+            const int dl = s.bpi * iv;
+            dlen[i] = (uint8_t)dl;
+            sum += dl;
+        }
+    }
+    uint64_t v[1] = {sum}, tot[1];
+    block_excl_scan<1>(v, tot, sh);
+    if (threadIdx.x == 0) tile_sums[blockIdx.x] = tot[0];
+}
+
+hipError_t launch_dec_lens(hipStream_t st, const uint64_t* flag_words, int64_t n_flag_words,
+                           const int64_t* end_pos, int64_t n, const SpGroups* gp, uint8_t* dlen,
+                           uint64_t* tile_sums) {
+    const int64_t tiles = sp_tiles(n, kSpTile);
+    if (tiles <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_dec_lens, dim3((unsigned)tiles), dim3(kSpThreads), 0, st, flag_words, n_flag_words,
+                       end_pos, n, gp, dlen, tile_sums);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(kSpThreads) void k_dec_deltas(const uint64_t* __restrict__ dw, int64_t ndw,
+                                                           const uint8_t* __restrict__ dlen, int64_t n,
+                                                           const uint64_t* __restrict__ tile_base,
+                                                           uint32_t* __restrict__ delta, uint64_t* __restrict__ tile_sums) {
+    __shared__ uint64_t sh[4];
+    const int64_t i0 = (int64_t)blockIdx.x * kSpTile + threadIdx.x * 8;
+    uint8_t l[8];
+    uint64_t sum = 0;
+    for (int j = 0; j < 8; j++) {
+        l[j] = i0 + j < n ? dlen[i0 + j] : 0;
+        sum += l[j];
+    }
+    uint64_t v[1] = {sum}, tot[1];
+    block_excl_scan<1>(v, tot, sh);
+    int64_t off = (int64_t)(tile_base[blockIdx.x] + v[0]);
+    uint64_t dsum = 0;
+    for (int j = 0; j < 8; j++) {
+        if (i0 + j >= n) break;
+        const uint32_t d = get_bits(dw, ndw, off, l[j]);
+        delta[i0 + j] = d;
+        dsum += d;
+        off += l[j];
+    }
+    uint64_t v2[1] = {dsum}, tot2[1];
+    block_excl_scan<1>(v2, tot2, sh);
+    if (threadIdx.x == 0) tile_sums[blockIdx.x] = tot2[0];
+}
+
+hipError_t launch_dec_deltas(hipStream_t st, const uint64_t* delta_words, int64_t n_delta_words,
+                             const uint8_t* dlen, int64_t n, const SpGroups* gp,
+                             const uint64_t* tile_base, uint32_t* delta, uint64_t* tile_sums) {
+    (void)gp;
+    const int64_t tiles = sp_tiles(n, kSpTile);
+    if (tiles <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_dec_deltas, dim3((unsigned)tiles), dim3(kSpThreads), 0, st, delta_words, n_delta_words,
+                       dlen, n, tile_base, delta, tile_sums);
+    return hipGetLastError();
+}
+
+// Exclusive delta prefix at each group's first element: tile base + the in-tile partial sum.
+__global__ __launch_bounds__(kSpThreads) void k_group_prefix(const uint32_t* __restrict__ delta, int64_t n,
+                                                             const SpGroups* __restrict__ gp,
+                                                             const uint64_t* __restrict__ tile_base,
+                                                             uint64_t* __restrict__ gpre) {
+    __shared__ uint64_t sh[4];
+    const int g = blockIdx.x;
+    const int64_t s0 = gp->gstart[g];
+    const int64_t tile = s0 / kSpTile, lo = tile * kSpTile;
+    uint64_t sum = 0;
+    for (int64_t i = lo + threadIdx.x; i < s0 && i < n; i += kSpThreads) sum += delta[i];
+    uint64_t v[1] = {sum}, tot[1];
+    block_excl_scan<1>(v, tot, sh);
+    if (threadIdx.x == 0) gpre[g] = (s0 < n ? tile_base[tile] : 0) + tot[0];
+}
+
+hipError_t launch_group_prefix(hipStream_t st, const uint32_t* delta, int64_t n, const SpGroups* gp, int G,
+                               const uint64_t* tile_base, uint64_t* gpre) {
+    hipLaunchKernelGGL(k_group_prefix, dim3(G), dim3(kSpThreads), 0, st, delta, n, gp, tile_base, gpre);
+    return hipGetLastError();
+}
+
+// keys: group-restarted prefix sums of the deltas (Java int wrap); bins: MinMaxSketch.query
+// (MinMaxSketch.java:64-73): the row value farthest from zero, the first row on ties.
+__global__ __launch_bounds__(kSpThreads) void k_dec_keys(const uint32_t* __restrict__ delta, int64_t n,
+                                                         const SpGroups* __restrict__ gp,
+                                                         const uint64_t* __restrict__ tile_base,
+                                                         const uint64_t* __restrict__ gpre,
+                                                         const int32_t* __restrict__ table,
+                                                         int32_t* __restrict__ gkeys, int32_t* __restrict__ gbins) {
+    __shared__ int64_t S[kMaxGroups + 1];
+    __shared__ uint64_t sh[4];
+    load_starts(gp, S);
+    __syncthreads();
+    const int64_t i0 = (int64_t)blockIdx.x * kSpTile + threadIdx.x * 8;
+    uint32_t d[8];
+    uint64_t sum = 0;
+    for (int j = 0; j < 8; j++) {
+        d[j] = i0 + j < n ? delta[i0 + j] : 0;
+        sum += d[j];
+    }
+    uint64_t v[1] = {sum}, tot[1];
+    block_excl_scan<1>(v, tot, sh);
+    if (i0 >= n) return;
+    uint64_t p = tile_base[blockIdx.x] + v[0];
+    const int zero = gp->zero, rows = gp->rows;
+    int g = group_of_elem(S, i0);
+    for (int j = 0; j < 8; j++) {
+        const int64_t i = i0 + j;
+        if (i >= n) break;
+        while (i >= S[g + 1]) g++;
+        p += d[j];
+        const int32_t key = (int32_t)(uint32_t)(p - gpre[g]);
+        const int32_t cols = gp->cols[g];
+        int32_t res = zero;
+        for (int r = 0; r < rows; r++) {
+            const int32_t tv = table[gp->tab_off[g] + (int64_t)r * cols + java_hash(gp->hash_ids[g][r], key, cols)];
+            if ((int32_t)((uint32_t)mm_dist(tv, zero) - (uint32_t)mm_dist(res, zero)) > 0) res = tv;
+        }
+        gkeys[i] = key;
+        gbins[i] = res;
+    }
+}
+
+hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, const SpGroups* gp,
+                           const uint64_t* tile_base, const uint64_t* gpre, const int32_t* table,
+                           int32_t* gkeys, int32_t* gbins) {
+    const int64_t tiles = sp_tiles(n, kSpTile);
+    if (tiles <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_dec_keys, dim3((unsigned)tiles), dim3(kSpThreads), 0, st, delta, n, gp, tile_base, gpre,
+                       table, gkeys, gbins);
+    return hipGetLastError();
+}
+
+// =============================================================================================
+// Merge rounds: runs r = [rs[r], rs[r+1]); pairs (2q, 2q+1) merge into the same range, ties
+// take the lower run first (Sort.merge scans heads in list order with a strict `<`).
+// Each thread produces kMergePer outputs found by a merge-path search.
+// =============================================================================================
+constexpr int kMergePer = 8;
+
+__device__ __forceinline__ int64_t merge_path(const int32_t* A, int64_t na, const int32_t* B, int64_t nb, int64_t d) {
+    int64_t lo = d > nb ? d - nb : 0, hi = d < na ? d : na;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (A[mid] <= B[d - mid - 1]) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(kSpThreads) void k_merge_round(const int32_t* __restrict__ kin,
+                                                            const int32_t* __restrict__ bin_in,
+                                                            int32_t* __restrict__ kout, int32_t* __restrict__ bout,
+                                                            const int64_t* __restrict__ rs, int nruns,
+                                                            int64_t total) {
+    const int64_t o = ((int64_t)blockIdx.x * kSpThreads + threadIdx.x) * kMergePer;
+    const int64_t stop = std::min<int64_t>(o + kMergePer, total);
+    int q = 0;
+    for (int64_t out = o; out < stop;) {
+        // the pair whose output range holds `out` (a thread's outputs may span pairs)
+        while (2 * q + 2 <= nruns && rs[2 * q + 2] <= out) q++;
+        const int64_t a0 = rs[2 * q];
+        const int64_t a1 = rs[std::min(2 * q + 1, nruns)];
+        const int64_t b1 = rs[std::min(2 * q + 2, nruns)];
+        const int32_t* A = kin + a0;
+        const int32_t* B = kin + a1;
+        const int64_t na = a1 - a0, nb = b1 - a1;
+        int64_t ia = merge_path(A, na, B, nb, out - a0), ib = (out - a0) - ia;
+        const int64_t end = std::min<int64_t>(stop, b1);
+        for (; out < end; out++) {
+            const bool takeA = ib >= nb || (ia < na && A[ia] <= B[ib]);
+            if (takeA) {
+                kout[out] = A[ia];
+                bout[out] = bin_in[a0 + ia];
+                ia++;
+            } else {
+                kout[out] = B[ib];
+                bout[out] = bin_in[a1 + ib];
+                ib++;
+            }
+        }
+    }
+}
+
+hipError_t launch_merge_round(hipStream_t st, const int32_t* kin, const int32_t* bin_in, int32_t* kout,
+                              int32_t* bout, const int64_t* run_start, int nruns, int64_t total) {
+    if (total <= 0) return hipSuccess;
+    const int64_t threads = (total + kMergePer - 1) / kMergePer;
+    hipLaunchKernelGGL(k_merge_round, dim3((unsigned)sp_tiles(threads, kSpThreads)), dim3(kSpThreads), 0, st,
+                       kin, bin_in, kout, bout, run_start, nruns, total);
+    return hipGetLastError();
+}
+
+// values[bins[i]] (SparseVectorCompressor.java:118-126) from the double quantValues LUT
+// (Quantizer.getValues, times any timesBy factors), returned as fp32.
+__global__ __launch_bounds__(kSpThreads) void k_bin_values(const int32_t* __restrict__ bins, int64_t n,
+                                                           const double* __restrict__ qv, int B,
+                                                           float* __restrict__ vals) {
+    __shared__ float lut[4096];
+    const bool lds = B <= 4096;
+    if (lds) {
+        for (int b = threadIdx.x; b < B; b += kSpThreads) lut[b] = (float)qv[b];
+        __syncthreads();
+    }
+    for (int64_t i = (int64_t)blockIdx.x * kSpThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kSpThreads) {
+        const int b = bins[i];
+        vals[i] = lds ? lut[b] : (float)qv[b];
+    }
+}
+
+hipError_t launch_bin_values(hipStream_t st, const int32_t* bins, int64_t n, const double* qvalues, int B,
+                             float* vals) {
+    if (n <= 0) return hipSuccess;
+    const int64_t grid = std::min<int64_t>(sp_tiles(n, kSpThreads * 4), 4096);
+    hipLaunchKernelGGL(k_bin_values, dim3((unsigned)grid), dim3(kSpThreads), 0, st, bins, n, qvalues, B, vals);
+    return hipGetLastError();
+}
+
+}  // namespace skml

@@ -1,0 +1,696 @@
+// skml_sparse_api.cpp -- host side of the sparse C ABI (include/skml.h, "Sparse path"):
+// SparseVectorCompressor.compressSparse / decompressSparse (sample/SparseVectorCompressor.java:
+// 52-67,118-126) over GroupedMinMaxSketch (frequency/GroupedMinMaxSketch.java:51-146) and the
+// standalone DeltaAdaptiveEncoder (binary/DeltaAdaptiveEncoder.java).  All element work runs in
+// skml_sparse.hip; the host plans launches, owns the per-group table and the tiny decisions
+// the reference makes on whole-group statistics (colNum, hash choice, interval choice).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "skml_internal.h"
+#include "skml_sparse.h"
+
+using namespace skml;
+
+namespace {
+
+int sfail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    return set_error(code, buf);
+}
+
+#define SP_HIP(expr)                                                                         \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            return sfail(SKML_E_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                         __FILE__, __LINE__);                                                \
+    } while (0)
+
+// scratch slots (device)
+enum {
+    kSlotTiles = 0,
+    kSlotGKeys,
+    kSlotGBins,
+    kSlotNeed,
+    kSlotCells,
+    kSlotSmall,  // hist + err + gpre + run offsets
+    kSlotEndPos,
+    kSlotDelta,
+    kSlotK1,
+    kSlotB1,
+    kSlotStatus,
+};
+
+// java.util.Random (JDK 8 spec): seed scramble, next(bits), nextInt(bound).
+struct JavaRandom {
+    uint64_t s;
+    explicit JavaRandom(int64_t seed) : s(((uint64_t)seed ^ 0x5DEECE66DULL) & ((1ULL << 48) - 1)) {}
+    int32_t next(int bits) {
+        s = (s * 0x5DEECE66DULL + 0xBULL) & ((1ULL << 48) - 1);
+        return (int32_t)(s >> (48 - bits));
+    }
+    int32_t next_int(int32_t bound) {
+        if ((bound & -bound) == bound) return (int32_t)(((int64_t)bound * (int64_t)next(31)) >> 31);
+        int32_t bits, val;
+        do {
+            bits = next(31);
+            val = bits % bound;
+        } while ((int32_t)((uint32_t)bits - (uint32_t)val + (uint32_t)(bound - 1)) < 0);  // int overflow test
+        return val;
+    }
+};
+
+// HashFactory.getRandomInt2IntHashes (hash/HashFactory.java:23-38) with Maths.shuffle
+// (util/Maths.java:41-49): Fisher-Yates from the end over the 8 hash ids; rows take the first.
+void pick_hashes(int64_t seed, int rows, int32_t* ids) {
+    int32_t idx[8];
+    for (int i = 0; i < 8; i++) idx[i] = i;
+    JavaRandom r(seed);
+    for (int i = 7; i > 0; i--) {
+        const int32_t j = r.next_int(i + 1);
+        std::swap(idx[i], idx[j]);
+    }
+    for (int i = 0; i < rows; i++) ids[i] = idx[i];
+}
+
+// FSketchUtils.calGroupEdges (frequency/FSketchUtils.java:9-28)
+int group_edges(int32_t zero, int32_t bins, int32_t G, int32_t* edges) {
+    if (G == 2) {
+        edges[0] = zero;
+        edges[1] = bins;
+        return SKML_OK;
+    }
+    const int32_t bpg = bins / G;
+    if (zero < bpg) edges[0] = zero;
+    else if (bpg == 0) return sfail(SKML_E_ARG, "calGroupEdges: / by zero (bin_num %d < group_num %d)", bins, G);
+    else if ((zero % bpg) < (bpg / 2)) edges[0] = bpg + zero % bpg;
+    else edges[0] = zero % bpg;
+    for (int32_t i = 1; i < G - 1; i++) edges[i] = edges[i - 1] + bpg;
+    edges[G - 1] = bins;
+    return SKML_OK;
+}
+
+int32_t log2nlz(int32_t k) { return 31 - __builtin_clz((uint32_t)k); }
+
+// DeltaAdaptiveEncoder.calOptimalIntervals (binary/DeltaAdaptiveEncoder.java:23-51), in the
+// reference's double summation order; prob[i] = count[i] / size.
+void delta_choose(const uint32_t* count, int64_t size, int32_t* m_out, int32_t* kind_out) {
+    double prob[32];
+    for (int i = 0; i < 32; i++) prob[i] = (double)count[i] / (double)size;
+    double best = 32.0;
+    int32_t bm = 1, bk = 0;
+    for (int32_t m = 2; m <= 16; m *= 2) {
+        double iprob[16] = {0};
+        const int32_t b = 32 / m;
+        double sum = 0.0;
+        for (int32_t i = 0; i < m; i++) {
+            for (int32_t j = 0; j < b; j++) iprob[i] += prob[i * b + j];
+            sum += (i + 1) * iprob[i];
+        }
+        const double t1 = sum * b + log2nlz(m);
+        if (t1 < best) {
+            best = t1;
+            bm = m;
+            bk = 0;
+        }
+        const double t2 = sum * (b + 1) + 1;
+        if (t2 < best) {
+            best = t2;
+            bm = m;
+            bk = 1;
+        }
+    }
+    *m_out = bm;
+    *kind_out = bk;
+}
+
+// MinMaxSketch.compare with Java int wrap (MinMaxSketch.java:80-86)
+int32_t mm_dist(int32_t v, int32_t zero) {
+    const int32_t d = (int32_t)((uint32_t)v - (uint32_t)zero);
+    return d < 0 ? (int32_t)(0u - (uint32_t)d) : d;
+}
+int32_t mm_cmp(int32_t a, int32_t b, int32_t zero) {
+    return (int32_t)((uint32_t)mm_dist(a, zero) - (uint32_t)mm_dist(b, zero));
+}
+
+template <class T>
+T* scratch(skml_ctx* c, int slot, size_t count) {
+    return reinterpret_cast<T*>(ctx_scratch(c, slot, sizeof(T) * (count ? count : 1)));
+}
+
+}  // namespace
+
+// =============================================================================================
+// library-owned sparse payload
+// =============================================================================================
+struct skml_sparse {
+    int device = 0;
+    int64_t nnz = 0;
+    skml_params params{};
+    void* qpayload = nullptr;  // dense payload of the values' quantizer (header, splits, codes)
+    size_t qbytes = 0;
+    skml_dense_header hdr{};
+    std::vector<double> splits;
+    std::vector<double> qvalues;  // SparseVectorCompressor.quantValues (getValues, timesBy'd)
+    SpGroups g{};               // host copy (complete after encode)
+    SpGroups* g_dev = nullptr;  // device copy
+    int32_t* tables = nullptr;  // all groups' MinMaxSketch tables, rows x cols each
+    int64_t ncells = 0;
+    uint64_t* flag_words = nullptr;  // concatenated DeltaAdaptive flag streams
+    uint64_t* delta_words = nullptr;
+    int64_t flag_bits = 0, delta_bits = 0;
+    int64_t n_flag_words = 0, n_delta_words = 0;
+};
+
+namespace {
+
+void sparse_release(skml_sparse* s) {
+    if (!s) return;
+    (void)hipSetDevice(s->device);
+    if (s->qpayload) (void)hipFree(s->qpayload);
+    if (s->g_dev) (void)hipFree(s->g_dev);
+    if (s->tables) (void)hipFree(s->tables);
+    if (s->flag_words) (void)hipFree(s->flag_words);
+    if (s->delta_words) (void)hipFree(s->delta_words);
+    delete s;
+}
+
+// The host table is edited between uploads, so each upload completes before returning.
+int upload_groups(skml_ctx* c, skml_sparse* s) {
+    SP_HIP(hipMemcpyAsync(s->g_dev, &s->g, sizeof(SpGroups), hipMemcpyHostToDevice, ctx_stream(c)));
+    SP_HIP(hipStreamSynchronize(ctx_stream(c)));
+    return SKML_OK;
+}
+
+int sync_to_host(skml_ctx* c, void* dst, const void* src, size_t bytes) {
+    if (!bytes) return SKML_OK;
+    void* pin = ctx_pinned(c, bytes);
+    if (!pin) return sfail(SKML_E_OOM, "pinned staging of %zu bytes", bytes);
+    SP_HIP(hipMemcpyAsync(pin, src, bytes, hipMemcpyDeviceToHost, ctx_stream(c)));
+    SP_HIP(hipStreamSynchronize(ctx_stream(c)));
+    std::memcpy(dst, pin, bytes);
+    return SKML_OK;
+}
+
+// Exclusive column scans of a [tiles][K] table; column totals copied to `totals` (host).
+int scan_tiles(skml_ctx* c, uint64_t* sums, int64_t tiles, int K, uint64_t* totals) {
+    SP_HIP(launch_scan_cols(ctx_stream(c), sums, tiles, K));
+    if (totals) return sync_to_host(c, totals, sums + tiles * K, sizeof(uint64_t) * (size_t)K);
+    return SKML_OK;
+}
+
+// DeltaAdaptive bit streams for the groups of s->g over grouped keys gk (n elements): interval
+// choice from the bitsNeeded histogram, lengths, scan, writer; fills s->g.fb/db and the words.
+int encode_delta_streams(skml_ctx* c, skml_sparse* s, const int32_t* gk, const uint8_t* need,
+                         const uint32_t* hist_host) {
+    hipStream_t st = ctx_stream(c);
+    SpGroups& G = s->g;
+    const int64_t n = s->nnz;
+    int32_t k1 = 0;
+    for (int g = 0; g < G.G; g++) {
+        const int64_t m = G.gstart[g + 1] - G.gstart[g];
+        G.kind1_before[g] = k1;
+        if (m == 0) {
+            G.m[g] = 1;
+            G.kind[g] = 0;
+            continue;
+        }
+        uint32_t cnt[32];
+        for (int i = 0; i < 32; i++) cnt[i] = hist_host[g * kDeltaHist + i];
+        // bitsNeeded == 32 cannot occur for positive int deltas; fold it in for safety
+        cnt[31] += hist_host[g * kDeltaHist + 32];
+        delta_choose(cnt, m, &G.m[g], &G.kind[g]);
+        if (G.kind[g]) k1 += (int32_t)m;
+    }
+    if (int e = upload_groups(c, s)) return e;
+    const int64_t tiles = sp_tiles(n, kSpTile);
+    uint64_t* ts = scratch<uint64_t>(c, kSlotTiles, (size_t)(tiles + 1) * 2);
+    if (!ts) return sfail(SKML_E_OOM, "tile sums");
+    SP_HIP(launch_delta_lens(st, need, n, s->g_dev, ts));
+    uint64_t tot[2] = {0, 0};
+    if (int e = scan_tiles(c, ts, tiles, 2, tot)) return e;
+    s->flag_bits = (int64_t)tot[0];
+    s->delta_bits = (int64_t)tot[1];
+    s->n_flag_words = (s->flag_bits + 63) / 64 + 1;
+    s->n_delta_words = (s->delta_bits + 63) / 64 + 1;
+    SP_HIP(hipMalloc(&s->flag_words, sizeof(uint64_t) * (size_t)s->n_flag_words));
+    SP_HIP(hipMalloc(&s->delta_words, sizeof(uint64_t) * (size_t)s->n_delta_words));
+    SP_HIP(hipMemsetAsync(s->flag_words, 0, sizeof(uint64_t) * (size_t)s->n_flag_words, st));
+    SP_HIP(hipMemsetAsync(s->delta_words, 0, sizeof(uint64_t) * (size_t)s->n_delta_words, st));
+    SP_HIP(launch_delta_write(st, gk, need, n, s->g_dev, ts, s->flag_words, s->delta_words));
+    // group bases: written by the kernel for non-empty groups; empty groups take the next base
+    SpGroups back;
+    if (int e = sync_to_host(c, &back, s->g_dev, sizeof(SpGroups))) return e;
+    G.fb[G.G] = s->flag_bits;
+    G.db[G.G] = s->delta_bits;
+    for (int g = G.G - 1; g >= 0; g--) {
+        const bool empty = G.gstart[g + 1] == G.gstart[g];
+        G.fb[g] = empty ? G.fb[g + 1] : back.fb[g];
+        G.db[g] = empty ? G.db[g + 1] : back.db[g];
+    }
+    return upload_groups(c, s);
+}
+
+int check_params(const skml_params* p) {
+    if (!p) return sfail(SKML_E_ARG, "params is NULL");
+    if (p->bin_num < 2 || p->bin_num > SKML_MAX_BINS)
+        return sfail(SKML_E_ARG, "bin_num %d outside [2, %d]", p->bin_num, SKML_MAX_BINS);
+    if (p->group_num < 2 || p->group_num > kMaxGroups)
+        return sfail(SKML_E_ARG, "group_num %d outside [2, %d]", p->group_num, kMaxGroups);
+    if (p->row_num < 1 || p->row_num > kMaxRows)
+        return sfail(SKML_E_ARG, "Currently only %d hash functions are available", kMaxRows);
+    if (!(p->col_ratio > 0.0)) return sfail(SKML_E_ARG, "col_ratio must be positive");
+    return SKML_OK;
+}
+
+int encode_kv(skml_ctx* c, const int32_t* keys, const float* vals, int64_t nnz, const skml_params* p,
+              skml_sparse** out) {
+    hipStream_t st = ctx_stream(c);
+    skml_sparse* s = new skml_sparse();
+    s->device = ctx_device(c);
+    s->nnz = nnz;
+    s->params = *p;
+    auto bail = [&](int code) {
+        sparse_release(s);
+        return code;
+    };
+    // ---- 1. QuantileQuantizer over the values (the dense codec) ----
+    s->qbytes = skml_dense_payload_bytes(nnz, p->bin_num);
+    if (hipMalloc(&s->qpayload, s->qbytes) != hipSuccess) return bail(sfail(SKML_E_OOM, "quantizer payload"));
+    skml_params qp = *p;
+    if (int e = skml_dense_encode_f32(c, vals, nnz, &qp, s->qpayload, s->qbytes)) return bail(e);
+    if (int e = sync_to_host(c, &s->hdr, s->qpayload, sizeof(skml_dense_header))) return bail(e);
+    if (s->hdr.status == SKML_E_NAN) return bail(sfail(SKML_E_NAN, "Encounter NaN value"));
+    s->splits.resize((size_t)std::max(s->hdr.bin_num - 1, 0));
+    if (int e = sync_to_host(c, s->splits.data(), (const uint8_t*)s->qpayload + kHeaderBytes,
+                             sizeof(double) * s->splits.size()))
+        return bail(e);
+    {  // Quantizer.getValues (base/Quantizer.java:39-47)
+        const int B = s->hdr.bin_num, ns = B - 1;
+        s->qvalues.resize((size_t)B);
+        for (int b = 0; b < B; b++) {
+            double v;
+            if (b == 0) v = 0.5 * (s->hdr.min + s->splits[0]);
+            else if (b == ns) v = 0.5 * (s->splits[ns - 1] + s->hdr.max);
+            else v = 0.5 * (s->splits[b - 1] + s->splits[b]);
+            s->qvalues[(size_t)b] = v;
+        }
+    }
+    // ---- 2. group edges, partition counts ----
+    SpGroups& G = s->g;
+    G.G = p->group_num;
+    G.rows = p->row_num;
+    G.zero = s->hdr.zero_idx;
+    G.bin_num = s->hdr.bin_num;
+    G.fill = mm_cmp(INT32_MIN, INT32_MAX, G.zero) <= 0 ? INT32_MIN : INT32_MAX;
+    if (int e = group_edges(G.zero, G.bin_num, G.G, G.edges)) return bail(e);
+    if (hipMalloc(&s->g_dev, sizeof(SpGroups)) != hipSuccess) return bail(sfail(SKML_E_OOM, "group table"));
+    if (int e = upload_groups(c, s)) return bail(e);
+    const int64_t tiles = sp_tiles(nnz, kSpTile);
+    uint64_t* tc = scratch<uint64_t>(c, kSlotTiles, (size_t)(tiles + 1) * G.G);
+    if (!tc) return bail(sfail(SKML_E_OOM, "tile counts"));
+    std::vector<uint64_t> sizes(G.G, 0);
+    if (nnz > 0) {
+        if (hipSuccess != launch_part_count(st, s->qpayload, nnz, s->g_dev, tc)) return bail(sfail(SKML_E_HIP, "part_count"));
+        if (int e = scan_tiles(c, tc, tiles, G.G, sizes.data())) return bail(e);
+    }
+    // ---- 3. per-group MinMaxSketch shape (GroupedMinMaxSketch.compOneGroup, :103-121) ----
+    G.gstart[0] = 0;
+    int64_t cells = 0;
+    for (int g = 0; g < G.G; g++) {
+        const int64_t m = (int64_t)sizes[g];
+        G.gstart[g + 1] = G.gstart[g] + m;
+        G.cols[g] = m > 0 ? (int32_t)std::ceil((double)m * p->col_ratio) : 1;
+        if (m > 0) pick_hashes(p->hash_seed + g, G.rows, G.hash_ids[g]);
+        G.tab_off[g] = cells;
+        if (m > 0) cells += (int64_t)G.rows * G.cols[g];
+    }
+    s->ncells = cells;
+    if (int e = upload_groups(c, s)) return bail(e);
+    if (nnz == 0) {
+        for (int g = 0; g <= G.G; g++) G.fb[g] = G.db[g] = 0;
+        for (int g = 0; g < G.G; g++) G.m[g] = 1;
+        if (int e = upload_groups(c, s)) return bail(e);
+        *out = s;
+        return SKML_OK;
+    }
+    int32_t* gk = scratch<int32_t>(c, kSlotGKeys, (size_t)nnz);
+    int32_t* gb = scratch<int32_t>(c, kSlotGBins, (size_t)nnz);
+    uint8_t* need = scratch<uint8_t>(c, kSlotNeed, (size_t)nnz);
+    uint64_t* cellbuf = scratch<uint64_t>(c, kSlotCells, (size_t)cells);
+    uint32_t* small = scratch<uint32_t>(c, kSlotSmall, (size_t)kMaxGroups * kDeltaHist + 64);
+    if (!gk || !gb || !need || !cellbuf || !small) return bail(sfail(SKML_E_OOM, "sparse scratch"));
+    if (hipSuccess != launch_part_scatter(st, keys, s->qpayload, nnz, s->g_dev, tc, gk, gb))
+        return bail(sfail(SKML_E_HIP, "part_scatter"));
+    // ---- 4. deltas / histogram / order check / MinMax insert ----
+    uint32_t* hist = small;
+    uint32_t* err = small + kMaxGroups * kDeltaHist;
+    if (hipMemsetAsync(small, 0, sizeof(uint32_t) * ((size_t)kMaxGroups * kDeltaHist + 64), st) != hipSuccess ||
+        hipMemsetAsync(cellbuf, 0xFF, sizeof(uint64_t) * (size_t)cells, st) != hipSuccess)
+        return bail(sfail(SKML_E_HIP, "memset"));
+    if (hipSuccess != launch_group_prep(st, gk, gb, nnz, s->g_dev, need, hist, err, cellbuf))
+        return bail(sfail(SKML_E_HIP, "group_prep"));
+    std::vector<uint32_t> hh((size_t)kMaxGroups * kDeltaHist + 1);
+    if (int e = sync_to_host(c, hh.data(), small, sizeof(uint32_t) * hh.size())) return bail(e);
+    if (hh[(size_t)kMaxGroups * kDeltaHist])
+        return bail(sfail(SKML_E_ORDER, "Log for a non-positive key delta (keys must ascend strictly)"));
+    if (hipMalloc(&s->tables, sizeof(int32_t) * (size_t)std::max<int64_t>(cells, 1)) != hipSuccess)
+        return bail(sfail(SKML_E_OOM, "tables"));
+    if (hipSuccess != launch_minmax_finalize(st, cellbuf, cells, G.fill, s->tables))
+        return bail(sfail(SKML_E_HIP, "minmax_finalize"));
+    // ---- 5. DeltaAdaptive key streams ----
+    if (int e = encode_delta_streams(c, s, gk, need, hh.data())) return bail(e);
+    if (hipStreamSynchronize(st) != hipSuccess) return bail(sfail(SKML_E_HIP, "sync"));
+    *out = s;
+    return SKML_OK;
+}
+
+// DeltaAdaptive decode of all groups + MinMax query: grouped keys/bins into gk/gb.
+int decode_groups(skml_ctx* c, const skml_sparse* s, int32_t* gk, int32_t* gb, bool query) {
+    hipStream_t st = ctx_stream(c);
+    const SpGroups& G = s->g;
+    const int64_t n = s->nnz;
+    bool any_unary = false;
+    for (int g = 0; g < G.G; g++) any_unary |= G.kind[g] && G.gstart[g + 1] > G.gstart[g];
+    int64_t* end_pos = nullptr;
+    if (any_unary) {
+        end_pos = scratch<int64_t>(c, kSlotEndPos, (size_t)n);
+        const int64_t wt = sp_tiles(s->n_flag_words, kSpTile);
+        uint64_t* ts = scratch<uint64_t>(c, kSlotTiles, (size_t)(wt + 1));
+        if (!end_pos || !ts) return sfail(SKML_E_OOM, "decode scratch");
+        SP_HIP(launch_unary_count(st, s->flag_words, s->n_flag_words, s->g_dev, ts));
+        if (int e = scan_tiles(c, ts, wt, 1, nullptr)) return e;
+        SP_HIP(launch_unary_select(st, s->flag_words, s->n_flag_words, s->g_dev, ts, end_pos));
+    }
+    const int64_t tiles = sp_tiles(n, kSpTile);
+    uint8_t* dlen = scratch<uint8_t>(c, kSlotNeed, (size_t)n);
+    uint32_t* delta = scratch<uint32_t>(c, kSlotDelta, (size_t)n);
+    uint64_t* ts = scratch<uint64_t>(c, kSlotTiles, (size_t)(tiles + 1) * 2);
+    uint64_t* gpre = scratch<uint64_t>(c, kSlotSmall, kMaxGroups + 8);
+    if (!dlen || !delta || !ts || !gpre) return sfail(SKML_E_OOM, "decode scratch");
+    uint64_t* ts2 = ts + (tiles + 1);
+    SP_HIP(launch_dec_lens(st, s->flag_words, s->n_flag_words, end_pos, n, s->g_dev, dlen, ts));
+    if (int e = scan_tiles(c, ts, tiles, 1, nullptr)) return e;
+    SP_HIP(launch_dec_deltas(st, s->delta_words, s->n_delta_words, dlen, n, s->g_dev, ts, delta, ts2));
+    if (int e = scan_tiles(c, ts2, tiles, 1, nullptr)) return e;
+    SP_HIP(launch_group_prefix(st, delta, n, s->g_dev, G.G, ts2, gpre));
+    SP_HIP(launch_dec_keys(st, delta, n, s->g_dev, ts2, gpre, query ? s->tables : nullptr, gk, gb));
+    return SKML_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int skml_sparse_compact_f32(skml_ctx* c, const float* dense, int64_t dim, int32_t* keys, float* vals,
+                            int64_t* nnz_out) {
+    if (!c || !nnz_out || dim < 0 || (dim > 0 && (!dense || !keys || !vals)))
+        return sfail(SKML_E_ARG, "bad compaction arguments");
+    if (dim > (int64_t)INT32_MAX) return sfail(SKML_E_ARG, "dim %lld exceeds Java int keys", (long long)dim);
+    SP_HIP(hipSetDevice(ctx_device(c)));
+    hipStream_t st = ctx_stream(c);
+    const int64_t tiles = sp_tiles(dim, kCompactTile);
+    uint64_t* status = scratch<uint64_t>(c, kSlotStatus, (size_t)tiles + 8);
+    if (!status) return sfail(SKML_E_OOM, "compaction status");
+    unsigned* ticket = reinterpret_cast<unsigned*>(status + tiles);
+    int64_t* nnz_dev = reinterpret_cast<int64_t*>(status + tiles + 1);
+    SP_HIP(hipMemsetAsync(status, 0, sizeof(uint64_t) * ((size_t)tiles + 8), st));
+    SP_HIP(launch_compact(st, dense, dim, keys, vals, status, ticket, nnz_dev));
+    return sync_to_host(c, nnz_out, nnz_dev, sizeof(int64_t));
+}
+
+int skml_sparse_encode_kv_f32(skml_ctx* c, const int32_t* keys, const float* vals, int64_t nnz,
+                              const skml_params* p, skml_sparse** out) {
+    if (!c || !out || nnz < 0 || (nnz > 0 && (!keys || !vals))) return sfail(SKML_E_ARG, "bad sparse arguments");
+    if (nnz > (int64_t)INT32_MAX) return sfail(SKML_E_ARG, "nnz exceeds Java int");
+    if (int e = check_params(p)) return e;
+    SP_HIP(hipSetDevice(ctx_device(c)));
+    *out = nullptr;
+    return encode_kv(c, keys, vals, nnz, p, out);
+}
+
+int skml_sparse_encode_f32(skml_ctx* c, const float* dense, int64_t dim, const skml_params* p,
+                           skml_sparse** out) {
+    if (!c || !out || dim < 0) return sfail(SKML_E_ARG, "bad sparse arguments");
+    if (int e = check_params(p)) return e;
+    SP_HIP(hipSetDevice(ctx_device(c)));
+    int32_t* keys = nullptr;
+    float* vals = nullptr;
+    const size_t cap = (size_t)std::max<int64_t>(dim, 1);
+    SP_HIP(hipMalloc(&keys, sizeof(int32_t) * cap));
+    if (hipMalloc(&vals, sizeof(float) * cap) != hipSuccess) {
+        (void)hipFree(keys);
+        return sfail(SKML_E_OOM, "compaction output");
+    }
+    int64_t nnz = 0;
+    int e = skml_sparse_compact_f32(c, dense, dim, keys, vals, &nnz);
+    if (!e) e = encode_kv(c, keys, vals, nnz, p, out);
+    (void)hipStreamSynchronize(ctx_stream(c));
+    (void)hipFree(keys);
+    (void)hipFree(vals);
+    return e;
+}
+
+int skml_sparse_decode_f32(skml_ctx* c, const skml_sparse* s, int32_t* keys_dev, float* vals_dev) {
+    if (!c || !s) return sfail(SKML_E_ARG, "bad decode arguments");
+    const int64_t n = s->nnz;
+    if (n == 0) return SKML_OK;
+    if (!keys_dev || !vals_dev) return sfail(SKML_E_ARG, "keys/vals are NULL");
+    SP_HIP(hipSetDevice(ctx_device(c)));
+    hipStream_t st = ctx_stream(c);
+    int32_t* gk = scratch<int32_t>(c, kSlotGKeys, (size_t)n);
+    int32_t* gb = scratch<int32_t>(c, kSlotGBins, (size_t)n);
+    int32_t* k1 = scratch<int32_t>(c, kSlotK1, (size_t)n);
+    int32_t* b1 = scratch<int32_t>(c, kSlotB1, (size_t)n);
+    if (!gk || !gb || !k1 || !b1) return sfail(SKML_E_OOM, "decode scratch");
+    if (int e = decode_groups(c, s, gk, gb, true)) return e;
+    // Sort.merge over the groups: rounds of pairwise stable merges
+    const SpGroups& G = s->g;
+    std::vector<int64_t> rs(G.gstart, G.gstart + G.G + 1);
+    int64_t* rs_dev = reinterpret_cast<int64_t*>(ctx_scratch(c, kSlotStatus, sizeof(int64_t) * 2 * (kMaxGroups + 1)));
+    if (!rs_dev) return sfail(SKML_E_OOM, "run offsets");
+    int32_t *kin = gk, *bin = gb, *kout = k1, *bout = b1;
+    int slot = 0;
+    while (rs.size() > 2) {
+        int64_t* rd = rs_dev + (slot & 1) * (kMaxGroups + 1);
+        SP_HIP(hipMemcpyAsync(rd, rs.data(), sizeof(int64_t) * rs.size(), hipMemcpyHostToDevice, st));
+        SP_HIP(launch_merge_round(st, kin, bin, kout, bout, rd, (int)rs.size() - 1, n));
+        std::vector<int64_t> nx;
+        for (size_t i = 0; i < rs.size(); i += 2) nx.push_back(rs[i]);
+        if (nx.back() != rs.back()) nx.push_back(rs.back());
+        rs.swap(nx);
+        std::swap(kin, kout);
+        std::swap(bin, bout);
+        // the H2D of the next round's offsets must not overwrite the buffer still in use
+        slot++;
+        SP_HIP(hipStreamSynchronize(st));
+    }
+    SP_HIP(hipMemcpyAsync(keys_dev, kin, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToDevice, st));
+    double* qv = reinterpret_cast<double*>(ctx_scratch(c, kSlotCells, sizeof(double) * s->qvalues.size()));
+    if (!qv) return sfail(SKML_E_OOM, "value table");
+    SP_HIP(hipMemcpyAsync(qv, s->qvalues.data(), sizeof(double) * s->qvalues.size(), hipMemcpyHostToDevice, st));
+    SP_HIP(launch_bin_values(st, bin, n, qv, (int)s->qvalues.size(), vals_dev));
+    SP_HIP(hipStreamSynchronize(st));
+    return SKML_OK;
+}
+
+int skml_sparse_times_by(skml_sparse* s, double x) {
+    if (!s) return sfail(SKML_E_ARG, "NULL argument");
+    for (double& v : s->qvalues) v *= x;  // SparseVectorCompressor.timesBy (:128-134)
+    return SKML_OK;
+}
+
+int skml_sparse_values(const skml_sparse* s, double* out, int32_t cap) {
+    if (!s || !out) return sfail(SKML_E_ARG, "NULL argument");
+    const size_t k = std::min<size_t>(s->qvalues.size(), (size_t)std::max(cap, 0));
+    std::memcpy(out, s->qvalues.data(), sizeof(double) * k);
+    return SKML_OK;
+}
+
+int skml_sparse_nnz(const skml_sparse* s, int64_t* nnz) {
+    if (!s || !nnz) return sfail(SKML_E_ARG, "NULL argument");
+    *nnz = s->nnz;
+    return SKML_OK;
+}
+
+int skml_sparse_quant_info(const skml_sparse* s, skml_dense_header* hdr, double* splits_host, int32_t cap) {
+    if (!s || !hdr) return sfail(SKML_E_ARG, "NULL argument");
+    *hdr = s->hdr;
+    if (splits_host) {
+        const size_t k = std::min<size_t>(s->splits.size(), (size_t)std::max(cap, 0));
+        std::memcpy(splits_host, s->splits.data(), sizeof(double) * k);
+    }
+    return SKML_OK;
+}
+
+// Copy bits [b0, b0 + nbits) of a device word stream into host words starting at bit 0.
+static int extract_bits(skml_ctx* c, const uint64_t* words, int64_t b0, int64_t nbits, uint64_t* out) {
+    const int64_t nw = (nbits + 63) / 64;
+    if (nw == 0) return SKML_OK;
+    const int64_t w0 = b0 >> 6, w1 = (b0 + nbits - 1) >> 6;
+    std::vector<uint64_t> buf((size_t)(w1 - w0 + 2), 0);
+    if (int e = sync_to_host(c, buf.data(), words + w0, sizeof(uint64_t) * (size_t)(w1 - w0 + 1))) return e;
+    const int sh = (int)(b0 & 63);
+    for (int64_t i = 0; i < nw; i++) {
+        uint64_t v = buf[(size_t)i] >> sh;
+        if (sh) v |= buf[(size_t)i + 1] << (64 - sh);
+        out[i] = v;
+    }
+    const int tail = (int)(nbits & 63);
+    if (tail) out[nw - 1] &= (1ULL << tail) - 1ULL;
+    return SKML_OK;
+}
+
+int skml_sparse_group_info(skml_ctx* c, const skml_sparse* s, int32_t g, skml_sparse_group* info,
+                           int32_t* table_host, uint64_t* flag_words_host, uint64_t* delta_words_host) {
+    if (!c || !s || !info || g < 0 || g >= s->g.G) return sfail(SKML_E_ARG, "bad group query");
+    SP_HIP(hipSetDevice(ctx_device(c)));
+    const SpGroups& G = s->g;
+    std::memset(info, 0, sizeof(*info));
+    info->size = (int32_t)(G.gstart[g + 1] - G.gstart[g]);
+    if (info->size == 0) return SKML_OK;  // null sketch / encoder (GroupedMinMaxSketch.java:105-109)
+    info->col_num = G.cols[g];
+    for (int r = 0; r < G.rows; r++) info->hash_ids[r] = G.hash_ids[g][r];
+    info->num_intervals = G.m[g];
+    info->flag_kind = G.kind[g];
+    info->n_flag_bits = G.fb[g + 1] - G.fb[g];
+    info->n_delta_bits = G.db[g + 1] - G.db[g];
+    if (table_host)
+        if (int e = sync_to_host(c, table_host, s->tables + G.tab_off[g], sizeof(int32_t) * (size_t)G.rows * G.cols[g]))
+            return e;
+    if (flag_words_host)
+        if (int e = extract_bits(c, s->flag_words, G.fb[g], info->n_flag_bits, flag_words_host)) return e;
+    if (delta_words_host)
+        if (int e = extract_bits(c, s->delta_words, G.db[g], info->n_delta_bits, delta_words_host)) return e;
+    return SKML_OK;
+}
+
+int skml_sparse_serialize(skml_ctx*, const skml_sparse*, uint8_t*, size_t, size_t*) {
+    return sfail(SKML_E_STATE, "sparse serialisation is not built yet");
+}
+
+int skml_sparse_free(skml_sparse* s) {
+    sparse_release(s);
+    return SKML_OK;
+}
+
+// ---- standalone DeltaAdaptiveEncoder: one group, no MinMax ----
+int skml_delta_encode(skml_ctx* c, const int32_t* keys, int64_t n, int32_t* num_intervals, int32_t* flag_kind,
+                      int64_t* n_flag_bits, int64_t* n_delta_bits, uint64_t* flag_words_dev,
+                      uint64_t* delta_words_dev, int64_t words_cap) {
+    if (!c || !keys || n <= 0 || !num_intervals || !flag_kind || !n_flag_bits || !n_delta_bits)
+        return sfail(SKML_E_ARG, "bad delta arguments");
+    if (n > (int64_t)INT32_MAX) return sfail(SKML_E_ARG, "n exceeds Java int");
+    SP_HIP(hipSetDevice(ctx_device(c)));
+    hipStream_t st = ctx_stream(c);
+    skml_sparse tmp;
+    tmp.device = ctx_device(c);
+    tmp.nnz = n;
+    SpGroups& G = tmp.g;
+    G.G = 1;
+    G.rows = 0;
+    G.gstart[0] = 0;
+    G.gstart[1] = n;
+    G.cols[0] = 1;
+    int rc = SKML_OK;
+    uint8_t* need = scratch<uint8_t>(c, kSlotNeed, (size_t)n);
+    uint32_t* small = scratch<uint32_t>(c, kSlotSmall, (size_t)kMaxGroups * kDeltaHist + 64);
+    if (!need || !small) return sfail(SKML_E_OOM, "delta scratch");
+    if (hipMalloc(&tmp.g_dev, sizeof(SpGroups)) != hipSuccess) return sfail(SKML_E_OOM, "group table");
+    std::vector<uint32_t> hh((size_t)kMaxGroups * kDeltaHist + 1);
+    do {
+        if ((rc = upload_groups(c, &tmp))) break;
+        if (hipMemsetAsync(small, 0, sizeof(uint32_t) * hh.size(), st) != hipSuccess) {
+            rc = sfail(SKML_E_HIP, "memset");
+            break;
+        }
+        if (launch_group_prep(st, keys, keys, n, tmp.g_dev, need, small, small + kMaxGroups * kDeltaHist,
+                              nullptr) != hipSuccess) {
+            rc = sfail(SKML_E_HIP, "group_prep");
+            break;
+        }
+        if ((rc = sync_to_host(c, hh.data(), small, sizeof(uint32_t) * hh.size()))) break;
+        if (hh[(size_t)kMaxGroups * kDeltaHist]) {
+            rc = sfail(SKML_E_ORDER, "Log for a non-positive key delta (keys must ascend strictly)");
+            break;
+        }
+        if ((rc = encode_delta_streams(c, &tmp, keys, need, hh.data()))) break;
+        *num_intervals = G.m[0];
+        *flag_kind = G.kind[0];
+        *n_flag_bits = tmp.flag_bits;
+        *n_delta_bits = tmp.delta_bits;
+        const int64_t fw = (tmp.flag_bits + 63) / 64, dw = (tmp.delta_bits + 63) / 64;
+        if (flag_words_dev || delta_words_dev) {
+            if (fw > words_cap || dw > words_cap) {
+                rc = sfail(SKML_E_ARG, "words_cap %lld < needed %lld", (long long)words_cap, (long long)std::max(fw, dw));
+                break;
+            }
+            if (flag_words_dev && fw &&
+                hipMemcpyAsync(flag_words_dev, tmp.flag_words, sizeof(uint64_t) * fw, hipMemcpyDeviceToDevice, st) != hipSuccess)
+                rc = sfail(SKML_E_HIP, "copy flags");
+            if (!rc && delta_words_dev && dw &&
+                hipMemcpyAsync(delta_words_dev, tmp.delta_words, sizeof(uint64_t) * dw, hipMemcpyDeviceToDevice, st) != hipSuccess)
+                rc = sfail(SKML_E_HIP, "copy deltas");
+        }
+        if (!rc && hipStreamSynchronize(st) != hipSuccess) rc = sfail(SKML_E_HIP, "sync");
+    } while (0);
+    (void)hipStreamSynchronize(st);
+    (void)hipFree(tmp.g_dev);
+    if (tmp.flag_words) (void)hipFree(tmp.flag_words);
+    if (tmp.delta_words) (void)hipFree(tmp.delta_words);
+    tmp.g_dev = nullptr;
+    tmp.flag_words = tmp.delta_words = nullptr;
+    return rc;
+}
+
+int skml_delta_decode(skml_ctx* c, int64_t n, int32_t num_intervals, int32_t flag_kind, const uint64_t* flag_words,
+                      int64_t n_flag_words, const uint64_t* delta_words, int64_t n_delta_words, int32_t* keys_dev) {
+    if (!c || n <= 0 || !keys_dev || !(num_intervals == 1 || num_intervals == 2 || num_intervals == 4 ||
+                                       num_intervals == 8 || num_intervals == 16))
+        return sfail(SKML_E_ARG, "bad delta decode arguments");
+    SP_HIP(hipSetDevice(ctx_device(c)));
+    hipStream_t st = ctx_stream(c);
+    skml_sparse tmp;
+    tmp.device = ctx_device(c);
+    tmp.nnz = n;
+    SpGroups& G = tmp.g;
+    G.G = 1;
+    G.gstart[0] = 0;
+    G.gstart[1] = n;
+    G.m[0] = num_intervals;
+    G.kind[0] = flag_kind ? 1 : 0;
+    G.fb[0] = 0;
+    G.fb[1] = n_flag_words * 64;  // trailing zero words were trimmed by toLongArray
+    G.db[0] = 0;
+    G.db[1] = n_delta_words * 64;
+    // toLongArray may trim to zero words; keep readable (zero) words behind the caller's streams
+    const int64_t nfw = std::max<int64_t>(n_flag_words, 0), ndw = std::max<int64_t>(n_delta_words, 0);
+    tmp.flag_words = const_cast<uint64_t*>(flag_words);
+    tmp.delta_words = const_cast<uint64_t*>(delta_words);
+    tmp.n_flag_words = nfw;
+    tmp.n_delta_words = ndw;
+    int32_t* gb = scratch<int32_t>(c, kSlotGBins, (size_t)n);
+    if (!gb) return sfail(SKML_E_OOM, "delta scratch");
+    if (hipMalloc(&tmp.g_dev, sizeof(SpGroups)) != hipSuccess) return sfail(SKML_E_OOM, "group table");
+    int rc = upload_groups(c, &tmp);
+    if (!rc) rc = decode_groups(c, &tmp, keys_dev, gb, false);
+    (void)hipStreamSynchronize(st);
+    (void)hipFree(tmp.g_dev);
+    tmp.g_dev = nullptr;
+    tmp.flag_words = tmp.delta_words = nullptr;  // caller-owned
+    return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,301 @@
+"""Sparse codec over the HIP kernels: SparseVectorCompressor, GroupedMinMaxSketch and
+DeltaAdaptiveEncoder, mirroring sample/SparseVectorCompressor.java:22-148,
+sketch/frequency/GroupedMinMaxSketch.java:19-172 and binary/DeltaAdaptiveEncoder.java:17-188.
+
+The encoded state is a library-owned skml_sparse object in device memory (quantizer payload,
+MinMaxSketch tables, DeltaAdaptive bit streams); the views below copy group data to the host
+only when asked (parity checks, serialisation).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _lib
+from .context import get_context
+from .exceptions import SketchMLException, check
+from .quantization import Quantizer, QuantizationType
+
+
+def _params(bin_num, group_num, row_num, col_ratio, seed, hash_seed, dedup=True):
+    p = _lib.Params()
+    _lib.lib.skml_params_default(C.byref(p))
+    p.bin_num = int(bin_num)
+    p.group_num = int(group_num)
+    p.row_num = int(row_num)
+    p.col_ratio = float(col_ratio)
+    p.seed = int(seed)
+    p.hash_seed = int(hash_seed)
+    p.dedup = 1 if dedup else 0
+    return p
+
+
+class SparsePayload:
+    """Owner of one skml_sparse handle (GroupedMinMaxSketch + the values' quantizer)."""
+
+    def __init__(self, handle: C.c_void_p, device: int, rows: int):
+        self.handle = handle
+        self.device = device
+        self.rows = rows
+
+    def _ctx(self):
+        return get_context(self.device)
+
+    def nnz(self) -> int:
+        v = C.c_int64()
+        check(_lib.lib.skml_sparse_nnz(self.handle, C.byref(v)), "sparse_nnz")
+        return v.value
+
+    def quant_header(self):
+        hdr = _lib.DenseHeader()
+        splits = np.zeros(_lib.SKML_MAX_BINS, dtype=np.float64)
+        check(_lib.lib.skml_sparse_quant_info(self.handle, C.byref(hdr), splits.ctypes.data_as(_lib.dblp),
+                                              len(splits)), "sparse_quant_info")
+        return hdr, splits[: max(hdr.bin_num - 1, 0)].copy()
+
+    def values(self) -> np.ndarray:
+        hdr, _ = self.quant_header()
+        out = np.zeros(max(hdr.bin_num, 1), dtype=np.float64)
+        check(_lib.lib.skml_sparse_values(self.handle, out.ctypes.data_as(_lib.dblp), len(out)), "sparse_values")
+        return out[: hdr.bin_num]
+
+    def group(self, g: int) -> dict:
+        info = _lib.SparseGroup()
+        check(_lib.lib.skml_sparse_group_info(self._ctx().handle, self.handle, g, C.byref(info), None, None, None),
+              "group_info")
+        res = dict(size=info.size)
+        if info.size == 0:
+            return res
+        table = np.zeros(max(info.col_num * self.rows, 1), dtype=np.int32)
+        fw = np.zeros((info.n_flag_bits + 63) // 64 + 1, dtype=np.uint64)
+        dw = np.zeros((info.n_delta_bits + 63) // 64 + 1, dtype=np.uint64)
+        check(_lib.lib.skml_sparse_group_info(
+            self._ctx().handle, self.handle, g, C.byref(info), table.ctypes.data_as(_lib.i32p),
+            fw.ctypes.data_as(C.POINTER(C.c_uint64)), dw.ctypes.data_as(C.POINTER(C.c_uint64))), "group_info")
+
+        def trim(w):  # BitSet.toLongArray: up to the last non-zero word
+            nz = np.nonzero(w)[0]
+            return w[: nz[-1] + 1] if len(nz) else w[:0]
+
+        res.update(col_num=info.col_num, hash_ids=list(info.hash_ids)[: self.rows], num_intervals=info.num_intervals,
+                   flag_kind=bool(info.flag_kind), n_flag_bits=info.n_flag_bits, n_delta_bits=info.n_delta_bits,
+                   table=table, flag_words=trim(fw), delta_words=trim(dw))
+        return res
+
+    def restore(self):
+        """GroupedMinMaxSketch.restore + SparseVectorCompressor.decompressSparse: device keys
+        (int32) and values (fp32 of the double quantValues)."""
+        n = self.nnz()
+        dev = torch.device("cuda", self.device)
+        keys = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        vals = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
+        check(_lib.lib.skml_sparse_decode_f32(self._ctx().handle, self.handle, C.c_void_p(keys.data_ptr()),
+                                              C.c_void_p(vals.data_ptr())), "sparse_decode")
+        return keys[:n], vals[:n]
+
+    def times_by(self, x: float) -> None:
+        check(_lib.lib.skml_sparse_times_by(self.handle, float(x)), "sparse_times_by")
+
+    def __del__(self):
+        try:
+            if self.handle:
+                _lib.lib.skml_sparse_free(self.handle)
+                self.handle = None
+        except Exception:
+            pass
+
+
+def _as_device(t, dtype, device=None):
+    t = torch.as_tensor(t)
+    if device is None:
+        device = t.device if t.is_cuda else torch.device("cuda", torch.cuda.current_device())
+    return t.to(device=device, dtype=dtype).contiguous()
+
+
+def encode_sparse(keys, values, bin_num=Quantizer.DEFAULT_BIN_NUM, group_num=8, row_num=2, col_ratio=0.3,
+                  seed=0, hash_seed=0, dedup=True) -> SparsePayload:
+    v = _as_device(values, torch.float32)
+    k = _as_device(keys, torch.int32, v.device)
+    if k.numel() != v.numel():
+        raise SketchMLException(
+            f"Lengths of key array and value array do not match: {k.numel()}, {v.numel()}")
+    dev = v.device.index
+    ctx = get_context(dev)
+    p = _params(bin_num, group_num, row_num, col_ratio, seed, hash_seed, dedup)
+    h = C.c_void_p()
+    check(_lib.lib.skml_sparse_encode_kv_f32(ctx.handle, C.c_void_p(k.data_ptr()), C.c_void_p(v.data_ptr()),
+                                             k.numel(), C.byref(p), C.byref(h)), "sparse_encode")
+    return SparsePayload(h, dev, int(row_num))
+
+
+def encode_dense_as_sparse(dense, bin_num=Quantizer.DEFAULT_BIN_NUM, group_num=8, row_num=2, col_ratio=0.3,
+                           seed=0, hash_seed=0) -> SparsePayload:
+    """SketchGradient.fromSparse after DenseDoubleGradient.toSparse (|x| > 1e-8), on device."""
+    x = _as_device(dense, torch.float32)
+    dev = x.device.index
+    ctx = get_context(dev)
+    p = _params(bin_num, group_num, row_num, col_ratio, seed, hash_seed, True)
+    h = C.c_void_p()
+    check(_lib.lib.skml_sparse_encode_f32(ctx.handle, C.c_void_p(x.data_ptr()), x.numel(), C.byref(p),
+                                          C.byref(h)), "sparse_encode")
+    return SparsePayload(h, dev, int(row_num))
+
+
+def to_sparse(dense):
+    """DenseDoubleGradient.countNNZ + toSparse (ml/gradient/DenseDoubleGradient.scala:64-89)."""
+    x = _as_device(dense, torch.float32)
+    ctx = get_context(x.device.index)
+    keys = torch.empty(max(x.numel(), 1), dtype=torch.int32, device=x.device)
+    vals = torch.empty(max(x.numel(), 1), dtype=torch.float32, device=x.device)
+    nnz = C.c_int64()
+    check(_lib.lib.skml_sparse_compact_f32(ctx.handle, C.c_void_p(x.data_ptr()), x.numel(),
+                                           C.c_void_p(keys.data_ptr()), C.c_void_p(vals.data_ptr()),
+                                           C.byref(nnz)), "sparse_compact")
+    return keys[: nnz.value], vals[: nnz.value]
+
+
+class GroupedMinMaxSketch:
+    """frequency/GroupedMinMaxSketch.java:19-172.  create(keys, values) runs the quantizer and
+    the grouped sketch in one device call (the reference passes the quantizer's bins)."""
+
+    DEFAULT_MINMAXSKETCH_GROUP_NUM = 8
+    DEFAULT_MINMAXSKETCH_COL_RATIO = 0.3
+
+    def __init__(self, groupNum=DEFAULT_MINMAXSKETCH_GROUP_NUM, rowNum=2, colRatio=DEFAULT_MINMAXSKETCH_COL_RATIO,
+                 binNum=Quantizer.DEFAULT_BIN_NUM, seed=0, hashSeed=0):
+        self.groupNum = int(groupNum)
+        self.rowNum = int(rowNum)
+        self.colRatio = float(colRatio)
+        self.binNum = int(binNum)
+        self.seed = seed
+        self.hashSeed = hashSeed
+        self.zeroValue = None
+        self.payload: SparsePayload | None = None
+
+    def create(self, keys, values, dedup=True) -> None:
+        self.payload = encode_sparse(keys, values, self.binNum, self.groupNum, self.rowNum, self.colRatio,
+                                     self.seed, self.hashSeed, dedup)
+        hdr, _ = self.payload.quant_header()
+        self.binNum = hdr.bin_num
+        self.zeroValue = hdr.zero_idx
+
+    def restore(self):
+        return self.payload.restore()
+
+    def getGroup(self, g: int) -> dict:
+        return self.payload.group(g)
+
+
+class DeltaAdaptiveEncoder:
+    """binary/DeltaAdaptiveEncoder.java:17-188 (BinaryEncoder, base/BinaryEncoder.java:6-11)."""
+
+    def __init__(self):
+        self.size = 0
+        self.numIntervals = 0
+        self.flagKind = False
+        self.nFlagBits = 0
+        self.nDeltaBits = 0
+        self.flagWords = None   # device uint64 (BitSet.toLongArray)
+        self.deltaWords = None
+
+    def encode(self, values) -> None:
+        k = _as_device(values, torch.int32)
+        n = k.numel()
+        ctx = get_context(k.device.index)
+        cap = n + 2  # >= the longer of the two streams in 64-bit words (<= 49 bits per key)
+        fw = torch.zeros(cap, dtype=torch.int64, device=k.device)
+        dw = torch.zeros(cap, dtype=torch.int64, device=k.device)
+        m, kind = C.c_int32(), C.c_int32()
+        nf, nd = C.c_int64(), C.c_int64()
+        check(_lib.lib.skml_delta_encode(ctx.handle, C.c_void_p(k.data_ptr()), n, C.byref(m), C.byref(kind),
+                                         C.byref(nf), C.byref(nd), C.c_void_p(fw.data_ptr()),
+                                         C.c_void_p(dw.data_ptr()), cap), "delta_encode")
+        self.size = n
+        self.numIntervals = m.value
+        self.flagKind = bool(kind.value)
+        self.nFlagBits = nf.value
+        self.nDeltaBits = nd.value
+
+        def trim(w, bits):
+            w = w[: (bits + 63) // 64]
+            nz = torch.nonzero(w).flatten()
+            return w[: int(nz[-1].item()) + 1] if nz.numel() else w[:0]
+
+        self.flagWords = trim(fw, nf.value)
+        self.deltaWords = trim(dw, nd.value)
+
+    def decode(self) -> torch.Tensor:
+        dev = self.flagWords.device if self.flagWords is not None else torch.device("cuda")
+        out = torch.empty(max(self.size, 1), dtype=torch.int32, device=dev)
+        ctx = get_context(dev.index)
+        fw = self.flagWords if self.flagWords.numel() else torch.zeros(1, dtype=torch.int64, device=dev)
+        dw = self.deltaWords if self.deltaWords.numel() else torch.zeros(1, dtype=torch.int64, device=dev)
+        check(_lib.lib.skml_delta_decode(ctx.handle, self.size, self.numIntervals, int(self.flagKind),
+                                         C.c_void_p(fw.data_ptr()), self.flagWords.numel(),
+                                         C.c_void_p(dw.data_ptr()), self.deltaWords.numel(),
+                                         C.c_void_p(out.data_ptr())), "delta_decode")
+        return out[: self.size]
+
+
+class SparseVectorCompressor:
+    """sample/SparseVectorCompressor.java:22-148."""
+
+    def __init__(self, quantType=QuantizationType.QUANTILE, quantBinNum: int = Quantizer.DEFAULT_BIN_NUM,
+                 mmSketchGroupNum: int = GroupedMinMaxSketch.DEFAULT_MINMAXSKETCH_GROUP_NUM,
+                 mmSketchRowNum: int = 2,
+                 mmSketchColRatio: float = GroupedMinMaxSketch.DEFAULT_MINMAXSKETCH_COL_RATIO,
+                 seed: int = 0, hashSeed: int = 0):
+        if str(quantType) != "QUANTILE":
+            raise SketchMLException(f"Unrecognizable quantization type: {quantType}")
+        self.quantType = quantType
+        self.quantBinNum = int(quantBinNum)
+        self.mmSketchGroupNum = int(mmSketchGroupNum)
+        self.mmSketchRowNum = int(mmSketchRowNum)
+        self.mmSketchColRatio = float(mmSketchColRatio)
+        self.seed = seed
+        self.hashSeed = hashSeed
+        self._size = 0
+        self.mmSketches: GroupedMinMaxSketch | None = None
+
+    def _compress(self, keys, values, dedup):
+        self.mmSketches = GroupedMinMaxSketch(self.mmSketchGroupNum, self.mmSketchRowNum, self.mmSketchColRatio,
+                                              self.quantBinNum, self.seed, self.hashSeed)
+        self.mmSketches.create(keys, values, dedup)
+        self._size = self.mmSketches.payload.nnz()
+
+    def compressDense(self, values) -> None:
+        v = _as_device(values, torch.float32)
+        keys = torch.arange(v.numel(), dtype=torch.int32, device=v.device)
+        self._compress(keys, v, True)
+
+    def compressSparse(self, keys, values) -> None:
+        self._compress(keys, values, True)
+
+    def parallelCompressDense(self, values) -> None:
+        v = _as_device(values, torch.float32)
+        keys = torch.arange(v.numel(), dtype=torch.int32, device=v.device)
+        self._compress(keys, v, False)
+
+    def parallelCompressSparse(self, keys, values) -> None:
+        """parallelQuantize (no Maths.unique) + parallelCreate (same groups)."""
+        self._compress(keys, values, False)
+
+    def decompressSparse(self):
+        return self.mmSketches.restore()
+
+    def decompressDense(self) -> torch.Tensor:
+        """Dense array of length maxKey + 1 (SparseVectorCompressor.java:106-114)."""
+        keys, vals = self.decompressSparse()
+        n = int(keys.max().item()) + 1 if keys.numel() else 1
+        out = torch.zeros(n, dtype=torch.float32, device=vals.device)
+        out[keys.long()] = vals
+        return out
+
+    def timesBy(self, x: float) -> None:
+        if self.mmSketches is not None and self.mmSketches.payload is not None:
+            self.mmSketches.payload.times_by(x)
+
+    def size(self) -> float:
+        return float(self._size)
