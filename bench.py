@@ -131,17 +131,11 @@ def main():
     params.bin_num = bins
     params.seed = 2 + rank
 
-    comm = None
+    exch = None
     allp = None
     if world > 1:
-        uid = (C.c_uint8 * _lib.UNIQUE_ID_BYTES)()
-        if rank == 0:
-            assert lib.skml_comm_unique_id(uid) == 0, _lib.last_error()
-        obj = [bytes(uid)]
-        dist.broadcast_object_list(obj, src=0)
-        uid = (C.c_uint8 * _lib.UNIQUE_ID_BYTES).from_buffer_copy(obj[0])
-        comm = C.c_void_p()
-        assert lib.skml_comm_init_rank(ctx, uid, world, rank, C.byref(comm)) == 0, _lib.last_error()
+        from sketchml_amd.distributed import PayloadExchange
+        exch = PayloadExchange(ctx)  # RCCL communicator; unique id broadcast over the process group
         allp = sk.alloc_aligned(nb * world, dev)
 
     def step(i):
@@ -150,11 +144,8 @@ def main():
                                        C.c_void_p(payload.data_ptr()), nb)
         if st:
             raise RuntimeError(_lib.last_error())
-        if comm is not None:
-            st = lib.skml_allgather(ctx, comm, C.c_void_p(payload.data_ptr()), nb,
-                                    C.c_void_p(allp.data_ptr()))
-            if st:
-                raise RuntimeError(_lib.last_error())
+        if exch is not None:
+            exch.allgather(payload, nb, allp)
 
     def barrier():
         if world > 1:
@@ -244,12 +235,39 @@ def main():
             tb = time.perf_counter()
             extras["h2d_d2h_inclusive_gbps"] = round(4.0 * n * reps / (tb - ta) / 1e9, 2)
 
+    # ---- N > 1: the exchange step alone, and a check of the gathered payloads ----
+    if exch is not None and not args.no_extras:
+        from sketchml_amd.distributed import decode_sum
+        reps = 10
+        barrier()
+        torch.cuda.synchronize()
+        ta = time.perf_counter()
+        for _ in range(reps):
+            exch.allgather(payload, nb, allp)
+        torch.cuda.synchronize()
+        tag = (time.perf_counter() - ta) / reps
+        t = torch.tensor([tag], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        tag = float(t.item())
+        algbw = world * nb / tag / 1e9
+        # fused decode + sum + 1/P of all gathered payloads vs the all-reduce of each rank's decode
+        summed = torch.empty(n, dtype=torch.float32, device=dev)
+        decode_sum(ctx, allp, world, nb, n, 1.0 / world, summed)
+        own = torch.empty(n, dtype=torch.float32, device=dev)
+        lib.skml_dense_decode_f32(ctx, C.c_void_p(payload.data_ptr()), C.c_void_p(own.data_ptr()), n)
+        ref = own.double()
+        dist.all_reduce(ref)
+        err = float((summed.double() - ref / world).abs().max().item())
+        extras["allgather"] = {"ms": round(tag * 1e3, 3), "bytes_per_rank": nb, "algbw_gbs": round(algbw, 1),
+                               "busbw_gbs": round(algbw * (world - 1) / world, 1),
+                               "decode_sum_max_abs_err_vs_allreduce": err}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(xs[0][: 2**22].cpu().numpy(), bins, args.cpu_seconds)
 
-    if world > 1:
-        lib.skml_comm_destroy(comm)
+    if exch is not None:
+        exch.close()
     if rank == 0:
         line = {
             "metric": "device-resident grad encode GB/s (fp32 in) + decode L2 err, 1/2/4/8 GPU",

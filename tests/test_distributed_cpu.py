@@ -1,0 +1,57 @@
+"""World-size-2 gloo tests of the multi-GPU control plane (sketchml_amd/distributed.py) on CPU:
+unique-id broadcast, payload-size agreement, bucket sharding.  The RCCL data path itself
+(skml_allgather) is exercised on the GPU box (tests/test_gpu_dense.py::test_decode_sum and
+bench.py --gpus N)."""
+import os
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from sketchml_amd import distributed as D
+        uid = D.broadcast_unique_id(lambda: bytes(range(128)))
+        lo, hi = D.shard_range(2**30, world, rank)
+        sizes = D.agree_sizes(1000 + 17 * rank)
+        q.put((rank, uid, lo, hi, sizes))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_control_plane():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    uids = {r[1] for r in res}
+    assert uids == {bytes(range(128))}                       # every rank got rank 0's id
+    assert res[0][2] == 0 and res[0][3] == res[1][2] and res[1][3] == 2**30  # contiguous shards
+    assert res[0][4] == res[1][4] == [1000, 1017]            # same size table everywhere
+
+
+@pytest.mark.parametrize("n,world", [(10, 3), (2**26, 8), (2**30, 8), (7, 8)])
+def test_shard_range_partitions(n, world):
+    from sketchml_amd.distributed import shard_range
+    spans = [shard_range(n, world, r) for r in range(world)]
+    assert spans[0][0] == 0 and spans[-1][1] == n
+    assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
