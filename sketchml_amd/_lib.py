@@ -10,7 +10,9 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libskml.so")
+# SKML_LIB selects another in-tree build of the same library (e.g. the profiling build in
+# lib_prof/); there is no non-native fallback.
+LIB_PATH = os.environ.get("SKML_LIB", os.path.join(_HERE, "lib", "libskml.so"))
 
 SKML_OK = 0
 SKML_E_ARG = 1

@@ -47,6 +47,48 @@ __device__ __forceinline__ void ce(uint32_t& a, uint32_t& b) {
     b = hi;
 }
 
+// Batcher's odd-even merge sort network for N = 2^m inputs ((m^2 - m + 4) 2^(m-2) - 1
+// comparators: 191 for 32 against bitonic's 240), built at compile time so every register
+// index is static.
+template <int N>
+struct OddEvenNet {
+    static constexpr int count() {
+        int c = 0;
+        for (int p = 1; p < N; p *= 2)
+            for (int k = p; k >= 1; k /= 2)
+                for (int j = k % p; j < N - k; j += 2 * k)
+                    for (int i = 0; i < (k < N - j - k ? k : N - j - k); i++)
+                        if ((i + j) / (2 * p) == (i + j + k) / (2 * p)) c++;
+        return c;
+    }
+    static constexpr int kCount = count();
+    struct Table {
+        unsigned char a[kCount], b[kCount];
+    };
+    static constexpr Table table() {
+        Table t{};
+        int c = 0;
+        for (int p = 1; p < N; p *= 2)
+            for (int k = p; k >= 1; k /= 2)
+                for (int j = k % p; j < N - k; j += 2 * k)
+                    for (int i = 0; i < (k < N - j - k ? k : N - j - k); i++)
+                        if ((i + j) / (2 * p) == (i + j + k) / (2 * p)) {
+                            t.a[c] = (unsigned char)(i + j);
+                            t.b[c] = (unsigned char)(i + j + k);
+                            c++;
+                        }
+        return t;
+    }
+};
+
+template <int R>
+__device__ __forceinline__ void sort_regs_oddeven(uint32_t (&v)[R]) {
+    constexpr int C = OddEvenNet<R>::kCount;
+    constexpr auto T = OddEvenNet<R>::table();
+#pragma unroll
+    for (int c = 0; c < C; c++) ce(v[T.a[c]], v[T.b[c]]);
+}
+
 // In-register bitonic sort of R keys, ascending, all comparators in "flip" form.
 template <int R>
 __device__ __forceinline__ void sort_regs(uint32_t (&v)[R]) {
@@ -158,6 +200,51 @@ __device__ __forceinline__ void compact_regs(const uint32_t (&v)[R], uint32_t (&
     for (int j = 0; j < R / 2; j++) w[j] = (v[2 * j + 1] & m) | (v[2 * j] & ~m);
 }
 
+// The last in-register stage of a bitonic merge compares positions (2j, 2j+1) and the
+// compaction that follows keeps one of them: fused into one v_med3 per pair, selecting
+// min (even position kept) or max (odd position kept).
+template <int R>
+__device__ __forceinline__ void halfclean_regs_compact(uint32_t (&v)[R], uint32_t (&w)[R / 2], bool odd) {
+#pragma unroll
+    for (int d = R >> 1; d >= 2; d >>= 1) {
+#pragma unroll
+        for (int i = 0; i < R; i++) {
+            int j = i ^ d;
+            if (j > i) ce(v[i], v[j]);
+        }
+    }
+    const uint32_t sel = odd ? 0xFFFFFFFFu : 0u;
+#pragma unroll
+    for (int j = 0; j < R / 2; j++) w[j] = umed3(v[2 * j], v[2 * j + 1], sel);
+}
+
+// merge_group + compaction
+template <int R>
+__device__ __forceinline__ void merge_group_compact(uint32_t (&v)[R], uint32_t (&w)[R / 2], int lane, bool odd) {
+    constexpr int G = 256 / R;
+    flip_lanes<R, G - 1>(v, lane);
+    halfclean_lanes_down<R, G / 4>(v, lane);
+    halfclean_regs_compact<R>(v, w, odd);
+}
+
+// sort_group256 + compaction (the last merge's final stage fused with the selection)
+template <int R, int S>
+__device__ __forceinline__ void sort_lanes_upto128(uint32_t (&v)[R], int lane) {
+    if constexpr (S <= 128) {
+        constexpr int M = S / R - 1;
+        flip_lanes<R, M>(v, lane);
+        halfclean_lanes_down<R, S / R / 4>(v, lane);
+        halfclean_regs<R>(v);
+        sort_lanes_upto128<R, S * 2>(v, lane);
+    }
+}
+template <int R>
+__device__ __forceinline__ void sort_group256_compact(uint32_t (&v)[R], uint32_t (&w)[R / 2], int lane, bool odd) {
+    sort_regs<R>(v);
+    sort_lanes_upto128<R, 2 * R>(v, lane);  // two sorted 128-runs per group
+    merge_group_compact<R>(v, w, lane, odd);  // the final 256 merge + selection
+}
+
 // ------------------------------------------------------------------------------------------
 // java.util.Random jump-ahead: state after `steps` LCG steps = A^steps * s + C_steps (mod 2^48),
 // from a 4-level byte-indexed table of (A^m, C_m) (built on the host, skml_api.cpp).
@@ -248,13 +335,19 @@ __device__ __forceinline__ void build_quant_lut(const float* sp, int nsplit, Qua
             if (sp[mid] < v0) lo = mid + 1;
             else hi = mid;
         }
+        // sp[p] and sp[q] stay in registers; LDS is read only when a pointer advances
+        const float kInf = __uint_as_float(0x7F800000u);
         int p = lo, q = lo;
+        float sp_p = p < nsplit ? sp[p] : kInf, sp_q = sp_p;
         for (int b = b0; b < b1; b++) {
             const float vmin = lut_bucket_value((uint32_t)b << (32 - kLutBits));
             const float vmax = lut_bucket_value(((uint32_t)(b + 1) << (32 - kLutBits)) - 1u);
-            while (p < nsplit && sp[p] < vmin) p++;
-            if (q < p) q = p;
-            while (q < nsplit && sp[q] <= vmax) q++;
+            while (p < nsplit && sp_p < vmin) sp_p = ++p < nsplit ? sp[p] : kInf;
+            if (q < p) {
+                q = p;
+                sp_q = sp_p;
+            }
+            while (q < nsplit && sp_q <= vmax) sp_q = ++q < nsplit ? sp[q] : kInf;
             lut->base[b] = (uint16_t)p;
             need_max = max(need_max, q - p);
         }

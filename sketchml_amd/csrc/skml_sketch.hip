@@ -24,6 +24,20 @@
 
 namespace skml {
 
+// Phase timestamps of the fused merge + summary workgroup (profiling builds only:
+// make EXTRA=-DSKML_PROF_SUMMARY); read back with skml_debug_prof.
+__device__ unsigned long long g_prof[32];
+#ifdef SKML_PROF_SUMMARY
+#define SKML_PROF(k)                                      \
+    do {                                                  \
+        if (threadIdx.x == 0) g_prof[(k)] = wall_clock64(); \
+    } while (0)
+#else
+#define SKML_PROF(k) \
+    do {             \
+    } while (0)
+#endif
+
 // =============================================================================================
 // shared memory
 // =============================================================================================
@@ -93,8 +107,7 @@ template <int R>
 __device__ __forceinline__ void wave_level(uint32_t (&v)[R], uint32_t (&w)[R / 2], int lane,
                                            uint32_t odd, bool exact, float* fb) {
     if (!exact) {
-        merge_group<R>(v, lane);
-        compact_regs<R>(v, w, odd);
+        merge_group_compact<R>(v, w, lane, odd != 0);
     } else {
         wave_exact_level<R>(v, w, lane, odd, fb);
     }
@@ -138,9 +151,8 @@ __device__ __forceinline__ void wave_pair_merge(const float* A, const float* B, 
                                : reinterpret_cast<const float4*>(B)[lane - 32];
     uint32_t v[4] = {f2key(__float_as_uint(f.x)), f2key(__float_as_uint(f.y)),
                      f2key(__float_as_uint(f.z)), f2key(__float_as_uint(f.w))};
-    merge_group<4>(v, lane);
     uint32_t o[2];
-    compact_regs<4>(v, o, odd);
+    merge_group_compact<4>(v, o, lane, odd != 0);
     reinterpret_cast<float2*>(out)[lane] = make_float2(__uint_as_float(key2f(o[0])), __uint_as_float(key2f(o[1])));
 }
 
@@ -265,9 +277,11 @@ __global__ __launch_bounds__(256, 4) void k_leaf2(const float* __restrict__ x, i
     for (int round = 0; round < nrounds; round++) {
         const int64_t c0 = c_tile + round * kChunksPerWave;
         const int64_t chunk = c0 + (lane >> 3);
-        const bool valid = chunk < chunks;
+        const bool valid = PARTIAL ? chunk < chunks : true;
         uint32_t v[32];
-        uint32_t rfl = 0;
+        // Only a zero test per element here (one v_cmp_class into a wave mask); NaN, min and max
+        // come from the sorted extremes below, the zero signs only when zeros are present.
+        uint64_t zmask = 0;
         {
             const float4* src = reinterpret_cast<const float4*>(x + (valid ? chunk : c0) * kChunk);
             float4 f[8];
@@ -275,22 +289,28 @@ __global__ __launch_bounds__(256, 4) void k_leaf2(const float* __restrict__ x, i
             for (int j = 0; j < 8; j++) f[j] = src[j * 8 + (lane & 7)];
 #pragma unroll
             for (int j = 0; j < 8; j++) {
-                const uint32_t b[4] = {__float_as_uint(f[j].x), __float_as_uint(f[j].y),
-                                       __float_as_uint(f[j].z), __float_as_uint(f[j].w)};
+                const float e4[4] = {f[j].x, f[j].y, f[j].z, f[j].w};
 #pragma unroll
                 for (int e = 0; e < 4; e++) {
-                    rfl |= is_nan_bits(b[e]) ? 1u : 0u;
-                    rfl |= (b[e] == 0x80000000u) ? 2u : 0u;
-                    rfl |= (b[e] == 0u) ? 4u : 0u;
-                    const uint32_t k = f2key(b[e]);
-                    if (valid) {
-                        mn = k < mn ? k : mn;
-                        mx = k > mx ? k : mx;
-                    }
-                    v[j * 4 + e] = k;
+                    zmask |= __ballot(__builtin_amdgcn_class(e4[e], 0x60));  // -0.0 | +0.0
+                    v[j * 4 + e] = f2key(__float_as_uint(e4[e]));
                 }
             }
-            if (!valid) rfl = 0u;
+            if (PARTIAL) zmask &= __ballot(valid);
+        }
+        uint32_t rfl = 0;
+        if (zmask) {  // wave-uniform: which zero signs (keys 0x7FFFFFFF = -0.0, 0x80000000 = +0.0)
+            uint64_t nz = 0, pz = 0;
+#pragma unroll
+            for (int r = 0; r < 32; r++) {
+                nz |= __ballot(v[r] == 0x7FFFFFFFu);
+                pz |= __ballot(v[r] == 0x80000000u);
+            }
+            if (PARTIAL) {
+                nz &= __ballot(valid);
+                pz &= __ballot(valid);
+            }
+            rfl = (nz ? 2u : 0u) | (pz ? 4u : 0u);
             fl |= rfl;
         }
         // compaction bits of this round's chunks (and their carries): draws [start, start+64)
@@ -307,16 +327,25 @@ __global__ __launch_bounds__(256, 4) void k_leaf2(const float* __restrict__ x, i
             acc ^= (uint32_t)mask;
             continue;
         }
-        neg_any = neg_any || (__ballot((rfl & 2u) != 0) != 0);
-        pos_any = pos_any || (__ballot((rfl & 4u) != 0) != 0);
+        neg_any = neg_any || (rfl & 2u);
+        pos_any = pos_any || (rfl & 4u);
         const bool exact = STAGE == 2 ? false : (neg_any && pos_any);
         auto bit = [&](int level, int64_t last_chunk) -> uint32_t {
             return (uint32_t)(mask >> (node_bit_index((uint64_t)last_chunk, level) - start)) & 1u;
         };
 
-        sort_group256<32>(v, lane);
         uint32_t w1[16];
-        compact_regs<32>(v, w1, bit(0, chunk));
+        {
+            sort_regs_oddeven<32>(v);
+            sort_lanes_upto128<32, 64>(v, lane);
+            // the chunk's two sorted 128-runs: its extremes are the chunk min / max (min at
+            // register 0 of one lane, max at register 31 of another)
+            if (valid) {
+                mn = min(mn, v[0]);
+                mx = max(mx, v[31]);
+            }
+            merge_group_compact<32>(v, w1, lane, bit(0, chunk) != 0);
+        }
         const WaveExport<PARTIAL> exp{lane, rem, round * kChunksPerWave, roots};
         exp.template at<16>(0, lane >> 3, w1);
         if constexpr (STAGE == 1) {
@@ -370,7 +399,7 @@ __global__ __launch_bounds__(256, 4) void k_leaf2(const float* __restrict__ x, i
         // a level-6 tree (bit 6 of the chunk count) is this single node
         if (((chunks >> 6) & 1) && tile == ((chunks >> 7) << 1)) store_node<2>(top, lane, roots + (size_t)6 * kK);
     }
-    // per-wave partial: min / max / flags
+    // per-wave partial: min / max / flags (NaN keys lie outside [key(-inf), key(+inf)])
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
         const uint32_t omn = (uint32_t)__shfl_xor((int)mn, off, 64);
@@ -384,7 +413,7 @@ __global__ __launch_bounds__(256, 4) void k_leaf2(const float* __restrict__ x, i
         LeafPartial p;
         p.min_key = mn;
         p.max_key = mx;
-        p.flags = fl;
+        p.flags = fl | ((mn < 0x007FFFFFu || mx > 0xFF800000u) ? 1u : 0u);
         p.pad = 0;
         part[tile] = p;
     }
@@ -672,6 +701,7 @@ __device__ void summary_block(const SummaryArgs& a, SummaryShared& S) {
     const int tail = (int)(n - chunks * kChunk);
     const float* xt = a.x + chunks * kChunk;
     const int req_bins = a.req_bins;
+    SKML_PROF(2);
 
     if (t == 0) {
         S.min_key = 0xFFFFFFFFu;
@@ -695,11 +725,20 @@ __device__ void summary_block(const SummaryArgs& a, SummaryShared& S) {
     // ---- min / max / NaN ----
     {
         uint32_t mn = 0xFFFFFFFFu, mx = 0u, fl = 0u;
-        for (int64_t i = t; i < a.nparts; i += T) {
-            const LeafPartial p = a.part[i];
-            mn = p.min_key < mn ? p.min_key : mn;
-            mx = p.max_key > mx ? p.max_key : mx;
-            fl |= p.flags;
+        // batches of 8 independent loads per thread (one memory latency per batch, not per load)
+        for (int64_t i0 = t; i0 < a.nparts; i0 += 8 * (int64_t)T) {
+            LeafPartial p[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const int64_t i = i0 + (int64_t)k * T;
+                p[k] = i < a.nparts ? a.part[i] : LeafPartial{0xFFFFFFFFu, 0u, 0u, 0u};
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                mn = p[k].min_key < mn ? p[k].min_key : mn;
+                mx = p[k].max_key > mx ? p[k].max_key : mx;
+                fl |= p[k].flags;
+            }
         }
         for (int i = t; i < tail; i += T) {
             const uint32_t b = __float_as_uint(xt[i]);
@@ -712,26 +751,32 @@ __device__ void summary_block(const SummaryArgs& a, SummaryShared& S) {
         atomicMax(&S.max_key, mx);
         if (fl) atomicOr(&S.flags, fl);
     }
+    SKML_PROF(3);
     // ---- gather runs; the tail is sorted in Arrays.sort total order by rank counting ----
     const int nruns = S.nruns;
     const int ns = S.run_off[nruns];
-    for (int r = 0; r + 1 < nruns; r++) {
-        const float* src = a.roots + (size_t)S.run_lvl[r] * kK;
-        for (int i = t; i < kK; i += T) S.smp[S.run_off[r] + i] = src[i];
+    // all level runs in one flat pass (independent loads), the raw tail staged in LDS
+    for (int idx = t; idx < (nruns - 1) * kK; idx += T) {
+        const int r = idx / kK, i = idx % kK;
+        S.smp[S.run_off[r] + i] = a.roots[(size_t)S.run_lvl[r] * kK + i];
     }
+    for (int i = t; i < tail; i += T) S.sorted[i] = xt[i];
+    __syncthreads();
     {
         const int toff = S.run_off[nruns - 1];
         for (int i = t; i < tail; i += T) {
-            const uint32_t ki = f2key(__float_as_uint(xt[i]));
+            const float xi = S.sorted[i];
+            const uint32_t ki = f2key(__float_as_uint(xi));
             int rank = 0;
             for (int j = 0; j < tail; j++) {
-                const uint32_t kj = f2key(__float_as_uint(xt[j]));
+                const uint32_t kj = f2key(__float_as_uint(S.sorted[j]));
                 rank += (kj < ki) || (kj == ki && j < i);
             }
-            S.smp[toff + rank] = xt[i];
+            S.smp[toff + rank] = xi;
         }
     }
     __syncthreads();
+    SKML_PROF(4);
 
     double vmin = 1.7976931348623157e308, vmax = 4.9e-324;  // HeapQuantileSketch.java:67-68
     if (n > 0) {
@@ -773,6 +818,7 @@ __device__ void summary_block(const SummaryArgs& a, SummaryShared& S) {
         S.w[rank] = S.run_lvl[r] < 0 ? 1 : ((int64_t)2 << S.run_lvl[r]);
     }
     __syncthreads();
+    SKML_PROF(5);
 
     // ---- exclusive prefix of weights (HeapQuantileSketch.java:137-142) ----
     {
@@ -790,6 +836,7 @@ __device__ void summary_block(const SummaryArgs& a, SummaryShared& S) {
         if (t == 0) S.w[ns] = S.total;
     }
     __syncthreads();
+    SKML_PROF(6);
 
     // ---- getQuantiles(int): split_i = samples[max idx with cut[idx] <= rank_i] ----
     const int nsplit_req = req_bins - 1;
@@ -813,6 +860,7 @@ __device__ void summary_block(const SummaryArgs& a, SummaryShared& S) {
     }
     if (!lds_raw) __threadfence();
     __syncthreads();
+    SKML_PROF(7);
 
     // ---- Maths.unique (IEEE !=, keep first) + findZeroIdx ----
     int bin_num;
@@ -827,6 +875,7 @@ __device__ void summary_block(const SummaryArgs& a, SummaryShared& S) {
             if (!a.dedup || i == 0 || raw[i] != raw[i - 1]) {
                 const double sp = raw[i];
                 splits[o] = sp;
+                if (o < kMaxSamples) S.smp[o] = (float)sp;  // LDS copy for the quantize LUT
                 if (!(sp < 0.0)) atomicMin(&S.zero, (int)o);
                 o++;
             }
@@ -834,6 +883,7 @@ __device__ void summary_block(const SummaryArgs& a, SummaryShared& S) {
         bin_num = (int)S.total + 1;
     }
     __syncthreads();
+    SKML_PROF(8);
     if (t == 0) {
         int zero;
         if (vmin > 0.0) zero = 0;
@@ -854,13 +904,12 @@ __device__ void summary_block(const SummaryArgs& a, SummaryShared& S) {
     // ---- quantize bucket LUT over the final split table ----
     const int nsplit = bin_num - 1;
     if (nsplit <= kMaxSamples && nsplit <= kLutMaxSplits && n > 0) {
-        __threadfence_block();
-        for (int i = t; i < nsplit; i += T) S.smp[i] = (float)splits[i];
-        __syncthreads();
+        SKML_PROF(9);
         build_quant_lut(S.smp, nsplit, a.lut, &S.zero);
     } else if (t == 0) {
         a.lut->cmax = -1;
     }
+    SKML_PROF(10);
 }
 
 __global__ __launch_bounds__(512) void k_summary(SummaryArgs a) {
@@ -898,6 +947,7 @@ __global__ __launch_bounds__(512) void k_merge(MergePass pass, const float* __re
     __shared__ MergeShared U;
     TileShared& sh = U.t;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    if (pass.fuse_summary && gridDim.x == 1) SKML_PROF(0);
     int j = 0;
     while (j + 1 < pass.njobs && (int)blockIdx.x >= pass.wg_prefix[j + 1]) j++;
     const MergeJob job = pass.job[j];
@@ -982,6 +1032,7 @@ __global__ __launch_bounds__(512) void k_merge(MergePass pass, const float* __re
     __syncthreads();
     if (!sh.is_last) return;
     __syncthreads();
+    SKML_PROF(1);
     summary_block(sa, U.s);
 }
 
@@ -1040,3 +1091,11 @@ hipError_t launch_set_splits(hipStream_t st, void* payload, int64_t n, const dou
 }
 
 }  // namespace skml
+
+extern "C" int skml_debug_prof(unsigned long long* out, int cap) {
+    if (!out || cap <= 0) return SKML_E_ARG;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(skml::g_prof), sizeof(unsigned long long) * (size_t)(cap < 32 ? cap : 32)) ==
+                   hipSuccess
+               ? SKML_OK
+               : SKML_E_HIP;
+}

@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Sparse-path measurement (BASELINE config 3): a 2^28-dim dense fp32 gradient with 10 % nnz,
+DenseDoubleGradient.toSparse -> SparseVectorCompressor.compressSparse -> decompressSparse.
+
+Prints one JSON line: per-phase device times (HIP events on the codec stream), dense-input
+throughput, and the algorithmic-byte roofline of SURVEY.md §8(d) (sparse encode ~ 6.2 B per
+dense element at rho = 0.1: 4 dense read + rho*(8 write kv + 4 sketch re-read + 8 partition
+re-read + ~2 payload)).
+
+usage: python tools/bench_sparse.py [--dim 268435456] [--density 0.1] [--reps 5]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+HBM = 8000.0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--dim", type=int, default=2**28)
+    ap.add_argument("--density", type=float, default=0.1)
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    import sketchml_amd as sk
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(3)
+    x = torch.randn(a.dim, device=dev, generator=g)
+    x[torch.rand(a.dim, device=dev, generator=g) >= a.density] = 0.0
+    torch.cuda.synchronize()
+
+    def timed(fn, reps):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            out = fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / reps, out
+
+    t_compact, (keys, vals) = timed(lambda: sk.to_sparse(x), a.reps)
+    nnz = keys.numel()
+    t_encode, pl = timed(lambda: sk.encode_sparse(keys, vals, 256, 8, 2, 0.3, 3, 3), a.reps)
+    t_e2e, pl2 = timed(lambda: sk.encode_dense_as_sparse(x, 256, 8, 2, 0.3, 3, 3), a.reps)
+    t_decode, (rk, rv) = timed(lambda: pl.restore(), a.reps)
+    ok = bool(torch.equal(rk, keys))
+    rho = nnz / a.dim
+    alg = (4.0 + rho * (8 + 4 + 8 + 2)) * a.dim
+    line = {
+        "metric": "sparse grad encode GB/s (fp32 dense in), C3",
+        "value": round(4.0 * a.dim / t_e2e / 1e9, 2), "unit": "GB/s",
+        "config": {"workload": f"C3: {a.dim}-dim dense fp32, {a.density:.0%} nnz (Bernoulli), 256 bins, "
+                               "8 groups, 2 rows, colRatio 0.3", "nnz": nnz},
+        "ms": {"compact": round(t_compact * 1e3, 3), "encode_kv": round(t_encode * 1e3, 3),
+               "dense_to_payload": round(t_e2e * 1e3, 3), "decode": round(t_decode * 1e3, 3)},
+        "roofline": {"bound": "hbm", "alg_bytes": alg, "achieved_gbs": round(alg / t_e2e / 1e9, 1),
+                     "peak": HBM, "frac": round(alg / t_e2e / 1e9 / HBM, 4)},
+        "compact_gbs": round((4.0 * a.dim + 8.0 * nnz) / t_compact / 1e9, 1),
+        "keys_roundtrip_exact": ok,
+        "note": "wall time of synchronising calls (encode reads group sizes and bit totals back "
+                "to the host between passes)",
+    }
+    print(json.dumps(line))
+
+
+if __name__ == "__main__":
+    main()
