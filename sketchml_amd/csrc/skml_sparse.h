@@ -85,6 +85,16 @@ hipError_t launch_merge_round(hipStream_t st, const int32_t* kin, const int32_t*
 hipError_t launch_bin_values(hipStream_t st, const int32_t* bins, int64_t n, const double* qvalues, int B,
                              float* vals);
 
+// HuffmanEncoder of the MinMaxSketch tables (serialisation): per-group histograms [G][B+1]
+// (symbol B = the fill value), code lengths per tile, and the MSB-first code stream writer
+// (gbit[g] = first bit of group g's stream).  lut[g*(B+1)+sym] = (numBits << 32) | bits.
+hipError_t launch_huff_hist(hipStream_t st, const int32_t* table, const SpGroups* gp, int G, int B,
+                            int64_t max_cells, uint32_t* hist);
+hipError_t launch_huff_lens(hipStream_t st, const int32_t* table, int64_t ncells, const SpGroups* gp, int B,
+                            const uint64_t* lut, uint64_t* tile_sums);
+hipError_t launch_huff_write(hipStream_t st, const int32_t* table, int64_t ncells, const SpGroups* gp, int B,
+                             const uint64_t* lut, const uint64_t* tile_base, uint64_t* words, int64_t* gbit);
+
 // ---- context services (skml_api.cpp) ----
 hipStream_t ctx_stream(skml_ctx* c);
 int ctx_device(skml_ctx* c);

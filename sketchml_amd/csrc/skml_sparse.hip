@@ -952,4 +952,140 @@ hipError_t launch_bin_values(hipStream_t st, const int32_t* bins, int64_t n, con
     return hipGetLastError();
 }
 
+// =============================================================================================
+// HuffmanEncoder of each MinMaxSketch table (binary/HuffmanEncoder.java:88-124, used by
+// MinMaxSketch.writeObject, MinMaxSketch.java:88-97): per-group value histograms, then the
+// MSB-first code stream of all tables (codes from the host-built tree, one LUT per group).
+// Symbol index: the value itself for bins in [0, B), B for the table's fill value.
+// =============================================================================================
+constexpr int kHuffLdsBins = 4097;
+
+__device__ __forceinline__ int huff_sym(int32_t v, int B) { return (v >= 0 && v < B) ? v : B; }
+
+__global__ __launch_bounds__(kSpThreads) void k_huff_hist(const int32_t* __restrict__ table,
+                                                          const SpGroups* __restrict__ gp, int B,
+                                                          uint32_t* __restrict__ hist) {
+    __shared__ uint32_t H[kHuffLdsBins];
+    const int g = blockIdx.y;
+    if (gp->gstart[g + 1] == gp->gstart[g]) return;  // empty group: null sketch
+    const int64_t cells = (int64_t)gp->rows * gp->cols[g], base = gp->tab_off[g];
+    const bool lds = B + 1 <= kHuffLdsBins;
+    uint32_t* gh = hist + (size_t)g * (B + 1);
+    if (lds) {
+        for (int j = threadIdx.x; j <= B; j += kSpThreads) H[j] = 0;
+        __syncthreads();
+    }
+    for (int64_t i = (int64_t)blockIdx.x * kSpThreads + threadIdx.x; i < cells; i += (int64_t)gridDim.x * kSpThreads) {
+        const int sidx = huff_sym(table[base + i], B);
+        if (lds) atomicAdd(&H[sidx], 1u);
+        else atomicAdd(&gh[sidx], 1u);
+    }
+    if (lds) {
+        __syncthreads();
+        for (int j = threadIdx.x; j <= B; j += kSpThreads)
+            if (H[j]) atomicAdd(&gh[j], H[j]);
+    }
+}
+
+hipError_t launch_huff_hist(hipStream_t st, const int32_t* table, const SpGroups* gp, int G, int B,
+                            int64_t max_cells, uint32_t* hist) {
+    const int64_t gx = std::max<int64_t>(1, std::min<int64_t>(sp_tiles(max_cells, kSpThreads * 8), 256));
+    hipLaunchKernelGGL(k_huff_hist, dim3((unsigned)gx, (unsigned)G), dim3(kSpThreads), 0, st, table, gp, B, hist);
+    return hipGetLastError();
+}
+
+// group owning table cell i: the last g with tab_off[g] <= i (empty groups share the next offset)
+__device__ __forceinline__ void load_tab_offs(const SpGroups* gp, int64_t* T) {
+    for (int j = threadIdx.x; j <= kMaxGroups; j += blockDim.x) T[j] = j < gp->G ? gp->tab_off[j] : INT64_MAX;
+}
+__device__ __forceinline__ int group_of_cell(const int64_t* T, int64_t i) {
+    int g = 0;
+#pragma unroll
+    for (int step = 32; step >= 1; step >>= 1)
+        if (T[g + step] <= i) g += step;
+    return g;
+}
+
+// lut[g * (B+1) + sym] = (numBits << 32) | bits
+__global__ __launch_bounds__(kSpThreads) void k_huff_lens(const int32_t* __restrict__ table, int64_t ncells,
+                                                          const SpGroups* __restrict__ gp, int B,
+                                                          const uint64_t* __restrict__ lut,
+                                                          uint64_t* __restrict__ tile_sums) {
+    __shared__ int64_t T[kMaxGroups + 1];
+    __shared__ uint64_t sh[4];
+    load_tab_offs(gp, T);
+    __syncthreads();
+    const int64_t i0 = (int64_t)blockIdx.x * kSpTile + threadIdx.x * 8;
+    uint64_t sum = 0;
+    for (int j = 0; j < 8; j++) {
+        const int64_t i = i0 + j;
+        if (i >= ncells) break;
+        const int g = group_of_cell(T, i);
+        sum += lut[(size_t)g * (B + 1) + huff_sym(table[i], B)] >> 32;
+    }
+    uint64_t v[1] = {sum}, tot[1];
+    block_excl_scan<1>(v, tot, sh);
+    if (threadIdx.x == 0) tile_sums[blockIdx.x] = tot[0];
+}
+
+hipError_t launch_huff_lens(hipStream_t st, const int32_t* table, int64_t ncells, const SpGroups* gp, int B,
+                            const uint64_t* lut, uint64_t* tile_sums) {
+    const int64_t tiles = sp_tiles(ncells, kSpTile);
+    if (tiles <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_huff_lens, dim3((unsigned)tiles), dim3(kSpThreads), 0, st, table, ncells, gp, B, lut,
+                       tile_sums);
+    return hipGetLastError();
+}
+
+constexpr int kHuffWin = (kSpTile * 32 + 63) / 64 + 2;
+
+__global__ __launch_bounds__(kSpThreads) void k_huff_write(const int32_t* __restrict__ table, int64_t ncells,
+                                                           const SpGroups* __restrict__ gp, int B,
+                                                           const uint64_t* __restrict__ lut,
+                                                           const uint64_t* __restrict__ tile_base,
+                                                           uint64_t* __restrict__ words, int64_t* __restrict__ gbit) {
+    __shared__ int64_t T[kMaxGroups + 1];
+    __shared__ uint64_t sh[4];
+    __shared__ uint64_t win[kHuffWin];
+    load_tab_offs(gp, T);
+    for (int j = threadIdx.x; j < kHuffWin; j += kSpThreads) win[j] = 0;
+    __syncthreads();
+    const int64_t i0 = (int64_t)blockIdx.x * kSpTile + threadIdx.x * 8;
+    uint64_t code[8];
+    uint64_t sum = 0;
+    for (int j = 0; j < 8; j++) {
+        const int64_t i = i0 + j;
+        code[j] = 0;
+        if (i >= ncells) continue;
+        const int g = group_of_cell(T, i);
+        code[j] = lut[(size_t)g * (B + 1) + huff_sym(table[i], B)];
+        sum += code[j] >> 32;
+    }
+    uint64_t v[1] = {sum}, tot[1];
+    block_excl_scan<1>(v, tot, sh);
+    const uint64_t base = tile_base[blockIdx.x];
+    const int64_t w0 = (int64_t)(base >> 6) << 6;
+    uint64_t off = base + v[0];
+    for (int j = 0; j < 8; j++) {
+        const int64_t i = i0 + j;
+        if (i >= ncells) break;
+        const int g = group_of_cell(T, i);
+        if (i == T[g]) gbit[g] = (int64_t)off;  // first cell of group g
+        const int nb = (int)(code[j] >> 32);
+        lds_put_bits(win, (int64_t)off - w0, (uint32_t)code[j], nb);
+        off += nb;
+    }
+    __syncthreads();
+    flush_window(win, (int64_t)base, tot[0], words);
+}
+
+hipError_t launch_huff_write(hipStream_t st, const int32_t* table, int64_t ncells, const SpGroups* gp, int B,
+                             const uint64_t* lut, const uint64_t* tile_base, uint64_t* words, int64_t* gbit) {
+    const int64_t tiles = sp_tiles(ncells, kSpTile);
+    if (tiles <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_huff_write, dim3((unsigned)tiles), dim3(kSpThreads), 0, st, table, ncells, gp, B, lut,
+                       tile_base, words, gbit);
+    return hipGetLastError();
+}
+
 }  // namespace skml

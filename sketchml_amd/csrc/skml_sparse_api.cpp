@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "skml_internal.h"
@@ -145,6 +146,92 @@ int32_t mm_cmp(int32_t a, int32_t b, int32_t zero) {
     return (int32_t)((uint32_t)mm_dist(a, zero) - (uint32_t)mm_dist(b, zero));
 }
 
+// HuffmanEncoder.encode's tree (binary/HuffmanEncoder.java:88-111): leaves fed in ascending
+// value order (Int2ObjectRBTreeMap) into a JDK 8 java.util.PriorityQueue ordered by occurrence
+// (binary heap, siftUp / siftDown as in the JDK), two polls per merge, the merged node offered
+// back; codes from the traversal (left 0, right 1; a lone leaf gets one bit).
+struct HuffItem {
+    int32_t value, bits, nbits;
+};
+struct HuffBuilder {
+    struct Node {
+        int32_t value;
+        int64_t occ;
+        int32_t left, right;
+        bool leaf;
+    };
+    std::vector<Node> pool;
+    std::vector<int32_t> heap;
+    bool less_than(int32_t a, int32_t b) const { return pool[(size_t)a].occ < pool[(size_t)b].occ; }
+    void sift_up(size_t k, int32_t x) {
+        while (k > 0) {
+            const size_t parent = (k - 1) >> 1;
+            const int32_t e = heap[parent];
+            if (!less_than(x, e)) break;  // comparator(x, e) >= 0
+            heap[k] = e;
+            k = parent;
+        }
+        heap[k] = x;
+    }
+    void sift_down(size_t k, int32_t x) {
+        const size_t n = heap.size(), half = n >> 1;
+        while (k < half) {
+            size_t child = 2 * k + 1;
+            int32_t c = heap[child];
+            const size_t right = child + 1;
+            if (right < n && less_than(heap[right], c)) c = heap[child = right];  // cmp(c, right) > 0
+            if (!less_than(c, x)) break;                                          // cmp(x, c) <= 0
+            heap[k] = c;
+            k = child;
+        }
+        heap[k] = x;
+    }
+    void offer(int32_t x) {
+        heap.push_back(x);
+        sift_up(heap.size() - 1, x);
+    }
+    int32_t poll() {
+        const int32_t res = heap[0];
+        const int32_t x = heap.back();
+        heap.pop_back();
+        if (!heap.empty()) sift_down(0, x);
+        return res;
+    }
+    // symbols: (value, count) in ascending signed value order, counts > 0
+    bool build(const std::vector<std::pair<int32_t, int64_t>>& syms, std::vector<HuffItem>& items) {
+        pool.clear();
+        heap.clear();
+        for (const auto& sv : syms) {
+            pool.push_back(Node{sv.first, sv.second, -1, -1, true});
+            offer((int32_t)pool.size() - 1);
+        }
+        while (heap.size() > 1) {
+            const int32_t x = poll(), y = poll();
+            pool.push_back(Node{-1, pool[(size_t)x].occ + pool[(size_t)y].occ, x, y, false});
+            offer((int32_t)pool.size() - 1);
+        }
+        items.clear();
+        if (heap.empty()) return true;
+        bool ok = true;
+        // iterative traversal (left first), collecting leaves
+        std::vector<std::tuple<int32_t, uint32_t, int>> st{{heap[0], 0u, 0}};
+        while (!st.empty()) {
+            auto [nd, bits, depth] = st.back();
+            st.pop_back();
+            const Node& n = pool[(size_t)nd];
+            if (n.leaf) {
+                items.push_back(HuffItem{n.value, (int32_t)bits, depth == 0 ? 1 : depth});
+                if (depth > 32) ok = false;
+            } else {
+                st.emplace_back(n.right, (bits << 1) | 1u, depth + 1);
+                st.emplace_back(n.left, bits << 1, depth + 1);
+            }
+        }
+        std::sort(items.begin(), items.end(), [](const HuffItem& a, const HuffItem& b) { return a.value < b.value; });
+        return ok;
+    }
+};
+
 template <class T>
 T* scratch(skml_ctx* c, int slot, size_t count) {
     return reinterpret_cast<T*>(ctx_scratch(c, slot, sizeof(T) * (count ? count : 1)));
@@ -172,6 +259,12 @@ struct skml_sparse {
     uint64_t* delta_words = nullptr;
     int64_t flag_bits = 0, delta_bits = 0;
     int64_t n_flag_words = 0, n_delta_words = 0;
+    // MinMaxSketch tables' HuffmanEncoder (built on the first serialisation)
+    bool huff_done = false;
+    std::vector<std::vector<HuffItem>> huff_items;  // per group, ascending value
+    std::vector<int64_t> huff_bit0, huff_bits;      // per group stream range
+    uint64_t* huff_words = nullptr;
+    int64_t n_huff_words = 0;
 };
 
 namespace {
@@ -184,6 +277,7 @@ void sparse_release(skml_sparse* s) {
     if (s->tables) (void)hipFree(s->tables);
     if (s->flag_words) (void)hipFree(s->flag_words);
     if (s->delta_words) (void)hipFree(s->delta_words);
+    if (s->huff_words) (void)hipFree(s->huff_words);
     delete s;
 }
 
@@ -577,8 +671,155 @@ int skml_sparse_group_info(skml_ctx* c, const skml_sparse* s, int32_t g, skml_sp
     return SKML_OK;
 }
 
-int skml_sparse_serialize(skml_ctx*, const skml_sparse*, uint8_t*, size_t, size_t*) {
-    return sfail(SKML_E_STATE, "sparse serialisation is not built yet");
+// Per-group HuffmanEncoder of the MinMaxSketch tables: device histograms, host trees, device
+// code stream (cached in the payload).
+static int build_huffman(skml_ctx* c, skml_sparse* s) {
+    if (s->huff_done) return SKML_OK;
+    hipStream_t st = ctx_stream(c);
+    const SpGroups& G = s->g;
+    const int B = G.bin_num;
+    const size_t nsym = (size_t)B + 1;
+    s->huff_items.assign((size_t)G.G, {});
+    s->huff_bit0.assign((size_t)G.G + 1, 0);
+    s->huff_bits.assign((size_t)G.G, 0);
+    if (s->ncells > 0) {
+        int64_t max_cells = 0;
+        for (int g = 0; g < G.G; g++)
+            if (G.gstart[g + 1] > G.gstart[g]) max_cells = std::max<int64_t>(max_cells, (int64_t)G.rows * G.cols[g]);
+        uint32_t* hist = scratch<uint32_t>(c, kSlotDelta, (size_t)G.G * nsym);
+        uint64_t* lut = scratch<uint64_t>(c, kSlotCells, (size_t)G.G * nsym);
+        if (!hist || !lut) return sfail(SKML_E_OOM, "huffman scratch");
+        SP_HIP(hipMemsetAsync(hist, 0, sizeof(uint32_t) * (size_t)G.G * nsym, st));
+        SP_HIP(launch_huff_hist(st, s->tables, s->g_dev, G.G, B, max_cells, hist));
+        std::vector<uint32_t> hh((size_t)G.G * nsym);
+        if (int e = sync_to_host(c, hh.data(), hist, sizeof(uint32_t) * hh.size())) return e;
+        std::vector<uint64_t> lh((size_t)G.G * nsym, 0);
+        HuffBuilder hb;
+        int64_t bit = 0;
+        for (int g = 0; g < G.G; g++) {
+            s->huff_bit0[(size_t)g] = bit;
+            if (G.gstart[g + 1] == G.gstart[g]) continue;
+            std::vector<std::pair<int32_t, int64_t>> syms;
+            const uint32_t* h = hh.data() + (size_t)g * nsym;
+            if (G.fill < 0 && h[B]) syms.emplace_back(G.fill, h[B]);  // ascending signed order
+            for (int v = 0; v < B; v++)
+                if (h[v]) syms.emplace_back(v, h[v]);
+            if (G.fill >= 0 && h[B]) syms.emplace_back(G.fill, h[B]);
+            if (!hb.build(syms, s->huff_items[(size_t)g]))
+                return sfail(SKML_E_STATE, "Huffman code longer than 32 bits (group %d)", g);
+            for (const HuffItem& it : s->huff_items[(size_t)g]) {
+                const int sym = (it.value >= 0 && it.value < B) ? it.value : B;
+                lh[(size_t)g * nsym + sym] = ((uint64_t)it.nbits << 32) | (uint32_t)it.bits;
+                s->huff_bits[(size_t)g] += (int64_t)it.nbits * h[sym];
+            }
+            bit += s->huff_bits[(size_t)g];
+        }
+        s->huff_bit0[(size_t)G.G] = bit;
+        SP_HIP(hipMemcpyAsync(lut, lh.data(), sizeof(uint64_t) * lh.size(), hipMemcpyHostToDevice, st));
+        const int64_t tiles = sp_tiles(s->ncells, kSpTile);
+        uint64_t* ts = scratch<uint64_t>(c, kSlotTiles, (size_t)tiles + 1);
+        int64_t* gbit = scratch<int64_t>(c, kSlotSmall, kMaxGroups + 1);
+        if (!ts || !gbit) return sfail(SKML_E_OOM, "huffman scratch");
+        SP_HIP(launch_huff_lens(st, s->tables, s->ncells, s->g_dev, B, lut, ts));
+        uint64_t total = 0;
+        if (int e = scan_tiles(c, ts, tiles, 1, &total)) return e;
+        if ((int64_t)total != bit) return sfail(SKML_E_STATE, "huffman bit count mismatch");
+        s->n_huff_words = (bit + 63) / 64 + 1;
+        SP_HIP(hipMalloc(&s->huff_words, sizeof(uint64_t) * (size_t)s->n_huff_words));
+        SP_HIP(hipMemsetAsync(s->huff_words, 0, sizeof(uint64_t) * (size_t)s->n_huff_words, st));
+        SP_HIP(launch_huff_write(st, s->tables, s->ncells, s->g_dev, B, lut, ts, s->huff_words, gbit));
+        SP_HIP(hipStreamSynchronize(st));
+    }
+    s->huff_done = true;
+    return SKML_OK;
+}
+
+namespace {
+struct BeWriter {
+    std::vector<uint8_t> b;
+    void u(uint64_t v, int n) {
+        for (int i = n - 1; i >= 0; i--) b.push_back((uint8_t)(v >> (8 * i)));
+    }
+    void i32(int32_t v) { u((uint32_t)v, 4); }
+    void i64(int64_t v) { u((uint64_t)v, 8); }
+    void f64(double d) {
+        uint64_t x;
+        std::memcpy(&x, &d, 8);
+        u(x, 8);
+    }
+    void byte(int v) { b.push_back((uint8_t)v); }
+};
+// BitSet.toLongArray of a device bit range (trailing zero words trimmed)
+int long_array(skml_ctx* c, const uint64_t* words, int64_t b0, int64_t nbits, std::vector<uint64_t>& out) {
+    out.assign((size_t)((nbits + 63) / 64), 0);
+    if (int e = extract_bits(c, words, b0, nbits, out.data())) return e;
+    while (!out.empty() && out.back() == 0) out.pop_back();
+    return SKML_OK;
+}
+}  // namespace
+
+// GroupedMinMaxSketch.writeObject field order (GroupedMinMaxSketch.java:148-158) with
+// MinMaxSketch.writeObject (MinMaxSketch.java:88-97), HuffmanEncoder.writeObject
+// (HuffmanEncoder.java:168-190) and DeltaAdaptiveEncoder.writeObject (:148-170); big-endian
+// DataOutput primitives; a 1-byte presence flag stands where Java writes a null object, and each
+// Int2IntHash object is (int HashFactory index, int size, int BKDR seed or 0).
+int skml_sparse_serialize(skml_ctx* c, const skml_sparse* cs, uint8_t* buf, size_t cap, size_t* written) {
+    if (!c || !cs) return sfail(SKML_E_ARG, "bad serialise arguments");
+    SP_HIP(hipSetDevice(ctx_device(c)));
+    skml_sparse* s = const_cast<skml_sparse*>(cs);  // the Huffman streams are a lazily built cache
+    if (int e = build_huffman(c, s)) return e;
+    static const int32_t kBkdrSeed[8] = {0, 0, 0, 31, 131, 267, 1313, 13131};
+    const SpGroups& G = s->g;
+    BeWriter w;
+    w.i32(G.G);
+    w.i32(G.rows);
+    w.f64(s->params.col_ratio);
+    w.i32(G.bin_num);
+    w.i32(G.zero);
+    std::vector<uint64_t> longs;
+    for (int g = 0; g < G.G; g++) {  // sketches
+        const bool present = G.gstart[g + 1] > G.gstart[g];
+        w.byte(present ? 1 : 0);
+        if (!present) continue;
+        w.i32(G.rows);
+        w.i32(G.cols[g]);
+        w.i32(G.zero);
+        for (int r = 0; r < G.rows; r++) {
+            w.i32(G.hash_ids[g][r]);
+            w.i32(G.cols[g]);
+            w.i32(kBkdrSeed[G.hash_ids[g][r] & 7]);
+        }
+        const auto& items = s->huff_items[(size_t)g];
+        w.i32((int32_t)items.size());
+        for (const HuffItem& it : items) {
+            w.i32(it.value);
+            w.i32(it.bits);
+            w.i32(it.nbits);
+        }
+        if (int e = long_array(c, s->huff_words, s->huff_bit0[(size_t)g], s->huff_bits[(size_t)g], longs)) return e;
+        w.i32((int32_t)longs.size());
+        for (uint64_t l : longs) w.i64((int64_t)l);
+        w.i32(G.rows * G.cols[g]);
+    }
+    for (int g = 0; g < G.G; g++) {  // encoders
+        const bool present = G.gstart[g + 1] > G.gstart[g];
+        w.byte(present ? 1 : 0);
+        if (!present) continue;
+        w.i32((int32_t)(G.gstart[g + 1] - G.gstart[g]));
+        w.i32(G.m[g]);
+        w.byte(G.kind[g] ? 1 : 0);
+        if (int e = long_array(c, s->flag_words, G.fb[g], G.fb[g + 1] - G.fb[g], longs)) return e;
+        w.i32((int32_t)longs.size());
+        for (uint64_t l : longs) w.i64((int64_t)l);
+        if (int e = long_array(c, s->delta_words, G.db[g], G.db[g + 1] - G.db[g], longs)) return e;
+        w.i32((int32_t)longs.size());
+        for (uint64_t l : longs) w.i64((int64_t)l);
+    }
+    if (written) *written = w.b.size();
+    if (!buf) return SKML_OK;
+    if (cap < w.b.size()) return sfail(SKML_E_ARG, "buffer capacity %zu < %zu", cap, w.b.size());
+    std::memcpy(buf, w.b.data(), w.b.size());
+    return SKML_OK;
 }
 
 int skml_sparse_free(skml_sparse* s) {

@@ -95,6 +95,15 @@ class SparsePayload:
                                               C.c_void_p(vals.data_ptr())), "sparse_decode")
         return keys[:n], vals[:n]
 
+    def serialize(self) -> bytes:
+        """GroupedMinMaxSketch.writeObject field stream (layout in DESIGN.md / skml_sparse_serialize)."""
+        need = C.c_size_t()
+        check(_lib.lib.skml_sparse_serialize(self._ctx().handle, self.handle, None, 0, C.byref(need)), "serialize")
+        buf = (C.c_uint8 * max(need.value, 1))()
+        check(_lib.lib.skml_sparse_serialize(self._ctx().handle, self.handle, buf, need.value, C.byref(need)),
+              "serialize")
+        return bytes(buf[: need.value])
+
     def times_by(self, x: float) -> None:
         check(_lib.lib.skml_sparse_times_by(self.handle, float(x)), "sparse_times_by")
 
@@ -186,6 +195,9 @@ class GroupedMinMaxSketch:
 
     def getGroup(self, g: int) -> dict:
         return self.payload.group(g)
+
+    def writeObject(self) -> bytes:
+        return self.payload.serialize()
 
 
 class DeltaAdaptiveEncoder:
@@ -299,3 +311,12 @@ class SparseVectorCompressor:
 
     def size(self) -> float:
         return float(self._size)
+
+    def memoryBytes(self) -> int:
+        """28 + 8 * binNum + the serialised GroupedMinMaxSketch (SparseVectorCompressor.java:142-147;
+        the field stream without Java object-stream framing)."""
+        res = 28
+        if self.mmSketches is not None and self.mmSketches.payload is not None:
+            res += 8 * len(self.mmSketches.payload.values())
+            res += len(self.mmSketches.writeObject())
+        return res

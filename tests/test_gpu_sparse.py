@@ -221,3 +221,66 @@ def test_c3_size_properties(gpu):
     z = hdr.zero_idx
     assert torch.all((got_bins - z).abs() <= (true_bins - z).abs())     # P6
     del x
+
+
+def _parse_sparse_stream(b):
+    """Reader of skml_sparse_serialize's field stream (GroupedMinMaxSketch.writeObject order)."""
+    import struct
+    off = 0
+
+    def take(fmt):
+        nonlocal off
+        v = struct.unpack_from(fmt, b, off)[0]
+        off += struct.calcsize(fmt)
+        return v
+
+    head = dict(G=take(">i"), rows=take(">i"), ratio=take(">d"), B=take(">i"), zero=take(">i"))
+    sketches, encoders = [], []
+    for _ in range(head["G"]):
+        if not take(">B"):
+            sketches.append(None)
+            continue
+        sk = dict(rows=take(">i"), cols=take(">i"), zero=take(">i"))
+        sk["hashes"] = [(take(">i"), take(">i"), take(">i")) for _ in range(sk["rows"])]
+        sk["items"] = [(take(">i"), take(">i"), take(">i")) for _ in range(take(">i"))]
+        sk["longs"] = np.array([take(">Q") for _ in range(take(">i"))], dtype=np.uint64)
+        sk["size"] = take(">i")
+        sketches.append(sk)
+    for _ in range(head["G"]):
+        if not take(">B"):
+            encoders.append(None)
+            continue
+        e = dict(size=take(">i"), m=take(">i"), kind=bool(take(">B")))
+        e["flags"] = np.array([take(">Q") for _ in range(take(">i"))], dtype=np.uint64)
+        e["deltas"] = np.array([take(">Q") for _ in range(take(">i"))], dtype=np.uint64)
+        encoders.append(e)
+    assert off == len(b)
+    return head, sketches, encoders
+
+
+@pytest.mark.parametrize("bins,groups,rows", [(256, 8, 2), (16, 4, 3), (1024, 2, 1)])
+def test_sparse_serialize_matches_oracle(gpu, bins, groups, rows):
+    """A14: the field stream carries each group's MinMaxSketch (hash ids, HuffmanEncoder of the
+    table: items + BitSet words + size) and DeltaAdaptiveEncoder, equal to the oracle's."""
+    keys, vals = _sparse_data(80000, 0.15, bins + groups, "normal")
+    pl, osp = _check_sparse(gpu, keys, vals, bins, groups, rows, 0.3, 2, 5)
+    head, sketches, encoders = _parse_sparse_stream(pl.serialize())
+    assert (head["G"], head["rows"], head["ratio"], head["B"], head["zero"]) == \
+        (groups, rows, 0.3, osp.q.bin_num, osp.q.zero_idx)
+    bkdr = {3: 31, 4: 131, 5: 267, 6: 1313, 7: 13131}
+    for g in range(groups):
+        if osp.tables[g] is None:
+            assert sketches[g] is None and encoders[g] is None
+            continue
+        sk = sketches[g]
+        assert (sk["rows"], sk["cols"], sk["zero"], sk["size"]) == (rows, osp.col_num[g], osp.q.zero_idx,
+                                                                   rows * osp.col_num[g])
+        assert sk["hashes"] == [(int(h), int(osp.col_num[g]), bkdr.get(int(h), 0)) for h in osp.hash_ids[g]]
+        want = O.huffman_encode(osp.tables[g])
+        assert sk["items"] == [tuple(int(v) for v in it) for it in want["items"]]
+        assert np.array_equal(sk["longs"], want["words"])
+        assert np.array_equal(want["decoded"], osp.tables[g])        # the oracle's own round trip
+        d = osp.deltas[g]
+        e = encoders[g]
+        assert (e["size"], e["m"], e["kind"]) == (d["size"], d["num_intervals"], d["flag_kind"])
+        assert np.array_equal(e["flags"], d["flag_words"]) and np.array_equal(e["deltas"], d["delta_words"])
