@@ -83,8 +83,9 @@ int skml_ctx_destroy(skml_ctx* ctx);
 int skml_ctx_sync(skml_ctx* ctx);
 int skml_ctx_set_stream(skml_ctx* ctx, void* hip_stream);
 
-/* Per-kernel timing with HIP events recorded on the context stream around every launch
- * (profiling aid for bench.py's roofline; off by default). */
+/* Per-kernel timing with HIP events recorded on the context stream around the launches of the
+ * selected kernels (profiling aid for bench.py's roofline; off by default).  `mask`: bit k
+ * times kernel id k; SKML_TIMING_ALL times every kernel; 0 turns timing off. */
 #define SKML_K_LEAF 0
 #define SKML_K_MERGE 1
 #define SKML_K_SUMMARY 2
@@ -93,7 +94,8 @@ int skml_ctx_set_stream(skml_ctx* ctx, void* hip_stream);
 #define SKML_K_DECODE_SUM 5
 #define SKML_K_SPARSE 6
 #define SKML_K_COUNT 7
-int skml_ctx_set_timing(skml_ctx* ctx, int enable);
+#define SKML_TIMING_ALL (-1)
+int skml_ctx_set_timing(skml_ctx* ctx, int mask);
 /* Synchronises; total device milliseconds and launch count of kernel `kid` since the reset. */
 int skml_ctx_kernel_stats(skml_ctx* ctx, int kid, int64_t* launches, double* total_ms);
 int skml_ctx_reset_stats(skml_ctx* ctx);

@@ -9,6 +9,10 @@ from __future__ import annotations
 import ctypes as C
 import os
 
+# torch first: its bundled HIP runtime must be the one in the process before libskml.so (which
+# links libamdhip64) is loaded, or the two runtimes disagree about the devices.
+import torch  # noqa: F401
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # SKML_LIB selects another in-tree build of the same library (e.g. the profiling build in
 # lib_prof/); there is no non-native fallback.

@@ -65,7 +65,7 @@ struct skml_ctx {
     void* pinned = nullptr;
     size_t pinned_cap = 0;
     // per-kernel event timing (skml_ctx_set_timing)
-    bool timing = false;
+    int timing = 0;  // bit k: time kernel id k
     std::vector<hipEvent_t> ev[SKML_K_COUNT];  // start/stop pairs
     size_t ev_used[SKML_K_COUNT] = {};
 };
@@ -76,7 +76,7 @@ struct KernelTimer {
     skml_ctx* c;
     int kid;
     bool on;
-    KernelTimer(skml_ctx* ctx, int k) : c(ctx), kid(k), on(ctx->timing) {
+    KernelTimer(skml_ctx* ctx, int k) : c(ctx), kid(k), on((ctx->timing >> k) & 1) {
         if (!on) return;
         auto& v = c->ev[kid];
         if (c->ev_used[kid] + 2 > v.size()) {
@@ -294,9 +294,9 @@ int skml_ctx_sync(skml_ctx* c) {
     return SKML_OK;
 }
 
-int skml_ctx_set_timing(skml_ctx* c, int enable) {
+int skml_ctx_set_timing(skml_ctx* c, int mask) {
     if (!c) return fail(SKML_E_ARG, "ctx is NULL");
-    c->timing = enable != 0;
+    c->timing = mask;
     return SKML_OK;
 }
 
@@ -694,7 +694,7 @@ namespace skml {
 hipStream_t ctx_stream(skml_ctx* c) { return c->stream; }
 int ctx_device(skml_ctx* c) { return c->device; }
 int set_error(int code, const char* msg) { return fail(code, "%s", msg); }
-bool ctx_timing(skml_ctx* c) { return c->timing; }
+bool ctx_timing(skml_ctx* c) { return c->timing != 0; }
 void* ctx_scratch(skml_ctx* c, int slot, size_t bytes) {
     if (slot < 0 || slot >= kScratchSlots) return nullptr;
     if (bytes == 0) bytes = 256;

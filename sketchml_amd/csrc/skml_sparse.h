@@ -49,12 +49,18 @@ hipError_t launch_part_count(hipStream_t st, const void* qpayload, int64_t n, co
 hipError_t launch_part_scatter(hipStream_t st, const int32_t* keys, const void* qpayload, int64_t n,
                                const SpGroups* gp, const uint64_t* tile_base, int32_t* gkeys,
                                int32_t* gbins);
-// Deltas, bitsNeeded histogram, order check and MinMaxSketch.insert (u64 cells, pre-filled ~0).
-hipError_t launch_group_prep(hipStream_t st, const int32_t* gkeys, const int32_t* gbins, int64_t n,
-                             const SpGroups* gp, uint8_t* need, uint32_t* hist, uint32_t* err,
-                             uint64_t* cells);
-hipError_t launch_minmax_finalize(hipStream_t st, const uint64_t* cells, int64_t ncells, int32_t fill,
-                                  int32_t* table);
+// Deltas, bitsNeeded histogram, order check, and the per-bucket pair counts of the bucketed
+// MinMaxSketch.insert (bucket_count: nbuckets u64, zeroed; unused when rows == 0).
+constexpr int kMmCellsPerBucket = 8192;
+hipError_t launch_group_prep(hipStream_t st, const int32_t* gkeys, int64_t n, const SpGroups* gp, uint8_t* need,
+                             uint32_t* hist, uint32_t* err, uint64_t* bucket_count, int nbuckets);
+// pairs in bucket order (bucket_base: exclusive scan of the counts; cursor: nbuckets u64, zeroed)
+hipError_t launch_mm_scatter(hipStream_t st, const int32_t* gkeys, const int32_t* gbins, int64_t n,
+                             const SpGroups* gp, const uint64_t* bucket_base, uint64_t* cursor, int nbuckets,
+                             uint64_t* pairs);
+// per-bucket minimum -> int32 MinMaxSketch tables (empty cells get the fill value)
+hipError_t launch_mm_bucket(hipStream_t st, const uint64_t* pairs, const uint64_t* bucket_base, int nbuckets,
+                            int64_t ncells, int32_t zero, int32_t fill, int32_t* table);
 // DeltaAdaptiveEncoder bit streams: tile sums of (flag bits, delta bits), then the writer.
 hipError_t launch_delta_lens(hipStream_t st, const uint8_t* need, int64_t n, const SpGroups* gp,
                              uint64_t* tile_sums);

@@ -61,11 +61,14 @@ __device__ __forceinline__ void block_excl_scan(uint64_t (&v)[K], uint64_t (&tot
     __syncthreads();
 }
 
-__device__ __forceinline__ uint64_t ld_acquire(const uint64_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+// Look-back status words carry their payload (flag | count) in the word itself, so relaxed
+// agent-scope atomics suffice: no release / acquire fences (an agent release writes back the
+// whole L2 -- per tile, that was 30x slower).
+__device__ __forceinline__ uint64_t ld_status(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void st_release(uint64_t* p, uint64_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ void st_status(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // packed code of element e (LSB-first codes, code_bits in {1,2,4,8,16})
@@ -196,28 +199,36 @@ __global__ __launch_bounds__(kSpThreads) void k_compact(const float* __restrict_
     for (int j = 0; j < 16; j++) keep |= (fabs((double)v[j]) > 1e-8) ? (1u << j) : 0u;  // Maths.scala:8 EPS
     uint64_t c[1] = {(uint64_t)__popc(keep)}, tot[1];
     block_excl_scan<1>(c, tot, sh);
-    if (t == 0) {
+    if (t < 64) {  // wave 0: publish the aggregate, then look back 64 predecessors per step
+        const int lane = t;
         uint64_t excl = 0;
         if (tile == 0) {
-            st_release(&status[0], kStPre | tot[0]);
+            if (lane == 0) st_status(&status[0], kStPre | tot[0]);
         } else {
-            st_release(&status[tile], kStAgg | tot[0]);
+            if (lane == 0) st_status(&status[tile], kStAgg | tot[0]);
             int64_t p = tile - 1;
             while (true) {
-                const uint64_t s = ld_acquire(&status[p]);
-                const uint64_t f = s & ~kStMask;
-                if (f == 0) {
+                const int64_t idx = p - lane;
+                uint64_t sv = idx >= 0 ? ld_status(&status[idx]) : kStPre;  // before tile 0: prefix 0
+                while (__ballot((sv & ~kStMask) == 0)) {
                     __builtin_amdgcn_s_sleep(1);
-                    continue;
+                    if ((sv & ~kStMask) == 0) sv = ld_status(&status[idx]);
                 }
-                excl += s & kStMask;
-                if (f == kStPre) break;
-                p--;
+                const uint64_t pre = __ballot((sv & ~kStMask) == kStPre);
+                const int stop = pre ? __ffsll((unsigned long long)pre) - 1 : 63;  // nearest prefix
+                uint64_t contrib = lane <= stop ? (sv & kStMask) : 0;
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) contrib += __shfl_xor(contrib, off, 64);
+                excl += contrib;
+                if (pre) break;
+                p -= 64;
             }
-            st_release(&status[tile], kStPre | (excl + tot[0]));
+            if (lane == 0) st_status(&status[tile], kStPre | (excl + tot[0]));
         }
-        s_excl = excl;
-        if (tile == ntiles - 1) *nnz_out = (int64_t)(excl + tot[0]);
+        if (lane == 0) {
+            s_excl = excl;
+            if (tile == ntiles - 1) *nnz_out = (int64_t)(excl + tot[0]);
+        }
     }
     __syncthreads();
     int64_t pos = (int64_t)(s_excl + c[0]);
@@ -382,21 +393,49 @@ hipError_t launch_part_scatter(hipStream_t st, const int32_t* keys, const void* 
 // =============================================================================================
 // Group prep: deltas / bitsNeeded / order check / MinMax insert
 // =============================================================================================
-__global__ __launch_bounds__(kSpThreads) void k_group_prep(const int32_t* __restrict__ gkeys,
-                                                           const int32_t* __restrict__ gbins, int64_t n,
+// MinMaxSketch.insert, bucketed: every (element, row) pair targets table cell c; pairs are
+// counted per bucket of 8192 cells, scattered into bucket order, and each bucket's minimum is
+// taken with LDS atomics by one workgroup (random global 64-bit atomics were HBM-latency bound).
+// Pair word: |bin - zero| [63:48], key [47:17], bin < zero [16], cell % 8192 [12:0]; its value
+// with the cell bits cleared orders by (distance, key): the smaller distance wins and ties keep
+// the earlier insert (keys ascend within a group).
+constexpr int kMmBucketBits = 13;
+constexpr int kMmBucketCells = 1 << kMmBucketBits;
+constexpr int kMmLdsBuckets = 8192;  // per-workgroup bucket histogram in LDS up to this many
+constexpr int kMmChunk = 16384;      // elements per workgroup in the count / scatter passes
+
+__device__ __forceinline__ int64_t mm_cell(const SpGroups* gp, int g, int r, int32_t key) {
+    const int32_t cols = gp->cols[g];
+    return gp->tab_off[g] + (int64_t)r * cols + java_hash(gp->hash_ids[g][r], key, cols);
+}
+__device__ __forceinline__ uint64_t mm_pair(int32_t key, int32_t bin, int32_t zero, int64_t cell) {
+    return ((uint64_t)mm_dist(bin, zero) << 48) | ((uint64_t)(uint32_t)key << 17) |
+           ((uint64_t)(bin < zero ? 1u : 0u) << 16) | (uint64_t)(cell & (kMmBucketCells - 1));
+}
+
+// Deltas, bitsNeeded histogram and order check (DeltaAdaptiveEncoder.encode step 1) plus the
+// per-bucket pair counts of the MinMax insert.
+__global__ __launch_bounds__(kSpThreads) void k_group_prep(const int32_t* __restrict__ gkeys, int64_t n,
                                                            const SpGroups* __restrict__ gp,
                                                            uint8_t* __restrict__ need, uint32_t* __restrict__ hist,
-                                                           uint32_t* __restrict__ err, uint64_t* __restrict__ cells) {
+                                                           uint32_t* __restrict__ err,
+                                                           unsigned long long* __restrict__ bucket_count,
+                                                           int nbuckets) {
     __shared__ int64_t S[kMaxGroups + 1];
     __shared__ uint32_t H[kMaxGroups * kDeltaHist];
-    const int G = gp->G, rows = gp->rows, zero = gp->zero;
+    __shared__ uint32_t BH[kMmLdsBuckets];
+    const int G = gp->G, rows = gp->rows;
+    const bool lds_b = nbuckets <= kMmLdsBuckets;
     load_starts(gp, S);
     for (int j = threadIdx.x; j < G * kDeltaHist; j += kSpThreads) H[j] = 0;
+    if (lds_b)
+        for (int j = threadIdx.x; j < nbuckets; j += kSpThreads) BH[j] = 0;
     __syncthreads();
     uint32_t bad = 0;
-    for (int64_t i = (int64_t)blockIdx.x * kSpThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kSpThreads) {
+    const int64_t c0 = (int64_t)blockIdx.x * kMmChunk, c1 = std::min<int64_t>(n, c0 + kMmChunk);
+    for (int64_t i = c0 + threadIdx.x; i < c1; i += kSpThreads) {
         const int g = group_of_elem(S, i);
-        const int32_t key = gkeys[i], bin = gbins[i];
+        const int32_t key = gkeys[i];
         const bool first = i == S[g];
         const int32_t d = first ? key : (int32_t)((uint32_t)key - (uint32_t)gkeys[i - 1]);
         int nb;
@@ -407,43 +446,115 @@ __global__ __launch_bounds__(kSpThreads) void k_group_prep(const int32_t* __rest
         }
         need[i] = (uint8_t)nb;
         atomicAdd(&H[g * kDeltaHist + nb], 1u);
-        const int32_t cols = gp->cols[g];
-        const uint64_t cell = ((uint64_t)mm_dist(bin, zero) << 47) | ((uint64_t)(uint32_t)key << 16) |
-                              (uint64_t)(uint32_t)bin;
         for (int r = 0; r < rows; r++) {
-            const int64_t idx = gp->tab_off[g] + (int64_t)r * cols + java_hash(gp->hash_ids[g][r], key, cols);
-            atomicMin(reinterpret_cast<unsigned long long*>(&cells[idx]), (unsigned long long)cell);
+            const int b = (int)(mm_cell(gp, g, r, key) >> kMmBucketBits);
+            if (lds_b) atomicAdd(&BH[b], 1u);
+            else atomicAdd(&bucket_count[b], 1ull);
         }
     }
     if (bad) atomicOr(err, 1u);
     __syncthreads();
     for (int j = threadIdx.x; j < G * kDeltaHist; j += kSpThreads)
         if (H[j]) atomicAdd(&hist[j], H[j]);
+    if (lds_b && rows > 0)
+        for (int j = threadIdx.x; j < nbuckets; j += kSpThreads)
+            if (BH[j]) atomicAdd(&bucket_count[j], (unsigned long long)BH[j]);
 }
 
-hipError_t launch_group_prep(hipStream_t st, const int32_t* gkeys, const int32_t* gbins, int64_t n,
-                             const SpGroups* gp, uint8_t* need, uint32_t* hist, uint32_t* err,
-                             uint64_t* cells) {
+hipError_t launch_group_prep(hipStream_t st, const int32_t* gkeys, int64_t n, const SpGroups* gp, uint8_t* need,
+                             uint32_t* hist, uint32_t* err, uint64_t* bucket_count, int nbuckets) {
     if (n <= 0) return hipSuccess;
-    const int64_t grid = std::min<int64_t>(sp_tiles(n, kSpThreads * 4), 2048);
-    hipLaunchKernelGGL(k_group_prep, dim3((unsigned)grid), dim3(kSpThreads), 0, st, gkeys, gbins, n, gp, need,
-                       hist, err, cells);
+    hipLaunchKernelGGL(k_group_prep, dim3((unsigned)sp_tiles(n, kMmChunk)), dim3(kSpThreads), 0, st, gkeys, n, gp,
+                       need, hist, err, reinterpret_cast<unsigned long long*>(bucket_count), nbuckets);
     return hipGetLastError();
 }
 
-__global__ void k_minmax_finalize(const uint64_t* __restrict__ cells, int64_t ncells, int32_t fill,
-                                  int32_t* __restrict__ table) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ncells; i += (int64_t)gridDim.x * blockDim.x) {
-        const uint64_t c = cells[i];
-        table[i] = c == ~0ull ? fill : (int32_t)(c & 0xFFFFu);
+// Scatter the pairs into bucket order: per-workgroup bucket counts reserve one range per bucket
+// (one global atomic per workgroup and bucket), lanes take slots with LDS atomics.
+__global__ __launch_bounds__(kSpThreads) void k_mm_scatter(const int32_t* __restrict__ gkeys,
+                                                           const int32_t* __restrict__ gbins, int64_t n,
+                                                           const SpGroups* __restrict__ gp,
+                                                           const uint64_t* __restrict__ bucket_base,
+                                                           unsigned long long* __restrict__ cursor, int nbuckets,
+                                                           uint64_t* __restrict__ pairs) {
+    __shared__ int64_t S[kMaxGroups + 1];
+    __shared__ uint32_t cnt[kMmLdsBuckets];
+    __shared__ uint32_t lofs[kMmLdsBuckets];
+    const int rows = gp->rows, zero = gp->zero;
+    const bool lds_b = nbuckets <= kMmLdsBuckets;
+    load_starts(gp, S);
+    if (lds_b)
+        for (int j = threadIdx.x; j < nbuckets; j += kSpThreads) cnt[j] = 0;
+    __syncthreads();
+    const int64_t c0 = (int64_t)blockIdx.x * kMmChunk, c1 = std::min<int64_t>(n, c0 + kMmChunk);
+    if (lds_b) {
+        for (int64_t i = c0 + threadIdx.x; i < c1; i += kSpThreads) {
+            const int g = group_of_elem(S, i);
+            const int32_t key = gkeys[i];
+            for (int r = 0; r < rows; r++) atomicAdd(&cnt[(int)(mm_cell(gp, g, r, key) >> kMmBucketBits)], 1u);
+        }
+        __syncthreads();
+        for (int j = threadIdx.x; j < nbuckets; j += kSpThreads) {
+            lofs[j] = cnt[j] ? (uint32_t)atomicAdd(&cursor[j], (unsigned long long)cnt[j]) : 0u;
+            cnt[j] = 0;
+        }
+        __syncthreads();
+    }
+    for (int64_t i = c0 + threadIdx.x; i < c1; i += kSpThreads) {
+        const int g = group_of_elem(S, i);
+        const int32_t key = gkeys[i], bin = gbins[i];
+        for (int r = 0; r < rows; r++) {
+            const int64_t cell = mm_cell(gp, g, r, key);
+            const int b = (int)(cell >> kMmBucketBits);
+            const uint64_t slot = lds_b ? (uint64_t)lofs[b] + atomicAdd(&cnt[b], 1u)
+                                        : (uint64_t)atomicAdd(&cursor[b], 1ull);
+            pairs[bucket_base[b] + slot] = mm_pair(key, bin, zero, cell);
+        }
     }
 }
 
-hipError_t launch_minmax_finalize(hipStream_t st, const uint64_t* cells, int64_t ncells, int32_t fill,
-                                  int32_t* table) {
-    if (ncells <= 0) return hipSuccess;
-    const int64_t grid = std::min<int64_t>(sp_tiles(ncells, kSpThreads), 4096);
-    hipLaunchKernelGGL(k_minmax_finalize, dim3((unsigned)grid), dim3(kSpThreads), 0, st, cells, ncells, fill, table);
+hipError_t launch_mm_scatter(hipStream_t st, const int32_t* gkeys, const int32_t* gbins, int64_t n,
+                             const SpGroups* gp, const uint64_t* bucket_base, uint64_t* cursor, int nbuckets,
+                             uint64_t* pairs) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_mm_scatter, dim3((unsigned)sp_tiles(n, kMmChunk)), dim3(kSpThreads), 0, st, gkeys, gbins, n,
+                       gp, bucket_base, reinterpret_cast<unsigned long long*>(cursor), nbuckets, pairs);
+    return hipGetLastError();
+}
+
+// One workgroup per bucket: LDS minimum per cell, then the int32 table cells (empty -> fill).
+__global__ __launch_bounds__(kSpThreads) void k_mm_bucket(const uint64_t* __restrict__ pairs,
+                                                          const uint64_t* __restrict__ bucket_base,
+                                                          int64_t ncells, int32_t zero, int32_t fill,
+                                                          int32_t* __restrict__ table) {
+    __shared__ unsigned long long cmin[kMmBucketCells];
+    const int b = blockIdx.x;
+    for (int j = threadIdx.x; j < kMmBucketCells; j += kSpThreads) cmin[j] = ~0ull;
+    __syncthreads();
+    const uint64_t p0 = bucket_base[b], p1 = bucket_base[b + 1];
+    constexpr uint64_t kLo = (uint64_t)(kMmBucketCells - 1);
+    for (uint64_t p = p0 + threadIdx.x; p < p1; p += kSpThreads) {
+        const uint64_t v = pairs[p];
+        atomicMin(&cmin[v & kLo], (unsigned long long)(v & ~kLo));
+    }
+    __syncthreads();
+    const int64_t cell0 = (int64_t)b << kMmBucketBits;
+    for (int j = threadIdx.x; j < kMmBucketCells && cell0 + j < ncells; j += kSpThreads) {
+        const uint64_t v = cmin[j];
+        int32_t out = fill;
+        if (v != ~0ull) {
+            const int32_t dist = (int32_t)(v >> 48);
+            out = ((v >> 16) & 1u) ? zero - dist : zero + dist;
+        }
+        table[cell0 + j] = out;
+    }
+}
+
+hipError_t launch_mm_bucket(hipStream_t st, const uint64_t* pairs, const uint64_t* bucket_base, int nbuckets,
+                            int64_t ncells, int32_t zero, int32_t fill, int32_t* table) {
+    if (nbuckets <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_mm_bucket, dim3((unsigned)nbuckets), dim3(kSpThreads), 0, st, pairs, bucket_base, ncells,
+                       zero, fill, table);
     return hipGetLastError();
 }
 
@@ -884,16 +995,20 @@ __device__ __forceinline__ int64_t merge_path(const int32_t* A, int64_t na, cons
     return lo;
 }
 
+// One workgroup per 2048 outputs: the tile's end points on each pair's merge path are found by
+// two global searches, the tile's A and B pieces are staged in LDS (coalesced), and every thread
+// merges 8 outputs from its LDS merge-path split.
 __global__ __launch_bounds__(kSpThreads) void k_merge_round(const int32_t* __restrict__ kin,
                                                             const int32_t* __restrict__ bin_in,
                                                             int32_t* __restrict__ kout, int32_t* __restrict__ bout,
                                                             const int64_t* __restrict__ rs, int nruns,
                                                             int64_t total) {
-    const int64_t o = ((int64_t)blockIdx.x * kSpThreads + threadIdx.x) * kMergePer;
-    const int64_t stop = std::min<int64_t>(o + kMergePer, total);
+    __shared__ int32_t sk[kSpTile], sb[kSpTile];
+    __shared__ int64_t s_a[2];
+    const int t = threadIdx.x;
+    const int64_t o1 = std::min<int64_t>(((int64_t)blockIdx.x + 1) * kSpTile, total);
     int q = 0;
-    for (int64_t out = o; out < stop;) {
-        // the pair whose output range holds `out` (a thread's outputs may span pairs)
+    for (int64_t out = (int64_t)blockIdx.x * kSpTile; out < o1;) {
         while (2 * q + 2 <= nruns && rs[2 * q + 2] <= out) q++;
         const int64_t a0 = rs[2 * q];
         const int64_t a1 = rs[std::min(2 * q + 1, nruns)];
@@ -901,29 +1016,39 @@ __global__ __launch_bounds__(kSpThreads) void k_merge_round(const int32_t* __res
         const int32_t* A = kin + a0;
         const int32_t* B = kin + a1;
         const int64_t na = a1 - a0, nb = b1 - a1;
-        int64_t ia = merge_path(A, na, B, nb, out - a0), ib = (out - a0) - ia;
-        const int64_t end = std::min<int64_t>(stop, b1);
-        for (; out < end; out++) {
-            const bool takeA = ib >= nb || (ia < na && A[ia] <= B[ib]);
-            if (takeA) {
-                kout[out] = A[ia];
-                bout[out] = bin_in[a0 + ia];
-                ia++;
-            } else {
-                kout[out] = B[ib];
-                bout[out] = bin_in[a1 + ib];
-                ib++;
+        const int64_t end = std::min(o1, b1);
+        if (t < 2) s_a[t] = merge_path(A, na, B, nb, (t == 0 ? out : end) - a0);
+        __syncthreads();
+        const int64_t ia0 = s_a[0], ia1 = s_a[1];
+        const int64_t ib0 = (out - a0) - ia0, ib1 = (end - a0) - ia1;
+        const int la = (int)(ia1 - ia0), lb = (int)(ib1 - ib0);
+        for (int k = t; k < la + lb; k += kSpThreads) {
+            const int64_t src = k < la ? a0 + ia0 + k : a1 + ib0 + (k - la);
+            sk[k] = kin[src];
+            sb[k] = bin_in[src];
+        }
+        __syncthreads();
+        const int d = t * kMergePer;
+        if (d < la + lb) {
+            int ia = (int)merge_path(sk, la, sk + la, lb, d), ib = d - ia;
+            const int cnt = std::min(kMergePer, la + lb - d);
+            for (int j = 0; j < cnt; j++) {
+                const bool takeA = ib >= lb || (ia < la && sk[ia] <= sk[la + ib]);
+                const int k = takeA ? ia++ : la + ib++;
+                kout[out + d + j] = sk[k];
+                bout[out + d + j] = sb[k];
             }
         }
+        __syncthreads();
+        out = end;
     }
 }
 
 hipError_t launch_merge_round(hipStream_t st, const int32_t* kin, const int32_t* bin_in, int32_t* kout,
                               int32_t* bout, const int64_t* run_start, int nruns, int64_t total) {
     if (total <= 0) return hipSuccess;
-    const int64_t threads = (total + kMergePer - 1) / kMergePer;
-    hipLaunchKernelGGL(k_merge_round, dim3((unsigned)sp_tiles(threads, kSpThreads)), dim3(kSpThreads), 0, st,
-                       kin, bin_in, kout, bout, run_start, nruns, total);
+    hipLaunchKernelGGL(k_merge_round, dim3((unsigned)sp_tiles(total, kSpTile)), dim3(kSpThreads), 0, st, kin, bin_in,
+                       kout, bout, run_start, nruns, total);
     return hipGetLastError();
 }
 

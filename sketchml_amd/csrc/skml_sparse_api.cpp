@@ -443,18 +443,21 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const float* vals, int64_t nnz, 
     int32_t* gk = scratch<int32_t>(c, kSlotGKeys, (size_t)nnz);
     int32_t* gb = scratch<int32_t>(c, kSlotGBins, (size_t)nnz);
     uint8_t* need = scratch<uint8_t>(c, kSlotNeed, (size_t)nnz);
-    uint64_t* cellbuf = scratch<uint64_t>(c, kSlotCells, (size_t)cells);
+    const int nbuckets = (int)((cells + kMmCellsPerBucket - 1) / kMmCellsPerBucket);
+    uint64_t* bucket = scratch<uint64_t>(c, kSlotCells, (size_t)2 * nbuckets + 2);  // counts->bases, cursors
+    uint64_t* pairs = scratch<uint64_t>(c, kSlotDelta, (size_t)G.rows * (size_t)nnz);
     uint32_t* small = scratch<uint32_t>(c, kSlotSmall, (size_t)kMaxGroups * kDeltaHist + 64);
-    if (!gk || !gb || !need || !cellbuf || !small) return bail(sfail(SKML_E_OOM, "sparse scratch"));
+    if (!gk || !gb || !need || !bucket || !pairs || !small) return bail(sfail(SKML_E_OOM, "sparse scratch"));
+    uint64_t* cursor = bucket + nbuckets + 1;
     if (hipSuccess != launch_part_scatter(st, keys, s->qpayload, nnz, s->g_dev, tc, gk, gb))
         return bail(sfail(SKML_E_HIP, "part_scatter"));
-    // ---- 4. deltas / histogram / order check / MinMax insert ----
+    // ---- 4. deltas / histogram / order check, then the bucketed MinMax insert ----
     uint32_t* hist = small;
     uint32_t* err = small + kMaxGroups * kDeltaHist;
     if (hipMemsetAsync(small, 0, sizeof(uint32_t) * ((size_t)kMaxGroups * kDeltaHist + 64), st) != hipSuccess ||
-        hipMemsetAsync(cellbuf, 0xFF, sizeof(uint64_t) * (size_t)cells, st) != hipSuccess)
+        hipMemsetAsync(bucket, 0, sizeof(uint64_t) * ((size_t)2 * nbuckets + 2), st) != hipSuccess)
         return bail(sfail(SKML_E_HIP, "memset"));
-    if (hipSuccess != launch_group_prep(st, gk, gb, nnz, s->g_dev, need, hist, err, cellbuf))
+    if (hipSuccess != launch_group_prep(st, gk, nnz, s->g_dev, need, hist, err, bucket, nbuckets))
         return bail(sfail(SKML_E_HIP, "group_prep"));
     std::vector<uint32_t> hh((size_t)kMaxGroups * kDeltaHist + 1);
     if (int e = sync_to_host(c, hh.data(), small, sizeof(uint32_t) * hh.size())) return bail(e);
@@ -462,8 +465,10 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const float* vals, int64_t nnz, 
         return bail(sfail(SKML_E_ORDER, "Log for a non-positive key delta (keys must ascend strictly)"));
     if (hipMalloc(&s->tables, sizeof(int32_t) * (size_t)std::max<int64_t>(cells, 1)) != hipSuccess)
         return bail(sfail(SKML_E_OOM, "tables"));
-    if (hipSuccess != launch_minmax_finalize(st, cellbuf, cells, G.fill, s->tables))
-        return bail(sfail(SKML_E_HIP, "minmax_finalize"));
+    if (int e = scan_tiles(c, bucket, nbuckets, 1, nullptr)) return bail(e);
+    if (hipSuccess != launch_mm_scatter(st, gk, gb, nnz, s->g_dev, bucket, cursor, nbuckets, pairs) ||
+        hipSuccess != launch_mm_bucket(st, pairs, bucket, nbuckets, cells, G.zero, G.fill, s->tables))
+        return bail(sfail(SKML_E_HIP, "minmax insert"));
     // ---- 5. DeltaAdaptive key streams ----
     if (int e = encode_delta_streams(c, s, gk, need, hh.data())) return bail(e);
     if (hipStreamSynchronize(st) != hipSuccess) return bail(sfail(SKML_E_HIP, "sync"));
@@ -857,8 +862,8 @@ int skml_delta_encode(skml_ctx* c, const int32_t* keys, int64_t n, int32_t* num_
             rc = sfail(SKML_E_HIP, "memset");
             break;
         }
-        if (launch_group_prep(st, keys, keys, n, tmp.g_dev, need, small, small + kMaxGroups * kDeltaHist,
-                              nullptr) != hipSuccess) {
+        if (launch_group_prep(st, keys, n, tmp.g_dev, need, small, small + kMaxGroups * kDeltaHist, nullptr,
+                              0) != hipSuccess) {
             rc = sfail(SKML_E_HIP, "group_prep");
             break;
         }
