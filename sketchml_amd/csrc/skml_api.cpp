@@ -396,7 +396,7 @@ int skml_dense_encode_f32(skml_ctx* c, const float* x, int64_t n, const skml_par
     if ((st = ensure_ws(c, chunks, &w))) return st;
     if ((st = ensure_ranks(c, n, p->bin_num))) return st;
     const uint64_t s0 = ((uint64_t)p->seed ^ kLcgMult) & kLcgMask;
-    const int64_t nwg = (chunks + kLeafChunks - 1) / kLeafChunks;
+    const int64_t nwg = (chunks + kLeafChunks - 1) / kLeafChunks;  // leaf partials (one per wave tile)
 
     bool fused = false;
     if (chunks > 0) {

@@ -310,51 +310,80 @@ __device__ __forceinline__ void exact_merge_task(const float* older, const float
 // Bucket LUT for the quantize pass (built by one workgroup; `sp` = splits in LDS as floats
 // rounded toward +inf, IEEE-sorted; `lut` in global memory).  For a non-NaN float x and a
 // double split s, s <= x  <=>  RU(s) <= x, so the float table gives the exact indexOf.
-// base[b] = #{s < vmin(b)} (IEEE), where vmin/vmax are the smallest / largest non-NaN values
-// whose key has prefix b (NaN-only buckets clamp to +-inf); need(b) = #{s <= vmax(b)} - base[b];
-// cmax = max need.  Each thread sweeps a contiguous bucket range with two pointers.
+//
+// Bucket of a value = top kLutBits of its total-order key, with -0.0 counted in +0.0's bucket.
+// base[b] = #{splits in buckets < b} (a histogram + exclusive scan) is a lower bound of indexOf
+// for every x in bucket b, and indexOf(x) - base[b] <= need(b) = #{splits in bucket b}, plus all
+// zero splits for the bucket holding -0.0 (IEEE -0.0 == +0.0); cmax = max need.  Quantize then
+// starts at base[b] and bisects over the next 2^ceil(log2(cmax+1)) splits.
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ float lut_bucket_value(uint32_t key) {
-    constexpr uint32_t kNegInf = 0x007FFFFFu, kPosInf = 0xFF800000u;  // f2key(-inf), f2key(+inf)
-    key = key < kNegInf ? kNegInf : (key > kPosInf ? kPosInf : key);
-    return __uint_as_float(key2f(key));
+__device__ __forceinline__ uint32_t lut_bucket_of(float f) {
+    uint32_t u = __float_as_uint(f);
+    if (u == 0x80000000u) u = 0u;  // -0.0 -> +0.0's bucket
+    return f2key(u) >> (32 - kLutBits);
 }
 
-__device__ __forceinline__ void build_quant_lut(const float* sp, int nsplit, QuantLut* lut, int* s_cmax) {
-    const int T = blockDim.x, t = threadIdx.x;
-    if (t == 0) *s_cmax = 0;
+// s_misc: 20 ints of LDS; lbuf: kLutSize / 2 uint32 of LDS (u16 counts, then u16 bases in place).
+__device__ __forceinline__ void build_quant_lut(const float* sp, int nsplit, QuantLut* lut, int* s_misc,
+                                                uint32_t* lbuf) {
+    const int T = blockDim.x, t = threadIdx.x, lane = t & 63, w = t >> 6, nw = T >> 6;
+    constexpr uint32_t kNegZeroBucket = 0x7FFFFFFFu >> (32 - kLutBits);
+    uint16_t* cnt = reinterpret_cast<uint16_t*>(lbuf);
+    for (int i = t; i < kLutSize / 2; i += T) lbuf[i] = 0u;
+    if (t < 20) s_misc[t] = 0;
     __syncthreads();
-    const int per = (kLutSize + T - 1) / T;
-    const int b0 = t * per, b1 = min(kLutSize, b0 + per);
-    int need_max = 0;
-    if (b0 < b1) {
-        const float v0 = lut_bucket_value((uint32_t)b0 << (32 - kLutBits));
-        int lo = 0, hi = nsplit;  // p = #{s < v0}
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (sp[mid] < v0) lo = mid + 1;
-            else hi = mid;
-        }
-        // sp[p] and sp[q] stay in registers; LDS is read only when a pointer advances
-        const float kInf = __uint_as_float(0x7F800000u);
-        int p = lo, q = lo;
-        float sp_p = p < nsplit ? sp[p] : kInf, sp_q = sp_p;
-        for (int b = b0; b < b1; b++) {
-            const float vmin = lut_bucket_value((uint32_t)b << (32 - kLutBits));
-            const float vmax = lut_bucket_value(((uint32_t)(b + 1) << (32 - kLutBits)) - 1u);
-            while (p < nsplit && sp_p < vmin) sp_p = ++p < nsplit ? sp[p] : kInf;
-            if (q < p) {
-                q = p;
-                sp_q = sp_p;
-            }
-            while (q < nsplit && sp_q <= vmax) sp_q = ++q < nsplit ? sp[q] : kInf;
-            lut->base[b] = (uint16_t)p;
-            need_max = max(need_max, q - p);
+    for (int i = t; i < nsplit; i += T) {  // histogram (u16 halves of u32 words)
+        const uint32_t b = lut_bucket_of(sp[i]);
+        atomicAdd(&lbuf[b >> 1], 1u << (16 * (b & 1)));
+        if ((__float_as_uint(sp[i]) & 0x7FFFFFFFu) == 0u) atomicAdd(&s_misc[0], 1);
+    }
+    __syncthreads();
+    // exclusive scan: each thread owns kLutSize / T consecutive buckets
+    const int per = kLutSize / T, b0 = t * per;  // per >= 16, a multiple of 8
+    const uint4* c4 = reinterpret_cast<const uint4*>(cnt + b0);
+    int sum = 0, cmax = 0;
+    for (int k = 0; k < per / 8; k++) {  // 8 u16 counts per 16-byte LDS read
+        const uint4 q = c4[k];
+        const uint32_t wds[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const int lo = (int)(wds[e] & 0xFFFFu), hi = (int)(wds[e] >> 16);
+            sum += lo + hi;
+            cmax = max(cmax, max(lo, hi));
         }
     }
-    atomicMax(s_cmax, need_max);
+    if (b0 <= (int)kNegZeroBucket && (int)kNegZeroBucket < b0 + per) cmax = max(cmax, cnt[kNegZeroBucket] + s_misc[0]);
+    int inc = sum;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(inc, off, 64);
+        if (lane >= off) inc += y;
+    }
+    if (lane == 63) s_misc[4 + w] = inc;
+    atomicMax(&s_misc[1], cmax);
     __syncthreads();
-    if (t == 0) lut->cmax = (*s_cmax <= kLutMaxNeed && nsplit <= kLutMaxSplits) ? *s_cmax : -1;
+    int run = inc - sum;
+    for (int j = 0; j < w; j++) run += s_misc[4 + j];
+    (void)nw;
+    uint4* o4 = reinterpret_cast<uint4*>(cnt + b0);
+    for (int k = 0; k < per / 8; k++) {  // counts -> bases in place, 8 per 16-byte access
+        const uint4 q = o4[k];
+        uint32_t wds[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const uint32_t lo = wds[e] & 0xFFFFu, hi = wds[e] >> 16;
+            const uint32_t blo = (uint32_t)run;
+            run += (int)lo;
+            wds[e] = blo | ((uint32_t)run << 16);
+            run += (int)hi;
+        }
+        o4[k] = make_uint4(wds[0], wds[1], wds[2], wds[3]);
+    }
+    __syncthreads();
+    const uint4* src = reinterpret_cast<const uint4*>(lbuf);
+    uint4* dst = reinterpret_cast<uint4*>(lut->base);
+    for (int i = t; i < (int)(sizeof(lut->base) / (sizeof(uint4))); i += T) dst[i] = src[i];
+    if (t == 0) lut->cmax = (s_misc[1] <= kLutMaxNeed && nsplit <= kLutMaxSplits) ? s_misc[1] : -1;
 }
 
 // Quantizer.indexOf (Quantizer.java:49-92) on a NaN value: the probe never succeeds, so the

@@ -71,6 +71,11 @@ struct SummaryShared {
     int64_t total;
 };
 
+static_assert(sizeof(float) * kMaxSamples + sizeof(int64_t) * (kMaxSamples + 1) >= sizeof(uint16_t) * kLutSize,
+              "LUT staging must fit in sorted[] + w[]");
+static_assert(offsetof(SummaryShared, w) == offsetof(SummaryShared, sorted) + sizeof(float) * kMaxSamples,
+              "sorted[] and w[] must be contiguous");
+
 union MergeShared {
     TileShared t;
     SummaryShared s;
@@ -415,7 +420,7 @@ __global__ __launch_bounds__(256, 4) void k_leaf2(const float* __restrict__ x, i
         p.max_key = mx;
         p.flags = fl | ((mn < 0x007FFFFFu || mx > 0xFF800000u) ? 1u : 0u);
         p.pad = 0;
-        part[tile] = p;
+        part[tile] = p;  // (a single atomic accumulator instead costs ~40 us of contention)
     }
 }
 
@@ -747,9 +752,19 @@ __device__ void summary_block(const SummaryArgs& a, SummaryShared& S) {
             mn = k < mn ? k : mn;
             mx = k > mx ? k : mx;
         }
-        atomicMin(&S.min_key, mn);
-        atomicMax(&S.max_key, mx);
-        if (fl) atomicOr(&S.flags, fl);
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {  // wave reduction: one LDS atomic per wave
+            const uint32_t omn = (uint32_t)__shfl_xor((int)mn, off, 64);
+            const uint32_t omx = (uint32_t)__shfl_xor((int)mx, off, 64);
+            mn = omn < mn ? omn : mn;
+            mx = omx > mx ? omx : mx;
+            fl |= (uint32_t)__shfl_xor((int)fl, off, 64);
+        }
+        if ((t & 63) == 0) {
+            atomicMin(&S.min_key, mn);
+            atomicMax(&S.max_key, mx);
+            if (fl) atomicOr(&S.flags, fl);
+        }
     }
     SKML_PROF(3);
     // ---- gather runs; the tail is sorted in Arrays.sort total order by rank counting ----
@@ -871,15 +886,19 @@ __device__ void summary_block(const SummaryArgs& a, SummaryShared& S) {
         for (int i = b0; i < b1; i++) loc += (!a.dedup || i == 0 || raw[i] != raw[i - 1]) ? 1 : 0;
         const int64_t base = block_scan_excl(loc, S.wsum, &S.total);
         int64_t o = base;
+        int zmin = 0x7FFFFFFF;
         for (int i = b0; i < b1; i++) {
             if (!a.dedup || i == 0 || raw[i] != raw[i - 1]) {
                 const double sp = raw[i];
                 splits[o] = sp;
                 if (o < kMaxSamples) S.smp[o] = (float)sp;  // LDS copy for the quantize LUT
-                if (!(sp < 0.0)) atomicMin(&S.zero, (int)o);
+                if (!(sp < 0.0)) zmin = min(zmin, (int)o);
                 o++;
             }
         }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) zmin = min(zmin, __shfl_xor(zmin, off, 64));
+        if ((t & 63) == 0 && zmin != 0x7FFFFFFF) atomicMin(&S.zero, zmin);  // one LDS atomic per wave
         bin_num = (int)S.total + 1;
     }
     __syncthreads();
@@ -905,7 +924,8 @@ __device__ void summary_block(const SummaryArgs& a, SummaryShared& S) {
     const int nsplit = bin_num - 1;
     if (nsplit <= kMaxSamples && nsplit <= kLutMaxSplits && n > 0) {
         SKML_PROF(9);
-        build_quant_lut(S.smp, nsplit, a.lut, &S.zero);
+        // LDS staging of the table aliases sorted[] + w[] (both dead after getQuantiles)
+        build_quant_lut(S.smp, nsplit, a.lut, reinterpret_cast<int*>(S.wsum), reinterpret_cast<uint32_t*>(S.sorted));
     } else if (t == 0) {
         a.lut->cmax = -1;
     }
@@ -1055,8 +1075,10 @@ __global__ __launch_bounds__(256) void k_set_splits(uint8_t* payload, int64_t n,
                                                     QuantLut* lut) {
     skml_dense_header* hdr = reinterpret_cast<skml_dense_header*>(payload);
     double* splits = reinterpret_cast<double*>(payload + kHeaderBytes);
-    __shared__ int s_zero, s_cmax;
+    __shared__ int s_zero;
+    __shared__ int s_misc[20];
     __shared__ float s_sp[kLutMaxSplits];
+    __shared__ __align__(16) uint32_t s_lbuf[kLutSize / 2];
     if (threadIdx.x == 0) s_zero = 0x7FFFFFFF;
     __syncthreads();
     for (int i = threadIdx.x; i < nsplits; i += blockDim.x) {
@@ -1065,7 +1087,7 @@ __global__ __launch_bounds__(256) void k_set_splits(uint8_t* payload, int64_t n,
         if (!(sp[i] < 0.0)) atomicMin(&s_zero, i);
     }
     __syncthreads();
-    if (nsplits <= kLutMaxSplits) build_quant_lut(s_sp, nsplits, lut, &s_cmax);
+    if (nsplits <= kLutMaxSplits) build_quant_lut(s_sp, nsplits, lut, s_misc, s_lbuf);
     else if (threadIdx.x == 0) lut->cmax = -1;
     if (threadIdx.x == 0) {
         const int bins = nsplits + 1;
