@@ -117,6 +117,21 @@ size_t skml_dense_payload_bytes(int64_t n, int32_t bin_num);
 int skml_dense_encode_f32(skml_ctx* ctx, const float* x_dev, int64_t n, const skml_params* params,
                           void* payload_dev, size_t payload_cap);
 
+/* The same on fp64 input (the reference's own double[] path): the sketch
+ * sorts and merges 64-bit keys, indexOf compares in double.  Asynchronous. */
+int skml_dense_encode_f64(skml_ctx* ctx, const double* x_dev, int64_t n, const skml_params* params,
+                          void* payload_dev, size_t payload_cap);
+
+/* UniformQuantizer.quantize(double[]) (quantization/UniformQuantizer.java:21-45): min / max
+ * (Double.MAX_VALUE / Double.MIN_VALUE initialised, NaN values skipped), bin_num-1 splits by
+ * repeated `+= (max-min)/bin_num`, findZeroIdx, bins[i] = indexOf(x[i]).  No Maths.unique; NaN
+ * values are binned, not rejected.  parallelQuantize is the same computation
+ * (UniformQuantizer.java:48-70).  params->seed / dedup are ignored.  Asynchronous. */
+int skml_dense_encode_uniform_f32(skml_ctx* ctx, const float* x_dev, int64_t n,
+                                  const skml_params* params, void* payload_dev, size_t payload_cap);
+int skml_dense_encode_uniform_f64(skml_ctx* ctx, const double* x_dev, int64_t n,
+                                  const skml_params* params, void* payload_dev, size_t payload_cap);
+
 /* Split-injected parity mode: quantise against a caller-given split table (host doubles,
  * sorted ascending), min and max, exactly as Quantizer.quantizeToBins would.  Asynchronous. */
 int skml_dense_encode_with_splits_f32(skml_ctx* ctx, const float* x_dev, int64_t n,
@@ -126,6 +141,10 @@ int skml_dense_encode_with_splits_f32(skml_ctx* ctx, const float* x_dev, int64_t
 /* DenseVectorCompressor.decompressDense (sample/DenseVectorCompressor.java:84-91):
  * out[i] = (float) Quantizer.getValues()[bin[i]].  Asynchronous. */
 int skml_dense_decode_f32(skml_ctx* ctx, const void* payload_dev, float* out_dev, int64_t n);
+
+/* decompressDense into double[] (the reference's return type): out[i] = getValues()[bin[i]]
+ * without the float rounding.  Asynchronous. */
+int skml_dense_decode_f64(skml_ctx* ctx, const void* payload_dev, double* out_dev, int64_t n);
 
 /* Fused decode of P payloads into one sum: out[i] = scale * sum_p values_p[bin_p[i]], the
  * decode half of Gradient.sum + timesBy(1/P) (ml/gradient/Gradient.scala:44-49,

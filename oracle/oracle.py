@@ -81,6 +81,7 @@ def lib():
         L.orc_quantize.argtypes = [dblp, C.c_int32, C.c_int32, C.c_int64, C.POINTER(QuantHeader), i32p]
         L.orc_parallel_quantize.argtypes = [dblp, C.c_int32, C.c_int32, C.c_int32, C.c_int64,
                                             C.POINTER(QuantHeader), i32p]
+        L.orc_uniform_quantize.argtypes = [dblp, C.c_int32, C.c_int32, C.POINTER(QuantHeader), i32p]
         L.orc_index_of.argtypes = [C.POINTER(QuantHeader), C.c_double]
         L.orc_index_of.restype = C.c_int32
         L.orc_get_values.argtypes = [C.POINTER(QuantHeader), dblp]
@@ -187,6 +188,17 @@ def quantize(values, bin_num=256, seed=0) -> OracleQuant:
     st = lib().orc_quantize(_p(v, dblp), len(v), bin_num, seed, C.byref(hdr), _p(bins, i32p))
     if st:
         raise OracleError(st, "quantize")
+    return OracleQuant(hdr, bins[: len(v)])
+
+
+def uniform_quantize(values, bin_num=256) -> OracleQuant:
+    """UniformQuantizer.quantize (quantization/UniformQuantizer.java:21-45)."""
+    v = np.ascontiguousarray(values, dtype=np.float64)
+    hdr = QuantHeader()
+    bins = np.zeros(max(len(v), 1), dtype=np.int32)
+    st = lib().orc_uniform_quantize(_p(v, dblp), len(v), bin_num, C.byref(hdr), _p(bins, i32p))
+    if st:
+        raise OracleError(st, "uniform_quantize")
     return OracleQuant(hdr, bins[: len(v)])
 
 

@@ -450,6 +450,31 @@ int orc_parallel_quantize(const double* values, int32_t n, int32_t bin_num, int3
     return st;
 }
 
+int orc_uniform_quantize(const double* values, int32_t n, int32_t bin_num, orc_quant_header* hdr,
+                         int32_t* bins) {
+    if (bin_num <= 1 || bin_num > 65536) return ORC_E_ARG;
+    /* UniformQuantizer.java:24-29 */
+    double mn = 1.7976931348623157e308, mx = 4.9e-324;
+    for (int32_t i = 0; i < n; i++) {
+        const double v = values[i];
+        if (v < mn) mn = v;
+        if (v > mx) mx = v;
+    }
+    /* UniformQuantizer.java:31-36: sequential accumulation, every add rounded */
+    const double step = (mx - mn) / bin_num;
+    const int32_t ns = bin_num - 1;
+    hdr->n = n;
+    hdr->min = mn;
+    hdr->max = mx;
+    hdr->bin_num = bin_num;
+    if (ns > 0) hdr->splits[0] = mn + step;
+    for (int32_t i = 1; i < ns; i++) hdr->splits[i] = hdr->splits[i - 1] + step;
+    find_zero_idx(hdr); /* UniformQuantizer.java:38 */
+    if (bins)
+        for (int32_t i = 0; i < n; i++) bins[i] = orc_index_of(hdr, values[i]);
+    return ORC_OK;
+}
+
 void orc_get_values(const orc_quant_header* h, double* out) {
     int32_t ns = h->bin_num - 1;
     out[0] = 0.5 * (h->min + h->splits[0]);

@@ -71,6 +71,12 @@ int orc_quantize(const double* values, int32_t n, int32_t bin_num, int64_t seed,
  * Slice t's sketch draws from Random(seed + t); merging continues slice 0's stream. */
 int orc_parallel_quantize(const double* values, int32_t n, int32_t bin_num, int32_t threads,
                           int64_t seed, orc_quant_header* hdr, int32_t* bins);
+/* UniformQuantizer.quantize (quantization/UniformQuantizer.java:21-45): min / max by IEEE `<` / `>`
+ * from Double.MAX_VALUE / Double.MIN_VALUE (NaN values skipped, the first zero wins the min),
+ * splits by repeated `+= step` in double, no Maths.unique.  NaN values are accepted and binned
+ * by indexOf.  bins may be NULL. */
+int orc_uniform_quantize(const double* values, int32_t n, int32_t bin_num, orc_quant_header* hdr,
+                         int32_t* bins);
 /* Quantizer.indexOf (Quantizer.java:49-72) */
 int32_t orc_index_of(const orc_quant_header* h, double x);
 /* Quantizer.getValues (Quantizer.java:39-47) */

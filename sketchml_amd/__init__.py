@@ -8,12 +8,12 @@ from . import _lib
 from .compressor import DenseVectorCompressor
 from .context import Context, alloc_aligned, get_context
 from .exceptions import QuantileSketchException, SketchMLException
-from .quantization import QuantileQuantizer, QuantizationType, Quantizer
+from .quantization import QuantileQuantizer, QuantizationType, Quantizer, UniformQuantizer
 from .sparse import (DeltaAdaptiveEncoder, GroupedMinMaxSketch, SparseVectorCompressor, encode_dense_as_sparse,
                      encode_sparse, to_sparse)
 
 __all__ = ["Context", "DeltaAdaptiveEncoder", "DenseVectorCompressor", "GroupedMinMaxSketch",
-           "SparseVectorCompressor", "encode_dense_as_sparse", "encode_sparse", "to_sparse", "QuantileQuantizer", "QuantizationType", "Quantizer",
+           "SparseVectorCompressor", "encode_dense_as_sparse", "encode_sparse", "to_sparse", "QuantileQuantizer", "QuantizationType", "Quantizer", "UniformQuantizer",
            "QuantileSketchException", "SketchMLException", "get_context", "alloc_aligned"]
 
 LIB_PATH = _lib.LIB_PATH

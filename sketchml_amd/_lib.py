@@ -75,7 +75,11 @@ _SIGS = {
     "skml_dense_encode_f32": (C.c_int, [vp, vp, i64, C.POINTER(Params), vp, C.c_size_t]),
     "skml_dense_encode_with_splits_f32": (C.c_int, [vp, vp, i64, dblp, i32, C.c_double, C.c_double,
                                                     vp, C.c_size_t]),
+    "skml_dense_encode_f64": (C.c_int, [vp, vp, i64, C.POINTER(Params), vp, C.c_size_t]),
+    "skml_dense_encode_uniform_f32": (C.c_int, [vp, vp, i64, C.POINTER(Params), vp, C.c_size_t]),
+    "skml_dense_encode_uniform_f64": (C.c_int, [vp, vp, i64, C.POINTER(Params), vp, C.c_size_t]),
     "skml_dense_decode_f32": (C.c_int, [vp, vp, vp, i64]),
+    "skml_dense_decode_f64": (C.c_int, [vp, vp, vp, i64]),
     "skml_dense_decode_sum_f32": (C.c_int, [vp, vp, i32, C.c_size_t, vp, i64, C.c_double]),
     "skml_dense_bins_i32": (C.c_int, [vp, vp, vp, i64]),
     "skml_dense_info": (C.c_int, [vp, vp, C.POINTER(DenseHeader), dblp, i32]),

@@ -3,7 +3,7 @@ from __future__ import annotations
 
 import torch
 
-from .context import as_device_f32
+from .context import as_device_values
 from .exceptions import SketchMLException
 from .quantization import Quantizer, QuantizationType
 
@@ -20,13 +20,13 @@ class DenseVectorCompressor:
         self.quantizer = None
 
     def compressDense(self, values) -> None:
-        x = as_device_f32(values)
+        x = as_device_values(values)
         self._size = x.numel()
         self.quantizer = Quantizer.newQuantizer(self.quantType, self.quantBinNum, self.seed)
         self.quantizer.quantize(x)
 
     def parallelCompressDense(self, values) -> None:
-        x = as_device_f32(values)
+        x = as_device_values(values)
         self._size = x.numel()
         self.quantizer = Quantizer.newQuantizer(self.quantType, self.quantBinNum, self.seed)
         self.quantizer.parallelQuantize(x)

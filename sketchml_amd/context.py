@@ -64,6 +64,29 @@ def alloc_aligned(nbytes: int, device, align: int = 256) -> torch.Tensor:
     return buf[off: off + nbytes]
 
 
+def as_device_values(values, device=None) -> torch.Tensor:
+    """Device-resident contiguous, 16-byte aligned view of a gradient: float64 input (a torch
+    float64 tensor or a numpy float64 array, the reference's double[]) stays fp64; everything
+    else becomes fp32."""
+    if isinstance(values, torch.Tensor):
+        wide = values.dtype == torch.float64
+    else:
+        import numpy as np
+        wide = np.asarray(values).dtype == np.float64
+    if not wide:
+        return as_device_f32(values, device)
+    if isinstance(values, torch.Tensor):
+        t = values if values.is_cuda else values.to(device or torch.cuda.current_device())
+    else:
+        import numpy as np
+        t = torch.from_numpy(np.ascontiguousarray(values, dtype=np.float64)).to(
+            device or torch.cuda.current_device())
+    t = t.contiguous().view(-1)
+    if t.data_ptr() % 16:
+        t = t.clone()
+    return t
+
+
 def as_device_f32(values, device=None) -> torch.Tensor:
     """Device-resident contiguous, 16-byte aligned fp32 view (copies host arrays to the GPU)."""
     if isinstance(values, torch.Tensor):

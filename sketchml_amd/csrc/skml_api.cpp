@@ -51,6 +51,9 @@ struct skml_ctx {
     // dense workspace (grow-only)
     void* ws = nullptr;
     size_t ws_cap = 0;
+    // fp64 sketch workspace (grow-only)
+    void* ws64 = nullptr;
+    size_t ws64_cap = 0;
     // rank table cache for (n, bin_num): HeapQuantileSketch.getQuantiles' curFrac ranks
     int64_t* ranks = nullptr;
     size_t ranks_cap = 0;
@@ -111,6 +114,8 @@ struct Workspace {
     float* upB;
     double* raw;
     QuantLut* lut;  // quantize bucket LUT, written by the summary / set-splits kernel
+    UniPartial* uni;  // uniform quantizer partials
+    int* qflags;      // fp64 quantize flags (bit 0: literal Quantizer.indexOf)
 };
 
 size_t ws_layout(int64_t chunks, Workspace* w, char* base) {
@@ -132,6 +137,8 @@ size_t ws_layout(int64_t chunks, Workspace* w, char* base) {
     t.upB = (float*)take(sizeof(float) * kK * (size_t)up);
     t.raw = (double*)take(sizeof(double) * SKML_MAX_BINS);
     t.lut = (QuantLut*)take(sizeof(QuantLut));
+    t.uni = (UniPartial*)take(sizeof(UniPartial) * kUniMaxParts);
+    t.qflags = (int*)take(sizeof(int) * 4);
     if (w) *w = t;
     return off;
 }
@@ -147,6 +154,48 @@ int ensure_ws(skml_ctx* ctx, int64_t chunks, Workspace* w) {
         ctx->ws_cap = cap;
     }
     ws_layout(chunks, w, (char*)ctx->ws);
+    return SKML_OK;
+}
+
+struct Workspace64 {
+    LeafPartial64* part;
+    double* nodes6;
+    double* roots;
+    double* upA;
+    double* upB;
+    double* raw;
+};
+
+size_t ws64_layout(int64_t chunks, Workspace64* w, char* base) {
+    const int64_t tiles = (chunks + kLeafChunks - 1) / kLeafChunks;
+    const int64_t up = (tiles >> 3) + 8;
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        size_t o = off;
+        off = align_up(off + bytes, 256);
+        return base ? (void*)(base + o) : nullptr;
+    };
+    Workspace64 t;
+    t.part = (LeafPartial64*)take(sizeof(LeafPartial64) * (size_t)(tiles + 1));
+    t.nodes6 = (double*)take(sizeof(double) * kK * (size_t)(tiles + 1));
+    t.roots = (double*)take(sizeof(double) * kK * kMaxLevels);
+    t.upA = (double*)take(sizeof(double) * kK * (size_t)up);
+    t.upB = (double*)take(sizeof(double) * kK * (size_t)up);
+    t.raw = (double*)take(sizeof(double) * SKML_MAX_BINS);
+    if (w) *w = t;
+    return off;
+}
+
+int ensure_ws64(skml_ctx* ctx, int64_t chunks, Workspace64* w) {
+    const size_t need = ws64_layout(chunks, nullptr, nullptr);
+    if (need > ctx->ws64_cap) {
+        if (ctx->ws64) HIP_TRY(hipFree(ctx->ws64));
+        ctx->ws64 = nullptr;
+        size_t cap = need + need / 4;
+        HIP_TRY(hipMalloc(&ctx->ws64, cap));
+        ctx->ws64_cap = cap;
+    }
+    ws64_layout(chunks, w, (char*)ctx->ws64);
     return SKML_OK;
 }
 
@@ -276,6 +325,7 @@ int skml_ctx_destroy(skml_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->jump_tab) (void)hipFree(c->jump_tab);
     if (c->ws) (void)hipFree(c->ws);
+    if (c->ws64) (void)hipFree(c->ws64);
     if (c->ranks) (void)hipFree(c->ranks);
     if (c->stage) (void)hipFree(c->stage);
     for (int k = 0; k < SKML_K_COUNT; k++)
@@ -367,7 +417,7 @@ size_t skml_dense_payload_bytes(int64_t n, int32_t bin_num) {
     return dense_codes_offset(bin_num) + align_up(rounded * (size_t)code_bits_for(bin_num) / 8, 256);
 }
 
-static int check_dense_args(skml_ctx* c, const float* x, int64_t n, int bins, const void* payload,
+static int check_dense_args(skml_ctx* c, const void* x, int64_t n, int bins, const void* payload,
                             size_t cap) {
     if (!c) return fail(SKML_E_ARG, "ctx is NULL");
     if (n < 0 || n > 0x7FFFFFFFLL) return fail(SKML_E_ARG, "n=%lld outside Java int range", (long long)n);
@@ -488,6 +538,115 @@ int skml_dense_encode_with_splits_f32(skml_ctx* c, const float* x, int64_t n, co
                               w.lut));
     HIP_TRY(launch_quantize(c->stream, x, n, payload, w.lut, nsplits + 1));
     HIP_TRY(hipStreamSynchronize(c->stream));  // the staged splits are reused by later calls
+    return SKML_OK;
+}
+
+int skml_dense_encode_f64(skml_ctx* c, const double* x, int64_t n, const skml_params* p, void* payload,
+                          size_t cap) {
+    skml_params def;
+    if (!p) {
+        skml_params_default(&def);
+        p = &def;
+    }
+    int st = check_dense_args(c, x, n, p->bin_num, payload, cap);
+    if (st) return st;
+    HIP_TRY(hipSetDevice(c->device));
+    const int64_t chunks = n / kChunk;
+    Workspace64 w;
+    if ((st = ensure_ws64(c, chunks, &w))) return st;
+    if ((st = ensure_ranks(c, n, p->bin_num))) return st;
+    const uint64_t s0 = ((uint64_t)p->seed ^ kLcgMult) & kLcgMask;
+    const int64_t tiles = (chunks + kLeafChunks - 1) / kLeafChunks;
+    {
+        KernelTimer kt(c, SKML_K_LEAF);
+        HIP_TRY(launch_leaf64(c->stream, x, chunks, s0, c->jump_tab, w.part, w.nodes6, w.roots));
+    }
+    // trees of bits l > 6 of the chunk count: carry their level-6 nodes down to one root,
+    // up to 2^3 nodes per wave and pass
+    for (int l = kLeafTopLevel + 1; l < kMaxLevels; l++) {
+        if (!((chunks >> l) & 1)) continue;
+        KernelTimer kt(c, SKML_K_MERGE);
+        const int64_t chunk_base = (chunks >> (l + 1)) << (l + 1);
+        const double* src = w.nodes6 + (size_t)(chunk_base >> kLeafTopLevel) * kK;
+        int64_t count = (int64_t)1 << (l - kLeafTopLevel);
+        int level = kLeafTopLevel;
+        double* dst = w.upA;
+        while (count > 1) {
+            int g = 0;
+            while (g < 3 && ((int64_t)1 << (g + 1)) <= count) g++;
+            const int64_t groups = count >> g;
+            double* out = groups == 1 ? w.roots + (size_t)l * kK : dst;
+            HIP_TRY(launch_tree64(c->stream, src, out, groups, g, level, chunk_base, s0, c->jump_tab));
+            src = out;
+            dst = (dst == w.upA) ? w.upB : w.upA;
+            count = groups;
+            level += g;
+        }
+    }
+    {
+        KernelTimer kt(c, SKML_K_SUMMARY);
+        HIP_TRY(launch_summary64(c->stream, x, n, w.part, tiles, w.roots, c->ranks, p->bin_num,
+                                 p->dedup ? 1 : 0, payload, w.raw));
+    }
+    {
+        KernelTimer kt(c, SKML_K_QUANTIZE);
+        HIP_TRY(launch_quantize64(c->stream, x, n, payload, nullptr));
+    }
+    return SKML_OK;
+}
+
+int skml_dense_encode_uniform_f32(skml_ctx* c, const float* x, int64_t n, const skml_params* p, void* payload,
+                                  size_t cap) {
+    skml_params def;
+    if (!p) {
+        skml_params_default(&def);
+        p = &def;
+    }
+    int st = check_dense_args(c, x, n, p->bin_num, payload, cap);
+    if (st) return st;
+    HIP_TRY(hipSetDevice(c->device));
+    Workspace w;
+    if ((st = ensure_ws(c, 0, &w))) return st;
+    {
+        KernelTimer kt(c, SKML_K_SUMMARY);
+        HIP_TRY(launch_uniform(c->stream, x, n, p->bin_num, w.uni, payload, w.lut, w.qflags));
+    }
+    {
+        KernelTimer kt(c, SKML_K_QUANTIZE);
+        HIP_TRY(launch_quantize(c->stream, x, n, payload, w.lut, p->bin_num));
+    }
+    return SKML_OK;
+}
+
+int skml_dense_encode_uniform_f64(skml_ctx* c, const double* x, int64_t n, const skml_params* p, void* payload,
+                                  size_t cap) {
+    skml_params def;
+    if (!p) {
+        skml_params_default(&def);
+        p = &def;
+    }
+    int st = check_dense_args(c, x, n, p->bin_num, payload, cap);
+    if (st) return st;
+    HIP_TRY(hipSetDevice(c->device));
+    Workspace w;
+    if ((st = ensure_ws(c, 0, &w))) return st;
+    {
+        KernelTimer kt(c, SKML_K_SUMMARY);
+        HIP_TRY(launch_uniform64(c->stream, x, n, p->bin_num, w.uni, payload, w.lut, w.qflags));
+    }
+    {
+        KernelTimer kt(c, SKML_K_QUANTIZE);
+        HIP_TRY(launch_quantize64(c->stream, x, n, payload, w.qflags));
+    }
+    return SKML_OK;
+}
+
+int skml_dense_decode_f64(skml_ctx* c, const void* payload, double* out, int64_t n) {
+    if (!c || !valid_payload_ptr(payload) || (n > 0 && (!out || ((uintptr_t)out) % 16)))
+        return fail(SKML_E_ARG, "bad decode arguments");
+    HIP_TRY(hipSetDevice(c->device));
+    KernelTimer kt(c, SKML_K_DECODE);
+    HIP_TRY(launch_decode64(c->stream, payload, out, n));
     return SKML_OK;
 }
 

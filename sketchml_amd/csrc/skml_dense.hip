@@ -47,13 +47,13 @@ __device__ __forceinline__ void store_codes4(uint8_t* codes, int64_t e0, uint32_
 //   kModeGlobal  binary search over the payload's double splits (> 4095 splits)
 // All compare the float value against splits rounded toward +inf, which is exact (see
 // build_quant_lut); NaN values take Quantizer.indexOf's NaN bin.
-constexpr int kModeEytz = 8, kModeGlobal = 9;
+constexpr int kModeEytz = 8, kModeGlobal = 9, kModeJava = 10;
 
 struct QuantTables {
     const uint16_t* base;  // LDS bucket bases
     const float* S;        // LDS splits (+NaN padding), or Eytzinger array
-    const double* sp;      // payload splits (global mode)
-    int nsplit, levels;
+    const double* sp;      // payload splits (global / Java mode)
+    int nsplit, levels, zero;
     uint32_t P, nan_bin;
 };
 
@@ -64,6 +64,8 @@ __device__ __forceinline__ uint32_t quant_bin(const QuantTables& q, float xv) {
         bin = q.base[f2key(__float_as_uint(xv)) >> (32 - kLutBits)];
 #pragma unroll
         for (int h = (1 << MODE) >> 1; h > 0; h >>= 1) bin += q.S[bin + h - 1] <= xv ? (uint32_t)h : 0u;
+    } else if constexpr (MODE == kModeJava) {
+        return java_index_of(q.sp, q.nsplit + 1, q.zero, (double)xv);
     } else if constexpr (MODE == kModeEytz) {
         uint32_t i = 1;
         for (int s = 0; s < q.levels; s++) i = 2 * i + (q.S[i] <= xv ? 1u : 0u);
@@ -137,6 +139,7 @@ __global__ __launch_bounds__(kQThreads) void k_quantize(const float* __restrict_
     q.sp = sp;
     q.nsplit = nsplit;
     q.nan_bin = (uint32_t)nan_bin_for(bins, hdr->zero_idx);
+    q.zero = hdr->zero_idx;
     q.P = 1;
     q.levels = 0;
     while (q.P < (uint32_t)bins) {
@@ -145,7 +148,9 @@ __global__ __launch_bounds__(kQThreads) void k_quantize(const float* __restrict_
     }
     const int cmax = lut ? lut->cmax : -1;
     int mode;
-    if (cmax >= 0 && nsplit + kLutPad <= lds_splits) {
+    if (cmax == kLutJavaMode) {
+        mode = kModeJava;
+    } else if (cmax >= 0 && nsplit + kLutPad <= lds_splits) {
         mode = cmax == 0 ? 0 : 32 - __clz((uint32_t)cmax);  // bisection steps: ceil(log2(cmax+1))
         uint16_t* base = reinterpret_cast<uint16_t*>(qsm);
         float* S = reinterpret_cast<float*>(qsm + sizeof(lut->base));
@@ -176,6 +181,7 @@ __global__ __launch_bounds__(kQThreads) void k_quantize(const float* __restrict_
         case 3: quant_tiles<3>(q, x, n, codes, bits); break;
         case 4: quant_tiles<4>(q, x, n, codes, bits); break;
         case kModeEytz: quant_tiles<kModeEytz>(q, x, n, codes, bits); break;
+        case kModeJava: quant_tiles<kModeJava>(q, x, n, codes, bits); break;
         default: quant_tiles<kModeGlobal>(q, x, n, codes, bits); break;
     }
 }

@@ -386,6 +386,30 @@ __device__ __forceinline__ void build_quant_lut(const float* sp, int nsplit, Qua
     if (t == 0) lut->cmax = (s_misc[1] <= kLutMaxNeed && nsplit <= kLutMaxSplits) ? s_misc[1] : -1;
 }
 
+// ------------------------------------------------------------------------------------------
+// Quantizer.indexOf (Quantizer.java:49-72), literally: used for split tables on which it is not
+// an upper bound (NaN or descending splits of a degenerate uniform range) and for NaN values.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t java_index_of(const double* s, int bin_num, int zero_idx, double x) {
+    const int last = bin_num - 2;
+    if (x < s[0]) return 0;
+    if (x >= s[last]) return (uint32_t)(bin_num - 1);
+    int l = zero_idx, r = zero_idx;
+    if (x < 0.0) l = 0;
+    else r = last;
+    while (l + 1 < r) {
+        const int mid = (l + r) >> 1;
+        if (s[mid] > x) {
+            if (mid == 0 || s[mid - 1] <= x) return (uint32_t)mid;
+            r = mid;
+        } else {
+            l = mid;
+        }
+    }
+    const int mid = (l + r) >> 1;
+    return s[mid] <= x ? (uint32_t)(mid + 1) : (uint32_t)mid;
+}
+
 // Quantizer.indexOf (Quantizer.java:49-92) on a NaN value: the probe never succeeds, so the
 // search runs from zeroIdx up to the last split and returns its final midpoint.
 __host__ __device__ inline int nan_bin_for(int bin_num, int zero_idx) {

@@ -1,0 +1,884 @@
+// skml_f64.hip -- CDNA4 (gfx950) kernels for double-precision input and the uniform quantizer.
+//
+// The reference codec takes double[] (QuantileQuantizer.quantize(double[]),
+// DenseVectorCompressor.compressDense(double[])).  This file builds the
+// same k=128 sketch over fp64 values:
+//
+//   k_leaf64      one wave per 64-chunk tile: each 256-value chunk is bitonic-sorted by its
+//                 64-bit total-order key (Arrays.sort order, HeapQuantileSketch.java:110) across
+//                 64 lanes x 4 registers, compacted by its RNG bit (QSketchUtils.java:45-51),
+//                 then carried through a register stack of levels 0..5 exactly like
+//                 inPlacePropagationUpdate (HeapQuantileSketch.java:116-124).  Every merge is
+//                 the exact count-based merge with the reference tie rule (IEEE `<`, ties emit
+//                 the newer run, QSketchUtils.java:53-69), so +-0.0 need no special path.
+//   k_tree64      the same carry stack over level-L nodes for the trees above level 6.
+//   k_summary64   makeSummary + getQuantiles + Maths.unique + findZeroIdx + header
+//                 (HeapQuantileSketch.java:126-174,293-323; Maths.java:51-67; Quantizer.java:74-85).
+//   k_quantize64  Quantizer.indexOf over an LDS split table (double compares), packed codes.
+//   k_decode64    getValues()[bin] in double (DenseVectorCompressor.decompressDense).
+//
+// Uniform quantizer (quantization/UniformQuantizer.java:21-45), fp32 and fp64 input:
+//   k_uni_minmax  per-workgroup IEEE min / max (NaN skipped) and the first zero's index
+//   k_uni_finish  Java min / max (MAX_VALUE / MIN_VALUE initialised, the first zero wins the
+//                 min), splits by repeated `+= step`, findZeroIdx, header, quantize LUT.
+#include "skml_device.hpp"
+
+namespace skml {
+
+__device__ __forceinline__ uint64_t d2key(uint64_t b) {
+    return b ^ ((uint64_t)((int64_t)b >> 63) | 0x8000000000000000ull);
+}
+__device__ __forceinline__ uint64_t key2d(uint64_t k) {
+    return k ^ ((k >> 63) ? 0x8000000000000000ull : ~0ull);
+}
+__device__ __forceinline__ double kd(uint64_t k) { return __longlong_as_double((long long)key2d(k)); }
+__device__ __forceinline__ uint64_t dk(double d) { return d2key((uint64_t)__double_as_longlong(d)); }
+__device__ __forceinline__ bool is_nan64(uint64_t b) {
+    return (b & 0x7FFFFFFFFFFFFFFFull) > 0x7FF0000000000000ull;
+}
+
+template <int M>
+__device__ __forceinline__ uint64_t lane_xor64(uint64_t v) {
+    const uint32_t lo = lane_xor<M>((uint32_t)v), hi = lane_xor<M>((uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Bitonic sort of one 256-key chunk: position p = 4 * lane + r, ascending.
+// ---------------------------------------------------------------------------------------------
+template <int K, int J>
+__device__ __forceinline__ void bitonic_stage64(uint64_t (&v)[4], int lane) {
+    if constexpr (J >= 4) {
+        constexpr int M = J / 4;
+        const bool asc = ((4 * lane) & K) == 0;
+        const bool lower = (lane & M) == 0;
+        const bool keep_min = asc == lower;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const uint64_t o = lane_xor64<M>(v[r]);
+            const uint64_t lo = v[r] < o ? v[r] : o, hi = v[r] < o ? o : v[r];
+            v[r] = keep_min ? lo : hi;
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            if (r & J) continue;
+            const bool asc = ((4 * lane + r) & K) == 0;
+            const uint64_t a = v[r], b = v[r + J];
+            const uint64_t lo = a < b ? a : b, hi = a < b ? b : a;
+            v[r] = asc ? lo : hi;
+            v[r + J] = asc ? hi : lo;
+        }
+    }
+}
+
+template <int K, int J>
+__device__ __forceinline__ void bitonic_merge_down64(uint64_t (&v)[4], int lane) {
+    if constexpr (J >= 1) {
+        bitonic_stage64<K, J>(v, lane);
+        bitonic_merge_down64<K, J / 2>(v, lane);
+    }
+}
+template <int K>
+__device__ __forceinline__ void bitonic_sort_from64(uint64_t (&v)[4], int lane) {
+    if constexpr (K <= 256) {
+        bitonic_merge_down64<K, K / 2>(v, lane);
+        bitonic_sort_from64<2 * K>(v, lane);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Exact merge + compaction of two register nodes (2 keys per lane, positions 2*lane + r).
+// `buf`: 384 doubles of wave-private LDS.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int count_le64(const double* run, double x) {  // #{run[i] <= x}
+    int lo = 0;
+#pragma unroll
+    for (int step = 64; step >= 1; step >>= 1)
+        if (run[lo + step - 1] <= x) lo += step;
+    return lo + ((lo == 127 && run[127] <= x) ? 1 : 0);
+}
+__device__ __forceinline__ int count_lt64(const double* run, double x) {  // #{run[i] < x}
+    int lo = 0;
+#pragma unroll
+    for (int step = 64; step >= 1; step >>= 1)
+        if (run[lo + step - 1] < x) lo += step;
+    return lo + ((lo == 127 && run[127] < x) ? 1 : 0);
+}
+
+__device__ __forceinline__ void node_merge64(const uint64_t (&A)[2], const uint64_t (&B)[2],
+                                             uint64_t (&out)[2], int lane, uint32_t odd, double* buf) {
+    double* a = buf;
+    double* b = buf + kK;
+    double* o = buf + 2 * kK;
+    a[2 * lane] = kd(A[0]);
+    a[2 * lane + 1] = kd(A[1]);
+    b[2 * lane] = kd(B[0]);
+    b[2 * lane + 1] = kd(B[1]);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int t = lane + 64 * q;
+        double v;
+        int pos;
+        if (t < kK) {  // older run: newer elements equal to it go first
+            v = a[t];
+            pos = t + count_le64(b, v);
+        } else {
+            v = b[t - kK];
+            pos = (t - kK) + count_lt64(a, v);
+        }
+        if (((uint32_t)pos & 1u) == odd) o[pos >> 1] = v;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    out[0] = dk(o[2 * lane]);
+    out[1] = dk(o[2 * lane + 1]);
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ void store_node64(const uint64_t (&w)[2], int lane, double* dst) {
+    reinterpret_cast<double2*>(dst)[lane] = make_double2(kd(w[0]), kd(w[1]));
+}
+
+// Register carry stack of levels 0..5 (two keys per lane each); indices are static.
+struct Stack64 {
+    uint64_t s[6][2];
+    __device__ __forceinline__ void get(int level, uint64_t (&o)[2]) const {
+#pragma unroll
+        for (int l = 0; l < 6; l++)
+            if (l == level) {
+                o[0] = s[l][0];
+                o[1] = s[l][1];
+            }
+    }
+    __device__ __forceinline__ void put(int level, const uint64_t (&v)[2]) {
+#pragma unroll
+        for (int l = 0; l < 6; l++)
+            if (l == level) {
+                s[l][0] = v[0];
+                s[l][1] = v[1];
+            }
+    }
+};
+
+// ---------------------------------------------------------------------------------------------
+// Leaf: one wave per 64-chunk tile (a level-6 node), chunks in order.
+// ---------------------------------------------------------------------------------------------
+constexpr int kLeaf64Waves = 4;
+
+__global__ __launch_bounds__(256) void k_leaf64(const double* __restrict__ x, int64_t chunks, uint64_t s0,
+                                                const uint64_t* __restrict__ tab,
+                                                LeafPartial64* __restrict__ part, double* __restrict__ nodes6,
+                                                double* __restrict__ roots) {
+    __shared__ double lds[kLeaf64Waves][3 * kK];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t tile = (int64_t)blockIdx.x * kLeaf64Waves + wave;
+    const int64_t c_tile = tile * kLeafChunks;
+    if (c_tile >= chunks) return;  // wave-uniform; no block barriers in this kernel
+    const int rem = (int)min<int64_t>(kLeafChunks, chunks - c_tile);
+    double* buf = lds[wave];
+    uint64_t mn = ~0ull, mx = 0ull;
+    uint32_t nanf = 0;
+    Stack64 st;
+    uint32_t occ = 0;
+    uint64_t top[2] = {0, 0};
+#pragma unroll 1
+    for (int c = 0; c < rem; c++) {
+        const int64_t chunk = c_tile + c;
+        const double2* src = reinterpret_cast<const double2*>(x + chunk * kChunk);
+        const double2 p0 = src[2 * lane], p1 = src[2 * lane + 1];
+        uint64_t v[4] = {(uint64_t)__double_as_longlong(p0.x), (uint64_t)__double_as_longlong(p0.y),
+                         (uint64_t)__double_as_longlong(p1.x), (uint64_t)__double_as_longlong(p1.y)};
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            nanf |= is_nan64(v[r]) ? 1u : 0u;
+            v[r] = d2key(v[r]);
+            mn = v[r] < mn ? v[r] : mn;
+            mx = v[r] > mx ? v[r] : mx;
+        }
+        bitonic_sort_from64<2>(v, lane);
+        const uint32_t odd0 = lcg_bit(tab, s0, node_bit_index((uint64_t)chunk, 0));
+        uint64_t nd[2] = {odd0 ? v[1] : v[0], odd0 ? v[3] : v[2]};
+        int level = 0;
+        while ((occ >> level) & 1u) {
+            uint64_t older[2];
+            st.get(level, older);
+            const uint32_t odd = lcg_bit(tab, s0, node_bit_index((uint64_t)chunk, level + 1));
+            node_merge64(older, nd, nd, lane, odd, buf);
+            occ &= ~(1u << level);
+            level++;
+        }
+        if (level == kLeafTopLevel) {
+            top[0] = nd[0];
+            top[1] = nd[1];
+        } else {
+            st.put(level, nd);
+            occ |= 1u << level;
+        }
+    }
+    if (rem == kLeafChunks) {
+        store_node64(top, lane, nodes6 + (size_t)tile * kK);
+        // the level-6 tree (bit 6 of the chunk count) is this single node
+        if (((chunks >> 6) & 1) && tile == ((chunks >> 7) << 1)) store_node64(top, lane, roots + (size_t)6 * kK);
+    } else {
+        // the partial tile's stack holds the roots of the trees of bits 0..5 of the chunk count
+#pragma unroll
+        for (int l = 0; l < 6; l++)
+            if ((occ >> l) & 1u) store_node64(st.s[l], lane, roots + (size_t)l * kK);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const uint64_t omn = __shfl_xor(mn, off, 64), omx = __shfl_xor(mx, off, 64);
+        mn = omn < mn ? omn : mn;
+        mx = omx > mx ? omx : mx;
+        nanf |= (uint32_t)__shfl_xor((int)nanf, off, 64);
+    }
+    if (lane == 0) {
+        LeafPartial64 p;
+        p.min_key = mn;
+        p.max_key = mx;
+        p.flags = nanf;
+        p.pad = 0;
+        part[tile] = p;
+    }
+}
+
+// Upper levels: each wave carries 2^g consecutive level-L nodes into one level-(L+g) node.
+// Node i of `src` covers chunks [chunk_base + i * 2^L, chunk_base + (i + 1) * 2^L).
+__global__ __launch_bounds__(256) void k_tree64(const double* __restrict__ src, double* __restrict__ dst,
+                                                int64_t groups, int g, int level_in, int64_t chunk_base,
+                                                uint64_t s0, const uint64_t* __restrict__ tab) {
+    __shared__ double lds[kLeaf64Waves][3 * kK];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t grp = (int64_t)blockIdx.x * kLeaf64Waves + wave;
+    if (grp >= groups) return;
+    double* buf = lds[wave];
+    Stack64 st;
+    uint32_t occ = 0;
+    uint64_t top[2] = {0, 0};
+    const int cnt = 1 << g;
+#pragma unroll 1
+    for (int i = 0; i < cnt; i++) {
+        const int64_t node = grp * cnt + i;
+        const double2 d = reinterpret_cast<const double2*>(src + (size_t)node * kK)[lane];
+        uint64_t nd[2] = {dk(d.x), dk(d.y)};
+        const uint64_t c_last = (uint64_t)chunk_base + ((uint64_t)(node + 1) << level_in) - 1;
+        int level = 0;
+        while ((occ >> level) & 1u) {
+            uint64_t older[2];
+            st.get(level, older);
+            const uint32_t odd = lcg_bit(tab, s0, node_bit_index(c_last, level_in + level + 1));
+            node_merge64(older, nd, nd, lane, odd, buf);
+            occ &= ~(1u << level);
+            level++;
+        }
+        if (level == g) {
+            top[0] = nd[0];
+            top[1] = nd[1];
+        } else {
+            st.put(level, nd);
+            occ |= 1u << level;
+        }
+    }
+    store_node64(top, lane, dst + (size_t)grp * kK);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Summary (one workgroup of 512 threads, dynamic LDS).
+// ---------------------------------------------------------------------------------------------
+constexpr int kMaxSamples64 = kMaxLevels * kK + kChunk;
+constexpr int kSum64Raw = 1024;
+struct Summary64Shared {
+    double smp[kMaxSamples64];
+    double sorted[kMaxSamples64];
+    int64_t w[kMaxSamples64 + 1];
+    double raw[kSum64Raw];
+    int64_t wsum[16];
+    int run_off[kMaxLevels + 2];
+    int run_lvl[kMaxLevels + 2];
+    int nruns;
+    unsigned long long min_key, max_key;
+    uint32_t flags;
+    int zero;
+    int64_t total;
+};
+
+__device__ int64_t block_scan_excl64(int64_t v, int64_t* wsum, int64_t* total) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, nw = blockDim.x >> 6;
+    int64_t x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int64_t y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    if (w == 0) {
+        int64_t s = lane < nw ? wsum[lane] : 0;
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+            const int64_t y = __shfl_up(s, off, 64);
+            if (lane >= off) s += y;
+        }
+        if (lane < nw) wsum[lane] = s;
+    }
+    __syncthreads();
+    const int64_t base = w > 0 ? wsum[w - 1] : 0;
+    *total = wsum[nw - 1];
+    __syncthreads();
+    return base + x - v;
+}
+
+__device__ __forceinline__ int run_count_le64(const double* r, int len, double x) {
+    int lo = 0, hi = len;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (r[mid] <= x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+__device__ __forceinline__ int run_count_lt64(const double* r, int len, double x) {
+    int lo = 0, hi = len;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (r[mid] < x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__device__ void write_header(skml_dense_header* hdr, int status, int64_t n, int bin_num, int zero,
+                             int req_bins, double vmin, double vmax) {
+    hdr->magic = SKML_DENSE_MAGIC;
+    hdr->status = status;
+    hdr->n = n;
+    hdr->bin_num = bin_num;
+    hdr->zero_idx = zero;
+    hdr->code_bits = code_bits_for(bin_num);
+    hdr->req_bins = req_bins;
+    hdr->min = vmin;
+    hdr->max = vmax;
+    hdr->codes_offset = (int64_t)dense_codes_offset(req_bins);
+    hdr->reserved = 0;
+}
+
+__global__ __launch_bounds__(512) void k_summary64(const double* __restrict__ x, int64_t n,
+                                                   const LeafPartial64* __restrict__ part, int64_t nparts,
+                                                   const double* __restrict__ roots,
+                                                   const int64_t* __restrict__ ranks, int req_bins, int dedup,
+                                                   uint8_t* __restrict__ payload, double* __restrict__ g_raw) {
+    extern __shared__ __align__(16) uint8_t smem64[];
+    Summary64Shared& S = *reinterpret_cast<Summary64Shared*>(smem64);
+    const int t = threadIdx.x, T = blockDim.x;
+    skml_dense_header* hdr = reinterpret_cast<skml_dense_header*>(payload);
+    double* splits = reinterpret_cast<double*>(payload + kHeaderBytes);
+    const int64_t chunks = n / kChunk;
+    const int tail = (int)(n - chunks * kChunk);
+    const double* xt = x + chunks * kChunk;
+
+    if (t == 0) {
+        S.min_key = ~0ull;
+        S.max_key = 0ull;
+        S.flags = 0u;
+        S.zero = 0x7FFFFFFF;
+        int nr = 0, off = 0;
+        for (int l = 0; l < kMaxLevels; l++)
+            if ((chunks >> l) & 1) {  // copyBuf2Arr: lowest level first (HeapQuantileSketch.java:151-161)
+                S.run_off[nr] = off;
+                S.run_lvl[nr] = l;
+                nr++;
+                off += kK;
+            }
+        S.run_off[nr] = off;  // tail = base buffer (weight 1)
+        S.run_lvl[nr] = -1;
+        S.run_off[nr + 1] = off + tail;
+        S.nruns = nr + 1;
+    }
+    __syncthreads();
+    {
+        uint64_t mn = ~0ull, mx = 0ull;
+        uint32_t fl = 0u;
+        for (int64_t i = t; i < nparts; i += T) {
+            const LeafPartial64 p = part[i];
+            mn = p.min_key < mn ? p.min_key : mn;
+            mx = p.max_key > mx ? p.max_key : mx;
+            fl |= p.flags;
+        }
+        for (int i = t; i < tail; i += T) {
+            const uint64_t b = (uint64_t)__double_as_longlong(xt[i]);
+            fl |= is_nan64(b) ? 1u : 0u;
+            const uint64_t k = d2key(b);
+            mn = k < mn ? k : mn;
+            mx = k > mx ? k : mx;
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const uint64_t omn = __shfl_xor(mn, off, 64), omx = __shfl_xor(mx, off, 64);
+            mn = omn < mn ? omn : mn;
+            mx = omx > mx ? omx : mx;
+            fl |= (uint32_t)__shfl_xor((int)fl, off, 64);
+        }
+        if ((t & 63) == 0) {
+            atomicMin(&S.min_key, (unsigned long long)mn);
+            atomicMax(&S.max_key, (unsigned long long)mx);
+            if (fl) atomicOr(&S.flags, fl);
+        }
+    }
+    const int nruns = S.nruns;
+    const int ns = S.run_off[nruns];
+    for (int idx = t; idx < (nruns - 1) * kK; idx += T) {
+        const int r = idx / kK, i = idx % kK;
+        S.smp[S.run_off[r] + i] = roots[(size_t)S.run_lvl[r] * kK + i];
+    }
+    for (int i = t; i < tail; i += T) S.sorted[i] = xt[i];
+    __syncthreads();
+    {  // the base buffer, sorted in Arrays.sort total order by rank counting (ties by position)
+        const int toff = S.run_off[nruns - 1];
+        for (int i = t; i < tail; i += T) {
+            const double xi = S.sorted[i];
+            const uint64_t ki = dk(xi);
+            int rank = 0;
+            for (int j = 0; j < tail; j++) {
+                const uint64_t kj = dk(S.sorted[j]);
+                rank += (kj < ki) || (kj == ki && j < i);
+            }
+            S.smp[toff + rank] = xi;
+        }
+    }
+    __syncthreads();
+
+    double vmin = 1.7976931348623157e308, vmax = 4.9e-324;  // HeapQuantileSketch.java:67-68
+    if (n > 0) {
+        const double fmin = kd(S.min_key), fmax = kd(S.max_key);
+        if (fmin <= vmin) vmin = fmin;  // Math.min(Double.MAX_VALUE, x)
+        if (fmax > vmax) vmax = fmax;   // Math.max(Double.MIN_VALUE, x)
+    }
+    if (S.flags & 1u) {  // NaN: QuantileSketchException("Encounter NaN value")
+        if (t == 0) write_header(hdr, SKML_E_NAN, n, req_bins, 0, req_bins, vmin, vmax);
+        return;
+    }
+    // blockyMergeSort == stable sort under IEEE `<=` (left run wins ties): rank across runs
+    for (int i = t; i < ns; i += T) {
+        int r = 0;
+        while (S.run_off[r + 1] <= i) r++;
+        const double v = S.smp[i];
+        int rank = i - S.run_off[r];
+        for (int q = 0; q < nruns; q++) {
+            if (q == r) continue;
+            const double* run = S.smp + S.run_off[q];
+            const int len = S.run_off[q + 1] - S.run_off[q];
+            rank += q < r ? run_count_le64(run, len, v) : run_count_lt64(run, len, v);
+        }
+        S.sorted[rank] = v;
+        S.w[rank] = S.run_lvl[r] < 0 ? 1 : ((int64_t)2 << S.run_lvl[r]);
+    }
+    __syncthreads();
+    {  // exclusive prefix of weights (HeapQuantileSketch.java:137-142)
+        const int per = (ns + T - 1) / T;
+        const int b0 = min(ns, t * per), b1 = min(ns, b0 + per);
+        int64_t loc = 0;
+        for (int i = b0; i < b1; i++) loc += S.w[i];
+        const int64_t base = block_scan_excl64(loc, S.wsum, &S.total);
+        int64_t acc = base;
+        for (int i = b0; i < b1; i++) {
+            const int64_t wv = S.w[i];
+            S.w[i] = acc;
+            acc += wv;
+        }
+        if (t == 0) S.w[ns] = S.total;
+    }
+    __syncthreads();
+    const int nsplit_req = req_bins - 1;
+    const bool lds_raw = nsplit_req <= kSum64Raw;
+    double* raw = lds_raw ? S.raw : g_raw;
+    for (int i = t; i < nsplit_req; i += T) {  // getQuantiles(int)
+        double sp;
+        if (ns == 0) {
+            sp = __longlong_as_double(0x7FF8000000000000LL);  // NaN (HeapQuantileSketch.java:299-301)
+        } else {
+            const int64_t rank = ranks[i];
+            int lo = 0, hi = ns;
+            while (lo + 1 < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (S.w[mid] <= rank) lo = mid;
+                else hi = mid;
+            }
+            sp = S.sorted[lo];
+        }
+        raw[i] = sp;
+    }
+    if (!lds_raw) __threadfence();
+    __syncthreads();
+    int bin_num;
+    {  // Maths.unique (IEEE !=, keep first) + findZeroIdx
+        const int per = (nsplit_req + T - 1) / T;
+        const int b0 = min(nsplit_req, t * per), b1 = min(nsplit_req, b0 + per);
+        int64_t loc = 0;
+        for (int i = b0; i < b1; i++) loc += (!dedup || i == 0 || raw[i] != raw[i - 1]) ? 1 : 0;
+        const int64_t base = block_scan_excl64(loc, S.wsum, &S.total);
+        int64_t o = base;
+        int zmin = 0x7FFFFFFF;
+        for (int i = b0; i < b1; i++) {
+            if (!dedup || i == 0 || raw[i] != raw[i - 1]) {
+                const double sp = raw[i];
+                splits[o] = sp;
+                if (!(sp < 0.0)) zmin = min(zmin, (int)o);
+                o++;
+            }
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) zmin = min(zmin, __shfl_xor(zmin, off, 64));
+        if ((t & 63) == 0 && zmin != 0x7FFFFFFF) atomicMin(&S.zero, zmin);
+        bin_num = (int)S.total + 1;
+    }
+    __syncthreads();
+    if (t == 0) {
+        int zero;
+        if (vmin > 0.0) zero = 0;
+        else if (vmax < 0.0) zero = bin_num - 1;
+        else zero = S.zero < bin_num - 1 ? S.zero : bin_num - 1;
+        write_header(hdr, SKML_OK, n, bin_num, zero, req_bins, vmin, vmax);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Quantize (fp64 input): Eytzinger upper_bound over the LDS split table in double.
+// `flags` bit 0: literal Java indexOf (degenerate split table).
+// ---------------------------------------------------------------------------------------------
+constexpr int kEytz64Max = 4096;
+
+__device__ __forceinline__ void pack_store4(uint8_t* codes, int64_t e0, const uint32_t (&c)[4], int bits,
+                                            int lane) {
+    switch (bits) {
+        case 8:
+            *reinterpret_cast<uint32_t*>(codes + e0) = c[0] | (c[1] << 8) | (c[2] << 16) | (c[3] << 24);
+            break;
+        case 16:
+            *reinterpret_cast<uint2*>(codes + e0 * 2) = make_uint2(c[0] | (c[1] << 16), c[2] | (c[3] << 16));
+            break;
+        case 4:
+            *reinterpret_cast<uint16_t*>(codes + e0 / 2) = (uint16_t)(c[0] | (c[1] << 4) | (c[2] << 8) | (c[3] << 12));
+            break;
+        case 2:
+            codes[e0 / 4] = (uint8_t)(c[0] | (c[1] << 2) | (c[2] << 4) | (c[3] << 6));
+            break;
+        default: {
+            const uint32_t nib = c[0] | (c[1] << 1) | (c[2] << 2) | (c[3] << 3);
+            const uint32_t other = lane_xor<1>(nib);
+            if ((lane & 1) == 0) codes[e0 / 8] = (uint8_t)(nib | (other << 4));
+            break;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_quantize64(const double* __restrict__ x, int64_t n,
+                                                    uint8_t* __restrict__ payload,
+                                                    const int* __restrict__ qflags) {
+    __shared__ double E[kEytz64Max];
+    const skml_dense_header* hdr = reinterpret_cast<const skml_dense_header*>(payload);
+    if (hdr->status != SKML_OK) return;
+    const int bins = hdr->bin_num, bits = hdr->code_bits, nsplit = bins - 1, zero = hdr->zero_idx;
+    const double* sp = reinterpret_cast<const double*>(payload + kHeaderBytes);
+    uint8_t* codes = payload + hdr->codes_offset;
+    const bool literal = qflags && (*qflags & 1);
+    uint32_t P = 1;
+    int levels = 0;
+    while (P < (uint32_t)bins) {
+        P <<= 1;
+        levels++;
+    }
+    const bool lds = !literal && P <= kEytz64Max;
+    if (lds) {
+        for (uint32_t i = threadIdx.x + 1; i < P; i += blockDim.x) {
+            const int d = 31 - __clz(i);
+            const uint32_t idx = ((2u * (i - (1u << d)) + 1u) << (levels - 1 - d)) - 1u;
+            E[i] = idx < (uint32_t)nsplit ? sp[idx] : __longlong_as_double(0x7FF0000000000000LL);  // +inf pad
+        }
+    }
+    __syncthreads();
+    const uint32_t nan_bin = (uint32_t)nan_bin_for(bins, zero);
+    auto bin_of = [&](double v) -> uint32_t {
+        if (literal) return java_index_of(sp, bins, zero, v);
+        if (v != v) return nan_bin;
+        if (lds) {
+            uint32_t i = 1;
+            for (int s = 0; s < levels; s++) i = 2 * i + (E[i] <= v ? 1u : 0u);
+            // +inf padding: v == +inf passes every pad; clamp to the split count
+            const uint32_t b = i - P;
+            return b > (uint32_t)nsplit ? (uint32_t)nsplit : b;
+        }
+        int lo = 0, hi = nsplit;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (sp[mid] <= v) lo = mid + 1;
+            else hi = mid;
+        }
+        return (uint32_t)lo;
+    };
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * 4, wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t full = n / 1024;
+    for (int64_t tile = wid; tile < full; tile += nw) {
+        const double2* src = reinterpret_cast<const double2*>(x + tile * 1024);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const double2 a = src[j * 128 + 2 * lane], b = src[j * 128 + 2 * lane + 1];
+            const uint32_t c[4] = {bin_of(a.x), bin_of(a.y), bin_of(b.x), bin_of(b.y)};
+            pack_store4(codes, tile * 1024 + j * 256 + lane * 4, c, bits, lane);
+        }
+    }
+    if (wid == full % nw && n % 1024) {
+        const int64_t base = full * 1024;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int64_t e0 = base + j * 256 + lane * 4;
+            uint32_t c[4] = {0, 0, 0, 0};
+            for (int e = 0; e < 4; e++)
+                if (e0 + e < n) c[e] = bin_of(x[e0 + e]);
+            if (bits == 1) {
+                const int64_t pair0 = base + j * 256 + (lane & ~1) * 4;
+                const uint32_t nib = c[0] | (c[1] << 1) | (c[2] << 2) | (c[3] << 3);
+                const uint32_t other = lane_xor<1>(nib);
+                if ((lane & 1) == 0 && pair0 < n) codes[pair0 / 8] = (uint8_t)(nib | (other << 4));
+            } else if (e0 < n) {
+                pack_store4(codes, e0, c, bits, lane);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Decode to double: getValues()[bin] (Quantizer.java:39-47), LUT in LDS.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ double lut_value64(const skml_dense_header* h, const double* sp, int b) {
+    const int ns = h->bin_num - 1;
+    if (b == 0) return 0.5 * (h->min + sp[0]);
+    if (b == ns) return 0.5 * (sp[ns - 1] + h->max);
+    return 0.5 * (sp[b - 1] + sp[b]);
+}
+
+__device__ __forceinline__ uint32_t code_at(const uint8_t* codes, int64_t e, int bits) {
+    switch (bits) {
+        case 8: return codes[e];
+        case 16: return reinterpret_cast<const uint16_t*>(codes)[e];
+        case 4: return (codes[e >> 1] >> ((e & 1) * 4)) & 15u;
+        case 2: return (codes[e >> 2] >> ((e & 3) * 2)) & 3u;
+        default: return (codes[e >> 3] >> (e & 7)) & 1u;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_decode64(const uint8_t* __restrict__ payload, double* __restrict__ out,
+                                                  int64_t n) {
+    __shared__ double lut[kEytz64Max];
+    const skml_dense_header* h = reinterpret_cast<const skml_dense_header*>(payload);
+    const double* sp = reinterpret_cast<const double*>(payload + kHeaderBytes);
+    const uint8_t* codes = payload + h->codes_offset;
+    const int bins = h->bin_num, bits = h->code_bits;
+    const bool lds = bins <= kEytz64Max;
+    if (lds)
+        for (int b = threadIdx.x; b < bins; b += blockDim.x) lut[b] = lut_value64(h, sp, b);
+    __syncthreads();
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 2; e0 < n; e0 += stride * 2) {
+        const uint32_t c0 = code_at(codes, e0, bits);
+        const double v0 = lds ? lut[c0] : lut_value64(h, sp, (int)c0);
+        if (e0 + 1 < n) {
+            const uint32_t c1 = code_at(codes, e0 + 1, bits);
+            const double v1 = lds ? lut[c1] : lut_value64(h, sp, (int)c1);
+            *reinterpret_cast<double2*>(out + e0) = make_double2(v0, v1);
+        } else {
+            out[e0] = v0;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Uniform quantizer: per-workgroup min / max / first zero, then one finishing workgroup.
+// ---------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void k_uni_minmax(const T* __restrict__ x, int64_t n, UniPartial* __restrict__ part) {
+    double mn = __longlong_as_double(0x7FF0000000000000LL), mx = -mn;  // +inf, -inf
+    int64_t z = INT64_MAX;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const double v = (double)x[i];
+        mn = v < mn ? v : mn;  // NaN never compares: skipped, as in `if (v < min)`
+        mx = v > mx ? v : mx;
+        if (v == 0.0 && i < z) z = i;
+    }
+    __shared__ double smn[4], smx[4];
+    __shared__ int64_t sz[4];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const double omn = __shfl_xor(mn, off, 64), omx = __shfl_xor(mx, off, 64);
+        const int64_t oz = __shfl_xor(z, off, 64);
+        mn = omn < mn ? omn : mn;
+        mx = omx > mx ? omx : mx;
+        z = oz < z ? oz : z;
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        smn[w] = mn;
+        smx[w] = mx;
+        sz[w] = z;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < (int)(blockDim.x >> 6); k++) {
+            mn = smn[k] < mn ? smn[k] : mn;
+            mx = smx[k] > mx ? smx[k] : mx;
+            z = sz[k] < z ? sz[k] : z;
+        }
+        part[blockIdx.x] = UniPartial{mn, mx, z, 0};
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_uni_finish(const T* __restrict__ x, int64_t n,
+                                                    const UniPartial* __restrict__ part, int nparts, int bin_num,
+                                                    uint8_t* __restrict__ payload, QuantLut* __restrict__ lut,
+                                                    int* __restrict__ qflags) {
+    skml_dense_header* hdr = reinterpret_cast<skml_dense_header*>(payload);
+    double* splits = reinterpret_cast<double*>(payload + kHeaderBytes);
+    __shared__ double s_mn, s_mx;
+    __shared__ int s_bad;
+    __shared__ int s_zero;
+    __shared__ int s_misc[20];
+    __shared__ float s_sp[kLutMaxSplits];
+    __shared__ __align__(16) uint32_t s_lbuf[kLutSize / 2];
+    if (threadIdx.x == 0) {
+        double mn = __longlong_as_double(0x7FF0000000000000LL), mx = -mn;
+        int64_t z = INT64_MAX;
+        for (int k = 0; k < nparts; k++) {
+            mn = part[k].mn < mn ? part[k].mn : mn;
+            mx = part[k].mx > mx ? part[k].mx : mx;
+            z = part[k].zidx < z ? part[k].zidx : z;
+        }
+        // UniformQuantizer.java:24-29: min from Double.MAX_VALUE by `<`, max from Double.MIN_VALUE
+        // by `>`; among equal minima the first wins, which only shows for a zero minimum
+        double jmin = 1.7976931348623157e308, jmax = 4.9e-324;
+        if (mn < jmin) jmin = (mn == 0.0) ? (double)x[z] : mn;
+        if (mx > jmax) jmax = mx;
+        s_mn = jmin;
+        s_mx = jmax;
+        // UniformQuantizer.java:31-36
+        const double step = (jmax - jmin) / bin_num;
+        const int ns = bin_num - 1;
+        double cur = jmin + step;
+        int bad = 0, zero = ns;
+        for (int i = 0; i < ns; i++) {
+            if (i > 0) cur = cur + step;
+            splits[i] = cur;
+            if (!(cur == cur)) bad = 1;
+            if (i > 0 && !(splits[i - 1] <= cur)) bad = 1;
+            if (zero == ns && !(cur < 0.0)) zero = i;
+        }
+        s_bad = bad;
+        s_zero = zero;
+        *qflags = bad;
+    }
+    __syncthreads();
+    const int ns = bin_num - 1;
+    const double jmin = s_mn, jmax = s_mx;
+    const bool lut_ok = !s_bad && ns <= kLutMaxSplits;
+    if (lut_ok) {
+        for (int i = threadIdx.x; i < ns; i += blockDim.x) s_sp[i] = __double2float_ru(splits[i]);
+        __syncthreads();
+        build_quant_lut(s_sp, ns, lut, s_misc, s_lbuf);
+    }
+    if (threadIdx.x == 0) {
+        if (s_bad) lut->cmax = kLutJavaMode;
+        else if (!lut_ok) lut->cmax = -1;
+        int zero;  // Quantizer.findZeroIdx (Quantizer.java:74-85)
+        if (jmin > 0.0) zero = 0;
+        else if (jmax < 0.0) zero = bin_num - 1;
+        else zero = s_zero;
+        write_header(hdr, SKML_OK, n, bin_num, zero, bin_num, jmin, jmax);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------------------------
+hipError_t launch_leaf64(hipStream_t st, const double* x, int64_t chunks, uint64_t s0, const uint64_t* tab,
+                         LeafPartial64* part, double* nodes6, double* roots) {
+    const int64_t tiles = (chunks + kLeafChunks - 1) / kLeafChunks;
+    if (tiles == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_leaf64, dim3((unsigned)((tiles + kLeaf64Waves - 1) / kLeaf64Waves)), dim3(256), 0, st,
+                       x, chunks, s0, tab, part, nodes6, roots);
+    return hipGetLastError();
+}
+
+hipError_t launch_tree64(hipStream_t st, const double* src, double* dst, int64_t groups, int g, int level_in,
+                         int64_t chunk_base, uint64_t s0, const uint64_t* tab) {
+    hipLaunchKernelGGL(k_tree64, dim3((unsigned)((groups + kLeaf64Waves - 1) / kLeaf64Waves)), dim3(256), 0, st,
+                       src, dst, groups, g, level_in, chunk_base, s0, tab);
+    return hipGetLastError();
+}
+
+hipError_t launch_summary64(hipStream_t st, const double* x, int64_t n, const LeafPartial64* part, int64_t nparts,
+                            const double* roots, const int64_t* ranks, int req_bins, int dedup, void* payload,
+                            double* g_raw) {
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_summary64),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)sizeof(Summary64Shared));
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_summary64, dim3(1), dim3(512), sizeof(Summary64Shared), st, x, n, part, nparts, roots,
+                       ranks, req_bins, dedup, reinterpret_cast<uint8_t*>(payload), g_raw);
+    return hipGetLastError();
+}
+
+static int grid_for(int64_t n, int per_wg, int cap) {
+    int64_t g = (n + per_wg - 1) / per_wg;
+    if (g > cap) g = cap;
+    if (g < 1) g = 1;
+    return (int)g;
+}
+
+hipError_t launch_quantize64(hipStream_t st, const double* x, int64_t n, void* payload, const int* qflags) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_quantize64, dim3(grid_for(n, 4096, 1024)), dim3(256), 0, st, x, n,
+                       reinterpret_cast<uint8_t*>(payload), qflags);
+    return hipGetLastError();
+}
+
+hipError_t launch_decode64(hipStream_t st, const void* payload, double* out, int64_t n) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_decode64, dim3(grid_for(n, 4096, 2048)), dim3(256), 0, st,
+                       reinterpret_cast<const uint8_t*>(payload), out, n);
+    return hipGetLastError();
+}
+
+int uniform_partials(int64_t n) { return grid_for(n, 1 << 16, kUniMaxParts); }
+
+template <typename T>
+static hipError_t launch_uniform_t(hipStream_t st, const T* x, int64_t n, int bin_num, UniPartial* part,
+                                   void* payload, QuantLut* lut, int* qflags) {
+    const int np = uniform_partials(n);
+    hipLaunchKernelGGL(k_uni_minmax<T>, dim3(np), dim3(256), 0, st, x, n, part);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_uni_finish<T>, dim3(1), dim3(256), 0, st, x, n, part, np, bin_num,
+                       reinterpret_cast<uint8_t*>(payload), lut, qflags);
+    return hipGetLastError();
+}
+
+hipError_t launch_uniform(hipStream_t st, const float* x, int64_t n, int bin_num, UniPartial* part, void* payload,
+                          QuantLut* lut, int* qflags) {
+    return launch_uniform_t<float>(st, x, n, bin_num, part, payload, lut, qflags);
+}
+hipError_t launch_uniform64(hipStream_t st, const double* x, int64_t n, int bin_num, UniPartial* part,
+                            void* payload, QuantLut* lut, int* qflags) {
+    return launch_uniform_t<double>(st, x, n, bin_num, part, payload, lut, qflags);
+}
+
+}  // namespace skml

@@ -30,9 +30,28 @@ constexpr int kLutMaxSplits = 4096;  // split table must fit the quantize kernel
 constexpr int kLutPad = 16;          // NaN padding after the last split (2^4 bisection reach)
 struct QuantLut {
     uint16_t base[kLutSize];
-    int32_t cmax;  // -1: LUT unusable (too many splits per bucket)
+    int32_t cmax;  // -1: LUT unusable (too many splits per bucket); kLutJavaMode: see below
     int32_t pad[15];
 };
+// cmax value asking the quantize pass for Quantizer.indexOf literally (a degenerate uniform split
+// table: NaN or descending splits, on which indexOf is not an upper bound).
+constexpr int32_t kLutJavaMode = -2;
+
+// fp64 leaf partials (one per 64-chunk tile): min / max total-order key, flags (bit0 NaN).
+struct LeafPartial64 {
+    uint64_t min_key;
+    uint64_t max_key;
+    uint32_t flags;
+    uint32_t pad;
+};
+// Uniform quantizer partials (one per workgroup): IEEE min / max of the non-NaN values and the
+// index of the first zero.
+struct UniPartial {
+    double mn, mx;
+    int64_t zidx;
+    int64_t pad;
+};
+constexpr int kUniMaxParts = 1024;
 
 // Per leaf workgroup partial results: min key, max key, flags (bit0 NaN, bit1 -0, bit2 +0).
 struct LeafPartial {
@@ -95,6 +114,21 @@ hipError_t launch_decode_sum(hipStream_t st, const void* payloads, int P, size_t
 hipError_t launch_bins(hipStream_t st, const void* payload, int32_t* bins, int64_t n);
 hipError_t launch_ref_body(hipStream_t st, const void* payload, uint8_t* out, int64_t n, int width);
 hipError_t launch_times_by(hipStream_t st, void* payload, double x);
+// ---- kernel launchers (skml_f64.hip) ----
+hipError_t launch_leaf64(hipStream_t st, const double* x, int64_t chunks, uint64_t s0, const uint64_t* tab,
+                         LeafPartial64* part, double* nodes6, double* roots);
+hipError_t launch_tree64(hipStream_t st, const double* src, double* dst, int64_t groups, int g, int level_in,
+                         int64_t chunk_base, uint64_t s0, const uint64_t* tab);
+hipError_t launch_summary64(hipStream_t st, const double* x, int64_t n, const LeafPartial64* part, int64_t nparts,
+                            const double* roots, const int64_t* ranks, int req_bins, int dedup, void* payload,
+                            double* g_raw);
+hipError_t launch_quantize64(hipStream_t st, const double* x, int64_t n, void* payload, const int* qflags);
+hipError_t launch_decode64(hipStream_t st, const void* payload, double* out, int64_t n);
+int uniform_partials(int64_t n);
+hipError_t launch_uniform(hipStream_t st, const float* x, int64_t n, int bin_num, UniPartial* part, void* payload,
+                          QuantLut* lut, int* qflags);
+hipError_t launch_uniform64(hipStream_t st, const double* x, int64_t n, int bin_num, UniPartial* part,
+                            void* payload, QuantLut* lut, int* qflags);
 hipError_t launch_pack_ref(hipStream_t st, const uint8_t* body, int width, int64_t n, void* payload);
 
 }  // namespace skml

@@ -15,7 +15,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .context import alloc_aligned, as_device_f32, get_context
+from .context import alloc_aligned, as_device_values, get_context
 from .exceptions import QuantileSketchException, SketchMLException, check
 
 
@@ -41,6 +41,7 @@ class Quantizer:
         self._hdr = None
         self._splits = None
         self._bins = None
+        self._wide = False           # input was fp64 (decode() then returns float64)
 
     # ---- abstract surface ----
     def quantize(self, values) -> None:
@@ -57,6 +58,8 @@ class Quantizer:
         """Quantizer.newQuantizer (Quantizer.java:126-136)."""
         if str(qtype) == "QUANTILE":
             return QuantileQuantizer(binNum, seed)
+        if str(qtype) == "UNIFORM":
+            return UniformQuantizer(binNum, seed)
         raise SketchMLException(f"Unrecognizable quantization type: {qtype}")
 
     # ---- device payload plumbing ----
@@ -75,8 +78,12 @@ class Quantizer:
             self.binNum = hdr.bin_num
         return self._hdr
 
-    def _encode(self, values, dedup: bool):
-        x = as_device_f32(values, self.device)
+    _ENTRY = {(False, False): "skml_dense_encode_f32", (False, True): "skml_dense_encode_f64",
+              (True, False): "skml_dense_encode_uniform_f32", (True, True): "skml_dense_encode_uniform_f64"}
+
+    def _encode(self, values, dedup: bool, uniform: bool = False):
+        x = as_device_values(values, self.device)
+        self._wide = x.dtype == torch.float64
         self.device = x.device
         self.n = x.numel()
         if self.binNum <= 1:
@@ -90,8 +97,9 @@ class Quantizer:
         p.bin_num = self.binNum
         p.seed = self.seed
         p.dedup = 1 if dedup else 0
-        st = _lib.lib.skml_dense_encode_f32(self._ctx().handle, C.c_void_p(x.data_ptr()), self.n,
-                                            C.byref(p), C.c_void_p(self.payload.data_ptr()), nbytes)
+        fn = getattr(_lib.lib, self._ENTRY[(uniform, self._wide)])
+        st = fn(self._ctx().handle, C.c_void_p(x.data_ptr()), self.n, C.byref(p),
+                C.c_void_p(self.payload.data_ptr()), nbytes)
         check(st, "quantize")
         self._hdr = None
         self._bins = None
@@ -176,13 +184,19 @@ class Quantizer:
                                            float(x)), "timesBy")
         self._hdr = None
 
-    def decode(self, out: torch.Tensor = None) -> torch.Tensor:
-        """values[bins[i]] in fp32 on the device (DenseVectorCompressor.decompressDense)."""
+    def decode(self, out: torch.Tensor = None, dtype=None) -> torch.Tensor:
+        """values[bins[i]] on the device (DenseVectorCompressor.decompressDense): fp32 for fp32
+        input, fp64 (the reference's double[]) for fp64 input or dtype=torch.float64."""
         self._load_header()
+        if dtype is None:
+            dtype = out.dtype if out is not None else (torch.float64 if self._wide else torch.float32)
         if out is None:
-            out = torch.empty(self.n, dtype=torch.float32, device=self.device)
-        check(_lib.lib.skml_dense_decode_f32(self._ctx().handle, C.c_void_p(self.payload.data_ptr()),
-                                             C.c_void_p(out.data_ptr()), self.n), "decode")
+            out = torch.empty(self.n, dtype=dtype, device=self.device)
+        if out.dtype != dtype or out.numel() != self.n or not out.is_contiguous():
+            raise SketchMLException("decode: output must be a contiguous tensor of n values of the decode dtype")
+        fn = _lib.lib.skml_dense_decode_f64 if dtype == torch.float64 else _lib.lib.skml_dense_decode_f32
+        check(fn(self._ctx().handle, C.c_void_p(self.payload.data_ptr()), C.c_void_p(out.data_ptr()), self.n),
+              "decode")
         return out
 
     # ---- java serialisation field stream ----
@@ -204,7 +218,7 @@ class Quantizer:
         if len(data) < 8:
             raise SketchMLException("truncated Quantizer stream")
         B, n = struct.unpack(">ii", data[:8])
-        q = QuantileQuantizer(B)
+        q = (QuantileQuantizer if cls is Quantizer else cls)(B)
         q.device = torch.device("cuda", torch.cuda.current_device()) if device is None else device
         q.n = n
         nbytes = _lib.lib.skml_dense_payload_bytes(n, B)
@@ -239,6 +253,27 @@ class QuantileQuantizer(Quantizer):
 
     def quantizationType(self) -> QuantizationType:
         return QuantizationType.QUANTILE
+
+
+class UniformQuantizer(Quantizer):
+    """quantization/UniformQuantizer.java:14-76 on the GPU: bin_num equal-width bins between the
+    Java min and max (MAX_VALUE / MIN_VALUE initialised), no Maths.unique, NaN values binned by
+    indexOf rather than rejected."""
+
+    def __init__(self, binNum: int = Quantizer.DEFAULT_BIN_NUM, seed: int = 0):
+        super().__init__(binNum, seed)
+
+    def quantize(self, values) -> None:
+        """UniformQuantizer.quantize (UniformQuantizer.java:21-45)."""
+        self._encode(values, dedup=False, uniform=True)
+
+    def parallelQuantize(self, values) -> None:
+        """UniformQuantizer.parallelQuantize (UniformQuantizer.java:48-70): the same splits and
+        bins as quantize (only the indexOf loop is sliced over threads in the reference)."""
+        self._encode(values, dedup=False, uniform=True)
+
+    def quantizationType(self) -> QuantizationType:
+        return QuantizationType.UNIFORM
 
 
 DEFAULT_BIN_NUM = Quantizer.DEFAULT_BIN_NUM

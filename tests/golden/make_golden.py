@@ -89,8 +89,45 @@ def misc_cases():
                  flag_words=d["flag_words"], delta_words=d["delta_words"])
 
 
+def wide_and_uniform_cases():
+    """fp64-input quantile cases (x stored as float64: values below fp32 precision) and uniform
+    quantizer cases (UniformQuantizer.java:21-45) on fp32 and fp64 input."""
+    rng = np.random.default_rng(20261016)
+    wide = {
+        "f64_normal_70001": (rng.standard_normal(70001), 256, 21),
+        "f64_close_40000": (1.0 + rng.integers(0, 5000, 40000) * 2.0**-40, 64, 22),
+        "f64_signed_zero_9000": (np.where(rng.random(9000) < 0.4, np.where(rng.random(9000) < 0.5, 0.0, -0.0),
+                                          rng.standard_normal(9000)), 256, 23),
+    }
+    for name, (x, bins, seed) in wide.items():
+        q = O.quantize(x, bins, seed)
+        np.savez(os.path.join(HERE, name + ".npz"), x=x, bin_num_req=bins, seed=seed,
+                 bin_num=q.bin_num, zero_idx=q.zero_idx, min=q.min, max=q.max, splits=q.splits,
+                 bins=q.bins.astype(np.int32), values=q.values(), write_ref=np.frombuffer(q.write_ref(), np.uint8))
+    x_nan = rng.standard_normal(20000)
+    x_nan[rng.random(20000) < 0.03] = np.nan
+    x_zero = np.abs(rng.standard_normal(5000)) + 1.0
+    x_zero[10] = -0.0
+    x_zero[20::7] = 0.0
+    uni = {
+        "uniform_f32_app_30000": (np.where(rng.random(30000) < 0.9, rng.standard_normal(30000), 0.0)
+                                  .astype(np.float32), 256),
+        "uniform_f64_nan_20000": (x_nan, 100),
+        "uniform_f64_zero_first_5000": (x_zero, 16),
+        "uniform_f32_negative_3000": ((-np.abs(rng.standard_normal(3000)) - 0.5).astype(np.float32), 8),
+    }
+    for name, (x, bins) in uni.items():
+        q = O.uniform_quantize(x.astype(np.float64), bins)
+        np.savez(os.path.join(HERE, name + ".npz"), x=x, bin_num_req=bins,
+                 bin_num=q.bin_num, zero_idx=q.zero_idx, min=q.min, max=q.max, splits=q.splits,
+                 bins=q.bins.astype(np.int32), values=q.values(), write_ref=np.frombuffer(q.write_ref(), np.uint8))
+
+
 if __name__ == "__main__":
-    dense_cases()
-    sparse_cases()
-    misc_cases()
+    # `make_golden.py wide` regenerates only the fp64 / uniform fixtures
+    if sys.argv[1:] != ["wide"]:
+        dense_cases()
+        sparse_cases()
+        misc_cases()
+    wide_and_uniform_cases()
     print("written:", sorted(f for f in os.listdir(HERE) if f.endswith(".npz")))

@@ -21,10 +21,36 @@ def _load(name):
 DENSE = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLD, "dense_*.npz")))
 SPARSE = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLD, "sparse_*.npz")))
 DELTA = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLD, "delta_*.npz")))
+WIDE = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLD, "f64_*.npz")))
+UNIFORM = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLD, "uniform_*.npz")))
 
 
 def test_fixtures_present():
     assert len(DENSE) >= 7 and len(SPARSE) >= 2 and len(DELTA) >= 3
+    assert len(WIDE) >= 3 and len(UNIFORM) >= 4
+
+
+def _check_quant(q, g):
+    assert q.bin_num == int(g["bin_num"]) and q.zero_idx == int(g["zero_idx"])
+    assert np.float64(q.min).tobytes() == np.float64(g["min"]).tobytes()
+    assert np.float64(q.max).tobytes() == np.float64(g["max"]).tobytes()
+    assert np.array_equal(q.splits, g["splits"], equal_nan=True)
+    assert np.array_equal(q.bins, g["bins"])
+    assert np.array_equal(q.values(), g["values"], equal_nan=True)
+    assert q.write_ref() == g["write_ref"].tobytes()
+
+
+@pytest.mark.parametrize("name", WIDE)
+def test_oracle_f64_golden(name):
+    g = _load(name)
+    assert g["x"].dtype == np.float64
+    _check_quant(O.quantize(g["x"], int(g["bin_num_req"]), int(g["seed"])), g)
+
+
+@pytest.mark.parametrize("name", UNIFORM)
+def test_oracle_uniform_golden(name):
+    g = _load(name)
+    _check_quant(O.uniform_quantize(g["x"].astype(np.float64), int(g["bin_num_req"])), g)
 
 
 @pytest.mark.parametrize("name", DENSE)

@@ -34,6 +34,32 @@ def test_dense_golden(gpu, name):
     assert q.writeObject() == g["write_ref"].tobytes()
 
 
+def _check_quant(q, g):
+    assert q.getBinNum() == int(g["bin_num"]) and q.getZeroIdx() == int(g["zero_idx"])
+    assert np.float64(q.getMin()).tobytes() == np.float64(g["min"]).tobytes()
+    assert np.float64(q.getMax()).tobytes() == np.float64(g["max"]).tobytes()
+    assert np.array_equal(q.getSplits(), g["splits"], equal_nan=True)
+    assert np.array_equal(q.getBins().cpu().numpy(), g["bins"])
+    assert np.array_equal(q.decode(dtype=torch.float64).cpu().numpy(), g["values"][g["bins"]], equal_nan=True)
+    assert q.writeObject() == g["write_ref"].tobytes()
+
+
+@pytest.mark.parametrize("name", _names("f64_"))
+def test_f64_golden(gpu, name):
+    g = _load(name)
+    q = gpu.QuantileQuantizer(int(g["bin_num_req"]), seed=int(g["seed"]))
+    q.quantize(torch.from_numpy(g["x"]).cuda())  # float64 tensor: the fp64 path
+    _check_quant(q, g)
+
+
+@pytest.mark.parametrize("name", _names("uniform_"))
+def test_uniform_golden(gpu, name):
+    g = _load(name)
+    q = gpu.UniformQuantizer(int(g["bin_num_req"]))
+    q.quantize(torch.from_numpy(g["x"]).cuda())
+    _check_quant(q, g)
+
+
 @pytest.mark.parametrize("name", _names("sparse_"))
 def test_sparse_golden(gpu, name):
     g = _load(name)

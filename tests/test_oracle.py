@@ -263,3 +263,44 @@ def test_sparse_roundtrip_properties():
     assert s.group_size.sum() == len(keys)
     e = O.group_edges(z, s.q.bin_num, 8)
     assert np.array_equal(e, N.group_edges(z, s.q.bin_num, 8))
+
+
+# ---------------------------------------------------------------- UniformQuantizer KATs
+def _uniform_py(values, B):
+    """UniformQuantizer.java:21-45 restated as plain Python loops (independent of the C oracle)."""
+    mn, mx = 1.7976931348623157e308, 4.9e-324
+    for v in values:
+        if v < mn:
+            mn = v
+        if v > mx:
+            mx = v
+    step = (mx - mn) / B
+    sp = [mn + step]
+    for _ in range(1, B - 1):
+        sp.append(sp[-1] + step)
+    return mn, mx, sp
+
+
+def test_uniform_kat():
+    q = O.uniform_quantize(np.array([0.0, 1.0, 2.0, 3.0, 4.0]), 4)
+    assert list(q.splits) == [1.0, 2.0, 3.0] and list(q.bins) == [0, 1, 2, 3, 3] and q.zero_idx == 0
+    # all-negative input: max stays Double.MIN_VALUE (UniformQuantizer.java:25)
+    q = O.uniform_quantize(np.array([-3.0, -1.0]), 2)
+    assert q.max == 5e-324 and list(q.splits) == [-1.5] and list(q.bins) == [0, 1] and q.zero_idx == 1
+    # the first zero decides the sign of a zero minimum; NaN is skipped, then binned by indexOf
+    q = O.uniform_quantize(np.array([5.0, 0.0, -0.0, 2.0]), 4)
+    assert np.signbit(q.min) == False and list(q.bins) == [3, 0, 0, 1]  # noqa: E712
+    q = O.uniform_quantize(np.array([5.0, -0.0, 0.0, np.nan]), 4)
+    assert np.signbit(q.min) and list(q.bins) == [3, 0, 0, 1]
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_uniform_crosscheck_python_loops(seed):
+    rng = np.random.default_rng(seed)
+    x = rng.standard_normal(3000) * 10.0 ** int(rng.integers(-3, 4))
+    x[rng.random(3000) < 0.01] = np.nan
+    B = int(rng.integers(2, 300))
+    q = O.uniform_quantize(x, B)
+    mn, mx, sp = _uniform_py(x, B)
+    assert q.min == mn and q.max == mx and list(q.splits) == sp
+    assert all(q.bins[i] == q.index_of(x[i]) for i in range(0, 3000, 7))
