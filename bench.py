@@ -41,6 +41,9 @@ def parse():
     ap.add_argument("--buffers", type=int, default=4,
                     help="rotating input buckets so a step never re-reads the previous step's "
                          "input from the 256 MB Infinity Cache")
+    ap.add_argument("--dtype", choices=["f32", "f64"], default="f32",
+                    help="input dtype (f64 = the reference's double[] path)")
+    ap.add_argument("--quant", choices=["quantile", "uniform"], default="quantile")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip decode / H2D measurements")
@@ -124,7 +127,8 @@ def main():
     xs = []
     for b in range(nbuf):
         gen.manual_seed(4 + rank + 1000 * b)  # config 4: bucket r seeded 4 + r
-        xs.append(torch.randn(n, device=dev, generator=gen))
+        xs.append(torch.randn(n, device=dev, generator=gen,
+                              dtype=torch.float64 if args.dtype == "f64" else torch.float32))
     payload = sk.alloc_aligned(nb, dev)
     params = _lib.Params()
     lib.skml_params_default(C.byref(params))
@@ -138,10 +142,15 @@ def main():
         exch = PayloadExchange(ctx)  # RCCL communicator; unique id broadcast over the process group
         allp = sk.alloc_aligned(nb * world, dev)
 
+    encode = getattr(lib, {("quantile", "f32"): "skml_dense_encode_f32",
+                           ("quantile", "f64"): "skml_dense_encode_f64",
+                           ("uniform", "f32"): "skml_dense_encode_uniform_f32",
+                           ("uniform", "f64"): "skml_dense_encode_uniform_f64"}[(args.quant, args.dtype)])
+    esize = 8 if args.dtype == "f64" else 4
+
     def step(i):
         x = xs[i % nbuf]
-        st = lib.skml_dense_encode_f32(ctx, C.c_void_p(x.data_ptr()), n, C.byref(params),
-                                       C.c_void_p(payload.data_ptr()), nb)
+        st = encode(ctx, C.c_void_p(x.data_ptr()), n, C.byref(params), C.c_void_p(payload.data_ptr()), nb)
         if st:
             raise RuntimeError(_lib.last_error())
         if exch is not None:
@@ -184,14 +193,14 @@ def main():
     steps_b = min(args.steps, 10)
 
     ms_per_step = 1000.0 * elapsed / args.steps
-    value = world * 4.0 * n * args.steps / elapsed / 1e9
+    value = world * esize * n * args.steps / elapsed / 1e9
 
     # ---- roofline of the dominant kernel (algorithmic bytes per launch / avg duration) ----
     hdr = _lib.DenseHeader()
     lib.skml_dense_info(ctx, C.c_void_p(payload.data_ptr()), C.byref(hdr), None, 0)
     code_bits = hdr.code_bits
-    alg_bytes = {"k_leaf": 4.0 * n, "k_quantize": 4.0 * n + n * code_bits / 8.0,
-                 "k_merge": 4.0 * 128 * max(1, n // 256 // 64), "k_summary": 0.0}
+    alg_bytes = {"k_leaf": esize * n, "k_quantize": esize * n + n * code_bits / 8.0,
+                 "k_merge": esize * 128 * max(1, n // 256 // 64), "k_summary": 0.0}
     # dominant kernel by device time in the full breakdown; its duration from the live timed region
     dom = max((k for k in allstats if k in alg_bytes), key=lambda k: allstats[k]["avg_us"] * allstats[k]["launches"])
     live = kstats.get(dom, allstats[dom])
@@ -205,7 +214,7 @@ def main():
     encode_device_us = sum(v["avg_us"] * v["launches"] for k, v in allstats.items()
                            if k in alg_bytes) / steps_b
     extras = {"encode_device_us": round(encode_device_us, 2),
-              "encode_roofline_frac": round((8.0 + code_bits / 8.0) * n / (encode_device_us * 1e-6)
+              "encode_roofline_frac": round((2 * esize + code_bits / 8.0) * n / (encode_device_us * 1e-6)
                                             / 1e9 / HBM_PEAK_GBS, 4),
               "kernels": {k: {"avg_us": round(v["avg_us"], 2), "launches": v["launches"]}
                           for k, v in allstats.items()},
@@ -215,40 +224,40 @@ def main():
 
     # ---- decode throughput + decode L2 error (rank-local) ----
     if not args.no_extras:
-        out = torch.empty(n, dtype=torch.float32, device=dev)
+        out = torch.empty(n, dtype=xs[0].dtype, device=dev)
+        decode = lib.skml_dense_decode_f64 if args.dtype == "f64" else lib.skml_dense_decode_f32
         x = xs[0]
         step(0)  # the payload decoded below is the encode of exactly this bucket
         lib.skml_ctx_set_timing(ctx, 1 << 4)
         lib.skml_ctx_reset_stats(ctx)
         for _ in range(10):
-            lib.skml_dense_decode_f32(ctx, C.c_void_p(payload.data_ptr()), C.c_void_p(out.data_ptr()), n)
+            decode(ctx, C.c_void_p(payload.data_ptr()), C.c_void_p(out.data_ptr()), n)
         dstats = kernel_stats(lib, ctx)
         lib.skml_ctx_set_timing(ctx, 0)
         dus = dstats["k_decode"]["avg_us"]
         diff = (out.double() - x.double())
         l2 = float(torch.linalg.vector_norm(diff).item())
-        extras["decode"] = {"gbps_fp32_out": round(4.0 * n / (dus * 1e-6) / 1e9, 1), "avg_us": round(dus, 2),
-                            "roofline_frac": round((4.0 + code_bits / 8.0) * n / (dus * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+        extras["decode"] = {"gbps_out": round(esize * n / (dus * 1e-6) / 1e9, 1), "avg_us": round(dus, 2),
+                            "roofline_frac": round((esize + code_bits / 8.0) * n / (dus * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
         extras["decode_l2_err"] = l2
         extras["decode_rmse"] = l2 / np.sqrt(n)
         extras["decode_rel_l2"] = l2 / float(torch.linalg.vector_norm(x.double()).item())
-        # end-to-end with PCIe: pinned host fp32 -> device -> encode -> payload back to host
+        # end-to-end with PCIe: pinned host gradient -> device -> encode -> payload back to host
         if rank == 0:
-            host = torch.empty(n, dtype=torch.float32, pin_memory=True)
+            host = torch.empty(n, dtype=x.dtype, pin_memory=True)
             host.copy_(x.cpu())
             hp = torch.empty(nb, dtype=torch.uint8, pin_memory=True)
-            xd = torch.empty(n, dtype=torch.float32, device=dev)
+            xd = torch.empty(n, dtype=x.dtype, device=dev)
             reps = 5
             torch.cuda.synchronize()
             ta = time.perf_counter()
             for _ in range(reps):
                 xd.copy_(host, non_blocking=True)
-                lib.skml_dense_encode_f32(ctx, C.c_void_p(xd.data_ptr()), n, C.byref(params),
-                                          C.c_void_p(payload.data_ptr()), nb)
+                encode(ctx, C.c_void_p(xd.data_ptr()), n, C.byref(params), C.c_void_p(payload.data_ptr()), nb)
                 hp.copy_(payload, non_blocking=True)
             torch.cuda.synchronize()
             tb = time.perf_counter()
-            extras["h2d_d2h_inclusive_gbps"] = round(4.0 * n * reps / (tb - ta) / 1e9, 2)
+            extras["h2d_d2h_inclusive_gbps"] = round(esize * n * reps / (tb - ta) / 1e9, 2)
 
     # ---- N > 1: the exchange step alone, and a check of the gathered payloads ----
     if exch is not None and not args.no_extras:
@@ -278,7 +287,7 @@ def main():
                                "decode_sum_max_abs_err_vs_allreduce": err}
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.quant == "quantile" and args.dtype == "f32":
         cpu = cpu_baseline(xs[0][: 2**22].cpu().numpy(), bins, args.cpu_seconds)
 
     if exch is not None:
@@ -288,9 +297,11 @@ def main():
             "metric": "device-resident grad encode GB/s (fp32 in) + decode L2 err, 1/2/4/8 GPU",
             "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic N(0,1), torch generator",
+            "scaling": "weak", "vs_baseline": None, "dtype": args.dtype, "data": "synthetic N(0,1), torch generator",
             "config": {"workload": ("C2: 2^26-float dense gradient bucket per GPU, 256 requested bins, "
-                                    "encode" + (" + RCCL all-gather of payloads (C4)" if world > 1 else "")),
+                                    + ("" if (args.quant, args.dtype) == ("quantile", "f32")
+                                       else f"{args.quant} quantizer, {args.dtype} input, ")
+                                    + "encode" + (" + RCCL all-gather of payloads (C4)" if world > 1 else "")),
                        "n_per_gpu": n, "bins": bins, "rotating_buffers": nbuf, "parallelism": f"dp{world}"},
             "roofline": roofline, "cpu_baseline": cpu, "extras": extras,
         }

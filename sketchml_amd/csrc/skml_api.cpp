@@ -583,14 +583,16 @@ int skml_dense_encode_f64(skml_ctx* c, const double* x, int64_t n, const skml_pa
             level += g;
         }
     }
+    Workspace wq;  // the quantize LUT lives in the fp32 workspace
+    if ((st = ensure_ws(c, 0, &wq))) return st;
     {
         KernelTimer kt(c, SKML_K_SUMMARY);
         HIP_TRY(launch_summary64(c->stream, x, n, w.part, tiles, w.roots, c->ranks, p->bin_num,
-                                 p->dedup ? 1 : 0, payload, w.raw));
+                                 p->dedup ? 1 : 0, payload, w.raw, wq.lut));
     }
     {
         KernelTimer kt(c, SKML_K_QUANTIZE);
-        HIP_TRY(launch_quantize64(c->stream, x, n, payload, nullptr));
+        HIP_TRY(launch_quantize64(c->stream, x, n, payload, wq.lut, nullptr, p->bin_num));
     }
     return SKML_OK;
 }
@@ -636,7 +638,7 @@ int skml_dense_encode_uniform_f64(skml_ctx* c, const double* x, int64_t n, const
     }
     {
         KernelTimer kt(c, SKML_K_QUANTIZE);
-        HIP_TRY(launch_quantize64(c->stream, x, n, payload, w.qflags));
+        HIP_TRY(launch_quantize64(c->stream, x, n, payload, w.lut, w.qflags, p->bin_num));
     }
     return SKML_OK;
 }

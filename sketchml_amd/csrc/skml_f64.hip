@@ -21,6 +21,8 @@
 //   k_uni_minmax  per-workgroup IEEE min / max (NaN skipped) and the first zero's index
 //   k_uni_finish  Java min / max (MAX_VALUE / MIN_VALUE initialised, the first zero wins the
 //                 min), splits by repeated `+= step`, findZeroIdx, header, quantize LUT.
+#include <algorithm>
+
 #include "skml_device.hpp"
 
 namespace skml {
@@ -36,6 +38,9 @@ __device__ __forceinline__ uint64_t dk(double d) { return d2key((uint64_t)__doub
 __device__ __forceinline__ bool is_nan64(uint64_t b) {
     return (b & 0x7FFFFFFFFFFFFFFFull) > 0x7FF0000000000000ull;
 }
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
 
 template <int M>
 __device__ __forceinline__ uint64_t lane_xor64(uint64_t v) {
@@ -371,7 +376,8 @@ __global__ __launch_bounds__(512) void k_summary64(const double* __restrict__ x,
                                                    const LeafPartial64* __restrict__ part, int64_t nparts,
                                                    const double* __restrict__ roots,
                                                    const int64_t* __restrict__ ranks, int req_bins, int dedup,
-                                                   uint8_t* __restrict__ payload, double* __restrict__ g_raw) {
+                                                   uint8_t* __restrict__ payload, double* __restrict__ g_raw,
+                                                   QuantLut* __restrict__ lut) {
     extern __shared__ __align__(16) uint8_t smem64[];
     Summary64Shared& S = *reinterpret_cast<Summary64Shared*>(smem64);
     const int t = threadIdx.x, T = blockDim.x;
@@ -527,6 +533,7 @@ __global__ __launch_bounds__(512) void k_summary64(const double* __restrict__ x,
             if (!dedup || i == 0 || raw[i] != raw[i - 1]) {
                 const double sp = raw[i];
                 splits[o] = sp;
+                if (o < kLutMaxSplits) reinterpret_cast<float*>(S.smp)[o] = __double2float_ru(sp);  // LUT input
                 if (!(sp < 0.0)) zmin = min(zmin, (int)o);
                 o++;
             }
@@ -543,6 +550,14 @@ __global__ __launch_bounds__(512) void k_summary64(const double* __restrict__ x,
         else if (vmax < 0.0) zero = bin_num - 1;
         else zero = S.zero < bin_num - 1 ? S.zero : bin_num - 1;
         write_header(hdr, SKML_OK, n, bin_num, zero, req_bins, vmin, vmax);
+    }
+    // quantize bucket LUT over the RU(fp32) images of the splits (staging aliases sorted[] + w[])
+    const int nsplit = bin_num - 1;
+    if (nsplit <= kLutMaxSplits && n > 0) {
+        build_quant_lut(reinterpret_cast<const float*>(S.smp), nsplit, lut, reinterpret_cast<int*>(S.wsum),
+                        reinterpret_cast<uint32_t*>(S.sorted));
+    } else if (t == 0) {
+        lut->cmax = -1;
     }
 }
 
@@ -576,59 +591,74 @@ __device__ __forceinline__ void pack_store4(uint8_t* codes, int64_t e0, const ui
     }
 }
 
-__global__ __launch_bounds__(256) void k_quantize64(const double* __restrict__ x, int64_t n,
-                                                    uint8_t* __restrict__ payload,
-                                                    const int* __restrict__ qflags) {
-    __shared__ double E[kEytz64Max];
-    const skml_dense_header* hdr = reinterpret_cast<const skml_dense_header*>(payload);
-    if (hdr->status != SKML_OK) return;
-    const int bins = hdr->bin_num, bits = hdr->code_bits, nsplit = bins - 1, zero = hdr->zero_idx;
-    const double* sp = reinterpret_cast<const double*>(payload + kHeaderBytes);
-    uint8_t* codes = payload + hdr->codes_offset;
-    const bool literal = qflags && (*qflags & 1);
-    uint32_t P = 1;
-    int levels = 0;
-    while (P < (uint32_t)bins) {
-        P <<= 1;
-        levels++;
-    }
-    const bool lds = !literal && P <= kEytz64Max;
-    if (lds) {
-        for (uint32_t i = threadIdx.x + 1; i < P; i += blockDim.x) {
-            const int d = 31 - __clz(i);
-            const uint32_t idx = ((2u * (i - (1u << d)) + 1u) << (levels - 1 - d)) - 1u;
-            E[i] = idx < (uint32_t)nsplit ? sp[idx] : __longlong_as_double(0x7FF0000000000000LL);  // +inf pad
-        }
-    }
-    __syncthreads();
-    const uint32_t nan_bin = (uint32_t)nan_bin_for(bins, zero);
-    auto bin_of = [&](double v) -> uint32_t {
-        if (literal) return java_index_of(sp, bins, zero, v);
-        if (v != v) return nan_bin;
-        if (lds) {
+// Modes: 0..4 = bucket LUT + that many float bisection steps; kQ64Eytz / kQ64Global / kQ64Java.
+//
+// LUT mode: y = RD(x), x rounded toward -inf to fp32, is <= x and lies in the same float-bounded
+// interval as x, and the fp32 machinery counts #{s <= y} exactly (s <= y <=> RU(s) <= y for a
+// float y, see build_quant_lut).  The splits in (y, x] -- within one fp32 ulp of x, almost
+// always none -- are then added by exact double compares.
+constexpr int kQ64Eytz = 8, kQ64Global = 9, kQ64Java = 10;
+
+struct Q64Tables {
+    const uint16_t* base;
+    const float* S;
+    const double* E;
+    const double* sp;
+    int nsplit, levels, zero, bins;
+    uint32_t P, nan_bin;
+};
+
+template <int MODE>
+__device__ __forceinline__ uint32_t q64_bin(const Q64Tables& q, double v) {
+    if constexpr (MODE == kQ64Java) {
+        return java_index_of(q.sp, q.bins, q.zero, v);
+    } else {
+        if (v != v) return q.nan_bin;
+        uint32_t bin;
+        if constexpr (MODE <= 4) {
+            const float y = __double2float_rd(v);
+            bin = q.base[f2key(__float_as_uint(y)) >> (32 - kLutBits)];
+#pragma unroll
+            for (int h = (1 << MODE) >> 1; h > 0; h >>= 1) bin += q.S[bin + h - 1] <= y ? (uint32_t)h : 0u;
+            // a split in (y, x] has RU(split) <= RU(x): only then compare in double
+            if (q.S[bin] <= __double2float_ru(v))
+                while (bin < (uint32_t)q.nsplit && q.sp[bin] <= v) bin++;
+        } else if constexpr (MODE == kQ64Eytz) {
             uint32_t i = 1;
-            for (int s = 0; s < levels; s++) i = 2 * i + (E[i] <= v ? 1u : 0u);
-            // +inf padding: v == +inf passes every pad; clamp to the split count
-            const uint32_t b = i - P;
-            return b > (uint32_t)nsplit ? (uint32_t)nsplit : b;
+            for (int s = 0; s < q.levels; s++) i = 2 * i + (q.E[i] <= v ? 1u : 0u);
+            bin = i - q.P;  // +inf padding: v == +inf passes every pad; clamp to the split count
+            bin = bin > (uint32_t)q.nsplit ? (uint32_t)q.nsplit : bin;
+        } else {
+            int lo = 0, hi = q.nsplit;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (q.sp[mid] <= v) lo = mid + 1;
+                else hi = mid;
+            }
+            bin = (uint32_t)lo;
         }
-        int lo = 0, hi = nsplit;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (sp[mid] <= v) lo = mid + 1;
-            else hi = mid;
-        }
-        return (uint32_t)lo;
-    };
+        return bin;
+    }
+}
+
+template <int MODE>
+__device__ __forceinline__ void q64_tiles(const Q64Tables& q, const double* __restrict__ x, int64_t n,
+                                          uint8_t* __restrict__ codes, int bits) {
     const int lane = threadIdx.x & 63;
     const int64_t nw = (int64_t)gridDim.x * 4, wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int64_t full = n / 1024;
     for (int64_t tile = wid; tile < full; tile += nw) {
-        const double2* src = reinterpret_cast<const double2*>(x + tile * 1024);
+        const f64x2* src = reinterpret_cast<const f64x2*>(x + tile * 1024);
+        f64x2 a[4], b[4];
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            const double2 a = src[j * 128 + 2 * lane], b = src[j * 128 + 2 * lane + 1];
-            const uint32_t c[4] = {bin_of(a.x), bin_of(a.y), bin_of(b.x), bin_of(b.y)};
+            a[j] = __builtin_nontemporal_load(src + j * 128 + 2 * lane);
+            b[j] = __builtin_nontemporal_load(src + j * 128 + 2 * lane + 1);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t c[4] = {q64_bin<MODE>(q, a[j].x), q64_bin<MODE>(q, a[j].y), q64_bin<MODE>(q, b[j].x),
+                                   q64_bin<MODE>(q, b[j].y)};
             pack_store4(codes, tile * 1024 + j * 256 + lane * 4, c, bits, lane);
         }
     }
@@ -639,7 +669,7 @@ __global__ __launch_bounds__(256) void k_quantize64(const double* __restrict__ x
             const int64_t e0 = base + j * 256 + lane * 4;
             uint32_t c[4] = {0, 0, 0, 0};
             for (int e = 0; e < 4; e++)
-                if (e0 + e < n) c[e] = bin_of(x[e0 + e]);
+                if (e0 + e < n) c[e] = q64_bin<MODE>(q, x[e0 + e]);
             if (bits == 1) {
                 const int64_t pair0 = base + j * 256 + (lane & ~1) * 4;
                 const uint32_t nib = c[0] | (c[1] << 1) | (c[2] << 2) | (c[3] << 3);
@@ -649,6 +679,68 @@ __global__ __launch_bounds__(256) void k_quantize64(const double* __restrict__ x
                 pack_store4(codes, e0, c, bits, lane);
             }
         }
+    }
+}
+
+// Dynamic LDS: LUT mode [0, 32 KB) bucket bases then `lds_splits` floats; Eytzinger mode reuses
+// it as up to 4096 doubles.
+__global__ __launch_bounds__(256) void k_quantize64(const double* __restrict__ x, int64_t n,
+                                                    uint8_t* __restrict__ payload, const QuantLut* __restrict__ lut,
+                                                    const int* __restrict__ qflags, int lds_splits) {
+    extern __shared__ __align__(16) uint8_t q64sm[];
+    const skml_dense_header* hdr = reinterpret_cast<const skml_dense_header*>(payload);
+    if (hdr->status != SKML_OK) return;
+    Q64Tables q;
+    q.bins = hdr->bin_num;
+    q.nsplit = q.bins - 1;
+    q.zero = hdr->zero_idx;
+    q.sp = reinterpret_cast<const double*>(payload + kHeaderBytes);
+    q.nan_bin = (uint32_t)nan_bin_for(q.bins, q.zero);
+    q.P = 1;
+    q.levels = 0;
+    while (q.P < (uint32_t)q.bins) {
+        q.P <<= 1;
+        q.levels++;
+    }
+    const int bits = hdr->code_bits;
+    uint8_t* codes = payload + hdr->codes_offset;
+    const int cmax = lut ? lut->cmax : -1;
+    int mode;
+    if ((qflags && (*qflags & 1)) || cmax == kLutJavaMode) {
+        mode = kQ64Java;
+    } else if (cmax >= 0 && q.nsplit + kLutPad <= lds_splits) {
+        mode = cmax == 0 ? 0 : 32 - __clz((uint32_t)cmax);
+        uint16_t* base = reinterpret_cast<uint16_t*>(q64sm);
+        float* S = reinterpret_cast<float*>(q64sm + sizeof(lut->base));
+        const uint4* src = reinterpret_cast<const uint4*>(lut->base);
+        for (int i = threadIdx.x; i < (int)(sizeof(lut->base) / 16); i += blockDim.x)
+            reinterpret_cast<uint4*>(base)[i] = src[i];
+        for (int i = threadIdx.x; i < q.nsplit + kLutPad; i += blockDim.x)
+            S[i] = i < q.nsplit ? __double2float_ru(q.sp[i]) : __uint_as_float(0x7FC00000u);
+        q.base = base;
+        q.S = S;
+    } else if (q.P <= kEytz64Max && (size_t)q.P * sizeof(double) <= sizeof(lut->base) + lds_splits * sizeof(float)) {
+        mode = kQ64Eytz;
+        double* E = reinterpret_cast<double*>(q64sm);
+        for (uint32_t i = threadIdx.x + 1; i < q.P; i += blockDim.x) {
+            const int d = 31 - __clz(i);
+            const uint32_t idx = ((2u * (i - (1u << d)) + 1u) << (q.levels - 1 - d)) - 1u;
+            E[i] = idx < (uint32_t)q.nsplit ? q.sp[idx] : __longlong_as_double(0x7FF0000000000000LL);
+        }
+        q.E = E;
+    } else {
+        mode = kQ64Global;
+    }
+    __syncthreads();
+    switch (mode) {
+        case 0: q64_tiles<0>(q, x, n, codes, bits); break;
+        case 1: q64_tiles<1>(q, x, n, codes, bits); break;
+        case 2: q64_tiles<2>(q, x, n, codes, bits); break;
+        case 3: q64_tiles<3>(q, x, n, codes, bits); break;
+        case 4: q64_tiles<4>(q, x, n, codes, bits); break;
+        case kQ64Eytz: q64_tiles<kQ64Eytz>(q, x, n, codes, bits); break;
+        case kQ64Java: q64_tiles<kQ64Java>(q, x, n, codes, bits); break;
+        default: q64_tiles<kQ64Global>(q, x, n, codes, bits); break;
     }
 }
 
@@ -672,6 +764,25 @@ __device__ __forceinline__ uint32_t code_at(const uint8_t* codes, int64_t e, int
     }
 }
 
+// Four consecutive codes starting at e0 (a multiple of 4) from one load.
+__device__ __forceinline__ void codes4(const uint8_t* codes, int64_t e0, int bits, uint32_t (&c)[4]) {
+    uint32_t w;
+    switch (bits) {
+        case 16: {
+            const uint2 q = *reinterpret_cast<const uint2*>(codes + e0 * 2);
+            c[0] = q.x & 0xFFFFu; c[1] = q.x >> 16; c[2] = q.y & 0xFFFFu; c[3] = q.y >> 16;
+            return;
+        }
+        case 8: w = *reinterpret_cast<const uint32_t*>(codes + e0); break;
+        case 4: w = *reinterpret_cast<const uint16_t*>(codes + e0 / 2); break;
+        case 2: w = codes[e0 / 4]; break;
+        default: w = (uint32_t)(codes[e0 / 8] >> (e0 & 4)); break;
+    }
+    const uint32_t m = (1u << bits) - 1u;
+#pragma unroll
+    for (int k = 0; k < 4; k++) c[k] = (w >> (k * bits)) & m;
+}
+
 __global__ __launch_bounds__(256) void k_decode64(const uint8_t* __restrict__ payload, double* __restrict__ out,
                                                   int64_t n) {
     __shared__ double lut[kEytz64Max];
@@ -683,40 +794,102 @@ __global__ __launch_bounds__(256) void k_decode64(const uint8_t* __restrict__ pa
     if (lds)
         for (int b = threadIdx.x; b < bins; b += blockDim.x) lut[b] = lut_value64(h, sp, b);
     __syncthreads();
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t e0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 2; e0 < n; e0 += stride * 2) {
-        const uint32_t c0 = code_at(codes, e0, bits);
-        const double v0 = lds ? lut[c0] : lut_value64(h, sp, (int)c0);
-        if (e0 + 1 < n) {
-            const uint32_t c1 = code_at(codes, e0 + 1, bits);
-            const double v1 = lds ? lut[c1] : lut_value64(h, sp, (int)c1);
-            *reinterpret_cast<double2*>(out + e0) = make_double2(v0, v1);
-        } else {
-            out[e0] = v0;
+    auto val = [&](uint32_t c) { return lds ? lut[c] : lut_value64(h, sp, (int)c); };
+    // 1024-value tiles per wave: each lane reads 4 codes and writes two double2 per step
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * 4, wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t full = n / 1024;
+    for (int64_t tile = wid; tile < full; tile += nw) {
+        f64x2* dst = reinterpret_cast<f64x2*>(out + tile * 1024);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int64_t e0 = tile * 1024 + j * 256 + lane * 4;
+            uint32_t c[4];
+            codes4(codes, e0, bits, c);
+            dst[j * 128 + 2 * lane] = f64x2{val(c[0]), val(c[1])};
+            dst[j * 128 + 2 * lane + 1] = f64x2{val(c[2]), val(c[3])};
         }
     }
+    if (wid == full % nw)
+        for (int64_t e = full * 1024 + lane; e < n; e += 64) out[e] = val(code_at(codes, e, bits));
 }
 
 // ---------------------------------------------------------------------------------------------
 // Uniform quantizer: per-workgroup min / max / first zero, then one finishing workgroup.
 // ---------------------------------------------------------------------------------------------
 template <typename T>
-__global__ __launch_bounds__(256) void k_uni_minmax(const T* __restrict__ x, int64_t n, UniPartial* __restrict__ part) {
-    double mn = __longlong_as_double(0x7FF0000000000000LL), mx = -mn;  // +inf, -inf
-    int64_t z = INT64_MAX;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const double v = (double)x[i];
-        mn = v < mn ? v : mn;  // NaN never compares: skipped, as in `if (v < min)`
-        mx = v > mx ? v : mx;
-        if (v == 0.0 && i < z) z = i;
+struct Vec16;  // 16-byte vector of T
+template <>
+struct Vec16<float> {
+    typedef f32x4 type;
+    static constexpr int N = 4;
+    __device__ static void get(const f32x4& v, float (&o)[4]) {
+        o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
     }
-    __shared__ double smn[4], smx[4];
-    __shared__ int64_t sz[4];
+};
+template <>
+struct Vec16<double> {
+    typedef f64x2 type;
+    static constexpr int N = 2;
+    __device__ static void get(const f64x2& v, double (&o)[2]) {
+        o[0] = v.x; o[1] = v.y;
+    }
+};
+
+// Streaming min / max / first zero over 16-byte loads (8 in flight per thread), compared in the
+// input type (IEEE order is the same as in double); the zero index is a Java int.
+template <typename T>
+__global__ __launch_bounds__(256) void k_uni_minmax(const T* __restrict__ x, int64_t n, UniPartial* __restrict__ part) {
+    using V = Vec16<T>;
+    typedef typename V::type VT;
+    constexpr int U = 8;
+    T mn = (T)__builtin_inf(), mx = -(T)__builtin_inf();
+    int32_t z = INT32_MAX;
+    const int64_t nv = n / V::N;
+    const VT* xv = reinterpret_cast<const VT*>(x);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + (U - 1) * stride < nv; i += U * stride) {
+        VT v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = __builtin_nontemporal_load(xv + i + u * stride);
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            T e[V::N];
+            V::get(v[u], e);
+#pragma unroll
+            for (int k = 0; k < V::N; k++) {
+                mn = e[k] < mn ? e[k] : mn;  // NaN never compares: skipped, as `if (v < min)`
+                mx = e[k] > mx ? e[k] : mx;
+                const int32_t idx = (int32_t)((i + u * stride) * V::N + k);
+                z = (e[k] == (T)0 && idx < z) ? idx : z;
+            }
+        }
+    }
+    for (; i < nv; i += stride) {
+        T e[V::N];
+        V::get(xv[i], e);
+#pragma unroll
+        for (int k = 0; k < V::N; k++) {
+            mn = e[k] < mn ? e[k] : mn;
+            mx = e[k] > mx ? e[k] : mx;
+            const int32_t idx = (int32_t)(i * V::N + k);
+            z = (e[k] == (T)0 && idx < z) ? idx : z;
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x < n - nv * V::N) {  // ragged tail
+        const int64_t idx = nv * V::N + threadIdx.x;
+        const T e = x[idx];
+        mn = e < mn ? e : mn;
+        mx = e > mx ? e : mx;
+        z = (e == (T)0 && (int32_t)idx < z) ? (int32_t)idx : z;
+    }
+    __shared__ T smn[4], smx[4];
+    __shared__ int32_t sz[4];
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
-        const double omn = __shfl_xor(mn, off, 64), omx = __shfl_xor(mx, off, 64);
-        const int64_t oz = __shfl_xor(z, off, 64);
+        const T omn = __shfl_xor(mn, off, 64), omx = __shfl_xor(mx, off, 64);
+        const int32_t oz = __shfl_xor(z, off, 64);
         mn = omn < mn ? omn : mn;
         mx = omx > mx ? omx : mx;
         z = oz < z ? oz : z;
@@ -734,7 +907,7 @@ __global__ __launch_bounds__(256) void k_uni_minmax(const T* __restrict__ x, int
             mx = smx[k] > mx ? smx[k] : mx;
             z = sz[k] < z ? sz[k] : z;
         }
-        part[blockIdx.x] = UniPartial{mn, mx, z, 0};
+        part[blockIdx.x] = UniPartial{(double)mn, (double)mx, z == INT32_MAX ? INT64_MAX : (int64_t)z, 0};
     }
 }
 
@@ -746,18 +919,44 @@ __global__ __launch_bounds__(256) void k_uni_finish(const T* __restrict__ x, int
     skml_dense_header* hdr = reinterpret_cast<skml_dense_header*>(payload);
     double* splits = reinterpret_cast<double*>(payload + kHeaderBytes);
     __shared__ double s_mn, s_mx;
+    __shared__ double s_rmn[4], s_rmx[4];
+    __shared__ int64_t s_rz[4];
     __shared__ int s_bad;
     __shared__ int s_zero;
     __shared__ int s_misc[20];
     __shared__ float s_sp[kLutMaxSplits];
     __shared__ __align__(16) uint32_t s_lbuf[kLutSize / 2];
-    if (threadIdx.x == 0) {
+    {  // reduce the partials (one per thread, then waves, then thread 0)
         double mn = __longlong_as_double(0x7FF0000000000000LL), mx = -mn;
         int64_t z = INT64_MAX;
-        for (int k = 0; k < nparts; k++) {
-            mn = part[k].mn < mn ? part[k].mn : mn;
-            mx = part[k].mx > mx ? part[k].mx : mx;
-            z = part[k].zidx < z ? part[k].zidx : z;
+        for (int k = threadIdx.x; k < nparts; k += blockDim.x) {
+            const UniPartial p = part[k];
+            mn = p.mn < mn ? p.mn : mn;
+            mx = p.mx > mx ? p.mx : mx;
+            z = p.zidx < z ? p.zidx : z;
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const double omn = __shfl_xor(mn, off, 64), omx = __shfl_xor(mx, off, 64);
+            const int64_t oz = __shfl_xor(z, off, 64);
+            mn = omn < mn ? omn : mn;
+            mx = omx > mx ? omx : mx;
+            z = oz < z ? oz : z;
+        }
+        if ((threadIdx.x & 63) == 0) {
+            s_rmn[threadIdx.x >> 6] = mn;
+            s_rmx[threadIdx.x >> 6] = mx;
+            s_rz[threadIdx.x >> 6] = z;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double mn = s_rmn[0], mx = s_rmx[0];
+        int64_t z = s_rz[0];
+        for (int k = 1; k < (int)(blockDim.x >> 6); k++) {
+            mn = s_rmn[k] < mn ? s_rmn[k] : mn;
+            mx = s_rmx[k] > mx ? s_rmx[k] : mx;
+            z = s_rz[k] < z ? s_rz[k] : z;
         }
         // UniformQuantizer.java:24-29: min from Double.MAX_VALUE by `<`, max from Double.MIN_VALUE
         // by `>`; among equal minima the first wins, which only shows for a zero minimum
@@ -769,14 +968,15 @@ __global__ __launch_bounds__(256) void k_uni_finish(const T* __restrict__ x, int
         // UniformQuantizer.java:31-36
         const double step = (jmax - jmin) / bin_num;
         const int ns = bin_num - 1;
-        double cur = jmin + step;
+        double cur = jmin + step, prev = cur;
         int bad = 0, zero = ns;
         for (int i = 0; i < ns; i++) {
             if (i > 0) cur = cur + step;
             splits[i] = cur;
-            if (!(cur == cur)) bad = 1;
-            if (i > 0 && !(splits[i - 1] <= cur)) bad = 1;
-            if (zero == ns && !(cur < 0.0)) zero = i;
+            if (i < kLutMaxSplits) s_sp[i] = __double2float_ru(cur);
+            bad |= (!(cur == cur) || !(prev <= cur)) ? 1 : 0;
+            zero = (zero == ns && !(cur < 0.0)) ? i : zero;
+            prev = cur;
         }
         s_bad = bad;
         s_zero = zero;
@@ -786,11 +986,7 @@ __global__ __launch_bounds__(256) void k_uni_finish(const T* __restrict__ x, int
     const int ns = bin_num - 1;
     const double jmin = s_mn, jmax = s_mx;
     const bool lut_ok = !s_bad && ns <= kLutMaxSplits;
-    if (lut_ok) {
-        for (int i = threadIdx.x; i < ns; i += blockDim.x) s_sp[i] = __double2float_ru(splits[i]);
-        __syncthreads();
-        build_quant_lut(s_sp, ns, lut, s_misc, s_lbuf);
-    }
+    if (lut_ok) build_quant_lut(s_sp, ns, lut, s_misc, s_lbuf);
     if (threadIdx.x == 0) {
         if (s_bad) lut->cmax = kLutJavaMode;
         else if (!lut_ok) lut->cmax = -1;
@@ -823,7 +1019,7 @@ hipError_t launch_tree64(hipStream_t st, const double* src, double* dst, int64_t
 
 hipError_t launch_summary64(hipStream_t st, const double* x, int64_t n, const LeafPartial64* part, int64_t nparts,
                             const double* roots, const int64_t* ranks, int req_bins, int dedup, void* payload,
-                            double* g_raw) {
+                            double* g_raw, QuantLut* lut) {
     static bool attr = false;
     if (!attr) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_summary64),
@@ -833,7 +1029,7 @@ hipError_t launch_summary64(hipStream_t st, const double* x, int64_t n, const Le
         attr = true;
     }
     hipLaunchKernelGGL(k_summary64, dim3(1), dim3(512), sizeof(Summary64Shared), st, x, n, part, nparts, roots,
-                       ranks, req_bins, dedup, reinterpret_cast<uint8_t*>(payload), g_raw);
+                       ranks, req_bins, dedup, reinterpret_cast<uint8_t*>(payload), g_raw, lut);
     return hipGetLastError();
 }
 
@@ -844,10 +1040,15 @@ static int grid_for(int64_t n, int per_wg, int cap) {
     return (int)g;
 }
 
-hipError_t launch_quantize64(hipStream_t st, const double* x, int64_t n, void* payload, const int* qflags) {
+hipError_t launch_quantize64(hipStream_t st, const double* x, int64_t n, void* payload, const QuantLut* lut,
+                             const int* qflags, int req_bins) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_quantize64, dim3(grid_for(n, 4096, 1024)), dim3(256), 0, st, x, n,
-                       reinterpret_cast<uint8_t*>(payload), qflags);
+    // LDS sized for this request's split table (LUT mode), at least the 32 KB Eytzinger table
+    const int lds_splits = std::min(std::max(req_bins - 1, 1), kLutMaxSplits) + kLutPad;
+    const size_t lds = std::max(sizeof(QuantLut::base) + (size_t)lds_splits * sizeof(float),
+                                (size_t)kEytz64Max * sizeof(double));
+    hipLaunchKernelGGL(k_quantize64, dim3(grid_for(n, 4096, 1024)), dim3(256), lds, st, x, n,
+                       reinterpret_cast<uint8_t*>(payload), lut, qflags, lds_splits);
     return hipGetLastError();
 }
 

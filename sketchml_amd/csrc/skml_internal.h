@@ -121,8 +121,11 @@ hipError_t launch_tree64(hipStream_t st, const double* src, double* dst, int64_t
                          int64_t chunk_base, uint64_t s0, const uint64_t* tab);
 hipError_t launch_summary64(hipStream_t st, const double* x, int64_t n, const LeafPartial64* part, int64_t nparts,
                             const double* roots, const int64_t* ranks, int req_bins, int dedup, void* payload,
-                            double* g_raw);
-hipError_t launch_quantize64(hipStream_t st, const double* x, int64_t n, void* payload, const int* qflags);
+                            double* g_raw, QuantLut* lut);
+// `lut` may be null; fp64 values are looked up by their round-down fp32 image, then corrected
+// by exact double compares.
+hipError_t launch_quantize64(hipStream_t st, const double* x, int64_t n, void* payload, const QuantLut* lut,
+                             const int* qflags, int req_bins);
 hipError_t launch_decode64(hipStream_t st, const void* payload, double* out, int64_t n);
 int uniform_partials(int64_t n);
 hipError_t launch_uniform(hipStream_t st, const float* x, int64_t n, int bin_num, UniPartial* part, void* payload,
