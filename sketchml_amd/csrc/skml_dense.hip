@@ -90,18 +90,30 @@ __device__ __forceinline__ void quant_tiles(const QuantTables& q, const float* _
     const int64_t nwaves_total = (int64_t)gridDim.x * (kQThreads / 64);
     const int64_t wave_id = (int64_t)blockIdx.x * (kQThreads / 64) + (threadIdx.x >> 6);
     const int64_t full_tiles = n / 1024;
-    for (int64_t tile = wave_id; tile < full_tiles; tile += nwaves_total) {
-        typedef float f32x4 __attribute__((ext_vector_type(4)));
-        const f32x4* src = reinterpret_cast<const f32x4*>(x + tile * 1024);
-        f32x4 f[4];
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    // software-pipelined: the next tile's 4 KiB is in flight while this one is binned
+    f32x4 f[4];
+    if (wave_id < full_tiles) {
+        const f32x4* src = reinterpret_cast<const f32x4*>(x + wave_id * 1024);
 #pragma unroll
         for (int j = 0; j < 4; j++) f[j] = __builtin_nontemporal_load(src + j * 64 + lane);
+    }
+    for (int64_t tile = wave_id; tile < full_tiles; tile += nwaves_total) {
+        f32x4 g[4];
+        const int64_t next = tile + nwaves_total;
+        if (next < full_tiles) {
+            const f32x4* src = reinterpret_cast<const f32x4*>(x + next * 1024);
+#pragma unroll
+            for (int j = 0; j < 4; j++) g[j] = __builtin_nontemporal_load(src + j * 64 + lane);
+        }
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const uint32_t c0 = quant_bin<MODE>(q, f[j].x), c1 = quant_bin<MODE>(q, f[j].y);
             const uint32_t c2 = quant_bin<MODE>(q, f[j].z), c3 = quant_bin<MODE>(q, f[j].w);
             store_codes4(codes, tile * 1024 + j * 256 + lane * 4, c0, c1, c2, c3, bits, lane);
         }
+#pragma unroll
+        for (int j = 0; j < 4; j++) f[j] = g[j];
     }
     // tail tile (n % 1024 values), one wave, guarded element loads
     if (wave_id == full_tiles % nwaves_total && n % 1024) {

@@ -193,6 +193,14 @@ __global__ __launch_bounds__(256) void k_leaf64(const double* __restrict__ x, in
     uint64_t top[2] = {0, 0};
 #pragma unroll 1
     for (int c = 0; c < rem; c++) {
+        if ((c & 15) == 0) {  // issue priority falls with progress (fair share of the SIMD)
+            switch (c >> 4) {
+                case 0: __builtin_amdgcn_s_setprio(3); break;
+                case 1: __builtin_amdgcn_s_setprio(2); break;
+                case 2: __builtin_amdgcn_s_setprio(1); break;
+                default: __builtin_amdgcn_s_setprio(0); break;
+            }
+        }
         const int64_t chunk = c_tile + c;
         const double2* src = reinterpret_cast<const double2*>(x + chunk * kChunk);
         const double2 p0 = src[2 * lane], p1 = src[2 * lane + 1];

@@ -27,6 +27,10 @@ namespace skml {
 // Phase timestamps of the fused merge + summary workgroup (profiling builds only:
 // make EXTRA=-DSKML_PROF_SUMMARY); read back with skml_debug_prof.
 __device__ unsigned long long g_prof[32];
+#ifdef SKML_PROF_LEAF
+// per-wave (start, end, hw_id, xcc_id) of the hot leaf kernel (profiling builds only)
+__device__ unsigned long long g_leafprof[4 * 65536];
+#endif
 #ifdef SKML_PROF_SUMMARY
 #define SKML_PROF(k)                                      \
     do {                                                  \
@@ -216,6 +220,16 @@ struct LeafExport {
 // 3..5 exactly like HeapQuantileSketch's binary counter (inPlacePropagationUpdate,
 // HeapQuantileSketch.java:116-124), so no workgroup barrier is ever needed.
 // ---------------------------------------------------------------------------------------------
+// s_setprio 3..0 by the fraction of the wave's rounds already done (wave-uniform).
+__device__ __forceinline__ void set_prio_by_progress(int round, int nrounds) {
+    switch ((4 * round) / nrounds) {
+        case 0: __builtin_amdgcn_s_setprio(3); break;
+        case 1: __builtin_amdgcn_s_setprio(2); break;
+        case 2: __builtin_amdgcn_s_setprio(1); break;
+        default: __builtin_amdgcn_s_setprio(0); break;
+    }
+}
+
 constexpr int kLeafWaveChunks = 64;
 constexpr int kLeaf2Waves = 4;
 
@@ -273,6 +287,9 @@ __global__ __launch_bounds__(256, 4) void k_leaf2(const float* __restrict__ x, i
     const int nrounds = rem ? (rem + kChunksPerWave - 1) / kChunksPerWave : kLeafWaveChunks / kChunksPerWave;
     float* wfb = fb[wave];
     const uint64_t ta = tab[lane * 2], tc = tab[lane * 2 + 1];  // A^lane, C_lane
+#ifdef SKML_PROF_LEAF
+    const unsigned long long prof_t0 = wall_clock64();
+#endif
 
     uint32_t mn = 0xFFFFFFFFu, mx = 0u, fl = 0u;
     bool neg_any = false, pos_any = false;
@@ -280,6 +297,10 @@ __global__ __launch_bounds__(256, 4) void k_leaf2(const float* __restrict__ x, i
     uint32_t acc = 0;
 #pragma unroll 1
     for (int round = 0; round < nrounds; round++) {
+        // Issue priority falls as the wave progresses: the SIMD's arbiter favours the oldest
+        // wave, so without this the 4 waves of a SIMD finish one after another (~50/72/95/118 us
+        // at 2^26) and the last quarter of the kernel runs with too few waves to hide latency.
+        set_prio_by_progress(round, nrounds);
         const int64_t c0 = c_tile + round * kChunksPerWave;
         const int64_t chunk = c0 + (lane >> 3);
         const bool valid = PARTIAL ? chunk < chunks : true;
@@ -421,6 +442,14 @@ __global__ __launch_bounds__(256, 4) void k_leaf2(const float* __restrict__ x, i
         p.flags = fl | ((mn < 0x007FFFFFu || mx > 0xFF800000u) ? 1u : 0u);
         p.pad = 0;
         part[tile] = p;  // (a single atomic accumulator instead costs ~40 us of contention)
+#ifdef SKML_PROF_LEAF
+        if (!PARTIAL && tile < 65536) {
+            g_leafprof[4 * tile] = prof_t0;
+            g_leafprof[4 * tile + 1] = wall_clock64();
+            g_leafprof[4 * tile + 2] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));   // HW_ID
+            g_leafprof[4 * tile + 3] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));  // XCC_ID
+        }
+#endif
     }
 }
 
@@ -1114,6 +1143,12 @@ hipError_t launch_set_splits(hipStream_t st, void* payload, int64_t n, const dou
 
 }  // namespace skml
 
+#ifdef SKML_PROF_LEAF
+extern "C" int skml_debug_leafprof(unsigned long long* out, int cap) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(skml::g_leafprof), sizeof(unsigned long long) * (size_t)cap) ==
+                   hipSuccess ? SKML_OK : SKML_E_HIP;
+}
+#endif
 extern "C" int skml_debug_prof(unsigned long long* out, int cap) {
     if (!out || cap <= 0) return SKML_E_ARG;
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(skml::g_prof), sizeof(unsigned long long) * (size_t)(cap < 32 ? cap : 32)) ==

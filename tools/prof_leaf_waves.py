@@ -1,0 +1,49 @@
+#!/usr/bin/env python3
+"""Per-wave start/end spread of the leaf kernel (profiling build):
+
+    make -C sketchml_amd/csrc OUT=../lib_prof EXTRA=-DSKML_PROF_LEAF
+    SKML_LIB=sketchml_amd/lib_prof/libskml.so python tools/prof_leaf_waves.py [n]
+"""
+import ctypes as C
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import sketchml_amd as sk  # noqa: E402
+from sketchml_amd import _lib  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 2**26
+tiles = min(65536, n // 256 // 64)
+x = torch.randn(n, device="cuda")
+q = sk.QuantileQuantizer(256, seed=1)
+fn = _lib.lib.skml_debug_leafprof
+fn.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+buf = (C.c_ulonglong * (4 * tiles))()
+for it in range(3):
+    q.quantize(x)
+    torch.cuda.synchronize()
+    assert fn(buf, 4 * tiles) == 0
+    a = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 4).astype(np.int64)
+    t0 = a[:, 0].min()
+    st = (a[:, 0] - t0) * 0.01
+    en = (a[:, 1] - t0) * 0.01
+    dur = en - st
+    xcc = a[:, 3] & 0xF
+    hw = a[:, 2]
+    cu = (hw >> 8) & 0xF
+    se = (hw >> 13) & 0x7
+    print(f"iter {it}: kernel span {en.max():.1f} us; start p50 {np.percentile(st, 50):.1f} max {st.max():.1f}; "
+          f"dur min {dur.min():.1f} p50 {np.percentile(dur, 50):.1f} p90 {np.percentile(dur, 90):.1f} "
+          f"max {dur.max():.1f}; end p10 {np.percentile(en, 10):.1f} p50 {np.percentile(en, 50):.1f} "
+          f"p90 {np.percentile(en, 90):.1f}")
+    if it == 2:
+        for k in range(8):
+            m = xcc == k
+            if m.any():
+                print(f"   xcc {k}: waves {m.sum()} dur p50 {np.percentile(dur[m], 50):.1f} max {dur[m].max():.1f} "
+                      f"end max {en[m].max():.1f}")
+        hist = np.histogram(dur, bins=10)
+        print("   dur histogram:", list(hist[0]), [round(v, 1) for v in hist[1]])
