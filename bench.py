@@ -77,6 +77,28 @@ def pmc_traffic(kernel, n):
     return best
 
 
+# VALU issue ceiling (wave-instructions / s, whole chip): tools/ubench/xlane2.hip measured 1.12
+# clocks per v_min_u32 wave-instruction per CU at 2.4 GHz on 256 CUs.
+VALU_PEAK_GINST = 2.4e9 / 1.12 * 256 / 1e9
+
+
+def sq_valu(kernel):
+    """VALU wave-instructions per launch of `kernel` from the committed SQ counter pass
+    (profiles/*sq_counters.json, written by tools/prof_round.sh)."""
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*sq_counters.json"))):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except Exception:
+            continue
+        for name, c in d.get("per_launch_mean", {}).items():
+            short = "k_leaf" if "k_leaf2" in name else name.split("(")[0].split("::")[-1]
+            if short == kernel and "SQ_INSTS_VALU" in c:
+                best = (c["SQ_INSTS_VALU"], os.path.relpath(path, ROOT))
+    return best
+
+
 def cpu_baseline(x_host, bins, budget_s):
     """Oracle (C restatement of QuantileQuantizer.quantize + 1-byte code write, scalar -O2,
     double arithmetic, 1 thread) on a bounded sample of the same workload."""
@@ -211,6 +233,12 @@ def main():
                 "traffic": traffic[0] if traffic else None,
                 "traffic_source": traffic[1] if traffic else None,
                 "alg_bytes_per_launch": alg_bytes[dom]}
+    valu = sq_valu(dom) if (args.n == 2**26 and args.dtype == "f32" and args.quant == "quantile") else None
+    if valu:
+        # the sort-dominated leaf is bound by VALU issue, not HBM: its issue rate against the ceiling
+        rate = valu[0] / (live["avg_us"] * 1e-6) / 1e9
+        roofline["valu"] = {"insts_per_launch": valu[0], "source": valu[1], "issue_ginst_s": round(rate, 1),
+                            "peak_ginst_s": round(VALU_PEAK_GINST, 1), "frac": round(rate / VALU_PEAK_GINST, 4)}
     encode_device_us = sum(v["avg_us"] * v["launches"] for k, v in allstats.items()
                            if k in alg_bytes) / steps_b
     extras = {"encode_device_us": round(encode_device_us, 2),
