@@ -225,6 +225,16 @@ int skml_sparse_group_info(skml_ctx* ctx, const skml_sparse* s, int32_t g, skml_
  * without Java object-stream framing; see DESIGN.md for the exact layout. */
 int skml_sparse_serialize(skml_ctx* ctx, const skml_sparse* s, uint8_t* buf_host, size_t cap,
                           size_t* written);
+/* GroupedMinMaxSketch.readObject (GroupedMinMaxSketch.java:161-172) with its MinMaxSketch,
+ * HuffmanEncoder and DeltaAdaptiveEncoder readObjects: parses the stream skml_sparse_serialize
+ * writes and rebuilds a device payload (the Huffman tables are decoded on the device).
+ * quant_values (SparseVectorCompressor.quantValues, may be NULL with nvalues 0) enable
+ * skml_sparse_decode_f32; without them only skml_sparse_restore_bins applies.  Synchronising. */
+int skml_sparse_deserialize(skml_ctx* ctx, const uint8_t* buf_host, size_t len, const double* quant_values,
+                            int32_t nvalues, skml_sparse** out);
+/* GroupedMinMaxSketch.restore (GroupedMinMaxSketch.java:123-146): keys in Sort.merge order and
+ * their int32 bins, on the device.  Synchronising. */
+int skml_sparse_restore_bins(skml_ctx* ctx, const skml_sparse* s, int32_t* keys_dev, int32_t* bins_dev);
 int skml_sparse_free(skml_sparse* s);
 
 /* ---- DeltaAdaptiveEncoder as a standalone BinaryEncoder (base/BinaryEncoder.java:6-11) ---- */

@@ -9,10 +9,10 @@ from .compressor import DenseVectorCompressor
 from .context import Context, alloc_aligned, get_context
 from .exceptions import QuantileSketchException, SketchMLException
 from .quantization import QuantileQuantizer, QuantizationType, Quantizer, UniformQuantizer
-from .sparse import (DeltaAdaptiveEncoder, GroupedMinMaxSketch, SparseVectorCompressor, encode_dense_as_sparse,
-                     encode_sparse, to_sparse)
+from .sparse import (DeltaAdaptiveEncoder, GroupedMinMaxSketch, SparsePayload, SparseVectorCompressor,
+                     encode_dense_as_sparse, encode_sparse, to_sparse)
 
-__all__ = ["Context", "DeltaAdaptiveEncoder", "DenseVectorCompressor", "GroupedMinMaxSketch",
+__all__ = ["Context", "DeltaAdaptiveEncoder", "DenseVectorCompressor", "GroupedMinMaxSketch", "SparsePayload",
            "SparseVectorCompressor", "encode_dense_as_sparse", "encode_sparse", "to_sparse", "QuantileQuantizer", "QuantizationType", "Quantizer", "UniformQuantizer",
            "QuantileSketchException", "SketchMLException", "get_context", "alloc_aligned"]
 

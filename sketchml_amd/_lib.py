@@ -97,6 +97,8 @@ _SIGS = {
     "skml_sparse_group_info": (C.c_int, [vp, vp, i32, C.POINTER(SparseGroup), i32p,
                                          C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "skml_sparse_serialize": (C.c_int, [vp, vp, u8p, C.c_size_t, szp]),
+    "skml_sparse_deserialize": (C.c_int, [vp, u8p, C.c_size_t, dblp, i32, C.POINTER(vp)]),
+    "skml_sparse_restore_bins": (C.c_int, [vp, vp, vp, vp]),
     "skml_sparse_free": (C.c_int, [vp]),
     "skml_delta_encode": (C.c_int, [vp, vp, i64, i32p, i32p, i64p, i64p, vp, vp, i64]),
     "skml_delta_decode": (C.c_int, [vp, i64, i32, i32, vp, i64, vp, i64, vp]),

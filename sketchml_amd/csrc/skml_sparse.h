@@ -101,6 +101,36 @@ hipError_t launch_huff_lens(hipStream_t st, const int32_t* table, int64_t ncells
 hipError_t launch_huff_write(hipStream_t st, const int32_t* table, int64_t ncells, const SpGroups* gp, int B,
                              const uint64_t* lut, const uint64_t* tile_base, uint64_t* words, int64_t* gbit);
 
+// HuffmanEncoder.decode (readObject side): speculative parallel decoding of the per-group code
+// streams (see skml_sparse.hip).  lut: kHuffLutSize int2 per group row, {value, length} or
+// {tree node, -1}; nodes: int4 {left, right, value, 0}, left < 0 for a leaf.
+constexpr int kHuffLutBits = 12;
+constexpr int kHuffLutSize = 1 << kHuffLutBits;
+constexpr int64_t kHuffSeg = 2048;  // bits per speculative segment
+struct HuffDecGroup {
+    int64_t word0;   // first word of the group's stream in the concatenated words
+    int64_t nwords;  // stored words (BitSet.toLongArray); bits beyond read as 0
+    int64_t tab_off; // first table cell
+    int64_t size;    // symbols (rows * cols)
+    int32_t lut_row;
+    int32_t seg0;    // first segment of the group
+};
+struct HuffSeg {
+    int64_t lim;  // nominal end: the next segment's nominal start
+    int32_t g;
+    int16_t first, last;
+};
+hipError_t launch_huff_spec(hipStream_t st, int nseg, const HuffSeg* segs, const HuffDecGroup* grp,
+                            const uint64_t* words, const int2* lut, const int4* nodes, int64_t* start, int64_t* end,
+                            uint64_t* cnt);
+hipError_t launch_huff_sync(hipStream_t st, int nseg, const HuffSeg* segs, const HuffDecGroup* grp,
+                            const uint64_t* words, const int2* lut, const int4* nodes, int64_t* start,
+                            const int64_t* end_in, int64_t* end_out, uint64_t* cnt, unsigned* changed);
+hipError_t launch_huff_decode_write(hipStream_t st, int nseg, const HuffSeg* segs, const HuffDecGroup* grp,
+                                    const uint64_t* words, const int2* lut, const int4* nodes, const int64_t* start,
+                                    const uint64_t* off, int32_t* table, unsigned* err);
+hipError_t launch_fill_i32(hipStream_t st, int32_t* dst, int64_t n, int32_t v);
+
 // ---- context services (skml_api.cpp) ----
 hipStream_t ctx_stream(skml_ctx* c);
 int ctx_device(skml_ctx* c);

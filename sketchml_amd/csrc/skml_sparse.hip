@@ -1213,4 +1213,154 @@ hipError_t launch_huff_write(hipStream_t st, const int32_t* table, int64_t ncell
     return hipGetLastError();
 }
 
+// =============================================================================================
+// HuffmanEncoder.decode (binary/HuffmanEncoder.java:127-166) of MinMaxSketch tables, the read
+// side of GroupedMinMaxSketch.readObject.  The stream has no sync points, so it is decoded
+// speculatively in parallel: every segment of kHuffSeg bits starts decoding at its nominal
+// boundary; rounds of k_huff_sync then restart each segment at the true end of its predecessor
+// until no start changes (prefix codes resynchronise within a few codewords); the per-segment
+// symbol counts are scanned into table offsets and k_huff_write decodes again, writing cells.
+// Codes are read MSB-first from BitSet words (bit i = word[i >> 6] >> (i & 63)), looked up in a
+// 2^12-entry table per group, and codes longer than 12 bits finish with a walk over tree nodes.
+// =============================================================================================
+__device__ __forceinline__ uint32_t huff_peek32(const uint64_t* __restrict__ w, int64_t nwords, int64_t pos) {
+    const int64_t wi = pos >> 6;
+    const int sh = (int)(pos & 63);
+    const uint64_t w0 = wi < nwords ? w[wi] : 0ull;  // BitSet.toLongArray trimmed zero words: read 0
+    const uint64_t w1 = wi + 1 < nwords ? w[wi + 1] : 0ull;
+    const uint64_t lo = sh ? ((w0 >> sh) | (w1 << (64 - sh))) : w0;
+    return __brev((uint32_t)lo);  // stream bit `pos` becomes bit 31
+}
+
+__device__ __forceinline__ int32_t huff_symbol(const HuffDecGroup& gr, const uint64_t* __restrict__ words,
+                                               const int2* __restrict__ lut, const int4* __restrict__ nodes,
+                                               int64_t& pos) {
+    const uint64_t* w = words + gr.word0;
+    const uint32_t u = huff_peek32(w, gr.nwords, pos);
+    const int2 e = lut[(size_t)gr.lut_row * kHuffLutSize + (u >> (32 - kHuffLutBits))];
+    if (e.y > 0) {
+        pos += e.y;
+        return e.x;
+    }
+    int node = e.x;  // a code longer than the table: walk the tree from depth kHuffLutBits
+    int64_t p = pos + kHuffLutBits;
+    int4 nd = nodes[node];
+    while (nd.x >= 0) {
+        const uint32_t b = huff_peek32(w, gr.nwords, p) >> 31;
+        p++;
+        node = b ? nd.y : nd.x;
+        nd = nodes[node];
+    }
+    pos = p;
+    return nd.z;
+}
+
+__global__ __launch_bounds__(256) void k_huff_spec(int nseg, const HuffSeg* __restrict__ segs,
+                                                   const HuffDecGroup* __restrict__ grp,
+                                                   const uint64_t* __restrict__ words, const int2* __restrict__ lut,
+                                                   const int4* __restrict__ nodes, int64_t* __restrict__ start,
+                                                   int64_t* __restrict__ end, uint64_t* __restrict__ cnt) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nseg) return;
+    const HuffSeg sg = segs[i];
+    int64_t pos = start[i];
+    uint64_t c = 0;
+    if (!sg.last) {
+        const HuffDecGroup gr = grp[sg.g];
+        while (pos < sg.lim) {
+            (void)huff_symbol(gr, words, lut, nodes, pos);
+            c++;
+        }
+    }
+    end[i] = pos;
+    cnt[i] = c;
+}
+
+__global__ __launch_bounds__(256) void k_huff_sync(int nseg, const HuffSeg* __restrict__ segs,
+                                                   const HuffDecGroup* __restrict__ grp,
+                                                   const uint64_t* __restrict__ words, const int2* __restrict__ lut,
+                                                   const int4* __restrict__ nodes, int64_t* __restrict__ start,
+                                                   const int64_t* __restrict__ end_in, int64_t* __restrict__ end_out,
+                                                   uint64_t* __restrict__ cnt, unsigned* __restrict__ changed) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nseg) return;
+    const HuffSeg sg = segs[i];
+    const int64_t ns = sg.first ? start[i] : end_in[i - 1];
+    if (ns == start[i]) {
+        end_out[i] = end_in[i];
+        return;
+    }
+    start[i] = ns;
+    int64_t pos = ns;
+    uint64_t c = 0;
+    if (!sg.last) {
+        const HuffDecGroup gr = grp[sg.g];
+        while (pos < sg.lim) {
+            (void)huff_symbol(gr, words, lut, nodes, pos);
+            c++;
+        }
+    }
+    end_out[i] = pos;
+    cnt[i] = c;
+    atomicOr(changed, 1u);
+}
+
+// off: exclusive scan of cnt (global); a group's cells start at its first segment's offset.
+__global__ __launch_bounds__(256) void k_huff_write(int nseg, const HuffSeg* __restrict__ segs,
+                                                    const HuffDecGroup* __restrict__ grp,
+                                                    const uint64_t* __restrict__ words, const int2* __restrict__ lut,
+                                                    const int4* __restrict__ nodes, const int64_t* __restrict__ start,
+                                                    const uint64_t* __restrict__ off, int32_t* __restrict__ table,
+                                                    unsigned* __restrict__ err) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nseg) return;
+    const HuffSeg sg = segs[i];
+    const HuffDecGroup gr = grp[sg.g];
+    const int64_t o = (int64_t)(off[i] - off[gr.seg0]);
+    const int64_t m = sg.last ? gr.size - o : (int64_t)(off[i + 1] - off[i]);
+    if (o < 0 || m < 0 || o + m > gr.size) {
+        atomicOr(err, 1u);
+        return;
+    }
+    int32_t* dst = table + gr.tab_off + o;
+    int64_t pos = start[i];
+    for (int64_t k = 0; k < m; k++) dst[k] = huff_symbol(gr, words, lut, nodes, pos);
+}
+
+__global__ __launch_bounds__(256) void k_fill_i32(int32_t* __restrict__ dst, int64_t n, int32_t v) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        dst[i] = v;
+}
+
+hipError_t launch_huff_spec(hipStream_t st, int nseg, const HuffSeg* segs, const HuffDecGroup* grp,
+                            const uint64_t* words, const int2* lut, const int4* nodes, int64_t* start, int64_t* end,
+                            uint64_t* cnt) {
+    if (nseg <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_huff_spec, dim3((nseg + 255) / 256), dim3(256), 0, st, nseg, segs, grp, words, lut, nodes,
+                       start, end, cnt);
+    return hipGetLastError();
+}
+hipError_t launch_huff_sync(hipStream_t st, int nseg, const HuffSeg* segs, const HuffDecGroup* grp,
+                            const uint64_t* words, const int2* lut, const int4* nodes, int64_t* start,
+                            const int64_t* end_in, int64_t* end_out, uint64_t* cnt, unsigned* changed) {
+    if (nseg <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_huff_sync, dim3((nseg + 255) / 256), dim3(256), 0, st, nseg, segs, grp, words, lut, nodes,
+                       start, end_in, end_out, cnt, changed);
+    return hipGetLastError();
+}
+hipError_t launch_huff_decode_write(hipStream_t st, int nseg, const HuffSeg* segs, const HuffDecGroup* grp,
+                                    const uint64_t* words, const int2* lut, const int4* nodes, const int64_t* start,
+                                    const uint64_t* off, int32_t* table, unsigned* err) {
+    if (nseg <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_huff_write, dim3((nseg + 255) / 256), dim3(256), 0, st, nseg, segs, grp, words, lut, nodes,
+                       start, off, table, err);
+    return hipGetLastError();
+}
+hipError_t launch_fill_i32(hipStream_t st, int32_t* dst, int64_t n, int32_t v) {
+    if (n <= 0) return hipSuccess;
+    const int64_t g = std::min<int64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_fill_i32, dim3((unsigned)g), dim3(256), 0, st, dst, n, v);
+    return hipGetLastError();
+}
+
 }  // namespace skml

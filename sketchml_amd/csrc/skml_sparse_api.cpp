@@ -265,6 +265,7 @@ struct skml_sparse {
     std::vector<int64_t> huff_bit0, huff_bits;      // per group stream range
     uint64_t* huff_words = nullptr;
     int64_t n_huff_words = 0;
+    std::vector<uint8_t> wire;  // the serialised field stream (built once; the payload is immutable)
 };
 
 namespace {
@@ -509,6 +510,40 @@ int decode_groups(skml_ctx* c, const skml_sparse* s, int32_t* gk, int32_t* gb, b
     return SKML_OK;
 }
 
+// Sort.merge (util/Sort.java:362-379) of the groups' (key, bin) runs: rounds of pairwise stable
+// merges on the device; keys and bins land in keys_out / bins_out.
+int merge_groups(skml_ctx* c, const skml_sparse* s, int32_t* gk, int32_t* gb, int32_t* keys_out,
+                 int32_t* bins_out) {
+    hipStream_t st = ctx_stream(c);
+    const int64_t n = s->nnz;
+    const SpGroups& G = s->g;
+    int32_t* k1 = scratch<int32_t>(c, kSlotK1, (size_t)n);
+    int32_t* b1 = scratch<int32_t>(c, kSlotB1, (size_t)n);
+    if (!k1 || !b1) return sfail(SKML_E_OOM, "merge scratch");
+    std::vector<int64_t> rs(G.gstart, G.gstart + G.G + 1);
+    int64_t* rs_dev = reinterpret_cast<int64_t*>(ctx_scratch(c, kSlotStatus, sizeof(int64_t) * 2 * (kMaxGroups + 1)));
+    if (!rs_dev) return sfail(SKML_E_OOM, "run offsets");
+    int32_t *kin = gk, *bin = gb, *kout = k1, *bout = b1;
+    int slot = 0;
+    while (rs.size() > 2) {
+        int64_t* rd = rs_dev + (slot & 1) * (kMaxGroups + 1);
+        SP_HIP(hipMemcpyAsync(rd, rs.data(), sizeof(int64_t) * rs.size(), hipMemcpyHostToDevice, st));
+        SP_HIP(launch_merge_round(st, kin, bin, kout, bout, rd, (int)rs.size() - 1, n));
+        std::vector<int64_t> nx;
+        for (size_t i = 0; i < rs.size(); i += 2) nx.push_back(rs[i]);
+        if (nx.back() != rs.back()) nx.push_back(rs.back());
+        rs.swap(nx);
+        std::swap(kin, kout);
+        std::swap(bin, bout);
+        // the H2D of the next round's offsets must not overwrite the buffer still in use
+        slot++;
+        SP_HIP(hipStreamSynchronize(st));
+    }
+    SP_HIP(hipMemcpyAsync(keys_out, kin, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToDevice, st));
+    if (bins_out != bin) SP_HIP(hipMemcpyAsync(bins_out, bin, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToDevice, st));
+    return SKML_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -569,34 +604,14 @@ int skml_sparse_decode_f32(skml_ctx* c, const skml_sparse* s, int32_t* keys_dev,
     if (!keys_dev || !vals_dev) return sfail(SKML_E_ARG, "keys/vals are NULL");
     SP_HIP(hipSetDevice(ctx_device(c)));
     hipStream_t st = ctx_stream(c);
+    if (s->qvalues.empty()) return sfail(SKML_E_STATE, "quantValues are not set (deserialised without them)");
     int32_t* gk = scratch<int32_t>(c, kSlotGKeys, (size_t)n);
     int32_t* gb = scratch<int32_t>(c, kSlotGBins, (size_t)n);
-    int32_t* k1 = scratch<int32_t>(c, kSlotK1, (size_t)n);
     int32_t* b1 = scratch<int32_t>(c, kSlotB1, (size_t)n);
-    if (!gk || !gb || !k1 || !b1) return sfail(SKML_E_OOM, "decode scratch");
+    if (!gk || !gb || !b1) return sfail(SKML_E_OOM, "decode scratch");
     if (int e = decode_groups(c, s, gk, gb, true)) return e;
-    // Sort.merge over the groups: rounds of pairwise stable merges
-    const SpGroups& G = s->g;
-    std::vector<int64_t> rs(G.gstart, G.gstart + G.G + 1);
-    int64_t* rs_dev = reinterpret_cast<int64_t*>(ctx_scratch(c, kSlotStatus, sizeof(int64_t) * 2 * (kMaxGroups + 1)));
-    if (!rs_dev) return sfail(SKML_E_OOM, "run offsets");
-    int32_t *kin = gk, *bin = gb, *kout = k1, *bout = b1;
-    int slot = 0;
-    while (rs.size() > 2) {
-        int64_t* rd = rs_dev + (slot & 1) * (kMaxGroups + 1);
-        SP_HIP(hipMemcpyAsync(rd, rs.data(), sizeof(int64_t) * rs.size(), hipMemcpyHostToDevice, st));
-        SP_HIP(launch_merge_round(st, kin, bin, kout, bout, rd, (int)rs.size() - 1, n));
-        std::vector<int64_t> nx;
-        for (size_t i = 0; i < rs.size(); i += 2) nx.push_back(rs[i]);
-        if (nx.back() != rs.back()) nx.push_back(rs.back());
-        rs.swap(nx);
-        std::swap(kin, kout);
-        std::swap(bin, bout);
-        // the H2D of the next round's offsets must not overwrite the buffer still in use
-        slot++;
-        SP_HIP(hipStreamSynchronize(st));
-    }
-    SP_HIP(hipMemcpyAsync(keys_dev, kin, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToDevice, st));
+    if (int e = merge_groups(c, s, gk, gb, keys_dev, b1)) return e;
+    const int32_t* bin = b1;
     double* qv = reinterpret_cast<double*>(ctx_scratch(c, kSlotCells, sizeof(double) * s->qvalues.size()));
     if (!qv) return sfail(SKML_E_OOM, "value table");
     SP_HIP(hipMemcpyAsync(qv, s->qvalues.data(), sizeof(double) * s->qvalues.size(), hipMemcpyHostToDevice, st));
@@ -753,6 +768,15 @@ struct BeWriter {
         u(x, 8);
     }
     void byte(int v) { b.push_back((uint8_t)v); }
+    // a long[] body: big-endian words appended in one resize
+    void longs(const std::vector<uint64_t>& v) {
+        const size_t o = b.size();
+        b.resize(o + 8 * v.size());
+        for (size_t i = 0; i < v.size(); i++) {
+            const uint64_t be = __builtin_bswap64(v[i]);
+            std::memcpy(b.data() + o + 8 * i, &be, 8);
+        }
+    }
 };
 // BitSet.toLongArray of a device bit range (trailing zero words trimmed)
 int long_array(skml_ctx* c, const uint64_t* words, int64_t b0, int64_t nbits, std::vector<uint64_t>& out) {
@@ -771,11 +795,19 @@ int long_array(skml_ctx* c, const uint64_t* words, int64_t b0, int64_t nbits, st
 int skml_sparse_serialize(skml_ctx* c, const skml_sparse* cs, uint8_t* buf, size_t cap, size_t* written) {
     if (!c || !cs) return sfail(SKML_E_ARG, "bad serialise arguments");
     SP_HIP(hipSetDevice(ctx_device(c)));
-    skml_sparse* s = const_cast<skml_sparse*>(cs);  // the Huffman streams are a lazily built cache
+    skml_sparse* s = const_cast<skml_sparse*>(cs);  // the Huffman streams and the bytes are lazily built caches
+    if (!s->wire.empty()) {
+        if (written) *written = s->wire.size();
+        if (!buf) return SKML_OK;
+        if (cap < s->wire.size()) return sfail(SKML_E_ARG, "buffer capacity %zu < %zu", cap, s->wire.size());
+        std::memcpy(buf, s->wire.data(), s->wire.size());
+        return SKML_OK;
+    }
     if (int e = build_huffman(c, s)) return e;
     static const int32_t kBkdrSeed[8] = {0, 0, 0, 31, 131, 267, 1313, 13131};
     const SpGroups& G = s->g;
     BeWriter w;
+    w.b.reserve((size_t)(8 * (s->n_flag_words + s->n_delta_words + s->n_huff_words) + 4096));
     w.i32(G.G);
     w.i32(G.rows);
     w.f64(s->params.col_ratio);
@@ -803,7 +835,7 @@ int skml_sparse_serialize(skml_ctx* c, const skml_sparse* cs, uint8_t* buf, size
         }
         if (int e = long_array(c, s->huff_words, s->huff_bit0[(size_t)g], s->huff_bits[(size_t)g], longs)) return e;
         w.i32((int32_t)longs.size());
-        for (uint64_t l : longs) w.i64((int64_t)l);
+        w.longs(longs);
         w.i32(G.rows * G.cols[g]);
     }
     for (int g = 0; g < G.G; g++) {  // encoders
@@ -815,15 +847,450 @@ int skml_sparse_serialize(skml_ctx* c, const skml_sparse* cs, uint8_t* buf, size
         w.byte(G.kind[g] ? 1 : 0);
         if (int e = long_array(c, s->flag_words, G.fb[g], G.fb[g + 1] - G.fb[g], longs)) return e;
         w.i32((int32_t)longs.size());
-        for (uint64_t l : longs) w.i64((int64_t)l);
+        w.longs(longs);
         if (int e = long_array(c, s->delta_words, G.db[g], G.db[g + 1] - G.db[g], longs)) return e;
         w.i32((int32_t)longs.size());
-        for (uint64_t l : longs) w.i64((int64_t)l);
+        w.longs(longs);
     }
-    if (written) *written = w.b.size();
+    s->wire.swap(w.b);
+    if (written) *written = s->wire.size();
     if (!buf) return SKML_OK;
-    if (cap < w.b.size()) return sfail(SKML_E_ARG, "buffer capacity %zu < %zu", cap, w.b.size());
-    std::memcpy(buf, w.b.data(), w.b.size());
+    if (cap < s->wire.size()) return sfail(SKML_E_ARG, "buffer capacity %zu < %zu", cap, s->wire.size());
+    std::memcpy(buf, s->wire.data(), s->wire.size());
+    return SKML_OK;
+}
+
+namespace {
+struct BeReader {
+    const uint8_t* p;
+    size_t n, i = 0;
+    bool bad = false;
+    uint64_t u(int k) {
+        if (i + (size_t)k > n) {
+            bad = true;
+            i = n;
+            return 0;
+        }
+        uint64_t v = 0;
+        for (int j = 0; j < k; j++) v = (v << 8) | p[i++];
+        return v;
+    }
+    int32_t i32() { return (int32_t)(uint32_t)u(4); }
+    int64_t i64() { return (int64_t)u(8); }
+    double f64() {
+        const uint64_t x = u(8);
+        double d;
+        std::memcpy(&d, &x, 8);
+        return d;
+    }
+    int byte() { return (int)u(1); }
+    bool longs(std::vector<uint64_t>& v, size_t count) {
+        if (i + 8 * count > n) {
+            bad = true;
+            return false;
+        }
+        v.resize(count);
+        for (size_t k = 0; k < count; k++) {
+            uint64_t be;
+            std::memcpy(&be, p + i + 8 * k, 8);
+            v[k] = __builtin_bswap64(be);
+        }
+        i += 8 * count;
+        return true;
+    }
+};
+
+struct HuffGroupIn {
+    std::vector<HuffItem> items;
+    std::vector<uint64_t> longs;
+    int64_t size = 0;
+};
+
+// Sum of the nf-bit MSB-first fields (BinaryUtils.getBits order) in bits [0, nbits) of a BitSet:
+// sum over k of 2^(nf-1-k) * popcount of the bits at positions = k (mod nf).
+int64_t bit_fields_sum(const std::vector<uint64_t>& w, int64_t nbits, int nf) {
+    if (nf == 0 || nbits == 0) return 0;
+    int64_t sum = 0;
+    const int64_t nw = std::min<int64_t>((int64_t)w.size(), (nbits + 63) / 64);
+    for (int64_t i = 0; i < nw; i++) {
+        uint64_t word = w[(size_t)i];
+        const int64_t hi = nbits - i * 64;
+        if (hi < 64) word &= (1ull << hi) - 1ull;
+        const int phase = (int)((i * 64) % nf);
+        for (int k = 0; k < nf; k++) {
+            uint64_t mask = 0;
+            for (int b = (k - phase + nf) % nf; b < 64; b += nf) mask |= 1ull << b;
+            sum += (int64_t)__builtin_popcountll(word & mask) << (nf - 1 - k);
+        }
+    }
+    return sum;
+}
+
+// Bit length of `size` unary flags (ones closed by a zero); zeros past the stored words are the
+// trimmed tail of the BitSet.
+int64_t unary_flags_length(const std::vector<uint64_t>& w, int64_t size) {
+    if (size <= 0) return 0;
+    int64_t zeros = 0;
+    for (size_t i = 0; i < w.size(); i++) {
+        const int64_t z = 64 - __builtin_popcountll(w[i]);
+        if (zeros + z >= size) {
+            uint64_t inv = ~w[i];
+            for (int64_t k = zeros; k < size - 1; k++) inv &= inv - 1;  // drop the zeros before the last one
+            return (int64_t)i * 64 + __builtin_ctzll(inv) + 1;
+        }
+        zeros += z;
+    }
+    return (int64_t)w.size() * 64 + (size - zeros);
+}
+
+// out[bit0, bit0 + nbits) = src[0, nbits) (src words past its end read as zero; out is zeroed).
+void put_bit_range(std::vector<uint64_t>& out, int64_t bit0, const std::vector<uint64_t>& src, int64_t nbits) {
+    const int sh = (int)(bit0 & 63);
+    const int64_t w0 = bit0 >> 6;
+    const int64_t nsrc = std::min<int64_t>((int64_t)src.size(), (nbits + 63) / 64);
+    for (int64_t i = 0; i < nsrc; i++) {
+        uint64_t v = src[(size_t)i];
+        const int64_t hi = nbits - i * 64;
+        if (hi < 64) v &= (1ull << hi) - 1ull;
+        out[(size_t)(w0 + i)] |= v << sh;
+        if (sh && (size_t)(w0 + i + 1) < out.size()) out[(size_t)(w0 + i + 1)] |= v >> (64 - sh);
+    }
+}
+
+// Decode tables of one group's HuffmanEncoder items (HuffmanEncoder.java:131-152 builds the same
+// tree): codes of <= kHuffLutBits bits fill their LUT ranges, longer codes end in tree nodes.
+int huff_tables(const std::vector<HuffItem>& items, int node_base, std::vector<int2>& lut,
+                std::vector<int4>& nodes) {
+    struct N {
+        int left = -1, right = -1, value = 0;
+        bool leaf = false;
+    };
+    const size_t l0 = lut.size();
+    lut.resize(l0 + kHuffLutSize, int2{0, 0});
+    std::vector<char> set(kHuffLutSize, 0);
+    std::vector<int> prefix_node(kHuffLutSize, -1);  // subtree root of a long-code prefix
+    std::vector<N> t;
+    for (const HuffItem& it : items) {
+        if (it.nbits <= 0 || it.nbits > 31) return sfail(SKML_E_ARG, "Huffman code of %d bits", it.nbits);
+        const uint32_t code = (uint32_t)it.bits;
+        if (it.nbits <= kHuffLutBits) {
+            const uint32_t lo = code << (kHuffLutBits - it.nbits), hi = (code + 1) << (kHuffLutBits - it.nbits);
+            if (hi > (uint32_t)kHuffLutSize) return sfail(SKML_E_ARG, "Huffman code wider than its length");
+            for (uint32_t k = lo; k < hi; k++) {
+                if (set[k]) return sfail(SKML_E_ARG, "Huffman codes are not prefix-free");
+                set[k] = 1;
+                lut[l0 + k] = int2{it.value, it.nbits};
+            }
+            continue;
+        }
+        const uint32_t pre = code >> (it.nbits - kHuffLutBits);
+        if (pre >= (uint32_t)kHuffLutSize) return sfail(SKML_E_ARG, "Huffman code wider than its length");
+        int node = prefix_node[pre];
+        if (node < 0) {
+            if (set[pre]) return sfail(SKML_E_ARG, "Huffman codes are not prefix-free");
+            node = (int)t.size();
+            t.push_back(N());
+            prefix_node[pre] = node;
+            set[pre] = 1;
+            lut[l0 + pre] = int2{node_base + node, -1};
+        }
+        for (int b = it.nbits - kHuffLutBits - 1; b >= 0; b--) {
+            if (t[(size_t)node].leaf) return sfail(SKML_E_ARG, "Huffman codes are not prefix-free");
+            const bool one = (code >> b) & 1u;
+            int child = one ? t[(size_t)node].right : t[(size_t)node].left;
+            if (child < 0) {
+                child = (int)t.size();
+                t.push_back(N());
+                if (one) t[(size_t)node].right = child;
+                else t[(size_t)node].left = child;
+            }
+            node = child;
+        }
+        N& leaf = t[(size_t)node];
+        if (leaf.leaf || leaf.left >= 0 || leaf.right >= 0) return sfail(SKML_E_ARG, "Huffman codes are not prefix-free");
+        leaf.leaf = true;
+        leaf.value = it.value;
+    }
+    for (int k = 0; k < kHuffLutSize; k++)
+        if (!set[k]) return sfail(SKML_E_ARG, "Huffman tree is not full");
+    for (const N& nd : t) {
+        if (nd.leaf) {
+            nodes.push_back(int4{-1, -1, nd.value, 0});
+        } else {
+            if (nd.left < 0 || nd.right < 0) return sfail(SKML_E_ARG, "Huffman tree is not full");
+            nodes.push_back(int4{node_base + nd.left, node_base + nd.right, 0, 0});
+        }
+    }
+    return SKML_OK;
+}
+}  // namespace
+
+// GroupedMinMaxSketch.readObject (GroupedMinMaxSketch.java:161-172), MinMaxSketch.readObject
+// (MinMaxSketch.java:99-108), HuffmanEncoder.readObject + decode (HuffmanEncoder.java:127-166,
+// 193-207) and DeltaAdaptiveEncoder.readObject (DeltaAdaptiveEncoder.java:172-188): the stream
+// skml_sparse_serialize writes, back into a device payload that restore/decode accept.
+int skml_sparse_deserialize(skml_ctx* c, const uint8_t* buf, size_t len, const double* qvalues, int32_t nvalues,
+                            skml_sparse** out) {
+    if (!c || !buf || !out || nvalues < 0 || (nvalues > 0 && !qvalues))
+        return sfail(SKML_E_ARG, "bad deserialise arguments");
+    *out = nullptr;
+    SP_HIP(hipSetDevice(ctx_device(c)));
+    hipStream_t st = ctx_stream(c);
+    BeReader r{buf, len};
+    skml_sparse* s = new skml_sparse();
+    s->device = ctx_device(c);
+    auto bail = [&](int e) {
+        sparse_release(s);
+        return e;
+    };
+    SpGroups& G = s->g;
+    G.G = r.i32();
+    G.rows = r.i32();
+    s->params.col_ratio = r.f64();
+    G.bin_num = r.i32();
+    G.zero = r.i32();
+    if (r.bad || G.G < 1 || G.G > kMaxGroups || G.rows < 0 || G.rows > kMaxRows || G.bin_num < 1)
+        return bail(sfail(SKML_E_ARG, "malformed GroupedMinMaxSketch stream (groups %d rows %d bins %d)", G.G, G.rows,
+                          G.bin_num));
+    s->params.group_num = G.G;
+    s->params.row_num = G.rows;
+    s->params.bin_num = G.bin_num;
+    G.fill = mm_cmp(INT32_MIN, INT32_MAX, G.zero) <= 0 ? INT32_MIN : INT32_MAX;
+    std::vector<HuffGroupIn> hg((size_t)G.G);
+    std::vector<char> present((size_t)G.G, 0);
+    int64_t cells = 0;
+    for (int g = 0; g < G.G; g++) {  // MinMaxSketch objects
+        present[(size_t)g] = (char)r.byte();
+        if (!present[(size_t)g]) continue;
+        const int32_t rows = r.i32(), cols = r.i32(), zero = r.i32();
+        if (rows != G.rows || cols < 0 || zero != G.zero) return bail(sfail(SKML_E_ARG, "malformed MinMaxSketch %d", g));
+        G.cols[g] = cols;
+        for (int k = 0; k < rows; k++) {
+            G.hash_ids[g][k] = r.i32();
+            (void)r.i32();  // hash size (= cols)
+            (void)r.i32();  // BKDR seed (a function of the hash id)
+            if (G.hash_ids[g][k] < 0 || G.hash_ids[g][k] > 7) return bail(sfail(SKML_E_ARG, "bad hash id"));
+        }
+        HuffGroupIn& h = hg[(size_t)g];
+        const int32_t ni = r.i32();
+        if (ni < 0 || (size_t)ni * 12 > len) return bail(sfail(SKML_E_ARG, "malformed Huffman items"));
+        h.items.resize((size_t)ni);
+        for (auto& it : h.items) {
+            it.value = r.i32();
+            it.bits = r.i32();
+            it.nbits = r.i32();
+        }
+        const int32_t nl = r.i32();
+        if (nl < 0 || !r.longs(h.longs, (size_t)nl)) return bail(sfail(SKML_E_ARG, "malformed Huffman bit set"));
+        h.size = r.i32();
+        if (h.size != (int64_t)rows * cols) return bail(sfail(SKML_E_ARG, "Huffman size %lld != rows*cols", (long long)h.size));
+        G.tab_off[g] = cells;
+        cells += h.size;
+    }
+    // DeltaAdaptiveEncoder objects.  toLongArray dropped each BitSet's trailing zero words, but
+    // the decode kernels index one contiguous stream per kind, so every group's exact bit lengths
+    // are recovered from the flags first: fixed-width flags take size * nf bits; unary flags end
+    // at the size-th zero; the deltas take bpi * sum(interval counts) bits.
+    std::vector<std::vector<uint64_t>> flags((size_t)G.G), deltas((size_t)G.G);
+    std::vector<int64_t> flen((size_t)G.G, 0), dlen((size_t)G.G, 0);
+    int64_t n = 0, fbits = 0, dbits = 0;
+    int32_t k1 = 0;
+    for (int g = 0; g < G.G; g++) {
+        G.gstart[g] = n;
+        G.kind1_before[g] = k1;
+        G.fb[g] = fbits;
+        G.db[g] = dbits;
+        const int pres = r.byte();
+        if (pres != present[(size_t)g]) return bail(sfail(SKML_E_ARG, "sketch / encoder presence mismatch in group %d", g));
+        if (!pres) {
+            G.m[g] = 1;
+            G.kind[g] = 0;
+            continue;
+        }
+        const int32_t size = r.i32();
+        const int32_t m = r.i32();
+        G.m[g] = m;
+        G.kind[g] = r.byte() ? 1 : 0;
+        if (size < 0 || (m != 1 && m != 2 && m != 4 && m != 8 && m != 16))
+            return bail(sfail(SKML_E_ARG, "malformed DeltaAdaptiveEncoder %d (numIntervals %d)", g, m));
+        for (auto* v : {&flags[(size_t)g], &deltas[(size_t)g]}) {
+            const int32_t nl = r.i32();
+            if (nl < 0 || !r.longs(*v, (size_t)nl)) return bail(sfail(SKML_E_ARG, "malformed BitSet"));
+        }
+        const int bpi = 32 / m;
+        int nf = 0;
+        while ((1 << (nf + 1)) <= m) nf++;  // floor(log2 m)
+        const std::vector<uint64_t>& fw = flags[(size_t)g];
+        int64_t ivsum;
+        if (!G.kind[g]) {
+            flen[(size_t)g] = (int64_t)size * nf;
+            ivsum = (int64_t)size + bit_fields_sum(fw, flen[(size_t)g], nf);
+        } else {
+            flen[(size_t)g] = unary_flags_length(fw, size);
+            ivsum = flen[(size_t)g] - size;  // each flag: iv ones and a closing zero
+        }
+        dlen[(size_t)g] = (int64_t)bpi * ivsum;
+        if ((int64_t)fw.size() > (flen[(size_t)g] + 63) / 64 ||
+            (int64_t)deltas[(size_t)g].size() > (dlen[(size_t)g] + 63) / 64)
+            return bail(sfail(SKML_E_ARG, "DeltaAdaptiveEncoder %d holds bits past its stream", g));
+        fbits += flen[(size_t)g];
+        dbits += dlen[(size_t)g];
+        if (G.kind[g]) k1 += size;
+        n += size;
+    }
+    G.gstart[G.G] = n;
+    G.fb[G.G] = fbits;
+    G.db[G.G] = dbits;
+    if (r.bad) return bail(sfail(SKML_E_ARG, "truncated GroupedMinMaxSketch stream"));
+    s->nnz = n;
+    s->ncells = cells;
+    s->flag_bits = fbits;
+    s->delta_bits = dbits;
+    s->n_flag_words = (fbits + 63) / 64 + 1;
+    s->n_delta_words = (dbits + 63) / 64 + 1;
+    s->hdr.magic = SKML_DENSE_MAGIC;
+    s->hdr.status = SKML_OK;
+    s->hdr.n = n;
+    s->hdr.bin_num = G.bin_num;
+    s->hdr.zero_idx = G.zero;
+    s->hdr.req_bins = G.bin_num;
+    s->hdr.code_bits = code_bits_for(G.bin_num);
+    s->qvalues.assign(qvalues, qvalues + nvalues);
+    // device: group table, the contiguous DeltaAdaptive streams, MinMax tables
+    if (hipMalloc(&s->g_dev, sizeof(SpGroups)) != hipSuccess ||
+        hipMalloc(&s->flag_words, sizeof(uint64_t) * (size_t)s->n_flag_words) != hipSuccess ||
+        hipMalloc(&s->delta_words, sizeof(uint64_t) * (size_t)s->n_delta_words) != hipSuccess ||
+        hipMalloc(&s->tables, sizeof(int32_t) * (size_t)std::max<int64_t>(cells, 1)) != hipSuccess)
+        return bail(sfail(SKML_E_OOM, "deserialised payload"));
+    {
+        std::vector<uint64_t> fw((size_t)s->n_flag_words, 0), dw((size_t)s->n_delta_words, 0);
+        for (int g = 0; g < G.G; g++) {
+            put_bit_range(fw, G.fb[g], flags[(size_t)g], flen[(size_t)g]);
+            put_bit_range(dw, G.db[g], deltas[(size_t)g], dlen[(size_t)g]);
+        }
+        SP_HIP(hipMemcpyAsync(s->flag_words, fw.data(), sizeof(uint64_t) * fw.size(), hipMemcpyHostToDevice, st));
+        SP_HIP(hipMemcpyAsync(s->delta_words, dw.data(), sizeof(uint64_t) * dw.size(), hipMemcpyHostToDevice, st));
+        SP_HIP(hipStreamSynchronize(st));
+    }
+    if (int e = upload_groups(c, s)) return bail(e);
+    // HuffmanEncoder.decode of every group's table
+    std::vector<HuffDecGroup> dg;
+    std::vector<HuffSeg> segs;
+    std::vector<int64_t> starts;
+    std::vector<int2> lut;
+    std::vector<int4> nodes;
+    std::vector<uint64_t> words;
+    for (int g = 0; g < G.G; g++) {
+        const HuffGroupIn& h = hg[(size_t)g];
+        if (!present[(size_t)g] || h.size == 0) continue;
+        if (h.items.empty()) return bail(sfail(SKML_E_ARG, "Huffman items missing in group %d", g));
+        if (h.items.size() == 1) {  // a one-symbol tree: zero-bit codes
+            SP_HIP(launch_fill_i32(st, s->tables + G.tab_off[g], h.size, h.items[0].value));
+            continue;
+        }
+        HuffDecGroup d;
+        d.word0 = (int64_t)words.size();
+        d.nwords = (int64_t)h.longs.size();
+        d.tab_off = G.tab_off[g];
+        d.size = h.size;
+        d.lut_row = (int32_t)(lut.size() / kHuffLutSize);
+        d.seg0 = (int32_t)segs.size();
+        std::vector<int4> gn;
+        if (int e = huff_tables(h.items, (int)nodes.size(), lut, gn)) return bail(e);
+        nodes.insert(nodes.end(), gn.begin(), gn.end());
+        words.insert(words.end(), h.longs.begin(), h.longs.end());
+        const int64_t bits = d.nwords * 64;
+        const int64_t nseg = std::max<int64_t>(1, (bits + kHuffSeg - 1) / kHuffSeg);
+        for (int64_t k = 0; k < nseg; k++) {
+            HuffSeg sg;
+            sg.g = (int32_t)dg.size();
+            sg.first = k == 0;
+            sg.last = k == nseg - 1;
+            sg.lim = (k + 1) * kHuffSeg;
+            segs.push_back(sg);
+            starts.push_back(k * kHuffSeg);
+        }
+        dg.push_back(d);
+    }
+    const int ns = (int)segs.size();
+    if (ns > 0) {
+        if (nodes.empty()) nodes.push_back(int4{-1, -1, 0, 0});
+        words.push_back(0);
+        // one device block: groups, segments, starts, 2 x ends, counts (+1 for the scan total),
+        // flags, LUT, nodes, words
+        const size_t b_grp = align_up(sizeof(HuffDecGroup) * dg.size(), 256);
+        const size_t b_seg = align_up(sizeof(HuffSeg) * (size_t)ns, 256);
+        const size_t b_i64 = align_up(sizeof(int64_t) * (size_t)ns, 256);
+        const size_t b_cnt = align_up(sizeof(uint64_t) * (size_t)(ns + 1), 256);
+        const size_t b_lut = align_up(sizeof(int2) * lut.size(), 256);
+        const size_t b_nod = align_up(sizeof(int4) * nodes.size(), 256);
+        const size_t b_wrd = align_up(sizeof(uint64_t) * words.size(), 256);
+        const size_t total = b_grp + b_seg + 3 * b_i64 + b_cnt + 256 + b_lut + b_nod + b_wrd;
+        char* blk = nullptr;
+        SP_HIP(hipMalloc(&blk, total));
+        auto run = [&]() -> int {
+            char* q = blk;
+            auto* d_grp = (HuffDecGroup*)q; q += b_grp;
+            auto* d_seg = (HuffSeg*)q; q += b_seg;
+            auto* d_start = (int64_t*)q; q += b_i64;
+            auto* d_ea = (int64_t*)q; q += b_i64;
+            auto* d_eb = (int64_t*)q; q += b_i64;
+            auto* d_cnt = (uint64_t*)q; q += b_cnt;
+            auto* d_flag = (unsigned*)q; q += 256;
+            auto* d_lut = (int2*)q; q += b_lut;
+            auto* d_nod = (int4*)q; q += b_nod;
+            auto* d_wrd = (uint64_t*)q;
+            SP_HIP(hipMemcpyAsync(d_grp, dg.data(), sizeof(HuffDecGroup) * dg.size(), hipMemcpyHostToDevice, st));
+            SP_HIP(hipMemcpyAsync(d_seg, segs.data(), sizeof(HuffSeg) * segs.size(), hipMemcpyHostToDevice, st));
+            SP_HIP(hipMemcpyAsync(d_start, starts.data(), sizeof(int64_t) * starts.size(), hipMemcpyHostToDevice, st));
+            SP_HIP(hipMemcpyAsync(d_lut, lut.data(), sizeof(int2) * lut.size(), hipMemcpyHostToDevice, st));
+            SP_HIP(hipMemcpyAsync(d_nod, nodes.data(), sizeof(int4) * nodes.size(), hipMemcpyHostToDevice, st));
+            SP_HIP(hipMemcpyAsync(d_wrd, words.data(), sizeof(uint64_t) * words.size(), hipMemcpyHostToDevice, st));
+            SP_HIP(hipMemsetAsync(d_cnt, 0, b_cnt, st));
+            SP_HIP(launch_huff_spec(st, ns, d_seg, d_grp, d_wrd, d_lut, d_nod, d_start, d_ea, d_cnt));
+            // resynchronise until every segment starts where its predecessor ends
+            for (int round = 0;; round++) {
+                if (round > ns + 1) return sfail(SKML_E_ARG, "Huffman stream does not resynchronise");
+                SP_HIP(hipMemsetAsync(d_flag, 0, sizeof(unsigned), st));
+                SP_HIP(launch_huff_sync(st, ns, d_seg, d_grp, d_wrd, d_lut, d_nod, d_start, d_ea, d_eb, d_cnt, d_flag));
+                unsigned changed = 0;
+                if (int e = sync_to_host(c, &changed, d_flag, sizeof(unsigned))) return e;
+                std::swap(d_ea, d_eb);
+                if (!changed) break;
+            }
+            SP_HIP(launch_scan_cols(st, d_cnt, ns, 1));  // exclusive scan: symbol offsets
+            SP_HIP(hipMemsetAsync(d_flag, 0, sizeof(unsigned), st));
+            SP_HIP(launch_huff_decode_write(st, ns, d_seg, d_grp, d_wrd, d_lut, d_nod, d_start, d_cnt, s->tables,
+                                            d_flag));
+            unsigned err = 0;
+            if (int e = sync_to_host(c, &err, d_flag, sizeof(unsigned))) return e;
+            if (err) return sfail(SKML_E_ARG, "Huffman stream holds a different number of symbols than size");
+            return SKML_OK;
+        };
+        const int e = run();
+        (void)hipStreamSynchronize(st);
+        (void)hipFree(blk);
+        if (e) return bail(e);
+    }
+    SP_HIP(hipStreamSynchronize(st));
+    *out = s;
+    return SKML_OK;
+}
+
+// GroupedMinMaxSketch.restore (GroupedMinMaxSketch.java:123-146) + Sort.merge: keys and int32 bins.
+int skml_sparse_restore_bins(skml_ctx* c, const skml_sparse* s, int32_t* keys_dev, int32_t* bins_dev) {
+    if (!c || !s) return sfail(SKML_E_ARG, "bad restore arguments");
+    const int64_t n = s->nnz;
+    if (n == 0) return SKML_OK;
+    if (!keys_dev || !bins_dev) return sfail(SKML_E_ARG, "keys/bins are NULL");
+    SP_HIP(hipSetDevice(ctx_device(c)));
+    hipStream_t st = ctx_stream(c);
+    int32_t* gk = scratch<int32_t>(c, kSlotGKeys, (size_t)n);
+    int32_t* gb = scratch<int32_t>(c, kSlotGBins, (size_t)n);
+    if (!gk || !gb) return sfail(SKML_E_OOM, "restore scratch");
+    if (int e = decode_groups(c, s, gk, gb, true)) return e;
+    if (int e = merge_groups(c, s, gk, gb, keys_dev, bins_dev)) return e;
+    SP_HIP(hipStreamSynchronize(st));
     return SKML_OK;
 }
 

@@ -99,10 +99,36 @@ class SparsePayload:
         """GroupedMinMaxSketch.writeObject field stream (layout in DESIGN.md / skml_sparse_serialize)."""
         need = C.c_size_t()
         check(_lib.lib.skml_sparse_serialize(self._ctx().handle, self.handle, None, 0, C.byref(need)), "serialize")
-        buf = (C.c_uint8 * max(need.value, 1))()
-        check(_lib.lib.skml_sparse_serialize(self._ctx().handle, self.handle, buf, need.value, C.byref(need)),
-              "serialize")
-        return bytes(buf[: need.value])
+        buf = np.empty(max(need.value, 1), dtype=np.uint8)
+        check(_lib.lib.skml_sparse_serialize(self._ctx().handle, self.handle, buf.ctypes.data_as(_lib.u8p),
+                                             need.value, C.byref(need)), "serialize")
+        return buf[: need.value].tobytes()
+
+    def restore_bins(self):
+        """GroupedMinMaxSketch.restore (GroupedMinMaxSketch.java:123-146): device keys and int32
+        bins in Sort.merge order."""
+        n = self.nnz()
+        dev = torch.device("cuda", self.device)
+        keys = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        bins = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        check(_lib.lib.skml_sparse_restore_bins(self._ctx().handle, self.handle, C.c_void_p(keys.data_ptr()),
+                                                C.c_void_p(bins.data_ptr())), "sparse_restore")
+        return keys[:n], bins[:n]
+
+    @classmethod
+    def deserialize(cls, data: bytes, quant_values=None, device=None) -> "SparsePayload":
+        """GroupedMinMaxSketch.readObject of the stream serialize() writes; quant_values (the
+        SparseVectorCompressor.quantValues doubles) make restore() return values as well."""
+        dev = torch.cuda.current_device() if device is None else torch.device(device).index
+        arr = np.frombuffer(bytes(data), dtype=np.uint8).copy()
+        qv = None if quant_values is None else np.ascontiguousarray(quant_values, dtype=np.float64)
+        h = C.c_void_p()
+        check(_lib.lib.skml_sparse_deserialize(
+            get_context(dev).handle, arr.ctypes.data_as(_lib.u8p), len(arr),
+            qv.ctypes.data_as(_lib.dblp) if qv is not None else None, 0 if qv is None else len(qv), C.byref(h)),
+            "readObject")
+        rows = int.from_bytes(arr[4:8].tobytes(), "big", signed=True) if len(arr) >= 8 else 0
+        return cls(h, dev, rows)
 
     def times_by(self, x: float) -> None:
         check(_lib.lib.skml_sparse_times_by(self.handle, float(x)), "sparse_times_by")
@@ -191,13 +217,26 @@ class GroupedMinMaxSketch:
         self.zeroValue = hdr.zero_idx
 
     def restore(self):
-        return self.payload.restore()
+        """GroupedMinMaxSketch.restore (GroupedMinMaxSketch.java:123-146): (keys, int32 bins)."""
+        return self.payload.restore_bins()
 
     def getGroup(self, g: int) -> dict:
         return self.payload.group(g)
 
     def writeObject(self) -> bytes:
         return self.payload.serialize()
+
+    @classmethod
+    def readObject(cls, data: bytes, device=None) -> "GroupedMinMaxSketch":
+        """GroupedMinMaxSketch.readObject (GroupedMinMaxSketch.java:161-172); restore() then gives
+        (keys, bins) like the reference's restore()."""
+        pl = SparsePayload.deserialize(data, None, device)
+        head = np.frombuffer(bytes(data[:28]), dtype=">i4", count=2)
+        sk = cls(int(head[0]), int(head[1]))
+        sk.colRatio = float(np.frombuffer(bytes(data[8:16]), dtype=">f8")[0])
+        sk.binNum, sk.zeroValue = (int(v) for v in np.frombuffer(bytes(data[16:24]), dtype=">i4"))
+        sk.payload = pl
+        return sk
 
 
 class DeltaAdaptiveEncoder:
@@ -295,7 +334,9 @@ class SparseVectorCompressor:
         self._compress(keys, values, False)
 
     def decompressSparse(self):
-        return self.mmSketches.restore()
+        """SparseVectorCompressor.decompressSparse (SparseVectorCompressor.java:118-126): keys and
+        quantValues[bins] (fp32 on the device)."""
+        return self.mmSketches.payload.restore()
 
     def decompressDense(self) -> torch.Tensor:
         """Dense array of length maxKey + 1 (SparseVectorCompressor.java:106-114)."""

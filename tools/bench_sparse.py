@@ -50,6 +50,15 @@ def main():
     t_e2e, pl2 = timed(lambda: sk.encode_dense_as_sparse(x, 256, 8, 2, 0.3, 3, 3), a.reps)
     t_decode, (rk, rv) = timed(lambda: pl.restore(), a.reps)
     ok = bool(torch.equal(rk, keys))
+    fresh = sk.encode_sparse(keys, vals, 256, 8, 2, 0.3, 3, 3)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    stream = fresh.serialize()  # first call: Huffman tables + field stream
+    t_ser = time.perf_counter() - t0
+    qv = pl.values()
+    t_read, back = timed(lambda: sk.SparsePayload.deserialize(stream, qv), a.reps)
+    bk, bv = back.restore()
+    read_ok = bool(torch.equal(bk, keys)) and bool(torch.equal(bv, rv))
     rho = nnz / a.dim
     alg = (4.0 + rho * (8 + 4 + 8 + 2)) * a.dim
     line = {
@@ -58,7 +67,9 @@ def main():
         "config": {"workload": f"C3: {a.dim}-dim dense fp32, {a.density:.0%} nnz (Bernoulli), 256 bins, "
                                "8 groups, 2 rows, colRatio 0.3", "nnz": nnz},
         "ms": {"compact": round(t_compact * 1e3, 3), "encode_kv": round(t_encode * 1e3, 3),
-               "dense_to_payload": round(t_e2e * 1e3, 3), "decode": round(t_decode * 1e3, 3)},
+               "dense_to_payload": round(t_e2e * 1e3, 3), "decode": round(t_decode * 1e3, 3),
+               "write_object": round(t_ser * 1e3, 3), "read_object": round(t_read * 1e3, 3)},
+        "stream_bytes": len(stream), "read_object_roundtrip_exact": read_ok,
         "roofline": {"bound": "hbm", "alg_bytes": alg, "achieved_gbs": round(alg / t_e2e / 1e9, 1),
                      "peak": HBM, "frac": round(alg / t_e2e / 1e9 / HBM, 4)},
         "compact_gbs": round((4.0 * a.dim + 8.0 * nnz) / t_compact / 1e9, 1),
