@@ -52,7 +52,13 @@ typedef struct skml_params {
     double col_ratio;  /* sparse: MinMax columns / group size, default 0.3 */
     int64_t seed;      /* java.util.Random seed of the sketch's compaction stream */
     int64_t hash_seed; /* sparse: group g's hashes are drawn from Random(hash_seed + g) */
+    int32_t quant_type; /* sparse: the values' quantizer, SKML_QUANTILE (default) or SKML_UNIFORM
+                           (Quantizer.newQuantizer, base/Quantizer.java:126-136); the dense path
+                           has separate entry points per quantizer */
+    int32_t reserved;
 } skml_params;
+#define SKML_QUANTILE 0
+#define SKML_UNIFORM 1
 
 /* Device payload header (little-endian, 64 bytes) followed by double splits[req_bins-1],
  * padded to 256 bytes, then the packed codes (code_bits per element, LSB-first). */

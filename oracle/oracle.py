@@ -108,6 +108,8 @@ def lib():
         L.orc_huffman_free.argtypes = [C.POINTER(Huffman)]
         L.orc_sparse_compress.argtypes = [i32p, dblp, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                           C.c_double, C.c_int64, C.c_int64, C.POINTER(Sparse), i32p]
+        L.orc_sparse_compress_q.argtypes = [i32p, dblp, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                            C.c_double, C.c_int64, C.c_int64, C.c_int32, C.POINTER(Sparse), i32p]
         L.orc_sparse_restore.argtypes = [C.POINTER(Sparse), i32p, i32p]
         L.orc_sparse_restore.restype = C.c_int32
         L.orc_sparse_free.argtypes = [C.POINTER(Sparse)]
@@ -350,13 +352,13 @@ class OracleSparse:
 
 
 def sparse_compress(keys, vals, bin_num=256, group_num=8, row_num=2, col_ratio=0.3, seed=0,
-                    hash_seed=0) -> OracleSparse:
+                    hash_seed=0, uniform=False) -> OracleSparse:
     k = np.ascontiguousarray(keys, dtype=np.int32)
     v = np.ascontiguousarray(vals, dtype=np.float64)
     s = Sparse()
     bins = np.zeros(max(len(k), 1), dtype=np.int32)
-    st = lib().orc_sparse_compress(_p(k, i32p), _p(v, dblp), len(k), bin_num, group_num, row_num,
-                                   col_ratio, seed, hash_seed, C.byref(s), _p(bins, i32p))
+    st = lib().orc_sparse_compress_q(_p(k, i32p), _p(v, dblp), len(k), bin_num, group_num, row_num,
+                                     col_ratio, seed, hash_seed, 1 if uniform else 0, C.byref(s), _p(bins, i32p))
     if st:
         lib().orc_sparse_free(C.byref(s))
         raise OracleError(st, "sparse_compress")

@@ -975,10 +975,19 @@ static int32_t mm_cmp(int32_t a, int32_t b, int32_t zero) {
 int orc_sparse_compress(const int32_t* keys, const double* vals, int32_t nnz, int32_t bin_num,
                         int32_t group_num, int32_t row_num, double col_ratio, int64_t seed,
                         int64_t hash_seed, orc_sparse* s, int32_t* bins_out) {
+    return orc_sparse_compress_q(keys, vals, nnz, bin_num, group_num, row_num, col_ratio, seed, hash_seed, 0, s,
+                                 bins_out);
+}
+
+int orc_sparse_compress_q(const int32_t* keys, const double* vals, int32_t nnz, int32_t bin_num,
+                          int32_t group_num, int32_t row_num, double col_ratio, int64_t seed,
+                          int64_t hash_seed, int32_t quant_type, orc_sparse* s, int32_t* bins_out) {
     memset(s, 0, sizeof(*s));
     if (group_num < 2 || group_num > 64 || row_num < 1 || row_num > 8) return ORC_E_ARG;
     int32_t* bins = (int32_t*)malloc(sizeof(int32_t) * (size_t)(nnz > 0 ? nnz : 1));
-    int st = orc_quantize(vals, nnz, bin_num, seed, &s->q, bins);
+    /* SparseVectorCompressor.java:60-62: Quantizer.newQuantizer(quantType, ...).quantize(values) */
+    int st = quant_type == 1 ? orc_uniform_quantize(vals, nnz, bin_num, &s->q, bins)
+                             : orc_quantize(vals, nnz, bin_num, seed, &s->q, bins);
     if (st) { free(bins); return st; }
     if (bins_out) memcpy(bins_out, bins, sizeof(int32_t) * (size_t)nnz);
     s->group_num = group_num;

@@ -155,6 +155,11 @@ typedef struct {
 int orc_sparse_compress(const int32_t* keys, const double* vals, int32_t nnz, int32_t bin_num,
                         int32_t group_num, int32_t row_num, double col_ratio, int64_t seed,
                         int64_t hash_seed, orc_sparse* out, int32_t* bins_out /*nullable*/);
+/* The same with the values' quantizer chosen by quant_type (0 QUANTILE, 1 UNIFORM;
+ * SparseVectorCompressor.java:60-62 Quantizer.newQuantizer). */
+int orc_sparse_compress_q(const int32_t* keys, const double* vals, int32_t nnz, int32_t bin_num,
+                          int32_t group_num, int32_t row_num, double col_ratio, int64_t seed,
+                          int64_t hash_seed, int32_t quant_type, orc_sparse* s, int32_t* bins_out);
 /* GroupedMinMaxSketch.restore + Sort.merge; returns nnz */
 int32_t orc_sparse_restore(const orc_sparse* s, int32_t* keys_out, int32_t* bins_out);
 void orc_sparse_free(orc_sparse* s);

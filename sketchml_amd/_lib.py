@@ -42,7 +42,7 @@ szp = C.POINTER(C.c_size_t)
 class Params(C.Structure):
     _fields_ = [("bin_num", C.c_int32), ("group_num", C.c_int32), ("row_num", C.c_int32),
                 ("dedup", C.c_int32), ("col_ratio", C.c_double), ("seed", C.c_int64),
-                ("hash_seed", C.c_int64)]
+                ("hash_seed", C.c_int64), ("quant_type", C.c_int32), ("reserved", C.c_int32)]
 
 
 class DenseHeader(C.Structure):

@@ -282,6 +282,8 @@ void skml_params_default(skml_params* p) {
     p->col_ratio = 0.3;
     p->seed = 0;
     p->hash_seed = 0;
+    p->quant_type = SKML_QUANTILE;
+    p->reserved = 0;
 }
 
 const char* skml_last_error(void) { return g_err.c_str(); }

@@ -367,6 +367,8 @@ int check_params(const skml_params* p) {
     if (p->row_num < 1 || p->row_num > kMaxRows)
         return sfail(SKML_E_ARG, "Currently only %d hash functions are available", kMaxRows);
     if (!(p->col_ratio > 0.0)) return sfail(SKML_E_ARG, "col_ratio must be positive");
+    if (p->quant_type != SKML_QUANTILE && p->quant_type != SKML_UNIFORM)
+        return sfail(SKML_E_ARG, "Unrecognizable quantization type: %d", p->quant_type);
     return SKML_OK;
 }
 
@@ -381,11 +383,13 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const float* vals, int64_t nnz, 
         sparse_release(s);
         return code;
     };
-    // ---- 1. QuantileQuantizer over the values (the dense codec) ----
+    // ---- 1. the values' quantizer (Quantizer.newQuantizer(quantType), SparseVectorCompressor.java:60-62) ----
     s->qbytes = skml_dense_payload_bytes(nnz, p->bin_num);
     if (hipMalloc(&s->qpayload, s->qbytes) != hipSuccess) return bail(sfail(SKML_E_OOM, "quantizer payload"));
     skml_params qp = *p;
-    if (int e = skml_dense_encode_f32(c, vals, nnz, &qp, s->qpayload, s->qbytes)) return bail(e);
+    if (int e = p->quant_type == SKML_UNIFORM ? skml_dense_encode_uniform_f32(c, vals, nnz, &qp, s->qpayload, s->qbytes)
+                                              : skml_dense_encode_f32(c, vals, nnz, &qp, s->qpayload, s->qbytes))
+        return bail(e);
     if (int e = sync_to_host(c, &s->hdr, s->qpayload, sizeof(skml_dense_header))) return bail(e);
     if (s->hdr.status == SKML_E_NAN) return bail(sfail(SKML_E_NAN, "Encounter NaN value"));
     s->splits.resize((size_t)std::max(s->hdr.bin_num - 1, 0));

@@ -19,7 +19,7 @@ from .exceptions import SketchMLException, check
 from .quantization import Quantizer, QuantizationType
 
 
-def _params(bin_num, group_num, row_num, col_ratio, seed, hash_seed, dedup=True):
+def _params(bin_num, group_num, row_num, col_ratio, seed, hash_seed, dedup=True, uniform=False):
     p = _lib.Params()
     _lib.lib.skml_params_default(C.byref(p))
     p.bin_num = int(bin_num)
@@ -29,6 +29,7 @@ def _params(bin_num, group_num, row_num, col_ratio, seed, hash_seed, dedup=True)
     p.seed = int(seed)
     p.hash_seed = int(hash_seed)
     p.dedup = 1 if dedup else 0
+    p.quant_type = 1 if uniform else 0  # SKML_UNIFORM / SKML_QUANTILE
     return p
 
 
@@ -150,7 +151,7 @@ def _as_device(t, dtype, device=None):
 
 
 def encode_sparse(keys, values, bin_num=Quantizer.DEFAULT_BIN_NUM, group_num=8, row_num=2, col_ratio=0.3,
-                  seed=0, hash_seed=0, dedup=True) -> SparsePayload:
+                  seed=0, hash_seed=0, dedup=True, uniform=False) -> SparsePayload:
     v = _as_device(values, torch.float32)
     k = _as_device(keys, torch.int32, v.device)
     if k.numel() != v.numel():
@@ -158,7 +159,7 @@ def encode_sparse(keys, values, bin_num=Quantizer.DEFAULT_BIN_NUM, group_num=8, 
             f"Lengths of key array and value array do not match: {k.numel()}, {v.numel()}")
     dev = v.device.index
     ctx = get_context(dev)
-    p = _params(bin_num, group_num, row_num, col_ratio, seed, hash_seed, dedup)
+    p = _params(bin_num, group_num, row_num, col_ratio, seed, hash_seed, dedup, uniform)
     h = C.c_void_p()
     check(_lib.lib.skml_sparse_encode_kv_f32(ctx.handle, C.c_void_p(k.data_ptr()), C.c_void_p(v.data_ptr()),
                                              k.numel(), C.byref(p), C.byref(h)), "sparse_encode")
@@ -166,12 +167,12 @@ def encode_sparse(keys, values, bin_num=Quantizer.DEFAULT_BIN_NUM, group_num=8, 
 
 
 def encode_dense_as_sparse(dense, bin_num=Quantizer.DEFAULT_BIN_NUM, group_num=8, row_num=2, col_ratio=0.3,
-                           seed=0, hash_seed=0) -> SparsePayload:
+                           seed=0, hash_seed=0, uniform=False) -> SparsePayload:
     """SketchGradient.fromSparse after DenseDoubleGradient.toSparse (|x| > 1e-8), on device."""
     x = _as_device(dense, torch.float32)
     dev = x.device.index
     ctx = get_context(dev)
-    p = _params(bin_num, group_num, row_num, col_ratio, seed, hash_seed, True)
+    p = _params(bin_num, group_num, row_num, col_ratio, seed, hash_seed, True, uniform)
     h = C.c_void_p()
     check(_lib.lib.skml_sparse_encode_f32(ctx.handle, C.c_void_p(x.data_ptr()), x.numel(), C.byref(p),
                                           C.byref(h)), "sparse_encode")
@@ -209,9 +210,9 @@ class GroupedMinMaxSketch:
         self.zeroValue = None
         self.payload: SparsePayload | None = None
 
-    def create(self, keys, values, dedup=True) -> None:
+    def create(self, keys, values, dedup=True, uniform=False) -> None:
         self.payload = encode_sparse(keys, values, self.binNum, self.groupNum, self.rowNum, self.colRatio,
-                                     self.seed, self.hashSeed, dedup)
+                                     self.seed, self.hashSeed, dedup, uniform)
         hdr, _ = self.payload.quant_header()
         self.binNum = hdr.bin_num
         self.zeroValue = hdr.zero_idx
@@ -298,7 +299,7 @@ class SparseVectorCompressor:
                  mmSketchRowNum: int = 2,
                  mmSketchColRatio: float = GroupedMinMaxSketch.DEFAULT_MINMAXSKETCH_COL_RATIO,
                  seed: int = 0, hashSeed: int = 0):
-        if str(quantType) != "QUANTILE":
+        if str(quantType) not in ("QUANTILE", "UNIFORM"):
             raise SketchMLException(f"Unrecognizable quantization type: {quantType}")
         self.quantType = quantType
         self.quantBinNum = int(quantBinNum)
@@ -313,7 +314,7 @@ class SparseVectorCompressor:
     def _compress(self, keys, values, dedup):
         self.mmSketches = GroupedMinMaxSketch(self.mmSketchGroupNum, self.mmSketchRowNum, self.mmSketchColRatio,
                                               self.quantBinNum, self.seed, self.hashSeed)
-        self.mmSketches.create(keys, values, dedup)
+        self.mmSketches.create(keys, values, dedup, str(self.quantType) == "UNIFORM")
         self._size = self.mmSketches.payload.nnz()
 
     def compressDense(self, values) -> None:

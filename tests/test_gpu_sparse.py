@@ -284,3 +284,25 @@ def test_sparse_serialize_matches_oracle(gpu, bins, groups, rows):
         e = encoders[g]
         assert (e["size"], e["m"], e["kind"]) == (d["size"], d["num_intervals"], d["flag_kind"])
         assert np.array_equal(e["flags"], d["flag_words"]) and np.array_equal(e["deltas"], d["delta_words"])
+
+
+@pytest.mark.parametrize("kind", ["normal", "positive", "dups"])
+def test_sparse_uniform_quantizer_matches_oracle(gpu, kind):
+    """SparseVectorCompressor with QuantizationType.UNIFORM (SparseVectorCompressor.java:60-62):
+    uniform splits, then the same grouped MinMax sketch and DeltaAdaptive keys."""
+    keys, vals = _sparse_data(120000, 0.1, 77, kind)
+    c = gpu.SparseVectorCompressor(gpu.QuantizationType.UNIFORM, 128, seed=1, hashSeed=2)
+    c.compressSparse(torch.from_numpy(keys).cuda(), torch.from_numpy(vals).cuda())
+    osp = O.sparse_compress(keys, vals.astype(np.float64), 128, 8, 2, 0.3, 1, 2, uniform=True)
+    hdr, splits = c.mmSketches.payload.quant_header()
+    assert hdr.bin_num == osp.q.bin_num == 128 and hdr.zero_idx == osp.q.zero_idx
+    assert np.array_equal(splits, osp.q.splits)
+    for g in range(8):
+        gg = c.mmSketches.payload.group(g)
+        assert gg["size"] == osp.group_size[g]
+        if osp.tables[g] is not None:
+            assert np.array_equal(gg["table"], osp.tables[g]), g
+    k, v = c.decompressSparse()
+    ok, ob = osp.restore()
+    assert np.array_equal(k.cpu().numpy(), ok)
+    assert np.array_equal(v.cpu().numpy(), osp.q.values()[ob].astype(np.float32))
