@@ -28,11 +28,12 @@ struct SpGroups {
     int64_t fb[kMaxGroups + 1];  // first flag bit of group g in the concatenated flag stream
     int64_t db[kMaxGroups + 1];  // first delta bit of group g in the concatenated delta stream
     int32_t kind1_before[kMaxGroups];  // elements of unary-flag groups before g (decode select)
+    double inv_cols[kMaxGroups];       // 1.0 / cols[g]: the hash's `% size` as a multiply (set on upload)
 };
 
 constexpr int kSpThreads = 256;
 constexpr int kSpTile = 2048;             // elements per workgroup tile (8 per thread)
-constexpr int kCompactTile = 4096;        // dense elements per compaction tile (16 per thread)
+constexpr int kCompactTile = 16384;       // dense elements per compaction tile (64 per thread)
 constexpr int kDeltaHist = 33;            // bitsNeeded in 1..32
 
 inline int64_t sp_tiles(int64_t n, int64_t tile) { return (n + tile - 1) / tile; }
@@ -52,12 +53,13 @@ hipError_t launch_part_scatter(hipStream_t st, const int32_t* keys, const void* 
 // Deltas, bitsNeeded histogram, order check, and the per-bucket pair counts of the bucketed
 // MinMaxSketch.insert (bucket_count: nbuckets u64, zeroed; unused when rows == 0).
 constexpr int kMmCellsPerBucket = 8192;
+// cells (rows x n int32, may be null): each (element, row) pair's table cell, kept for the scatter.
 hipError_t launch_group_prep(hipStream_t st, const int32_t* gkeys, int64_t n, const SpGroups* gp, uint8_t* need,
-                             uint32_t* hist, uint32_t* err, uint64_t* bucket_count, int nbuckets);
+                             uint32_t* hist, uint32_t* err, uint64_t* bucket_count, int nbuckets, int32_t* cells);
 // pairs in bucket order (bucket_base: exclusive scan of the counts; cursor: nbuckets u64, zeroed)
 hipError_t launch_mm_scatter(hipStream_t st, const int32_t* gkeys, const int32_t* gbins, int64_t n,
                              const SpGroups* gp, const uint64_t* bucket_base, uint64_t* cursor, int nbuckets,
-                             uint64_t* pairs);
+                             uint64_t* pairs, const int32_t* cells);
 // per-bucket minimum -> int32 MinMaxSketch tables (empty cells get the fill value)
 hipError_t launch_mm_bucket(hipStream_t st, const uint64_t* pairs, const uint64_t* bucket_base, int nbuckets,
                             int64_t ncells, int32_t zero, int32_t fill, int32_t* table);

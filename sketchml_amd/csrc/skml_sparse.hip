@@ -22,6 +22,7 @@
 namespace skml {
 
 constexpr uint64_t kStAgg = 1ULL << 62, kStPre = 2ULL << 62, kStMask = (1ULL << 62) - 1;
+constexpr uint32_t kEpsBelowBits = 0x322BCC77u;  // the largest float <= 1e-8 (Maths.scala:8 EPS)
 
 // ---------------------------------------------------------------------------------------------
 // block scan helpers (256 threads)
@@ -112,7 +113,7 @@ __device__ __forceinline__ void load_starts(const SpGroups* gp, int64_t* S) {
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t sar(uint32_t c, int s) { return (uint32_t)((int32_t)c >> s); }
 
-__device__ __forceinline__ int32_t java_hash(int id, int32_t key, int32_t size) {
+__device__ __forceinline__ uint32_t java_hash_mix(int id, int32_t key) {
     uint32_t c = (uint32_t)key;
     if (id == 0) {
         c = (c + 0x7ed55d16u) + (c << 12);
@@ -145,8 +146,22 @@ __device__ __forceinline__ int32_t java_hash(int id, int32_t key, int32_t size) 
             k /= 10;
         }
     }
-    int32_t r = (int32_t)c % size;
+    return c;
+}
+__device__ __forceinline__ int32_t java_hash(int id, int32_t key, int32_t size) {
+    const int32_t r = (int32_t)java_hash_mix(id, key) % size;
     return r >= 0 ? r : r + size;
+}
+// The same with `% size` folded non-negative as r - floor(r * (1/size)) * size: the double
+// product is within one of the true quotient and one correction step makes the result exact (an
+// integer division by a run-time divisor is a long instruction sequence on the GPU).
+__device__ __forceinline__ int32_t java_hash_fm(int id, int32_t key, int32_t size, double inv) {
+    const int32_t r = (int32_t)java_hash_mix(id, key);
+    const int64_t q = (int64_t)floor((double)r * inv);
+    int64_t m = (int64_t)r - q * (int64_t)size;
+    if (m < 0) m += size;
+    else if (m >= size) m -= size;
+    return (int32_t)m;
 }
 
 // |v - zero| with Java int wrap (MinMaxSketch.compare, MinMaxSketch.java:80-86)
@@ -158,54 +173,99 @@ __device__ __forceinline__ int32_t mm_dist(int32_t v, int32_t zero) {
 // =============================================================================================
 // Compaction (decoupled look-back)
 // =============================================================================================
+// Each workgroup compacts one tile of kCompactTile = 16,384 values, all of it held in registers
+// (16 float4 per thread, slab j of the tile = float4 j * 256 + t), so a tile keeps 64 KiB of loads
+// in flight and takes one look-back.  Ranks follow index order: slab by slab, and within a slab
+// by float4, from wave-level scans of 16-bit packed per-slab counts plus the waves' slab totals.
+constexpr int kCompactSlabs = kCompactTile / (4 * kSpThreads);
+
 __global__ __launch_bounds__(kSpThreads) void k_compact(const float* __restrict__ x, int64_t dim,
                                                         int32_t* __restrict__ keys, float* __restrict__ vals,
                                                         uint64_t* status, unsigned* ticket, int64_t ntiles,
                                                         int64_t* nnz_out) {
-    __shared__ float4 sx[kCompactTile / 4];
-    __shared__ uint64_t sh[8];
+    __shared__ uint32_t wtot[kSpThreads / 64][kCompactSlabs];  // per-wave kept counts of each slab
     __shared__ int64_t s_tile;
     __shared__ uint64_t s_excl;
-    const int t = threadIdx.x;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     if (t == 0) s_tile = (int64_t)atomicAdd(ticket, 1u);
     __syncthreads();
     const int64_t tile = s_tile;
     const int64_t base = tile * kCompactTile;
     const int64_t lim = dim - base;
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    f32x4 f[kCompactSlabs];
     if (lim >= kCompactTile && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
-        typedef float f32x4 __attribute__((ext_vector_type(4)));
         const f32x4* src = reinterpret_cast<const f32x4*>(x + base);
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const f32x4 f = __builtin_nontemporal_load(src + j * kSpThreads + t);
-            sx[j * kSpThreads + t] = make_float4(f.x, f.y, f.z, f.w);
-        }
+        for (int j = 0; j < kCompactSlabs; j++) f[j] = __builtin_nontemporal_load(src + j * kSpThreads + t);
     } else {
-        float* s = reinterpret_cast<float*>(sx);
-        for (int i = t; i < kCompactTile; i += kSpThreads) s[i] = i < lim ? x[base + i] : 0.0f;
+#pragma unroll
+        for (int j = 0; j < kCompactSlabs; j++) {
+            const int64_t e = 4 * ((int64_t)j * kSpThreads + t);
+            f[j].x = e < lim ? x[base + e] : 0.0f;
+            f[j].y = e + 1 < lim ? x[base + e + 1] : 0.0f;
+            f[j].z = e + 2 < lim ? x[base + e + 2] : 0.0f;
+            f[j].w = e + 3 < lim ? x[base + e + 3] : 0.0f;
+        }
+    }
+    // Maths.scala:8 EPS: |x| > 1e-8 in double.  For a float x that is |x| > RD_f32(1e-8) on the
+    // magnitude bits, NaN excluded (abs bits above +inf's).
+    uint64_t keep = 0;
+#pragma unroll
+    for (int j = 0; j < kCompactSlabs; j++) {
+        const float e4[4] = {f[j].x, f[j].y, f[j].z, f[j].w};
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const uint32_t a = __float_as_uint(e4[e]) & 0x7FFFFFFFu;
+            keep |= (a > kEpsBelowBits && a <= 0x7F800000u) ? (1ull << (4 * j + e)) : 0ull;
+        }
+    }
+    // wave-inclusive scans of the per-slab counts, four 16-bit lanes per u64
+    uint64_t P[kCompactSlabs / 4];
+#pragma unroll
+    for (int k = 0; k < kCompactSlabs / 4; k++) {
+        uint64_t v = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) v |= (uint64_t)__popcll((keep >> (16 * k + 4 * q)) & 15ull) << (16 * q);
+        P[k] = v;
+    }
+    uint64_t own[kCompactSlabs / 4];
+#pragma unroll
+    for (int k = 0; k < kCompactSlabs / 4; k++) own[k] = P[k];
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+#pragma unroll
+        for (int k = 0; k < kCompactSlabs / 4; k++) {
+            const uint64_t y = __shfl_up(P[k], off, 64);
+            if (lane >= off) P[k] += y;
+        }
+    }
+    if (lane == 63) {
+#pragma unroll
+        for (int j = 0; j < kCompactSlabs; j++) wtot[w][j] = (uint32_t)(P[j >> 2] >> (16 * (j & 3))) & 0xFFFFu;
     }
     __syncthreads();
-    float v[16];
+    // slab totals, this wave's offset inside each slab, and the tile total
+    uint32_t slab_pre[kCompactSlabs];
+    uint32_t tile_total = 0;
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const float4 f = sx[t * 4 + q];
-        v[4 * q] = f.x;
-        v[4 * q + 1] = f.y;
-        v[4 * q + 2] = f.z;
-        v[4 * q + 3] = f.w;
+    for (int j = 0; j < kCompactSlabs; j++) {
+        uint32_t before = 0, tot = 0;
+#pragma unroll
+        for (int u = 0; u < kSpThreads / 64; u++) {
+            const uint32_t c = wtot[u][j];
+            before += u < w ? c : 0u;
+            tot += c;
+        }
+        slab_pre[j] = tile_total + before;
+        tile_total += tot;
     }
-    uint32_t keep = 0;
-#pragma unroll
-    for (int j = 0; j < 16; j++) keep |= (fabs((double)v[j]) > 1e-8) ? (1u << j) : 0u;  // Maths.scala:8 EPS
-    uint64_t c[1] = {(uint64_t)__popc(keep)}, tot[1];
-    block_excl_scan<1>(c, tot, sh);
     if (t < 64) {  // wave 0: publish the aggregate, then look back 64 predecessors per step
-        const int lane = t;
         uint64_t excl = 0;
         if (tile == 0) {
-            if (lane == 0) st_status(&status[0], kStPre | tot[0]);
+            if (lane == 0) st_status(&status[0], kStPre | tile_total);
         } else {
-            if (lane == 0) st_status(&status[tile], kStAgg | tot[0]);
+            if (lane == 0) st_status(&status[tile], kStAgg | tile_total);
             int64_t p = tile - 1;
             while (true) {
                 const int64_t idx = p - lane;
@@ -223,23 +283,30 @@ __global__ __launch_bounds__(kSpThreads) void k_compact(const float* __restrict_
                 if (pre) break;
                 p -= 64;
             }
-            if (lane == 0) st_status(&status[tile], kStPre | (excl + tot[0]));
+            if (lane == 0) st_status(&status[tile], kStPre | (excl + tile_total));
         }
         if (lane == 0) {
             s_excl = excl;
-            if (tile == ntiles - 1) *nnz_out = (int64_t)(excl + tot[0]);
+            if (tile == ntiles - 1) *nnz_out = (int64_t)(excl + tile_total);
         }
     }
     __syncthreads();
-    int64_t pos = (int64_t)(s_excl + c[0]);
-    const int64_t e0 = base + t * 16;
+    const int64_t out0 = (int64_t)s_excl;
 #pragma unroll
-    for (int j = 0; j < 16; j++)
-        if (keep & (1u << j)) {
-            keys[pos] = (int32_t)(e0 + j);
-            vals[pos] = v[j];
-            pos++;
-        }
+    for (int j = 0; j < kCompactSlabs; j++) {
+        const uint64_t incl = (P[j >> 2] >> (16 * (j & 3))) & 0xFFFFull;
+        const uint64_t mine = (own[j >> 2] >> (16 * (j & 3))) & 0xFFFFull;
+        int64_t pos = out0 + slab_pre[j] + (int64_t)(incl - mine);
+        const int32_t e0 = (int32_t)(base + 4 * ((int64_t)j * kSpThreads + t));
+        const float e4[4] = {f[j].x, f[j].y, f[j].z, f[j].w};
+#pragma unroll
+        for (int e = 0; e < 4; e++)
+            if ((keep >> (4 * j + e)) & 1ull) {
+                keys[pos] = e0 + e;
+                vals[pos] = e4[e];
+                pos++;
+            }
+    }
 }
 
 hipError_t launch_compact(hipStream_t st, const float* x, int64_t dim, int32_t* keys, float* vals,
@@ -406,7 +473,7 @@ constexpr int kMmChunk = 16384;      // elements per workgroup in the count / sc
 
 __device__ __forceinline__ int64_t mm_cell(const SpGroups* gp, int g, int r, int32_t key) {
     const int32_t cols = gp->cols[g];
-    return gp->tab_off[g] + (int64_t)r * cols + java_hash(gp->hash_ids[g][r], key, cols);
+    return gp->tab_off[g] + (int64_t)r * cols + java_hash_fm(gp->hash_ids[g][r], key, cols, gp->inv_cols[g]);
 }
 __device__ __forceinline__ uint64_t mm_pair(int32_t key, int32_t bin, int32_t zero, int64_t cell) {
     return ((uint64_t)mm_dist(bin, zero) << 48) | ((uint64_t)(uint32_t)key << 17) |
@@ -420,7 +487,7 @@ __global__ __launch_bounds__(kSpThreads) void k_group_prep(const int32_t* __rest
                                                            uint8_t* __restrict__ need, uint32_t* __restrict__ hist,
                                                            uint32_t* __restrict__ err,
                                                            unsigned long long* __restrict__ bucket_count,
-                                                           int nbuckets) {
+                                                           int nbuckets, int32_t* __restrict__ cells_out) {
     __shared__ int64_t S[kMaxGroups + 1];
     __shared__ uint32_t H[kMaxGroups * kDeltaHist];
     __shared__ uint32_t BH[kMmLdsBuckets];
@@ -447,7 +514,9 @@ __global__ __launch_bounds__(kSpThreads) void k_group_prep(const int32_t* __rest
         need[i] = (uint8_t)nb;
         atomicAdd(&H[g * kDeltaHist + nb], 1u);
         for (int r = 0; r < rows; r++) {
-            const int b = (int)(mm_cell(gp, g, r, key) >> kMmBucketBits);
+            const int64_t cell = mm_cell(gp, g, r, key);
+            if (cells_out) cells_out[(int64_t)r * n + i] = (int32_t)cell;  // hashed once, reused by the scatter
+            const int b = (int)(cell >> kMmBucketBits);
             if (lds_b) atomicAdd(&BH[b], 1u);
             else atomicAdd(&bucket_count[b], 1ull);
         }
@@ -462,10 +531,10 @@ __global__ __launch_bounds__(kSpThreads) void k_group_prep(const int32_t* __rest
 }
 
 hipError_t launch_group_prep(hipStream_t st, const int32_t* gkeys, int64_t n, const SpGroups* gp, uint8_t* need,
-                             uint32_t* hist, uint32_t* err, uint64_t* bucket_count, int nbuckets) {
+                             uint32_t* hist, uint32_t* err, uint64_t* bucket_count, int nbuckets, int32_t* cells) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_group_prep, dim3((unsigned)sp_tiles(n, kMmChunk)), dim3(kSpThreads), 0, st, gkeys, n, gp,
-                       need, hist, err, reinterpret_cast<unsigned long long*>(bucket_count), nbuckets);
+                       need, hist, err, reinterpret_cast<unsigned long long*>(bucket_count), nbuckets, cells);
     return hipGetLastError();
 }
 
@@ -476,7 +545,8 @@ __global__ __launch_bounds__(kSpThreads) void k_mm_scatter(const int32_t* __rest
                                                            const SpGroups* __restrict__ gp,
                                                            const uint64_t* __restrict__ bucket_base,
                                                            unsigned long long* __restrict__ cursor, int nbuckets,
-                                                           uint64_t* __restrict__ pairs) {
+                                                           uint64_t* __restrict__ pairs,
+                                                           const int32_t* __restrict__ cells_in) {
     __shared__ int64_t S[kMaxGroups + 1];
     __shared__ uint32_t cnt[kMmLdsBuckets];
     __shared__ uint32_t lofs[kMmLdsBuckets];
@@ -487,11 +557,15 @@ __global__ __launch_bounds__(kSpThreads) void k_mm_scatter(const int32_t* __rest
         for (int j = threadIdx.x; j < nbuckets; j += kSpThreads) cnt[j] = 0;
     __syncthreads();
     const int64_t c0 = (int64_t)blockIdx.x * kMmChunk, c1 = std::min<int64_t>(n, c0 + kMmChunk);
+    // cell of (element i, row r): from k_group_prep's table when it kept one, else hashed again
+    auto cell_of = [&](int g, int r, int64_t i, int32_t key) -> int64_t {
+        return cells_in ? (int64_t)cells_in[(int64_t)r * n + i] : mm_cell(gp, g, r, key);
+    };
     if (lds_b) {
         for (int64_t i = c0 + threadIdx.x; i < c1; i += kSpThreads) {
-            const int g = group_of_elem(S, i);
-            const int32_t key = gkeys[i];
-            for (int r = 0; r < rows; r++) atomicAdd(&cnt[(int)(mm_cell(gp, g, r, key) >> kMmBucketBits)], 1u);
+            const int g = cells_in ? 0 : group_of_elem(S, i);
+            const int32_t key = cells_in ? 0 : gkeys[i];
+            for (int r = 0; r < rows; r++) atomicAdd(&cnt[(int)(cell_of(g, r, i, key) >> kMmBucketBits)], 1u);
         }
         __syncthreads();
         for (int j = threadIdx.x; j < nbuckets; j += kSpThreads) {
@@ -501,10 +575,10 @@ __global__ __launch_bounds__(kSpThreads) void k_mm_scatter(const int32_t* __rest
         __syncthreads();
     }
     for (int64_t i = c0 + threadIdx.x; i < c1; i += kSpThreads) {
-        const int g = group_of_elem(S, i);
+        const int g = cells_in ? 0 : group_of_elem(S, i);
         const int32_t key = gkeys[i], bin = gbins[i];
         for (int r = 0; r < rows; r++) {
-            const int64_t cell = mm_cell(gp, g, r, key);
+            const int64_t cell = cell_of(g, r, i, key);
             const int b = (int)(cell >> kMmBucketBits);
             const uint64_t slot = lds_b ? (uint64_t)lofs[b] + atomicAdd(&cnt[b], 1u)
                                         : (uint64_t)atomicAdd(&cursor[b], 1ull);
@@ -515,10 +589,10 @@ __global__ __launch_bounds__(kSpThreads) void k_mm_scatter(const int32_t* __rest
 
 hipError_t launch_mm_scatter(hipStream_t st, const int32_t* gkeys, const int32_t* gbins, int64_t n,
                              const SpGroups* gp, const uint64_t* bucket_base, uint64_t* cursor, int nbuckets,
-                             uint64_t* pairs) {
+                             uint64_t* pairs, const int32_t* cells) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_mm_scatter, dim3((unsigned)sp_tiles(n, kMmChunk)), dim3(kSpThreads), 0, st, gkeys, gbins, n,
-                       gp, bucket_base, reinterpret_cast<unsigned long long*>(cursor), nbuckets, pairs);
+                       gp, bucket_base, reinterpret_cast<unsigned long long*>(cursor), nbuckets, pairs, cells);
     return hipGetLastError();
 }
 
@@ -958,9 +1032,10 @@ __global__ __launch_bounds__(kSpThreads) void k_dec_keys(const uint32_t* __restr
         p += d[j];
         const int32_t key = (int32_t)(uint32_t)(p - gpre[g]);
         const int32_t cols = gp->cols[g];
+        const double inv = gp->inv_cols[g];
         int32_t res = zero;
         for (int r = 0; r < rows; r++) {
-            const int32_t tv = table[gp->tab_off[g] + (int64_t)r * cols + java_hash(gp->hash_ids[g][r], key, cols)];
+            const int32_t tv = table[gp->tab_off[g] + (int64_t)r * cols + java_hash_fm(gp->hash_ids[g][r], key, cols, inv)];
             if ((int32_t)((uint32_t)mm_dist(tv, zero) - (uint32_t)mm_dist(res, zero)) > 0) res = tv;
         }
         gkeys[i] = key;

@@ -52,6 +52,7 @@ enum {
     kSlotK1,
     kSlotB1,
     kSlotStatus,
+    kSlotCellIdx,
 };
 
 // java.util.Random (JDK 8 spec): seed scramble, next(bits), nextInt(bound).
@@ -284,6 +285,7 @@ void sparse_release(skml_sparse* s) {
 
 // The host table is edited between uploads, so each upload completes before returning.
 int upload_groups(skml_ctx* c, skml_sparse* s) {
+    for (int g = 0; g < kMaxGroups; g++) s->g.inv_cols[g] = s->g.cols[g] > 0 ? 1.0 / (double)s->g.cols[g] : 0.0;
     SP_HIP(hipMemcpyAsync(s->g_dev, &s->g, sizeof(SpGroups), hipMemcpyHostToDevice, ctx_stream(c)));
     SP_HIP(hipStreamSynchronize(ctx_stream(c)));
     return SKML_OK;
@@ -462,7 +464,9 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const float* vals, int64_t nnz, 
     if (hipMemsetAsync(small, 0, sizeof(uint32_t) * ((size_t)kMaxGroups * kDeltaHist + 64), st) != hipSuccess ||
         hipMemsetAsync(bucket, 0, sizeof(uint64_t) * ((size_t)2 * nbuckets + 2), st) != hipSuccess)
         return bail(sfail(SKML_E_HIP, "memset"));
-    if (hipSuccess != launch_group_prep(st, gk, nnz, s->g_dev, need, hist, err, bucket, nbuckets))
+    // the pairs' table cells, hashed once (int32 cells; without room or past 2^31 cells the scatter rehashes)
+    int32_t* cellbuf = cells < INT32_MAX ? scratch<int32_t>(c, kSlotCellIdx, (size_t)G.rows * (size_t)nnz) : nullptr;
+    if (hipSuccess != launch_group_prep(st, gk, nnz, s->g_dev, need, hist, err, bucket, nbuckets, cellbuf))
         return bail(sfail(SKML_E_HIP, "group_prep"));
     std::vector<uint32_t> hh((size_t)kMaxGroups * kDeltaHist + 1);
     if (int e = sync_to_host(c, hh.data(), small, sizeof(uint32_t) * hh.size())) return bail(e);
@@ -471,7 +475,7 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const float* vals, int64_t nnz, 
     if (hipMalloc(&s->tables, sizeof(int32_t) * (size_t)std::max<int64_t>(cells, 1)) != hipSuccess)
         return bail(sfail(SKML_E_OOM, "tables"));
     if (int e = scan_tiles(c, bucket, nbuckets, 1, nullptr)) return bail(e);
-    if (hipSuccess != launch_mm_scatter(st, gk, gb, nnz, s->g_dev, bucket, cursor, nbuckets, pairs) ||
+    if (hipSuccess != launch_mm_scatter(st, gk, gb, nnz, s->g_dev, bucket, cursor, nbuckets, pairs, cellbuf) ||
         hipSuccess != launch_mm_bucket(st, pairs, bucket, nbuckets, cells, G.zero, G.fill, s->tables))
         return bail(sfail(SKML_E_HIP, "minmax insert"));
     // ---- 5. DeltaAdaptive key streams ----
@@ -1334,7 +1338,7 @@ int skml_delta_encode(skml_ctx* c, const int32_t* keys, int64_t n, int32_t* num_
             break;
         }
         if (launch_group_prep(st, keys, n, tmp.g_dev, need, small, small + kMaxGroups * kDeltaHist, nullptr,
-                              0) != hipSuccess) {
+                              0, nullptr) != hipSuccess) {
             rc = sfail(SKML_E_HIP, "group_prep");
             break;
         }

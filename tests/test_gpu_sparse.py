@@ -131,7 +131,7 @@ def test_sparse_length_mismatch(gpu):
 
 def test_compaction_exact(gpu):
     rng = np.random.default_rng(3)
-    for dim in (1, 4095, 4096, 4097, 2**18 + 3, 2**22 + 1234):
+    for dim in (1, 4095, 4096, 4097, 16383, 16384, 16385, 3 * 16384 + 5, 2**18 + 3, 2**22 + 1234):
         x = rng.standard_normal(dim).astype(np.float32)
         r = rng.random(dim)
         x[r < 0.5] = 0.0
