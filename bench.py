@@ -77,9 +77,12 @@ def pmc_traffic(kernel, n):
     return best
 
 
-# VALU issue ceiling (wave-instructions / s, whole chip): tools/ubench/xlane2.hip measured 1.12
-# clocks per v_min_u32 wave-instruction per CU at 2.4 GHz on 256 CUs.
-VALU_PEAK_GINST = 2.4e9 / 1.12 * 256 / 1e9
+# VALU issue ceiling (wave-instructions / s, whole chip): one 64-lane VALU wave-instruction per
+# clock per CU (4 SIMDs x 16 lanes) at the 2.4 GHz peak engine clock on 256 CUs.  (The
+# tools/ubench/xlane2.hip dependent-chain probe reached 1.12 clocks per instruction; the leaf,
+# with 8 independent waves per SIMD, issues faster than that, so the architectural rate is the
+# honest denominator.)
+VALU_PEAK_GINST = 2.4e9 * 256 / 1e9
 
 
 def sq_valu(kernel):

@@ -500,13 +500,17 @@ int skml_dense_encode_f32(skml_ctx* c, const float* x, int64_t n, const skml_par
         if (!passes.empty()) passes.back().fuse_summary = 1;
         const float* src = w.nodes6;
         float* dst = w.upA;
-        for (const MergePass& pass : passes) {
+        for (size_t i = 0; i < passes.size(); i++) {
+            // a final one-workgroup pass runs inside the previous pass's last workgroup
+            const bool fuse_next = i + 2 == passes.size() && passes[i + 1].wg_prefix[passes[i + 1].njobs] == 1;
+            float* next_dst = (dst == w.upA) ? w.upB : w.upA;
             KernelTimer kt(c, SKML_K_MERGE);
-            HIP_TRY(launch_merge_pass(c->stream, pass, src, dst, w.roots, s0, c->jump_tab, w.done, x, n,
-                                      w.part, nwg, c->ranks, p->bin_num, p->dedup ? 1 : 0, payload,
-                                      w.raw, w.lut));
+            HIP_TRY(launch_merge_pass(c->stream, passes[i], fuse_next ? &passes[i + 1] : nullptr, src, dst, next_dst,
+                                      w.roots, s0, c->jump_tab, w.done, x, n, w.part, nwg, c->ranks, p->bin_num,
+                                      p->dedup ? 1 : 0, payload, w.raw, w.lut));
             src = dst;
-            dst = (dst == w.upA) ? w.upB : w.upA;
+            dst = next_dst;
+            if (fuse_next) break;
         }
         fused = !passes.empty();
     }

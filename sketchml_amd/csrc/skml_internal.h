@@ -94,9 +94,11 @@ hipError_t launch_leaf(hipStream_t st, const float* x, int64_t chunks, uint64_t 
                        const uint64_t* jump_tab, LeafPartial* part, float* nodes6, float* roots);
 hipError_t launch_leaf_stage(hipStream_t st, int stage, const float* x, int64_t chunks, uint64_t s0,
                              const uint64_t* jump_tab, LeafPartial* part, float* scratch, float* roots);
-hipError_t launch_merge_pass(hipStream_t st, const MergePass& pass, const float* src, float* dst,
-                             float* roots, uint64_t s0, const uint64_t* jump_tab, unsigned* done,
-                             const float* x, int64_t n, const LeafPartial* part, int64_t nparts,
+// `next` (may be null): a one-workgroup pass run by this pass's last workgroup (its src is `dst`,
+// its output `next_dst`), saving a launch.
+hipError_t launch_merge_pass(hipStream_t st, const MergePass& pass, const MergePass* next, const float* src,
+                             float* dst, float* next_dst, float* roots, uint64_t s0, const uint64_t* jump_tab,
+                             unsigned* done, const float* x, int64_t n, const LeafPartial* part, int64_t nparts,
                              const int64_t* ranks, int req_bins, int dedup, void* payload,
                              double* scratch_raw, QuantLut* lut);
 hipError_t launch_summary(hipStream_t st, const float* x, int64_t n, const LeafPartial* part,

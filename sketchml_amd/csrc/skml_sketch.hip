@@ -20,6 +20,8 @@
 // Bitonic merges sort by total-order key; they equal the reference merge (IEEE `<`, ties emit
 // the newer run) unless a merge sees both -0.0 and +0.0, in which case that workgroup takes the
 // exact LDS path (count-based merge positions with the reference tie rule).
+#include <cstring>
+
 #include "skml_device.hpp"
 
 namespace skml {
@@ -989,18 +991,15 @@ struct MergeExport {
     }
 };
 
-__global__ __launch_bounds__(512) void k_merge(MergePass pass, const float* __restrict__ src,
-                                               float* __restrict__ dst, float* __restrict__ roots,
-                                               uint64_t s0, const uint64_t* __restrict__ tab,
-                                               unsigned* __restrict__ done, SummaryArgs sa) {
-    __shared__ MergeShared U;
-    TileShared& sh = U.t;
+// One workgroup's share of a merge pass: 2^g consecutive level-L nodes of one tree -> one node.
+__device__ __forceinline__ void merge_group_wg(const MergePass& pass, int wg, const float* __restrict__ src,
+                                               float* __restrict__ dst, float* __restrict__ roots, uint64_t s0,
+                                               const uint64_t* __restrict__ tab, TileShared& sh) {
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    if (pass.fuse_summary && gridDim.x == 1) SKML_PROF(0);
     int j = 0;
-    while (j + 1 < pass.njobs && (int)blockIdx.x >= pass.wg_prefix[j + 1]) j++;
+    while (j + 1 < pass.njobs && wg >= pass.wg_prefix[j + 1]) j++;
     const MergeJob job = pass.job[j];
-    const int grp = (int)blockIdx.x - pass.wg_prefix[j];
+    const int grp = wg - pass.wg_prefix[j];
     const int g = job.group_log, L = job.level_in;
     const int nodes = 1 << g;
     const int64_t node0 = job.src_node + ((int64_t)grp << g);
@@ -1061,9 +1060,24 @@ __global__ __launch_bounds__(512) void k_merge(MergePass pass, const float* __re
         crosswave_levels(sh, tid, sh.wgbits, (sh.flags & 6u) == 6u);
         if (tid < kK) out[tid] = g == 4 ? sh.l4[0][tid] : (g == 5 ? sh.l5[0][tid] : sh.l6[tid]);
     }
-    if (!pass.fuse_summary) return;
+}
 
-    // ---- last workgroup of the last pass: summary (release/acquire per Guideline 16) ----
+// A merge pass.  `next` (njobs > 0) is a one-workgroup pass that the pass's last workgroup runs
+// itself once every output of this pass is written (the last-arriver protocol below), so the
+// two passes need one launch; the summary then follows in the same workgroup.
+__global__ __launch_bounds__(512) void k_merge(MergePass pass, MergePass next, const float* __restrict__ src,
+                                               float* __restrict__ dst, float* __restrict__ next_dst,
+                                               float* __restrict__ roots, uint64_t s0,
+                                               const uint64_t* __restrict__ tab, unsigned* __restrict__ done,
+                                               SummaryArgs sa) {
+    __shared__ MergeShared U;
+    const int tid = threadIdx.x;
+    if (pass.fuse_summary && gridDim.x == 1) SKML_PROF(0);
+    merge_group_wg(pass, (int)blockIdx.x, src, dst, roots, s0, tab, U.t);
+    const bool has_next = next.njobs > 0;
+    if (!pass.fuse_summary && !has_next) return;
+
+    // ---- last workgroup: the trailing pass and / or the summary (release/acquire per Guideline 16) ----
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
@@ -1076,25 +1090,39 @@ __global__ __launch_bounds__(512) void k_merge(MergePass pass, const float* __re
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        sh.is_last = last;
+        U.t.is_last = last;
     }
     __syncthreads();
-    if (!sh.is_last) return;
+    if (!U.t.is_last) return;
     __syncthreads();
+    if (has_next) {
+        SKML_PROF(0);
+        merge_group_wg(next, 0, dst, next_dst, roots, s0, tab, U.t);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        __syncthreads();
+        if (!next.fuse_summary) return;
+    }
     SKML_PROF(1);
     summary_block(sa, U.s);
 }
 
-hipError_t launch_merge_pass(hipStream_t st, const MergePass& pass, const float* src, float* dst,
-                             float* roots, uint64_t s0, const uint64_t* jump_tab, unsigned* done,
-                             const float* x, int64_t n, const LeafPartial* part, int64_t nparts,
+hipError_t launch_merge_pass(hipStream_t st, const MergePass& pass, const MergePass* next, const float* src,
+                             float* dst, float* next_dst, float* roots, uint64_t s0, const uint64_t* jump_tab,
+                             unsigned* done, const float* x, int64_t n, const LeafPartial* part, int64_t nparts,
                              const int64_t* ranks, int req_bins, int dedup, void* payload,
                              double* scratch_raw, QuantLut* lut) {
     const int nwg = pass.wg_prefix[pass.njobs];
     if (nwg <= 0) return hipSuccess;
     SummaryArgs a{x, n, part, nparts, roots, ranks, reinterpret_cast<uint8_t*>(payload), scratch_raw,
                   lut, req_bins, dedup};
-    hipLaunchKernelGGL(k_merge, dim3(nwg), dim3(512), 0, st, pass, src, dst, roots, s0, jump_tab, done, a);
+    MergePass none;
+    if (!next) {
+        std::memset(&none, 0, sizeof(none));
+        next = &none;
+    }
+    hipLaunchKernelGGL(k_merge, dim3(nwg), dim3(512), 0, st, pass, *next, src, dst, next_dst, roots, s0, jump_tab,
+                       done, a);
     return hipGetLastError();
 }
 
