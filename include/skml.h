@@ -55,7 +55,10 @@ typedef struct skml_params {
     int32_t quant_type; /* sparse: the values' quantizer, SKML_QUANTILE (default) or SKML_UNIFORM
                            (Quantizer.newQuantizer, base/Quantizer.java:126-136); the dense path
                            has separate entry points per quantizer */
-    int32_t reserved;
+    int32_t parallelism; /* sparse path: slice sketches of the values' parallelQuantize when > 1
+                            (Constants.Parallel, SparseVectorCompressor.java:90-91); 0 or 1: one.
+                            The dense path takes T as an argument
+                            (skml_dense_encode_parallel_f32) */
 } skml_params;
 #define SKML_QUANTILE 0
 #define SKML_UNIFORM 1
@@ -136,6 +139,39 @@ int skml_dense_encode_f64(skml_ctx* ctx, const double* x_dev, int64_t n, const s
 int skml_dense_encode_uniform_f32(skml_ctx* ctx, const float* x_dev, int64_t n,
                                   const skml_params* params, void* payload_dev, size_t payload_cap);
 int skml_dense_encode_uniform_f64(skml_ctx* ctx, const double* x_dev, int64_t n,
+                                  const skml_params* params, void* payload_dev, size_t payload_cap);
+
+/* QuantileQuantizer.parallelQuantize (QuantileQuantizer.java:53-92) with `threads` slices
+ * (Constants.Parallel.getParallelism): slice t = [t*(n/T), ...), the last slice takes the
+ * remainder; each slice is sketched, the sketches merged in slice order (HeapQuantileSketch.merge,
+ * HeapQuantileSketch.java:186-228), no Maths.unique unless params->dedup (default params: 0).
+ * The reference draws every compaction bit from one static Random (QSketchUtils.java:9) in a
+ * thread-interleaved order; this is the schedule that runs the slice sketches one after another
+ * and then the merges, with Random(params->seed).  threads = 1 equals skml_dense_encode_f32 with
+ * dedup = 0.  Asynchronous. */
+int skml_dense_encode_parallel_f32(skml_ctx* ctx, const float* x_dev, int64_t n, int32_t threads,
+                                   const skml_params* params, void* payload_dev, size_t payload_cap);
+
+/* The same split table over P devices (SURVEY §8e single-split-table mode): shard s holds
+ * shard_n[s] consecutive values of one logical gradient.  Each rank sketches its shard into a
+ * fixed-size device record (skml_sketch_record_bytes(0)), the records are all-gathered in shard
+ * order (skml_allgather), and every rank merges them identically and quantises its own shard.
+ * The result equals skml_dense_encode_parallel_f32 over the concatenation when the shards follow
+ * its slicing; any shard sizes are accepted (merge order = shard order).  The payload header
+ * carries the global splits / min / max / zeroIdx and n = shard_n[shard]. */
+size_t skml_sketch_record_bytes(int32_t fp64);
+int skml_dense_sketch_shard_f32(skml_ctx* ctx, const float* x_dev, int64_t n, const int64_t* shard_n,
+                                int32_t nshards, int32_t shard, int64_t seed, void* record_dev);
+int skml_dense_encode_sharded_f32(skml_ctx* ctx, const float* x_dev, int64_t n, const int64_t* shard_n,
+                                  int32_t nshards, int32_t shard, const void* records_dev,
+                                  const skml_params* params, void* payload_dev, size_t payload_cap);
+/* fp64 input (the reference's double[] itself): records of skml_sketch_record_bytes(1) bytes. */
+int skml_dense_encode_parallel_f64(skml_ctx* ctx, const double* x_dev, int64_t n, int32_t threads,
+                                   const skml_params* params, void* payload_dev, size_t payload_cap);
+int skml_dense_sketch_shard_f64(skml_ctx* ctx, const double* x_dev, int64_t n, const int64_t* shard_n,
+                                int32_t nshards, int32_t shard, int64_t seed, void* record_dev);
+int skml_dense_encode_sharded_f64(skml_ctx* ctx, const double* x_dev, int64_t n, const int64_t* shard_n,
+                                  int32_t nshards, int32_t shard, const void* records_dev,
                                   const skml_params* params, void* payload_dev, size_t payload_cap);
 
 /* Split-injected parity mode: quantise against a caller-given split table (host doubles,

@@ -6,6 +6,7 @@ SURVEY.md §8a-A2 derives, not as the carry-propagating buffer of HeapQuantileSk
 that agreement between the two is evidence for both.  Small inputs only (pure-Python loops).
 
 Covered: java.util.Random, the sketch summary + getQuantiles(int), Maths.unique, findZeroIdx,
+parallelQuantize (here as the carry-propagating buffer: the merge has no tree form),
 bins = upper_bound(splits, x), getValues, the 8 hashes, calGroupEdges, DeltaAdaptive encode.
 """
 from __future__ import annotations
@@ -168,6 +169,102 @@ def quantize(values, bin_num, seed):
           [0.5 * (uniq[-1] + vmax)]
     return dict(bin_num=B, zero_idx=zero, min=vmin, max=vmax, splits=sp, bins=bins,
                 values=np.array(lut))
+
+
+# -------------------------------------------------------------------------- parallelQuantize
+class _CarrySketch:
+    """HeapQuantileSketch as its carry-propagating buffer (update / merge /
+    inPlacePropagation*, HeapQuantileSketch.java:74-124,186-228), levels as a dict."""
+
+    def __init__(self, rng):
+        self.rng = rng
+        self.n = 0
+        self.base = []
+        self.levels = {}
+        self.mn = 1.7976931348623157e308  # HeapQuantileSketch.java:67-68
+        self.mx = 4.9e-324
+
+    def _halve(self, buf):  # QSketchUtils.compactBuffer (QSketchUtils.java:45-51)
+        odd = 1 if self.rng.next_boolean() else 0
+        return buf[odd::2][:128]
+
+    def _carry(self, node, level):  # levelwisePropagation (QSketchUtils.java:71-82)
+        while level in self.levels:
+            node = self._halve(_merge_newer_first(self.levels.pop(level), node))
+            level += 1
+        self.levels[level] = node
+
+    def update(self, v):
+        if v != v:
+            raise ValueError("Encounter NaN value")
+        self.mx = max(self.mx, v, key=_total_key)  # Math.max / Math.min: -0.0 < 0.0
+        self.mn = min(self.mn, v, key=_total_key)
+        self.base.append(v)
+        self.n += 1
+        if len(self.base) == 256:
+            buf = sorted(self.base, key=_total_key)
+            self.base = []
+            self._carry(self._halve(buf), 0)
+
+    def merge(self, o):
+        if o.n == 0:
+            return
+        if self.n == 0:  # copy(other)
+            self.n, self.base, self.levels = o.n, list(o.base), dict(o.levels)
+            self.mn, self.mx = o.mn, o.mx
+            return
+        total = self.n + o.n
+        for v in o.base:
+            self.update(v)
+        for lv in sorted(o.levels):  # inPlacePropagationMerge: the copied node is not halved
+            self._carry(list(o.levels[lv]), lv)
+        self.n = total
+        self.mx = max(self.mx, o.mx, key=_total_key)
+        self.mn = min(self.mn, o.mn, key=_total_key)
+
+
+def parallel_quantize(values, bin_num, threads, seed):
+    """QuantileQuantizer.parallelQuantize (QuantileQuantizer.java:53-92), the slice sketches
+    run one after another and then merged in slice order, all from one Random(seed); no
+    Maths.unique."""
+    rng = JRandom(seed)
+    vals = [float(v) for v in values]
+    n = len(vals)
+    per = n // threads
+    sks = []
+    for t in range(threads):
+        lo = t * per
+        hi = n if t == threads - 1 else lo + per
+        sk = _CarrySketch(rng)
+        for v in vals[lo:hi]:
+            sk.update(v)
+        sks.append(sk)
+    acc = sks[0]
+    for o in sks[1:]:
+        acc.merge(o)
+    samples, weights = [], []
+    for lv in sorted(acc.levels):  # copyBuf2Arr: lowest level first, then the sorted base
+        samples += acc.levels[lv]
+        weights += [2 << lv] * 128
+    tail = sorted(acc.base, key=_total_key)
+    samples += tail
+    weights += [1] * len(tail)
+    order = sorted(range(len(samples)), key=lambda i: (samples[i] if samples[i] != 0 else 0.0, i))
+    smp = [samples[i] for i in order]
+    prefix = [0]
+    for i in order:
+        prefix.append(prefix[-1] + weights[i])
+    splits = quantiles(smp, prefix, n, bin_num)
+    vmin, vmax = acc.mn, acc.mx
+    if vmin > 0:
+        zero = 0
+    elif vmax < 0:
+        zero = bin_num - 1
+    else:
+        zero = next((t for t, sp in enumerate(splits) if not sp < 0.0), bin_num - 1)
+    sp = np.array(splits)
+    bins = np.searchsorted(sp, np.asarray(vals), side="right").astype(np.int32)
+    return dict(bin_num=bin_num, zero_idx=zero, min=vmin, max=vmax, splits=sp, bins=bins)
 
 
 # -------------------------------------------------------------------------- hashes

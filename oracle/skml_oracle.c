@@ -424,13 +424,15 @@ int orc_quantize(const double* values, int32_t n, int32_t bin_num, int64_t seed,
 int orc_parallel_quantize(const double* values, int32_t n, int32_t bin_num, int32_t threads,
                           int64_t seed, orc_quant_header* hdr, int32_t* bins) {
     if (bin_num <= 1 || bin_num > 65536 || threads < 1) return ORC_E_ARG;
-    orc_jrandom* rngs = (orc_jrandom*)malloc(sizeof(orc_jrandom) * (size_t)threads);
+    /* One schedule the reference can run: the T slice sketches one after another, then the
+     * merges, all drawing from the one static Random (QSketchUtils.java:9) seeded with `seed`. */
+    orc_jrandom rng;
+    orc_jr_seed(&rng, seed);
     qsk* sk = (qsk*)malloc(sizeof(qsk) * (size_t)threads);
     int st = ORC_OK;
     int32_t per = n / threads;
     for (int32_t t = 0; t < threads && !st; t++) {
-        orc_jr_seed(&rngs[t], seed + t);
-        qsk_init(&sk[t], &rngs[t]);
+        qsk_init(&sk[t], &rng);
         int32_t from = t * per, to = (t + 1 == threads) ? n : from + per;
         for (int32_t i = from; i < to && !st; i++) st = qsk_update(&sk[t], values[i]);
     }
@@ -446,7 +448,6 @@ int orc_parallel_quantize(const double* values, int32_t n, int32_t bin_num, int3
             for (int32_t i = 0; i < n; i++) bins[i] = orc_index_of(hdr, values[i]);
     }
     free(sk);
-    free(rngs);
     return st;
 }
 

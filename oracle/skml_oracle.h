@@ -67,8 +67,9 @@ typedef struct {
 /* QuantileQuantizer.quantize (QuantileQuantizer.java:27-50).  bins may be NULL. */
 int orc_quantize(const double* values, int32_t n, int32_t bin_num, int64_t seed,
                  orc_quant_header* hdr, int32_t* bins);
-/* QuantileQuantizer.parallelQuantize (QuantileQuantizer.java:53-92) with T slices.
- * Slice t's sketch draws from Random(seed + t); merging continues slice 0's stream. */
+/* QuantileQuantizer.parallelQuantize (QuantileQuantizer.java:53-92) with T slices, in the
+ * schedule where the slice sketches run one after another and then merge in slice order, all
+ * drawing from the one Random(seed) (the reference's static Random, QSketchUtils.java:9). */
 int orc_parallel_quantize(const double* values, int32_t n, int32_t bin_num, int32_t threads,
                           int64_t seed, orc_quant_header* hdr, int32_t* bins);
 /* UniformQuantizer.quantize (quantization/UniformQuantizer.java:21-45): min / max by IEEE `<` / `>`

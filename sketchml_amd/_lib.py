@@ -42,7 +42,7 @@ szp = C.POINTER(C.c_size_t)
 class Params(C.Structure):
     _fields_ = [("bin_num", C.c_int32), ("group_num", C.c_int32), ("row_num", C.c_int32),
                 ("dedup", C.c_int32), ("col_ratio", C.c_double), ("seed", C.c_int64),
-                ("hash_seed", C.c_int64), ("quant_type", C.c_int32), ("reserved", C.c_int32)]
+                ("hash_seed", C.c_int64), ("quant_type", C.c_int32), ("parallelism", C.c_int32)]
 
 
 class DenseHeader(C.Structure):
@@ -77,6 +77,15 @@ _SIGS = {
                                                     vp, C.c_size_t]),
     "skml_dense_encode_f64": (C.c_int, [vp, vp, i64, C.POINTER(Params), vp, C.c_size_t]),
     "skml_dense_encode_uniform_f32": (C.c_int, [vp, vp, i64, C.POINTER(Params), vp, C.c_size_t]),
+    "skml_dense_encode_parallel_f32": (C.c_int, [vp, vp, i64, i32, C.POINTER(Params), vp, C.c_size_t]),
+    "skml_sketch_record_bytes": (C.c_size_t, [i32]),
+    "skml_dense_encode_parallel_f64": (C.c_int, [vp, vp, i64, i32, C.POINTER(Params), vp, C.c_size_t]),
+    "skml_dense_sketch_shard_f64": (C.c_int, [vp, vp, i64, i64p, i32, i32, i64, vp]),
+    "skml_dense_encode_sharded_f64": (C.c_int, [vp, vp, i64, i64p, i32, i32, vp, C.POINTER(Params), vp,
+                                                C.c_size_t]),
+    "skml_dense_sketch_shard_f32": (C.c_int, [vp, vp, i64, i64p, i32, i32, i64, vp]),
+    "skml_dense_encode_sharded_f32": (C.c_int, [vp, vp, i64, i64p, i32, i32, vp, C.POINTER(Params), vp,
+                                                C.c_size_t]),
     "skml_dense_encode_uniform_f64": (C.c_int, [vp, vp, i64, C.POINTER(Params), vp, C.c_size_t]),
     "skml_dense_decode_f32": (C.c_int, [vp, vp, vp, i64]),
     "skml_dense_decode_f64": (C.c_int, [vp, vp, vp, i64]),

@@ -59,6 +59,9 @@ struct skml_ctx {
     size_t ranks_cap = 0;
     int64_t ranks_n = -1;
     int ranks_bins = -1;
+    // parallelQuantize: slice records + the merged sketch's export (grow-only)
+    void* sk = nullptr;
+    size_t sk_cap = 0;
     // staging
     void* stage = nullptr;
     size_t stage_cap = 0;
@@ -283,7 +286,7 @@ void skml_params_default(skml_params* p) {
     p->seed = 0;
     p->hash_seed = 0;
     p->quant_type = SKML_QUANTILE;
-    p->reserved = 0;
+    p->parallelism = 1;
 }
 
 const char* skml_last_error(void) { return g_err.c_str(); }
@@ -330,6 +333,7 @@ int skml_ctx_destroy(skml_ctx* c) {
     if (c->ws64) (void)hipFree(c->ws64);
     if (c->ranks) (void)hipFree(c->ranks);
     if (c->stage) (void)hipFree(c->stage);
+    if (c->sk) (void)hipFree(c->sk);
     for (int k = 0; k < SKML_K_COUNT; k++)
         for (hipEvent_t e : c->ev[k]) (void)hipEventDestroy(e);
     for (int i = 0; i < kScratchSlots; i++)
@@ -433,23 +437,16 @@ static int check_dense_args(skml_ctx* c, const void* x, int64_t n, int bins, con
     return SKML_OK;
 }
 
-int skml_dense_encode_f32(skml_ctx* c, const float* x, int64_t n, const skml_params* p,
-                          void* payload, size_t cap) {
-    skml_params def;
-    if (!p) {
-        skml_params_default(&def);
-        p = &def;
-    }
-    int st = check_dense_args(c, x, n, p->bin_num, payload, cap);
-    if (st) return st;
-    HIP_TRY(hipSetDevice(c->device));
-    const int64_t chunks = n / kChunk;
-    Workspace w;
-    if ((st = ensure_ws(c, chunks, &w))) return st;
-    if ((st = ensure_ranks(c, n, p->bin_num))) return st;
-    const uint64_t s0 = ((uint64_t)p->seed ^ kLcgMult) & kLcgMask;
-    const int64_t nwg = (chunks + kLeafChunks - 1) / kLeafChunks;  // leaf partials (one per wave tile)
+}  // extern "C"
 
+namespace {
+// The sketch of x[0, n): leaf + upper merge passes.  summary: the last pass's last workgroup
+// also runs the summary into `payload` (returns *fused = true); otherwise the levels stay in
+// w.roots and the partials in w.part for a caller-side summary or a SketchRecord.
+int run_sketch_f32(skml_ctx* c, const float* x, int64_t n, uint64_t s0, const Workspace& w, const skml_params* p,
+                   void* payload, bool summary, bool* fused_out) {
+    const int64_t chunks = n / kChunk;
+    const int64_t nwg = (chunks + kLeafChunks - 1) / kLeafChunks;  // leaf partials (one per wave tile)
     bool fused = false;
     if (chunks > 0) {
         {
@@ -497,7 +494,7 @@ int skml_dense_encode_f32(skml_ctx* c, const float* x, int64_t n, const skml_par
             pass.wg_prefix[pass.njobs] = wg;
             passes.push_back(pass);
         }
-        if (!passes.empty()) passes.back().fuse_summary = 1;
+        if (summary && !passes.empty()) passes.back().fuse_summary = 1;
         const float* src = w.nodes6;
         float* dst = w.upA;
         for (size_t i = 0; i < passes.size(); i++) {
@@ -512,8 +509,51 @@ int skml_dense_encode_f32(skml_ctx* c, const float* x, int64_t n, const skml_par
             dst = next_dst;
             if (fuse_next) break;
         }
-        fused = !passes.empty();
+        fused = summary && !passes.empty();
     }
+    *fused_out = fused;
+    return SKML_OK;
+}
+
+// java.util.Random state after k more draws (affine jump-ahead by squaring)
+uint64_t lcg_skip(uint64_t s, uint64_t k) {
+    uint64_t a = kLcgMult, c = kLcgAdd;
+    while (k) {
+        if (k & 1) s = (a * s + c) & kLcgMask;
+        c = (a * c + c) & kLcgMask;
+        a = (a * a) & kLcgMask;
+        k >>= 1;
+    }
+    return s;
+}
+// Random draws of one sketch over n updates: chunk c's leaf compaction plus its carries,
+// sum over c < C of (1 + trailing_ones(c)) = 2C - popcount(C).
+uint64_t sketch_draws(int64_t n) {
+    const uint64_t C = (uint64_t)(n / kChunk);
+    return 2 * C - (uint64_t)__builtin_popcountll(C);
+}
+}  // namespace
+
+extern "C" {
+
+int skml_dense_encode_f32(skml_ctx* c, const float* x, int64_t n, const skml_params* p,
+                          void* payload, size_t cap) {
+    skml_params def;
+    if (!p) {
+        skml_params_default(&def);
+        p = &def;
+    }
+    int st = check_dense_args(c, x, n, p->bin_num, payload, cap);
+    if (st) return st;
+    HIP_TRY(hipSetDevice(c->device));
+    const int64_t chunks = n / kChunk;
+    Workspace w;
+    if ((st = ensure_ws(c, chunks, &w))) return st;
+    if ((st = ensure_ranks(c, n, p->bin_num))) return st;
+    const uint64_t s0 = ((uint64_t)p->seed ^ kLcgMult) & kLcgMask;
+    const int64_t nwg = (chunks + kLeafChunks - 1) / kLeafChunks;
+    bool fused = false;
+    if ((st = run_sketch_f32(c, x, n, s0, w, p, payload, true, &fused))) return st;
     if (!fused) {
         KernelTimer kt(c, SKML_K_SUMMARY);
         HIP_TRY(launch_summary(c->stream, x, n, w.part, nwg, w.roots, c->ranks, p->bin_num,
@@ -525,6 +565,164 @@ int skml_dense_encode_f32(skml_ctx* c, const float* x, int64_t n, const skml_par
     }
     return SKML_OK;
 }
+
+}  // extern "C"
+
+namespace {
+struct SkScratch {
+    SketchRecord* recs;  // own records (parallel path)
+    float* roots;
+    float* tail;
+    LeafPartial* part;
+};
+int ensure_sk(skml_ctx* c, int nrec_own, int nrec, SkScratch* out) {
+    const size_t rec_bytes = align_up(sizeof(SketchRecord) * (size_t)nrec_own, 256);
+    const size_t roots_bytes = align_up(sizeof(float) * kMaxLevels * kK, 256);
+    const size_t tail_bytes = align_up(sizeof(float) * kChunk, 256);
+    const size_t need = rec_bytes + roots_bytes + tail_bytes + sizeof(LeafPartial) * (size_t)nrec;
+    if (need > c->sk_cap) {
+        if (c->sk) {
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            HIP_TRY(hipFree(c->sk));
+            c->sk = nullptr;
+            c->sk_cap = 0;
+        }
+        if (hipMalloc(&c->sk, need) != hipSuccess) return fail(SKML_E_OOM, "sketch scratch %zu B", need);
+        c->sk_cap = need;
+    }
+    uint8_t* b = static_cast<uint8_t*>(c->sk);
+    out->recs = reinterpret_cast<SketchRecord*>(b);
+    out->roots = reinterpret_cast<float*>(b + rec_bytes);
+    out->tail = reinterpret_cast<float*>(b + rec_bytes + roots_bytes);
+    out->part = reinterpret_cast<LeafPartial*>(b + rec_bytes + roots_bytes + tail_bytes);
+    return SKML_OK;
+}
+
+int check_shards(const int64_t* shard_n, int32_t nshards, int32_t shard, int64_t n, int64_t* total,
+                 uint64_t* draws_before, uint64_t* draws_all) {
+    if (!shard_n || nshards < 1 || shard < 0 || shard >= nshards)
+        return fail(SKML_E_ARG, "bad shard table (nshards=%d shard=%d)", nshards, shard);
+    int64_t tot = 0;
+    uint64_t before = 0, all = 0;
+    for (int i = 0; i < nshards; i++) {
+        if (shard_n[i] < 0) return fail(SKML_E_ARG, "shard %d has %lld values", i, (long long)shard_n[i]);
+        tot += shard_n[i];
+        if (tot > 0x7FFFFFFFLL) return fail(SKML_E_ARG, "total n=%lld outside Java int range", (long long)tot);
+        if (i < shard) before += sketch_draws(shard_n[i]);
+        all += sketch_draws(shard_n[i]);
+    }
+    if (shard_n[shard] != n)
+        return fail(SKML_E_ARG, "shard %d: n=%lld but the table says %lld", shard, (long long)n,
+                    (long long)shard_n[shard]);
+    *total = tot;
+    *draws_before = before;
+    *draws_all = all;
+    return SKML_OK;
+}
+
+// Sketch x[0, n) with draws starting after `skip` draws of Random(seed) into rec.
+int sketch_into_record(skml_ctx* c, const float* x, int64_t n, int64_t seed, uint64_t skip, SketchRecord* rec) {
+    const int64_t chunks = n / kChunk;
+    Workspace w;
+    int st = ensure_ws(c, chunks, &w);
+    if (st) return st;
+    skml_params p;
+    skml_params_default(&p);
+    const uint64_t s0 = lcg_skip(((uint64_t)seed ^ kLcgMult) & kLcgMask, skip);
+    bool fused = false;
+    if ((st = run_sketch_f32(c, x, n, s0, w, &p, nullptr, false, &fused))) return st;
+    KernelTimer kt(c, SKML_K_SUMMARY);
+    HIP_TRY(launch_sketch_record(c->stream, x, n, w.part, (chunks + kLeafChunks - 1) / kLeafChunks, w.roots, rec));
+    return SKML_OK;
+}
+
+// Merge nrec records, summary of n_total values, quantize x[0, n).
+int merge_and_quantize(skml_ctx* c, const float* x, int64_t n, const SketchRecord* recs, int nrec, int64_t n_total,
+                       uint64_t draws_all, const skml_params* p, void* payload, const SkScratch& sk) {
+    Workspace w;
+    int st = ensure_ws(c, n / kChunk, &w);
+    if (st) return st;
+    if ((st = ensure_ranks(c, n_total, p->bin_num))) return st;
+    const uint64_t s0 = ((uint64_t)p->seed ^ kLcgMult) & kLcgMask;
+    {
+        KernelTimer kt(c, SKML_K_SUMMARY);
+        HIP_TRY(launch_sketch_merge(c->stream, recs, nrec, s0, draws_all, c->jump_tab, n_total, n, c->ranks,
+                                    p->bin_num, p->dedup ? 1 : 0, payload, w.raw, w.lut, sk.roots, sk.tail, sk.part));
+    }
+    KernelTimer kt(c, SKML_K_QUANTIZE);
+    HIP_TRY(launch_quantize(c->stream, x, n, payload, w.lut, p->bin_num));
+    return SKML_OK;
+}
+}  // namespace
+
+extern "C" {
+
+size_t skml_sketch_record_bytes(int32_t fp64) { return fp64 ? sizeof(SketchRecord64) : sizeof(SketchRecord); }
+
+int skml_dense_sketch_shard_f32(skml_ctx* c, const float* x, int64_t n, const int64_t* shard_n, int32_t nshards,
+                                int32_t shard, int64_t seed, void* record_dev) {
+    if (!c) return fail(SKML_E_ARG, "ctx is NULL");
+    if (n > 0 && (!x || ((uintptr_t)x) % 16 != 0))
+        return fail(SKML_E_ARG, "input must be a 16-byte aligned device pointer");
+    if (!record_dev || ((uintptr_t)record_dev) % 16 != 0)
+        return fail(SKML_E_ARG, "record must be a 16-byte aligned device pointer");
+    int64_t total;
+    uint64_t before, all;
+    int st = check_shards(shard_n, nshards, shard, n, &total, &before, &all);
+    if (st) return st;
+    HIP_TRY(hipSetDevice(c->device));
+    return sketch_into_record(c, x, n, seed, before, static_cast<SketchRecord*>(record_dev));
+}
+
+int skml_dense_encode_sharded_f32(skml_ctx* c, const float* x, int64_t n, const int64_t* shard_n, int32_t nshards,
+                                  int32_t shard, const void* records_dev, const skml_params* p, void* payload,
+                                  size_t cap) {
+    skml_params def;
+    if (!p) {
+        skml_params_default(&def);
+        def.dedup = 0;
+        p = &def;
+    }
+    int st = check_dense_args(c, x, n, p->bin_num, payload, cap);
+    if (st) return st;
+    if (!records_dev || ((uintptr_t)records_dev) % 16 != 0)
+        return fail(SKML_E_ARG, "records must be a 16-byte aligned device pointer");
+    int64_t total;
+    uint64_t before, all;
+    if ((st = check_shards(shard_n, nshards, shard, n, &total, &before, &all))) return st;
+    HIP_TRY(hipSetDevice(c->device));
+    SkScratch sk;
+    if ((st = ensure_sk(c, 0, nshards, &sk))) return st;
+    return merge_and_quantize(c, x, n, static_cast<const SketchRecord*>(records_dev), nshards, total, all, p, payload,
+                              sk);
+}
+
+int skml_dense_encode_parallel_f32(skml_ctx* c, const float* x, int64_t n, int32_t threads, const skml_params* p,
+                                   void* payload, size_t cap) {
+    skml_params def;
+    if (!p) {
+        skml_params_default(&def);
+        def.dedup = 0;
+        p = &def;
+    }
+    int st = check_dense_args(c, x, n, p->bin_num, payload, cap);
+    if (st) return st;
+    if (threads < 1 || threads > 65536) return fail(SKML_E_ARG, "Invalid parallelism: %d", threads);
+    HIP_TRY(hipSetDevice(c->device));
+    // QuantileQuantizer.java:66-68: thread t takes [t*(n/T), ...), the last one the remainder
+    std::vector<int64_t> shard_n((size_t)threads, n / threads);
+    shard_n.back() = n - (int64_t)(threads - 1) * (n / threads);
+    SkScratch sk;
+    if ((st = ensure_sk(c, threads, threads, &sk))) return st;
+    uint64_t skip = 0;
+    for (int t = 0; t < threads; t++) {
+        const float* xt = x + (int64_t)t * (n / threads);
+        if ((st = sketch_into_record(c, xt, shard_n[t], p->seed, skip, sk.recs + t))) return st;
+        skip += sketch_draws(shard_n[t]);
+    }
+    return merge_and_quantize(c, x, n, sk.recs, threads, n, skip, p, payload, sk);
+}
+
 
 int skml_dense_encode_with_splits_f32(skml_ctx* c, const float* x, int64_t n, const double* splits,
                                       int32_t nsplits, double mn, double mx, void* payload,
@@ -547,22 +745,12 @@ int skml_dense_encode_with_splits_f32(skml_ctx* c, const float* x, int64_t n, co
     return SKML_OK;
 }
 
-int skml_dense_encode_f64(skml_ctx* c, const double* x, int64_t n, const skml_params* p, void* payload,
-                          size_t cap) {
-    skml_params def;
-    if (!p) {
-        skml_params_default(&def);
-        p = &def;
-    }
-    int st = check_dense_args(c, x, n, p->bin_num, payload, cap);
-    if (st) return st;
-    HIP_TRY(hipSetDevice(c->device));
+}  // extern "C"
+
+namespace {
+// fp64 sketch of x[0, n): leaf + per-tree merge passes; levels in w.roots, partials in w.part.
+int run_sketch_f64(skml_ctx* c, const double* x, int64_t n, uint64_t s0, const Workspace64& w) {
     const int64_t chunks = n / kChunk;
-    Workspace64 w;
-    if ((st = ensure_ws64(c, chunks, &w))) return st;
-    if ((st = ensure_ranks(c, n, p->bin_num))) return st;
-    const uint64_t s0 = ((uint64_t)p->seed ^ kLcgMult) & kLcgMask;
-    const int64_t tiles = (chunks + kLeafChunks - 1) / kLeafChunks;
     {
         KernelTimer kt(c, SKML_K_LEAF);
         HIP_TRY(launch_leaf64(c->stream, x, chunks, s0, c->jump_tab, w.part, w.nodes6, w.roots));
@@ -589,6 +777,91 @@ int skml_dense_encode_f64(skml_ctx* c, const double* x, int64_t n, const skml_pa
             level += g;
         }
     }
+    return SKML_OK;
+}
+
+struct SkScratch64 {
+    SketchRecord64* recs;
+    double* roots;
+    double* tail;
+    LeafPartial64* part;
+};
+int ensure_sk64(skml_ctx* c, int nrec_own, int nrec, SkScratch64* out) {
+    const size_t rec_bytes = align_up(sizeof(SketchRecord64) * (size_t)nrec_own, 256);
+    const size_t roots_bytes = align_up(sizeof(double) * kMaxLevels * kK, 256);
+    const size_t tail_bytes = align_up(sizeof(double) * kChunk, 256);
+    const size_t need = rec_bytes + roots_bytes + tail_bytes + sizeof(LeafPartial64) * (size_t)nrec;
+    if (need > c->sk_cap) {
+        if (c->sk) {
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            HIP_TRY(hipFree(c->sk));
+            c->sk = nullptr;
+            c->sk_cap = 0;
+        }
+        if (hipMalloc(&c->sk, need) != hipSuccess) return fail(SKML_E_OOM, "sketch scratch %zu B", need);
+        c->sk_cap = need;
+    }
+    uint8_t* b = static_cast<uint8_t*>(c->sk);
+    out->recs = reinterpret_cast<SketchRecord64*>(b);
+    out->roots = reinterpret_cast<double*>(b + rec_bytes);
+    out->tail = reinterpret_cast<double*>(b + rec_bytes + roots_bytes);
+    out->part = reinterpret_cast<LeafPartial64*>(b + rec_bytes + roots_bytes + tail_bytes);
+    return SKML_OK;
+}
+
+int sketch_into_record64(skml_ctx* c, const double* x, int64_t n, int64_t seed, uint64_t skip, SketchRecord64* rec) {
+    const int64_t chunks = n / kChunk;
+    Workspace64 w;
+    int st = ensure_ws64(c, chunks, &w);
+    if (st) return st;
+    const uint64_t s0 = lcg_skip(((uint64_t)seed ^ kLcgMult) & kLcgMask, skip);
+    if ((st = run_sketch_f64(c, x, n, s0, w))) return st;
+    KernelTimer kt(c, SKML_K_SUMMARY);
+    HIP_TRY(launch_sketch_record64(c->stream, x, n, w.part, (chunks + kLeafChunks - 1) / kLeafChunks, w.roots, rec));
+    return SKML_OK;
+}
+
+int merge_and_quantize64(skml_ctx* c, const double* x, int64_t n, const SketchRecord64* recs, int nrec,
+                         int64_t n_total, uint64_t draws_all, const skml_params* p, void* payload,
+                         const SkScratch64& sk) {
+    Workspace64 w;
+    int st = ensure_ws64(c, n / kChunk, &w);
+    if (st) return st;
+    Workspace wq;  // the quantize LUT lives in the fp32 workspace
+    if ((st = ensure_ws(c, 0, &wq))) return st;
+    if ((st = ensure_ranks(c, n_total, p->bin_num))) return st;
+    const uint64_t s0 = ((uint64_t)p->seed ^ kLcgMult) & kLcgMask;
+    {
+        KernelTimer kt(c, SKML_K_SUMMARY);
+        HIP_TRY(launch_sketch_merge64(c->stream, recs, nrec, s0, draws_all, c->jump_tab, sk.roots, sk.tail, sk.part));
+        HIP_TRY(launch_summary64(c->stream, nullptr, n_total, sk.part, nrec, sk.roots, c->ranks, p->bin_num,
+                                 p->dedup ? 1 : 0, payload, w.raw, wq.lut, sk.tail, 1, n));
+    }
+    KernelTimer kt(c, SKML_K_QUANTIZE);
+    HIP_TRY(launch_quantize64(c->stream, x, n, payload, wq.lut, nullptr, p->bin_num));
+    return SKML_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int skml_dense_encode_f64(skml_ctx* c, const double* x, int64_t n, const skml_params* p, void* payload,
+                          size_t cap) {
+    skml_params def;
+    if (!p) {
+        skml_params_default(&def);
+        p = &def;
+    }
+    int st = check_dense_args(c, x, n, p->bin_num, payload, cap);
+    if (st) return st;
+    HIP_TRY(hipSetDevice(c->device));
+    const int64_t chunks = n / kChunk;
+    Workspace64 w;
+    if ((st = ensure_ws64(c, chunks, &w))) return st;
+    if ((st = ensure_ranks(c, n, p->bin_num))) return st;
+    const uint64_t s0 = ((uint64_t)p->seed ^ kLcgMult) & kLcgMask;
+    const int64_t tiles = (chunks + kLeafChunks - 1) / kLeafChunks;
+    if ((st = run_sketch_f64(c, x, n, s0, w))) return st;
     Workspace wq;  // the quantize LUT lives in the fp32 workspace
     if ((st = ensure_ws(c, 0, &wq))) return st;
     {
@@ -601,6 +874,69 @@ int skml_dense_encode_f64(skml_ctx* c, const double* x, int64_t n, const skml_pa
         HIP_TRY(launch_quantize64(c->stream, x, n, payload, wq.lut, nullptr, p->bin_num));
     }
     return SKML_OK;
+}
+
+int skml_dense_sketch_shard_f64(skml_ctx* c, const double* x, int64_t n, const int64_t* shard_n, int32_t nshards,
+                                int32_t shard, int64_t seed, void* record_dev) {
+    if (!c) return fail(SKML_E_ARG, "ctx is NULL");
+    if (n > 0 && (!x || ((uintptr_t)x) % 16 != 0))
+        return fail(SKML_E_ARG, "input must be a 16-byte aligned device pointer");
+    if (!record_dev || ((uintptr_t)record_dev) % 16 != 0)
+        return fail(SKML_E_ARG, "record must be a 16-byte aligned device pointer");
+    int64_t total;
+    uint64_t before, all;
+    int st = check_shards(shard_n, nshards, shard, n, &total, &before, &all);
+    if (st) return st;
+    HIP_TRY(hipSetDevice(c->device));
+    return sketch_into_record64(c, x, n, seed, before, static_cast<SketchRecord64*>(record_dev));
+}
+
+int skml_dense_encode_sharded_f64(skml_ctx* c, const double* x, int64_t n, const int64_t* shard_n, int32_t nshards,
+                                  int32_t shard, const void* records_dev, const skml_params* p, void* payload,
+                                  size_t cap) {
+    skml_params def;
+    if (!p) {
+        skml_params_default(&def);
+        def.dedup = 0;
+        p = &def;
+    }
+    int st = check_dense_args(c, x, n, p->bin_num, payload, cap);
+    if (st) return st;
+    if (!records_dev || ((uintptr_t)records_dev) % 16 != 0)
+        return fail(SKML_E_ARG, "records must be a 16-byte aligned device pointer");
+    int64_t total;
+    uint64_t before, all;
+    if ((st = check_shards(shard_n, nshards, shard, n, &total, &before, &all))) return st;
+    HIP_TRY(hipSetDevice(c->device));
+    SkScratch64 sk;
+    if ((st = ensure_sk64(c, 0, nshards, &sk))) return st;
+    return merge_and_quantize64(c, x, n, static_cast<const SketchRecord64*>(records_dev), nshards, total, all, p,
+                                payload, sk);
+}
+
+int skml_dense_encode_parallel_f64(skml_ctx* c, const double* x, int64_t n, int32_t threads, const skml_params* p,
+                                   void* payload, size_t cap) {
+    skml_params def;
+    if (!p) {
+        skml_params_default(&def);
+        def.dedup = 0;
+        p = &def;
+    }
+    int st = check_dense_args(c, x, n, p->bin_num, payload, cap);
+    if (st) return st;
+    if (threads < 1 || threads > 65536) return fail(SKML_E_ARG, "Invalid parallelism: %d", threads);
+    HIP_TRY(hipSetDevice(c->device));
+    std::vector<int64_t> shard_n((size_t)threads, n / threads);
+    shard_n.back() = n - (int64_t)(threads - 1) * (n / threads);
+    SkScratch64 sk;
+    if ((st = ensure_sk64(c, threads, threads, &sk))) return st;
+    uint64_t skip = 0;
+    for (int t = 0; t < threads; t++) {
+        const double* xt = x + (int64_t)t * (n / threads);
+        if ((st = sketch_into_record64(c, xt, shard_n[t], p->seed, skip, sk.recs + t))) return st;
+        skip += sketch_draws(shard_n[t]);
+    }
+    return merge_and_quantize64(c, x, n, sk.recs, threads, n, skip, p, payload, sk);
 }
 
 int skml_dense_encode_uniform_f32(skml_ctx* c, const float* x, int64_t n, const skml_params* p, void* payload,

@@ -385,7 +385,8 @@ __global__ __launch_bounds__(512) void k_summary64(const double* __restrict__ x,
                                                    const double* __restrict__ roots,
                                                    const int64_t* __restrict__ ranks, int req_bins, int dedup,
                                                    uint8_t* __restrict__ payload, double* __restrict__ g_raw,
-                                                   QuantLut* __restrict__ lut) {
+                                                   QuantLut* __restrict__ lut, const double* __restrict__ tail_in,
+                                                   int sharded, int64_t n_local) {
     extern __shared__ __align__(16) uint8_t smem64[];
     Summary64Shared& S = *reinterpret_cast<Summary64Shared*>(smem64);
     const int t = threadIdx.x, T = blockDim.x;
@@ -393,7 +394,8 @@ __global__ __launch_bounds__(512) void k_summary64(const double* __restrict__ x,
     double* splits = reinterpret_cast<double*>(payload + kHeaderBytes);
     const int64_t chunks = n / kChunk;
     const int tail = (int)(n - chunks * kChunk);
-    const double* xt = x + chunks * kChunk;
+    const double* xt = tail_in ? tail_in : x + chunks * kChunk;
+    const int64_t n_hdr = sharded ? n_local : n;
 
     if (t == 0) {
         S.min_key = ~0ull;
@@ -473,7 +475,7 @@ __global__ __launch_bounds__(512) void k_summary64(const double* __restrict__ x,
         if (fmax > vmax) vmax = fmax;   // Math.max(Double.MIN_VALUE, x)
     }
     if (S.flags & 1u) {  // NaN: QuantileSketchException("Encounter NaN value")
-        if (t == 0) write_header(hdr, SKML_E_NAN, n, req_bins, 0, req_bins, vmin, vmax);
+        if (t == 0) write_header(hdr, SKML_E_NAN, n_hdr, req_bins, 0, req_bins, vmin, vmax);
         return;
     }
     // blockyMergeSort == stable sort under IEEE `<=` (left run wins ties): rank across runs
@@ -557,7 +559,7 @@ __global__ __launch_bounds__(512) void k_summary64(const double* __restrict__ x,
         if (vmin > 0.0) zero = 0;
         else if (vmax < 0.0) zero = bin_num - 1;
         else zero = S.zero < bin_num - 1 ? S.zero : bin_num - 1;
-        write_header(hdr, SKML_OK, n, bin_num, zero, req_bins, vmin, vmax);
+        write_header(hdr, SKML_OK, n_hdr, bin_num, zero, req_bins, vmin, vmax);
     }
     // quantize bucket LUT over the RU(fp32) images of the splits (staging aliases sorted[] + w[])
     const int nsplit = bin_num - 1;
@@ -1027,7 +1029,7 @@ hipError_t launch_tree64(hipStream_t st, const double* src, double* dst, int64_t
 
 hipError_t launch_summary64(hipStream_t st, const double* x, int64_t n, const LeafPartial64* part, int64_t nparts,
                             const double* roots, const int64_t* ranks, int req_bins, int dedup, void* payload,
-                            double* g_raw, QuantLut* lut) {
+                            double* g_raw, QuantLut* lut, const double* tail, int sharded, int64_t n_local) {
     static bool attr = false;
     if (!attr) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_summary64),
@@ -1037,7 +1039,8 @@ hipError_t launch_summary64(hipStream_t st, const double* x, int64_t n, const Le
         attr = true;
     }
     hipLaunchKernelGGL(k_summary64, dim3(1), dim3(512), sizeof(Summary64Shared), st, x, n, part, nparts, roots,
-                       ranks, req_bins, dedup, reinterpret_cast<uint8_t*>(payload), g_raw, lut);
+                       ranks, req_bins, dedup, reinterpret_cast<uint8_t*>(payload), g_raw, lut, tail, sharded,
+                       n_local);
     return hipGetLastError();
 }
 
@@ -1088,6 +1091,167 @@ hipError_t launch_uniform(hipStream_t st, const float* x, int64_t n, int bin_num
 hipError_t launch_uniform64(hipStream_t st, const double* x, int64_t n, int bin_num, UniPartial* part,
                             void* payload, QuantLut* lut, int* qflags) {
     return launch_uniform_t<double>(st, x, n, bin_num, part, payload, lut, qflags);
+}
+
+// =============================================================================================
+// parallelQuantize over fp64 slices: record export and the in-order HeapQuantileSketch.merge
+// (see k_sketch_merge in skml_sketch.hip; HeapQuantileSketch.java:186-228).  The merged state is
+// written in the summary's layout and k_summary64 runs on it.
+// =============================================================================================
+__global__ __launch_bounds__(512) void k_sketch_record64(const double* __restrict__ x, int64_t n,
+                                                         const LeafPartial64* __restrict__ part, int64_t nparts,
+                                                         const double* __restrict__ roots, SketchRecord64* rec) {
+    __shared__ unsigned long long s_mn, s_mx;
+    __shared__ uint32_t s_fl;
+    const int t = threadIdx.x, T = blockDim.x;
+    const int64_t chunks = n / kChunk;
+    const int tail = (int)(n - chunks * kChunk);
+    const double* xt = x + chunks * kChunk;
+    if (t == 0) {
+        s_mn = ~0ull;
+        s_mx = 0ull;
+        s_fl = 0u;
+    }
+    __syncthreads();
+    uint64_t mn = ~0ull, mx = 0ull;
+    uint32_t fl = 0u;
+    for (int64_t i = t; i < nparts; i += T) {
+        const LeafPartial64 p = part[i];
+        mn = p.min_key < mn ? p.min_key : mn;
+        mx = p.max_key > mx ? p.max_key : mx;
+        fl |= p.flags;
+    }
+    for (int i = t; i < tail; i += T) {
+        const uint64_t b = (uint64_t)__double_as_longlong(xt[i]);
+        fl |= is_nan64(b) ? 1u : 0u;
+        const uint64_t k = d2key(b);
+        mn = k < mn ? k : mn;
+        mx = k > mx ? k : mx;
+        rec->tail[i] = xt[i];
+    }
+    atomicMin(&s_mn, (unsigned long long)mn);
+    atomicMax(&s_mx, (unsigned long long)mx);
+    if (fl) atomicOr(&s_fl, fl);
+    for (int l = 0; l < kMaxLevels; l++)
+        if ((chunks >> l) & 1)
+            for (int i = t; i < kK; i += T) rec->level[l][i] = roots[(size_t)l * kK + i];
+    __syncthreads();
+    if (t == 0) {
+        rec->n = n;
+        rec->mm = LeafPartial64{s_mn, s_mx, s_fl, 0u};
+    }
+}
+
+hipError_t launch_sketch_record64(hipStream_t st, const double* x, int64_t n, const LeafPartial64* part,
+                                  int64_t nparts, const double* roots, SketchRecord64* rec) {
+    hipLaunchKernelGGL(k_sketch_record64, dim3(1), dim3(512), 0, st, x, n, part, nparts, roots, rec);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(512) void k_sketch_merge64(const SketchRecord64* __restrict__ recs, int nrec,
+                                                        uint64_t s0, uint64_t bit0,
+                                                        const uint64_t* __restrict__ tab, double* g_roots,
+                                                        double* g_tail, LeafPartial64* g_part) {
+    __shared__ double lv[kMaxLevels][kK];
+    __shared__ double base[kChunk];
+    __shared__ double tmp[kChunk];
+    const int t = threadIdx.x;
+    uint64_t pattern = 0, bit = bit0;
+    int64_t nacc = 0;
+    int base_cnt = 0;
+    auto first_free = [&](int from) {
+        int l = from;
+        while ((pattern >> l) & 1ull) l++;
+        return l;
+    };
+    // levelwisePropagation: mergeArrays (IEEE `<`, a tie emits the carried node first) + compact
+    auto carry = [&](int from, int dest) {
+        for (int l = from; l < dest; l++) {
+            const uint32_t odd = lcg_bit(tab, s0, bit++);
+            if (t < kChunk) {
+                double v;
+                int pos;
+                if (t < kK) {
+                    v = lv[l][t];
+                    pos = t + count_le64(lv[dest], v);
+                } else {
+                    v = lv[dest][t - kK];
+                    pos = (t - kK) + count_lt64(lv[l], v);
+                }
+                if (((uint32_t)pos & 1u) == odd) tmp[pos >> 1] = v;
+            }
+            __syncthreads();
+            if (t < kK) lv[dest][t] = tmp[t];
+            __syncthreads();
+        }
+    };
+    auto flush_base = [&]() {
+        if (t < kChunk) {
+            const double v = base[t];
+            const uint64_t kv = dk(v);
+            int rank = 0;
+            for (int j = 0; j < kChunk; j++) {
+                const uint64_t kj = dk(base[j]);
+                rank += (kj < kv) || (kj == kv && j < t);
+            }
+            tmp[rank] = v;
+        }
+        __syncthreads();
+        const int dest = first_free(0);
+        const uint32_t odd = lcg_bit(tab, s0, bit++);
+        if (t < kK) lv[dest][t] = tmp[2 * t + odd];
+        __syncthreads();
+        carry(0, dest);
+        pattern += 1;
+        base_cnt = 0;
+    };
+    for (int r = 0; r < nrec; r++) {
+        const SketchRecord64* R = recs + r;
+        const int64_t rn = R->n;
+        if (rn <= 0) continue;
+        const uint64_t rpat = (uint64_t)(rn / kChunk);
+        const int rtail = (int)(rn % kChunk);
+        if (nacc == 0) {
+            for (int l = 0; l < kMaxLevels; l++)
+                if ((rpat >> l) & 1ull)
+                    if (t < kK) lv[l][t] = R->level[l][t];
+            if (t < rtail) base[t] = R->tail[t];
+            __syncthreads();
+            pattern = rpat;
+            base_cnt = rtail;
+            nacc = rn;
+            continue;
+        }
+        for (int i = 0; i < rtail;) {
+            const int take = min(rtail - i, kChunk - base_cnt);
+            if (t < take) base[base_cnt + t] = R->tail[i + t];
+            __syncthreads();
+            base_cnt += take;
+            i += take;
+            if (base_cnt == kChunk) flush_base();
+        }
+        for (int l = 0; l < kMaxLevels; l++) {
+            if (!((rpat >> l) & 1ull)) continue;
+            const int dest = first_free(l);
+            if (t < kK) lv[dest][t] = R->level[l][t];
+            __syncthreads();
+            carry(l, dest);
+            pattern += 1ull << l;
+        }
+        nacc += rn;
+    }
+    for (int l = 0; l < kMaxLevels; l++)
+        if ((pattern >> l) & 1ull)
+            if (t < kK) g_roots[(size_t)l * kK + t] = lv[l][t];
+    if (t < base_cnt) g_tail[t] = base[t];
+    for (int r = t; r < nrec; r += blockDim.x) g_part[r] = recs[r].mm;
+}
+
+hipError_t launch_sketch_merge64(hipStream_t st, const SketchRecord64* recs, int nrec, uint64_t s0, uint64_t bit0,
+                                 const uint64_t* jump_tab, double* roots, double* tail, LeafPartial64* part) {
+    hipLaunchKernelGGL(k_sketch_merge64, dim3(1), dim3(512), 0, st, recs, nrec, s0, bit0, jump_tab, roots, tail,
+                       part);
+    return hipGetLastError();
 }
 
 }  // namespace skml

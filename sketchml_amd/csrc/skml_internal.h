@@ -61,6 +61,29 @@ struct LeafPartial {
     uint32_t pad;
 };
 
+// One HeapQuantileSketch's state (a parallelQuantize slice sketch, QuantileQuantizer.java:63-75),
+// fixed size so that P of them all-gather as one buffer.  Levels are the bits of n / 256.
+struct SketchRecord {
+    int64_t n;
+    LeafPartial mm;               // min / max total-order keys, flags (bit0 NaN)
+    int64_t pad;
+    float tail[kChunk];           // base buffer in insertion order (n % 256 used)
+    float level[kMaxLevels][kK];  // level l: 128 samples, IEEE-sorted
+};
+
+// fp64 counterpart of SketchRecord.
+struct SketchRecord64 {
+    int64_t n;
+    LeafPartial64 mm;
+    double tail[kChunk];
+    double level[kMaxLevels][kK];
+};
+hipError_t launch_sketch_record64(hipStream_t st, const double* x, int64_t n, const LeafPartial64* part,
+                                  int64_t nparts, const double* roots, SketchRecord64* rec);
+// Merge of fp64 records into (roots, tail, part) for launch_summary64 (tail, sharded = 1).
+hipError_t launch_sketch_merge64(hipStream_t st, const SketchRecord64* recs, int nrec, uint64_t s0, uint64_t bit0,
+                                 const uint64_t* jump_tab, double* roots, double* tail, LeafPartial64* part);
+
 struct MergeJob {
     int64_t src_node;      // first input node index (in src buffer)
     int64_t dst_node;      // first output node index (in dst buffer), or -1 -> root slot
@@ -94,6 +117,17 @@ hipError_t launch_leaf(hipStream_t st, const float* x, int64_t chunks, uint64_t 
                        const uint64_t* jump_tab, LeafPartial* part, float* nodes6, float* roots);
 hipError_t launch_leaf_stage(hipStream_t st, int stage, const float* x, int64_t chunks, uint64_t s0,
                              const uint64_t* jump_tab, LeafPartial* part, float* scratch, float* roots);
+// Slice sketch -> record (after the leaf and the merge passes without a summary).
+hipError_t launch_sketch_record(hipStream_t st, const float* x, int64_t n, const LeafPartial* part, int64_t nparts,
+                                const float* roots, SketchRecord* rec);
+// HeapQuantileSketch.merge of recs[0..nrec) in order (compaction bits from stream index bit0
+// on), then the summary of the merged sketch (n_total values) into payload's header, splits and
+// the quantize LUT; the header's n is n_local.  scratch: kMaxLevels*kK + kChunk floats and nrec
+// LeafPartials (device).
+hipError_t launch_sketch_merge(hipStream_t st, const SketchRecord* recs, int nrec, uint64_t s0, uint64_t bit0,
+                               const uint64_t* jump_tab, int64_t n_total, int64_t n_local, const int64_t* ranks,
+                               int req_bins, int dedup, void* payload, double* scratch_raw, QuantLut* lut,
+                               float* scratch_roots, float* scratch_tail, LeafPartial* scratch_part);
 // `next` (may be null): a one-workgroup pass run by this pass's last workgroup (its src is `dst`,
 // its output `next_dst`), saving a launch.
 hipError_t launch_merge_pass(hipStream_t st, const MergePass& pass, const MergePass* next, const float* src,
@@ -123,7 +157,8 @@ hipError_t launch_tree64(hipStream_t st, const double* src, double* dst, int64_t
                          int64_t chunk_base, uint64_t s0, const uint64_t* tab);
 hipError_t launch_summary64(hipStream_t st, const double* x, int64_t n, const LeafPartial64* part, int64_t nparts,
                             const double* roots, const int64_t* ranks, int req_bins, int dedup, void* payload,
-                            double* g_raw, QuantLut* lut);
+                            double* g_raw, QuantLut* lut,
+                            const double* tail = nullptr, int sharded = 0, int64_t n_local = 0);
 // `lut` may be null; fp64 values are looked up by their round-down fp32 image, then corrected
 // by exact double compares.
 hipError_t launch_quantize64(hipStream_t st, const double* x, int64_t n, void* payload, const QuantLut* lut,

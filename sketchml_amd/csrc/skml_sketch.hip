@@ -726,6 +726,9 @@ struct SummaryArgs {
     QuantLut* lut;
     int req_bins;
     int dedup;
+    const float* tail;  // base buffer (n % 256 values); null: the input's last n % 256 values
+    int sharded;        // 1: the header's n is n_local (a parallelQuantize shard's codes)
+    int64_t n_local;
 };
 
 __device__ void summary_block(const SummaryArgs& a, SummaryShared& S) {
@@ -735,7 +738,7 @@ __device__ void summary_block(const SummaryArgs& a, SummaryShared& S) {
     const int64_t n = a.n;
     const int64_t chunks = n / kChunk;
     const int tail = (int)(n - chunks * kChunk);
-    const float* xt = a.x + chunks * kChunk;
+    const float* xt = a.tail ? a.tail : a.x + chunks * kChunk;
     const int req_bins = a.req_bins;
     SKML_PROF(2);
 
@@ -835,7 +838,7 @@ __device__ void summary_block(const SummaryArgs& a, SummaryShared& S) {
         if (t == 0) {
             hdr->magic = SKML_DENSE_MAGIC;
             hdr->status = SKML_E_NAN;
-            hdr->n = n;
+            hdr->n = a.sharded ? a.n_local : n;
             hdr->bin_num = req_bins;
             hdr->zero_idx = 0;
             hdr->code_bits = code_bits_for(req_bins);
@@ -941,7 +944,7 @@ __device__ void summary_block(const SummaryArgs& a, SummaryShared& S) {
         else zero = S.zero < bin_num - 1 ? S.zero : bin_num - 1;
         hdr->magic = SKML_DENSE_MAGIC;
         hdr->status = SKML_OK;
-        hdr->n = n;
+        hdr->n = a.sharded ? a.n_local : n;
         hdr->bin_num = bin_num;
         hdr->zero_idx = zero;
         hdr->code_bits = code_bits_for(bin_num);
@@ -1166,6 +1169,182 @@ hipError_t launch_set_splits(hipStream_t st, void* payload, int64_t n, const dou
                              int nsplits, double mn, double mx, int req_bins, QuantLut* lut) {
     hipLaunchKernelGGL(k_set_splits, dim3(1), dim3(256), 0, st, reinterpret_cast<uint8_t*>(payload),
                        n, splits_dev, nsplits, mn, mx, req_bins, lut);
+    return hipGetLastError();
+}
+
+// =============================================================================================
+// QuantileQuantizer.parallelQuantize with T slices (QuantileQuantizer.java:53-92): each slice is
+// sketched by the normal leaf + merge passes (its compaction bits from its own offset into the
+// one Random stream), exported as a SketchRecord, and the records are merged in slice order by
+// one workgroup replaying HeapQuantileSketch.merge (HeapQuantileSketch.java:186-228): the other
+// sketch's base items go through update() (a full base buffer is sorted, compacted and carried),
+// then each of its levels is carried up from its own level (inPlacePropagationMerge).  The
+// merged state feeds summary_block unchanged.
+// =============================================================================================
+__global__ __launch_bounds__(512) void k_sketch_record(const float* __restrict__ x, int64_t n,
+                                                       const LeafPartial* __restrict__ part, int64_t nparts,
+                                                       const float* __restrict__ roots, SketchRecord* rec) {
+    __shared__ uint32_t s_mn, s_mx, s_fl;
+    const int t = threadIdx.x, T = blockDim.x;
+    const int64_t chunks = n / kChunk;
+    const int tail = (int)(n - chunks * kChunk);
+    const float* xt = x + chunks * kChunk;
+    if (t == 0) {
+        s_mn = 0xFFFFFFFFu;
+        s_mx = 0u;
+        s_fl = 0u;
+    }
+    __syncthreads();
+    uint32_t mn = 0xFFFFFFFFu, mx = 0u, fl = 0u;
+    for (int64_t i = t; i < nparts; i += T) {
+        const LeafPartial p = part[i];
+        mn = p.min_key < mn ? p.min_key : mn;
+        mx = p.max_key > mx ? p.max_key : mx;
+        fl |= p.flags;
+    }
+    for (int i = t; i < tail; i += T) {
+        const uint32_t b = __float_as_uint(xt[i]);
+        fl |= is_nan_bits(b) ? 1u : 0u;
+        const uint32_t k = f2key(b);
+        mn = k < mn ? k : mn;
+        mx = k > mx ? k : mx;
+        rec->tail[i] = xt[i];
+    }
+    atomicMin(&s_mn, mn);
+    atomicMax(&s_mx, mx);
+    if (fl) atomicOr(&s_fl, fl);
+    for (int l = 0; l < kMaxLevels; l++)
+        if ((chunks >> l) & 1)
+            for (int i = t; i < kK; i += T) rec->level[l][i] = roots[(size_t)l * kK + i];
+    __syncthreads();
+    if (t == 0) {
+        rec->n = n;
+        rec->mm = LeafPartial{s_mn, s_mx, s_fl, 0u};
+        rec->pad = 0;
+    }
+}
+
+hipError_t launch_sketch_record(hipStream_t st, const float* x, int64_t n, const LeafPartial* part, int64_t nparts,
+                                const float* roots, SketchRecord* rec) {
+    hipLaunchKernelGGL(k_sketch_record, dim3(1), dim3(512), 0, st, x, n, part, nparts, roots, rec);
+    return hipGetLastError();
+}
+
+struct SkMergeShared {
+    float lv[kMaxLevels][kK];
+    float base[kChunk];
+    float tmp[kChunk];
+};
+union SkMergeUnion {
+    SkMergeShared m;
+    SummaryShared s;
+};
+
+__global__ __launch_bounds__(512) void k_sketch_merge(const SketchRecord* __restrict__ recs, int nrec, uint64_t s0,
+                                                      uint64_t bit0, const uint64_t* __restrict__ tab,
+                                                      SummaryArgs a, float* g_roots, float* g_tail,
+                                                      LeafPartial* g_part) {
+    __shared__ SkMergeUnion U;
+    SkMergeShared& M = U.m;
+    const int t = threadIdx.x;
+    // control state is uniform: every thread keeps its own identical copy
+    uint64_t pattern = 0, bit = bit0;
+    int64_t nacc = 0;
+    int base_cnt = 0;
+
+    auto first_free = [&](int from) {
+        int l = from;
+        while ((pattern >> l) & 1ull) l++;
+        return l;
+    };
+    // levelwisePropagation (QSketchUtils.java:71-82): carry lv[dest] through levels [from, dest)
+    auto carry = [&](int from, int dest) {
+        for (int l = from; l < dest; l++) {
+            const uint32_t odd = lcg_bit(tab, s0, bit++);
+            if (t < kChunk) exact_merge_task(M.lv[l], M.lv[dest], M.tmp, t, odd);
+            __syncthreads();
+            if (t < kK) M.lv[dest][t] = M.tmp[t];
+            __syncthreads();
+        }
+    };
+    // fullBaseBufferPropagation (HeapQuantileSketch.java:107-124): Arrays.sort, compact, carry
+    auto flush_base = [&]() {
+        if (t < kChunk) {
+            const float v = M.base[t];
+            const uint32_t kv = f2key(__float_as_uint(v));
+            int rank = 0;
+            for (int j = 0; j < kChunk; j++) {
+                const uint32_t kj = f2key(__float_as_uint(M.base[j]));
+                rank += (kj < kv) || (kj == kv && j < t);
+            }
+            M.tmp[rank] = v;
+        }
+        __syncthreads();
+        const int dest = first_free(0);
+        const uint32_t odd = lcg_bit(tab, s0, bit++);
+        if (t < kK) M.lv[dest][t] = M.tmp[2 * t + odd];
+        __syncthreads();
+        carry(0, dest);
+        pattern += 1;
+        base_cnt = 0;
+    };
+
+    for (int r = 0; r < nrec; r++) {
+        const SketchRecord* R = recs + r;
+        const int64_t rn = R->n;
+        if (rn <= 0) continue;  // other.isEmpty()
+        const uint64_t rpat = (uint64_t)(rn / kChunk);
+        const int rtail = (int)(rn % kChunk);
+        if (nacc == 0) {  // this.isEmpty(): copy(other), no compaction
+            for (int l = 0; l < kMaxLevels; l++)
+                if ((rpat >> l) & 1ull)
+                    if (t < kK) M.lv[l][t] = R->level[l][t];
+            if (t < rtail) M.base[t] = R->tail[t];
+            __syncthreads();
+            pattern = rpat;
+            base_cnt = rtail;
+            nacc = rn;
+            continue;
+        }
+        // other's base items through update()
+        for (int i = 0; i < rtail;) {
+            const int take = min(rtail - i, kChunk - base_cnt);
+            if (t < take) M.base[base_cnt + t] = R->tail[i + t];
+            __syncthreads();
+            base_cnt += take;
+            i += take;
+            if (base_cnt == kChunk) flush_base();
+        }
+        // other's levels, bottom-up (inPlacePropagationMerge)
+        for (int l = 0; l < kMaxLevels; l++) {
+            if (!((rpat >> l) & 1ull)) continue;
+            const int dest = first_free(l);
+            if (t < kK) M.lv[dest][t] = R->level[l][t];
+            __syncthreads();
+            carry(l, dest);
+            pattern += 1ull << l;
+        }
+        nacc += rn;
+    }
+    // export the merged sketch in the summary's layout (levels by index, base buffer, partials)
+    for (int l = 0; l < kMaxLevels; l++)
+        if ((pattern >> l) & 1ull)
+            if (t < kK) g_roots[(size_t)l * kK + t] = M.lv[l][t];
+    if (t < base_cnt) g_tail[t] = M.base[t];
+    for (int r = t; r < nrec; r += blockDim.x) g_part[r] = recs[r].mm;
+    __threadfence();
+    __syncthreads();
+    summary_block(a, U.s);
+}
+
+hipError_t launch_sketch_merge(hipStream_t st, const SketchRecord* recs, int nrec, uint64_t s0, uint64_t bit0,
+                               const uint64_t* jump_tab, int64_t n_total, int64_t n_local, const int64_t* ranks,
+                               int req_bins, int dedup, void* payload, double* scratch_raw, QuantLut* lut,
+                               float* scratch_roots, float* scratch_tail, LeafPartial* scratch_part) {
+    SummaryArgs a{nullptr, n_total, scratch_part, nrec, scratch_roots, ranks, reinterpret_cast<uint8_t*>(payload),
+                  scratch_raw, lut, req_bins, dedup, scratch_tail, 1, n_local};
+    hipLaunchKernelGGL(k_sketch_merge, dim3(1), dim3(512), 0, st, recs, nrec, s0, bit0, jump_tab, a, scratch_roots,
+                       scratch_tail, scratch_part);
     return hipGetLastError();
 }
 

@@ -371,6 +371,8 @@ int check_params(const skml_params* p) {
     if (!(p->col_ratio > 0.0)) return sfail(SKML_E_ARG, "col_ratio must be positive");
     if (p->quant_type != SKML_QUANTILE && p->quant_type != SKML_UNIFORM)
         return sfail(SKML_E_ARG, "Unrecognizable quantization type: %d", p->quant_type);
+    if (p->parallelism < 0 || p->parallelism > 65536)
+        return sfail(SKML_E_ARG, "Invalid parallelism: %d", p->parallelism);
     return SKML_OK;
 }
 
@@ -389,8 +391,11 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const float* vals, int64_t nnz, 
     s->qbytes = skml_dense_payload_bytes(nnz, p->bin_num);
     if (hipMalloc(&s->qpayload, s->qbytes) != hipSuccess) return bail(sfail(SKML_E_OOM, "quantizer payload"));
     skml_params qp = *p;
-    if (int e = p->quant_type == SKML_UNIFORM ? skml_dense_encode_uniform_f32(c, vals, nnz, &qp, s->qpayload, s->qbytes)
-                                              : skml_dense_encode_f32(c, vals, nnz, &qp, s->qpayload, s->qbytes))
+    if (int e = p->quant_type == SKML_UNIFORM
+                    ? skml_dense_encode_uniform_f32(c, vals, nnz, &qp, s->qpayload, s->qbytes)
+                    : (p->parallelism > 1 ? skml_dense_encode_parallel_f32(c, vals, nnz, p->parallelism, &qp,
+                                                                            s->qpayload, s->qbytes)
+                                          : skml_dense_encode_f32(c, vals, nnz, &qp, s->qpayload, s->qbytes)))
         return bail(e);
     if (int e = sync_to_host(c, &s->hdr, s->qpayload, sizeof(skml_dense_header))) return bail(e);
     if (s->hdr.status == SKML_E_NAN) return bail(sfail(SKML_E_NAN, "Encounter NaN value"));

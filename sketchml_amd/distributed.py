@@ -18,8 +18,11 @@ from typing import Callable, Optional
 import torch
 import torch.distributed as dist
 
+import numpy as np
+
 from . import _lib
-from .exceptions import check
+from .context import as_device_values, get_context
+from .exceptions import SketchMLException, check
 
 
 def shard_range(n_total: int, world: int, rank: int) -> tuple[int, int]:
@@ -98,3 +101,62 @@ def decode_sum(ctx_handle, payloads: torch.Tensor, nranks: int, stride: int, n: 
     (Gradient.sum then timesBy(1/P), ml/gradient/Gradient.scala:44-49)."""
     check(_lib.lib.skml_dense_decode_sum_f32(ctx_handle, C.c_void_p(payloads.data_ptr()), nranks, stride,
                                              C.c_void_p(out.data_ptr()), n, float(scale)), "decode_sum")
+
+
+# ---- one split table across ranks (SURVEY §8e single-split-table mode) ----------------------
+def parallel_slices(n_total: int, parts: int) -> list[int]:
+    """Slice sizes of QuantileQuantizer.parallelQuantize (QuantileQuantizer.java:66-68): n/T
+    each, the last slice takes the remainder."""
+    if parts < 1:
+        raise SketchMLException(f"Invalid parallelism: {parts}")
+    per = n_total // parts
+    return [per] * (parts - 1) + [n_total - per * (parts - 1)]
+
+
+def record_bytes(fp64: bool = False) -> int:
+    return int(_lib.lib.skml_sketch_record_bytes(1 if fp64 else 0))
+
+
+def sketch_shard(values, shard_sizes, shard: int, seed: int = 0) -> torch.Tensor:
+    """This rank's slice sketch as a fixed-size device record (skml_dense_sketch_shard_f32 / _f64:
+    fp64 values, the reference's double[], stay fp64)."""
+    x = as_device_values(values)
+    wide = x.dtype == torch.float64
+    sizes = np.ascontiguousarray(shard_sizes, dtype=np.int64)
+    rec = torch.empty(record_bytes(wide), dtype=torch.uint8, device=x.device)
+    ctx = get_context(x.device)
+    fn = _lib.lib.skml_dense_sketch_shard_f64 if wide else _lib.lib.skml_dense_sketch_shard_f32
+    check(fn(ctx.handle, C.c_void_p(x.data_ptr()), x.numel(), sizes.ctypes.data_as(_lib.i64p), len(sizes),
+             int(shard), int(seed), C.c_void_p(rec.data_ptr())), "sketch_shard")
+    return rec
+
+
+def quantize_sharded(values, shard_sizes, shard: int, records: torch.Tensor, binNum: int = 256, seed: int = 0,
+                     dedup: bool = False):
+    """QuantileQuantizer of shard `shard` against the merged sketch of all shards' records."""
+    from .quantization import QuantileQuantizer
+    q = QuantileQuantizer(binNum, seed)
+    q._encode_sharded(values, shard_sizes, shard, records, dedup)
+    return q
+
+
+def parallel_quantize_across_ranks(values, n_total: int, binNum: int = 256, seed: int = 0, group=None,
+                                   exchange: Optional[PayloadExchange] = None):
+    """parallelQuantize with T = world size over one logical gradient of n_total values whose
+    rank-r slice (parallel_slices) is `values` on this rank's GPU: sketch, all-gather the
+    records in rank order (RCCL, via `exchange` or the torch process group), merge, quantise."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    sizes = parallel_slices(n_total, world)
+    rec = sketch_shard(values, sizes, rank, seed)
+    nb = rec.numel()
+    allrec = torch.empty(nb * world, dtype=torch.uint8, device=rec.device)
+    if exchange is not None:
+        exchange.allgather(rec, nb, allrec)
+    elif dist.get_backend(group) == "nccl":  # RCCL; its stream waits on the codec's (current) stream
+        dist.all_gather_into_tensor(allrec, rec, group=group)
+    else:  # a host-memory process group (gloo): the records (~13 KB each) go through the host
+        parts = [torch.empty(nb, dtype=torch.uint8) for _ in range(world)]
+        dist.all_gather(parts, rec.cpu(), group=group)
+        allrec.copy_(torch.cat(parts))
+    return quantize_sharded(values, sizes, rank, allrec, binNum, seed)

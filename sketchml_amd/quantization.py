@@ -15,6 +15,7 @@ import numpy as np
 import torch
 
 from . import _lib
+from .constants import Parallel
 from .context import alloc_aligned, as_device_values, get_context
 from .exceptions import QuantileSketchException, SketchMLException, check
 
@@ -81,7 +82,7 @@ class Quantizer:
     _ENTRY = {(False, False): "skml_dense_encode_f32", (False, True): "skml_dense_encode_f64",
               (True, False): "skml_dense_encode_uniform_f32", (True, True): "skml_dense_encode_uniform_f64"}
 
-    def _encode(self, values, dedup: bool, uniform: bool = False):
+    def _encode(self, values, dedup: bool, uniform: bool = False, threads: int = 1):
         x = as_device_values(values, self.device)
         self._wide = x.dtype == torch.float64
         self.device = x.device
@@ -97,14 +98,46 @@ class Quantizer:
         p.bin_num = self.binNum
         p.seed = self.seed
         p.dedup = 1 if dedup else 0
-        fn = getattr(_lib.lib, self._ENTRY[(uniform, self._wide)])
-        st = fn(self._ctx().handle, C.c_void_p(x.data_ptr()), self.n, C.byref(p),
-                C.c_void_p(self.payload.data_ptr()), nbytes)
+        if threads > 1 and not uniform:
+            fn = _lib.lib.skml_dense_encode_parallel_f64 if self._wide else _lib.lib.skml_dense_encode_parallel_f32
+            st = fn(self._ctx().handle, C.c_void_p(x.data_ptr()), self.n, threads, C.byref(p),
+                    C.c_void_p(self.payload.data_ptr()), nbytes)
+        else:
+            fn = getattr(_lib.lib, self._ENTRY[(uniform, self._wide)])
+            st = fn(self._ctx().handle, C.c_void_p(x.data_ptr()), self.n, C.byref(p),
+                    C.c_void_p(self.payload.data_ptr()), nbytes)
         check(st, "quantize")
         self._hdr = None
         self._bins = None
         self._x = x  # keep the input alive until the stream has consumed it
         self._load_header()  # surfaces NaN as QuantileSketchException, like update() throws
+        self._x = None
+
+    def _encode_sharded(self, values, shard_sizes, shard: int, records: torch.Tensor, dedup: bool = False):
+        """Quantise shard `shard` of one logical gradient against the split table of the merged
+        shard sketches (skml_dense_encode_sharded_f32); records = all shards' records in order."""
+        x = as_device_values(values, self.device)
+        self._wide = x.dtype == torch.float64
+        self.device = x.device
+        self.n = x.numel()
+        sizes = np.ascontiguousarray(shard_sizes, dtype=np.int64)
+        nbytes = _lib.lib.skml_dense_payload_bytes(self.n, self.binNum)
+        if nbytes == 0:
+            raise SketchMLException(f"bad quantizer arguments n={self.n} binNum={self.binNum}")
+        self.payload = alloc_aligned(nbytes, x.device)
+        p = _lib.Params()
+        _lib.lib.skml_params_default(C.byref(p))
+        p.bin_num = self.binNum
+        p.seed = self.seed
+        p.dedup = 1 if dedup else 0
+        fn = _lib.lib.skml_dense_encode_sharded_f64 if self._wide else _lib.lib.skml_dense_encode_sharded_f32
+        st = fn(self._ctx().handle, C.c_void_p(x.data_ptr()), self.n, sizes.ctypes.data_as(_lib.i64p), len(sizes),
+                int(shard), C.c_void_p(records.data_ptr()), C.byref(p), C.c_void_p(self.payload.data_ptr()), nbytes)
+        check(st, "quantize")
+        self._hdr = None
+        self._bins = None
+        self._x = (x, records)
+        self._load_header()
         self._x = None
 
     # ---- Quantizer getters ----
@@ -247,9 +280,12 @@ class QuantileQuantizer(Quantizer):
         self._encode(values, dedup=True)
 
     def parallelQuantize(self, values) -> None:
-        """QuantileQuantizer.parallelQuantize (QuantileQuantizer.java:53-92): one device sketch
-        (T = 1 merge order) and, as in the reference, no Maths.unique of the splits."""
-        self._encode(values, dedup=False)
+        """QuantileQuantizer.parallelQuantize (QuantileQuantizer.java:53-92): T =
+        Constants.Parallel.getParallelism() slice sketches merged in slice order, and, as in the
+        reference, no Maths.unique of the splits.  The compaction bits follow the schedule that
+        runs the slices one after another, then the merges, from Random(seed)
+        (skml_dense_encode_parallel_f32)."""
+        self._encode(values, dedup=False, threads=Parallel.getParallelism())
 
     def quantizationType(self) -> QuantizationType:
         return QuantizationType.QUANTILE
@@ -270,6 +306,7 @@ class UniformQuantizer(Quantizer):
     def parallelQuantize(self, values) -> None:
         """UniformQuantizer.parallelQuantize (UniformQuantizer.java:48-70): the same splits and
         bins as quantize (only the indexOf loop is sliced over threads in the reference)."""
+        Parallel.getParallelism()  # parallelQuantizeToBins reads it (Quantizer.java:94-117)
         self._encode(values, dedup=False, uniform=True)
 
     def quantizationType(self) -> QuantizationType:

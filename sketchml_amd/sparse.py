@@ -14,12 +14,13 @@ import numpy as np
 import torch
 
 from . import _lib
+from .constants import Parallel
 from .context import get_context
 from .exceptions import SketchMLException, check
 from .quantization import Quantizer, QuantizationType
 
 
-def _params(bin_num, group_num, row_num, col_ratio, seed, hash_seed, dedup=True, uniform=False):
+def _params(bin_num, group_num, row_num, col_ratio, seed, hash_seed, dedup=True, uniform=False, parallelism=1):
     p = _lib.Params()
     _lib.lib.skml_params_default(C.byref(p))
     p.bin_num = int(bin_num)
@@ -30,6 +31,7 @@ def _params(bin_num, group_num, row_num, col_ratio, seed, hash_seed, dedup=True,
     p.hash_seed = int(hash_seed)
     p.dedup = 1 if dedup else 0
     p.quant_type = 1 if uniform else 0  # SKML_UNIFORM / SKML_QUANTILE
+    p.parallelism = int(parallelism)
     return p
 
 
@@ -151,7 +153,7 @@ def _as_device(t, dtype, device=None):
 
 
 def encode_sparse(keys, values, bin_num=Quantizer.DEFAULT_BIN_NUM, group_num=8, row_num=2, col_ratio=0.3,
-                  seed=0, hash_seed=0, dedup=True, uniform=False) -> SparsePayload:
+                  seed=0, hash_seed=0, dedup=True, uniform=False, parallelism=1) -> SparsePayload:
     v = _as_device(values, torch.float32)
     k = _as_device(keys, torch.int32, v.device)
     if k.numel() != v.numel():
@@ -159,7 +161,7 @@ def encode_sparse(keys, values, bin_num=Quantizer.DEFAULT_BIN_NUM, group_num=8, 
             f"Lengths of key array and value array do not match: {k.numel()}, {v.numel()}")
     dev = v.device.index
     ctx = get_context(dev)
-    p = _params(bin_num, group_num, row_num, col_ratio, seed, hash_seed, dedup, uniform)
+    p = _params(bin_num, group_num, row_num, col_ratio, seed, hash_seed, dedup, uniform, parallelism)
     h = C.c_void_p()
     check(_lib.lib.skml_sparse_encode_kv_f32(ctx.handle, C.c_void_p(k.data_ptr()), C.c_void_p(v.data_ptr()),
                                              k.numel(), C.byref(p), C.byref(h)), "sparse_encode")
@@ -210,9 +212,9 @@ class GroupedMinMaxSketch:
         self.zeroValue = None
         self.payload: SparsePayload | None = None
 
-    def create(self, keys, values, dedup=True, uniform=False) -> None:
+    def create(self, keys, values, dedup=True, uniform=False, parallelism=1) -> None:
         self.payload = encode_sparse(keys, values, self.binNum, self.groupNum, self.rowNum, self.colRatio,
-                                     self.seed, self.hashSeed, dedup, uniform)
+                                     self.seed, self.hashSeed, dedup, uniform, parallelism)
         hdr, _ = self.payload.quant_header()
         self.binNum = hdr.bin_num
         self.zeroValue = hdr.zero_idx
@@ -311,10 +313,10 @@ class SparseVectorCompressor:
         self._size = 0
         self.mmSketches: GroupedMinMaxSketch | None = None
 
-    def _compress(self, keys, values, dedup):
+    def _compress(self, keys, values, dedup, parallelism=1):
         self.mmSketches = GroupedMinMaxSketch(self.mmSketchGroupNum, self.mmSketchRowNum, self.mmSketchColRatio,
                                               self.quantBinNum, self.seed, self.hashSeed)
-        self.mmSketches.create(keys, values, dedup, str(self.quantType) == "UNIFORM")
+        self.mmSketches.create(keys, values, dedup, str(self.quantType) == "UNIFORM", parallelism)
         self._size = self.mmSketches.payload.nnz()
 
     def compressDense(self, values) -> None:
@@ -328,11 +330,12 @@ class SparseVectorCompressor:
     def parallelCompressDense(self, values) -> None:
         v = _as_device(values, torch.float32)
         keys = torch.arange(v.numel(), dtype=torch.int32, device=v.device)
-        self._compress(keys, v, False)
+        self._compress(keys, v, False, Parallel.getParallelism())
 
     def parallelCompressSparse(self, keys, values) -> None:
-        """parallelQuantize (no Maths.unique) + parallelCreate (same groups)."""
-        self._compress(keys, values, False)
+        """parallelQuantize with T = Constants.Parallel.getParallelism() slice sketches (no
+        Maths.unique) + parallelCreate (same groups), SparseVectorCompressor.java:80-98."""
+        self._compress(keys, values, False, Parallel.getParallelism())
 
     def decompressSparse(self):
         """SparseVectorCompressor.decompressSparse (SparseVectorCompressor.java:118-126): keys and

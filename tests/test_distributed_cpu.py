@@ -55,3 +55,13 @@ def test_shard_range_partitions(n, world):
     spans = [shard_range(n, world, r) for r in range(world)]
     assert spans[0][0] == 0 and spans[-1][1] == n
     assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+
+
+@pytest.mark.parametrize("n,world", [(10, 3), (2**26 + 5, 8), (7, 8), (0, 2)])
+def test_parallel_slices_are_the_parallelquantize_slicing(n, world):
+    """QuantileQuantizer.java:66-68: n/T per slice, the last takes the remainder; the same
+    split as the bucket sharding."""
+    from sketchml_amd.distributed import parallel_slices, shard_range
+    sizes = parallel_slices(n, world)
+    assert sum(sizes) == n and all(s == n // world for s in sizes[:-1])
+    assert sizes == [hi - lo for lo, hi in (shard_range(n, world, r) for r in range(world))]

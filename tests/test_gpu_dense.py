@@ -147,6 +147,7 @@ def test_parallel_quantize_keeps_duplicate_splits(gpu):
     n = 70000
     x = _data(n, 9, "dups")
     gq = gpu.QuantileQuantizer(64, seed=5)
+    gpu.Parallel.setParallelism(1)
     gq.parallelQuantize(torch.from_numpy(x).cuda())
     oq = O.parallel_quantize(x.astype(np.float64), 64, threads=1, seed=5)
     assert gq.getBinNum() == 64

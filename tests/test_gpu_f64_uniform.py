@@ -109,6 +109,7 @@ def test_f64_of_f32_values_equals_f32_path(gpu):
 def test_f64_parallel_quantize_keeps_duplicates(gpu):
     x = _data64(50000, 9, "dups")
     gq = gpu.QuantileQuantizer(64, seed=5)
+    gpu.Parallel.setParallelism(1)
     gq.parallelQuantize(torch.from_numpy(x).cuda())
     _check(gq, O.parallel_quantize(x, 64, threads=1, seed=5), x)
 
@@ -168,6 +169,7 @@ def test_uniform_bin_counts(gpu, bins, wide):
     if not wide:
         x = x.astype(np.float32)
     gq = gpu.UniformQuantizer(bins)
+    gpu.Parallel.setParallelism(4)
     gq.parallelQuantize(torch.from_numpy(x).cuda())
     _check(gq, O.uniform_quantize(x.astype(np.float64), bins), x)
 

@@ -224,6 +224,23 @@ def test_parallel_quantize_split_ranks_within_epsilon(threads):
     assert np.array_equal(q.bins, np.searchsorted(q.splits, x, side="right"))
 
 
+@pytest.mark.parametrize("n,threads,bins,seed", [
+    (10000, 3, 64, 1), (1000, 4, 16, 2), (777, 8, 256, 4), (3, 5, 4, 5), (40000, 7, 256, 6),
+    (256 * 9, 2, 32, 7), (256 * 9 + 5, 3, 32, 8), (70000, 2, 256, 9)])
+def test_parallel_quantize_crosscheck_carry_buffer(n, threads, bins, seed):
+    """C oracle vs the independent Python carry-buffer HeapQuantileSketch (update / merge)."""
+    rng = np.random.default_rng(seed)
+    x = rng.standard_normal(n)
+    if seed % 2:
+        x[rng.random(n) < 0.2] = 0.0
+        x[rng.random(n) < 0.05] = -0.0
+    a = O.parallel_quantize(x, bins, threads=threads, seed=seed)
+    b = N.parallel_quantize(x, bins, threads, seed)
+    assert (a.bin_num, a.zero_idx, a.min, a.max) == (b["bin_num"], b["zero_idx"], b["min"], b["max"])
+    assert np.array_equal(a.splits, b["splits"])
+    assert np.array_equal(a.bins, b["bins"])
+
+
 def test_nan_is_rejected():
     with pytest.raises(O.OracleError) as e:
         O.quantize(np.array([1.0, np.nan, 2.0]), 16)
