@@ -39,10 +39,45 @@ __device__ __forceinline__ uint32_t lane_xor(uint32_t v) {
         return (uint32_t)__builtin_amdgcn_ds_bpermute((lane ^ M) << 2, x);
     }
 }
+template <int M>
+__device__ __forceinline__ float lane_xor(float v) {
+    return __uint_as_float(lane_xor<M>(__float_as_uint(v)));
+}
+
+// Sort elements are either uint32 total-order keys or the raw floats.  Floats compare with
+// v_min/v_max/v_med3_f32, whose order is Arrays.sort's except for -0.0 vs 0.0 (equal) and NaN
+// (dropped by min/max): the leaf takes the float path only in rounds without mixed-sign zeros and
+// flags NaN from a class test at load (k_leaf2).  fbits: the float's bit pattern.
+__device__ __forceinline__ uint32_t elem_fbits(uint32_t k) { return key2f(k); }
+__device__ __forceinline__ uint32_t elem_fbits(float f) { return __float_as_uint(f); }
+template <typename T>
+__device__ __forceinline__ T elem_of_fbits(uint32_t b);
+template <>
+__device__ __forceinline__ uint32_t elem_of_fbits<uint32_t>(uint32_t b) { return f2key(b); }
+template <>
+__device__ __forceinline__ float elem_of_fbits<float>(uint32_t b) { return __uint_as_float(b); }
+// compare-exchange selector: med3(a, b, sel_of(false)) = min, med3(a, b, sel_of(true)) = max
+template <typename T>
+__device__ __forceinline__ T sel_of(bool upper);
+template <>
+__device__ __forceinline__ uint32_t sel_of<uint32_t>(bool upper) { return upper ? 0xFFFFFFFFu : 0u; }
+template <>
+__device__ __forceinline__ float sel_of<float>(bool upper) {
+    return __uint_as_float(upper ? 0x7F800000u : 0xFF800000u);
+}
 
 __device__ __forceinline__ void ce(uint32_t& a, uint32_t& b) {
     uint32_t lo = a < b ? a : b;
     uint32_t hi = a < b ? b : a;
+    a = lo;
+    b = hi;
+}
+// Float compare-exchange as bare v_min_f32 / v_max_f32: the compiler's minnum lowering would
+// first canonicalize every operand that comes from memory or a DPP move (one more VALU op each).
+__device__ __forceinline__ void ce(float& a, float& b) {
+    float lo, hi;
+    asm("v_min_f32 %0, %1, %2" : "=v"(lo) : "v"(a), "v"(b));
+    asm("v_max_f32 %0, %1, %2" : "=v"(hi) : "v"(a), "v"(b));
     a = lo;
     b = hi;
 }
@@ -81,17 +116,17 @@ struct OddEvenNet {
     }
 };
 
-template <int R>
-__device__ __forceinline__ void sort_regs_oddeven(uint32_t (&v)[R]) {
+template <int R, typename T>
+__device__ __forceinline__ void sort_regs_oddeven(T (&v)[R]) {
     constexpr int C = OddEvenNet<R>::kCount;
-    constexpr auto T = OddEvenNet<R>::table();
+    constexpr auto net = OddEvenNet<R>::table();
 #pragma unroll
-    for (int c = 0; c < C; c++) ce(v[T.a[c]], v[T.b[c]]);
+    for (int c = 0; c < C; c++) ce(v[net.a[c]], v[net.b[c]]);
 }
 
 // In-register bitonic sort of R keys, ascending, all comparators in "flip" form.
-template <int R>
-__device__ __forceinline__ void sort_regs(uint32_t (&v)[R]) {
+template <int R, typename T>
+__device__ __forceinline__ void sort_regs(T (&v)[R]) {
 #pragma unroll
     for (int k = 2; k <= R; k <<= 1) {
 #pragma unroll
@@ -110,8 +145,8 @@ __device__ __forceinline__ void sort_regs(uint32_t (&v)[R]) {
     }
 }
 
-template <int R>
-__device__ __forceinline__ void halfclean_regs(uint32_t (&v)[R]) {
+template <int R, typename T>
+__device__ __forceinline__ void halfclean_regs(T (&v)[R]) {
 #pragma unroll
     for (int d = R >> 1; d >= 1; d >>= 1) {
 #pragma unroll
@@ -128,34 +163,36 @@ __device__ __forceinline__ void halfclean_regs(uint32_t (&v)[R]) {
 __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
     return min(max(a, b), max(min(a, b), c));
 }
+__device__ __forceinline__ uint32_t med3(uint32_t a, uint32_t b, uint32_t c) { return umed3(a, b, c); }
+__device__ __forceinline__ float med3(float a, float b, float c) { return __builtin_amdgcn_fmed3f(a, b, c); }
 
 // Flip stage across a block of (M+1) lanes: element (lane, r) meets (lane^M, R-1-r).
-template <int R, int M>
-__device__ __forceinline__ void flip_lanes(uint32_t (&v)[R], int lane) {
-    const uint32_t sel = (lane & ((M + 1) >> 1)) ? 0xFFFFFFFFu : 0u;
+template <int R, int M, typename T>
+__device__ __forceinline__ void flip_lanes(T (&v)[R], int lane) {
+    const T sel = sel_of<T>((lane & ((M + 1) >> 1)) != 0);
 #pragma unroll
     for (int r = 0; r < R / 2; r++) {
-        const uint32_t pa = lane_xor<M>(v[R - 1 - r]);
-        const uint32_t pb = lane_xor<M>(v[r]);
-        v[r] = umed3(v[r], pa, sel);
-        v[R - 1 - r] = umed3(v[R - 1 - r], pb, sel);
+        const T pa = lane_xor<M>(v[R - 1 - r]);
+        const T pb = lane_xor<M>(v[r]);
+        v[r] = med3(v[r], pa, sel);
+        v[R - 1 - r] = med3(v[R - 1 - r], pb, sel);
         // keep the scheduler from hoisting every exchange of the stage (register pressure)
         if ((r & 3) == 3) __builtin_amdgcn_sched_barrier(0);
     }
 }
 
-template <int R, int D>
-__device__ __forceinline__ void halfclean_lanes(uint32_t (&v)[R], int lane) {
-    const uint32_t sel = (lane & D) ? 0xFFFFFFFFu : 0u;
+template <int R, int D, typename T>
+__device__ __forceinline__ void halfclean_lanes(T (&v)[R], int lane) {
+    const T sel = sel_of<T>((lane & D) != 0);
 #pragma unroll
     for (int r = 0; r < R; r++) {
-        v[r] = umed3(v[r], lane_xor<D>(v[r]), sel);
+        v[r] = med3(v[r], lane_xor<D>(v[r]), sel);
         if ((r & 7) == 7) __builtin_amdgcn_sched_barrier(0);
     }
 }
 
-template <int R, int D>
-__device__ __forceinline__ void halfclean_lanes_down(uint32_t (&v)[R], int lane) {
+template <int R, int D, typename T>
+__device__ __forceinline__ void halfclean_lanes_down(T (&v)[R], int lane) {
     if constexpr (D >= 1) {
         halfclean_lanes<R, D>(v, lane);
         halfclean_lanes_down<R, D / 2>(v, lane);
@@ -164,8 +201,8 @@ __device__ __forceinline__ void halfclean_lanes_down(uint32_t (&v)[R], int lane)
 
 // Bitonic merge of a group of G = 256/R lanes holding two sorted 128-runs (lower G/2 lanes and
 // upper G/2 lanes, positions lane_in_group*R + r) into one sorted 256-run.
-template <int R>
-__device__ __forceinline__ void merge_group(uint32_t (&v)[R], int lane) {
+template <int R, typename T>
+__device__ __forceinline__ void merge_group(T (&v)[R], int lane) {
     constexpr int G = 256 / R;
     flip_lanes<R, G - 1>(v, lane);
     halfclean_lanes_down<R, G / 4>(v, lane);
@@ -173,8 +210,8 @@ __device__ __forceinline__ void merge_group(uint32_t (&v)[R], int lane) {
 }
 
 // Sort 256 keys held by a group of G = 256/R lanes (any initial placement).
-template <int R, int S>
-__device__ __forceinline__ void sort_lanes_from(uint32_t (&v)[R], int lane) {
+template <int R, int S, typename T>
+__device__ __forceinline__ void sort_lanes_from(T (&v)[R], int lane) {
     if constexpr (S <= 256) {
         constexpr int M = S / R - 1;
         flip_lanes<R, M>(v, lane);
@@ -183,8 +220,8 @@ __device__ __forceinline__ void sort_lanes_from(uint32_t (&v)[R], int lane) {
         sort_lanes_from<R, S * 2>(v, lane);
     }
 }
-template <int R>
-__device__ __forceinline__ void sort_group256(uint32_t (&v)[R], int lane) {
+template <int R, typename T>
+__device__ __forceinline__ void sort_group256(T (&v)[R], int lane) {
     sort_regs<R>(v);
     sort_lanes_from<R, 2 * R>(v, lane);
 }
@@ -203,8 +240,8 @@ __device__ __forceinline__ void compact_regs(const uint32_t (&v)[R], uint32_t (&
 // The last in-register stage of a bitonic merge compares positions (2j, 2j+1) and the
 // compaction that follows keeps one of them: fused into one v_med3 per pair, selecting
 // min (even position kept) or max (odd position kept).
-template <int R>
-__device__ __forceinline__ void halfclean_regs_compact(uint32_t (&v)[R], uint32_t (&w)[R / 2], bool odd) {
+template <int R, typename T>
+__device__ __forceinline__ void halfclean_regs_compact(T (&v)[R], T (&w)[R / 2], bool odd) {
 #pragma unroll
     for (int d = R >> 1; d >= 2; d >>= 1) {
 #pragma unroll
@@ -213,14 +250,14 @@ __device__ __forceinline__ void halfclean_regs_compact(uint32_t (&v)[R], uint32_
             if (j > i) ce(v[i], v[j]);
         }
     }
-    const uint32_t sel = odd ? 0xFFFFFFFFu : 0u;
+    const T sel = sel_of<T>(odd);
 #pragma unroll
-    for (int j = 0; j < R / 2; j++) w[j] = umed3(v[2 * j], v[2 * j + 1], sel);
+    for (int j = 0; j < R / 2; j++) w[j] = med3(v[2 * j], v[2 * j + 1], sel);
 }
 
 // merge_group + compaction
-template <int R>
-__device__ __forceinline__ void merge_group_compact(uint32_t (&v)[R], uint32_t (&w)[R / 2], int lane, bool odd) {
+template <int R, typename T>
+__device__ __forceinline__ void merge_group_compact(T (&v)[R], T (&w)[R / 2], int lane, bool odd) {
     constexpr int G = 256 / R;
     flip_lanes<R, G - 1>(v, lane);
     halfclean_lanes_down<R, G / 4>(v, lane);
@@ -228,8 +265,8 @@ __device__ __forceinline__ void merge_group_compact(uint32_t (&v)[R], uint32_t (
 }
 
 // sort_group256 + compaction (the last merge's final stage fused with the selection)
-template <int R, int S>
-__device__ __forceinline__ void sort_lanes_upto128(uint32_t (&v)[R], int lane) {
+template <int R, int S, typename T>
+__device__ __forceinline__ void sort_lanes_upto128(T (&v)[R], int lane) {
     if constexpr (S <= 128) {
         constexpr int M = S / R - 1;
         flip_lanes<R, M>(v, lane);
@@ -238,8 +275,8 @@ __device__ __forceinline__ void sort_lanes_upto128(uint32_t (&v)[R], int lane) {
         sort_lanes_upto128<R, S * 2>(v, lane);
     }
 }
-template <int R>
-__device__ __forceinline__ void sort_group256_compact(uint32_t (&v)[R], uint32_t (&w)[R / 2], int lane, bool odd) {
+template <int R, typename T>
+__device__ __forceinline__ void sort_group256_compact(T (&v)[R], T (&w)[R / 2], int lane, bool odd) {
     sort_regs<R>(v);
     sort_lanes_upto128<R, 2 * R>(v, lane);  // two sorted 128-runs per group
     merge_group_compact<R>(v, w, lane, odd);  // the final 256 merge + selection

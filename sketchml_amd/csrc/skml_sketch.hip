@@ -94,15 +94,14 @@ union MergeShared {
 // Exact path for one in-wave merge level (R keys / lane, G = 256/R lanes per merge group).
 // fb holds 1536 floats: runs in [0, 1024), merged nodes in [1024, 1536).  The element loop is
 // kept rolled and reads back from LDS so this rare path adds no register pressure.
-template <int R>
-__device__ __forceinline__ void wave_exact_level(uint32_t (&v)[R], uint32_t (&w)[R / 2], int lane,
-                                                 uint32_t odd, float* fb) {
+template <int R, typename T>
+__device__ __forceinline__ void wave_exact_level(T (&v)[R], T (&w)[R / 2], int lane, uint32_t odd, float* fb) {
     constexpr int G = 256 / R;
     const int grp = lane / G, li = lane % G;
     float* run = fb + grp * 256;
     float* out = fb + 1024 + grp * 128;
 #pragma unroll
-    for (int r = 0; r < R; r++) run[li * R + r] = __uint_as_float(key2f(v[r]));
+    for (int r = 0; r < R; r++) run[li * R + r] = __uint_as_float(elem_fbits(v[r]));
 #pragma unroll 1
     for (int r = 0; r < R; r++) {
         const int p = li * R + r;
@@ -111,12 +110,12 @@ __device__ __forceinline__ void wave_exact_level(uint32_t (&v)[R], uint32_t (&w)
         if (((uint32_t)pos & 1u) == odd) out[pos >> 1] = x;
     }
 #pragma unroll
-    for (int j = 0; j < R / 2; j++) w[j] = f2key(__float_as_uint(out[li * (R / 2) + j]));
+    for (int j = 0; j < R / 2; j++) w[j] = elem_of_fbits<T>(__float_as_uint(out[li * (R / 2) + j]));
 }
 
-template <int R>
-__device__ __forceinline__ void wave_level(uint32_t (&v)[R], uint32_t (&w)[R / 2], int lane,
-                                           uint32_t odd, bool exact, float* fb) {
+template <int R, typename T>
+__device__ __forceinline__ void wave_level(T (&v)[R], T (&w)[R / 2], int lane, uint32_t odd, bool exact,
+                                           float* fb) {
     if (!exact) {
         merge_group_compact<R>(v, w, lane, odd != 0);
     } else {
@@ -125,28 +124,28 @@ __device__ __forceinline__ void wave_level(uint32_t (&v)[R], uint32_t (&w)[R / 2
 }
 
 // Write the node held by lanes [g*G, g*G+G) (R keys per lane) as 128 floats.
-template <int R>
-__device__ __forceinline__ void store_node(const uint32_t (&w)[R], int lane, float* dst) {
+template <int R, typename T>
+__device__ __forceinline__ void store_node(const T (&w)[R], int lane, float* dst) {
     constexpr int G = kK / R;
     const int li = lane % G;
     if constexpr (R >= 4) {  // vector stores: few address registers
         float4* d = reinterpret_cast<float4*>(dst + li * R);
 #pragma unroll
         for (int q = 0; q < R / 4; q++)
-            d[q] = make_float4(__uint_as_float(key2f(w[4 * q])), __uint_as_float(key2f(w[4 * q + 1])),
-                               __uint_as_float(key2f(w[4 * q + 2])), __uint_as_float(key2f(w[4 * q + 3])));
+            d[q] = make_float4(__uint_as_float(elem_fbits(w[4 * q])), __uint_as_float(elem_fbits(w[4 * q + 1])),
+                               __uint_as_float(elem_fbits(w[4 * q + 2])), __uint_as_float(elem_fbits(w[4 * q + 3])));
     } else {
         reinterpret_cast<float2*>(dst + li * R)[0] =
-            make_float2(__uint_as_float(key2f(w[0])), __uint_as_float(key2f(w[1])));
+            make_float2(__uint_as_float(elem_fbits(w[0])), __uint_as_float(elem_fbits(w[1])));
     }
 }
 
 // Levels +1..+3 inside a wave.  bits: 0..3 -> level+1 nodes, 4..5 -> level+2, 6 -> level+3.
 // Exp(level_offset, node_in_wave, regs...) is called after each level for root exports.
-template <class Exp>
-__device__ __forceinline__ void inwave_levels(uint32_t (&w1)[16], uint32_t (&w4)[2], int lane,
-                                              uint32_t bits, bool exact, float* fb, Exp&& exp) {
-    uint32_t w2[8], w3[4];
+template <typename T, class Exp>
+__device__ __forceinline__ void inwave_levels(T (&w1)[16], T (&w4)[2], int lane, uint32_t bits, bool exact,
+                                              float* fb, Exp&& exp) {
+    T w2[8], w3[4];
     wave_level<16>(w1, w2, lane, (bits >> (lane >> 4)) & 1u, exact, fb);
     exp.template at<8>(1, lane >> 4, w2);
     wave_level<8>(w2, w3, lane, (bits >> (4 + (lane >> 5))) & 1u, exact, fb);
@@ -156,15 +155,17 @@ __device__ __forceinline__ void inwave_levels(uint32_t (&w1)[16], uint32_t (&w4)
 }
 
 // One wave merges two 128-float nodes from LDS into `out` (bitonic, 64 lanes x 4 keys).
+template <typename T = uint32_t>
 __device__ __forceinline__ void wave_pair_merge(const float* A, const float* B, float* out, int lane,
                                                 uint32_t odd) {
     const float4 f = lane < 32 ? reinterpret_cast<const float4*>(A)[lane]
                                : reinterpret_cast<const float4*>(B)[lane - 32];
-    uint32_t v[4] = {f2key(__float_as_uint(f.x)), f2key(__float_as_uint(f.y)),
-                     f2key(__float_as_uint(f.z)), f2key(__float_as_uint(f.w))};
-    uint32_t o[2];
+    T v[4] = {elem_of_fbits<T>(__float_as_uint(f.x)), elem_of_fbits<T>(__float_as_uint(f.y)),
+              elem_of_fbits<T>(__float_as_uint(f.z)), elem_of_fbits<T>(__float_as_uint(f.w))};
+    T o[2];
     merge_group_compact<4>(v, o, lane, odd != 0);
-    reinterpret_cast<float2*>(out)[lane] = make_float2(__uint_as_float(key2f(o[0])), __uint_as_float(key2f(o[1])));
+    reinterpret_cast<float2*>(out)[lane] =
+        make_float2(__uint_as_float(elem_fbits(o[0])), __uint_as_float(elem_fbits(o[1])));
 }
 
 // Levels +4..+6 across the 8 waves.  bits: 0..3 level+4, 4..5 level+5, 6 level+6.
@@ -198,8 +199,8 @@ __device__ __forceinline__ void crosswave_levels(TileShared& sh, int tid, uint32
 // Leaf kernel
 // =============================================================================================
 struct NoExport {
-    template <int R>
-    __device__ void at(int, int, const uint32_t (&)[R]) const {}
+    template <int R, typename T>
+    __device__ void at(int, int, const T (&)[R]) const {}
 };
 
 // Roots of the small trees (chunks mod 64) in the last, partial leaf workgroup.
@@ -207,8 +208,8 @@ struct LeafExport {
     int lane, rem;
     int64_t wave_off;  // first chunk of the wave, relative to the workgroup
     float* roots;
-    template <int R>
-    __device__ __forceinline__ void at(int level, int node, const uint32_t (&w)[R]) const {
+    template <int R, typename T>
+    __device__ __forceinline__ void at(int level, int node, const T (&w)[R]) const {
         if (!rem || !((rem >> level) & 1)) return;
         const int64_t cs = ((int64_t)rem >> (level + 1)) << (level + 1);
         if (wave_off + ((int64_t)node << level) != cs) return;
@@ -236,23 +237,23 @@ constexpr int kLeafWaveChunks = 64;
 constexpr int kLeaf2Waves = 4;
 
 // Merge two register-resident nodes (64 lanes x 2 keys, positions lane*2 + r): older A, newer B.
-__device__ __forceinline__ void wave_node_merge(const uint32_t (&A)[2], const uint32_t (&B)[2],
-                                                uint32_t (&out)[2], int lane, uint32_t odd, bool exact,
-                                                float* buf) {
+template <typename T>
+__device__ __forceinline__ void wave_node_merge(const T (&A)[2], const T (&B)[2], T (&out)[2], int lane, uint32_t odd,
+                                                bool exact, float* buf) {
     float* a = buf;
     float* b = buf + kK;
     float* o = buf + 2 * kK;
-    reinterpret_cast<float2*>(a)[lane] = make_float2(__uint_as_float(key2f(A[0])), __uint_as_float(key2f(A[1])));
-    reinterpret_cast<float2*>(b)[lane] = make_float2(__uint_as_float(key2f(B[0])), __uint_as_float(key2f(B[1])));
+    reinterpret_cast<float2*>(a)[lane] = make_float2(__uint_as_float(elem_fbits(A[0])), __uint_as_float(elem_fbits(A[1])));
+    reinterpret_cast<float2*>(b)[lane] = make_float2(__uint_as_float(elem_fbits(B[0])), __uint_as_float(elem_fbits(B[1])));
     if (!exact) {
-        wave_pair_merge(a, b, o, lane, odd);
+        wave_pair_merge<T>(a, b, o, lane, odd);
     } else {
 #pragma unroll
         for (int k = 0; k < 4; k++) exact_merge_task(a, b, o, lane + 64 * k, odd);
     }
     const float2 r = reinterpret_cast<const float2*>(o)[lane];
-    out[0] = f2key(__float_as_uint(r.x));
-    out[1] = f2key(__float_as_uint(r.y));
+    out[0] = elem_of_fbits<T>(__float_as_uint(r.x));
+    out[1] = elem_of_fbits<T>(__float_as_uint(r.y));
 }
 
 // Roots of the small trees inside the partial 64-chunk tile (compiled only into the PARTIAL
@@ -262,8 +263,8 @@ struct WaveExport {
     int lane, rem;
     int64_t round_off;  // first chunk of the round relative to the tile
     float* roots;
-    template <int R>
-    __device__ __forceinline__ void at(int level, int node, const uint32_t (&w)[R]) const {
+    template <int R, typename T>
+    __device__ __forceinline__ void at(int level, int node, const T (&w)[R]) const {
         if constexpr (PARTIAL) {
             if (!((rem >> level) & 1)) return;
             const int64_t cs = ((int64_t)rem >> (level + 1)) << (level + 1);
@@ -295,7 +296,7 @@ __global__ __launch_bounds__(256, 4) void k_leaf2(const float* __restrict__ x, i
 
     uint32_t mn = 0xFFFFFFFFu, mx = 0u, fl = 0u;
     bool neg_any = false, pos_any = false;
-    uint32_t st3[2], st4[2], st5[2], top[2];
+    float st3[2], st4[2], st5[2], top[2];
     uint32_t acc = 0;
 #pragma unroll 1
     for (int round = 0; round < nrounds; round++) {
@@ -306,9 +307,11 @@ __global__ __launch_bounds__(256, 4) void k_leaf2(const float* __restrict__ x, i
         const int64_t c0 = c_tile + round * kChunksPerWave;
         const int64_t chunk = c0 + (lane >> 3);
         const bool valid = PARTIAL ? chunk < chunks : true;
-        uint32_t v[32];
-        // Only a zero test per element here (one v_cmp_class into a wave mask); NaN, min and max
-        // come from the sorted extremes below, the zero signs only when zeros are present.
+        // The values are sorted as floats (v_min/v_max/v_med3_f32, no key conversion): on gfx950
+        // these order -0.0 before 0.0 (tools/ubench/zero_minmax.hip), i.e. Arrays.sort's total
+        // order, for every value but NaN, which they drop.  One class test per element flags
+        // zeros and NaN into a wave mask; NaN is reported from it.
+        float v[32];
         uint64_t zmask = 0;
         {
             const float4* src = reinterpret_cast<const float4*>(x + (valid ? chunk : c0) * kChunk);
@@ -320,25 +323,27 @@ __global__ __launch_bounds__(256, 4) void k_leaf2(const float* __restrict__ x, i
                 const float e4[4] = {f[j].x, f[j].y, f[j].z, f[j].w};
 #pragma unroll
                 for (int e = 0; e < 4; e++) {
-                    zmask |= __ballot(__builtin_amdgcn_class(e4[e], 0x60));  // -0.0 | +0.0
-                    v[j * 4 + e] = f2key(__float_as_uint(e4[e]));
+                    zmask |= __ballot(__builtin_amdgcn_classf(e4[e], 0x63));  // -0.0 | +0.0 | NaN
+                    v[j * 4 + e] = e4[e];
                 }
             }
             if (PARTIAL) zmask &= __ballot(valid);
         }
         uint32_t rfl = 0;
-        if (zmask) {  // wave-uniform: which zero signs (keys 0x7FFFFFFF = -0.0, 0x80000000 = +0.0)
-            uint64_t nz = 0, pz = 0;
+        if (zmask) {  // wave-uniform: which zero signs, and NaN
+            uint64_t nz = 0, pz = 0, nan = 0;
 #pragma unroll
             for (int r = 0; r < 32; r++) {
-                nz |= __ballot(v[r] == 0x7FFFFFFFu);
-                pz |= __ballot(v[r] == 0x80000000u);
+                nz |= __ballot(__builtin_amdgcn_classf(v[r], 0x20));
+                pz |= __ballot(__builtin_amdgcn_classf(v[r], 0x40));
+                nan |= __ballot(__builtin_amdgcn_classf(v[r], 0x03));
             }
             if (PARTIAL) {
                 nz &= __ballot(valid);
                 pz &= __ballot(valid);
+                nan &= __ballot(valid);
             }
-            rfl = (nz ? 2u : 0u) | (pz ? 4u : 0u);
+            rfl = (nz ? 2u : 0u) | (pz ? 4u : 0u) | (nan ? 1u : 0u);
             fl |= rfl;
         }
         // compaction bits of this round's chunks (and their carries): draws [start, start+64)
@@ -351,7 +356,7 @@ __global__ __launch_bounds__(256, 4) void k_leaf2(const float* __restrict__ x, i
         }
         if constexpr (STAGE == 0) {
 #pragma unroll
-            for (int r = 0; r < 32; r++) acc ^= v[r];
+            for (int r = 0; r < 32; r++) acc ^= __float_as_uint(v[r]);
             acc ^= (uint32_t)mask;
             continue;
         }
@@ -362,15 +367,15 @@ __global__ __launch_bounds__(256, 4) void k_leaf2(const float* __restrict__ x, i
             return (uint32_t)(mask >> (node_bit_index((uint64_t)last_chunk, level) - start)) & 1u;
         };
 
-        uint32_t w1[16];
+        float w1[16];
         {
             sort_regs_oddeven<32>(v);
             sort_lanes_upto128<32, 64>(v, lane);
             // the chunk's two sorted 128-runs: its extremes are the chunk min / max (min at
             // register 0 of one lane, max at register 31 of another)
             if (valid) {
-                mn = min(mn, v[0]);
-                mx = max(mx, v[31]);
+                mn = min(mn, f2key(__float_as_uint(v[0])));
+                mx = max(mx, f2key(__float_as_uint(v[31])));
             }
             merge_group_compact<32>(v, w1, lane, bit(0, chunk) != 0);
         }
@@ -378,16 +383,16 @@ __global__ __launch_bounds__(256, 4) void k_leaf2(const float* __restrict__ x, i
         exp.template at<16>(0, lane >> 3, w1);
         if constexpr (STAGE == 1) {
 #pragma unroll
-            for (int r = 0; r < 16; r++) acc ^= w1[r];
+            for (int r = 0; r < 16; r++) acc ^= __float_as_uint(w1[r]);
             continue;
         }
         uint32_t ibits = 0;
         for (int j = 0; j < 4; j++) ibits |= bit(1, c0 + 2 * j + 1) << j;
         ibits |= bit(2, c0 + 3) << 4 | bit(2, c0 + 7) << 5 | bit(3, c0 + 7) << 6;
-        uint32_t node[2];
+        float node[2];
         inwave_levels(w1, node, lane, ibits, exact, wfb, exp);
         if constexpr (STAGE == 2) {
-            acc ^= node[0] ^ node[1];
+            acc ^= __float_as_uint(node[0]) ^ __float_as_uint(node[1]);
             continue;
         }
 
@@ -397,7 +402,7 @@ __global__ __launch_bounds__(256, 4) void k_leaf2(const float* __restrict__ x, i
             st3[1] = node[1];
             continue;
         }
-        uint32_t n4[2];
+        float n4[2];
         wave_node_merge(st3, node, n4, lane, bit(4, c0 + 7), exact, wfb);
         if constexpr (PARTIAL)
             if (((rem >> 4) & 1) && (int64_t)(round - 1) * kChunksPerWave == ((int64_t)(rem >> 5) << 5))
@@ -407,7 +412,7 @@ __global__ __launch_bounds__(256, 4) void k_leaf2(const float* __restrict__ x, i
             st4[1] = n4[1];
             continue;
         }
-        uint32_t n5[2];
+        float n5[2];
         wave_node_merge(st4, n4, n5, lane, bit(5, c0 + 7), exact, wfb);
         if constexpr (PARTIAL)
             if (((rem >> 5) & 1) && round == 3) store_node<2>(n5, lane, roots + (size_t)5 * kK);
@@ -988,8 +993,8 @@ hipError_t launch_summary(hipStream_t st, const float* x, int64_t n, const LeafP
 struct MergeExport {
     int lane, wave, g;
     float* out;
-    template <int R>
-    __device__ __forceinline__ void at(int level, int node, const uint32_t (&w)[R]) const {
+    template <int R, typename T>
+    __device__ __forceinline__ void at(int level, int node, const T (&w)[R]) const {
         if (level == g && wave == 0 && node == 0) store_node<R>(w, lane, out);
     }
 };
