@@ -52,7 +52,7 @@ hipError_t launch_part_scatter(hipStream_t st, const int32_t* keys, const void* 
                                int32_t* gbins);
 // Deltas, bitsNeeded histogram, order check, and the per-bucket pair counts of the bucketed
 // MinMaxSketch.insert (bucket_count: nbuckets u64, zeroed; unused when rows == 0).
-constexpr int kMmCellsPerBucket = 8192;
+constexpr int kMmCellsPerBucket = 4096;  // MinMax cells per bucket (32 KB of u64 minima in LDS)
 // cells (rows x n int32, may be null): each (element, row) pair's table cell, kept for the scatter.
 hipError_t launch_group_prep(hipStream_t st, const int32_t* gkeys, int64_t n, const SpGroups* gp, uint8_t* need,
                              uint32_t* hist, uint32_t* err, uint64_t* bucket_count, int nbuckets, int32_t* cells);

@@ -466,9 +466,10 @@ hipError_t launch_part_scatter(hipStream_t st, const int32_t* keys, const void* 
 // Pair word: |bin - zero| [63:48], key [47:17], bin < zero [16], cell % 8192 [12:0]; its value
 // with the cell bits cleared orders by (distance, key): the smaller distance wins and ties keep
 // the earlier insert (keys ascend within a group).
-constexpr int kMmBucketBits = 13;
-constexpr int kMmBucketCells = 1 << kMmBucketBits;
-constexpr int kMmLdsBuckets = 8192;  // per-workgroup bucket histogram in LDS up to this many
+constexpr int kMmBucketBits = 12;
+constexpr int kMmBucketCells = kMmCellsPerBucket;
+static_assert(kMmBucketCells == 1 << kMmBucketBits, "bucket size");
+constexpr int kMmLdsBuckets = 8192;  // per-workgroup bucket tables in LDS up to this many (96 KB in the scatter)
 constexpr int kMmChunk = 16384;      // elements per workgroup in the count / scatter passes
 
 __device__ __forceinline__ int64_t mm_cell(const SpGroups* gp, int g, int r, int32_t key) {
@@ -490,7 +491,7 @@ __global__ __launch_bounds__(kSpThreads) void k_group_prep(const int32_t* __rest
                                                            int nbuckets, int32_t* __restrict__ cells_out) {
     __shared__ int64_t S[kMaxGroups + 1];
     __shared__ uint32_t H[kMaxGroups * kDeltaHist];
-    __shared__ uint32_t BH[kMmLdsBuckets];
+    extern __shared__ uint32_t BH[];  // nbuckets counters (dynamic: occupancy follows the table size)
     const int G = gp->G, rows = gp->rows;
     const bool lds_b = nbuckets <= kMmLdsBuckets;
     load_starts(gp, S);
@@ -533,13 +534,25 @@ __global__ __launch_bounds__(kSpThreads) void k_group_prep(const int32_t* __rest
 hipError_t launch_group_prep(hipStream_t st, const int32_t* gkeys, int64_t n, const SpGroups* gp, uint8_t* need,
                              uint32_t* hist, uint32_t* err, uint64_t* bucket_count, int nbuckets, int32_t* cells) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_group_prep, dim3((unsigned)sp_tiles(n, kMmChunk)), dim3(kSpThreads), 0, st, gkeys, n, gp,
+    const size_t lds = nbuckets <= kMmLdsBuckets ? sizeof(uint32_t) * (size_t)(nbuckets > 0 ? nbuckets : 1) : 0;
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_group_prep),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)(sizeof(uint32_t) * kMmLdsBuckets));
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_group_prep, dim3((unsigned)sp_tiles(n, kMmChunk)), dim3(kSpThreads), lds, st, gkeys, n, gp,
                        need, hist, err, reinterpret_cast<unsigned long long*>(bucket_count), nbuckets, cells);
     return hipGetLastError();
 }
 
 // Scatter the pairs into bucket order: per-workgroup bucket counts reserve one range per bucket
-// (one global atomic per workgroup and bucket), lanes take slots with LDS atomics.
+// (one global atomic per workgroup and bucket), lanes take slots with LDS atomics.  Each thread
+// handles 4 elements per step (4 independent load -> LDS atomic -> store chains), and the
+// reserved 64-bit destinations sit in LDS, so the scatter never waits on a global load.
+constexpr int kMmUnroll = 4;
 __global__ __launch_bounds__(kSpThreads) void k_mm_scatter(const int32_t* __restrict__ gkeys,
                                                            const int32_t* __restrict__ gbins, int64_t n,
                                                            const SpGroups* __restrict__ gp,
@@ -548,8 +561,9 @@ __global__ __launch_bounds__(kSpThreads) void k_mm_scatter(const int32_t* __rest
                                                            uint64_t* __restrict__ pairs,
                                                            const int32_t* __restrict__ cells_in) {
     __shared__ int64_t S[kMaxGroups + 1];
-    __shared__ uint32_t cnt[kMmLdsBuckets];
-    __shared__ uint32_t lofs[kMmLdsBuckets];
+    extern __shared__ uint64_t dyn64[];  // dst[nbuckets] (u64), cnt[nbuckets] (u32): dynamic, see launch
+    uint64_t* dstb = dyn64;
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(dyn64 + nbuckets);
     const int rows = gp->rows, zero = gp->zero;
     const bool lds_b = nbuckets <= kMmLdsBuckets;
     load_starts(gp, S);
@@ -562,27 +576,37 @@ __global__ __launch_bounds__(kSpThreads) void k_mm_scatter(const int32_t* __rest
         return cells_in ? (int64_t)cells_in[(int64_t)r * n + i] : mm_cell(gp, g, r, key);
     };
     if (lds_b) {
-        for (int64_t i = c0 + threadIdx.x; i < c1; i += kSpThreads) {
-            const int g = cells_in ? 0 : group_of_elem(S, i);
-            const int32_t key = cells_in ? 0 : gkeys[i];
-            for (int r = 0; r < rows; r++) atomicAdd(&cnt[(int)(cell_of(g, r, i, key) >> kMmBucketBits)], 1u);
+        for (int64_t base = c0; base < c1; base += kMmUnroll * kSpThreads) {
+#pragma unroll
+            for (int u = 0; u < kMmUnroll; u++) {
+                const int64_t i = base + u * kSpThreads + threadIdx.x;
+                if (i >= c1) break;
+                const int g = cells_in ? 0 : group_of_elem(S, i);
+                const int32_t key = cells_in ? 0 : gkeys[i];
+                for (int r = 0; r < rows; r++) atomicAdd(&cnt[(int)(cell_of(g, r, i, key) >> kMmBucketBits)], 1u);
+            }
         }
         __syncthreads();
         for (int j = threadIdx.x; j < nbuckets; j += kSpThreads) {
-            lofs[j] = cnt[j] ? (uint32_t)atomicAdd(&cursor[j], (unsigned long long)cnt[j]) : 0u;
+            dstb[j] = cnt[j] ? bucket_base[j] + atomicAdd(&cursor[j], (unsigned long long)cnt[j]) : 0ull;
             cnt[j] = 0;
         }
         __syncthreads();
     }
-    for (int64_t i = c0 + threadIdx.x; i < c1; i += kSpThreads) {
-        const int g = cells_in ? 0 : group_of_elem(S, i);
-        const int32_t key = gkeys[i], bin = gbins[i];
-        for (int r = 0; r < rows; r++) {
-            const int64_t cell = cell_of(g, r, i, key);
-            const int b = (int)(cell >> kMmBucketBits);
-            const uint64_t slot = lds_b ? (uint64_t)lofs[b] + atomicAdd(&cnt[b], 1u)
-                                        : (uint64_t)atomicAdd(&cursor[b], 1ull);
-            pairs[bucket_base[b] + slot] = mm_pair(key, bin, zero, cell);
+    for (int64_t base = c0; base < c1; base += kMmUnroll * kSpThreads) {
+#pragma unroll
+        for (int u = 0; u < kMmUnroll; u++) {
+            const int64_t i = base + u * kSpThreads + threadIdx.x;
+            if (i >= c1) break;
+            const int g = cells_in ? 0 : group_of_elem(S, i);
+            const int32_t key = gkeys[i], bin = gbins[i];
+            for (int r = 0; r < rows; r++) {
+                const int64_t cell = cell_of(g, r, i, key);
+                const int b = (int)(cell >> kMmBucketBits);
+                const uint64_t dst = lds_b ? dstb[b] + atomicAdd(&cnt[b], 1u)
+                                           : bucket_base[b] + (uint64_t)atomicAdd(&cursor[b], 1ull);
+                pairs[dst] = mm_pair(key, bin, zero, cell);
+            }
         }
     }
 }
@@ -591,7 +615,16 @@ hipError_t launch_mm_scatter(hipStream_t st, const int32_t* gkeys, const int32_t
                              const SpGroups* gp, const uint64_t* bucket_base, uint64_t* cursor, int nbuckets,
                              uint64_t* pairs, const int32_t* cells) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_mm_scatter, dim3((unsigned)sp_tiles(n, kMmChunk)), dim3(kSpThreads), 0, st, gkeys, gbins, n,
+    constexpr size_t kPer = sizeof(uint64_t) + sizeof(uint32_t);
+    const size_t lds = nbuckets <= kMmLdsBuckets ? kPer * (size_t)(nbuckets > 0 ? nbuckets : 1) : 0;
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mm_scatter),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kPer * kMmLdsBuckets));
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_mm_scatter, dim3((unsigned)sp_tiles(n, kMmChunk)), dim3(kSpThreads), lds, st, gkeys, gbins, n,
                        gp, bucket_base, reinterpret_cast<unsigned long long*>(cursor), nbuckets, pairs, cells);
     return hipGetLastError();
 }
