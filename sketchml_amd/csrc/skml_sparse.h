@@ -54,12 +54,16 @@ hipError_t launch_part_scatter(hipStream_t st, const int32_t* keys, const void* 
 // MinMaxSketch.insert (bucket_count: nbuckets u64, zeroed; unused when rows == 0).
 constexpr int kMmCellsPerBucket = 4096;  // MinMax cells per bucket (32 KB of u64 minima in LDS)
 // cells (rows x n int32, may be null): each (element, row) pair's table cell, kept for the scatter.
+// tile_off ([tiles of kMmChunk][nbuckets] u32, may be null): each tile's reserved offset inside
+// each bucket, taken while counting, so the scatter needs neither a count pass nor atomics.
 hipError_t launch_group_prep(hipStream_t st, const int32_t* gkeys, int64_t n, const SpGroups* gp, uint8_t* need,
-                             uint32_t* hist, uint32_t* err, uint64_t* bucket_count, int nbuckets, int32_t* cells);
+                             uint32_t* hist, uint32_t* err, uint64_t* bucket_count, int nbuckets, int32_t* cells,
+                             uint32_t* tile_off);
 // pairs in bucket order (bucket_base: exclusive scan of the counts; cursor: nbuckets u64, zeroed)
 hipError_t launch_mm_scatter(hipStream_t st, const int32_t* gkeys, const int32_t* gbins, int64_t n,
                              const SpGroups* gp, const uint64_t* bucket_base, uint64_t* cursor, int nbuckets,
-                             uint64_t* pairs, const int32_t* cells);
+                             uint64_t* pairs, const int32_t* cells, const uint32_t* tile_off);
+constexpr int64_t kMmChunkElems = 16384;  // elements per workgroup tile of the count / scatter passes
 // per-bucket minimum -> int32 MinMaxSketch tables (empty cells get the fill value)
 hipError_t launch_mm_bucket(hipStream_t st, const uint64_t* pairs, const uint64_t* bucket_base, int nbuckets,
                             int64_t ncells, int32_t zero, int32_t fill, int32_t* table);

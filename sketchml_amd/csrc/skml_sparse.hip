@@ -470,7 +470,7 @@ constexpr int kMmBucketBits = 12;
 constexpr int kMmBucketCells = kMmCellsPerBucket;
 static_assert(kMmBucketCells == 1 << kMmBucketBits, "bucket size");
 constexpr int kMmLdsBuckets = 8192;  // per-workgroup bucket tables in LDS up to this many (96 KB in the scatter)
-constexpr int kMmChunk = 16384;      // elements per workgroup in the count / scatter passes
+constexpr int kMmChunk = (int)kMmChunkElems;
 
 __device__ __forceinline__ int64_t mm_cell(const SpGroups* gp, int g, int r, int32_t key) {
     const int32_t cols = gp->cols[g];
@@ -488,7 +488,8 @@ __global__ __launch_bounds__(kSpThreads) void k_group_prep(const int32_t* __rest
                                                            uint8_t* __restrict__ need, uint32_t* __restrict__ hist,
                                                            uint32_t* __restrict__ err,
                                                            unsigned long long* __restrict__ bucket_count,
-                                                           int nbuckets, int32_t* __restrict__ cells_out) {
+                                                           int nbuckets, int32_t* __restrict__ cells_out,
+                                                           uint32_t* __restrict__ tile_off) {
     __shared__ int64_t S[kMaxGroups + 1];
     __shared__ uint32_t H[kMaxGroups * kDeltaHist];
     extern __shared__ uint32_t BH[];  // nbuckets counters (dynamic: occupancy follows the table size)
@@ -526,13 +527,32 @@ __global__ __launch_bounds__(kSpThreads) void k_group_prep(const int32_t* __rest
     __syncthreads();
     for (int j = threadIdx.x; j < G * kDeltaHist; j += kSpThreads)
         if (H[j]) atomicAdd(&hist[j], H[j]);
-    if (lds_b && rows > 0)
-        for (int j = threadIdx.x; j < nbuckets; j += kSpThreads)
-            if (BH[j]) atomicAdd(&bucket_count[j], (unsigned long long)BH[j]);
+    if (lds_b && rows > 0) {
+        if (tile_off) {  // reserve this tile's range in every bucket: 8 independent atomics in flight
+            uint32_t* row = tile_off + (int64_t)blockIdx.x * nbuckets;
+            for (int j0 = threadIdx.x; j0 < nbuckets; j0 += 8 * kSpThreads) {
+                unsigned long long o[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const int j = j0 + u * kSpThreads;
+                    o[u] = (j < nbuckets && BH[j]) ? atomicAdd(&bucket_count[j], (unsigned long long)BH[j]) : 0ull;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const int j = j0 + u * kSpThreads;
+                    if (j < nbuckets) row[j] = (uint32_t)o[u];
+                }
+            }
+        } else {
+            for (int j = threadIdx.x; j < nbuckets; j += kSpThreads)
+                if (BH[j]) atomicAdd(&bucket_count[j], (unsigned long long)BH[j]);
+        }
+    }
 }
 
 hipError_t launch_group_prep(hipStream_t st, const int32_t* gkeys, int64_t n, const SpGroups* gp, uint8_t* need,
-                             uint32_t* hist, uint32_t* err, uint64_t* bucket_count, int nbuckets, int32_t* cells) {
+                             uint32_t* hist, uint32_t* err, uint64_t* bucket_count, int nbuckets, int32_t* cells,
+                             uint32_t* tile_off) {
     if (n <= 0) return hipSuccess;
     const size_t lds = nbuckets <= kMmLdsBuckets ? sizeof(uint32_t) * (size_t)(nbuckets > 0 ? nbuckets : 1) : 0;
     static bool attr = false;
@@ -544,7 +564,8 @@ hipError_t launch_group_prep(hipStream_t st, const int32_t* gkeys, int64_t n, co
         attr = true;
     }
     hipLaunchKernelGGL(k_group_prep, dim3((unsigned)sp_tiles(n, kMmChunk)), dim3(kSpThreads), lds, st, gkeys, n, gp,
-                       need, hist, err, reinterpret_cast<unsigned long long*>(bucket_count), nbuckets, cells);
+                       need, hist, err, reinterpret_cast<unsigned long long*>(bucket_count), nbuckets, cells,
+                       nbuckets <= kMmLdsBuckets ? tile_off : nullptr);
     return hipGetLastError();
 }
 
@@ -559,7 +580,8 @@ __global__ __launch_bounds__(kSpThreads) void k_mm_scatter(const int32_t* __rest
                                                            const uint64_t* __restrict__ bucket_base,
                                                            unsigned long long* __restrict__ cursor, int nbuckets,
                                                            uint64_t* __restrict__ pairs,
-                                                           const int32_t* __restrict__ cells_in) {
+                                                           const int32_t* __restrict__ cells_in,
+                                                           const uint32_t* __restrict__ tile_off) {
     __shared__ int64_t S[kMaxGroups + 1];
     extern __shared__ uint64_t dyn64[];  // dst[nbuckets] (u64), cnt[nbuckets] (u32): dynamic, see launch
     uint64_t* dstb = dyn64;
@@ -575,7 +597,11 @@ __global__ __launch_bounds__(kSpThreads) void k_mm_scatter(const int32_t* __rest
     auto cell_of = [&](int g, int r, int64_t i, int32_t key) -> int64_t {
         return cells_in ? (int64_t)cells_in[(int64_t)r * n + i] : mm_cell(gp, g, r, key);
     };
-    if (lds_b) {
+    if (lds_b && tile_off) {  // ranges reserved by k_group_prep
+        const uint32_t* row = tile_off + (int64_t)blockIdx.x * nbuckets;
+        for (int j = threadIdx.x; j < nbuckets; j += kSpThreads) dstb[j] = bucket_base[j] + row[j];
+        __syncthreads();
+    } else if (lds_b) {
         for (int64_t base = c0; base < c1; base += kMmUnroll * kSpThreads) {
 #pragma unroll
             for (int u = 0; u < kMmUnroll; u++) {
@@ -613,7 +639,7 @@ __global__ __launch_bounds__(kSpThreads) void k_mm_scatter(const int32_t* __rest
 
 hipError_t launch_mm_scatter(hipStream_t st, const int32_t* gkeys, const int32_t* gbins, int64_t n,
                              const SpGroups* gp, const uint64_t* bucket_base, uint64_t* cursor, int nbuckets,
-                             uint64_t* pairs, const int32_t* cells) {
+                             uint64_t* pairs, const int32_t* cells, const uint32_t* tile_off) {
     if (n <= 0) return hipSuccess;
     constexpr size_t kPer = sizeof(uint64_t) + sizeof(uint32_t);
     const size_t lds = nbuckets <= kMmLdsBuckets ? kPer * (size_t)(nbuckets > 0 ? nbuckets : 1) : 0;
@@ -625,7 +651,8 @@ hipError_t launch_mm_scatter(hipStream_t st, const int32_t* gkeys, const int32_t
         attr = true;
     }
     hipLaunchKernelGGL(k_mm_scatter, dim3((unsigned)sp_tiles(n, kMmChunk)), dim3(kSpThreads), lds, st, gkeys, gbins, n,
-                       gp, bucket_base, reinterpret_cast<unsigned long long*>(cursor), nbuckets, pairs, cells);
+                       gp, bucket_base, reinterpret_cast<unsigned long long*>(cursor), nbuckets, pairs, cells,
+                       nbuckets <= kMmLdsBuckets ? tile_off : nullptr);
     return hipGetLastError();
 }
 

@@ -53,6 +53,7 @@ enum {
     kSlotB1,
     kSlotStatus,
     kSlotCellIdx,
+    kSlotTileOff,
 };
 
 // java.util.Random (JDK 8 spec): seed scramble, next(bits), nextInt(bound).
@@ -471,7 +472,12 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const float* vals, int64_t nnz, 
         return bail(sfail(SKML_E_HIP, "memset"));
     // the pairs' table cells, hashed once (int32 cells; without room or past 2^31 cells the scatter rehashes)
     int32_t* cellbuf = cells < INT32_MAX ? scratch<int32_t>(c, kSlotCellIdx, (size_t)G.rows * (size_t)nnz) : nullptr;
-    if (hipSuccess != launch_group_prep(st, gk, nnz, s->g_dev, need, hist, err, bucket, nbuckets, cellbuf))
+    // per (tile, bucket) reserved offsets (u32: a bucket holds fewer than 2^32 pairs)
+    const int64_t mm_tiles = sp_tiles(nnz, kMmChunkElems);
+    uint32_t* tile_off = (uint64_t)G.rows * (uint64_t)nnz < (1ull << 32)
+                             ? scratch<uint32_t>(c, kSlotTileOff, (size_t)mm_tiles * (size_t)nbuckets)
+                             : nullptr;
+    if (hipSuccess != launch_group_prep(st, gk, nnz, s->g_dev, need, hist, err, bucket, nbuckets, cellbuf, tile_off))
         return bail(sfail(SKML_E_HIP, "group_prep"));
     std::vector<uint32_t> hh((size_t)kMaxGroups * kDeltaHist + 1);
     if (int e = sync_to_host(c, hh.data(), small, sizeof(uint32_t) * hh.size())) return bail(e);
@@ -480,7 +486,7 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const float* vals, int64_t nnz, 
     if (hipMalloc(&s->tables, sizeof(int32_t) * (size_t)std::max<int64_t>(cells, 1)) != hipSuccess)
         return bail(sfail(SKML_E_OOM, "tables"));
     if (int e = scan_tiles(c, bucket, nbuckets, 1, nullptr)) return bail(e);
-    if (hipSuccess != launch_mm_scatter(st, gk, gb, nnz, s->g_dev, bucket, cursor, nbuckets, pairs, cellbuf) ||
+    if (hipSuccess != launch_mm_scatter(st, gk, gb, nnz, s->g_dev, bucket, cursor, nbuckets, pairs, cellbuf, tile_off) ||
         hipSuccess != launch_mm_bucket(st, pairs, bucket, nbuckets, cells, G.zero, G.fill, s->tables))
         return bail(sfail(SKML_E_HIP, "minmax insert"));
     // ---- 5. DeltaAdaptive key streams ----
@@ -1343,7 +1349,7 @@ int skml_delta_encode(skml_ctx* c, const int32_t* keys, int64_t n, int32_t* num_
             break;
         }
         if (launch_group_prep(st, keys, n, tmp.g_dev, need, small, small + kMaxGroups * kDeltaHist, nullptr,
-                              0, nullptr) != hipSuccess) {
+                              0, nullptr, nullptr) != hipSuccess) {
             rc = sfail(SKML_E_HIP, "group_prep");
             break;
         }
