@@ -753,7 +753,7 @@ int run_sketch_f64(skml_ctx* c, const double* x, int64_t n, uint64_t s0, const W
     const int64_t chunks = n / kChunk;
     {
         KernelTimer kt(c, SKML_K_LEAF);
-        HIP_TRY(launch_leaf64(c->stream, x, chunks, s0, c->jump_tab, w.part, w.nodes6, w.roots));
+        HIP_TRY(launch_leaf2_f64(c->stream, x, chunks, s0, c->jump_tab, w.part, w.nodes6, w.roots));
     }
     // trees of bits l > 6 of the chunk count: carry their level-6 nodes down to one root,
     // up to 2^3 nodes per wave and pass

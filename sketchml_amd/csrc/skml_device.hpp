@@ -43,11 +43,17 @@ template <int M>
 __device__ __forceinline__ float lane_xor(float v) {
     return __uint_as_float(lane_xor<M>(__float_as_uint(v)));
 }
+template <int M>
+__device__ __forceinline__ double lane_xor(double v) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = lane_xor<M>((uint32_t)b), hi = lane_xor<M>((uint32_t)(b >> 32));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
 
-// Sort elements are either uint32 total-order keys or the raw floats.  Floats compare with
-// v_min/v_max/v_med3_f32, whose order is Arrays.sort's except for -0.0 vs 0.0 (equal) and NaN
-// (dropped by min/max): the leaf takes the float path only in rounds without mixed-sign zeros and
-// flags NaN from a class test at load (k_leaf2).  fbits: the float's bit pattern.
+// Sort elements are uint32 total-order keys, raw floats or raw doubles.  Floats and doubles
+// compare with v_min/v_max(/v_med3)_f32/f64, which on gfx950 order -0.0 before 0.0 like
+// Arrays.sort (tools/ubench/zero_minmax.hip) and drop NaN, so the leaf flags NaN from a class
+// test at load (k_leaf2).  fbits: the float's bit pattern.
 __device__ __forceinline__ uint32_t elem_fbits(uint32_t k) { return key2f(k); }
 __device__ __forceinline__ uint32_t elem_fbits(float f) { return __float_as_uint(f); }
 template <typename T>
@@ -65,6 +71,31 @@ template <>
 __device__ __forceinline__ float sel_of<float>(bool upper) {
     return __uint_as_float(upper ? 0x7F800000u : 0xFF800000u);
 }
+template <>
+__device__ __forceinline__ double sel_of<double>(bool upper) {
+    return __longlong_as_double(upper ? 0x7FF0000000000000LL : (long long)0xFFF0000000000000ULL);
+}
+
+// How each element type is held in LDS / global node buffers (float for keys and floats,
+// double for doubles) and converted.
+template <typename T>
+struct Elem {  // uint32 total-order keys
+    using S = float;
+    __device__ static __forceinline__ S to_s(uint32_t k) { return __uint_as_float(key2f(k)); }
+    __device__ static __forceinline__ uint32_t from_s(S f) { return f2key(__float_as_uint(f)); }
+};
+template <>
+struct Elem<float> {
+    using S = float;
+    __device__ static __forceinline__ S to_s(float f) { return f; }
+    __device__ static __forceinline__ float from_s(S f) { return f; }
+};
+template <>
+struct Elem<double> {
+    using S = double;
+    __device__ static __forceinline__ S to_s(double d) { return d; }
+    __device__ static __forceinline__ double from_s(S d) { return d; }
+};
 
 __device__ __forceinline__ void ce(uint32_t& a, uint32_t& b) {
     uint32_t lo = a < b ? a : b;
@@ -78,6 +109,13 @@ __device__ __forceinline__ void ce(float& a, float& b) {
     float lo, hi;
     asm("v_min_f32 %0, %1, %2" : "=v"(lo) : "v"(a), "v"(b));
     asm("v_max_f32 %0, %1, %2" : "=v"(hi) : "v"(a), "v"(b));
+    a = lo;
+    b = hi;
+}
+__device__ __forceinline__ void ce(double& a, double& b) {
+    double lo, hi;
+    asm("v_min_f64 %0, %1, %2" : "=v"(lo) : "v"(a), "v"(b));
+    asm("v_max_f64 %0, %1, %2" : "=v"(hi) : "v"(a), "v"(b));
     a = lo;
     b = hi;
 }
@@ -165,6 +203,13 @@ __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
 }
 __device__ __forceinline__ uint32_t med3(uint32_t a, uint32_t b, uint32_t c) { return umed3(a, b, c); }
 __device__ __forceinline__ float med3(float a, float b, float c) { return __builtin_amdgcn_fmed3f(a, b, c); }
+// no v_med3_f64: c is +inf (keep the max) or -inf (keep the min)
+__device__ __forceinline__ double med3(double a, double b, double c) {
+    double lo, hi;
+    asm("v_min_f64 %0, %1, %2" : "=v"(lo) : "v"(a), "v"(b));
+    asm("v_max_f64 %0, %1, %2" : "=v"(hi) : "v"(a), "v"(b));
+    return __double_as_longlong(c) > 0 ? hi : lo;
+}
 
 // Flip stage across a block of (M+1) lanes: element (lane, r) meets (lane^M, R-1-r).
 template <int R, int M, typename T>
@@ -315,23 +360,25 @@ __device__ __forceinline__ uint64_t node_bit_index(uint64_t c, int level) {
 // QSketchUtils.java:53-69: IEEE `<`, a tie emits the NEWER run first) followed by compaction.
 // Task t in [0,256): element t of older (t<128) or newer.  Writes kept elements to out.
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ int count_le(const float* run, float x) {  // #{run[i] <= x}
+template <typename S>
+__device__ __forceinline__ int count_le(const S* run, S x) {  // #{run[i] <= x}
     int lo = 0;
 #pragma unroll
     for (int step = 64; step >= 1; step >>= 1)
         if (run[lo + step - 1] <= x) lo += step;
     return lo + (run[lo] <= x ? 1 : 0) * (lo == 127 ? 1 : 0);
 }
-__device__ __forceinline__ int count_lt(const float* run, float x) {  // #{run[i] < x}
+template <typename S>
+__device__ __forceinline__ int count_lt(const S* run, S x) {  // #{run[i] < x}
     int lo = 0;
 #pragma unroll
     for (int step = 64; step >= 1; step >>= 1)
         if (run[lo + step - 1] < x) lo += step;
     return lo + (run[lo] < x ? 1 : 0) * (lo == 127 ? 1 : 0);
 }
-__device__ __forceinline__ void exact_merge_task(const float* older, const float* newer, float* out,
-                                                 int t, uint32_t odd) {
-    float v;
+template <typename S>
+__device__ __forceinline__ void exact_merge_task(const S* older, const S* newer, S* out, int t, uint32_t odd) {
+    S v;
     int pos;
     if (t < 128) {
         v = older[t];

@@ -78,6 +78,9 @@ struct SketchRecord64 {
     double tail[kChunk];
     double level[kMaxLevels][kK];
 };
+// fp64 leaf in the fp32 leaf's layout (8 lanes x 32 values per chunk), skml_sketch.hip
+hipError_t launch_leaf2_f64(hipStream_t st, const double* x, int64_t chunks, uint64_t s0, const uint64_t* jump_tab,
+                            LeafPartial64* part, double* nodes6, double* roots);
 hipError_t launch_sketch_record64(hipStream_t st, const double* x, int64_t n, const LeafPartial64* part,
                                   int64_t nparts, const double* roots, SketchRecord64* rec);
 // Merge of fp64 records into (roots, tail, part) for launch_summary64 (tail, sharded = 1).

@@ -21,6 +21,7 @@
 // the newer run) unless a merge sees both -0.0 and +0.0, in which case that workgroup takes the
 // exact LDS path (count-based merge positions with the reference tie rule).
 #include <cstring>
+#include <type_traits>
 
 #include "skml_device.hpp"
 
@@ -94,28 +95,27 @@ union MergeShared {
 // Exact path for one in-wave merge level (R keys / lane, G = 256/R lanes per merge group).
 // fb holds 1536 floats: runs in [0, 1024), merged nodes in [1024, 1536).  The element loop is
 // kept rolled and reads back from LDS so this rare path adds no register pressure.
-template <int R, typename T>
-__device__ __forceinline__ void wave_exact_level(T (&v)[R], T (&w)[R / 2], int lane, uint32_t odd, float* fb) {
+template <int R, typename T, typename S = typename Elem<T>::S>
+__device__ __forceinline__ void wave_exact_level(T (&v)[R], T (&w)[R / 2], int lane, uint32_t odd, S* fb) {
     constexpr int G = 256 / R;
     const int grp = lane / G, li = lane % G;
-    float* run = fb + grp * 256;
-    float* out = fb + 1024 + grp * 128;
+    S* run = fb + grp * 256;
+    S* out = fb + 1024 + grp * 128;
 #pragma unroll
-    for (int r = 0; r < R; r++) run[li * R + r] = __uint_as_float(elem_fbits(v[r]));
+    for (int r = 0; r < R; r++) run[li * R + r] = Elem<T>::to_s(v[r]);
 #pragma unroll 1
     for (int r = 0; r < R; r++) {
         const int p = li * R + r;
-        const float x = run[p];
+        const S x = run[p];
         const int pos = p < 128 ? p + count_le(run + 128, x) : (p - 128) + count_lt(run, x);
         if (((uint32_t)pos & 1u) == odd) out[pos >> 1] = x;
     }
 #pragma unroll
-    for (int j = 0; j < R / 2; j++) w[j] = elem_of_fbits<T>(__float_as_uint(out[li * (R / 2) + j]));
+    for (int j = 0; j < R / 2; j++) w[j] = Elem<T>::from_s(out[li * (R / 2) + j]);
 }
 
-template <int R, typename T>
-__device__ __forceinline__ void wave_level(T (&v)[R], T (&w)[R / 2], int lane, uint32_t odd, bool exact,
-                                           float* fb) {
+template <int R, typename T, typename S>
+__device__ __forceinline__ void wave_level(T (&v)[R], T (&w)[R / 2], int lane, uint32_t odd, bool exact, S* fb) {
     if (!exact) {
         merge_group_compact<R>(v, w, lane, odd != 0);
     } else {
@@ -125,26 +125,29 @@ __device__ __forceinline__ void wave_level(T (&v)[R], T (&w)[R / 2], int lane, u
 
 // Write the node held by lanes [g*G, g*G+G) (R keys per lane) as 128 floats.
 template <int R, typename T>
-__device__ __forceinline__ void store_node(const T (&w)[R], int lane, float* dst) {
+__device__ __forceinline__ void store_node(const T (&w)[R], int lane, typename Elem<T>::S* dst) {
     constexpr int G = kK / R;
     const int li = lane % G;
-    if constexpr (R >= 4) {  // vector stores: few address registers
+    if constexpr (std::is_same<T, double>::value) {
+        double2* d = reinterpret_cast<double2*>(dst + li * R);
+#pragma unroll
+        for (int q = 0; q < R / 2; q++) d[q] = make_double2(w[2 * q], w[2 * q + 1]);
+    } else if constexpr (R >= 4) {  // vector stores: few address registers
         float4* d = reinterpret_cast<float4*>(dst + li * R);
 #pragma unroll
         for (int q = 0; q < R / 4; q++)
-            d[q] = make_float4(__uint_as_float(elem_fbits(w[4 * q])), __uint_as_float(elem_fbits(w[4 * q + 1])),
-                               __uint_as_float(elem_fbits(w[4 * q + 2])), __uint_as_float(elem_fbits(w[4 * q + 3])));
+            d[q] = make_float4(Elem<T>::to_s(w[4 * q]), Elem<T>::to_s(w[4 * q + 1]), Elem<T>::to_s(w[4 * q + 2]),
+                               Elem<T>::to_s(w[4 * q + 3]));
     } else {
-        reinterpret_cast<float2*>(dst + li * R)[0] =
-            make_float2(__uint_as_float(elem_fbits(w[0])), __uint_as_float(elem_fbits(w[1])));
+        reinterpret_cast<float2*>(dst + li * R)[0] = make_float2(Elem<T>::to_s(w[0]), Elem<T>::to_s(w[1]));
     }
 }
 
 // Levels +1..+3 inside a wave.  bits: 0..3 -> level+1 nodes, 4..5 -> level+2, 6 -> level+3.
 // Exp(level_offset, node_in_wave, regs...) is called after each level for root exports.
-template <typename T, class Exp>
-__device__ __forceinline__ void inwave_levels(T (&w1)[16], T (&w4)[2], int lane, uint32_t bits, bool exact,
-                                              float* fb, Exp&& exp) {
+template <typename T, typename S, class Exp>
+__device__ __forceinline__ void inwave_levels(T (&w1)[16], T (&w4)[2], int lane, uint32_t bits, bool exact, S* fb,
+                                              Exp&& exp) {
     T w2[8], w3[4];
     wave_level<16>(w1, w2, lane, (bits >> (lane >> 4)) & 1u, exact, fb);
     exp.template at<8>(1, lane >> 4, w2);
@@ -155,17 +158,22 @@ __device__ __forceinline__ void inwave_levels(T (&w1)[16], T (&w4)[2], int lane,
 }
 
 // One wave merges two 128-float nodes from LDS into `out` (bitonic, 64 lanes x 4 keys).
-template <typename T = uint32_t>
-__device__ __forceinline__ void wave_pair_merge(const float* A, const float* B, float* out, int lane,
-                                                uint32_t odd) {
-    const float4 f = lane < 32 ? reinterpret_cast<const float4*>(A)[lane]
-                               : reinterpret_cast<const float4*>(B)[lane - 32];
-    T v[4] = {elem_of_fbits<T>(__float_as_uint(f.x)), elem_of_fbits<T>(__float_as_uint(f.y)),
-              elem_of_fbits<T>(__float_as_uint(f.z)), elem_of_fbits<T>(__float_as_uint(f.w))};
-    T o[2];
-    merge_group_compact<4>(v, o, lane, odd != 0);
-    reinterpret_cast<float2*>(out)[lane] =
-        make_float2(__uint_as_float(elem_fbits(o[0])), __uint_as_float(elem_fbits(o[1])));
+template <typename T = uint32_t, typename S = typename Elem<T>::S>
+__device__ __forceinline__ void wave_pair_merge(const S* A, const S* B, S* out, int lane, uint32_t odd) {
+    const S* src = lane < 32 ? A + 4 * lane : B + 4 * (lane - 32);
+    T v[4], o[2];
+    if constexpr (std::is_same<S, double>::value) {
+        const double2 p = reinterpret_cast<const double2*>(src)[0], q = reinterpret_cast<const double2*>(src)[1];
+        v[0] = p.x, v[1] = p.y, v[2] = q.x, v[3] = q.y;
+        merge_group_compact<4>(v, o, lane, odd != 0);
+        reinterpret_cast<double2*>(out)[lane] = make_double2(o[0], o[1]);
+    } else {
+        const float4 f = reinterpret_cast<const float4*>(src)[0];
+        v[0] = Elem<T>::from_s(f.x), v[1] = Elem<T>::from_s(f.y), v[2] = Elem<T>::from_s(f.z),
+        v[3] = Elem<T>::from_s(f.w);
+        merge_group_compact<4>(v, o, lane, odd != 0);
+        reinterpret_cast<float2*>(out)[lane] = make_float2(Elem<T>::to_s(o[0]), Elem<T>::to_s(o[1]));
+    }
 }
 
 // Levels +4..+6 across the 8 waves.  bits: 0..3 level+4, 4..5 level+5, 6 level+6.
@@ -237,32 +245,33 @@ constexpr int kLeafWaveChunks = 64;
 constexpr int kLeaf2Waves = 4;
 
 // Merge two register-resident nodes (64 lanes x 2 keys, positions lane*2 + r): older A, newer B.
-template <typename T>
+template <typename T, typename S>
 __device__ __forceinline__ void wave_node_merge(const T (&A)[2], const T (&B)[2], T (&out)[2], int lane, uint32_t odd,
-                                                bool exact, float* buf) {
-    float* a = buf;
-    float* b = buf + kK;
-    float* o = buf + 2 * kK;
-    reinterpret_cast<float2*>(a)[lane] = make_float2(__uint_as_float(elem_fbits(A[0])), __uint_as_float(elem_fbits(A[1])));
-    reinterpret_cast<float2*>(b)[lane] = make_float2(__uint_as_float(elem_fbits(B[0])), __uint_as_float(elem_fbits(B[1])));
+                                                bool exact, S* buf) {
+    S* a = buf;
+    S* b = buf + kK;
+    S* o = buf + 2 * kK;
+    using S2 = typename std::conditional<std::is_same<S, double>::value, double2, float2>::type;
+    reinterpret_cast<S2*>(a)[lane] = S2{Elem<T>::to_s(A[0]), Elem<T>::to_s(A[1])};
+    reinterpret_cast<S2*>(b)[lane] = S2{Elem<T>::to_s(B[0]), Elem<T>::to_s(B[1])};
     if (!exact) {
         wave_pair_merge<T>(a, b, o, lane, odd);
     } else {
 #pragma unroll
         for (int k = 0; k < 4; k++) exact_merge_task(a, b, o, lane + 64 * k, odd);
     }
-    const float2 r = reinterpret_cast<const float2*>(o)[lane];
-    out[0] = elem_of_fbits<T>(__float_as_uint(r.x));
-    out[1] = elem_of_fbits<T>(__float_as_uint(r.y));
+    const S2 r = reinterpret_cast<const S2*>(o)[lane];
+    out[0] = Elem<T>::from_s(r.x);
+    out[1] = Elem<T>::from_s(r.y);
 }
 
 // Roots of the small trees inside the partial 64-chunk tile (compiled only into the PARTIAL
 // variant: a divergent export in the hot kernel costs ~50 VGPRs).
-template <bool PARTIAL>
+template <bool PARTIAL, typename S = float>
 struct WaveExport {
     int lane, rem;
     int64_t round_off;  // first chunk of the round relative to the tile
-    float* roots;
+    S* roots;
     template <int R, typename T>
     __device__ __forceinline__ void at(int level, int node, const T (&w)[R]) const {
         if constexpr (PARTIAL) {
@@ -274,13 +283,39 @@ struct WaveExport {
     }
 };
 
-template <int STAGE, bool PARTIAL = false>
-__global__ __launch_bounds__(256, 4) void k_leaf2(const float* __restrict__ x, int64_t chunks,
-                                               uint64_t s0, const uint64_t* __restrict__ tab,
-                                               LeafPartial* __restrict__ part,
-                                               float* __restrict__ nodes6,
-                                               float* __restrict__ roots, int64_t tile0) {
-    __shared__ float fb[kLeaf2Waves][kWaveFb];
+// E = float (fp32 input) or double (the reference's double[] itself: 2 registers per value,
+// hence at least 2 waves per SIMD instead of 4).
+template <typename E>
+struct LeafTypes {
+    using Key = uint32_t;
+    using Part = LeafPartial;
+    static constexpr int kMinWaves = 4;
+};
+template <>
+struct LeafTypes<double> {
+    using Key = uint64_t;
+    using Part = LeafPartial64;
+    static constexpr int kMinWaves = 2;
+};
+__device__ __forceinline__ uint32_t total_key(float f) { return f2key(__float_as_uint(f)); }
+__device__ __forceinline__ uint64_t total_key(double d) {
+    const uint64_t b = (uint64_t)__double_as_longlong(d);
+    return b ^ ((uint64_t)((int64_t)b >> 63) | 0x8000000000000000ull);
+}
+__device__ __forceinline__ bool is_class(float f, int mask) { return __builtin_amdgcn_classf(f, mask); }
+__device__ __forceinline__ bool is_class(double d, int mask) { return __builtin_amdgcn_class(d, mask); }
+__device__ __forceinline__ uint32_t fold32(float f) { return __float_as_uint(f); }
+__device__ __forceinline__ uint32_t fold32(double d) {
+    const uint64_t b = (uint64_t)__double_as_longlong(d);
+    return (uint32_t)b ^ (uint32_t)(b >> 32);
+}
+
+template <int STAGE, bool PARTIAL = false, typename E = float>
+__global__ __launch_bounds__(256, LeafTypes<E>::kMinWaves) void k_leaf2(
+    const E* __restrict__ x, int64_t chunks, uint64_t s0, const uint64_t* __restrict__ tab,
+    typename LeafTypes<E>::Part* __restrict__ part, E* __restrict__ nodes6, E* __restrict__ roots, int64_t tile0) {
+    using Key = typename LeafTypes<E>::Key;
+    __shared__ E fb[kLeaf2Waves][kWaveFb];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t tile = tile0 + (int64_t)blockIdx.x * kLeaf2Waves + wave;
     const int64_t c_tile = tile * kLeafWaveChunks;
@@ -288,15 +323,16 @@ __global__ __launch_bounds__(256, 4) void k_leaf2(const float* __restrict__ x, i
     const int64_t left = chunks - c_tile;
     const int rem = left < kLeafWaveChunks ? (int)left : 0;
     const int nrounds = rem ? (rem + kChunksPerWave - 1) / kChunksPerWave : kLeafWaveChunks / kChunksPerWave;
-    float* wfb = fb[wave];
+    E* wfb = fb[wave];
     const uint64_t ta = tab[lane * 2], tc = tab[lane * 2 + 1];  // A^lane, C_lane
 #ifdef SKML_PROF_LEAF
     const unsigned long long prof_t0 = wall_clock64();
 #endif
 
-    uint32_t mn = 0xFFFFFFFFu, mx = 0u, fl = 0u;
+    Key mn = ~(Key)0, mx = 0;
+    uint32_t fl = 0u;
     bool neg_any = false, pos_any = false;
-    float st3[2], st4[2], st5[2], top[2];
+    E st3[2], st4[2], st5[2], top[2];
     uint32_t acc = 0;
 #pragma unroll 1
     for (int round = 0; round < nrounds; round++) {
@@ -311,9 +347,20 @@ __global__ __launch_bounds__(256, 4) void k_leaf2(const float* __restrict__ x, i
         // these order -0.0 before 0.0 (tools/ubench/zero_minmax.hip), i.e. Arrays.sort's total
         // order, for every value but NaN, which they drop.  One class test per element flags
         // zeros and NaN into a wave mask; NaN is reported from it.
-        float v[32];
+        E v[32];
         uint64_t zmask = 0;
-        {
+        if constexpr (std::is_same<E, double>::value) {
+            const double2* src = reinterpret_cast<const double2*>(x + (valid ? chunk : c0) * kChunk);
+            double2 f[16];
+#pragma unroll
+            for (int j = 0; j < 16; j++) f[j] = src[j * 8 + (lane & 7)];
+#pragma unroll
+            for (int j = 0; j < 16; j++) {
+                zmask |= __ballot(is_class(f[j].x, 0x63) || is_class(f[j].y, 0x63));  // -0.0 | +0.0 | NaN
+                v[2 * j] = f[j].x;
+                v[2 * j + 1] = f[j].y;
+            }
+        } else {
             const float4* src = reinterpret_cast<const float4*>(x + (valid ? chunk : c0) * kChunk);
             float4 f[8];
 #pragma unroll
@@ -323,20 +370,20 @@ __global__ __launch_bounds__(256, 4) void k_leaf2(const float* __restrict__ x, i
                 const float e4[4] = {f[j].x, f[j].y, f[j].z, f[j].w};
 #pragma unroll
                 for (int e = 0; e < 4; e++) {
-                    zmask |= __ballot(__builtin_amdgcn_classf(e4[e], 0x63));  // -0.0 | +0.0 | NaN
+                    zmask |= __ballot(is_class(e4[e], 0x63));  // -0.0 | +0.0 | NaN
                     v[j * 4 + e] = e4[e];
                 }
             }
-            if (PARTIAL) zmask &= __ballot(valid);
         }
+        if (PARTIAL) zmask &= __ballot(valid);
         uint32_t rfl = 0;
         if (zmask) {  // wave-uniform: which zero signs, and NaN
             uint64_t nz = 0, pz = 0, nan = 0;
 #pragma unroll
             for (int r = 0; r < 32; r++) {
-                nz |= __ballot(__builtin_amdgcn_classf(v[r], 0x20));
-                pz |= __ballot(__builtin_amdgcn_classf(v[r], 0x40));
-                nan |= __ballot(__builtin_amdgcn_classf(v[r], 0x03));
+                nz |= __ballot(is_class(v[r], 0x20));
+                pz |= __ballot(is_class(v[r], 0x40));
+                nan |= __ballot(is_class(v[r], 0x03));
             }
             if (PARTIAL) {
                 nz &= __ballot(valid);
@@ -356,7 +403,7 @@ __global__ __launch_bounds__(256, 4) void k_leaf2(const float* __restrict__ x, i
         }
         if constexpr (STAGE == 0) {
 #pragma unroll
-            for (int r = 0; r < 32; r++) acc ^= __float_as_uint(v[r]);
+            for (int r = 0; r < 32; r++) acc ^= fold32(v[r]);
             acc ^= (uint32_t)mask;
             continue;
         }
@@ -367,32 +414,33 @@ __global__ __launch_bounds__(256, 4) void k_leaf2(const float* __restrict__ x, i
             return (uint32_t)(mask >> (node_bit_index((uint64_t)last_chunk, level) - start)) & 1u;
         };
 
-        float w1[16];
+        E w1[16];
         {
             sort_regs_oddeven<32>(v);
             sort_lanes_upto128<32, 64>(v, lane);
             // the chunk's two sorted 128-runs: its extremes are the chunk min / max (min at
             // register 0 of one lane, max at register 31 of another)
             if (valid) {
-                mn = min(mn, f2key(__float_as_uint(v[0])));
-                mx = max(mx, f2key(__float_as_uint(v[31])));
+                const Key k0 = total_key(v[0]), k31 = total_key(v[31]);
+                mn = k0 < mn ? k0 : mn;
+                mx = k31 > mx ? k31 : mx;
             }
             merge_group_compact<32>(v, w1, lane, bit(0, chunk) != 0);
         }
-        const WaveExport<PARTIAL> exp{lane, rem, round * kChunksPerWave, roots};
+        const WaveExport<PARTIAL, E> exp{lane, rem, round * kChunksPerWave, roots};
         exp.template at<16>(0, lane >> 3, w1);
         if constexpr (STAGE == 1) {
 #pragma unroll
-            for (int r = 0; r < 16; r++) acc ^= __float_as_uint(w1[r]);
+            for (int r = 0; r < 16; r++) acc ^= fold32(w1[r]);
             continue;
         }
         uint32_t ibits = 0;
         for (int j = 0; j < 4; j++) ibits |= bit(1, c0 + 2 * j + 1) << j;
         ibits |= bit(2, c0 + 3) << 4 | bit(2, c0 + 7) << 5 | bit(3, c0 + 7) << 6;
-        float node[2];
+        E node[2];
         inwave_levels(w1, node, lane, ibits, exact, wfb, exp);
         if constexpr (STAGE == 2) {
-            acc ^= __float_as_uint(node[0]) ^ __float_as_uint(node[1]);
+            acc ^= fold32(node[0]) ^ fold32(node[1]);
             continue;
         }
 
@@ -402,7 +450,7 @@ __global__ __launch_bounds__(256, 4) void k_leaf2(const float* __restrict__ x, i
             st3[1] = node[1];
             continue;
         }
-        float n4[2];
+        E n4[2];
         wave_node_merge(st3, node, n4, lane, bit(4, c0 + 7), exact, wfb);
         if constexpr (PARTIAL)
             if (((rem >> 4) & 1) && (int64_t)(round - 1) * kChunksPerWave == ((int64_t)(rem >> 5) << 5))
@@ -412,7 +460,7 @@ __global__ __launch_bounds__(256, 4) void k_leaf2(const float* __restrict__ x, i
             st4[1] = n4[1];
             continue;
         }
-        float n5[2];
+        E n5[2];
         wave_node_merge(st4, n4, n5, lane, bit(5, c0 + 7), exact, wfb);
         if constexpr (PARTIAL)
             if (((rem >> 5) & 1) && round == 3) store_node<2>(n5, lane, roots + (size_t)5 * kK);
@@ -424,7 +472,7 @@ __global__ __launch_bounds__(256, 4) void k_leaf2(const float* __restrict__ x, i
         wave_node_merge(st5, n5, top, lane, bit(6, c0 + 7), exact, wfb);
     }
     if constexpr (STAGE <= 2) {
-        nodes6[(size_t)tile * 64 + lane] = __uint_as_float(acc ^ mn ^ mx ^ fl);
+        nodes6[(size_t)tile * 64 + lane] = (E)(acc ^ (uint32_t)mn ^ (uint32_t)mx ^ fl);
         return;
     }
     if constexpr (!PARTIAL) {
@@ -435,18 +483,19 @@ __global__ __launch_bounds__(256, 4) void k_leaf2(const float* __restrict__ x, i
     // per-wave partial: min / max / flags (NaN keys lie outside [key(-inf), key(+inf)])
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
-        const uint32_t omn = (uint32_t)__shfl_xor((int)mn, off, 64);
-        const uint32_t omx = (uint32_t)__shfl_xor((int)mx, off, 64);
+        const Key omn = __shfl_xor(mn, off, 64);
+        const Key omx = __shfl_xor(mx, off, 64);
         const uint32_t ofl = (uint32_t)__shfl_xor((int)fl, off, 64);
         mn = omn < mn ? omn : mn;
         mx = omx > mx ? omx : mx;
         fl |= ofl;
     }
     if (lane == 0) {
-        LeafPartial p;
+        typename LeafTypes<E>::Part p;
         p.min_key = mn;
         p.max_key = mx;
-        p.flags = fl | ((mn < 0x007FFFFFu || mx > 0xFF800000u) ? 1u : 0u);
+        p.flags = fl;
+        if constexpr (std::is_same<E, float>::value) p.flags |= (mn < 0x007FFFFFu || mx > 0xFF800000u) ? 1u : 0u;
         p.pad = 0;
         part[tile] = p;  // (a single atomic accumulator instead costs ~40 us of contention)
 #ifdef SKML_PROF_LEAF
@@ -634,6 +683,20 @@ hipError_t launch_leaf(hipStream_t st, const float* x, int64_t chunks, uint64_t 
     if (chunks % kLeafWaveChunks)  // the small trees of the last chunks: one wave
         hipLaunchKernelGGL((k_leaf2<3, true>), dim3(1), dim3(64), 0, st, x, chunks, s0, jump_tab, part,
                            nodes6, roots, full);
+    return hipGetLastError();
+}
+
+// fp64 leaf: the same wave-persistent kernel over doubles (level-6 nodes and roots as doubles).
+hipError_t launch_leaf2_f64(hipStream_t st, const double* x, int64_t chunks, uint64_t s0, const uint64_t* jump_tab,
+                            LeafPartial64* part, double* nodes6, double* roots) {
+    const int64_t full = chunks / kLeafWaveChunks;
+    if (full > 0)
+        hipLaunchKernelGGL((k_leaf2<3, false, double>), dim3((unsigned)((full + kLeaf2Waves - 1) / kLeaf2Waves)),
+                           dim3(64 * kLeaf2Waves), 0, st, x, full * kLeafWaveChunks, s0, jump_tab, part, nodes6, roots,
+                           (int64_t)0);
+    if (chunks % kLeafWaveChunks)
+        hipLaunchKernelGGL((k_leaf2<3, true, double>), dim3(1), dim3(64), 0, st, x, chunks, s0, jump_tab, part, nodes6,
+                           roots, full);
     return hipGetLastError();
 }
 
