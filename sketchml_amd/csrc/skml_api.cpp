@@ -440,6 +440,58 @@ static int check_dense_args(skml_ctx* c, const void* x, int64_t n, int bins, con
 }  // extern "C"
 
 namespace {
+// Upper merge passes for the trees of bits l >= 7 of the chunk count (bit 6 is a single leaf
+// node): each pass merges up to 2^kMergeGroupLog nodes of a tree per workgroup.
+std::vector<MergePass> plan_merge_passes(int64_t chunks) {
+    std::vector<Tree> trees;
+    for (int l = kMaxLevels - 1; l > kLeafTopLevel; l--) {
+        if (!((chunks >> l) & 1)) continue;
+        Tree t;
+        t.level = l;
+        t.m = l - kLeafTopLevel;
+        t.cur_level = kLeafTopLevel;
+        t.chunk_base = (chunks >> (l + 1)) << (l + 1);
+        t.src = t.chunk_base >> kLeafTopLevel;
+        trees.push_back(t);
+    }
+    std::vector<MergePass> passes;
+    while (true) {
+        MergePass pass;
+        std::memset(&pass, 0, sizeof(pass));
+        int64_t dst_off = 0;
+        int wg = 0;
+        for (auto& t : trees) {
+            if (t.m == 0) continue;
+            const int g = t.m < kMergeGroupLog ? t.m : kMergeGroupLog;
+            MergeJob& j = pass.job[pass.njobs];
+            j.src_node = t.src;
+            j.dst_node = dst_off;
+            j.chunk_base = t.chunk_base;
+            j.level_in = t.cur_level;
+            j.group_log = g;
+            j.groups = 1 << (t.m - g);
+            j.root_level = (t.m - g == 0) ? t.level : -1;
+            pass.wg_prefix[pass.njobs] = wg;
+            wg += j.groups;
+            pass.njobs++;
+            t.src = dst_off;
+            dst_off += j.groups;
+            t.m -= g;
+            t.cur_level += g;
+        }
+        if (pass.njobs == 0) break;
+        pass.wg_prefix[pass.njobs] = wg;
+        passes.push_back(pass);
+    }
+    return passes;
+}
+// a final one-workgroup pass runs inside the previous pass's last workgroup
+bool fuse_next_pass(const std::vector<MergePass>& passes, size_t i) {
+    return i + 2 == passes.size() && passes[i + 1].wg_prefix[passes[i + 1].njobs] == 1;
+}
+}  // namespace
+
+namespace {
 // The sketch of x[0, n): leaf + upper merge passes.  summary: the last pass's last workgroup
 // also runs the summary into `payload` (returns *fused = true); otherwise the levels stay in
 // w.roots and the partials in w.part for a caller-side summary or a SketchRecord.
@@ -453,53 +505,12 @@ int run_sketch_f32(skml_ctx* c, const float* x, int64_t n, uint64_t s0, const Wo
             KernelTimer kt(c, SKML_K_LEAF);
             HIP_TRY(launch_leaf(c->stream, x, chunks, s0, c->jump_tab, w.part, w.nodes6, w.roots));
         }
-        // ---- upper trees: bits l >= 7 of chunks (bit 6 is a single leaf-workgroup node) ----
-        std::vector<Tree> trees;
-        for (int l = kMaxLevels - 1; l > kLeafTopLevel; l--) {
-            if (!((chunks >> l) & 1)) continue;
-            Tree t;
-            t.level = l;
-            t.m = l - kLeafTopLevel;
-            t.cur_level = kLeafTopLevel;
-            t.chunk_base = (chunks >> (l + 1)) << (l + 1);
-            t.src = t.chunk_base >> kLeafTopLevel;
-            trees.push_back(t);
-        }
-        std::vector<MergePass> passes;
-        while (true) {
-            MergePass pass;
-            std::memset(&pass, 0, sizeof(pass));
-            int64_t dst_off = 0;
-            int wg = 0;
-            for (auto& t : trees) {
-                if (t.m == 0) continue;
-                const int g = t.m < kMergeGroupLog ? t.m : kMergeGroupLog;
-                MergeJob& j = pass.job[pass.njobs];
-                j.src_node = t.src;
-                j.dst_node = dst_off;
-                j.chunk_base = t.chunk_base;
-                j.level_in = t.cur_level;
-                j.group_log = g;
-                j.groups = 1 << (t.m - g);
-                j.root_level = (t.m - g == 0) ? t.level : -1;
-                pass.wg_prefix[pass.njobs] = wg;
-                wg += j.groups;
-                pass.njobs++;
-                t.src = dst_off;
-                dst_off += j.groups;
-                t.m -= g;
-                t.cur_level += g;
-            }
-            if (pass.njobs == 0) break;
-            pass.wg_prefix[pass.njobs] = wg;
-            passes.push_back(pass);
-        }
+        std::vector<MergePass> passes = plan_merge_passes(chunks);
         if (summary && !passes.empty()) passes.back().fuse_summary = 1;
         const float* src = w.nodes6;
         float* dst = w.upA;
         for (size_t i = 0; i < passes.size(); i++) {
-            // a final one-workgroup pass runs inside the previous pass's last workgroup
-            const bool fuse_next = i + 2 == passes.size() && passes[i + 1].wg_prefix[passes[i + 1].njobs] == 1;
+            const bool fuse_next = fuse_next_pass(passes, i);
             float* next_dst = (dst == w.upA) ? w.upB : w.upA;
             KernelTimer kt(c, SKML_K_MERGE);
             HIP_TRY(launch_merge_pass(c->stream, passes[i], fuse_next ? &passes[i + 1] : nullptr, src, dst, next_dst,
@@ -755,27 +766,21 @@ int run_sketch_f64(skml_ctx* c, const double* x, int64_t n, uint64_t s0, const W
         KernelTimer kt(c, SKML_K_LEAF);
         HIP_TRY(launch_leaf2_f64(c->stream, x, chunks, s0, c->jump_tab, w.part, w.nodes6, w.roots));
     }
-    // trees of bits l > 6 of the chunk count: carry their level-6 nodes down to one root,
-    // up to 2^3 nodes per wave and pass
-    for (int l = kLeafTopLevel + 1; l < kMaxLevels; l++) {
-        if (!((chunks >> l) & 1)) continue;
+    // upper trees: the fp32 pass plan over double nodes (k_merge64)
+    const std::vector<MergePass> passes = plan_merge_passes(chunks);
+    Workspace wq;  // for its self-resetting arrival counter
+    if (int st = ensure_ws(c, 0, &wq)) return st;
+    const double* src = w.nodes6;
+    double* dst = w.upA;
+    for (size_t i = 0; i < passes.size(); i++) {
+        const bool fuse_next = fuse_next_pass(passes, i);
+        double* next_dst = (dst == w.upA) ? w.upB : w.upA;
         KernelTimer kt(c, SKML_K_MERGE);
-        const int64_t chunk_base = (chunks >> (l + 1)) << (l + 1);
-        const double* src = w.nodes6 + (size_t)(chunk_base >> kLeafTopLevel) * kK;
-        int64_t count = (int64_t)1 << (l - kLeafTopLevel);
-        int level = kLeafTopLevel;
-        double* dst = w.upA;
-        while (count > 1) {
-            int g = 0;
-            while (g < 3 && ((int64_t)1 << (g + 1)) <= count) g++;
-            const int64_t groups = count >> g;
-            double* out = groups == 1 ? w.roots + (size_t)l * kK : dst;
-            HIP_TRY(launch_tree64(c->stream, src, out, groups, g, level, chunk_base, s0, c->jump_tab));
-            src = out;
-            dst = (dst == w.upA) ? w.upB : w.upA;
-            count = groups;
-            level += g;
-        }
+        HIP_TRY(launch_merge_pass64(c->stream, passes[i], fuse_next ? &passes[i + 1] : nullptr, src, dst, next_dst,
+                                    w.roots, s0, c->jump_tab, wq.done));
+        src = dst;
+        dst = next_dst;
+        if (fuse_next) break;
     }
     return SKML_OK;
 }

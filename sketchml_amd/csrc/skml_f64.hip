@@ -4,14 +4,9 @@
 // DenseVectorCompressor.compressDense(double[])).  This file builds the
 // same k=128 sketch over fp64 values:
 //
-//   k_leaf64      one wave per 64-chunk tile: each 256-value chunk is bitonic-sorted by its
-//                 64-bit total-order key (Arrays.sort order, HeapQuantileSketch.java:110) across
-//                 64 lanes x 4 registers, compacted by its RNG bit (QSketchUtils.java:45-51),
-//                 then carried through a register stack of levels 0..5 exactly like
-//                 inPlacePropagationUpdate (HeapQuantileSketch.java:116-124).  Every merge is
-//                 the exact count-based merge with the reference tie rule (IEEE `<`, ties emit
-//                 the newer run, QSketchUtils.java:53-69), so +-0.0 need no special path.
-//   k_tree64      the same carry stack over level-L nodes for the trees above level 6.
+//   leaf / merge  k_leaf2<.., double> and k_merge64 in skml_sketch.hip: the fp32 leaf's layout
+//                 (8 lanes x 32 values per chunk) and merge passes over doubles, compared with
+//                 v_min/v_max_f64 (Arrays.sort order incl. -0.0 < 0.0 on gfx950).
 //   k_summary64   makeSummary + getQuantiles + Maths.unique + findZeroIdx + header
 //                 (HeapQuantileSketch.java:126-174,293-323; Maths.java:51-67; Quantizer.java:74-85).
 //   k_quantize64  Quantizer.indexOf over an LDS split table (double compares), packed codes.
@@ -42,60 +37,7 @@ __device__ __forceinline__ bool is_nan64(uint64_t b) {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 
-template <int M>
-__device__ __forceinline__ uint64_t lane_xor64(uint64_t v) {
-    const uint32_t lo = lane_xor<M>((uint32_t)v), hi = lane_xor<M>((uint32_t)(v >> 32));
-    return ((uint64_t)hi << 32) | lo;
-}
-
-// ---------------------------------------------------------------------------------------------
-// Bitonic sort of one 256-key chunk: position p = 4 * lane + r, ascending.
-// ---------------------------------------------------------------------------------------------
-template <int K, int J>
-__device__ __forceinline__ void bitonic_stage64(uint64_t (&v)[4], int lane) {
-    if constexpr (J >= 4) {
-        constexpr int M = J / 4;
-        const bool asc = ((4 * lane) & K) == 0;
-        const bool lower = (lane & M) == 0;
-        const bool keep_min = asc == lower;
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const uint64_t o = lane_xor64<M>(v[r]);
-            const uint64_t lo = v[r] < o ? v[r] : o, hi = v[r] < o ? o : v[r];
-            v[r] = keep_min ? lo : hi;
-        }
-    } else {
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            if (r & J) continue;
-            const bool asc = ((4 * lane + r) & K) == 0;
-            const uint64_t a = v[r], b = v[r + J];
-            const uint64_t lo = a < b ? a : b, hi = a < b ? b : a;
-            v[r] = asc ? lo : hi;
-            v[r + J] = asc ? hi : lo;
-        }
-    }
-}
-
-template <int K, int J>
-__device__ __forceinline__ void bitonic_merge_down64(uint64_t (&v)[4], int lane) {
-    if constexpr (J >= 1) {
-        bitonic_stage64<K, J>(v, lane);
-        bitonic_merge_down64<K, J / 2>(v, lane);
-    }
-}
-template <int K>
-__device__ __forceinline__ void bitonic_sort_from64(uint64_t (&v)[4], int lane) {
-    if constexpr (K <= 256) {
-        bitonic_merge_down64<K, K / 2>(v, lane);
-        bitonic_sort_from64<2 * K>(v, lane);
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
-// Exact merge + compaction of two register nodes (2 keys per lane, positions 2*lane + r).
-// `buf`: 384 doubles of wave-private LDS.
-// ---------------------------------------------------------------------------------------------
+// #{run[i] <= x} / #{run[i] < x} over a sorted 128-run (the record merge, k_sketch_merge64)
 __device__ __forceinline__ int count_le64(const double* run, double x) {  // #{run[i] <= x}
     int lo = 0;
 #pragma unroll
@@ -110,196 +52,6 @@ __device__ __forceinline__ int count_lt64(const double* run, double x) {  // #{r
         if (run[lo + step - 1] < x) lo += step;
     return lo + ((lo == 127 && run[127] < x) ? 1 : 0);
 }
-
-__device__ __forceinline__ void node_merge64(const uint64_t (&A)[2], const uint64_t (&B)[2],
-                                             uint64_t (&out)[2], int lane, uint32_t odd, double* buf) {
-    double* a = buf;
-    double* b = buf + kK;
-    double* o = buf + 2 * kK;
-    a[2 * lane] = kd(A[0]);
-    a[2 * lane + 1] = kd(A[1]);
-    b[2 * lane] = kd(B[0]);
-    b[2 * lane + 1] = kd(B[1]);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const int t = lane + 64 * q;
-        double v;
-        int pos;
-        if (t < kK) {  // older run: newer elements equal to it go first
-            v = a[t];
-            pos = t + count_le64(b, v);
-        } else {
-            v = b[t - kK];
-            pos = (t - kK) + count_lt64(a, v);
-        }
-        if (((uint32_t)pos & 1u) == odd) o[pos >> 1] = v;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    out[0] = dk(o[2 * lane]);
-    out[1] = dk(o[2 * lane + 1]);
-    __builtin_amdgcn_wave_barrier();
-}
-
-__device__ __forceinline__ void store_node64(const uint64_t (&w)[2], int lane, double* dst) {
-    reinterpret_cast<double2*>(dst)[lane] = make_double2(kd(w[0]), kd(w[1]));
-}
-
-// Register carry stack of levels 0..5 (two keys per lane each); indices are static.
-struct Stack64 {
-    uint64_t s[6][2];
-    __device__ __forceinline__ void get(int level, uint64_t (&o)[2]) const {
-#pragma unroll
-        for (int l = 0; l < 6; l++)
-            if (l == level) {
-                o[0] = s[l][0];
-                o[1] = s[l][1];
-            }
-    }
-    __device__ __forceinline__ void put(int level, const uint64_t (&v)[2]) {
-#pragma unroll
-        for (int l = 0; l < 6; l++)
-            if (l == level) {
-                s[l][0] = v[0];
-                s[l][1] = v[1];
-            }
-    }
-};
-
-// ---------------------------------------------------------------------------------------------
-// Leaf: one wave per 64-chunk tile (a level-6 node), chunks in order.
-// ---------------------------------------------------------------------------------------------
-constexpr int kLeaf64Waves = 4;
-
-__global__ __launch_bounds__(256) void k_leaf64(const double* __restrict__ x, int64_t chunks, uint64_t s0,
-                                                const uint64_t* __restrict__ tab,
-                                                LeafPartial64* __restrict__ part, double* __restrict__ nodes6,
-                                                double* __restrict__ roots) {
-    __shared__ double lds[kLeaf64Waves][3 * kK];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t tile = (int64_t)blockIdx.x * kLeaf64Waves + wave;
-    const int64_t c_tile = tile * kLeafChunks;
-    if (c_tile >= chunks) return;  // wave-uniform; no block barriers in this kernel
-    const int rem = (int)min<int64_t>(kLeafChunks, chunks - c_tile);
-    double* buf = lds[wave];
-    uint64_t mn = ~0ull, mx = 0ull;
-    uint32_t nanf = 0;
-    Stack64 st;
-    uint32_t occ = 0;
-    uint64_t top[2] = {0, 0};
-#pragma unroll 1
-    for (int c = 0; c < rem; c++) {
-        if ((c & 15) == 0) {  // issue priority falls with progress (fair share of the SIMD)
-            switch (c >> 4) {
-                case 0: __builtin_amdgcn_s_setprio(3); break;
-                case 1: __builtin_amdgcn_s_setprio(2); break;
-                case 2: __builtin_amdgcn_s_setprio(1); break;
-                default: __builtin_amdgcn_s_setprio(0); break;
-            }
-        }
-        const int64_t chunk = c_tile + c;
-        const double2* src = reinterpret_cast<const double2*>(x + chunk * kChunk);
-        const double2 p0 = src[2 * lane], p1 = src[2 * lane + 1];
-        uint64_t v[4] = {(uint64_t)__double_as_longlong(p0.x), (uint64_t)__double_as_longlong(p0.y),
-                         (uint64_t)__double_as_longlong(p1.x), (uint64_t)__double_as_longlong(p1.y)};
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            nanf |= is_nan64(v[r]) ? 1u : 0u;
-            v[r] = d2key(v[r]);
-            mn = v[r] < mn ? v[r] : mn;
-            mx = v[r] > mx ? v[r] : mx;
-        }
-        bitonic_sort_from64<2>(v, lane);
-        const uint32_t odd0 = lcg_bit(tab, s0, node_bit_index((uint64_t)chunk, 0));
-        uint64_t nd[2] = {odd0 ? v[1] : v[0], odd0 ? v[3] : v[2]};
-        int level = 0;
-        while ((occ >> level) & 1u) {
-            uint64_t older[2];
-            st.get(level, older);
-            const uint32_t odd = lcg_bit(tab, s0, node_bit_index((uint64_t)chunk, level + 1));
-            node_merge64(older, nd, nd, lane, odd, buf);
-            occ &= ~(1u << level);
-            level++;
-        }
-        if (level == kLeafTopLevel) {
-            top[0] = nd[0];
-            top[1] = nd[1];
-        } else {
-            st.put(level, nd);
-            occ |= 1u << level;
-        }
-    }
-    if (rem == kLeafChunks) {
-        store_node64(top, lane, nodes6 + (size_t)tile * kK);
-        // the level-6 tree (bit 6 of the chunk count) is this single node
-        if (((chunks >> 6) & 1) && tile == ((chunks >> 7) << 1)) store_node64(top, lane, roots + (size_t)6 * kK);
-    } else {
-        // the partial tile's stack holds the roots of the trees of bits 0..5 of the chunk count
-#pragma unroll
-        for (int l = 0; l < 6; l++)
-            if ((occ >> l) & 1u) store_node64(st.s[l], lane, roots + (size_t)l * kK);
-    }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const uint64_t omn = __shfl_xor(mn, off, 64), omx = __shfl_xor(mx, off, 64);
-        mn = omn < mn ? omn : mn;
-        mx = omx > mx ? omx : mx;
-        nanf |= (uint32_t)__shfl_xor((int)nanf, off, 64);
-    }
-    if (lane == 0) {
-        LeafPartial64 p;
-        p.min_key = mn;
-        p.max_key = mx;
-        p.flags = nanf;
-        p.pad = 0;
-        part[tile] = p;
-    }
-}
-
-// Upper levels: each wave carries 2^g consecutive level-L nodes into one level-(L+g) node.
-// Node i of `src` covers chunks [chunk_base + i * 2^L, chunk_base + (i + 1) * 2^L).
-__global__ __launch_bounds__(256) void k_tree64(const double* __restrict__ src, double* __restrict__ dst,
-                                                int64_t groups, int g, int level_in, int64_t chunk_base,
-                                                uint64_t s0, const uint64_t* __restrict__ tab) {
-    __shared__ double lds[kLeaf64Waves][3 * kK];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t grp = (int64_t)blockIdx.x * kLeaf64Waves + wave;
-    if (grp >= groups) return;
-    double* buf = lds[wave];
-    Stack64 st;
-    uint32_t occ = 0;
-    uint64_t top[2] = {0, 0};
-    const int cnt = 1 << g;
-#pragma unroll 1
-    for (int i = 0; i < cnt; i++) {
-        const int64_t node = grp * cnt + i;
-        const double2 d = reinterpret_cast<const double2*>(src + (size_t)node * kK)[lane];
-        uint64_t nd[2] = {dk(d.x), dk(d.y)};
-        const uint64_t c_last = (uint64_t)chunk_base + ((uint64_t)(node + 1) << level_in) - 1;
-        int level = 0;
-        while ((occ >> level) & 1u) {
-            uint64_t older[2];
-            st.get(level, older);
-            const uint32_t odd = lcg_bit(tab, s0, node_bit_index(c_last, level_in + level + 1));
-            node_merge64(older, nd, nd, lane, odd, buf);
-            occ &= ~(1u << level);
-            level++;
-        }
-        if (level == g) {
-            top[0] = nd[0];
-            top[1] = nd[1];
-        } else {
-            st.put(level, nd);
-            occ |= 1u << level;
-        }
-    }
-    store_node64(top, lane, dst + (size_t)grp * kK);
-}
-
 // ---------------------------------------------------------------------------------------------
 // Summary (one workgroup of 512 threads, dynamic LDS).
 // ---------------------------------------------------------------------------------------------
@@ -1011,22 +763,6 @@ __global__ __launch_bounds__(256) void k_uni_finish(const T* __restrict__ x, int
 // ---------------------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------------------
-hipError_t launch_leaf64(hipStream_t st, const double* x, int64_t chunks, uint64_t s0, const uint64_t* tab,
-                         LeafPartial64* part, double* nodes6, double* roots) {
-    const int64_t tiles = (chunks + kLeafChunks - 1) / kLeafChunks;
-    if (tiles == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_leaf64, dim3((unsigned)((tiles + kLeaf64Waves - 1) / kLeaf64Waves)), dim3(256), 0, st,
-                       x, chunks, s0, tab, part, nodes6, roots);
-    return hipGetLastError();
-}
-
-hipError_t launch_tree64(hipStream_t st, const double* src, double* dst, int64_t groups, int g, int level_in,
-                         int64_t chunk_base, uint64_t s0, const uint64_t* tab) {
-    hipLaunchKernelGGL(k_tree64, dim3((unsigned)((groups + kLeaf64Waves - 1) / kLeaf64Waves)), dim3(256), 0, st,
-                       src, dst, groups, g, level_in, chunk_base, s0, tab);
-    return hipGetLastError();
-}
-
 hipError_t launch_summary64(hipStream_t st, const double* x, int64_t n, const LeafPartial64* part, int64_t nparts,
                             const double* roots, const int64_t* ranks, int req_bins, int dedup, void* payload,
                             double* g_raw, QuantLut* lut, const double* tail, int sharded, int64_t n_local) {

@@ -120,6 +120,10 @@ hipError_t launch_leaf(hipStream_t st, const float* x, int64_t chunks, uint64_t 
                        const uint64_t* jump_tab, LeafPartial* part, float* nodes6, float* roots);
 hipError_t launch_leaf_stage(hipStream_t st, int stage, const float* x, int64_t chunks, uint64_t s0,
                              const uint64_t* jump_tab, LeafPartial* part, float* scratch, float* roots);
+// fp64 merge pass over double nodes (no summary; `next` as in launch_merge_pass).
+hipError_t launch_merge_pass64(hipStream_t st, const MergePass& pass, const MergePass* next, const double* src,
+                               double* dst, double* next_dst, double* roots, uint64_t s0, const uint64_t* jump_tab,
+                               unsigned* done);
 // Slice sketch -> record (after the leaf and the merge passes without a summary).
 hipError_t launch_sketch_record(hipStream_t st, const float* x, int64_t n, const LeafPartial* part, int64_t nparts,
                                 const float* roots, SketchRecord* rec);
@@ -154,10 +158,6 @@ hipError_t launch_bins(hipStream_t st, const void* payload, int32_t* bins, int64
 hipError_t launch_ref_body(hipStream_t st, const void* payload, uint8_t* out, int64_t n, int width);
 hipError_t launch_times_by(hipStream_t st, void* payload, double x);
 // ---- kernel launchers (skml_f64.hip) ----
-hipError_t launch_leaf64(hipStream_t st, const double* x, int64_t chunks, uint64_t s0, const uint64_t* tab,
-                         LeafPartial64* part, double* nodes6, double* roots);
-hipError_t launch_tree64(hipStream_t st, const double* src, double* dst, int64_t groups, int g, int level_in,
-                         int64_t chunk_base, uint64_t s0, const uint64_t* tab);
 hipError_t launch_summary64(hipStream_t st, const double* x, int64_t n, const LeafPartial64* part, int64_t nparts,
                             const double* roots, const int64_t* ranks, int req_bins, int dedup, void* payload,
                             double* g_raw, QuantLut* lut,

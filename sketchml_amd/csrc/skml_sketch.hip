@@ -48,19 +48,21 @@ __device__ unsigned long long g_leafprof[4 * 65536];
 // =============================================================================================
 // shared memory
 // =============================================================================================
-constexpr int kWaveFb = 1536;  // per-wave exact-merge area, floats
-struct TileShared {
-    float fb[kLeafWaves][kWaveFb];  // per-wave exact-merge area (mixed +/-0 only)
-    float wn[kLeafWaves][kK];    // level L0+3 node of each wave
-    float l4[4][kK];
-    float l5[2][kK];
-    float l6[kK];
+constexpr int kWaveFb = 1536;  // per-wave exact-merge area, elements
+template <typename S>
+struct TileSharedT {
+    S fb[kLeafWaves][kWaveFb];  // per-wave exact-merge area (mixed +/-0 only)
+    S wn[kLeafWaves][kK];       // level L0+3 node of each wave
+    S l4[4][kK];
+    S l5[2][kK];
+    S l6[kK];
     uint64_t mask[kLeafWaves];   // leaf: RNG draws [start, start+64) of each wave's chunks
     uint64_t start[kLeafWaves];
     uint32_t wgbits;             // bits of the 7 cross-wave merges
     uint32_t min_key, max_key, flags;
     int is_last;
 };
+using TileShared = TileSharedT<float>;
 
 constexpr int kSumMaxRaw = 1024;  // raw splits kept in LDS up to this many
 constexpr int kMaxSamples = kMaxLevels * kK + kChunk;
@@ -177,10 +179,11 @@ __device__ __forceinline__ void wave_pair_merge(const S* A, const S* B, S* out, 
 }
 
 // Levels +4..+6 across the 8 waves.  bits: 0..3 level+4, 4..5 level+5, 6 level+6.
-__device__ __forceinline__ void crosswave_levels(TileShared& sh, int tid, uint32_t bits, bool exact) {
+template <typename T = uint32_t, typename S = typename Elem<T>::S>
+__device__ __forceinline__ void crosswave_levels(TileSharedT<S>& sh, int tid, uint32_t bits, bool exact) {
     const int wave = tid >> 6, lane = tid & 63;
     if (!exact) {
-        if (wave < 4) wave_pair_merge(sh.wn[2 * wave], sh.wn[2 * wave + 1], sh.l4[wave], lane, (bits >> wave) & 1u);
+        if (wave < 4) wave_pair_merge<T>(sh.wn[2 * wave], sh.wn[2 * wave + 1], sh.l4[wave], lane, (bits >> wave) & 1u);
     } else {
         for (int task = tid; task < 4 * 256; task += 512) {
             const int m = task >> 8;
@@ -189,14 +192,14 @@ __device__ __forceinline__ void crosswave_levels(TileShared& sh, int tid, uint32
     }
     __syncthreads();
     if (!exact) {
-        if (wave < 2) wave_pair_merge(sh.l4[2 * wave], sh.l4[2 * wave + 1], sh.l5[wave], lane, (bits >> (4 + wave)) & 1u);
+        if (wave < 2) wave_pair_merge<T>(sh.l4[2 * wave], sh.l4[2 * wave + 1], sh.l5[wave], lane, (bits >> (4 + wave)) & 1u);
     } else {
         const int m = tid >> 8;
         exact_merge_task(sh.l4[2 * m], sh.l4[2 * m + 1], sh.l5[m], tid & 255, (bits >> (4 + m)) & 1u);
     }
     __syncthreads();
     if (!exact) {
-        if (wave == 0) wave_pair_merge(sh.l5[0], sh.l5[1], sh.l6, lane, (bits >> 6) & 1u);
+        if (wave == 0) wave_pair_merge<T>(sh.l5[0], sh.l5[1], sh.l6, lane, (bits >> 6) & 1u);
     } else if (tid < 256) {
         exact_merge_task(sh.l5[0], sh.l5[1], sh.l6, tid, (bits >> 6) & 1u);
     }
@@ -1053,9 +1056,10 @@ hipError_t launch_summary(hipStream_t st, const float* x, int64_t n, const LeafP
 // Input nodes are placed like leaf chunks (8 per wave, 8 lanes x 16 keys per node); missing
 // nodes (g < 6) are padding whose merges are never exported.
 // =============================================================================================
+template <typename S = float>
 struct MergeExport {
     int lane, wave, g;
-    float* out;
+    S* out;
     template <int R, typename T>
     __device__ __forceinline__ void at(int level, int node, const T (&w)[R]) const {
         if (level == g && wave == 0 && node == 0) store_node<R>(w, lane, out);
@@ -1063,9 +1067,12 @@ struct MergeExport {
 };
 
 // One workgroup's share of a merge pass: 2^g consecutive level-L nodes of one tree -> one node.
-__device__ __forceinline__ void merge_group_wg(const MergePass& pass, int wg, const float* __restrict__ src,
-                                               float* __restrict__ dst, float* __restrict__ roots, uint64_t s0,
-                                               const uint64_t* __restrict__ tab, TileShared& sh) {
+// E = float: nodes sorted as total-order keys; E = double: as doubles (v_min/v_max_f64).
+template <typename E = float>
+__device__ __forceinline__ void merge_group_wg(const MergePass& pass, int wg, const E* __restrict__ src,
+                                               E* __restrict__ dst, E* __restrict__ roots, uint64_t s0,
+                                               const uint64_t* __restrict__ tab, TileSharedT<E>& sh) {
+    using T = typename std::conditional<std::is_same<E, double>::value, double, uint32_t>::type;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     int j = 0;
     while (j + 1 < pass.njobs && wg >= pass.wg_prefix[j + 1]) j++;
@@ -1075,19 +1082,31 @@ __device__ __forceinline__ void merge_group_wg(const MergePass& pass, int wg, co
     const int nodes = 1 << g;
     const int64_t node0 = job.src_node + ((int64_t)grp << g);
     const int64_t chunk0 = job.chunk_base + ((int64_t)grp << (g + L));
-    float* out = job.root_level >= 0 ? roots + (size_t)job.root_level * kK
-                                     : dst + (size_t)(job.dst_node + grp) * kK;
+    E* out = job.root_level >= 0 ? roots + (size_t)job.root_level * kK : dst + (size_t)(job.dst_node + grp) * kK;
     if (tid == 0) sh.flags = 0u;
     __syncthreads();
 
     // ---- load: node nd = 8*wave + lane/8, 16 floats per lane ----
     const int nd = wave * 8 + (lane >> 3);
     const bool valid = nd < nodes;
-    uint32_t w1[16];
+    T w1[16];
     uint32_t fl = 0;
-    {
-        const float4* p = reinterpret_cast<const float4*>(src + (size_t)(node0 + (valid ? nd : 0)) * kK) +
-                          (lane & 7) * 4;
+    if constexpr (std::is_same<E, double>::value) {
+        const double2* p = reinterpret_cast<const double2*>(src + (size_t)(node0 + (valid ? nd : 0)) * kK) + (lane & 7) * 8;
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const double2 f = p[q];
+            const double e2[2] = {f.x, f.y};
+#pragma unroll
+            for (int e = 0; e < 2; e++) {
+                const uint64_t b = (uint64_t)__double_as_longlong(e2[e]);
+                fl |= (b == 0x8000000000000000ull) ? 2u : 0u;
+                fl |= (b == 0ull) ? 4u : 0u;
+                w1[q * 2 + e] = e2[e];  // padding nodes (g < 6) never meet a real node
+            }
+        }
+    } else {
+        const float4* p = reinterpret_cast<const float4*>(src + (size_t)(node0 + (valid ? nd : 0)) * kK) + (lane & 7) * 4;
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             const float4 f = p[q];
@@ -1100,8 +1119,8 @@ __device__ __forceinline__ void merge_group_wg(const MergePass& pass, int wg, co
                 w1[q * 4 + e] = valid ? f2key(b[e]) : 0xFFFFFFFFu;
             }
         }
-        if (!valid) fl = 0;
     }
+    if (!valid) fl = 0;
     // ---- RNG bits: lane k < 7 computes one in-wave merge bit; wave 0 also the 7 cross-wave ones ----
     auto node_bit = [&](int level_off, int last_node) -> uint32_t {
         const uint64_t c = (uint64_t)chunk0 + ((uint64_t)(last_node + 1) << L) - 1;
@@ -1122,13 +1141,13 @@ __device__ __forceinline__ void merge_group_wg(const MergePass& pass, int wg, co
     }
     if (fl) atomicOr(&sh.flags, fl);
     const bool wexact = (__ballot((fl & 2u) != 0) != 0) && (__ballot((fl & 4u) != 0) != 0);
-    const MergeExport exp{lane, wave, g, out};
-    uint32_t w4[2];
+    const MergeExport<E> exp{lane, wave, g, out};
+    T w4[2];
     inwave_levels(w1, w4, lane, ibits, wexact, sh.fb[wave], exp);
     store_node<2>(w4, lane, sh.wn[wave]);
     __syncthreads();
     if (g >= 4) {
-        crosswave_levels(sh, tid, sh.wgbits, (sh.flags & 6u) == 6u);
+        crosswave_levels<T>(sh, tid, sh.wgbits, (sh.flags & 6u) == 6u);
         if (tid < kK) out[tid] = g == 4 ? sh.l4[0][tid] : (g == 5 ? sh.l5[0][tid] : sh.l6[tid]);
     }
 }
@@ -1194,6 +1213,50 @@ hipError_t launch_merge_pass(hipStream_t st, const MergePass& pass, const MergeP
     }
     hipLaunchKernelGGL(k_merge, dim3(nwg), dim3(512), 0, st, pass, *next, src, dst, next_dst, roots, s0, jump_tab,
                        done, a);
+    return hipGetLastError();
+}
+
+// fp64 merge pass (no fused summary: k_summary64 follows); `next` as in k_merge.
+__global__ __launch_bounds__(512) void k_merge64(MergePass pass, MergePass next, const double* __restrict__ src,
+                                                 double* __restrict__ dst, double* __restrict__ next_dst,
+                                                 double* __restrict__ roots, uint64_t s0,
+                                                 const uint64_t* __restrict__ tab, unsigned* __restrict__ done) {
+    __shared__ TileSharedT<double> T64;
+    const int tid = threadIdx.x;
+    merge_group_wg<double>(pass, (int)blockIdx.x, src, dst, roots, s0, tab, T64);
+    if (next.njobs == 0) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned old = atomicAdd(done, 1u);
+        const int last = old == (unsigned)(pass.wg_prefix[pass.njobs] - 1);
+        if (last) {
+            *done = 0u;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        T64.is_last = last;
+    }
+    __syncthreads();
+    if (!T64.is_last) return;
+    __syncthreads();
+    merge_group_wg<double>(next, 0, dst, next_dst, roots, s0, tab, T64);
+}
+
+hipError_t launch_merge_pass64(hipStream_t st, const MergePass& pass, const MergePass* next, const double* src,
+                               double* dst, double* next_dst, double* roots, uint64_t s0, const uint64_t* jump_tab,
+                               unsigned* done) {
+    const int nwg = pass.wg_prefix[pass.njobs];
+    if (nwg <= 0) return hipSuccess;
+    MergePass none;
+    if (!next) {
+        std::memset(&none, 0, sizeof(none));
+        next = &none;
+    }
+    hipLaunchKernelGGL(k_merge64, dim3(nwg), dim3(512), 0, st, pass, *next, src, dst, next_dst, roots, s0, jump_tab,
+                       done);
     return hipGetLastError();
 }
 
