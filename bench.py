@@ -34,8 +34,8 @@ KNAMES = {0: "k_leaf", 1: "k_merge", 2: "k_summary", 3: "k_quantize", 4: "k_deco
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--n", type=int, default=2**26, help="floats per GPU bucket")
     ap.add_argument("--bins", type=int, default=256)
     ap.add_argument("--buffers", type=int, default=4,
