@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip decode / H2D measurements")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the fp64 and C3 sparse measurements reported under extras.other_configs")
     return ap.parse_args()
 
 
@@ -114,6 +116,54 @@ def cpu_baseline(x_host, bins, budget_s):
     return {"value": round(gbs, 4), "unit": "GB/s", "cores": 1, "kind": "port",
             "sample": f"first 2^22 floats of the bucket, {reps} encode(s), {t:.1f} s",
             "cpu": _cpu_model()}
+
+
+def other_configs(sk, lib, ctx, dev, x32):
+    """The reference's other dense / sparse configurations at one GPU, each timed over a few
+    synchronised repetitions (not part of `value`): the fp64 path on the same bucket (the
+    reference's double[] itself) and the C3 sparse path (2^28-dim dense, 10 % nnz)."""
+    out = {}
+
+    def timed(fn, reps):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            r = fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / reps, r
+
+    n = x32.numel()
+    x64 = x32.double()
+    nb = lib.skml_dense_payload_bytes(n, 256)
+    pl = sk.alloc_aligned(nb, dev)
+    p = _lib_params(256)
+    t64, _ = timed(lambda: lib.skml_dense_encode_f64(ctx, C.c_void_p(x64.data_ptr()), n, C.byref(p),
+                                                      C.c_void_p(pl.data_ptr()), nb), 20)
+    out["fp64_encode"] = {"workload": "C2 bucket as fp64 (2^26 doubles), 256 bins", "ms": round(t64 * 1e3, 4),
+                          "gbps_fp64_in": round(8.0 * n / t64 / 1e9, 1)}
+    del x64, pl
+    dim = 2**28
+    g = torch.Generator(device=dev).manual_seed(3)
+    d = torch.randn(dim, device=dev, generator=g)
+    d[torch.rand(dim, device=dev, generator=g) >= 0.1] = 0.0
+    te, spl = timed(lambda: sk.encode_dense_as_sparse(d, 256, 8, 2, 0.3, 3, 3), 3)
+    td, (rk, rv) = timed(lambda: spl.restore(), 3)
+    nnz = int(rk.numel())
+    alg = (4.0 + nnz / dim * (8 + 4 + 8 + 2)) * dim
+    out["sparse_c3"] = {"workload": "C3: 2^28-dim dense fp32, 10 % nnz, 256 bins, 8 groups, 2 rows, colRatio 0.3",
+                        "nnz": nnz, "encode_ms": round(te * 1e3, 3), "gbps_dense_in": round(4.0 * dim / te / 1e9, 1),
+                        "roofline_frac": round(alg / te / 1e9 / HBM_PEAK_GBS, 4), "restore_ms": round(td * 1e3, 3),
+                        "note": "wall time of synchronising calls (host reads group sizes between passes)"}
+    return out
+
+
+def _lib_params(bins):
+    from sketchml_amd import _lib
+    p = _lib.Params()
+    _lib.lib.skml_params_default(C.byref(p))
+    p.bin_num = bins
+    return p
 
 
 def _cpu_model():
@@ -316,6 +366,10 @@ def main():
         extras["allgather"] = {"ms": round(tag * 1e3, 3), "bytes_per_rank": nb, "algbw_gbs": round(algbw, 1),
                                "busbw_gbs": round(algbw * (world - 1) / world, 1),
                                "decode_sum_max_abs_err_vs_allreduce": err}
+
+    if (rank == 0 and world == 1 and not args.no_extras and not args.no_configs and args.quant == "quantile"
+            and args.dtype == "f32" and args.n == 2**26):
+        extras["other_configs"] = other_configs(sk, lib, ctx, dev, xs[0])
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.quant == "quantile" and args.dtype == "f32":

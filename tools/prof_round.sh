@@ -9,7 +9,7 @@ cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats" -o run --output-format csv \
-    -- python3 bench.py --no-cpu-baseline --steps 20 > "$OUT/bench_under_rocprof.json" 2> "$OUT/stats.log"
+    -- python3 bench.py --no-cpu-baseline --no-configs --steps 20 > "$OUT/bench_under_rocprof.json" 2> "$OUT/stats.log"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv \
     -- python3 bench.py --no-cpu-baseline --no-extras --steps 10 > "$OUT/fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv \
