@@ -1084,22 +1084,40 @@ __global__ __launch_bounds__(kSpThreads) void k_dec_keys(const uint32_t* __restr
     if (i0 >= n) return;
     uint64_t p = tile_base[blockIdx.x] + v[0];
     const int zero = gp->zero, rows = gp->rows;
+    // keys and groups of the 8 elements first, then per row 8 independent table gathers in
+    // flight (the gathers are random 4-byte reads: latency, not bandwidth, bounds this kernel)
+    int32_t key[8], res[8];
+    int grp[8];
     int g = group_of_elem(S, i0);
+#pragma unroll
     for (int j = 0; j < 8; j++) {
         const int64_t i = i0 + j;
-        if (i >= n) break;
-        while (i >= S[g + 1]) g++;
+        if (i < n)
+            while (i >= S[g + 1]) g++;
         p += d[j];
-        const int32_t key = (int32_t)(uint32_t)(p - gpre[g]);
-        const int32_t cols = gp->cols[g];
-        const double inv = gp->inv_cols[g];
-        int32_t res = zero;
-        for (int r = 0; r < rows; r++) {
-            const int32_t tv = table[gp->tab_off[g] + (int64_t)r * cols + java_hash_fm(gp->hash_ids[g][r], key, cols, inv)];
-            if ((int32_t)((uint32_t)mm_dist(tv, zero) - (uint32_t)mm_dist(res, zero)) > 0) res = tv;
+        grp[j] = g;
+        key[j] = (int32_t)(uint32_t)(p - gpre[g]);
+        res[j] = zero;
+    }
+    for (int r = 0; r < rows; r++) {
+        int32_t tv[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int gj = grp[j];
+            const int32_t cols = gp->cols[gj];
+            tv[j] = i0 + j < n ? table[gp->tab_off[gj] + (int64_t)r * cols +
+                                       java_hash_fm(gp->hash_ids[gj][r], key[j], cols, gp->inv_cols[gj])]
+                               : zero;
         }
-        gkeys[i] = key;
-        gbins[i] = res;
+#pragma unroll
+        for (int j = 0; j < 8; j++)  // MinMaxSketch.query: the strictly farther value wins, ties keep the earlier row
+            if ((int32_t)((uint32_t)mm_dist(tv[j], zero) - (uint32_t)mm_dist(res[j], zero)) > 0) res[j] = tv[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        if (i0 + j >= n) break;
+        gkeys[i0 + j] = key[j];
+        gbins[i0 + j] = res[j];
     }
 }
 
