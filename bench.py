@@ -118,7 +118,7 @@ def cpu_baseline(x_host, bins, budget_s):
             "cpu": _cpu_model()}
 
 
-def other_configs(sk, lib, ctx, dev, x32):
+def other_configs(sk, lib, ctx, dev, xs):
     """The reference's other dense / sparse configurations at one GPU, each timed over a few
     synchronised repetitions (not part of `value`): the fp64 path on the same bucket (the
     reference's double[] itself) and the C3 sparse path (2^28-dim dense, 10 % nnz)."""
@@ -133,6 +133,7 @@ def other_configs(sk, lib, ctx, dev, x32):
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / reps, r
 
+    x32 = xs[0]
     n = x32.numel()
     x64 = x32.double()
     nb = lib.skml_dense_payload_bytes(n, 256)
@@ -143,6 +144,18 @@ def other_configs(sk, lib, ctx, dev, x32):
     out["fp64_encode"] = {"workload": "C2 bucket as fp64 (2^26 doubles), 256 bins", "ms": round(t64 * 1e3, 4),
                           "gbps_fp64_in": round(8.0 * n / t64 / 1e9, 1)}
     del x64, pl
+    # several independent buckets per call (skml_dense_encode_batch_f32: two streams, so one
+    # bucket's VALU-bound sketch overlaps the previous bucket's HBM-bound quantize)
+    nbk = 8
+    pls = [sk.alloc_aligned(nb, dev) for _ in range(nbk)]
+    ptrs = (C.c_void_p * nbk)(*[xs[i % len(xs)].data_ptr() for i in range(nbk)])
+    pptr = (C.c_void_p * nbk)(*[q.data_ptr() for q in pls])
+    ns = (C.c_int64 * nbk)(*([n] * nbk))
+    caps = (C.c_size_t * nbk)(*([nb] * nbk))
+    tb, _ = timed(lambda: lib.skml_dense_encode_batch_f32(ctx, nbk, ptrs, ns, C.byref(p), pptr, caps), 10)
+    out["batched_buckets"] = {"workload": f"{nbk} independent 2^26-float buckets per call, 256 bins",
+                              "ms_per_bucket": round(tb / nbk * 1e3, 4), "gbps": round(4.0 * n * nbk / tb / 1e9, 1)}
+    del pls
     dim = 2**28
     g = torch.Generator(device=dev).manual_seed(3)
     d = torch.randn(dim, device=dev, generator=g)
@@ -369,7 +382,7 @@ def main():
 
     if (rank == 0 and world == 1 and not args.no_extras and not args.no_configs and args.quant == "quantile"
             and args.dtype == "f32" and args.n == 2**26):
-        extras["other_configs"] = other_configs(sk, lib, ctx, dev, xs[0])
+        extras["other_configs"] = other_configs(sk, lib, ctx, dev, xs)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.quant == "quantile" and args.dtype == "f32":

@@ -141,6 +141,14 @@ int skml_dense_encode_uniform_f32(skml_ctx* ctx, const float* x_dev, int64_t n,
 int skml_dense_encode_uniform_f64(skml_ctx* ctx, const double* x_dev, int64_t n,
                                   const skml_params* params, void* payload_dev, size_t payload_cap);
 
+/* Several independent buckets (QuantileQuantizer.quantize of each, e.g. the gradient buckets of
+ * one DDP step): results identical to skml_dense_encode_f32 per bucket.  The buckets run on two
+ * internal streams so that one bucket's sketch (VALU-bound) overlaps the previous bucket's
+ * quantize pass (HBM-bound).  xs / ns / payloads / caps: host arrays of nbuckets entries
+ * (device pointers).  Ordered after, and waited for by, the context's stream.  Asynchronous. */
+int skml_dense_encode_batch_f32(skml_ctx* ctx, int32_t nbuckets, const float* const* xs_dev, const int64_t* ns,
+                                const skml_params* params, void* const* payloads_dev, const size_t* payload_caps);
+
 /* QuantileQuantizer.parallelQuantize (QuantileQuantizer.java:53-92) with `threads` slices
  * (Constants.Parallel.getParallelism): slice t = [t*(n/T), ...), the last slice takes the
  * remainder; each slice is sketched, the sketches merged in slice order (HeapQuantileSketch.merge,

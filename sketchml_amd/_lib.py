@@ -78,6 +78,8 @@ _SIGS = {
     "skml_dense_encode_f64": (C.c_int, [vp, vp, i64, C.POINTER(Params), vp, C.c_size_t]),
     "skml_dense_encode_uniform_f32": (C.c_int, [vp, vp, i64, C.POINTER(Params), vp, C.c_size_t]),
     "skml_dense_encode_parallel_f32": (C.c_int, [vp, vp, i64, i32, C.POINTER(Params), vp, C.c_size_t]),
+    "skml_dense_encode_batch_f32": (C.c_int, [vp, i32, C.POINTER(vp), i64p, C.POINTER(Params), C.POINTER(vp),
+                                              C.POINTER(C.c_size_t)]),
     "skml_sketch_record_bytes": (C.c_size_t, [i32]),
     "skml_dense_encode_parallel_f64": (C.c_int, [vp, vp, i64, i32, C.POINTER(Params), vp, C.c_size_t]),
     "skml_dense_sketch_shard_f64": (C.c_int, [vp, vp, i64, i64p, i32, i32, i64, vp]),

@@ -59,6 +59,10 @@ struct skml_ctx {
     size_t ranks_cap = 0;
     int64_t ranks_n = -1;
     int ranks_bins = -1;
+    // batched encode: a child context (own high-priority stream and workspace) and its events
+    skml_ctx* side = nullptr;
+    hipEvent_t ev_join = nullptr, ev_leaf = nullptr;
+    hipEvent_t after_leaf = nullptr;  // when set, recorded right after the next leaf launch
     // parallelQuantize: slice records + the merged sketch's export (grow-only)
     void* sk = nullptr;
     size_t sk_cap = 0;
@@ -333,6 +337,9 @@ int skml_ctx_destroy(skml_ctx* c) {
     if (c->ws64) (void)hipFree(c->ws64);
     if (c->ranks) (void)hipFree(c->ranks);
     if (c->stage) (void)hipFree(c->stage);
+    if (c->side) skml_ctx_destroy(c->side);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+    if (c->ev_leaf) (void)hipEventDestroy(c->ev_leaf);
     if (c->sk) (void)hipFree(c->sk);
     for (int k = 0; k < SKML_K_COUNT; k++)
         for (hipEvent_t e : c->ev[k]) (void)hipEventDestroy(e);
@@ -504,6 +511,10 @@ int run_sketch_f32(skml_ctx* c, const float* x, int64_t n, uint64_t s0, const Wo
         {
             KernelTimer kt(c, SKML_K_LEAF);
             HIP_TRY(launch_leaf(c->stream, x, chunks, s0, c->jump_tab, w.part, w.nodes6, w.roots));
+        }
+        if (c->after_leaf) {
+            HIP_TRY(hipEventRecord(c->after_leaf, c->stream));
+            c->after_leaf = nullptr;
         }
         std::vector<MergePass> passes = plan_merge_passes(chunks);
         if (summary && !passes.empty()) passes.back().fuse_summary = 1;
@@ -734,6 +745,68 @@ int skml_dense_encode_parallel_f32(skml_ctx* c, const float* x, int64_t n, int32
     return merge_and_quantize(c, x, n, sk.recs, threads, n, skip, p, payload, sk);
 }
 
+
+// Independent buckets, alternately on the caller's stream and a side stream: bucket i+1's
+// VALU-bound leaf runs beside bucket i's HBM-bound quantize pass (and its latency-bound merge),
+// which a single stream serialises.  Ordered after earlier work on ctx's stream; ctx's stream
+// waits for all buckets.  (Forking both lanes off the caller's stream with events measured no
+// overlap at all when that stream is the legacy null stream.)
+int skml_dense_encode_batch_f32(skml_ctx* c, int32_t nbuckets, const float* const* xs, const int64_t* ns,
+                                const skml_params* p, void* const* payloads, const size_t* caps) {
+    if (!c) return fail(SKML_E_ARG, "ctx is NULL");
+    if (nbuckets < 0 || (nbuckets > 0 && (!xs || !ns || !payloads || !caps)))
+        return fail(SKML_E_ARG, "bad bucket arrays (nbuckets=%d)", nbuckets);
+    if (nbuckets == 0) return SKML_OK;
+    skml_params def;
+    if (!p) {
+        skml_params_default(&def);
+        p = &def;
+    }
+    for (int i = 0; i < nbuckets; i++) {
+        int st = check_dense_args(c, xs[i], ns[i], p->bin_num, payloads[i], caps[i]);
+        if (st) return st;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    if (nbuckets == 1) return skml_dense_encode_f32(c, xs[0], ns[0], p, payloads[0], caps[0]);
+    // Lane 0 is the caller's stream itself; lane 1 is a child context on its own stream, created
+    // at high priority: HIP keeps hardware queues per priority, so the two never share a queue
+    // (with GPU_MAX_HW_QUEUES = 4, a normal-priority stream created after the framework's own
+    // streams was measured to share one and serialise the lanes).
+    if (!c->side) {
+        int lo = 0, hi = 0;
+        HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        hipStream_t s = nullptr;
+        HIP_TRY(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, hi));
+        int st = skml_ctx_create(c->device, s, &c->side);
+        if (st) {
+            (void)hipStreamDestroy(s);
+            return st;
+        }
+        c->side->own_stream = true;
+        HIP_TRY(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+    }
+    if (!c->ev_leaf) HIP_TRY(hipEventCreateWithFlags(&c->ev_leaf, hipEventDisableTiming));
+    skml_ctx* lane[2] = {c, c->side};
+    // lane 1 starts when bucket 0's sketch pass is done (which also orders it after earlier work
+    // on the caller's stream), so the lanes stay half a bucket apart: each lane's leaf runs
+    // beside the other lane's merge and quantize
+    c->after_leaf = c->ev_leaf;
+    for (int i = 0; i < nbuckets; i++) {
+        if (i == 1) HIP_TRY(hipStreamWaitEvent(lane[1]->stream, c->ev_leaf, 0));
+        int st = skml_dense_encode_f32(lane[i & 1], xs[i], ns[i], p, payloads[i], caps[i]);
+        if (st) {
+            c->after_leaf = nullptr;
+            return st;
+        }
+        if (i == 0 && c->after_leaf) {  // bucket 0 had no leaf (n < 256): order lane 1 after it
+            c->after_leaf = nullptr;
+            HIP_TRY(hipEventRecord(c->ev_leaf, c->stream));
+        }
+    }
+    HIP_TRY(hipEventRecord(c->ev_join, c->side->stream));
+    HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_join, 0));
+    return SKML_OK;
+}
 
 int skml_dense_encode_with_splits_f32(skml_ctx* c, const float* x, int64_t n, const double* splits,
                                       int32_t nsplits, double mn, double mx, void* payload,

@@ -290,6 +290,44 @@ class QuantileQuantizer(Quantizer):
     def quantizationType(self) -> QuantizationType:
         return QuantizationType.QUANTILE
 
+    @classmethod
+    def quantizeBuckets(cls, buckets, binNum: int = Quantizer.DEFAULT_BIN_NUM, seed: int = 0) -> list:
+        """QuantileQuantizer.quantize of each of several independent buckets (e.g. the gradient
+        buckets of one step), identical per bucket to quantize(); fp32 buckets are encoded by
+        skml_dense_encode_batch_f32, which overlaps one bucket's sketch with the previous
+        bucket's quantize pass on two streams."""
+        xs = [as_device_values(b) for b in buckets]
+        qs = [cls(binNum, seed) for _ in xs]
+        if not xs:
+            return qs
+        if any(x.dtype != torch.float32 for x in xs) or len({x.device for x in xs}) != 1:
+            for q, x in zip(qs, xs):
+                q.quantize(x)
+            return qs
+        p = _lib.Params()
+        _lib.lib.skml_params_default(C.byref(p))
+        p.bin_num = int(binNum)
+        p.seed = int(seed)
+        p.dedup = 1
+        nb = len(xs)
+        ptrs = (C.c_void_p * nb)()
+        pls = (C.c_void_p * nb)()
+        ns = np.zeros(nb, dtype=np.int64)
+        caps = (C.c_size_t * nb)()
+        for i, (q, x) in enumerate(zip(qs, xs)):
+            q.device, q.n, q._wide = x.device, x.numel(), False
+            cap = _lib.lib.skml_dense_payload_bytes(q.n, q.binNum)
+            if cap == 0:
+                raise SketchMLException(f"bad quantizer arguments n={q.n} binNum={q.binNum}")
+            q.payload = alloc_aligned(cap, x.device)
+            ptrs[i], pls[i], ns[i], caps[i] = x.data_ptr(), q.payload.data_ptr(), q.n, cap
+        st = _lib.lib.skml_dense_encode_batch_f32(qs[0]._ctx().handle, nb, ptrs, ns.ctypes.data_as(_lib.i64p),
+                                                  C.byref(p), pls, caps)
+        check(st, "quantize")
+        for q in qs:
+            q._load_header()  # synchronises; surfaces NaN as QuantileSketchException
+        return qs
+
 
 class UniformQuantizer(Quantizer):
     """quantization/UniformQuantizer.java:14-76 on the GPU: bin_num equal-width bins between the

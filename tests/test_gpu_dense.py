@@ -320,3 +320,29 @@ def test_dense_vector_compressor_surface(gpu):
     assert keys.numel() == 12345 and torch.equal(vals.cpu(), torch.from_numpy(dec))
     assert comp.size() == 12345.0
     assert comp.memoryBytes() == 12 + len(oq.write_ref())
+
+
+@pytest.mark.parametrize("sizes", [[2**20, 2**20 + 77, 3, 300000, 2**21], [2**22, 2**22]])
+def test_quantize_buckets_matches_single_encodes(gpu, sizes):
+    """skml_dense_encode_batch_f32 (two internal streams) == skml_dense_encode_f32 per bucket."""
+    xs = [torch.from_numpy(_data(n, 40 + i, "normal")).cuda() for i, n in enumerate(sizes)]
+    qs = gpu.QuantileQuantizer.quantizeBuckets(xs, 256, seed=3)
+    for x, q in zip(xs, qs):
+        one = gpu.QuantileQuantizer(256, seed=3)
+        one.quantize(x)
+        h = one._load_header()
+        assert np.array_equal(q.getSplits(), one.getSplits())
+        assert q._load_header().zero_idx == h.zero_idx
+        nbytes = (x.numel() * h.code_bits + 7) // 8
+        assert torch.equal(q.payload[h.codes_offset:h.codes_offset + nbytes],
+                           one.payload[h.codes_offset:h.codes_offset + nbytes])
+        oq = O.quantize(x.cpu().numpy().astype(np.float64), 256, seed=3) if x.numel() < 400000 else None
+        if oq is not None:
+            assert np.array_equal(q.getBins().cpu().numpy(), oq.bins)
+
+
+def test_quantize_buckets_nan_raises(gpu):
+    xs = [torch.randn(5000, device="cuda") for _ in range(3)]
+    xs[1][17] = float("nan")
+    with pytest.raises(gpu.QuantileSketchException):
+        gpu.QuantileQuantizer.quantizeBuckets(xs, 256)
