@@ -287,17 +287,20 @@ __global__ __launch_bounds__(256) void k_decode(const uint8_t* __restrict__ payl
     const int lane = threadIdx.x & 63;
     const int64_t nw = (int64_t)gridDim.x * 4, wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int64_t full = n / 1024;
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
     for (int64_t tile = wid; tile < full; tile += nw) {
-        float4* dst = reinterpret_cast<float4*>(out + tile * 1024);
+        f32x4* dst = reinterpret_cast<f32x4*>(out + tile * 1024);
+        uint32_t c[4][4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) read_codes4(codes, tile * 1024 + j * 256 + lane * 4, bits, c[j]);
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            uint32_t c[4];
-            read_codes4(codes, tile * 1024 + j * 256 + lane * 4, bits, c);
-            float4 o;
-            if (lds) o = make_float4(lut[c[0]], lut[c[1]], lut[c[2]], lut[c[3]]);
-            else o = make_float4((float)lut_value(h, sp, c[0]), (float)lut_value(h, sp, c[1]),
-                                 (float)lut_value(h, sp, c[2]), (float)lut_value(h, sp, c[3]));
-            dst[j * 64 + lane] = o;
+            f32x4 o;
+            if (lds) o = f32x4{lut[c[j][0]], lut[c[j][1]], lut[c[j][2]], lut[c[j][3]]};
+            else o = f32x4{(float)lut_value(h, sp, c[j][0]), (float)lut_value(h, sp, c[j][1]),
+                           (float)lut_value(h, sp, c[j][2]), (float)lut_value(h, sp, c[j][3])};
+            // the decoded gradient is written once and not re-read by this pass: stream it past L2
+            __builtin_nontemporal_store(o, dst + j * 64 + lane);
         }
     }
     if (wid == full % nw) {
