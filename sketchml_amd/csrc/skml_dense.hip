@@ -20,8 +20,9 @@ __device__ __forceinline__ void store_codes4(uint8_t* codes, int64_t e0, uint32_
                                              uint32_t c2, uint32_t c3, int bits, int lane) {
     // e0 is a multiple of 4; lanes l and l^1 cover adjacent 4-element groups
     switch (bits) {
-        case 8:
-            *reinterpret_cast<uint32_t*>(codes + e0) = c0 | (c1 << 8) | (c2 << 16) | (c3 << 24);
+        case 8:  // codes are written once and read by the next pass at the earliest: stream past L2
+            __builtin_nontemporal_store(c0 | (c1 << 8) | (c2 << 16) | (c3 << 24),
+                                        reinterpret_cast<uint32_t*>(codes + e0));
             break;
         case 16:
             *reinterpret_cast<uint2*>(codes + e0 * 2) = make_uint2(c0 | (c1 << 16), c2 | (c3 << 16));
@@ -30,7 +31,7 @@ __device__ __forceinline__ void store_codes4(uint8_t* codes, int64_t e0, uint32_
             *reinterpret_cast<uint16_t*>(codes + e0 / 2) = (uint16_t)(c0 | (c1 << 4) | (c2 << 8) | (c3 << 12));
             break;
         case 2:
-            codes[e0 / 4] = (uint8_t)(c0 | (c1 << 2) | (c2 << 4) | (c3 << 6));
+            __builtin_nontemporal_store((uint8_t)(c0 | (c1 << 2) | (c2 << 4) | (c3 << 6)), codes + e0 / 4);
             break;
         default: {  // 1 bit: pair with the neighbour lane into one byte
             const uint32_t nib = c0 | (c1 << 1) | (c2 << 2) | (c3 << 3);
