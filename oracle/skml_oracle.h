@@ -9,7 +9,7 @@
  * (no JDK / javac / mvn) and ships no tests or golden vectors (§4).  This
  * restatement is therefore pinned only by known-answer tests derived by hand from the Java sources
  * and the public JDK specifications (java.util.Random LCG, Arrays.sort total order, BitSet word
- * layout, DataOutput big-endian) -- see tests/test_oracle_kat.py -- and cross-checked against an
+ * layout, DataOutput big-endian) -- see tests/test_oracle.py (K1-K8) -- and cross-checked against an
  * independent numpy restatement (oracle/np_oracle.py).  No output of the reference itself pins it:
  * "parity unpinned" against a live reference run.
  *

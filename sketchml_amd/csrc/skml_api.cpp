@@ -63,6 +63,7 @@ struct skml_ctx {
     skml_ctx* side = nullptr;
     hipEvent_t ev_join = nullptr, ev_leaf = nullptr;
     hipEvent_t after_leaf = nullptr;  // when set, recorded right after the next leaf launch
+    hipEvent_t ev_switch = nullptr;   // skml_ctx_set_stream: orders the new stream after the old one
     // parallelQuantize: slice records + the merged sketch's export (grow-only)
     void* sk = nullptr;
     size_t sk_cap = 0;
@@ -340,6 +341,7 @@ int skml_ctx_destroy(skml_ctx* c) {
     if (c->side) skml_ctx_destroy(c->side);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     if (c->ev_leaf) (void)hipEventDestroy(c->ev_leaf);
+    if (c->ev_switch) (void)hipEventDestroy(c->ev_switch);
     if (c->sk) (void)hipFree(c->sk);
     for (int k = 0; k < SKML_K_COUNT; k++)
         for (hipEvent_t e : c->ev[k]) (void)hipEventDestroy(e);
@@ -415,12 +417,22 @@ int skml_debug_leaf_stage(skml_ctx* c, const float* x, int64_t n, int stage, int
 
 int skml_ctx_set_stream(skml_ctx* c, void* hip_stream) {
     if (!c) return fail(SKML_E_ARG, "ctx is NULL");
+    if (hip_stream == SKML_STREAM_OWN) return fail(SKML_E_ARG, "SKML_STREAM_OWN is only valid at creation");
+    hipStream_t next = (hipStream_t)hip_stream;
+    if (next == c->stream) return SKML_OK;
+    HIP_TRY(hipSetDevice(c->device));
     if (c->own_stream) {
         HIP_TRY(hipStreamSynchronize(c->stream));
         HIP_TRY(hipStreamDestroy(c->stream));
         c->own_stream = false;
+    } else {
+        // the context's workspace (merge arrival counter, LUT, stage, scratch) is reused by the next
+        // call: order the new stream after everything still queued on the old one
+        if (!c->ev_switch) HIP_TRY(hipEventCreateWithFlags(&c->ev_switch, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(c->ev_switch, c->stream));
+        HIP_TRY(hipStreamWaitEvent(next, c->ev_switch, 0));
     }
-    c->stream = (hipStream_t)hip_stream;
+    c->stream = next;
     return SKML_OK;
 }
 
@@ -796,6 +808,10 @@ int skml_dense_encode_batch_f32(skml_ctx* c, int32_t nbuckets, const float* cons
         int st = skml_dense_encode_f32(lane[i & 1], xs[i], ns[i], p, payloads[i], caps[i]);
         if (st) {
             c->after_leaf = nullptr;
+            if (i >= 1) {  // lane 1 holds queued buckets: the caller's stream must still wait for them
+                (void)hipEventRecord(c->ev_join, c->side->stream);
+                (void)hipStreamWaitEvent(c->stream, c->ev_join, 0);
+            }
             return st;
         }
         if (i == 0 && c->after_leaf) {  // bucket 0 had no leaf (n < 256): order lane 1 after it
@@ -1087,6 +1103,23 @@ int skml_dense_decode_sum_f32(skml_ctx* c, const void* payloads, int32_t P, size
         (n > 0 && (!out || ((uintptr_t)out) % 16)))
         return fail(SKML_E_ARG, "bad decode_sum arguments (P in [1,16], 256-B aligned payloads)");
     HIP_TRY(hipSetDevice(c->device));
+    // Gradient.sum adds gradients of one dimension (ml/gradient/Gradient.scala:44-49): every
+    // payload must be a finished dense payload of exactly n codes that fits its stride.
+    skml_dense_header h[16];
+    HIP_TRY(hipMemcpy2DAsync(h, sizeof(skml_dense_header), payloads, stride, sizeof(skml_dense_header), (size_t)P,
+                             hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    for (int p = 0; p < P; p++) {
+        if (h[p].magic != SKML_DENSE_MAGIC) return fail(SKML_E_STATE, "payload %d is not a dense payload", p);
+        if (h[p].status == SKML_E_NAN) return fail(SKML_E_NAN, "payload %d: Encounter NaN value", p);
+        if (h[p].status != SKML_OK) return fail(SKML_E_STATE, "payload %d has status %d", p, h[p].status);
+        if (h[p].n != n)
+            return fail(SKML_E_ARG, "payload %d holds %lld values, the sum %lld", p, (long long)h[p].n, (long long)n);
+        if (h[p].bin_num < 2 || h[p].bin_num > SKML_MAX_BINS || h[p].code_bits != code_bits_for(h[p].bin_num) ||
+            h[p].bin_num > h[p].req_bins || h[p].codes_offset != (int64_t)dense_codes_offset(h[p].req_bins) ||
+            skml_dense_payload_bytes(n, h[p].req_bins) > stride)
+            return fail(SKML_E_ARG, "payload %d: inconsistent header or larger than the stride %zu", p, stride);
+    }
     KernelTimer kt(c, SKML_K_DECODE_SUM);
     HIP_TRY(launch_decode_sum(c->stream, payloads, P, stride, out, n, scale));
     return SKML_OK;
@@ -1198,22 +1231,35 @@ int skml_dense_deserialize_ref(skml_ctx* c, const uint8_t* buf, size_t len, void
     const int32_t nb = (int32_t)get_be(p, 4); p += 4;
     if (nb != n || len < head + (size_t)width * (size_t)n) return fail(SKML_E_ARG, "truncated bins");
     if (cap < skml_dense_payload_bytes(n, B)) return fail(SKML_E_ARG, "payload too small");
+    // Quantizer.findZeroIdx only yields indices of bins (Quantizer.java:74-85)
+    if (h.zero_idx < 0 || h.zero_idx >= B) return fail(SKML_E_ARG, "zeroIdx %d outside [0, %d)", h.zero_idx, B);
     h.n = n;
     h.bin_num = B;
     h.code_bits = code_bits_for(B);
     h.req_bins = B;
     h.codes_offset = (int64_t)dense_codes_offset(B);
     HIP_TRY(hipSetDevice(c->device));
-    int st = ensure_stage(c, (size_t)width * (size_t)n + 16);
+    const size_t body = align_up((size_t)width * (size_t)n, 16);
+    int st = ensure_stage(c, body + 16);
     if (st) return st;
+    int* bad = reinterpret_cast<int*>((char*)c->stage + body);
+    HIP_TRY(hipMemsetAsync(bad, 0, sizeof(int), c->stream));
     HIP_TRY(hipMemcpyAsync(payload, &h, sizeof(h), hipMemcpyHostToDevice, c->stream));
     if (ns) HIP_TRY(hipMemcpyAsync((char*)payload + kHeaderBytes, sp.data(), sizeof(double) * ns,
                                    hipMemcpyHostToDevice, c->stream));
     if (n) {
         HIP_TRY(hipMemcpyAsync(c->stage, p, (size_t)width * (size_t)n, hipMemcpyHostToDevice, c->stream));
-        HIP_TRY(launch_pack_ref(c->stream, (const uint8_t*)c->stage, width, n, payload));
+        HIP_TRY(launch_pack_ref(c->stream, (const uint8_t*)c->stage, width, n, payload, bad));
     }
+    int nbad = 0;
+    HIP_TRY(hipMemcpyAsync(&nbad, bad, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    if (nbad) {
+        // leave no usable payload behind
+        const uint32_t zero = 0;
+        HIP_TRY(hipMemcpy(payload, &zero, sizeof(zero), hipMemcpyHostToDevice));
+        return fail(SKML_E_ARG, "bin outside [0, %d) in the stream", B);
+    }
     return SKML_OK;
 }
 

@@ -319,7 +319,9 @@ hipError_t launch_decode(hipStream_t st, const void* payload, float* out, int64_
     return hipGetLastError();
 }
 
-// Fused decode of P payloads + sum in double (Gradient.sum adds doubles) + scale.
+// Fused decode of P payloads + sum in double (Gradient.sum adds doubles) + scale.  Payloads of at
+// most kSumLutBins bins look their values up in an LDS table; wider ones (16-bit codes) compute
+// the midpoint from the payload's splits, as k_decode does above kLutMax.
 constexpr int kMaxSumPayloads = 16;
 constexpr int kSumLutBins = 256;
 __global__ __launch_bounds__(256) void k_decode_sum(const uint8_t* __restrict__ payloads, int P,
@@ -330,7 +332,8 @@ __global__ __launch_bounds__(256) void k_decode_sum(const uint8_t* __restrict__ 
         const uint8_t* pl = payloads + (size_t)p * stride;
         const skml_dense_header* h = reinterpret_cast<const skml_dense_header*>(pl);
         const double* sp = reinterpret_cast<const double*>(pl + kHeaderBytes);
-        for (int b = threadIdx.x; b < h->bin_num && b < kSumLutBins; b += 256) lut[p][b] = lut_value(h, sp, b);
+        if (h->bin_num > kSumLutBins) continue;
+        for (int b = threadIdx.x; b < h->bin_num; b += 256) lut[p][b] = lut_value(h, sp, b);
     }
     __syncthreads();
     const int64_t stride_e = (int64_t)gridDim.x * 256;
@@ -344,7 +347,12 @@ __global__ __launch_bounds__(256) void k_decode_sum(const uint8_t* __restrict__ 
             if (e0 + 4 <= n) read_codes4(codes, e0, h->code_bits, c);
             else
                 for (int e = 0; e < 4; e++) c[e] = e0 + e < n ? read_code(codes, e0 + e, h->code_bits) : 0;
-            for (int e = 0; e < 4; e++) acc[e] += lut[p][c[e]];
+            if (h->bin_num <= kSumLutBins) {
+                for (int e = 0; e < 4; e++) acc[e] += lut[p][c[e]];
+            } else {
+                const double* sp = reinterpret_cast<const double*>(pl + kHeaderBytes);
+                for (int e = 0; e < 4; e++) acc[e] += lut_value(h, sp, (int)c[e]);
+            }
         }
         if (e0 + 4 <= n) {
             *reinterpret_cast<float4*>(out + e0) = make_float4((float)(acc[0] * scale), (float)(acc[1] * scale),
@@ -426,14 +434,18 @@ hipError_t launch_times_by(hipStream_t st, void* payload, double x) {
 }  // namespace skml
 
 namespace skml {
-// Quantizer.readObject bin stream (Quantizer.java:216-225) -> packed codes of the payload.
+// Quantizer.readObject bin stream (Quantizer.java:216-225) -> packed codes of the payload.  A bin
+// outside [0, binNum) (a malformed stream; Java fails on it with ArrayIndexOutOfBounds in
+// getValues) is counted in *bad and stored as 0, so no code field overflows into its neighbour.
 __global__ void k_pack_ref(const uint8_t* __restrict__ body, int width, int64_t n,
-                           uint8_t* __restrict__ payload) {
+                           uint8_t* __restrict__ payload, int* __restrict__ bad) {
     const skml_dense_header* h = reinterpret_cast<const skml_dense_header*>(payload);
     uint8_t* codes = payload + h->codes_offset;
+    const uint32_t bins = (uint32_t)h->bin_num;
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t e0 = g * 4;
     uint32_t c[4] = {0, 0, 0, 0};
+    bool out_of_range = false;
     for (int e = 0; e < 4; e++) {
         const int64_t i = e0 + e;
         if (i >= n) break;
@@ -443,7 +455,12 @@ __global__ void k_pack_ref(const uint8_t* __restrict__ body, int width, int64_t 
         else
             c[e] = ((uint32_t)body[4 * i] << 24) | ((uint32_t)body[4 * i + 1] << 16) |
                    ((uint32_t)body[4 * i + 2] << 8) | body[4 * i + 3];
+        if (c[e] >= bins) {
+            out_of_range = true;
+            c[e] = 0;
+        }
     }
+    if (__ballot(out_of_range) != 0 && (threadIdx.x & 63) == 0) atomicAdd(bad, 1);
     const int lane = threadIdx.x & 63;
     if (h->code_bits == 1) {
         const uint32_t nib = c[0] | (c[1] << 1) | (c[2] << 2) | (c[3] << 3);
@@ -454,11 +471,11 @@ __global__ void k_pack_ref(const uint8_t* __restrict__ body, int width, int64_t 
     }
 }
 
-hipError_t launch_pack_ref(hipStream_t st, const uint8_t* body, int width, int64_t n, void* payload) {
+hipError_t launch_pack_ref(hipStream_t st, const uint8_t* body, int width, int64_t n, void* payload, int* bad) {
     if (n <= 0) return hipSuccess;
     const int64_t groups = (n + 3) / 4;
     hipLaunchKernelGGL(k_pack_ref, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, st, body,
-                       width, n, reinterpret_cast<uint8_t*>(payload));
+                       width, n, reinterpret_cast<uint8_t*>(payload), bad);
     return hipGetLastError();
 }
 }  // namespace skml

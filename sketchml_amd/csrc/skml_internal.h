@@ -172,6 +172,7 @@ hipError_t launch_uniform(hipStream_t st, const float* x, int64_t n, int bin_num
                           QuantLut* lut, int* qflags);
 hipError_t launch_uniform64(hipStream_t st, const double* x, int64_t n, int bin_num, UniPartial* part,
                             void* payload, QuantLut* lut, int* qflags);
-hipError_t launch_pack_ref(hipStream_t st, const uint8_t* body, int width, int64_t n, void* payload);
+// *bad (device int, zeroed by the caller) counts waves that met a bin outside [0, binNum)
+hipError_t launch_pack_ref(hipStream_t st, const uint8_t* body, int width, int64_t n, void* payload, int* bad);
 
 }  // namespace skml

@@ -1,7 +1,8 @@
 """World-size-2 gloo tests of the multi-GPU control plane (sketchml_amd/distributed.py) on CPU:
 unique-id broadcast, payload-size agreement, bucket sharding.  The RCCL data path itself
-(skml_allgather) is exercised on the GPU box (tests/test_gpu_dense.py::test_decode_sum and
-bench.py --gpus N)."""
+(skml_comm_init_rank + skml_allgather) runs on the GPU box with a world-size-1 communicator in
+tests/test_gpu_configs.py (byte-identical copy, PayloadExchange + decode_sum, and the C4
+eight-bucket all-gather layout), and with N ranks in bench.py --gpus N."""
 import os
 import socket
 

@@ -1,0 +1,387 @@
+"""BASELINE.json configurations at their full sizes on one MI355X, against the oracle, plus the
+RCCL exchange and the guards of the aggregation path.
+
+- C1: 10^6-float App-distribution gradient (sample/App.java:33-40): oracle parity + the per-element
+  half-bin-width bound (property P2) and the loopback L2 the oracle predicts.
+- C2: 2^26-float bucket, 256 bins: splits, header and every bin against O.quantize.
+- C4 on one GPU: 8 x 2^26 buckets through skml_dense_encode_batch_f32, each payload moved by an
+  RCCL (world size 1) all-gather into the slot an 8-rank all-gather would leave it in, then
+  skml_dense_decode_sum_f32 against the oracle's per-bucket decode summed in double
+  (Gradient.sum + timesBy(1/P), ml/gradient/Gradient.scala:44-49,
+  ml/algorithm/GeneralizedLinearModel.scala:145-150).
+- C5 shard: 2^27 values (one of the 8 shards of the 2^30-float gradient), 4 bins = 2-bit codes.
+- P4 determinism over 10 runs.
+The oracle (oracle/skml_oracle.c through ctypes, which releases the GIL) is only the checker; all
+device work goes through libskml.so.
+"""
+import ctypes as C
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _lib():
+    from sketchml_amd import _lib
+    return _lib
+
+
+def _params(bins=256, seed=0):
+    L = _lib()
+    p = L.Params()
+    L.lib.skml_params_default(C.byref(p))
+    p.bin_num = bins
+    p.seed = seed
+    return p
+
+
+def _normal(n, seed):
+    return np.random.default_rng(seed).standard_normal(n, dtype=np.float32)
+
+
+def _bins_of(gpu, payload, n):
+    L = _lib()
+    ctx = gpu.get_context()
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    assert L.lib.skml_dense_bins_i32(ctx.handle, C.c_void_p(payload.data_ptr()), C.c_void_p(out.data_ptr()), n) == 0
+    torch.cuda.synchronize()
+    return out
+
+
+def _header(gpu, payload, cap=65536):
+    L = _lib()
+    h = L.DenseHeader()
+    sp = np.zeros(cap, dtype=np.float64)
+    st = L.lib.skml_dense_info(gpu.get_context().handle, C.c_void_p(payload.data_ptr()), C.byref(h),
+                               sp.ctypes.data_as(L.dblp), cap)
+    return st, h, sp[: max(h.bin_num - 1, 0)]
+
+
+def _assert_matches(gpu, payload, n, oq):
+    st, h, sp = _header(gpu, payload)
+    assert st == 0
+    assert (h.bin_num, h.zero_idx, h.min, h.max, h.n) == (oq.bin_num, oq.zero_idx, oq.min, oq.max, n)
+    assert np.array_equal(sp, oq.splits)
+    bins = _bins_of(gpu, payload, n).cpu().numpy()
+    assert np.array_equal(bins, oq.bins)
+
+
+# --------------------------------------------------------------------------------------------
+# RCCL exchange (world size 1 on the one-GPU box: a real communicator and a real ncclAllGather)
+# --------------------------------------------------------------------------------------------
+class _Comm:
+    def __init__(self, ctx_handle):
+        L = _lib()
+        uid = (C.c_uint8 * L.UNIQUE_ID_BYTES)()
+        assert L.lib.skml_comm_unique_id(uid) == 0, L.last_error()
+        self.h = C.c_void_p()
+        assert L.lib.skml_comm_init_rank(ctx_handle, uid, 1, 0, C.byref(self.h)) == 0, L.last_error()
+        self.ctx = ctx_handle
+
+    def allgather(self, src, nbytes, dst_ptr):
+        L = _lib()
+        assert L.lib.skml_allgather(self.ctx, self.h, C.c_void_p(src.data_ptr()), nbytes, C.c_void_p(dst_ptr)) == 0, \
+            L.last_error()
+
+    def close(self):
+        _lib().lib.skml_comm_destroy(self.h)
+
+
+def test_rccl_world1_allgather_is_a_byte_identical_copy(gpu):
+    ctx = gpu.get_context()
+    n = 3 * 2**20 + 7
+    x = torch.from_numpy(_normal(n, 1)).cuda()
+    L = _lib()
+    nb = L.lib.skml_dense_payload_bytes(n, 256)
+    pl = gpu.alloc_aligned(nb, "cuda")
+    assert L.lib.skml_dense_encode_f32(ctx.handle, C.c_void_p(x.data_ptr()), n, C.byref(_params(256, 3)),
+                                       C.c_void_p(pl.data_ptr()), nb) == 0
+    out = gpu.alloc_aligned(nb, "cuda")
+    out.fill_(0xA5)
+    comm = _Comm(ctx.handle)
+    try:
+        comm.allgather(pl, nb, out.data_ptr())
+        torch.cuda.synchronize()
+    finally:
+        comm.close()
+    assert torch.equal(out, pl)
+
+
+def test_payload_exchange_world1_through_process_group(gpu):
+    """sketchml_amd.distributed.PayloadExchange (unique id over a world-1 gloo group, RCCL data
+    path) followed by decode_sum: equal to the bucket's own decode."""
+    import torch.distributed as dist
+    from sketchml_amd import distributed as D
+    store = dist.HashStore()
+    dist.init_process_group("gloo", store=store, rank=0, world_size=1)
+    try:
+        ctx = gpu.get_context()
+        n = 2**20 + 11
+        x = torch.from_numpy(_normal(n, 2)).cuda()
+        L = _lib()
+        nb = L.lib.skml_dense_payload_bytes(n, 256)
+        pl = gpu.alloc_aligned(nb, "cuda")
+        assert L.lib.skml_dense_encode_f32(ctx.handle, C.c_void_p(x.data_ptr()), n, C.byref(_params(256, 5)),
+                                           C.c_void_p(pl.data_ptr()), nb) == 0
+        ex = D.PayloadExchange(ctx.handle)
+        allp = gpu.alloc_aligned(nb, "cuda")
+        ex.allgather(pl, nb, allp)
+        summed = torch.empty(n, dtype=torch.float32, device="cuda")
+        D.decode_sum(ctx.handle, allp, 1, nb, n, 1.0, summed)
+        own = torch.empty(n, dtype=torch.float32, device="cuda")
+        assert L.lib.skml_dense_decode_f32(ctx.handle, C.c_void_p(pl.data_ptr()), C.c_void_p(own.data_ptr()), n) == 0
+        torch.cuda.synchronize()
+        ex.close()
+        assert torch.equal(summed, own)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_c4_eight_buckets_batch_rccl_decode_sum(gpu):
+    """C4 on one GPU: 8 x 2^26 buckets (bucket r seeded 4 + r), batched encode, RCCL placement
+    into the all-gather layout, fused decode + double sum + 1/8 against the oracle."""
+    L = _lib()
+    ctx = gpu.get_context()
+    P, n = 8, 2**26
+    xs_host = [_normal(n, 4 + r) for r in range(P)]
+    xs = [torch.from_numpy(a).cuda() for a in xs_host]
+    nb = L.lib.skml_dense_payload_bytes(n, 256)
+    pls = [gpu.alloc_aligned(nb, "cuda") for _ in range(P)]
+    p = _params(256, 4)
+    ptrs = (C.c_void_p * P)(*[x.data_ptr() for x in xs])
+    pptr = (C.c_void_p * P)(*[q.data_ptr() for q in pls])
+    ns = (C.c_int64 * P)(*([n] * P))
+    caps = (C.c_size_t * P)(*([nb] * P))
+    assert L.lib.skml_dense_encode_batch_f32(ctx.handle, P, ptrs, ns, C.byref(p), pptr, caps) == 0, L.last_error()
+    allp = gpu.alloc_aligned(nb * P, "cuda")
+    comm = _Comm(ctx.handle)
+    try:
+        for r in range(P):  # rank r's payload lands at r * nb, as an 8-rank all-gather leaves it
+            comm.allgather(pls[r], nb, allp.data_ptr() + r * nb)
+        torch.cuda.synchronize()
+    finally:
+        comm.close()
+    del xs
+    out = torch.empty(n, dtype=torch.float32, device="cuda")
+    assert L.lib.skml_dense_decode_sum_f32(ctx.handle, C.c_void_p(allp.data_ptr()), P, nb,
+                                           C.c_void_p(out.data_ptr()), n, 1.0 / P) == 0, L.last_error()
+    torch.cuda.synchronize()
+    with ThreadPoolExecutor(8) as ex:
+        oqs = list(ex.map(lambda a: O.quantize(a.astype(np.float64), 256, 4), xs_host))
+    want = np.zeros(n, dtype=np.float64)
+    for r, oq in enumerate(oqs):
+        # every bucket bit-exact first (splits, header, bins), then the aggregate
+        _assert_matches(gpu, pls[r], n, oq)
+        want += oq.values()[oq.bins]
+    assert np.array_equal(out.cpu().numpy(), (want * (1.0 / P)).astype(np.float32))
+
+
+def test_c5_shard_two_bit_codes(gpu):
+    """One C5 shard: 2^27 values (seed 5), B = 4 -> 2-bit codes, against the oracle."""
+    L = _lib()
+    ctx = gpu.get_context()
+    n = 2**27
+    xh = _normal(n, 5)
+    x = torch.from_numpy(xh).cuda()
+    nb = L.lib.skml_dense_payload_bytes(n, 4)
+    pl = gpu.alloc_aligned(nb, "cuda")
+    assert L.lib.skml_dense_encode_f32(ctx.handle, C.c_void_p(x.data_ptr()), n, C.byref(_params(4, 5)),
+                                       C.c_void_p(pl.data_ptr()), nb) == 0
+    del x
+    oq = O.quantize(xh.astype(np.float64), 4, 5)
+    assert oq.bin_num == 4
+    st, h, _ = _header(gpu, pl)
+    assert st == 0 and h.code_bits == 2
+    _assert_matches(gpu, pl, n, oq)
+
+
+def test_c2_full_size_matches_oracle(gpu):
+    """C2 at its full size: 2^26 floats, 256 requested bins (129 effective), oracle parity."""
+    L = _lib()
+    ctx = gpu.get_context()
+    n = 2**26
+    xh = _normal(n, 2)
+    x = torch.from_numpy(xh).cuda()
+    nb = L.lib.skml_dense_payload_bytes(n, 256)
+    pl = gpu.alloc_aligned(nb, "cuda")
+    assert L.lib.skml_dense_encode_f32(ctx.handle, C.c_void_p(x.data_ptr()), n, C.byref(_params(256, 2)),
+                                       C.c_void_p(pl.data_ptr()), nb) == 0
+    oq = O.quantize(xh.astype(np.float64), 256, 2)
+    assert oq.bin_num == 129
+    _assert_matches(gpu, pl, n, oq)
+    dec = torch.empty(n, dtype=torch.float32, device="cuda")
+    assert L.lib.skml_dense_decode_f32(ctx.handle, C.c_void_p(pl.data_ptr()), C.c_void_p(dec.data_ptr()), n) == 0
+    want = oq.values()[oq.bins].astype(np.float32)
+    assert np.array_equal(dec.cpu().numpy().view(np.uint32), want.view(np.uint32))
+
+
+def test_c1_app_loopback_l2_bound(gpu):
+    """C1 (the reference's App.dense loopback, sample/App.java:33-63) at exactly 10^6 values:
+    oracle parity, the half-bin-width bound per element (P2) and the loopback L2 error equal to
+    the oracle's (decoded fp32 is bit-exact, so the L2 difference to the oracle is 0 <= the stated
+    tolerance 2^-24 * ||oracle||_2)."""
+    n = 10**6
+    rng = np.random.default_rng(1)
+    xh = np.where(rng.random(n) < 0.9, rng.standard_normal(n), 0.0).astype(np.float32)
+    gq = gpu.QuantileQuantizer(256, seed=1)
+    gq.quantize(torch.from_numpy(xh).cuda())
+    oq = O.quantize(xh.astype(np.float64), 256, 1)
+    assert gq.getBinNum() == oq.bin_num and np.array_equal(gq.getSplits(), oq.splits)
+    bins = gq.getBins().cpu().numpy()
+    assert np.array_equal(bins, oq.bins)
+    dec = gq.decode().cpu().numpy().astype(np.float64)
+    want = oq.values()[oq.bins].astype(np.float32).astype(np.float64)
+    assert np.linalg.norm(dec - want) <= 2.0**-24 * np.linalg.norm(want)
+    edges = np.concatenate([[oq.min], oq.splits, [oq.max]])
+    half = (edges[1:] - edges[:-1]) / 2
+    err = np.abs(dec - xh.astype(np.float64))
+    assert np.all(err <= half[bins] * (1 + 1e-6) + 1e-6 * np.abs(dec))
+    l2 = np.linalg.norm(dec - xh)
+    assert l2 == pytest.approx(np.linalg.norm(want - xh), rel=0, abs=0)
+    assert 0 < l2 / np.linalg.norm(xh) < 0.2
+
+
+# --------------------------------------------------------------------------------------------
+# aggregation guards (k_decode_sum)
+# --------------------------------------------------------------------------------------------
+def _encode_into(gpu, allp, slot, nb, x, bins, seed):
+    L = _lib()
+    ctx = gpu.get_context()
+    return L.lib.skml_dense_encode_f32(ctx.handle, C.c_void_p(x.data_ptr()), x.numel(), C.byref(_params(bins, seed)),
+                                       C.c_void_p(allp.data_ptr() + slot * nb), nb)
+
+
+@pytest.mark.parametrize("bins", [1000, 4096, 300])
+def test_decode_sum_wide_codes(gpu, bins):
+    """More than 256 bins (16-bit codes): the sum looks values up from the splits, not past the
+    LDS table; mixed widths in one call too (the last payload has 256 bins)."""
+    L = _lib()
+    n, P = 300007, 3
+    nb = L.lib.skml_dense_payload_bytes(n, max(bins, 256))
+    allp = gpu.alloc_aligned(nb * P, "cuda")
+    want = np.zeros(n, dtype=np.float64)
+    for p in range(P):
+        b = bins if p < P - 1 else 256
+        xh = _normal(n, 300 + p)
+        assert _encode_into(gpu, allp, p, nb, torch.from_numpy(xh).cuda(), b, p) == 0
+        torch.cuda.synchronize()
+        oq = O.quantize(xh.astype(np.float64), b, p)
+        want += oq.values()[oq.bins]
+    out = torch.empty(n, dtype=torch.float32, device="cuda")
+    assert L.lib.skml_dense_decode_sum_f32(gpu.get_context().handle, C.c_void_p(allp.data_ptr()), P, nb,
+                                           C.c_void_p(out.data_ptr()), n, 1.0 / P) == 0, L.last_error()
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), (want * (1.0 / P)).astype(np.float32))
+
+
+def test_decode_sum_rejects_bad_payloads(gpu):
+    L = _lib()
+    ctx = gpu.get_context()
+    n, P = 50000, 2
+    nb = L.lib.skml_dense_payload_bytes(n, 256)
+    allp = gpu.alloc_aligned(nb * P, "cuda")
+    out = torch.empty(n, dtype=torch.float32, device="cuda")
+    xh = _normal(n, 9)
+    assert _encode_into(gpu, allp, 0, nb, torch.from_numpy(xh).cuda(), 256, 1) == 0
+    bad = xh.copy()
+    bad[77] = np.nan  # payload 1 carries the NaN status (HeapQuantileSketch.update throws)
+    assert _encode_into(gpu, allp, 1, nb, torch.from_numpy(bad).cuda(), 256, 1) == 0
+
+    def call(m=n, p=P):
+        return L.lib.skml_dense_decode_sum_f32(ctx.handle, C.c_void_p(allp.data_ptr()), p, nb,
+                                               C.c_void_p(out.data_ptr()), m, 1.0)
+
+    assert call() == L.SKML_E_NAN
+    assert call(p=1) == 0
+    assert call(m=n - 1, p=1) == L.SKML_E_ARG  # Gradient.sum of a different dimension
+    allp[nb: nb + 4].zero_()  # not a payload at all
+    assert call() == L.SKML_E_STATE
+    torch.cuda.synchronize()
+
+
+# --------------------------------------------------------------------------------------------
+# readObject of malformed streams (Quantizer.readObject, Quantizer.java:205-226)
+# --------------------------------------------------------------------------------------------
+def test_read_object_rejects_out_of_range_bins_and_zero_idx(gpu):
+    n, bins = 5000, 200
+    xh = _normal(n, 21)
+    oq = O.quantize(xh.astype(np.float64), bins, 3)
+    B = oq.bin_num
+    good = bytearray(oq.write_ref())
+    q = gpu.Quantizer.readObject(bytes(good))
+    assert np.array_equal(q.getBins().cpu().numpy(), oq.bins)
+    body = len(good) - n  # 1-byte bins (B <= 256) written as (bin - 128)
+    bad = bytearray(good)
+    bad[body + 123] = (B + 5 - 128) & 0xFF  # a bin >= binNum
+    with pytest.raises(gpu.SketchMLException, match="outside"):
+        gpu.Quantizer.readObject(bytes(bad))
+    zoff = 8 + 8 * (B - 1)
+    bad = bytearray(good)
+    bad[zoff:zoff + 4] = int(B).to_bytes(4, "big")  # zeroIdx == binNum
+    with pytest.raises(gpu.SketchMLException, match="zeroIdx"):
+        gpu.Quantizer.readObject(bytes(bad))
+    bad = bytearray(good)
+    bad[zoff:zoff + 4] = (-1 & 0xFFFFFFFF).to_bytes(4, "big")
+    with pytest.raises(gpu.SketchMLException, match="zeroIdx"):
+        gpu.Quantizer.readObject(bytes(bad))
+
+
+# --------------------------------------------------------------------------------------------
+# determinism and stream switching
+# --------------------------------------------------------------------------------------------
+def test_determinism_ten_runs(gpu):
+    """P4: the same seed gives a byte-identical payload over 10 runs."""
+    L = _lib()
+    ctx = gpu.get_context()
+    n = 2**22 + 2**13 + 123  # several trees and a tail
+    x = torch.from_numpy(_normal(n, 33)).cuda()
+    nb = L.lib.skml_dense_payload_bytes(n, 256)
+    ref = None
+    for _ in range(10):
+        pl = gpu.alloc_aligned(nb, "cuda")
+        pl.zero_()
+        assert L.lib.skml_dense_encode_f32(ctx.handle, C.c_void_p(x.data_ptr()), n, C.byref(_params(256, 7)),
+                                           C.c_void_p(pl.data_ptr()), nb) == 0
+        torch.cuda.synchronize()
+        if ref is None:
+            ref = pl.clone()
+        else:
+            assert torch.equal(pl, ref)
+
+
+def test_context_follows_stream_switches(gpu):
+    """One context, encodes alternating between two torch streams with no synchronisation in
+    between (skml_ctx_set_stream orders the new stream after the old one): every result equals a
+    single-stream encode."""
+    ctx = gpu.get_context()
+    L = _lib()
+    n = 2**21 + 999
+    xs = [torch.from_numpy(_normal(n, 50 + i)).cuda() for i in range(4)]
+    nb = L.lib.skml_dense_payload_bytes(n, 256)
+    want = []
+    for x in xs:
+        pl = gpu.alloc_aligned(nb, "cuda")
+        pl.zero_()  # the bytes past the last code word are never written
+        assert L.lib.skml_dense_encode_f32(ctx.handle, C.c_void_p(x.data_ptr()), n, C.byref(_params(256, 1)),
+                                           C.c_void_p(pl.data_ptr()), nb) == 0
+        want.append(pl)
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    got = []
+    for i, x in enumerate(xs):
+        pl = gpu.alloc_aligned(nb, "cuda")
+        pl.zero_()
+        s = streams[i & 1]
+        s.wait_stream(torch.cuda.default_stream())
+        with torch.cuda.stream(s):
+            assert L.lib.skml_dense_encode_f32(ctx.handle, C.c_void_p(x.data_ptr()), n, C.byref(_params(256, 1)),
+                                               C.c_void_p(pl.data_ptr()), nb) == 0
+        got.append(pl)
+    torch.cuda.synchronize()
+    for g, w in zip(got, want):
+        assert torch.equal(g, w)

@@ -1,0 +1,140 @@
+// Microbenchmark (profiling aid): VALU issue cost on gfx950 of the building blocks a sorting
+// network uses, at 1 / 2 / 4 / 8 waves per SIMD.  Each lane runs 32 independent chains of one
+// instruction pattern; reported: SIMD cycles per wave-instruction (in-kernel clock from
+// s_memtime / s_memrealtime) and the kernel's wall time.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+
+#define N_ITER 4096
+#define NV 32
+
+struct Stamp {
+    unsigned long long t0, t1, r0, r1;
+};
+
+template <int KIND>
+__global__ __launch_bounds__(256) void kern(float* out, Stamp* st, float seed) {
+    extern __shared__ float pad[];
+    float v[NV];
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int i = 0; i < NV; i++) v[i] = seed * (float)(threadIdx.x + 1) * (float)(i + 7) - 3.0f;
+    const float sel = (lane & 1) ? __builtin_inff() : -__builtin_inff();
+    unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    for (int it = 0; it < N_ITER; it++) {
+#pragma unroll
+        for (int i = 0; i < NV; i++) {
+            float a = v[i], b = v[(i + 1) & (NV - 1)], r = a;
+            if constexpr (KIND == 0) { asm volatile("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); }
+            else if constexpr (KIND == 1) { asm volatile("v_med3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(sel)); }
+            else if constexpr (KIND == 2) { asm volatile("v_min_u32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); }
+            else if constexpr (KIND == 3) { asm volatile("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(sel)); }
+            else if constexpr (KIND == 4) { asm volatile("v_min3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(sel)); }
+            else if constexpr (KIND == 5) { asm volatile("v_min_i32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); }
+            else if constexpr (KIND == 6) { asm volatile("v_add_u32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); }
+            else if constexpr (KIND == 7) { asm volatile("v_sub_u32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); }
+            else if constexpr (KIND == 8) { asm volatile("v_and_b32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); }
+            else if constexpr (KIND == 9) { asm volatile("v_xor_b32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); }
+            else if constexpr (KIND == 10) { asm volatile("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(sel)); }
+            else if constexpr (KIND == 11) { asm volatile("v_perm_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(sel)); }
+            else if constexpr (KIND == 12) { asm volatile("v_mov_b32_dpp %0, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(b)); }
+            else if constexpr (KIND == 13) { asm volatile("v_min_u32_dpp %0, %1, %2 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(a), "v"(b)); }
+            else if constexpr (KIND == 14) { asm volatile("v_add_u32_dpp %0, %1, %2 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(a), "v"(b)); }
+            else if constexpr (KIND == 15) { asm volatile("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); }
+            else if constexpr (KIND == 16) { asm volatile("v_pk_max_f16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); }
+            else if constexpr (KIND == 17) { asm volatile("v_min_f16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); }
+            else if constexpr (KIND == 18) { asm volatile("v_mul_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); }
+            else if constexpr (KIND == 19) { asm volatile("v_fma_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(sel)); }
+            else if constexpr (KIND == 20) { asm volatile("v_max_f32_e64 %0, -%1, %2" : "=v"(r) : "v"(a), "v"(b)); }
+            else if constexpr (KIND == 21) { asm volatile("v_cmp_lt_u32_e64 s[40:41], %1, %2" : "=v"(r) : "v"(a), "v"(b) : "s40", "s41"); }
+            else if constexpr (KIND == 22) { asm volatile("v_cndmask_b32_e64 %0, %1, %2, s[40:41]" : "=v"(r) : "v"(a), "v"(b) : "s40", "s41"); }
+            else if constexpr (KIND == 23) { asm volatile("v_lshrrev_b32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); }
+            else if constexpr (KIND == 24) { asm volatile("v_sad_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(sel)); }
+            else if constexpr (KIND == 25) { asm volatile("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(sel)); }
+            else if constexpr (KIND == 26) { asm volatile("v_permlane32_swap_b32 %0, %1" : "+v"(a) : "v"(b)); r = a; }
+            v[i] = r;
+        }
+    }
+    unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; i++) acc += v[i];
+    out[blockIdx.x * 256 + threadIdx.x] = acc;
+    if (lane == 0) st[blockIdx.x * 4 + (threadIdx.x >> 6)] = Stamp{t0, t1, r0, r1};
+    if (acc == 12345.f) pad[threadIdx.x] = acc;
+}
+
+template <int K>
+void run(const char* name, float* d, Stamp* st, Stamp* hst, int cus) {
+    for (int wps = 4; wps <= 8; wps *= 2) {
+        const int blocks = cus * wps;
+        const size_t lds = (160 * 1024) / wps - 1024;
+        hipFuncSetAttribute((const void*)kern<K>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipEvent_t a, b;
+        hipEventCreate(&a);
+        hipEventCreate(&b);
+        hipLaunchKernelGGL(kern<K>, dim3(blocks), dim3(256), lds, 0, d, st, 1.0001f);
+        hipEventRecord(a);
+        const int reps = 5;
+        for (int r = 0; r < reps; r++) hipLaunchKernelGGL(kern<K>, dim3(blocks), dim3(256), lds, 0, d, st, 1.0001f);
+        hipEventRecord(b);
+        hipEventSynchronize(b);
+        float ms;
+        hipEventElapsedTime(&ms, a, b);
+        ms /= reps;
+        hipMemcpy(hst, st, sizeof(Stamp) * blocks * 4, hipMemcpyDeviceToHost);
+        double cyc = 0, real = 0;
+        for (int i = 0; i < blocks * 4; i++) {
+            cyc += (double)(hst[i].t1 - hst[i].t0);
+            real += (double)(hst[i].r1 - hst[i].r0);
+        }
+        cyc /= blocks * 4;
+        real /= blocks * 4;
+        const double ghz = cyc / real * 0.1;  // s_memrealtime runs at 100 MHz
+        const double instr = (double)N_ITER * NV;  // per wave
+        // per SIMD: wps waves, each `instr` instructions, over `cyc` cycles
+        printf("%-28s waves/SIMD %d  %6.2f cyc/instr/SIMD (in-wave)  %6.2f (wall)  clk %.2f GHz  %.3f ms\n", name,
+               wps, cyc / (instr * wps), ms * 1e-3 * ghz * 1e9 / (instr * wps), ghz, ms);
+    }
+}
+
+int main() {
+    int dev = 0;
+    hipDeviceProp_t p;
+    hipGetDeviceProperties(&p, dev);
+    const int cus = p.multiProcessorCount;
+    float* d;
+    Stamp *st, *hst;
+    hipMalloc(&d, sizeof(float) * 256 * cus * 8);
+    hipMalloc(&st, sizeof(Stamp) * cus * 8 * 4);
+    hst = (Stamp*)malloc(sizeof(Stamp) * cus * 8 * 4);
+    printf("CUs %d\n", cus);
+    run<0>("v_min_f32", d, st, hst, cus);
+    run<1>("v_med3_f32", d, st, hst, cus);
+    run<2>("v_min_u32", d, st, hst, cus);
+    run<3>("v_med3_u32", d, st, hst, cus);
+    run<4>("v_min3_u32", d, st, hst, cus);
+    run<5>("v_min_i32", d, st, hst, cus);
+    run<6>("v_add_u32", d, st, hst, cus);
+    run<7>("v_sub_u32", d, st, hst, cus);
+    run<8>("v_and_b32", d, st, hst, cus);
+    run<9>("v_xor_b32", d, st, hst, cus);
+    run<10>("v_bfi_b32", d, st, hst, cus);
+    run<11>("v_perm_b32", d, st, hst, cus);
+    run<12>("v_mov_b32_dpp", d, st, hst, cus);
+    run<13>("v_min_u32_dpp", d, st, hst, cus);
+    run<14>("v_add_u32_dpp", d, st, hst, cus);
+    run<15>("v_pk_min_u16", d, st, hst, cus);
+    run<16>("v_pk_max_f16", d, st, hst, cus);
+    run<17>("v_min_f16", d, st, hst, cus);
+    run<18>("v_mul_f32", d, st, hst, cus);
+    run<19>("v_fma_f32", d, st, hst, cus);
+    run<20>("v_max_f32_e64_neg", d, st, hst, cus);
+    run<21>("v_cmp_lt_u32_e64", d, st, hst, cus);
+    run<22>("v_cndmask_e64_s", d, st, hst, cus);
+    run<23>("v_lshrrev_b32", d, st, hst, cus);
+    run<24>("v_sad_u32", d, st, hst, cus);
+    run<25>("v_max3_f32", d, st, hst, cus);
+    run<26>("v_permlane32_swap", d, st, hst, cus);
+    return 0;
+}
