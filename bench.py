@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--dtype", choices=["f32", "f64"], default="f32",
                     help="input dtype (f64 = the reference's double[] path)")
     ap.add_argument("--quant", choices=["quantile", "uniform"], default="quantile")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
+    ap.add_argument("--cpu-seconds", type=float, default=16.0, help="CPU baseline budget (both legs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip decode / H2D measurements")
     ap.add_argument("--no-configs", action="store_true",
@@ -80,11 +80,13 @@ def pmc_traffic(kernel, n):
     return best
 
 
-# VALU issue ceiling (wave-instructions / s, whole chip): one 64-lane VALU wave-instruction per
-# clock per CU (4 SIMDs x 16 lanes) at the 2.4 GHz peak engine clock on 256 CUs.  (The
-# tools/ubench/xlane2.hip dependent-chain probe reached 1.12 clocks per instruction; the leaf,
-# with 8 independent waves per SIMD, issues faster than that, so the architectural rate is the
-# honest denominator.)
+# VALU issue ceiling of the sketch's instruction classes (wave-instructions / s, whole chip).
+# tools/ubench/issue.hip measured on gfx950, 8 waves per SIMD of independent chains: v_min/v_max/
+# v_med3/v_min3 (f32 and u32), every DPP move or DPP-fused op, v_cndmask_e64 and v_perm take
+# ~4.4 SIMD cycles per wave-instruction (the 4-cycle "quarter-wave" rate: one wave-instruction per
+# clock per CU), while v_add/v_sub/v_and/v_xor/v_lshr/v_mul_f32/v_fma_f32 take ~2.6 (the SIMD-32
+# rate).  A sorting network is almost all of the former, so the denominator is 1 wave-instruction
+# per clock per CU at the 2.4 GHz peak engine clock on 256 CUs.
 VALU_PEAK_GINST = 2.4e9 * 256 / 1e9
 
 
@@ -105,18 +107,43 @@ def sq_valu(kernel):
     return best
 
 
+def _cpu_threads():
+    """Host threads this process may use: the affinity mask, capped by OMP_NUM_THREADS (16 on the
+    GPU box, which shares a many-core host)."""
+    try:
+        t = len(os.sched_getaffinity(0))
+    except Exception:
+        t = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        t = min(t, int(omp))
+    return max(1, t)
+
+
 def cpu_baseline(x_host, bins, budget_s):
-    """Oracle (C restatement of QuantileQuantizer.quantize + 1-byte code write, scalar -O2,
-    double arithmetic, 1 thread) on a bounded sample of the same workload."""
+    """The reference's dense encode on this host's cores (oracle/cpu_baseline.cpp, checked against
+    the oracle in tests/test_cpu_baseline.py), on bounded samples of the same workload:
+      1 thread : QuantileQuantizer.quantize + quantizeToBins (the path ml uses,
+                 SketchGradient.scala:27), on the first 2^22 floats of the bucket;
+      T threads: parallelQuantize + parallelQuantizeToBins (QuantileQuantizer.java:53-92,
+                 Quantizer.java:94-117), T = the usable host threads, on the first 2^24 floats.
+    `value` is the faster (threaded) leg."""
     from oracle import oracle as O
-    sample = x_host[: 2**22]
-    t, _ = O.bench_dense_encode(sample, bins, seed=1, reps=1)
-    reps = max(1, int(budget_s / max(t, 1e-3)))
-    t, _ = O.bench_dense_encode(sample, bins, seed=1, reps=reps)
-    gbs = 4.0 * len(sample) * reps / t / 1e9
-    return {"value": round(gbs, 4), "unit": "GB/s", "cores": 1, "kind": "port",
-            "sample": f"first 2^22 floats of the bucket, {reps} encode(s), {t:.1f} s",
-            "cpu": _cpu_model()}
+    legs = {}
+    for name, threads, n in (("1_thread", 1, 2**22), ("threads", _cpu_threads(), 2**24)):
+        sample = np.ascontiguousarray(x_host[:n])
+        t1 = O.cpu_bench(sample, bins, 1, threads, 1)
+        reps = max(1, int(budget_s / 2 / max(t1, 1e-3)))
+        t = O.cpu_bench(sample, bins, 1, threads, reps)
+        legs[name] = {"gbps": round(4.0 * len(sample) * reps / t / 1e9, 4), "threads": threads,
+                      "sample": f"first {len(sample)} floats of the bucket, {reps} encode(s), {t:.1f} s"}
+    best = legs["threads"]
+    return {"value": best["gbps"], "unit": "GB/s", "cores": best["threads"], "kind": "port",
+            "sample": best["sample"] + " (parallelQuantize + parallelQuantizeToBins)",
+            "legs": legs, "cpu": _cpu_model(),
+            "what": "oracle/cpu_baseline.cpp: C++ -O3 restatement of the reference Java encode "
+                    "(std::sort per 256-value base buffer, sketch merges, getQuantiles, binary-search "
+                    "indexOf, 1-byte code write), not a JVM"}
 
 
 def other_configs(sk, lib, ctx, dev, xs):
@@ -170,6 +197,7 @@ def other_configs(sk, lib, ctx, dev, xs):
     out["batched_buckets"] = {"workload": f"{nbk} independent 2^26-float buckets per call, 256 bins",
                               "ms_per_bucket": round(tb / nbk * 1e3, 4), "gbps": round(4.0 * n * nbk / tb / 1e9, 1)}
     del pls
+    out["dense_2p28"] = dense_north_star(sk, lib, ctx, dev)
     dim = 2**28
     g = torch.Generator(device=dev).manual_seed(3)
     d = torch.randn(dim, device=dev, generator=g)
@@ -183,6 +211,118 @@ def other_configs(sk, lib, ctx, dev, xs):
                         "roofline_frac": round(alg / te / 1e9 / HBM_PEAK_GBS, 4), "restore_ms": round(td * 1e3, 3),
                         "note": "median wall time of 5 synchronised calls (host reads group sizes between passes)"}
     return out
+
+
+def dense_north_star(sk, lib, ctx, dev, n=2**28, bins=256, reps=10):
+    """The north-star size: a 2^28-float (1 GiB) bucket, larger than the 256 MB Infinity Cache, so
+    the quantize pass re-reads the input from HBM (at 2^26 part of it can still be on-die).
+    Encode time = mean of `reps` back-to-back encodes between two synchronisations; the
+    per-kernel split comes from HIP events on the codec stream in a separate pass."""
+    g = torch.Generator(device=dev).manual_seed(6)
+    x = torch.randn(n, device=dev, generator=g)
+    nb = lib.skml_dense_payload_bytes(n, bins)
+    pl = sk.alloc_aligned(nb, dev)
+    p = _lib_params(bins)
+    p.seed = 6
+
+    def enc():
+        st = lib.skml_dense_encode_f32(ctx, C.c_void_p(x.data_ptr()), n, C.byref(p), C.c_void_p(pl.data_ptr()), nb)
+        if st:
+            raise RuntimeError("encode failed")
+
+    enc()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        enc()
+    torch.cuda.synchronize()
+    t = (time.perf_counter() - t0) / reps
+    lib.skml_ctx_set_timing(ctx, -1)
+    lib.skml_ctx_reset_stats(ctx)
+    for _ in range(3):
+        enc()
+    ks = kernel_stats(lib, ctx)
+    lib.skml_ctx_set_timing(ctx, 0)
+    hdr = _lib_header(lib, ctx, pl)
+    alg = (8.0 + hdr.code_bits / 8.0) * n
+    res = {"workload": "2^28-float (1 GiB) dense gradient, 256 requested bins, encode", "ms": round(t * 1e3, 4),
+           "gbps_fp32_in": round(4.0 * n / t / 1e9, 1), "roofline_frac_9B": round(alg / t / 1e9 / HBM_PEAK_GBS, 4),
+           "bin_num_effective": hdr.bin_num,
+           "kernels_us": {k: round(v["avg_us"], 2) for k, v in ks.items()}}
+    if "k_quantize" in ks:
+        q = ks["k_quantize"]["avg_us"] * 1e-6
+        res["k_quantize_gbps"] = round((4.0 + hdr.code_bits / 8.0) * n / q / 1e9, 1)
+    del x, pl
+    return res
+
+
+def _lib_header(lib, ctx, payload):
+    from sketchml_amd import _lib
+    hdr = _lib.DenseHeader()
+    lib.skml_dense_info(ctx, C.c_void_p(payload.data_ptr()), C.byref(hdr), None, 0)
+    return hdr
+
+
+def host_path_rates(lib, ctx, x, n, params, reps=5):
+    """fp32-in GB/s of skml_dense_encode_host_f32 (host gradient -> device -> encode -> payload
+    bytes back in host memory, synchronous), from pageable memory (a numpy array, as a JVM
+    float[] pinned by GetPrimitiveArrayCritical is) and from skml_host_alloc pinned memory (a Java
+    direct ByteBuffer), plus the PCIe copy rates alone for the same byte counts."""
+    from sketchml_amd import _lib
+    host = x.cpu().numpy()
+    cap = lib.skml_dense_payload_bytes(n, params.bin_num)
+    out = np.zeros(cap, dtype=np.uint8)
+    wrote = C.c_size_t()
+    res = {}
+
+    def run(src_ptr, dst_ptr):
+        st = lib.skml_dense_encode_host_f32(ctx, src_ptr, n, C.byref(params), dst_ptr, cap, C.byref(wrote))
+        if st:
+            raise RuntimeError(_lib.last_error())
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            lib.skml_dense_encode_host_f32(ctx, src_ptr, n, C.byref(params), dst_ptr, cap, C.byref(wrote))
+        return (time.perf_counter() - t0) / reps
+
+    t = run(host.ctypes.data_as(C.c_void_p), out.ctypes.data_as(C.c_void_p))
+    res["pageable"] = {"ms": round(t * 1e3, 3), "gbps_fp32_in": round(4.0 * n / t / 1e9, 2)}
+    px, pp = C.c_void_p(), C.c_void_p()
+    if lib.skml_host_alloc(4 * n, C.byref(px)) == 0 and lib.skml_host_alloc(cap, C.byref(pp)) == 0:
+        np.ctypeslib.as_array(C.cast(px, C.POINTER(C.c_float)), shape=(n,))[:] = host
+        t = run(px, pp)
+        res["pinned"] = {"ms": round(t * 1e3, 3), "gbps_fp32_in": round(4.0 * n / t / 1e9, 2)}
+        # the PCIe floor for the same bytes: H2D of the input + D2H of the payload, pinned
+        pin_x = torch.from_numpy(host).pin_memory()
+        d = torch.empty(n, dtype=torch.float32, device="cuda")
+        pin_o = torch.empty(wrote.value, dtype=torch.uint8).pin_memory()
+        do = torch.empty(wrote.value, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            d.copy_(pin_x, non_blocking=True)
+            pin_o.copy_(do, non_blocking=True)
+        torch.cuda.synchronize()
+        t = (time.perf_counter() - t0) / reps
+        res["pcie_copies_only"] = {"ms": round(t * 1e3, 3), "gbps_fp32_in": round(4.0 * n / t / 1e9, 2)}
+    lib.skml_host_free(px)
+    lib.skml_host_free(pp)
+    res["payload_bytes"] = wrote.value
+    return res
+
+
+def _workload_label(args, world):
+    """config.workload from the run's own arguments (BASELINE configs named where they match)."""
+    n, bins = args.n, args.bins
+    npow = f"2^{n.bit_length() - 1}" if n & (n - 1) == 0 else str(n)
+    tag = ""
+    if (args.quant, args.dtype) == ("quantile", "f32"):
+        if n == 2**26 and bins == 256:
+            tag = "C4: " if world > 1 else "C2: "
+        elif n == 2**27 and bins == 4 and world > 1:
+            tag = "C5 shard: "
+    kind = "" if (args.quant, args.dtype) == ("quantile", "f32") else f"{args.quant} quantizer, {args.dtype} input, "
+    return (f"{tag}{npow}-{'double' if args.dtype == 'f64' else 'float'} dense gradient bucket per GPU, "
+            f"{bins} requested bins, {kind}encode" + (" + RCCL all-gather of payloads" if world > 1 else ""))
 
 
 def _lib_params(bins):
@@ -350,22 +490,11 @@ def main():
         extras["decode_l2_err"] = l2
         extras["decode_rmse"] = l2 / np.sqrt(n)
         extras["decode_rel_l2"] = l2 / float(torch.linalg.vector_norm(x.double()).item())
-        # end-to-end with PCIe: pinned host gradient -> device -> encode -> payload back to host
-        if rank == 0:
-            host = torch.empty(n, dtype=x.dtype, pin_memory=True)
-            host.copy_(x.cpu())
-            hp = torch.empty(nb, dtype=torch.uint8, pin_memory=True)
-            xd = torch.empty(n, dtype=x.dtype, device=dev)
-            reps = 5
-            torch.cuda.synchronize()
-            ta = time.perf_counter()
-            for _ in range(reps):
-                xd.copy_(host, non_blocking=True)
-                encode(ctx, C.c_void_p(xd.data_ptr()), n, C.byref(params), C.c_void_p(payload.data_ptr()), nb)
-                hp.copy_(payload, non_blocking=True)
-            torch.cuda.synchronize()
-            tb = time.perf_counter()
-            extras["h2d_d2h_inclusive_gbps"] = round(esize * n * reps / (tb - ta) / 1e9, 2)
+        # end-to-end with PCIe through the host entry point (the JNI path): host float[] ->
+        # skml_dense_encode_host_f32 -> payload bytes in host memory
+        if rank == 0 and args.dtype == "f32" and args.quant == "quantile":
+            extras["host_path"] = host_path_rates(lib, ctx, x, n, params)
+            extras["h2d_d2h_inclusive_gbps"] = extras["host_path"]["pageable"]["gbps_fp32_in"]
 
     # ---- N > 1: the exchange step alone, and a check of the gathered payloads ----
     if exch is not None and not args.no_extras:
@@ -400,7 +529,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.quant == "quantile" and args.dtype == "f32":
-        cpu = cpu_baseline(xs[0][: 2**22].cpu().numpy(), bins, args.cpu_seconds)
+        cpu = cpu_baseline(xs[0][: 2**24].cpu().numpy(), bins, args.cpu_seconds)
 
     if exch is not None:
         exch.close()
@@ -410,10 +539,7 @@ def main():
             "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": args.dtype, "data": "synthetic N(0,1), torch generator",
-            "config": {"workload": ("C2: 2^26-float dense gradient bucket per GPU, 256 requested bins, "
-                                    + ("" if (args.quant, args.dtype) == ("quantile", "f32")
-                                       else f"{args.quant} quantizer, {args.dtype} input, ")
-                                    + "encode" + (" + RCCL all-gather of payloads (C4)" if world > 1 else "")),
+            "config": {"workload": _workload_label(args, world),
                        "n_per_gpu": n, "bins": bins, "rotating_buffers": nbuf, "parallelism": f"dp{world}"},
             "roofline": roofline, "cpu_baseline": cpu, "extras": extras,
         }

@@ -224,6 +224,26 @@ int skml_dense_serialize_ref(skml_ctx* ctx, const void* payload_dev, uint8_t* bu
 int skml_dense_deserialize_ref(skml_ctx* ctx, const uint8_t* buf_host, size_t len,
                                void* payload_dev, size_t payload_cap);
 
+/* ---- Host memory in and out (the JNI path: a JVM float[] on its way to a socket) ---- */
+
+/* Pinned host memory (hipHostMalloc): a Java direct ByteBuffer over it (JNI NewDirectByteBuffer)
+ * lets the host entry points DMA the gradient without the staging copy. */
+int skml_host_alloc(size_t bytes, void** out);
+int skml_host_free(void* p);
+
+/* DenseVectorCompressor.compressDense (sample/DenseVectorCompressor.java:34-41) from host memory:
+ * x_host (pageable or pinned) -> device -> QuantileQuantizer.quantize (as skml_dense_encode_f32)
+ * -> the payload (header, splits, packed codes) back in payload_host.  Pageable input is staged
+ * through library-owned pinned buffers, the host copy of one piece overlapping the DMA of the
+ * previous one.  payload_host NULL: *written = an upper bound of the payload size.  Otherwise
+ * *written = the bytes written (codes_offset + ceil(n * code_bits / 8)).  Synchronising. */
+int skml_dense_encode_host_f32(skml_ctx* ctx, const float* x_host, int64_t n, const skml_params* params,
+                               void* payload_host, size_t payload_cap, size_t* written);
+/* DenseVectorCompressor.decompressDense (DenseVectorCompressor.java:84-91) from a host payload
+ * (as written above) into a host float[n].  Synchronising. */
+int skml_dense_decode_host_f32(skml_ctx* ctx, const void* payload_host, size_t payload_len, float* out_host,
+                               int64_t n);
+
 /* ---- Sparse path: SketchGradient.fromSparse / SparseVectorCompressor ---- */
 
 typedef struct skml_sparse skml_sparse; /* library-owned; free with skml_sparse_free */

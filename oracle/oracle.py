@@ -371,3 +371,51 @@ def bench_dense_encode(x_f32, bin_num=256, seed=0, reps=1):
     t = lib().orc_bench_dense_encode(x.ctypes.data_as(C.POINTER(C.c_float)), len(x), bin_num, seed,
                                      reps, _p(codes, u8p))
     return t, codes
+
+
+# ---------------------------------------------------------------- CPU baseline (bench.py)
+class CpbHeader(C.Structure):
+    _fields_ = [("bin_num", C.c_int32), ("zero_idx", C.c_int32), ("status", C.c_int32), ("pad", C.c_int32),
+                ("min", C.c_double), ("max", C.c_double)]
+
+
+_cpb = None
+
+
+def cpb_lib():
+    """oracle/cpu_baseline.cpp: the reference's dense encode (quantize / parallelQuantize +
+    (parallel)quantizeToBins) in optimised C++ on host threads -- bench.py's CPU baseline."""
+    global _cpb
+    if _cpb is None:
+        so = os.path.join(_HERE, "_build", "libskml_cpubase.so")
+        if not os.path.exists(so):
+            subprocess.check_call(["make", "-s", "-C", _HERE])
+        L = C.CDLL(so)
+        fp = C.POINTER(C.c_float)
+        L.cpb_encode.argtypes = [fp, C.c_int32, C.c_int32, C.c_int64, C.c_int32, u8p, C.POINTER(CpbHeader), dblp]
+        L.cpb_encode.restype = C.c_int
+        L.cpb_bench.argtypes = [fp, C.c_int32, C.c_int32, C.c_int64, C.c_int32, C.c_int32, u8p]
+        L.cpb_bench.restype = C.c_double
+        _cpb = L
+    return _cpb
+
+
+def cpu_encode(x_f32, bin_num=256, seed=0, threads=1):
+    """One CPU-baseline encode: (header, splits, 1-byte (bin - 128) codes)."""
+    x = np.ascontiguousarray(x_f32, dtype=np.float32)
+    codes = np.zeros(max(len(x), 1), dtype=np.uint8)
+    h = CpbHeader()
+    sp = np.zeros(max(bin_num - 1, 1), dtype=np.float64)
+    st = cpb_lib().cpb_encode(x.ctypes.data_as(C.POINTER(C.c_float)), len(x), bin_num, seed, threads,
+                              _p(codes, u8p), C.byref(h), _p(sp, dblp))
+    if st:
+        raise OracleError(st, "cpu_encode")
+    return h, sp[: h.bin_num - 1], codes[: len(x)]
+
+
+def cpu_bench(x_f32, bin_num=256, seed=0, threads=1, reps=1):
+    """Wall seconds of `reps` CPU-baseline encodes."""
+    x = np.ascontiguousarray(x_f32, dtype=np.float32)
+    codes = np.zeros(max(len(x), 1), dtype=np.uint8)
+    return cpb_lib().cpb_bench(x.ctypes.data_as(C.POINTER(C.c_float)), len(x), bin_num, seed, threads, reps,
+                               _p(codes, u8p))

@@ -97,6 +97,10 @@ _SIGS = {
     "skml_dense_times_by": (C.c_int, [vp, vp, C.c_double]),
     "skml_dense_serialize_ref": (C.c_int, [vp, vp, u8p, C.c_size_t, szp]),
     "skml_dense_deserialize_ref": (C.c_int, [vp, u8p, C.c_size_t, vp, C.c_size_t]),
+    "skml_host_alloc": (C.c_int, [C.c_size_t, C.POINTER(vp)]),
+    "skml_host_free": (C.c_int, [vp]),
+    "skml_dense_encode_host_f32": (C.c_int, [vp, vp, i64, C.POINTER(Params), vp, C.c_size_t, szp]),
+    "skml_dense_decode_host_f32": (C.c_int, [vp, vp, C.c_size_t, vp, i64]),
     "skml_sparse_compact_f32": (C.c_int, [vp, vp, i64, vp, vp, i64p]),
     "skml_sparse_encode_kv_f32": (C.c_int, [vp, vp, vp, i64, C.POINTER(Params), C.POINTER(vp)]),
     "skml_sparse_encode_f32": (C.c_int, [vp, vp, i64, C.POINTER(Params), C.POINTER(vp)]),

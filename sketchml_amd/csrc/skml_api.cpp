@@ -4,11 +4,15 @@
 #include <rccl/rccl.h>
 
 #include <cmath>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "skml_internal.h"
@@ -75,6 +79,16 @@ struct skml_ctx {
     size_t scratch_cap[kScratchSlots] = {};
     void* pinned = nullptr;
     size_t pinned_cap = 0;
+    // host-memory entry points (skml_dense_encode_host_f32 / _decode_host_f32): device copies of
+    // the input / payload, two pinned staging buffers and a pool of host copy threads
+    void* hx = nullptr;
+    size_t hx_cap = 0;
+    void* hp = nullptr;
+    size_t hp_cap = 0;
+    void* hpin[2] = {nullptr, nullptr};
+    size_t hpin_cap = 0;
+    hipEvent_t hev[2] = {nullptr, nullptr};
+    struct CopyPool* pool = nullptr;
     // per-kernel event timing (skml_ctx_set_timing)
     int timing = 0;  // bit k: time kernel id k
     std::vector<hipEvent_t> ev[SKML_K_COUNT];  // start/stop pairs
@@ -278,6 +292,8 @@ struct Tree {
 
 bool valid_payload_ptr(const void* p) { return p && (((uintptr_t)p) % 256 == 0); }
 
+void destroy_host_path(skml_ctx* c);
+
 }  // namespace
 
 extern "C" {
@@ -348,6 +364,7 @@ int skml_ctx_destroy(skml_ctx* c) {
     for (int i = 0; i < kScratchSlots; i++)
         if (c->scratch[i]) (void)hipFree(c->scratch[i]);
     if (c->pinned) (void)hipHostFree(c->pinned);
+    destroy_host_path(c);
     if (c->own_stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return SKML_OK;
@@ -1312,6 +1329,274 @@ int skml_allgather(skml_ctx* c, skml_comm* cm, const void* payload, size_t bytes
     ncclResult_t r = ncclAllGather(payload, all, bytes, ncclUint8, cm->comm, c->stream);
     if (r != ncclSuccess) return fail(SKML_E_RCCL, "ncclAllGather: %s", ncclGetErrorString(r));
     return SKML_OK;
+}
+
+}  // extern "C"
+
+// =============================================================================================
+// Host-memory entry points: the path starts and ends in a JVM float[] / byte[] (north star).
+// Pageable host memory is staged through two library-owned pinned buffers: host threads copy
+// piece i+1 into one while the DMA engine moves piece i out of the other, so the pageable copy
+// runs beside the PCIe transfer instead of before it.  Pinned caller memory (skml_host_alloc,
+// e.g. behind a Java direct ByteBuffer) is transferred directly.
+// =============================================================================================
+struct CopyPool {
+    std::vector<std::thread> th;
+    std::mutex m;
+    std::condition_variable cv, done_cv;
+    std::function<void(int)> job;
+    int parts = 0, next = 0, done = 0;
+    uint64_t gen = 0;
+    bool stop = false;
+    explicit CopyPool(int n) {
+        for (int i = 0; i < n; i++) th.emplace_back([this] { run(); });
+    }
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> g(m);
+            stop = true;
+        }
+        cv.notify_all();
+        for (auto& t : th) t.join();
+    }
+    void run() {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> lk(m);
+        while (true) {
+            cv.wait(lk, [&] { return stop || gen != seen; });
+            if (stop) return;
+            seen = gen;
+            while (next < parts) {
+                const int k = next++;
+                lk.unlock();
+                job(k);
+                lk.lock();
+                if (++done == parts) done_cv.notify_all();
+            }
+        }
+    }
+    // f(0..parts-1) on the pool plus the calling thread; returns when all are done
+    void parallel(int nparts, const std::function<void(int)>& f) {
+        std::unique_lock<std::mutex> lk(m);
+        job = f;
+        parts = nparts;
+        next = 0;
+        done = 0;
+        gen++;
+        cv.notify_all();
+        while (next < parts) {
+            const int k = next++;
+            lk.unlock();
+            f(k);
+            lk.lock();
+            if (++done == parts) done_cv.notify_all();
+        }
+        done_cv.wait(lk, [&] { return done == parts; });
+        parts = 0;
+    }
+};
+
+namespace {
+
+constexpr size_t kHostPiece = 8u << 20;  // bytes per staged piece
+
+void destroy_host_path(skml_ctx* c) {
+    delete c->pool;
+    c->pool = nullptr;
+    for (int b = 0; b < 2; b++) {
+        if (c->hpin[b]) (void)hipHostFree(c->hpin[b]);
+        if (c->hev[b]) (void)hipEventDestroy(c->hev[b]);
+        c->hpin[b] = nullptr;
+        c->hev[b] = nullptr;
+    }
+    if (c->hx) (void)hipFree(c->hx);
+    if (c->hp) (void)hipFree(c->hp);
+    c->hx = c->hp = nullptr;
+}
+
+int ensure_dev_buf(void** p, size_t* cap, size_t bytes, hipStream_t st) {
+    if (bytes <= *cap) return SKML_OK;
+    if (*p) {
+        HIP_TRY(hipStreamSynchronize(st));
+        HIP_TRY(hipFree(*p));
+        *p = nullptr;
+        *cap = 0;
+    }
+    const size_t want = align_up(bytes, 1u << 20);
+    if (hipMalloc(p, want) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(SKML_E_OOM, "device buffer of %zu B", want);
+    }
+    *cap = want;
+    return SKML_OK;
+}
+
+int ensure_host_path(skml_ctx* c) {
+    if (!c->hpin[0]) {
+        for (int b = 0; b < 2; b++) {
+            if (hipHostMalloc(&c->hpin[b], kHostPiece, hipHostMallocDefault) != hipSuccess)
+                return fail(SKML_E_OOM, "pinned staging of %zu B", kHostPiece);
+            HIP_TRY(hipEventCreateWithFlags(&c->hev[b], hipEventDisableTiming));
+        }
+        c->hpin_cap = kHostPiece;
+    }
+    if (!c->pool) {
+        int n = 4;  // host copy threads besides the caller (SKML_HOST_THREADS overrides)
+        if (const char* e = std::getenv("SKML_HOST_THREADS")) n = std::max(0, std::min(64, std::atoi(e)));
+        c->pool = new CopyPool(n);
+    }
+    return SKML_OK;
+}
+
+// memcpy on the pool, split into cache-friendly slices
+void pool_copy(skml_ctx* c, void* dst, const void* src, size_t bytes) {
+    const size_t slice = 1u << 20;
+    const int parts = (int)((bytes + slice - 1) / slice);
+    if (parts <= 1) {
+        std::memcpy(dst, src, bytes);
+        return;
+    }
+    c->pool->parallel(parts, [&](int k) {
+        const size_t o = (size_t)k * slice, len = std::min(slice, bytes - o);
+        std::memcpy((char*)dst + o, (const char*)src + o, len);
+    });
+}
+
+bool is_pinned(const void* p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();  // a plain pageable pointer: not an error for us
+        return false;
+    }
+    return a.type == hipMemoryTypeHost && a.hostPointer != nullptr;
+}
+
+// host -> device, staged through the pinned pair unless the source is pinned itself
+int upload(skml_ctx* c, void* dev, const void* host, size_t bytes) {
+    if (!bytes) return SKML_OK;
+    if (is_pinned(host)) {
+        HIP_TRY(hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, c->stream));
+        return SKML_OK;
+    }
+    size_t off = 0;
+    for (int i = 0; off < bytes; i++) {
+        const int b = i & 1;
+        const size_t len = std::min(kHostPiece, bytes - off);
+        if (i >= 2) HIP_TRY(hipEventSynchronize(c->hev[b]));  // the DMA out of buffer b is done
+        pool_copy(c, c->hpin[b], (const char*)host + off, len);
+        HIP_TRY(hipMemcpyAsync((char*)dev + off, c->hpin[b], len, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipEventRecord(c->hev[b], c->stream));
+        off += len;
+    }
+    return SKML_OK;
+}
+
+// device -> host (synchronous: returns with the bytes in `host`)
+int download(skml_ctx* c, void* host, const void* dev, size_t bytes) {
+    if (!bytes) {
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        return SKML_OK;
+    }
+    if (is_pinned(host)) {
+        HIP_TRY(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        return SKML_OK;
+    }
+    const size_t pieces = (bytes + kHostPiece - 1) / kHostPiece;
+    auto issue = [&](size_t i) -> int {
+        const int b = (int)(i & 1);
+        const size_t off = i * kHostPiece, len = std::min(kHostPiece, bytes - off);
+        HIP_TRY(hipMemcpyAsync(c->hpin[b], (const char*)dev + off, len, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipEventRecord(c->hev[b], c->stream));
+        return SKML_OK;
+    };
+    int st = issue(0);
+    if (!st && pieces > 1) st = issue(1);
+    for (size_t i = 0; i < pieces && !st; i++) {
+        const int b = (int)(i & 1);
+        const size_t off = i * kHostPiece, len = std::min(kHostPiece, bytes - off);
+        HIP_TRY(hipEventSynchronize(c->hev[b]));
+        pool_copy(c, (char*)host + off, c->hpin[b], len);
+        if (i + 2 < pieces) st = issue(i + 2);
+    }
+    return st;
+}
+
+}  // namespace
+
+extern "C" {
+
+int skml_host_alloc(size_t bytes, void** out) {
+    if (!out) return fail(SKML_E_ARG, "out is NULL");
+    *out = nullptr;
+    if (hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(SKML_E_OOM, "pinned host allocation of %zu B", bytes);
+    }
+    return SKML_OK;
+}
+
+int skml_host_free(void* p) {
+    if (p) HIP_TRY(hipHostFree(p));
+    return SKML_OK;
+}
+
+// Bytes of the payload the host entry points write (header, splits, codes): a size query before
+// the encode, exact after it (skml_dense_encode_host_f32's *written).
+int skml_dense_encode_host_f32(skml_ctx* c, const float* x, int64_t n, const skml_params* p, void* payload,
+                               size_t cap, size_t* written) {
+    skml_params def;
+    if (!p) {
+        skml_params_default(&def);
+        p = &def;
+    }
+    if (!c) return fail(SKML_E_ARG, "ctx is NULL");
+    if (n < 0 || n > 0x7FFFFFFFLL) return fail(SKML_E_ARG, "n=%lld outside Java int range", (long long)n);
+    if (p->bin_num < 2 || p->bin_num > SKML_MAX_BINS) return fail(SKML_E_ARG, "Invalid partition number: %d", p->bin_num);
+    const size_t nb = skml_dense_payload_bytes(n, p->bin_num);
+    if (!payload) {  // size query: an upper bound of the bytes written
+        if (written) *written = nb;
+        return SKML_OK;
+    }
+    if (n > 0 && !x) return fail(SKML_E_ARG, "x is NULL");
+    HIP_TRY(hipSetDevice(c->device));
+    int st;
+    if ((st = ensure_host_path(c))) return st;
+    if ((st = ensure_dev_buf(&c->hx, &c->hx_cap, std::max<size_t>(16, 4 * (size_t)n), c->stream))) return st;
+    if ((st = ensure_dev_buf(&c->hp, &c->hp_cap, nb, c->stream))) return st;
+    if ((st = upload(c, c->hx, x, 4 * (size_t)n))) return st;
+    if ((st = skml_dense_encode_f32(c, (const float*)c->hx, n, p, c->hp, c->hp_cap))) return st;
+    skml_dense_header h;
+    HIP_TRY(hipMemcpyAsync(&h, c->hp, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (h.status == SKML_E_NAN) return fail(SKML_E_NAN, "Encounter NaN value");
+    const size_t used = (size_t)h.codes_offset + ((size_t)n * (size_t)h.code_bits + 7) / 8;
+    if (written) *written = used;
+    if (cap < used) return fail(SKML_E_ARG, "payload capacity %zu < %zu", cap, used);
+    return download(c, payload, c->hp, used);
+}
+
+// decompressDense from a host payload into a host float[] (payload bytes as written above).
+int skml_dense_decode_host_f32(skml_ctx* c, const void* payload, size_t len, float* out, int64_t n) {
+    if (!c || !payload || len < sizeof(skml_dense_header) || (n > 0 && !out)) return fail(SKML_E_ARG, "bad arguments");
+    skml_dense_header h;
+    std::memcpy(&h, payload, sizeof(h));
+    if (h.magic != SKML_DENSE_MAGIC) return fail(SKML_E_STATE, "not a dense payload");
+    if (h.status != SKML_OK) return fail(h.status == SKML_E_NAN ? SKML_E_NAN : SKML_E_STATE, "payload status %d", h.status);
+    if (h.n != n) return fail(SKML_E_ARG, "payload holds %lld values, asked for %lld", (long long)h.n, (long long)n);
+    if (h.bin_num < 2 || h.bin_num > h.req_bins || h.req_bins > SKML_MAX_BINS || h.code_bits != code_bits_for(h.bin_num) ||
+        h.codes_offset != (int64_t)dense_codes_offset(h.req_bins))
+        return fail(SKML_E_ARG, "inconsistent payload header");
+    const size_t used = (size_t)h.codes_offset + ((size_t)n * (size_t)h.code_bits + 7) / 8;
+    if (len < used) return fail(SKML_E_ARG, "payload of %zu B, header needs %zu", len, used);
+    HIP_TRY(hipSetDevice(c->device));
+    int st;
+    if ((st = ensure_host_path(c))) return st;
+    if ((st = ensure_dev_buf(&c->hp, &c->hp_cap, skml_dense_payload_bytes(n, h.req_bins), c->stream))) return st;
+    if ((st = ensure_dev_buf(&c->hx, &c->hx_cap, std::max<size_t>(16, 4 * (size_t)n), c->stream))) return st;
+    if ((st = upload(c, c->hp, payload, used))) return st;
+    if ((st = skml_dense_decode_f32(c, c->hp, (float*)c->hx, n))) return st;
+    return download(c, out, c->hx, 4 * (size_t)n);
 }
 
 }  // extern "C"

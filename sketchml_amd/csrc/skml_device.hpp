@@ -470,6 +470,16 @@ __device__ __forceinline__ void build_quant_lut(const float* sp, int nsplit, Qua
     if (t == 0) lut->cmax = (s_misc[1] <= kLutMaxNeed && nsplit <= kLutMaxSplits) ? s_misc[1] : -1;
 }
 
+// Zero the payload bytes between the last written split and the codes (unused split slots after
+// Maths.unique, and the 256-B alignment pad), so an encode's payload bytes are a pure function of
+// its input and seed (determinism, and byte-equal payloads from any buffer).  Block-strided.
+__device__ __forceinline__ void payload_zero_tail(uint8_t* payload, int nsplit_written, int req_bins) {
+    double* sp = reinterpret_cast<double*>(payload + kHeaderBytes);
+    const int end = (int)((dense_codes_offset(req_bins) - kHeaderBytes) / sizeof(double));
+    for (int i = (nsplit_written > 0 ? nsplit_written : 0) + (int)threadIdx.x; i < end; i += (int)blockDim.x)
+        sp[i] = 0.0;
+}
+
 // ------------------------------------------------------------------------------------------
 // Quantizer.indexOf (Quantizer.java:49-72), literally: used for split tables on which it is not
 // an upper bound (NaN or descending splits of a degenerate uniform range) and for NaN values.

@@ -227,6 +227,7 @@ __global__ __launch_bounds__(512) void k_summary64(const double* __restrict__ x,
         if (fmax > vmax) vmax = fmax;   // Math.max(Double.MIN_VALUE, x)
     }
     if (S.flags & 1u) {  // NaN: QuantileSketchException("Encounter NaN value")
+        payload_zero_tail(reinterpret_cast<uint8_t*>(hdr), 0, req_bins);
         if (t == 0) write_header(hdr, SKML_E_NAN, n_hdr, req_bins, 0, req_bins, vmin, vmax);
         return;
     }
@@ -306,6 +307,7 @@ __global__ __launch_bounds__(512) void k_summary64(const double* __restrict__ x,
         bin_num = (int)S.total + 1;
     }
     __syncthreads();
+    payload_zero_tail(reinterpret_cast<uint8_t*>(hdr), bin_num - 1, req_bins);
     if (t == 0) {
         int zero;
         if (vmin > 0.0) zero = 0;
@@ -748,6 +750,7 @@ __global__ __launch_bounds__(256) void k_uni_finish(const T* __restrict__ x, int
     const int ns = bin_num - 1;
     const double jmin = s_mn, jmax = s_mx;
     const bool lut_ok = !s_bad && ns <= kLutMaxSplits;
+    payload_zero_tail(reinterpret_cast<uint8_t*>(hdr), ns, bin_num);
     if (lut_ok) build_quant_lut(s_sp, ns, lut, s_misc, s_lbuf);
     if (threadIdx.x == 0) {
         if (s_bad) lut->cmax = kLutJavaMode;

@@ -906,6 +906,7 @@ __device__ void summary_block(const SummaryArgs& a, SummaryShared& S) {
         if (fmax > vmax) vmax = fmax;   // Math.max(Double.MIN_VALUE, x)
     }
     if (S.flags & 1u) {  // NaN: QuantileSketchException("Encounter NaN value")
+        payload_zero_tail(a.payload, 0, req_bins);
         if (t == 0) {
             hdr->magic = SKML_DENSE_MAGIC;
             hdr->status = SKML_E_NAN;
@@ -1007,6 +1008,7 @@ __device__ void summary_block(const SummaryArgs& a, SummaryShared& S) {
         bin_num = (int)S.total + 1;
     }
     __syncthreads();
+    payload_zero_tail(a.payload, bin_num - 1, req_bins);
     SKML_PROF(8);
     if (t == 0) {
         int zero;
@@ -1277,6 +1279,7 @@ __global__ __launch_bounds__(256) void k_set_splits(uint8_t* payload, int64_t n,
         if (i < kLutMaxSplits) s_sp[i] = __double2float_ru(sp[i]);
         if (!(sp[i] < 0.0)) atomicMin(&s_zero, i);
     }
+    payload_zero_tail(payload, nsplits, req_bins);
     __syncthreads();
     if (nsplits <= kLutMaxSplits) build_quant_lut(s_sp, nsplits, lut, s_misc, s_lbuf);
     else if (threadIdx.x == 0) lut->cmax = -1;
