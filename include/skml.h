@@ -236,13 +236,29 @@ int skml_host_free(void* p);
  * -> the payload (header, splits, packed codes) back in payload_host.  Pageable input is staged
  * through library-owned pinned buffers, the host copy of one piece overlapping the DMA of the
  * previous one.  payload_host NULL: *written = an upper bound of the payload size.  Otherwise
- * *written = the bytes written (codes_offset + ceil(n * code_bits / 8)).  Synchronising. */
+ * *written = the bytes written (codes_offset + ceil(n * code_bits / 8)).  params->parallelism > 1
+ * selects parallelQuantize (QuantileQuantizer.java:53-92) with that many slices, as on the sparse
+ * path (params->dedup then applies as given).  Synchronising. */
 int skml_dense_encode_host_f32(skml_ctx* ctx, const float* x_host, int64_t n, const skml_params* params,
                                void* payload_host, size_t payload_cap, size_t* written);
+/* The reference's own double[] input (QuantileQuantizer.quantize(double[]), no fp32 rounding):
+ * as skml_dense_encode_host_f32 over skml_dense_encode_f64. */
+int skml_dense_encode_host_f64(skml_ctx* ctx, const double* x_host, int64_t n, const skml_params* params,
+                               void* payload_host, size_t payload_cap, size_t* written);
 /* DenseVectorCompressor.decompressDense (DenseVectorCompressor.java:84-91) from a host payload
- * (as written above) into a host float[n].  Synchronising. */
+ * (as written above) into a host float[n] / double[n].  Synchronising. */
 int skml_dense_decode_host_f32(skml_ctx* ctx, const void* payload_host, size_t payload_len, float* out_host,
                                int64_t n);
+int skml_dense_decode_host_f64(skml_ctx* ctx, const void* payload_host, size_t payload_len, double* out_host,
+                               int64_t n);
+/* Host payloads without a device (pure host code):
+ *   skml_dense_info_host     Quantizer.getBinNum/getSplits/getZeroIdx/getMin/getMax/getN
+ *   skml_dense_bins_host     Quantizer.getBins() (Quantizer.java:163-165): unpacked int32 bins
+ *   skml_dense_times_by_host Quantizer.timesBy (Quantizer.java:119-124), in place */
+int skml_dense_info_host(const void* payload_host, size_t payload_len, skml_dense_header* hdr, double* splits_host,
+                         int32_t splits_cap);
+int skml_dense_bins_host(const void* payload_host, size_t payload_len, int32_t* bins_host, int64_t n);
+int skml_dense_times_by_host(void* payload_host, size_t payload_len, double x);
 
 /* ---- Sparse path: SketchGradient.fromSparse / SparseVectorCompressor ---- */
 
@@ -306,6 +322,10 @@ int skml_sparse_deserialize(skml_ctx* ctx, const uint8_t* buf_host, size_t len, 
  * their int32 bins, on the device.  Synchronising. */
 int skml_sparse_restore_bins(skml_ctx* ctx, const skml_sparse* s, int32_t* keys_dev, int32_t* bins_dev);
 int skml_sparse_free(skml_sparse* s);
+/* Host-memory forms of encode_kv / decode (int[] keys and float[] values in JVM arrays). */
+int skml_sparse_encode_kv_host_f32(skml_ctx* ctx, const int32_t* keys_host, const float* vals_host, int64_t nnz,
+                                   const skml_params* params, skml_sparse** out);
+int skml_sparse_decode_host_f32(skml_ctx* ctx, const skml_sparse* s, int32_t* keys_host, float* vals_host);
 
 /* ---- DeltaAdaptiveEncoder as a standalone BinaryEncoder (base/BinaryEncoder.java:6-11) ---- */
 /* encode(int[]): keys strictly increasing (keys[0] >= 0).  Outputs the choice and the two
@@ -317,6 +337,15 @@ int skml_delta_encode(skml_ctx* ctx, const int32_t* keys_dev, int64_t n, int32_t
 int skml_delta_decode(skml_ctx* ctx, int64_t n, int32_t num_intervals, int32_t flag_kind,
                       const uint64_t* flag_words_dev, int64_t n_flag_words,
                       const uint64_t* delta_words_dev, int64_t n_delta_words, int32_t* keys_dev);
+
+/* Host-memory forms (a JVM int[] in, BitSet.toLongArray long[]s out, and back): words_cap is the
+ * capacity of each word array; NULL word arrays query the bit counts only. */
+int skml_delta_encode_host(skml_ctx* ctx, const int32_t* keys_host, int64_t n, int32_t* num_intervals,
+                           int32_t* flag_kind, int64_t* n_flag_bits, int64_t* n_delta_bits, uint64_t* flag_words_host,
+                           uint64_t* delta_words_host, int64_t words_cap);
+int skml_delta_decode_host(skml_ctx* ctx, int64_t n, int32_t num_intervals, int32_t flag_kind,
+                           const uint64_t* flag_words_host, int64_t n_flag_words, const uint64_t* delta_words_host,
+                           int64_t n_delta_words, int32_t* keys_host);
 
 /* ---- Multi-GPU: RCCL all-gather of payloads over xGMI ---- */
 typedef struct skml_comm skml_comm;

@@ -1,0 +1,104 @@
+package org.dma.sketchml.hip;
+
+import org.apache.commons.lang3.tuple.ImmutablePair;
+import org.apache.commons.lang3.tuple.Pair;
+import org.dma.sketchml.sketch.base.Quantizer;
+import org.dma.sketchml.sketch.base.SketchMLException;
+import org.dma.sketchml.sketch.base.VectorCompressor;
+import org.dma.sketchml.sketch.common.Constants;
+
+import java.io.IOException;
+import java.io.ObjectInputStream;
+import java.io.ObjectOutputStream;
+import java.util.Arrays;
+
+/**
+ * Same surface as sample/DenseVectorCompressor.java:18-117 with the quantile quantizer on the GPU.
+ * The compressed state is the packed payload (header, splits, b-bit codes) in a byte[]; its
+ * writeObject ships those bytes (b bits per value instead of the reference's 8).
+ */
+public class HipDenseVectorCompressor implements VectorCompressor {
+    private final int binNum;
+    private final long seed;
+    private int size;
+    private byte[] payload;
+
+    public HipDenseVectorCompressor(Quantizer.QuantizationType type, int binNum) {
+        this(type, binNum, 0L);
+    }
+
+    public HipDenseVectorCompressor(Quantizer.QuantizationType type, int binNum, long seed) {
+        if (type != Quantizer.QuantizationType.QUANTILE)
+            throw new SketchMLException("HipDenseVectorCompressor implements the QUANTILE quantizer");
+        this.binNum = binNum;
+        this.seed = seed;
+    }
+
+    @Override
+    public void compressDense(double[] values) {
+        size = values.length;
+        payload = HipCodec.encodeDenseF64(HipCodec.ctx(), values, binNum, true, seed, 1);
+    }
+
+    @Override
+    public void compressSparse(int[] keys, double[] values) {  // DenseVectorCompressor.java:44-55
+        int maxKey = Arrays.stream(keys).max().orElse(0);
+        double[] dense = new double[maxKey + 1];
+        for (int i = 0; i < keys.length; i++)
+            dense[keys[i]] = values[i];
+        compressDense(dense);
+    }
+
+    @Override
+    public void parallelCompressDense(double[] values) {
+        size = values.length;
+        payload = HipCodec.encodeDenseF64(HipCodec.ctx(), values, binNum, false, seed,
+                Constants.Parallel.getParallelism());
+    }
+
+    @Override
+    public void parallelCompressSparse(int[] keys, double[] values) {
+        compressSparse(keys, values);
+    }
+
+    @Override
+    public double[] decompressDense() {
+        double[] out = new double[size];
+        HipCodec.decodeDenseF64(HipCodec.ctx(), payload, out);
+        return out;
+    }
+
+    @Override
+    public Pair<int[], double[]> decompressSparse() {
+        int[] keys = new int[size];
+        Arrays.setAll(keys, i -> i);
+        return new ImmutablePair<>(keys, decompressDense());
+    }
+
+    @Override
+    public void timesBy(double x) {
+        HipCodec.timesBy(payload, x);
+    }
+
+    @Override
+    public double size() {
+        return size;
+    }
+
+    @Override
+    public int memoryBytes() throws IOException {
+        return 12 + payload.length;
+    }
+
+    private void writeObject(ObjectOutputStream oos) throws IOException {
+        oos.writeInt(size);
+        oos.writeInt(payload.length);
+        oos.write(payload);
+    }
+
+    private void readObject(ObjectInputStream ois) throws IOException {
+        size = ois.readInt();
+        payload = new byte[ois.readInt()];
+        ois.readFully(payload);
+    }
+}

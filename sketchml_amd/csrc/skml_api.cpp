@@ -85,6 +85,8 @@ struct skml_ctx {
     size_t hx_cap = 0;
     void* hp = nullptr;
     size_t hp_cap = 0;
+    void* hk = nullptr;
+    size_t hk_cap = 0;
     void* hpin[2] = {nullptr, nullptr};
     size_t hpin_cap = 0;
     hipEvent_t hev[2] = {nullptr, nullptr};
@@ -1411,7 +1413,8 @@ void destroy_host_path(skml_ctx* c) {
     }
     if (c->hx) (void)hipFree(c->hx);
     if (c->hp) (void)hipFree(c->hp);
-    c->hx = c->hp = nullptr;
+    if (c->hk) (void)hipFree(c->hk);
+    c->hx = c->hp = c->hk = nullptr;
 }
 
 int ensure_dev_buf(void** p, size_t* cap, size_t bytes, hipStream_t st) {
@@ -1482,7 +1485,8 @@ int upload(skml_ctx* c, void* dev, const void* host, size_t bytes) {
     for (int i = 0; off < bytes; i++) {
         const int b = i & 1;
         const size_t len = std::min(kHostPiece, bytes - off);
-        if (i >= 2) HIP_TRY(hipEventSynchronize(c->hev[b]));  // the DMA out of buffer b is done
+        // the DMA out of buffer b (this call's piece i-2, or an earlier call's last pieces) is done
+        HIP_TRY(hipEventSynchronize(c->hev[b]));
         pool_copy(c, c->hpin[b], (const char*)host + off, len);
         HIP_TRY(hipMemcpyAsync((char*)dev + off, c->hpin[b], len, hipMemcpyHostToDevice, c->stream));
         HIP_TRY(hipEventRecord(c->hev[b], c->stream));
@@ -1541,10 +1545,34 @@ int skml_host_free(void* p) {
     return SKML_OK;
 }
 
-// Bytes of the payload the host entry points write (header, splits, codes): a size query before
-// the encode, exact after it (skml_dense_encode_host_f32's *written).
-int skml_dense_encode_host_f32(skml_ctx* c, const float* x, int64_t n, const skml_params* p, void* payload,
-                               size_t cap, size_t* written) {
+}  // extern "C"
+
+namespace {
+
+// the device payload written by an encode on device buffers -> bytes in use (header, splits, codes)
+size_t payload_used(const skml_dense_header& h) {
+    return (size_t)h.codes_offset + ((size_t)h.n * (size_t)h.code_bits + 7) / 8;
+}
+
+// A host payload's header, checked for self-consistency against its length.
+int host_header(const void* payload, size_t len, skml_dense_header* h, bool need_ok = true) {
+    if (!payload || len < sizeof(skml_dense_header)) return fail(SKML_E_ARG, "payload too short");
+    std::memcpy(h, payload, sizeof(*h));
+    if (h->magic != SKML_DENSE_MAGIC) return fail(SKML_E_STATE, "not a dense payload");
+    if (need_ok && h->status == SKML_E_NAN) return fail(SKML_E_NAN, "Encounter NaN value");
+    if (need_ok && h->status != SKML_OK) return fail(SKML_E_STATE, "payload status %d", h->status);
+    if (h->n < 0 || h->n > 0x7FFFFFFFLL || h->bin_num < 2 || h->bin_num > h->req_bins || h->req_bins > SKML_MAX_BINS ||
+        h->code_bits != code_bits_for(h->bin_num) || h->codes_offset != (int64_t)dense_codes_offset(h->req_bins) ||
+        h->zero_idx < 0 || h->zero_idx >= h->bin_num)
+        return fail(SKML_E_ARG, "inconsistent payload header");
+    if (h->status == SKML_OK && len < payload_used(*h))
+        return fail(SKML_E_ARG, "payload of %zu B, header needs %zu", len, payload_used(*h));
+    return SKML_OK;
+}
+
+template <typename T, typename Encode>
+int encode_host(skml_ctx* c, const T* x, int64_t n, const skml_params* p, void* payload, size_t cap, size_t* written,
+                Encode encode) {
     skml_params def;
     if (!p) {
         skml_params_default(&def);
@@ -1562,41 +1590,191 @@ int skml_dense_encode_host_f32(skml_ctx* c, const float* x, int64_t n, const skm
     HIP_TRY(hipSetDevice(c->device));
     int st;
     if ((st = ensure_host_path(c))) return st;
-    if ((st = ensure_dev_buf(&c->hx, &c->hx_cap, std::max<size_t>(16, 4 * (size_t)n), c->stream))) return st;
+    if ((st = ensure_dev_buf(&c->hx, &c->hx_cap, std::max<size_t>(16, sizeof(T) * (size_t)n), c->stream))) return st;
     if ((st = ensure_dev_buf(&c->hp, &c->hp_cap, nb, c->stream))) return st;
-    if ((st = upload(c, c->hx, x, 4 * (size_t)n))) return st;
-    if ((st = skml_dense_encode_f32(c, (const float*)c->hx, n, p, c->hp, c->hp_cap))) return st;
+    if ((st = upload(c, c->hx, x, sizeof(T) * (size_t)n))) return st;
+    if ((st = encode(c, (const T*)c->hx, n, p, c->hp, c->hp_cap))) return st;
     skml_dense_header h;
     HIP_TRY(hipMemcpyAsync(&h, c->hp, sizeof(h), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (h.status == SKML_E_NAN) return fail(SKML_E_NAN, "Encounter NaN value");
-    const size_t used = (size_t)h.codes_offset + ((size_t)n * (size_t)h.code_bits + 7) / 8;
+    const size_t used = payload_used(h);
     if (written) *written = used;
     if (cap < used) return fail(SKML_E_ARG, "payload capacity %zu < %zu", cap, used);
     return download(c, payload, c->hp, used);
 }
 
-// decompressDense from a host payload into a host float[] (payload bytes as written above).
-int skml_dense_decode_host_f32(skml_ctx* c, const void* payload, size_t len, float* out, int64_t n) {
-    if (!c || !payload || len < sizeof(skml_dense_header) || (n > 0 && !out)) return fail(SKML_E_ARG, "bad arguments");
+template <typename T, typename Decode>
+int decode_host(skml_ctx* c, const void* payload, size_t len, T* out, int64_t n, Decode decode) {
+    if (!c || (n > 0 && !out)) return fail(SKML_E_ARG, "bad arguments");
     skml_dense_header h;
-    std::memcpy(&h, payload, sizeof(h));
-    if (h.magic != SKML_DENSE_MAGIC) return fail(SKML_E_STATE, "not a dense payload");
-    if (h.status != SKML_OK) return fail(h.status == SKML_E_NAN ? SKML_E_NAN : SKML_E_STATE, "payload status %d", h.status);
+    int st = host_header(payload, len, &h);
+    if (st) return st;
     if (h.n != n) return fail(SKML_E_ARG, "payload holds %lld values, asked for %lld", (long long)h.n, (long long)n);
-    if (h.bin_num < 2 || h.bin_num > h.req_bins || h.req_bins > SKML_MAX_BINS || h.code_bits != code_bits_for(h.bin_num) ||
-        h.codes_offset != (int64_t)dense_codes_offset(h.req_bins))
-        return fail(SKML_E_ARG, "inconsistent payload header");
-    const size_t used = (size_t)h.codes_offset + ((size_t)n * (size_t)h.code_bits + 7) / 8;
-    if (len < used) return fail(SKML_E_ARG, "payload of %zu B, header needs %zu", len, used);
+    HIP_TRY(hipSetDevice(c->device));
+    if ((st = ensure_host_path(c))) return st;
+    if ((st = ensure_dev_buf(&c->hp, &c->hp_cap, skml_dense_payload_bytes(n, h.req_bins), c->stream))) return st;
+    if ((st = ensure_dev_buf(&c->hx, &c->hx_cap, std::max<size_t>(16, sizeof(T) * (size_t)n), c->stream))) return st;
+    if ((st = upload(c, c->hp, payload, payload_used(h)))) return st;
+    if ((st = decode(c, c->hp, (T*)c->hx, n))) return st;
+    return download(c, out, c->hx, sizeof(T) * (size_t)n);
+}
+
+}  // namespace
+
+extern "C" {
+
+// params->parallelism > 1 selects QuantileQuantizer.parallelQuantize with that many slices (as
+// on the sparse path); otherwise quantize.
+int skml_dense_encode_host_f32(skml_ctx* c, const float* x, int64_t n, const skml_params* p, void* payload,
+                               size_t cap, size_t* written) {
+    return encode_host<float>(c, x, n, p, payload, cap, written,
+                              [](skml_ctx* c2, const float* xd, int64_t m, const skml_params* q, void* pl, size_t cp) {
+                                  return q->parallelism > 1
+                                             ? skml_dense_encode_parallel_f32(c2, xd, m, q->parallelism, q, pl, cp)
+                                             : skml_dense_encode_f32(c2, xd, m, q, pl, cp);
+                              });
+}
+
+int skml_dense_encode_host_f64(skml_ctx* c, const double* x, int64_t n, const skml_params* p, void* payload,
+                               size_t cap, size_t* written) {
+    return encode_host<double>(c, x, n, p, payload, cap, written,
+                               [](skml_ctx* c2, const double* xd, int64_t m, const skml_params* q, void* pl, size_t cp) {
+                                   return q->parallelism > 1
+                                              ? skml_dense_encode_parallel_f64(c2, xd, m, q->parallelism, q, pl, cp)
+                                              : skml_dense_encode_f64(c2, xd, m, q, pl, cp);
+                               });
+}
+
+int skml_dense_decode_host_f32(skml_ctx* c, const void* payload, size_t len, float* out, int64_t n) {
+    return decode_host<float>(c, payload, len, out, n, skml_dense_decode_f32);
+}
+
+int skml_dense_decode_host_f64(skml_ctx* c, const void* payload, size_t len, double* out, int64_t n) {
+    return decode_host<double>(c, payload, len, out, n, skml_dense_decode_f64);
+}
+
+int skml_dense_info_host(const void* payload, size_t len, skml_dense_header* hdr, double* splits, int32_t cap) {
+    if (!hdr) return fail(SKML_E_ARG, "hdr is NULL");
+    int st = host_header(payload, len, hdr, false);
+    if (st) return st;
+    if (hdr->status == SKML_E_NAN) return fail(SKML_E_NAN, "Encounter NaN value");
+    if (splits) {
+        const int ns = hdr->bin_num - 1;
+        if (ns > cap) return fail(SKML_E_ARG, "splits capacity %d < %d", cap, ns);
+        std::memcpy(splits, (const char*)payload + kHeaderBytes, sizeof(double) * (size_t)ns);
+    }
+    return hdr->status;
+}
+
+int skml_dense_bins_host(const void* payload, size_t len, int32_t* bins, int64_t n) {
+    skml_dense_header h;
+    int st = host_header(payload, len, &h);
+    if (st) return st;
+    if (h.n != n || (n > 0 && !bins)) return fail(SKML_E_ARG, "bins of %lld values, payload holds %lld", (long long)n,
+                                                  (long long)h.n);
+    const uint8_t* codes = (const uint8_t*)payload + h.codes_offset;
+    const int b = h.code_bits;
+    for (int64_t e = 0; e < n; e++) {  // LSB-first packed codes (include/skml.h)
+        const uint64_t bit = (uint64_t)e * (uint64_t)b;
+        uint32_t v;
+        if (b == 16) v = (uint32_t)codes[2 * e] | ((uint32_t)codes[2 * e + 1] << 8);
+        else v = (codes[bit >> 3] >> (bit & 7)) & ((1u << b) - 1u);
+        bins[e] = (int32_t)v;
+    }
+    return SKML_OK;
+}
+
+int skml_dense_times_by_host(void* payload, size_t len, double x) {
+    skml_dense_header h;
+    int st = host_header(payload, len, &h);
+    if (st) return st;
+    double* sp = reinterpret_cast<double*>((char*)payload + kHeaderBytes);  // Quantizer.timesBy (:119-124)
+    for (int i = 0; i < h.bin_num - 1; i++) sp[i] *= x;
+    h.min *= x;
+    h.max *= x;
+    std::memcpy(payload, &h, sizeof(h));
+    return SKML_OK;
+}
+
+int skml_sparse_encode_kv_host_f32(skml_ctx* c, const int32_t* keys, const float* vals, int64_t nnz,
+                                   const skml_params* p, skml_sparse** out) {
+    if (!c || !out || nnz < 0 || (nnz > 0 && (!keys || !vals))) return fail(SKML_E_ARG, "bad arguments");
+    HIP_TRY(hipSetDevice(c->device));
+    int st;
+    const size_t bytes = std::max<size_t>(16, 4 * (size_t)nnz);
+    if ((st = ensure_host_path(c))) return st;
+    if ((st = ensure_dev_buf(&c->hx, &c->hx_cap, bytes, c->stream))) return st;
+    if ((st = ensure_dev_buf(&c->hk, &c->hk_cap, bytes, c->stream))) return st;
+    if ((st = upload(c, c->hk, keys, 4 * (size_t)nnz))) return st;
+    if ((st = upload(c, c->hx, vals, 4 * (size_t)nnz))) return st;
+    return skml_sparse_encode_kv_f32(c, (const int32_t*)c->hk, (const float*)c->hx, nnz, p, out);
+}
+
+int skml_sparse_decode_host_f32(skml_ctx* c, const skml_sparse* s, int32_t* keys, float* vals) {
+    int64_t n = 0;
+    if (!c || !s || skml_sparse_nnz(s, &n)) return fail(SKML_E_ARG, "bad arguments");
+    if (n > 0 && (!keys || !vals)) return fail(SKML_E_ARG, "keys/vals are NULL");
+    HIP_TRY(hipSetDevice(c->device));
+    int st;
+    const size_t bytes = std::max<size_t>(16, 4 * (size_t)n);
+    if ((st = ensure_host_path(c))) return st;
+    if ((st = ensure_dev_buf(&c->hx, &c->hx_cap, bytes, c->stream))) return st;
+    if ((st = ensure_dev_buf(&c->hk, &c->hk_cap, bytes, c->stream))) return st;
+    if ((st = skml_sparse_decode_f32(c, s, (int32_t*)c->hk, (float*)c->hx))) return st;
+    if ((st = download(c, keys, c->hk, 4 * (size_t)n))) return st;
+    return download(c, vals, c->hx, 4 * (size_t)n);
+}
+
+int skml_delta_encode_host(skml_ctx* c, const int32_t* keys, int64_t n, int32_t* num_intervals, int32_t* flag_kind,
+                           int64_t* n_flag_bits, int64_t* n_delta_bits, uint64_t* flag_words, uint64_t* delta_words,
+                           int64_t words_cap) {
+    if (!c || n <= 0 || !keys) return fail(SKML_E_ARG, "bad delta arguments");
     HIP_TRY(hipSetDevice(c->device));
     int st;
     if ((st = ensure_host_path(c))) return st;
-    if ((st = ensure_dev_buf(&c->hp, &c->hp_cap, skml_dense_payload_bytes(n, h.req_bins), c->stream))) return st;
-    if ((st = ensure_dev_buf(&c->hx, &c->hx_cap, std::max<size_t>(16, 4 * (size_t)n), c->stream))) return st;
-    if ((st = upload(c, c->hp, payload, used))) return st;
-    if ((st = skml_dense_decode_f32(c, c->hp, (float*)c->hx, n))) return st;
-    return download(c, out, c->hx, 4 * (size_t)n);
+    // a stream never exceeds 33 bits per key (16-bit flags are at most 4 bits, deltas at most 32)
+    const size_t wcap = ((size_t)n * 33 + 63) / 64 + 1;
+    if ((st = ensure_dev_buf(&c->hk, &c->hk_cap, 4 * (size_t)n, c->stream))) return st;
+    if ((st = ensure_dev_buf(&c->hx, &c->hx_cap, 8 * wcap, c->stream))) return st;
+    if ((st = ensure_dev_buf(&c->hp, &c->hp_cap, 8 * wcap, c->stream))) return st;
+    if ((st = upload(c, c->hk, keys, 4 * (size_t)n))) return st;
+    int64_t nfb = 0, ndb = 0;
+    if ((st = skml_delta_encode(c, (const int32_t*)c->hk, n, num_intervals, flag_kind, &nfb, &ndb, (uint64_t*)c->hx,
+                                (uint64_t*)c->hp, (int64_t)wcap)))
+        return st;
+    if (n_flag_bits) *n_flag_bits = nfb;
+    if (n_delta_bits) *n_delta_bits = ndb;
+    const int64_t fw = (nfb + 63) / 64, dw = (ndb + 63) / 64;
+    if (!flag_words && !delta_words) return SKML_OK;
+    if (fw > words_cap || dw > words_cap)
+        return fail(SKML_E_ARG, "words_cap %lld < needed %lld", (long long)words_cap, (long long)std::max(fw, dw));
+    if (flag_words && (st = download(c, flag_words, c->hx, 8 * (size_t)fw))) return st;
+    if (delta_words && (st = download(c, delta_words, c->hp, 8 * (size_t)dw))) return st;
+    return SKML_OK;
+}
+
+int skml_delta_decode_host(skml_ctx* c, int64_t n, int32_t num_intervals, int32_t flag_kind, const uint64_t* flag_words,
+                           int64_t n_flag_words, const uint64_t* delta_words, int64_t n_delta_words, int32_t* keys) {
+    if (!c || n <= 0 || !keys || n_flag_words < 0 || n_delta_words < 0 || (n_flag_words && !flag_words) ||
+        (n_delta_words && !delta_words))
+        return fail(SKML_E_ARG, "bad delta decode arguments");
+    HIP_TRY(hipSetDevice(c->device));
+    int st;
+    if ((st = ensure_host_path(c))) return st;
+    // zero words past the trimmed streams (BitSet.toLongArray drops trailing zero words)
+    const size_t fpad = 8 * ((size_t)n_flag_words + 64), dpad = 8 * ((size_t)n_delta_words + 64);
+    if ((st = ensure_dev_buf(&c->hx, &c->hx_cap, fpad, c->stream))) return st;
+    if ((st = ensure_dev_buf(&c->hp, &c->hp_cap, dpad, c->stream))) return st;
+    if ((st = ensure_dev_buf(&c->hk, &c->hk_cap, 4 * (size_t)n, c->stream))) return st;
+    HIP_TRY(hipMemsetAsync(c->hx, 0, fpad, c->stream));
+    HIP_TRY(hipMemsetAsync(c->hp, 0, dpad, c->stream));
+    if ((st = upload(c, c->hx, flag_words, 8 * (size_t)n_flag_words))) return st;
+    if ((st = upload(c, c->hp, delta_words, 8 * (size_t)n_delta_words))) return st;
+    if ((st = skml_delta_decode(c, n, num_intervals, flag_kind, (const uint64_t*)c->hx, n_flag_words,
+                                (const uint64_t*)c->hp, n_delta_words, (int32_t*)c->hk)))
+        return st;
+    return download(c, keys, c->hk, 4 * (size_t)n);
 }
 
 }  // extern "C"

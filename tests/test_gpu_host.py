@@ -125,3 +125,80 @@ def test_encode_host_errors(gpu):
                                             dec.ctypes.data_as(C.c_void_p), len(x)) == L.SKML_E_ARG  # truncated
     assert L.lib.skml_dense_decode_host_f32(gpu.get_context().handle, pl.ctypes.data_as(C.c_void_p), len(pl),
                                             dec.ctypes.data_as(C.c_void_p), len(x) + 1) == L.SKML_E_ARG  # wrong n
+
+
+def test_encode_host_f64_and_host_helpers(gpu):
+    """The double[] entry (the reference's own input), getBins / info / timesBy on the host
+    payload, and decode back into a double[]."""
+    L = _L()
+    ctx = gpu.get_context()
+    n = 2**20 + 333
+    x = np.random.default_rng(8).standard_normal(n)  # float64
+    cap = C.c_size_t()
+    assert L.lib.skml_dense_encode_host_f64(ctx.handle, None, n, C.byref(_params(300, 2)), None, 0, C.byref(cap)) == 0
+    pl = np.zeros(cap.value, dtype=np.uint8)
+    wrote = C.c_size_t()
+    assert L.lib.skml_dense_encode_host_f64(ctx.handle, x.ctypes.data_as(C.c_void_p), n, C.byref(_params(300, 2)),
+                                            pl.ctypes.data_as(C.c_void_p), pl.nbytes, C.byref(wrote)) == 0
+    pl = pl[: wrote.value]
+    oq = O.quantize(x, 300, 2)
+    h = L.DenseHeader()
+    sp = np.zeros(400, dtype=np.float64)
+    assert L.lib.skml_dense_info_host(pl.ctypes.data_as(C.c_void_p), len(pl), C.byref(h),
+                                      sp.ctypes.data_as(L.dblp), 400) == 0
+    assert (h.bin_num, h.zero_idx, h.min, h.max, h.n) == (oq.bin_num, oq.zero_idx, oq.min, oq.max, n)
+    assert np.array_equal(sp[: h.bin_num - 1], oq.splits)
+    bins = np.zeros(n, dtype=np.int32)
+    assert L.lib.skml_dense_bins_host(pl.ctypes.data_as(C.c_void_p), len(pl), bins.ctypes.data_as(C.c_void_p), n) == 0
+    assert np.array_equal(bins, oq.bins)
+    assert L.lib.skml_dense_times_by_host(pl.ctypes.data_as(C.c_void_p), len(pl), 0.5) == 0
+    O.lib().orc_times_by(C.byref(oq.hdr), 0.5)
+    want = O.OracleQuant(oq.hdr, oq.bins).values()[oq.bins]
+    out = np.zeros(n, dtype=np.float64)
+    assert L.lib.skml_dense_decode_host_f64(ctx.handle, pl.ctypes.data_as(C.c_void_p), len(pl),
+                                            out.ctypes.data_as(C.c_void_p), n) == 0
+    assert np.array_equal(out, want)
+
+
+def test_sparse_and_delta_host_entries(gpu):
+    L = _L()
+    ctx = gpu.get_context()
+    rng = np.random.default_rng(5)
+    keys = np.nonzero(rng.random(400000) < 0.1)[0].astype(np.int32)
+    vals = rng.standard_normal(len(keys)).astype(np.float32)
+    p = _params(256, 3)
+    p.hash_seed = 4
+    h = C.c_void_p()
+    assert L.lib.skml_sparse_encode_kv_host_f32(ctx.handle, keys.ctypes.data_as(C.c_void_p),
+                                                vals.ctypes.data_as(C.c_void_p), len(keys), C.byref(p),
+                                                C.byref(h)) == 0, L.last_error()
+    try:
+        rk = np.zeros(len(keys), dtype=np.int32)
+        rv = np.zeros(len(keys), dtype=np.float32)
+        assert L.lib.skml_sparse_decode_host_f32(ctx.handle, h, rk.ctypes.data_as(C.c_void_p),
+                                                 rv.ctypes.data_as(C.c_void_p)) == 0
+    finally:
+        L.lib.skml_sparse_free(h)
+    osp = O.sparse_compress(keys, vals.astype(np.float64), 256, 8, 2, 0.3, 3, 4)
+    ok, ob = osp.restore()
+    assert np.array_equal(rk, ok)
+    assert np.array_equal(rv, osp.q.values()[ob].astype(np.float32))
+    # DeltaAdaptiveEncoder as a BinaryEncoder over host int[] / long[]
+    ref = O.delta_encode(keys)
+    m, kind = C.c_int32(), C.c_int32()
+    nfb, ndb = C.c_int64(), C.c_int64()
+    cap = len(keys)
+    fw = np.zeros(cap, dtype=np.uint64)
+    dw = np.zeros(cap, dtype=np.uint64)
+    assert L.lib.skml_delta_encode_host(ctx.handle, keys.ctypes.data_as(C.c_void_p), len(keys), C.byref(m),
+                                        C.byref(kind), C.byref(nfb), C.byref(ndb), fw.ctypes.data_as(C.c_void_p),
+                                        dw.ctypes.data_as(C.c_void_p), cap) == 0, L.last_error()
+    assert (m.value, bool(kind.value), nfb.value, ndb.value) == (
+        ref["num_intervals"], ref["flag_kind"], ref["n_flag_bits"], ref["n_delta_bits"])
+    nf, nd = len(ref["flag_words"]), len(ref["delta_words"])
+    assert np.array_equal(fw[:nf], ref["flag_words"]) and np.array_equal(dw[:nd], ref["delta_words"])
+    back = np.zeros(len(keys), dtype=np.int32)
+    assert L.lib.skml_delta_decode_host(ctx.handle, len(keys), m.value, kind.value, ref["flag_words"].ctypes.data_as(C.c_void_p),
+                                        nf, ref["delta_words"].ctypes.data_as(C.c_void_p), nd,
+                                        back.ctypes.data_as(C.c_void_p)) == 0, L.last_error()
+    assert np.array_equal(back, keys)
