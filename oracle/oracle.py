@@ -100,6 +100,7 @@ def lib():
         L.orc_hash.restype = C.c_int32
         L.orc_pick_hashes.argtypes = [C.c_int64, C.c_int32, i32p]
         L.orc_group_edges.argtypes = [C.c_int32, C.c_int32, C.c_int32, i32p]
+        L.orc_group_edges.restype = C.c_int
         L.orc_delta_encode.argtypes = [i32p, C.c_int32, C.POINTER(Delta)]
         L.orc_delta_decode.argtypes = [C.POINTER(Delta), i32p]
         L.orc_delta_free.argtypes = [C.POINTER(Delta)]

@@ -643,19 +643,22 @@ void orc_pick_hashes(int64_t seed, int32_t rows, int32_t* ids) {
     for (int i = 0; i < rows; i++) ids[i] = idx[i];
 }
 
-/* FSketchUtils.calGroupEdges (frequency/FSketchUtils.java:9-28) */
-void orc_group_edges(int32_t zero_idx, int32_t bin_num, int32_t group_num, int32_t* edges) {
+/* FSketchUtils.calGroupEdges (frequency/FSketchUtils.java:9-28).  Returns ORC_E_ARG where Java's
+ * `zeroIdx % bpg` throws ArithmeticException (bin_num < group_num and zeroIdx >= 0 = bpg). */
+int orc_group_edges(int32_t zero_idx, int32_t bin_num, int32_t group_num, int32_t* edges) {
     if (group_num == 2) {
         edges[0] = zero_idx;
         edges[1] = bin_num;
-        return;
+        return ORC_OK;
     }
     int32_t bpg = bin_num / group_num;
     if (zero_idx < bpg) edges[0] = zero_idx;
+    else if (bpg == 0) return ORC_E_ARG;
     else if ((zero_idx % bpg) < (bpg / 2)) edges[0] = bpg + zero_idx % bpg;
     else edges[0] = zero_idx % bpg;
     for (int32_t i = 1; i < group_num - 1; i++) edges[i] = edges[i - 1] + bpg;
     edges[group_num - 1] = bin_num;
+    return ORC_OK;
 }
 
 /* ---- BitSet as little-endian uint64 words; BinaryUtils.setBits writes MSB first ---- */
@@ -994,7 +997,10 @@ int orc_sparse_compress_q(const int32_t* keys, const double* vals, int32_t nnz, 
     s->group_num = group_num;
     s->row_num = row_num;
     s->col_ratio = col_ratio;
-    orc_group_edges(s->q.zero_idx, s->q.bin_num, group_num, s->edges);
+    if (orc_group_edges(s->q.zero_idx, s->q.bin_num, group_num, s->edges)) {
+        free(bins);
+        return ORC_E_ARG;
+    }
     /* FSketchUtils.partition (FSketchUtils.java:30-47): first group whose edge > bin, stable */
     int32_t* gid = (int32_t*)malloc(sizeof(int32_t) * (size_t)(nnz > 0 ? nnz : 1));
     for (int32_t i = 0; i < nnz; i++) {

@@ -108,7 +108,8 @@ int32_t orc_hash(int32_t id, int32_t key, int32_t size);
 /* HashFactory.getRandomInt2IntHashes's Maths.shuffle draw, on Random(seed) */
 void orc_pick_hashes(int64_t seed, int32_t rows, int32_t* ids);
 
-void orc_group_edges(int32_t zero_idx, int32_t bin_num, int32_t group_num, int32_t* edges);
+/* FSketchUtils.calGroupEdges; ORC_E_ARG where Java divides by zero (bin_num < group_num) */
+int orc_group_edges(int32_t zero_idx, int32_t bin_num, int32_t group_num, int32_t* edges);
 
 /* DeltaAdaptiveEncoder (binary/DeltaAdaptiveEncoder.java) */
 typedef struct {
