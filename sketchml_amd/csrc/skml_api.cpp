@@ -140,6 +140,8 @@ struct Workspace {
     QuantLut* lut;  // quantize bucket LUT, written by the summary / set-splits kernel
     UniPartial* uni;  // uniform quantizer partials
     int* qflags;      // fp64 quantize flags (bit 0: literal Quantizer.indexOf)
+    uint8_t* ubits;   // compaction bits of the upper merge tree, drawn by the leaf
+    LeafPartial* part_red;  // leaf partials reduced per first-pass merge workgroup
 };
 
 size_t ws_layout(int64_t chunks, Workspace* w, char* base) {
@@ -163,6 +165,8 @@ size_t ws_layout(int64_t chunks, Workspace* w, char* base) {
     t.lut = (QuantLut*)take(sizeof(QuantLut));
     t.uni = (UniPartial*)take(sizeof(UniPartial) * kUniMaxParts);
     t.qflags = (int*)take(sizeof(int) * 4);
+    t.ubits = (uint8_t*)take((size_t)upper_node_count(full * kLeafChunks) + 64);
+    t.part_red = (LeafPartial*)take(sizeof(LeafPartial) * (size_t)(full + 8));
     if (w) *w = t;
     return off;
 }
@@ -188,6 +192,7 @@ struct Workspace64 {
     double* upA;
     double* upB;
     double* raw;
+    uint8_t* ubits;
 };
 
 size_t ws64_layout(int64_t chunks, Workspace64* w, char* base) {
@@ -206,6 +211,7 @@ size_t ws64_layout(int64_t chunks, Workspace64* w, char* base) {
     t.upA = (double*)take(sizeof(double) * kK * (size_t)up);
     t.upB = (double*)take(sizeof(double) * kK * (size_t)up);
     t.raw = (double*)take(sizeof(double) * SKML_MAX_BINS);
+    t.ubits = (uint8_t*)take((size_t)upper_node_count(tiles * kLeafChunks) + 64);
     if (w) *w = t;
     return off;
 }
@@ -541,7 +547,7 @@ int run_sketch_f32(skml_ctx* c, const float* x, int64_t n, uint64_t s0, const Wo
     if (chunks > 0) {
         {
             KernelTimer kt(c, SKML_K_LEAF);
-            HIP_TRY(launch_leaf(c->stream, x, chunks, s0, c->jump_tab, w.part, w.nodes6, w.roots));
+            HIP_TRY(launch_leaf(c->stream, x, chunks, s0, c->jump_tab, w.part, w.nodes6, w.roots, w.ubits));
         }
         if (c->after_leaf) {
             HIP_TRY(hipEventRecord(c->after_leaf, c->stream));
@@ -549,6 +555,10 @@ int run_sketch_f32(skml_ctx* c, const float* x, int64_t n, uint64_t s0, const Wo
         }
         std::vector<MergePass> passes = plan_merge_passes(chunks);
         if (summary && !passes.empty()) passes.back().fuse_summary = 1;
+        // the first pass reduces the leaf partials of the tiles it merges (every tile of the
+        // trees of level >= 7: [0, 2 * (chunks >> 7))) for the summary, one per workgroup
+        const int64_t nred = passes.empty() ? 0 : passes[0].wg_prefix[passes[0].njobs];
+        const int64_t part_from = passes.empty() ? 0 : (chunks >> 7) << 1;
         const float* src = w.nodes6;
         float* dst = w.upA;
         for (size_t i = 0; i < passes.size(); i++) {
@@ -557,7 +567,8 @@ int run_sketch_f32(skml_ctx* c, const float* x, int64_t n, uint64_t s0, const Wo
             KernelTimer kt(c, SKML_K_MERGE);
             HIP_TRY(launch_merge_pass(c->stream, passes[i], fuse_next ? &passes[i + 1] : nullptr, src, dst, next_dst,
                                       w.roots, s0, c->jump_tab, w.done, x, n, w.part, nwg, c->ranks, p->bin_num,
-                                      p->dedup ? 1 : 0, payload, w.raw, w.lut));
+                                      p->dedup ? 1 : 0, payload, w.raw, w.lut, w.ubits,
+                                      summary ? w.part_red : nullptr, summary ? nred : 0, summary ? part_from : 0));
             src = dst;
             dst = next_dst;
             if (fuse_next) break;
@@ -872,7 +883,7 @@ int run_sketch_f64(skml_ctx* c, const double* x, int64_t n, uint64_t s0, const W
     const int64_t chunks = n / kChunk;
     {
         KernelTimer kt(c, SKML_K_LEAF);
-        HIP_TRY(launch_leaf2_f64(c->stream, x, chunks, s0, c->jump_tab, w.part, w.nodes6, w.roots));
+        HIP_TRY(launch_leaf2_f64(c->stream, x, chunks, s0, c->jump_tab, w.part, w.nodes6, w.roots, w.ubits));
     }
     // upper trees: the fp32 pass plan over double nodes (k_merge64)
     const std::vector<MergePass> passes = plan_merge_passes(chunks);
@@ -885,7 +896,8 @@ int run_sketch_f64(skml_ctx* c, const double* x, int64_t n, uint64_t s0, const W
         double* next_dst = (dst == w.upA) ? w.upB : w.upA;
         KernelTimer kt(c, SKML_K_MERGE);
         HIP_TRY(launch_merge_pass64(c->stream, passes[i], fuse_next ? &passes[i + 1] : nullptr, src, dst, next_dst,
-                                    w.roots, s0, c->jump_tab, wq.done));
+                                    w.roots, s0, c->jump_tab, wq.done, w.ubits,
+                                    (chunks / kLeafChunks) * kLeafChunks));
         src = dst;
         dst = next_dst;
         if (fuse_next) break;

@@ -80,7 +80,7 @@ struct SketchRecord64 {
 };
 // fp64 leaf in the fp32 leaf's layout (8 lanes x 32 values per chunk), skml_sketch.hip
 hipError_t launch_leaf2_f64(hipStream_t st, const double* x, int64_t chunks, uint64_t s0, const uint64_t* jump_tab,
-                            LeafPartial64* part, double* nodes6, double* roots);
+                            LeafPartial64* part, double* nodes6, double* roots, uint8_t* ubits);
 hipError_t launch_sketch_record64(hipStream_t st, const double* x, int64_t n, const LeafPartial64* part,
                                   int64_t nparts, const double* roots, SketchRecord64* rec);
 // Merge of fp64 records into (roots, tail, part) for launch_summary64 (tail, sharded = 1).
@@ -115,15 +115,27 @@ __host__ __device__ inline size_t dense_codes_offset(int req_bins) {
     return align_up(kHeaderBytes + 8 * (size_t)(req_bins - 1), 256);
 }
 
+// Upper merge nodes (tree levels >= kLeafTopLevel + 1) of the fixed merge tree over C chunks,
+// numbered level by level: node i of level L covers chunks [i 2^L, (i+1) 2^L), and its number is
+// upper_level_offset(C, L) + i.  The leaf kernel draws their compaction bits (one per wave) into
+// a byte array so the merge passes look them up instead of jumping the LCG themselves.
+__host__ __device__ inline int64_t upper_level_offset(int64_t C, int L) {
+    int64_t o = 0;
+    for (int l = kLeafTopLevel + 1; l < L; l++) o += C >> l;
+    return o;
+}
+__host__ __device__ inline int64_t upper_node_count(int64_t C) { return upper_level_offset(C, kMaxLevels); }
+
 // ---- kernel launchers (skml_sketch.hip) ----
+// ubits: upper_node_count(full tiles * 64) bytes; the leaf draws the upper merge tree's bits into it
 hipError_t launch_leaf(hipStream_t st, const float* x, int64_t chunks, uint64_t s0,
-                       const uint64_t* jump_tab, LeafPartial* part, float* nodes6, float* roots);
+                       const uint64_t* jump_tab, LeafPartial* part, float* nodes6, float* roots, uint8_t* ubits);
 hipError_t launch_leaf_stage(hipStream_t st, int stage, const float* x, int64_t chunks, uint64_t s0,
                              const uint64_t* jump_tab, LeafPartial* part, float* scratch, float* roots);
 // fp64 merge pass over double nodes (no summary; `next` as in launch_merge_pass).
 hipError_t launch_merge_pass64(hipStream_t st, const MergePass& pass, const MergePass* next, const double* src,
                                double* dst, double* next_dst, double* roots, uint64_t s0, const uint64_t* jump_tab,
-                               unsigned* done);
+                               unsigned* done, const uint8_t* ubits, int64_t uchunks);
 // Slice sketch -> record (after the leaf and the merge passes without a summary).
 hipError_t launch_sketch_record(hipStream_t st, const float* x, int64_t n, const LeafPartial* part, int64_t nparts,
                                 const float* roots, SketchRecord* rec);
@@ -141,7 +153,8 @@ hipError_t launch_merge_pass(hipStream_t st, const MergePass& pass, const MergeP
                              float* dst, float* next_dst, float* roots, uint64_t s0, const uint64_t* jump_tab,
                              unsigned* done, const float* x, int64_t n, const LeafPartial* part, int64_t nparts,
                              const int64_t* ranks, int req_bins, int dedup, void* payload,
-                             double* scratch_raw, QuantLut* lut);
+                             double* scratch_raw, QuantLut* lut, const uint8_t* ubits, LeafPartial* part_red,
+                             int64_t nred, int64_t part_from);
 hipError_t launch_summary(hipStream_t st, const float* x, int64_t n, const LeafPartial* part,
                           int64_t nparts, const float* roots, const int64_t* ranks, int req_bins,
                           int dedup, void* payload, double* scratch_raw, QuantLut* lut);

@@ -149,13 +149,23 @@ __device__ __forceinline__ void store_node(const T (&w)[R], int lane, typename E
 // Exp(level_offset, node_in_wave, regs...) is called after each level for root exports.
 template <typename T, typename S, class Exp>
 __device__ __forceinline__ void inwave_levels(T (&w1)[16], T (&w4)[2], int lane, uint32_t bits, bool exact, S* fb,
-                                              Exp&& exp) {
+                                              Exp&& exp, bool stamp = false) {
     T w2[8], w3[4];
     wave_level<16>(w1, w2, lane, (bits >> (lane >> 4)) & 1u, exact, fb);
+#ifdef SKML_PROF_SUMMARY
+    if (stamp && threadIdx.x == 0) g_prof[23] = wall_clock64();
+#endif
     exp.template at<8>(1, lane >> 4, w2);
     wave_level<8>(w2, w3, lane, (bits >> (4 + (lane >> 5))) & 1u, exact, fb);
+#ifdef SKML_PROF_SUMMARY
+    if (stamp && threadIdx.x == 0) g_prof[24] = wall_clock64();
+#endif
     exp.template at<4>(2, lane >> 5, w3);
     wave_level<4>(w3, w4, lane, (bits >> 6) & 1u, exact, fb);
+#ifdef SKML_PROF_SUMMARY
+    if (stamp && threadIdx.x == 0) g_prof[25] = wall_clock64();
+#endif
+    (void)stamp;
     exp.template at<2>(3, 0, w4);
 }
 
@@ -316,7 +326,8 @@ __device__ __forceinline__ uint32_t fold32(double d) {
 template <int STAGE, bool PARTIAL = false, typename E = float>
 __global__ __launch_bounds__(256, LeafTypes<E>::kMinWaves) void k_leaf2(
     const E* __restrict__ x, int64_t chunks, uint64_t s0, const uint64_t* __restrict__ tab,
-    typename LeafTypes<E>::Part* __restrict__ part, E* __restrict__ nodes6, E* __restrict__ roots, int64_t tile0) {
+    typename LeafTypes<E>::Part* __restrict__ part, E* __restrict__ nodes6, E* __restrict__ roots, int64_t tile0,
+    uint8_t* __restrict__ ubits = nullptr) {
     using Key = typename LeafTypes<E>::Key;
     __shared__ E fb[kLeaf2Waves][kWaveFb];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -477,6 +488,17 @@ __global__ __launch_bounds__(256, LeafTypes<E>::kMinWaves) void k_leaf2(
     if constexpr (STAGE <= 2) {
         nodes6[(size_t)tile * 64 + lane] = (E)(acc ^ (uint32_t)mn ^ (uint32_t)mx ^ fl);
         return;
+    }
+    if constexpr (!PARTIAL) {
+        // one compaction bit of the upper merge tree per wave (upper_level_offset numbering);
+        // `chunks` here counts the full 64-chunk tiles, which hold every node of level >= 7
+        if (ubits && tile < upper_node_count(chunks)) {
+            int L = kLeafTopLevel + 1;
+            int64_t i = tile;
+            while (i >= (chunks >> L)) i -= chunks >> L++;
+            const uint64_t c = ((uint64_t)(i + 1) << L) - 1;
+            if (lane == 0) ubits[tile] = (uint8_t)lcg_bit(tab, s0, node_bit_index(c, L));
+        }
     }
     if constexpr (!PARTIAL) {
         store_node<2>(top, lane, nodes6 + (size_t)tile * kK);
@@ -677,12 +699,12 @@ __global__ __launch_bounds__(512, MINW) void k_leaf(const float* __restrict__ x,
 }
 
 hipError_t launch_leaf(hipStream_t st, const float* x, int64_t chunks, uint64_t s0,
-                       const uint64_t* jump_tab, LeafPartial* part, float* nodes6, float* roots) {
+                       const uint64_t* jump_tab, LeafPartial* part, float* nodes6, float* roots, uint8_t* ubits) {
     const int64_t full = chunks / kLeafWaveChunks;
     if (full > 0)
         hipLaunchKernelGGL((k_leaf2<3, false>), dim3((unsigned)((full + kLeaf2Waves - 1) / kLeaf2Waves)),
                            dim3(64 * kLeaf2Waves), 0, st, x, full * kLeafWaveChunks, s0, jump_tab, part,
-                           nodes6, roots, (int64_t)0);
+                           nodes6, roots, (int64_t)0, ubits);
     if (chunks % kLeafWaveChunks)  // the small trees of the last chunks: one wave
         hipLaunchKernelGGL((k_leaf2<3, true>), dim3(1), dim3(64), 0, st, x, chunks, s0, jump_tab, part,
                            nodes6, roots, full);
@@ -691,12 +713,12 @@ hipError_t launch_leaf(hipStream_t st, const float* x, int64_t chunks, uint64_t 
 
 // fp64 leaf: the same wave-persistent kernel over doubles (level-6 nodes and roots as doubles).
 hipError_t launch_leaf2_f64(hipStream_t st, const double* x, int64_t chunks, uint64_t s0, const uint64_t* jump_tab,
-                            LeafPartial64* part, double* nodes6, double* roots) {
+                            LeafPartial64* part, double* nodes6, double* roots, uint8_t* ubits) {
     const int64_t full = chunks / kLeafWaveChunks;
     if (full > 0)
         hipLaunchKernelGGL((k_leaf2<3, false, double>), dim3((unsigned)((full + kLeaf2Waves - 1) / kLeaf2Waves)),
                            dim3(64 * kLeaf2Waves), 0, st, x, full * kLeafWaveChunks, s0, jump_tab, part, nodes6, roots,
-                           (int64_t)0);
+                           (int64_t)0, ubits);
     if (chunks % kLeafWaveChunks)
         hipLaunchKernelGGL((k_leaf2<3, true, double>), dim3(1), dim3(64), 0, st, x, chunks, s0, jump_tab, part, nodes6,
                            roots, full);
@@ -800,9 +822,17 @@ struct SummaryArgs {
     const float* tail;  // base buffer (n % 256 values); null: the input's last n % 256 values
     int sharded;        // 1: the header's n is n_local (a parallelQuantize shard's codes)
     int64_t n_local;
+    // min / max / flags pre-reduced by the first merge pass (one per workgroup), which covered
+    // leaf tiles [0, part_from); tiles [part_from, nparts) are read from `part` itself
+    const LeafPartial* part_red = nullptr;
+    int64_t nred = 0;
+    int64_t part_from = 0;
 };
 
-__device__ void summary_block(const SummaryArgs& a, SummaryShared& S) {
+// pre: this thread's min / max / flags of the leaf partials, already loaded by the caller (the
+// fused merge workgroup fetches them before its merge so the load latency hides there); null:
+// load them here.
+__device__ void summary_block(const SummaryArgs& a, SummaryShared& S, const LeafPartial* pre = nullptr) {
     const int t = threadIdx.x, T = blockDim.x;
     skml_dense_header* hdr = reinterpret_cast<skml_dense_header*>(a.payload);
     double* splits = reinterpret_cast<double*>(a.payload + kHeaderBytes);
@@ -835,13 +865,21 @@ __device__ void summary_block(const SummaryArgs& a, SummaryShared& S) {
     // ---- min / max / NaN ----
     {
         uint32_t mn = 0xFFFFFFFFu, mx = 0u, fl = 0u;
-        // batches of 8 independent loads per thread (one memory latency per batch, not per load)
-        for (int64_t i0 = t; i0 < a.nparts; i0 += 8 * (int64_t)T) {
+        if (pre) {
+            mn = pre->min_key;
+            mx = pre->max_key;
+            fl = pre->flags;
+        }
+        // the pre-reduced partials first, then the uncovered tiles: batches of 8 independent loads
+        // per thread (one memory latency per batch, not per load)
+        const int64_t ntot = pre ? 0 : a.nred + (a.nparts - a.part_from);
+        for (int64_t i0 = t; i0 < ntot; i0 += 8 * (int64_t)T) {
             LeafPartial p[8];
 #pragma unroll
             for (int k = 0; k < 8; k++) {
                 const int64_t i = i0 + (int64_t)k * T;
-                p[k] = i < a.nparts ? a.part[i] : LeafPartial{0xFFFFFFFFu, 0u, 0u, 0u};
+                p[k] = i < a.nred ? a.part_red[i]
+                                  : (i < ntot ? a.part[a.part_from + (i - a.nred)] : LeafPartial{0xFFFFFFFFu, 0u, 0u, 0u});
             }
 #pragma unroll
             for (int k = 0; k < 8; k++) {
@@ -1031,12 +1069,18 @@ __device__ void summary_block(const SummaryArgs& a, SummaryShared& S) {
     const int nsplit = bin_num - 1;
     if (nsplit <= kMaxSamples && nsplit <= kLutMaxSplits && n > 0) {
         SKML_PROF(9);
+#ifdef SKML_PROF_SUMMARY
+        if (threadIdx.x == 0) g_prof[28] = __builtin_amdgcn_s_memtime();
+#endif
         // LDS staging of the table aliases sorted[] + w[] (both dead after getQuantiles)
         build_quant_lut(S.smp, nsplit, a.lut, reinterpret_cast<int*>(S.wsum), reinterpret_cast<uint32_t*>(S.sorted));
     } else if (t == 0) {
         a.lut->cmax = -1;
     }
     SKML_PROF(10);
+#ifdef SKML_PROF_SUMMARY
+    if (threadIdx.x == 0) g_prof[29] = __builtin_amdgcn_s_memtime();
+#endif
 }
 
 __global__ __launch_bounds__(512) void k_summary(SummaryArgs a) {
@@ -1073,7 +1117,21 @@ struct MergeExport {
 template <typename E = float>
 __device__ __forceinline__ void merge_group_wg(const MergePass& pass, int wg, const E* __restrict__ src,
                                                E* __restrict__ dst, E* __restrict__ roots, uint64_t s0,
-                                               const uint64_t* __restrict__ tab, TileSharedT<E>& sh) {
+                                               const uint64_t* __restrict__ tab, TileSharedT<E>& sh,
+                                               const uint8_t* __restrict__ ubits, int64_t uchunks,
+                                               const LeafPartial* __restrict__ part_in = nullptr,
+                                               LeafPartial* __restrict__ part_red = nullptr, int prof = -1) {
+#ifdef SKML_PROF_SUMMARY
+#define SKML_PROF_AT(k)                                                  \
+    do {                                                                 \
+        if (prof >= 0 && threadIdx.x == 0) g_prof[prof + (k)] = wall_clock64(); \
+    } while (0)
+#else
+#define SKML_PROF_AT(k) \
+    do {                \
+    } while (0)
+#endif
+    SKML_PROF_AT(0);
     using T = typename std::conditional<std::is_same<E, double>::value, double, uint32_t>::type;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     int j = 0;
@@ -1086,6 +1144,34 @@ __device__ __forceinline__ void merge_group_wg(const MergePass& pass, int wg, co
     const int64_t chunk0 = job.chunk_base + ((int64_t)grp << (g + L));
     E* out = job.root_level >= 0 ? roots + (size_t)job.root_level * kK : dst + (size_t)(job.dst_node + grp) * kK;
     if (tid == 0) sh.flags = 0u;
+    // this lane's compaction bit, drawn by the leaf (k_leaf2, upper_level_offset numbering); the
+    // load is issued first so its latency hides behind the node loads.  Padding merges (g < 6)
+    // read a clamped index: their bits are never used.
+    uint32_t bsel = 0;
+    {
+        int lo = -1, last_node = 0;
+        if (lane < 4) lo = 1, last_node = wave * 8 + 2 * lane + 1;
+        else if (lane < 6) lo = 2, last_node = wave * 8 + 4 * (lane - 4) + 3;
+        else if (lane == 6) lo = 3, last_node = wave * 8 + 7;
+        else if (wave == 0 && lane >= 8 && lane < 12) lo = 4, last_node = 16 * (lane - 8) + 15;
+        else if (wave == 0 && lane >= 12 && lane < 14) lo = 5, last_node = 32 * (lane - 12) + 31;
+        else if (wave == 0 && lane == 14) lo = 6, last_node = 63;
+        if (lo > 0) {
+            const int lvl = L + lo;
+            const int64_t i = ((chunk0 + ((int64_t)(last_node + 1) << L)) >> lvl) - 1;
+            const int64_t cnt = upper_node_count(uchunks);
+            int64_t idx = upper_level_offset(uchunks, lvl) + i;
+            idx = idx < cnt ? idx : cnt - 1;
+            bsel = ubits[idx < 0 ? 0 : idx];
+        }
+    }
+    (void)tab;
+    (void)s0;
+    // first pass (level-6 input nodes = leaf tiles): wave 0 reduces the tiles' min / max / flags
+    // for the summary (SummaryArgs::part_red); the load hides behind the node loads too
+    const bool reduce_parts = part_red && L == kLeafTopLevel && wave == 0;
+    LeafPartial tp{0xFFFFFFFFu, 0u, 0u, 0u};
+    if (reduce_parts && lane < nodes) tp = part_in[node0 + lane];
     __syncthreads();
 
     // ---- load: node nd = 8*wave + lane/8, 16 floats per lane ----
@@ -1123,35 +1209,42 @@ __device__ __forceinline__ void merge_group_wg(const MergePass& pass, int wg, co
         }
     }
     if (!valid) fl = 0;
-    // ---- RNG bits: lane k < 7 computes one in-wave merge bit; wave 0 also the 7 cross-wave ones ----
-    auto node_bit = [&](int level_off, int last_node) -> uint32_t {
-        const uint64_t c = (uint64_t)chunk0 + ((uint64_t)(last_node + 1) << L) - 1;
-        return lcg_bit(tab, s0, node_bit_index(c, L + level_off));
-    };
+    SKML_PROF_AT(1);
+    if (reduce_parts) {
+        uint32_t mn = tp.min_key, mx = tp.max_key, f = tp.flags;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const uint32_t omn = (uint32_t)__shfl_xor((int)mn, off, 64), omx = (uint32_t)__shfl_xor((int)mx, off, 64);
+            mn = omn < mn ? omn : mn;
+            mx = omx > mx ? omx : mx;
+            f |= (uint32_t)__shfl_xor((int)f, off, 64);
+        }
+        if (lane == 0) part_red[wg] = LeafPartial{mn, mx, f, 0u};
+    }
+    // ---- the RNG bits fetched at the top (lane k < 7: an in-wave merge; wave 0 lanes 8..14: the
+    // cross-wave ones) ----
     uint32_t ibits;
     {
-        uint32_t b = 0;
-        if (lane < 4) b = node_bit(1, wave * 8 + 2 * lane + 1);
-        else if (lane < 6) b = node_bit(2, wave * 8 + 4 * (lane - 4) + 3);
-        else if (lane == 6) b = node_bit(3, wave * 8 + 7);
-        else if (wave == 0 && lane >= 8 && lane < 12) b = node_bit(4, 16 * (lane - 8) + 15);
-        else if (wave == 0 && lane >= 12 && lane < 14) b = node_bit(5, 32 * (lane - 12) + 31);
-        else if (wave == 0 && lane == 14) b = node_bit(6, 63);
-        const uint64_t m = __ballot(b != 0);
+        const uint64_t m = __ballot(bsel != 0);
         ibits = (uint32_t)m & 0x7Fu;
         if (wave == 0 && lane == 0) sh.wgbits = (uint32_t)(m >> 8) & 0x7Fu;
     }
+#ifdef SKML_PROF_SUMMARY
+    if (prof == 16 && threadIdx.x == 0) g_prof[22] = wall_clock64();
+#endif
     if (fl) atomicOr(&sh.flags, fl);
     const bool wexact = (__ballot((fl & 2u) != 0) != 0) && (__ballot((fl & 4u) != 0) != 0);
     const MergeExport<E> exp{lane, wave, g, out};
     T w4[2];
-    inwave_levels(w1, w4, lane, ibits, wexact, sh.fb[wave], exp);
+    inwave_levels(w1, w4, lane, ibits, wexact, sh.fb[wave], exp, prof == 16);
     store_node<2>(w4, lane, sh.wn[wave]);
     __syncthreads();
+    SKML_PROF_AT(2);
     if (g >= 4) {
         crosswave_levels<T>(sh, tid, sh.wgbits, (sh.flags & 6u) == 6u);
         if (tid < kK) out[tid] = g == 4 ? sh.l4[0][tid] : (g == 5 ? sh.l5[0][tid] : sh.l6[tid]);
     }
+    SKML_PROF_AT(3);
 }
 
 // A merge pass.  `next` (njobs > 0) is a one-workgroup pass that the pass's last workgroup runs
@@ -1161,11 +1254,12 @@ __global__ __launch_bounds__(512) void k_merge(MergePass pass, MergePass next, c
                                                float* __restrict__ dst, float* __restrict__ next_dst,
                                                float* __restrict__ roots, uint64_t s0,
                                                const uint64_t* __restrict__ tab, unsigned* __restrict__ done,
-                                               SummaryArgs sa) {
+                                               SummaryArgs sa, const uint8_t* __restrict__ ubits, int64_t uchunks) {
     __shared__ MergeShared U;
     const int tid = threadIdx.x;
     if (pass.fuse_summary && gridDim.x == 1) SKML_PROF(0);
-    merge_group_wg(pass, (int)blockIdx.x, src, dst, roots, s0, tab, U.t);
+    merge_group_wg(pass, (int)blockIdx.x, src, dst, roots, s0, tab, U.t, ubits, uchunks, sa.part,
+                   const_cast<LeafPartial*>(sa.part_red), blockIdx.x == 0 ? 12 : -1);
     const bool has_next = next.njobs > 0;
     if (!pass.fuse_summary && !has_next) return;
 
@@ -1178,43 +1272,68 @@ __global__ __launch_bounds__(512) void k_merge(MergePass pass, MergePass next, c
         const unsigned old = atomicAdd(done, 1u);
         const int last = old == (unsigned)(pass.wg_prefix[pass.njobs] - 1);
         if (last) {
+#ifdef SKML_PROF_SUMMARY
+            g_prof[20] = wall_clock64();
+#endif
             *done = 0u;  // reset for the next encode
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef SKML_PROF_SUMMARY
+            g_prof[21] = wall_clock64();
+#endif
         }
         U.t.is_last = last;
     }
     __syncthreads();
     if (!U.t.is_last) return;
     __syncthreads();
+    // the summary's leaf partials, fetched now so their latency hides behind the merge below
+    LeafPartial pre{0xFFFFFFFFu, 0u, 0u, 0u};
+    const int64_t npre = sa.nred + (sa.nparts - sa.part_from);
+    const bool prefetch = pass.fuse_summary || next.fuse_summary ? npre <= (int64_t)blockDim.x : false;
+    if (prefetch && tid < npre) pre = tid < sa.nred ? sa.part_red[tid] : sa.part[sa.part_from + (tid - sa.nred)];
     if (has_next) {
         SKML_PROF(0);
-        merge_group_wg(next, 0, dst, next_dst, roots, s0, tab, U.t);
+        merge_group_wg(next, 0, dst, next_dst, roots, s0, tab, U.t, ubits, uchunks, nullptr, nullptr, 16);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         __syncthreads();
         if (!next.fuse_summary) return;
     }
     SKML_PROF(1);
+    summary_block(sa, U.s, prefetch ? &pre : nullptr);
+#ifdef SKML_PROF_WARM
+    // diagnostic build: the summary again with warm instruction / data caches (phases 2..10 then
+    // hold the second run; 26 / 27 bracket it)
+    __syncthreads();
+    if (threadIdx.x == 0) g_prof[26] = wall_clock64();
     summary_block(sa, U.s);
+    __syncthreads();
+    if (threadIdx.x == 0) g_prof[27] = wall_clock64();
+#endif
 }
 
 hipError_t launch_merge_pass(hipStream_t st, const MergePass& pass, const MergePass* next, const float* src,
                              float* dst, float* next_dst, float* roots, uint64_t s0, const uint64_t* jump_tab,
                              unsigned* done, const float* x, int64_t n, const LeafPartial* part, int64_t nparts,
                              const int64_t* ranks, int req_bins, int dedup, void* payload,
-                             double* scratch_raw, QuantLut* lut) {
+                             double* scratch_raw, QuantLut* lut, const uint8_t* ubits, LeafPartial* part_red,
+                             int64_t nred, int64_t part_from) {
     const int nwg = pass.wg_prefix[pass.njobs];
     if (nwg <= 0) return hipSuccess;
     SummaryArgs a{x, n, part, nparts, roots, ranks, reinterpret_cast<uint8_t*>(payload), scratch_raw,
                   lut, req_bins, dedup};
+    a.part_red = part_red;  // written by the first pass (this launch or an earlier one)
+    a.nred = nred;
+    a.part_from = part_from;
     MergePass none;
     if (!next) {
         std::memset(&none, 0, sizeof(none));
         next = &none;
     }
+    const int64_t uchunks = (n / kChunk / kLeafWaveChunks) * kLeafWaveChunks;
     hipLaunchKernelGGL(k_merge, dim3(nwg), dim3(512), 0, st, pass, *next, src, dst, next_dst, roots, s0, jump_tab,
-                       done, a);
+                       done, a, ubits, uchunks);
     return hipGetLastError();
 }
 
@@ -1222,10 +1341,11 @@ hipError_t launch_merge_pass(hipStream_t st, const MergePass& pass, const MergeP
 __global__ __launch_bounds__(512) void k_merge64(MergePass pass, MergePass next, const double* __restrict__ src,
                                                  double* __restrict__ dst, double* __restrict__ next_dst,
                                                  double* __restrict__ roots, uint64_t s0,
-                                                 const uint64_t* __restrict__ tab, unsigned* __restrict__ done) {
+                                                 const uint64_t* __restrict__ tab, unsigned* __restrict__ done,
+                                                 const uint8_t* __restrict__ ubits, int64_t uchunks) {
     __shared__ TileSharedT<double> T64;
     const int tid = threadIdx.x;
-    merge_group_wg<double>(pass, (int)blockIdx.x, src, dst, roots, s0, tab, T64);
+    merge_group_wg<double>(pass, (int)blockIdx.x, src, dst, roots, s0, tab, T64, ubits, uchunks);
     if (next.njobs == 0) return;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -1244,12 +1364,12 @@ __global__ __launch_bounds__(512) void k_merge64(MergePass pass, MergePass next,
     __syncthreads();
     if (!T64.is_last) return;
     __syncthreads();
-    merge_group_wg<double>(next, 0, dst, next_dst, roots, s0, tab, T64);
+    merge_group_wg<double>(next, 0, dst, next_dst, roots, s0, tab, T64, ubits, uchunks);
 }
 
 hipError_t launch_merge_pass64(hipStream_t st, const MergePass& pass, const MergePass* next, const double* src,
                                double* dst, double* next_dst, double* roots, uint64_t s0, const uint64_t* jump_tab,
-                               unsigned* done) {
+                               unsigned* done, const uint8_t* ubits, int64_t uchunks) {
     const int nwg = pass.wg_prefix[pass.njobs];
     if (nwg <= 0) return hipSuccess;
     MergePass none;
@@ -1258,7 +1378,7 @@ hipError_t launch_merge_pass64(hipStream_t st, const MergePass& pass, const Merg
         next = &none;
     }
     hipLaunchKernelGGL(k_merge64, dim3(nwg), dim3(512), 0, st, pass, *next, src, dst, next_dst, roots, s0, jump_tab,
-                       done);
+                       done, ubits, uchunks);
     return hipGetLastError();
 }
 
