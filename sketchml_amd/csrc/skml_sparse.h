@@ -12,12 +12,15 @@ namespace skml {
 constexpr int kMaxGroups = 64;  // GroupedMinMaxSketch groups (Java: any int; 8 by default)
 constexpr int kMaxRows = 8;     // MinMaxSketch rows <= the 8 hash functions (HashFactory.java:24-27)
 
-// Group table in device memory, filled by the host between the partition and the encode passes.
+// Group table in device memory.  The encode fills it on the device (k_sp_plan_*: edges from the
+// quantizer header, shapes from the partition counts, interval choice from the bitsNeeded
+// histogram) and the host reads it back once at the end; decode-side payloads fill it on the host.
 // Group g holds grouped elements [gstart[g], gstart[g+1]).
+enum : int32_t { kSpNan = 1, kSpEdges = 2, kSpOrder = 4 };  // SpGroups.status bits
 struct SpGroups {
     int32_t G, rows, zero, bin_num;
-    int32_t fill;  // MinMaxSketch table sentinel (MinMaxSketch.java:30-33)
-    int32_t pad0;
+    int32_t fill;    // MinMaxSketch table sentinel (MinMaxSketch.java:30-33)
+    int32_t status;  // kSp* of a failed encode: the encode's later kernels return at once
     int32_t edges[kMaxGroups];  // FSketchUtils.calGroupEdges
     int64_t gstart[kMaxGroups + 1];
     int32_t cols[kMaxGroups];
@@ -29,6 +32,16 @@ struct SpGroups {
     int64_t db[kMaxGroups + 1];  // first delta bit of group g in the concatenated delta stream
     int32_t kind1_before[kMaxGroups];  // elements of unary-flag groups before g (decode select)
     double inv_cols[kMaxGroups];       // 1.0 / cols[g]: the hash's `% size` as a multiply (set on upload)
+    double col_ratio;                  // GroupedMinMaxSketch colRatio
+    int64_t ncells;                    // all groups' table cells
+};
+
+// What the host knows before an encode starts: the shape parameters and every group's hash
+// choice (HashFactory.getRandomInt2IntHashes(seed + g) depends on g only); passed by value.
+struct SpInit {
+    int32_t G, rows;
+    double col_ratio;
+    int32_t hash_ids[kMaxGroups][kMaxRows];
 };
 
 constexpr int kSpThreads = 256;
@@ -39,6 +52,19 @@ constexpr int kDeltaHist = 33;            // bitsNeeded in 1..32
 inline int64_t sp_tiles(int64_t n, int64_t tile) { return (n + tile - 1) / tile; }
 
 // ---- launchers (skml_sparse.hip) ----
+// Device-side encode plan (one workgroup each, no host round trip):
+//   edges: the table from `init`, then calGroupEdges / fill from the quantizer header (status on NaN / error);
+//   groups: gstart, cols, tab_off, ncells from the partition totals sizes[G];
+//   delta: calOptimalIntervals per group from hist, the order-check flag, kind1_before;
+//   finalize: fb / db of empty groups and the stream totals (tot = the scanned tile sums' total row).
+hipError_t launch_sp_plan_edges(hipStream_t st, const void* qpayload, const SpInit& init, SpGroups* gp);
+hipError_t launch_sp_plan_groups(hipStream_t st, SpGroups* gp, const uint64_t* sizes);
+hipError_t launch_sp_plan_delta(hipStream_t st, SpGroups* gp, const uint32_t* hist, const uint32_t* err);
+hipError_t launch_sp_finalize(hipStream_t st, SpGroups* gp, const uint64_t* tot);
+// Zero the stream words the writer ORs into (every tile's first and last word, and the word
+// after the end) from the scanned [tiles + 1][2] tile sums.
+hipError_t launch_sp_zero_edges(hipStream_t st, const uint64_t* tile_base, int64_t tiles, const SpGroups* gp,
+                                uint64_t* flag_words, uint64_t* delta_words);
 // DenseDoubleGradient.toSparse: keys/vals of |x| > 1e-8 in index order.  status/ticket zeroed.
 hipError_t launch_compact(hipStream_t st, const float* x, int64_t dim, int32_t* keys, float* vals,
                           uint64_t* status, unsigned* ticket, int64_t* nnz_out);
@@ -52,7 +78,7 @@ hipError_t launch_part_scatter(hipStream_t st, const int32_t* keys, const void* 
                                int32_t* gbins);
 // Deltas, bitsNeeded histogram, order check, and the per-bucket pair counts of the bucketed
 // MinMaxSketch.insert (bucket_count: nbuckets u64, zeroed; unused when rows == 0).
-constexpr int kMmCellsPerBucket = 4096;  // MinMax cells per bucket (32 KB of u64 minima in LDS)
+constexpr int kMmCellsPerBucket = 8192;  // MinMax cells per bucket (64 KB of u64 minima in LDS)
 // cells (rows x n int32, may be null): each (element, row) pair's table cell, kept for the scatter.
 // tile_off ([tiles of kMmChunk][nbuckets] u32, may be null): each tile's reserved offset inside
 // each bucket, taken while counting, so the scatter needs neither a count pass nor atomics.
@@ -63,10 +89,11 @@ hipError_t launch_group_prep(hipStream_t st, const int32_t* gkeys, int64_t n, co
 hipError_t launch_mm_scatter(hipStream_t st, const int32_t* gkeys, const int32_t* gbins, int64_t n,
                              const SpGroups* gp, const uint64_t* bucket_base, uint64_t* cursor, int nbuckets,
                              uint64_t* pairs, const int32_t* cells, const uint32_t* tile_off);
-constexpr int64_t kMmChunkElems = 16384;  // elements per workgroup tile of the count / scatter passes
-// per-bucket minimum -> int32 MinMaxSketch tables (empty cells get the fill value)
+constexpr int64_t kMmChunkElems = 65536;  // elements per workgroup tile of the count / scatter passes
+// per-bucket minimum -> int32 MinMaxSketch tables (empty cells get the fill value); nbuckets may
+// exceed the table's (gp->ncells) buckets: the extra workgroups exit
 hipError_t launch_mm_bucket(hipStream_t st, const uint64_t* pairs, const uint64_t* bucket_base, int nbuckets,
-                            int64_t ncells, int32_t zero, int32_t fill, int32_t* table);
+                            const SpGroups* gp, int32_t* table);
 // DeltaAdaptiveEncoder bit streams: tile sums of (flag bits, delta bits), then the writer.
 hipError_t launch_delta_lens(hipStream_t st, const uint8_t* need, int64_t n, const SpGroups* gp,
                              uint64_t* tile_sums);

@@ -139,11 +139,20 @@ __device__ __forceinline__ uint32_t java_hash_mix(int id, int32_t key) {
         c = c ^ sar(c, 16);
     } else {
         const uint32_t seed = id == 3 ? 31u : id == 4 ? 131u : id == 5 ? 267u : id == 6 ? 1313u : 13131u;
-        int32_t k = key;
         c = 0;
-        while (k != 0) {
-            c = seed * c + (uint32_t)(k % 10);
-            k /= 10;
+        if (key >= 0) {  // every valid key: Java's int % and / are the unsigned ones (shorter code)
+            uint32_t k = (uint32_t)key;
+            while (k != 0) {
+                const uint32_t q = k / 10u;
+                c = seed * c + (k - 10u * q);
+                k = q;
+            }
+        } else {
+            int32_t k = key;
+            while (k != 0) {
+                c = seed * c + (uint32_t)(k % 10);
+                k /= 10;
+            }
         }
     }
     return c;
@@ -358,6 +367,7 @@ hipError_t launch_scan_cols(hipStream_t st, uint64_t* sums, int64_t tiles, int K
 __global__ __launch_bounds__(kSpThreads) void k_part_count(const uint8_t* __restrict__ qpayload, int64_t n,
                                                            const SpGroups* __restrict__ gp,
                                                            uint64_t* __restrict__ tile_counts) {
+    if (gp->status) return;
     __shared__ int32_t E[kMaxGroups];
     __shared__ uint32_t cnt[kMaxGroups];
     const skml_dense_header* h = reinterpret_cast<const skml_dense_header*>(qpayload);
@@ -391,6 +401,7 @@ __global__ __launch_bounds__(kSpThreads) void k_part_scatter(const int32_t* __re
                                                              const SpGroups* __restrict__ gp,
                                                              const uint64_t* __restrict__ tile_base,
                                                              int32_t* __restrict__ gkeys, int32_t* __restrict__ gbins) {
+    if (gp->status) return;
     constexpr int kWaves = kSpThreads / 64, kSteps = kSpTile / kSpThreads;
     __shared__ int32_t E[kMaxGroups];
     __shared__ int64_t wb[kWaves][kMaxGroups];  // running output position per (wave, group)
@@ -466,11 +477,12 @@ hipError_t launch_part_scatter(hipStream_t st, const int32_t* keys, const void* 
 // Pair word: |bin - zero| [63:48], key [47:17], bin < zero [16], cell % 8192 [12:0]; its value
 // with the cell bits cleared orders by (distance, key): the smaller distance wins and ties keep
 // the earlier insert (keys ascend within a group).
-constexpr int kMmBucketBits = 12;
+constexpr int kMmBucketBits = 13;
 constexpr int kMmBucketCells = kMmCellsPerBucket;
 static_assert(kMmBucketCells == 1 << kMmBucketBits, "bucket size");
 constexpr int kMmLdsBuckets = 8192;  // per-workgroup bucket tables in LDS up to this many (96 KB in the scatter)
 constexpr int kMmChunk = (int)kMmChunkElems;
+constexpr int kMmThreads = 1024;  // count / scatter workgroups: big tiles, long per-bucket runs
 
 __device__ __forceinline__ int64_t mm_cell(const SpGroups* gp, int g, int r, int32_t key) {
     const int32_t cols = gp->cols[g];
@@ -483,26 +495,27 @@ __device__ __forceinline__ uint64_t mm_pair(int32_t key, int32_t bin, int32_t ze
 
 // Deltas, bitsNeeded histogram and order check (DeltaAdaptiveEncoder.encode step 1) plus the
 // per-bucket pair counts of the MinMax insert.
-__global__ __launch_bounds__(kSpThreads) void k_group_prep(const int32_t* __restrict__ gkeys, int64_t n,
+__global__ __launch_bounds__(kMmThreads) void k_group_prep(const int32_t* __restrict__ gkeys, int64_t n,
                                                            const SpGroups* __restrict__ gp,
                                                            uint8_t* __restrict__ need, uint32_t* __restrict__ hist,
                                                            uint32_t* __restrict__ err,
                                                            unsigned long long* __restrict__ bucket_count,
                                                            int nbuckets, int32_t* __restrict__ cells_out,
                                                            uint32_t* __restrict__ tile_off) {
+    if (gp->status) return;
     __shared__ int64_t S[kMaxGroups + 1];
     __shared__ uint32_t H[kMaxGroups * kDeltaHist];
     extern __shared__ uint32_t BH[];  // nbuckets counters (dynamic: occupancy follows the table size)
     const int G = gp->G, rows = gp->rows;
     const bool lds_b = nbuckets <= kMmLdsBuckets;
     load_starts(gp, S);
-    for (int j = threadIdx.x; j < G * kDeltaHist; j += kSpThreads) H[j] = 0;
+    for (int j = threadIdx.x; j < G * kDeltaHist; j += kMmThreads) H[j] = 0;
     if (lds_b)
-        for (int j = threadIdx.x; j < nbuckets; j += kSpThreads) BH[j] = 0;
+        for (int j = threadIdx.x; j < nbuckets; j += kMmThreads) BH[j] = 0;
     __syncthreads();
     uint32_t bad = 0;
     const int64_t c0 = (int64_t)blockIdx.x * kMmChunk, c1 = std::min<int64_t>(n, c0 + kMmChunk);
-    for (int64_t i = c0 + threadIdx.x; i < c1; i += kSpThreads) {
+    for (int64_t i = c0 + threadIdx.x; i < c1; i += kMmThreads) {
         const int g = group_of_elem(S, i);
         const int32_t key = gkeys[i];
         const bool first = i == S[g];
@@ -525,26 +538,26 @@ __global__ __launch_bounds__(kSpThreads) void k_group_prep(const int32_t* __rest
     }
     if (bad) atomicOr(err, 1u);
     __syncthreads();
-    for (int j = threadIdx.x; j < G * kDeltaHist; j += kSpThreads)
+    for (int j = threadIdx.x; j < G * kDeltaHist; j += kMmThreads)
         if (H[j]) atomicAdd(&hist[j], H[j]);
     if (lds_b && rows > 0) {
         if (tile_off) {  // reserve this tile's range in every bucket: 8 independent atomics in flight
             uint32_t* row = tile_off + (int64_t)blockIdx.x * nbuckets;
-            for (int j0 = threadIdx.x; j0 < nbuckets; j0 += 8 * kSpThreads) {
+            for (int j0 = threadIdx.x; j0 < nbuckets; j0 += 8 * kMmThreads) {
                 unsigned long long o[8];
 #pragma unroll
                 for (int u = 0; u < 8; u++) {
-                    const int j = j0 + u * kSpThreads;
+                    const int j = j0 + u * kMmThreads;
                     o[u] = (j < nbuckets && BH[j]) ? atomicAdd(&bucket_count[j], (unsigned long long)BH[j]) : 0ull;
                 }
 #pragma unroll
                 for (int u = 0; u < 8; u++) {
-                    const int j = j0 + u * kSpThreads;
+                    const int j = j0 + u * kMmThreads;
                     if (j < nbuckets) row[j] = (uint32_t)o[u];
                 }
             }
         } else {
-            for (int j = threadIdx.x; j < nbuckets; j += kSpThreads)
+            for (int j = threadIdx.x; j < nbuckets; j += kMmThreads)
                 if (BH[j]) atomicAdd(&bucket_count[j], (unsigned long long)BH[j]);
         }
     }
@@ -563,7 +576,7 @@ hipError_t launch_group_prep(hipStream_t st, const int32_t* gkeys, int64_t n, co
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL(k_group_prep, dim3((unsigned)sp_tiles(n, kMmChunk)), dim3(kSpThreads), lds, st, gkeys, n, gp,
+    hipLaunchKernelGGL(k_group_prep, dim3((unsigned)sp_tiles(n, kMmChunk)), dim3(kMmThreads), lds, st, gkeys, n, gp,
                        need, hist, err, reinterpret_cast<unsigned long long*>(bucket_count), nbuckets, cells,
                        nbuckets <= kMmLdsBuckets ? tile_off : nullptr);
     return hipGetLastError();
@@ -574,7 +587,7 @@ hipError_t launch_group_prep(hipStream_t st, const int32_t* gkeys, int64_t n, co
 // handles 4 elements per step (4 independent load -> LDS atomic -> store chains), and the
 // reserved 64-bit destinations sit in LDS, so the scatter never waits on a global load.
 constexpr int kMmUnroll = 4;
-__global__ __launch_bounds__(kSpThreads) void k_mm_scatter(const int32_t* __restrict__ gkeys,
+__global__ __launch_bounds__(kMmThreads) void k_mm_scatter(const int32_t* __restrict__ gkeys,
                                                            const int32_t* __restrict__ gbins, int64_t n,
                                                            const SpGroups* __restrict__ gp,
                                                            const uint64_t* __restrict__ bucket_base,
@@ -582,6 +595,7 @@ __global__ __launch_bounds__(kSpThreads) void k_mm_scatter(const int32_t* __rest
                                                            uint64_t* __restrict__ pairs,
                                                            const int32_t* __restrict__ cells_in,
                                                            const uint32_t* __restrict__ tile_off) {
+    if (gp->status) return;
     __shared__ int64_t S[kMaxGroups + 1];
     extern __shared__ uint64_t dyn64[];  // dst[nbuckets] (u64), cnt[nbuckets] (u32): dynamic, see launch
     uint64_t* dstb = dyn64;
@@ -590,7 +604,7 @@ __global__ __launch_bounds__(kSpThreads) void k_mm_scatter(const int32_t* __rest
     const bool lds_b = nbuckets <= kMmLdsBuckets;
     load_starts(gp, S);
     if (lds_b)
-        for (int j = threadIdx.x; j < nbuckets; j += kSpThreads) cnt[j] = 0;
+        for (int j = threadIdx.x; j < nbuckets; j += kMmThreads) cnt[j] = 0;
     __syncthreads();
     const int64_t c0 = (int64_t)blockIdx.x * kMmChunk, c1 = std::min<int64_t>(n, c0 + kMmChunk);
     // cell of (element i, row r): from k_group_prep's table when it kept one, else hashed again
@@ -599,13 +613,13 @@ __global__ __launch_bounds__(kSpThreads) void k_mm_scatter(const int32_t* __rest
     };
     if (lds_b && tile_off) {  // ranges reserved by k_group_prep
         const uint32_t* row = tile_off + (int64_t)blockIdx.x * nbuckets;
-        for (int j = threadIdx.x; j < nbuckets; j += kSpThreads) dstb[j] = bucket_base[j] + row[j];
+        for (int j = threadIdx.x; j < nbuckets; j += kMmThreads) dstb[j] = bucket_base[j] + row[j];
         __syncthreads();
     } else if (lds_b) {
-        for (int64_t base = c0; base < c1; base += kMmUnroll * kSpThreads) {
+        for (int64_t base = c0; base < c1; base += kMmUnroll * kMmThreads) {
 #pragma unroll
             for (int u = 0; u < kMmUnroll; u++) {
-                const int64_t i = base + u * kSpThreads + threadIdx.x;
+                const int64_t i = base + u * kMmThreads + threadIdx.x;
                 if (i >= c1) break;
                 const int g = cells_in ? 0 : group_of_elem(S, i);
                 const int32_t key = cells_in ? 0 : gkeys[i];
@@ -613,16 +627,16 @@ __global__ __launch_bounds__(kSpThreads) void k_mm_scatter(const int32_t* __rest
             }
         }
         __syncthreads();
-        for (int j = threadIdx.x; j < nbuckets; j += kSpThreads) {
+        for (int j = threadIdx.x; j < nbuckets; j += kMmThreads) {
             dstb[j] = cnt[j] ? bucket_base[j] + atomicAdd(&cursor[j], (unsigned long long)cnt[j]) : 0ull;
             cnt[j] = 0;
         }
         __syncthreads();
     }
-    for (int64_t base = c0; base < c1; base += kMmUnroll * kSpThreads) {
+    for (int64_t base = c0; base < c1; base += kMmUnroll * kMmThreads) {
 #pragma unroll
         for (int u = 0; u < kMmUnroll; u++) {
-            const int64_t i = base + u * kSpThreads + threadIdx.x;
+            const int64_t i = base + u * kMmThreads + threadIdx.x;
             if (i >= c1) break;
             const int g = cells_in ? 0 : group_of_elem(S, i);
             const int32_t key = gkeys[i], bin = gbins[i];
@@ -650,30 +664,33 @@ hipError_t launch_mm_scatter(hipStream_t st, const int32_t* gkeys, const int32_t
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL(k_mm_scatter, dim3((unsigned)sp_tiles(n, kMmChunk)), dim3(kSpThreads), lds, st, gkeys, gbins, n,
+    hipLaunchKernelGGL(k_mm_scatter, dim3((unsigned)sp_tiles(n, kMmChunk)), dim3(kMmThreads), lds, st, gkeys, gbins, n,
                        gp, bucket_base, reinterpret_cast<unsigned long long*>(cursor), nbuckets, pairs, cells,
                        nbuckets <= kMmLdsBuckets ? tile_off : nullptr);
     return hipGetLastError();
 }
 
 // One workgroup per bucket: LDS minimum per cell, then the int32 table cells (empty -> fill).
-__global__ __launch_bounds__(kSpThreads) void k_mm_bucket(const uint64_t* __restrict__ pairs,
+__global__ __launch_bounds__(kMmThreads) void k_mm_bucket(const uint64_t* __restrict__ pairs,
                                                           const uint64_t* __restrict__ bucket_base,
-                                                          int64_t ncells, int32_t zero, int32_t fill,
+                                                          const SpGroups* __restrict__ gp,
                                                           int32_t* __restrict__ table) {
     __shared__ unsigned long long cmin[kMmBucketCells];
     const int b = blockIdx.x;
-    for (int j = threadIdx.x; j < kMmBucketCells; j += kSpThreads) cmin[j] = ~0ull;
+    const int64_t ncells = gp->ncells;
+    if (gp->status || ((int64_t)b << kMmBucketBits) >= ncells) return;
+    const int32_t zero = gp->zero, fill = gp->fill;
+    for (int j = threadIdx.x; j < kMmBucketCells; j += kMmThreads) cmin[j] = ~0ull;
     __syncthreads();
     const uint64_t p0 = bucket_base[b], p1 = bucket_base[b + 1];
     constexpr uint64_t kLo = (uint64_t)(kMmBucketCells - 1);
-    for (uint64_t p = p0 + threadIdx.x; p < p1; p += kSpThreads) {
+    for (uint64_t p = p0 + threadIdx.x; p < p1; p += kMmThreads) {
         const uint64_t v = pairs[p];
         atomicMin(&cmin[v & kLo], (unsigned long long)(v & ~kLo));
     }
     __syncthreads();
     const int64_t cell0 = (int64_t)b << kMmBucketBits;
-    for (int j = threadIdx.x; j < kMmBucketCells && cell0 + j < ncells; j += kSpThreads) {
+    for (int j = threadIdx.x; j < kMmBucketCells && cell0 + j < ncells; j += kMmThreads) {
         const uint64_t v = cmin[j];
         int32_t out = fill;
         if (v != ~0ull) {
@@ -685,10 +702,10 @@ __global__ __launch_bounds__(kSpThreads) void k_mm_bucket(const uint64_t* __rest
 }
 
 hipError_t launch_mm_bucket(hipStream_t st, const uint64_t* pairs, const uint64_t* bucket_base, int nbuckets,
-                            int64_t ncells, int32_t zero, int32_t fill, int32_t* table) {
+                            const SpGroups* gp, int32_t* table) {
     if (nbuckets <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_mm_bucket, dim3((unsigned)nbuckets), dim3(kSpThreads), 0, st, pairs, bucket_base, ncells,
-                       zero, fill, table);
+    hipLaunchKernelGGL(k_mm_bucket, dim3((unsigned)nbuckets), dim3(kMmThreads), 0, st, pairs, bucket_base, gp,
+                       table);
     return hipGetLastError();
 }
 
@@ -717,6 +734,7 @@ __device__ __forceinline__ void delta_lens(const DeltaShape& s, int nb, int& iv,
 __global__ __launch_bounds__(kSpThreads) void k_delta_lens(const uint8_t* __restrict__ need, int64_t n,
                                                            const SpGroups* __restrict__ gp,
                                                            uint64_t* __restrict__ tile_sums) {
+    if (gp->status) return;
     __shared__ int64_t S[kMaxGroups + 1];
     __shared__ uint64_t sh[8];
     load_starts(gp, S);
@@ -783,6 +801,7 @@ __global__ __launch_bounds__(kSpThreads) void k_delta_write(const int32_t* __res
                                                             const uint64_t* __restrict__ tile_base,
                                                             uint64_t* __restrict__ flag_words,
                                                             uint64_t* __restrict__ delta_words) {
+    if (gp->status) return;
     __shared__ int64_t S[kMaxGroups + 1];
     __shared__ uint64_t sh[8];
     __shared__ uint64_t fwin[kFlagWin];
@@ -854,6 +873,195 @@ hipError_t launch_delta_write(hipStream_t st, const int32_t* gkeys, const uint8_
     if (tiles <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_delta_write, dim3((unsigned)tiles), dim3(kSpThreads), 0, st, gkeys, need, n, gp,
                        tile_base, flag_words, delta_words);
+    return hipGetLastError();
+}
+
+// =============================================================================================
+// Device-side encode plan: the per-group decisions the reference takes on whole-group
+// statistics, made where the statistics are, so an encode never waits on a host round trip.
+// =============================================================================================
+// MinMaxSketch.compare with Java int wrap (MinMaxSketch.java:80-86)
+__device__ __forceinline__ int32_t mm_cmp(int32_t a, int32_t b, int32_t zero) {
+    return (int32_t)((uint32_t)mm_dist(a, zero) - (uint32_t)mm_dist(b, zero));
+}
+
+// Table from `init` (every field of the reused device struct rewritten), then
+// FSketchUtils.calGroupEdges (frequency/FSketchUtils.java:9-28) on the quantizer's zeroIdx and
+// binNum, and the MinMaxSketch fill (MinMaxSketch.java:30-33).
+__global__ __launch_bounds__(64) void k_sp_plan_edges(const skml_dense_header* __restrict__ h, SpInit init,
+                                                      SpGroups* __restrict__ gp) {
+    uint32_t* w = reinterpret_cast<uint32_t*>(gp);
+    for (int j = threadIdx.x; j < (int)(sizeof(SpGroups) / 4); j += 64) w[j] = 0u;
+    __syncthreads();
+    for (int j = threadIdx.x; j < kMaxGroups * kMaxRows; j += 64)
+        gp->hash_ids[j / kMaxRows][j % kMaxRows] = init.hash_ids[j / kMaxRows][j % kMaxRows];
+    if (threadIdx.x) return;
+    const int32_t G = init.G;
+    gp->G = G;
+    gp->rows = init.rows;
+    gp->col_ratio = init.col_ratio;
+    if (h->status != SKML_OK) {  // "Encounter NaN value": nothing else runs
+        gp->status = kSpNan;
+        return;
+    }
+    const int32_t zero = h->zero_idx, bins = h->bin_num;
+    gp->zero = zero;
+    gp->bin_num = bins;
+    gp->fill = mm_cmp(INT32_MIN, INT32_MAX, zero) <= 0 ? INT32_MIN : INT32_MAX;
+    if (G == 2) {
+        gp->edges[0] = zero;
+        gp->edges[1] = bins;
+        return;
+    }
+    const int32_t bpg = bins / G;
+    int32_t e;
+    if (zero < bpg) e = zero;
+    else if (bpg == 0) {  // Java: ArithmeticException "/ by zero"
+        gp->status = kSpEdges;
+        return;
+    } else if ((zero % bpg) < (bpg / 2)) e = bpg + zero % bpg;
+    else e = zero % bpg;
+    for (int32_t i = 0; i < G - 1; i++, e += bpg) gp->edges[i] = e;
+    gp->edges[G - 1] = bins;
+}
+
+// GroupedMinMaxSketch.compOneGroup's shapes (GroupedMinMaxSketch.java:103-121): colNum =
+// ceil(size * colRatio) (no multiply-add contraction: the product rounds as in Java).
+__global__ __launch_bounds__(64) void k_sp_plan_groups(SpGroups* __restrict__ gp, const uint64_t* __restrict__ sizes) {
+    if (gp->status || threadIdx.x) return;
+    const int G = gp->G, rows = gp->rows;
+    const double ratio = gp->col_ratio;
+    int64_t start = 0, cells = 0;
+    for (int g = 0; g < G; g++) {
+        const int64_t m = (int64_t)sizes[g];
+        gp->gstart[g] = start;
+        start += m;
+        const int32_t cols = m > 0 ? (int32_t)ceil(__dmul_rn((double)m, ratio)) : 1;
+        gp->cols[g] = cols;
+        gp->inv_cols[g] = __ddiv_rn(1.0, (double)cols);
+        gp->tab_off[g] = cells;
+        if (m > 0) cells += (int64_t)rows * cols;
+        else
+            for (int r = 0; r < kMaxRows; r++) gp->hash_ids[g][r] = 0;  // an empty group picks no hashes
+    }
+    gp->gstart[G] = start;
+    gp->ncells = cells;
+}
+
+// DeltaAdaptiveEncoder.calOptimalIntervals (binary/DeltaAdaptiveEncoder.java:23-51) in the
+// reference's double summation order, every operation rounded on its own.
+__device__ void delta_choose(const uint32_t* __restrict__ count, int64_t size, int32_t& bm, int32_t& bk) {
+    double prob[32];
+    for (int i = 0; i < 32; i++) prob[i] = __ddiv_rn((double)count[i], (double)size);
+    double best = 32.0;
+    bm = 1;
+    bk = 0;
+    for (int32_t m = 2, lg = 1; m <= 16; m *= 2, lg++) {
+        const int32_t b = 32 / m;
+        double sum = 0.0;
+        for (int32_t i = 0; i < m; i++) {
+            double ip = 0.0;
+            for (int32_t j = 0; j < b; j++) ip = __dadd_rn(ip, prob[i * b + j]);
+            sum = __dadd_rn(sum, __dmul_rn((double)(i + 1), ip));
+        }
+        const double t1 = __dadd_rn(__dmul_rn(sum, (double)b), (double)lg);
+        if (t1 < best) {
+            best = t1;
+            bm = m;
+            bk = 0;
+        }
+        const double t2 = __dadd_rn(__dmul_rn(sum, (double)(b + 1)), 1.0);
+        if (t2 < best) {
+            best = t2;
+            bm = m;
+            bk = 1;
+        }
+    }
+}
+
+// One lane per group: its interval choice; lane 0 then the order check and kind1_before.
+__global__ __launch_bounds__(64) void k_sp_plan_delta(SpGroups* __restrict__ gp, const uint32_t* __restrict__ hist,
+                                                      const uint32_t* __restrict__ err) {
+    if (gp->status) return;
+    const int G = gp->G, g = threadIdx.x;
+    if (g < G) {
+        const int64_t m = gp->gstart[g + 1] - gp->gstart[g];
+        int32_t bm = 1, bk = 0;
+        if (m > 0) {
+            uint32_t cnt[32];
+            for (int i = 0; i < 32; i++) cnt[i] = hist[g * kDeltaHist + i];
+            cnt[31] += hist[g * kDeltaHist + 32];  // bitsNeeded 32 cannot occur for positive deltas
+            delta_choose(cnt, m, bm, bk);
+        }
+        gp->m[g] = bm;
+        gp->kind[g] = bk;
+    }
+    __syncthreads();
+    if (g) return;
+    if (*err) {  // Maths.log2nlz: "Log for <d>" (util/Maths.java:16-21)
+        gp->status = kSpOrder;
+        return;
+    }
+    int32_t k1 = 0;
+    for (int j = 0; j < G; j++) {
+        gp->kind1_before[j] = k1;
+        if (gp->kind[j]) k1 += (int32_t)(gp->gstart[j + 1] - gp->gstart[j]);
+    }
+}
+
+__global__ __launch_bounds__(kSpThreads) void k_sp_zero_edges(const uint64_t* __restrict__ ts, int64_t tiles,
+                                                              const SpGroups* __restrict__ gp,
+                                                              uint64_t* __restrict__ fw, uint64_t* __restrict__ dw) {
+    if (gp->status) return;
+    const int64_t i = (int64_t)blockIdx.x * kSpThreads + threadIdx.x;
+    if (i > tiles) return;
+    const uint64_t f0 = ts[2 * i], d0 = ts[2 * i + 1];
+    fw[f0 >> 6] = 0;
+    dw[d0 >> 6] = 0;
+    if (i < tiles) {
+        const uint64_t f1 = ts[2 * i + 2], d1 = ts[2 * i + 3];
+        if (f1 > f0) fw[(f1 - 1) >> 6] = 0;
+        if (d1 > d0) dw[(d1 - 1) >> 6] = 0;
+    } else {  // the trailing word of each stream (n_words = ceil(bits / 64) + 1)
+        fw[(f0 >> 6) + 1] = 0;
+        dw[(d0 >> 6) + 1] = 0;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_sp_finalize(SpGroups* __restrict__ gp, const uint64_t* __restrict__ tot) {
+    if (gp->status || threadIdx.x) return;
+    const int G = gp->G;
+    gp->fb[G] = (int64_t)tot[0];
+    gp->db[G] = (int64_t)tot[1];
+    for (int g = G - 1; g >= 0; g--)  // k_delta_write set the non-empty groups' bases
+        if (gp->gstart[g + 1] == gp->gstart[g]) {
+            gp->fb[g] = gp->fb[g + 1];
+            gp->db[g] = gp->db[g + 1];
+        }
+}
+
+hipError_t launch_sp_plan_edges(hipStream_t st, const void* qpayload, const SpInit& init, SpGroups* gp) {
+    hipLaunchKernelGGL(k_sp_plan_edges, dim3(1), dim3(64), 0, st,
+                       reinterpret_cast<const skml_dense_header*>(qpayload), init, gp);
+    return hipGetLastError();
+}
+hipError_t launch_sp_plan_groups(hipStream_t st, SpGroups* gp, const uint64_t* sizes) {
+    hipLaunchKernelGGL(k_sp_plan_groups, dim3(1), dim3(64), 0, st, gp, sizes);
+    return hipGetLastError();
+}
+hipError_t launch_sp_plan_delta(hipStream_t st, SpGroups* gp, const uint32_t* hist, const uint32_t* err) {
+    hipLaunchKernelGGL(k_sp_plan_delta, dim3(1), dim3(64), 0, st, gp, hist, err);
+    return hipGetLastError();
+}
+hipError_t launch_sp_finalize(hipStream_t st, SpGroups* gp, const uint64_t* tot) {
+    hipLaunchKernelGGL(k_sp_finalize, dim3(1), dim3(64), 0, st, gp, tot);
+    return hipGetLastError();
+}
+hipError_t launch_sp_zero_edges(hipStream_t st, const uint64_t* tile_base, int64_t tiles, const SpGroups* gp,
+                                uint64_t* flag_words, uint64_t* delta_words) {
+    const unsigned grid = (unsigned)((tiles + 1 + kSpThreads - 1) / kSpThreads);
+    hipLaunchKernelGGL(k_sp_zero_edges, dim3(grid), dim3(kSpThreads), 0, st, tile_base, tiles, gp, flag_words,
+                       delta_words);
     return hipGetLastError();
 }
 

@@ -11,6 +11,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <tuple>
 #include <vector>
@@ -54,7 +55,11 @@ enum {
     kSlotStatus,
     kSlotCellIdx,
     kSlotTileOff,
+    kSlotCKeys,     // toSparse output of skml_sparse_encode_f32
+    kSlotCVals,
+    kSlotDeltaEnc,  // standalone DeltaAdaptiveEncoder: group table + stream words
 };
+static_assert(kSlotDeltaEnc < kScratchSlots, "scratch slots");
 
 // java.util.Random (JDK 8 spec): seed scramble, next(bits), nextInt(bound).
 struct JavaRandom {
@@ -106,38 +111,6 @@ int group_edges(int32_t zero, int32_t bins, int32_t G, int32_t* edges) {
 }
 
 int32_t log2nlz(int32_t k) { return 31 - __builtin_clz((uint32_t)k); }
-
-// DeltaAdaptiveEncoder.calOptimalIntervals (binary/DeltaAdaptiveEncoder.java:23-51), in the
-// reference's double summation order; prob[i] = count[i] / size.
-void delta_choose(const uint32_t* count, int64_t size, int32_t* m_out, int32_t* kind_out) {
-    double prob[32];
-    for (int i = 0; i < 32; i++) prob[i] = (double)count[i] / (double)size;
-    double best = 32.0;
-    int32_t bm = 1, bk = 0;
-    for (int32_t m = 2; m <= 16; m *= 2) {
-        double iprob[16] = {0};
-        const int32_t b = 32 / m;
-        double sum = 0.0;
-        for (int32_t i = 0; i < m; i++) {
-            for (int32_t j = 0; j < b; j++) iprob[i] += prob[i * b + j];
-            sum += (i + 1) * iprob[i];
-        }
-        const double t1 = sum * b + log2nlz(m);
-        if (t1 < best) {
-            best = t1;
-            bm = m;
-            bk = 0;
-        }
-        const double t2 = sum * (b + 1) + 1;
-        if (t2 < best) {
-            best = t2;
-            bm = m;
-            bk = 1;
-        }
-    }
-    *m_out = bm;
-    *kind_out = bk;
-}
 
 // MinMaxSketch.compare with Java int wrap (MinMaxSketch.java:80-86)
 int32_t mm_dist(int32_t v, int32_t zero) {
@@ -254,6 +227,8 @@ struct skml_sparse {
     std::vector<double> splits;
     std::vector<double> qvalues;  // SparseVectorCompressor.quantValues (getValues, timesBy'd)
     SpGroups g{};               // host copy (complete after encode)
+    void* block = nullptr;      // encode: one pooled device block holding everything below
+    size_t block_cap = 0;
     SpGroups* g_dev = nullptr;  // device copy
     int32_t* tables = nullptr;  // all groups' MinMaxSketch tables, rows x cols each
     int64_t ncells = 0;
@@ -272,14 +247,97 @@ struct skml_sparse {
 
 namespace {
 
+// Device blocks of encoded payloads, recycled across encodes: a hipMalloc / hipFree pair per
+// payload cost more than all the rest of an encode's host work (hipFree also waits for the
+// device).  Every sparse call completes its device work before it returns (a failing encode
+// synchronises before releasing), so a freed payload's block has no pending users.
+struct BlockPool {
+    struct Blk {
+        int dev;
+        void* p;
+        size_t cap;
+    };
+    std::mutex mu;
+    std::vector<Blk> free;
+};
+constexpr size_t kPoolMaxBlocks = 8;
+BlockPool& block_pool() {
+    static BlockPool* bp = new BlockPool();  // never destroyed: payloads may be freed during exit
+    return *bp;
+}
+void pool_drop(std::vector<BlockPool::Blk>& v, int cur_dev) {
+    for (const auto& b : v) {
+        (void)hipSetDevice(b.dev);
+        (void)hipFree(b.p);
+    }
+    if (!v.empty()) (void)hipSetDevice(cur_dev);
+}
+// smallest pooled block of `dev` holding `bytes` without wasting more than bytes + 64 MiB
+void* block_get(int dev, size_t bytes, size_t* cap) {
+    BlockPool& bp = block_pool();
+    {
+        std::lock_guard<std::mutex> lk(bp.mu);
+        size_t best = bp.free.size();
+        for (size_t i = 0; i < bp.free.size(); i++) {
+            const BlockPool::Blk& b = bp.free[i];
+            if (b.dev == dev && b.cap >= bytes && b.cap <= 2 * bytes + ((size_t)64 << 20) &&
+                (best == bp.free.size() || b.cap < bp.free[best].cap))
+                best = i;
+        }
+        if (best < bp.free.size()) {
+            void* p = bp.free[best].p;
+            *cap = bp.free[best].cap;
+            bp.free.erase(bp.free.begin() + (ptrdiff_t)best);
+            return p;
+        }
+    }
+    const size_t c = align_up(std::max<size_t>(bytes, 1), (size_t)2 << 20);
+    void* p = nullptr;
+    if (hipMalloc(&p, c) != hipSuccess) {  // out of memory: return this device's pooled blocks, retry once
+        (void)hipGetLastError();
+        std::vector<BlockPool::Blk> drop;
+        {
+            std::lock_guard<std::mutex> lk(bp.mu);
+            for (size_t i = 0; i < bp.free.size();)
+                if (bp.free[i].dev == dev) {
+                    drop.push_back(bp.free[i]);
+                    bp.free.erase(bp.free.begin() + (ptrdiff_t)i);
+                } else {
+                    i++;
+                }
+        }
+        pool_drop(drop, dev);
+        if (hipMalloc(&p, c) != hipSuccess) return nullptr;
+    }
+    *cap = c;
+    return p;
+}
+void block_put(int dev, void* p, size_t cap) {
+    BlockPool& bp = block_pool();
+    std::vector<BlockPool::Blk> drop;
+    {
+        std::lock_guard<std::mutex> lk(bp.mu);
+        bp.free.push_back(BlockPool::Blk{dev, p, cap});
+        while (bp.free.size() > kPoolMaxBlocks) {
+            drop.push_back(bp.free.front());
+            bp.free.erase(bp.free.begin());
+        }
+    }
+    pool_drop(drop, dev);
+}
+
 void sparse_release(skml_sparse* s) {
     if (!s) return;
     (void)hipSetDevice(s->device);
-    if (s->qpayload) (void)hipFree(s->qpayload);
-    if (s->g_dev) (void)hipFree(s->g_dev);
-    if (s->tables) (void)hipFree(s->tables);
-    if (s->flag_words) (void)hipFree(s->flag_words);
-    if (s->delta_words) (void)hipFree(s->delta_words);
+    if (s->block) {
+        block_put(s->device, s->block, s->block_cap);
+    } else {
+        if (s->qpayload) (void)hipFree(s->qpayload);
+        if (s->g_dev) (void)hipFree(s->g_dev);
+        if (s->tables) (void)hipFree(s->tables);
+        if (s->flag_words) (void)hipFree(s->flag_words);
+        if (s->delta_words) (void)hipFree(s->delta_words);
+    }
     if (s->huff_words) (void)hipFree(s->huff_words);
     delete s;
 }
@@ -309,56 +367,27 @@ int scan_tiles(skml_ctx* c, uint64_t* sums, int64_t tiles, int K, uint64_t* tota
     return SKML_OK;
 }
 
-// DeltaAdaptive bit streams for the groups of s->g over grouped keys gk (n elements): interval
-// choice from the bitsNeeded histogram, lengths, scan, writer; fills s->g.fb/db and the words.
-int encode_delta_streams(skml_ctx* c, skml_sparse* s, const int32_t* gk, const uint8_t* need,
-                         const uint32_t* hist_host) {
+// Worst-case stream words of n keys: 17 flag bits (unary, 16 intervals) and 32 delta bits each,
+// the trailing word, and the edge words' slack.
+inline int64_t flag_words_max(int64_t n) { return (17 * n + 63) / 64 + 3; }
+inline int64_t delta_words_max(int64_t n) { return (32 * n + 63) / 64 + 3; }
+
+// DeltaAdaptiveEncoder.encode (binary/DeltaAdaptiveEncoder.java:54-109) of every group of g_dev
+// over the grouped keys gk (n of them), all on the stream: interval choice from the bitsNeeded
+// histogram, bit lengths, their scan, the edge words, the writer, the group bases.
+int encode_delta_device(skml_ctx* c, SpGroups* g_dev, const int32_t* gk, const uint8_t* need, int64_t n,
+                        const uint32_t* hist, const uint32_t* err, uint64_t* fw, uint64_t* dw) {
     hipStream_t st = ctx_stream(c);
-    SpGroups& G = s->g;
-    const int64_t n = s->nnz;
-    int32_t k1 = 0;
-    for (int g = 0; g < G.G; g++) {
-        const int64_t m = G.gstart[g + 1] - G.gstart[g];
-        G.kind1_before[g] = k1;
-        if (m == 0) {
-            G.m[g] = 1;
-            G.kind[g] = 0;
-            continue;
-        }
-        uint32_t cnt[32];
-        for (int i = 0; i < 32; i++) cnt[i] = hist_host[g * kDeltaHist + i];
-        // bitsNeeded == 32 cannot occur for positive int deltas; fold it in for safety
-        cnt[31] += hist_host[g * kDeltaHist + 32];
-        delta_choose(cnt, m, &G.m[g], &G.kind[g]);
-        if (G.kind[g]) k1 += (int32_t)m;
-    }
-    if (int e = upload_groups(c, s)) return e;
     const int64_t tiles = sp_tiles(n, kSpTile);
     uint64_t* ts = scratch<uint64_t>(c, kSlotTiles, (size_t)(tiles + 1) * 2);
     if (!ts) return sfail(SKML_E_OOM, "tile sums");
-    SP_HIP(launch_delta_lens(st, need, n, s->g_dev, ts));
-    uint64_t tot[2] = {0, 0};
-    if (int e = scan_tiles(c, ts, tiles, 2, tot)) return e;
-    s->flag_bits = (int64_t)tot[0];
-    s->delta_bits = (int64_t)tot[1];
-    s->n_flag_words = (s->flag_bits + 63) / 64 + 1;
-    s->n_delta_words = (s->delta_bits + 63) / 64 + 1;
-    SP_HIP(hipMalloc(&s->flag_words, sizeof(uint64_t) * (size_t)s->n_flag_words));
-    SP_HIP(hipMalloc(&s->delta_words, sizeof(uint64_t) * (size_t)s->n_delta_words));
-    SP_HIP(hipMemsetAsync(s->flag_words, 0, sizeof(uint64_t) * (size_t)s->n_flag_words, st));
-    SP_HIP(hipMemsetAsync(s->delta_words, 0, sizeof(uint64_t) * (size_t)s->n_delta_words, st));
-    SP_HIP(launch_delta_write(st, gk, need, n, s->g_dev, ts, s->flag_words, s->delta_words));
-    // group bases: written by the kernel for non-empty groups; empty groups take the next base
-    SpGroups back;
-    if (int e = sync_to_host(c, &back, s->g_dev, sizeof(SpGroups))) return e;
-    G.fb[G.G] = s->flag_bits;
-    G.db[G.G] = s->delta_bits;
-    for (int g = G.G - 1; g >= 0; g--) {
-        const bool empty = G.gstart[g + 1] == G.gstart[g];
-        G.fb[g] = empty ? G.fb[g + 1] : back.fb[g];
-        G.db[g] = empty ? G.db[g + 1] : back.db[g];
-    }
-    return upload_groups(c, s);
+    SP_HIP(launch_sp_plan_delta(st, g_dev, hist, err));
+    SP_HIP(launch_delta_lens(st, need, n, g_dev, ts));
+    SP_HIP(launch_scan_cols(st, ts, tiles, 2));
+    SP_HIP(launch_sp_zero_edges(st, ts, tiles, g_dev, fw, dw));
+    SP_HIP(launch_delta_write(st, gk, need, n, g_dev, ts, fw, dw));
+    SP_HIP(launch_sp_finalize(st, g_dev, ts + tiles * 2));
+    return SKML_OK;
 }
 
 int check_params(const skml_params* p) {
@@ -377,6 +406,10 @@ int check_params(const skml_params* p) {
     return SKML_OK;
 }
 
+// SparseVectorCompressor.compressSparse (sample/SparseVectorCompressor.java:52-67) over
+// GroupedMinMaxSketch.insert (frequency/GroupedMinMaxSketch.java:51-121).  Everything is queued
+// on the stream without a host round trip -- the per-group decisions are made on the device
+// (k_sp_plan_*) -- and the host reads the quantizer header, splits and group table back once.
 int encode_kv(skml_ctx* c, const int32_t* keys, const float* vals, int64_t nnz, const skml_params* p,
               skml_sparse** out) {
     hipStream_t st = ctx_stream(c);
@@ -385,12 +418,36 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const float* vals, int64_t nnz, 
     s->nnz = nnz;
     s->params = *p;
     auto bail = [&](int code) {
+        (void)hipStreamSynchronize(st);  // the block returns to the pool: nothing may still use it
         sparse_release(s);
         return code;
     };
-    // ---- 1. the values' quantizer (Quantizer.newQuantizer(quantType), SparseVectorCompressor.java:60-62) ----
+#define SP_TRY(expr)                                                                                    \
+    do {                                                                                                \
+        hipError_t e_ = (expr);                                                                         \
+        if (e_ != hipSuccess) return bail(sfail(SKML_E_HIP, "%s failed: %s", #expr, hipGetErrorString(e_))); \
+    } while (0)
+    const int G = p->group_num, rows = p->row_num;
+    // ---- the payload's device block, sized for the worst case (no count has to come back first) ----
+    const double cols_all = std::ceil((double)nnz * p->col_ratio);
+    if (cols_all * rows > 4.0e12) return bail(sfail(SKML_E_OOM, "MinMaxSketch tables of colRatio %g", p->col_ratio));
+    const int64_t cells_max = nnz > 0 ? (int64_t)rows * ((int64_t)cols_all + 2 * G + 2) : 0;
+    const int64_t fwn = flag_words_max(nnz), dwn = delta_words_max(nnz);
     s->qbytes = skml_dense_payload_bytes(nnz, p->bin_num);
-    if (hipMalloc(&s->qpayload, s->qbytes) != hipSuccess) return bail(sfail(SKML_E_OOM, "quantizer payload"));
+    const size_t o_g = align_up(s->qbytes, 256);
+    const size_t o_tab = o_g + align_up(sizeof(SpGroups), 256);
+    const size_t o_fw = o_tab + align_up(sizeof(int32_t) * (size_t)std::max<int64_t>(cells_max, 1), 256);
+    const size_t o_dw = o_fw + align_up(sizeof(uint64_t) * (size_t)fwn, 256);
+    const size_t total = o_dw + sizeof(uint64_t) * (size_t)dwn;
+    char* blk = static_cast<char*>(block_get(s->device, total, &s->block_cap));
+    if (!blk) return bail(sfail(SKML_E_OOM, "sparse payload of %zu bytes", total));
+    s->block = blk;
+    s->qpayload = blk;
+    s->g_dev = reinterpret_cast<SpGroups*>(blk + o_g);
+    s->tables = reinterpret_cast<int32_t*>(blk + o_tab);
+    s->flag_words = reinterpret_cast<uint64_t*>(blk + o_fw);
+    s->delta_words = reinterpret_cast<uint64_t*>(blk + o_dw);
+    // ---- 1. the values' quantizer (Quantizer.newQuantizer(quantType), SparseVectorCompressor.java:60-62) ----
     skml_params qp = *p;
     if (int e = p->quant_type == SKML_UNIFORM
                     ? skml_dense_encode_uniform_f32(c, vals, nnz, &qp, s->qpayload, s->qbytes)
@@ -398,14 +455,72 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const float* vals, int64_t nnz, 
                                                                             s->qpayload, s->qbytes)
                                           : skml_dense_encode_f32(c, vals, nnz, &qp, s->qpayload, s->qbytes)))
         return bail(e);
-    if (int e = sync_to_host(c, &s->hdr, s->qpayload, sizeof(skml_dense_header))) return bail(e);
-    if (s->hdr.status == SKML_E_NAN) return bail(sfail(SKML_E_NAN, "Encounter NaN value"));
-    s->splits.resize((size_t)std::max(s->hdr.bin_num - 1, 0));
-    if (int e = sync_to_host(c, s->splits.data(), (const uint8_t*)s->qpayload + kHeaderBytes,
-                             sizeof(double) * s->splits.size()))
+    // ---- 2. group edges (device), partition counts, per-group MinMaxSketch shapes ----
+    SpInit init{};
+    init.G = G;
+    init.rows = rows;
+    init.col_ratio = p->col_ratio;
+    for (int g = 0; g < G; g++) pick_hashes(p->hash_seed + g, rows, init.hash_ids[g]);
+    SP_TRY(launch_sp_plan_edges(st, s->qpayload, init, s->g_dev));
+    const int64_t tiles = sp_tiles(nnz, kSpTile);
+    uint64_t* tc = scratch<uint64_t>(c, kSlotTiles, (size_t)(tiles + 1) * G);
+    if (!tc) return bail(sfail(SKML_E_OOM, "tile counts"));
+    SP_TRY(launch_part_count(st, s->qpayload, nnz, s->g_dev, tc));
+    SP_TRY(launch_scan_cols(st, tc, tiles, G));
+    SP_TRY(launch_sp_plan_groups(st, s->g_dev, tc + tiles * G));
+    // ---- 3. partition, deltas / histogram / order check, bucketed MinMax insert ----
+    int32_t* gk = scratch<int32_t>(c, kSlotGKeys, (size_t)nnz);
+    int32_t* gb = scratch<int32_t>(c, kSlotGBins, (size_t)nnz);
+    uint8_t* need = scratch<uint8_t>(c, kSlotNeed, (size_t)nnz);
+    const int nbuckets = (int)((cells_max + kMmCellsPerBucket - 1) / kMmCellsPerBucket);
+    uint64_t* bucket = scratch<uint64_t>(c, kSlotCells, (size_t)2 * nbuckets + 2);  // counts->bases, cursors
+    uint64_t* pairs = scratch<uint64_t>(c, kSlotDelta, (size_t)rows * (size_t)nnz);
+    uint32_t* small = scratch<uint32_t>(c, kSlotSmall, (size_t)kMaxGroups * kDeltaHist + 64);
+    if (!gk || !gb || !need || !bucket || !pairs || !small) return bail(sfail(SKML_E_OOM, "sparse scratch"));
+    uint64_t* cursor = bucket + nbuckets + 1;
+    uint32_t* hist = small;
+    uint32_t* err = small + kMaxGroups * kDeltaHist;
+    SP_TRY(launch_part_scatter(st, keys, s->qpayload, nnz, s->g_dev, tc, gk, gb));
+    SP_TRY(hipMemsetAsync(small, 0, sizeof(uint32_t) * ((size_t)kMaxGroups * kDeltaHist + 64), st));
+    SP_TRY(hipMemsetAsync(bucket, 0, sizeof(uint64_t) * ((size_t)2 * nbuckets + 2), st));
+    // the pairs' table cells, hashed once (int32 cells; without room or past 2^31 cells the scatter rehashes)
+    int32_t* cellbuf =
+        cells_max < INT32_MAX ? scratch<int32_t>(c, kSlotCellIdx, (size_t)rows * (size_t)nnz) : nullptr;
+    // per (tile, bucket) reserved offsets (u32: a bucket holds fewer than 2^32 pairs)
+    const int64_t mm_tiles = sp_tiles(nnz, kMmChunkElems);
+    uint32_t* tile_off = (uint64_t)rows * (uint64_t)nnz < (1ull << 32)
+                             ? scratch<uint32_t>(c, kSlotTileOff, (size_t)mm_tiles * (size_t)nbuckets)
+                             : nullptr;
+    SP_TRY(launch_group_prep(st, gk, nnz, s->g_dev, need, hist, err, bucket, nbuckets, cellbuf, tile_off));
+    SP_TRY(launch_scan_cols(st, bucket, nbuckets, 1));
+    SP_TRY(launch_mm_scatter(st, gk, gb, nnz, s->g_dev, bucket, cursor, nbuckets, pairs, cellbuf, tile_off));
+    SP_TRY(launch_mm_bucket(st, pairs, bucket, nbuckets, s->g_dev, s->tables));
+    // ---- 4. DeltaAdaptive key streams ----
+    if (int e = encode_delta_device(c, s->g_dev, gk, need, nnz, hist, err, s->flag_words, s->delta_words))
         return bail(e);
+    // ---- 5. the one read-back: quantizer header and splits, group table ----
+    const size_t qh = kHeaderBytes + sizeof(double) * (size_t)(p->bin_num - 1);
+    const size_t o_pg = align_up(qh, 256);
+    uint8_t* pin = static_cast<uint8_t*>(ctx_pinned(c, o_pg + sizeof(SpGroups)));
+    if (!pin) return bail(sfail(SKML_E_OOM, "pinned staging"));
+    SP_TRY(hipMemcpyAsync(pin, s->qpayload, qh, hipMemcpyDeviceToHost, st));
+    SP_TRY(hipMemcpyAsync(pin + o_pg, s->g_dev, sizeof(SpGroups), hipMemcpyDeviceToHost, st));
+    SP_TRY(hipStreamSynchronize(st));
+#undef SP_TRY
+    std::memcpy(&s->hdr, pin, sizeof(skml_dense_header));
+    std::memcpy(&s->g, pin + o_pg, sizeof(SpGroups));
+    if (s->hdr.status == SKML_E_NAN || (s->g.status & kSpNan)) return bail(sfail(SKML_E_NAN, "Encounter NaN value"));
+    if (s->g.status & kSpEdges) {
+        int32_t e_host[kMaxGroups];
+        const int e = group_edges(s->hdr.zero_idx, s->hdr.bin_num, G, e_host);
+        return bail(e ? e : sfail(SKML_E_HIP, "group plan disagrees with calGroupEdges"));
+    }
+    if (s->g.status & kSpOrder)
+        return bail(sfail(SKML_E_ORDER, "Log for a non-positive key delta (keys must ascend strictly)"));
     {  // Quantizer.getValues (base/Quantizer.java:39-47)
         const int B = s->hdr.bin_num, ns = B - 1;
+        const double* sp = reinterpret_cast<const double*>(pin + kHeaderBytes);
+        s->splits.assign(sp, sp + std::max(ns, 0));
         s->qvalues.resize((size_t)B);
         for (int b = 0; b < B; b++) {
             double v;
@@ -415,83 +530,11 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const float* vals, int64_t nnz, 
             s->qvalues[(size_t)b] = v;
         }
     }
-    // ---- 2. group edges, partition counts ----
-    SpGroups& G = s->g;
-    G.G = p->group_num;
-    G.rows = p->row_num;
-    G.zero = s->hdr.zero_idx;
-    G.bin_num = s->hdr.bin_num;
-    G.fill = mm_cmp(INT32_MIN, INT32_MAX, G.zero) <= 0 ? INT32_MIN : INT32_MAX;
-    if (int e = group_edges(G.zero, G.bin_num, G.G, G.edges)) return bail(e);
-    if (hipMalloc(&s->g_dev, sizeof(SpGroups)) != hipSuccess) return bail(sfail(SKML_E_OOM, "group table"));
-    if (int e = upload_groups(c, s)) return bail(e);
-    const int64_t tiles = sp_tiles(nnz, kSpTile);
-    uint64_t* tc = scratch<uint64_t>(c, kSlotTiles, (size_t)(tiles + 1) * G.G);
-    if (!tc) return bail(sfail(SKML_E_OOM, "tile counts"));
-    std::vector<uint64_t> sizes(G.G, 0);
-    if (nnz > 0) {
-        if (hipSuccess != launch_part_count(st, s->qpayload, nnz, s->g_dev, tc)) return bail(sfail(SKML_E_HIP, "part_count"));
-        if (int e = scan_tiles(c, tc, tiles, G.G, sizes.data())) return bail(e);
-    }
-    // ---- 3. per-group MinMaxSketch shape (GroupedMinMaxSketch.compOneGroup, :103-121) ----
-    G.gstart[0] = 0;
-    int64_t cells = 0;
-    for (int g = 0; g < G.G; g++) {
-        const int64_t m = (int64_t)sizes[g];
-        G.gstart[g + 1] = G.gstart[g] + m;
-        G.cols[g] = m > 0 ? (int32_t)std::ceil((double)m * p->col_ratio) : 1;
-        if (m > 0) pick_hashes(p->hash_seed + g, G.rows, G.hash_ids[g]);
-        G.tab_off[g] = cells;
-        if (m > 0) cells += (int64_t)G.rows * G.cols[g];
-    }
-    s->ncells = cells;
-    if (int e = upload_groups(c, s)) return bail(e);
-    if (nnz == 0) {
-        for (int g = 0; g <= G.G; g++) G.fb[g] = G.db[g] = 0;
-        for (int g = 0; g < G.G; g++) G.m[g] = 1;
-        if (int e = upload_groups(c, s)) return bail(e);
-        *out = s;
-        return SKML_OK;
-    }
-    int32_t* gk = scratch<int32_t>(c, kSlotGKeys, (size_t)nnz);
-    int32_t* gb = scratch<int32_t>(c, kSlotGBins, (size_t)nnz);
-    uint8_t* need = scratch<uint8_t>(c, kSlotNeed, (size_t)nnz);
-    const int nbuckets = (int)((cells + kMmCellsPerBucket - 1) / kMmCellsPerBucket);
-    uint64_t* bucket = scratch<uint64_t>(c, kSlotCells, (size_t)2 * nbuckets + 2);  // counts->bases, cursors
-    uint64_t* pairs = scratch<uint64_t>(c, kSlotDelta, (size_t)G.rows * (size_t)nnz);
-    uint32_t* small = scratch<uint32_t>(c, kSlotSmall, (size_t)kMaxGroups * kDeltaHist + 64);
-    if (!gk || !gb || !need || !bucket || !pairs || !small) return bail(sfail(SKML_E_OOM, "sparse scratch"));
-    uint64_t* cursor = bucket + nbuckets + 1;
-    if (hipSuccess != launch_part_scatter(st, keys, s->qpayload, nnz, s->g_dev, tc, gk, gb))
-        return bail(sfail(SKML_E_HIP, "part_scatter"));
-    // ---- 4. deltas / histogram / order check, then the bucketed MinMax insert ----
-    uint32_t* hist = small;
-    uint32_t* err = small + kMaxGroups * kDeltaHist;
-    if (hipMemsetAsync(small, 0, sizeof(uint32_t) * ((size_t)kMaxGroups * kDeltaHist + 64), st) != hipSuccess ||
-        hipMemsetAsync(bucket, 0, sizeof(uint64_t) * ((size_t)2 * nbuckets + 2), st) != hipSuccess)
-        return bail(sfail(SKML_E_HIP, "memset"));
-    // the pairs' table cells, hashed once (int32 cells; without room or past 2^31 cells the scatter rehashes)
-    int32_t* cellbuf = cells < INT32_MAX ? scratch<int32_t>(c, kSlotCellIdx, (size_t)G.rows * (size_t)nnz) : nullptr;
-    // per (tile, bucket) reserved offsets (u32: a bucket holds fewer than 2^32 pairs)
-    const int64_t mm_tiles = sp_tiles(nnz, kMmChunkElems);
-    uint32_t* tile_off = (uint64_t)G.rows * (uint64_t)nnz < (1ull << 32)
-                             ? scratch<uint32_t>(c, kSlotTileOff, (size_t)mm_tiles * (size_t)nbuckets)
-                             : nullptr;
-    if (hipSuccess != launch_group_prep(st, gk, nnz, s->g_dev, need, hist, err, bucket, nbuckets, cellbuf, tile_off))
-        return bail(sfail(SKML_E_HIP, "group_prep"));
-    std::vector<uint32_t> hh((size_t)kMaxGroups * kDeltaHist + 1);
-    if (int e = sync_to_host(c, hh.data(), small, sizeof(uint32_t) * hh.size())) return bail(e);
-    if (hh[(size_t)kMaxGroups * kDeltaHist])
-        return bail(sfail(SKML_E_ORDER, "Log for a non-positive key delta (keys must ascend strictly)"));
-    if (hipMalloc(&s->tables, sizeof(int32_t) * (size_t)std::max<int64_t>(cells, 1)) != hipSuccess)
-        return bail(sfail(SKML_E_OOM, "tables"));
-    if (int e = scan_tiles(c, bucket, nbuckets, 1, nullptr)) return bail(e);
-    if (hipSuccess != launch_mm_scatter(st, gk, gb, nnz, s->g_dev, bucket, cursor, nbuckets, pairs, cellbuf, tile_off) ||
-        hipSuccess != launch_mm_bucket(st, pairs, bucket, nbuckets, cells, G.zero, G.fill, s->tables))
-        return bail(sfail(SKML_E_HIP, "minmax insert"));
-    // ---- 5. DeltaAdaptive key streams ----
-    if (int e = encode_delta_streams(c, s, gk, need, hh.data())) return bail(e);
-    if (hipStreamSynchronize(st) != hipSuccess) return bail(sfail(SKML_E_HIP, "sync"));
+    s->ncells = s->g.ncells;
+    s->flag_bits = s->g.fb[G];
+    s->delta_bits = s->g.db[G];
+    s->n_flag_words = (s->flag_bits + 63) / 64 + 1;
+    s->n_delta_words = (s->delta_bits + 63) / 64 + 1;
     *out = s;
     return SKML_OK;
 }
@@ -599,21 +642,13 @@ int skml_sparse_encode_f32(skml_ctx* c, const float* dense, int64_t dim, const s
     if (!c || !out || dim < 0) return sfail(SKML_E_ARG, "bad sparse arguments");
     if (int e = check_params(p)) return e;
     SP_HIP(hipSetDevice(ctx_device(c)));
-    int32_t* keys = nullptr;
-    float* vals = nullptr;
     const size_t cap = (size_t)std::max<int64_t>(dim, 1);
-    SP_HIP(hipMalloc(&keys, sizeof(int32_t) * cap));
-    if (hipMalloc(&vals, sizeof(float) * cap) != hipSuccess) {
-        (void)hipFree(keys);
-        return sfail(SKML_E_OOM, "compaction output");
-    }
+    int32_t* keys = scratch<int32_t>(c, kSlotCKeys, cap);
+    float* vals = scratch<float>(c, kSlotCVals, cap);
+    if (!keys || !vals) return sfail(SKML_E_OOM, "compaction output");
     int64_t nnz = 0;
-    int e = skml_sparse_compact_f32(c, dense, dim, keys, vals, &nnz);
-    if (!e) e = encode_kv(c, keys, vals, nnz, p, out);
-    (void)hipStreamSynchronize(ctx_stream(c));
-    (void)hipFree(keys);
-    (void)hipFree(vals);
-    return e;
+    if (int e = skml_sparse_compact_f32(c, dense, dim, keys, vals, &nnz)) return e;
+    return encode_kv(c, keys, vals, nnz, p, out);
 }
 
 int skml_sparse_decode_f32(skml_ctx* c, const skml_sparse* s, int32_t* keys_dev, float* vals_dev) {
@@ -1336,55 +1371,41 @@ int skml_delta_encode(skml_ctx* c, const int32_t* keys, int64_t n, int32_t* num_
     G.gstart[0] = 0;
     G.gstart[1] = n;
     G.cols[0] = 1;
-    int rc = SKML_OK;
     uint8_t* need = scratch<uint8_t>(c, kSlotNeed, (size_t)n);
     uint32_t* small = scratch<uint32_t>(c, kSlotSmall, (size_t)kMaxGroups * kDeltaHist + 64);
-    if (!need || !small) return sfail(SKML_E_OOM, "delta scratch");
-    if (hipMalloc(&tmp.g_dev, sizeof(SpGroups)) != hipSuccess) return sfail(SKML_E_OOM, "group table");
-    std::vector<uint32_t> hh((size_t)kMaxGroups * kDeltaHist + 1);
-    do {
-        if ((rc = upload_groups(c, &tmp))) break;
-        if (hipMemsetAsync(small, 0, sizeof(uint32_t) * hh.size(), st) != hipSuccess) {
-            rc = sfail(SKML_E_HIP, "memset");
-            break;
-        }
-        if (launch_group_prep(st, keys, n, tmp.g_dev, need, small, small + kMaxGroups * kDeltaHist, nullptr,
-                              0, nullptr, nullptr) != hipSuccess) {
-            rc = sfail(SKML_E_HIP, "group_prep");
-            break;
-        }
-        if ((rc = sync_to_host(c, hh.data(), small, sizeof(uint32_t) * hh.size()))) break;
-        if (hh[(size_t)kMaxGroups * kDeltaHist]) {
-            rc = sfail(SKML_E_ORDER, "Log for a non-positive key delta (keys must ascend strictly)");
-            break;
-        }
-        if ((rc = encode_delta_streams(c, &tmp, keys, need, hh.data()))) break;
-        *num_intervals = G.m[0];
-        *flag_kind = G.kind[0];
-        *n_flag_bits = tmp.flag_bits;
-        *n_delta_bits = tmp.delta_bits;
-        const int64_t fw = (tmp.flag_bits + 63) / 64, dw = (tmp.delta_bits + 63) / 64;
-        if (flag_words_dev || delta_words_dev) {
-            if (fw > words_cap || dw > words_cap) {
-                rc = sfail(SKML_E_ARG, "words_cap %lld < needed %lld", (long long)words_cap, (long long)std::max(fw, dw));
-                break;
-            }
-            if (flag_words_dev && fw &&
-                hipMemcpyAsync(flag_words_dev, tmp.flag_words, sizeof(uint64_t) * fw, hipMemcpyDeviceToDevice, st) != hipSuccess)
-                rc = sfail(SKML_E_HIP, "copy flags");
-            if (!rc && delta_words_dev && dw &&
-                hipMemcpyAsync(delta_words_dev, tmp.delta_words, sizeof(uint64_t) * dw, hipMemcpyDeviceToDevice, st) != hipSuccess)
-                rc = sfail(SKML_E_HIP, "copy deltas");
-        }
-        if (!rc && hipStreamSynchronize(st) != hipSuccess) rc = sfail(SKML_E_HIP, "sync");
-    } while (0);
-    (void)hipStreamSynchronize(st);
-    (void)hipFree(tmp.g_dev);
-    if (tmp.flag_words) (void)hipFree(tmp.flag_words);
-    if (tmp.delta_words) (void)hipFree(tmp.delta_words);
-    tmp.g_dev = nullptr;
-    tmp.flag_words = tmp.delta_words = nullptr;
-    return rc;
+    const int64_t fwn = flag_words_max(n), dwn = delta_words_max(n);
+    const size_t o_w = align_up(sizeof(SpGroups), 256);
+    char* blk = static_cast<char*>(ctx_scratch(c, kSlotDeltaEnc, o_w + sizeof(uint64_t) * (size_t)(fwn + dwn)));
+    if (!need || !small || !blk) return sfail(SKML_E_OOM, "delta scratch");
+    tmp.g_dev = reinterpret_cast<SpGroups*>(blk);
+    uint64_t* fwd = reinterpret_cast<uint64_t*>(blk + o_w);
+    uint64_t* dwd = fwd + fwn;
+    int rc = upload_groups(c, &tmp);
+    tmp.g_dev = nullptr;  // scratch-owned
+    if (rc) return rc;
+    SpGroups* g_dev = reinterpret_cast<SpGroups*>(blk);
+    SP_HIP(hipMemsetAsync(small, 0, sizeof(uint32_t) * ((size_t)kMaxGroups * kDeltaHist + 1), st));
+    SP_HIP(launch_group_prep(st, keys, n, g_dev, need, small, small + kMaxGroups * kDeltaHist, nullptr, 0, nullptr,
+                             nullptr));
+    if (int e = encode_delta_device(c, g_dev, keys, need, n, small, small + kMaxGroups * kDeltaHist, fwd, dwd))
+        return e;
+    if (int e = sync_to_host(c, &G, g_dev, sizeof(SpGroups))) return e;
+    if (G.status & kSpOrder) return sfail(SKML_E_ORDER, "Log for a non-positive key delta (keys must ascend strictly)");
+    *num_intervals = G.m[0];
+    *flag_kind = G.kind[0];
+    *n_flag_bits = G.fb[1];
+    *n_delta_bits = G.db[1];
+    const int64_t fw = (G.fb[1] + 63) / 64, dw = (G.db[1] + 63) / 64;
+    if (flag_words_dev || delta_words_dev) {
+        if (fw > words_cap || dw > words_cap)
+            return sfail(SKML_E_ARG, "words_cap %lld < needed %lld", (long long)words_cap, (long long)std::max(fw, dw));
+        if (flag_words_dev && fw)
+            SP_HIP(hipMemcpyAsync(flag_words_dev, fwd, sizeof(uint64_t) * fw, hipMemcpyDeviceToDevice, st));
+        if (delta_words_dev && dw)
+            SP_HIP(hipMemcpyAsync(delta_words_dev, dwd, sizeof(uint64_t) * dw, hipMemcpyDeviceToDevice, st));
+        SP_HIP(hipStreamSynchronize(st));
+    }
+    return SKML_OK;
 }
 
 int skml_delta_decode(skml_ctx* c, int64_t n, int32_t num_intervals, int32_t flag_kind, const uint64_t* flag_words,

@@ -74,8 +74,8 @@ def main():
                      "peak": HBM, "frac": round(alg / t_e2e / 1e9 / HBM, 4)},
         "compact_gbs": round((4.0 * a.dim + 8.0 * nnz) / t_compact / 1e9, 1),
         "keys_roundtrip_exact": ok,
-        "note": "wall time of synchronising calls (encode reads group sizes and bit totals back "
-                "to the host between passes)",
+        "note": "wall time of synchronising calls (the encode plans on the device and reads the "
+                "quantizer header and group table back once; dense_to_payload adds the compaction's nnz read-back)",
     }
     print(json.dumps(line))
 
