@@ -187,6 +187,7 @@ __device__ __forceinline__ int32_t mm_dist(int32_t v, int32_t zero) {
 // in flight and takes one look-back.  Ranks follow index order: slab by slab, and within a slab
 // by float4, from wave-level scans of 16-bit packed per-slab counts plus the waves' slab totals.
 constexpr int kCompactSlabs = kCompactTile / (4 * kSpThreads);
+constexpr int kCompactStage = 4096;  // kept elements staged in LDS (32 KB); denser tiles store directly
 
 __global__ __launch_bounds__(kSpThreads) void k_compact(const float* __restrict__ x, int64_t dim,
                                                         int32_t* __restrict__ keys, float* __restrict__ vals,
@@ -195,6 +196,8 @@ __global__ __launch_bounds__(kSpThreads) void k_compact(const float* __restrict_
     __shared__ uint32_t wtot[kSpThreads / 64][kCompactSlabs];  // per-wave kept counts of each slab
     __shared__ int64_t s_tile;
     __shared__ uint64_t s_excl;
+    __shared__ int32_t stage_k[kCompactStage];
+    __shared__ float stage_v[kCompactStage];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     if (t == 0) s_tile = (int64_t)atomicAdd(ticket, 1u);
     __syncthreads();
@@ -301,6 +304,29 @@ __global__ __launch_bounds__(kSpThreads) void k_compact(const float* __restrict_
     }
     __syncthreads();
     const int64_t out0 = (int64_t)s_excl;
+    if (tile_total <= (uint32_t)kCompactStage) {  // the tile's output through LDS: coalesced stores
+#pragma unroll
+        for (int j = 0; j < kCompactSlabs; j++) {
+            const uint32_t incl = (uint32_t)(P[j >> 2] >> (16 * (j & 3))) & 0xFFFFu;
+            const uint32_t mine = (uint32_t)(own[j >> 2] >> (16 * (j & 3))) & 0xFFFFu;
+            uint32_t pos = slab_pre[j] + incl - mine;
+            const int32_t e0 = (int32_t)(base + 4 * ((int64_t)j * kSpThreads + t));
+            const float e4[4] = {f[j].x, f[j].y, f[j].z, f[j].w};
+#pragma unroll
+            for (int e = 0; e < 4; e++)
+                if ((keep >> (4 * j + e)) & 1ull) {
+                    stage_k[pos] = e0 + e;
+                    stage_v[pos] = e4[e];
+                    pos++;
+                }
+        }
+        __syncthreads();
+        for (uint32_t q = t; q < tile_total; q += kSpThreads) {
+            keys[out0 + q] = stage_k[q];
+            vals[out0 + q] = stage_v[q];
+        }
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < kCompactSlabs; j++) {
         const uint64_t incl = (P[j >> 2] >> (16 * (j & 3))) & 0xFFFFull;
@@ -483,7 +509,26 @@ static_assert(kMmBucketCells == 1 << kMmBucketBits, "bucket size");
 constexpr int kMmLdsBuckets = 8192;  // per-workgroup bucket tables in LDS up to this many (96 KB in the scatter)
 constexpr int kMmChunk = (int)kMmChunkElems;
 constexpr int kMmThreads = 1024;  // count / scatter workgroups: big tiles, long per-bucket runs
+constexpr int kMmBatch = 8;       // elements per thread in flight (count, scatter, bucket minima)
 
+// a group's MinMaxSketch shape, staged in LDS by the count pass
+struct MmGroup {
+    int64_t tab_off;
+    double inv;
+    int32_t cols;
+    int32_t hid[kMaxRows];
+};
+__device__ __forceinline__ void load_mm_groups(const SpGroups* gp, MmGroup* GP) {
+    for (int g = threadIdx.x; g < gp->G; g += blockDim.x) {
+        GP[g].tab_off = gp->tab_off[g];
+        GP[g].inv = gp->inv_cols[g];
+        GP[g].cols = gp->cols[g];
+        for (int r = 0; r < kMaxRows; r++) GP[g].hid[r] = gp->hash_ids[g][r];
+    }
+}
+// reserved pair slots of a (tile, bucket) range: whole 128-byte lines, padding = kMmNoPair
+__device__ __forceinline__ uint32_t mm_pad(uint32_t c) { return (c + 15u) & ~15u; }
+constexpr uint64_t kMmNoPair = ~0ull;
 __device__ __forceinline__ int64_t mm_cell(const SpGroups* gp, int g, int r, int32_t key) {
     const int32_t cols = gp->cols[g];
     return gp->tab_off[g] + (int64_t)r * cols + java_hash_fm(gp->hash_ids[g][r], key, cols, gp->inv_cols[g]);
@@ -505,35 +550,51 @@ __global__ __launch_bounds__(kMmThreads) void k_group_prep(const int32_t* __rest
     if (gp->status) return;
     __shared__ int64_t S[kMaxGroups + 1];
     __shared__ uint32_t H[kMaxGroups * kDeltaHist];
+    __shared__ MmGroup GP[kMaxGroups];
     extern __shared__ uint32_t BH[];  // nbuckets counters (dynamic: occupancy follows the table size)
     const int G = gp->G, rows = gp->rows;
     const bool lds_b = nbuckets <= kMmLdsBuckets;
     load_starts(gp, S);
+    load_mm_groups(gp, GP);
     for (int j = threadIdx.x; j < G * kDeltaHist; j += kMmThreads) H[j] = 0;
     if (lds_b)
         for (int j = threadIdx.x; j < nbuckets; j += kMmThreads) BH[j] = 0;
     __syncthreads();
     uint32_t bad = 0;
     const int64_t c0 = (int64_t)blockIdx.x * kMmChunk, c1 = std::min<int64_t>(n, c0 + kMmChunk);
-    for (int64_t i = c0 + threadIdx.x; i < c1; i += kMmThreads) {
-        const int g = group_of_elem(S, i);
-        const int32_t key = gkeys[i];
-        const bool first = i == S[g];
-        const int32_t d = first ? key : (int32_t)((uint32_t)key - (uint32_t)gkeys[i - 1]);
-        int nb;
-        if (first && d == 0) nb = 1;
-        else {
-            if (d <= 0) bad = 1;  // Maths.log2nlz: "Log for <d>" (util/Maths.java:16-21)
-            nb = d > 0 ? 32 - __clz(d) : 1;
+    // kMmBatch elements per thread in flight: their keys and predecessors load together
+    for (int64_t base = c0; base < c1; base += kMmBatch * kMmThreads) {
+        int32_t key[kMmBatch], prv[kMmBatch];
+#pragma unroll
+        for (int u = 0; u < kMmBatch; u++) {
+            const int64_t i = base + u * kMmThreads + threadIdx.x;
+            const int64_t j = i < c1 ? i : c1 - 1;
+            key[u] = gkeys[j];
+            prv[u] = j > 0 ? gkeys[j - 1] : 0;
         }
-        need[i] = (uint8_t)nb;
-        atomicAdd(&H[g * kDeltaHist + nb], 1u);
-        for (int r = 0; r < rows; r++) {
-            const int64_t cell = mm_cell(gp, g, r, key);
-            if (cells_out) cells_out[(int64_t)r * n + i] = (int32_t)cell;  // hashed once, reused by the scatter
-            const int b = (int)(cell >> kMmBucketBits);
-            if (lds_b) atomicAdd(&BH[b], 1u);
-            else atomicAdd(&bucket_count[b], 1ull);
+#pragma unroll
+        for (int u = 0; u < kMmBatch; u++) {
+            const int64_t i = base + u * kMmThreads + threadIdx.x;
+            if (i >= c1) continue;
+            const int g = group_of_elem(S, i);
+            const bool first = i == S[g];
+            const int32_t d = first ? key[u] : (int32_t)((uint32_t)key[u] - (uint32_t)prv[u]);
+            int nb;
+            if (first && d == 0) nb = 1;
+            else {
+                if (d <= 0) bad = 1;  // Maths.log2nlz: "Log for <d>" (util/Maths.java:16-21)
+                nb = d > 0 ? 32 - __clz(d) : 1;
+            }
+            need[i] = (uint8_t)nb;
+            atomicAdd(&H[g * kDeltaHist + nb], 1u);
+            const MmGroup& q = GP[g];
+            for (int r = 0; r < rows; r++) {
+                const int64_t cell = q.tab_off + (int64_t)r * q.cols + java_hash_fm(q.hid[r], key[u], q.cols, q.inv);
+                if (cells_out) cells_out[(int64_t)r * n + i] = (int32_t)cell;  // hashed once, reused by the scatter
+                const int b = (int)(cell >> kMmBucketBits);
+                if (lds_b) atomicAdd(&BH[b], 1u);
+                else atomicAdd(&bucket_count[b], 1ull);
+            }
         }
     }
     if (bad) atomicOr(err, 1u);
@@ -542,13 +603,15 @@ __global__ __launch_bounds__(kMmThreads) void k_group_prep(const int32_t* __rest
         if (H[j]) atomicAdd(&hist[j], H[j]);
     if (lds_b && rows > 0) {
         if (tile_off) {  // reserve this tile's range in every bucket: 8 independent atomics in flight
+            // Ranges are padded to whole 128-byte lines, so every line of the pair array is written by
+            // one workgroup only (no partial-line write-backs from two XCDs' L2s).
             uint32_t* row = tile_off + (int64_t)blockIdx.x * nbuckets;
             for (int j0 = threadIdx.x; j0 < nbuckets; j0 += 8 * kMmThreads) {
                 unsigned long long o[8];
 #pragma unroll
                 for (int u = 0; u < 8; u++) {
                     const int j = j0 + u * kMmThreads;
-                    o[u] = (j < nbuckets && BH[j]) ? atomicAdd(&bucket_count[j], (unsigned long long)BH[j]) : 0ull;
+                    o[u] = (j < nbuckets && BH[j]) ? atomicAdd(&bucket_count[j], (unsigned long long)mm_pad(BH[j])) : 0ull;
                 }
 #pragma unroll
                 for (int u = 0; u < 8; u++) {
@@ -633,28 +696,217 @@ __global__ __launch_bounds__(kMmThreads) void k_mm_scatter(const int32_t* __rest
         }
         __syncthreads();
     }
-    for (int64_t base = c0; base < c1; base += kMmUnroll * kMmThreads) {
+    if (lds_b && tile_off && cells_in) {
+        // The common path, batched for memory-level parallelism: kMmBatch elements' keys, bins and
+        // cells are loaded together (indices clamped into the tile), then ranked and stored.
+        for (int64_t base = c0; base < c1; base += kMmBatch * kMmThreads) {
+            int32_t key[kMmBatch], bin[kMmBatch];
+            int64_t idx[kMmBatch];
 #pragma unroll
-        for (int u = 0; u < kMmUnroll; u++) {
-            const int64_t i = base + u * kMmThreads + threadIdx.x;
-            if (i >= c1) break;
-            const int g = cells_in ? 0 : group_of_elem(S, i);
-            const int32_t key = gkeys[i], bin = gbins[i];
+            for (int u = 0; u < kMmBatch; u++) {
+                const int64_t i = base + u * kMmThreads + threadIdx.x;
+                idx[u] = i < c1 ? i : c1 - 1;
+                key[u] = gkeys[idx[u]];
+                bin[u] = gbins[idx[u]];
+            }
             for (int r = 0; r < rows; r++) {
-                const int64_t cell = cell_of(g, r, i, key);
-                const int b = (int)(cell >> kMmBucketBits);
-                const uint64_t dst = lds_b ? dstb[b] + atomicAdd(&cnt[b], 1u)
-                                           : bucket_base[b] + (uint64_t)atomicAdd(&cursor[b], 1ull);
-                pairs[dst] = mm_pair(key, bin, zero, cell);
+                int32_t cell[kMmBatch];
+#pragma unroll
+                for (int u = 0; u < kMmBatch; u++) cell[u] = cells_in[(int64_t)r * n + idx[u]];
+#pragma unroll
+                for (int u = 0; u < kMmBatch; u++) {
+                    if (base + u * kMmThreads + threadIdx.x >= c1) continue;
+                    const int b = cell[u] >> kMmBucketBits;
+                    pairs[dstb[b] + atomicAdd(&cnt[b], 1u)] = mm_pair(key[u], bin[u], zero, cell[u]);
+                }
+            }
+        }
+    } else {
+        for (int64_t base = c0; base < c1; base += kMmUnroll * kMmThreads) {
+#pragma unroll
+            for (int u = 0; u < kMmUnroll; u++) {
+                const int64_t i = base + u * kMmThreads + threadIdx.x;
+                if (i >= c1) break;
+                const int g = cells_in ? 0 : group_of_elem(S, i);
+                const int32_t key = gkeys[i], bin = gbins[i];
+                for (int r = 0; r < rows; r++) {
+                    const int64_t cell = cell_of(g, r, i, key);
+                    const int b = (int)(cell >> kMmBucketBits);
+                    const uint64_t dst = lds_b ? dstb[b] + atomicAdd(&cnt[b], 1u)
+                                               : bucket_base[b] + (uint64_t)atomicAdd(&cursor[b], 1ull);
+                    pairs[dst] = mm_pair(key, bin, zero, cell);
+                }
             }
         }
     }
+    if (lds_b && tile_off) {  // fill each range's padding (k_group_prep reserved mm_pad(count) slots)
+        __syncthreads();
+        for (int j = threadIdx.x; j < nbuckets * 16; j += kMmThreads) {
+            const uint32_t c = cnt[j >> 4], slot = c + (uint32_t)(j & 15);
+            if (c && slot < mm_pad(c)) pairs[dstb[j >> 4] + slot] = kMmNoPair;
+        }
+    }
+}
+
+
+// LDS-staged scatter (the common case: cells kept by k_group_prep, reserved ranges, at most
+// kStageBuckets buckets).  The tile is cut into chunks of up to 8 pairs per thread; each chunk is
+// ranked per bucket (LDS atomics), counting-sorted by bucket into LDS and stored bucket run by
+// bucket run, so the pair stores go out as runs of consecutive addresses instead of one random
+// 8-byte store per lane.  The next chunk's loads are issued before the current chunk's LDS phases.
+constexpr int kStageBuckets = 4096;
+
+template <int T>
+__device__ __forceinline__ uint32_t block_excl_scan_u32(uint32_t v, uint32_t* sh, uint32_t& total) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    uint32_t inc = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(inc, off, 64);
+        if (lane >= off) inc += y;
+    }
+    if (lane == 63) sh[w] = inc;
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+#pragma unroll
+    for (int j = 0; j < T / 64; j++) {
+        const uint32_t x = sh[j];
+        before += j < w ? x : 0u;
+        tot += x;
+    }
+    total = tot;
+    return before + inc - v;
+}
+
+template <int T>
+__global__ __launch_bounds__(T) void k_mm_scatter_staged(const int32_t* __restrict__ gkeys,
+                                                         const int32_t* __restrict__ gbins, int64_t n,
+                                                         const SpGroups* __restrict__ gp,
+                                                         const uint64_t* __restrict__ bucket_base, int nbuckets,
+                                                         uint64_t* __restrict__ pairs,
+                                                         const int32_t* __restrict__ cells_in,
+                                                         const uint32_t* __restrict__ tile_off) {
+    if (gp->status) return;
+    constexpr int kStage = 8 * T;
+    // LDS: stage[kStage] u64 | dstb[nb] u64 | lc[nb] u32 | lofs[nb + 1] u32 | sb[kStage] u16
+    extern __shared__ uint64_t dyn64[];
+    __shared__ uint32_t scan_sh[T / 64];
+    uint64_t* stage = dyn64;
+    uint64_t* dstb = stage + kStage;
+    uint32_t* lc = reinterpret_cast<uint32_t*>(dstb + nbuckets);
+    uint32_t* lofs = lc + nbuckets;
+    uint16_t* sb = reinterpret_cast<uint16_t*>(lofs + nbuckets + 1);
+    const int t = threadIdx.x, rows = gp->rows, zero = gp->zero;
+    const uint32_t* row = tile_off + (int64_t)blockIdx.x * nbuckets;
+    for (int j = t; j < nbuckets; j += T) {
+        dstb[j] = bucket_base[j] + row[j];
+        lc[j] = 0;
+    }
+    const int64_t c0 = (int64_t)blockIdx.x * kMmChunk, c1 = std::min<int64_t>(n, c0 + kMmChunk);
+    const int et = 8 / rows;  // elements per thread per chunk: et * rows <= 8 pairs each
+    const int np = et * rows;
+    const int64_t step = (int64_t)et * T;
+    constexpr int kPer = (kStageBuckets + T - 1) / T;
+    int32_t nk[8], nbn[8], nc[8];  // the next chunk's loads
+    auto load = [&](int64_t base) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const int u = k / rows, r = k - u * rows;
+            const int64_t i = base + (int64_t)u * T + t;
+            nc[k] = -1;
+            if (k < np && i < c1) {
+                nc[k] = cells_in[(int64_t)r * n + i];
+                nk[k] = gkeys[i];
+                nbn[k] = gbins[i];
+            }
+        }
+    };
+    load(c0);
+    __syncthreads();
+    for (int64_t base = c0; base < c1; base += step) {
+        uint64_t pv[8];
+        int32_t bk[8];
+        uint32_t rk[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            bk[k] = nc[k] >= 0 ? nc[k] >> kMmBucketBits : -1;
+            if (bk[k] >= 0) pv[k] = mm_pair(nk[k], nbn[k], zero, nc[k]);
+        }
+        if (base + step < c1) load(base + step);
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            if (bk[k] >= 0) rk[k] = atomicAdd(&lc[bk[k]], 1u);
+        __syncthreads();
+        // exclusive scan of the chunk's bucket counts
+        uint32_t loc[kPer], sum = 0;
+#pragma unroll
+        for (int q = 0; q < kPer; q++) {
+            const int j = t * kPer + q;
+            loc[q] = j < nbuckets ? lc[j] : 0u;
+            sum += loc[q];
+        }
+        uint32_t total;
+        uint32_t run = block_excl_scan_u32<T>(sum, scan_sh, total);
+#pragma unroll
+        for (int q = 0; q < kPer; q++) {
+            const int j = t * kPer + q;
+            if (j < nbuckets) lofs[j] = run;
+            run += loc[q];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            if (bk[k] >= 0) {
+                const uint32_t q = lofs[bk[k]] + rk[k];
+                stage[q] = pv[k];
+                sb[q] = (uint16_t)bk[k];
+            }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const uint32_t q = (uint32_t)(u * T + t);
+            if (q < total) {
+                const int b = sb[q];
+                pairs[dstb[b] + (q - lofs[b])] = stage[q];
+            }
+        }
+        __syncthreads();
+        for (int j = t; j < nbuckets; j += T)
+            if (lc[j]) {
+                dstb[j] += lc[j];
+                lc[j] = 0;
+            }
+        __syncthreads();
+    }
+    // padding of each reserved range (mm_pad(count) slots): from the range's end up to the pad
+    for (int j = t; j < nbuckets * 16; j += T) {
+        const uint64_t b0 = bucket_base[j >> 4] + row[j >> 4], e = dstb[j >> 4];
+        const uint64_t c = e - b0, slot = e + (uint64_t)(j & 15);
+        if (c && slot < b0 + mm_pad((uint32_t)c)) pairs[slot] = kMmNoPair;
+    }
+}
+constexpr int kStageThreads = 512;
+inline size_t staged_lds(int nbuckets) {
+    return (sizeof(uint64_t) + sizeof(uint16_t)) * 8 * kStageThreads + 16 * (size_t)nbuckets + 4;
 }
 
 hipError_t launch_mm_scatter(hipStream_t st, const int32_t* gkeys, const int32_t* gbins, int64_t n,
                              const SpGroups* gp, const uint64_t* bucket_base, uint64_t* cursor, int nbuckets,
                              uint64_t* pairs, const int32_t* cells, const uint32_t* tile_off) {
     if (n <= 0) return hipSuccess;
+    if (cells && tile_off && nbuckets <= kStageBuckets) {
+        static bool attr_s = false;
+        if (!attr_s) {
+            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mm_scatter_staged<kStageThreads>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)staged_lds(kStageBuckets));
+            if (e != hipSuccess) return e;
+            attr_s = true;
+        }
+        hipLaunchKernelGGL(k_mm_scatter_staged<kStageThreads>, dim3((unsigned)sp_tiles(n, kMmChunk)),
+                           dim3(kStageThreads), staged_lds(nbuckets), st, gkeys, gbins, n, gp, bucket_base, nbuckets,
+                           pairs, cells, tile_off);
+        return hipGetLastError();
+    }
     constexpr size_t kPer = sizeof(uint64_t) + sizeof(uint32_t);
     const size_t lds = nbuckets <= kMmLdsBuckets ? kPer * (size_t)(nbuckets > 0 ? nbuckets : 1) : 0;
     static bool attr = false;
@@ -684,9 +936,13 @@ __global__ __launch_bounds__(kMmThreads) void k_mm_bucket(const uint64_t* __rest
     __syncthreads();
     const uint64_t p0 = bucket_base[b], p1 = bucket_base[b + 1];
     constexpr uint64_t kLo = (uint64_t)(kMmBucketCells - 1);
-    for (uint64_t p = p0 + threadIdx.x; p < p1; p += kMmThreads) {
-        const uint64_t v = pairs[p];
-        atomicMin(&cmin[v & kLo], (unsigned long long)(v & ~kLo));
+    for (uint64_t p = p0 + threadIdx.x; p < p1; p += kMmBatch * kMmThreads) {
+        uint64_t v[kMmBatch];
+#pragma unroll
+        for (int u = 0; u < kMmBatch; u++) v[u] = p + u * kMmThreads < p1 ? pairs[p + u * kMmThreads] : kMmNoPair;
+#pragma unroll
+        for (int u = 0; u < kMmBatch; u++)
+            if (v[u] != kMmNoPair) atomicMin(&cmin[v[u] & kLo], (unsigned long long)(v[u] & ~kLo));
     }
     __syncthreads();
     const int64_t cell0 = (int64_t)b << kMmBucketBits;

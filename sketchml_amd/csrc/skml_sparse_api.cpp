@@ -474,7 +474,13 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const float* vals, int64_t nnz, 
     uint8_t* need = scratch<uint8_t>(c, kSlotNeed, (size_t)nnz);
     const int nbuckets = (int)((cells_max + kMmCellsPerBucket - 1) / kMmCellsPerBucket);
     uint64_t* bucket = scratch<uint64_t>(c, kSlotCells, (size_t)2 * nbuckets + 2);  // counts->bases, cursors
-    uint64_t* pairs = scratch<uint64_t>(c, kSlotDelta, (size_t)rows * (size_t)nnz);
+    // per (tile, bucket) reserved offsets (u32: a bucket holds fewer than 2^32 pairs)
+    const int64_t mm_tiles = sp_tiles(nnz, kMmChunkElems);
+    const bool reserve = (uint64_t)rows * (uint64_t)nnz < (1ull << 31);
+    uint32_t* tile_off = reserve ? scratch<uint32_t>(c, kSlotTileOff, (size_t)mm_tiles * (size_t)nbuckets) : nullptr;
+    // reserved ranges are padded to 16 pairs
+    const size_t npairs = (size_t)rows * (size_t)nnz + (tile_off ? (size_t)15 * mm_tiles * nbuckets : 0);
+    uint64_t* pairs = scratch<uint64_t>(c, kSlotDelta, npairs);
     uint32_t* small = scratch<uint32_t>(c, kSlotSmall, (size_t)kMaxGroups * kDeltaHist + 64);
     if (!gk || !gb || !need || !bucket || !pairs || !small) return bail(sfail(SKML_E_OOM, "sparse scratch"));
     uint64_t* cursor = bucket + nbuckets + 1;
@@ -486,11 +492,6 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const float* vals, int64_t nnz, 
     // the pairs' table cells, hashed once (int32 cells; without room or past 2^31 cells the scatter rehashes)
     int32_t* cellbuf =
         cells_max < INT32_MAX ? scratch<int32_t>(c, kSlotCellIdx, (size_t)rows * (size_t)nnz) : nullptr;
-    // per (tile, bucket) reserved offsets (u32: a bucket holds fewer than 2^32 pairs)
-    const int64_t mm_tiles = sp_tiles(nnz, kMmChunkElems);
-    uint32_t* tile_off = (uint64_t)rows * (uint64_t)nnz < (1ull << 32)
-                             ? scratch<uint32_t>(c, kSlotTileOff, (size_t)mm_tiles * (size_t)nbuckets)
-                             : nullptr;
     SP_TRY(launch_group_prep(st, gk, nnz, s->g_dev, need, hist, err, bucket, nbuckets, cellbuf, tile_off));
     SP_TRY(launch_scan_cols(st, bucket, nbuckets, 1));
     SP_TRY(launch_mm_scatter(st, gk, gb, nnz, s->g_dev, bucket, cursor, nbuckets, pairs, cellbuf, tile_off));
