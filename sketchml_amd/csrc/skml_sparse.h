@@ -89,7 +89,10 @@ hipError_t launch_group_prep(hipStream_t st, const int32_t* gkeys, int64_t n, co
 hipError_t launch_mm_scatter(hipStream_t st, const int32_t* gkeys, const int32_t* gbins, int64_t n,
                              const SpGroups* gp, const uint64_t* bucket_base, uint64_t* cursor, int nbuckets,
                              uint64_t* pairs, const int32_t* cells, const uint32_t* tile_off);
-constexpr int64_t kMmChunkElems = 65536;  // elements per workgroup tile of the count / scatter passes
+#ifndef SKML_MM_CHUNK
+#define SKML_MM_CHUNK 32768
+#endif
+constexpr int64_t kMmChunkElems = SKML_MM_CHUNK;  // elements per workgroup tile of the count / scatter passes
 // per-bucket minimum -> int32 MinMaxSketch tables (empty cells get the fill value); nbuckets may
 // exceed the table's (gp->ncells) buckets: the extra workgroups exit
 hipError_t launch_mm_bucket(hipStream_t st, const uint64_t* pairs, const uint64_t* bucket_base, int nbuckets,

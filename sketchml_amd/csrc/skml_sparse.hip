@@ -356,34 +356,44 @@ hipError_t launch_compact(hipStream_t st, const float* x, int64_t dim, int32_t* 
 // =============================================================================================
 // Column scan of [tiles][K] u64 tile sums (one workgroup per column)
 // =============================================================================================
-__global__ __launch_bounds__(kSpThreads) void k_scan_cols(uint64_t* sums, int64_t tiles, int K) {
-    __shared__ uint64_t sh[4];
-    const int k = blockIdx.x, t = threadIdx.x;
+constexpr int kScanThreads = 1024, kScanPer = 8;  // one workgroup per column, 8K entries per pass
+__global__ __launch_bounds__(kScanThreads) void k_scan_cols(uint64_t* sums, int64_t tiles, int K) {
+    __shared__ uint64_t sh[kScanThreads / 64];
+    const int k = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
     uint64_t carry = 0;
-    for (int64_t c0 = 0; c0 < tiles; c0 += kSpThreads * 8) {
-        uint64_t loc[8], s = 0;
+    for (int64_t c0 = 0; c0 < tiles; c0 += kScanThreads * kScanPer) {
+        uint64_t loc[kScanPer], s = 0;
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const int64_t i = c0 + t * 8 + j;
+        for (int j = 0; j < kScanPer; j++) {
+            const int64_t i = c0 + t * kScanPer + j;
             loc[j] = i < tiles ? sums[i * K + k] : 0;
             s += loc[j];
         }
-        uint64_t v[1] = {s}, tot[1];
-        block_excl_scan<1>(v, tot, sh);
-        uint64_t run = carry + v[0];
+        const uint64_t inc = wave_incl_u64(s, lane);
+        if (lane == 63) sh[w] = inc;
+        __syncthreads();
+        uint64_t before = 0, tot = 0;
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const int64_t i = c0 + t * 8 + j;
+        for (int j = 0; j < kScanThreads / 64; j++) {
+            const uint64_t x = sh[j];
+            before += j < w ? x : 0;
+            tot += x;
+        }
+        __syncthreads();
+        uint64_t run = carry + before + inc - s;
+#pragma unroll
+        for (int j = 0; j < kScanPer; j++) {
+            const int64_t i = c0 + t * kScanPer + j;
             if (i < tiles) sums[i * K + k] = run;
             run += loc[j];
         }
-        carry += tot[0];
+        carry += tot;
     }
     if (t == 0) sums[tiles * K + k] = carry;
 }
 
 hipError_t launch_scan_cols(hipStream_t st, uint64_t* sums, int64_t tiles, int K) {
-    hipLaunchKernelGGL(k_scan_cols, dim3(K), dim3(kSpThreads), 0, st, sums, tiles, K);
+    hipLaunchKernelGGL(k_scan_cols, dim3(K), dim3(kScanThreads), 0, st, sums, tiles, K);
     return hipGetLastError();
 }
 
