@@ -159,7 +159,11 @@ __device__ __forceinline__ void sort_regs_oddeven(T (&v)[R]) {
     constexpr int C = OddEvenNet<R>::kCount;
     constexpr auto net = OddEvenNet<R>::table();
 #pragma unroll
-    for (int c = 0; c < C; c++) ce(v[net.a[c]], v[net.b[c]]);
+    for (int c = 0; c < C; c++) {
+        ce(v[net.a[c]], v[net.b[c]]);
+        // 64 keys per lane: keep the scheduler from stretching live ranges past the register budget
+        if (R >= 64 && (c & 31) == 31) __builtin_amdgcn_sched_barrier(0);
+    }
 }
 
 // In-register bitonic sort of R keys, ascending, all comparators in "flip" form.

@@ -97,23 +97,28 @@ union MergeShared {
 // Exact path for one in-wave merge level (R keys / lane, G = 256/R lanes per merge group).
 // fb holds 1536 floats: runs in [0, 1024), merged nodes in [1024, 1536).  The element loop is
 // kept rolled and reads back from LDS so this rare path adds no register pressure.
+// More than 4 merge groups per wave (R = 32: 8 groups) take the area in passes of 4 groups.
 template <int R, typename T, typename S = typename Elem<T>::S>
 __device__ __forceinline__ void wave_exact_level(T (&v)[R], T (&w)[R / 2], int lane, uint32_t odd, S* fb) {
-    constexpr int G = 256 / R;
+    constexpr int G = 256 / R, kGroups = 64 / G, kPasses = kGroups > 4 ? kGroups / 4 : 1;
     const int grp = lane / G, li = lane % G;
-    S* run = fb + grp * 256;
-    S* out = fb + 1024 + grp * 128;
-#pragma unroll
-    for (int r = 0; r < R; r++) run[li * R + r] = Elem<T>::to_s(v[r]);
+    S* run = fb + (grp & 3) * 256;
+    S* out = fb + 1024 + (grp & 3) * 128;
 #pragma unroll 1
-    for (int r = 0; r < R; r++) {
-        const int p = li * R + r;
-        const S x = run[p];
-        const int pos = p < 128 ? p + count_le(run + 128, x) : (p - 128) + count_lt(run, x);
-        if (((uint32_t)pos & 1u) == odd) out[pos >> 1] = x;
-    }
+    for (int h = 0; h < kPasses; h++) {
+        if ((grp >> 2) != h) continue;
 #pragma unroll
-    for (int j = 0; j < R / 2; j++) w[j] = Elem<T>::from_s(out[li * (R / 2) + j]);
+        for (int r = 0; r < R; r++) run[li * R + r] = Elem<T>::to_s(v[r]);
+#pragma unroll 1
+        for (int r = 0; r < R; r++) {
+            const int p = li * R + r;
+            const S x = run[p];
+            const int pos = p < 128 ? p + count_le(run + 128, x) : (p - 128) + count_lt(run, x);
+            if (((uint32_t)pos & 1u) == odd) out[pos >> 1] = x;
+        }
+#pragma unroll
+        for (int j = 0; j < R / 2; j++) w[j] = Elem<T>::from_s(out[li * (R / 2) + j]);
+    }
 }
 
 template <int R, typename T, typename S>
@@ -534,6 +539,139 @@ __global__ __launch_bounds__(256, LeafTypes<E>::kMinWaves) void k_leaf2(
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// 64-keys-per-lane leaf (fp32, full 64-chunk tiles): 4 lanes per chunk, 16 chunks per round, 4
+// rounds per wave.  The chunk sort is Batcher's odd-even network over 64 registers (543
+// comparators) plus 3 cross-lane stages (6 with 32 keys per lane), and tree levels 1..4 run in
+// registers (levels 5 and 6 through LDS).  Same outputs as k_leaf2<3, false, float>.
+// ---------------------------------------------------------------------------------------------
+constexpr int kL64Lanes = 4;                         // lanes per chunk
+constexpr int kL64Chunks = 64 / kL64Lanes;           // chunks per round
+constexpr int kL64Rounds = kLeafWaveChunks / kL64Chunks;
+
+__global__ __launch_bounds__(256, 4) void k_leaf64(const float* __restrict__ x, int64_t chunks, uint64_t s0,
+                                                   const uint64_t* __restrict__ tab, LeafPartial* __restrict__ part,
+                                                   float* __restrict__ nodes6, float* __restrict__ roots,
+                                                   uint8_t* __restrict__ ubits) {
+    __shared__ float fb[kLeaf2Waves][kWaveFb];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t tile = (int64_t)blockIdx.x * kLeaf2Waves + wave;
+    const int64_t c_tile = tile * kLeafWaveChunks;
+    if (c_tile >= chunks) return;  // wave-uniform; no block barriers in this kernel
+    float* wfb = fb[wave];
+    const uint64_t ta = tab[lane * 2], tc = tab[lane * 2 + 1];  // A^lane, C_lane
+    uint32_t mn = ~0u, mx = 0, fl = 0u;
+    bool neg_any = false, pos_any = false;
+    float st4[2], st5[2], top[2];
+#pragma unroll 1
+    for (int round = 0; round < kL64Rounds; round++) {
+        set_prio_by_progress(round, kL64Rounds);
+        const int64_t c0 = c_tile + round * kL64Chunks;
+        const int64_t chunk = c0 + (lane >> 2);
+        float v[64];
+        uint64_t zmask = 0;
+        {
+            const float4* src = reinterpret_cast<const float4*>(x + chunk * kChunk);
+            float4 f[16];
+#pragma unroll
+            for (int j = 0; j < 16; j++) f[j] = src[j * kL64Lanes + (lane & 3)];
+#pragma unroll
+            for (int j = 0; j < 16; j++) {
+                const float e4[4] = {f[j].x, f[j].y, f[j].z, f[j].w};
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    zmask |= __ballot(is_class(e4[e], 0x63));  // -0.0 | +0.0 | NaN
+                    v[j * 4 + e] = e4[e];
+                }
+            }
+        }
+        uint32_t rfl = 0;
+        if (zmask) {  // wave-uniform: which zero signs, and NaN
+            uint64_t nz = 0, pz = 0, nan = 0;
+#pragma unroll
+            for (int r = 0; r < 64; r++) {
+                nz |= __ballot(is_class(v[r], 0x20));
+                pz |= __ballot(is_class(v[r], 0x40));
+                nan |= __ballot(is_class(v[r], 0x03));
+            }
+            rfl = (nz ? 2u : 0u) | (pz ? 4u : 0u) | (nan ? 1u : 0u);
+            fl |= rfl;
+        }
+        // compaction bits of this round's 16 chunks and their carries: draws [start, start+64)
+        const uint64_t start = node_bit_index((uint64_t)c0, 0);
+        uint64_t mask;
+        {
+            const uint64_t s_start = lcg_jump(tab, s0, start + 1);
+            const uint64_t s = lane == 0 ? s_start : ((ta * s_start + tc) & kLcgMask);
+            mask = __ballot((s >> 47) & 1ull);
+        }
+        neg_any = neg_any || (rfl & 2u);
+        pos_any = pos_any || (rfl & 4u);
+        const bool exact = neg_any && pos_any;
+        // c0 is a multiple of 16, so the draw of the level-L node ending at chunk c0 + d sits at
+        // offset 2d - popcount(d) + L from `start`: a per-lane constant
+        auto bit = [&](int level, int d) -> uint32_t {
+            return (uint32_t)(mask >> (2 * d - __popc((unsigned)d) + level)) & 1u;
+        };
+        float w1[32];
+        sort_regs_oddeven<64>(v);
+        sort_lanes_upto128<64, 128>(v, lane);  // two sorted 128-runs per chunk
+        {
+            const uint32_t k0 = total_key(v[0]), k63 = total_key(v[63]);
+            mn = k0 < mn ? k0 : mn;
+            mx = k63 > mx ? k63 : mx;
+        }
+        merge_group_compact<64>(v, w1, lane, bit(0, lane >> 2) != 0);
+        // levels 1..4 in registers: 8, 16, 32, 64 lanes per merge
+        float w2[16], w3[8], w4[4], n4[2];
+        wave_level<32>(w1, w2, lane, bit(1, 2 * (lane >> 3) + 1), exact, wfb);
+        wave_level<16>(w2, w3, lane, bit(2, 4 * (lane >> 4) + 3), exact, wfb);
+        wave_level<8>(w3, w4, lane, bit(3, 8 * (lane >> 5) + 7), exact, wfb);
+        wave_level<4>(w4, n4, lane, bit(4, 15), exact, wfb);
+        // levels 5 and 6: the binary-counter carry over rounds (older node first)
+        if (!(round & 1)) {
+            st4[0] = n4[0];
+            st4[1] = n4[1];
+            continue;
+        }
+        float n5[2];
+        wave_node_merge(st4, n4, n5, lane, bit(5, 15), exact, wfb);
+        if (!(round & 2)) {
+            st5[0] = n5[0];
+            st5[1] = n5[1];
+            continue;
+        }
+        wave_node_merge(st5, n5, top, lane, bit(6, 15), exact, wfb);
+    }
+    // one compaction bit of the upper merge tree per wave (upper_level_offset numbering)
+    if (ubits && tile < upper_node_count(chunks)) {
+        int L = kLeafTopLevel + 1;
+        int64_t i = tile;
+        while (i >= (chunks >> L)) i -= chunks >> L++;
+        const uint64_t c = ((uint64_t)(i + 1) << L) - 1;
+        if (lane == 0) ubits[tile] = (uint8_t)lcg_bit(tab, s0, node_bit_index(c, L));
+    }
+    store_node<2>(top, lane, nodes6 + (size_t)tile * kK);
+    if (((chunks >> 6) & 1) && tile == ((chunks >> 7) << 1)) store_node<2>(top, lane, roots + (size_t)6 * kK);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const uint32_t omn = __shfl_xor(mn, off, 64);
+        const uint32_t omx = __shfl_xor(mx, off, 64);
+        const uint32_t ofl = (uint32_t)__shfl_xor((int)fl, off, 64);
+        mn = omn < mn ? omn : mn;
+        mx = omx > mx ? omx : mx;
+        fl |= ofl;
+    }
+    if (lane == 0) {
+        LeafPartial p;
+        p.min_key = mn;
+        p.max_key = mx;
+        p.flags = fl | ((mn < 0x007FFFFFu || mx > 0xFF800000u) ? 1u : 0u);
+        p.pad = 0;
+        part[tile] = p;
+    }
+}
+
 template <int STAGE, int MINW = 1>
 __global__ __launch_bounds__(512, MINW) void k_leaf(const float* __restrict__ x, int64_t chunks,
                                               uint64_t s0, const uint64_t* __restrict__ tab,
@@ -702,9 +840,8 @@ hipError_t launch_leaf(hipStream_t st, const float* x, int64_t chunks, uint64_t 
                        const uint64_t* jump_tab, LeafPartial* part, float* nodes6, float* roots, uint8_t* ubits) {
     const int64_t full = chunks / kLeafWaveChunks;
     if (full > 0)
-        hipLaunchKernelGGL((k_leaf2<3, false>), dim3((unsigned)((full + kLeaf2Waves - 1) / kLeaf2Waves)),
-                           dim3(64 * kLeaf2Waves), 0, st, x, full * kLeafWaveChunks, s0, jump_tab, part,
-                           nodes6, roots, (int64_t)0, ubits);
+        hipLaunchKernelGGL(k_leaf64, dim3((unsigned)((full + kLeaf2Waves - 1) / kLeaf2Waves)), dim3(64 * kLeaf2Waves),
+                           0, st, x, full * kLeafWaveChunks, s0, jump_tab, part, nodes6, roots, ubits);
     if (chunks % kLeafWaveChunks)  // the small trees of the last chunks: one wave
         hipLaunchKernelGGL((k_leaf2<3, true>), dim3(1), dim3(64), 0, st, x, chunks, s0, jump_tab, part,
                            nodes6, roots, full);
