@@ -549,11 +549,15 @@ constexpr int kL64Lanes = 4;                         // lanes per chunk
 constexpr int kL64Chunks = 64 / kL64Lanes;           // chunks per round
 constexpr int kL64Rounds = kLeafWaveChunks / kL64Chunks;
 
-__global__ __launch_bounds__(256, 4) void k_leaf64(const float* __restrict__ x, int64_t chunks, uint64_t s0,
+#ifndef SKML_LEAF64_WAVES
+#define SKML_LEAF64_WAVES 4
+#endif
+__global__ __launch_bounds__(256, SKML_LEAF64_WAVES) void k_leaf64(const float* __restrict__ x, int64_t chunks, uint64_t s0,
                                                    const uint64_t* __restrict__ tab, LeafPartial* __restrict__ part,
                                                    float* __restrict__ nodes6, float* __restrict__ roots,
                                                    uint8_t* __restrict__ ubits) {
     __shared__ float fb[kLeaf2Waves][kWaveFb];
+    __shared__ float2 stk[kLeaf2Waves][2][64];  // the carry stack (levels 4, 5) in LDS, not registers
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t tile = (int64_t)blockIdx.x * kLeaf2Waves + wave;
     const int64_t c_tile = tile * kLeafWaveChunks;
@@ -562,87 +566,104 @@ __global__ __launch_bounds__(256, 4) void k_leaf64(const float* __restrict__ x, 
     const uint64_t ta = tab[lane * 2], tc = tab[lane * 2 + 1];  // A^lane, C_lane
     uint32_t mn = ~0u, mx = 0, fl = 0u;
     bool neg_any = false, pos_any = false;
-    float st4[2], st5[2], top[2];
-#pragma unroll 1
-    for (int round = 0; round < kL64Rounds; round++) {
+    float top[2];
+    // A round either runs fast (no merge can meet both zero signs) or exact; once the wave has
+    // seen -0.0 and +0.0 it redoes the round and the rest on the exact loop, a separate code
+    // region so its LDS merge paths do not take registers from the fast one.
+    auto run_round = [&](auto ex, int round) -> bool {
+        constexpr bool EX = decltype(ex)::value;
         set_prio_by_progress(round, kL64Rounds);
-        const int64_t c0 = c_tile + round * kL64Chunks;
-        const int64_t chunk = c0 + (lane >> 2);
-        float v[64];
-        uint64_t zmask = 0;
-        {
-            const float4* src = reinterpret_cast<const float4*>(x + chunk * kChunk);
-            float4 f[16];
+            const int64_t c0 = c_tile + round * kL64Chunks;
+            const int64_t chunk = c0 + (lane >> 2);
+            float v[64];
+            uint64_t zmask = 0;
+            {
+                const float4* src = reinterpret_cast<const float4*>(x + chunk * kChunk);
+                float4 f[16];
 #pragma unroll
-            for (int j = 0; j < 16; j++) f[j] = src[j * kL64Lanes + (lane & 3)];
+                for (int j = 0; j < 16; j++) f[j] = src[j * kL64Lanes + (lane & 3)];
 #pragma unroll
-            for (int j = 0; j < 16; j++) {
-                const float e4[4] = {f[j].x, f[j].y, f[j].z, f[j].w};
+                for (int j = 0; j < 16; j++) {
+                    const float e4[4] = {f[j].x, f[j].y, f[j].z, f[j].w};
 #pragma unroll
-                for (int e = 0; e < 4; e++) {
-                    zmask |= __ballot(is_class(e4[e], 0x63));  // -0.0 | +0.0 | NaN
-                    v[j * 4 + e] = e4[e];
+                    for (int e = 0; e < 4; e++) {
+                        zmask |= __ballot(is_class(e4[e], 0x63));  // -0.0 | +0.0 | NaN
+                        v[j * 4 + e] = e4[e];
+                    }
                 }
             }
-        }
-        uint32_t rfl = 0;
-        if (zmask) {  // wave-uniform: which zero signs, and NaN
-            uint64_t nz = 0, pz = 0, nan = 0;
+            uint32_t rfl = 0;
+            if (zmask) {  // wave-uniform: which zero signs, and NaN
+                uint64_t nz = 0, pz = 0, nan = 0;
 #pragma unroll
-            for (int r = 0; r < 64; r++) {
-                nz |= __ballot(is_class(v[r], 0x20));
-                pz |= __ballot(is_class(v[r], 0x40));
-                nan |= __ballot(is_class(v[r], 0x03));
+                for (int r = 0; r < 64; r++) {
+                    nz |= __ballot(is_class(v[r], 0x20));
+                    pz |= __ballot(is_class(v[r], 0x40));
+                    nan |= __ballot(is_class(v[r], 0x03));
+                }
+                rfl = (nz ? 2u : 0u) | (pz ? 4u : 0u) | (nan ? 1u : 0u);
+                fl |= rfl;
             }
-            rfl = (nz ? 2u : 0u) | (pz ? 4u : 0u) | (nan ? 1u : 0u);
-            fl |= rfl;
-        }
-        // compaction bits of this round's 16 chunks and their carries: draws [start, start+64)
-        const uint64_t start = node_bit_index((uint64_t)c0, 0);
-        uint64_t mask;
-        {
-            const uint64_t s_start = lcg_jump(tab, s0, start + 1);
-            const uint64_t s = lane == 0 ? s_start : ((ta * s_start + tc) & kLcgMask);
-            mask = __ballot((s >> 47) & 1ull);
-        }
-        neg_any = neg_any || (rfl & 2u);
-        pos_any = pos_any || (rfl & 4u);
-        const bool exact = neg_any && pos_any;
-        // c0 is a multiple of 16, so the draw of the level-L node ending at chunk c0 + d sits at
-        // offset 2d - popcount(d) + L from `start`: a per-lane constant
-        auto bit = [&](int level, int d) -> uint32_t {
-            return (uint32_t)(mask >> (2 * d - __popc((unsigned)d) + level)) & 1u;
-        };
-        float w1[32];
-        sort_regs_oddeven<64>(v);
-        sort_lanes_upto128<64, 128>(v, lane);  // two sorted 128-runs per chunk
-        {
-            const uint32_t k0 = total_key(v[0]), k63 = total_key(v[63]);
-            mn = k0 < mn ? k0 : mn;
-            mx = k63 > mx ? k63 : mx;
-        }
-        merge_group_compact<64>(v, w1, lane, bit(0, lane >> 2) != 0);
-        // levels 1..4 in registers: 8, 16, 32, 64 lanes per merge
-        float w2[16], w3[8], w4[4], n4[2];
-        wave_level<32>(w1, w2, lane, bit(1, 2 * (lane >> 3) + 1), exact, wfb);
-        wave_level<16>(w2, w3, lane, bit(2, 4 * (lane >> 4) + 3), exact, wfb);
-        wave_level<8>(w3, w4, lane, bit(3, 8 * (lane >> 5) + 7), exact, wfb);
-        wave_level<4>(w4, n4, lane, bit(4, 15), exact, wfb);
-        // levels 5 and 6: the binary-counter carry over rounds (older node first)
-        if (!(round & 1)) {
-            st4[0] = n4[0];
-            st4[1] = n4[1];
-            continue;
-        }
-        float n5[2];
-        wave_node_merge(st4, n4, n5, lane, bit(5, 15), exact, wfb);
-        if (!(round & 2)) {
-            st5[0] = n5[0];
-            st5[1] = n5[1];
-            continue;
-        }
-        wave_node_merge(st5, n5, top, lane, bit(6, 15), exact, wfb);
-    }
+            // compaction bits of this round's 16 chunks and their carries: draws [start, start+64)
+            const uint64_t start = node_bit_index((uint64_t)c0, 0);
+            uint64_t mask;
+            {
+                const uint64_t s_start = lcg_jump(tab, s0, start + 1);
+                const uint64_t s = lane == 0 ? s_start : ((ta * s_start + tc) & kLcgMask);
+                mask = __ballot((s >> 47) & 1ull);
+            }
+            neg_any = neg_any || (rfl & 2u);
+            pos_any = pos_any || (rfl & 4u);
+            if constexpr (!EX) {
+                if (neg_any && pos_any) return false;  // mixed zero signs from here on: the exact loop
+            }
+            const bool exact = EX;
+            // c0 is a multiple of 16, so the draw of the level-L node ending at chunk c0 + d sits at
+            // offset 2d - popcount(d) + L from `start`: a per-lane constant
+            auto bit = [&](int level, int d) -> uint32_t {
+                return (uint32_t)(mask >> (2 * d - __popc((unsigned)d) + level)) & 1u;
+            };
+            float w1[32];
+            sort_regs_oddeven<64>(v);
+            sort_lanes_upto128<64, 128>(v, lane);  // two sorted 128-runs per chunk
+            {
+                const uint32_t k0 = total_key(v[0]), k63 = total_key(v[63]);
+                mn = k0 < mn ? k0 : mn;
+                mx = k63 > mx ? k63 : mx;
+            }
+            merge_group_compact<64>(v, w1, lane, bit(0, lane >> 2) != 0);
+            // levels 1..4 in registers: 8, 16, 32, 64 lanes per merge
+            float w2[16], w3[8], w4[4], n4[2];
+            wave_level<32>(w1, w2, lane, bit(1, 2 * (lane >> 3) + 1), exact, wfb);
+            wave_level<16>(w2, w3, lane, bit(2, 4 * (lane >> 4) + 3), exact, wfb);
+            wave_level<8>(w3, w4, lane, bit(3, 8 * (lane >> 5) + 7), exact, wfb);
+            wave_level<4>(w4, n4, lane, bit(4, 15), exact, wfb);
+            // levels 5 and 6: the binary-counter carry over rounds (older node first)
+            if (!(round & 1)) {
+                stk[wave][0][lane] = make_float2(n4[0], n4[1]);
+                return true;
+            }
+            float n5[2];
+            {
+                const float2 o = stk[wave][0][lane];
+                const float st4[2] = {o.x, o.y};
+                wave_node_merge(st4, n4, n5, lane, bit(5, 15), exact, wfb);
+            }
+            if (!(round & 2)) {
+                stk[wave][1][lane] = make_float2(n5[0], n5[1]);
+                return true;
+            }
+            const float2 o = stk[wave][1][lane];
+            const float st5[2] = {o.x, o.y};
+            wave_node_merge(st5, n5, top, lane, bit(6, 15), exact, wfb);
+            return true;
+    };
+    int round = 0;
+#pragma unroll 1
+    for (; round < kL64Rounds; round++)
+        if (!run_round(std::false_type{}, round)) break;
+#pragma unroll 1
+    for (; round < kL64Rounds; round++) run_round(std::true_type{}, round);
     // one compaction bit of the upper merge tree per wave (upper_level_offset numbering)
     if (ubits && tile < upper_node_count(chunks)) {
         int L = kLeafTopLevel + 1;
@@ -839,9 +860,16 @@ __global__ __launch_bounds__(512, MINW) void k_leaf(const float* __restrict__ x,
 hipError_t launch_leaf(hipStream_t st, const float* x, int64_t chunks, uint64_t s0,
                        const uint64_t* jump_tab, LeafPartial* part, float* nodes6, float* roots, uint8_t* ubits) {
     const int64_t full = chunks / kLeafWaveChunks;
-    if (full > 0)
+#ifndef SKML_LEAF64
+#define SKML_LEAF64 1
+#endif
+    if (full > 0 && SKML_LEAF64)
         hipLaunchKernelGGL(k_leaf64, dim3((unsigned)((full + kLeaf2Waves - 1) / kLeaf2Waves)), dim3(64 * kLeaf2Waves),
                            0, st, x, full * kLeafWaveChunks, s0, jump_tab, part, nodes6, roots, ubits);
+    else if (full > 0)
+        hipLaunchKernelGGL((k_leaf2<3, false>), dim3((unsigned)((full + kLeaf2Waves - 1) / kLeaf2Waves)),
+                           dim3(64 * kLeaf2Waves), 0, st, x, full * kLeafWaveChunks, s0, jump_tab, part,
+                           nodes6, roots, (int64_t)0, ubits);
     if (chunks % kLeafWaveChunks)  // the small trees of the last chunks: one wave
         hipLaunchKernelGGL((k_leaf2<3, true>), dim3(1), dim3(64), 0, st, x, chunks, s0, jump_tab, part,
                            nodes6, roots, full);
