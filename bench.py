@@ -101,7 +101,7 @@ def sq_valu(kernel):
         except Exception:
             continue
         for name, c in d.get("per_launch_mean", {}).items():
-            short = "k_leaf" if "k_leaf2" in name else name.split("(")[0].split("::")[-1]
+            short = "k_leaf" if ("k_leaf2" in name or "k_leaf64" in name) else name.split("(")[0].split("::")[-1]
             if short == kernel and "SQ_INSTS_VALU" in c:
                 best = (c["SQ_INSTS_VALU"], os.path.relpath(path, ROOT))
     return best

@@ -563,7 +563,6 @@ __global__ __launch_bounds__(256, SKML_LEAF64_WAVES) void k_leaf64(const float* 
     const int64_t c_tile = tile * kLeafWaveChunks;
     if (c_tile >= chunks) return;  // wave-uniform; no block barriers in this kernel
     float* wfb = fb[wave];
-    const uint64_t ta = tab[lane * 2], tc = tab[lane * 2 + 1];  // A^lane, C_lane
     uint32_t mn = ~0u, mx = 0, fl = 0u;
     bool neg_any = false, pos_any = false;
     float top[2];
@@ -572,16 +571,20 @@ __global__ __launch_bounds__(256, SKML_LEAF64_WAVES) void k_leaf64(const float* 
     // region so its LDS merge paths do not take registers from the fast one.
     auto run_round = [&](auto ex, int round) -> bool {
         constexpr bool EX = decltype(ex)::value;
+        // lane-derived values (selectors, draw offsets, addresses) are recomputed each round: held
+        // across the loop they push the fast path past 128 registers
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
         set_prio_by_progress(round, kL64Rounds);
             const int64_t c0 = c_tile + round * kL64Chunks;
-            const int64_t chunk = c0 + (lane >> 2);
+            const int64_t chunk = c0 + (ln >> 2);
             float v[64];
             uint64_t zmask = 0;
             {
                 const float4* src = reinterpret_cast<const float4*>(x + chunk * kChunk);
                 float4 f[16];
 #pragma unroll
-                for (int j = 0; j < 16; j++) f[j] = src[j * kL64Lanes + (lane & 3)];
+                for (int j = 0; j < 16; j++) f[j] = src[j * kL64Lanes + (ln & 3)];
 #pragma unroll
                 for (int j = 0; j < 16; j++) {
                     const float e4[4] = {f[j].x, f[j].y, f[j].z, f[j].w};
@@ -608,8 +611,10 @@ __global__ __launch_bounds__(256, SKML_LEAF64_WAVES) void k_leaf64(const float* 
             const uint64_t start = node_bit_index((uint64_t)c0, 0);
             uint64_t mask;
             {
+                // A^ln, C_lane reloaded each round (L2-resident) rather than held in 4 registers
+                const uint64_t ta = tab[ln * 2], tc = tab[ln * 2 + 1];
                 const uint64_t s_start = lcg_jump(tab, s0, start + 1);
-                const uint64_t s = lane == 0 ? s_start : ((ta * s_start + tc) & kLcgMask);
+                const uint64_t s = ln == 0 ? s_start : ((ta * s_start + tc) & kLcgMask);
                 mask = __ballot((s >> 47) & 1ull);
             }
             neg_any = neg_any || (rfl & 2u);
@@ -619,43 +624,43 @@ __global__ __launch_bounds__(256, SKML_LEAF64_WAVES) void k_leaf64(const float* 
             }
             const bool exact = EX;
             // c0 is a multiple of 16, so the draw of the level-L node ending at chunk c0 + d sits at
-            // offset 2d - popcount(d) + L from `start`: a per-lane constant
+            // offset 2d - popcount(d) + L from `start`: a per-ln constant
             auto bit = [&](int level, int d) -> uint32_t {
                 return (uint32_t)(mask >> (2 * d - __popc((unsigned)d) + level)) & 1u;
             };
             float w1[32];
             sort_regs_oddeven<64>(v);
-            sort_lanes_upto128<64, 128>(v, lane);  // two sorted 128-runs per chunk
+            sort_lanes_upto128<64, 128>(v, ln);  // two sorted 128-runs per chunk
             {
                 const uint32_t k0 = total_key(v[0]), k63 = total_key(v[63]);
                 mn = k0 < mn ? k0 : mn;
                 mx = k63 > mx ? k63 : mx;
             }
-            merge_group_compact<64>(v, w1, lane, bit(0, lane >> 2) != 0);
+            merge_group_compact<64>(v, w1, ln, bit(0, ln >> 2) != 0);
             // levels 1..4 in registers: 8, 16, 32, 64 lanes per merge
             float w2[16], w3[8], w4[4], n4[2];
-            wave_level<32>(w1, w2, lane, bit(1, 2 * (lane >> 3) + 1), exact, wfb);
-            wave_level<16>(w2, w3, lane, bit(2, 4 * (lane >> 4) + 3), exact, wfb);
-            wave_level<8>(w3, w4, lane, bit(3, 8 * (lane >> 5) + 7), exact, wfb);
-            wave_level<4>(w4, n4, lane, bit(4, 15), exact, wfb);
+            wave_level<32>(w1, w2, ln, bit(1, 2 * (ln >> 3) + 1), exact, wfb);
+            wave_level<16>(w2, w3, ln, bit(2, 4 * (ln >> 4) + 3), exact, wfb);
+            wave_level<8>(w3, w4, ln, bit(3, 8 * (ln >> 5) + 7), exact, wfb);
+            wave_level<4>(w4, n4, ln, bit(4, 15), exact, wfb);
             // levels 5 and 6: the binary-counter carry over rounds (older node first)
             if (!(round & 1)) {
-                stk[wave][0][lane] = make_float2(n4[0], n4[1]);
+                stk[wave][0][ln] = make_float2(n4[0], n4[1]);
                 return true;
             }
             float n5[2];
             {
-                const float2 o = stk[wave][0][lane];
+                const float2 o = stk[wave][0][ln];
                 const float st4[2] = {o.x, o.y};
-                wave_node_merge(st4, n4, n5, lane, bit(5, 15), exact, wfb);
+                wave_node_merge(st4, n4, n5, ln, bit(5, 15), exact, wfb);
             }
             if (!(round & 2)) {
-                stk[wave][1][lane] = make_float2(n5[0], n5[1]);
+                stk[wave][1][ln] = make_float2(n5[0], n5[1]);
                 return true;
             }
-            const float2 o = stk[wave][1][lane];
+            const float2 o = stk[wave][1][ln];
             const float st5[2] = {o.x, o.y};
-            wave_node_merge(st5, n5, top, lane, bit(6, 15), exact, wfb);
+            wave_node_merge(st5, n5, top, ln, bit(6, 15), exact, wfb);
             return true;
     };
     int round = 0;

@@ -17,7 +17,7 @@ import re
 import statistics
 
 # kernel symbol -> the name bench.py's per-kernel timers use
-ALIAS = {"k_leaf2": "k_leaf"}
+ALIAS = {"k_leaf2": "k_leaf", "k_leaf64": "k_leaf"}
 
 
 def short_name(sym):
