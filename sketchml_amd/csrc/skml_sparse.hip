@@ -522,10 +522,35 @@ constexpr int kMmThreads = 1024;  // count / scatter workgroups: big tiles, long
 constexpr int kMmBatch = 8;       // elements per thread in flight (count, scatter, bucket minima)
 
 // a group's MinMaxSketch shape, staged in LDS by the count pass
+// Unsigned division by a run-time d through a multiplier (the round-up method: exact for every
+// 32-bit dividend); sh < 0 marks d == 1.
+struct DivU32 {
+    uint32_t m;
+    int32_t sh;
+};
+__device__ __forceinline__ DivU32 divu32_make(uint32_t d) {
+    if (d <= 1) return DivU32{0u, -1};
+    const int l = 32 - __clz(d - 1);  // ceil(log2 d)
+    return DivU32{(uint32_t)(((((uint64_t)1 << l) - d) << 32) / d + 1), l - 1};
+}
+__device__ __forceinline__ uint32_t divu32(uint32_t n, DivU32 v) {
+    const uint32_t t = __umulhi(n, v.m);
+    return (t + ((n - t) >> 1)) >> v.sh;
+}
+// Int2IntHash's `code %= size; return code >= 0 ? code : code + size` (the floor modulus)
+__device__ __forceinline__ int32_t java_mod(int32_t code, int32_t d, DivU32 v) {
+    if (v.sh < 0) return 0;
+    const uint32_t u = code < 0 ? 0u - (uint32_t)code : (uint32_t)code;
+    const uint32_t rem = u - divu32(u, v) * (uint32_t)d;
+    return (code < 0 && rem) ? d - (int32_t)rem : (int32_t)rem;
+}
+
+// a group's MinMaxSketch shape, staged in LDS by the count pass
 struct MmGroup {
     int64_t tab_off;
     double inv;
     int32_t cols;
+    DivU32 div;
     int32_t hid[kMaxRows];
 };
 __device__ __forceinline__ void load_mm_groups(const SpGroups* gp, MmGroup* GP) {
@@ -533,6 +558,7 @@ __device__ __forceinline__ void load_mm_groups(const SpGroups* gp, MmGroup* GP) 
         GP[g].tab_off = gp->tab_off[g];
         GP[g].inv = gp->inv_cols[g];
         GP[g].cols = gp->cols[g];
+        GP[g].div = divu32_make((uint32_t)gp->cols[g]);
         for (int r = 0; r < kMaxRows; r++) GP[g].hid[r] = gp->hash_ids[g][r];
     }
 }
@@ -548,6 +574,73 @@ __device__ __forceinline__ uint64_t mm_pair(int32_t key, int32_t bin, int32_t ze
            ((uint64_t)(bin < zero ? 1u : 0u) << 16) | (uint64_t)(cell & (kMmBucketCells - 1));
 }
 
+// BKDRHash over 3-digit chunks (hash/BKDRHash.java:13-21).  The loop consumes a key's decimal
+// digits least significant first, code = code * seed + digit, so a full 3-digit chunk c (digits
+// d0 d1 d2, d0 the lowest) advances the code to code * seed^3 + (d0 seed^2 + d1 seed + d2), and
+// the last chunk v (1..3 digits) to code * seed^len(v) + BKDR(v).  LDS tables per seed:
+// f3[c] for full chunks, b3[v] = BKDR(v); one quarter-rate multiply per chunk instead of two per
+// digit.  Keys are >= 0 here (a negative key fails the order check; java_hash_mix keeps the
+// reference's signed digits for it).
+constexpr int kBkSeeds = 5;  // hash ids 3..7
+struct BkdrTables {
+    uint32_t f3[kBkSeeds][1000];
+    uint32_t b3[kBkSeeds][1000];
+};
+__device__ __forceinline__ uint32_t bkdr_seed(int id) {
+    return id == 3 ? 31u : id == 4 ? 131u : id == 5 ? 267u : id == 6 ? 1313u : 13131u;
+}
+__device__ __forceinline__ void load_bkdr_tables(BkdrTables* T) {
+    for (int e = threadIdx.x; e < kBkSeeds * 1000; e += blockDim.x) {
+        const int si = e / 1000, v = e % 1000;
+        const uint32_t sd = bkdr_seed(si + 3);
+        const uint32_t d0 = (uint32_t)v % 10u, d1 = (uint32_t)v / 10u % 10u, d2 = (uint32_t)v / 100u;
+        T->f3[si][v] = (d0 * sd + d1) * sd + d2;
+        uint32_t c = 0, k = (uint32_t)v;
+        while (k) {
+            c = c * sd + k % 10u;
+            k /= 10u;
+        }
+        T->b3[si][v] = c;
+    }
+}
+template <int ID>
+__device__ __forceinline__ uint32_t bkdr_fast(uint32_t k, const BkdrTables* T) {
+    constexpr uint32_t sd = ID == 3 ? 31u : ID == 4 ? 131u : ID == 5 ? 267u : ID == 6 ? 1313u : 13131u;
+    constexpr uint32_t s2 = sd * sd, s3 = s2 * sd;
+    uint32_t c = 0;
+    while (k >= 1000u) {
+        const uint32_t q = k / 1000u;
+        c = c * s3 + T->f3[ID - 3][k - q * 1000u];
+        k = q;
+    }
+    const uint32_t pw = k >= 100u ? s3 : k >= 10u ? s2 : sd;
+    return k ? c * pw + T->b3[ID - 3][k] : c;
+}
+
+// One row's cells of a batch whose group (and so hash) is uniform: the hash specialised at
+// compile time, the modulus by multiplication.  Same cells as java_hash_fm.
+template <int ID>
+__device__ __forceinline__ void mm_cells(const int32_t (&key)[kMmBatch], int64_t base, int64_t c1, int64_t n, int r,
+                                         int64_t row0, const MmGroup& q, const BkdrTables* BK,
+                                         int32_t* __restrict__ cells_out, bool lds_b, uint32_t* BH,
+                                         unsigned long long* __restrict__ bucket_count) {
+    const int32_t cols = q.cols;
+    const DivU32 dv = q.div;
+#pragma unroll
+    for (int u = 0; u < kMmBatch; u++) {
+        const int64_t i = base + u * kMmThreads + threadIdx.x;
+        if (i >= c1) continue;
+        uint32_t h;
+        if constexpr (ID >= 3) h = key[u] >= 0 ? bkdr_fast<ID>((uint32_t)key[u], BK) : java_hash_mix(ID, key[u]);
+        else h = java_hash_mix(ID, key[u]);
+        const int64_t cell = row0 + java_mod((int32_t)h, cols, dv);
+        if (cells_out) cells_out[(int64_t)r * n + i] = (int32_t)cell;  // hashed once, reused by the scatter
+        const int b = (int)(cell >> kMmBucketBits);
+        if (lds_b) atomicAdd(&BH[b], 1u);
+        else atomicAdd(&bucket_count[b], 1ull);
+    }
+}
+
 // Deltas, bitsNeeded histogram and order check (DeltaAdaptiveEncoder.encode step 1) plus the
 // per-bucket pair counts of the MinMax insert.
 __global__ __launch_bounds__(kMmThreads) void k_group_prep(const int32_t* __restrict__ gkeys, int64_t n,
@@ -561,11 +654,14 @@ __global__ __launch_bounds__(kMmThreads) void k_group_prep(const int32_t* __rest
     __shared__ int64_t S[kMaxGroups + 1];
     __shared__ uint32_t H[kMaxGroups * kDeltaHist];
     __shared__ MmGroup GP[kMaxGroups];
+    __shared__ BkdrTables BKs;
     extern __shared__ uint32_t BH[];  // nbuckets counters (dynamic: occupancy follows the table size)
     const int G = gp->G, rows = gp->rows;
     const bool lds_b = nbuckets <= kMmLdsBuckets;
+    const BkdrTables* BK = &BKs;
     load_starts(gp, S);
     load_mm_groups(gp, GP);
+    if (rows > 0) load_bkdr_tables(&BKs);
     for (int j = threadIdx.x; j < G * kDeltaHist; j += kMmThreads) H[j] = 0;
     if (lds_b)
         for (int j = threadIdx.x; j < nbuckets; j += kMmThreads) BH[j] = 0;
@@ -582,11 +678,19 @@ __global__ __launch_bounds__(kMmThreads) void k_group_prep(const int32_t* __rest
             key[u] = gkeys[j];
             prv[u] = j > 0 ? gkeys[j - 1] : 0;
         }
+        // almost every batch lies inside one group: then its hash ids are workgroup-uniform and
+        // each row's cells come from a loop specialised for that hash
+        const int64_t last = std::min<int64_t>(c1, base + kMmBatch * kMmThreads) - 1;
+        const int g_lo = group_of_elem(S, base), g_hi = group_of_elem(S, last);
+        const bool one = g_lo == g_hi;
+        int gg[kMmBatch];
 #pragma unroll
         for (int u = 0; u < kMmBatch; u++) {
             const int64_t i = base + u * kMmThreads + threadIdx.x;
+            gg[u] = 0;
             if (i >= c1) continue;
-            const int g = group_of_elem(S, i);
+            const int g = one ? g_lo : group_of_elem(S, i);
+            gg[u] = g;
             const bool first = i == S[g];
             const int32_t d = first ? key[u] : (int32_t)((uint32_t)key[u] - (uint32_t)prv[u]);
             int nb;
@@ -597,13 +701,37 @@ __global__ __launch_bounds__(kMmThreads) void k_group_prep(const int32_t* __rest
             }
             need[i] = (uint8_t)nb;
             atomicAdd(&H[g * kDeltaHist + nb], 1u);
-            const MmGroup& q = GP[g];
+        }
+        if (one) {
+            const MmGroup& q = GP[g_lo];
             for (int r = 0; r < rows; r++) {
-                const int64_t cell = q.tab_off + (int64_t)r * q.cols + java_hash_fm(q.hid[r], key[u], q.cols, q.inv);
-                if (cells_out) cells_out[(int64_t)r * n + i] = (int32_t)cell;  // hashed once, reused by the scatter
-                const int b = (int)(cell >> kMmBucketBits);
-                if (lds_b) atomicAdd(&BH[b], 1u);
-                else atomicAdd(&bucket_count[b], 1ull);
+                const int id = __builtin_amdgcn_readfirstlane(q.hid[r]);
+                const int64_t row0 = q.tab_off + (int64_t)r * q.cols;
+                switch (id) {
+                    case 0: mm_cells<0>(key, base, c1, n, r, row0, q, BK, cells_out, lds_b, BH, bucket_count); break;
+                    case 1: mm_cells<1>(key, base, c1, n, r, row0, q, BK, cells_out, lds_b, BH, bucket_count); break;
+                    case 2: mm_cells<2>(key, base, c1, n, r, row0, q, BK, cells_out, lds_b, BH, bucket_count); break;
+                    case 3: mm_cells<3>(key, base, c1, n, r, row0, q, BK, cells_out, lds_b, BH, bucket_count); break;
+                    case 4: mm_cells<4>(key, base, c1, n, r, row0, q, BK, cells_out, lds_b, BH, bucket_count); break;
+                    case 5: mm_cells<5>(key, base, c1, n, r, row0, q, BK, cells_out, lds_b, BH, bucket_count); break;
+                    case 6: mm_cells<6>(key, base, c1, n, r, row0, q, BK, cells_out, lds_b, BH, bucket_count); break;
+                    default: mm_cells<7>(key, base, c1, n, r, row0, q, BK, cells_out, lds_b, BH, bucket_count); break;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < kMmBatch; u++) {
+                const int64_t i = base + u * kMmThreads + threadIdx.x;
+                if (i >= c1) continue;
+                const MmGroup& q = GP[gg[u]];
+                for (int r = 0; r < rows; r++) {
+                    const int64_t cell =
+                        q.tab_off + (int64_t)r * q.cols + java_hash_fm(q.hid[r], key[u], q.cols, q.inv);
+                    if (cells_out) cells_out[(int64_t)r * n + i] = (int32_t)cell;
+                    const int b = (int)(cell >> kMmBucketBits);
+                    if (lds_b) atomicAdd(&BH[b], 1u);
+                    else atomicAdd(&bucket_count[b], 1ull);
+                }
             }
         }
     }
