@@ -209,7 +209,7 @@ def other_configs(sk, lib, ctx, dev, xs):
     out["sparse_c3"] = {"workload": "C3: 2^28-dim dense fp32, 10 % nnz, 256 bins, 8 groups, 2 rows, colRatio 0.3",
                         "nnz": nnz, "encode_ms": round(te * 1e3, 3), "gbps_dense_in": round(4.0 * dim / te / 1e9, 1),
                         "roofline_frac": round(alg / te / 1e9 / HBM_PEAK_GBS, 4), "restore_ms": round(td * 1e3, 3),
-                        "note": "median wall time of 5 synchronised calls (host reads group sizes between passes)"}
+                        "note": "median wall time of 5 synchronised calls (one nnz read after the compaction, one read-back at the end)"}
     return out
 
 

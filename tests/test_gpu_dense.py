@@ -86,6 +86,24 @@ def test_quantize_edge_data(gpu, kind, n):
     _check(gq, oq, x)
 
 
+def test_leaf_exact_path_handover(gpu):
+    """The 64-keys-per-lane leaf runs a wave's rounds on a fast loop until the wave has seen both
+    -0.0 and +0.0, then redoes that round and the rest on the exact-merge loop.  Zeros placed so
+    that the switch happens in rounds 0..3 of different waves (16 chunks per round, 64 per wave),
+    with the carry stack already holding nodes from the fast loop."""
+    n = 2**20 + 4097  # 64 full 64-chunk tiles plus a partial one
+    x = _data(n, 11, "normal")
+    chunk = lambda tile, c: (tile * 64 + c) * 256
+    for tile, c_neg, c_pos in [(1, 0, 0), (3, 20, 50), (5, 33, 34), (8, 5, 63), (9, 63, 2), (20, 47, 48)]:
+        x[chunk(tile, c_neg) + 7] = -0.0
+        x[chunk(tile, c_pos) + 100] = 0.0
+    x[chunk(30, 12) + 1] = -0.0  # only one sign: stays on the fast loop
+    for seed in (5, 6):
+        gq = gpu.QuantileQuantizer(256, seed=seed)
+        gq.quantize(torch.from_numpy(x).cuda())
+        _check(gq, O.quantize(x.astype(np.float64), 256, seed), x)
+
+
 @pytest.mark.parametrize("bins", [2, 3, 4, 16, 17, 255, 256, 1000, 4096])
 def test_bin_counts_and_code_widths(gpu, bins):
     n = 3 * 2**16 + 999
