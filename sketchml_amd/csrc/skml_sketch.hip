@@ -639,10 +639,18 @@ __global__ __launch_bounds__(256, SKML_LEAF64_WAVES) void k_leaf64(const float* 
             merge_group_compact<64>(v, w1, ln, bit(0, ln >> 2) != 0);
             // levels 1..4 in registers: 8, 16, 32, 64 lanes per merge
             float w2[16], w3[8], w4[4], n4[2];
+#ifdef SKML_LEAF_ABLATE_TREE  // profiling ablation: levels 1..4 replaced by a fold (wrong results)
+            for (int q = 0; q < 16; q++) w2[q] = fminf(w1[2 * q], w1[2 * q + 1]);
+            for (int q = 0; q < 8; q++) w3[q] = w2[2 * q];
+            for (int q = 0; q < 4; q++) w4[q] = w3[2 * q];
+            n4[0] = w4[0];
+            n4[1] = w4[2];
+#else
             wave_level<32>(w1, w2, ln, bit(1, 2 * (ln >> 3) + 1), exact, wfb);
             wave_level<16>(w2, w3, ln, bit(2, 4 * (ln >> 4) + 3), exact, wfb);
             wave_level<8>(w3, w4, ln, bit(3, 8 * (ln >> 5) + 7), exact, wfb);
             wave_level<4>(w4, n4, ln, bit(4, 15), exact, wfb);
+#endif
             // levels 5 and 6: the binary-counter carry over rounds (older node first)
             if (!(round & 1)) {
                 stk[wave][0][ln] = make_float2(n4[0], n4[1]);
