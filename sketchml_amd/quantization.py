@@ -33,9 +33,14 @@ class Quantizer:
 
     DEFAULT_BIN_NUM = 256
 
-    def __init__(self, binNum: int = DEFAULT_BIN_NUM, seed: int = 0):
+    def __init__(self, binNum: int = DEFAULT_BIN_NUM, seed: int = 0, deferred: bool = False):
+        """deferred=True: quantize() only queues the encode on the stream and returns (no host
+        synchronisation; the payload buffer is reused across calls); the header is read, and a
+        NaN input raises QuantileSketchException, at the first getter (getBins, getSplits,
+        writeObject, ...).  The default keeps the reference's eager behaviour."""
         self.binNum = int(binNum)
         self.seed = int(seed)
+        self._deferred = bool(deferred)
         self.n = 0
         self.payload = None          # torch.uint8 device tensor
         self.device = None
@@ -77,6 +82,7 @@ class Quantizer:
             self._hdr = hdr
             self._splits = splits[: hdr.bin_num - 1].copy()
             self.binNum = hdr.bin_num
+            self._x = None  # a deferred encode has consumed its input
         return self._hdr
 
     _ENTRY = {(False, False): "skml_dense_encode_f32", (False, True): "skml_dense_encode_f64",
@@ -92,7 +98,9 @@ class Quantizer:
         nbytes = _lib.lib.skml_dense_payload_bytes(self.n, self.binNum)
         if nbytes == 0:
             raise SketchMLException(f"bad quantizer arguments n={self.n} binNum={self.binNum}")
-        self.payload = alloc_aligned(nbytes, x.device)
+        if not (self._deferred and self.payload is not None and self.payload.numel() >= nbytes
+                and self.payload.device == x.device):
+            self.payload = alloc_aligned(nbytes, x.device)
         p = _lib.Params()
         _lib.lib.skml_params_default(C.byref(p))
         p.bin_num = self.binNum
@@ -110,8 +118,8 @@ class Quantizer:
         self._hdr = None
         self._bins = None
         self._x = x  # keep the input alive until the stream has consumed it
-        self._load_header()  # surfaces NaN as QuantileSketchException, like update() throws
-        self._x = None
+        if not self._deferred:
+            self._load_header()  # surfaces NaN as QuantileSketchException, like update() throws
 
     def _encode_sharded(self, values, shard_sizes, shard: int, records: torch.Tensor, dedup: bool = False):
         """Quantise shard `shard` of one logical gradient against the split table of the merged
@@ -272,8 +280,8 @@ class QuantileQuantizer(Quantizer):
     Random (QSketchUtils.java:9): same seed -> same splits and bins as the oracle.
     """
 
-    def __init__(self, binNum: int = Quantizer.DEFAULT_BIN_NUM, seed: int = 0):
-        super().__init__(binNum, seed)
+    def __init__(self, binNum: int = Quantizer.DEFAULT_BIN_NUM, seed: int = 0, deferred: bool = False):
+        super().__init__(binNum, seed, deferred)
 
     def quantize(self, values) -> None:
         """QuantileQuantizer.quantize (QuantileQuantizer.java:27-50)."""
@@ -334,8 +342,8 @@ class UniformQuantizer(Quantizer):
     Java min and max (MAX_VALUE / MIN_VALUE initialised), no Maths.unique, NaN values binned by
     indexOf rather than rejected."""
 
-    def __init__(self, binNum: int = Quantizer.DEFAULT_BIN_NUM, seed: int = 0):
-        super().__init__(binNum, seed)
+    def __init__(self, binNum: int = Quantizer.DEFAULT_BIN_NUM, seed: int = 0, deferred: bool = False):
+        super().__init__(binNum, seed, deferred)
 
     def quantize(self, values) -> None:
         """UniformQuantizer.quantize (UniformQuantizer.java:21-45)."""

@@ -86,6 +86,21 @@ def test_quantize_edge_data(gpu, kind, n):
     _check(gq, oq, x)
 
 
+def test_deferred_quantize(gpu):
+    """deferred=True queues the encode without a host synchronisation and reuses the payload;
+    results equal the eager path, and NaN surfaces at the first getter."""
+    q = gpu.QuantileQuantizer(256, seed=3, deferred=True)
+    for n, s in [(2**20 + 5, 1), (2**20 + 5, 2), (70000, 3)]:
+        x = _data(n, s, "normal")
+        req = q.binNum  # Quantizer.binNum becomes the effective count after each quantize (Java too)
+        q.quantize(torch.from_numpy(x).cuda())
+        _check(q, O.quantize(x.astype(np.float64), req, 3), x)
+    x[5] = np.nan
+    q.quantize(torch.from_numpy(x).cuda())  # queued: no exception yet
+    with pytest.raises(gpu.QuantileSketchException):
+        q.getBinNum()
+
+
 def test_leaf_exact_path_handover(gpu):
     """The 64-keys-per-lane leaf runs a wave's rounds on a fast loop until the wave has seen both
     -0.0 and +0.0, then redoes that round and the rest on the exact-merge loop.  Zeros placed so
