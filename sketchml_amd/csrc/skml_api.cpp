@@ -66,6 +66,7 @@ struct skml_ctx {
     // batched encode: a child context (own high-priority stream and workspace) and its events
     skml_ctx* side = nullptr;
     hipEvent_t ev_join = nullptr, ev_leaf = nullptr;
+    hipEvent_t ev_fork2 = nullptr, ev_join2 = nullptr;  // sparse encode: its side-stream chain
     hipEvent_t after_leaf = nullptr;  // when set, recorded right after the next leaf launch
     hipEvent_t ev_switch = nullptr;   // skml_ctx_set_stream: orders the new stream after the old one
     // parallelQuantize: slice records + the merged sketch's export (grow-only)
@@ -365,6 +366,8 @@ int skml_ctx_destroy(skml_ctx* c) {
     if (c->side) skml_ctx_destroy(c->side);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     if (c->ev_leaf) (void)hipEventDestroy(c->ev_leaf);
+    if (c->ev_fork2) (void)hipEventDestroy(c->ev_fork2);
+    if (c->ev_join2) (void)hipEventDestroy(c->ev_join2);
     if (c->ev_switch) (void)hipEventDestroy(c->ev_switch);
     if (c->sk) (void)hipFree(c->sk);
     for (int k = 0; k < SKML_K_COUNT; k++)
@@ -793,6 +796,30 @@ int skml_dense_encode_parallel_f32(skml_ctx* c, const float* x, int64_t n, int32
 // which a single stream serialises.  Ordered after earlier work on ctx's stream; ctx's stream
 // waits for all buckets.  (Forking both lanes off the caller's stream with events measured no
 // overlap at all when that stream is the legacy null stream.)
+}  // extern "C"
+
+// The side context: a child context on its own stream, created at high priority (HIP keeps
+// hardware queues per priority, so the two never share a queue; with GPU_MAX_HW_QUEUES = 4, a
+// normal-priority stream created after the framework's own streams was measured to share one and
+// serialise the lanes).  Used by the batched encode and the sparse encode's DeltaAdaptive chain.
+static int ensure_side(skml_ctx* c) {
+    if (c->side) return SKML_OK;
+    int lo = 0, hi = 0;
+    HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    hipStream_t s = nullptr;
+    HIP_TRY(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, hi));
+    int st = skml_ctx_create(c->device, s, &c->side);
+    if (st) {
+        (void)hipStreamDestroy(s);
+        return st;
+    }
+    c->side->own_stream = true;
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+    return SKML_OK;
+}
+
+extern "C" {
+
 int skml_dense_encode_batch_f32(skml_ctx* c, int32_t nbuckets, const float* const* xs, const int64_t* ns,
                                 const skml_params* p, void* const* payloads, const size_t* caps) {
     if (!c) return fail(SKML_E_ARG, "ctx is NULL");
@@ -810,23 +837,8 @@ int skml_dense_encode_batch_f32(skml_ctx* c, int32_t nbuckets, const float* cons
     }
     HIP_TRY(hipSetDevice(c->device));
     if (nbuckets == 1) return skml_dense_encode_f32(c, xs[0], ns[0], p, payloads[0], caps[0]);
-    // Lane 0 is the caller's stream itself; lane 1 is a child context on its own stream, created
-    // at high priority: HIP keeps hardware queues per priority, so the two never share a queue
-    // (with GPU_MAX_HW_QUEUES = 4, a normal-priority stream created after the framework's own
-    // streams was measured to share one and serialise the lanes).
-    if (!c->side) {
-        int lo = 0, hi = 0;
-        HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-        hipStream_t s = nullptr;
-        HIP_TRY(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, hi));
-        int st = skml_ctx_create(c->device, s, &c->side);
-        if (st) {
-            (void)hipStreamDestroy(s);
-            return st;
-        }
-        c->side->own_stream = true;
-        HIP_TRY(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
-    }
+    // Lane 0 is the caller's stream itself; lane 1 is the side context (ensure_side).
+    if (int st = ensure_side(c)) return st;
     if (!c->ev_leaf) HIP_TRY(hipEventCreateWithFlags(&c->ev_leaf, hipEventDisableTiming));
     skml_ctx* lane[2] = {c, c->side};
     // lane 1 starts when bucket 0's sketch pass is done (which also orders it after earlier work
@@ -1794,6 +1806,15 @@ int skml_delta_decode_host(skml_ctx* c, int64_t n, int32_t num_intervals, int32_
 // ---- accessors used by the sparse translation unit ----
 namespace skml {
 hipStream_t ctx_stream(skml_ctx* c) { return c->stream; }
+int ctx_side_fork(skml_ctx* c, hipStream_t* side, hipEvent_t* fork, hipEvent_t* join) {
+    if (int st = ensure_side(c)) return st;
+    if (!c->ev_fork2) HIP_TRY(hipEventCreateWithFlags(&c->ev_fork2, hipEventDisableTiming));
+    if (!c->ev_join2) HIP_TRY(hipEventCreateWithFlags(&c->ev_join2, hipEventDisableTiming));
+    *side = c->side->stream;
+    *fork = c->ev_fork2;
+    *join = c->ev_join2;
+    return SKML_OK;
+}
 int ctx_device(skml_ctx* c) { return c->device; }
 int set_error(int code, const char* msg) { return fail(code, "%s", msg); }
 bool ctx_timing(skml_ctx* c) { return c->timing != 0; }

@@ -169,6 +169,8 @@ hipError_t launch_fill_i32(hipStream_t st, int32_t* dst, int64_t n, int32_t v);
 
 // ---- context services (skml_api.cpp) ----
 hipStream_t ctx_stream(skml_ctx* c);
+// the context's side stream (a high-priority child context) and two events for a fork / join
+int ctx_side_fork(skml_ctx* c, hipStream_t* side, hipEvent_t* fork, hipEvent_t* join);
 int ctx_device(skml_ctx* c);
 // grow-only device scratch buffer `slot` (< kScratchSlots) of at least `bytes`; null on failure
 constexpr int kScratchSlots = 16;

@@ -656,7 +656,9 @@ __global__ __launch_bounds__(kMmThreads) void k_group_prep(const int32_t* __rest
     __shared__ MmGroup GP[kMaxGroups];
     __shared__ BkdrTables BKs;
     extern __shared__ uint32_t BH[];  // nbuckets counters (dynamic: occupancy follows the table size)
-    const int G = gp->G, rows = gp->rows;
+    // need == nullptr: the MinMax part only; bucket_count == nullptr: the DeltaAdaptive part only
+    const bool do_delta = need != nullptr, do_mm = bucket_count != nullptr;
+    const int G = gp->G, rows = do_mm ? gp->rows : 0;
     const bool lds_b = nbuckets <= kMmLdsBuckets;
     const BkdrTables* BK = &BKs;
     load_starts(gp, S);
@@ -676,7 +678,7 @@ __global__ __launch_bounds__(kMmThreads) void k_group_prep(const int32_t* __rest
             const int64_t i = base + u * kMmThreads + threadIdx.x;
             const int64_t j = i < c1 ? i : c1 - 1;
             key[u] = gkeys[j];
-            prv[u] = j > 0 ? gkeys[j - 1] : 0;
+            prv[u] = do_delta && j > 0 ? gkeys[j - 1] : 0;
         }
         // almost every batch lies inside one group: then its hash ids are workgroup-uniform and
         // each row's cells come from a loop specialised for that hash
@@ -691,6 +693,7 @@ __global__ __launch_bounds__(kMmThreads) void k_group_prep(const int32_t* __rest
             if (i >= c1) continue;
             const int g = one ? g_lo : group_of_elem(S, i);
             gg[u] = g;
+            if (!do_delta) continue;
             const bool first = i == S[g];
             const int32_t d = first ? key[u] : (int32_t)((uint32_t)key[u] - (uint32_t)prv[u]);
             int nb;
@@ -737,8 +740,9 @@ __global__ __launch_bounds__(kMmThreads) void k_group_prep(const int32_t* __rest
     }
     if (bad) atomicOr(err, 1u);
     __syncthreads();
-    for (int j = threadIdx.x; j < G * kDeltaHist; j += kMmThreads)
-        if (H[j]) atomicAdd(&hist[j], H[j]);
+    if (do_delta)
+        for (int j = threadIdx.x; j < G * kDeltaHist; j += kMmThreads)
+            if (H[j]) atomicAdd(&hist[j], H[j]);
     if (lds_b && rows > 0) {
         if (tile_off) {  // reserve this tile's range in every bucket: 8 independent atomics in flight
             // Ranges are padded to whole 128-byte lines, so every line of the pair array is written by

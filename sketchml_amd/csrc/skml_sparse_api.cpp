@@ -375,9 +375,8 @@ inline int64_t delta_words_max(int64_t n) { return (32 * n + 63) / 64 + 3; }
 // DeltaAdaptiveEncoder.encode (binary/DeltaAdaptiveEncoder.java:54-109) of every group of g_dev
 // over the grouped keys gk (n of them), all on the stream: interval choice from the bitsNeeded
 // histogram, bit lengths, their scan, the edge words, the writer, the group bases.
-int encode_delta_device(skml_ctx* c, SpGroups* g_dev, const int32_t* gk, const uint8_t* need, int64_t n,
-                        const uint32_t* hist, const uint32_t* err, uint64_t* fw, uint64_t* dw) {
-    hipStream_t st = ctx_stream(c);
+int encode_delta_device(skml_ctx* c, hipStream_t st, SpGroups* g_dev, const int32_t* gk, const uint8_t* need,
+                        int64_t n, const uint32_t* hist, const uint32_t* err, uint64_t* fw, uint64_t* dw) {
     const int64_t tiles = sp_tiles(n, kSpTile);
     uint64_t* ts = scratch<uint64_t>(c, kSlotTiles, (size_t)(tiles + 1) * 2);
     if (!ts) return sfail(SKML_E_OOM, "tile sums");
@@ -417,8 +416,10 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const float* vals, int64_t nnz, 
     s->device = ctx_device(c);
     s->nnz = nnz;
     s->params = *p;
+    hipStream_t side = nullptr;  // the DeltaAdaptive chain's stream, once forked
     auto bail = [&](int code) {
         (void)hipStreamSynchronize(st);  // the block returns to the pool: nothing may still use it
+        if (side) (void)hipStreamSynchronize(side);
         sparse_release(s);
         return code;
     };
@@ -493,12 +494,27 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const float* vals, int64_t nnz, 
     int32_t* cellbuf =
         cells_max < INT32_MAX ? scratch<int32_t>(c, kSlotCellIdx, (size_t)rows * (size_t)nnz) : nullptr;
     SP_TRY(launch_group_prep(st, gk, nnz, s->g_dev, need, hist, err, bucket, nbuckets, cellbuf, tile_off));
+    // ---- 4. DeltaAdaptive key streams on the side stream, beside the MinMax scatter and minima:
+    // the VALU-bound stream writer runs while the scatter waits on memory.  The two chains touch
+    // disjoint fields of the group table and disjoint buffers; the main stream joins before the
+    // read-back.  (Forking before the count pass instead, with the deltas and histogram computed
+    // on the side, overlapped the two VALU-bound passes and was slower.) ----
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    hipStream_t ds = st;
+    if (nnz > 0 && ctx_side_fork(c, &side, &ev_fork, &ev_join) == SKML_OK) {
+        SP_TRY(hipEventRecord(ev_fork, st));
+        SP_TRY(hipStreamWaitEvent(side, ev_fork, 0));
+        ds = side;
+    } else {
+        side = nullptr;
+    }
+    if (int e = encode_delta_device(c, ds, s->g_dev, gk, need, nnz, hist, err, s->flag_words, s->delta_words))
+        return bail(e);
+    if (side) SP_TRY(hipEventRecord(ev_join, side));
     SP_TRY(launch_scan_cols(st, bucket, nbuckets, 1));
     SP_TRY(launch_mm_scatter(st, gk, gb, nnz, s->g_dev, bucket, cursor, nbuckets, pairs, cellbuf, tile_off));
     SP_TRY(launch_mm_bucket(st, pairs, bucket, nbuckets, s->g_dev, s->tables));
-    // ---- 4. DeltaAdaptive key streams ----
-    if (int e = encode_delta_device(c, s->g_dev, gk, need, nnz, hist, err, s->flag_words, s->delta_words))
-        return bail(e);
+    if (side) SP_TRY(hipStreamWaitEvent(st, ev_join, 0));
     // ---- 5. the one read-back: quantizer header and splits, group table ----
     const size_t qh = kHeaderBytes + sizeof(double) * (size_t)(p->bin_num - 1);
     const size_t o_pg = align_up(qh, 256);
@@ -1388,7 +1404,7 @@ int skml_delta_encode(skml_ctx* c, const int32_t* keys, int64_t n, int32_t* num_
     SP_HIP(hipMemsetAsync(small, 0, sizeof(uint32_t) * ((size_t)kMaxGroups * kDeltaHist + 1), st));
     SP_HIP(launch_group_prep(st, keys, n, g_dev, need, small, small + kMaxGroups * kDeltaHist, nullptr, 0, nullptr,
                              nullptr));
-    if (int e = encode_delta_device(c, g_dev, keys, need, n, small, small + kMaxGroups * kDeltaHist, fwd, dwd))
+    if (int e = encode_delta_device(c, st, g_dev, keys, need, n, small, small + kMaxGroups * kDeltaHist, fwd, dwd))
         return e;
     if (int e = sync_to_host(c, &G, g_dev, sizeof(SpGroups))) return e;
     if (G.status & kSpOrder) return sfail(SKML_E_ORDER, "Log for a non-positive key delta (keys must ascend strictly)");
