@@ -329,20 +329,18 @@ __device__ __forceinline__ uint32_t fold32(double d) {
 }
 
 template <int STAGE, bool PARTIAL = false, typename E = float>
-__global__ __launch_bounds__(256, LeafTypes<E>::kMinWaves) void k_leaf2(
-    const E* __restrict__ x, int64_t chunks, uint64_t s0, const uint64_t* __restrict__ tab,
-    typename LeafTypes<E>::Part* __restrict__ part, E* __restrict__ nodes6, E* __restrict__ roots, int64_t tile0,
-    uint8_t* __restrict__ ubits = nullptr) {
+__device__ __forceinline__ void leaf2_wave(const E* __restrict__ x, int64_t chunks, uint64_t s0,
+                                           const uint64_t* __restrict__ tab,
+                                           typename LeafTypes<E>::Part* __restrict__ part, E* __restrict__ nodes6,
+                                           E* __restrict__ roots, int64_t tile, uint8_t* __restrict__ ubits,
+                                           E* wfb) {
     using Key = typename LeafTypes<E>::Key;
-    __shared__ E fb[kLeaf2Waves][kWaveFb];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t tile = tile0 + (int64_t)blockIdx.x * kLeaf2Waves + wave;
+    const int lane = threadIdx.x & 63;
     const int64_t c_tile = tile * kLeafWaveChunks;
     if (c_tile >= chunks) return;  // wave-uniform; no block barriers in this kernel
     const int64_t left = chunks - c_tile;
     const int rem = left < kLeafWaveChunks ? (int)left : 0;
     const int nrounds = rem ? (rem + kChunksPerWave - 1) / kChunksPerWave : kLeafWaveChunks / kChunksPerWave;
-    E* wfb = fb[wave];
     const uint64_t ta = tab[lane * 2], tc = tab[lane * 2 + 1];  // A^lane, C_lane
 #ifdef SKML_PROF_LEAF
     const unsigned long long prof_t0 = wall_clock64();
@@ -539,6 +537,17 @@ __global__ __launch_bounds__(256, LeafTypes<E>::kMinWaves) void k_leaf2(
     }
 }
 
+template <int STAGE, bool PARTIAL = false, typename E = float>
+__global__ __launch_bounds__(256, LeafTypes<E>::kMinWaves) void k_leaf2(
+    const E* __restrict__ x, int64_t chunks, uint64_t s0, const uint64_t* __restrict__ tab,
+    typename LeafTypes<E>::Part* __restrict__ part, E* __restrict__ nodes6, E* __restrict__ roots, int64_t tile0,
+    uint8_t* __restrict__ ubits = nullptr) {
+    __shared__ E fb[kLeaf2Waves][kWaveFb];
+    const int wave = threadIdx.x >> 6;
+    leaf2_wave<STAGE, PARTIAL, E>(x, chunks, s0, tab, part, nodes6, roots,
+                                  tile0 + (int64_t)blockIdx.x * kLeaf2Waves + wave, ubits, fb[wave]);
+}
+
 // ---------------------------------------------------------------------------------------------
 // 64-keys-per-lane leaf (fp32, full 64-chunk tiles): 4 lanes per chunk, 16 chunks per round, 4
 // rounds per wave.  The chunk sort is Batcher's odd-even network over 64 registers (543
@@ -552,14 +561,27 @@ constexpr int kL64Rounds = kLeafWaveChunks / kL64Chunks;
 #ifndef SKML_LEAF64_WAVES
 #define SKML_LEAF64_WAVES 4
 #endif
+// `chunks` counts the full tiles' chunks; when total_chunks holds a partial tile as well, that
+// tile's small trees (k_leaf2's PARTIAL path, one wave) run in workgroup 0, which is dispatched
+// first, so they overlap the full tiles instead of following them.
 __global__ __launch_bounds__(256, SKML_LEAF64_WAVES) void k_leaf64(const float* __restrict__ x, int64_t chunks, uint64_t s0,
                                                    const uint64_t* __restrict__ tab, LeafPartial* __restrict__ part,
                                                    float* __restrict__ nodes6, float* __restrict__ roots,
-                                                   uint8_t* __restrict__ ubits) {
+                                                   uint8_t* __restrict__ ubits, int64_t total_chunks) {
     __shared__ float fb[kLeaf2Waves][kWaveFb];
     __shared__ float2 stk[kLeaf2Waves][2][64];  // the carry stack (levels 4, 5) in LDS, not registers
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t tile = (int64_t)blockIdx.x * kLeaf2Waves + wave;
+    int64_t blk = blockIdx.x;
+    if (total_chunks > chunks) {
+        if (blk == 0) {
+            if (wave == 0)
+                leaf2_wave<3, true, float>(x, total_chunks, s0, tab, part, nodes6, roots, chunks / kLeafWaveChunks,
+                                           nullptr, fb[0]);
+            return;
+        }
+        blk -= 1;
+    }
+    const int64_t tile = blk * kLeaf2Waves + wave;
     const int64_t c_tile = tile * kLeafWaveChunks;
     if (c_tile >= chunks) return;  // wave-uniform; no block barriers in this kernel
     float* wfb = fb[wave];
@@ -876,10 +898,12 @@ hipError_t launch_leaf(hipStream_t st, const float* x, int64_t chunks, uint64_t 
 #ifndef SKML_LEAF64
 #define SKML_LEAF64 1
 #endif
-    if (full > 0 && SKML_LEAF64)
-        hipLaunchKernelGGL(k_leaf64, dim3((unsigned)((full + kLeaf2Waves - 1) / kLeaf2Waves)), dim3(64 * kLeaf2Waves),
-                           0, st, x, full * kLeafWaveChunks, s0, jump_tab, part, nodes6, roots, ubits);
-    else if (full > 0)
+    if (full > 0 && SKML_LEAF64) {  // the partial tile, if any, rides in the same launch
+        const unsigned grid = (unsigned)((full + kLeaf2Waves - 1) / kLeaf2Waves + (chunks % kLeafWaveChunks ? 1 : 0));
+        hipLaunchKernelGGL(k_leaf64, dim3(grid), dim3(64 * kLeaf2Waves), 0, st, x, full * kLeafWaveChunks, s0, jump_tab,
+                           part, nodes6, roots, ubits, chunks);
+        return hipGetLastError();
+    } else if (full > 0)
         hipLaunchKernelGGL((k_leaf2<3, false>), dim3((unsigned)((full + kLeaf2Waves - 1) / kLeaf2Waves)),
                            dim3(64 * kLeaf2Waves), 0, st, x, full * kLeafWaveChunks, s0, jump_tab, part,
                            nodes6, roots, (int64_t)0, ubits);
