@@ -71,8 +71,9 @@ hipError_t launch_compact(hipStream_t st, const float* x, int64_t dim, int32_t* 
 // Exclusive scan, in place, of each of K columns of a [tiles][K] u64 table; totals -> row `tiles`.
 hipError_t launch_scan_cols(hipStream_t st, uint64_t* sums, int64_t tiles, int K);
 // FSketchUtils.partition: per-tile group counts, then the stable scatter into group order.
+// The grid also zeroes z32[0, n32) and z64[0, n64) (the next passes' counters: no memset launches).
 hipError_t launch_part_count(hipStream_t st, const void* qpayload, int64_t n, const SpGroups* gp,
-                             uint64_t* tile_counts);
+                             uint64_t* tile_counts, uint32_t* z32, int64_t n32, uint64_t* z64, int64_t n64);
 hipError_t launch_part_scatter(hipStream_t st, const int32_t* keys, const void* qpayload, int64_t n,
                                const SpGroups* gp, const uint64_t* tile_base, int32_t* gkeys,
                                int32_t* gbins);

@@ -400,19 +400,90 @@ hipError_t launch_scan_cols(hipStream_t st, uint64_t* sums, int64_t tiles, int K
 // =============================================================================================
 // Partition by group (stable)
 // =============================================================================================
+// Up to kFewGroups groups (the default is 8): the edges sit in registers, the group of a bin is a
+// sum of compares, and the per-group counts are 8-bit fields of one u64 per lane (at most 8
+// elements per lane and step), reduced across the wave as two u64 of 16-bit fields.
+constexpr int kFewGroups = 8;
+struct FewEdges {
+    int32_t e[kFewGroups - 1];  // edges[0 .. G-2], INT32_MAX beyond (edges[G-1] = binNum is above every bin)
+};
+__device__ __forceinline__ FewEdges few_edges(const SpGroups* gp, int G) {
+    FewEdges f;
+#pragma unroll
+    for (int j = 0; j < kFewGroups - 1; j++) f.e[j] = j < G - 1 ? gp->edges[j] : INT32_MAX;
+    return f;
+}
+__device__ __forceinline__ int few_group(const FewEdges& f, int32_t bin) {
+    int g = 0;
+#pragma unroll
+    for (int j = 0; j < kFewGroups - 1; j++) g += f.e[j] <= bin ? 1 : 0;
+    return g;
+}
+// wave sums of the 8-bit fields of acc, as 16-bit fields: groups 0,2,4,6 in lo and 1,3,5,7 in hi
+__device__ __forceinline__ void few_wave_sum(uint64_t acc, uint64_t& lo, uint64_t& hi) {
+    lo = acc & 0x00FF00FF00FF00FFull;
+    hi = (acc >> 8) & 0x00FF00FF00FF00FFull;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        lo += __shfl_xor(lo, off, 64);
+        hi += __shfl_xor(hi, off, 64);
+    }
+}
+__device__ __forceinline__ uint32_t few_field(uint64_t lo, uint64_t hi, int g) {
+    return (uint32_t)(((g & 1) ? hi : lo) >> (16 * (g >> 1))) & 0xFFFFu;
+}
+
 __global__ __launch_bounds__(kSpThreads) void k_part_count(const uint8_t* __restrict__ qpayload, int64_t n,
                                                            const SpGroups* __restrict__ gp,
-                                                           uint64_t* __restrict__ tile_counts) {
+                                                           uint64_t* __restrict__ tile_counts,
+                                                           uint32_t* __restrict__ z32, int64_t n32,
+                                                           uint64_t* __restrict__ z64, int64_t n64) {
+    for (int64_t z = (int64_t)blockIdx.x * kSpThreads + threadIdx.x, step = (int64_t)gridDim.x * kSpThreads;
+         z < n32 || z < n64; z += step) {
+        if (z < n32) z32[z] = 0;
+        if (z < n64) z64[z] = 0;
+    }
     if (gp->status) return;
     __shared__ int32_t E[kMaxGroups];
     __shared__ uint32_t cnt[kMaxGroups];
+    __shared__ uint64_t wsum[kSpThreads / 64][2];
     const skml_dense_header* h = reinterpret_cast<const skml_dense_header*>(qpayload);
     const uint8_t* codes = qpayload + h->codes_offset;
     const int bits = h->code_bits, G = gp->G;
+    const int64_t base = (int64_t)blockIdx.x * kSpTile;
+    if (G <= kFewGroups) {  // 8 consecutive elements per lane, counted in registers
+        static_assert(kSpTile == 8 * kSpThreads, "one 8-element run per lane");
+        const FewEdges fe = few_edges(gp, G);
+        const int t = threadIdx.x;
+        const int64_t i0 = base + 8 * t;
+        uint64_t acc = 0;
+        if (bits == 8 && i0 + 8 <= n && ((reinterpret_cast<uintptr_t>(codes) & 7) == 0)) {
+            const uint64_t w8 = *reinterpret_cast<const uint64_t*>(codes + i0);
+#pragma unroll
+            for (int k = 0; k < 8; k++) acc += 1ull << (8 * few_group(fe, (int32_t)((w8 >> (8 * k)) & 255u)));
+        } else {
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                if (i0 + k < n) acc += 1ull << (8 * few_group(fe, code_at(codes, i0 + k, bits)));
+        }
+        uint64_t lo, hi;
+        few_wave_sum(acc, lo, hi);
+        if ((t & 63) == 0) {
+            wsum[t >> 6][0] = lo;
+            wsum[t >> 6][1] = hi;
+        }
+        __syncthreads();
+        if (t < G) {
+            uint32_t c = 0;
+#pragma unroll
+            for (int w = 0; w < kSpThreads / 64; w++) c += few_field(wsum[w][0], wsum[w][1], t);
+            tile_counts[(int64_t)blockIdx.x * G + t] = c;
+        }
+        return;
+    }
     load_edges(gp, E);
     for (int j = threadIdx.x; j < kMaxGroups; j += kSpThreads) cnt[j] = 0;
     __syncthreads();
-    const int64_t base = (int64_t)blockIdx.x * kSpTile;
     for (int j = threadIdx.x; j < kSpTile; j += kSpThreads) {
         const int64_t i = base + j;
         if (i < n) atomicAdd(&cnt[group_of_bin(E, code_at(codes, i, bits))], 1u);
@@ -422,16 +493,24 @@ __global__ __launch_bounds__(kSpThreads) void k_part_count(const uint8_t* __rest
 }
 
 hipError_t launch_part_count(hipStream_t st, const void* qpayload, int64_t n, const SpGroups* gp,
-                             uint64_t* tile_counts) {
+                             uint64_t* tile_counts, uint32_t* z32, int64_t n32, uint64_t* z64, int64_t n64) {
     const int64_t tiles = sp_tiles(n, kSpTile);
-    if (tiles <= 0) return hipSuccess;
+    if (tiles <= 0) {
+        if (n32 > 0) {
+            hipError_t e = hipMemsetAsync(z32, 0, sizeof(uint32_t) * (size_t)n32, st);
+            if (e != hipSuccess) return e;
+        }
+        return n64 > 0 ? hipMemsetAsync(z64, 0, sizeof(uint64_t) * (size_t)n64, st) : hipSuccess;
+    }
     hipLaunchKernelGGL(k_part_count, dim3((unsigned)tiles), dim3(kSpThreads), 0, st,
-                       reinterpret_cast<const uint8_t*>(qpayload), n, gp, tile_counts);
+                       reinterpret_cast<const uint8_t*>(qpayload), n, gp, tile_counts, z32, n32, z64, n64);
     return hipGetLastError();
 }
 
 // Wave w of the tile owns elements [w*512, (w+1)*512), 64 per step in order; lanes with the same
-// group are ranked by lane (peer mask from log2(G) ballots), so the scatter is stable.
+// group are ranked by lane (peer mask from log2(G) ballots), so the scatter is stable.  The tile
+// is first laid out in group order in LDS, then each group's run is stored with consecutive lanes
+// on consecutive output indices (direct per-lane stores split every step into G short segments).
 __global__ __launch_bounds__(kSpThreads) void k_part_scatter(const int32_t* __restrict__ keys,
                                                              const uint8_t* __restrict__ qpayload, int64_t n,
                                                              const SpGroups* __restrict__ gp,
@@ -440,34 +519,74 @@ __global__ __launch_bounds__(kSpThreads) void k_part_scatter(const int32_t* __re
     if (gp->status) return;
     constexpr int kWaves = kSpThreads / 64, kSteps = kSpTile / kSpThreads;
     __shared__ int32_t E[kMaxGroups];
-    __shared__ int64_t wb[kWaves][kMaxGroups];  // running output position per (wave, group)
+    __shared__ int64_t wb[kWaves][kMaxGroups];  // counts, then running LDS slot per (wave, group)
+    __shared__ int64_t gdst[kMaxGroups];        // output index of a group's slot 0 in the tile
+    __shared__ int32_t sk[kSpTile], sb[kSpTile];
+    __shared__ uint8_t sg[kSpTile];
     const skml_dense_header* h = reinterpret_cast<const skml_dense_header*>(qpayload);
     const uint8_t* codes = qpayload + h->codes_offset;
     const int bits = h->code_bits, G = gp->G;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    load_edges(gp, E);
-    for (int j = t; j < kWaves * kMaxGroups; j += kSpThreads) wb[j / kMaxGroups][j % kMaxGroups] = 0;
-    __syncthreads();
+    const bool few = G <= kFewGroups;
+    if (!few) {
+        load_edges(gp, E);
+        for (int j = t; j < kWaves * kMaxGroups; j += kSpThreads) wb[j / kMaxGroups][j % kMaxGroups] = 0;
+        __syncthreads();
+    }
     const int64_t base = (int64_t)blockIdx.x * kSpTile + (int64_t)w * (kSpTile / kWaves);
     int32_t kk[kSteps], gg[kSteps], bb[kSteps];
+    if (few) {  // the wave's group counts from register fields (see k_part_count)
+        static_assert(kSteps <= 8, "8-bit count fields");
+        const FewEdges fe = few_edges(gp, G);
+        uint64_t acc = 0;
 #pragma unroll
-    for (int s = 0; s < kSteps; s++) {
-        const int64_t i = base + s * 64 + lane;
-        gg[s] = -1;
-        if (i < n) {
-            kk[s] = keys[i];
-            bb[s] = code_at(codes, i, bits);
-            gg[s] = group_of_bin(E, bb[s]);
-            atomicAdd(reinterpret_cast<unsigned long long*>(&wb[w][gg[s]]), 1ull);
+        for (int s = 0; s < kSteps; s++) {
+            const int64_t i = base + s * 64 + lane;
+            gg[s] = -1;
+            if (i < n) {
+                kk[s] = keys[i];
+                bb[s] = code_at(codes, i, bits);
+                gg[s] = few_group(fe, bb[s]);
+                acc += 1ull << (8 * gg[s]);
+            }
+        }
+        uint64_t lo, hi;
+        few_wave_sum(acc, lo, hi);
+        if (lane < G) wb[w][lane] = few_field(lo, hi, lane);
+    } else {
+#pragma unroll
+        for (int s = 0; s < kSteps; s++) {
+            const int64_t i = base + s * 64 + lane;
+            gg[s] = -1;
+            if (i < n) {
+                kk[s] = keys[i];
+                bb[s] = code_at(codes, i, bits);
+                gg[s] = group_of_bin(E, bb[s]);
+                atomicAdd(reinterpret_cast<unsigned long long*>(&wb[w][gg[s]]), 1ull);
+            }
         }
     }
     __syncthreads();
-    if (t < G) {  // wave-exclusive offsets per group, plus the group's start and tile base
-        int64_t run = gp->gstart[t] + (int64_t)tile_base[(int64_t)blockIdx.x * G + t];
-        for (int j = 0; j < kWaves; j++) {
-            const int64_t c = wb[j][t];
-            wb[j][t] = run;
-            run += c;
+    // the tile in group order in LDS: wave w's elements of group g at loc[g] + (earlier waves' g)
+    if (t < 64) {
+        const int64_t tb = (int64_t)blockIdx.x * G;
+        uint32_t c = 0;
+        if (lane < G)
+            for (int j = 0; j < kWaves; j++) c += (uint32_t)wb[j][lane];
+        uint32_t x = c;  // inclusive scan over the groups
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(x, off, 64);
+            if (lane >= off) x += y;
+        }
+        if (lane < G) {
+            uint32_t run = x - c;
+            gdst[lane] = gp->gstart[lane] + (int64_t)tile_base[tb + lane] - (int64_t)run;
+            for (int j = 0; j < kWaves; j++) {
+                const uint32_t cj = (uint32_t)wb[j][lane];
+                wb[j][lane] = run;
+                run += cj;
+            }
         }
     }
     __syncthreads();
@@ -483,14 +602,23 @@ __global__ __launch_bounds__(kSpThreads) void k_part_scatter(const int32_t* __re
             peers &= ((gg[s] >> b) & 1) ? bal : ~bal;
         }
         if (valid) {
-            const int64_t dst = wb[w][gg[s]] + __popcll(peers & lt);
-            gkeys[dst] = kk[s];
-            gbins[dst] = bb[s];
+            const int pos = (int)wb[w][gg[s]] + __popcll(peers & lt);
+            sk[pos] = kk[s];
+            sb[pos] = bb[s];
+            sg[pos] = (uint8_t)gg[s];
         }
         // every lane has read its base; the leader of each peer set advances it
         __builtin_amdgcn_wave_barrier();
         if (valid && (peers & lt) == 0) wb[w][gg[s]] += __popcll(peers);
         __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    // each group's run of the tile goes out with consecutive lanes on consecutive addresses
+    const int tile_n = (int)std::min<int64_t>(kSpTile, n - (int64_t)blockIdx.x * kSpTile);
+    for (int q = t; q < tile_n; q += kSpThreads) {
+        const int64_t dst = gdst[sg[q]] + q;
+        gkeys[dst] = sk[q];
+        gbins[dst] = sb[q];
     }
 }
 

@@ -466,15 +466,19 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const float* vals, int64_t nnz, 
     const int64_t tiles = sp_tiles(nnz, kSpTile);
     uint64_t* tc = scratch<uint64_t>(c, kSlotTiles, (size_t)(tiles + 1) * G);
     if (!tc) return bail(sfail(SKML_E_OOM, "tile counts"));
-    SP_TRY(launch_part_count(st, s->qpayload, nnz, s->g_dev, tc));
+    // partition counts; the grid also zeroes the histogram, error flag and bucket counters below
+    const int nbuckets = (int)((cells_max + kMmCellsPerBucket - 1) / kMmCellsPerBucket);
+    uint64_t* bucket = scratch<uint64_t>(c, kSlotCells, (size_t)2 * nbuckets + 2);  // counts->bases, cursors
+    uint32_t* small = scratch<uint32_t>(c, kSlotSmall, (size_t)kMaxGroups * kDeltaHist + 64);
+    if (!bucket || !small) return bail(sfail(SKML_E_OOM, "sparse scratch"));
+    SP_TRY(launch_part_count(st, s->qpayload, nnz, s->g_dev, tc, small, (int64_t)kMaxGroups * kDeltaHist + 64, bucket,
+                             (int64_t)2 * nbuckets + 2));
     SP_TRY(launch_scan_cols(st, tc, tiles, G));
     SP_TRY(launch_sp_plan_groups(st, s->g_dev, tc + tiles * G));
     // ---- 3. partition, deltas / histogram / order check, bucketed MinMax insert ----
     int32_t* gk = scratch<int32_t>(c, kSlotGKeys, (size_t)nnz);
     int32_t* gb = scratch<int32_t>(c, kSlotGBins, (size_t)nnz);
     uint8_t* need = scratch<uint8_t>(c, kSlotNeed, (size_t)nnz);
-    const int nbuckets = (int)((cells_max + kMmCellsPerBucket - 1) / kMmCellsPerBucket);
-    uint64_t* bucket = scratch<uint64_t>(c, kSlotCells, (size_t)2 * nbuckets + 2);  // counts->bases, cursors
     // per (tile, bucket) reserved offsets (u32: a bucket holds fewer than 2^32 pairs)
     const int64_t mm_tiles = sp_tiles(nnz, kMmChunkElems);
     const bool reserve = (uint64_t)rows * (uint64_t)nnz < (1ull << 31);
@@ -482,14 +486,11 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const float* vals, int64_t nnz, 
     // reserved ranges are padded to 16 pairs
     const size_t npairs = (size_t)rows * (size_t)nnz + (tile_off ? (size_t)15 * mm_tiles * nbuckets : 0);
     uint64_t* pairs = scratch<uint64_t>(c, kSlotDelta, npairs);
-    uint32_t* small = scratch<uint32_t>(c, kSlotSmall, (size_t)kMaxGroups * kDeltaHist + 64);
-    if (!gk || !gb || !need || !bucket || !pairs || !small) return bail(sfail(SKML_E_OOM, "sparse scratch"));
+    if (!gk || !gb || !need || !pairs) return bail(sfail(SKML_E_OOM, "sparse scratch"));
     uint64_t* cursor = bucket + nbuckets + 1;
     uint32_t* hist = small;
     uint32_t* err = small + kMaxGroups * kDeltaHist;
     SP_TRY(launch_part_scatter(st, keys, s->qpayload, nnz, s->g_dev, tc, gk, gb));
-    SP_TRY(hipMemsetAsync(small, 0, sizeof(uint32_t) * ((size_t)kMaxGroups * kDeltaHist + 64), st));
-    SP_TRY(hipMemsetAsync(bucket, 0, sizeof(uint64_t) * ((size_t)2 * nbuckets + 2), st));
     // the pairs' table cells, hashed once (int32 cells; without room or past 2^31 cells the scatter rehashes)
     int32_t* cellbuf =
         cells_max < INT32_MAX ? scratch<int32_t>(c, kSlotCellIdx, (size_t)rows * (size_t)nnz) : nullptr;
