@@ -58,7 +58,7 @@ inline int64_t sp_tiles(int64_t n, int64_t tile) { return (n + tile - 1) / tile;
 //   delta: calOptimalIntervals per group from hist, the order-check flag, kind1_before;
 //   finalize: fb / db of empty groups and the stream totals (tot = the scanned tile sums' total row).
 hipError_t launch_sp_plan_edges(hipStream_t st, const void* qpayload, const SpInit& init, SpGroups* gp);
-hipError_t launch_sp_plan_groups(hipStream_t st, SpGroups* gp, const uint64_t* sizes);
+hipError_t launch_sp_plan_groups(hipStream_t st, SpGroups* gp, const uint64_t* sizes, int64_t stride);
 hipError_t launch_sp_plan_delta(hipStream_t st, SpGroups* gp, const uint32_t* hist, const uint32_t* err);
 hipError_t launch_sp_finalize(hipStream_t st, SpGroups* gp, const uint64_t* tot);
 // Zero the stream words the writer ORs into (every tile's first and last word, and the word
@@ -70,7 +70,10 @@ hipError_t launch_compact(hipStream_t st, const float* x, int64_t dim, int32_t* 
                           uint64_t* status, unsigned* ticket, int64_t* nnz_out);
 // Exclusive scan, in place, of each of K columns of a [tiles][K] u64 table; totals -> row `tiles`.
 hipError_t launch_scan_cols(hipStream_t st, uint64_t* sums, int64_t tiles, int K);
-// FSketchUtils.partition: per-tile group counts, then the stable scatter into group order.
+// The same over K columns of tiles + 1 entries each, column k at sums + k * (tiles + 1).
+hipError_t launch_scan_cols_major(hipStream_t st, uint64_t* sums, int64_t tiles, int K);
+// FSketchUtils.partition: per-tile group counts (column-major: group g's column of tiles + 1 at
+// tile_counts + g * (tiles + 1)), then the stable scatter into group order.
 // The grid also zeroes z32[0, n32) and z64[0, n64) (the next passes' counters: no memset launches).
 hipError_t launch_part_count(hipStream_t st, const void* qpayload, int64_t n, const SpGroups* gp,
                              uint64_t* tile_counts, uint32_t* z32, int64_t n32, uint64_t* z64, int64_t n64);

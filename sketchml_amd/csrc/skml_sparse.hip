@@ -357,7 +357,9 @@ hipError_t launch_compact(hipStream_t st, const float* x, int64_t dim, int32_t* 
 // Column scan of [tiles][K] u64 tile sums (one workgroup per column)
 // =============================================================================================
 constexpr int kScanThreads = 1024, kScanPer = 8;  // one workgroup per column, 8K entries per pass
-__global__ __launch_bounds__(kScanThreads) void k_scan_cols(uint64_t* sums, int64_t tiles, int K) {
+// Entry (i, k) at sums[k * ld + i * es]: [tiles][K] row-major (ld 1, es K) or one column of
+// tiles + 1 entries per k (ld tiles + 1, es 1: contiguous column reads).
+__global__ __launch_bounds__(kScanThreads) void k_scan_cols(uint64_t* sums, int64_t tiles, int64_t ld, int64_t es) {
     __shared__ uint64_t sh[kScanThreads / 64];
     const int k = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
     uint64_t carry = 0;
@@ -366,7 +368,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_cols(uint64_t* sums, int6
 #pragma unroll
         for (int j = 0; j < kScanPer; j++) {
             const int64_t i = c0 + t * kScanPer + j;
-            loc[j] = i < tiles ? sums[i * K + k] : 0;
+            loc[j] = i < tiles ? sums[k * ld + i * es] : 0;
             s += loc[j];
         }
         const uint64_t inc = wave_incl_u64(s, lane);
@@ -384,16 +386,20 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_cols(uint64_t* sums, int6
 #pragma unroll
         for (int j = 0; j < kScanPer; j++) {
             const int64_t i = c0 + t * kScanPer + j;
-            if (i < tiles) sums[i * K + k] = run;
+            if (i < tiles) sums[k * ld + i * es] = run;
             run += loc[j];
         }
         carry += tot;
     }
-    if (t == 0) sums[tiles * K + k] = carry;
+    if (t == 0) sums[k * ld + tiles * es] = carry;
 }
 
 hipError_t launch_scan_cols(hipStream_t st, uint64_t* sums, int64_t tiles, int K) {
-    hipLaunchKernelGGL(k_scan_cols, dim3(K), dim3(kScanThreads), 0, st, sums, tiles, K);
+    hipLaunchKernelGGL(k_scan_cols, dim3(K), dim3(kScanThreads), 0, st, sums, tiles, (int64_t)1, (int64_t)K);
+    return hipGetLastError();
+}
+hipError_t launch_scan_cols_major(hipStream_t st, uint64_t* sums, int64_t tiles, int K) {
+    hipLaunchKernelGGL(k_scan_cols, dim3(K), dim3(kScanThreads), 0, st, sums, tiles, tiles + 1, (int64_t)1);
     return hipGetLastError();
 }
 
@@ -477,7 +483,7 @@ __global__ __launch_bounds__(kSpThreads) void k_part_count(const uint8_t* __rest
             uint32_t c = 0;
 #pragma unroll
             for (int w = 0; w < kSpThreads / 64; w++) c += few_field(wsum[w][0], wsum[w][1], t);
-            tile_counts[(int64_t)blockIdx.x * G + t] = c;
+            tile_counts[(int64_t)t * (gridDim.x + 1) + blockIdx.x] = c;
         }
         return;
     }
@@ -489,7 +495,7 @@ __global__ __launch_bounds__(kSpThreads) void k_part_count(const uint8_t* __rest
         if (i < n) atomicAdd(&cnt[group_of_bin(E, code_at(codes, i, bits))], 1u);
     }
     __syncthreads();
-    for (int g = threadIdx.x; g < G; g += kSpThreads) tile_counts[(int64_t)blockIdx.x * G + g] = cnt[g];
+    for (int g = threadIdx.x; g < G; g += kSpThreads) tile_counts[(int64_t)g * (gridDim.x + 1) + blockIdx.x] = cnt[g];
 }
 
 hipError_t launch_part_count(hipStream_t st, const void* qpayload, int64_t n, const SpGroups* gp,
@@ -569,7 +575,7 @@ __global__ __launch_bounds__(kSpThreads) void k_part_scatter(const int32_t* __re
     __syncthreads();
     // the tile in group order in LDS: wave w's elements of group g at loc[g] + (earlier waves' g)
     if (t < 64) {
-        const int64_t tb = (int64_t)blockIdx.x * G;
+        const int64_t ld = (int64_t)gridDim.x + 1;  // tile_base: one column of tiles + 1 per group
         uint32_t c = 0;
         if (lane < G)
             for (int j = 0; j < kWaves; j++) c += (uint32_t)wb[j][lane];
@@ -581,7 +587,7 @@ __global__ __launch_bounds__(kSpThreads) void k_part_scatter(const int32_t* __re
         }
         if (lane < G) {
             uint32_t run = x - c;
-            gdst[lane] = gp->gstart[lane] + (int64_t)tile_base[tb + lane] - (int64_t)run;
+            gdst[lane] = gp->gstart[lane] + (int64_t)tile_base[lane * ld + blockIdx.x] - (int64_t)run;
             for (int j = 0; j < kWaves; j++) {
                 const uint32_t cj = (uint32_t)wb[j][lane];
                 wb[j][lane] = run;
@@ -1453,13 +1459,14 @@ __global__ __launch_bounds__(64) void k_sp_plan_edges(const skml_dense_header* _
 
 // GroupedMinMaxSketch.compOneGroup's shapes (GroupedMinMaxSketch.java:103-121): colNum =
 // ceil(size * colRatio) (no multiply-add contraction: the product rounds as in Java).
-__global__ __launch_bounds__(64) void k_sp_plan_groups(SpGroups* __restrict__ gp, const uint64_t* __restrict__ sizes) {
+__global__ __launch_bounds__(64) void k_sp_plan_groups(SpGroups* __restrict__ gp, const uint64_t* __restrict__ sizes,
+                                                       int64_t stride) {
     if (gp->status || threadIdx.x) return;
     const int G = gp->G, rows = gp->rows;
     const double ratio = gp->col_ratio;
     int64_t start = 0, cells = 0;
     for (int g = 0; g < G; g++) {
-        const int64_t m = (int64_t)sizes[g];
+        const int64_t m = (int64_t)sizes[g * stride];
         gp->gstart[g] = start;
         start += m;
         const int32_t cols = m > 0 ? (int32_t)ceil(__dmul_rn((double)m, ratio)) : 1;
@@ -1571,8 +1578,8 @@ hipError_t launch_sp_plan_edges(hipStream_t st, const void* qpayload, const SpIn
                        reinterpret_cast<const skml_dense_header*>(qpayload), init, gp);
     return hipGetLastError();
 }
-hipError_t launch_sp_plan_groups(hipStream_t st, SpGroups* gp, const uint64_t* sizes) {
-    hipLaunchKernelGGL(k_sp_plan_groups, dim3(1), dim3(64), 0, st, gp, sizes);
+hipError_t launch_sp_plan_groups(hipStream_t st, SpGroups* gp, const uint64_t* sizes, int64_t stride) {
+    hipLaunchKernelGGL(k_sp_plan_groups, dim3(1), dim3(64), 0, st, gp, sizes, stride);
     return hipGetLastError();
 }
 hipError_t launch_sp_plan_delta(hipStream_t st, SpGroups* gp, const uint32_t* hist, const uint32_t* err) {

@@ -473,8 +473,8 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const float* vals, int64_t nnz, 
     if (!bucket || !small) return bail(sfail(SKML_E_OOM, "sparse scratch"));
     SP_TRY(launch_part_count(st, s->qpayload, nnz, s->g_dev, tc, small, (int64_t)kMaxGroups * kDeltaHist + 64, bucket,
                              (int64_t)2 * nbuckets + 2));
-    SP_TRY(launch_scan_cols(st, tc, tiles, G));
-    SP_TRY(launch_sp_plan_groups(st, s->g_dev, tc + tiles * G));
+    SP_TRY(launch_scan_cols_major(st, tc, tiles, G));
+    SP_TRY(launch_sp_plan_groups(st, s->g_dev, tc + tiles, tiles + 1));
     // ---- 3. partition, deltas / histogram / order check, bucketed MinMax insert ----
     int32_t* gk = scratch<int32_t>(c, kSlotGKeys, (size_t)nnz);
     int32_t* gb = scratch<int32_t>(c, kSlotGBins, (size_t)nnz);
