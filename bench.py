@@ -64,9 +64,10 @@ def kernel_stats(lib, ctx):
     return out
 
 
-def pmc_traffic(kernel, n):
+def pmc_traffic(kernel, n, dtype="f32", quant="quantile"):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc summary, if one exists
-    for this problem size (profiles/*pmc*.json, written by tools/pmc_summary.py)."""
+    for this problem size, input type and quantizer (profiles/*pmc*.json, written by
+    tools/pmc_summary.py; summaries without dtype/quant keys are fp32 quantile runs)."""
     best = None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
         try:
@@ -75,7 +76,8 @@ def pmc_traffic(kernel, n):
         except Exception:
             continue
         k = d.get("kernels", {}).get(kernel)
-        if k and d.get("n") == n and "hbm_bytes_per_launch" in k:
+        if (k and d.get("n") == n and d.get("dtype", "f32") == dtype and d.get("quant", "quantile") == quant
+                and "hbm_bytes_per_launch" in k):
             best = (k["hbm_bytes_per_launch"], os.path.relpath(path, ROOT))
     return best
 
@@ -442,12 +444,14 @@ def main():
     lib.skml_dense_info(ctx, C.c_void_p(payload.data_ptr()), C.byref(hdr), None, 0)
     code_bits = hdr.code_bits
     alg_bytes = {"k_leaf": esize * n, "k_quantize": esize * n + n * code_bits / 8.0,
-                 "k_merge": esize * 128 * max(1, n // 256 // 64), "k_summary": 0.0}
+                 "k_merge": esize * 128 * max(1, n // 256 // 64),
+                 # the uniform quantizer's min/max pass reads the bucket once (k_uni_minmax + finish)
+                 "k_summary": esize * n if args.quant == "uniform" else 0.0}
     # dominant kernel by device time in the full breakdown; its duration from the live timed region
     dom = max((k for k in allstats if k in alg_bytes), key=lambda k: allstats[k]["avg_us"] * allstats[k]["launches"])
     live = kstats.get(dom, allstats[dom])
     ach = alg_bytes[dom] / (live["avg_us"] * 1e-6) / 1e9
-    traffic = pmc_traffic(dom, n)
+    traffic = pmc_traffic(dom, n, args.dtype, args.quant)
     roofline = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                 "traffic": traffic[0] if traffic else None,
