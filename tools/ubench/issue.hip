@@ -52,6 +52,14 @@ __global__ __launch_bounds__(256) void kern(float* out, Stamp* st, float seed) {
             else if constexpr (KIND == 24) { asm volatile("v_sad_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(sel)); }
             else if constexpr (KIND == 25) { asm volatile("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(sel)); }
             else if constexpr (KIND == 26) { asm volatile("v_permlane32_swap_b32 %0, %1" : "+v"(a) : "v"(b)); r = a; }
+            else if constexpr (KIND == 27) { asm volatile("v_max_f32_dpp %0, -%1, %2 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(b), "v"(a)); }
+            else if constexpr (KIND == 28) { asm volatile("v_max_f32_dpp %0, -%1, %2 row_mirror row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(b), "v"(a)); }
+            else if constexpr (KIND == 29) {  // two values per instruction: count as 2 per pair
+                typedef float f2v __attribute__((ext_vector_type(2)));
+                f2v p = {a, b}, q = {sel, sel};
+                if (i & 1) { asm volatile("v_pk_mul_f32 %0, %1, %2" : "=v"(p) : "v"(p), "v"(q)); r = p.x + 0.f; }
+                else { asm volatile("v_mul_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); }
+            }
             v[i] = r;
         }
     }
@@ -98,7 +106,7 @@ void run(const char* name, float* d, Stamp* st, Stamp* hst, int cus) {
     }
 }
 
-int main() {
+int main(int argc, char** argv) {
     int dev = 0;
     hipDeviceProp_t p;
     hipGetDeviceProperties(&p, dev);
@@ -136,5 +144,8 @@ int main() {
     run<24>("v_sad_u32", d, st, hst, cus);
     run<25>("v_max3_f32", d, st, hst, cus);
     run<26>("v_permlane32_swap", d, st, hst, cus);
+    run<27>("v_max_f32_dpp_neg_quad", d, st, hst, cus);
+    run<28>("v_max_f32_dpp_neg_mirror", d, st, hst, cus);
+    run<29>("v_pk_mul_f32/v_mul_f32 alt", d, st, hst, cus);
     return 0;
 }
