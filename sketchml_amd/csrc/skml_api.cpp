@@ -532,9 +532,12 @@ std::vector<MergePass> plan_merge_passes(int64_t chunks) {
     }
     return passes;
 }
-// a final one-workgroup pass runs inside the previous pass's last workgroup
+// a final pass of at most kFuseMaxWg workgroup-merges runs inside the previous pass's last
+// workgroup, one merge after another (sizes that are not 64^k chunks end with a few small trees:
+// C3's 26.8 M values leave 2, which otherwise cost a launch of their own)
+constexpr int kFuseMaxWg = 4;
 bool fuse_next_pass(const std::vector<MergePass>& passes, size_t i) {
-    return i + 2 == passes.size() && passes[i + 1].wg_prefix[passes[i + 1].njobs] == 1;
+    return i + 2 == passes.size() && passes[i + 1].wg_prefix[passes[i + 1].njobs] <= kFuseMaxWg;
 }
 }  // namespace
 

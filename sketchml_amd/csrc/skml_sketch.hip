@@ -1653,7 +1653,13 @@ __global__ __launch_bounds__(512) void k_merge(MergePass pass, MergePass next, c
     if (prefetch && tid < npre) pre = tid < sa.nred ? sa.part_red[tid] : sa.part[sa.part_from + (tid - sa.nred)];
     if (has_next) {
         SKML_PROF(0);
-        merge_group_wg(next, 0, dst, next_dst, roots, s0, tab, U.t, ubits, uchunks, nullptr, nullptr, 16);
+        // the trailing pass's merges (independent trees), one after another in this workgroup
+        const int nnext = next.wg_prefix[next.njobs];
+        for (int w = 0; w < nnext; w++) {
+            if (w) __syncthreads();
+            merge_group_wg(next, w, dst, next_dst, roots, s0, tab, U.t, ubits, uchunks, nullptr, nullptr,
+                           w == 0 ? 16 : -1);
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         __syncthreads();
@@ -1723,7 +1729,11 @@ __global__ __launch_bounds__(512) void k_merge64(MergePass pass, MergePass next,
     __syncthreads();
     if (!T64.is_last) return;
     __syncthreads();
-    merge_group_wg<double>(next, 0, dst, next_dst, roots, s0, tab, T64, ubits, uchunks);
+    const int nnext = next.wg_prefix[next.njobs];
+    for (int w = 0; w < nnext; w++) {
+        if (w) __syncthreads();
+        merge_group_wg<double>(next, w, dst, next_dst, roots, s0, tab, T64, ubits, uchunks);
+    }
 }
 
 hipError_t launch_merge_pass64(hipStream_t st, const MergePass& pass, const MergePass* next, const double* src,
