@@ -380,6 +380,32 @@ __device__ __forceinline__ int count_lt(const S* run, S x) {  // #{run[i] < x}
         if (run[lo + step - 1] < x) lo += step;
     return lo + (run[lo] < x ? 1 : 0) * (lo == 127 ? 1 : 0);
 }
+// blockyMergeSort rank contribution of two sorted kK-sample runs a, b for a sample v: #{s < v},
+// plus the ties s == v where `tie` (the run precedes v's own run: IEEE `<=`).  The two binary
+// searches are independent chains (their LDS reads overlap) and branch-free; `use_a` / `use_b`
+// mask a run out (v's own run, or b repeating a).
+__device__ __forceinline__ uint32_t tie_pred(float s, float v, uint32_t tie) {
+    return (uint32_t)(s < v) | ((uint32_t)(s == v) & tie);
+}
+__device__ __forceinline__ uint32_t tie_pred(double s, double v, uint32_t tie) {
+    return (uint32_t)(s < v) | ((uint32_t)(s == v) & tie);
+}
+template <typename S>
+__device__ __forceinline__ int rank_in_run_pair(const S* a, const S* b, S v, uint32_t tie_a, uint32_t tie_b,
+                                                uint32_t use_a, uint32_t use_b) {
+    int la = 0, lb = 0;
+#pragma unroll
+    for (int step = kK / 2; step >= 1; step >>= 1) {
+        const S sa = a[la + step - 1], sb = b[lb + step - 1];
+        la += (int)tie_pred(sa, v, tie_a) * step;
+        lb += (int)tie_pred(sb, v, tie_b) * step;
+    }
+    const S ea = a[la], eb = b[lb];
+    la += (int)(tie_pred(ea, v, tie_a) & (uint32_t)(la == kK - 1));
+    lb += (int)(tie_pred(eb, v, tie_b) & (uint32_t)(lb == kK - 1));
+    return (int)use_a * la + (int)use_b * lb;
+}
+
 template <typename S>
 __device__ __forceinline__ void exact_merge_task(const S* older, const S* newer, S* out, int t, uint32_t odd) {
     S v;

@@ -231,20 +231,28 @@ __global__ __launch_bounds__(512) void k_summary64(const double* __restrict__ x,
         if (t == 0) write_header(hdr, SKML_E_NAN, n_hdr, req_bins, 0, req_bins, vmin, vmax);
         return;
     }
-    // blockyMergeSort == stable sort under IEEE `<=` (left run wins ties): rank across runs
-    for (int i = t; i < ns; i += T) {
-        int r = 0;
-        while (S.run_off[r + 1] <= i) r++;
-        const double v = S.smp[i];
-        int rank = i - S.run_off[r];
-        for (int q = 0; q < nruns; q++) {
-            if (q == r) continue;
-            const double* run = S.smp + S.run_off[q];
-            const int len = S.run_off[q + 1] - S.run_off[q];
-            rank += q < r ? run_count_le64(run, len, v) : run_count_lt64(run, len, v);
+    // blockyMergeSort == stable sort under IEEE `<=` (left run wins ties): rank across runs.  The
+    // level runs hold kK samples each at q * kK (the base buffer last).
+    {
+        const int nfull = nruns - 1;
+        const double* tail_run = S.smp + S.run_off[nfull];
+        for (int i = t; i < ns; i += T) {
+            const int r = i < nfull * kK ? i / kK : nfull;
+            const double v = S.smp[i];
+            int rank = i - S.run_off[r];
+            // two level runs at a time: two independent 7-step searches per loop trip, with the
+            // IEEE `<=` / `<` choice as a branch-free predicate (a divergent le/lt branch ran
+            // both sides); a run paired with itself or the sample's own run counts 0
+            for (int q0 = 0; q0 < nfull; q0 += 2) {
+                const int q1 = q0 + 1 < nfull ? q0 + 1 : q0;
+                rank += rank_in_run_pair(S.smp + q0 * kK, S.smp + q1 * kK, v, (uint32_t)(q0 < r),
+                                         (uint32_t)(q1 < r), (uint32_t)(q0 != r),
+                                         (uint32_t)(q1 != r) & (uint32_t)(q1 != q0));
+            }
+            if (r < nfull) rank += run_count_lt64(tail_run, tail, v);  // the base buffer comes last
+            S.sorted[rank] = v;
+            S.w[rank] = S.run_lvl[r] < 0 ? 1 : ((int64_t)2 << S.run_lvl[r]);
         }
-        S.sorted[rank] = v;
-        S.w[rank] = S.run_lvl[r] < 0 ? 1 : ((int64_t)2 << S.run_lvl[r]);
     }
     __syncthreads();
     {  // exclusive prefix of weights (HeapQuantileSketch.java:137-142)

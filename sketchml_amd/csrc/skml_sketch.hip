@@ -561,132 +561,6 @@ constexpr int kL64Rounds = kLeafWaveChunks / kL64Chunks;
 #ifndef SKML_LEAF64_WAVES
 #define SKML_LEAF64_WAVES 4
 #endif
-
-// ---------------------------------------------------------------------------------------------
-// Sign-alternating network (the fast loop of k_leaf64).  Odd lanes hold -x instead of x, and every
-// lane keeps its registers sorted ascending in that stored form, so an odd lane's values run in
-// descending real order.  Merging two runs then starts with a flip stage whose partners (lane ^
-// (2^j - 1), same register) always have opposite signs, and that stage is ONE fused op per value:
-// v_max_f32_dpp y, -partner(y), y leaves the real max in the + lane and -min in the - lane.  (The
-// plain network needs a DPP move plus a v_med3 per value for it.)  The later stages of a merge
-// pair same-sign lanes: lane ^ 2^(j-1) with reversed registers, then lane ^ 2^(j-2) .. lane ^ 2
-// with equal registers, each a DPP / swizzle move plus a v_med3 whose selector keeps the stored
-// max where ((lane & D) == 0) ^ bit j of the lane.  After level j a group of 2^j lanes holds its
-// run in lane order [1, 3, 5, .., 2^j - 1, 2^j - 2, .., 2, 0].  The layout was derived and checked
-// against sort-and-compact on random, tied and denormal data by a numpy model of exactly these
-// stages (tests/test_leaf_network_model.py).
-// ---------------------------------------------------------------------------------------------
-#define SKML_DPP_FLIP1 "quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
-#define SKML_DPP_FLIP3 "quad_perm:[3,2,1,0] row_mask:0xf bank_mask:0xf"
-#define SKML_DPP_FLIP7 "row_half_mirror row_mask:0xf bank_mask:0xf"
-#define SKML_DPP_FLIP15 "row_mirror row_mask:0xf bank_mask:0xf"
-#define SKML_FLIP8(CTL)                                                                           \
-    "s_nop 1\n"                                                                                   \
-    "v_max_f32_dpp %0, -%0, %0 " CTL "\nv_max_f32_dpp %1, -%1, %1 " CTL "\n"                       \
-    "v_max_f32_dpp %2, -%2, %2 " CTL "\nv_max_f32_dpp %3, -%3, %3 " CTL "\n"                       \
-    "v_max_f32_dpp %4, -%4, %4 " CTL "\nv_max_f32_dpp %5, -%5, %5 " CTL "\n"                       \
-    "v_max_f32_dpp %6, -%6, %6 " CTL "\nv_max_f32_dpp %7, -%7, %7 " CTL "\n"                       \
-    "s_nop 1"
-
-// Flip stage of level j (partner lane ^ M, M = 2^j - 1, same register), in place.  DPP masks run
-// as inline asm in blocks of 8 registers: the compiler's hazard recognizer does not see DPP reads
-// inside asm, so each block waits out the VALU-write -> DPP-read hazard itself (s_nop 1 on entry
-// and exit).  Registers inside a block are distinct, so no read in it follows a write of the same
-// register.
-template <int M, int R>
-__device__ __forceinline__ void sgn_flip(float (&v)[R]) {
-    if constexpr (M == 1 || M == 3 || M == 7 || M == 15) {
-        static_assert(R % 8 == 0, "DPP flip blocks of 8 registers");
-#pragma unroll
-        for (int b = 0; b < R; b += 8) {
-            if constexpr (M == 1)
-                asm(SKML_FLIP8(SKML_DPP_FLIP1)
-                             : "+v"(v[b]), "+v"(v[b + 1]), "+v"(v[b + 2]), "+v"(v[b + 3]), "+v"(v[b + 4]),
-                               "+v"(v[b + 5]), "+v"(v[b + 6]), "+v"(v[b + 7]));
-            else if constexpr (M == 3)
-                asm(SKML_FLIP8(SKML_DPP_FLIP3)
-                             : "+v"(v[b]), "+v"(v[b + 1]), "+v"(v[b + 2]), "+v"(v[b + 3]), "+v"(v[b + 4]),
-                               "+v"(v[b + 5]), "+v"(v[b + 6]), "+v"(v[b + 7]));
-            else if constexpr (M == 7)
-                asm(SKML_FLIP8(SKML_DPP_FLIP7)
-                             : "+v"(v[b]), "+v"(v[b + 1]), "+v"(v[b + 2]), "+v"(v[b + 3]), "+v"(v[b + 4]),
-                               "+v"(v[b + 5]), "+v"(v[b + 6]), "+v"(v[b + 7]));
-            else
-                asm(SKML_FLIP8(SKML_DPP_FLIP15)
-                             : "+v"(v[b]), "+v"(v[b + 1]), "+v"(v[b + 2]), "+v"(v[b + 3]), "+v"(v[b + 4]),
-                               "+v"(v[b + 5]), "+v"(v[b + 6]), "+v"(v[b + 7]));
-        }
-    } else {  // ds_swizzle / ds_bpermute exchange (LDS pipe) + one fused negate-max
-#pragma unroll
-        for (int r = 0; r < R; r++) {
-            const float p = lane_xor<M>(v[r]);
-            asm("v_max_f32 %0, -%1, %0" : "+v"(v[r]) : "v"(p));
-        }
-    }
-}
-
-// v_med3 selector of a same-sign stage with lane mask D at level j: keep the stored max where
-// ((lane & D) == 0) ^ bit j of the lane.
-__device__ __forceinline__ float sgn_sel(int lane, int D, int j) {
-    return sel_of<float>((((lane & D) == 0) ? 1 : 0) ^ ((lane >> j) & 1));
-}
-
-// lane ^ 4 as two DPP row shifts with bank masks (banks 0 and 2 read lane + 4, banks 1 and 3 lane
-// - 4): two VALU moves instead of a ds_swizzle, whose LDS latency sits in the level-3 chain.
-__device__ __forceinline__ float lane_xor4_dpp(float v) {
-    const int x = __float_as_int(v);
-    int t = __builtin_amdgcn_mov_dpp(x, 0x104, 0xF, 0x5, false);        // row_shl:4
-    t = __builtin_amdgcn_update_dpp(t, x, 0x114, 0xF, 0xA, false);      // row_shr:4
-    return __int_as_float(t);
-}
-template <int D>
-__device__ __forceinline__ float sgn_xchg(float v) {
-#ifndef SKML_SGN_XOR4_DPP
-#define SKML_SGN_XOR4_DPP 1
-#endif
-    if constexpr (D == 4 && SKML_SGN_XOR4_DPP) return lane_xor4_dpp(v);
-    else return lane_xor<D>(v);
-}
-
-// Stage lane ^ D with registers reversed (r meets partner's R-1-r).
-template <int R, int D>
-__device__ __forceinline__ void sgn_stage_rev(float (&v)[R], float sel) {
-#pragma unroll
-    for (int r = 0; r < R / 2; r++) {
-        const float pa = sgn_xchg<D>(v[R - 1 - r]);
-        const float pb = sgn_xchg<D>(v[r]);
-        v[r] = med3(v[r], pa, sel);
-        v[R - 1 - r] = med3(v[R - 1 - r], pb, sel);
-        if ((r & 3) == 3) __builtin_amdgcn_sched_barrier(0);
-    }
-}
-
-// Stages lane ^ D for D = 2^(J-2) .. 2 (equal registers).
-template <int R, int J, int D>
-__device__ __forceinline__ void sgn_stages_eq(float (&v)[R], int lane) {
-    if constexpr (D >= 2) {
-        const float sel = sgn_sel(lane, D, J);
-#pragma unroll
-        for (int r = 0; r < R; r++) {
-            v[r] = med3(v[r], lane_xor<D>(v[r]), sel);
-            if ((r & 7) == 7) __builtin_amdgcn_sched_barrier(0);
-        }
-        sgn_stages_eq<R, J, D / 2>(v, lane);
-    }
-}
-
-// Level J (2^J lanes merge two runs of 2^(J-1) lanes, R registers each) + compaction with the
-// node's RNG bit `odd` (the real parity kept; odd lanes hold reversed ranks).
-template <int R, int J>
-__device__ __forceinline__ void sgn_level_compact(float (&v)[R], float (&w)[R / 2], int lane, uint32_t odd) {
-    sgn_flip<(1 << J) - 1>(v);
-    if constexpr (J >= 2) sgn_stage_rev<R, 1 << (J - 1)>(v, sgn_sel(lane, 1 << (J - 1), J));
-    sgn_stages_eq<R, J, (1 << (J - 2))>(v, lane);
-    halfclean_regs_compact<R>(v, w, ((odd ^ (uint32_t)lane) & 1u) != 0);
-}
-
-// Run position of a lane after level 6 (lane order [1, 3, .., 63, 62, .., 2, 0]).
-__device__ __forceinline__ int sgn_run_pos(int lane) { return (lane & 1) ? (lane >> 1) : 63 - (lane >> 1); }
 // `chunks` counts the full tiles' chunks; when total_chunks holds a partial tile as well, that
 // tile's small trees (k_leaf2's PARTIAL path, one wave) run in workgroup 0, which is dispatched
 // first, so they overlap the full tiles instead of following them.
@@ -776,60 +650,29 @@ __global__ __launch_bounds__(256, SKML_LEAF64_WAVES) void k_leaf64(const float* 
             auto bit = [&](int level, int d) -> uint32_t {
                 return (uint32_t)(mask >> (2 * d - __popc((unsigned)d) + level)) & 1u;
             };
-            float w1[32], n4[2];
-            if constexpr (!EX) {
-                // sign-alternating network: odd lanes negate their values, then chunk levels 1-2
-                // and tree levels 1-4 (levels 3-6 of the 64-lane layout) as fused flips +
-                // same-sign stages
-                {  // a sign-bit XOR (2.6 SIMD cycles; v_pk_mul_f32 takes ~9 for two values)
-                    const uint32_t sb = (uint32_t)(ln & 1) << 31;
-#pragma unroll
-                    for (int r = 0; r < 64; r++) v[r] = __uint_as_float(__float_as_uint(v[r]) ^ sb);
-                }
-                sort_regs_oddeven<64>(v);
-                sgn_flip<1>(v);  // level 1: lane pairs
-                halfclean_regs<64>(v);
-                {  // each lane's values are sorted: its real extremes are the chunk's candidates
-                    const bool ng = (ln & 1) != 0;
-                    const uint32_t k0 = total_key(ng ? -v[63] : v[0]), k63 = total_key(ng ? -v[0] : v[63]);
-                    mn = k0 < mn ? k0 : mn;
-                    mx = k63 > mx ? k63 : mx;
-                }
-                sgn_level_compact<64, 2>(v, w1, ln, bit(0, ln >> 2));
-                float w2[16], w3[8], w4[4];
-                sgn_level_compact<32, 3>(w1, w2, ln, bit(1, 2 * (ln >> 3) + 1));
-                sgn_level_compact<16, 4>(w2, w3, ln, bit(2, 4 * (ln >> 4) + 3));
-                sgn_level_compact<8, 5>(w3, w4, ln, bit(3, 8 * (ln >> 5) + 7));
-                sgn_level_compact<4, 6>(w4, n4, ln, bit(4, 15));
-                // back to real values in rank order (row-major: position 2 * lane + r) through LDS
-                {
-                    const bool ng = (ln & 1) != 0;
-                    const float2 pr = ng ? make_float2(-n4[1], -n4[0]) : make_float2(n4[0], n4[1]);
-                    float2* t = reinterpret_cast<float2*>(wfb);
-                    t[sgn_run_pos(ln)] = pr;
-                    __builtin_amdgcn_wave_barrier();
-                    asm volatile("" ::: "memory");
-                    const float2 q = t[ln];
-                    n4[0] = q.x;
-                    n4[1] = q.y;
-                    asm volatile("" ::: "memory");
-                }
-            } else {
-                sort_regs_oddeven<64>(v);
-                sort_lanes_upto128<64, 128>(v, ln);  // two sorted 128-runs per chunk
-                {
-                    const uint32_t k0 = total_key(v[0]), k63 = total_key(v[63]);
-                    mn = k0 < mn ? k0 : mn;
-                    mx = k63 > mx ? k63 : mx;
-                }
-                merge_group_compact<64>(v, w1, ln, bit(0, ln >> 2) != 0);
-                // levels 1..4 in registers: 8, 16, 32, 64 lanes per merge
-                float w2[16], w3[8], w4[4];
-                wave_level<32>(w1, w2, ln, bit(1, 2 * (ln >> 3) + 1), exact, wfb);
-                wave_level<16>(w2, w3, ln, bit(2, 4 * (ln >> 4) + 3), exact, wfb);
-                wave_level<8>(w3, w4, ln, bit(3, 8 * (ln >> 5) + 7), exact, wfb);
-                wave_level<4>(w4, n4, ln, bit(4, 15), exact, wfb);
+            float w1[32];
+            sort_regs_oddeven<64>(v);
+            sort_lanes_upto128<64, 128>(v, ln);  // two sorted 128-runs per chunk
+            {
+                const uint32_t k0 = total_key(v[0]), k63 = total_key(v[63]);
+                mn = k0 < mn ? k0 : mn;
+                mx = k63 > mx ? k63 : mx;
             }
+            merge_group_compact<64>(v, w1, ln, bit(0, ln >> 2) != 0);
+            // levels 1..4 in registers: 8, 16, 32, 64 lanes per merge
+            float w2[16], w3[8], w4[4], n4[2];
+#ifdef SKML_LEAF_ABLATE_TREE  // profiling ablation: levels 1..4 replaced by a fold (wrong results)
+            for (int q = 0; q < 16; q++) w2[q] = fminf(w1[2 * q], w1[2 * q + 1]);
+            for (int q = 0; q < 8; q++) w3[q] = w2[2 * q];
+            for (int q = 0; q < 4; q++) w4[q] = w3[2 * q];
+            n4[0] = w4[0];
+            n4[1] = w4[2];
+#else
+            wave_level<32>(w1, w2, ln, bit(1, 2 * (ln >> 3) + 1), exact, wfb);
+            wave_level<16>(w2, w3, ln, bit(2, 4 * (ln >> 4) + 3), exact, wfb);
+            wave_level<8>(w3, w4, ln, bit(3, 8 * (ln >> 5) + 7), exact, wfb);
+            wave_level<4>(w4, n4, ln, bit(4, 15), exact, wfb);
+#endif
             // levels 5 and 6: the binary-counter carry over rounds (older node first)
             if (!(round & 1)) {
                 stk[wave][0][ln] = make_float2(n4[0], n4[1]);
@@ -1321,19 +1164,27 @@ __device__ void summary_block(const SummaryArgs& a, SummaryShared& S, const Leaf
     }
 
     // ---- blockyMergeSort == stable sort under IEEE `<=` (left run wins ties): rank across runs ----
-    for (int i = t; i < ns; i += T) {
-        int r = 0;
-        while (S.run_off[r + 1] <= i) r++;
-        const float v = S.smp[i];
-        int rank = i - S.run_off[r];
-        for (int q = 0; q < nruns; q++) {
-            if (q == r) continue;
-            const float* run = S.smp + S.run_off[q];
-            const int len = S.run_off[q + 1] - S.run_off[q];
-            rank += q < r ? run_count_le(run, len, v) : run_count_lt(run, len, v);
+    // The level runs hold kK samples each at q * kK (the base buffer last).
+    {
+        const int nfull = nruns - 1;
+        const float* tail_run = S.smp + S.run_off[nfull];
+        for (int i = t; i < ns; i += T) {
+            const int r = i < nfull * kK ? i / kK : nfull;
+            const float v = S.smp[i];
+            int rank = i - S.run_off[r];
+            // two level runs at a time: two independent 7-step searches per loop trip, with the
+            // IEEE `<=` / `<` choice as a branch-free predicate (a divergent le/lt branch ran
+            // both sides); a run paired with itself or the sample's own run counts 0
+            for (int q0 = 0; q0 < nfull; q0 += 2) {
+                const int q1 = q0 + 1 < nfull ? q0 + 1 : q0;
+                rank += rank_in_run_pair(S.smp + q0 * kK, S.smp + q1 * kK, v, (uint32_t)(q0 < r),
+                                         (uint32_t)(q1 < r), (uint32_t)(q0 != r),
+                                         (uint32_t)(q1 != r) & (uint32_t)(q1 != q0));
+            }
+            if (r < nfull) rank += run_count_lt(tail_run, tail, v);  // the base buffer comes last
+            S.sorted[rank] = v;
+            S.w[rank] = S.run_lvl[r] < 0 ? 1 : ((int64_t)2 << S.run_lvl[r]);
         }
-        S.sorted[rank] = v;
-        S.w[rank] = S.run_lvl[r] < 0 ? 1 : ((int64_t)2 << S.run_lvl[r]);
     }
     __syncthreads();
     SKML_PROF(5);

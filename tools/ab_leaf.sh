@@ -4,7 +4,7 @@
 set -e
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"
-for i in 1 2; do
+for i in $(seq ${REPS:-2}); do
 for L in ${LIBS:-lib_old lib}; do
 SKML_LIB=sketchml_amd/$L/libskml.so timeout -k 10 120 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --no-extras --no-configs > gpurun_out/ab_$L.log 2>&1
 python -c "
