@@ -381,10 +381,22 @@ def main():
 
     exch = None
     allp = None
+    payloads = [payload]
     if world > 1:
         from sketchml_amd.distributed import PayloadExchange
-        exch = PayloadExchange(ctx)  # RCCL communicator; unique id broadcast over the process group
+        # The exchange runs on its own stream and context, so step i's all-gather overlaps step
+        # i + 1's encode (the gradient buckets of one DDP step are independent): two payload
+        # buffers, each reused only after its previous all-gather has read it.
+        ex_stream = torch.cuda.Stream(dev)
+        with torch.cuda.stream(ex_stream):
+            ex_ctx_obj = sk.Context(dev.index)  # bound to ex_stream at creation
+        exch = PayloadExchange(ex_ctx_obj._h)  # RCCL communicator; unique id broadcast over the group
         allp = sk.alloc_aligned(nb * world, dev)
+        payloads.append(sk.alloc_aligned(nb, dev))
+        ev_enc = [torch.cuda.Event(), torch.cuda.Event()]
+        ev_ex = [torch.cuda.Event(), torch.cuda.Event()]
+        ex_used = [False, False]
+        main_stream = torch.cuda.current_stream(dev)
 
     encode = getattr(lib, {("quantile", "f32"): "skml_dense_encode_f32",
                            ("quantile", "f64"): "skml_dense_encode_f64",
@@ -394,11 +406,19 @@ def main():
 
     def step(i):
         x = xs[i % nbuf]
-        st = encode(ctx, C.c_void_p(x.data_ptr()), n, C.byref(params), C.c_void_p(payload.data_ptr()), nb)
+        b = i % len(payloads)
+        if exch is not None and ex_used[b]:
+            main_stream.wait_event(ev_ex[b])  # the previous all-gather of this buffer has read it
+        p = payloads[b]
+        st = encode(ctx, C.c_void_p(x.data_ptr()), n, C.byref(params), C.c_void_p(p.data_ptr()), nb)
         if st:
             raise RuntimeError(_lib.last_error())
         if exch is not None:
-            exch.allgather(payload, nb, allp)
+            ev_enc[b].record(main_stream)
+            ex_stream.wait_event(ev_enc[b])
+            exch.allgather(p, nb, allp)
+            ev_ex[b].record(ex_stream)
+            ex_used[b] = True
 
     def barrier():
         if world > 1:
