@@ -439,7 +439,7 @@ __device__ __forceinline__ uint32_t lut_bucket_of(float f) {
 
 // s_misc: 20 ints of LDS; lbuf: kLutSize / 2 uint32 of LDS (u16 counts, then u16 bases in place).
 __device__ __forceinline__ void build_quant_lut(const float* sp, int nsplit, QuantLut* lut, int* s_misc,
-                                                uint32_t* lbuf) {
+                                                uint32_t* lbuf, unsigned long long* prof = nullptr) {
     const int T = blockDim.x, t = threadIdx.x, lane = t & 63, w = t >> 6, nw = T >> 6;
     constexpr uint32_t kNegZeroBucket = 0x7FFFFFFFu >> (32 - kLutBits);
     uint16_t* cnt = reinterpret_cast<uint16_t*>(lbuf);
@@ -452,6 +452,7 @@ __device__ __forceinline__ void build_quant_lut(const float* sp, int nsplit, Qua
         if ((__float_as_uint(sp[i]) & 0x7FFFFFFFu) == 0u) atomicAdd(&s_misc[0], 1);
     }
     __syncthreads();
+    if (prof && t == 0) prof[0] = wall_clock64();  // profiling builds: histogram done
     // exclusive scan: each thread owns kLutSize / T consecutive buckets
     const int per = kLutSize / T, b0 = t * per;  // per >= 16, a multiple of 8
     const uint4* c4 = reinterpret_cast<const uint4*>(cnt + b0);
@@ -474,7 +475,10 @@ __device__ __forceinline__ void build_quant_lut(const float* sp, int nsplit, Qua
         if (lane >= off) inc += y;
     }
     if (lane == 63) s_misc[4 + w] = inc;
-    atomicMax(&s_misc[1], cmax);
+    // one LDS atomic per wave (512 same-address atomics serialise: ~2 us)
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) cmax = max(cmax, __shfl_xor(cmax, off, 64));
+    if (lane == 0) atomicMax(&s_misc[1], cmax);
     __syncthreads();
     int run = inc - sum;
     for (int j = 0; j < w; j++) run += s_misc[4 + j];
@@ -494,6 +498,7 @@ __device__ __forceinline__ void build_quant_lut(const float* sp, int nsplit, Qua
         o4[k] = make_uint4(wds[0], wds[1], wds[2], wds[3]);
     }
     __syncthreads();
+    if (prof && t == 0) prof[1] = wall_clock64();  // profiling builds: scan done
     const uint4* src = reinterpret_cast<const uint4*>(lbuf);
     uint4* dst = reinterpret_cast<uint4*>(lut->base);
     for (int i = t; i < (int)(sizeof(lut->base) / (sizeof(uint4))); i += T) dst[i] = src[i];

@@ -245,9 +245,10 @@ __global__ __launch_bounds__(512) void k_summary64(const double* __restrict__ x,
             // both sides); a run paired with itself or the sample's own run counts 0
             for (int q0 = 0; q0 < nfull; q0 += 2) {
                 const int q1 = q0 + 1 < nfull ? q0 + 1 : q0;
+                const uint32_t use_a = (uint32_t)(q0 != r), use_b = (uint32_t)(q1 != r) & (uint32_t)(q1 != q0);
+                if (!(use_a | use_b)) continue;  // e.g. a single level run: nothing to search
                 rank += rank_in_run_pair(S.smp + q0 * kK, S.smp + q1 * kK, v, (uint32_t)(q0 < r),
-                                         (uint32_t)(q1 < r), (uint32_t)(q0 != r),
-                                         (uint32_t)(q1 != r) & (uint32_t)(q1 != q0));
+                                         (uint32_t)(q1 < r), use_a, use_b);
             }
             if (r < nfull) rank += run_count_lt64(tail_run, tail, v);  // the base buffer comes last
             S.sorted[rank] = v;

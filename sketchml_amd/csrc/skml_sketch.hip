@@ -1177,9 +1177,10 @@ __device__ void summary_block(const SummaryArgs& a, SummaryShared& S, const Leaf
             // both sides); a run paired with itself or the sample's own run counts 0
             for (int q0 = 0; q0 < nfull; q0 += 2) {
                 const int q1 = q0 + 1 < nfull ? q0 + 1 : q0;
+                const uint32_t use_a = (uint32_t)(q0 != r), use_b = (uint32_t)(q1 != r) & (uint32_t)(q1 != q0);
+                if (!(use_a | use_b)) continue;  // e.g. a single level run: nothing to search
                 rank += rank_in_run_pair(S.smp + q0 * kK, S.smp + q1 * kK, v, (uint32_t)(q0 < r),
-                                         (uint32_t)(q1 < r), (uint32_t)(q0 != r),
-                                         (uint32_t)(q1 != r) & (uint32_t)(q1 != q0));
+                                         (uint32_t)(q1 < r), use_a, use_b);
             }
             if (r < nfull) rank += run_count_lt(tail_run, tail, v);  // the base buffer comes last
             S.sorted[rank] = v;
@@ -1283,7 +1284,13 @@ __device__ void summary_block(const SummaryArgs& a, SummaryShared& S, const Leaf
         if (threadIdx.x == 0) g_prof[28] = __builtin_amdgcn_s_memtime();
 #endif
         // LDS staging of the table aliases sorted[] + w[] (both dead after getQuantiles)
-        build_quant_lut(S.smp, nsplit, a.lut, reinterpret_cast<int*>(S.wsum), reinterpret_cast<uint32_t*>(S.sorted));
+#ifdef SKML_PROF_SUMMARY
+        unsigned long long* lprof = g_prof + 30;
+#else
+        unsigned long long* lprof = nullptr;
+#endif
+        build_quant_lut(S.smp, nsplit, a.lut, reinterpret_cast<int*>(S.wsum), reinterpret_cast<uint32_t*>(S.sorted),
+                        lprof);
     } else if (t == 0) {
         a.lut->cmax = -1;
     }

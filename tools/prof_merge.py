@@ -23,7 +23,7 @@ q = sk.QuantileQuantizer(256, seed=1)
 slots = {"p1wg0_start": 12, "p1wg0_loaded": 13, "p1wg0_inwave": 14, "p1wg0_done": 15, "last_arrival": 20,
          "last_acquired": 21, "p2_start": 16, "p2_loaded": 17, "p2_bits": 22, "p2_l1": 23, "p2_l2": 24, "p2_l3": 25, "p2_inwave": 18, "p2_done": 19,
          "summary_start": 1, "setup": 2, "minmax": 3, "gather": 4, "blocky_rank": 5, "prefix": 6,
-         "quantiles": 7, "unique_zero": 8, "lut_start": 9, "lut_end": 10, "warm_start": 26, "warm_end": 27}
+         "quantiles": 7, "unique_zero": 8, "lut_start": 9, "lut_hist": 30, "lut_scan": 31, "lut_end": 10, "warm_start": 26, "warm_end": 27}
 buf = (C.c_ulonglong * 32)()
 fn = _lib.lib.skml_debug_prof
 fn.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
