@@ -385,3 +385,22 @@ def test_context_follows_stream_switches(gpu):
     torch.cuda.synchronize()
     for g, w in zip(got, want):
         assert torch.equal(g, w)
+
+
+# chunk counts whose upper merge ends in a pass of several small trees (2^16 + 2^15 chunks: the
+# level-16 and level-15 trees each leave one workgroup-merge for the last pass, which runs inside
+# the previous pass's last workgroup), and the summary then ranks across many level runs
+@pytest.mark.parametrize("chunks,tail,dtype", [((1 << 16) + (1 << 15), 77, "f32"),
+                                               ((1 << 16) + (1 << 15) + (1 << 13) + 37, 200, "f32"),
+                                               ((1 << 16) + (1 << 14), 5, "f64")])
+def test_multi_tree_sizes_match_oracle(gpu, chunks, tail, dtype):
+    n = chunks * 256 + tail
+    xh = np.random.default_rng(chunks % 1000).standard_normal(n)
+    if dtype == "f32":
+        xh = xh.astype(np.float32)
+    gq = gpu.QuantileQuantizer(256, seed=chunks % 13)
+    gq.quantize(torch.from_numpy(xh).cuda())
+    oq = O.quantize(xh.astype(np.float64), 256, chunks % 13)
+    assert gq.getBinNum() == oq.bin_num and gq.getZeroIdx() == oq.zero_idx
+    assert np.array_equal(np.asarray(gq.getSplits(), dtype=np.float64), oq.splits)
+    assert np.array_equal(gq.getBins().cpu().numpy(), oq.bins)
