@@ -738,25 +738,42 @@ __global__ __launch_bounds__(256) void k_uni_finish(const T* __restrict__ x, int
         if (mx > jmax) jmax = mx;
         s_mn = jmin;
         s_mx = jmax;
-        // UniformQuantizer.java:31-36
+        // UniformQuantizer.java:31-36: split i is min + step followed by i more `+= step`, a
+        // serial chain of rounded adds; only the adds stay on one thread (the conversions and
+        // checks below run on the whole workgroup: one thread doing all of it took ~30 us)
         const double step = (jmax - jmin) / bin_num;
         const int ns = bin_num - 1;
-        double cur = jmin + step, prev = cur;
-        int bad = 0, zero = ns;
+        double cur = jmin + step;
         for (int i = 0; i < ns; i++) {
             if (i > 0) cur = cur + step;
             splits[i] = cur;
-            if (i < kLutMaxSplits) s_sp[i] = __double2float_ru(cur);
-            bad |= (!(cur == cur) || !(prev <= cur)) ? 1 : 0;
-            zero = (zero == ns && !(cur < 0.0)) ? i : zero;
-            prev = cur;
         }
-        s_bad = bad;
-        s_zero = zero;
-        *qflags = bad;
+        s_bad = 0;
+        s_zero = ns;
     }
+    __threadfence_block();
     __syncthreads();
     const int ns = bin_num - 1;
+    {
+        int bad = 0, zero = ns;
+        for (int i = threadIdx.x; i < ns; i += blockDim.x) {
+            const double cur = splits[i], prev = i > 0 ? splits[i - 1] : cur;
+            if (i < kLutMaxSplits) s_sp[i] = __double2float_ru(cur);
+            bad |= (!(cur == cur) || !(prev <= cur)) ? 1 : 0;
+            zero = (zero == ns && !(cur < 0.0)) ? i : zero;  // ascending i per thread: its first
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            bad |= __shfl_xor(bad, off, 64);
+            zero = min(zero, __shfl_xor(zero, off, 64));
+        }
+        if ((threadIdx.x & 63) == 0) {
+            if (bad) atomicOr(&s_bad, 1);
+            atomicMin(&s_zero, zero);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) *qflags = s_bad;
     const double jmin = s_mn, jmax = s_mx;
     const bool lut_ok = !s_bad && ns <= kLutMaxSplits;
     payload_zero_tail(reinterpret_cast<uint8_t*>(hdr), ns, bin_num);
