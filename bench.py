@@ -351,8 +351,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    # SKML_BENCH_EXCHANGE=1 runs the N > 1 exchange path (RCCL all-gather on its own stream) with a
+    # world-size-1 communicator: a one-GPU rehearsal of the code the multi-GPU runs take
+    rehearse = world == 1 and os.environ.get("SKML_BENCH_EXCHANGE") == "1"
+    if world > 1 or rehearse:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
@@ -382,7 +388,7 @@ def main():
     exch = None
     allp = None
     payloads = [payload]
-    if world > 1:
+    if world > 1 or rehearse:
         from sketchml_amd.distributed import PayloadExchange
         # The exchange runs on its own stream and context, so step i's all-gather overlaps step
         # i + 1's encode (the gradient buckets of one DDP step are independent): two payload
@@ -421,7 +427,7 @@ def main():
             ex_used[b] = True
 
     def barrier():
-        if world > 1:
+        if dist.is_initialized():
             dist.barrier()
 
     for i in range(args.warmup):
@@ -568,7 +574,9 @@ def main():
             "roofline": roofline, "cpu_baseline": cpu, "extras": extras,
         }
         print(json.dumps(line))
-    if world > 1:
+    if exch is not None:
+        exch.close()
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
