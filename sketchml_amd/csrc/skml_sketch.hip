@@ -1034,7 +1034,10 @@ struct SummaryArgs {
 // pre: this thread's min / max / flags of the leaf partials, already loaded by the caller (the
 // fused merge workgroup fetches them before its merge so the load latency hides there); null:
 // load them here.
-__device__ void summary_block(const SummaryArgs& a, SummaryShared& S, const LeafPartial* pre = nullptr) {
+// has_pre: `pre` holds this thread's share of the leaf partials, loaded ahead by the caller (by
+// value: a pointer to the caller's local put it in scratch memory, a store and a reload away).
+__device__ void summary_block(const SummaryArgs& a, SummaryShared& S, bool has_pre = false,
+                              LeafPartial pre = LeafPartial{0xFFFFFFFFu, 0u, 0u, 0u}) {
     const int t = threadIdx.x, T = blockDim.x;
     skml_dense_header* hdr = reinterpret_cast<skml_dense_header*>(a.payload);
     double* splits = reinterpret_cast<double*>(a.payload + kHeaderBytes);
@@ -1067,14 +1070,14 @@ __device__ void summary_block(const SummaryArgs& a, SummaryShared& S, const Leaf
     // ---- min / max / NaN ----
     {
         uint32_t mn = 0xFFFFFFFFu, mx = 0u, fl = 0u;
-        if (pre) {
-            mn = pre->min_key;
-            mx = pre->max_key;
-            fl = pre->flags;
+        if (has_pre) {
+            mn = pre.min_key;
+            mx = pre.max_key;
+            fl = pre.flags;
         }
         // the pre-reduced partials first, then the uncovered tiles: batches of 8 independent loads
         // per thread (one memory latency per batch, not per load)
-        const int64_t ntot = pre ? 0 : a.nred + (a.nparts - a.part_from);
+        const int64_t ntot = has_pre ? 0 : a.nred + (a.nparts - a.part_from);
         for (int64_t i0 = t; i0 < ntot; i0 += 8 * (int64_t)T) {
             LeafPartial p[8];
 #pragma unroll
@@ -1524,7 +1527,7 @@ __global__ __launch_bounds__(512) void k_merge(MergePass pass, MergePass next, c
         if (!next.fuse_summary) return;
     }
     SKML_PROF(1);
-    summary_block(sa, U.s, prefetch ? &pre : nullptr);
+    summary_block(sa, U.s, prefetch, pre);
 #ifdef SKML_PROF_WARM
     // diagnostic build: the summary again with warm instruction / data caches (phases 2..10 then
     // hold the second run; 26 / 27 bracket it)
