@@ -50,6 +50,20 @@ __device__ __forceinline__ double lane_xor(double v) {
     return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
+// Inclusive wave-64 prefix sum of 32-bit values in 6 DPP adds (row shifts 1, 2, 4, 8 inside each
+// 16-lane row, then row_bcast:15 / row_bcast:31 carry the row totals): a dependent chain of VALU
+// ops instead of six LDS-pipe shuffles (ds_bpermute, ~100+ cycles each).
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
+    int x = (int)v;
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, true);  // row_shr:1 (row edge reads 0)
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, true);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, true);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, true);  // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15 into rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31 into rows 2, 3
+    return (uint32_t)x;
+}
+
 // Sort elements are uint32 total-order keys, raw floats or raw doubles.  Floats and doubles
 // compare with v_min/v_max(/v_med3)_f32/f64, which on gfx950 order -0.0 before 0.0 like
 // Arrays.sort (tools/ubench/zero_minmax.hip) and drop NaN, so the leaf flags NaN from a class
@@ -468,12 +482,7 @@ __device__ __forceinline__ void build_quant_lut(const float* sp, int nsplit, Qua
         }
     }
     if (b0 <= (int)kNegZeroBucket && (int)kNegZeroBucket < b0 + per) cmax = max(cmax, cnt[kNegZeroBucket] + s_misc[0]);
-    int inc = sum;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int y = __shfl_up(inc, off, 64);
-        if (lane >= off) inc += y;
-    }
+    const int inc = (int)wave_incl_scan_u32((uint32_t)sum);
     if (lane == 63) s_misc[4 + w] = inc;
     // one LDS atomic per wave (512 same-address atomics serialise: ~2 us)
 #pragma unroll

@@ -982,24 +982,16 @@ __device__ __forceinline__ int run_count_lt(const float* r, int len, float x) {
     return lo;
 }
 
-// Exclusive block scan of one int64 per thread (wave shuffles + one LDS round).
+// Exclusive block scan of one non-negative value per thread whose block total stays below 2^32
+// (the summary's weights sum to n < 2^31, its split counts to < 2^16): DPP wave scans + one LDS
+// round.
 __device__ int64_t block_scan_excl(int64_t v, int64_t* wsum, int64_t* total) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, nw = blockDim.x >> 6;
-    int64_t x = v;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int64_t y = __shfl_up(x, off, 64);
-        if (lane >= off) x += y;
-    }
+    const int64_t x = (int64_t)wave_incl_scan_u32((uint32_t)v);
     if (lane == 63) wsum[w] = x;
     __syncthreads();
     if (w == 0) {
-        int64_t s = lane < nw ? wsum[lane] : 0;
-#pragma unroll
-        for (int off = 1; off < 16; off <<= 1) {
-            const int64_t y = __shfl_up(s, off, 64);
-            if (lane >= off) s += y;
-        }
+        const int64_t s = (int64_t)wave_incl_scan_u32(lane < nw ? (uint32_t)wsum[lane] : 0u);
         if (lane < nw) wsum[lane] = s;
     }
     __syncthreads();
