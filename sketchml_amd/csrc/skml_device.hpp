@@ -64,6 +64,25 @@ __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
     return (uint32_t)x;
 }
 
+// Wave-64 reductions (min / max / or of uint32) with the same DPP steps: the result is valid in
+// lane 63, which the callers use for their one LDS atomic per wave.
+template <int OP>  // 0 min, 1 max, 2 or
+__device__ __forceinline__ uint32_t dpp_op(uint32_t a, uint32_t b) {
+    return OP == 0 ? (a < b ? a : b) : OP == 1 ? (a > b ? a : b) : (a | b);
+}
+template <int OP>
+__device__ __forceinline__ uint32_t wave_reduce_u32_lane63(uint32_t v) {
+    constexpr int id = OP == 0 ? -1 : 0;  // identity in the lanes a shift leaves without a source
+    int x = (int)v;
+    x = (int)dpp_op<OP>((uint32_t)x, (uint32_t)__builtin_amdgcn_update_dpp(id, x, 0x111, 0xF, 0xF, false));
+    x = (int)dpp_op<OP>((uint32_t)x, (uint32_t)__builtin_amdgcn_update_dpp(id, x, 0x112, 0xF, 0xF, false));
+    x = (int)dpp_op<OP>((uint32_t)x, (uint32_t)__builtin_amdgcn_update_dpp(id, x, 0x114, 0xF, 0xF, false));
+    x = (int)dpp_op<OP>((uint32_t)x, (uint32_t)__builtin_amdgcn_update_dpp(id, x, 0x118, 0xF, 0xF, false));
+    x = (int)dpp_op<OP>((uint32_t)x, (uint32_t)__builtin_amdgcn_update_dpp(id, x, 0x142, 0xA, 0xF, false));
+    x = (int)dpp_op<OP>((uint32_t)x, (uint32_t)__builtin_amdgcn_update_dpp(id, x, 0x143, 0xC, 0xF, false));
+    return (uint32_t)x;
+}
+
 // Sort elements are uint32 total-order keys, raw floats or raw doubles.  Floats and doubles
 // compare with v_min/v_max(/v_med3)_f32/f64, which on gfx950 order -0.0 before 0.0 like
 // Arrays.sort (tools/ubench/zero_minmax.hip) and drop NaN, so the leaf flags NaN from a class
@@ -485,9 +504,8 @@ __device__ __forceinline__ void build_quant_lut(const float* sp, int nsplit, Qua
     const int inc = (int)wave_incl_scan_u32((uint32_t)sum);
     if (lane == 63) s_misc[4 + w] = inc;
     // one LDS atomic per wave (512 same-address atomics serialise: ~2 us)
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) cmax = max(cmax, __shfl_xor(cmax, off, 64));
-    if (lane == 0) atomicMax(&s_misc[1], cmax);
+    cmax = (int)wave_reduce_u32_lane63<1>((uint32_t)cmax);  // counts are >= 0
+    if (lane == 63) atomicMax(&s_misc[1], cmax);
     __syncthreads();
     int run = inc - sum;
     for (int j = 0; j < w; j++) run += s_misc[4 + j];

@@ -1092,15 +1092,11 @@ __device__ void summary_block(const SummaryArgs& a, SummaryShared& S, bool has_p
             mn = k < mn ? k : mn;
             mx = k > mx ? k : mx;
         }
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {  // wave reduction: one LDS atomic per wave
-            const uint32_t omn = (uint32_t)__shfl_xor((int)mn, off, 64);
-            const uint32_t omx = (uint32_t)__shfl_xor((int)mx, off, 64);
-            mn = omn < mn ? omn : mn;
-            mx = omx > mx ? omx : mx;
-            fl |= (uint32_t)__shfl_xor((int)fl, off, 64);
-        }
-        if ((t & 63) == 0) {
+        // wave reduction (DPP, result in lane 63): one LDS atomic per wave
+        mn = wave_reduce_u32_lane63<0>(mn);
+        mx = wave_reduce_u32_lane63<1>(mx);
+        fl = wave_reduce_u32_lane63<2>(fl);
+        if ((t & 63) == 63) {
             atomicMin(&S.min_key, mn);
             atomicMax(&S.max_key, mx);
             if (fl) atomicOr(&S.flags, fl);
@@ -1246,9 +1242,8 @@ __device__ void summary_block(const SummaryArgs& a, SummaryShared& S, bool has_p
                 o++;
             }
         }
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) zmin = min(zmin, __shfl_xor(zmin, off, 64));
-        if ((t & 63) == 0 && zmin != 0x7FFFFFFF) atomicMin(&S.zero, zmin);  // one LDS atomic per wave
+        zmin = (int)wave_reduce_u32_lane63<0>((uint32_t)zmin);  // indices >= 0: unsigned min
+        if ((t & 63) == 63 && zmin != 0x7FFFFFFF) atomicMin(&S.zero, zmin);  // one LDS atomic per wave
         bin_num = (int)S.total + 1;
     }
     __syncthreads();
