@@ -269,6 +269,9 @@ typedef struct skml_sparse skml_sparse; /* library-owned; free with skml_sparse_
  * Synchronising (returns nnz through *nnz_out). */
 int skml_sparse_compact_f32(skml_ctx* ctx, const float* dense_dev, int64_t dim, int32_t* keys_dev,
                             float* vals_dev, int64_t* nnz_out);
+/* The same over the reference's own double[] (DenseDoubleGradient.values): |x| > 1e-8 in double. */
+int skml_sparse_compact_f64(skml_ctx* ctx, const double* dense_dev, int64_t dim, int32_t* keys_dev,
+                            double* vals_dev, int64_t* nnz_out);
 
 /* SparseVectorCompressor.compressSparse (sample/SparseVectorCompressor.java:52-67):
  * QuantileQuantizer.quantize(values) then GroupedMinMaxSketch.create(keys, bins)
@@ -276,14 +279,28 @@ int skml_sparse_compact_f32(skml_ctx* ctx, const float* dense_dev, int64_t dim, 
  * encoding (binary/DeltaAdaptiveEncoder.java:54-112).  Synchronising. */
 int skml_sparse_encode_kv_f32(skml_ctx* ctx, const int32_t* keys_dev, const float* vals_dev,
                               int64_t nnz, const skml_params* params, skml_sparse** out);
+/* SparseVectorCompressor.compressSparse(int[], double[]) / SketchGradient.fromSparse on the
+ * reference's own double values (SketchGradient.scala:35-48, SparseVectorCompressor.java:52-67):
+ * the values' quantizer sketches and bins the doubles themselves (skml_dense_encode_f64, or the
+ * uniform / parallel f64 forms), so split samples and bins equal the Java double[] path even for
+ * values that are not fp32-representable.  Synchronising. */
+int skml_sparse_encode_kv_f64(skml_ctx* ctx, const int32_t* keys_dev, const double* vals_dev,
+                              int64_t nnz, const skml_params* params, skml_sparse** out);
 /* SketchGradient.fromSparse after toAuto's compaction: compact + encode_kv. */
 int skml_sparse_encode_f32(skml_ctx* ctx, const float* dense_dev, int64_t dim,
+                           const skml_params* params, skml_sparse** out);
+/* The ml path itself: DenseDoubleGradient.toAuto / toSparse (DenseDoubleGradient.scala:64-95) of a
+ * double[] gradient, then SketchGradient.fromSparse on the double values. */
+int skml_sparse_encode_f64(skml_ctx* ctx, const double* dense_dev, int64_t dim,
                            const skml_params* params, skml_sparse** out);
 /* GroupedMinMaxSketch.restore + Sort.merge (GroupedMinMaxSketch.java:123-146,
  * util/Sort.java:362-379) and SparseVectorCompressor.decompressSparse's value lookup
  * (SparseVectorCompressor.java:118-126).  keys/vals device buffers of nnz capacity. */
 int skml_sparse_decode_f32(skml_ctx* ctx, const skml_sparse* s, int32_t* keys_dev,
                            float* vals_dev);
+/* The same with the values as the reference's doubles (quantValues[bin], no fp32 rounding). */
+int skml_sparse_decode_f64(skml_ctx* ctx, const skml_sparse* s, int32_t* keys_dev,
+                           double* vals_dev);
 int skml_sparse_nnz(const skml_sparse* s, int64_t* nnz);
 /* SparseVectorCompressor.timesBy (sample/SparseVectorCompressor.java:128-134): scales the
  * double quantValues table in place (the scaled values are what decode returns, as fp32). */
@@ -325,7 +342,12 @@ int skml_sparse_free(skml_sparse* s);
 /* Host-memory forms of encode_kv / decode (int[] keys and float[] values in JVM arrays). */
 int skml_sparse_encode_kv_host_f32(skml_ctx* ctx, const int32_t* keys_host, const float* vals_host, int64_t nnz,
                                    const skml_params* params, skml_sparse** out);
+/* int[] keys and double[] values (SparseVectorCompressor.compressSparse(int[], double[])). */
+int skml_sparse_encode_kv_host_f64(skml_ctx* ctx, const int32_t* keys_host, const double* vals_host, int64_t nnz,
+                                   const skml_params* params, skml_sparse** out);
 int skml_sparse_decode_host_f32(skml_ctx* ctx, const skml_sparse* s, int32_t* keys_host, float* vals_host);
+/* keys into an int[] and quantValues[bin] into a double[] (SparseVectorCompressor.decompressSparse). */
+int skml_sparse_decode_host_f64(skml_ctx* ctx, const skml_sparse* s, int32_t* keys_host, double* vals_host);
 
 /* ---- DeltaAdaptiveEncoder as a standalone BinaryEncoder (base/BinaryEncoder.java:6-11) ---- */
 /* encode(int[]): keys strictly increasing (keys[0] >= 0).  Outputs the choice and the two

@@ -35,10 +35,11 @@ final class HipCodec {
     static native void timesBy(byte[] payload, double x);
 
     // SparseVectorCompressor: quantize(values) + GroupedMinMaxSketch.create(keys, bins)
-    static native long encodeSparse(long ctx, int[] keys, float[] vals, int binNum, int groupNum, int rowNum,
+    static native long encodeSparse(long ctx, int[] keys, double[] vals, int binNum, int groupNum, int rowNum,
                                     double colRatio, long seed, long hashSeed, boolean uniform, int parallelism);
 
-    static native void decodeSparse(long ctx, long sparse, int[] keys, float[] vals);
+    /** keys and quantValues[bin] as doubles; both arrays must hold sparseNnz(sparse) entries */
+    static native void decodeSparse(long ctx, long sparse, int[] keys, double[] vals);
 
     static native int sparseNnz(long sparse);
 

@@ -15,9 +15,10 @@ import java.util.Arrays;
 /**
  * Same surface as sample/SparseVectorCompressor.java:18-148: quantize the values, then
  * GroupedMinMaxSketch.create over (keys, bins) -- group partition, MinMaxSketch tables,
- * DeltaAdaptiveEncoder keys -- on the GPU.  The device sparse path quantises fp32 values: double
- * inputs are narrowed to float (exact for float-valued gradients).  writeObject ships the
- * GroupedMinMaxSketch field stream (HuffmanEncoder tables, BitSet words) and quantValues.
+ * DeltaAdaptiveEncoder keys -- on the GPU.  The double values are quantised as doubles (the
+ * sketch samples and bins are those of the reference's double[] path) and decompressSparse returns
+ * quantValues[bin] in double.  writeObject ships the GroupedMinMaxSketch field stream (HuffmanEncoder
+ * tables, BitSet words) and quantValues.
  */
 public class HipSparseVectorCompressor implements VectorCompressor, AutoCloseable {
     private final Quantizer.QuantizationType quantType;
@@ -44,20 +45,13 @@ public class HipSparseVectorCompressor implements VectorCompressor, AutoCloseabl
         this.hashSeed = hashSeed;
     }
 
-    private static float[] narrow(double[] v) {
-        float[] f = new float[v.length];
-        for (int i = 0; i < v.length; i++)
-            f[i] = (float) v[i];
-        return f;
-    }
-
     private void encode(int[] keys, double[] values, int parallelism) {
         if (keys.length != values.length)
             throw new SketchMLException(String.format(
                     "Lengths of key array and value array do not match: %d, %d", keys.length, values.length));
         close();
         size = keys.length;
-        handle = HipCodec.encodeSparse(HipCodec.ctx(), keys, narrow(values), quantBinNum, groupNum, rowNum,
+        handle = HipCodec.encodeSparse(HipCodec.ctx(), keys, values, quantBinNum, groupNum, rowNum,
                 colRatio, seed, hashSeed, quantType == Quantizer.QuantizationType.UNIFORM, parallelism);
         quantValues = HipCodec.sparseValues(handle, quantBinNum);
     }
@@ -93,19 +87,18 @@ public class HipSparseVectorCompressor implements VectorCompressor, AutoCloseabl
         for (int k : kv.getLeft())
             maxKey = Math.max(k, maxKey);
         double[] res = new double[maxKey + 1];
-        for (int i = 0; i < size; i++)
+        for (int i = 0; i < kv.getLeft().length; i++)
             res[kv.getLeft()[i]] = kv.getRight()[i];
         return res;
     }
 
     @Override
     public Pair<int[], double[]> decompressSparse() {
-        int[] keys = new int[size];
-        float[] vals = new float[size];
-        HipCodec.decodeSparse(HipCodec.ctx(), handle, keys, vals);
-        double[] values = new double[size];
-        for (int i = 0; i < size; i++)
-            values[i] = vals[i];
+        // sized by the payload itself (a deserialised `size` field may disagree with the stream)
+        final int nnz = HipCodec.sparseNnz(handle);
+        int[] keys = new int[nnz];
+        double[] values = new double[nnz];
+        HipCodec.decodeSparse(HipCodec.ctx(), handle, keys, values);
         return new ImmutablePair<>(keys, values);
     }
 

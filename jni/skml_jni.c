@@ -52,6 +52,17 @@ static jbyteArray to_byte_array(JNIEnv* env, const uint8_t* buf, size_t len) {
     return out;
 }
 
+/* GetPrimitiveArrayCritical may return NULL (out of memory): throw OutOfMemoryError unless the JVM
+ * already has an exception pending.  Returns 1 when the caller must bail out. */
+static int pin_failed(JNIEnv* env, const void* a, const void* b) {
+    if (a && b) return 0;
+    if (!(*env)->ExceptionCheck(env)) {
+        jclass k = (*env)->FindClass(env, "java/lang/OutOfMemoryError");
+        if (k) (*env)->ThrowNew(env, k, "cannot pin a Java array for the GPU codec");
+    }
+    return 1;
+}
+
 /* ---------------------------------------------------------------- context */
 JNIEXPORT jlong JNICALL Java_org_dma_sketchml_hip_HipCodec_ctxCreate(JNIEnv* env, jclass cls, jint device) {
     (void)cls;
@@ -81,6 +92,10 @@ JNIEXPORT jbyteArray JNICALL Java_org_dma_sketchml_hip_HipCodec_encodeDense(JNIE
     uint8_t* buf = (uint8_t*)malloc(cap ? cap : 1);
     if (!buf) return NULL;
     float* x = (float*)(*env)->GetPrimitiveArrayCritical(env, xs, NULL);
+    if (pin_failed(env, x, buf)) {
+        free(buf);
+        return NULL;
+    }
     int st = skml_dense_encode_host_f32(CTX(ctx), x, n, &p, buf, cap, &wrote);
     (*env)->ReleasePrimitiveArrayCritical(env, xs, x, JNI_ABORT);
     jbyteArray out = st ? NULL : to_byte_array(env, buf, wrote);
@@ -104,6 +119,10 @@ JNIEXPORT jbyteArray JNICALL Java_org_dma_sketchml_hip_HipCodec_encodeDenseF64(J
     uint8_t* buf = (uint8_t*)malloc(cap ? cap : 1);
     if (!buf) return NULL;
     double* x = (double*)(*env)->GetPrimitiveArrayCritical(env, xs, NULL);
+    if (pin_failed(env, x, buf)) {
+        free(buf);
+        return NULL;
+    }
     int st = skml_dense_encode_host_f64(CTX(ctx), x, n, &p, buf, cap, &wrote);
     (*env)->ReleasePrimitiveArrayCritical(env, xs, x, JNI_ABORT);
     jbyteArray out = st ? NULL : to_byte_array(env, buf, wrote);
@@ -118,7 +137,11 @@ JNIEXPORT void JNICALL Java_org_dma_sketchml_hip_HipCodec_decodeDense(JNIEnv* en
     (void)cls;
     const jsize len = (*env)->GetArrayLength(env, payload), n = (*env)->GetArrayLength(env, out);
     void* pl = (*env)->GetPrimitiveArrayCritical(env, payload, NULL);
-    float* o = (float*)(*env)->GetPrimitiveArrayCritical(env, out, NULL);
+    float* o = pl ? (float*)(*env)->GetPrimitiveArrayCritical(env, out, NULL) : NULL;
+    if (pin_failed(env, pl, o)) {
+        if (pl) (*env)->ReleasePrimitiveArrayCritical(env, payload, pl, JNI_ABORT);
+        return;
+    }
     int st = skml_dense_decode_host_f32(CTX(ctx), pl, (size_t)len, o, n);
     (*env)->ReleasePrimitiveArrayCritical(env, out, o, 0);
     (*env)->ReleasePrimitiveArrayCritical(env, payload, pl, JNI_ABORT);
@@ -131,7 +154,11 @@ JNIEXPORT void JNICALL Java_org_dma_sketchml_hip_HipCodec_decodeDenseF64(JNIEnv*
     (void)cls;
     const jsize len = (*env)->GetArrayLength(env, payload), n = (*env)->GetArrayLength(env, out);
     void* pl = (*env)->GetPrimitiveArrayCritical(env, payload, NULL);
-    double* o = (double*)(*env)->GetPrimitiveArrayCritical(env, out, NULL);
+    double* o = pl ? (double*)(*env)->GetPrimitiveArrayCritical(env, out, NULL) : NULL;
+    if (pin_failed(env, pl, o)) {
+        if (pl) (*env)->ReleasePrimitiveArrayCritical(env, payload, pl, JNI_ABORT);
+        return;
+    }
     int st = skml_dense_decode_host_f64(CTX(ctx), pl, (size_t)len, o, n);
     (*env)->ReleasePrimitiveArrayCritical(env, out, o, 0);
     (*env)->ReleasePrimitiveArrayCritical(env, payload, pl, JNI_ABORT);
@@ -144,7 +171,11 @@ JNIEXPORT void JNICALL Java_org_dma_sketchml_hip_HipCodec_getBins(JNIEnv* env, j
     (void)cls;
     const jsize len = (*env)->GetArrayLength(env, payload), n = (*env)->GetArrayLength(env, out);
     void* pl = (*env)->GetPrimitiveArrayCritical(env, payload, NULL);
-    jint* o = (jint*)(*env)->GetPrimitiveArrayCritical(env, out, NULL);
+    jint* o = pl ? (jint*)(*env)->GetPrimitiveArrayCritical(env, out, NULL) : NULL;
+    if (pin_failed(env, pl, o)) {
+        if (pl) (*env)->ReleasePrimitiveArrayCritical(env, payload, pl, JNI_ABORT);
+        return;
+    }
     int st = skml_dense_bins_host(pl, (size_t)len, (int32_t*)o, n);
     (*env)->ReleasePrimitiveArrayCritical(env, out, o, 0);
     (*env)->ReleasePrimitiveArrayCritical(env, payload, pl, JNI_ABORT);
@@ -159,6 +190,10 @@ JNIEXPORT jdoubleArray JNICALL Java_org_dma_sketchml_hip_HipCodec_info(JNIEnv* e
     double* sp = (double*)malloc(sizeof(double) * SKML_MAX_BINS);
     if (!sp) return NULL;
     void* pl = (*env)->GetPrimitiveArrayCritical(env, payload, NULL);
+    if (pin_failed(env, pl, pl)) {
+        free(sp);
+        return NULL;
+    }
     int st = skml_dense_info_host(pl, (size_t)len, &h, sp, SKML_MAX_BINS);
     (*env)->ReleasePrimitiveArrayCritical(env, payload, pl, JNI_ABORT);
     jdoubleArray out = NULL;
@@ -182,24 +217,31 @@ JNIEXPORT void JNICALL Java_org_dma_sketchml_hip_HipCodec_timesBy(JNIEnv* env, j
     (void)cls;
     const jsize len = (*env)->GetArrayLength(env, payload);
     void* pl = (*env)->GetPrimitiveArrayCritical(env, payload, NULL);
+    if (pin_failed(env, pl, pl)) return;
     int st = skml_dense_times_by_host(pl, (size_t)len, x);
     (*env)->ReleasePrimitiveArrayCritical(env, payload, pl, 0);
     throw_status(env, st);
 }
 
 /* ---------------------------------------------------------------- sparse: GroupedMinMaxSketch */
-/* long encodeSparse(long ctx, int[] keys, float[] vals, int binNum, int groupNum, int rowNum,
- *                   double colRatio, long seed, long hashSeed, boolean uniform, int parallelism) */
+static void throw_class(JNIEnv* env, const char* cls, const char* msg) {
+    jclass k = (*env)->FindClass(env, cls);
+    if (k) (*env)->ThrowNew(env, k, msg);
+}
+
+/* long encodeSparse(long ctx, int[] keys, double[] vals, int binNum, int groupNum, int rowNum,
+ *                   double colRatio, long seed, long hashSeed, boolean uniform, int parallelism):
+ * the reference's double values themselves (skml_sparse_encode_kv_host_f64: the quantizer sketches
+ * and bins the doubles, SparseVectorCompressor.java:52-67, SketchGradient.scala:35-48). */
 JNIEXPORT jlong JNICALL Java_org_dma_sketchml_hip_HipCodec_encodeSparse(JNIEnv* env, jclass cls, jlong ctx,
-                                                                      jintArray keys, jfloatArray vals, jint bins,
+                                                                      jintArray keys, jdoubleArray vals, jint bins,
                                                                       jint groups, jint rows, jdouble ratio,
                                                                       jlong seed, jlong hash_seed,
                                                                       jboolean uniform, jint parallelism) {
     (void)cls;
     const jsize n = (*env)->GetArrayLength(env, keys);
     if ((*env)->GetArrayLength(env, vals) != n) {
-        jclass k = (*env)->FindClass(env, CLS_SKETCHML);
-        if (k) (*env)->ThrowNew(env, k, "Lengths of key array and value array do not match");
+        throw_class(env, CLS_SKETCHML, "Lengths of key array and value array do not match");
         return 0;
     }
     skml_params p;
@@ -211,21 +253,37 @@ JNIEXPORT jlong JNICALL Java_org_dma_sketchml_hip_HipCodec_encodeSparse(JNIEnv* 
     p.quant_type = uniform ? SKML_UNIFORM : SKML_QUANTILE;
     skml_sparse* s = NULL;
     jint* k = (jint*)(*env)->GetPrimitiveArrayCritical(env, keys, NULL);
-    float* v = (float*)(*env)->GetPrimitiveArrayCritical(env, vals, NULL);
-    int st = skml_sparse_encode_kv_host_f32(CTX(ctx), (const int32_t*)k, v, n, &p, &s);
+    double* v = k ? (double*)(*env)->GetPrimitiveArrayCritical(env, vals, NULL) : NULL;
+    if (pin_failed(env, k, v)) {
+        if (k) (*env)->ReleasePrimitiveArrayCritical(env, keys, k, JNI_ABORT);
+        return 0;
+    }
+    int st = skml_sparse_encode_kv_host_f64(CTX(ctx), (const int32_t*)k, v, n, &p, &s);
     (*env)->ReleasePrimitiveArrayCritical(env, vals, v, JNI_ABORT);
     (*env)->ReleasePrimitiveArrayCritical(env, keys, k, JNI_ABORT);
     if (throw_status(env, st)) return 0;
     return (jlong)(uintptr_t)s;
 }
 
-/* void decodeSparse(long ctx, long sparse, int[] keys, float[] vals): restore + value lookup */
+/* void decodeSparse(long ctx, long sparse, int[] keys, double[] vals): restore + Sort.merge +
+ * quantValues[bin] in double (SparseVectorCompressor.decompressSparse, :118-126).  Both arrays must
+ * hold the payload's nnz entries (skml_sparse_nnz): checked before anything is written. */
 JNIEXPORT void JNICALL Java_org_dma_sketchml_hip_HipCodec_decodeSparse(JNIEnv* env, jclass cls, jlong ctx,
-                                                                     jlong sp, jintArray keys, jfloatArray vals) {
+                                                                     jlong sp, jintArray keys, jdoubleArray vals) {
     (void)cls;
+    int64_t nnz = 0;
+    if (throw_status(env, skml_sparse_nnz((const skml_sparse*)(uintptr_t)sp, &nnz))) return;
+    if ((int64_t)(*env)->GetArrayLength(env, keys) < nnz || (int64_t)(*env)->GetArrayLength(env, vals) < nnz) {
+        throw_class(env, CLS_SKETCHML, "decodeSparse: key / value arrays shorter than the payload's nnz");
+        return;
+    }
     jint* k = (jint*)(*env)->GetPrimitiveArrayCritical(env, keys, NULL);
-    float* v = (float*)(*env)->GetPrimitiveArrayCritical(env, vals, NULL);
-    int st = skml_sparse_decode_host_f32(CTX(ctx), (const skml_sparse*)(uintptr_t)sp, (int32_t*)k, v);
+    double* v = k ? (double*)(*env)->GetPrimitiveArrayCritical(env, vals, NULL) : NULL;
+    if (pin_failed(env, k, v)) {
+        if (k) (*env)->ReleasePrimitiveArrayCritical(env, keys, k, JNI_ABORT);
+        return;
+    }
+    int st = skml_sparse_decode_host_f64(CTX(ctx), (const skml_sparse*)(uintptr_t)sp, (int32_t*)k, v);
     (*env)->ReleasePrimitiveArrayCritical(env, vals, v, 0);
     (*env)->ReleasePrimitiveArrayCritical(env, keys, k, 0);
     throw_status(env, st);
@@ -286,7 +344,11 @@ JNIEXPORT jlong JNICALL Java_org_dma_sketchml_hip_HipCodec_readSparse(JNIEnv* en
     const jsize nq = qv ? (*env)->GetArrayLength(env, qv) : 0;
     skml_sparse* s = NULL;
     void* d = (*env)->GetPrimitiveArrayCritical(env, data, NULL);
-    double* q = qv ? (double*)(*env)->GetPrimitiveArrayCritical(env, qv, NULL) : NULL;
+    double* q = (d && qv) ? (double*)(*env)->GetPrimitiveArrayCritical(env, qv, NULL) : NULL;
+    if (pin_failed(env, d, qv ? (const void*)q : d)) {
+        if (d) (*env)->ReleasePrimitiveArrayCritical(env, data, d, JNI_ABORT);
+        return 0;
+    }
     int st = skml_sparse_deserialize(CTX(ctx), (const uint8_t*)d, (size_t)len, q, nq, &s);
     if (q) (*env)->ReleasePrimitiveArrayCritical(env, qv, q, JNI_ABORT);
     (*env)->ReleasePrimitiveArrayCritical(env, data, d, JNI_ABORT);
@@ -319,6 +381,11 @@ JNIEXPORT jlongArray JNICALL Java_org_dma_sketchml_hip_HipCodec_deltaEncode(JNIE
     int32_t m = 0, kind = 0;
     int64_t nfb = 0, ndb = 0;
     jint* k = (jint*)(*env)->GetPrimitiveArrayCritical(env, keys, NULL);
+    if (pin_failed(env, k, k)) {
+        free(fw);
+        free(dw);
+        return NULL;
+    }
     int st = skml_delta_encode_host(CTX(ctx), (const int32_t*)k, n, &m, &kind, &nfb, &ndb, fw, dw, cap);
     (*env)->ReleasePrimitiveArrayCritical(env, keys, k, JNI_ABORT);
     jlongArray out = NULL;
@@ -350,8 +417,13 @@ JNIEXPORT jintArray JNICALL Java_org_dma_sketchml_hip_HipCodec_deltaDecode(JNIEn
     jintArray out = (*env)->NewIntArray(env, size);
     if (!out || size <= 0) return out;
     jlong* f = (jlong*)(*env)->GetPrimitiveArrayCritical(env, flags, NULL);
-    jlong* d = (jlong*)(*env)->GetPrimitiveArrayCritical(env, deltas, NULL);
-    jint* o = (jint*)(*env)->GetPrimitiveArrayCritical(env, out, NULL);
+    jlong* d = f ? (jlong*)(*env)->GetPrimitiveArrayCritical(env, deltas, NULL) : NULL;
+    jint* o = d ? (jint*)(*env)->GetPrimitiveArrayCritical(env, out, NULL) : NULL;
+    if (pin_failed(env, f, d) || pin_failed(env, o, o)) {
+        if (d) (*env)->ReleasePrimitiveArrayCritical(env, deltas, d, JNI_ABORT);
+        if (f) (*env)->ReleasePrimitiveArrayCritical(env, flags, f, JNI_ABORT);
+        return NULL;
+    }
     int st = skml_delta_decode_host(CTX(ctx), size, m, kind ? 1 : 0, (const uint64_t*)f, nf, (const uint64_t*)d, nd,
                                     (int32_t*)o);
     (*env)->ReleasePrimitiveArrayCritical(env, out, o, 0);

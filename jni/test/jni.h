@@ -53,5 +53,6 @@ struct JNINativeInterface_ {
     void (*SetDoubleArrayRegion)(JNIEnv* env, jdoubleArray array, jsize start, jsize len, const jdouble* buf);
     void* (*GetPrimitiveArrayCritical)(JNIEnv* env, jarray array, jboolean* isCopy);
     void (*ReleasePrimitiveArrayCritical)(JNIEnv* env, jarray array, void* carray, jint mode);
+    jboolean (*ExceptionCheck)(JNIEnv* env);
 };
 #endif

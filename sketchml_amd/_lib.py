@@ -107,13 +107,19 @@ _SIGS = {
     "skml_dense_bins_host": (C.c_int, [vp, C.c_size_t, vp, i64]),
     "skml_dense_times_by_host": (C.c_int, [vp, C.c_size_t, C.c_double]),
     "skml_sparse_encode_kv_host_f32": (C.c_int, [vp, vp, vp, i64, C.POINTER(Params), C.POINTER(vp)]),
+    "skml_sparse_encode_kv_host_f64": (C.c_int, [vp, vp, vp, i64, C.POINTER(Params), C.POINTER(vp)]),
     "skml_sparse_decode_host_f32": (C.c_int, [vp, vp, vp, vp]),
+    "skml_sparse_decode_host_f64": (C.c_int, [vp, vp, vp, vp]),
     "skml_delta_encode_host": (C.c_int, [vp, vp, i64, i32p, i32p, i64p, i64p, vp, vp, i64]),
     "skml_delta_decode_host": (C.c_int, [vp, i64, i32, i32, vp, i64, vp, i64, vp]),
     "skml_sparse_compact_f32": (C.c_int, [vp, vp, i64, vp, vp, i64p]),
+    "skml_sparse_compact_f64": (C.c_int, [vp, vp, i64, vp, vp, i64p]),
     "skml_sparse_encode_kv_f32": (C.c_int, [vp, vp, vp, i64, C.POINTER(Params), C.POINTER(vp)]),
+    "skml_sparse_encode_kv_f64": (C.c_int, [vp, vp, vp, i64, C.POINTER(Params), C.POINTER(vp)]),
     "skml_sparse_encode_f32": (C.c_int, [vp, vp, i64, C.POINTER(Params), C.POINTER(vp)]),
+    "skml_sparse_encode_f64": (C.c_int, [vp, vp, i64, C.POINTER(Params), C.POINTER(vp)]),
     "skml_sparse_decode_f32": (C.c_int, [vp, vp, vp, vp]),
+    "skml_sparse_decode_f64": (C.c_int, [vp, vp, vp, vp]),
     "skml_sparse_nnz": (C.c_int, [vp, i64p]),
     "skml_sparse_times_by": (C.c_int, [vp, C.c_double]),
     "skml_sparse_values": (C.c_int, [vp, dblp, i32]),

@@ -1738,19 +1738,46 @@ int skml_sparse_encode_kv_host_f32(skml_ctx* c, const int32_t* keys, const float
     return skml_sparse_encode_kv_f32(c, (const int32_t*)c->hk, (const float*)c->hx, nnz, p, out);
 }
 
-int skml_sparse_decode_host_f32(skml_ctx* c, const skml_sparse* s, int32_t* keys, float* vals) {
+int skml_sparse_encode_kv_host_f64(skml_ctx* c, const int32_t* keys, const double* vals, int64_t nnz,
+                                   const skml_params* p, skml_sparse** out) {
+    if (!c || !out || nnz < 0 || (nnz > 0 && (!keys || !vals))) return fail(SKML_E_ARG, "bad arguments");
+    HIP_TRY(hipSetDevice(c->device));
+    int st;
+    if ((st = ensure_host_path(c))) return st;
+    if ((st = ensure_dev_buf(&c->hx, &c->hx_cap, std::max<size_t>(16, 8 * (size_t)nnz), c->stream))) return st;
+    if ((st = ensure_dev_buf(&c->hk, &c->hk_cap, std::max<size_t>(16, 4 * (size_t)nnz), c->stream))) return st;
+    if ((st = upload(c, c->hk, keys, 4 * (size_t)nnz))) return st;
+    if ((st = upload(c, c->hx, vals, 8 * (size_t)nnz))) return st;
+    return skml_sparse_encode_kv_f64(c, (const int32_t*)c->hk, (const double*)c->hx, nnz, p, out);
+}
+
+}  // extern "C"
+
+namespace {
+template <typename T, typename Dec>
+int sparse_decode_host(skml_ctx* c, const skml_sparse* s, int32_t* keys, T* vals, Dec dec) {
     int64_t n = 0;
     if (!c || !s || skml_sparse_nnz(s, &n)) return fail(SKML_E_ARG, "bad arguments");
     if (n > 0 && (!keys || !vals)) return fail(SKML_E_ARG, "keys/vals are NULL");
     HIP_TRY(hipSetDevice(c->device));
     int st;
-    const size_t bytes = std::max<size_t>(16, 4 * (size_t)n);
     if ((st = ensure_host_path(c))) return st;
-    if ((st = ensure_dev_buf(&c->hx, &c->hx_cap, bytes, c->stream))) return st;
-    if ((st = ensure_dev_buf(&c->hk, &c->hk_cap, bytes, c->stream))) return st;
-    if ((st = skml_sparse_decode_f32(c, s, (int32_t*)c->hk, (float*)c->hx))) return st;
+    if ((st = ensure_dev_buf(&c->hx, &c->hx_cap, std::max<size_t>(16, sizeof(T) * (size_t)n), c->stream))) return st;
+    if ((st = ensure_dev_buf(&c->hk, &c->hk_cap, std::max<size_t>(16, 4 * (size_t)n), c->stream))) return st;
+    if ((st = dec(c, s, (int32_t*)c->hk, (T*)c->hx))) return st;
     if ((st = download(c, keys, c->hk, 4 * (size_t)n))) return st;
-    return download(c, vals, c->hx, 4 * (size_t)n);
+    return download(c, vals, c->hx, sizeof(T) * (size_t)n);
+}
+}  // namespace
+
+extern "C" {
+
+int skml_sparse_decode_host_f32(skml_ctx* c, const skml_sparse* s, int32_t* keys, float* vals) {
+    return sparse_decode_host<float>(c, s, keys, vals, skml_sparse_decode_f32);
+}
+
+int skml_sparse_decode_host_f64(skml_ctx* c, const skml_sparse* s, int32_t* keys, double* vals) {
+    return sparse_decode_host<double>(c, s, keys, vals, skml_sparse_decode_f64);
 }
 
 int skml_delta_encode_host(skml_ctx* c, const int32_t* keys, int64_t n, int32_t* num_intervals, int32_t* flag_kind,

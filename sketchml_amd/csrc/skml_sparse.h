@@ -68,6 +68,9 @@ hipError_t launch_sp_zero_edges(hipStream_t st, const uint64_t* tile_base, int64
 // DenseDoubleGradient.toSparse: keys/vals of |x| > 1e-8 in index order.  status/ticket zeroed.
 hipError_t launch_compact(hipStream_t st, const float* x, int64_t dim, int32_t* keys, float* vals,
                           uint64_t* status, unsigned* ticket, int64_t* nnz_out);
+// the same over doubles (DenseDoubleGradient's own values); tiles of kCompactTile / 2
+hipError_t launch_compact64(hipStream_t st, const double* x, int64_t dim, int32_t* keys, double* vals,
+                            uint64_t* status, unsigned* ticket, int64_t* nnz_out);
 // Exclusive scan, in place, of each of K columns of a [tiles][K] u64 table; totals -> row `tiles`.
 hipError_t launch_scan_cols(hipStream_t st, uint64_t* sums, int64_t tiles, int K);
 // The same over K columns of tiles + 1 entries each, column k at sums + k * (tiles + 1).
@@ -130,6 +133,8 @@ hipError_t launch_merge_round(hipStream_t st, const int32_t* kin, const int32_t*
 // values[bins[i]] from the double quantValues LUT (SparseVectorCompressor.java:118-126).
 hipError_t launch_bin_values(hipStream_t st, const int32_t* bins, int64_t n, const double* qvalues, int B,
                              float* vals);
+hipError_t launch_bin_values64(hipStream_t st, const int32_t* bins, int64_t n, const double* qvalues, int B,
+                               double* vals);
 
 // HuffmanEncoder of the MinMaxSketch tables (serialisation): per-group histograms [G][B+1]
 // (symbol B = the fill value), code lengths per tile, and the MSB-first code stream writer

@@ -182,86 +182,112 @@ __device__ __forceinline__ int32_t mm_dist(int32_t v, int32_t zero) {
 // =============================================================================================
 // Compaction (decoupled look-back)
 // =============================================================================================
-// Each workgroup compacts one tile of kCompactTile = 16,384 values, all of it held in registers
-// (16 float4 per thread, slab j of the tile = float4 j * 256 + t), so a tile keeps 64 KiB of loads
-// in flight and takes one look-back.  Ranks follow index order: slab by slab, and within a slab
+// Each workgroup compacts one tile of values, all of it held in registers (fp32: 16,384 values,
+// 16 float4 per thread, slab j of the tile = float4 j * 256 + t; fp64: 8,192 values, two double2
+// per slab), so a tile keeps 64 KiB of loads in flight and takes one look-back.  Ranks follow index order: slab by slab, and within a slab
 // by float4, from wave-level scans of 16-bit packed per-slab counts plus the waves' slab totals.
-constexpr int kCompactSlabs = kCompactTile / (4 * kSpThreads);
-constexpr int kCompactStage = 4096;  // kept elements staged in LDS (32 KB); denser tiles store directly
+constexpr int kCompactStage = 4096;  // kept elements staged in LDS; denser tiles store directly
 
-__global__ __launch_bounds__(kSpThreads) void k_compact(const float* __restrict__ x, int64_t dim,
-                                                        int32_t* __restrict__ keys, float* __restrict__ vals,
+// Element traits: fp32 tiles of 16,384 (64 per thread, 16 float4 slabs), fp64 tiles of 8,192 (32
+// per thread, 8 slabs of two double2): 64 KiB of loads in flight per tile either way.
+template <typename T> struct CompactT;
+template <> struct CompactT<float> {
+    static constexpr int kTile = kCompactTile;
+    typedef float v2 __attribute__((ext_vector_type(4)));  // one slab = one 16-byte load
+    // Maths.scala:8 EPS: |x| > 1e-8 in double; for a float x that is |x| > RD_f32(1e-8) on the
+    // magnitude bits, NaN excluded (abs bits above +inf's).
+    static __device__ __forceinline__ bool keep(float v) {
+        const uint32_t a = __float_as_uint(v) & 0x7FFFFFFFu;
+        return a > kEpsBelowBits && a <= 0x7F800000u;
+    }
+};
+template <> struct CompactT<double> {
+    static constexpr int kTile = kCompactTile / 2;
+    typedef double v2 __attribute__((ext_vector_type(2)));  // one slab = two 16-byte loads
+    static __device__ __forceinline__ bool keep(double v) {  // |x| > 1e-8, NaN excluded
+        const uint64_t a = (uint64_t)__double_as_longlong(v) & 0x7FFFFFFFFFFFFFFFull;
+        return a > 0x3E45798EE2308C3Aull && a <= 0x7FF0000000000000ull;
+    }
+};
+template <typename T>
+constexpr int compact_tile() { return CompactT<T>::kTile; }
+
+template <typename T>
+__global__ __launch_bounds__(kSpThreads) void k_compact(const T* __restrict__ x, int64_t dim,
+                                                        int32_t* __restrict__ keys, T* __restrict__ vals,
                                                         uint64_t* status, unsigned* ticket, int64_t ntiles,
                                                         int64_t* nnz_out) {
-    __shared__ uint32_t wtot[kSpThreads / 64][kCompactSlabs];  // per-wave kept counts of each slab
+    constexpr int kTile = CompactT<T>::kTile;
+    constexpr int kSlabs = kTile / (4 * kSpThreads);  // 4 elements per thread per slab
+    static_assert(kSlabs % 4 == 0 && kSlabs <= 16, "16-bit slab counts, 4 per u64, 64-bit keep mask");
+    typedef typename CompactT<T>::v2 vec;
+    __shared__ uint32_t wtot[kSpThreads / 64][kSlabs];  // per-wave kept counts of each slab
     __shared__ int64_t s_tile;
     __shared__ uint64_t s_excl;
     __shared__ int32_t stage_k[kCompactStage];
-    __shared__ float stage_v[kCompactStage];
+    __shared__ T stage_v[kCompactStage];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     if (t == 0) s_tile = (int64_t)atomicAdd(ticket, 1u);
     __syncthreads();
     const int64_t tile = s_tile;
-    const int64_t base = tile * kCompactTile;
+    const int64_t base = tile * kTile;
     const int64_t lim = dim - base;
-    typedef float f32x4 __attribute__((ext_vector_type(4)));
-    f32x4 f[kCompactSlabs];
-    if (lim >= kCompactTile && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
-        const f32x4* src = reinterpret_cast<const f32x4*>(x + base);
+    T f[kSlabs][4];  // slab j of the tile = elements 4 * (j * 256 + t) .. + 3
+    if (lim >= kTile && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+        const vec* src = reinterpret_cast<const vec*>(x + base);
+        constexpr int kVec = 4 / (16 / (int)sizeof(T) >= 4 ? 4 : 16 / (int)sizeof(T));  // loads per slab
+        constexpr int kPer = 4 / kVec;                                                 // elements per load
 #pragma unroll
-        for (int j = 0; j < kCompactSlabs; j++) f[j] = __builtin_nontemporal_load(src + j * kSpThreads + t);
+        for (int j = 0; j < kSlabs; j++)
+#pragma unroll
+            for (int u = 0; u < kVec; u++) {
+                const vec v = __builtin_nontemporal_load(src + ((int64_t)j * kSpThreads + t) * kVec + u);
+#pragma unroll
+                for (int e = 0; e < kPer; e++) f[j][u * kPer + e] = v[e];
+            }
     } else {
 #pragma unroll
-        for (int j = 0; j < kCompactSlabs; j++) {
-            const int64_t e = 4 * ((int64_t)j * kSpThreads + t);
-            f[j].x = e < lim ? x[base + e] : 0.0f;
-            f[j].y = e + 1 < lim ? x[base + e + 1] : 0.0f;
-            f[j].z = e + 2 < lim ? x[base + e + 2] : 0.0f;
-            f[j].w = e + 3 < lim ? x[base + e + 3] : 0.0f;
+        for (int j = 0; j < kSlabs; j++) {
+            const int64_t e0 = 4 * ((int64_t)j * kSpThreads + t);
+#pragma unroll
+            for (int e = 0; e < 4; e++) f[j][e] = e0 + e < lim ? x[base + e0 + e] : (T)0;
         }
     }
-    // Maths.scala:8 EPS: |x| > 1e-8 in double.  For a float x that is |x| > RD_f32(1e-8) on the
-    // magnitude bits, NaN excluded (abs bits above +inf's).
     uint64_t keep = 0;
 #pragma unroll
-    for (int j = 0; j < kCompactSlabs; j++) {
-        const float e4[4] = {f[j].x, f[j].y, f[j].z, f[j].w};
+    for (int j = 0; j < kSlabs; j++)
 #pragma unroll
-        for (int e = 0; e < 4; e++) {
-            const uint32_t a = __float_as_uint(e4[e]) & 0x7FFFFFFFu;
-            keep |= (a > kEpsBelowBits && a <= 0x7F800000u) ? (1ull << (4 * j + e)) : 0ull;
-        }
-    }
+        for (int e = 0; e < 4; e++) keep |= CompactT<T>::keep(f[j][e]) ? (1ull << (4 * j + e)) : 0ull;
     // wave-inclusive scans of the per-slab counts, four 16-bit lanes per u64
-    uint64_t P[kCompactSlabs / 4];
+    uint64_t P[kSlabs / 4];
 #pragma unroll
-    for (int k = 0; k < kCompactSlabs / 4; k++) {
+    for (int k = 0; k < kSlabs / 4; k++) {
         uint64_t v = 0;
 #pragma unroll
         for (int q = 0; q < 4; q++) v |= (uint64_t)__popcll((keep >> (16 * k + 4 * q)) & 15ull) << (16 * q);
         P[k] = v;
     }
-    uint64_t own[kCompactSlabs / 4];
+    uint64_t own[kSlabs / 4];
 #pragma unroll
-    for (int k = 0; k < kCompactSlabs / 4; k++) own[k] = P[k];
+    for (int k = 0; k < kSlabs / 4; k++) own[k] = P[k];
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
 #pragma unroll
-        for (int k = 0; k < kCompactSlabs / 4; k++) {
+        for (int k = 0; k < kSlabs / 4; k++) {
             const uint64_t y = __shfl_up(P[k], off, 64);
             if (lane >= off) P[k] += y;
         }
     }
     if (lane == 63) {
 #pragma unroll
-        for (int j = 0; j < kCompactSlabs; j++) wtot[w][j] = (uint32_t)(P[j >> 2] >> (16 * (j & 3))) & 0xFFFFu;
+        for (int j = 0; j < kSlabs; j++) wtot[w][j] = (uint32_t)(P[j >> 2] >> (16 * (j & 3))) & 0xFFFFu;
     }
     __syncthreads();
     // slab totals, this wave's offset inside each slab, and the tile total
-    uint32_t slab_pre[kCompactSlabs];
+    uint32_t slab_pre[kSlabs];
     uint32_t tile_total = 0;
 #pragma unroll
-    for (int j = 0; j < kCompactSlabs; j++) {
+    for (int j = 0; j < kSlabs; j++) {
         uint32_t before = 0, tot = 0;
 #pragma unroll
         for (int u = 0; u < kSpThreads / 64; u++) {
@@ -306,17 +332,16 @@ __global__ __launch_bounds__(kSpThreads) void k_compact(const float* __restrict_
     const int64_t out0 = (int64_t)s_excl;
     if (tile_total <= (uint32_t)kCompactStage) {  // the tile's output through LDS: coalesced stores
 #pragma unroll
-        for (int j = 0; j < kCompactSlabs; j++) {
+        for (int j = 0; j < kSlabs; j++) {
             const uint32_t incl = (uint32_t)(P[j >> 2] >> (16 * (j & 3))) & 0xFFFFu;
             const uint32_t mine = (uint32_t)(own[j >> 2] >> (16 * (j & 3))) & 0xFFFFu;
             uint32_t pos = slab_pre[j] + incl - mine;
             const int32_t e0 = (int32_t)(base + 4 * ((int64_t)j * kSpThreads + t));
-            const float e4[4] = {f[j].x, f[j].y, f[j].z, f[j].w};
 #pragma unroll
             for (int e = 0; e < 4; e++)
                 if ((keep >> (4 * j + e)) & 1ull) {
                     stage_k[pos] = e0 + e;
-                    stage_v[pos] = e4[e];
+                    stage_v[pos] = f[j][e];
                     pos++;
                 }
         }
@@ -328,29 +353,37 @@ __global__ __launch_bounds__(kSpThreads) void k_compact(const float* __restrict_
         return;
     }
 #pragma unroll
-    for (int j = 0; j < kCompactSlabs; j++) {
+    for (int j = 0; j < kSlabs; j++) {
         const uint64_t incl = (P[j >> 2] >> (16 * (j & 3))) & 0xFFFFull;
         const uint64_t mine = (own[j >> 2] >> (16 * (j & 3))) & 0xFFFFull;
         int64_t pos = out0 + slab_pre[j] + (int64_t)(incl - mine);
         const int32_t e0 = (int32_t)(base + 4 * ((int64_t)j * kSpThreads + t));
-        const float e4[4] = {f[j].x, f[j].y, f[j].z, f[j].w};
 #pragma unroll
         for (int e = 0; e < 4; e++)
             if ((keep >> (4 * j + e)) & 1ull) {
                 keys[pos] = e0 + e;
-                vals[pos] = e4[e];
+                vals[pos] = f[j][e];
                 pos++;
             }
     }
 }
 
-hipError_t launch_compact(hipStream_t st, const float* x, int64_t dim, int32_t* keys, float* vals,
-                          uint64_t* status, unsigned* ticket, int64_t* nnz_out) {
-    const int64_t tiles = sp_tiles(dim, kCompactTile);
+template <typename T>
+hipError_t launch_compact_t(hipStream_t st, const T* x, int64_t dim, int32_t* keys, T* vals, uint64_t* status,
+                            unsigned* ticket, int64_t* nnz_out) {
+    const int64_t tiles = sp_tiles(dim, compact_tile<T>());
     if (tiles <= 0) return hipMemsetAsync(nnz_out, 0, sizeof(int64_t), st);
-    hipLaunchKernelGGL(k_compact, dim3((unsigned)tiles), dim3(kSpThreads), 0, st, x, dim, keys, vals, status,
+    hipLaunchKernelGGL(k_compact<T>, dim3((unsigned)tiles), dim3(kSpThreads), 0, st, x, dim, keys, vals, status,
                        ticket, tiles, nnz_out);
     return hipGetLastError();
+}
+hipError_t launch_compact(hipStream_t st, const float* x, int64_t dim, int32_t* keys, float* vals,
+                          uint64_t* status, unsigned* ticket, int64_t* nnz_out) {
+    return launch_compact_t<float>(st, x, dim, keys, vals, status, ticket, nnz_out);
+}
+hipError_t launch_compact64(hipStream_t st, const double* x, int64_t dim, int32_t* keys, double* vals,
+                            uint64_t* status, unsigned* ticket, int64_t* nnz_out) {
+    return launch_compact_t<double>(st, x, dim, keys, vals, status, ticket, nnz_out);
 }
 
 // =============================================================================================
@@ -1947,28 +1980,37 @@ hipError_t launch_merge_round(hipStream_t st, const int32_t* kin, const int32_t*
 }
 
 // values[bins[i]] (SparseVectorCompressor.java:118-126) from the double quantValues LUT
-// (Quantizer.getValues, times any timesBy factors), returned as fp32.
+// (Quantizer.getValues, times any timesBy factors): as fp32, or the doubles themselves.
+template <typename T>
 __global__ __launch_bounds__(kSpThreads) void k_bin_values(const int32_t* __restrict__ bins, int64_t n,
                                                            const double* __restrict__ qv, int B,
-                                                           float* __restrict__ vals) {
-    __shared__ float lut[4096];
+                                                           T* __restrict__ vals) {
+    __shared__ T lut[4096];
     const bool lds = B <= 4096;
     if (lds) {
-        for (int b = threadIdx.x; b < B; b += kSpThreads) lut[b] = (float)qv[b];
+        for (int b = threadIdx.x; b < B; b += kSpThreads) lut[b] = (T)qv[b];
         __syncthreads();
     }
     for (int64_t i = (int64_t)blockIdx.x * kSpThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kSpThreads) {
         const int b = bins[i];
-        vals[i] = lds ? lut[b] : (float)qv[b];
+        vals[i] = lds ? lut[b] : (T)qv[b];
     }
 }
 
-hipError_t launch_bin_values(hipStream_t st, const int32_t* bins, int64_t n, const double* qvalues, int B,
-                             float* vals) {
+template <typename T>
+hipError_t launch_bin_values_t(hipStream_t st, const int32_t* bins, int64_t n, const double* qvalues, int B, T* vals) {
     if (n <= 0) return hipSuccess;
     const int64_t grid = std::min<int64_t>(sp_tiles(n, kSpThreads * 4), 4096);
-    hipLaunchKernelGGL(k_bin_values, dim3((unsigned)grid), dim3(kSpThreads), 0, st, bins, n, qvalues, B, vals);
+    hipLaunchKernelGGL(k_bin_values<T>, dim3((unsigned)grid), dim3(kSpThreads), 0, st, bins, n, qvalues, B, vals);
     return hipGetLastError();
+}
+hipError_t launch_bin_values(hipStream_t st, const int32_t* bins, int64_t n, const double* qvalues, int B,
+                             float* vals) {
+    return launch_bin_values_t<float>(st, bins, n, qvalues, B, vals);
+}
+hipError_t launch_bin_values64(hipStream_t st, const int32_t* bins, int64_t n, const double* qvalues, int B,
+                               double* vals) {
+    return launch_bin_values_t<double>(st, bins, n, qvalues, B, vals);
 }
 
 // =============================================================================================

@@ -409,7 +409,9 @@ int check_params(const skml_params* p) {
 // GroupedMinMaxSketch.insert (frequency/GroupedMinMaxSketch.java:51-121).  Everything is queued
 // on the stream without a host round trip -- the per-group decisions are made on the device
 // (k_sp_plan_*) -- and the host reads the quantizer header, splits and group table back once.
-int encode_kv(skml_ctx* c, const int32_t* keys, const float* vals, int64_t nnz, const skml_params* p,
+// vals: nnz floats, or nnz doubles when f64 (the reference's own double[] values: the quantizer
+// sketches and bins the doubles themselves, QuantileQuantizer.quantize(double[])).
+int encode_kv(skml_ctx* c, const int32_t* keys, const void* vals, bool f64, int64_t nnz, const skml_params* p,
               skml_sparse** out) {
     hipStream_t st = ctx_stream(c);
     skml_sparse* s = new skml_sparse();
@@ -450,12 +452,19 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const float* vals, int64_t nnz, 
     s->delta_words = reinterpret_cast<uint64_t*>(blk + o_dw);
     // ---- 1. the values' quantizer (Quantizer.newQuantizer(quantType), SparseVectorCompressor.java:60-62) ----
     skml_params qp = *p;
-    if (int e = p->quant_type == SKML_UNIFORM
-                    ? skml_dense_encode_uniform_f32(c, vals, nnz, &qp, s->qpayload, s->qbytes)
-                    : (p->parallelism > 1 ? skml_dense_encode_parallel_f32(c, vals, nnz, p->parallelism, &qp,
-                                                                            s->qpayload, s->qbytes)
-                                          : skml_dense_encode_f32(c, vals, nnz, &qp, s->qpayload, s->qbytes)))
-        return bail(e);
+    int qe;
+    if (f64) {
+        const double* v = static_cast<const double*>(vals);
+        qe = p->quant_type == SKML_UNIFORM ? skml_dense_encode_uniform_f64(c, v, nnz, &qp, s->qpayload, s->qbytes)
+             : p->parallelism > 1 ? skml_dense_encode_parallel_f64(c, v, nnz, p->parallelism, &qp, s->qpayload, s->qbytes)
+                                  : skml_dense_encode_f64(c, v, nnz, &qp, s->qpayload, s->qbytes);
+    } else {
+        const float* v = static_cast<const float*>(vals);
+        qe = p->quant_type == SKML_UNIFORM ? skml_dense_encode_uniform_f32(c, v, nnz, &qp, s->qpayload, s->qbytes)
+             : p->parallelism > 1 ? skml_dense_encode_parallel_f32(c, v, nnz, p->parallelism, &qp, s->qpayload, s->qbytes)
+                                  : skml_dense_encode_f32(c, v, nnz, &qp, s->qpayload, s->qbytes);
+    }
+    if (qe) return bail(qe);
     // ---- 2. group edges (device), partition counts, per-group MinMaxSketch shapes ----
     SpInit init{};
     init.G = G;
@@ -628,21 +637,38 @@ int merge_groups(skml_ctx* c, const skml_sparse* s, int32_t* gk, int32_t* gb, in
 
 extern "C" {
 
-int skml_sparse_compact_f32(skml_ctx* c, const float* dense, int64_t dim, int32_t* keys, float* vals,
-                            int64_t* nnz_out) {
+}  // extern "C"
+
+namespace {
+template <typename T>
+int compact_any(skml_ctx* c, const T* dense, int64_t dim, int32_t* keys, T* vals, int64_t* nnz_out) {
     if (!c || !nnz_out || dim < 0 || (dim > 0 && (!dense || !keys || !vals)))
         return sfail(SKML_E_ARG, "bad compaction arguments");
     if (dim > (int64_t)INT32_MAX) return sfail(SKML_E_ARG, "dim %lld exceeds Java int keys", (long long)dim);
     SP_HIP(hipSetDevice(ctx_device(c)));
     hipStream_t st = ctx_stream(c);
-    const int64_t tiles = sp_tiles(dim, kCompactTile);
+    const int64_t tiles = sp_tiles(dim, sizeof(T) == 8 ? kCompactTile / 2 : kCompactTile);
     uint64_t* status = scratch<uint64_t>(c, kSlotStatus, (size_t)tiles + 8);
     if (!status) return sfail(SKML_E_OOM, "compaction status");
     unsigned* ticket = reinterpret_cast<unsigned*>(status + tiles);
     int64_t* nnz_dev = reinterpret_cast<int64_t*>(status + tiles + 1);
     SP_HIP(hipMemsetAsync(status, 0, sizeof(uint64_t) * ((size_t)tiles + 8), st));
-    SP_HIP(launch_compact(st, dense, dim, keys, vals, status, ticket, nnz_dev));
+    if constexpr (sizeof(T) == 8) SP_HIP(launch_compact64(st, dense, dim, keys, vals, status, ticket, nnz_dev));
+    else SP_HIP(launch_compact(st, dense, dim, keys, vals, status, ticket, nnz_dev));
     return sync_to_host(c, nnz_out, nnz_dev, sizeof(int64_t));
+}
+}  // namespace
+
+extern "C" {
+
+int skml_sparse_compact_f32(skml_ctx* c, const float* dense, int64_t dim, int32_t* keys, float* vals,
+                            int64_t* nnz_out) {
+    return compact_any<float>(c, dense, dim, keys, vals, nnz_out);
+}
+
+int skml_sparse_compact_f64(skml_ctx* c, const double* dense, int64_t dim, int32_t* keys, double* vals,
+                            int64_t* nnz_out) {
+    return compact_any<double>(c, dense, dim, keys, vals, nnz_out);
 }
 
 int skml_sparse_encode_kv_f32(skml_ctx* c, const int32_t* keys, const float* vals, int64_t nnz,
@@ -652,7 +678,17 @@ int skml_sparse_encode_kv_f32(skml_ctx* c, const int32_t* keys, const float* val
     if (int e = check_params(p)) return e;
     SP_HIP(hipSetDevice(ctx_device(c)));
     *out = nullptr;
-    return encode_kv(c, keys, vals, nnz, p, out);
+    return encode_kv(c, keys, vals, false, nnz, p, out);
+}
+
+int skml_sparse_encode_kv_f64(skml_ctx* c, const int32_t* keys, const double* vals, int64_t nnz,
+                              const skml_params* p, skml_sparse** out) {
+    if (!c || !out || nnz < 0 || (nnz > 0 && (!keys || !vals))) return sfail(SKML_E_ARG, "bad sparse arguments");
+    if (nnz > (int64_t)INT32_MAX) return sfail(SKML_E_ARG, "nnz exceeds Java int");
+    if (int e = check_params(p)) return e;
+    SP_HIP(hipSetDevice(ctx_device(c)));
+    *out = nullptr;
+    return encode_kv(c, keys, vals, true, nnz, p, out);
 }
 
 int skml_sparse_encode_f32(skml_ctx* c, const float* dense, int64_t dim, const skml_params* p,
@@ -666,10 +702,30 @@ int skml_sparse_encode_f32(skml_ctx* c, const float* dense, int64_t dim, const s
     if (!keys || !vals) return sfail(SKML_E_OOM, "compaction output");
     int64_t nnz = 0;
     if (int e = skml_sparse_compact_f32(c, dense, dim, keys, vals, &nnz)) return e;
-    return encode_kv(c, keys, vals, nnz, p, out);
+    return encode_kv(c, keys, vals, false, nnz, p, out);
 }
 
-int skml_sparse_decode_f32(skml_ctx* c, const skml_sparse* s, int32_t* keys_dev, float* vals_dev) {
+int skml_sparse_encode_f64(skml_ctx* c, const double* dense, int64_t dim, const skml_params* p,
+                           skml_sparse** out) {
+    if (!c || !out || dim < 0) return sfail(SKML_E_ARG, "bad sparse arguments");
+    if (int e = check_params(p)) return e;
+    SP_HIP(hipSetDevice(ctx_device(c)));
+    const size_t cap = (size_t)std::max<int64_t>(dim, 1);
+    int32_t* keys = scratch<int32_t>(c, kSlotCKeys, cap);
+    double* vals = scratch<double>(c, kSlotCVals, cap);
+    if (!keys || !vals) return sfail(SKML_E_OOM, "compaction output");
+    int64_t nnz = 0;
+    if (int e = skml_sparse_compact_f64(c, dense, dim, keys, vals, &nnz)) return e;
+    return encode_kv(c, keys, vals, true, nnz, p, out);
+}
+
+}  // extern "C"
+
+namespace {
+// restore + Sort.merge + quantValues[bin] (SparseVectorCompressor.decompressSparse,
+// SparseVectorCompressor.java:118-126) as fp32 or as the reference's doubles
+template <typename T>
+int decode_values(skml_ctx* c, const skml_sparse* s, int32_t* keys_dev, T* vals_dev) {
     if (!c || !s) return sfail(SKML_E_ARG, "bad decode arguments");
     const int64_t n = s->nnz;
     if (n == 0) return SKML_OK;
@@ -687,9 +743,21 @@ int skml_sparse_decode_f32(skml_ctx* c, const skml_sparse* s, int32_t* keys_dev,
     double* qv = reinterpret_cast<double*>(ctx_scratch(c, kSlotCells, sizeof(double) * s->qvalues.size()));
     if (!qv) return sfail(SKML_E_OOM, "value table");
     SP_HIP(hipMemcpyAsync(qv, s->qvalues.data(), sizeof(double) * s->qvalues.size(), hipMemcpyHostToDevice, st));
-    SP_HIP(launch_bin_values(st, bin, n, qv, (int)s->qvalues.size(), vals_dev));
+    if constexpr (sizeof(T) == 8) SP_HIP(launch_bin_values64(st, bin, n, qv, (int)s->qvalues.size(), vals_dev));
+    else SP_HIP(launch_bin_values(st, bin, n, qv, (int)s->qvalues.size(), vals_dev));
     SP_HIP(hipStreamSynchronize(st));
     return SKML_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int skml_sparse_decode_f32(skml_ctx* c, const skml_sparse* s, int32_t* keys_dev, float* vals_dev) {
+    return decode_values<float>(c, s, keys_dev, vals_dev);
+}
+
+int skml_sparse_decode_f64(skml_ctx* c, const skml_sparse* s, int32_t* keys_dev, double* vals_dev) {
+    return decode_values<double>(c, s, keys_dev, vals_dev);
 }
 
 int skml_sparse_times_by(skml_sparse* s, double x) {

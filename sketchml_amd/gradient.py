@@ -49,11 +49,9 @@ class DenseDoubleGradient:
         self.values = values
 
     def _sparse(self):
-        if self.values.dtype == torch.float32:
-            return to_sparse(self.values)  # |v| > EPS compaction on the device (k_compact)
-        # fp64 values: the test in double (an fp32 image could move values across EPS)
-        keys = torch.nonzero(self.values.abs() > EPS).flatten().to(torch.int32)
-        return keys, self.values[keys.long()]
+        # |v| > EPS compaction on the device (k_compact; fp64 values are tested in double and kept
+        # as doubles, so fromSparse bins the reference's own double values)
+        return to_sparse(self.values)
 
     def countNNZ(self) -> int:
         return int(self._sparse()[0].numel())

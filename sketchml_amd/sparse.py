@@ -87,15 +87,18 @@ class SparsePayload:
                    table=table, flag_words=trim(fw), delta_words=trim(dw))
         return res
 
-    def restore(self):
+    def restore(self, dtype=torch.float32):
         """GroupedMinMaxSketch.restore + SparseVectorCompressor.decompressSparse: device keys
-        (int32) and values (fp32 of the double quantValues)."""
+        (int32) and values quantValues[bin] (fp32 of the doubles, or the doubles themselves with
+        dtype=torch.float64, as the reference returns them)."""
         n = self.nnz()
         dev = torch.device("cuda", self.device)
+        wide = dtype == torch.float64
         keys = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
-        vals = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
-        check(_lib.lib.skml_sparse_decode_f32(self._ctx().handle, self.handle, C.c_void_p(keys.data_ptr()),
-                                              C.c_void_p(vals.data_ptr())), "sparse_decode")
+        vals = torch.empty(max(n, 1), dtype=torch.float64 if wide else torch.float32, device=dev)
+        fn = _lib.lib.skml_sparse_decode_f64 if wide else _lib.lib.skml_sparse_decode_f32
+        check(fn(self._ctx().handle, self.handle, C.c_void_p(keys.data_ptr()), C.c_void_p(vals.data_ptr())),
+              "sparse_decode")
         return keys[:n], vals[:n]
 
     def serialize(self) -> bytes:
@@ -152,9 +155,18 @@ def _as_device(t, dtype, device=None):
     return t.to(device=device, dtype=dtype).contiguous()
 
 
+def _values_dtype(values):
+    """fp64 values (the reference's double[]) stay fp64; everything else is binned as fp32."""
+    dt = values.dtype if isinstance(values, torch.Tensor) else np.asarray(values).dtype
+    return torch.float64 if dt in (torch.float64, np.float64) else torch.float32
+
+
 def encode_sparse(keys, values, bin_num=Quantizer.DEFAULT_BIN_NUM, group_num=8, row_num=2, col_ratio=0.3,
                   seed=0, hash_seed=0, dedup=True, uniform=False, parallelism=1) -> SparsePayload:
-    v = _as_device(values, torch.float32)
+    """SparseVectorCompressor.compressSparse (SparseVectorCompressor.java:52-67).  Double values
+    go through skml_sparse_encode_kv_f64 (the quantizer sketches the doubles themselves, as the
+    Java double[] path does); float values through the fp32 kernels."""
+    v = _as_device(values, _values_dtype(values))
     k = _as_device(keys, torch.int32, v.device)
     if k.numel() != v.numel():
         raise SketchMLException(
@@ -163,32 +175,36 @@ def encode_sparse(keys, values, bin_num=Quantizer.DEFAULT_BIN_NUM, group_num=8, 
     ctx = get_context(dev)
     p = _params(bin_num, group_num, row_num, col_ratio, seed, hash_seed, dedup, uniform, parallelism)
     h = C.c_void_p()
-    check(_lib.lib.skml_sparse_encode_kv_f32(ctx.handle, C.c_void_p(k.data_ptr()), C.c_void_p(v.data_ptr()),
-                                             k.numel(), C.byref(p), C.byref(h)), "sparse_encode")
+    fn = _lib.lib.skml_sparse_encode_kv_f64 if v.dtype == torch.float64 else _lib.lib.skml_sparse_encode_kv_f32
+    check(fn(ctx.handle, C.c_void_p(k.data_ptr()), C.c_void_p(v.data_ptr()), k.numel(), C.byref(p), C.byref(h)),
+          "sparse_encode")
     return SparsePayload(h, dev, int(row_num))
 
 
 def encode_dense_as_sparse(dense, bin_num=Quantizer.DEFAULT_BIN_NUM, group_num=8, row_num=2, col_ratio=0.3,
                            seed=0, hash_seed=0, uniform=False) -> SparsePayload:
-    """SketchGradient.fromSparse after DenseDoubleGradient.toSparse (|x| > 1e-8), on device."""
-    x = _as_device(dense, torch.float32)
+    """SketchGradient.fromSparse after DenseDoubleGradient.toSparse (|x| > 1e-8), on device; a
+    float64 gradient (DenseDoubleGradient.values itself) is compacted and binned as doubles."""
+    x = _as_device(dense, _values_dtype(dense))
     dev = x.device.index
     ctx = get_context(dev)
     p = _params(bin_num, group_num, row_num, col_ratio, seed, hash_seed, True, uniform)
     h = C.c_void_p()
-    check(_lib.lib.skml_sparse_encode_f32(ctx.handle, C.c_void_p(x.data_ptr()), x.numel(), C.byref(p),
-                                          C.byref(h)), "sparse_encode")
+    fn = _lib.lib.skml_sparse_encode_f64 if x.dtype == torch.float64 else _lib.lib.skml_sparse_encode_f32
+    check(fn(ctx.handle, C.c_void_p(x.data_ptr()), x.numel(), C.byref(p), C.byref(h)), "sparse_encode")
     return SparsePayload(h, dev, int(row_num))
 
 
 def to_sparse(dense):
-    """DenseDoubleGradient.countNNZ + toSparse (ml/gradient/DenseDoubleGradient.scala:64-89)."""
-    x = _as_device(dense, torch.float32)
+    """DenseDoubleGradient.countNNZ + toSparse (ml/gradient/DenseDoubleGradient.scala:64-89);
+    float64 input keeps float64 values."""
+    x = _as_device(dense, _values_dtype(dense))
     ctx = get_context(x.device.index)
     keys = torch.empty(max(x.numel(), 1), dtype=torch.int32, device=x.device)
-    vals = torch.empty(max(x.numel(), 1), dtype=torch.float32, device=x.device)
+    vals = torch.empty(max(x.numel(), 1), dtype=x.dtype, device=x.device)
     nnz = C.c_int64()
-    check(_lib.lib.skml_sparse_compact_f32(ctx.handle, C.c_void_p(x.data_ptr()), x.numel(),
+    fn = _lib.lib.skml_sparse_compact_f64 if x.dtype == torch.float64 else _lib.lib.skml_sparse_compact_f32
+    check(fn(ctx.handle, C.c_void_p(x.data_ptr()), x.numel(),
                                            C.c_void_p(keys.data_ptr()), C.c_void_p(vals.data_ptr()),
                                            C.byref(nnz)), "sparse_compact")
     return keys[: nnz.value], vals[: nnz.value]
