@@ -50,7 +50,75 @@ def parse():
     ap.add_argument("--no-extras", action="store_true", help="skip decode / H2D measurements")
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the fp64 and C3 sparse measurements reported under extras.other_configs")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher check without a GPU: every rank joins a gloo group and reports itself")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args) -> int:
+    """`python bench.py --gpus N` without a launcher: start N fresh worker processes of this script,
+    one per GPU (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set as torch.distributed.run sets them),
+    before this process makes any GPU call; forward rank 0's JSON line; fail if any rank fails."""
+    import subprocess
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    import threading
+    import time as _t
+    out0 = []
+    reader = threading.Thread(target=lambda: out0.append(procs[0].stdout.read()), daemon=True)
+    reader.start()
+    # a rank that dies leaves the others waiting in a collective: stop them (our own children)
+    first_bad = []
+    while any(p.poll() is None for p in procs):
+        first_bad = [r for r, p in enumerate(procs) if p.poll() not in (None, 0)]
+        if first_bad:
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+            break
+        _t.sleep(0.2)
+    reader.join(timeout=30)
+    rcs = [p.wait() for p in procs]
+    bad = first_bad or [r for r, rc in enumerate(rcs) if rc != 0]
+    if bad:
+        print(f"bench.py: rank(s) {bad} failed with exit codes {[rcs[r] for r in bad]}; all exit codes {rcs}",
+              file=sys.stderr)
+        return 1
+    sys.stdout.write((out0[0] if out0 else b"").decode())
+    sys.stdout.flush()
+    return 0
+
+
+def dry_run(args, world: int, rank: int) -> None:
+    """Launcher rehearsal on the CPU: gloo group, one all-gather of the ranks, rank 0 reports.
+    SKML_DRYRUN_FAIL_RANK=r makes rank r exit with status 3 (the launcher's failure path)."""
+    if os.environ.get("SKML_DRYRUN_FAIL_RANK") == str(rank):
+        sys.exit(3)
+    dist.init_process_group("gloo")
+    t = torch.tensor([rank], dtype=torch.int64)
+    out = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    if rank == 0:
+        print(json.dumps({"metric": "dry-run", "n_gpus": world, "ranks_seen": [int(v.item()) for v in out],
+                          "gpus_arg": args.gpus}))
+    dist.destroy_process_group()
 
 
 def kernel_stats(lib, ctx):
@@ -109,6 +177,13 @@ def sq_valu(kernel):
     return best
 
 
+def _affinity():
+    try:
+        return len(os.sched_getaffinity(0))
+    except Exception:
+        return os.cpu_count() or 1
+
+
 def _cpu_threads():
     """Host threads this process may use: the affinity mask, capped by OMP_NUM_THREADS (16 on the
     GPU box, which shares a many-core host)."""
@@ -140,7 +215,10 @@ def cpu_baseline(x_host, bins, budget_s):
         legs[name] = {"gbps": round(4.0 * len(sample) * reps / t / 1e9, 4), "threads": threads,
                       "sample": f"first {len(sample)} floats of the bucket, {reps} encode(s), {t:.1f} s"}
     best = legs["threads"]
+    omp = os.environ.get("OMP_NUM_THREADS")
     return {"value": best["gbps"], "unit": "GB/s", "cores": best["threads"], "kind": "port",
+            "cores_note": f"{best['threads']} threads: this process's CPU affinity ({_affinity()} CPUs) capped by "
+                          f"OMP_NUM_THREADS={omp} (the GPU box's per-job CPU share); the host has {os.cpu_count()}",
             "sample": best["sample"] + " (parallelQuantize + parallelQuantizeToBins)",
             "legs": legs, "cpu": _cpu_model(),
             "what": "oracle/cpu_baseline.cpp: C++ -O3 restatement of the reference Java encode "
@@ -348,9 +426,20 @@ def _cpu_model():
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args))  # one process per GPU, started before any GPU call
+    world = int(env_world or "1")
+    if world != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+        return dry_run(args, world, rank)
     # SKML_BENCH_EXCHANGE=1 runs the N > 1 exchange path (RCCL all-gather on its own stream) with a
     # world-size-1 communicator: a one-GPU rehearsal of the code the multi-GPU runs take
     rehearse = world == 1 and os.environ.get("SKML_BENCH_EXCHANGE") == "1"
@@ -558,9 +647,11 @@ def main():
         extras["other_configs"] = other_configs(sk, lib, ctx, dev, xs)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.quant == "quantile" and args.dtype == "f32":
+    if rank == 0 and not args.no_cpu_baseline and args.quant == "quantile" and args.dtype == "f32":
+        # after every timed GPU region (the other ranks wait at the barrier below)
         cpu = cpu_baseline(xs[0][: 2**24].cpu().numpy(), bins, args.cpu_seconds)
 
+    barrier()
     if exch is not None:
         exch.close()
     if rank == 0:
