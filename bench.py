@@ -29,7 +29,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, MI355X_MICROARCH.md "Chip-level parameters"
-KNAMES = {0: "k_leaf", 1: "k_merge", 2: "k_summary", 3: "k_quantize", 4: "k_decode"}
+KNAMES = {0: "k_leaf", 1: "k_merge", 2: "k_summary", 3: "k_quantize", 4: "k_decode", 5: "k_decode_sum"}
 
 
 def parse():
@@ -277,6 +277,7 @@ def other_configs(sk, lib, ctx, dev, xs):
     out["batched_buckets"] = {"workload": f"{nbk} independent 2^26-float buckets per call, 256 bins",
                               "ms_per_bucket": round(tb / nbk * 1e3, 4), "gbps": round(4.0 * n * nbk / tb / 1e9, 1)}
     del pls
+    out["dense_decode_sum_c4"] = dense_decode_sum(sk, lib, ctx, dev, xs, n, p)
     out["dense_2p28"] = dense_north_star(sk, lib, ctx, dev)
     dim = 2**28
     g = torch.Generator(device=dev).manual_seed(3)
@@ -290,7 +291,69 @@ def other_configs(sk, lib, ctx, dev, xs):
                         "nnz": nnz, "encode_ms": round(te * 1e3, 3), "gbps_dense_in": round(4.0 * dim / te / 1e9, 1),
                         "roofline_frac": round(alg / te / 1e9 / HBM_PEAK_GBS, 4), "restore_ms": round(td * 1e3, 3),
                         "note": "median wall time of 5 synchronised calls (one nnz read after the compaction, one read-back at the end)"}
+    del d, rk, rv
+    out["sparse_aggregate"] = sparse_aggregate(sk, spl, dim, timed_median)
     return out
+
+
+def sparse_aggregate(sk, spl, dim, timed_median, P=8):
+    """The ml path's DP step after the all-gather: P exported C3 payloads in
+    stride-spaced slots -> Gradient.sum in double on the device (skml_sparse_decode_sum_f64), plus
+    the export itself.  The P slots hold copies of one C3 payload (every rank's payload has the
+    C3 shape; the cost per payload does not depend on its values)."""
+    from sketchml_amd.distributed import blob_stride
+    nb = spl.export_bytes()
+    stride = blob_stride([nb])
+    allb = torch.empty(stride * P, dtype=torch.uint8, device="cuda")
+    tx, _ = timed_median(lambda: spl.export(allb[:stride]), 5)
+    for q in range(1, P):
+        allb[q * stride:(q + 1) * stride].copy_(allb[:stride])
+    out = torch.empty(dim, dtype=torch.float64, device="cuda")
+    ts, _ = timed_median(lambda: sk.decode_sum(allb, P, stride, dim, 1.0 / P, out), 3)
+    t1, _ = timed_median(lambda: sk.decode_sum(allb, 1, stride, dim, 1.0, out), 3)
+    nnz = spl.nnz()
+    res = {"workload": f"Gradient.sum of {P} C3 sparse payloads (nnz {nnz} each) into a 2^28-dim double sum, x 1/{P}",
+           "blob_bytes": nb, "export_ms": round(tx * 1e3, 3), "decode_sum_ms": round(ts * 1e3, 3),
+           "decode_sum_one_payload_ms": round(t1 * 1e3, 3),
+           "per_payload_ms": round((ts - t1) / (P - 1) * 1e3, 3),
+           "note": "median wall time of synchronised calls; one payload = DeltaAdaptive decode + MinMax query "
+                   "+ scatter-add into the double sum (no Sort.merge: keys are unique); the fixed part is the "
+                   "2 GiB zero fill and the x 1/P pass"}
+    del allb, out
+    return res
+
+
+def dense_decode_sum(sk, lib, ctx, dev, xs, n, p, P=8):
+    """C4's consumer on one GPU: P = 8 gathered 2^26-value dense payloads -> fused decode + sum in
+    double + x 1/P (skml_dense_decode_sum_f32), HIP-event timed on the codec stream.  Algorithmic
+    bytes = P * n * b / 8 (codes) + 4 n (fp32 out)."""
+    nb = lib.skml_dense_payload_bytes(n, 256)
+    stride = (nb + 255) // 256 * 256
+    allp = sk.alloc_aligned(stride * P, dev)
+    ptrs = (C.c_void_p * P)(*[xs[i % len(xs)].data_ptr() for i in range(P)])
+    pptr = (C.c_void_p * P)(*[allp.data_ptr() + i * stride for i in range(P)])
+    ns = (C.c_int64 * P)(*([n] * P))
+    caps = (C.c_size_t * P)(*([stride] * P))
+    if lib.skml_dense_encode_batch_f32(ctx, P, ptrs, ns, C.byref(p), pptr, caps):
+        raise RuntimeError("batch encode failed")
+    out = torch.empty(n, dtype=torch.float32, device=dev)
+    run = lambda: lib.skml_dense_decode_sum_f32(ctx, C.c_void_p(allp.data_ptr()), P, stride,  # noqa: E731
+                                                 C.c_void_p(out.data_ptr()), n, 1.0 / P)
+    run()
+    torch.cuda.synchronize()
+    lib.skml_ctx_set_timing(ctx, 1 << 5)
+    lib.skml_ctx_reset_stats(ctx)
+    for _ in range(10):
+        run()
+    ks = kernel_stats(lib, ctx)
+    lib.skml_ctx_set_timing(ctx, 0)
+    hdr = _lib_header(lib, ctx, allp)
+    us = ks["k_decode_sum"]["avg_us"]
+    alg = P * n * hdr.code_bits / 8.0 + 4.0 * n
+    del allp, out
+    return {"workload": f"{P} dense payloads of 2^26 codes ({hdr.code_bits}-bit) -> one fp32 sum x 1/{P}",
+            "k_decode_sum_us": round(us, 2), "alg_bytes": alg,
+            "gbps": round(alg / (us * 1e-6) / 1e9, 1), "roofline_frac": round(alg / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
 def dense_north_star(sk, lib, ctx, dev, n=2**28, bins=256, reps=10):
@@ -334,6 +397,48 @@ def dense_north_star(sk, lib, ctx, dev, n=2**28, bins=256, reps=10):
         res["k_quantize_gbps"] = round((4.0 + hdr.code_bits / 8.0) * n / q / 1e9, 1)
     del x, pl
     return res
+
+
+def sparse_exchange_step(sk, exch, dev, rank, world, barrier, reps=3):
+    """The ml path's exchange at C3 shape on every rank (GeneralizedLinearModel.scala:145-156):
+    rank r encodes its own 2^28-dim, 10 %-nnz gradient (seed 3 + r), then sizes are all-gathered,
+    the blob is exported into its padded slot, the slots are all-gathered over RCCL and every rank
+    computes Gradient.sum x 1/P in double.  Max over ranks of the median of `reps` steps."""
+    from sketchml_amd import distributed as D
+    dim = 2**28
+    g = torch.Generator(device=dev).manual_seed(3 + rank)
+    d = torch.randn(dim, device=dev, generator=g)
+    d[torch.rand(dim, device=dev, generator=g) >= 0.1] = 0.0
+    spl = sk.encode_dense_as_sparse(d, 256, 8, 2, 0.3, 3 + rank, 3 + rank)
+    del d
+    nb = spl.export_bytes()
+    ts, tg = [], []
+    for _ in range(reps):
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        stride = D.blob_stride(D.agree_sizes(nb))
+        local = torch.empty(stride, dtype=torch.uint8, device=dev)
+        spl.export(local)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        allb = D.gather_blobs(local, stride, exchange=exch)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        avg = sk.decode_sum(allb, world, stride, dim, 1.0 / world)
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        ts.append(t3 - t0)
+        tg.append(t2 - t1)
+        del allb, avg, local
+    t = torch.tensor([statistics.median(ts), statistics.median(tg)], device=dev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    step, gat = float(t[0].item()), float(t[1].item())
+    algbw = world * stride / gat / 1e9
+    return {"workload": "C3-shape sparse gradient per rank: sizes + export + RCCL all-gather of the padded blobs "
+                        "+ Gradient.sum x 1/P in double on every rank",
+            "blob_bytes_rank0": nb, "stride": stride, "step_ms": round(step * 1e3, 3),
+            "allgather_ms": round(gat * 1e3, 3), "allgather_busbw_gbs": round(algbw * (world - 1) / world, 1)}
 
 
 def _lib_header(lib, ctx, payload):
@@ -641,6 +746,8 @@ def main():
         extras["allgather"] = {"ms": round(tag * 1e3, 3), "bytes_per_rank": nb, "algbw_gbs": round(algbw, 1),
                                "busbw_gbs": round(algbw * (world - 1) / world, 1),
                                "decode_sum_max_abs_err_vs_allreduce": err}
+        del summed, own, ref
+        extras["sparse_exchange"] = sparse_exchange_step(sk, exch, dev, rank, world, barrier)
 
     if (rank == 0 and world == 1 and not args.no_extras and not args.no_configs and args.quant == "quantile"
             and args.dtype == "f32" and args.n == 2**26):

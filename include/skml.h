@@ -339,6 +339,29 @@ int skml_sparse_deserialize(skml_ctx* ctx, const uint8_t* buf_host, size_t len, 
  * their int32 bins, on the device.  Synchronising. */
 int skml_sparse_restore_bins(skml_ctx* ctx, const skml_sparse* s, int32_t* keys_dev, int32_t* bins_dev);
 int skml_sparse_free(skml_sparse* s);
+
+/* ---- Sparse payloads between GPUs (the ml path's exchange) ----
+ * A payload exported as one contiguous, relocatable device blob: a 256-byte header (magic "SKSP",
+ * section offsets), the group table, the quantizer header + splits, quantValues (doubles, timesBy
+ * applied), the MinMaxSketch tables and the two DeltaAdaptive word streams.  It is what the RCCL
+ * all-gather moves (sizes first, then the blobs padded to the largest: skml_allgather), with no
+ * host round trip.  The blob replaces the Java-serialised SketchGradient that Spark's collect /
+ * broadcast ship (ml/algorithm/GeneralizedLinearModel.scala:145-156). */
+int skml_sparse_export_bytes(const skml_sparse* s, size_t* bytes);
+/* dst_dev: 256-byte aligned device memory of at least export_bytes.  Asynchronous. */
+int skml_sparse_export(skml_ctx* ctx, const skml_sparse* s, void* dst_dev, size_t cap);
+/* A library-owned copy of the blob at blob_dev (len bytes available there); the blob is checked
+ * (magic, section offsets, group-table invariants) before anything runs on it.  Synchronising. */
+int skml_sparse_import(skml_ctx* ctx, const void* blob_dev, size_t len, skml_sparse** out);
+/* Gradient.sum (ml/gradient/Gradient.scala:44-49) of P blobs laid out `stride` bytes apart (the
+ * all-gather output): out[0, dim) = +0.0, then payload by payload, in order,
+ * DenseDoubleGradient.plusBy(SketchGradient.toAuto) (DenseDoubleGradient.scala:38) -- every restored
+ * key adds quantValues[bin] in double (the live values only, plus the dense form's +0.0, when the
+ * payload's live count exceeds dim * 2 / 3: SparseDoubleGradient.toAuto); then out *= scale when
+ * scale != 1 (the 1/P average, one double multiply per element).  A key outside [0, dim) fails
+ * with SKML_E_ARG (SparseDoubleGradient's bound check).  Synchronising. */
+int skml_sparse_decode_sum_f64(skml_ctx* ctx, const void* blobs_dev, int32_t P, size_t stride, int64_t dim,
+                               double scale, double* out_dev);
 /* Host-memory forms of encode_kv / decode (int[] keys and float[] values in JVM arrays). */
 int skml_sparse_encode_kv_host_f32(skml_ctx* ctx, const int32_t* keys_host, const float* vals_host, int64_t nnz,
                                    const skml_params* params, skml_sparse** out);

@@ -11,11 +11,11 @@ from .context import Context, alloc_aligned, get_context
 from .exceptions import QuantileSketchException, SketchMLException
 from .gradient import DenseDoubleGradient, Kind, SketchGradient, SparseDoubleGradient
 from .quantization import QuantileQuantizer, QuantizationType, Quantizer, UniformQuantizer
-from .sparse import (DeltaAdaptiveEncoder, GroupedMinMaxSketch, SparsePayload, SparseVectorCompressor,
+from .sparse import (DeltaAdaptiveEncoder, GroupedMinMaxSketch, SparsePayload, SparseVectorCompressor, decode_sum,
                      encode_dense_as_sparse, encode_sparse, to_sparse)
 
 __all__ = ["Constants", "Parallel", "DenseDoubleGradient", "Kind", "SketchGradient", "SparseDoubleGradient", "Context", "DeltaAdaptiveEncoder", "DenseVectorCompressor", "GroupedMinMaxSketch", "SparsePayload",
-           "SparseVectorCompressor", "encode_dense_as_sparse", "encode_sparse", "to_sparse", "QuantileQuantizer", "QuantizationType", "Quantizer", "UniformQuantizer",
+           "SparseVectorCompressor", "decode_sum", "encode_dense_as_sparse", "encode_sparse", "to_sparse", "QuantileQuantizer", "QuantizationType", "Quantizer", "UniformQuantizer",
            "QuantileSketchException", "SketchMLException", "get_context", "alloc_aligned"]
 
 LIB_PATH = _lib.LIB_PATH

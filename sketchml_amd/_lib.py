@@ -130,6 +130,10 @@ _SIGS = {
     "skml_sparse_deserialize": (C.c_int, [vp, u8p, C.c_size_t, dblp, i32, C.POINTER(vp)]),
     "skml_sparse_restore_bins": (C.c_int, [vp, vp, vp, vp]),
     "skml_sparse_free": (C.c_int, [vp]),
+    "skml_sparse_export_bytes": (C.c_int, [vp, szp]),
+    "skml_sparse_export": (C.c_int, [vp, vp, vp, C.c_size_t]),
+    "skml_sparse_import": (C.c_int, [vp, vp, C.c_size_t, C.POINTER(vp)]),
+    "skml_sparse_decode_sum_f64": (C.c_int, [vp, vp, i32, C.c_size_t, i64, C.c_double, vp]),
     "skml_delta_encode": (C.c_int, [vp, vp, i64, i32p, i32p, i64p, i64p, vp, vp, i64]),
     "skml_delta_decode": (C.c_int, [vp, i64, i32, i32, vp, i64, vp, i64, vp]),
     "skml_comm_unique_id": (C.c_int, [u8p]),

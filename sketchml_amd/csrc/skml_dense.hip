@@ -324,42 +324,70 @@ hipError_t launch_decode(hipStream_t st, const void* payload, float* out, int64_
 // the midpoint from the payload's splits, as k_decode does above kLutMax.
 constexpr int kMaxSumPayloads = 16;
 constexpr int kSumLutBins = 256;
+// The payload headers are read once per workgroup into LDS (codes pointer, code width, LUT row);
+// each wave then owns 1024-element tiles as k_decode does: per payload four 4-code reads per
+// lane (256 contiguous code bytes per wave-instruction at 8 bits), 16 double accumulators per lane
+// added in payload order, and four nontemporal float4 stores.
 __global__ __launch_bounds__(256) void k_decode_sum(const uint8_t* __restrict__ payloads, int P,
                                                     size_t stride, float* __restrict__ out, int64_t n,
                                                     double scale) {
     __shared__ double lut[kMaxSumPayloads][kSumLutBins];
+    __shared__ const uint8_t* s_codes[kMaxSumPayloads];
+    __shared__ int s_bits[kMaxSumPayloads], s_lds[kMaxSumPayloads];
     for (int p = 0; p < P; p++) {
         const uint8_t* pl = payloads + (size_t)p * stride;
         const skml_dense_header* h = reinterpret_cast<const skml_dense_header*>(pl);
         const double* sp = reinterpret_cast<const double*>(pl + kHeaderBytes);
-        if (h->bin_num > kSumLutBins) continue;
-        for (int b = threadIdx.x; b < h->bin_num; b += 256) lut[p][b] = lut_value(h, sp, b);
+        const bool in_lds = h->bin_num <= kSumLutBins;
+        if (threadIdx.x == 0) {
+            s_codes[p] = pl + h->codes_offset;
+            s_bits[p] = h->code_bits;
+            s_lds[p] = in_lds ? 1 : 0;
+        }
+        if (in_lds)
+            for (int b = threadIdx.x; b < h->bin_num; b += 256) lut[p][b] = lut_value(h, sp, b);
     }
     __syncthreads();
-    const int64_t stride_e = (int64_t)gridDim.x * 256;
-    for (int64_t e0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; e0 < n; e0 += stride_e * 4) {
-        double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * 4, wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t full = n / 1024;
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    auto value = [&](int p, uint32_t c) -> double {
+        if (s_lds[p]) return lut[p][c];
+        const uint8_t* pl = payloads + (size_t)p * stride;
+        return lut_value(reinterpret_cast<const skml_dense_header*>(pl),
+                         reinterpret_cast<const double*>(pl + kHeaderBytes), (int)c);
+    };
+    for (int64_t tile = wid; tile < full; tile += nw) {
+        double acc[4][4];
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+#pragma unroll
+            for (int e = 0; e < 4; e++) acc[j][e] = 0.0;
         for (int p = 0; p < P; p++) {
-            const uint8_t* pl = payloads + (size_t)p * stride;
-            const skml_dense_header* h = reinterpret_cast<const skml_dense_header*>(pl);
-            const uint8_t* codes = pl + h->codes_offset;
-            uint32_t c[4];
-            if (e0 + 4 <= n) read_codes4(codes, e0, h->code_bits, c);
-            else
-                for (int e = 0; e < 4; e++) c[e] = e0 + e < n ? read_code(codes, e0 + e, h->code_bits) : 0;
-            if (h->bin_num <= kSumLutBins) {
-                for (int e = 0; e < 4; e++) acc[e] += lut[p][c[e]];
-            } else {
-                const double* sp = reinterpret_cast<const double*>(pl + kHeaderBytes);
-                for (int e = 0; e < 4; e++) acc[e] += lut_value(h, sp, (int)c[e]);
-            }
+            const int bits = __builtin_amdgcn_readfirstlane(s_bits[p]);
+            const uint8_t* codes = s_codes[p];
+            uint32_t c[4][4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) read_codes4(codes, tile * 1024 + j * 256 + lane * 4, bits, c[j]);
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+#pragma unroll
+                for (int e = 0; e < 4; e++) acc[j][e] += value(p, c[j][e]);
         }
-        if (e0 + 4 <= n) {
-            *reinterpret_cast<float4*>(out + e0) = make_float4((float)(acc[0] * scale), (float)(acc[1] * scale),
-                                                               (float)(acc[2] * scale), (float)(acc[3] * scale));
-        } else {
-            for (int e = 0; e < 4; e++)
-                if (e0 + e < n) out[e0 + e] = (float)(acc[e] * scale);
+        f32x4* dst = reinterpret_cast<f32x4*>(out + tile * 1024);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const f32x4 o = {(float)(acc[j][0] * scale), (float)(acc[j][1] * scale), (float)(acc[j][2] * scale),
+                             (float)(acc[j][3] * scale)};
+            __builtin_nontemporal_store(o, dst + j * 64 + lane);
+        }
+    }
+    if (wid == full % nw) {
+        for (int64_t e = full * 1024 + lane; e < n; e += 64) {
+            double a = 0.0;
+            for (int p = 0; p < P; p++) a += value(p, read_code(s_codes[p], e, s_bits[p]));
+            out[e] = (float)(a * scale);
         }
     }
 }

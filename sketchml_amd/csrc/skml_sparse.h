@@ -123,9 +123,37 @@ hipError_t launch_dec_deltas(hipStream_t st, const uint64_t* delta_words, int64_
                              const uint64_t* tile_base, uint32_t* delta, uint64_t* tile_sums);
 hipError_t launch_group_prefix(hipStream_t st, const uint32_t* delta, int64_t n, const SpGroups* gp, int G,
                                const uint64_t* tile_base, uint64_t* gpre);
+// sum_out != null: add quantValues[bin] (sum_qv) into sum_out[key] instead of storing keys / bins
 hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, const SpGroups* gp,
                            const uint64_t* tile_base, const uint64_t* gpre, const int32_t* table,
-                           int32_t* gkeys, int32_t* gbins);
+                           int32_t* gkeys, int32_t* gbins, const double* sum_qv = nullptr, int nq = 0,
+                           double* sum_out = nullptr, int64_t dim = 0, unsigned* err = nullptr, int live_only = 0);
+// the DP sum's helpers (skml_sparse_decode_sum_f64): -0.0 -> +0.0, *= scale, live count, pair adds
+hipError_t launch_sum_add_zero(hipStream_t st, double* out, int64_t n);
+hipError_t launch_scale(hipStream_t st, double* out, int64_t n, double x);
+hipError_t launch_count_live(hipStream_t st, const int32_t* bins, int64_t n, const double* qv, int nq,
+                             uint64_t* count);
+hipError_t launch_add_pairs(hipStream_t st, const int32_t* keys, const int32_t* bins, int64_t n, const double* qv,
+                            int nq, double* out, int64_t dim, unsigned* err, int live_only);
+
+// Exported sparse payload: one contiguous device blob (skml_sparse_export / _import, the unit the
+// RCCL all-gather moves).  Offsets are from the blob start, every section 256-byte aligned.
+constexpr uint32_t kSpBlobMagic = 0x50534B53u;  // "SKSP"
+struct SpBlobHeader {
+    uint32_t magic;
+    int32_t version;
+    int64_t total_bytes;
+    int64_t nnz;
+    int64_t ncells;
+    int64_t n_flag_words, n_delta_words;  // stored words (bit streams + one trailing zero word)
+    int64_t flag_bits, delta_bits;
+    int32_t nvalues;                      // quantValues doubles
+    int32_t quant_bytes;                  // dense header + splits
+    int64_t off_groups, off_quant, off_values, off_tables, off_flags, off_deltas;
+    skml_params params;
+    int64_t reserved[8];
+};
+static_assert(sizeof(SpBlobHeader) <= 256, "blob header fits its 256-byte section");
 // One round of pairwise stable merges of sorted runs (Sort.merge order: lower run first on ties).
 // run_start: nruns + 1 device offsets; total = run_start[nruns].
 hipError_t launch_merge_round(hipStream_t st, const int32_t* kin, const int32_t* bin_in, int32_t* kout,

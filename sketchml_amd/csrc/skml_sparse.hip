@@ -1836,24 +1836,39 @@ hipError_t launch_group_prefix(hipStream_t st, const uint32_t* delta, int64_t n,
 
 // keys: group-restarted prefix sums of the deltas (Java int wrap); bins: MinMaxSketch.query
 // (MinMaxSketch.java:64-73): the row value farthest from zero, the first row on ties.
+// Summing mode (sum_out != null): instead of storing (key, bin), add quantValues[bin] into
+// sum_out[key] -- DenseDoubleGradient.plusBy(SparseDoubleGradient) of one payload
+// (DenseDoubleGradient.scala:38-45): keys are unique within a payload, so no atomics, and
+// payloads go one launch after another, so every element's sum is added in payload order.
+// live_only: only |v| > 1e-8 are added (the payload reached plusBy through toAuto's dense form,
+// SparseDoubleGradient.toDense, SparseDoubleGradient.scala:39-44).
+struct DecSum {
+    const double* qv;  // quantValues (the payload's bucket values, timesBy'd)
+    double* out;       // the dense double sum
+    int64_t dim;       // its length: a key outside [0, dim) sets *err and is skipped
+    unsigned* err;     // (SparseDoubleGradient's "out of bounds" require, SparseDoubleGradient.scala:13)
+    int nq;            // quantValues entries: a bin outside [0, nq) sets *err too
+    int live_only;
+};
 __global__ __launch_bounds__(kSpThreads) void k_dec_keys(const uint32_t* __restrict__ delta, int64_t n,
                                                          const SpGroups* __restrict__ gp,
                                                          const uint64_t* __restrict__ tile_base,
                                                          const uint64_t* __restrict__ gpre,
                                                          const int32_t* __restrict__ table,
-                                                         int32_t* __restrict__ gkeys, int32_t* __restrict__ gbins) {
+                                                         int32_t* __restrict__ gkeys, int32_t* __restrict__ gbins,
+                                                         DecSum sum) {
     __shared__ int64_t S[kMaxGroups + 1];
     __shared__ uint64_t sh[4];
     load_starts(gp, S);
     __syncthreads();
     const int64_t i0 = (int64_t)blockIdx.x * kSpTile + threadIdx.x * 8;
     uint32_t d[8];
-    uint64_t sum = 0;
+    uint64_t sum8 = 0;
     for (int j = 0; j < 8; j++) {
         d[j] = i0 + j < n ? delta[i0 + j] : 0;
-        sum += d[j];
+        sum8 += d[j];
     }
-    uint64_t v[1] = {sum}, tot[1];
+    uint64_t v[1] = {sum8}, tot[1];
     block_excl_scan<1>(v, tot, sh);
     if (i0 >= n) return;
     uint64_t p = tile_base[blockIdx.x] + v[0];
@@ -1887,6 +1902,25 @@ __global__ __launch_bounds__(kSpThreads) void k_dec_keys(const uint32_t* __restr
         for (int j = 0; j < 8; j++)  // MinMaxSketch.query: the strictly farther value wins, ties keep the earlier row
             if ((int32_t)((uint32_t)mm_dist(tv[j], zero) - (uint32_t)mm_dist(res[j], zero)) > 0) res[j] = tv[j];
     }
+    if (sum.out) {
+        double x[8];
+        bool ok[8];
+        unsigned bad = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            ok[j] = i0 + j < n && key[j] >= 0 && (int64_t)key[j] < sum.dim && res[j] >= 0 && res[j] < sum.nq;
+            bad |= (i0 + j < n && !ok[j]) ? 1u : 0u;
+            x[j] = ok[j] ? sum.qv[res[j]] : 0.0;
+        }
+        if (bad) atomicOr(sum.err, 1u);
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            if (!ok[j]) continue;
+            if (sum.live_only && !(fabs(x[j]) > 1e-8)) continue;  // Maths.EPS (ml/util/Maths.scala:8)
+            sum.out[key[j]] += x[j];
+        }
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < 8; j++) {
         if (i0 + j >= n) break;
@@ -1897,11 +1931,87 @@ __global__ __launch_bounds__(kSpThreads) void k_dec_keys(const uint32_t* __restr
 
 hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, const SpGroups* gp,
                            const uint64_t* tile_base, const uint64_t* gpre, const int32_t* table,
-                           int32_t* gkeys, int32_t* gbins) {
+                           int32_t* gkeys, int32_t* gbins, const double* sum_qv, int nq, double* sum_out,
+                           int64_t dim, unsigned* err, int live_only) {
     const int64_t tiles = sp_tiles(n, kSpTile);
     if (tiles <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_dec_keys, dim3((unsigned)tiles), dim3(kSpThreads), 0, st, delta, n, gp, tile_base, gpre,
-                       table, gkeys, gbins);
+                       table, gkeys, gbins, DecSum{sum_qv, sum_out, dim, err, nq, live_only});
+    return hipGetLastError();
+}
+
+// x + 0.0 over the whole sum (the dense form's zero entries are added too: -0.0 becomes +0.0)
+__global__ __launch_bounds__(kSpThreads) void k_sum_add_zero(double* __restrict__ out, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * kSpThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kSpThreads)
+        if (__double_as_longlong(out[i]) == (long long)0x8000000000000000ull) out[i] = 0.0;
+}
+hipError_t launch_sum_add_zero(hipStream_t st, double* out, int64_t n) {
+    if (n <= 0) return hipSuccess;
+    const int64_t grid = std::min<int64_t>(sp_tiles(n, kSpThreads * 8), 8192);
+    hipLaunchKernelGGL(k_sum_add_zero, dim3((unsigned)grid), dim3(kSpThreads), 0, st, out, n);
+    return hipGetLastError();
+}
+
+// out[i] *= scale (the 1/P of the DP average, one double multiply per element)
+__global__ __launch_bounds__(kSpThreads) void k_scale(double* __restrict__ out, int64_t n, double x) {
+    for (int64_t i = (int64_t)blockIdx.x * kSpThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kSpThreads)
+        out[i] = __dmul_rn(out[i], x);
+}
+hipError_t launch_scale(hipStream_t st, double* out, int64_t n, double x) {
+    if (n <= 0) return hipSuccess;
+    const int64_t grid = std::min<int64_t>(sp_tiles(n, kSpThreads * 8), 8192);
+    hipLaunchKernelGGL(k_scale, dim3((unsigned)grid), dim3(kSpThreads), 0, st, out, n, x);
+    return hipGetLastError();
+}
+
+// live entries (|quantValues[bin]| > 1e-8) of a restored payload, for toAuto's dense / sparse choice
+__global__ __launch_bounds__(kSpThreads) void k_count_live(const int32_t* __restrict__ bins, int64_t n,
+                                                           const double* __restrict__ qv, int nq,
+                                                           unsigned long long* __restrict__ count) {
+    uint64_t c = 0;
+    for (int64_t i = (int64_t)blockIdx.x * kSpThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kSpThreads) {
+        const int32_t b = bins[i];
+        c += (b >= 0 && b < nq && fabs(qv[b]) > 1e-8) ? 1u : 0u;
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) c += __shfl_xor(c, off, 64);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(count, (unsigned long long)c);
+}
+hipError_t launch_count_live(hipStream_t st, const int32_t* bins, int64_t n, const double* qv, int nq,
+                             uint64_t* count) {
+    hipError_t e = hipMemsetAsync(count, 0, sizeof(uint64_t), st);
+    if (e != hipSuccess || n <= 0) return e;
+    const int64_t grid = std::min<int64_t>(sp_tiles(n, kSpThreads * 8), 4096);
+    hipLaunchKernelGGL(k_count_live, dim3((unsigned)grid), dim3(kSpThreads), 0, st, bins, n, qv, nq,
+                       reinterpret_cast<unsigned long long*>(count));
+    return hipGetLastError();
+}
+
+// sum_out[keys[i]] += quantValues[bins[i]] (|v| > 1e-8 only when live_only): the add step of the
+// two-pass path (payloads whose toAuto may pick the dense form)
+// One thread per pair in index order is not required: keys are unique within a payload.
+__global__ __launch_bounds__(kSpThreads) void k_add_pairs(const int32_t* __restrict__ keys,
+                                                          const int32_t* __restrict__ bins, int64_t n,
+                                                          const double* __restrict__ qv, int nq,
+                                                          double* __restrict__ out, int64_t dim,
+                                                          unsigned* __restrict__ err, int live_only) {
+    for (int64_t i = (int64_t)blockIdx.x * kSpThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kSpThreads) {
+        const int32_t k = keys[i], b = bins[i];
+        if (k < 0 || (int64_t)k >= dim || b < 0 || b >= nq) {
+            atomicOr(err, 1u);
+            continue;
+        }
+        const double v = qv[b];
+        if (live_only && !(fabs(v) > 1e-8)) continue;
+        out[k] += v;
+    }
+}
+hipError_t launch_add_pairs(hipStream_t st, const int32_t* keys, const int32_t* bins, int64_t n, const double* qv,
+                            int nq, double* out, int64_t dim, unsigned* err, int live_only) {
+    if (n <= 0) return hipSuccess;
+    const int64_t grid = std::min<int64_t>(sp_tiles(n, kSpThreads * 4), 8192);
+    hipLaunchKernelGGL(k_add_pairs, dim3((unsigned)grid), dim3(kSpThreads), 0, st, keys, bins, n, qv, nq, out, dim,
+                       err, live_only);
     return hipGetLastError();
 }
 

@@ -567,7 +567,18 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const void* vals, bool f64, int6
 }
 
 // DeltaAdaptive decode of all groups + MinMax query: grouped keys/bins into gk/gb.
-int decode_groups(skml_ctx* c, const skml_sparse* s, int32_t* gk, int32_t* gb, bool query) {
+// sum != nullptr: the last step adds quantValues[bin] into the dense double sum instead of
+// storing (key, bin) (DenseDoubleGradient.plusBy of one payload; k_dec_keys summing mode)
+struct SumTarget {
+    const double* qv;
+    int nq;
+    double* out;
+    int64_t dim;
+    unsigned* err;
+    int live_only;
+};
+int decode_groups(skml_ctx* c, const skml_sparse* s, int32_t* gk, int32_t* gb, bool query,
+                  const SumTarget* sum = nullptr) {
     hipStream_t st = ctx_stream(c);
     const SpGroups& G = s->g;
     const int64_t n = s->nnz;
@@ -595,7 +606,11 @@ int decode_groups(skml_ctx* c, const skml_sparse* s, int32_t* gk, int32_t* gb, b
     SP_HIP(launch_dec_deltas(st, s->delta_words, s->n_delta_words, dlen, n, s->g_dev, ts, delta, ts2));
     if (int e = scan_tiles(c, ts2, tiles, 1, nullptr)) return e;
     SP_HIP(launch_group_prefix(st, delta, n, s->g_dev, G.G, ts2, gpre));
-    SP_HIP(launch_dec_keys(st, delta, n, s->g_dev, ts2, gpre, query ? s->tables : nullptr, gk, gb));
+    if (sum)
+        SP_HIP(launch_dec_keys(st, delta, n, s->g_dev, ts2, gpre, s->tables, nullptr, nullptr, sum->qv, sum->nq,
+                               sum->out, sum->dim, sum->err, sum->live_only));
+    else
+        SP_HIP(launch_dec_keys(st, delta, n, s->g_dev, ts2, gpre, query ? s->tables : nullptr, gk, gb));
     return SKML_OK;
 }
 
@@ -1431,6 +1446,287 @@ int skml_sparse_restore_bins(skml_ctx* c, const skml_sparse* s, int32_t* keys_de
     if (int e = decode_groups(c, s, gk, gb, true)) return e;
     if (int e = merge_groups(c, s, gk, gb, keys_dev, bins_dev)) return e;
     SP_HIP(hipStreamSynchronize(st));
+    return SKML_OK;
+}
+
+// ---- exchange: one contiguous device blob per payload (SpBlobHeader, skml_sparse.h) ----
+}  // extern "C"
+
+namespace {
+struct BlobLayout {
+    size_t off_groups, off_quant, off_values, off_tables, off_flags, off_deltas, total;
+    int32_t quant_bytes;
+};
+BlobLayout blob_layout(const skml_sparse* s) {
+    BlobLayout L;
+    L.quant_bytes = (int32_t)(kHeaderBytes + sizeof(double) * (size_t)std::max(s->hdr.bin_num - 1, 0));
+    L.off_groups = 256;
+    L.off_quant = L.off_groups + align_up(sizeof(SpGroups), 256);
+    L.off_values = L.off_quant + align_up((size_t)L.quant_bytes, 256);
+    L.off_tables = L.off_values + align_up(sizeof(double) * std::max<size_t>(s->qvalues.size(), 1), 256);
+    L.off_flags = L.off_tables + align_up(sizeof(int32_t) * (size_t)std::max<int64_t>(s->ncells, 1), 256);
+    L.off_deltas = L.off_flags + align_up(sizeof(uint64_t) * (size_t)s->n_flag_words, 256);
+    L.total = L.off_deltas + align_up(sizeof(uint64_t) * (size_t)s->n_delta_words, 256);
+    return L;
+}
+
+// A blob's group table, checked for the invariants the decode kernels index by (a corrupt or
+// foreign blob must fail here, not fault on the device).
+int check_blob_groups(const SpBlobHeader& h, const SpGroups& G) {
+    auto bad = [](const char* what) { return sfail(SKML_E_ARG, "sparse blob: inconsistent %s", what); };
+    if (G.G < 1 || G.G > kMaxGroups || G.rows < 0 || G.rows > kMaxRows) return bad("group / row count");
+    if (G.bin_num < 1 || G.bin_num > h.nvalues || G.zero < 0 || G.zero >= G.bin_num) return bad("bins");
+    if (G.gstart[0] != 0 || G.gstart[G.G] != h.nnz || G.fb[0] != 0 || G.db[0] != 0) return bad("stream starts");
+    if (G.fb[G.G] != h.flag_bits || G.db[G.G] != h.delta_bits || G.ncells != h.ncells) return bad("stream totals");
+    if (h.n_flag_words < (h.flag_bits + 63) / 64 + 1 || h.n_delta_words < (h.delta_bits + 63) / 64 + 1)
+        return bad("word counts");
+    int32_t k1 = 0;
+    for (int g = 0; g < G.G; g++) {
+        if (G.gstart[g + 1] < G.gstart[g] || G.fb[g + 1] < G.fb[g] || G.db[g + 1] < G.db[g]) return bad("offsets");
+        const int64_t size = G.gstart[g + 1] - G.gstart[g];
+        const int32_t m = G.m[g];
+        if (m != 1 && m != 2 && m != 4 && m != 8 && m != 16) return bad("numIntervals");
+        if (G.kind[g] != 0 && G.kind[g] != 1) return bad("flagKind");
+        if (G.kind1_before[g] != k1) return bad("unary counts");
+        if (G.kind[g]) k1 += (int32_t)size;
+        if (size == 0) continue;
+        if (G.cols[g] < 1 || G.tab_off[g] < 0 || G.tab_off[g] + (int64_t)G.rows * G.cols[g] > G.ncells)
+            return bad("table shape");
+        if (G.inv_cols[g] != 1.0 / (double)G.cols[g]) return bad("column reciprocal");
+        for (int r = 0; r < G.rows; r++)
+            if (G.hash_ids[g][r] < 0 || G.hash_ids[g][r] > 7) return bad("hash id");
+    }
+    return SKML_OK;
+}
+
+// The host meta of a blob at `dev` (header, group table, quantizer header + splits, values), read
+// with one device-to-host copy, and a non-owning skml_sparse view of its device sections.
+int blob_meta(skml_ctx* c, const uint8_t* dev, size_t len, SpBlobHeader* h, skml_sparse* view) {
+    if (!dev || len < 256 || (reinterpret_cast<uintptr_t>(dev) & 255))
+        return sfail(SKML_E_ARG, "sparse blob: NULL, shorter than its header or not 256-byte aligned");
+    if (int e = sync_to_host(c, h, dev, sizeof(*h))) return e;
+    if (h->magic != kSpBlobMagic || h->version != 1) return sfail(SKML_E_STATE, "not a sparse blob");
+    const size_t meta_end = (size_t)h->off_tables;
+    if (h->total_bytes < 256 || (size_t)h->total_bytes > len || h->nnz < 0 || h->nnz > INT32_MAX || h->ncells < 0 ||
+        h->nvalues < 1 || h->nvalues > SKML_MAX_BINS || h->quant_bytes < kHeaderBytes ||
+        h->off_groups != 256 || h->off_quant < h->off_groups + (int64_t)sizeof(SpGroups) ||
+        h->off_values < h->off_quant + h->quant_bytes || h->off_tables < h->off_values + 8 * (int64_t)h->nvalues ||
+        h->off_flags < h->off_tables + 4 * h->ncells || h->off_deltas < h->off_flags + 8 * h->n_flag_words ||
+        h->total_bytes < h->off_deltas + 8 * h->n_delta_words || (h->off_tables | h->off_flags | h->off_deltas) & 255)
+        return sfail(SKML_E_ARG, "sparse blob: inconsistent section offsets");
+    std::vector<uint8_t> meta(meta_end);
+    if (int e = sync_to_host(c, meta.data(), dev, meta_end)) return e;
+    std::memcpy(&view->g, meta.data() + h->off_groups, sizeof(SpGroups));
+    if (int e = check_blob_groups(*h, view->g)) return e;
+    std::memcpy(&view->hdr, meta.data() + h->off_quant, sizeof(skml_dense_header));
+    const double* sp = reinterpret_cast<const double*>(meta.data() + h->off_quant + kHeaderBytes);
+    const int ns = (h->quant_bytes - kHeaderBytes) / 8;
+    view->splits.assign(sp, sp + ns);
+    const double* qv = reinterpret_cast<const double*>(meta.data() + h->off_values);
+    view->qvalues.assign(qv, qv + h->nvalues);
+    view->device = ctx_device(c);
+    view->nnz = h->nnz;
+    view->params = h->params;
+    view->ncells = h->ncells;
+    view->flag_bits = h->flag_bits;
+    view->delta_bits = h->delta_bits;
+    view->n_flag_words = h->n_flag_words;
+    view->n_delta_words = h->n_delta_words;
+    view->g_dev = reinterpret_cast<SpGroups*>(const_cast<uint8_t*>(dev) + h->off_groups);
+    view->tables = reinterpret_cast<int32_t*>(const_cast<uint8_t*>(dev) + h->off_tables);
+    view->flag_words = reinterpret_cast<uint64_t*>(const_cast<uint8_t*>(dev) + h->off_flags);
+    view->delta_words = reinterpret_cast<uint64_t*>(const_cast<uint8_t*>(dev) + h->off_deltas);
+    return SKML_OK;
+}
+
+// a view points into memory it does not own: cleared before it goes out of scope, so no later
+// change to skml_sparse's destruction can free the caller's blob
+struct ViewGuard {
+    skml_sparse* v;
+    ~ViewGuard() {
+        v->g_dev = nullptr;
+        v->tables = nullptr;
+        v->flag_words = v->delta_words = nullptr;
+        v->qpayload = nullptr;
+    }
+};
+}  // namespace
+
+extern "C" {
+
+int skml_sparse_export_bytes(const skml_sparse* s, size_t* bytes) {
+    if (!s || !bytes) return sfail(SKML_E_ARG, "NULL argument");
+    *bytes = blob_layout(s).total;
+    return SKML_OK;
+}
+
+int skml_sparse_export(skml_ctx* c, const skml_sparse* s, void* dst, size_t cap) {
+    if (!c || !s || !dst || (reinterpret_cast<uintptr_t>(dst) & 255)) return sfail(SKML_E_ARG, "bad export arguments");
+    const BlobLayout L = blob_layout(s);
+    if (cap < L.total) return sfail(SKML_E_ARG, "export capacity %zu < %zu", cap, L.total);
+    SP_HIP(hipSetDevice(ctx_device(c)));
+    hipStream_t st = ctx_stream(c);
+    // the host-side sections go through the context's pinned staging in one copy
+    const size_t host_bytes = L.off_tables;
+    uint8_t* pin = static_cast<uint8_t*>(ctx_pinned(c, host_bytes));
+    if (!pin) return sfail(SKML_E_OOM, "pinned staging");
+    SP_HIP(hipStreamSynchronize(st));  // the staging buffer may still feed an earlier copy
+    std::memset(pin, 0, host_bytes);
+    SpBlobHeader h{};
+    h.magic = kSpBlobMagic;
+    h.version = 1;
+    h.total_bytes = (int64_t)L.total;
+    h.nnz = s->nnz;
+    h.ncells = s->ncells;
+    h.n_flag_words = s->n_flag_words;
+    h.n_delta_words = s->n_delta_words;
+    h.flag_bits = s->flag_bits;
+    h.delta_bits = s->delta_bits;
+    h.nvalues = (int32_t)s->qvalues.size();
+    h.quant_bytes = L.quant_bytes;
+    h.off_groups = (int64_t)L.off_groups;
+    h.off_quant = (int64_t)L.off_quant;
+    h.off_values = (int64_t)L.off_values;
+    h.off_tables = (int64_t)L.off_tables;
+    h.off_flags = (int64_t)L.off_flags;
+    h.off_deltas = (int64_t)L.off_deltas;
+    h.params = s->params;
+    std::memcpy(pin, &h, sizeof(h));
+    SpGroups g = s->g;
+    for (int k = 0; k < kMaxGroups; k++) g.inv_cols[k] = g.cols[k] > 0 ? 1.0 / (double)g.cols[k] : 0.0;
+    std::memcpy(pin + L.off_groups, &g, sizeof(g));
+    std::memcpy(pin + L.off_quant, &s->hdr, sizeof(skml_dense_header));
+    if (!s->splits.empty())
+        std::memcpy(pin + L.off_quant + kHeaderBytes, s->splits.data(), sizeof(double) * s->splits.size());
+    if (!s->qvalues.empty()) std::memcpy(pin + L.off_values, s->qvalues.data(), sizeof(double) * s->qvalues.size());
+    uint8_t* d = static_cast<uint8_t*>(dst);
+    SP_HIP(hipMemcpyAsync(d, pin, host_bytes, hipMemcpyHostToDevice, st));
+    if (s->ncells > 0)
+        SP_HIP(hipMemcpyAsync(d + L.off_tables, s->tables, sizeof(int32_t) * (size_t)s->ncells, hipMemcpyDeviceToDevice, st));
+    if (s->n_flag_words > 0)
+        SP_HIP(hipMemcpyAsync(d + L.off_flags, s->flag_words, sizeof(uint64_t) * (size_t)s->n_flag_words,
+                              hipMemcpyDeviceToDevice, st));
+    if (s->n_delta_words > 0)
+        SP_HIP(hipMemcpyAsync(d + L.off_deltas, s->delta_words, sizeof(uint64_t) * (size_t)s->n_delta_words,
+                              hipMemcpyDeviceToDevice, st));
+    return SKML_OK;
+}
+
+int skml_sparse_import(skml_ctx* c, const void* blob, size_t len, skml_sparse** out) {
+    if (!c || !out) return sfail(SKML_E_ARG, "bad import arguments");
+    *out = nullptr;
+    SP_HIP(hipSetDevice(ctx_device(c)));
+    hipStream_t st = ctx_stream(c);
+    SpBlobHeader h;
+    skml_sparse view;
+    ViewGuard vg{&view};
+    if (int e = blob_meta(c, static_cast<const uint8_t*>(blob), len, &h, &view)) return e;
+    // an owned copy: the caller's gathered buffer may be reused by the next exchange
+    skml_sparse* s = new skml_sparse();
+    s->device = view.device;
+    s->nnz = view.nnz;
+    s->params = view.params;
+    s->hdr = view.hdr;
+    s->splits = view.splits;
+    s->qvalues = view.qvalues;
+    s->g = view.g;
+    s->ncells = view.ncells;
+    s->flag_bits = view.flag_bits;
+    s->delta_bits = view.delta_bits;
+    s->n_flag_words = view.n_flag_words;
+    s->n_delta_words = view.n_delta_words;
+    const size_t o_tab = align_up(sizeof(SpGroups), 256);
+    const size_t o_fw = o_tab + align_up(sizeof(int32_t) * (size_t)std::max<int64_t>(s->ncells, 1), 256);
+    const size_t o_dw = o_fw + align_up(sizeof(uint64_t) * (size_t)s->n_flag_words, 256);
+    const size_t total = o_dw + sizeof(uint64_t) * (size_t)s->n_delta_words;
+    char* blk = static_cast<char*>(block_get(s->device, total, &s->block_cap));
+    if (!blk) {
+        sparse_release(s);
+        return sfail(SKML_E_OOM, "imported sparse payload of %zu bytes", total);
+    }
+    s->block = blk;
+    s->g_dev = reinterpret_cast<SpGroups*>(blk);
+    s->tables = reinterpret_cast<int32_t*>(blk + o_tab);
+    s->flag_words = reinterpret_cast<uint64_t*>(blk + o_fw);
+    s->delta_words = reinterpret_cast<uint64_t*>(blk + o_dw);
+    auto fail_rel = [&](int e) {
+        (void)hipStreamSynchronize(st);
+        sparse_release(s);
+        return e;
+    };
+#define IMP_HIP(expr)                                                                                        \
+    do {                                                                                                     \
+        hipError_t e_ = (expr);                                                                              \
+        if (e_ != hipSuccess) return fail_rel(sfail(SKML_E_HIP, "%s failed: %s", #expr, hipGetErrorString(e_))); \
+    } while (0)
+    IMP_HIP(hipMemcpyAsync(s->g_dev, view.g_dev, sizeof(SpGroups), hipMemcpyDeviceToDevice, st));
+    if (s->ncells > 0)
+        IMP_HIP(hipMemcpyAsync(s->tables, view.tables, sizeof(int32_t) * (size_t)s->ncells, hipMemcpyDeviceToDevice, st));
+    if (s->n_flag_words > 0)
+        IMP_HIP(hipMemcpyAsync(s->flag_words, view.flag_words, sizeof(uint64_t) * (size_t)s->n_flag_words,
+                               hipMemcpyDeviceToDevice, st));
+    if (s->n_delta_words > 0)
+        IMP_HIP(hipMemcpyAsync(s->delta_words, view.delta_words, sizeof(uint64_t) * (size_t)s->n_delta_words,
+                               hipMemcpyDeviceToDevice, st));
+    IMP_HIP(hipStreamSynchronize(st));
+#undef IMP_HIP
+    *out = s;
+    return SKML_OK;
+}
+
+// Gradient.sum over P exported sparse payloads (ml/gradient/Gradient.scala:44-49): out = +0.0,
+// then for p = 0..P-1 in order DenseDoubleGradient.plusBy(payload p .toAuto)
+// (DenseDoubleGradient.scala:38; SketchGradient.toSparse -> SparseDoubleGradient.toAuto), then
+// out *= scale unless scale == 1.  A payload whose live count (|v| > 1e-8) exceeds dim * 2 / 3 (Java
+// int arithmetic) reaches plusBy in dense form: only its live values are added, and every entry
+// takes the dense form's + 0.0.
+int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t stride, int64_t dim, double scale,
+                               double* out) {
+    if (!c || !blobs || P < 1 || dim < 0 || dim > (int64_t)INT32_MAX || (dim > 0 && !out) || stride % 256)
+        return sfail(SKML_E_ARG, "bad sparse decode_sum arguments (P >= 1, 256-byte stride, dim in Java int)");
+    SP_HIP(hipSetDevice(ctx_device(c)));
+    hipStream_t st = ctx_stream(c);
+    std::vector<SpBlobHeader> hs((size_t)P);
+    std::vector<skml_sparse> views((size_t)P);  // non-owning: skml_sparse frees nothing on destruction
+    for (int p = 0; p < P; p++) {
+        if (int e = blob_meta(c, static_cast<const uint8_t*>(blobs) + (size_t)p * stride, stride, &hs[(size_t)p],
+                              &views[(size_t)p]))
+            return sfail(e, "payload %d: %s", p, skml_last_error());
+    }
+    uint8_t* small = scratch<uint8_t>(c, kSlotStatus, 1024);
+    if (!small) return sfail(SKML_E_OOM, "decode_sum scratch");
+    unsigned* err = reinterpret_cast<unsigned*>(small);
+    uint64_t* live = reinterpret_cast<uint64_t*>(small + 256);
+    SP_HIP(hipMemsetAsync(err, 0, sizeof(unsigned), st));
+    if (dim > 0) SP_HIP(hipMemsetAsync(out, 0, sizeof(double) * (size_t)dim, st));
+    const int64_t lim = (int64_t)(int32_t)((uint32_t)dim * 2u) / 3;  // dim * 2 / 3 with Java int wrap
+    for (int p = 0; p < P; p++) {
+        const skml_sparse& v = views[(size_t)p];
+        if (v.nnz == 0) continue;  // an empty restore adds nothing (its toAuto is sparse)
+        const double* qv = reinterpret_cast<const double*>(static_cast<const uint8_t*>(blobs) + (size_t)p * stride +
+                                                           hs[(size_t)p].off_values);
+        const int nq = (int)v.qvalues.size();
+        if (v.nnz <= lim) {  // live <= nnz <= dim * 2 / 3: toAuto keeps the sparse form
+            SumTarget t{qv, nq, out, dim, err, 0};
+            if (int e = decode_groups(c, &v, nullptr, nullptr, true, &t)) return e;
+            continue;
+        }
+        // the live count decides: restore into scratch, count, add in the chosen form
+        int32_t* gk = scratch<int32_t>(c, kSlotGKeys, (size_t)v.nnz);
+        int32_t* gb = scratch<int32_t>(c, kSlotGBins, (size_t)v.nnz);
+        if (!gk || !gb) return sfail(SKML_E_OOM, "decode_sum scratch");
+        if (int e = decode_groups(c, &v, gk, gb, true)) return e;
+        SP_HIP(launch_count_live(st, gb, v.nnz, qv, nq, live));
+        uint64_t nlive = 0;
+        if (int e = sync_to_host(c, &nlive, live, sizeof(nlive))) return e;
+        const bool dense_form = (int64_t)nlive > lim;
+        if (dense_form) SP_HIP(launch_sum_add_zero(st, out, dim));
+        SP_HIP(launch_add_pairs(st, gk, gb, v.nnz, qv, nq, out, dim, err, dense_form ? 1 : 0));
+    }
+    if (scale != 1.0) SP_HIP(launch_scale(st, out, dim, scale));
+    unsigned bad = 0;
+    if (int e = sync_to_host(c, &bad, err, sizeof(bad))) return e;
+    if (bad) return sfail(SKML_E_ARG, "a payload holds a key outside [0, %lld) or a bin outside its values", (long long)dim);
     return SKML_OK;
 }
 

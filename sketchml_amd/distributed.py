@@ -95,6 +95,52 @@ class PayloadExchange:
             pass
 
 
+def blob_stride(sizes: list[int]) -> int:
+    """Slot size of the padded all-gather: the largest payload, rounded up to 256 bytes (every
+    slot, and so every blob, stays 256-byte aligned)."""
+    return max(256, (max(sizes) + 255) // 256 * 256)
+
+
+def gather_blobs(local: torch.Tensor, stride: int, group=None, exchange: Optional[PayloadExchange] = None):
+    """All-gather of one `stride`-byte slot per rank (a blob padded to the agreed stride): rank r's
+    slot lands at r * stride.  RCCL through `exchange` (or the nccl process group); a host-memory
+    group (gloo) goes through host copies."""
+    world = dist.get_world_size(group)
+    if local.numel() * local.element_size() != stride:
+        raise ValueError("the local slot must be exactly `stride` bytes")
+    allb = torch.empty(stride * world, dtype=torch.uint8, device=local.device)
+    if exchange is not None:
+        # the communicator's context may run on its own stream: the slot is complete before the
+        # all-gather reads it, and the gathered blobs before the caller's stream uses them
+        torch.cuda.current_stream(local.device).synchronize()
+        exchange.allgather(local, stride, allb)
+        check(_lib.lib.skml_ctx_sync(exchange._ctx), "ctx_sync")
+    elif dist.get_backend(group) == "nccl":
+        dist.all_gather_into_tensor(allb, local.view(torch.uint8), group=group)
+    else:
+        parts = [torch.empty(stride, dtype=torch.uint8) for _ in range(world)]
+        dist.all_gather(parts, local.view(torch.uint8).cpu(), group=group)
+        allb.copy_(torch.cat(parts).to(local.device))
+    return allb
+
+
+def exchange_sparse(payload, dim: int, group=None, exchange: Optional[PayloadExchange] = None,
+                    scale: float | None = None):
+    """One DP step of the ml path on P GPUs (GeneralizedLinearModel.scala:145-156): the sizes are
+    all-gathered, every rank exports its compressed sparse gradient straight into a slot of the
+    largest size, the slots are all-gathered (RCCL over xGMI), and every rank computes Gradient.sum
+    of all P payloads (rank order) and the 1/P average, in double, on its own GPU.
+    Returns (the dense double average, the gathered blobs, stride)."""
+    from .sparse import decode_sum as _sparse_decode_sum
+    world = dist.get_world_size(group)
+    stride = blob_stride(agree_sizes(payload.export_bytes(), group))
+    local = torch.empty(stride, dtype=torch.uint8, device=torch.device("cuda", payload.device))
+    payload.export(local)
+    allb = gather_blobs(local, stride, group, exchange)
+    avg = _sparse_decode_sum(allb, world, stride, dim, 1.0 / world if scale is None else scale)
+    return avg, allb, stride
+
+
 def decode_sum(ctx_handle, payloads: torch.Tensor, nranks: int, stride: int, n: int, scale: float,
                out: torch.Tensor) -> None:
     """Fused decode of `nranks` gathered payloads + double-precision sum + scale

@@ -139,6 +139,35 @@ class SparsePayload:
     def times_by(self, x: float) -> None:
         check(_lib.lib.skml_sparse_times_by(self.handle, float(x)), "sparse_times_by")
 
+    def export_bytes(self) -> int:
+        n = C.c_size_t()
+        check(_lib.lib.skml_sparse_export_bytes(self.handle, C.byref(n)), "sparse_export_bytes")
+        return n.value
+
+    def export(self, out: torch.Tensor | None = None) -> torch.Tensor:
+        """The payload as one relocatable device blob (skml_sparse_export; the unit the RCCL
+        all-gather moves).  `out`: a 256-byte aligned uint8 device tensor of >= export_bytes()."""
+        nb = self.export_bytes()
+        if out is None:
+            out = torch.empty(nb, dtype=torch.uint8, device=torch.device("cuda", self.device))
+        if out.numel() * out.element_size() < nb:
+            raise SketchMLException(f"export buffer of {out.numel()} bytes < {nb}")
+        check(_lib.lib.skml_sparse_export(self._ctx().handle, self.handle, C.c_void_p(out.data_ptr()), nb),
+              "sparse_export")
+        return out
+
+    @classmethod
+    def from_blob(cls, blob: torch.Tensor, nbytes: int | None = None) -> "SparsePayload":
+        """skml_sparse_import: an owned payload from a blob in device memory (checked first)."""
+        dev = blob.device.index
+        h = C.c_void_p()
+        n = blob.numel() * blob.element_size() if nbytes is None else int(nbytes)
+        check(_lib.lib.skml_sparse_import(get_context(dev).handle, C.c_void_p(blob.data_ptr()), n, C.byref(h)),
+              "sparse_import")
+        pl = cls(h, dev, 0)
+        pl.rows = int(np.frombuffer(blob[256 + 4: 256 + 8].cpu().numpy().tobytes(), dtype=np.int32)[0])
+        return pl
+
     def __del__(self):
         try:
             if self.handle:
@@ -146,6 +175,20 @@ class SparsePayload:
                 self.handle = None
         except Exception:
             pass
+
+
+def decode_sum(blobs: torch.Tensor, nblobs: int, stride: int, dim: int, scale: float = 1.0,
+               out: torch.Tensor | None = None) -> torch.Tensor:
+    """Gradient.sum (ml/gradient/Gradient.scala:44-49) of `nblobs` exported sparse payloads laid out
+    `stride` bytes apart: a float64 dense sum of length dim, payloads added in order (then scaled
+    when scale != 1).  skml_sparse_decode_sum_f64."""
+    dev = blobs.device
+    if out is None:
+        out = torch.empty(max(int(dim), 1), dtype=torch.float64, device=dev)
+    check(_lib.lib.skml_sparse_decode_sum_f64(get_context(dev.index).handle, C.c_void_p(blobs.data_ptr()),
+                                              int(nblobs), int(stride), int(dim), float(scale),
+                                              C.c_void_p(out.data_ptr())), "sparse_decode_sum")
+    return out[: int(dim)]
 
 
 def _as_device(t, dtype, device=None):

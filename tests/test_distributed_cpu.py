@@ -66,3 +66,43 @@ def test_parallel_slices_are_the_parallelquantize_slicing(n, world):
     sizes = parallel_slices(n, world)
     assert sum(sizes) == n and all(s == n // world for s in sizes[:-1])
     assert sizes == [hi - lo for lo, hi in (shard_range(n, world, r) for r in range(world))]
+
+
+def _blob_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from sketchml_amd import distributed as D
+        nbytes = 1000 + 700 * rank                      # variable-size payloads
+        stride = D.blob_stride(D.agree_sizes(nbytes))
+        local = torch.zeros(stride, dtype=torch.uint8)
+        local[:nbytes] = (rank + 1) % 256
+        allb = D.gather_blobs(local, stride)
+        q.put((rank, stride, allb.numpy().copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_padded_blob_gather():
+    """Sparse payloads differ in size: sizes are agreed first, each rank's blob goes in a slot of
+    the largest size rounded to 256 bytes, and slot r holds rank r's bytes on every rank."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_blob_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    stride = (1700 + 255) // 256 * 256
+    for rank, st, allb in res:
+        assert st == stride and len(allb) == world * stride
+        for r in range(world):
+            n = 1000 + 700 * r
+            assert (allb[r * stride: r * stride + n] == r + 1).all()
+            assert (allb[r * stride + n: (r + 1) * stride] == 0).all()

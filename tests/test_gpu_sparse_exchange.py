@@ -1,0 +1,177 @@
+"""The ml path's DP exchange of sparse gradients on one GPU.
+
+- export / import: one contiguous device blob per payload (skml_sparse_export / _import) that
+  round-trips to the same restore() and the same writeObject stream; corrupt blobs are refused.
+- Gradient.sum (ml/gradient/Gradient.scala:44-49) of P payloads, skml_sparse_decode_sum_f64:
+  bit-exact against the oracle's restore() of each payload summed in double, payload by payload,
+  with SparseDoubleGradient.toAuto's dense/sparse rule (DenseDoubleGradient.plusBy).
+- the RCCL path with a world-1 communicator: sizes agreed, blob exported into its padded slot,
+  all-gathered, summed.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+EPS = 1e-8
+
+
+def _java_lim(dim):
+    """dim * 2 / 3 in Java int arithmetic (DenseDoubleGradient / SparseDoubleGradient.toAuto)."""
+    v = (dim * 2) & 0xFFFFFFFF
+    v = v - (1 << 32) if v >= 1 << 31 else v
+    return int(v / 3)
+
+
+def oracle_sum(osps, dim, scale=1.0):
+    """Gradient.sum over the oracle's payloads: DenseDoubleGradient(dim), then plusBy(p.toAuto) in
+    order; returns (sum, forms) where forms[p] is 'dense' or 'sparse'."""
+    out = np.zeros(dim, dtype=np.float64)
+    forms = []
+    for osp in osps:
+        k, b = osp.restore()
+        v = osp.q.values()[b]
+        live = np.abs(v) > EPS
+        if int(live.sum()) > _java_lim(dim):      # SparseDoubleGradient.toDense: live values only
+            out = out + 0.0
+            out[k[live]] += v[live]
+            forms.append("dense")
+        else:
+            out[k] += v
+            forms.append("sparse")
+    if scale != 1.0:
+        out = out * scale
+    return out, forms
+
+
+def _payload(gpu, dim, density, seed, bins=256, tiny=0.0):
+    rng = np.random.default_rng(seed)
+    keys = np.nonzero(rng.random(dim) < density)[0].astype(np.int32)
+    vals = rng.standard_normal(len(keys))
+    if tiny:
+        t = rng.random(len(keys)) < tiny
+        vals[t] = rng.uniform(-3e-9, 3e-9, int(t.sum()))
+    pl = gpu.encode_sparse(torch.from_numpy(keys).cuda(), torch.from_numpy(vals).cuda(), bins, 8, 2, 0.3, seed,
+                           seed + 100)
+    osp = O.sparse_compress(keys, vals, bins, 8, 2, 0.3, seed, seed + 100)
+    return pl, osp
+
+
+def _gather_local(payloads):
+    """The all-gather's output layout on one GPU: slot p = payload p's blob, stride = the largest."""
+    from sketchml_amd.distributed import blob_stride
+    sizes = [p.export_bytes() for p in payloads]
+    stride = blob_stride(sizes)
+    allb = torch.zeros(stride * len(payloads), dtype=torch.uint8, device="cuda")
+    for i, p in enumerate(payloads):
+        p.export(allb[i * stride:(i + 1) * stride])
+    return allb, stride
+
+
+def test_export_import_round_trip(gpu):
+    pl, osp = _payload(gpu, 300000, 0.15, 1)
+    blob = pl.export()
+    assert blob.numel() == pl.export_bytes() and blob.numel() % 256 == 0
+    back = gpu.SparsePayload.from_blob(blob)
+    blob.fill_(0)                                 # the import owns its copy
+    k0, b0 = pl.restore_bins()
+    k1, b1 = back.restore_bins()
+    assert torch.equal(k0, k1) and torch.equal(b0, b1)
+    _, v1 = back.restore(torch.float64)
+    ok, ob = osp.restore()
+    assert np.array_equal(v1.cpu().numpy(), osp.q.values()[ob])
+    assert back.serialize() == pl.serialize()     # writeObject of the imported payload is the same stream
+    h0, s0 = pl.quant_header()
+    h1, s1 = back.quant_header()
+    assert (h0.bin_num, h0.zero_idx, h0.min, h0.max) == (h1.bin_num, h1.zero_idx, h1.min, h1.max)
+    assert np.array_equal(s0, s1)
+    pl.times_by(0.5)                              # quantValues travel timesBy'd
+    back2 = gpu.SparsePayload.from_blob(pl.export())
+    _, v2 = back2.restore(torch.float64)
+    assert np.array_equal(v2.cpu().numpy(), (osp.q.values() * 0.5)[ob])
+
+
+def test_corrupt_blobs_are_refused(gpu):
+    pl, _ = _payload(gpu, 50000, 0.2, 2)
+    blob = pl.export()
+    bad = blob.clone()
+    bad[0] ^= 0xFF                                # magic
+    with pytest.raises(gpu.SketchMLException):
+        gpu.SparsePayload.from_blob(bad)
+    bad = blob.clone()
+    G = 8
+    off = 256 + 280 + 8 * G                       # SpGroups.gstart[G] (the total) inside the blob
+    bad[off:off + 8] = torch.tensor(np.array([123456789], dtype=np.int64).view(np.uint8), device="cuda")
+    with pytest.raises(gpu.SketchMLException, match="inconsistent"):
+        gpu.SparsePayload.from_blob(bad)
+    with pytest.raises(gpu.SketchMLException):    # shorter than the blob says
+        gpu.SparsePayload.from_blob(blob, 1024)
+    # a key beyond the sum's dimension (SparseDoubleGradient's bound check)
+    with pytest.raises(gpu.SketchMLException, match="outside"):
+        gpu.decode_sum(blob, 1, blob.numel(), 1000)
+
+
+def test_decode_sum_eight_payloads_matches_oracle(gpu):
+    dim = 2**20 + 5
+    pls, osps = zip(*[_payload(gpu, dim, 0.1 + 0.02 * p, 10 + p) for p in range(8)])
+    allb, stride = _gather_local(pls)
+    got = gpu.decode_sum(allb, 8, stride, dim).cpu().numpy()
+    want, forms = oracle_sum(osps, dim)
+    assert set(forms) == {"sparse"}
+    assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
+    got_avg = gpu.decode_sum(allb, 8, stride, dim, 1.0 / 8).cpu().numpy()
+    assert np.array_equal(got_avg.view(np.uint64), (want * (1.0 / 8)).view(np.uint64))
+
+
+def test_decode_sum_dense_form_payloads(gpu):
+    """Payloads with more than dim * 2 / 3 live values reach plusBy in dense form: bucket values with
+    |v| <= 1e-8 (the tiny cluster's midpoints) are not added."""
+    dim = 30011
+    p0, o0 = _payload(gpu, dim, 0.97, 21, tiny=0.15)    # dense form
+    p1, o1 = _payload(gpu, dim, 0.3, 22, tiny=0.5)      # sparse form: its tiny values are added
+    p2, o2 = _payload(gpu, dim, 0.95, 23, tiny=0.12)    # dense again
+    allb, stride = _gather_local([p0, p1, p2])
+    got = gpu.decode_sum(allb, 3, stride, dim).cpu().numpy()
+    want, forms = oracle_sum([o0, o1, o2], dim)
+    assert forms == ["dense", "sparse", "dense"]
+    assert np.any(np.abs(o1.q.values()) <= EPS)          # the tiny values really exist
+    assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
+
+
+def test_decode_sum_skips_empty_payloads(gpu):
+    dim = 4096
+    empty = gpu.encode_sparse(torch.zeros(0, dtype=torch.int32).cuda(), torch.zeros(0, dtype=torch.float64).cuda())
+    p1, o1 = _payload(gpu, dim, 0.2, 31)
+    allb, stride = _gather_local([empty, p1])
+    got = gpu.decode_sum(allb, 2, stride, dim).cpu().numpy()
+    want, _ = oracle_sum([o1], dim)
+    assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
+
+
+def test_sparse_exchange_world1_rccl(gpu):
+    """distributed.exchange_sparse over a world-1 group with the RCCL communicator
+    (PayloadExchange): sizes, the padded slot, the all-gather, the sum and 1/P."""
+    import torch.distributed as dist
+    from sketchml_amd import distributed as D
+    store = dist.HashStore()
+    dist.init_process_group("gloo", store=store, rank=0, world_size=1)
+    try:
+        dim = 700001
+        pl, osp = _payload(gpu, dim, 0.1, 41)
+        ex = D.PayloadExchange(gpu.get_context().handle)
+        try:
+            avg, allb, stride = D.exchange_sparse(pl, dim, exchange=ex)
+            torch.cuda.synchronize()
+        finally:
+            ex.close()
+        assert stride % 256 == 0 and stride >= pl.export_bytes()
+        assert torch.equal(allb[: pl.export_bytes()], pl.export())
+        want, _ = oracle_sum([osp], dim)
+        assert np.array_equal(avg.cpu().numpy().view(np.uint64), want.view(np.uint64))
+    finally:
+        dist.destroy_process_group()
