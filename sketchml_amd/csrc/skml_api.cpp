@@ -1166,8 +1166,11 @@ int skml_dense_decode_sum_f32(skml_ctx* c, const void* payloads, int32_t P, size
             skml_dense_payload_bytes(n, h[p].req_bins) > stride)
             return fail(SKML_E_ARG, "payload %d: inconsistent header or larger than the stride %zu", p, stride);
     }
+    int common_bits = h[0].code_bits;
+    for (int p = 1; p < P; p++)
+        if (h[p].code_bits != common_bits) common_bits = 0;
     KernelTimer kt(c, SKML_K_DECODE_SUM);
-    HIP_TRY(launch_decode_sum(c->stream, payloads, P, stride, out, n, scale));
+    HIP_TRY(launch_decode_sum(c->stream, payloads, P, stride, out, n, scale, common_bits));
     return SKML_OK;
 }
 

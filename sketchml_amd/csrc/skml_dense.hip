@@ -139,7 +139,7 @@ __device__ __forceinline__ void quant_tiles(const QuantTables& q, const float* _
 
 // Dynamic LDS: [0, 32 KB) bucket bases, then `lds_splits` floats (LUT mode); Eytzinger mode
 // reuses the start of the same buffer (P <= 4096 floats).
-__global__ __launch_bounds__(kQThreads) void k_quantize(const float* __restrict__ x, int64_t n,
+__global__ __launch_bounds__(kQThreads) __attribute__((amdgpu_waves_per_eu(8))) void k_quantize(const float* __restrict__ x, int64_t n,
                                                         uint8_t* __restrict__ payload,
                                                         const QuantLut* __restrict__ lut, int lds_splits) {
     extern __shared__ __align__(16) uint8_t qsm[];
@@ -324,10 +324,47 @@ hipError_t launch_decode(hipStream_t st, const void* payload, float* out, int64_
 // the midpoint from the payload's splits, as k_decode does above kLutMax.
 constexpr int kMaxSumPayloads = 16;
 constexpr int kSumLutBins = 256;
-// The payload headers are read once per workgroup into LDS (codes pointer, code width, LUT row);
-// each wave then owns 1024-element tiles as k_decode does: per payload four 4-code reads per
-// lane (256 contiguous code bytes per wave-instruction at 8 bits), 16 double accumulators per lane
-// added in payload order, and four nontemporal float4 stores.
+// 16 consecutive codes of one payload starting at e0 (a multiple of 16): one load of 2..32 bytes.
+__device__ __forceinline__ void load_codes16(const uint8_t* codes, int64_t e0, int bits, uint32_t (&w)[8]) {
+    switch (bits) {
+        case 8: {
+            const uint4 v = *reinterpret_cast<const uint4*>(codes + e0);
+            w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+            break;
+        }
+        case 16: {
+            const uint4 a = *reinterpret_cast<const uint4*>(codes + 2 * e0);
+            const uint4 b = *reinterpret_cast<const uint4*>(codes + 2 * e0 + 16);
+            w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w; w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+            break;
+        }
+        case 4: {
+            const uint2 v = *reinterpret_cast<const uint2*>(codes + e0 / 2);
+            w[0] = v.x; w[1] = v.y;
+            break;
+        }
+        case 2: w[0] = *reinterpret_cast<const uint32_t*>(codes + e0 / 4); break;
+        default: w[0] = *reinterpret_cast<const uint16_t*>(codes + e0 / 8); break;
+    }
+}
+__device__ __forceinline__ uint32_t code16_at(const uint32_t (&w)[8], int e, int bits) {
+    switch (bits) {
+        case 8: return (w[e >> 2] >> (8 * (e & 3))) & 255u;
+        case 16: return (w[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
+        case 4: return (w[e >> 3] >> (4 * (e & 7))) & 15u;
+        case 2: return (w[0] >> (2 * e)) & 3u;
+        default: return (w[0] >> e) & 1u;
+    }
+}
+
+// The payload headers are read once per workgroup into LDS (codes pointer, code width, LUT row).
+// Each lane owns 16 consecutive elements per step: it issues the code loads of up to 8 payloads
+// first (one 16-byte load per payload at 8 bits), then adds their LUT values in payload order
+// into 16 double accumulators (Gradient.sum adds doubles in gradient order), the next 8 payloads
+// likewise, and stores 64 contiguous bytes of fp32 (nontemporal).  BITS: the code width when all
+// payloads share it (the common case: one bin count), 0 = per payload.
+constexpr int kSumChunk = 8;
+template <int BITS>
 __global__ __launch_bounds__(256) void k_decode_sum(const uint8_t* __restrict__ payloads, int P,
                                                     size_t stride, float* __restrict__ out, int64_t n,
                                                     double scale) {
@@ -348,43 +385,47 @@ __global__ __launch_bounds__(256) void k_decode_sum(const uint8_t* __restrict__ 
             for (int b = threadIdx.x; b < h->bin_num; b += 256) lut[p][b] = lut_value(h, sp, b);
     }
     __syncthreads();
-    const int lane = threadIdx.x & 63;
-    const int64_t nw = (int64_t)gridDim.x * 4, wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int64_t full = n / 1024;
-    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    bool all_lds = true;
+    for (int p = 0; p < P; p++) all_lds &= s_lds[p] != 0;
     auto value = [&](int p, uint32_t c) -> double {
-        if (s_lds[p]) return lut[p][c];
+        if (all_lds || s_lds[p]) return lut[p][c];
         const uint8_t* pl = payloads + (size_t)p * stride;
         return lut_value(reinterpret_cast<const skml_dense_header*>(pl),
                          reinterpret_cast<const double*>(pl + kHeaderBytes), (int)c);
     };
-    for (int64_t tile = wid; tile < full; tile += nw) {
-        double acc[4][4];
+    const int64_t full = n / 16;
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    for (int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x; g < full; g += (int64_t)gridDim.x * 256) {
+        const int64_t e0 = g * 16;
+        double acc[16];
 #pragma unroll
-        for (int j = 0; j < 4; j++)
+        for (int e = 0; e < 16; e++) acc[e] = 0.0;
+        for (int p0 = 0; p0 < P; p0 += kSumChunk) {
+            uint32_t w[kSumChunk][8];
 #pragma unroll
-            for (int e = 0; e < 4; e++) acc[j][e] = 0.0;
-        for (int p = 0; p < P; p++) {
-            const int bits = __builtin_amdgcn_readfirstlane(s_bits[p]);
-            const uint8_t* codes = s_codes[p];
-            uint32_t c[4][4];
+            for (int q = 0; q < kSumChunk; q++)
+                if (p0 + q < P)
+                    load_codes16(s_codes[p0 + q], e0, BITS ? BITS : __builtin_amdgcn_readfirstlane(s_bits[p0 + q]),
+                                 w[q]);
 #pragma unroll
-            for (int j = 0; j < 4; j++) read_codes4(codes, tile * 1024 + j * 256 + lane * 4, bits, c[j]);
+            for (int q = 0; q < kSumChunk; q++) {
+                if (p0 + q >= P) break;
+                const int bits = BITS ? BITS : __builtin_amdgcn_readfirstlane(s_bits[p0 + q]);
 #pragma unroll
-            for (int j = 0; j < 4; j++)
-#pragma unroll
-                for (int e = 0; e < 4; e++) acc[j][e] += value(p, c[j][e]);
+                for (int e = 0; e < 16; e++) acc[e] += value(p0 + q, code16_at(w[q], e, bits));
+            }
         }
-        f32x4* dst = reinterpret_cast<f32x4*>(out + tile * 1024);
+        f32x4* dst = reinterpret_cast<f32x4*>(out + e0);
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            const f32x4 o = {(float)(acc[j][0] * scale), (float)(acc[j][1] * scale), (float)(acc[j][2] * scale),
-                             (float)(acc[j][3] * scale)};
-            __builtin_nontemporal_store(o, dst + j * 64 + lane);
+            const f32x4 o = {(float)(acc[4 * j] * scale), (float)(acc[4 * j + 1] * scale),
+                             (float)(acc[4 * j + 2] * scale), (float)(acc[4 * j + 3] * scale)};
+            __builtin_nontemporal_store(o, dst + j);
         }
     }
-    if (wid == full % nw) {
-        for (int64_t e = full * 1024 + lane; e < n; e += 64) {
+    if (blockIdx.x == 0 && threadIdx.x < 16) {  // the last n % 16 elements
+        const int64_t e = full * 16 + threadIdx.x;
+        if (e < n) {
             double a = 0.0;
             for (int p = 0; p < P; p++) a += value(p, read_code(s_codes[p], e, s_bits[p]));
             out[e] = (float)(a * scale);
@@ -393,11 +434,19 @@ __global__ __launch_bounds__(256) void k_decode_sum(const uint8_t* __restrict__ 
 }
 
 hipError_t launch_decode_sum(hipStream_t st, const void* payloads, int P, size_t stride, float* out,
-                             int64_t n, double scale) {
+                             int64_t n, double scale, int common_bits) {
     if (n <= 0) return hipSuccess;
     if (P < 1 || P > kMaxSumPayloads) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_decode_sum, dim3(quant_grid(n)), dim3(256), 0, st,
-                       reinterpret_cast<const uint8_t*>(payloads), P, stride, out, n, scale);
+    const int64_t groups = n / 16;
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((groups + 255) / 256, 2048));
+    const uint8_t* pl = reinterpret_cast<const uint8_t*>(payloads);
+    switch (common_bits) {
+        case 8: hipLaunchKernelGGL(k_decode_sum<8>, dim3(grid), dim3(256), 0, st, pl, P, stride, out, n, scale); break;
+        case 2: hipLaunchKernelGGL(k_decode_sum<2>, dim3(grid), dim3(256), 0, st, pl, P, stride, out, n, scale); break;
+        case 4: hipLaunchKernelGGL(k_decode_sum<4>, dim3(grid), dim3(256), 0, st, pl, P, stride, out, n, scale); break;
+        case 1: hipLaunchKernelGGL(k_decode_sum<1>, dim3(grid), dim3(256), 0, st, pl, P, stride, out, n, scale); break;
+        default: hipLaunchKernelGGL(k_decode_sum<0>, dim3(grid), dim3(256), 0, st, pl, P, stride, out, n, scale); break;
+    }
     return hipGetLastError();
 }
 
