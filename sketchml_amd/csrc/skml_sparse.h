@@ -49,7 +49,7 @@ constexpr int kSpTile = 2048;             // elements per workgroup tile (8 per 
 constexpr int kCompactTile = 16384;       // dense elements per compaction tile (64 per thread)
 constexpr int kDeltaHist = 33;            // bitsNeeded in 1..32
 
-inline int64_t sp_tiles(int64_t n, int64_t tile) { return (n + tile - 1) / tile; }
+__host__ __device__ inline int64_t sp_tiles(int64_t n, int64_t tile) { return (n + tile - 1) / tile; }
 
 // ---- launchers (skml_sparse.hip) ----
 // Device-side encode plan (one workgroup each, no host round trip):
@@ -204,13 +204,53 @@ hipError_t launch_huff_decode_write(hipStream_t st, int nseg, const HuffSeg* seg
                                     const uint64_t* off, int32_t* table, unsigned* err);
 hipError_t launch_fill_i32(hipStream_t st, int32_t* dst, int64_t n, int32_t v);
 
+// ---- the GroupedMinMaxSketch field stream on the device (skml_wire.hip) ----
+struct WireSrc {
+    const uint64_t* flags;   // concatenated DeltaAdaptive flag bits
+    const uint64_t* deltas;  // concatenated DeltaAdaptive delta bits
+    const uint64_t* huff;    // concatenated HuffmanEncoder code bits of the tables
+};
+struct WireSec {          // one long array of the stream
+    int64_t dst;          // byte offset of its first long in the stream
+    int64_t bit0, nbits;  // its bit range in the source stream
+    int64_t nwords;       // longs written (BitSet.toLongArray: trailing zero words trimmed)
+    int32_t src;          // 0 flags, 1 deltas, 2 Huffman
+    int32_t pad;
+};
+constexpr int kWireMaxSec = 3 * kMaxGroups;
+hipError_t launch_wire_lastnz(hipStream_t st, const WireSrc& src, const WireSec* secs, int nsec, uint64_t* nz);
+hipError_t launch_wire_longs(hipStream_t st, const WireSrc& src, const WireSec* secs, const int64_t* npre, int nsec,
+                             int64_t total_words, uint8_t* wire);
+hipError_t launch_wire_pieces(hipStream_t st, const uint8_t* small, const int64_t* pieces, int npieces, uint8_t* wire);
+struct RdFlagSec {   // one group's stored flag long array in the device copy of the stream
+    int64_t pos;     // byte offset of its first long
+    int64_t nstored; // longs stored
+    int64_t nbits;   // fixed flags: size * nf (the bits that hold fields)
+    int64_t size;    // keys of the group
+    int32_t nf;      // fixed flags: bits per field
+    int32_t pad;
+};
+struct RdBitSec {
+    int64_t pos, nstored;
+};
+hipError_t launch_rd_fixed_sum(hipStream_t st, const uint8_t* stream, const RdFlagSec* secs, const int64_t* wpre, int nsec,
+                               int64_t total_words, uint64_t* sums);
+constexpr int64_t kRdTileWords = 2048;  // k_rd_unary_tiles' words per tile
+// tpre: per-section prefix of ceil(nstored / kRdTileWords) tiles; flen[s] = bit length of its `size` unary flags
+hipError_t launch_rd_unary(hipStream_t st, const uint8_t* stream, const RdFlagSec* secs, const int64_t* tpre, int nsec,
+                           int64_t total_tiles, uint32_t* tile_zeros, int64_t* flen);
+hipError_t launch_rd_stream(hipStream_t st, const uint8_t* stream, const RdBitSec* secs, const int64_t* off, int G,
+                            int64_t nwords, uint64_t* out);
+hipError_t launch_rd_words(hipStream_t st, const uint8_t* stream, const int64_t* pos, const int64_t* wpre, int nsec,
+                           int64_t total_words, uint64_t* words);
+
 // ---- context services (skml_api.cpp) ----
 hipStream_t ctx_stream(skml_ctx* c);
 // the context's side stream (a high-priority child context) and two events for a fork / join
 int ctx_side_fork(skml_ctx* c, hipStream_t* side, hipEvent_t* fork, hipEvent_t* join);
 int ctx_device(skml_ctx* c);
 // grow-only device scratch buffer `slot` (< kScratchSlots) of at least `bytes`; null on failure
-constexpr int kScratchSlots = 16;
+constexpr int kScratchSlots = 20;
 void* ctx_scratch(skml_ctx* c, int slot, size_t bytes);
 // pinned host staging of at least `bytes`
 void* ctx_pinned(skml_ctx* c, size_t bytes);

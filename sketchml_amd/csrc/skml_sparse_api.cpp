@@ -58,6 +58,8 @@ enum {
     kSlotCKeys,     // toSparse output of skml_sparse_encode_f32
     kSlotCVals,
     kSlotDeltaEnc,  // standalone DeltaAdaptiveEncoder: group table + stream words
+    kSlotWire,      // readObject: the device copy of the field stream
+    kSlotWireMeta,  // the wire kernels' section tables and small results
 };
 static_assert(kSlotDeltaEnc < kScratchSlots, "scratch slots");
 
@@ -242,7 +244,8 @@ struct skml_sparse {
     std::vector<int64_t> huff_bit0, huff_bits;      // per group stream range
     uint64_t* huff_words = nullptr;
     int64_t n_huff_words = 0;
-    std::vector<uint8_t> wire;  // the serialised field stream (built once; the payload is immutable)
+    void* wire_dev = nullptr;   // the serialised field stream on the device (built once; the
+    size_t wire_bytes = 0;      // encoded state is immutable: timesBy scales quantValues only)
 };
 
 namespace {
@@ -339,6 +342,7 @@ void sparse_release(skml_sparse* s) {
         if (s->delta_words) (void)hipFree(s->delta_words);
     }
     if (s->huff_words) (void)hipFree(s->huff_words);
+    if (s->wire_dev) (void)hipFree(s->wire_dev);
     delete s;
 }
 
@@ -910,69 +914,92 @@ static int build_huffman(skml_ctx* c, skml_sparse* s) {
 }
 
 namespace {
-struct BeWriter {
-    std::vector<uint8_t> b;
-    void u(uint64_t v, int n) {
-        for (int i = n - 1; i >= 0; i--) b.push_back((uint8_t)(v >> (8 * i)));
+// Host layout of the field stream: small fields are appended to `small` and form pieces of the
+// stream; a long array leaves a gap of 8 * nwords bytes that k_wire_longs fills on the device.
+struct WireBuilder {
+    std::vector<uint8_t> small;
+    std::vector<int64_t> pieces;  // {small offset, stream offset, length} triples
+    int64_t total = 0;
+    bool open = false;
+    void put(uint64_t v, int n) {
+        if (!open) {
+            pieces.push_back((int64_t)small.size());
+            pieces.push_back(total);
+            pieces.push_back(0);
+            open = true;
+        }
+        for (int i = n - 1; i >= 0; i--) small.push_back((uint8_t)(v >> (8 * i)));
+        pieces.back() += n;
+        total += n;
     }
-    void i32(int32_t v) { u((uint32_t)v, 4); }
-    void i64(int64_t v) { u((uint64_t)v, 8); }
+    void i32(int32_t v) { put((uint32_t)v, 4); }
     void f64(double d) {
         uint64_t x;
         std::memcpy(&x, &d, 8);
-        u(x, 8);
+        put(x, 8);
     }
-    void byte(int v) { b.push_back((uint8_t)v); }
-    // a long[] body: big-endian words appended in one resize
-    void longs(const std::vector<uint64_t>& v) {
-        const size_t o = b.size();
-        b.resize(o + 8 * v.size());
-        for (size_t i = 0; i < v.size(); i++) {
-            const uint64_t be = __builtin_bswap64(v[i]);
-            std::memcpy(b.data() + o + 8 * i, &be, 8);
-        }
+    void byte(int v) { put((uint8_t)v, 1); }
+    int64_t gap(int64_t bytes) {  // returns the gap's stream offset
+        open = false;
+        const int64_t at = total;
+        total += bytes;
+        return at;
     }
 };
-// BitSet.toLongArray of a device bit range (trailing zero words trimmed)
-int long_array(skml_ctx* c, const uint64_t* words, int64_t b0, int64_t nbits, std::vector<uint64_t>& out) {
-    out.assign((size_t)((nbits + 63) / 64), 0);
-    if (int e = extract_bits(c, words, b0, nbits, out.data())) return e;
-    while (!out.empty() && out.back() == 0) out.pop_back();
-    return SKML_OK;
-}
-}  // namespace
 
-// GroupedMinMaxSketch.writeObject field order (GroupedMinMaxSketch.java:148-158) with
-// MinMaxSketch.writeObject (MinMaxSketch.java:88-97), HuffmanEncoder.writeObject
-// (HuffmanEncoder.java:168-190) and DeltaAdaptiveEncoder.writeObject (:148-170); big-endian
-// DataOutput primitives; a 1-byte presence flag stands where Java writes a null object, and each
-// Int2IntHash object is (int HashFactory index, int size, int BKDR seed or 0).
-int skml_sparse_serialize(skml_ctx* c, const skml_sparse* cs, uint8_t* buf, size_t cap, size_t* written) {
-    if (!c || !cs) return sfail(SKML_E_ARG, "bad serialise arguments");
-    SP_HIP(hipSetDevice(ctx_device(c)));
-    skml_sparse* s = const_cast<skml_sparse*>(cs);  // the Huffman streams and the bytes are lazily built caches
-    if (!s->wire.empty()) {
-        if (written) *written = s->wire.size();
-        if (!buf) return SKML_OK;
-        if (cap < s->wire.size()) return sfail(SKML_E_ARG, "buffer capacity %zu < %zu", cap, s->wire.size());
-        std::memcpy(buf, s->wire.data(), s->wire.size());
-        return SKML_OK;
-    }
+// The device field stream of a payload (cached in s->wire_dev): Huffman codes of the tables,
+// the trims of every long array (one small read-back), the layout on the host, then two kernels.
+int build_wire(skml_ctx* c, skml_sparse* s) {
     if (int e = build_huffman(c, s)) return e;
-    static const int32_t kBkdrSeed[8] = {0, 0, 0, 31, 131, 267, 1313, 13131};
+    hipStream_t st = ctx_stream(c);
     const SpGroups& G = s->g;
-    BeWriter w;
-    w.b.reserve((size_t)(8 * (s->n_flag_words + s->n_delta_words + s->n_huff_words) + 4096));
+    static const int32_t kBkdrSeed[8] = {0, 0, 0, 31, 131, 267, 1313, 13131};
+    // the long arrays in stream order: every present sketch's Huffman words, then every present
+    // encoder's flag and delta words
+    std::vector<WireSec> secs;
+    std::vector<int> present;
+    for (int g = 0; g < G.G; g++)
+        if (G.gstart[g + 1] > G.gstart[g]) present.push_back(g);
+    for (int g : present) secs.push_back(WireSec{0, s->huff_bit0[(size_t)g], s->huff_bits[(size_t)g], 0, 2, 0});
+    for (int g : present) {
+        secs.push_back(WireSec{0, G.fb[g], G.fb[g + 1] - G.fb[g], 0, 0, 0});
+        secs.push_back(WireSec{0, G.db[g], G.db[g + 1] - G.db[g], 0, 1, 0});
+    }
+    const int nsec = (int)secs.size();
+    std::vector<int64_t> wpre((size_t)nsec + 1, 0);
+    for (int k = 0; k < nsec; k++) wpre[(size_t)k + 1] = wpre[(size_t)k] + (secs[(size_t)k].nbits + 63) / 64;
+    const WireSrc src{s->flag_words, s->delta_words, s->huff_words};
+    // section tables and the trims in one scratch block: secs | wpre | nz | npre
+    const size_t o_pre = align_up(sizeof(WireSec) * (size_t)std::max(nsec, 1), 256);
+    const size_t o_nz = o_pre + align_up(sizeof(int64_t) * ((size_t)nsec + 1), 256);
+    const size_t o_npre = o_nz + align_up(sizeof(uint64_t) * (size_t)std::max(nsec, 1), 256);
+    const size_t meta_bytes = o_npre + sizeof(int64_t) * ((size_t)nsec + 1);
+    uint8_t* meta = scratch<uint8_t>(c, kSlotWireMeta, meta_bytes);
+    if (!meta) return sfail(SKML_E_OOM, "wire scratch");
+    WireSec* d_secs = reinterpret_cast<WireSec*>(meta);
+    int64_t* d_pre = reinterpret_cast<int64_t*>(meta + o_pre);
+    uint64_t* d_nz = reinterpret_cast<uint64_t*>(meta + o_nz);
+    int64_t* d_npre = reinterpret_cast<int64_t*>(meta + o_npre);
+    std::vector<uint64_t> nz((size_t)nsec, 0);
+    if (nsec > 0) {
+        SP_HIP(hipMemcpyAsync(d_secs, secs.data(), sizeof(WireSec) * (size_t)nsec, hipMemcpyHostToDevice, st));
+        SP_HIP(hipMemcpyAsync(d_pre, wpre.data(), sizeof(int64_t) * wpre.size(), hipMemcpyHostToDevice, st));
+        SP_HIP(hipMemsetAsync(d_nz, 0, sizeof(uint64_t) * (size_t)nsec, st));
+        SP_HIP(launch_wire_lastnz(st, src, d_secs, nsec, d_nz));
+        if (int e = sync_to_host(c, nz.data(), d_nz, sizeof(uint64_t) * (size_t)nsec)) return e;
+    }
+    // the layout (GroupedMinMaxSketch.writeObject field order, see skml_sparse_serialize)
+    WireBuilder w;
     w.i32(G.G);
     w.i32(G.rows);
     w.f64(s->params.col_ratio);
     w.i32(G.bin_num);
     w.i32(G.zero);
-    std::vector<uint64_t> longs;
+    int k = 0;
     for (int g = 0; g < G.G; g++) {  // sketches
-        const bool present = G.gstart[g + 1] > G.gstart[g];
-        w.byte(present ? 1 : 0);
-        if (!present) continue;
+        const bool pres = G.gstart[g + 1] > G.gstart[g];
+        w.byte(pres ? 1 : 0);
+        if (!pres) continue;
         w.i32(G.rows);
         w.i32(G.cols[g]);
         w.i32(G.zero);
@@ -988,30 +1015,83 @@ int skml_sparse_serialize(skml_ctx* c, const skml_sparse* cs, uint8_t* buf, size
             w.i32(it.bits);
             w.i32(it.nbits);
         }
-        if (int e = long_array(c, s->huff_words, s->huff_bit0[(size_t)g], s->huff_bits[(size_t)g], longs)) return e;
-        w.i32((int32_t)longs.size());
-        w.longs(longs);
+        WireSec& sc = secs[(size_t)k++];
+        sc.nwords = (int64_t)nz[(size_t)(&sc - secs.data())];
+        w.i32((int32_t)sc.nwords);
+        sc.dst = w.gap(8 * sc.nwords);
         w.i32(G.rows * G.cols[g]);
     }
     for (int g = 0; g < G.G; g++) {  // encoders
-        const bool present = G.gstart[g + 1] > G.gstart[g];
-        w.byte(present ? 1 : 0);
-        if (!present) continue;
+        const bool pres = G.gstart[g + 1] > G.gstart[g];
+        w.byte(pres ? 1 : 0);
+        if (!pres) continue;
         w.i32((int32_t)(G.gstart[g + 1] - G.gstart[g]));
         w.i32(G.m[g]);
         w.byte(G.kind[g] ? 1 : 0);
-        if (int e = long_array(c, s->flag_words, G.fb[g], G.fb[g + 1] - G.fb[g], longs)) return e;
-        w.i32((int32_t)longs.size());
-        w.longs(longs);
-        if (int e = long_array(c, s->delta_words, G.db[g], G.db[g + 1] - G.db[g], longs)) return e;
-        w.i32((int32_t)longs.size());
-        w.longs(longs);
+        for (int t = 0; t < 2; t++) {
+            WireSec& sc = secs[(size_t)k];
+            sc.nwords = (int64_t)nz[(size_t)k];
+            k++;
+            w.i32((int32_t)sc.nwords);
+            sc.dst = w.gap(8 * sc.nwords);
+        }
     }
-    s->wire.swap(w.b);
-    if (written) *written = s->wire.size();
+    std::vector<int64_t> npre((size_t)nsec + 1, 0);
+    for (int q = 0; q < nsec; q++) npre[(size_t)q + 1] = npre[(size_t)q] + secs[(size_t)q].nwords;
+    // the stream: the small fields' pieces, then the long arrays
+    void* wire = nullptr;
+    SP_HIP(hipMalloc(&wire, (size_t)std::max<int64_t>(w.total, 1)));
+    const int npieces = (int)(w.pieces.size() / 3);
+    const size_t o_pcs = align_up(w.small.size(), 256);
+    uint8_t* sm = scratch<uint8_t>(c, kSlotSmall, o_pcs + sizeof(int64_t) * w.pieces.size() + 8);
+    if (!sm) {
+        (void)hipFree(wire);
+        return sfail(SKML_E_OOM, "wire scratch");
+    }
+    auto fail_free = [&](int e) {
+        (void)hipStreamSynchronize(st);
+        (void)hipFree(wire);
+        return e;
+    };
+#define W_HIP(expr)                                                                                         \
+    do {                                                                                                    \
+        hipError_t e_ = (expr);                                                                             \
+        if (e_ != hipSuccess) return fail_free(sfail(SKML_E_HIP, "%s failed: %s", #expr, hipGetErrorString(e_))); \
+    } while (0)
+    if (!w.small.empty()) W_HIP(hipMemcpyAsync(sm, w.small.data(), w.small.size(), hipMemcpyHostToDevice, st));
+    if (npieces > 0)
+        W_HIP(hipMemcpyAsync(sm + o_pcs, w.pieces.data(), sizeof(int64_t) * w.pieces.size(), hipMemcpyHostToDevice, st));
+    if (nsec > 0) {
+        W_HIP(hipMemcpyAsync(d_secs, secs.data(), sizeof(WireSec) * (size_t)nsec, hipMemcpyHostToDevice, st));
+        W_HIP(hipMemcpyAsync(d_npre, npre.data(), sizeof(int64_t) * npre.size(), hipMemcpyHostToDevice, st));
+    }
+    W_HIP(launch_wire_pieces(st, sm, reinterpret_cast<const int64_t*>(sm + o_pcs), npieces, static_cast<uint8_t*>(wire)));
+    if (nsec > 0) W_HIP(launch_wire_longs(st, src, d_secs, d_npre, nsec, npre.back(), static_cast<uint8_t*>(wire)));
+    W_HIP(hipStreamSynchronize(st));  // the host vectors above are the copies' sources
+#undef W_HIP
+    s->wire_dev = wire;
+    s->wire_bytes = (size_t)w.total;
+    return SKML_OK;
+}
+}  // namespace
+
+// GroupedMinMaxSketch.writeObject field order (GroupedMinMaxSketch.java:148-158) with
+// MinMaxSketch.writeObject (MinMaxSketch.java:88-97), HuffmanEncoder.writeObject
+// (HuffmanEncoder.java:168-190) and DeltaAdaptiveEncoder.writeObject (:148-170); big-endian
+// DataOutput primitives; a 1-byte presence flag stands where Java writes a null object, and each
+// Int2IntHash object is (int HashFactory index, int size, int BKDR seed or 0).  Assembled on the
+// device (skml_wire.hip) and copied out once.
+int skml_sparse_serialize(skml_ctx* c, const skml_sparse* cs, uint8_t* buf, size_t cap, size_t* written) {
+    if (!c || !cs) return sfail(SKML_E_ARG, "bad serialise arguments");
+    SP_HIP(hipSetDevice(ctx_device(c)));
+    skml_sparse* s = const_cast<skml_sparse*>(cs);  // the Huffman streams and the wire are lazily built caches
+    if (!s->wire_dev)
+        if (int e = build_wire(c, s)) return e;
+    if (written) *written = s->wire_bytes;
     if (!buf) return SKML_OK;
-    if (cap < s->wire.size()) return sfail(SKML_E_ARG, "buffer capacity %zu < %zu", cap, s->wire.size());
-    std::memcpy(buf, s->wire.data(), s->wire.size());
+    if (cap < s->wire_bytes) return sfail(SKML_E_ARG, "buffer capacity %zu < %zu", cap, s->wire_bytes);
+    SP_HIP(hipMemcpyAsync(buf, s->wire_dev, s->wire_bytes, hipMemcpyDeviceToHost, ctx_stream(c)));
+    SP_HIP(hipStreamSynchronize(ctx_stream(c)));
     return SKML_OK;
 }
 
@@ -1039,17 +1119,14 @@ struct BeReader {
         return d;
     }
     int byte() { return (int)u(1); }
-    bool longs(std::vector<uint64_t>& v, size_t count) {
-        if (i + 8 * count > n) {
+    // a long[] body: its byte position, the contents stay in the stream (read on the device)
+    bool skip_longs(size_t count, int64_t* pos) {
+        if (count > (n - i) / 8) {
             bad = true;
+            i = n;
             return false;
         }
-        v.resize(count);
-        for (size_t k = 0; k < count; k++) {
-            uint64_t be;
-            std::memcpy(&be, p + i + 8 * k, 8);
-            v[k] = __builtin_bswap64(be);
-        }
+        *pos = (int64_t)i;
         i += 8 * count;
         return true;
     }
@@ -1057,60 +1134,9 @@ struct BeReader {
 
 struct HuffGroupIn {
     std::vector<HuffItem> items;
-    std::vector<uint64_t> longs;
+    int64_t pos = 0, nlongs = 0;  // the HuffmanEncoder's long[] in the stream
     int64_t size = 0;
 };
-
-// Sum of the nf-bit MSB-first fields (BinaryUtils.getBits order) in bits [0, nbits) of a BitSet:
-// sum over k of 2^(nf-1-k) * popcount of the bits at positions = k (mod nf).
-int64_t bit_fields_sum(const std::vector<uint64_t>& w, int64_t nbits, int nf) {
-    if (nf == 0 || nbits == 0) return 0;
-    int64_t sum = 0;
-    const int64_t nw = std::min<int64_t>((int64_t)w.size(), (nbits + 63) / 64);
-    for (int64_t i = 0; i < nw; i++) {
-        uint64_t word = w[(size_t)i];
-        const int64_t hi = nbits - i * 64;
-        if (hi < 64) word &= (1ull << hi) - 1ull;
-        const int phase = (int)((i * 64) % nf);
-        for (int k = 0; k < nf; k++) {
-            uint64_t mask = 0;
-            for (int b = (k - phase + nf) % nf; b < 64; b += nf) mask |= 1ull << b;
-            sum += (int64_t)__builtin_popcountll(word & mask) << (nf - 1 - k);
-        }
-    }
-    return sum;
-}
-
-// Bit length of `size` unary flags (ones closed by a zero); zeros past the stored words are the
-// trimmed tail of the BitSet.
-int64_t unary_flags_length(const std::vector<uint64_t>& w, int64_t size) {
-    if (size <= 0) return 0;
-    int64_t zeros = 0;
-    for (size_t i = 0; i < w.size(); i++) {
-        const int64_t z = 64 - __builtin_popcountll(w[i]);
-        if (zeros + z >= size) {
-            uint64_t inv = ~w[i];
-            for (int64_t k = zeros; k < size - 1; k++) inv &= inv - 1;  // drop the zeros before the last one
-            return (int64_t)i * 64 + __builtin_ctzll(inv) + 1;
-        }
-        zeros += z;
-    }
-    return (int64_t)w.size() * 64 + (size - zeros);
-}
-
-// out[bit0, bit0 + nbits) = src[0, nbits) (src words past its end read as zero; out is zeroed).
-void put_bit_range(std::vector<uint64_t>& out, int64_t bit0, const std::vector<uint64_t>& src, int64_t nbits) {
-    const int sh = (int)(bit0 & 63);
-    const int64_t w0 = bit0 >> 6;
-    const int64_t nsrc = std::min<int64_t>((int64_t)src.size(), (nbits + 63) / 64);
-    for (int64_t i = 0; i < nsrc; i++) {
-        uint64_t v = src[(size_t)i];
-        const int64_t hi = nbits - i * 64;
-        if (hi < 64) v &= (1ull << hi) - 1ull;
-        out[(size_t)(w0 + i)] |= v << sh;
-        if (sh && (size_t)(w0 + i + 1) < out.size()) out[(size_t)(w0 + i + 1)] |= v >> (64 - sh);
-    }
-}
 
 // Decode tables of one group's HuffmanEncoder items (HuffmanEncoder.java:131-152 builds the same
 // tree): codes of <= kHuffLutBits bits fill their LUT ranges, longer codes end in tree nodes.
@@ -1236,25 +1262,28 @@ int skml_sparse_deserialize(skml_ctx* c, const uint8_t* buf, size_t len, const d
             it.nbits = r.i32();
         }
         const int32_t nl = r.i32();
-        if (nl < 0 || !r.longs(h.longs, (size_t)nl)) return bail(sfail(SKML_E_ARG, "malformed Huffman bit set"));
+        if (nl < 0 || !r.skip_longs((size_t)nl, &h.pos)) return bail(sfail(SKML_E_ARG, "malformed Huffman bit set"));
+        h.nlongs = nl;
         h.size = r.i32();
         if (h.size != (int64_t)rows * cols) return bail(sfail(SKML_E_ARG, "Huffman size %lld != rows*cols", (long long)h.size));
         G.tab_off[g] = cells;
         cells += h.size;
     }
-    // DeltaAdaptiveEncoder objects.  toLongArray dropped each BitSet's trailing zero words, but
-    // the decode kernels index one contiguous stream per kind, so every group's exact bit lengths
-    // are recovered from the flags first: fixed-width flags take size * nf bits; unary flags end
-    // at the size-th zero; the deltas take bpi * sum(interval counts) bits.
-    std::vector<std::vector<uint64_t>> flags((size_t)G.G), deltas((size_t)G.G);
-    std::vector<int64_t> flen((size_t)G.G, 0), dlen((size_t)G.G, 0);
-    int64_t n = 0, fbits = 0, dbits = 0;
+    // DeltaAdaptiveEncoder objects: the small fields here, the BitSets' positions in the stream.
+    // toLongArray dropped each BitSet's trailing zero words, but the decode kernels index one
+    // contiguous stream per kind, so every group's exact bit lengths are recovered on the device
+    // (fixed-width flags: size * nf bits, and the deltas take bpi * (size + the flags' field sum);
+    // unary flags end at the size-th zero, the deltas take bpi * (that length - size)).
+    struct EncIn {
+        int32_t size = 0, nf = 0, bpi = 0;
+        int64_t fpos = 0, fn = 0, dpos = 0, dn = 0;
+    };
+    std::vector<EncIn> enc((size_t)G.G);
+    int64_t n = 0;
     int32_t k1 = 0;
     for (int g = 0; g < G.G; g++) {
         G.gstart[g] = n;
         G.kind1_before[g] = k1;
-        G.fb[g] = fbits;
-        G.db[g] = dbits;
         const int pres = r.byte();
         if (pres != present[(size_t)g]) return bail(sfail(SKML_E_ARG, "sketch / encoder presence mismatch in group %d", g));
         if (!pres) {
@@ -1262,41 +1291,101 @@ int skml_sparse_deserialize(skml_ctx* c, const uint8_t* buf, size_t len, const d
             G.kind[g] = 0;
             continue;
         }
-        const int32_t size = r.i32();
+        EncIn& e = enc[(size_t)g];
+        e.size = r.i32();
         const int32_t m = r.i32();
         G.m[g] = m;
         G.kind[g] = r.byte() ? 1 : 0;
-        if (size < 0 || (m != 1 && m != 2 && m != 4 && m != 8 && m != 16))
+        if (e.size < 0 || (m != 1 && m != 2 && m != 4 && m != 8 && m != 16))
             return bail(sfail(SKML_E_ARG, "malformed DeltaAdaptiveEncoder %d (numIntervals %d)", g, m));
-        for (auto* v : {&flags[(size_t)g], &deltas[(size_t)g]}) {
-            const int32_t nl = r.i32();
-            if (nl < 0 || !r.longs(*v, (size_t)nl)) return bail(sfail(SKML_E_ARG, "malformed BitSet"));
+        const int32_t nfl = r.i32();
+        if (nfl < 0 || !r.skip_longs((size_t)nfl, &e.fpos)) return bail(sfail(SKML_E_ARG, "malformed BitSet"));
+        const int32_t ndl = r.i32();
+        if (ndl < 0 || !r.skip_longs((size_t)ndl, &e.dpos)) return bail(sfail(SKML_E_ARG, "malformed BitSet"));
+        e.fn = nfl;
+        e.dn = ndl;
+        e.bpi = 32 / m;
+        while ((1 << (e.nf + 1)) <= m) e.nf++;  // floor(log2 m)
+        if (G.kind[g]) k1 += e.size;
+        n += e.size;
+    }
+    G.gstart[G.G] = n;
+    if (r.bad) return bail(sfail(SKML_E_ARG, "truncated GroupedMinMaxSketch stream"));
+    // the stream on the device, once
+    uint8_t* dstream = scratch<uint8_t>(c, kSlotWire, std::max<size_t>(len, 8));
+    if (!dstream) return bail(sfail(SKML_E_OOM, "device copy of the stream"));
+    SP_HIP(hipMemcpyAsync(dstream, buf, len, hipMemcpyHostToDevice, st));
+    // the flags' lengths: field sums of the fixed groups, zero selects of the unary ones
+    std::vector<RdFlagSec> fx, un;
+    std::vector<int> fx_g, un_g;
+    for (int g = 0; g < G.G; g++) {
+        if (!present[(size_t)g]) continue;
+        const EncIn& e = enc[(size_t)g];
+        RdFlagSec sc{e.fpos, e.fn, (int64_t)e.size * e.nf, e.size, e.nf, 0};
+        if (G.kind[g]) {
+            un.push_back(sc);
+            un_g.push_back(g);
+        } else if (e.nf > 0) {
+            fx.push_back(sc);
+            fx_g.push_back(g);
         }
-        const int bpi = 32 / m;
-        int nf = 0;
-        while ((1 << (nf + 1)) <= m) nf++;  // floor(log2 m)
-        const std::vector<uint64_t>& fw = flags[(size_t)g];
-        int64_t ivsum;
-        if (!G.kind[g]) {
-            flen[(size_t)g] = (int64_t)size * nf;
-            ivsum = (int64_t)size + bit_fields_sum(fw, flen[(size_t)g], nf);
-        } else {
-            flen[(size_t)g] = unary_flags_length(fw, size);
-            ivsum = flen[(size_t)g] - size;  // each flag: iv ones and a closing zero
+    }
+    std::vector<int64_t> fx_pre(fx.size() + 1, 0), un_pre(un.size() + 1, 0);
+    for (size_t q = 0; q < fx.size(); q++) fx_pre[q + 1] = fx_pre[q] + (fx[q].nbits + 63) / 64;
+    for (size_t q = 0; q < un.size(); q++) un_pre[q + 1] = un_pre[q] + (un[q].nstored + kRdTileWords - 1) / kRdTileWords;
+    const size_t nfx = fx.size(), nun = un.size();
+    const size_t o_un = align_up(sizeof(RdFlagSec) * std::max<size_t>(nfx, 1), 256);
+    const size_t o_fxp = o_un + align_up(sizeof(RdFlagSec) * std::max<size_t>(nun, 1), 256);
+    const size_t o_unp = o_fxp + align_up(sizeof(int64_t) * (nfx + 1), 256);
+    const size_t o_res = o_unp + align_up(sizeof(int64_t) * (nun + 1), 256);  // sums[nfx] | flen[nun]
+    const size_t o_tz = o_res + align_up(sizeof(int64_t) * (nfx + nun + 1), 256);
+    uint8_t* meta = scratch<uint8_t>(c, kSlotWireMeta, o_tz + sizeof(uint32_t) * (size_t)std::max<int64_t>(un_pre.back(), 1));
+    if (!meta) return bail(sfail(SKML_E_OOM, "readObject scratch"));
+    int64_t* d_res = reinterpret_cast<int64_t*>(meta + o_res);
+    std::vector<int64_t> res(nfx + nun, 0);
+    if (nfx + nun > 0) {
+        if (nfx) SP_HIP(hipMemcpyAsync(meta, fx.data(), sizeof(RdFlagSec) * nfx, hipMemcpyHostToDevice, st));
+        if (nun) SP_HIP(hipMemcpyAsync(meta + o_un, un.data(), sizeof(RdFlagSec) * nun, hipMemcpyHostToDevice, st));
+        SP_HIP(hipMemcpyAsync(meta + o_fxp, fx_pre.data(), sizeof(int64_t) * fx_pre.size(), hipMemcpyHostToDevice, st));
+        SP_HIP(hipMemcpyAsync(meta + o_unp, un_pre.data(), sizeof(int64_t) * un_pre.size(), hipMemcpyHostToDevice, st));
+        SP_HIP(hipMemsetAsync(d_res, 0, sizeof(int64_t) * (nfx + nun), st));
+        SP_HIP(launch_rd_fixed_sum(st, dstream, reinterpret_cast<const RdFlagSec*>(meta),
+                                   reinterpret_cast<const int64_t*>(meta + o_fxp), (int)nfx, fx_pre.back(),
+                                   reinterpret_cast<uint64_t*>(d_res)));
+        SP_HIP(launch_rd_unary(st, dstream, reinterpret_cast<const RdFlagSec*>(meta + o_un),
+                               reinterpret_cast<const int64_t*>(meta + o_unp), (int)nun, un_pre.back(),
+                               reinterpret_cast<uint32_t*>(meta + o_tz), d_res + nfx));
+        if (int e = sync_to_host(c, res.data(), d_res, sizeof(int64_t) * res.size())) return bail(e);
+    }
+    std::vector<int64_t> flen((size_t)G.G, 0), dlen((size_t)G.G, 0);
+    for (size_t q = 0; q < nfx; q++) {
+        const int g = fx_g[q];
+        flen[(size_t)g] = fx[q].nbits;
+        dlen[(size_t)g] = (int64_t)enc[(size_t)g].bpi * ((int64_t)enc[(size_t)g].size + res[q]);
+    }
+    for (size_t q = 0; q < nun; q++) {
+        const int g = un_g[q];
+        flen[(size_t)g] = res[nfx + q];
+        if (flen[(size_t)g] < enc[(size_t)g].size) return bail(sfail(SKML_E_ARG, "unary flags of group %d do not end", g));
+        dlen[(size_t)g] = (int64_t)enc[(size_t)g].bpi * (flen[(size_t)g] - enc[(size_t)g].size);
+    }
+    int64_t fbits = 0, dbits = 0;
+    for (int g = 0; g < G.G; g++) {
+        G.fb[g] = fbits;
+        G.db[g] = dbits;
+        if (!present[(size_t)g]) continue;
+        const EncIn& e = enc[(size_t)g];
+        if (!G.kind[g] && e.nf == 0) {  // one interval per key: no flag bits, 32-bit deltas
+            flen[(size_t)g] = 0;
+            dlen[(size_t)g] = (int64_t)e.bpi * e.size;
         }
-        dlen[(size_t)g] = (int64_t)bpi * ivsum;
-        if ((int64_t)fw.size() > (flen[(size_t)g] + 63) / 64 ||
-            (int64_t)deltas[(size_t)g].size() > (dlen[(size_t)g] + 63) / 64)
+        if (e.fn > (flen[(size_t)g] + 63) / 64 || e.dn > (dlen[(size_t)g] + 63) / 64)
             return bail(sfail(SKML_E_ARG, "DeltaAdaptiveEncoder %d holds bits past its stream", g));
         fbits += flen[(size_t)g];
         dbits += dlen[(size_t)g];
-        if (G.kind[g]) k1 += size;
-        n += size;
     }
-    G.gstart[G.G] = n;
     G.fb[G.G] = fbits;
     G.db[G.G] = dbits;
-    if (r.bad) return bail(sfail(SKML_E_ARG, "truncated GroupedMinMaxSketch stream"));
     s->nnz = n;
     s->ncells = cells;
     s->flag_bits = fbits;
@@ -1318,14 +1407,24 @@ int skml_sparse_deserialize(skml_ctx* c, const uint8_t* buf, size_t len, const d
         hipMalloc(&s->tables, sizeof(int32_t) * (size_t)std::max<int64_t>(cells, 1)) != hipSuccess)
         return bail(sfail(SKML_E_OOM, "deserialised payload"));
     {
-        std::vector<uint64_t> fw((size_t)s->n_flag_words, 0), dw((size_t)s->n_delta_words, 0);
+        std::vector<RdBitSec> fsec((size_t)G.G), dsec((size_t)G.G);
         for (int g = 0; g < G.G; g++) {
-            put_bit_range(fw, G.fb[g], flags[(size_t)g], flen[(size_t)g]);
-            put_bit_range(dw, G.db[g], deltas[(size_t)g], dlen[(size_t)g]);
+            fsec[(size_t)g] = RdBitSec{enc[(size_t)g].fpos, enc[(size_t)g].fn};
+            dsec[(size_t)g] = RdBitSec{enc[(size_t)g].dpos, enc[(size_t)g].dn};
         }
-        SP_HIP(hipMemcpyAsync(s->flag_words, fw.data(), sizeof(uint64_t) * fw.size(), hipMemcpyHostToDevice, st));
-        SP_HIP(hipMemcpyAsync(s->delta_words, dw.data(), sizeof(uint64_t) * dw.size(), hipMemcpyHostToDevice, st));
-        SP_HIP(hipStreamSynchronize(st));
+        const size_t o_d = align_up(sizeof(RdBitSec) * (size_t)G.G, 256);
+        const size_t o_fo = 2 * o_d, o_do = o_fo + align_up(sizeof(int64_t) * (size_t)(G.G + 1), 256);
+        uint8_t* m2 = scratch<uint8_t>(c, kSlotStatus, o_do + sizeof(int64_t) * (size_t)(G.G + 1));
+        if (!m2) return bail(sfail(SKML_E_OOM, "readObject scratch"));
+        SP_HIP(hipMemcpyAsync(m2, fsec.data(), sizeof(RdBitSec) * fsec.size(), hipMemcpyHostToDevice, st));
+        SP_HIP(hipMemcpyAsync(m2 + o_d, dsec.data(), sizeof(RdBitSec) * dsec.size(), hipMemcpyHostToDevice, st));
+        SP_HIP(hipMemcpyAsync(m2 + o_fo, G.fb, sizeof(int64_t) * (size_t)(G.G + 1), hipMemcpyHostToDevice, st));
+        SP_HIP(hipMemcpyAsync(m2 + o_do, G.db, sizeof(int64_t) * (size_t)(G.G + 1), hipMemcpyHostToDevice, st));
+        SP_HIP(launch_rd_stream(st, dstream, reinterpret_cast<const RdBitSec*>(m2),
+                                reinterpret_cast<const int64_t*>(m2 + o_fo), G.G, s->n_flag_words, s->flag_words));
+        SP_HIP(launch_rd_stream(st, dstream, reinterpret_cast<const RdBitSec*>(m2 + o_d),
+                                reinterpret_cast<const int64_t*>(m2 + o_do), G.G, s->n_delta_words, s->delta_words));
+        SP_HIP(hipStreamSynchronize(st));  // the host tables above are the copies' sources
     }
     if (int e = upload_groups(c, s)) return bail(e);
     // HuffmanEncoder.decode of every group's table
@@ -1334,7 +1433,7 @@ int skml_sparse_deserialize(skml_ctx* c, const uint8_t* buf, size_t len, const d
     std::vector<int64_t> starts;
     std::vector<int2> lut;
     std::vector<int4> nodes;
-    std::vector<uint64_t> words;
+    std::vector<int64_t> wpos, wpre{0};  // the groups' Huffman long[]s: stream positions, word prefix
     for (int g = 0; g < G.G; g++) {
         const HuffGroupIn& h = hg[(size_t)g];
         if (!present[(size_t)g] || h.size == 0) continue;
@@ -1344,8 +1443,8 @@ int skml_sparse_deserialize(skml_ctx* c, const uint8_t* buf, size_t len, const d
             continue;
         }
         HuffDecGroup d;
-        d.word0 = (int64_t)words.size();
-        d.nwords = (int64_t)h.longs.size();
+        d.word0 = wpre.back();
+        d.nwords = h.nlongs;
         d.tab_off = G.tab_off[g];
         d.size = h.size;
         d.lut_row = (int32_t)(lut.size() / kHuffLutSize);
@@ -1353,7 +1452,8 @@ int skml_sparse_deserialize(skml_ctx* c, const uint8_t* buf, size_t len, const d
         std::vector<int4> gn;
         if (int e = huff_tables(h.items, (int)nodes.size(), lut, gn)) return bail(e);
         nodes.insert(nodes.end(), gn.begin(), gn.end());
-        words.insert(words.end(), h.longs.begin(), h.longs.end());
+        wpos.push_back(h.pos);
+        wpre.push_back(wpre.back() + h.nlongs);
         const int64_t bits = d.nwords * 64;
         const int64_t nseg = std::max<int64_t>(1, (bits + kHuffSeg - 1) / kHuffSeg);
         for (int64_t k = 0; k < nseg; k++) {
@@ -1370,7 +1470,7 @@ int skml_sparse_deserialize(skml_ctx* c, const uint8_t* buf, size_t len, const d
     const int ns = (int)segs.size();
     if (ns > 0) {
         if (nodes.empty()) nodes.push_back(int4{-1, -1, 0, 0});
-        words.push_back(0);
+        const size_t nwords_all = (size_t)wpre.back() + 1;  // + a zero word read past the last one
         // one device block: groups, segments, starts, 2 x ends, counts (+1 for the scan total),
         // flags, LUT, nodes, words
         const size_t b_grp = align_up(sizeof(HuffDecGroup) * dg.size(), 256);
@@ -1379,8 +1479,9 @@ int skml_sparse_deserialize(skml_ctx* c, const uint8_t* buf, size_t len, const d
         const size_t b_cnt = align_up(sizeof(uint64_t) * (size_t)(ns + 1), 256);
         const size_t b_lut = align_up(sizeof(int2) * lut.size(), 256);
         const size_t b_nod = align_up(sizeof(int4) * nodes.size(), 256);
-        const size_t b_wrd = align_up(sizeof(uint64_t) * words.size(), 256);
-        const size_t total = b_grp + b_seg + 3 * b_i64 + b_cnt + 256 + b_lut + b_nod + b_wrd;
+        const size_t b_wrd = align_up(sizeof(uint64_t) * nwords_all, 256);
+        const size_t b_wp = align_up(sizeof(int64_t) * (wpos.size() + wpre.size()), 256);
+        const size_t total = b_grp + b_seg + 3 * b_i64 + b_cnt + 256 + b_lut + b_nod + b_wrd + b_wp;
         char* blk = nullptr;
         SP_HIP(hipMalloc(&blk, total));
         auto run = [&]() -> int {
@@ -1394,13 +1495,17 @@ int skml_sparse_deserialize(skml_ctx* c, const uint8_t* buf, size_t len, const d
             auto* d_flag = (unsigned*)q; q += 256;
             auto* d_lut = (int2*)q; q += b_lut;
             auto* d_nod = (int4*)q; q += b_nod;
-            auto* d_wrd = (uint64_t*)q;
+            auto* d_wrd = (uint64_t*)q; q += b_wrd;
+            auto* d_wp = (int64_t*)q;
+            SP_HIP(hipMemcpyAsync(d_wp, wpos.data(), sizeof(int64_t) * wpos.size(), hipMemcpyHostToDevice, st));
+            SP_HIP(hipMemcpyAsync(d_wp + wpos.size(), wpre.data(), sizeof(int64_t) * wpre.size(), hipMemcpyHostToDevice, st));
+            SP_HIP(hipMemsetAsync(d_wrd + wpre.back(), 0, sizeof(uint64_t), st));
+            SP_HIP(launch_rd_words(st, dstream, d_wp, d_wp + wpos.size(), (int)wpos.size(), wpre.back(), d_wrd));
             SP_HIP(hipMemcpyAsync(d_grp, dg.data(), sizeof(HuffDecGroup) * dg.size(), hipMemcpyHostToDevice, st));
             SP_HIP(hipMemcpyAsync(d_seg, segs.data(), sizeof(HuffSeg) * segs.size(), hipMemcpyHostToDevice, st));
             SP_HIP(hipMemcpyAsync(d_start, starts.data(), sizeof(int64_t) * starts.size(), hipMemcpyHostToDevice, st));
             SP_HIP(hipMemcpyAsync(d_lut, lut.data(), sizeof(int2) * lut.size(), hipMemcpyHostToDevice, st));
             SP_HIP(hipMemcpyAsync(d_nod, nodes.data(), sizeof(int4) * nodes.size(), hipMemcpyHostToDevice, st));
-            SP_HIP(hipMemcpyAsync(d_wrd, words.data(), sizeof(uint64_t) * words.size(), hipMemcpyHostToDevice, st));
             SP_HIP(hipMemsetAsync(d_cnt, 0, b_cnt, st));
             SP_HIP(launch_huff_spec(st, ns, d_seg, d_grp, d_wrd, d_lut, d_nod, d_start, d_ea, d_cnt));
             // resynchronise until every segment starts where its predecessor ends

@@ -126,7 +126,7 @@ class SparsePayload:
         """GroupedMinMaxSketch.readObject of the stream serialize() writes; quant_values (the
         SparseVectorCompressor.quantValues doubles) make restore() return values as well."""
         dev = torch.cuda.current_device() if device is None else torch.device(device).index
-        arr = np.frombuffer(bytes(data), dtype=np.uint8).copy()
+        arr = np.frombuffer(data, dtype=np.uint8)  # read only: the C call takes a const stream
         qv = None if quant_values is None else np.ascontiguousarray(quant_values, dtype=np.float64)
         h = C.c_void_p()
         check(_lib.lib.skml_sparse_deserialize(
