@@ -784,17 +784,6 @@ __device__ __forceinline__ uint32_t bkdr_fast(uint32_t k, const BkdrTables* T) {
     return k ? c * pw + T->b3[ID - 3][k] : c;
 }
 
-// Int2IntHash.hash of 8 keys by a compile-time hash id (before the `% size`): BKDR through the
-// 3-digit LDS tables for non-negative keys, java_hash_mix otherwise.
-template <int ID>
-__device__ __forceinline__ void hash8(const int32_t (&key)[8], uint32_t (&h)[8], const BkdrTables* BK) {
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-        if constexpr (ID >= 3) h[j] = key[j] >= 0 ? bkdr_fast<ID>((uint32_t)key[j], BK) : java_hash_mix(ID, key[j]);
-        else h[j] = java_hash_mix(ID, key[j]);
-    }
-}
-
 // One row's cells of a batch whose group (and so hash) is uniform: the hash specialised at
 // compile time, the modulus by multiplication.  Same cells as java_hash_fm.
 template <int ID>
@@ -1861,13 +1850,18 @@ struct DecSum {
     int nq;            // quantValues entries: a bin outside [0, nq) sets *err too
     int live_only;
 };
-// One tile of kSpTile elements (every thread of the workgroup takes part: block scan).
-__device__ __forceinline__ void dec_keys_tile(int64_t tile, const uint32_t* __restrict__ delta, int64_t n,
-                                              const SpGroups* __restrict__ gp, const uint64_t* __restrict__ tile_base,
-                                              const uint64_t* __restrict__ gpre, const int32_t* __restrict__ table,
-                                              int32_t* __restrict__ gkeys, int32_t* __restrict__ gbins, const DecSum& sum,
-                                              const int64_t* S, uint64_t* sh, const BkdrTables* BK) {
-    const int64_t i0 = tile * kSpTile + threadIdx.x * 8;
+__global__ __launch_bounds__(kSpThreads) void k_dec_keys(const uint32_t* __restrict__ delta, int64_t n,
+                                                         const SpGroups* __restrict__ gp,
+                                                         const uint64_t* __restrict__ tile_base,
+                                                         const uint64_t* __restrict__ gpre,
+                                                         const int32_t* __restrict__ table,
+                                                         int32_t* __restrict__ gkeys, int32_t* __restrict__ gbins,
+                                                         DecSum sum) {
+    __shared__ int64_t S[kMaxGroups + 1];
+    __shared__ uint64_t sh[4];
+    load_starts(gp, S);
+    __syncthreads();
+    const int64_t i0 = (int64_t)blockIdx.x * kSpTile + threadIdx.x * 8;
     uint32_t d[8];
     uint64_t sum8 = 0;
     for (int j = 0; j < 8; j++) {
@@ -1876,13 +1870,14 @@ __device__ __forceinline__ void dec_keys_tile(int64_t tile, const uint32_t* __re
     }
     uint64_t v[1] = {sum8}, tot[1];
     block_excl_scan<1>(v, tot, sh);
-    uint64_t p = tile_base[tile] + v[0];
-    const int zero = gp->zero, rows = table ? gp->rows : 0;
+    if (i0 >= n) return;
+    uint64_t p = tile_base[blockIdx.x] + v[0];
+    const int zero = gp->zero, rows = gp->rows;
     // keys and groups of the 8 elements first, then per row 8 independent table gathers in
-    // flight (random 4-byte reads)
+    // flight (the gathers are random 4-byte reads: latency, not bandwidth, bounds this kernel)
     int32_t key[8], res[8];
     int grp[8];
-    int g = group_of_elem(S, std::min<int64_t>(i0, n - 1));
+    int g = group_of_elem(S, i0);
 #pragma unroll
     for (int j = 0; j < 8; j++) {
         const int64_t i = i0 + j;
@@ -1893,53 +1888,20 @@ __device__ __forceinline__ void dec_keys_tile(int64_t tile, const uint32_t* __re
         key[j] = (int32_t)(uint32_t)(p - gpre[g]);
         res[j] = zero;
     }
-    // a tile inside one group (all but G - 1 tiles): its hash ids are workgroup-uniform, so each
-    // row's cells come from the specialised hash (BKDR by 3-digit LDS tables, the modulus by a
-    // multiplier) instead of java_hash_fm's per-digit loop
-    const int64_t t0 = tile * kSpTile, t1 = std::min<int64_t>(n, t0 + kSpTile) - 1;
-    const int g_lo = group_of_elem(S, t0), g_hi = group_of_elem(S, t1);
-    const bool one = g_lo == g_hi && rows > 0;
-    if (one) {
-        const int32_t cols = gp->cols[g_lo];
-        const DivU32 dv = divu32_make((uint32_t)cols);
-        for (int r = 0; r < rows; r++) {
-            const int id = __builtin_amdgcn_readfirstlane(gp->hash_ids[g_lo][r]);
-            const int64_t row0 = gp->tab_off[g_lo] + (int64_t)r * cols;
-            uint32_t h[8];
-            switch (id) {
-                case 0: hash8<0>(key, h, BK); break;
-                case 1: hash8<1>(key, h, BK); break;
-                case 2: hash8<2>(key, h, BK); break;
-                case 3: hash8<3>(key, h, BK); break;
-                case 4: hash8<4>(key, h, BK); break;
-                case 5: hash8<5>(key, h, BK); break;
-                case 6: hash8<6>(key, h, BK); break;
-                default: hash8<7>(key, h, BK); break;
-            }
-            int32_t tv[8];
+    for (int r = 0; r < rows; r++) {
+        int32_t tv[8];
 #pragma unroll
-            for (int j = 0; j < 8; j++) tv[j] = i0 + j < n ? table[row0 + java_mod((int32_t)h[j], cols, dv)] : zero;
-#pragma unroll
-            for (int j = 0; j < 8; j++)  // MinMaxSketch.query: the strictly farther value wins, ties keep the earlier row
-                if ((int32_t)((uint32_t)mm_dist(tv[j], zero) - (uint32_t)mm_dist(res[j], zero)) > 0) res[j] = tv[j];
+        for (int j = 0; j < 8; j++) {
+            const int gj = grp[j];
+            const int32_t cols = gp->cols[gj];
+            tv[j] = i0 + j < n ? table[gp->tab_off[gj] + (int64_t)r * cols +
+                                       java_hash_fm(gp->hash_ids[gj][r], key[j], cols, gp->inv_cols[gj])]
+                               : zero;
         }
-    } else {
-        for (int r = 0; r < rows; r++) {
-            int32_t tv[8];
 #pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const int gj = grp[j];
-                const int32_t cols = gp->cols[gj];
-                tv[j] = i0 + j < n ? table[gp->tab_off[gj] + (int64_t)r * cols +
-                                           java_hash_fm(gp->hash_ids[gj][r], key[j], cols, gp->inv_cols[gj])]
-                                   : zero;
-            }
-#pragma unroll
-            for (int j = 0; j < 8; j++)
-                if ((int32_t)((uint32_t)mm_dist(tv[j], zero) - (uint32_t)mm_dist(res[j], zero)) > 0) res[j] = tv[j];
-        }
+        for (int j = 0; j < 8; j++)  // MinMaxSketch.query: the strictly farther value wins, ties keep the earlier row
+            if ((int32_t)((uint32_t)mm_dist(tv[j], zero) - (uint32_t)mm_dist(res[j], zero)) > 0) res[j] = tv[j];
     }
-    if (i0 >= n) return;
     if (sum.out) {
         double x[8];
         bool ok[8];
@@ -1967,36 +1929,14 @@ __device__ __forceinline__ void dec_keys_tile(int64_t tile, const uint32_t* __re
     }
 }
 
-constexpr int kDecTilesPerWg = 8;  // tiles of kSpTile per workgroup: the BKDR tables are built once per 16 K keys
-__global__ __launch_bounds__(kSpThreads) void k_dec_keys(const uint32_t* __restrict__ delta, int64_t n,
-                                                         const SpGroups* __restrict__ gp,
-                                                         const uint64_t* __restrict__ tile_base,
-                                                         const uint64_t* __restrict__ gpre,
-                                                         const int32_t* __restrict__ table,
-                                                         int32_t* __restrict__ gkeys, int32_t* __restrict__ gbins,
-                                                         DecSum sum) {
-    __shared__ int64_t S[kMaxGroups + 1];
-    __shared__ uint64_t sh[4];
-    __shared__ BkdrTables BKs;
-    const BkdrTables* BK = &BKs;
-    load_starts(gp, S);
-    if (table && gp->rows > 0) load_bkdr_tables(&BKs);
-    __syncthreads();
-    const int64_t ntiles = sp_tiles(n, kSpTile);
-    for (int64_t tile = (int64_t)blockIdx.x * kDecTilesPerWg;
-         tile < std::min<int64_t>(ntiles, ((int64_t)blockIdx.x + 1) * kDecTilesPerWg); tile++) {
-        dec_keys_tile(tile, delta, n, gp, tile_base, gpre, table, gkeys, gbins, sum, S, sh, BK);
-    }
-}
-
 hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, const SpGroups* gp,
                            const uint64_t* tile_base, const uint64_t* gpre, const int32_t* table,
                            int32_t* gkeys, int32_t* gbins, const double* sum_qv, int nq, double* sum_out,
                            int64_t dim, unsigned* err, int live_only) {
     const int64_t tiles = sp_tiles(n, kSpTile);
     if (tiles <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_dec_keys, dim3((unsigned)sp_tiles(tiles, kDecTilesPerWg)), dim3(kSpThreads), 0, st, delta, n, gp,
-                       tile_base, gpre, table, gkeys, gbins, DecSum{sum_qv, sum_out, dim, err, nq, live_only});
+    hipLaunchKernelGGL(k_dec_keys, dim3((unsigned)tiles), dim3(kSpThreads), 0, st, delta, n, gp, tile_base, gpre,
+                       table, gkeys, gbins, DecSum{sum_qv, sum_out, dim, err, nq, live_only});
     return hipGetLastError();
 }
 
