@@ -123,18 +123,26 @@ hipError_t launch_dec_deltas(hipStream_t st, const uint64_t* delta_words, int64_
                              const uint64_t* tile_base, uint32_t* delta, uint64_t* tile_sums);
 hipError_t launch_group_prefix(hipStream_t st, const uint32_t* delta, int64_t n, const SpGroups* gp, int G,
                                const uint64_t* tile_base, uint64_t* gpre);
-// sum_out != null: add quantValues[bin] (sum_qv) into sum_out[key] instead of storing keys / bins
 hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, const SpGroups* gp,
                            const uint64_t* tile_base, const uint64_t* gpre, const int32_t* table,
-                           int32_t* gkeys, int32_t* gbins, const double* sum_qv = nullptr, int nq = 0,
-                           double* sum_out = nullptr, int64_t dim = 0, unsigned* err = nullptr, int live_only = 0);
-// the DP sum's helpers (skml_sparse_decode_sum_f64): -0.0 -> +0.0, *= scale, live count, pair adds
-hipError_t launch_sum_add_zero(hipStream_t st, double* out, int64_t n);
-hipError_t launch_scale(hipStream_t st, double* out, int64_t n, double x);
+                           int32_t* gkeys, int32_t* gbins);
+// live entries of a restored payload (skml_sparse_decode_sum_f64's toAuto choice)
 hipError_t launch_count_live(hipStream_t st, const int32_t* bins, int64_t n, const double* qv, int nq,
                              uint64_t* count);
-hipError_t launch_add_pairs(hipStream_t st, const int32_t* keys, const int32_t* bins, int64_t n, const double* qv,
-                            int nq, double* out, int64_t dim, unsigned* err, int live_only);
+// the tiled Gradient.sum: per-payload run bounds per dense tile, then the tiles built in LDS
+constexpr int kAggTile = 4096;  // dense keys per tile (32 KB of doubles in LDS)
+struct AggPayload {
+    const int32_t* gk;      // restored keys, grouped order
+    const int32_t* gb;      // their bins
+    const double* qv;       // quantValues
+    const int32_t* bounds;  // [G][ntiles + 1]
+    const SpGroups* gp;     // the payload's group table (device)
+    int32_t nq, G, dense_form, pad;
+};
+hipError_t launch_agg_bounds(hipStream_t st, const int32_t* gk, int64_t n, const SpGroups* gp, int64_t ntiles,
+                             int64_t dim, int32_t* bounds, unsigned* err);
+hipError_t launch_agg_tiles(hipStream_t st, const AggPayload* pays, int P, int64_t ntiles, int64_t dim, double* out,
+                            int from_out, double scale, unsigned* err);
 
 // Exported sparse payload: one contiguous device blob (skml_sparse_export / _import, the unit the
 // RCCL all-gather moves).  Offsets are from the blob start, every section 256-byte aligned.

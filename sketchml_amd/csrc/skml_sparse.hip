@@ -686,7 +686,11 @@ static_assert(kMmBucketCells == 1 << kMmBucketBits, "bucket size");
 constexpr int kMmLdsBuckets = 8192;  // per-workgroup bucket tables in LDS up to this many (96 KB in the scatter)
 constexpr int kMmChunk = (int)kMmChunkElems;
 constexpr int kMmThreads = 1024;  // count / scatter workgroups: big tiles, long per-bucket runs
-constexpr int kMmBatch = 8;       // elements per thread in flight (count, scatter, bucket minima)
+constexpr int kMmBatch = 8;       // elements per thread in flight (count, scatter)
+#ifndef SKML_BUCKET_BATCH
+#define SKML_BUCKET_BATCH 8
+#endif
+constexpr int kBucketBatch = SKML_BUCKET_BATCH;  // pairs per thread in flight in the bucket minima
 
 // a group's MinMaxSketch shape, staged in LDS by the count pass
 // Unsigned division by a run-time d through a multiplier (the round-up method: exact for every
@@ -1194,7 +1198,10 @@ __global__ __launch_bounds__(T) void k_mm_scatter_staged(const int32_t* __restri
         if (c && slot < b0 + mm_pad((uint32_t)c)) pairs[slot] = kMmNoPair;
     }
 }
-constexpr int kStageThreads = 512;
+#ifndef SKML_STAGE_THREADS
+#define SKML_STAGE_THREADS 512
+#endif
+constexpr int kStageThreads = SKML_STAGE_THREADS;
 inline size_t staged_lds(int nbuckets) {
     return (sizeof(uint64_t) + sizeof(uint16_t)) * 8 * kStageThreads + 16 * (size_t)nbuckets + 4;
 }
@@ -1245,12 +1252,12 @@ __global__ __launch_bounds__(kMmThreads) void k_mm_bucket(const uint64_t* __rest
     __syncthreads();
     const uint64_t p0 = bucket_base[b], p1 = bucket_base[b + 1];
     constexpr uint64_t kLo = (uint64_t)(kMmBucketCells - 1);
-    for (uint64_t p = p0 + threadIdx.x; p < p1; p += kMmBatch * kMmThreads) {
-        uint64_t v[kMmBatch];
+    for (uint64_t p = p0 + threadIdx.x; p < p1; p += kBucketBatch * kMmThreads) {
+        uint64_t v[kBucketBatch];
 #pragma unroll
-        for (int u = 0; u < kMmBatch; u++) v[u] = p + u * kMmThreads < p1 ? pairs[p + u * kMmThreads] : kMmNoPair;
+        for (int u = 0; u < kBucketBatch; u++) v[u] = p + u * kMmThreads < p1 ? pairs[p + u * kMmThreads] : kMmNoPair;
 #pragma unroll
-        for (int u = 0; u < kMmBatch; u++)
+        for (int u = 0; u < kBucketBatch; u++)
             if (v[u] != kMmNoPair) atomicMin(&cmin[v[u] & kLo], (unsigned long long)(v[u] & ~kLo));
     }
     __syncthreads();
@@ -1836,27 +1843,12 @@ hipError_t launch_group_prefix(hipStream_t st, const uint32_t* delta, int64_t n,
 
 // keys: group-restarted prefix sums of the deltas (Java int wrap); bins: MinMaxSketch.query
 // (MinMaxSketch.java:64-73): the row value farthest from zero, the first row on ties.
-// Summing mode (sum_out != null): instead of storing (key, bin), add quantValues[bin] into
-// sum_out[key] -- DenseDoubleGradient.plusBy(SparseDoubleGradient) of one payload
-// (DenseDoubleGradient.scala:38-45): keys are unique within a payload, so no atomics, and
-// payloads go one launch after another, so every element's sum is added in payload order.
-// live_only: only |v| > 1e-8 are added (the payload reached plusBy through toAuto's dense form,
-// SparseDoubleGradient.toDense, SparseDoubleGradient.scala:39-44).
-struct DecSum {
-    const double* qv;  // quantValues (the payload's bucket values, timesBy'd)
-    double* out;       // the dense double sum
-    int64_t dim;       // its length: a key outside [0, dim) sets *err and is skipped
-    unsigned* err;     // (SparseDoubleGradient's "out of bounds" require, SparseDoubleGradient.scala:13)
-    int nq;            // quantValues entries: a bin outside [0, nq) sets *err too
-    int live_only;
-};
 __global__ __launch_bounds__(kSpThreads) void k_dec_keys(const uint32_t* __restrict__ delta, int64_t n,
                                                          const SpGroups* __restrict__ gp,
                                                          const uint64_t* __restrict__ tile_base,
                                                          const uint64_t* __restrict__ gpre,
                                                          const int32_t* __restrict__ table,
-                                                         int32_t* __restrict__ gkeys, int32_t* __restrict__ gbins,
-                                                         DecSum sum) {
+                                                         int32_t* __restrict__ gkeys, int32_t* __restrict__ gbins) {
     __shared__ int64_t S[kMaxGroups + 1];
     __shared__ uint64_t sh[4];
     load_starts(gp, S);
@@ -1902,25 +1894,6 @@ __global__ __launch_bounds__(kSpThreads) void k_dec_keys(const uint32_t* __restr
         for (int j = 0; j < 8; j++)  // MinMaxSketch.query: the strictly farther value wins, ties keep the earlier row
             if ((int32_t)((uint32_t)mm_dist(tv[j], zero) - (uint32_t)mm_dist(res[j], zero)) > 0) res[j] = tv[j];
     }
-    if (sum.out) {
-        double x[8];
-        bool ok[8];
-        unsigned bad = 0;
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            ok[j] = i0 + j < n && key[j] >= 0 && (int64_t)key[j] < sum.dim && res[j] >= 0 && res[j] < sum.nq;
-            bad |= (i0 + j < n && !ok[j]) ? 1u : 0u;
-            x[j] = ok[j] ? sum.qv[res[j]] : 0.0;
-        }
-        if (bad) atomicOr(sum.err, 1u);
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            if (!ok[j]) continue;
-            if (sum.live_only && !(fabs(x[j]) > 1e-8)) continue;  // Maths.EPS (ml/util/Maths.scala:8)
-            sum.out[key[j]] += x[j];
-        }
-        return;
-    }
 #pragma unroll
     for (int j = 0; j < 8; j++) {
         if (i0 + j >= n) break;
@@ -1931,36 +1904,113 @@ __global__ __launch_bounds__(kSpThreads) void k_dec_keys(const uint32_t* __restr
 
 hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, const SpGroups* gp,
                            const uint64_t* tile_base, const uint64_t* gpre, const int32_t* table,
-                           int32_t* gkeys, int32_t* gbins, const double* sum_qv, int nq, double* sum_out,
-                           int64_t dim, unsigned* err, int live_only) {
+                           int32_t* gkeys, int32_t* gbins) {
     const int64_t tiles = sp_tiles(n, kSpTile);
     if (tiles <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_dec_keys, dim3((unsigned)tiles), dim3(kSpThreads), 0, st, delta, n, gp, tile_base, gpre,
-                       table, gkeys, gbins, DecSum{sum_qv, sum_out, dim, err, nq, live_only});
+                       table, gkeys, gbins);
     return hipGetLastError();
 }
 
-// x + 0.0 over the whole sum (the dense form's zero entries are added too: -0.0 becomes +0.0)
-__global__ __launch_bounds__(kSpThreads) void k_sum_add_zero(double* __restrict__ out, int64_t n) {
-    for (int64_t i = (int64_t)blockIdx.x * kSpThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kSpThreads)
-        if (__double_as_longlong(out[i]) == (long long)0x8000000000000000ull) out[i] = 0.0;
+// ---- Gradient.sum of P restored payloads, tiled over the dense sum (skml_sparse_decode_sum_f64) ----
+// Each payload is restored (DeltaAdaptive keys + MinMax bins, grouped order, no Sort.merge) into
+// scratch; k_agg_bounds records where every (payload, group) run enters each dense tile of
+// kAggTile keys; k_agg_tiles then builds each tile of the double sum in LDS, payload after payload
+// in payload order (keys are unique within a payload: no atomics), and writes it once.  The dense
+// sum is read and written once instead of one random read-modify-write per restored key.
+// bounds[g * (ntiles + 1) + t] = first element of group g's run with key >= t * kAggTile, local to
+// the run.
+__global__ __launch_bounds__(kSpThreads) void k_agg_bounds(const int32_t* __restrict__ gk, int64_t n,
+                                                           const SpGroups* __restrict__ gp, int64_t ntiles, int64_t dim,
+                                                           int32_t* __restrict__ bounds, unsigned* __restrict__ err) {
+    __shared__ int64_t S[kMaxGroups + 1];
+    load_starts(gp, S);
+    __syncthreads();
+    const int64_t ld = ntiles + 1;
+    for (int64_t i = (int64_t)blockIdx.x * kSpThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kSpThreads) {
+        const int g = group_of_elem(S, i);
+        const int64_t lo = S[g], hi = S[g + 1];
+        auto tile_of = [&](int32_t k) -> int64_t { return k < 0 ? 0 : std::min<int64_t>((int64_t)k / kAggTile, ntiles); };
+        const int32_t key = gk[i];
+        if (key < 0 || (int64_t)key >= dim) atomicOr(err, 1u);  // SparseDoubleGradient's bound check
+        const int64_t ti = tile_of(key);
+        const int64_t pt = i > lo ? tile_of(gk[i - 1]) : -1;
+        int32_t* b = bounds + (int64_t)g * ld;
+        for (int64_t t = pt + 1; t <= ti; t++) b[t] = (int32_t)(i - lo);
+        if (i == hi - 1)
+            for (int64_t t = ti + 1; t <= ntiles; t++) b[t] = (int32_t)(hi - lo);
+    }
 }
-hipError_t launch_sum_add_zero(hipStream_t st, double* out, int64_t n) {
+hipError_t launch_agg_bounds(hipStream_t st, const int32_t* gk, int64_t n, const SpGroups* gp, int64_t ntiles,
+                             int64_t dim, int32_t* bounds, unsigned* err) {
     if (n <= 0) return hipSuccess;
-    const int64_t grid = std::min<int64_t>(sp_tiles(n, kSpThreads * 8), 8192);
-    hipLaunchKernelGGL(k_sum_add_zero, dim3((unsigned)grid), dim3(kSpThreads), 0, st, out, n);
+    const int64_t grid = std::min<int64_t>(sp_tiles(n, kSpThreads), 8192);
+    hipLaunchKernelGGL(k_agg_bounds, dim3((unsigned)grid), dim3(kSpThreads), 0, st, gk, n, gp, ntiles, dim, bounds, err);
     return hipGetLastError();
 }
 
-// out[i] *= scale (the 1/P of the DP average, one double multiply per element)
-__global__ __launch_bounds__(kSpThreads) void k_scale(double* __restrict__ out, int64_t n, double x) {
-    for (int64_t i = (int64_t)blockIdx.x * kSpThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kSpThreads)
-        out[i] = __dmul_rn(out[i], x);
+__global__ __launch_bounds__(kSpThreads) void k_agg_tiles(const AggPayload* __restrict__ pays, int P, int64_t ntiles,
+                                                          int64_t dim, double* __restrict__ out, int from_out,
+                                                          double scale, unsigned* __restrict__ err) {
+    __shared__ double acc[kAggTile];
+    __shared__ int64_t pre[kMaxGroups + 1];
+    __shared__ int64_t base[kMaxGroups];
+    const int64_t t = blockIdx.x;
+    const int64_t k0 = t * kAggTile, nk = std::min<int64_t>(kAggTile, dim - k0);
+    for (int x = threadIdx.x; x < kAggTile; x += kSpThreads) acc[x] = (from_out && x < nk) ? out[k0 + x] : 0.0;
+    unsigned bad = 0;
+    for (int p = 0; p < P; p++) {
+        const AggPayload a = pays[p];
+        __syncthreads();  // the previous payload's adds (and the initial fill) are complete
+        if (threadIdx.x < 64) {  // this tile's segment of every group's run: lengths, their scan
+            const int g = threadIdx.x;
+            int64_t len = 0;
+            if (g < a.G) {
+                const int32_t* b = a.bounds + (int64_t)g * (ntiles + 1);
+                const int32_t b0 = b[t], b1 = b[t + 1];
+                len = b1 > b0 ? b1 - b0 : 0;
+                base[g] = a.gp->gstart[g] + b0;
+            }
+            int64_t x = len;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const int64_t y = __shfl_up(x, off, 64);
+                if (g >= off) x += y;
+            }
+            if (g < a.G) pre[g + 1] = x;
+            if (g == 0) pre[0] = 0;
+        }
+        __syncthreads();
+        const int64_t total = pre[a.G];
+        for (int64_t j = threadIdx.x; j < total; j += kSpThreads) {
+            int g = 0;  // the segment holding j
+            for (int step = 32; step >= 1; step >>= 1)
+                if (g + step < a.G && pre[g + step] <= j) g += step;
+            const int64_t i = base[g] + (j - pre[g]);
+            const int32_t key = a.gk[i], bin = a.gb[i];
+            if (key < k0 || (int64_t)key >= k0 + nk || bin < 0 || bin >= a.nq) {
+                bad = 1;
+                continue;
+            }
+            const double v = a.qv[bin];
+            if (a.dense_form && !(fabs(v) > 1e-8)) continue;  // SparseDoubleGradient.toDense keeps |v| > EPS
+            acc[key - k0] += v;
+        }
+        if (a.dense_form) {  // the dense form adds +0.0 everywhere else: -0.0 becomes +0.0
+            __syncthreads();
+            for (int x = threadIdx.x; x < kAggTile; x += kSpThreads)
+                if (__double_as_longlong(acc[x]) == (long long)0x8000000000000000ull) acc[x] = 0.0;
+        }
+    }
+    if (bad) atomicOr(err, 1u);
+    __syncthreads();
+    for (int x = threadIdx.x; x < nk; x += kSpThreads) out[k0 + x] = scale == 1.0 ? acc[x] : __dmul_rn(acc[x], scale);
 }
-hipError_t launch_scale(hipStream_t st, double* out, int64_t n, double x) {
-    if (n <= 0) return hipSuccess;
-    const int64_t grid = std::min<int64_t>(sp_tiles(n, kSpThreads * 8), 8192);
-    hipLaunchKernelGGL(k_scale, dim3((unsigned)grid), dim3(kSpThreads), 0, st, out, n, x);
+hipError_t launch_agg_tiles(hipStream_t st, const AggPayload* pays, int P, int64_t ntiles, int64_t dim, double* out,
+                            int from_out, double scale, unsigned* err) {
+    if (ntiles <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_agg_tiles, dim3((unsigned)ntiles), dim3(kSpThreads), 0, st, pays, P, ntiles, dim, out, from_out,
+                       scale, err);
     return hipGetLastError();
 }
 
@@ -1984,34 +2034,6 @@ hipError_t launch_count_live(hipStream_t st, const int32_t* bins, int64_t n, con
     const int64_t grid = std::min<int64_t>(sp_tiles(n, kSpThreads * 8), 4096);
     hipLaunchKernelGGL(k_count_live, dim3((unsigned)grid), dim3(kSpThreads), 0, st, bins, n, qv, nq,
                        reinterpret_cast<unsigned long long*>(count));
-    return hipGetLastError();
-}
-
-// sum_out[keys[i]] += quantValues[bins[i]] (|v| > 1e-8 only when live_only): the add step of the
-// two-pass path (payloads whose toAuto may pick the dense form)
-// One thread per pair in index order is not required: keys are unique within a payload.
-__global__ __launch_bounds__(kSpThreads) void k_add_pairs(const int32_t* __restrict__ keys,
-                                                          const int32_t* __restrict__ bins, int64_t n,
-                                                          const double* __restrict__ qv, int nq,
-                                                          double* __restrict__ out, int64_t dim,
-                                                          unsigned* __restrict__ err, int live_only) {
-    for (int64_t i = (int64_t)blockIdx.x * kSpThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kSpThreads) {
-        const int32_t k = keys[i], b = bins[i];
-        if (k < 0 || (int64_t)k >= dim || b < 0 || b >= nq) {
-            atomicOr(err, 1u);
-            continue;
-        }
-        const double v = qv[b];
-        if (live_only && !(fabs(v) > 1e-8)) continue;
-        out[k] += v;
-    }
-}
-hipError_t launch_add_pairs(hipStream_t st, const int32_t* keys, const int32_t* bins, int64_t n, const double* qv,
-                            int nq, double* out, int64_t dim, unsigned* err, int live_only) {
-    if (n <= 0) return hipSuccess;
-    const int64_t grid = std::min<int64_t>(sp_tiles(n, kSpThreads * 4), 8192);
-    hipLaunchKernelGGL(k_add_pairs, dim3((unsigned)grid), dim3(kSpThreads), 0, st, keys, bins, n, qv, nq, out, dim,
-                       err, live_only);
     return hipGetLastError();
 }
 

@@ -571,18 +571,7 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const void* vals, bool f64, int6
 }
 
 // DeltaAdaptive decode of all groups + MinMax query: grouped keys/bins into gk/gb.
-// sum != nullptr: the last step adds quantValues[bin] into the dense double sum instead of
-// storing (key, bin) (DenseDoubleGradient.plusBy of one payload; k_dec_keys summing mode)
-struct SumTarget {
-    const double* qv;
-    int nq;
-    double* out;
-    int64_t dim;
-    unsigned* err;
-    int live_only;
-};
-int decode_groups(skml_ctx* c, const skml_sparse* s, int32_t* gk, int32_t* gb, bool query,
-                  const SumTarget* sum = nullptr) {
+int decode_groups(skml_ctx* c, const skml_sparse* s, int32_t* gk, int32_t* gb, bool query) {
     hipStream_t st = ctx_stream(c);
     const SpGroups& G = s->g;
     const int64_t n = s->nnz;
@@ -610,11 +599,7 @@ int decode_groups(skml_ctx* c, const skml_sparse* s, int32_t* gk, int32_t* gb, b
     SP_HIP(launch_dec_deltas(st, s->delta_words, s->n_delta_words, dlen, n, s->g_dev, ts, delta, ts2));
     if (int e = scan_tiles(c, ts2, tiles, 1, nullptr)) return e;
     SP_HIP(launch_group_prefix(st, delta, n, s->g_dev, G.G, ts2, gpre));
-    if (sum)
-        SP_HIP(launch_dec_keys(st, delta, n, s->g_dev, ts2, gpre, s->tables, nullptr, nullptr, sum->qv, sum->nq,
-                               sum->out, sum->dim, sum->err, sum->live_only));
-    else
-        SP_HIP(launch_dec_keys(st, delta, n, s->g_dev, ts2, gpre, query ? s->tables : nullptr, gk, gb));
+    SP_HIP(launch_dec_keys(st, delta, n, s->g_dev, ts2, gpre, query ? s->tables : nullptr, gk, gb));
     return SKML_OK;
 }
 
@@ -1798,37 +1783,76 @@ int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t
                               &views[(size_t)p]))
             return sfail(e, "payload %d: %s", p, skml_last_error());
     }
-    uint8_t* small = scratch<uint8_t>(c, kSlotStatus, 1024);
+    const int64_t lim = (int64_t)(int32_t)((uint32_t)dim * 2u) / 3;  // dim * 2 / 3 with Java int wrap
+    const int64_t ntiles = sp_tiles(dim, kAggTile);
+    // payloads in batches whose restored keys + bins + run bounds fit the scratch budget; the first
+    // batch starts the sum at +0.0, later ones continue from it, the last one applies the scale
+    constexpr size_t kBudget = (size_t)3 << 30;
+    auto need_of = [&](int p) {
+        return (size_t)views[(size_t)p].nnz * 8 + (size_t)views[(size_t)p].g.G * (size_t)(ntiles + 1) * 4 + 1024;
+    };
+    std::vector<int> todo;
+    for (int p = 0; p < P; p++)
+        if (views[(size_t)p].nnz > 0) todo.push_back(p);  // an empty restore adds nothing (sparse form)
+    uint8_t* small = scratch<uint8_t>(c, kSlotStatus, 1024 + sizeof(AggPayload) * (size_t)P);
     if (!small) return sfail(SKML_E_OOM, "decode_sum scratch");
     unsigned* err = reinterpret_cast<unsigned*>(small);
     uint64_t* live = reinterpret_cast<uint64_t*>(small + 256);
+    AggPayload* d_pays = reinterpret_cast<AggPayload*>(small + 1024);
     SP_HIP(hipMemsetAsync(err, 0, sizeof(unsigned), st));
-    if (dim > 0) SP_HIP(hipMemsetAsync(out, 0, sizeof(double) * (size_t)dim, st));
-    const int64_t lim = (int64_t)(int32_t)((uint32_t)dim * 2u) / 3;  // dim * 2 / 3 with Java int wrap
-    for (int p = 0; p < P; p++) {
-        const skml_sparse& v = views[(size_t)p];
-        if (v.nnz == 0) continue;  // an empty restore adds nothing (its toAuto is sparse)
-        const double* qv = reinterpret_cast<const double*>(static_cast<const uint8_t*>(blobs) + (size_t)p * stride +
-                                                           hs[(size_t)p].off_values);
-        const int nq = (int)v.qvalues.size();
-        if (v.nnz <= lim) {  // live <= nnz <= dim * 2 / 3: toAuto keeps the sparse form
-            SumTarget t{qv, nq, out, dim, err, 0};
-            if (int e = decode_groups(c, &v, nullptr, nullptr, true, &t)) return e;
-            continue;
-        }
-        // the live count decides: restore into scratch, count, add in the chosen form
-        int32_t* gk = scratch<int32_t>(c, kSlotGKeys, (size_t)v.nnz);
-        int32_t* gb = scratch<int32_t>(c, kSlotGBins, (size_t)v.nnz);
-        if (!gk || !gb) return sfail(SKML_E_OOM, "decode_sum scratch");
-        if (int e = decode_groups(c, &v, gk, gb, true)) return e;
-        SP_HIP(launch_count_live(st, gb, v.nnz, qv, nq, live));
-        uint64_t nlive = 0;
-        if (int e = sync_to_host(c, &nlive, live, sizeof(nlive))) return e;
-        const bool dense_form = (int64_t)nlive > lim;
-        if (dense_form) SP_HIP(launch_sum_add_zero(st, out, dim));
-        SP_HIP(launch_add_pairs(st, gk, gb, v.nnz, qv, nq, out, dim, err, dense_form ? 1 : 0));
+    if (todo.empty()) {
+        if (dim > 0) SP_HIP(hipMemsetAsync(out, 0, sizeof(double) * (size_t)dim, st));
+        SP_HIP(hipStreamSynchronize(st));
+        return SKML_OK;
     }
-    if (scale != 1.0) SP_HIP(launch_scale(st, out, dim, scale));
+    size_t at = 0;
+    bool first = true;
+    while (at < todo.size()) {
+        size_t end = at, bytes = 0;
+        while (end < todo.size() && (end == at || bytes + need_of(todo[end]) <= kBudget)) bytes += need_of(todo[end++]);
+        int64_t nk = 0, nb = 0;
+        for (size_t q = at; q < end; q++) {
+            nk += views[(size_t)todo[q]].nnz;
+            nb += (int64_t)views[(size_t)todo[q]].g.G * (ntiles + 1);
+        }
+        int32_t* gk = scratch<int32_t>(c, kSlotCKeys, (size_t)nk);
+        int32_t* gb = scratch<int32_t>(c, kSlotCVals, (size_t)nk);
+        int32_t* bounds = scratch<int32_t>(c, kSlotCells, (size_t)nb);
+        if (!gk || !gb || !bounds) return sfail(SKML_E_OOM, "decode_sum scratch (%lld keys)", (long long)nk);
+        SP_HIP(hipMemsetAsync(bounds, 0, sizeof(int32_t) * (size_t)nb, st));  // empty groups: every bound 0
+        std::vector<AggPayload> pays;
+        int64_t ko = 0, bo = 0;
+        for (size_t q = at; q < end; q++) {
+            const int p = todo[q];
+            const skml_sparse& v = views[(size_t)p];
+            AggPayload a{};
+            a.gk = gk + ko;
+            a.gb = gb + ko;
+            a.qv = reinterpret_cast<const double*>(static_cast<const uint8_t*>(blobs) + (size_t)p * stride +
+                                                   hs[(size_t)p].off_values);
+            a.bounds = bounds + bo;
+            a.gp = v.g_dev;
+            a.nq = (int32_t)v.qvalues.size();
+            a.G = v.g.G;
+            if (int e = decode_groups(c, &v, const_cast<int32_t*>(a.gk), const_cast<int32_t*>(a.gb), true)) return e;
+            if (v.nnz > lim) {  // live <= nnz: only then can toAuto pick the dense form
+                SP_HIP(launch_count_live(st, a.gb, v.nnz, a.qv, a.nq, live));
+                uint64_t nlive = 0;
+                if (int e = sync_to_host(c, &nlive, live, sizeof(nlive))) return e;
+                a.dense_form = (int64_t)nlive > lim ? 1 : 0;
+            }
+            SP_HIP(launch_agg_bounds(st, a.gk, v.nnz, v.g_dev, ntiles, dim, const_cast<int32_t*>(a.bounds), err));
+            pays.push_back(a);
+            ko += v.nnz;
+            bo += (int64_t)v.g.G * (ntiles + 1);
+        }
+        const bool last = end == todo.size();
+        SP_HIP(hipMemcpyAsync(d_pays, pays.data(), sizeof(AggPayload) * pays.size(), hipMemcpyHostToDevice, st));
+        SP_HIP(launch_agg_tiles(st, d_pays, (int)pays.size(), ntiles, dim, out, first ? 0 : 1, last ? scale : 1.0, err));
+        SP_HIP(hipStreamSynchronize(st));  // `pays` (host) and the scratch are reused by the next batch
+        first = false;
+        at = end;
+    }
     unsigned bad = 0;
     if (int e = sync_to_host(c, &bad, err, sizeof(bad))) return e;
     if (bad) return sfail(SKML_E_ARG, "a payload holds a key outside [0, %lld) or a bin outside its values", (long long)dim);
