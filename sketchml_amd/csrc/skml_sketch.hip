@@ -7,19 +7,25 @@
 // (levelwisePropagation / mergeArrays, QSketchUtils.java:53-82).  The bit used by the node at
 // `level` whose last chunk is c is draw #(2c - popcount(c) + level) of java.util.Random(seed).
 //
-//   k_leaf    one pass over the bucket.  512 threads = 8 waves; wave w owns 8 chunks as 32 keys
-//             per lane (8 lanes per chunk).  In registers: bitonic sort of every chunk +
-//             compaction, then tree levels 1..3 (bitonic merges, DPP / swizzle exchanges); levels
-//             4..6 across waves via LDS.  Output: one level-6 node per 64 chunks.
+//   k_leaf64  the fp32 pass over the bucket's full 64-chunk tiles (the hot kernel).  One wave owns
+//             one tile: 4 rounds of 16 chunks, 64 values per lane (4 lanes per chunk).  In
+//             registers: Batcher's odd-even network over the lane's 64 values (543 comparators,
+//             v_min/v_max_f32), 3 cross-lane merge stages (DPP move + v_med3_f32) fused with the
+//             compaction, then tree levels 1..4; levels 5..6 through a carry stack in LDS.  No
+//             workgroup barriers.  Output: one level-6 node per 64 chunks, the tile's min / max /
+//             NaN / zero-sign flags, and the upper tree's compaction bit of this tile.
+//   k_leaf2   the same tree with 32 values per lane (8 lanes per chunk): the partial tile (run in
+//             workgroup 0 of the k_leaf64 launch) and the fp64 leaf.
 //   k_merge   64 nodes of level L -> one node of level L+6 with the same machinery; the last
 //             workgroup of the last pass also runs the summary (makeSummary + getQuantiles +
 //             Maths.unique + findZeroIdx, HeapQuantileSketch.java:126-174,293-323,
 //             Maths.java:51-67, Quantizer.java:74-85) and writes the payload header.
 //   k_summary the summary alone (buckets with < 128 chunks).
 //
-// Bitonic merges sort by total-order key; they equal the reference merge (IEEE `<`, ties emit
-// the newer run) unless a merge sees both -0.0 and +0.0, in which case that workgroup takes the
-// exact LDS path (count-based merge positions with the reference tie rule).
+// Values are sorted as floats: gfx950's v_min/v_max/v_med3_f32 order -0.0 before +0.0, which is
+// Arrays.sort's order for everything but NaN (flagged at load).  The merges equal the reference
+// merge (IEEE `<`, ties emit the newer run) unless a merge sees both -0.0 and +0.0; a wave that
+// has seen both takes the exact LDS path (count-based merge positions with the reference tie rule).
 #include <cstring>
 #include <type_traits>
 

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--dim", type=int, default=2**28)
     ap.add_argument("--density", type=float, default=0.1)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--aggregate", type=int, default=0,
+                    help="also time Gradient.sum of this many payloads (skml_sparse_decode_sum_f64)")
     a = ap.parse_args()
     import sketchml_amd as sk
     dev = torch.device("cuda", 0)
@@ -100,6 +102,17 @@ def main():
         "note": "wall time of synchronising calls (the encode plans on the device and reads the "
                 "quantizer header and group table back once; dense_to_payload adds the compaction's nnz read-back)",
     }
+    if a.aggregate:
+        from sketchml_amd.distributed import blob_stride
+        pls = [sk.encode_sparse(keys, vals, 256, 8, 2, 0.3, 3 + p, 3 + p) for p in range(a.aggregate)]
+        stride = blob_stride([p.export_bytes() for p in pls])
+        allb = torch.zeros(stride * len(pls), dtype=torch.uint8, device=dev)
+        for i, p in enumerate(pls):
+            p.export(allb[i * stride:(i + 1) * stride])
+        del pls
+        t_sum, _ = timed(lambda: sk.decode_sum(allb, a.aggregate, stride, a.dim, 1.0 / a.aggregate), a.reps)
+        line["ms"]["decode_sum"] = round(t_sum * 1e3, 3)
+        line["aggregate"] = {"payloads": a.aggregate, "blob_stride": stride}
     print(json.dumps(line))
 
 
