@@ -34,12 +34,18 @@ struct SpGroups {
     double inv_cols[kMaxGroups];       // 1.0 / cols[g]: the hash's `% size` as a multiply (set on upload)
     double col_ratio;                  // GroupedMinMaxSketch colRatio
     int64_t ncells;                    // all groups' table cells
+    // 1 when the MinMax insert runs on 4-byte pairs: every group's bins lie on one side of zeroIdx
+    // (so a cell's minimum distance fixes its value and no insert order is needed) and the staged
+    // scatter runs (init.narrow_ok); 0 = 8-byte pairs that carry the key for the tie rule
+    int32_t mm_narrow;
+    int32_t pad_;
 };
 
 // What the host knows before an encode starts: the shape parameters and every group's hash
 // choice (HashFactory.getRandomInt2IntHashes(seed + g) depends on g only); passed by value.
 struct SpInit {
     int32_t G, rows;
+    int32_t narrow_ok;  // the host runs the staged scatter (cells kept, ranges reserved)
     double col_ratio;
     int32_t hash_ids[kMaxGroups][kMaxRows];
 };
@@ -92,17 +98,19 @@ constexpr int kMmCellsPerBucket = 8192;  // MinMax cells per bucket (64 KB of u6
 hipError_t launch_group_prep(hipStream_t st, const int32_t* gkeys, int64_t n, const SpGroups* gp, uint8_t* need,
                              uint32_t* hist, uint32_t* err, uint64_t* bucket_count, int nbuckets, int32_t* cells,
                              uint32_t* tile_off);
-// pairs in bucket order (bucket_base: exclusive scan of the counts; cursor: nbuckets u64, zeroed)
+// pairs in bucket order (bucket_base: exclusive scan of the counts; cursor: nbuckets u64, zeroed).
+// Pairs are u64, or u32 when gp->mm_narrow (only with the staged scatter: mm_scatter_staged).
+bool mm_scatter_staged(bool cells, bool reserved, int nbuckets);
 hipError_t launch_mm_scatter(hipStream_t st, const int32_t* gkeys, const int32_t* gbins, int64_t n,
                              const SpGroups* gp, const uint64_t* bucket_base, uint64_t* cursor, int nbuckets,
-                             uint64_t* pairs, const int32_t* cells, const uint32_t* tile_off);
+                             void* pairs, const int32_t* cells, const uint32_t* tile_off);
 #ifndef SKML_MM_CHUNK
 #define SKML_MM_CHUNK 32768
 #endif
 constexpr int64_t kMmChunkElems = SKML_MM_CHUNK;  // elements per workgroup tile of the count / scatter passes
 // per-bucket minimum -> int32 MinMaxSketch tables (empty cells get the fill value); nbuckets may
 // exceed the table's (gp->ncells) buckets: the extra workgroups exit
-hipError_t launch_mm_bucket(hipStream_t st, const uint64_t* pairs, const uint64_t* bucket_base, int nbuckets,
+hipError_t launch_mm_bucket(hipStream_t st, const void* pairs, const uint64_t* bucket_base, int nbuckets,
                             const SpGroups* gp, int32_t* table);
 // DeltaAdaptiveEncoder bit streams: tile sums of (flag bits, delta bits), then the writer.
 hipError_t launch_delta_lens(hipStream_t st, const uint8_t* need, int64_t n, const SpGroups* gp,
@@ -123,9 +131,14 @@ hipError_t launch_dec_deltas(hipStream_t st, const uint64_t* delta_words, int64_
                              const uint64_t* tile_base, uint32_t* delta, uint64_t* tile_sums);
 hipError_t launch_group_prefix(hipStream_t st, const uint32_t* delta, int64_t n, const SpGroups* gp, int G,
                                const uint64_t* tile_base, uint64_t* gpre);
-hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, const SpGroups* gp,
-                           const uint64_t* tile_base, const uint64_t* gpre, const int32_t* table,
-                           int32_t* gkeys, int32_t* gbins);
+// keys and MinMax bins; gh: the host copy of *gp (the grid follows the group sizes).  width 8 / 16:
+// tnar is launch_narrow_table's image of `table` (int32 cells outside [0, 2^width - 1) read back
+// from `table`); width 32: `table` alone (nullptr with gp->rows == 0: keys only)
+hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, const SpGroups* gp, const SpGroups& gh,
+                           const uint64_t* tile_base, const uint64_t* gpre, const int32_t* table, const void* tnar,
+                           int width, int32_t* gkeys, int32_t* gbins);
+// the narrow (width 8 or 16) image of int32 MinMax tables for k_dec_keys; t32 16-byte aligned
+hipError_t launch_narrow_table(hipStream_t st, const int32_t* t32, int64_t ncells, int width, void* tn);
 // live entries of a restored payload (skml_sparse_decode_sum_f64's toAuto choice)
 hipError_t launch_count_live(hipStream_t st, const int32_t* bins, int64_t n, const double* qv, int nq,
                              uint64_t* count);

@@ -733,9 +733,20 @@ __device__ __forceinline__ void load_mm_groups(const SpGroups* gp, MmGroup* GP) 
         for (int r = 0; r < kMaxRows; r++) GP[g].hid[r] = gp->hash_ids[g][r];
     }
 }
-// reserved pair slots of a (tile, bucket) range: whole 128-byte lines, padding = kMmNoPair
+// reserved pair slots of a (tile, bucket) range: whole 128-byte lines (16 wide or 32 narrow
+// pairs), padding = kMmNoPair / kMmNoPair32
 __device__ __forceinline__ uint32_t mm_pad(uint32_t c) { return (c + 15u) & ~15u; }
+__device__ __forceinline__ uint32_t mm_pad(uint32_t c, bool narrow) {
+    return narrow ? (c + 31u) & ~31u : (c + 15u) & ~15u;
+}
 constexpr uint64_t kMmNoPair = ~0ull;
+constexpr uint32_t kMmNoPair32 = ~0u;
+// Narrow pair word (SpGroups.mm_narrow): |bin - zero| [29:14], bin < zero [13], cell % 8192 [12:0].
+// In a one-sided group the sign bit is constant, so the minimum over a cell is the nearest bin.
+__device__ __forceinline__ uint32_t mm_pair32(int32_t bin, int32_t zero, int64_t cell) {
+    return ((uint32_t)mm_dist(bin, zero) << 14) | ((bin < zero ? 1u : 0u) << 13) |
+           (uint32_t)(cell & (kMmBucketCells - 1));
+}
 __device__ __forceinline__ int64_t mm_cell(const SpGroups* gp, int g, int r, int32_t key) {
     const int32_t cols = gp->cols[g];
     return gp->tab_off[g] + (int64_t)r * cols + java_hash_fm(gp->hash_ids[g][r], key, cols, gp->inv_cols[g]);
@@ -916,6 +927,7 @@ __global__ __launch_bounds__(kMmThreads) void k_group_prep(const int32_t* __rest
             if (H[j]) atomicAdd(&hist[j], H[j]);
     if (lds_b && rows > 0) {
         if (tile_off) {  // reserve this tile's range in every bucket: 8 independent atomics in flight
+            const bool narrow = gp->mm_narrow != 0;
             // Ranges are padded to whole 128-byte lines, so every line of the pair array is written by
             // one workgroup only (no partial-line write-backs from two XCDs' L2s).
             uint32_t* row = tile_off + (int64_t)blockIdx.x * nbuckets;
@@ -924,7 +936,8 @@ __global__ __launch_bounds__(kMmThreads) void k_group_prep(const int32_t* __rest
 #pragma unroll
                 for (int u = 0; u < 8; u++) {
                     const int j = j0 + u * kMmThreads;
-                    o[u] = (j < nbuckets && BH[j]) ? atomicAdd(&bucket_count[j], (unsigned long long)mm_pad(BH[j])) : 0ull;
+                    o[u] = (j < nbuckets && BH[j]) ? atomicAdd(&bucket_count[j], (unsigned long long)mm_pad(BH[j], narrow))
+                                                   : 0ull;
                 }
 #pragma unroll
                 for (int u = 0; u < 8; u++) {
@@ -1091,22 +1104,21 @@ __device__ __forceinline__ uint32_t block_excl_scan_u32(uint32_t v, uint32_t* sh
     return before + inc - v;
 }
 
-template <int T>
-__global__ __launch_bounds__(T) void k_mm_scatter_staged(const int32_t* __restrict__ gkeys,
-                                                         const int32_t* __restrict__ gbins, int64_t n,
-                                                         const SpGroups* __restrict__ gp,
-                                                         const uint64_t* __restrict__ bucket_base, int nbuckets,
-                                                         uint64_t* __restrict__ pairs,
-                                                         const int32_t* __restrict__ cells_in,
-                                                         const uint32_t* __restrict__ tile_off) {
-    if (gp->status) return;
+// PAIR: uint64_t (key-carrying pairs) or uint32_t (narrow pairs, SpGroups.mm_narrow).
+template <int T, typename PAIR>
+__device__ __forceinline__ void mm_scatter_staged_body(const int32_t* __restrict__ gkeys,
+                                                       const int32_t* __restrict__ gbins, int64_t n,
+                                                       const SpGroups* __restrict__ gp,
+                                                       const uint64_t* __restrict__ bucket_base, int nbuckets,
+                                                       PAIR* __restrict__ pairs, const int32_t* __restrict__ cells_in,
+                                                       const uint32_t* __restrict__ tile_off, uint64_t* dyn64,
+                                                       uint32_t* scan_sh) {
+    constexpr bool kNarrow = sizeof(PAIR) == 4;
     constexpr int kStage = 8 * T;
-    // LDS: stage[kStage] u64 | dstb[nb] u64 | lc[nb] u32 | lofs[nb + 1] u32 | sb[kStage] u16
-    extern __shared__ uint64_t dyn64[];
-    __shared__ uint32_t scan_sh[T / 64];
-    uint64_t* stage = dyn64;
-    uint64_t* dstb = stage + kStage;
-    uint32_t* lc = reinterpret_cast<uint32_t*>(dstb + nbuckets);
+    // LDS: dstb[nb] u64 | stage[kStage] PAIR | lc[nb] u32 | lofs[nb + 1] u32 | sb[kStage] u16
+    uint64_t* dstb = dyn64;
+    PAIR* stage = reinterpret_cast<PAIR*>(dstb + nbuckets);
+    uint32_t* lc = reinterpret_cast<uint32_t*>(stage + kStage);
     uint32_t* lofs = lc + nbuckets;
     uint16_t* sb = reinterpret_cast<uint16_t*>(lofs + nbuckets + 1);
     const int t = threadIdx.x, rows = gp->rows, zero = gp->zero;
@@ -1129,7 +1141,7 @@ __global__ __launch_bounds__(T) void k_mm_scatter_staged(const int32_t* __restri
             nc[k] = -1;
             if (k < np && i < c1) {
                 nc[k] = cells_in[(int64_t)r * n + i];
-                nk[k] = gkeys[i];
+                if constexpr (!kNarrow) nk[k] = gkeys[i];
                 nbn[k] = gbins[i];
             }
         }
@@ -1137,13 +1149,16 @@ __global__ __launch_bounds__(T) void k_mm_scatter_staged(const int32_t* __restri
     load(c0);
     __syncthreads();
     for (int64_t base = c0; base < c1; base += step) {
-        uint64_t pv[8];
+        PAIR pv[8];
         int32_t bk[8];
         uint32_t rk[8];
 #pragma unroll
         for (int k = 0; k < 8; k++) {
             bk[k] = nc[k] >= 0 ? nc[k] >> kMmBucketBits : -1;
-            if (bk[k] >= 0) pv[k] = mm_pair(nk[k], nbn[k], zero, nc[k]);
+            if (bk[k] >= 0) {
+                if constexpr (kNarrow) pv[k] = mm_pair32(nbn[k], zero, nc[k]);
+                else pv[k] = mm_pair(nk[k], nbn[k], zero, nc[k]);
+            }
         }
         if (base + step < c1) load(base + step);
 #pragma unroll
@@ -1192,11 +1207,32 @@ __global__ __launch_bounds__(T) void k_mm_scatter_staged(const int32_t* __restri
         __syncthreads();
     }
     // padding of each reserved range (mm_pad(count) slots): from the range's end up to the pad
-    for (int j = t; j < nbuckets * 16; j += T) {
-        const uint64_t b0 = bucket_base[j >> 4] + row[j >> 4], e = dstb[j >> 4];
-        const uint64_t c = e - b0, slot = e + (uint64_t)(j & 15);
-        if (c && slot < b0 + mm_pad((uint32_t)c)) pairs[slot] = kMmNoPair;
+    constexpr int kPadMax = kNarrow ? 32 : 16;
+    for (int j = t; j < nbuckets * kPadMax; j += T) {
+        const int bb = j / kPadMax;
+        const uint64_t b0 = bucket_base[bb] + row[bb], e = dstb[bb];
+        const uint64_t c = e - b0, slot = e + (uint64_t)(j % kPadMax);
+        if (c && slot < b0 + mm_pad((uint32_t)c, kNarrow)) pairs[slot] = kNarrow ? (PAIR)kMmNoPair32 : (PAIR)kMmNoPair;
     }
+}
+
+template <int T>
+__global__ __launch_bounds__(T) void k_mm_scatter_staged(const int32_t* __restrict__ gkeys,
+                                                         const int32_t* __restrict__ gbins, int64_t n,
+                                                         const SpGroups* __restrict__ gp,
+                                                         const uint64_t* __restrict__ bucket_base, int nbuckets,
+                                                         void* __restrict__ pairs,
+                                                         const int32_t* __restrict__ cells_in,
+                                                         const uint32_t* __restrict__ tile_off) {
+    if (gp->status) return;
+    extern __shared__ uint64_t dyn64[];
+    __shared__ uint32_t scan_sh[T / 64];
+    if (gp->mm_narrow)
+        mm_scatter_staged_body<T, uint32_t>(gkeys, gbins, n, gp, bucket_base, nbuckets,
+                                            static_cast<uint32_t*>(pairs), cells_in, tile_off, dyn64, scan_sh);
+    else
+        mm_scatter_staged_body<T, uint64_t>(gkeys, gbins, n, gp, bucket_base, nbuckets,
+                                            static_cast<uint64_t*>(pairs), cells_in, tile_off, dyn64, scan_sh);
 }
 #ifndef SKML_STAGE_THREADS
 #define SKML_STAGE_THREADS 512
@@ -1206,11 +1242,16 @@ inline size_t staged_lds(int nbuckets) {
     return (sizeof(uint64_t) + sizeof(uint16_t)) * 8 * kStageThreads + 16 * (size_t)nbuckets + 4;
 }
 
+bool mm_scatter_staged(bool cells, bool reserved, int nbuckets) {
+    return cells && reserved && nbuckets <= kStageBuckets;
+}
+
 hipError_t launch_mm_scatter(hipStream_t st, const int32_t* gkeys, const int32_t* gbins, int64_t n,
                              const SpGroups* gp, const uint64_t* bucket_base, uint64_t* cursor, int nbuckets,
-                             uint64_t* pairs, const int32_t* cells, const uint32_t* tile_off) {
+                             void* pairs_v, const int32_t* cells, const uint32_t* tile_off) {
+    uint64_t* pairs = static_cast<uint64_t*>(pairs_v);  // the unstaged scatter: key-carrying pairs only
     if (n <= 0) return hipSuccess;
-    if (cells && tile_off && nbuckets <= kStageBuckets) {
+    if (mm_scatter_staged(cells != nullptr, tile_off != nullptr, nbuckets)) {
         static bool attr_s = false;
         if (!attr_s) {
             hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mm_scatter_staged<kStageThreads>),
@@ -1220,7 +1261,7 @@ hipError_t launch_mm_scatter(hipStream_t st, const int32_t* gkeys, const int32_t
         }
         hipLaunchKernelGGL(k_mm_scatter_staged<kStageThreads>, dim3((unsigned)sp_tiles(n, kMmChunk)),
                            dim3(kStageThreads), staged_lds(nbuckets), st, gkeys, gbins, n, gp, bucket_base, nbuckets,
-                           pairs, cells, tile_off);
+                           pairs_v, cells, tile_off);
         return hipGetLastError();
     }
     constexpr size_t kPer = sizeof(uint64_t) + sizeof(uint32_t);
@@ -1239,7 +1280,8 @@ hipError_t launch_mm_scatter(hipStream_t st, const int32_t* gkeys, const int32_t
 }
 
 // One workgroup per bucket: LDS minimum per cell, then the int32 table cells (empty -> fill).
-__global__ __launch_bounds__(kMmThreads) void k_mm_bucket(const uint64_t* __restrict__ pairs,
+// Narrow pairs (SpGroups.mm_narrow) take 32-bit LDS minima over (distance, sign).
+__global__ __launch_bounds__(kMmThreads) void k_mm_bucket(const void* __restrict__ pairs_v,
                                                           const uint64_t* __restrict__ bucket_base,
                                                           const SpGroups* __restrict__ gp,
                                                           int32_t* __restrict__ table) {
@@ -1248,9 +1290,38 @@ __global__ __launch_bounds__(kMmThreads) void k_mm_bucket(const uint64_t* __rest
     const int64_t ncells = gp->ncells;
     if (gp->status || ((int64_t)b << kMmBucketBits) >= ncells) return;
     const int32_t zero = gp->zero, fill = gp->fill;
+    const uint64_t p0 = bucket_base[b], p1 = bucket_base[b + 1];
+    const int64_t cell0 = (int64_t)b << kMmBucketBits;
+    if (gp->mm_narrow) {
+        const uint32_t* pairs = static_cast<const uint32_t*>(pairs_v);
+        uint32_t* cm = reinterpret_cast<uint32_t*>(cmin);
+        for (int j = threadIdx.x; j < kMmBucketCells; j += kMmThreads) cm[j] = ~0u;
+        __syncthreads();
+        constexpr uint32_t kLo = (uint32_t)(kMmBucketCells - 1);
+        constexpr int kB = 2 * kBucketBatch;  // half the bytes per pair: twice the pairs in flight
+        for (uint64_t p = p0 + threadIdx.x; p < p1; p += kB * kMmThreads) {
+            uint32_t v[kB];
+#pragma unroll
+            for (int u = 0; u < kB; u++) v[u] = p + u * kMmThreads < p1 ? pairs[p + u * kMmThreads] : kMmNoPair32;
+#pragma unroll
+            for (int u = 0; u < kB; u++)
+                if (v[u] != kMmNoPair32) atomicMin(&cm[v[u] & kLo], v[u] >> kMmBucketBits);
+        }
+        __syncthreads();
+        for (int j = threadIdx.x; j < kMmBucketCells && cell0 + j < ncells; j += kMmThreads) {
+            const uint32_t v = cm[j];
+            int32_t out = fill;
+            if (v != ~0u) {
+                const int32_t dist = (int32_t)(v >> 1);
+                out = (v & 1u) ? zero - dist : zero + dist;
+            }
+            table[cell0 + j] = out;
+        }
+        return;
+    }
+    const uint64_t* pairs = static_cast<const uint64_t*>(pairs_v);
     for (int j = threadIdx.x; j < kMmBucketCells; j += kMmThreads) cmin[j] = ~0ull;
     __syncthreads();
-    const uint64_t p0 = bucket_base[b], p1 = bucket_base[b + 1];
     constexpr uint64_t kLo = (uint64_t)(kMmBucketCells - 1);
     for (uint64_t p = p0 + threadIdx.x; p < p1; p += kBucketBatch * kMmThreads) {
         uint64_t v[kBucketBatch];
@@ -1261,7 +1332,6 @@ __global__ __launch_bounds__(kMmThreads) void k_mm_bucket(const uint64_t* __rest
             if (v[u] != kMmNoPair) atomicMin(&cmin[v[u] & kLo], (unsigned long long)(v[u] & ~kLo));
     }
     __syncthreads();
-    const int64_t cell0 = (int64_t)b << kMmBucketBits;
     for (int j = threadIdx.x; j < kMmBucketCells && cell0 + j < ncells; j += kMmThreads) {
         const uint64_t v = cmin[j];
         int32_t out = fill;
@@ -1273,7 +1343,7 @@ __global__ __launch_bounds__(kMmThreads) void k_mm_bucket(const uint64_t* __rest
     }
 }
 
-hipError_t launch_mm_bucket(hipStream_t st, const uint64_t* pairs, const uint64_t* bucket_base, int nbuckets,
+hipError_t launch_mm_bucket(hipStream_t st, const void* pairs, const uint64_t* bucket_base, int nbuckets,
                             const SpGroups* gp, int32_t* table) {
     if (nbuckets <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_mm_bucket, dim3((unsigned)nbuckets), dim3(kMmThreads), 0, st, pairs, bucket_base, gp,
@@ -1457,6 +1527,19 @@ __device__ __forceinline__ int32_t mm_cmp(int32_t a, int32_t b, int32_t zero) {
     return (int32_t)((uint32_t)mm_dist(a, zero) - (uint32_t)mm_dist(b, zero));
 }
 
+// 4-byte MinMax pairs when no group holds bins on both sides of zeroIdx (FSketchUtils.partition:
+// group g takes the bins in [edges[g-1], edges[g])).  calGroupEdges puts zeroIdx on an edge
+// unless it falls in the last group or two, so this is the common case.
+__device__ void mm_plan_narrow(SpGroups* gp, const SpInit& init) {
+    int32_t lo = 0, narrow = init.narrow_ok ? 1 : 0;
+    for (int g = 0; g < gp->G; g++) {
+        const int32_t hi = gp->edges[g];
+        if (lo < gp->zero && gp->zero < hi - 1) narrow = 0;  // a bin below zero and one above
+        lo = hi > lo ? hi : lo;
+    }
+    gp->mm_narrow = narrow;
+}
+
 // Table from `init` (every field of the reused device struct rewritten), then
 // FSketchUtils.calGroupEdges (frequency/FSketchUtils.java:9-28) on the quantizer's zeroIdx and
 // binNum, and the MinMaxSketch fill (MinMaxSketch.java:30-33).
@@ -1483,6 +1566,7 @@ __global__ __launch_bounds__(64) void k_sp_plan_edges(const skml_dense_header* _
     if (G == 2) {
         gp->edges[0] = zero;
         gp->edges[1] = bins;
+        mm_plan_narrow(gp, init);
         return;
     }
     const int32_t bpg = bins / G;
@@ -1495,6 +1579,7 @@ __global__ __launch_bounds__(64) void k_sp_plan_edges(const skml_dense_header* _
     else e = zero % bpg;
     for (int32_t i = 0; i < G - 1; i++, e += bpg) gp->edges[i] = e;
     gp->edges[G - 1] = bins;
+    mm_plan_narrow(gp, init);
 }
 
 // GroupedMinMaxSketch.compOneGroup's shapes (GroupedMinMaxSketch.java:103-121): colNum =
@@ -1841,19 +1926,70 @@ hipError_t launch_group_prefix(hipStream_t st, const uint32_t* delta, int64_t n,
     return hipGetLastError();
 }
 
+// A narrow image of the int32 MinMax tables for the query: values in [0, 2^W - 1) exactly, the
+// rest (the fill of empty cells, and the top code itself) as the sentinel 2^W - 1, which sends the
+// query back to the int32 cell.  A valid payload only queries inserted cells, so at W = 8 (binNum
+// <= 256) the int32 table is read for bin 255 alone.  At C3 a group's two rows are 2 MB of bytes:
+// with each group's tiles on one XCD (k_dec_keys) the gathers hit that XCD's 4 MB L2.
+template <typename TN>
+__global__ __launch_bounds__(kSpThreads) void k_narrow_table(const int32_t* __restrict__ t32, int64_t ncells,
+                                                             TN* __restrict__ tn) {
+    constexpr uint32_t kTop = (uint32_t)(TN)~(TN)0;
+    const int64_t i0 = ((int64_t)blockIdx.x * kSpThreads + threadIdx.x) * 4;
+    if (i0 + 4 <= ncells) {
+        const int4 v = *reinterpret_cast<const int4*>(t32 + i0);
+        const int32_t e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; j++) tn[i0 + j] = (TN)((uint32_t)e[j] < kTop ? (uint32_t)e[j] : kTop);
+    } else {
+        for (int64_t i = i0; i < ncells; i++) tn[i] = (TN)((uint32_t)t32[i] < kTop ? (uint32_t)t32[i] : kTop);
+    }
+}
+
+hipError_t launch_narrow_table(hipStream_t st, const int32_t* t32, int64_t ncells, int width, void* tn) {
+    if (ncells <= 0) return hipSuccess;
+    if ((reinterpret_cast<uintptr_t>(t32) & 15) != 0) return hipErrorInvalidValue;
+    const unsigned grid = (unsigned)sp_tiles(ncells, (int64_t)kSpThreads * 4);
+    if (width == 8)
+        hipLaunchKernelGGL(k_narrow_table<uint8_t>, dim3(grid), dim3(kSpThreads), 0, st, t32, ncells,
+                           static_cast<uint8_t*>(tn));
+    else
+        hipLaunchKernelGGL(k_narrow_table<uint16_t>, dim3(grid), dim3(kSpThreads), 0, st, t32, ncells,
+                           static_cast<uint16_t*>(tn));
+    return hipGetLastError();
+}
+
+// Workgroup -> tile of k_dec_keys: each tile belongs to the group holding its first element, and
+// the tiles of group g go to workgroups b with b % 8 == g % 8, which the dispatcher deals to one XCD
+// (speed only: any placement gives the same result).  -1: an idle workgroup.
+__device__ __forceinline__ int64_t dec_tile_of_block(const int64_t* S, int G, int64_t b) {
+    const int x = (int)(b & 7);
+    int64_t j = b >> 3;
+    for (int g = x; g < G; g += 8) {
+        const int64_t t0 = sp_tiles(S[g], kSpTile), t1 = sp_tiles(S[g + 1], kSpTile);
+        if (j < t1 - t0) return t0 + j;
+        j -= t1 > t0 ? t1 - t0 : 0;
+    }
+    return -1;
+}
+
 // keys: group-restarted prefix sums of the deltas (Java int wrap); bins: MinMaxSketch.query
-// (MinMaxSketch.java:64-73): the row value farthest from zero, the first row on ties.
+// (MinMaxSketch.java:64-73): the row value farthest from zero, the first row on ties.  TN: the
+// narrow table's cell type (int32_t: the int32 table itself).
+template <typename TN>
 __global__ __launch_bounds__(kSpThreads) void k_dec_keys(const uint32_t* __restrict__ delta, int64_t n,
                                                          const SpGroups* __restrict__ gp,
                                                          const uint64_t* __restrict__ tile_base,
                                                          const uint64_t* __restrict__ gpre,
-                                                         const int32_t* __restrict__ table,
+                                                         const int32_t* __restrict__ table, const TN* __restrict__ tnar,
                                                          int32_t* __restrict__ gkeys, int32_t* __restrict__ gbins) {
     __shared__ int64_t S[kMaxGroups + 1];
     __shared__ uint64_t sh[4];
     load_starts(gp, S);
     __syncthreads();
-    const int64_t i0 = (int64_t)blockIdx.x * kSpTile + threadIdx.x * 8;
+    const int64_t tile = dec_tile_of_block(S, gp->G, blockIdx.x);
+    if (tile < 0) return;  // workgroup-uniform
+    const int64_t i0 = tile * kSpTile + threadIdx.x * 8;
     uint32_t d[8];
     uint64_t sum8 = 0;
     for (int j = 0; j < 8; j++) {
@@ -1863,10 +1999,10 @@ __global__ __launch_bounds__(kSpThreads) void k_dec_keys(const uint32_t* __restr
     uint64_t v[1] = {sum8}, tot[1];
     block_excl_scan<1>(v, tot, sh);
     if (i0 >= n) return;
-    uint64_t p = tile_base[blockIdx.x] + v[0];
+    uint64_t p = tile_base[tile] + v[0];
     const int zero = gp->zero, rows = gp->rows;
     // keys and groups of the 8 elements first, then per row 8 independent table gathers in
-    // flight (the gathers are random 4-byte reads: latency, not bandwidth, bounds this kernel)
+    // flight (the gathers are random reads: latency, not bandwidth, bounds this kernel)
     int32_t key[8], res[8];
     int grp[8];
     int g = group_of_elem(S, i0);
@@ -1880,15 +2016,24 @@ __global__ __launch_bounds__(kSpThreads) void k_dec_keys(const uint32_t* __restr
         key[j] = (int32_t)(uint32_t)(p - gpre[g]);
         res[j] = zero;
     }
+    constexpr uint32_t kTop = sizeof(TN) == 4 ? 0u : (uint32_t)(TN)~(TN)0;
     for (int r = 0; r < rows; r++) {
+        int64_t idx[8];
         int32_t tv[8];
 #pragma unroll
         for (int j = 0; j < 8; j++) {
             const int gj = grp[j];
             const int32_t cols = gp->cols[gj];
-            tv[j] = i0 + j < n ? table[gp->tab_off[gj] + (int64_t)r * cols +
-                                       java_hash_fm(gp->hash_ids[gj][r], key[j], cols, gp->inv_cols[gj])]
-                               : zero;
+            idx[j] = i0 + j < n ? gp->tab_off[gj] + (int64_t)r * cols +
+                                      java_hash_fm(gp->hash_ids[gj][r], key[j], cols, gp->inv_cols[gj])
+                                : -1;
+            if constexpr (sizeof(TN) == 4) tv[j] = idx[j] >= 0 ? table[idx[j]] : zero;
+            else tv[j] = idx[j] >= 0 ? (int32_t)tnar[idx[j]] : zero;
+        }
+        if constexpr (sizeof(TN) < 4) {
+#pragma unroll
+            for (int j = 0; j < 8; j++)  // the sentinel: the cell's int32 value
+                if (idx[j] >= 0 && (uint32_t)tv[j] == kTop) tv[j] = table[idx[j]];
         }
 #pragma unroll
         for (int j = 0; j < 8; j++)  // MinMaxSketch.query: the strictly farther value wins, ties keep the earlier row
@@ -1902,13 +2047,27 @@ __global__ __launch_bounds__(kSpThreads) void k_dec_keys(const uint32_t* __restr
     }
 }
 
-hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, const SpGroups* gp,
-                           const uint64_t* tile_base, const uint64_t* gpre, const int32_t* table,
-                           int32_t* gkeys, int32_t* gbins) {
-    const int64_t tiles = sp_tiles(n, kSpTile);
-    if (tiles <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_dec_keys, dim3((unsigned)tiles), dim3(kSpThreads), 0, st, delta, n, gp, tile_base, gpre,
-                       table, gkeys, gbins);
+hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, const SpGroups* gp, const SpGroups& gh,
+                           const uint64_t* tile_base, const uint64_t* gpre, const int32_t* table, const void* tnar,
+                           int width, int32_t* gkeys, int32_t* gbins) {
+    if (sp_tiles(n, kSpTile) <= 0) return hipSuccess;
+    int64_t per[8] = {};  // tiles per XCD slot (dec_tile_of_block)
+    for (int g = 0; g < gh.G; g++) {
+        const int64_t t0 = sp_tiles(gh.gstart[g], kSpTile), t1 = sp_tiles(gh.gstart[g + 1], kSpTile);
+        if (t1 > t0) per[g & 7] += t1 - t0;
+    }
+    int64_t most = 0;
+    for (int x = 0; x < 8; x++) most = std::max(most, per[x]);
+    const unsigned grid = (unsigned)(8 * most);
+    if (width == 8)
+        hipLaunchKernelGGL(k_dec_keys<uint8_t>, dim3(grid), dim3(kSpThreads), 0, st, delta, n, gp, tile_base, gpre,
+                           table, static_cast<const uint8_t*>(tnar), gkeys, gbins);
+    else if (width == 16)
+        hipLaunchKernelGGL(k_dec_keys<uint16_t>, dim3(grid), dim3(kSpThreads), 0, st, delta, n, gp, tile_base, gpre,
+                           table, static_cast<const uint16_t*>(tnar), gkeys, gbins);
+    else
+        hipLaunchKernelGGL(k_dec_keys<int32_t>, dim3(grid), dim3(kSpThreads), 0, st, delta, n, gp, tile_base, gpre,
+                           table, static_cast<const int32_t*>(nullptr), gkeys, gbins);
     return hipGetLastError();
 }
 
@@ -1949,57 +2108,115 @@ hipError_t launch_agg_bounds(hipStream_t st, const int32_t* gk, int64_t n, const
     return hipGetLastError();
 }
 
+// Payloads are taken kAggPB at a time: one step loads every (payload, group) run bound of the
+// tile, and each batch of up to kAggE elements per thread issues all its key / bin / value loads
+// before any add, so a tile waits on a few load latencies instead of three per payload.  The adds
+// then run payload by payload (keys are unique within a payload; one barrier between payloads),
+// which keeps Gradient.sum's order for every key.
+constexpr int kAggPB = 8, kAggE = 16;
+__device__ __forceinline__ int agg_search(const int64_t* pre, int n, int64_t j) {  // largest i < n: pre[i] <= j
+    int i = 0;
+    for (int step = 32; step >= 1; step >>= 1)
+        if (i + step < n && pre[i + step] <= j) i += step;
+    return i;
+}
 __global__ __launch_bounds__(kSpThreads) void k_agg_tiles(const AggPayload* __restrict__ pays, int P, int64_t ntiles,
                                                           int64_t dim, double* __restrict__ out, int from_out,
                                                           double scale, unsigned* __restrict__ err) {
+    static_assert(kMaxGroups == 64, "one lane per group");
     __shared__ double acc[kAggTile];
-    __shared__ int64_t pre[kMaxGroups + 1];
-    __shared__ int64_t base[kMaxGroups];
+    __shared__ int64_t pre[kAggPB][kMaxGroups + 1];  // a payload's segments in this tile, scanned
+    __shared__ int64_t base[kAggPB][kMaxGroups];     // first element of each segment in its payload
+    __shared__ int64_t poff[kAggPB + 1];             // the batch's payloads concatenated
+    __shared__ int32_t dform[kAggPB];
     const int64_t t = blockIdx.x;
     const int64_t k0 = t * kAggTile, nk = std::min<int64_t>(kAggTile, dim - k0);
     for (int x = threadIdx.x; x < kAggTile; x += kSpThreads) acc[x] = (from_out && x < nk) ? out[k0 + x] : 0.0;
     unsigned bad = 0;
-    for (int p = 0; p < P; p++) {
-        const AggPayload a = pays[p];
-        __syncthreads();  // the previous payload's adds (and the initial fill) are complete
-        if (threadIdx.x < 64) {  // this tile's segment of every group's run: lengths, their scan
-            const int g = threadIdx.x;
+    for (int p0 = 0; p0 < P; p0 += kAggPB) {
+        const int np = std::min(kAggPB, P - p0);
+        __syncthreads();  // the previous batch is done with pre / base / poff
+        for (int pl = threadIdx.x >> 6; pl < np; pl += kSpThreads / 64) {  // a wave per payload, a lane per group
+            const int g = threadIdx.x & 63;
+            const AggPayload& a = pays[p0 + pl];
             int64_t len = 0;
             if (g < a.G) {
-                const int32_t* b = a.bounds + (int64_t)g * (ntiles + 1);
-                const int32_t b0 = b[t], b1 = b[t + 1];
+                const int32_t* bd = a.bounds + (int64_t)g * (ntiles + 1);
+                const int32_t b0 = bd[t], b1 = bd[t + 1];
                 len = b1 > b0 ? b1 - b0 : 0;
-                base[g] = a.gp->gstart[g] + b0;
+                base[pl][g] = a.gp->gstart[g] + b0;
             }
+            if (g == 0) dform[pl] = a.dense_form;
             int64_t x = len;
 #pragma unroll
             for (int off = 1; off < 64; off <<= 1) {
                 const int64_t y = __shfl_up(x, off, 64);
                 if (g >= off) x += y;
             }
-            if (g < a.G) pre[g + 1] = x;
-            if (g == 0) pre[0] = 0;
+            pre[pl][g + 1] = x;
+            if (g == 0) pre[pl][0] = 0;
         }
         __syncthreads();
-        const int64_t total = pre[a.G];
-        for (int64_t j = threadIdx.x; j < total; j += kSpThreads) {
-            int g = 0;  // the segment holding j
-            for (int step = 32; step >= 1; step >>= 1)
-                if (g + step < a.G && pre[g + step] <= j) g += step;
-            const int64_t i = base[g] + (j - pre[g]);
-            const int32_t key = a.gk[i], bin = a.gb[i];
-            if (key < k0 || (int64_t)key >= k0 + nk || bin < 0 || bin >= a.nq) {
-                bad = 1;
-                continue;
+        if (threadIdx.x == 0) {
+            int64_t o = 0;
+            for (int pl = 0; pl < np; pl++) {
+                poff[pl] = o;
+                o += pre[pl][kMaxGroups];
             }
-            const double v = a.qv[bin];
-            if (a.dense_form && !(fabs(v) > 1e-8)) continue;  // SparseDoubleGradient.toDense keeps |v| > EPS
-            acc[key - k0] += v;
+            poff[np] = o;
         }
-        if (a.dense_form) {  // the dense form adds +0.0 everywhere else: -0.0 becomes +0.0
-            __syncthreads();
-            for (int x = threadIdx.x; x < kAggTile; x += kSpThreads)
-                if (__double_as_longlong(acc[x]) == (long long)0x8000000000000000ull) acc[x] = 0.0;
+        __syncthreads();
+        const int64_t total = poff[np];
+        int next = 0;  // the first payload of the batch whose adds are not complete
+        for (int64_t e0 = 0; e0 < total || next < np; e0 += (int64_t)kSpThreads * kAggE) {
+            const int64_t e1 = std::min<int64_t>(total, e0 + (int64_t)kSpThreads * kAggE);
+            int8_t pe[kAggE];
+            int32_t kk[kAggE];
+            double vv[kAggE];
+#pragma unroll
+            for (int u = 0; u < kAggE; u++) {
+                const int64_t j = e0 + u * kSpThreads + threadIdx.x;
+                pe[u] = -1;
+                if (j < e1) {
+                    const int pl = agg_search(poff, np, j);
+                    const int64_t jl = j - poff[pl];
+                    const int g = agg_search(pre[pl], kMaxGroups, jl);
+                    const AggPayload& a = pays[p0 + pl];
+                    const int64_t i = base[pl][g] + (jl - pre[pl][g]);
+                    kk[u] = a.gk[i];
+                    vv[u] = (double)a.gb[i];  // the bin for now
+                    pe[u] = (int8_t)pl;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kAggE; u++) {
+                if (pe[u] < 0) continue;
+                const AggPayload& a = pays[p0 + pe[u]];
+                const int32_t bin = (int32_t)vv[u];
+                if (kk[u] < k0 || (int64_t)kk[u] >= k0 + nk || bin < 0 || bin >= a.nq) {
+                    bad = 1;
+                    pe[u] = -1;
+                    continue;
+                }
+                vv[u] = a.qv[bin];
+            }
+#pragma unroll
+            for (int u = 0; u < kAggE; u++)  // SparseDoubleGradient.toDense keeps |v| > EPS
+                if (pe[u] >= 0 && dform[pe[u]] && !(fabs(vv[u]) > 1e-8)) pe[u] = -1;
+            // the payload holding element e1 - 1 (every remaining one in the last batch)
+            const int last = e1 >= total ? np - 1 : agg_search(poff, np, e1 - 1);
+            for (int pl = next; pl <= last; pl++) {
+#pragma unroll
+                for (int u = 0; u < kAggE; u++)
+                    if (pe[u] == pl) acc[kk[u] - k0] += vv[u];
+                __syncthreads();
+                if (poff[pl + 1] <= e1 && dform[pl]) {  // complete: the dense form adds +0.0 elsewhere
+                    for (int x = threadIdx.x; x < kAggTile; x += kSpThreads)
+                        if (__double_as_longlong(acc[x]) == (long long)0x8000000000000000ull) acc[x] = 0.0;
+                    __syncthreads();
+                }
+            }
+            next = poff[last + 1] <= e1 ? last + 1 : last;
         }
     }
     if (bad) atomicOr(err, 1u);

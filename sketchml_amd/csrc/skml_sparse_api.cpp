@@ -60,8 +60,10 @@ enum {
     kSlotDeltaEnc,  // standalone DeltaAdaptiveEncoder: group table + stream words
     kSlotWire,      // readObject: the device copy of the field stream
     kSlotWireMeta,  // the wire kernels' section tables and small results
+    kSlotNarrowTab, // the MinMax query's narrow table image
+    kSlotCount_,
 };
-static_assert(kSlotDeltaEnc < kScratchSlots, "scratch slots");
+static_assert(kSlotCount_ <= kScratchSlots, "scratch slots");
 
 // java.util.Random (JDK 8 spec): seed scramble, next(bits), nextInt(bound).
 struct JavaRandom {
@@ -473,6 +475,10 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const void* vals, bool f64, int6
     SpInit init{};
     init.G = G;
     init.rows = rows;
+    // the staged scatter's conditions (cells kept, ranges reserved), known from the sizes alone
+    const int nbuckets = (int)((cells_max + kMmCellsPerBucket - 1) / kMmCellsPerBucket);
+    const bool reserve = (uint64_t)rows * (uint64_t)nnz < (1ull << 31);
+    init.narrow_ok = mm_scatter_staged(cells_max < INT32_MAX, reserve, nbuckets) ? 1 : 0;
     init.col_ratio = p->col_ratio;
     for (int g = 0; g < G; g++) pick_hashes(p->hash_seed + g, rows, init.hash_ids[g]);
     SP_TRY(launch_sp_plan_edges(st, s->qpayload, init, s->g_dev));
@@ -480,7 +486,6 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const void* vals, bool f64, int6
     uint64_t* tc = scratch<uint64_t>(c, kSlotTiles, (size_t)(tiles + 1) * G);
     if (!tc) return bail(sfail(SKML_E_OOM, "tile counts"));
     // partition counts; the grid also zeroes the histogram, error flag and bucket counters below
-    const int nbuckets = (int)((cells_max + kMmCellsPerBucket - 1) / kMmCellsPerBucket);
     uint64_t* bucket = scratch<uint64_t>(c, kSlotCells, (size_t)2 * nbuckets + 2);  // counts->bases, cursors
     uint32_t* small = scratch<uint32_t>(c, kSlotSmall, (size_t)kMaxGroups * kDeltaHist + 64);
     if (!bucket || !small) return bail(sfail(SKML_E_OOM, "sparse scratch"));
@@ -494,11 +499,11 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const void* vals, bool f64, int6
     uint8_t* need = scratch<uint8_t>(c, kSlotNeed, (size_t)nnz);
     // per (tile, bucket) reserved offsets (u32: a bucket holds fewer than 2^32 pairs)
     const int64_t mm_tiles = sp_tiles(nnz, kMmChunkElems);
-    const bool reserve = (uint64_t)rows * (uint64_t)nnz < (1ull << 31);
     uint32_t* tile_off = reserve ? scratch<uint32_t>(c, kSlotTileOff, (size_t)mm_tiles * (size_t)nbuckets) : nullptr;
-    // reserved ranges are padded to 16 pairs
+    // reserved ranges are padded to 16 wide (u64) or 32 narrow (u32) pairs
     const size_t npairs = (size_t)rows * (size_t)nnz + (tile_off ? (size_t)15 * mm_tiles * nbuckets : 0);
-    uint64_t* pairs = scratch<uint64_t>(c, kSlotDelta, npairs);
+    const size_t npairs32 = (size_t)rows * (size_t)nnz + (tile_off ? (size_t)31 * mm_tiles * nbuckets : 0);
+    uint64_t* pairs = scratch<uint64_t>(c, kSlotDelta, std::max(npairs, (npairs32 + 1) / 2));
     if (!gk || !gb || !need || !pairs) return bail(sfail(SKML_E_OOM, "sparse scratch"));
     uint64_t* cursor = bucket + nbuckets + 1;
     uint32_t* hist = small;
@@ -507,6 +512,9 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const void* vals, bool f64, int6
     // the pairs' table cells, hashed once (int32 cells; without room or past 2^31 cells the scatter rehashes)
     int32_t* cellbuf =
         cells_max < INT32_MAX ? scratch<int32_t>(c, kSlotCellIdx, (size_t)rows * (size_t)nnz) : nullptr;
+    // k_sp_plan_edges chose narrow pairs on init.narrow_ok: the staged scatter must run
+    if (init.narrow_ok && !mm_scatter_staged(cellbuf != nullptr, tile_off != nullptr, nbuckets))
+        return bail(sfail(SKML_E_OOM, "sparse scratch (MinMax cells)"));
     SP_TRY(launch_group_prep(st, gk, nnz, s->g_dev, need, hist, err, bucket, nbuckets, cellbuf, tile_off));
     // ---- 4. DeltaAdaptive key streams on the side stream, beside the MinMax scatter and minima:
     // the VALU-bound stream writer runs while the scatter waits on memory.  The two chains touch
@@ -599,7 +607,17 @@ int decode_groups(skml_ctx* c, const skml_sparse* s, int32_t* gk, int32_t* gb, b
     SP_HIP(launch_dec_deltas(st, s->delta_words, s->n_delta_words, dlen, n, s->g_dev, ts, delta, ts2));
     if (int e = scan_tiles(c, ts2, tiles, 1, nullptr)) return e;
     SP_HIP(launch_group_prefix(st, delta, n, s->g_dev, G.G, ts2, gpre));
-    SP_HIP(launch_dec_keys(st, delta, n, s->g_dev, ts2, gpre, query ? s->tables : nullptr, gk, gb));
+    // the query gathers from a byte (binNum <= 256) or 16-bit image of the tables
+    const int32_t* tab = query ? s->tables : nullptr;
+    int width = 32;
+    void* tnar = nullptr;
+    if (tab && s->ncells > 0 && (reinterpret_cast<uintptr_t>(tab) & 15) == 0) {
+        width = G.bin_num <= 256 ? 8 : 16;  // any width gives the same bins (the sentinel reads back)
+        tnar = ctx_scratch(c, kSlotNarrowTab, (size_t)s->ncells * (size_t)(width / 8));
+        if (!tnar) return sfail(SKML_E_OOM, "decode scratch (table image)");
+        SP_HIP(launch_narrow_table(st, tab, s->ncells, width, tnar));
+    }
+    SP_HIP(launch_dec_keys(st, delta, n, s->g_dev, G, ts2, gpre, tab, tnar, width, gk, gb));
     return SKML_OK;
 }
 

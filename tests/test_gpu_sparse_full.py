@@ -178,3 +178,41 @@ def test_sparse_f32_still_matches(gpu):
     keys = np.nonzero(rng.random(50000) < 0.2)[0].astype(np.int32)
     vals = rng.standard_normal(len(keys)).astype(np.float32)
     _check_sparse(gpu, keys, vals, seed=3, hash_seed=4)
+
+
+def _cal_group_edges(zero, bins, groups):
+    """FSketchUtils.calGroupEdges (frequency/FSketchUtils.java:9-28)."""
+    if groups == 2:
+        return [zero, bins]
+    bpg = bins // groups
+    e = zero if zero < bpg else (bpg + zero % bpg if zero % bpg < bpg // 2 else zero % bpg)
+    return [e + i * bpg for i in range(groups - 1)] + [bins]
+
+
+def _has_mixed_group(zero, bins, groups):
+    """A group with bins on both sides of zeroIdx: there the MinMax insert needs the key order for
+    ties (the 8-byte pair path); everywhere else the device inserts 4-byte (distance, sign) pairs."""
+    lo = 0
+    for hi in _cal_group_edges(zero, bins, groups):
+        if lo < zero < hi - 1:
+            return True
+        lo = max(lo, hi)
+    return False
+
+
+@pytest.mark.parametrize("pos_frac,mixed", [(0.02, True), (0.05, True), (0.5, False)])
+def test_minmax_pair_width_paths(gpu, pos_frac, mixed):
+    """Mostly negative values put zeroIdx in the last group, which then holds bins on both sides of
+    it (8-byte pairs, the first insert wins a distance tie); balanced values keep every group
+    one-sided (4-byte pairs).  Both give the oracle's tables, bit for bit."""
+    rng = np.random.default_rng(5)
+    keys = np.nonzero(rng.random(200000) < 0.3)[0].astype(np.int32)
+    vals = -np.abs(rng.standard_normal(len(keys)))
+    vals[rng.random(len(keys)) < pos_frac] *= -1
+    osp = O.sparse_compress(keys, vals, 256, 8, 2, 0.3, 1, 2)
+    assert _has_mixed_group(osp.q.zero_idx, osp.q.bin_num, 8) == mixed
+    pl = gpu.encode_sparse(torch.from_numpy(keys).cuda(), torch.from_numpy(vals).cuda(), 256, 8, 2, 0.3, 1, 2)
+    _compare_groups(pl, osp, 8)
+    rk, rb = pl.restore_bins()
+    ok, ob = osp.restore()
+    assert np.array_equal(rk.cpu().numpy(), ok) and np.array_equal(rb.cpu().numpy(), ob)
