@@ -133,25 +133,25 @@ hipError_t launch_group_prefix(hipStream_t st, const uint32_t* delta, int64_t n,
                                const uint64_t* tile_base, uint64_t* gpre);
 // keys and MinMax bins; gh: the host copy of *gp (the grid follows the group sizes).  width 8 / 16:
 // tnar is launch_narrow_table's image of `table` (int32 cells outside [0, 2^width - 1) read back
-// from `table`); width 32: `table` alone (nullptr with gp->rows == 0: keys only)
+// from `table`); width 32: `table` alone (nullptr with gp->rows == 0: keys only).  gbins may be
+// null; gvals (optional) receives quantValues[bin] from qv[nq], a bin outside it sets *err
 hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, const SpGroups* gp, const SpGroups& gh,
                            const uint64_t* tile_base, const uint64_t* gpre, const int32_t* table, const void* tnar,
-                           int width, int32_t* gkeys, int32_t* gbins);
+                           int width, int32_t* gkeys, int32_t* gbins, const double* qv = nullptr, int nq = 0,
+                           double* gvals = nullptr, unsigned* err = nullptr);
 // the narrow (width 8 or 16) image of int32 MinMax tables for k_dec_keys; t32 16-byte aligned
 hipError_t launch_narrow_table(hipStream_t st, const int32_t* t32, int64_t ncells, int width, void* tn);
 // live entries of a restored payload (skml_sparse_decode_sum_f64's toAuto choice)
-hipError_t launch_count_live(hipStream_t st, const int32_t* bins, int64_t n, const double* qv, int nq,
-                             uint64_t* count);
+hipError_t launch_count_live(hipStream_t st, const double* vals, int64_t n, uint64_t* count);
 // the tiled Gradient.sum: per-payload run bounds per dense tile, then the tiles built in LDS
 constexpr int kAggTile = 4096;  // dense keys per tile (32 KB of doubles in LDS)
 struct AggPayload {
     const int32_t* gk;      // restored keys, grouped order
-    const int32_t* gb;      // their bins
-    const double* qv;       // quantValues
+    const double* gv;       // their values, quantValues[bin]
     const int32_t* bounds;  // [G][ntiles + 1]
-    const SpGroups* gp;     // the payload's group table (device)
-    int32_t nq, G, dense_form, pad;
+    int32_t G, dense_form;
 };
+static_assert(sizeof(AggPayload) % 8 == 0, "copied as u64 words");
 hipError_t launch_agg_bounds(hipStream_t st, const int32_t* gk, int64_t n, const SpGroups* gp, int64_t ntiles,
                              int64_t dim, int32_t* bounds, unsigned* err);
 hipError_t launch_agg_tiles(hipStream_t st, const AggPayload* pays, int P, int64_t ntiles, int64_t dim, double* out,

@@ -113,6 +113,32 @@ __device__ __forceinline__ void load_starts(const SpGroups* gp, int64_t* S) {
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t sar(uint32_t c, int s) { return (uint32_t)((int32_t)c >> s); }
 
+// BKDRHash's digit loop over a non-negative key, three decimal digits per step: a full chunk r
+// (digits d0 d1 d2, d0 the lowest) advances the code to code * s^3 + d0 s^2 + d1 s + d2, the last
+// chunk by as many digits as it has.  Divisions by 1000 / 100 / 10 as multiply-shifts, exact for
+// every 31-bit key and every r < 1000 (checked exhaustively against the digit loop on the host).
+__device__ __forceinline__ uint32_t bkdr_chunks(uint32_t seed, uint32_t k) {
+    const uint32_t s2 = seed * seed, s3 = s2 * seed;
+    uint32_t c = 0;
+    while (k >= 1000u) {
+        const uint32_t q = __umulhi(k, 0x10624DD3u) >> 6;  // k / 1000
+        const uint32_t r = k - 1000u * q;
+        const uint32_t t = (r * 205u) >> 11, h = (r * 41u) >> 12;  // r / 10, r / 100
+        c = c * s3 + (r - 10u * t) * s2 + (t - 10u * h) * seed + h;
+        k = q;
+    }
+    if (k >= 100u) {
+        const uint32_t t = (k * 205u) >> 11, h = (k * 41u) >> 12;
+        c = c * s3 + (k - 10u * t) * s2 + (t - 10u * h) * seed + h;
+    } else if (k >= 10u) {
+        const uint32_t t = (k * 205u) >> 11;
+        c = c * s2 + (k - 10u * t) * seed + t;
+    } else if (k) {
+        c = c * seed + k;
+    }
+    return c;
+}
+
 __device__ __forceinline__ uint32_t java_hash_mix(int id, int32_t key) {
     uint32_t c = (uint32_t)key;
     if (id == 0) {
@@ -140,13 +166,8 @@ __device__ __forceinline__ uint32_t java_hash_mix(int id, int32_t key) {
     } else {
         const uint32_t seed = id == 3 ? 31u : id == 4 ? 131u : id == 5 ? 267u : id == 6 ? 1313u : 13131u;
         c = 0;
-        if (key >= 0) {  // every valid key: Java's int % and / are the unsigned ones (shorter code)
-            uint32_t k = (uint32_t)key;
-            while (k != 0) {
-                const uint32_t q = k / 10u;
-                c = seed * c + (k - 10u * q);
-                k = q;
-            }
+        if (key >= 0) {  // every valid key: Java's int % and / are the unsigned ones
+            c = bkdr_chunks(seed, (uint32_t)key);
         } else {
             int32_t k = key;
             while (k != 0) {
@@ -1975,39 +1996,51 @@ __device__ __forceinline__ int64_t dec_tile_of_block(const int64_t* S, int G, in
 
 // keys: group-restarted prefix sums of the deltas (Java int wrap); bins: MinMaxSketch.query
 // (MinMaxSketch.java:64-73): the row value farthest from zero, the first row on ties.  TN: the
-// narrow table's cell type (int32_t: the int32 table itself).
+// narrow table's cell type (int32_t: the int32 table itself).  512 threads per 2,048-element tile,
+// 4 consecutive elements per thread (16-byte delta loads and key stores; few registers, so 8
+// waves per SIMD hide the table gathers).
+constexpr int kDecThreads = 512;
+static_assert(kDecThreads * 4 == kSpTile, "dec_keys tile");
 template <typename TN>
-__global__ __launch_bounds__(kSpThreads) void k_dec_keys(const uint32_t* __restrict__ delta, int64_t n,
-                                                         const SpGroups* __restrict__ gp,
-                                                         const uint64_t* __restrict__ tile_base,
-                                                         const uint64_t* __restrict__ gpre,
-                                                         const int32_t* __restrict__ table, const TN* __restrict__ tnar,
-                                                         int32_t* __restrict__ gkeys, int32_t* __restrict__ gbins) {
+__global__ __launch_bounds__(kDecThreads) void k_dec_keys(const uint32_t* __restrict__ delta, int64_t n,
+                                                          const SpGroups* __restrict__ gp,
+                                                          const uint64_t* __restrict__ tile_base,
+                                                          const uint64_t* __restrict__ gpre,
+                                                          const int32_t* __restrict__ table, const TN* __restrict__ tnar,
+                                                          int32_t* __restrict__ gkeys, int32_t* __restrict__ gbins,
+                                                          const double* __restrict__ qv, int nq,
+                                                          double* __restrict__ gvals, unsigned* __restrict__ err) {
     __shared__ int64_t S[kMaxGroups + 1];
-    __shared__ uint64_t sh[4];
+    __shared__ uint64_t sh[kDecThreads / 64];
     load_starts(gp, S);
     __syncthreads();
     const int64_t tile = dec_tile_of_block(S, gp->G, blockIdx.x);
     if (tile < 0) return;  // workgroup-uniform
-    const int64_t i0 = tile * kSpTile + threadIdx.x * 8;
-    uint32_t d[8];
-    uint64_t sum8 = 0;
-    for (int j = 0; j < 8; j++) {
-        d[j] = i0 + j < n ? delta[i0 + j] : 0;
-        sum8 += d[j];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int64_t i0 = tile * kSpTile + t * 4;
+    uint32_t d[4];
+    if (i0 + 4 <= n) {
+        const uint4 v = *reinterpret_cast<const uint4*>(delta + i0);
+        d[0] = v.x, d[1] = v.y, d[2] = v.z, d[3] = v.w;
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; j++) d[j] = i0 + j < n ? delta[i0 + j] : 0u;
     }
-    uint64_t v[1] = {sum8}, tot[1];
-    block_excl_scan<1>(v, tot, sh);
+    // the tile's exclusive prefix of the deltas (64-bit: a tile's deltas may pass 2^32)
+    const uint64_t own = (uint64_t)d[0] + d[1] + d[2] + d[3];
+    const uint64_t inc = wave_incl_u64(own, lane);
+    if (lane == 63) sh[w] = inc;
+    __syncthreads();
+    uint64_t p = tile_base[tile] + inc - own;
+#pragma unroll
+    for (int j = 0; j < kDecThreads / 64; j++) p += j < w ? sh[j] : 0ull;
     if (i0 >= n) return;
-    uint64_t p = tile_base[tile] + v[0];
     const int zero = gp->zero, rows = gp->rows;
-    // keys and groups of the 8 elements first, then per row 8 independent table gathers in
-    // flight (the gathers are random reads: latency, not bandwidth, bounds this kernel)
-    int32_t key[8], res[8];
-    int grp[8];
+    int32_t key[4], res[4];
+    int grp[4];
     int g = group_of_elem(S, i0);
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
+    for (int j = 0; j < 4; j++) {
         const int64_t i = i0 + j;
         if (i < n)
             while (i >= S[g + 1]) g++;
@@ -2018,10 +2051,10 @@ __global__ __launch_bounds__(kSpThreads) void k_dec_keys(const uint32_t* __restr
     }
     constexpr uint32_t kTop = sizeof(TN) == 4 ? 0u : (uint32_t)(TN)~(TN)0;
     for (int r = 0; r < rows; r++) {
-        int64_t idx[8];
-        int32_t tv[8];
+        int64_t idx[4];
+        int32_t tv[4];
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
+        for (int j = 0; j < 4; j++) {
             const int gj = grp[j];
             const int32_t cols = gp->cols[gj];
             idx[j] = i0 + j < n ? gp->tab_off[gj] + (int64_t)r * cols +
@@ -2032,24 +2065,55 @@ __global__ __launch_bounds__(kSpThreads) void k_dec_keys(const uint32_t* __restr
         }
         if constexpr (sizeof(TN) < 4) {
 #pragma unroll
-            for (int j = 0; j < 8; j++)  // the sentinel: the cell's int32 value
+            for (int j = 0; j < 4; j++)  // the sentinel: the cell's int32 value
                 if (idx[j] >= 0 && (uint32_t)tv[j] == kTop) tv[j] = table[idx[j]];
         }
 #pragma unroll
-        for (int j = 0; j < 8; j++)  // MinMaxSketch.query: the strictly farther value wins, ties keep the earlier row
+        for (int j = 0; j < 4; j++)  // MinMaxSketch.query: the strictly farther value wins, ties keep the earlier row
             if ((int32_t)((uint32_t)mm_dist(tv[j], zero) - (uint32_t)mm_dist(res[j], zero)) > 0) res[j] = tv[j];
     }
+    const bool full = i0 + 4 <= n;
+    if (gvals) {  // quantValues[bin] (Gradient.sum's restore): a bin outside the values is an error
+        bool bad = false;
+        double v[4];
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
-        if (i0 + j >= n) break;
-        gkeys[i0 + j] = key[j];
-        gbins[i0 + j] = res[j];
+        for (int j = 0; j < 4; j++) {
+            const bool ok = res[j] >= 0 && res[j] < nq;
+            bad |= !ok && i0 + j < n;
+            v[j] = ok ? qv[res[j]] : 0.0;
+        }
+        if (bad) atomicOr(err, 1u);
+        if (full && (reinterpret_cast<uintptr_t>(gvals + i0) & 15) == 0) {
+            reinterpret_cast<double2*>(gvals + i0)[0] = make_double2(v[0], v[1]);
+            reinterpret_cast<double2*>(gvals + i0)[1] = make_double2(v[2], v[3]);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                if (i0 + j < n) gvals[i0 + j] = v[j];
+        }
+    }
+    if (full && (reinterpret_cast<uintptr_t>(gkeys + i0) & 15) == 0) {
+        *reinterpret_cast<int4*>(gkeys + i0) = make_int4(key[0], key[1], key[2], key[3]);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            if (i0 + j < n) gkeys[i0 + j] = key[j];
+    }
+    if (gbins) {
+        if (full && (reinterpret_cast<uintptr_t>(gbins + i0) & 15) == 0) {
+            *reinterpret_cast<int4*>(gbins + i0) = make_int4(res[0], res[1], res[2], res[3]);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                if (i0 + j < n) gbins[i0 + j] = res[j];
+        }
     }
 }
 
 hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, const SpGroups* gp, const SpGroups& gh,
                            const uint64_t* tile_base, const uint64_t* gpre, const int32_t* table, const void* tnar,
-                           int width, int32_t* gkeys, int32_t* gbins) {
+                           int width, int32_t* gkeys, int32_t* gbins, const double* qv, int nq, double* gvals,
+                           unsigned* err) {
     if (sp_tiles(n, kSpTile) <= 0) return hipSuccess;
     int64_t per[8] = {};  // tiles per XCD slot (dec_tile_of_block)
     for (int g = 0; g < gh.G; g++) {
@@ -2060,14 +2124,14 @@ hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, con
     for (int x = 0; x < 8; x++) most = std::max(most, per[x]);
     const unsigned grid = (unsigned)(8 * most);
     if (width == 8)
-        hipLaunchKernelGGL(k_dec_keys<uint8_t>, dim3(grid), dim3(kSpThreads), 0, st, delta, n, gp, tile_base, gpre,
-                           table, static_cast<const uint8_t*>(tnar), gkeys, gbins);
+        hipLaunchKernelGGL(k_dec_keys<uint8_t>, dim3(grid), dim3(kDecThreads), 0, st, delta, n, gp, tile_base, gpre,
+                           table, static_cast<const uint8_t*>(tnar), gkeys, gbins, qv, nq, gvals, err);
     else if (width == 16)
-        hipLaunchKernelGGL(k_dec_keys<uint16_t>, dim3(grid), dim3(kSpThreads), 0, st, delta, n, gp, tile_base, gpre,
-                           table, static_cast<const uint16_t*>(tnar), gkeys, gbins);
+        hipLaunchKernelGGL(k_dec_keys<uint16_t>, dim3(grid), dim3(kDecThreads), 0, st, delta, n, gp, tile_base, gpre,
+                           table, static_cast<const uint16_t*>(tnar), gkeys, gbins, qv, nq, gvals, err);
     else
-        hipLaunchKernelGGL(k_dec_keys<int32_t>, dim3(grid), dim3(kSpThreads), 0, st, delta, n, gp, tile_base, gpre,
-                           table, static_cast<const int32_t*>(nullptr), gkeys, gbins);
+        hipLaunchKernelGGL(k_dec_keys<int32_t>, dim3(grid), dim3(kDecThreads), 0, st, delta, n, gp, tile_base, gpre,
+                           table, static_cast<const int32_t*>(nullptr), gkeys, gbins, qv, nq, gvals, err);
     return hipGetLastError();
 }
 
@@ -2077,8 +2141,8 @@ hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, con
 // kAggTile keys; k_agg_tiles then builds each tile of the double sum in LDS, payload after payload
 // in payload order (keys are unique within a payload: no atomics), and writes it once.  The dense
 // sum is read and written once instead of one random read-modify-write per restored key.
-// bounds[g * (ntiles + 1) + t] = first element of group g's run with key >= t * kAggTile, local to
-// the run.
+// bounds[g * (ntiles + 1) + t] = first element (payload index) of group g's run with key >=
+// t * kAggTile; 0 throughout for an empty group.
 __global__ __launch_bounds__(kSpThreads) void k_agg_bounds(const int32_t* __restrict__ gk, int64_t n,
                                                            const SpGroups* __restrict__ gp, int64_t ntiles, int64_t dim,
                                                            int32_t* __restrict__ bounds, unsigned* __restrict__ err) {
@@ -2095,9 +2159,9 @@ __global__ __launch_bounds__(kSpThreads) void k_agg_bounds(const int32_t* __rest
         const int64_t ti = tile_of(key);
         const int64_t pt = i > lo ? tile_of(gk[i - 1]) : -1;
         int32_t* b = bounds + (int64_t)g * ld;
-        for (int64_t t = pt + 1; t <= ti; t++) b[t] = (int32_t)(i - lo);
+        for (int64_t t = pt + 1; t <= ti; t++) b[t] = (int32_t)i;
         if (i == hi - 1)
-            for (int64_t t = ti + 1; t <= ntiles; t++) b[t] = (int32_t)(hi - lo);
+            for (int64_t t = ti + 1; t <= ntiles; t++) b[t] = (int32_t)hi;
     }
 }
 hipError_t launch_agg_bounds(hipStream_t st, const int32_t* gk, int64_t n, const SpGroups* gp, int64_t ntiles,
@@ -2113,14 +2177,14 @@ hipError_t launch_agg_bounds(hipStream_t st, const int32_t* gk, int64_t n, const
 // before any add, so a tile waits on a few load latencies instead of three per payload.  The adds
 // then run payload by payload (keys are unique within a payload; one barrier between payloads),
 // which keeps Gradient.sum's order for every key.
-constexpr int kAggPB = 8, kAggE = 16;
+constexpr int kAggPB = 8, kAggE = 8, kAggThreads = 512;
 __device__ __forceinline__ int agg_search(const int64_t* pre, int n, int64_t j) {  // largest i < n: pre[i] <= j
     int i = 0;
     for (int step = 32; step >= 1; step >>= 1)
         if (i + step < n && pre[i + step] <= j) i += step;
     return i;
 }
-__global__ __launch_bounds__(kSpThreads) void k_agg_tiles(const AggPayload* __restrict__ pays, int P, int64_t ntiles,
+__global__ __launch_bounds__(kAggThreads) void k_agg_tiles(const AggPayload* __restrict__ pays, int P, int64_t ntiles,
                                                           int64_t dim, double* __restrict__ out, int from_out,
                                                           double scale, unsigned* __restrict__ err) {
     static_assert(kMaxGroups == 64, "one lane per group");
@@ -2129,14 +2193,17 @@ __global__ __launch_bounds__(kSpThreads) void k_agg_tiles(const AggPayload* __re
     __shared__ int64_t base[kAggPB][kMaxGroups];     // first element of each segment in its payload
     __shared__ int64_t poff[kAggPB + 1];             // the batch's payloads concatenated
     __shared__ int32_t dform[kAggPB];
+    __shared__ AggPayload pl_s[kAggPB];
     const int64_t t = blockIdx.x;
     const int64_t k0 = t * kAggTile, nk = std::min<int64_t>(kAggTile, dim - k0);
-    for (int x = threadIdx.x; x < kAggTile; x += kSpThreads) acc[x] = (from_out && x < nk) ? out[k0 + x] : 0.0;
+    for (int x = threadIdx.x; x < kAggTile; x += kAggThreads) acc[x] = (from_out && x < nk) ? out[k0 + x] : 0.0;
     unsigned bad = 0;
     for (int p0 = 0; p0 < P; p0 += kAggPB) {
         const int np = std::min(kAggPB, P - p0);
-        __syncthreads();  // the previous batch is done with pre / base / poff
-        for (int pl = threadIdx.x >> 6; pl < np; pl += kSpThreads / 64) {  // a wave per payload, a lane per group
+        __syncthreads();  // the previous batch is done with pre / base / poff / pl_s
+        if (threadIdx.x < np * (int)(sizeof(AggPayload) / 8))
+            reinterpret_cast<uint64_t*>(pl_s)[threadIdx.x] = reinterpret_cast<const uint64_t*>(pays + p0)[threadIdx.x];
+        for (int pl = threadIdx.x >> 6; pl < np; pl += kAggThreads / 64) {  // a wave per payload, a lane per group
             const int g = threadIdx.x & 63;
             const AggPayload& a = pays[p0 + pl];
             int64_t len = 0;
@@ -2144,7 +2211,7 @@ __global__ __launch_bounds__(kSpThreads) void k_agg_tiles(const AggPayload* __re
                 const int32_t* bd = a.bounds + (int64_t)g * (ntiles + 1);
                 const int32_t b0 = bd[t], b1 = bd[t + 1];
                 len = b1 > b0 ? b1 - b0 : 0;
-                base[pl][g] = a.gp->gstart[g] + b0;
+                base[pl][g] = b0;
             }
             if (g == 0) dform[pl] = a.dense_form;
             int64_t x = len;
@@ -2168,38 +2235,31 @@ __global__ __launch_bounds__(kSpThreads) void k_agg_tiles(const AggPayload* __re
         __syncthreads();
         const int64_t total = poff[np];
         int next = 0;  // the first payload of the batch whose adds are not complete
-        for (int64_t e0 = 0; e0 < total || next < np; e0 += (int64_t)kSpThreads * kAggE) {
-            const int64_t e1 = std::min<int64_t>(total, e0 + (int64_t)kSpThreads * kAggE);
+        for (int64_t e0 = 0; e0 < total || next < np; e0 += (int64_t)kAggThreads * kAggE) {
+            const int64_t e1 = std::min<int64_t>(total, e0 + (int64_t)kAggThreads * kAggE);
             int8_t pe[kAggE];
             int32_t kk[kAggE];
             double vv[kAggE];
 #pragma unroll
             for (int u = 0; u < kAggE; u++) {
-                const int64_t j = e0 + u * kSpThreads + threadIdx.x;
+                const int64_t j = e0 + u * kAggThreads + threadIdx.x;
                 pe[u] = -1;
                 if (j < e1) {
                     const int pl = agg_search(poff, np, j);
                     const int64_t jl = j - poff[pl];
                     const int g = agg_search(pre[pl], kMaxGroups, jl);
-                    const AggPayload& a = pays[p0 + pl];
                     const int64_t i = base[pl][g] + (jl - pre[pl][g]);
-                    kk[u] = a.gk[i];
-                    vv[u] = (double)a.gb[i];  // the bin for now
+                    kk[u] = pl_s[pl].gk[i];
+                    vv[u] = pl_s[pl].gv[i];
                     pe[u] = (int8_t)pl;
                 }
             }
 #pragma unroll
-            for (int u = 0; u < kAggE; u++) {
-                if (pe[u] < 0) continue;
-                const AggPayload& a = pays[p0 + pe[u]];
-                const int32_t bin = (int32_t)vv[u];
-                if (kk[u] < k0 || (int64_t)kk[u] >= k0 + nk || bin < 0 || bin >= a.nq) {
+            for (int u = 0; u < kAggE; u++)
+                if (pe[u] >= 0 && (kk[u] < k0 || (int64_t)kk[u] >= k0 + nk)) {
                     bad = 1;
                     pe[u] = -1;
-                    continue;
                 }
-                vv[u] = a.qv[bin];
-            }
 #pragma unroll
             for (int u = 0; u < kAggE; u++)  // SparseDoubleGradient.toDense keeps |v| > EPS
                 if (pe[u] >= 0 && dform[pe[u]] && !(fabs(vv[u]) > 1e-8)) pe[u] = -1;
@@ -2211,7 +2271,7 @@ __global__ __launch_bounds__(kSpThreads) void k_agg_tiles(const AggPayload* __re
                     if (pe[u] == pl) acc[kk[u] - k0] += vv[u];
                 __syncthreads();
                 if (poff[pl + 1] <= e1 && dform[pl]) {  // complete: the dense form adds +0.0 elsewhere
-                    for (int x = threadIdx.x; x < kAggTile; x += kSpThreads)
+                    for (int x = threadIdx.x; x < kAggTile; x += kAggThreads)
                         if (__double_as_longlong(acc[x]) == (long long)0x8000000000000000ull) acc[x] = 0.0;
                     __syncthreads();
                 }
@@ -2221,35 +2281,31 @@ __global__ __launch_bounds__(kSpThreads) void k_agg_tiles(const AggPayload* __re
     }
     if (bad) atomicOr(err, 1u);
     __syncthreads();
-    for (int x = threadIdx.x; x < nk; x += kSpThreads) out[k0 + x] = scale == 1.0 ? acc[x] : __dmul_rn(acc[x], scale);
+    for (int x = threadIdx.x; x < nk; x += kAggThreads) out[k0 + x] = scale == 1.0 ? acc[x] : __dmul_rn(acc[x], scale);
 }
 hipError_t launch_agg_tiles(hipStream_t st, const AggPayload* pays, int P, int64_t ntiles, int64_t dim, double* out,
                             int from_out, double scale, unsigned* err) {
     if (ntiles <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_agg_tiles, dim3((unsigned)ntiles), dim3(kSpThreads), 0, st, pays, P, ntiles, dim, out, from_out,
+    hipLaunchKernelGGL(k_agg_tiles, dim3((unsigned)ntiles), dim3(kAggThreads), 0, st, pays, P, ntiles, dim, out, from_out,
                        scale, err);
     return hipGetLastError();
 }
 
 // live entries (|quantValues[bin]| > 1e-8) of a restored payload, for toAuto's dense / sparse choice
-__global__ __launch_bounds__(kSpThreads) void k_count_live(const int32_t* __restrict__ bins, int64_t n,
-                                                           const double* __restrict__ qv, int nq,
+__global__ __launch_bounds__(kSpThreads) void k_count_live(const double* __restrict__ vals, int64_t n,
                                                            unsigned long long* __restrict__ count) {
     uint64_t c = 0;
-    for (int64_t i = (int64_t)blockIdx.x * kSpThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kSpThreads) {
-        const int32_t b = bins[i];
-        c += (b >= 0 && b < nq && fabs(qv[b]) > 1e-8) ? 1u : 0u;
-    }
+    for (int64_t i = (int64_t)blockIdx.x * kSpThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kSpThreads)
+        c += fabs(vals[i]) > 1e-8 ? 1u : 0u;
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) c += __shfl_xor(c, off, 64);
     if ((threadIdx.x & 63) == 0 && c) atomicAdd(count, (unsigned long long)c);
 }
-hipError_t launch_count_live(hipStream_t st, const int32_t* bins, int64_t n, const double* qv, int nq,
-                             uint64_t* count) {
+hipError_t launch_count_live(hipStream_t st, const double* vals, int64_t n, uint64_t* count) {
     hipError_t e = hipMemsetAsync(count, 0, sizeof(uint64_t), st);
     if (e != hipSuccess || n <= 0) return e;
     const int64_t grid = std::min<int64_t>(sp_tiles(n, kSpThreads * 8), 4096);
-    hipLaunchKernelGGL(k_count_live, dim3((unsigned)grid), dim3(kSpThreads), 0, st, bins, n, qv, nq,
+    hipLaunchKernelGGL(k_count_live, dim3((unsigned)grid), dim3(kSpThreads), 0, st, vals, n,
                        reinterpret_cast<unsigned long long*>(count));
     return hipGetLastError();
 }

@@ -579,7 +579,16 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const void* vals, bool f64, int6
 }
 
 // DeltaAdaptive decode of all groups + MinMax query: grouped keys/bins into gk/gb.
-int decode_groups(skml_ctx* c, const skml_sparse* s, int32_t* gk, int32_t* gb, bool query) {
+// DecodeValues: restore quantValues[bin] (qv on the device, nq of them) into gv instead of / beside
+// the bins (Gradient.sum's restore); a bin outside qv sets *err.
+struct DecodeValues {
+    const double* qv;
+    int nq;
+    double* gv;
+    unsigned* err;
+};
+int decode_groups(skml_ctx* c, const skml_sparse* s, int32_t* gk, int32_t* gb, bool query,
+                  const DecodeValues* dv = nullptr) {
     hipStream_t st = ctx_stream(c);
     const SpGroups& G = s->g;
     const int64_t n = s->nnz;
@@ -617,7 +626,8 @@ int decode_groups(skml_ctx* c, const skml_sparse* s, int32_t* gk, int32_t* gb, b
         if (!tnar) return sfail(SKML_E_OOM, "decode scratch (table image)");
         SP_HIP(launch_narrow_table(st, tab, s->ncells, width, tnar));
     }
-    SP_HIP(launch_dec_keys(st, delta, n, s->g_dev, G, ts2, gpre, tab, tnar, width, gk, gb));
+    SP_HIP(launch_dec_keys(st, delta, n, s->g_dev, G, ts2, gpre, tab, tnar, width, gk, gb, dv ? dv->qv : nullptr,
+                           dv ? dv->nq : 0, dv ? dv->gv : nullptr, dv ? dv->err : nullptr));
     return SKML_OK;
 }
 
@@ -1807,7 +1817,7 @@ int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t
     // batch starts the sum at +0.0, later ones continue from it, the last one applies the scale
     constexpr size_t kBudget = (size_t)3 << 30;
     auto need_of = [&](int p) {
-        return (size_t)views[(size_t)p].nnz * 8 + (size_t)views[(size_t)p].g.G * (size_t)(ntiles + 1) * 4 + 1024;
+        return (size_t)views[(size_t)p].nnz * 12 + (size_t)views[(size_t)p].g.G * (size_t)(ntiles + 1) * 4 + 1024;
     };
     std::vector<int> todo;
     for (int p = 0; p < P; p++)
@@ -1834,9 +1844,9 @@ int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t
             nb += (int64_t)views[(size_t)todo[q]].g.G * (ntiles + 1);
         }
         int32_t* gk = scratch<int32_t>(c, kSlotCKeys, (size_t)nk);
-        int32_t* gb = scratch<int32_t>(c, kSlotCVals, (size_t)nk);
+        double* gv = scratch<double>(c, kSlotCVals, (size_t)nk);
         int32_t* bounds = scratch<int32_t>(c, kSlotCells, (size_t)nb);
-        if (!gk || !gb || !bounds) return sfail(SKML_E_OOM, "decode_sum scratch (%lld keys)", (long long)nk);
+        if (!gk || !gv || !bounds) return sfail(SKML_E_OOM, "decode_sum scratch (%lld keys)", (long long)nk);
         SP_HIP(hipMemsetAsync(bounds, 0, sizeof(int32_t) * (size_t)nb, st));  // empty groups: every bound 0
         std::vector<AggPayload> pays;
         int64_t ko = 0, bo = 0;
@@ -1845,16 +1855,15 @@ int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t
             const skml_sparse& v = views[(size_t)p];
             AggPayload a{};
             a.gk = gk + ko;
-            a.gb = gb + ko;
-            a.qv = reinterpret_cast<const double*>(static_cast<const uint8_t*>(blobs) + (size_t)p * stride +
-                                                   hs[(size_t)p].off_values);
+            a.gv = gv + ko;
             a.bounds = bounds + bo;
-            a.gp = v.g_dev;
-            a.nq = (int32_t)v.qvalues.size();
             a.G = v.g.G;
-            if (int e = decode_groups(c, &v, const_cast<int32_t*>(a.gk), const_cast<int32_t*>(a.gb), true)) return e;
+            const DecodeValues dv{reinterpret_cast<const double*>(static_cast<const uint8_t*>(blobs) + (size_t)p * stride +
+                                                                  hs[(size_t)p].off_values),
+                                  (int)v.qvalues.size(), gv + ko, err};
+            if (int e = decode_groups(c, &v, gk + ko, nullptr, true, &dv)) return e;
             if (v.nnz > lim) {  // live <= nnz: only then can toAuto pick the dense form
-                SP_HIP(launch_count_live(st, a.gb, v.nnz, a.qv, a.nq, live));
+                SP_HIP(launch_count_live(st, a.gv, v.nnz, live));
                 uint64_t nlive = 0;
                 if (int e = sync_to_host(c, &nlive, live, sizeof(nlive))) return e;
                 a.dense_form = (int64_t)nlive > lim ? 1 : 0;
