@@ -389,6 +389,205 @@ __global__ __launch_bounds__(kSpThreads) void k_compact(const T* __restrict__ x,
     }
 }
 
+// fp32 compaction over big tiles: kCbSub sub-tiles of 8,192 values per workgroup, processed in
+// turn (the next sub-tile's 32 KiB of loads in flight while the current one is ranked), their kept
+// values and in-sub-tile offsets staged in LDS; one decoupled look-back per 65,536 values (a
+// quarter of k_compact's: its prefix frontier, 64 tiles per look-back step, no longer trails the
+// tiles' arrival), then coalesced stores.  A tile keeping more than kCbCap values re-reads its
+// input and stores directly.
+constexpr int kCbSlabs = 8;                              // float4 slabs per thread per sub-tile
+constexpr int kCbSubElems = kCbSlabs * 4 * kSpThreads;  // 8,192 values
+constexpr int kCbSub = 8, kCbTile = kCbSub * kCbSubElems, kCbCap = 8192;
+static_assert(kCbSlabs % 4 == 0, "16-bit slab counts, 4 per u64");
+
+// keep mask and in-sub-tile ranks of one sub-tile held as f[kCbSlabs][4] (slab j = float4 j * 256 + t)
+struct CbRanks {
+    uint32_t keep;
+    uint32_t slab_pre[kCbSlabs];  // exclusive start of this thread's kept values of slab j in the sub-tile
+    uint32_t total;               // kept values in the sub-tile
+};
+__device__ __forceinline__ void cb_rank(const float (&f)[kCbSlabs][4], uint32_t (*wtot)[kCbSlabs], CbRanks& R) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    uint32_t keep = 0;
+#pragma unroll
+    for (int j = 0; j < kCbSlabs; j++)
+#pragma unroll
+        for (int e = 0; e < 4; e++) keep |= CompactT<float>::keep(f[j][e]) ? (1u << (4 * j + e)) : 0u;
+    constexpr int kW = kCbSlabs / 4;
+    uint64_t P[kW], own[kW];
+#pragma unroll
+    for (int k = 0; k < kW; k++) {
+        uint64_t v = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) v |= (uint64_t)__popc((keep >> (16 * k + 4 * q)) & 15u) << (16 * q);
+        P[k] = own[k] = v;
+    }
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+#pragma unroll
+        for (int k = 0; k < kW; k++) {
+            const uint64_t y = __shfl_up(P[k], off, 64);
+            if (lane >= off) P[k] += y;
+        }
+    }
+    if (lane == 63) {
+#pragma unroll
+        for (int j = 0; j < kCbSlabs; j++) wtot[w][j] = (uint32_t)(P[j >> 2] >> (16 * (j & 3))) & 0xFFFFu;
+    }
+    __syncthreads();
+    uint32_t total = 0;
+#pragma unroll
+    for (int j = 0; j < kCbSlabs; j++) {
+        uint32_t before = 0, tot = 0;
+#pragma unroll
+        for (int u = 0; u < kSpThreads / 64; u++) {
+            const uint32_t c = wtot[u][j];
+            before += u < w ? c : 0u;
+            tot += c;
+        }
+        const uint32_t incl = (uint32_t)(P[j >> 2] >> (16 * (j & 3))) & 0xFFFFu;
+        const uint32_t mine = (uint32_t)(own[j >> 2] >> (16 * (j & 3))) & 0xFFFFu;
+        R.slab_pre[j] = total + before + incl - mine;
+        total += tot;
+    }
+    R.keep = keep;
+    R.total = total;
+    __syncthreads();  // wtot is reused by the next sub-tile
+}
+
+__device__ __forceinline__ void cb_load(const float* __restrict__ x, int64_t base, int64_t dim,
+                                        float (&f)[kCbSlabs][4]) {
+    const int t = threadIdx.x;
+    if (base + kCbSubElems <= dim) {
+        typedef float vec4 __attribute__((ext_vector_type(4)));
+        const vec4* src = reinterpret_cast<const vec4*>(x + base);
+#pragma unroll
+        for (int j = 0; j < kCbSlabs; j++) {
+            const vec4 v = __builtin_nontemporal_load(src + j * kSpThreads + t);
+            f[j][0] = v[0], f[j][1] = v[1], f[j][2] = v[2], f[j][3] = v[3];
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < kCbSlabs; j++) {
+            const int64_t e0 = base + 4 * ((int64_t)j * kSpThreads + t);
+#pragma unroll
+            for (int e = 0; e < 4; e++) f[j][e] = e0 + e < dim ? x[e0 + e] : 0.0f;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kSpThreads) __attribute__((amdgpu_waves_per_eu(3))) void k_compact_big(const float* __restrict__ x, int64_t dim,
+                                                            int32_t* __restrict__ keys, float* __restrict__ vals,
+                                                            uint64_t* status, unsigned* ticket, int64_t ntiles,
+                                                            int64_t* nnz_out) {
+    __shared__ float st_v[kCbCap];
+    __shared__ uint16_t st_k[kCbCap];  // offset inside the sub-tile (< 2^14)
+    __shared__ uint32_t wtot[kSpThreads / 64][kCbSlabs];
+    __shared__ uint32_t sub_pre[kCbSub + 1];
+    __shared__ int64_t s_tile;
+    __shared__ uint64_t s_excl;
+    const int t = threadIdx.x;
+    if (t == 0) s_tile = (int64_t)atomicAdd(ticket, 1u);
+    __syncthreads();
+    const int64_t tile = s_tile;
+    const int64_t base = tile * kCbTile;
+    if ((reinterpret_cast<uintptr_t>(x) & 15) != 0) __builtin_trap();  // the launcher checks alignment
+    float f[kCbSlabs][4], g[kCbSlabs][4];
+    uint32_t run = 0;
+    cb_load(x, base, dim, f);
+#pragma unroll 1
+    for (int sb = 0; sb < kCbSub; sb++) {
+        float (&cur)[kCbSlabs][4] = f;
+        if (sb + 1 < kCbSub) cb_load(x, base + (int64_t)(sb + 1) * kCbSubElems, dim, g);
+        CbRanks R;
+        cb_rank(cur, wtot, R);
+        if (t == 0) sub_pre[sb] = run;
+        if (run + R.total <= (uint32_t)kCbCap) {
+#pragma unroll
+            for (int j = 0; j < kCbSlabs; j++) {
+                uint32_t pos = run + R.slab_pre[j];
+                const int off0 = 4 * (j * kSpThreads + t);
+#pragma unroll
+                for (int e = 0; e < 4; e++)
+                    if ((R.keep >> (4 * j + e)) & 1u) {
+                        st_v[pos] = cur[j][e];
+                        st_k[pos] = (uint16_t)(off0 + e);
+                        pos++;
+                    }
+            }
+        }
+        run += R.total;
+#pragma unroll
+        for (int j = 0; j < kCbSlabs; j++)
+#pragma unroll
+            for (int e = 0; e < 4; e++) f[j][e] = g[j][e];
+    }
+    const uint32_t tile_total = run;
+    if (t < 64) {  // wave 0: publish the aggregate, then look back 64 predecessors per step
+        const int lane = t;
+        uint64_t excl = 0;
+        if (tile == 0) {
+            if (lane == 0) st_status(&status[0], kStPre | tile_total);
+        } else {
+            if (lane == 0) st_status(&status[tile], kStAgg | tile_total);
+            int64_t p = tile - 1;
+            while (true) {
+                const int64_t idx = p - lane;
+                uint64_t sv = idx >= 0 ? ld_status(&status[idx]) : kStPre;
+                while (__ballot((sv & ~kStMask) == 0)) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if ((sv & ~kStMask) == 0) sv = ld_status(&status[idx]);
+                }
+                const uint64_t pre = __ballot((sv & ~kStMask) == kStPre);
+                const int stop = pre ? __ffsll((unsigned long long)pre) - 1 : 63;
+                uint64_t contrib = lane <= stop ? (sv & kStMask) : 0;
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) contrib += __shfl_xor(contrib, off, 64);
+                excl += contrib;
+                if (pre) break;
+                p -= 64;
+            }
+            if (lane == 0) st_status(&status[tile], kStPre | (excl + tile_total));
+        }
+        if (lane == 0) {
+            s_excl = excl;
+            sub_pre[kCbSub] = tile_total;
+            if (tile == ntiles - 1) *nnz_out = (int64_t)(excl + tile_total);
+        }
+    }
+    __syncthreads();
+    const int64_t out0 = (int64_t)s_excl;
+    if (tile_total <= (uint32_t)kCbCap) {
+        for (uint32_t q = t; q < tile_total; q += kSpThreads) {
+            int sb = 0;
+#pragma unroll
+            for (int k = 1; k < kCbSub; k++) sb += q >= sub_pre[k] ? 1 : 0;
+            keys[out0 + q] = (int32_t)(base + (int64_t)sb * kCbSubElems + st_k[q]);
+            vals[out0 + q] = st_v[q];
+        }
+        return;
+    }
+    // more kept values than the stage holds: read each sub-tile again and store directly
+    for (int sb = 0; sb < kCbSub; sb++) {
+        const int64_t sbase = base + (int64_t)sb * kCbSubElems;
+        cb_load(x, sbase, dim, f);
+        CbRanks R;
+        cb_rank(f, wtot, R);
+#pragma unroll
+        for (int j = 0; j < kCbSlabs; j++) {
+            int64_t pos = out0 + sub_pre[sb] + R.slab_pre[j];
+            const int64_t e0 = sbase + 4 * ((int64_t)j * kSpThreads + t);
+#pragma unroll
+            for (int e = 0; e < 4; e++)
+                if ((R.keep >> (4 * j + e)) & 1u) {
+                    keys[pos] = (int32_t)(e0 + e);
+                    vals[pos] = f[j][e];
+                    pos++;
+                }
+        }
+    }
+}
+
 template <typename T>
 hipError_t launch_compact_t(hipStream_t st, const T* x, int64_t dim, int32_t* keys, T* vals, uint64_t* status,
                             unsigned* ticket, int64_t* nnz_out) {
@@ -400,7 +599,12 @@ hipError_t launch_compact_t(hipStream_t st, const T* x, int64_t dim, int32_t* ke
 }
 hipError_t launch_compact(hipStream_t st, const float* x, int64_t dim, int32_t* keys, float* vals,
                           uint64_t* status, unsigned* ticket, int64_t* nnz_out) {
-    return launch_compact_t<float>(st, x, dim, keys, vals, status, ticket, nnz_out);
+    if ((reinterpret_cast<uintptr_t>(x) & 15) != 0 || dim < kCbTile)  // small or unaligned: the one-tile kernel
+        return launch_compact_t<float>(st, x, dim, keys, vals, status, ticket, nnz_out);
+    const int64_t tiles = sp_tiles(dim, kCbTile);
+    hipLaunchKernelGGL(k_compact_big, dim3((unsigned)tiles), dim3(kSpThreads), 0, st, x, dim, keys, vals, status,
+                       ticket, tiles, nnz_out);
+    return hipGetLastError();
 }
 hipError_t launch_compact64(hipStream_t st, const double* x, int64_t dim, int32_t* keys, double* vals,
                             uint64_t* status, unsigned* ticket, int64_t* nnz_out) {

@@ -145,6 +145,20 @@ def test_compaction_exact(gpu):
         assert np.array_equal(v.cpu().numpy().view(np.uint32), x[want].view(np.uint32))
 
 
+@pytest.mark.parametrize("dim,density", [(65535, 0.1), (65536, 0.1), (65537, 0.05), (5 * 65536 + 77, 0.1),
+                                         (2**21 + 9, 0.124), (2**21 + 9, 0.13), (3 * 65536, 0.0)])
+def test_compaction_big_tiles(gpu, dim, density):
+    """The 65,536-value tiles of k_compact_big: kept values staged in LDS up to 8,192 per tile (a
+    tile above that re-reads its input), partial last tiles, all-zero input."""
+    rng = np.random.default_rng(dim)
+    x = np.where(rng.random(dim) < density, rng.standard_normal(dim), 0.0).astype(np.float32)
+    x[rng.random(dim) < 0.001] = np.float32(1e-8)
+    k, v = gpu.to_sparse(torch.from_numpy(x).cuda())
+    want = np.nonzero(np.abs(x.astype(np.float64)) > 1e-8)[0]
+    assert np.array_equal(k.cpu().numpy(), want)
+    assert np.array_equal(v.cpu().numpy().view(np.uint32), x[want].view(np.uint32))
+
+
 def test_dense_as_sparse_matches_oracle(gpu):
     rng = np.random.default_rng(8)
     dim = 400000
