@@ -1465,11 +1465,30 @@ int ensure_dev_buf(void** p, size_t* cap, size_t bytes, hipStream_t st) {
 }
 
 int ensure_host_path(skml_ctx* c) {
-    if (!c->hpin[0]) {
+    if (!c->hpin[0] || !c->hpin[1] || !c->hev[0] || !c->hev[1]) {
+        // all four or nothing: a partial setup is freed so the next call starts over
+        auto undo = [c]() {
+            for (int b = 0; b < 2; b++) {
+                if (c->hpin[b]) (void)hipHostFree(c->hpin[b]);
+                if (c->hev[b]) (void)hipEventDestroy(c->hev[b]);
+                c->hpin[b] = nullptr;
+                c->hev[b] = nullptr;
+            }
+            c->hpin_cap = 0;
+            (void)hipGetLastError();
+        };
+        undo();
         for (int b = 0; b < 2; b++) {
-            if (hipHostMalloc(&c->hpin[b], kHostPiece, hipHostMallocDefault) != hipSuccess)
+            if (hipHostMalloc(&c->hpin[b], kHostPiece, hipHostMallocDefault) != hipSuccess) {
+                c->hpin[b] = nullptr;
+                undo();
                 return fail(SKML_E_OOM, "pinned staging of %zu B", kHostPiece);
-            HIP_TRY(hipEventCreateWithFlags(&c->hev[b], hipEventDisableTiming));
+            }
+            if (hipEventCreateWithFlags(&c->hev[b], hipEventDisableTiming) != hipSuccess) {
+                c->hev[b] = nullptr;
+                undo();
+                return fail(SKML_E_HIP, "staging event");
+            }
         }
         c->hpin_cap = kHostPiece;
     }
@@ -1840,6 +1859,12 @@ int skml_delta_decode_host(skml_ctx* c, int64_t n, int32_t num_intervals, int32_
 namespace skml {
 hipStream_t ctx_stream(skml_ctx* c) { return c->stream; }
 int ctx_side_fork(skml_ctx* c, hipStream_t* side, hipEvent_t* fork, hipEvent_t* join) {
+    // SKML_SERIAL=1 (profiling): no fork, every kernel runs alone on the caller's stream
+    static const bool serial = [] {
+        const char* e = std::getenv("SKML_SERIAL");
+        return e && e[0] == '1';
+    }();
+    if (serial) return SKML_E_STATE;
     if (int st = ensure_side(c)) return st;
     if (!c->ev_fork2) HIP_TRY(hipEventCreateWithFlags(&c->ev_fork2, hipEventDisableTiming));
     if (!c->ev_join2) HIP_TRY(hipEventCreateWithFlags(&c->ev_join2, hipEventDisableTiming));

@@ -35,9 +35,13 @@ class Quantizer:
 
     def __init__(self, binNum: int = DEFAULT_BIN_NUM, seed: int = 0, deferred: bool = False):
         """deferred=True: quantize() only queues the encode on the stream and returns (no host
-        synchronisation; the payload buffer is reused across calls); the header is read, and a
-        NaN input raises QuantileSketchException, at the first getter (getBins, getSplits,
-        writeObject, ...).  The default keeps the reference's eager behaviour."""
+        synchronisation); the header is read, and a NaN input raises QuantileSketchException, at
+        the first getter (getBins, getSplits, writeObject, ...) or at the next quantize(),
+        whichever comes first.  The next quantize() reads the previous header first (one
+        synchronisation) because QuantileQuantizer.java:42 carries the binNum that Maths.unique
+        reduced into the next encode.  Every encode gets a payload buffer of its own, so a
+        `payload` reference taken earlier keeps its bytes.  The default keeps the reference's
+        eager behaviour."""
         self.binNum = int(binNum)
         self.seed = int(seed)
         self._deferred = bool(deferred)
@@ -89,6 +93,12 @@ class Quantizer:
               (True, False): "skml_dense_encode_uniform_f32", (True, True): "skml_dense_encode_uniform_f64"}
 
     def _encode(self, values, dedup: bool, uniform: bool = False, threads: int = 1):
+        if self._deferred and self.payload is not None and self._hdr is None:
+            try:
+                self._load_header()  # the previous encode's effective binNum (and its NaN status)
+            except QuantileSketchException:
+                self.payload = None  # reported once; the next quantize starts clean
+                raise
         x = as_device_values(values, self.device)
         self._wide = x.dtype == torch.float64
         self.device = x.device
@@ -98,9 +108,7 @@ class Quantizer:
         nbytes = _lib.lib.skml_dense_payload_bytes(self.n, self.binNum)
         if nbytes == 0:
             raise SketchMLException(f"bad quantizer arguments n={self.n} binNum={self.binNum}")
-        if not (self._deferred and self.payload is not None and self.payload.numel() >= nbytes
-                and self.payload.device == x.device):
-            self.payload = alloc_aligned(nbytes, x.device)
+        self.payload = alloc_aligned(nbytes, x.device)
         p = _lib.Params()
         _lib.lib.skml_params_default(C.byref(p))
         p.bin_num = self.binNum

@@ -101,6 +101,32 @@ def test_deferred_quantize(gpu):
         q.getBinNum()
 
 
+def test_deferred_back_to_back_matches_eager(gpu):
+    """Two deferred quantizes with no getter between them: the second runs with the binNum that
+    Maths.unique reduced in the first (QuantileQuantizer.java:42), as the eager path does, and the
+    first payload keeps its bytes (each encode owns its buffer)."""
+    rng = np.random.default_rng(9)
+    xs = [np.round(rng.standard_normal(200_003), 1).astype(np.float32) for _ in range(2)]  # ~80 distinct values
+    eager = gpu.QuantileQuantizer(256, seed=4)
+    lazy = gpu.QuantileQuantizer(256, seed=4, deferred=True)
+    kept = []
+    for x in xs:
+        eager.quantize(torch.from_numpy(x).cuda())
+        lazy.quantize(torch.from_numpy(x).cuda())
+        kept.append((lazy.payload, eager.getBinNum(), eager.getBins().clone()))
+    assert kept[0][1] < 256  # unique shrank the first encode's binNum
+    assert lazy.getBinNum() == eager.getBinNum()
+    assert torch.equal(lazy.getBins(), eager.getBins())
+    first = gpu.QuantileQuantizer(256, seed=4)
+    first.quantize(torch.from_numpy(xs[0]).cuda())
+    assert torch.equal(kept[0][0][: first.payload.numel()].cpu(), first.payload.cpu())
+    lazy.quantize(torch.from_numpy(np.array([1.0, np.nan, 2.0] * 100, np.float32)).cuda())
+    with pytest.raises(gpu.QuantileSketchException):
+        lazy.quantize(torch.from_numpy(xs[0]).cuda())  # the queued NaN encode surfaces here
+    lazy.quantize(torch.from_numpy(xs[0]).cuda())  # reported once; this one runs
+    assert lazy.getBinNum() == kept[0][1]
+
+
 def test_leaf_exact_path_handover(gpu):
     """The 64-keys-per-lane leaf runs a wave's rounds on a fast loop until the wave has seen both
     -0.0 and +0.0, then redoes that round and the rest on the exact-merge loop.  Zeros placed so
