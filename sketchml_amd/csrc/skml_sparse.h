@@ -91,7 +91,12 @@ hipError_t launch_part_scatter(hipStream_t st, const int32_t* keys, const void* 
                                int32_t* gbins);
 // Deltas, bitsNeeded histogram, order check, and the per-bucket pair counts of the bucketed
 // MinMaxSketch.insert (bucket_count: nbuckets u64, zeroed; unused when rows == 0).
-constexpr int kMmCellsPerBucket = 8192;  // MinMax cells per bucket (64 KB of u64 minima in LDS)
+#ifndef SKML_MM_BUCKET_BITS
+#define SKML_MM_BUCKET_BITS 15
+#endif
+// MinMax cells per bucket: 128 KB of u32 minima in LDS (narrow pairs); key-carrying pairs take
+// the bucket in sub-ranges of 8192 cells (64 KB of u64 minima each)
+constexpr int kMmCellsPerBucket = 1 << SKML_MM_BUCKET_BITS;
 // cells (rows x n int32, may be null): each (element, row) pair's table cell, kept for the scatter.
 // tile_off ([tiles of kMmChunk][nbuckets] u32, may be null): each tile's reserved offset inside
 // each bucket, taken while counting, so the scatter needs neither a count pass nor atomics.

@@ -900,12 +900,15 @@ hipError_t launch_part_scatter(hipStream_t st, const int32_t* keys, const void* 
 // Group prep: deltas / bitsNeeded / order check / MinMax insert
 // =============================================================================================
 // MinMaxSketch.insert, bucketed: every (element, row) pair targets table cell c; pairs are
-// counted per bucket of 8192 cells, scattered into bucket order, and each bucket's minimum is
+// counted per bucket of kMmBucketCells cells, scattered into bucket order, and each bucket's minimum is
 // taken with LDS atomics by one workgroup (random global 64-bit atomics were HBM-latency bound).
-// Pair word: |bin - zero| [63:48], key [47:17], bin < zero [16], cell % 8192 [12:0]; its value
-// with the cell bits cleared orders by (distance, key): the smaller distance wins and ties keep
-// the earlier insert (keys ascend within a group).
-constexpr int kMmBucketBits = 13;
+// Pair word: |bin - zero| [63:48], key [47:17], bin < zero [16], cell % kMmBucketCells [14:0]; its
+// value with the cell bits cleared orders by (distance, key): the smaller distance wins and ties
+// keep the earlier insert (keys ascend within a group).
+constexpr int kMmBucketBits = SKML_MM_BUCKET_BITS;
+static_assert(kMmBucketBits >= 13 && kMmBucketBits <= 15, "pair layouts hold 13..15 cell bits");
+constexpr int kMmSubBits = 13;  // key-carrying pairs: u64 LDS minima over 8192-cell sub-ranges
+constexpr int kMmSubCells = 1 << kMmSubBits;
 constexpr int kMmBucketCells = kMmCellsPerBucket;
 static_assert(kMmBucketCells == 1 << kMmBucketBits, "bucket size");
 constexpr int kMmLdsBuckets = 8192;  // per-workgroup bucket tables in LDS up to this many (96 KB in the scatter)
@@ -966,10 +969,11 @@ __device__ __forceinline__ uint32_t mm_pad(uint32_t c, bool narrow) {
 }
 constexpr uint64_t kMmNoPair = ~0ull;
 constexpr uint32_t kMmNoPair32 = ~0u;
-// Narrow pair word (SpGroups.mm_narrow): |bin - zero| [29:14], bin < zero [13], cell % 8192 [12:0].
-// In a one-sided group the sign bit is constant, so the minimum over a cell is the nearest bin.
+// Narrow pair word (SpGroups.mm_narrow): |bin - zero| [31:B+1], bin < zero [B], cell % 2^B
+// [B-1:0] with B = kMmBucketBits (|bin - zero| < 65536 fits 31 - B >= 16 bits).  In a one-sided
+// group the sign bit is constant, so the minimum over a cell is the nearest bin.
 __device__ __forceinline__ uint32_t mm_pair32(int32_t bin, int32_t zero, int64_t cell) {
-    return ((uint32_t)mm_dist(bin, zero) << 14) | ((bin < zero ? 1u : 0u) << 13) |
+    return ((uint32_t)mm_dist(bin, zero) << (kMmBucketBits + 1)) | ((bin < zero ? 1u : 0u) << kMmBucketBits) |
            (uint32_t)(cell & (kMmBucketCells - 1));
 }
 __device__ __forceinline__ int64_t mm_cell(const SpGroups* gp, int g, int r, int32_t key) {
@@ -1505,12 +1509,16 @@ hipError_t launch_mm_scatter(hipStream_t st, const int32_t* gkeys, const int32_t
 }
 
 // One workgroup per bucket: LDS minimum per cell, then the int32 table cells (empty -> fill).
-// Narrow pairs (SpGroups.mm_narrow) take 32-bit LDS minima over (distance, sign).
+// Narrow pairs (SpGroups.mm_narrow) take 32-bit LDS minima over (distance, sign) for the whole
+// bucket; key-carrying pairs take 64-bit minima, one 8192-cell sub-range after the other (each
+// sub-range re-reads the bucket's pairs; this path only runs for groups on both sides of zeroIdx).
 __global__ __launch_bounds__(kMmThreads) void k_mm_bucket(const void* __restrict__ pairs_v,
                                                           const uint64_t* __restrict__ bucket_base,
                                                           const SpGroups* __restrict__ gp,
                                                           int32_t* __restrict__ table) {
-    __shared__ unsigned long long cmin[kMmBucketCells];
+    constexpr int kWords = kMmBucketCells / 2 > kMmSubCells ? kMmBucketCells / 2 : kMmSubCells;
+    __shared__ unsigned long long cm64[kWords];  // u32 minima of the bucket, or u64 of a sub-range
+    uint32_t* cm = reinterpret_cast<uint32_t*>(cm64);
     const int b = blockIdx.x;
     const int64_t ncells = gp->ncells;
     if (gp->status || ((int64_t)b << kMmBucketBits) >= ncells) return;
@@ -1519,7 +1527,6 @@ __global__ __launch_bounds__(kMmThreads) void k_mm_bucket(const void* __restrict
     const int64_t cell0 = (int64_t)b << kMmBucketBits;
     if (gp->mm_narrow) {
         const uint32_t* pairs = static_cast<const uint32_t*>(pairs_v);
-        uint32_t* cm = reinterpret_cast<uint32_t*>(cmin);
         for (int j = threadIdx.x; j < kMmBucketCells; j += kMmThreads) cm[j] = ~0u;
         __syncthreads();
         constexpr uint32_t kLo = (uint32_t)(kMmBucketCells - 1);
@@ -1545,26 +1552,33 @@ __global__ __launch_bounds__(kMmThreads) void k_mm_bucket(const void* __restrict
         return;
     }
     const uint64_t* pairs = static_cast<const uint64_t*>(pairs_v);
-    for (int j = threadIdx.x; j < kMmBucketCells; j += kMmThreads) cmin[j] = ~0ull;
-    __syncthreads();
-    constexpr uint64_t kLo = (uint64_t)(kMmBucketCells - 1);
-    for (uint64_t p = p0 + threadIdx.x; p < p1; p += kBucketBatch * kMmThreads) {
-        uint64_t v[kBucketBatch];
+    unsigned long long* cmin = cm64;
+    constexpr uint64_t kLo = (uint64_t)(kMmBucketCells - 1), kSubLo = (uint64_t)(kMmSubCells - 1);
+    for (int sub = 0; sub < kMmBucketCells / kMmSubCells; sub++) {
+        const int64_t s0 = cell0 + (int64_t)sub * kMmSubCells;
+        if (s0 >= ncells) break;
+        if (sub) __syncthreads();  // the previous sub-range's cells are written
+        for (int j = threadIdx.x; j < kMmSubCells; j += kMmThreads) cmin[j] = ~0ull;
+        __syncthreads();
+        for (uint64_t p = p0 + threadIdx.x; p < p1; p += kBucketBatch * kMmThreads) {
+            uint64_t v[kBucketBatch];
 #pragma unroll
-        for (int u = 0; u < kBucketBatch; u++) v[u] = p + u * kMmThreads < p1 ? pairs[p + u * kMmThreads] : kMmNoPair;
+            for (int u = 0; u < kBucketBatch; u++) v[u] = p + u * kMmThreads < p1 ? pairs[p + u * kMmThreads] : kMmNoPair;
 #pragma unroll
-        for (int u = 0; u < kBucketBatch; u++)
-            if (v[u] != kMmNoPair) atomicMin(&cmin[v[u] & kLo], (unsigned long long)(v[u] & ~kLo));
-    }
-    __syncthreads();
-    for (int j = threadIdx.x; j < kMmBucketCells && cell0 + j < ncells; j += kMmThreads) {
-        const uint64_t v = cmin[j];
-        int32_t out = fill;
-        if (v != ~0ull) {
-            const int32_t dist = (int32_t)(v >> 48);
-            out = ((v >> 16) & 1u) ? zero - dist : zero + dist;
+            for (int u = 0; u < kBucketBatch; u++)
+                if (v[u] != kMmNoPair && (int)((v[u] & kLo) >> kMmSubBits) == sub)
+                    atomicMin(&cmin[v[u] & kSubLo], (unsigned long long)(v[u] & ~kLo));
         }
-        table[cell0 + j] = out;
+        __syncthreads();
+        for (int j = threadIdx.x; j < kMmSubCells && s0 + j < ncells; j += kMmThreads) {
+            const uint64_t v = cmin[j];
+            int32_t out = fill;
+            if (v != ~0ull) {
+                const int32_t dist = (int32_t)(v >> 48);
+                out = ((v >> 16) & 1u) ? zero - dist : zero + dist;
+            }
+            table[s0 + j] = out;
+        }
     }
 }
 

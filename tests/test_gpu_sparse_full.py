@@ -200,13 +200,15 @@ def _has_mixed_group(zero, bins, groups):
     return False
 
 
-@pytest.mark.parametrize("pos_frac,mixed", [(0.02, True), (0.05, True), (0.5, False)])
-def test_minmax_pair_width_paths(gpu, pos_frac, mixed):
+@pytest.mark.parametrize("pos_frac,mixed,dim", [(0.02, True, 200000), (0.05, True, 200000), (0.5, False, 200000),
+                                                  (0.03, True, 2000003), (0.5, False, 2000003)])
+def test_minmax_pair_width_paths(gpu, pos_frac, mixed, dim):
     """Mostly negative values put zeroIdx in the last group, which then holds bins on both sides of
     it (8-byte pairs, the first insert wins a distance tie); balanced values keep every group
-    one-sided (4-byte pairs).  Both give the oracle's tables, bit for bit."""
+    one-sided (4-byte pairs).  Both give the oracle's tables, bit for bit.  The larger dim spans
+    several 32768-cell buckets (the 8-byte path takes each in four 8192-cell sub-ranges)."""
     rng = np.random.default_rng(5)
-    keys = np.nonzero(rng.random(200000) < 0.3)[0].astype(np.int32)
+    keys = np.nonzero(rng.random(dim) < 0.3)[0].astype(np.int32)
     vals = -np.abs(rng.standard_normal(len(keys)))
     vals[rng.random(len(keys)) < pos_frac] *= -1
     osp = O.sparse_compress(keys, vals, 256, 8, 2, 0.3, 1, 2)
