@@ -86,9 +86,10 @@ hipError_t launch_scan_cols_major(hipStream_t st, uint64_t* sums, int64_t tiles,
 // The grid also zeroes z32[0, n32) and z64[0, n64) (the next passes' counters: no memset launches).
 hipError_t launch_part_count(hipStream_t st, const void* qpayload, int64_t n, const SpGroups* gp,
                              uint64_t* tile_counts, uint32_t* z32, int64_t n32, uint64_t* z64, int64_t n64);
+// gbins: u16 (bins < SKML_MAX_BINS = 65536)
 hipError_t launch_part_scatter(hipStream_t st, const int32_t* keys, const void* qpayload, int64_t n,
                                const SpGroups* gp, const uint64_t* tile_base, int32_t* gkeys,
-                               int32_t* gbins);
+                               uint16_t* gbins);
 // Deltas, bitsNeeded histogram, order check, and the per-bucket pair counts of the bucketed
 // MinMaxSketch.insert (bucket_count: nbuckets u64, zeroed; unused when rows == 0).
 #ifndef SKML_MM_BUCKET_BITS
@@ -106,7 +107,7 @@ hipError_t launch_group_prep(hipStream_t st, const int32_t* gkeys, int64_t n, co
 // pairs in bucket order (bucket_base: exclusive scan of the counts; cursor: nbuckets u64, zeroed).
 // Pairs are u64, or u32 when gp->mm_narrow (only with the staged scatter: mm_scatter_staged).
 bool mm_scatter_staged(bool cells, bool reserved, int nbuckets);
-hipError_t launch_mm_scatter(hipStream_t st, const int32_t* gkeys, const int32_t* gbins, int64_t n,
+hipError_t launch_mm_scatter(hipStream_t st, const int32_t* gkeys, const uint16_t* gbins, int64_t n,
                              const SpGroups* gp, const uint64_t* bucket_base, uint64_t* cursor, int nbuckets,
                              void* pairs, const int32_t* cells, const uint32_t* tile_off);
 #ifndef SKML_MM_CHUNK

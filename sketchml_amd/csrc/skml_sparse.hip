@@ -779,7 +779,7 @@ __global__ __launch_bounds__(kSpThreads) void k_part_scatter(const int32_t* __re
                                                              const uint8_t* __restrict__ qpayload, int64_t n,
                                                              const SpGroups* __restrict__ gp,
                                                              const uint64_t* __restrict__ tile_base,
-                                                             int32_t* __restrict__ gkeys, int32_t* __restrict__ gbins) {
+                                                             int32_t* __restrict__ gkeys, uint16_t* __restrict__ gbins) {
     if (gp->status) return;
     constexpr int kWaves = kSpThreads / 64, kSteps = kSpTile / kSpThreads;
     __shared__ int32_t E[kMaxGroups];
@@ -792,6 +792,9 @@ __global__ __launch_bounds__(kSpThreads) void k_part_scatter(const int32_t* __re
     const int bits = h->code_bits, G = gp->G;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const bool few = G <= kFewGroups;
+    // the output base of group t's run in this tile, read before the counting (no round trip later)
+    int64_t gbase = 0;
+    if (t < G) gbase = gp->gstart[t] + (int64_t)tile_base[(int64_t)t * ((int64_t)gridDim.x + 1) + blockIdx.x];
     if (!few) {
         load_edges(gp, E);
         for (int j = t; j < kWaves * kMaxGroups; j += kSpThreads) wb[j / kMaxGroups][j % kMaxGroups] = 0;
@@ -833,7 +836,6 @@ __global__ __launch_bounds__(kSpThreads) void k_part_scatter(const int32_t* __re
     __syncthreads();
     // the tile in group order in LDS: wave w's elements of group g at loc[g] + (earlier waves' g)
     if (t < 64) {
-        const int64_t ld = (int64_t)gridDim.x + 1;  // tile_base: one column of tiles + 1 per group
         uint32_t c = 0;
         if (lane < G)
             for (int j = 0; j < kWaves; j++) c += (uint32_t)wb[j][lane];
@@ -845,7 +847,7 @@ __global__ __launch_bounds__(kSpThreads) void k_part_scatter(const int32_t* __re
         }
         if (lane < G) {
             uint32_t run = x - c;
-            gdst[lane] = gp->gstart[lane] + (int64_t)tile_base[lane * ld + blockIdx.x] - (int64_t)run;
+            gdst[lane] = gbase - (int64_t)run;
             for (int j = 0; j < kWaves; j++) {
                 const uint32_t cj = (uint32_t)wb[j][lane];
                 wb[j][lane] = run;
@@ -882,13 +884,13 @@ __global__ __launch_bounds__(kSpThreads) void k_part_scatter(const int32_t* __re
     for (int q = t; q < tile_n; q += kSpThreads) {
         const int64_t dst = gdst[sg[q]] + q;
         gkeys[dst] = sk[q];
-        gbins[dst] = sb[q];
+        gbins[dst] = (uint16_t)sb[q];
     }
 }
 
 hipError_t launch_part_scatter(hipStream_t st, const int32_t* keys, const void* qpayload, int64_t n,
                                const SpGroups* gp, const uint64_t* tile_base, int32_t* gkeys,
-                               int32_t* gbins) {
+                               uint16_t* gbins) {
     const int64_t tiles = sp_tiles(n, kSpTile);
     if (tiles <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_part_scatter, dim3((unsigned)tiles), dim3(kSpThreads), 0, st, keys,
@@ -1114,7 +1116,9 @@ __global__ __launch_bounds__(kMmThreads) void k_group_prep(const int32_t* __rest
                 nb = d > 0 ? 32 - __clz(d) : 1;
             }
             need[i] = (uint8_t)nb;
+#ifndef SKML_ABLATE_GP_HIST  // timing ablation only (wrong histogram)
             atomicAdd(&H[g * kDeltaHist + nb], 1u);
+#endif
         }
         if (one) {
             const MmGroup& q = GP[g_lo];
@@ -1206,7 +1210,7 @@ hipError_t launch_group_prep(hipStream_t st, const int32_t* gkeys, int64_t n, co
 // reserved 64-bit destinations sit in LDS, so the scatter never waits on a global load.
 constexpr int kMmUnroll = 4;
 __global__ __launch_bounds__(kMmThreads) void k_mm_scatter(const int32_t* __restrict__ gkeys,
-                                                           const int32_t* __restrict__ gbins, int64_t n,
+                                                           const uint16_t* __restrict__ gbins, int64_t n,
                                                            const SpGroups* __restrict__ gp,
                                                            const uint64_t* __restrict__ bucket_base,
                                                            unsigned long long* __restrict__ cursor, int nbuckets,
@@ -1336,7 +1340,7 @@ __device__ __forceinline__ uint32_t block_excl_scan_u32(uint32_t v, uint32_t* sh
 // PAIR: uint64_t (key-carrying pairs) or uint32_t (narrow pairs, SpGroups.mm_narrow).
 template <int T, typename PAIR>
 __device__ __forceinline__ void mm_scatter_staged_body(const int32_t* __restrict__ gkeys,
-                                                       const int32_t* __restrict__ gbins, int64_t n,
+                                                       const uint16_t* __restrict__ gbins, int64_t n,
                                                        const SpGroups* __restrict__ gp,
                                                        const uint64_t* __restrict__ bucket_base, int nbuckets,
                                                        PAIR* __restrict__ pairs, const int32_t* __restrict__ cells_in,
@@ -1447,7 +1451,7 @@ __device__ __forceinline__ void mm_scatter_staged_body(const int32_t* __restrict
 
 template <int T>
 __global__ __launch_bounds__(T) void k_mm_scatter_staged(const int32_t* __restrict__ gkeys,
-                                                         const int32_t* __restrict__ gbins, int64_t n,
+                                                         const uint16_t* __restrict__ gbins, int64_t n,
                                                          const SpGroups* __restrict__ gp,
                                                          const uint64_t* __restrict__ bucket_base, int nbuckets,
                                                          void* __restrict__ pairs,
@@ -1475,7 +1479,7 @@ bool mm_scatter_staged(bool cells, bool reserved, int nbuckets) {
     return cells && reserved && nbuckets <= kStageBuckets;
 }
 
-hipError_t launch_mm_scatter(hipStream_t st, const int32_t* gkeys, const int32_t* gbins, int64_t n,
+hipError_t launch_mm_scatter(hipStream_t st, const int32_t* gkeys, const uint16_t* gbins, int64_t n,
                              const SpGroups* gp, const uint64_t* bucket_base, uint64_t* cursor, int nbuckets,
                              void* pairs_v, const int32_t* cells, const uint32_t* tile_off) {
     uint64_t* pairs = static_cast<uint64_t*>(pairs_v);  // the unstaged scatter: key-carrying pairs only
@@ -1612,6 +1616,32 @@ __device__ __forceinline__ void delta_lens(const DeltaShape& s, int nb, int& iv,
     dl = s.bpi * iv;
 }
 
+// need[i0, i0 + 8) (one 8-byte load when the run is whole; i0 is a multiple of 8)
+__device__ __forceinline__ void load8_need(const uint8_t* __restrict__ need, int64_t i0, int64_t n, uint8_t (&nb)[8]) {
+    if (i0 + 8 <= n) {
+        const uint2 w = *reinterpret_cast<const uint2*>(need + i0);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            nb[j] = (uint8_t)(w.x >> (8 * j));
+            nb[4 + j] = (uint8_t)(w.y >> (8 * j));
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; j++) nb[j] = i0 + j < n ? need[i0 + j] : (uint8_t)0;
+    }
+}
+// gkeys[i0, i0 + 8) (two 16-byte loads when the run is whole)
+__device__ __forceinline__ void load8_keys(const int32_t* __restrict__ k, int64_t i0, int64_t n, int32_t (&key)[8]) {
+    if (i0 + 8 <= n) {
+        const int4 a = *reinterpret_cast<const int4*>(k + i0), b = *reinterpret_cast<const int4*>(k + i0 + 4);
+        key[0] = a.x, key[1] = a.y, key[2] = a.z, key[3] = a.w;
+        key[4] = b.x, key[5] = b.y, key[6] = b.z, key[7] = b.w;
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; j++) key[j] = i0 + j < n ? k[i0 + j] : 0;
+    }
+}
+
 __global__ __launch_bounds__(kSpThreads) void k_delta_lens(const uint8_t* __restrict__ need, int64_t n,
                                                            const SpGroups* __restrict__ gp,
                                                            uint64_t* __restrict__ tile_sums) {
@@ -1623,13 +1653,15 @@ __global__ __launch_bounds__(kSpThreads) void k_delta_lens(const uint8_t* __rest
     const int64_t i0 = (int64_t)blockIdx.x * kSpTile + threadIdx.x * 8;
     uint64_t fsum = 0, dsum = 0;
     if (i0 < n) {
+        uint8_t nb[8];
+        load8_need(need, i0, n, nb);
         int g = group_of_elem(S, i0);
         DeltaShape s = delta_shape(gp, g);
         for (int j = 0; j < 8 && i0 + j < n; j++) {
             const int64_t i = i0 + j;
             while (i >= S[g + 1]) s = delta_shape(gp, ++g);
             int iv, fl, dl;
-            delta_lens(s, need[i], iv, fl, dl);
+            delta_lens(s, nb[j], iv, fl, dl);
             fsum += fl;
             dsum += dl;
         }
@@ -1696,7 +1728,14 @@ __global__ __launch_bounds__(kSpThreads) void k_delta_write(const int32_t* __res
     uint8_t nb[8];
     uint64_t fsum = 0, dsum = 0;
     int g0 = 0;
+    // every global read is issued here, before the scan: the tile's bases, the run's keys and
+    // lengths, and the key before the run (used when the run does not start its group)
+    const uint64_t fbase = tile_base[blockIdx.x * 2], dbase = tile_base[blockIdx.x * 2 + 1];
+    int32_t prev0 = 0;
     if (i0 < n) {
+        load8_keys(gkeys, i0, n, key);
+        load8_need(need, i0, n, nb);
+        prev0 = i0 > 0 ? gkeys[i0 - 1] : 0;
         g0 = group_of_elem(S, i0);
         int g = g0;
         DeltaShape s = delta_shape(gp, g);
@@ -1704,8 +1743,6 @@ __global__ __launch_bounds__(kSpThreads) void k_delta_write(const int32_t* __res
             const int64_t i = i0 + j;
             if (i >= n) break;
             while (i >= S[g + 1]) s = delta_shape(gp, ++g);
-            key[j] = gkeys[i];
-            nb[j] = need[i];
             int iv, fl, dl;
             delta_lens(s, nb[j], iv, fl, dl);
             fsum += fl;
@@ -1714,13 +1751,12 @@ __global__ __launch_bounds__(kSpThreads) void k_delta_write(const int32_t* __res
     }
     uint64_t v[2] = {fsum, dsum}, tot[2];
     block_excl_scan<2>(v, tot, sh);
-    const uint64_t fbase = tile_base[blockIdx.x * 2], dbase = tile_base[blockIdx.x * 2 + 1];
     const int64_t fw0 = (int64_t)(fbase >> 6) << 6, dw0 = (int64_t)(dbase >> 6) << 6;
     if (i0 < n) {
         int g = g0;
         DeltaShape s = delta_shape(gp, g);
         uint64_t fo = fbase + v[0], dof = dbase + v[1];
-        int32_t prev = i0 > S[g] ? gkeys[i0 - 1] : 0;
+        int32_t prev = i0 > S[g] ? prev0 : 0;
         for (int j = 0; j < 8; j++) {
             const int64_t i = i0 + j;
             if (i >= n) break;

@@ -495,7 +495,7 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const void* vals, bool f64, int6
     SP_TRY(launch_sp_plan_groups(st, s->g_dev, tc + tiles, tiles + 1));
     // ---- 3. partition, deltas / histogram / order check, bucketed MinMax insert ----
     int32_t* gk = scratch<int32_t>(c, kSlotGKeys, (size_t)nnz);
-    int32_t* gb = scratch<int32_t>(c, kSlotGBins, (size_t)nnz);
+    uint16_t* gb = scratch<uint16_t>(c, kSlotGBins, (size_t)nnz);  // grouped bins (< 65536)
     uint8_t* need = scratch<uint8_t>(c, kSlotNeed, (size_t)nnz);
     // per (tile, bucket) reserved offsets (u32: a bucket holds fewer than 2^32 pairs)
     const int64_t mm_tiles = sp_tiles(nnz, kMmChunkElems);
