@@ -26,6 +26,7 @@
 // Arrays.sort's order for everything but NaN (flagged at load).  The merges equal the reference
 // merge (IEEE `<`, ties emit the newer run) unless a merge sees both -0.0 and +0.0; a wave that
 // has seen both takes the exact LDS path (count-based merge positions with the reference tie rule).
+#include <cstdlib>
 #include <cstring>
 #include <type_traits>
 
@@ -567,15 +568,24 @@ constexpr int kL64Rounds = kLeafWaveChunks / kL64Chunks;
 #ifndef SKML_LEAF64_WAVES
 #define SKML_LEAF64_WAVES 4
 #endif
+#ifndef SKML_LEAF_SPLIT_BELOW
+#define SKML_LEAF_SPLIT_BELOW 3072  // full tiles under which k_leaf64<true> runs
+#endif
 // `chunks` counts the full tiles' chunks; when total_chunks holds a partial tile as well, that
 // tile's small trees (k_leaf2's PARTIAL path, one wave) run in workgroup 0, which is dispatched
 // first, so they overlap the full tiles instead of following them.
+// SPLIT (buckets with fewer tiles than the chip has wave slots): the workgroup's 4 waves share one
+// tile, wave w running round w to its level-4 node; waves 1 and 3 merge the pairs to level 5 and
+// wave 3 the level-6 node (exact merges there when the waves' zero signs differ), so a small
+// bucket runs 4x the waves with the same outputs.
+template <bool SPLIT>
 __global__ __launch_bounds__(256, SKML_LEAF64_WAVES) void k_leaf64(const float* __restrict__ x, int64_t chunks, uint64_t s0,
                                                    const uint64_t* __restrict__ tab, LeafPartial* __restrict__ part,
                                                    float* __restrict__ nodes6, float* __restrict__ roots,
                                                    uint8_t* __restrict__ ubits, int64_t total_chunks) {
     __shared__ float fb[kLeaf2Waves][kWaveFb];
     __shared__ float2 stk[kLeaf2Waves][2][64];  // the carry stack (levels 4, 5) in LDS, not registers
+    __shared__ uint32_t wpart[kLeaf2Waves][4];  // SPLIT: each wave's min / max / flags / zero signs
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     int64_t blk = blockIdx.x;
     if (total_chunks > chunks) {
@@ -587,13 +597,14 @@ __global__ __launch_bounds__(256, SKML_LEAF64_WAVES) void k_leaf64(const float* 
         }
         blk -= 1;
     }
-    const int64_t tile = blk * kLeaf2Waves + wave;
+    const int64_t tile = SPLIT ? blk : blk * kLeaf2Waves + wave;
     const int64_t c_tile = tile * kLeafWaveChunks;
-    if (c_tile >= chunks) return;  // wave-uniform; no block barriers in this kernel
+    if (c_tile >= chunks) return;  // workgroup-uniform under SPLIT, wave-uniform otherwise
     float* wfb = fb[wave];
     uint32_t mn = ~0u, mx = 0, fl = 0u;
     bool neg_any = false, pos_any = false;
     float top[2];
+    uint64_t split_mask = 0;  // SPLIT: this wave's round draws (levels 5 and 6 read from them)
     // A round either runs fast (no merge can meet both zero signs) or exact; once the wave has
     // seen -0.0 and +0.0 it redoes the round and the rest on the exact loop, a separate code
     // region so its LDS merge paths do not take registers from the fast one.
@@ -603,7 +614,7 @@ __global__ __launch_bounds__(256, SKML_LEAF64_WAVES) void k_leaf64(const float* 
         // across the loop they push the fast path past 128 registers
         int ln = lane;
         asm volatile("" : "+v"(ln));
-        set_prio_by_progress(round, kL64Rounds);
+        if constexpr (!SPLIT) set_prio_by_progress(round, kL64Rounds);
             const int64_t c0 = c_tile + round * kL64Chunks;
             const int64_t chunk = c0 + (ln >> 2);
             float v[64];
@@ -679,6 +690,11 @@ __global__ __launch_bounds__(256, SKML_LEAF64_WAVES) void k_leaf64(const float* 
             wave_level<8>(w3, w4, ln, bit(3, 8 * (ln >> 5) + 7), exact, wfb);
             wave_level<4>(w4, n4, ln, bit(4, 15), exact, wfb);
 #endif
+            if constexpr (SPLIT) {  // the cross-wave levels follow the round loops
+                stk[wave][0][ln] = make_float2(n4[0], n4[1]);
+                split_mask = mask;
+                return true;
+            }
             // levels 5 and 6: the binary-counter carry over rounds (older node first)
             if (!(round & 1)) {
                 stk[wave][0][ln] = make_float2(n4[0], n4[1]);
@@ -699,12 +715,55 @@ __global__ __launch_bounds__(256, SKML_LEAF64_WAVES) void k_leaf64(const float* 
             wave_node_merge(st5, n5, top, ln, bit(6, 15), exact, wfb);
             return true;
     };
-    int round = 0;
+    if constexpr (SPLIT) {
+        if (!run_round(std::false_type{}, wave)) run_round(std::true_type{}, wave);
+        // per-wave partial, then levels 5 and 6 across the waves
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const uint32_t omn = __shfl_xor(mn, off, 64);
+            const uint32_t omx = __shfl_xor(mx, off, 64);
+            const uint32_t ofl = (uint32_t)__shfl_xor((int)fl, off, 64);
+            mn = omn < mn ? omn : mn;
+            mx = omx > mx ? omx : mx;
+            fl |= ofl;
+        }
+        if (lane == 0) {
+            wpart[wave][0] = mn;
+            wpart[wave][1] = mx;
+            wpart[wave][2] = fl;
+        }
+        __syncthreads();
+        // the reference's zero signs seen by a merge: a node carries its chunks' values
+        auto zs = [&](int w) { return wpart[w][2] & 6u; };
+        // draw offsets inside round 1's / 3's mask: 2 * 15 - popcount(15) + level
+        const uint32_t b5 = (uint32_t)(split_mask >> 31) & 1u, b6 = (uint32_t)(split_mask >> 32) & 1u;
+        if (wave & 1) {
+            const uint32_t z = zs(wave - 1) | zs(wave);
+            const float2 o = stk[wave - 1][0][lane], m = stk[wave][0][lane];
+            const float A[2] = {o.x, o.y}, B[2] = {m.x, m.y};
+            float n5[2];
+            wave_node_merge(A, B, n5, lane, b5, z == 6u, wfb);
+            stk[wave][1][lane] = make_float2(n5[0], n5[1]);
+        }
+        __syncthreads();
+        if (wave != 3) return;
+        {
+            const uint32_t z = zs(0) | zs(1) | zs(2) | zs(3);
+            const float2 o = stk[1][1][lane], m = stk[3][1][lane];
+            const float A[2] = {o.x, o.y}, B[2] = {m.x, m.y};
+            wave_node_merge(A, B, top, lane, b6, z == 6u, wfb);
+        }
+        mn = min(min(wpart[0][0], wpart[1][0]), min(wpart[2][0], wpart[3][0]));
+        mx = max(max(wpart[0][1], wpart[1][1]), max(wpart[2][1], wpart[3][1]));
+        fl = wpart[0][2] | wpart[1][2] | wpart[2][2] | wpart[3][2];
+    } else {
+        int round = 0;
 #pragma unroll 1
-    for (; round < kL64Rounds; round++)
-        if (!run_round(std::false_type{}, round)) break;
+        for (; round < kL64Rounds; round++)
+            if (!run_round(std::false_type{}, round)) break;
 #pragma unroll 1
-    for (; round < kL64Rounds; round++) run_round(std::true_type{}, round);
+        for (; round < kL64Rounds; round++) run_round(std::true_type{}, round);
+    }
     // one compaction bit of the upper merge tree per wave (upper_level_offset numbering)
     if (ubits && tile < upper_node_count(chunks)) {
         int L = kLeafTopLevel + 1;
@@ -715,14 +774,16 @@ __global__ __launch_bounds__(256, SKML_LEAF64_WAVES) void k_leaf64(const float* 
     }
     store_node<2>(top, lane, nodes6 + (size_t)tile * kK);
     if (((chunks >> 6) & 1) && tile == ((chunks >> 7) << 1)) store_node<2>(top, lane, roots + (size_t)6 * kK);
+    if constexpr (!SPLIT) {
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const uint32_t omn = __shfl_xor(mn, off, 64);
-        const uint32_t omx = __shfl_xor(mx, off, 64);
-        const uint32_t ofl = (uint32_t)__shfl_xor((int)fl, off, 64);
-        mn = omn < mn ? omn : mn;
-        mx = omx > mx ? omx : mx;
-        fl |= ofl;
+        for (int off = 32; off >= 1; off >>= 1) {
+            const uint32_t omn = __shfl_xor(mn, off, 64);
+            const uint32_t omx = __shfl_xor(mx, off, 64);
+            const uint32_t ofl = (uint32_t)__shfl_xor((int)fl, off, 64);
+            mn = omn < mn ? omn : mn;
+            mx = omx > mx ? omx : mx;
+            fl |= ofl;
+        }
     }
     if (lane == 0) {
         LeafPartial p;
@@ -898,6 +959,17 @@ __global__ __launch_bounds__(512, MINW) void k_leaf(const float* __restrict__ x,
     }
 }
 
+// One wave per tile fills the chip from 4,096 tiles (2^26 values) up; below that the split form
+// (four waves per tile) keeps more waves in flight.  SKML_LEAF_SPLIT=0/1 forces either (A/B runs).
+static bool leaf_split(int64_t full_tiles) {
+    static const int force = [] {
+        const char* e = std::getenv("SKML_LEAF_SPLIT");
+        return e ? std::atoi(e) : -1;
+    }();
+    if (force >= 0) return force != 0;
+    return full_tiles < SKML_LEAF_SPLIT_BELOW;
+}
+
 hipError_t launch_leaf(hipStream_t st, const float* x, int64_t chunks, uint64_t s0,
                        const uint64_t* jump_tab, LeafPartial* part, float* nodes6, float* roots, uint8_t* ubits) {
     const int64_t full = chunks / kLeafWaveChunks;
@@ -905,9 +977,15 @@ hipError_t launch_leaf(hipStream_t st, const float* x, int64_t chunks, uint64_t 
 #define SKML_LEAF64 1
 #endif
     if (full > 0 && SKML_LEAF64) {  // the partial tile, if any, rides in the same launch
-        const unsigned grid = (unsigned)((full + kLeaf2Waves - 1) / kLeaf2Waves + (chunks % kLeafWaveChunks ? 1 : 0));
-        hipLaunchKernelGGL(k_leaf64, dim3(grid), dim3(64 * kLeaf2Waves), 0, st, x, full * kLeafWaveChunks, s0, jump_tab,
-                           part, nodes6, roots, ubits, chunks);
+        const int extra = chunks % kLeafWaveChunks ? 1 : 0;
+        if (leaf_split(full)) {
+            hipLaunchKernelGGL(k_leaf64<true>, dim3((unsigned)(full + extra)), dim3(64 * kLeaf2Waves), 0, st, x,
+                               full * kLeafWaveChunks, s0, jump_tab, part, nodes6, roots, ubits, chunks);
+            return hipGetLastError();
+        }
+        const unsigned grid = (unsigned)((full + kLeaf2Waves - 1) / kLeaf2Waves + extra);
+        hipLaunchKernelGGL(k_leaf64<false>, dim3(grid), dim3(64 * kLeaf2Waves), 0, st, x, full * kLeafWaveChunks, s0,
+                           jump_tab, part, nodes6, roots, ubits, chunks);
         return hipGetLastError();
     } else if (full > 0)
         hipLaunchKernelGGL((k_leaf2<3, false>), dim3((unsigned)((full + kLeaf2Waves - 1) / kLeaf2Waves)),

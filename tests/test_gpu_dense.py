@@ -119,12 +119,19 @@ def test_deferred_back_to_back_matches_eager(gpu):
     assert torch.equal(lazy.getBins(), eager.getBins())
     first = gpu.QuantileQuantizer(256, seed=4)
     first.quantize(torch.from_numpy(xs[0]).cuda())
-    assert torch.equal(kept[0][0][: first.payload.numel()].cpu(), first.payload.cpu())
-    lazy.quantize(torch.from_numpy(np.array([1.0, np.nan, 2.0] * 100, np.float32)).cuda())
+    h = first._load_header()
+    used = h.codes_offset + (len(xs[0]) * h.code_bits + 7) // 8  # header, splits and codes (not the tail pad)
+    assert torch.equal(kept[0][0][:used].cpu(), first.payload[:used].cpu())
+    bad = torch.from_numpy(np.array([1.0, np.nan, 2.0] * 100, np.float32)).cuda()
+    with pytest.raises(gpu.QuantileSketchException):
+        eager.quantize(bad)
+    lazy.quantize(bad)
     with pytest.raises(gpu.QuantileSketchException):
         lazy.quantize(torch.from_numpy(xs[0]).cuda())  # the queued NaN encode surfaces here
+    eager.quantize(torch.from_numpy(xs[0]).cuda())
     lazy.quantize(torch.from_numpy(xs[0]).cuda())  # reported once; this one runs
-    assert lazy.getBinNum() == kept[0][1]
+    assert lazy.getBinNum() == eager.getBinNum()
+    assert torch.equal(lazy.getBins(), eager.getBins())
 
 
 def test_leaf_exact_path_handover(gpu):
