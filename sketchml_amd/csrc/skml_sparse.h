@@ -183,8 +183,10 @@ struct SpBlobHeader {
 static_assert(sizeof(SpBlobHeader) <= 256, "blob header fits its 256-byte section");
 // One round of pairwise stable merges of sorted runs (Sort.merge order: lower run first on ties).
 // run_start: nruns + 1 device offsets; total = run_start[nruns].
+// run_start: nruns + 1 HOST offsets (passed to the kernels by value); split: (total / 2048 + 2)
+// int64 device scratch (the tile boundaries' merge-path split points)
 hipError_t launch_merge_round(hipStream_t st, const int32_t* kin, const int32_t* bin_in, int32_t* kout,
-                              int32_t* bout, const int64_t* run_start, int nruns, int64_t total);
+                              int32_t* bout, const int64_t* run_start, int nruns, int64_t total, int64_t* split);
 // values[bins[i]] from the double quantValues LUT (SparseVectorCompressor.java:118-126).
 hipError_t launch_bin_values(hipStream_t st, const int32_t* bins, int64_t n, const double* qvalues, int B,
                              float* vals);

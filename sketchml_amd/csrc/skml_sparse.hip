@@ -2581,34 +2581,78 @@ __device__ __forceinline__ int64_t merge_path(const int32_t* A, int64_t na, cons
     return lo;
 }
 
-// One workgroup per 2048 outputs: the tile's end points on each pair's merge path are found by
-// two global searches, the tile's A and B pieces are staged in LDS (coalesced), and every thread
-// merges 8 outputs from its LDS merge-path split.
-__global__ __launch_bounds__(kSpThreads) void k_merge_round(const int32_t* __restrict__ kin,
-                                                            const int32_t* __restrict__ bin_in,
-                                                            int32_t* __restrict__ kout, int32_t* __restrict__ bout,
-                                                            const int64_t* __restrict__ rs, int nruns,
-                                                            int64_t total) {
-    __shared__ int32_t sk[kSpTile], sb[kSpTile];
-    __shared__ int64_t s_a[2];
+// merge_path by one wave: each step probes 64 evenly spaced points of the remaining range (the
+// predicate A[i] <= B[d-i-1] is true then false along i), so a run of 13 M keys takes 4 dependent
+// global reads instead of 24.
+__device__ __forceinline__ int64_t merge_path_wave(const int32_t* A, int64_t na, const int32_t* B, int64_t nb,
+                                                   int64_t d, int lane) {
+    int64_t lo = d > nb ? d - nb : 0, hi = d < na ? d : na;
+    while (hi - lo > 64) {
+        const int64_t step = (hi - lo + 63) / 64;
+        const int64_t i = lo + (int64_t)lane * step;
+        const bool p = i < hi && A[i] <= B[d - i - 1];
+        const int c = __popcll(__ballot(p));
+        if (c == 0) return lo;
+        const int64_t nlo = lo + (int64_t)(c - 1) * step + 1, nhi = lo + (int64_t)c * step;
+        lo = nlo;
+        hi = nhi < hi ? nhi : hi;
+    }
+    const int64_t i = lo + lane;
+    const bool p = i < hi && A[i] <= B[d - i - 1];
+    return lo + __popcll(__ballot(p));
+}
+
+// The round's run offsets by value (kernel arguments: no dependent loads before the searches).
+struct MergeRuns {
+    int64_t r[kMaxGroups + 1];
+};
+constexpr int kMergeTile = 4096, kMergeThreads = 512;  // outputs and threads per merge workgroup
+static_assert(kMergeTile == kMergePer * kMergeThreads, "8 outputs per thread");
+
+// Split points of the merge paths at every tile boundary (outputs b * kMergeTile, b in [0, tiles]),
+// one wave per boundary: split[b] = how many of the boundary's pair's lower run precede it.
+__global__ __launch_bounds__(256) void k_merge_splits(const int32_t* __restrict__ kin, MergeRuns rs, int nruns,
+                                                      int64_t total, int64_t nb_bounds, int64_t* __restrict__ split) {
+    const int lane = threadIdx.x & 63;
+    const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (b >= nb_bounds) return;
+    const int64_t pos = std::min<int64_t>(b * kMergeTile, total);
+    int q = 0;  // the pair holding pos: the last even run start <= pos (runs [rs[2q], rs[2q+2]))
+    while (2 * q + 2 < nruns && rs.r[2 * q + 2] <= pos) q++;
+    const int64_t a0 = rs.r[2 * q], a1 = rs.r[std::min(2 * q + 1, nruns)], b1 = rs.r[std::min(2 * q + 2, nruns)];
+    int64_t ia = 0;
+    if (pos > a0) ia = pos >= b1 ? a1 - a0 : merge_path_wave(kin + a0, a1 - a0, kin + a1, b1 - a1, pos - a0, lane);
+    if (lane == 0) split[b] = ia;
+}
+
+// One workgroup per kMergeTile outputs: the tile's end points on its pairs' merge paths come from
+// k_merge_splits (or are a pair's ends), the tile's A and B pieces are staged in LDS (coalesced),
+// every thread merges 8 outputs from its LDS merge-path split into an LDS output tile, and the tile
+// is stored coalesced.
+__global__ __launch_bounds__(kMergeThreads) void k_merge_round(const int32_t* __restrict__ kin,
+                                                               const int32_t* __restrict__ bin_in,
+                                                               int32_t* __restrict__ kout, int32_t* __restrict__ bout,
+                                                               MergeRuns rs, int nruns, int64_t total,
+                                                               const int64_t* __restrict__ split) {
+    __shared__ int32_t sk[kMergeTile], sb[kMergeTile], ok[kMergeTile], ob[kMergeTile];
     const int t = threadIdx.x;
-    const int64_t o1 = std::min<int64_t>(((int64_t)blockIdx.x + 1) * kSpTile, total);
+    const int64_t o0 = (int64_t)blockIdx.x * kMergeTile;
+    const int64_t o1 = std::min<int64_t>(o0 + kMergeTile, total);
+    const int64_t sp0 = split[blockIdx.x], sp1 = split[blockIdx.x + 1];
     int q = 0;
-    for (int64_t out = (int64_t)blockIdx.x * kSpTile; out < o1;) {
-        while (2 * q + 2 <= nruns && rs[2 * q + 2] <= out) q++;
-        const int64_t a0 = rs[2 * q];
-        const int64_t a1 = rs[std::min(2 * q + 1, nruns)];
-        const int64_t b1 = rs[std::min(2 * q + 2, nruns)];
-        const int32_t* A = kin + a0;
-        const int32_t* B = kin + a1;
-        const int64_t na = a1 - a0, nb = b1 - a1;
+    for (int64_t out = o0; out < o1;) {
+        while (2 * q + 2 <= nruns && rs.r[2 * q + 2] <= out) q++;
+        const int64_t a0 = rs.r[2 * q];
+        const int64_t a1 = rs.r[std::min(2 * q + 1, nruns)];
+        const int64_t b1 = rs.r[std::min(2 * q + 2, nruns)];
+        const int64_t na = a1 - a0;
         const int64_t end = std::min(o1, b1);
-        if (t < 2) s_a[t] = merge_path(A, na, B, nb, (t == 0 ? out : end) - a0);
-        __syncthreads();
-        const int64_t ia0 = s_a[0], ia1 = s_a[1];
+        // a segment starts at the tile start or at a pair start, and ends at the tile end or a pair end
+        const int64_t ia0 = out == a0 ? 0 : sp0;
+        const int64_t ia1 = end == b1 ? na : sp1;
         const int64_t ib0 = (out - a0) - ia0, ib1 = (end - a0) - ia1;
         const int la = (int)(ia1 - ia0), lb = (int)(ib1 - ib0);
-        for (int k = t; k < la + lb; k += kSpThreads) {
+        for (int k = t; k < la + lb; k += kMergeThreads) {
             const int64_t src = k < la ? a0 + ia0 + k : a1 + ib0 + (k - la);
             sk[k] = kin[src];
             sb[k] = bin_in[src];
@@ -2621,9 +2665,16 @@ __global__ __launch_bounds__(kSpThreads) void k_merge_round(const int32_t* __res
             for (int j = 0; j < cnt; j++) {
                 const bool takeA = ib >= lb || (ia < la && sk[ia] <= sk[la + ib]);
                 const int k = takeA ? ia++ : la + ib++;
-                kout[out + d + j] = sk[k];
-                bout[out + d + j] = sb[k];
+                ok[d + j] = sk[k];
+                ob[d + j] = sb[k];
             }
+        }
+        __syncthreads();
+        // the merged segment leaves with consecutive lanes on consecutive addresses (a thread's
+        // own 8 outputs would be 32-byte strided stores)
+        for (int k = t; k < la + lb; k += kMergeThreads) {
+            kout[out + k] = ok[k];
+            bout[out + k] = ob[k];
         }
         __syncthreads();
         out = end;
@@ -2631,10 +2682,16 @@ __global__ __launch_bounds__(kSpThreads) void k_merge_round(const int32_t* __res
 }
 
 hipError_t launch_merge_round(hipStream_t st, const int32_t* kin, const int32_t* bin_in, int32_t* kout,
-                              int32_t* bout, const int64_t* run_start, int nruns, int64_t total) {
+                              int32_t* bout, const int64_t* run_start, int nruns, int64_t total, int64_t* split) {
     if (total <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_merge_round, dim3((unsigned)sp_tiles(total, kSpTile)), dim3(kSpThreads), 0, st, kin, bin_in,
-                       kout, bout, run_start, nruns, total);
+    if (nruns > kMaxGroups) return hipErrorInvalidValue;
+    MergeRuns rs{};
+    for (int i = 0; i <= nruns; i++) rs.r[i] = run_start[i];
+    const int64_t tiles = sp_tiles(total, kMergeTile), nb = tiles + 1;
+    hipLaunchKernelGGL(k_merge_splits, dim3((unsigned)sp_tiles(nb, 4)), dim3(256), 0, st, kin, rs, nruns, total, nb,
+                       split);
+    hipLaunchKernelGGL(k_merge_round, dim3((unsigned)tiles), dim3(kMergeThreads), 0, st, kin, bin_in, kout, bout, rs,
+                       nruns, total, split);
     return hipGetLastError();
 }
 

@@ -641,27 +641,33 @@ int merge_groups(skml_ctx* c, const skml_sparse* s, int32_t* gk, int32_t* gb, in
     int32_t* k1 = scratch<int32_t>(c, kSlotK1, (size_t)n);
     int32_t* b1 = scratch<int32_t>(c, kSlotB1, (size_t)n);
     if (!k1 || !b1) return sfail(SKML_E_OOM, "merge scratch");
+    // every round's run offsets (the rounds halve the run count) go to the kernels by value
     std::vector<int64_t> rs(G.gstart, G.gstart + G.G + 1);
-    int64_t* rs_dev = reinterpret_cast<int64_t*>(ctx_scratch(c, kSlotStatus, sizeof(int64_t) * 2 * (kMaxGroups + 1)));
-    if (!rs_dev) return sfail(SKML_E_OOM, "run offsets");
+    int64_t* split = rs.size() > 2 ? scratch<int64_t>(c, kSlotEndPos, (size_t)sp_tiles(n, kSpTile) + 2) : nullptr;
+    if (rs.size() > 2 && !split) return sfail(SKML_E_OOM, "merge split points");
     int32_t *kin = gk, *bin = gb, *kout = k1, *bout = b1;
-    int slot = 0;
+    // the last round writes straight into the outputs (bins too unless bins_out is a scratch buffer)
+    const bool bins_direct = bins_out && bins_out != gb && bins_out != b1;
+    bool keys_done = false, bins_done = false;
     while (rs.size() > 2) {
-        int64_t* rd = rs_dev + (slot & 1) * (kMaxGroups + 1);
-        SP_HIP(hipMemcpyAsync(rd, rs.data(), sizeof(int64_t) * rs.size(), hipMemcpyHostToDevice, st));
-        SP_HIP(launch_merge_round(st, kin, bin, kout, bout, rd, (int)rs.size() - 1, n));
+        const bool last = rs.size() <= 3;
+        int32_t* ko = last ? keys_out : kout;
+        int32_t* bo = last && bins_direct ? bins_out : bout;
+        SP_HIP(launch_merge_round(st, kin, bin, ko, bo, rs.data(), (int)rs.size() - 1, n, split));
         std::vector<int64_t> nx;
         for (size_t i = 0; i < rs.size(); i += 2) nx.push_back(rs[i]);
         if (nx.back() != rs.back()) nx.push_back(rs.back());
         rs.swap(nx);
-        std::swap(kin, kout);
-        std::swap(bin, bout);
-        // the H2D of the next round's offsets must not overwrite the buffer still in use
-        slot++;
-        SP_HIP(hipStreamSynchronize(st));
+        keys_done = last;
+        bins_done = last && bins_direct;
+        kin = ko;
+        bin = bo;
+        kout = kin == k1 ? gk : k1;
+        bout = bin == b1 ? gb : b1;
     }
-    SP_HIP(hipMemcpyAsync(keys_out, kin, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToDevice, st));
-    if (bins_out != bin) SP_HIP(hipMemcpyAsync(bins_out, bin, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToDevice, st));
+    if (!keys_done) SP_HIP(hipMemcpyAsync(keys_out, kin, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToDevice, st));
+    if (!bins_done && bins_out && bins_out != bin)
+        SP_HIP(hipMemcpyAsync(bins_out, bin, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToDevice, st));
     return SKML_OK;
 }
 
