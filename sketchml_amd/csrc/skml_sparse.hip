@@ -916,7 +916,10 @@ static_assert(kMmBucketCells == 1 << kMmBucketBits, "bucket size");
 constexpr int kMmLdsBuckets = 8192;  // per-workgroup bucket tables in LDS up to this many (96 KB in the scatter)
 constexpr int kMmChunk = (int)kMmChunkElems;
 constexpr int kMmThreads = 1024;  // count / scatter workgroups: big tiles, long per-bucket runs
-constexpr int kMmBatch = 8;       // elements per thread in flight (count, scatter)
+#ifndef SKML_MM_BATCH
+#define SKML_MM_BATCH 4
+#endif
+constexpr int kMmBatch = SKML_MM_BATCH;  // elements per thread in flight (count, scatter)
 #ifndef SKML_BUCKET_BATCH
 #define SKML_BUCKET_BATCH 8
 #endif
@@ -1056,7 +1059,12 @@ __device__ __forceinline__ void mm_cells(const int32_t (&key)[kMmBatch], int64_t
 
 // Deltas, bitsNeeded histogram and order check (DeltaAdaptiveEncoder.encode step 1) plus the
 // per-bucket pair counts of the MinMax insert.
-__global__ __launch_bounds__(kMmThreads) void k_group_prep(const int32_t* __restrict__ gkeys, int64_t n,
+// 8 waves per SIMD (64 VGPRs, with kMmBatch = 4): two 1,024-thread workgroups per CU instead of
+// one at 103 VGPRs and 8 elements in flight (C3: 195 -> 176 us; at 8 elements the cap spills)
+#ifndef SKML_GP_WAVES
+#define SKML_GP_WAVES 8
+#endif
+__global__ __launch_bounds__(kMmThreads, SKML_GP_WAVES) void k_group_prep(const int32_t* __restrict__ gkeys, int64_t n,
                                                            const SpGroups* __restrict__ gp,
                                                            uint8_t* __restrict__ need, uint32_t* __restrict__ hist,
                                                            uint32_t* __restrict__ err,
