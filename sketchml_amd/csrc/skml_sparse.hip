@@ -2412,24 +2412,42 @@ __global__ __launch_bounds__(kSpThreads) void k_agg_bounds(const int32_t* __rest
     load_starts(gp, S);
     __syncthreads();
     const int64_t ld = ntiles + 1;
-    for (int64_t i = (int64_t)blockIdx.x * kSpThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kSpThreads) {
-        const int g = group_of_elem(S, i);
-        const int64_t lo = S[g], hi = S[g + 1];
-        auto tile_of = [&](int32_t k) -> int64_t { return k < 0 ? 0 : std::min<int64_t>((int64_t)k / kAggTile, ntiles); };
-        const int32_t key = gk[i];
-        if (key < 0 || (int64_t)key >= dim) atomicOr(err, 1u);  // SparseDoubleGradient's bound check
-        const int64_t ti = tile_of(key);
-        const int64_t pt = i > lo ? tile_of(gk[i - 1]) : -1;
-        int32_t* b = bounds + (int64_t)g * ld;
-        for (int64_t t = pt + 1; t <= ti; t++) b[t] = (int32_t)i;
-        if (i == hi - 1)
-            for (int64_t t = ti + 1; t <= ntiles; t++) b[t] = (int32_t)hi;
+    auto tile_of = [&](int32_t k) -> int64_t { return k < 0 ? 0 : std::min<int64_t>((int64_t)k / kAggTile, ntiles); };
+    // 4 consecutive elements per thread (one 16-byte load and the key before them)
+    const int64_t nq = (n + 3) / 4;
+    for (int64_t qd = (int64_t)blockIdx.x * kSpThreads + threadIdx.x; qd < nq; qd += (int64_t)gridDim.x * kSpThreads) {
+        const int64_t i0 = 4 * qd;
+        int32_t key[4];
+        if (i0 + 4 <= n && (reinterpret_cast<uintptr_t>(gk) & 15) == 0) {
+            const int4 v = *reinterpret_cast<const int4*>(gk + i0);
+            key[0] = v.x, key[1] = v.y, key[2] = v.z, key[3] = v.w;
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; e++) key[e] = i0 + e < n ? gk[i0 + e] : 0;
+        }
+        int32_t prev = i0 > 0 ? gk[i0 - 1] : 0;
+        int g = group_of_elem(S, i0);
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const int64_t i = i0 + e;
+            if (i >= n) break;
+            while (i >= S[g + 1]) g++;
+            const int64_t lo = S[g], hi = S[g + 1];
+            if (key[e] < 0 || (int64_t)key[e] >= dim) atomicOr(err, 1u);  // SparseDoubleGradient's bound check
+            const int64_t ti = tile_of(key[e]);
+            const int64_t pt = i > lo ? tile_of(prev) : -1;
+            int32_t* b = bounds + (int64_t)g * ld;
+            for (int64_t t = pt + 1; t <= ti; t++) b[t] = (int32_t)i;
+            if (i == hi - 1)
+                for (int64_t t = ti + 1; t <= ntiles; t++) b[t] = (int32_t)hi;
+            prev = key[e];
+        }
     }
 }
 hipError_t launch_agg_bounds(hipStream_t st, const int32_t* gk, int64_t n, const SpGroups* gp, int64_t ntiles,
                              int64_t dim, int32_t* bounds, unsigned* err) {
     if (n <= 0) return hipSuccess;
-    const int64_t grid = std::min<int64_t>(sp_tiles(n, kSpThreads), 8192);
+    const int64_t grid = std::min<int64_t>(sp_tiles((n + 3) / 4, kSpThreads), 8192);
     hipLaunchKernelGGL(k_agg_bounds, dim3((unsigned)grid), dim3(kSpThreads), 0, st, gk, n, gp, ntiles, dim, bounds, err);
     return hipGetLastError();
 }

@@ -1846,7 +1846,7 @@ int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t
         while (end < todo.size() && (end == at || bytes + need_of(todo[end]) <= kBudget)) bytes += need_of(todo[end++]);
         int64_t nk = 0, nb = 0;
         for (size_t q = at; q < end; q++) {
-            nk += views[(size_t)todo[q]].nnz;
+            nk += (views[(size_t)todo[q]].nnz + 3) & ~int64_t{3};  // every payload's keys 16-byte aligned
             nb += (int64_t)views[(size_t)todo[q]].g.G * (ntiles + 1);
         }
         int32_t* gk = scratch<int32_t>(c, kSlotCKeys, (size_t)nk);
@@ -1876,7 +1876,7 @@ int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t
             }
             SP_HIP(launch_agg_bounds(st, a.gk, v.nnz, v.g_dev, ntiles, dim, const_cast<int32_t*>(a.bounds), err));
             pays.push_back(a);
-            ko += v.nnz;
+            ko += (v.nnz + 3) & ~int64_t{3};
             bo += (int64_t)v.g.G * (ntiles + 1);
         }
         const bool last = end == todo.size();
