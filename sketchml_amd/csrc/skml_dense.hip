@@ -13,7 +13,13 @@ namespace skml {
 // =============================================================================================
 // Quantize: Eytzinger search over the LDS split table; codes packed LSB-first.
 // =============================================================================================
-constexpr int kQThreads = 256;
+#ifndef SKML_Q_THREADS
+#define SKML_Q_THREADS 256
+#endif
+#ifndef SKML_Q_GRID
+#define SKML_Q_GRID 1024
+#endif
+constexpr int kQThreads = SKML_Q_THREADS;
 constexpr int kEytzMax = 4096;
 
 __device__ __forceinline__ void store_codes4(uint8_t* codes, int64_t e0, uint32_t c0, uint32_t c1,
@@ -214,7 +220,7 @@ hipError_t launch_quantize(hipStream_t st, const float* x, int64_t n, void* payl
     const int lds_splits = std::min(std::max(req_bins - 1, 1), kLutMaxSplits) + kLutPad;
     const size_t lds = sizeof(QuantLut::base) + (size_t)lds_splits * sizeof(float);
     const int64_t tiles = (n + 1023) / 1024;
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((tiles + 3) / 4, 1024));
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((tiles + 3) / 4, SKML_Q_GRID));
     hipLaunchKernelGGL(k_quantize, dim3(grid), dim3(kQThreads), lds, st, x, n,
                        reinterpret_cast<uint8_t*>(payload), lut, lds_splits);
     return hipGetLastError();
