@@ -77,10 +77,20 @@ def test_sparse_edge_values(gpu, kind):
 
 
 @pytest.mark.parametrize("groups,rows,ratio,bins", [(2, 1, 0.3, 256), (4, 3, 0.5, 64), (16, 8, 0.1, 1024),
-                                                    (64, 2, 0.3, 4096), (8, 2, 1.7, 16)])
+                                                    (64, 2, 0.3, 4096), (8, 2, 1.7, 16), (3, 1, 0.3, 128),
+                                                    (5, 2, 0.3, 256), (7, 3, 0.2, 512)])
 def test_sparse_shapes(gpu, groups, rows, ratio, bins):
+    """Odd group counts leave an unpaired run in restore's Sort.merge rounds."""
     keys, vals = _sparse_data(120000, 0.15, groups * 100 + rows, "normal")
     _check_sparse(gpu, keys, vals, bins, groups, rows, ratio, seed=7, hash_seed=groups)
+
+
+@pytest.mark.parametrize("groups", [7, 8])
+def test_sparse_restore_many_merge_tiles(gpu, groups):
+    """~630 K keys: every Sort.merge round spans ~150 merge tiles of 4,096 outputs, with tile
+    boundaries inside and at the ends of the merged pairs (k_merge_splits)."""
+    keys, vals = _sparse_data(2**21 + 3, 0.3, 40 + groups, "normal")
+    _check_sparse(gpu, keys, vals, 256, groups, 2, 0.3, seed=11, hash_seed=groups)
 
 
 def test_sparse_key_gaps_choose_each_interval_kind(gpu):
