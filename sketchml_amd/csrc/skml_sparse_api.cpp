@@ -1331,7 +1331,8 @@ int skml_sparse_deserialize(skml_ctx* c, const uint8_t* buf, size_t len, const d
     G.gstart[G.G] = n;
     if (r.bad) return bail(sfail(SKML_E_ARG, "truncated GroupedMinMaxSketch stream"));
     // the stream on the device, once
-    uint8_t* dstream = scratch<uint8_t>(c, kSlotWire, std::max<size_t>(len, 8));
+    // 16 bytes of slack: be64_at reads the aligned word after an unaligned long
+    uint8_t* dstream = scratch<uint8_t>(c, kSlotWire, std::max<size_t>(len + 16, 64));
     if (!dstream) return bail(sfail(SKML_E_OOM, "device copy of the stream"));
     SP_HIP(hipMemcpyAsync(dstream, buf, len, hipMemcpyHostToDevice, st));
     // the flags' lengths: field sums of the fixed groups, zero selects of the unary ones

@@ -120,12 +120,16 @@ hipError_t launch_wire_pieces(hipStream_t st, const uint8_t* small, const int64_
 }
 
 // ---------------------------------------------------------------- read side
-// ObjectInputStream.readLong of the word at byte p (any alignment)
+// ObjectInputStream.readLong of the word at byte p (any alignment): the big-endian long from the
+// aligned words around it (two 8-byte loads and a funnel shift instead of eight byte loads).  The device copy of the stream is allocated with 16 bytes of
+// slack, so the second word never lies outside it.
 __device__ __forceinline__ uint64_t be64_at(const uint8_t* __restrict__ p) {
-    uint64_t v = 0;
-#pragma unroll
-    for (int k = 0; k < 8; k++) v = (v << 8) | p[k];
-    return v;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint64_t* q = reinterpret_cast<const uint64_t*>(a & ~static_cast<uintptr_t>(7));
+    const int sh = (int)(a & 7) * 8;
+    uint64_t v = q[0];
+    if (sh) v = (v >> sh) | (q[1] << (64 - sh));
+    return __builtin_bswap64(v);
 }
 // bits [q, q + 64) of a stored long array (ns words at byte pos; words past ns read as 0)
 __device__ __forceinline__ uint64_t stored_bits(const uint8_t* __restrict__ stream, int64_t pos, int64_t ns, int64_t q) {
@@ -155,7 +159,9 @@ __global__ __launch_bounds__(256) void k_rd_fixed_sum(const uint8_t* __restrict_
                                                       const int64_t* __restrict__ wpre, int nsec,
                                                       unsigned long long* __restrict__ sums) {
     __shared__ int64_t pre[kMaxGroups + 1];
+    __shared__ unsigned long long ssum[kMaxGroups];  // the workgroup's per-section sums
     for (int j = threadIdx.x; j <= nsec; j += 256) pre[j] = wpre[j];
+    for (int j = threadIdx.x; j < kMaxGroups; j += 256) ssum[j] = 0ull;
     __syncthreads();
     const int64_t total = pre[nsec];
     // every lane takes part in every trip (the wave reduction below)
@@ -169,20 +175,26 @@ __global__ __launch_bounds__(256) void k_rd_fixed_sum(const uint8_t* __restrict_
         const int64_t rem = sc.nbits - 64 * i;
         if (rem < 64) v &= rem > 0 ? ((1ull << rem) - 1ull) : 0ull;
         const int nf = sc.nf;
-        const int ph = (int)((64 * i) % nf);  // position 64 i + b has residue (ph + b) mod nf
+        // position 64 i + b has residue (ph + b) mod nf (i < 2^32: a section's word index)
+        const int ph = nf > 0 ? (int)(((uint32_t)i % (uint32_t)nf) * (64u % (uint32_t)nf) % (uint32_t)nf) : 0;
         uint64_t sum = 0;
         for (int k = 0; k < nf; k++)
             sum += (uint64_t)__popcll(v & residue_mask(nf, (k - ph + nf) % nf)) << (nf - 1 - k);
-        // one atomic per wave when the wave's words lie in one section (all but a few waves)
+        // one LDS atomic per wave when the wave's words lie in one section (all but a few waves)
         const int s0 = __builtin_amdgcn_readfirstlane(s);
         if (__all(s == s0)) {
 #pragma unroll
             for (int off = 32; off >= 1; off >>= 1) sum += __shfl_xor(sum, off, 64);
-            if ((threadIdx.x & 63) == 0 && sum) atomicAdd(&sums[s0], (unsigned long long)sum);
+            if ((threadIdx.x & 63) == 0 && sum) atomicAdd(&ssum[s0], (unsigned long long)sum);
         } else if (sum) {
-            atomicAdd(&sums[s], (unsigned long long)sum);
+            atomicAdd(&ssum[s], (unsigned long long)sum);
         }
     }
+    // one global atomic per (workgroup, section): thousands of same-address global atomics (one
+    // per wave) serialised at the memory side
+    __syncthreads();
+    for (int j = threadIdx.x; j < nsec; j += 256)
+        if (ssum[j]) atomicAdd(&sums[j], ssum[j]);
 }
 
 // Unary flags (flagKind true): the bit length of `size` flags is the position of the size-th zero
@@ -321,7 +333,7 @@ __global__ __launch_bounds__(256) void k_rd_words(const uint8_t* __restrict__ st
 hipError_t launch_rd_fixed_sum(hipStream_t st, const uint8_t* stream, const RdFlagSec* secs, const int64_t* wpre, int nsec,
                                int64_t total_words, uint64_t* sums) {
     if (total_words <= 0 || nsec <= 0) return hipSuccess;
-    const int64_t grid = std::min<int64_t>((total_words + 255) / 256, 8192);
+    const int64_t grid = std::min<int64_t>((total_words + 255) / 256, 1024);
     hipLaunchKernelGGL(k_rd_fixed_sum, dim3((unsigned)grid), dim3(256), 0, st, stream, secs, wpre, nsec,
                        reinterpret_cast<unsigned long long*>(sums));
     return hipGetLastError();
