@@ -208,7 +208,10 @@ hipError_t launch_huff_write(hipStream_t st, const int32_t* table, int64_t ncell
 // {tree node, -1}; nodes: int4 {left, right, value, 0}, left < 0 for a leaf.
 constexpr int kHuffLutBits = 12;
 constexpr int kHuffLutSize = 1 << kHuffLutBits;
-constexpr int64_t kHuffSeg = 2048;  // bits per speculative segment
+#ifndef SKML_HUFF_SEG
+#define SKML_HUFF_SEG 2048
+#endif
+constexpr int64_t kHuffSeg = SKML_HUFF_SEG;  // bits per speculative segment
 struct HuffDecGroup {
     int64_t word0;   // first word of the group's stream in the concatenated words
     int64_t nwords;  // stored words (BitSet.toLongArray); bits beyond read as 0
