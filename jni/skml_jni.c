@@ -10,6 +10,10 @@
  * through library-owned pinned buffers.  Dense payloads live in Java byte[]s
  * (header, splits, packed codes); sparse payloads are library-owned device objects behind a
  * long handle, freed by freeSparse (HipSparseVectorCompressor.close / a Cleaner).
+ * A critical region holds off the JVM's garbage collector for the length of the call (the
+ * host-path encode of 2^26 floats: 6-9 ms); the alternative, Get<Type>ArrayRegion
+ * into the library's pinned staging, adds a second full host copy of the array, so the shim keeps
+ * the critical regions and states the cost here.
  *
  * Errors: a non-zero status becomes the reference's unchecked exception:
  * SKML_E_NAN -> QuantileSketchException("Encounter NaN value") (HeapQuantileSketch.java:75-76);
