@@ -1,11 +1,12 @@
 #!/usr/bin/env python
 """Benchmark of the MI355X SketchML gradient codec (BASELINE.json metric).
 
-One step = encode one 2^26-float fp32 gradient bucket resident in HBM (k=128 quantile sketch ->
-getQuantiles(256) -> Maths.unique -> bucket quantise -> packed codes), i.e. BASELINE config 2
-(SURVEY.md C2).  With --gpus N > 1 (launched by torch.distributed.run) every rank encodes its own
-2^26 bucket (config 4, weak scaling) and the step adds the RCCL all-gather of the compressed
-payloads over xGMI.  `value` = fp32-input GB/s of the whole job.
+One step = encode one 2^28-float (1 GiB) fp32 gradient resident in HBM (k=128 quantile sketch ->
+getQuantiles(256) -> Maths.unique -> bucket quantise -> packed codes): the north-star
+configuration of BASELINE.json ("device-resident encode of a 256 M-float gradient at 1 GPU").
+BASELINE config 2 (a 2^26-float bucket) is timed under extras.other_configs.dense_c2.
+With --gpus N > 1 every rank encodes its own 2^28-float gradient (weak scaling) and the step adds
+the RCCL all-gather of the compressed payloads over xGMI.  `value` = fp32-input GB/s of the whole job.
 
 Extra fields: decode GB/s and decode L2 error (the metric's "+ decode L2 err"), per-kernel
 device times, the roofline of the dominant kernel, the CPU baseline (the C restatement of the
@@ -37,11 +38,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--n", type=int, default=2**26, help="floats per GPU bucket")
+    ap.add_argument("--n", type=int, default=2**28, help="floats per GPU bucket (default: the north-star 2^28)")
     ap.add_argument("--bins", type=int, default=256)
-    ap.add_argument("--buffers", type=int, default=4,
+    ap.add_argument("--buffers", type=int, default=0,
                     help="rotating input buckets so a step never re-reads the previous step's "
-                         "input from the 256 MB Infinity Cache")
+                         "input from the 256 MB Infinity Cache (default: 2 of 1 GiB and more, else "
+                         "enough for 1 GiB in total)")
     ap.add_argument("--dtype", choices=["f32", "f64"], default="f32",
                     help="input dtype (f64 = the reference's double[] path)")
     ap.add_argument("--quant", choices=["quantile", "uniform"], default="quantile")
@@ -160,15 +162,18 @@ def pmc_traffic(kernel, n, dtype="f32", quant="quantile"):
 VALU_PEAK_GINST = 2.4e9 * 256 / 1e9
 
 
-def sq_valu(kernel):
-    """VALU wave-instructions per launch of `kernel` from the committed SQ counter pass
-    (profiles/*sq_counters.json, written by tools/prof_round.sh)."""
+def sq_valu(kernel, n):
+    """VALU wave-instructions per launch of `kernel` at problem size n from the committed SQ counter
+    pass (profiles/*sq_counters.json, written by tools/prof_round.sh; files without an "n" key are
+    the 2^26 runs of rounds 1-3)."""
     best = None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*sq_counters.json"))):
         try:
             with open(path) as f:
                 d = json.load(f)
         except Exception:
+            continue
+        if d.get("n", 2**26) != n:
             continue
         for name, c in d.get("per_launch_mean", {}).items():
             short = "k_leaf" if ("k_leaf2" in name or "k_leaf64" in name) else name.split("(")[0].split("::")[-1]
@@ -226,11 +231,19 @@ def cpu_baseline(x_host, bins, budget_s):
                     "indexOf, 1-byte code write), not a JVM"}
 
 
-def other_configs(sk, lib, ctx, dev, xs):
+def other_configs(sk, lib, ctx, dev):
     """The reference's other dense / sparse configurations at one GPU, each timed over a few
-    synchronised repetitions (not part of `value`): the fp64 path on the same bucket (the
-    reference's double[] itself) and the C3 sparse path (2^28-dim dense, 10 % nnz)."""
+    synchronised repetitions (not part of `value`): C2 (a 2^26-float bucket), the fp64 path on the
+    C2 bucket (the reference's double[] itself), 8 buckets per call, C4's decode-sum and the C3
+    sparse path (2^28-dim dense, 10 % nnz) with its aggregation."""
     out = {}
+    gen = torch.Generator(device=dev)
+    xs = []
+    for b in range(4):  # C2: 4 rotating 2^26-float buckets (1 GiB in total, beyond the 256 MB MALL)
+        gen.manual_seed(4 + 1000 * b)
+        xs.append(torch.randn(2**26, device=dev, generator=gen))
+    out["dense_c2"] = dense_bucket(sk, lib, ctx, dev, xs, "C2: 2^26-float dense gradient bucket, 256 requested bins, "
+                                   "encode (4 rotating buckets)")
 
     def timed(fn, reps):
         fn()
@@ -278,7 +291,7 @@ def other_configs(sk, lib, ctx, dev, xs):
                               "ms_per_bucket": round(tb / nbk * 1e3, 4), "gbps": round(4.0 * n * nbk / tb / 1e9, 1)}
     del pls
     out["dense_decode_sum_c4"] = dense_decode_sum(sk, lib, ctx, dev, xs, n, p)
-    out["dense_2p28"] = dense_north_star(sk, lib, ctx, dev)
+    del xs
     dim = 2**28
     g = torch.Generator(device=dev).manual_seed(3)
     d = torch.randn(dim, device=dev, generator=g)
@@ -312,13 +325,17 @@ def sparse_aggregate(sk, spl, dim, timed_median, P=8):
     ts, _ = timed_median(lambda: sk.decode_sum(allb, P, stride, dim, 1.0 / P, out), 3)
     t1, _ = timed_median(lambda: sk.decode_sum(allb, 1, stride, dim, 1.0, out), 3)
     nnz = spl.nnz()
+    # algorithmic bytes: every blob read once, the 2^28 double sum written once
+    alg = P * nb + 8.0 * dim
     res = {"workload": f"Gradient.sum of {P} C3 sparse payloads (nnz {nnz} each) into a 2^28-dim double sum, x 1/{P}",
            "blob_bytes": nb, "export_ms": round(tx * 1e3, 3), "decode_sum_ms": round(ts * 1e3, 3),
            "decode_sum_one_payload_ms": round(t1 * 1e3, 3),
            "per_payload_ms": round((ts - t1) / (P - 1) * 1e3, 3),
+           "alg_bytes": alg, "roofline_frac": round(alg / ts / 1e9 / HBM_PEAK_GBS, 4),
            "note": "median wall time of synchronised calls; one payload = DeltaAdaptive decode + MinMax query "
-                   "+ scatter-add into the double sum (no Sort.merge: keys are unique); the fixed part is the "
-                   "2 GiB zero fill and the x 1/P pass"}
+                   "+ add into the double sum tile by tile (no Sort.merge: keys are unique); the fixed part is "
+                   "the 2 GiB write of the sum (the x 1/P scale is fused into it); alg_bytes = P blobs read + "
+                   "the sum written"}
     del allb, out
     return res
 
@@ -356,46 +373,48 @@ def dense_decode_sum(sk, lib, ctx, dev, xs, n, p, P=8):
             "gbps": round(alg / (us * 1e-6) / 1e9, 1), "roofline_frac": round(alg / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
-def dense_north_star(sk, lib, ctx, dev, n=2**28, bins=256, reps=10):
-    """The north-star size: a 2^28-float (1 GiB) bucket, larger than the 256 MB Infinity Cache, so
-    the quantize pass re-reads the input from HBM (at 2^26 part of it can still be on-die).
-    Encode time = mean of `reps` back-to-back encodes between two synchronisations; the
-    per-kernel split comes from HIP events on the codec stream in a separate pass."""
-    g = torch.Generator(device=dev).manual_seed(6)
-    x = torch.randn(n, device=dev, generator=g)
+def dense_bucket(sk, lib, ctx, dev, xs, label, bins=256, reps=50):
+    """One dense configuration (rotating device buckets `xs`) outside the headline: encode time =
+    mean of `reps` back-to-back encodes between two synchronisations; the per-kernel split comes
+    from HIP events on the codec stream in a separate pass."""
+    n = xs[0].numel()
     nb = lib.skml_dense_payload_bytes(n, bins)
     pl = sk.alloc_aligned(nb, dev)
     p = _lib_params(bins)
-    p.seed = 6
+    p.seed = 2
 
-    def enc():
-        st = lib.skml_dense_encode_f32(ctx, C.c_void_p(x.data_ptr()), n, C.byref(p), C.c_void_p(pl.data_ptr()), nb)
+    def enc(i):
+        st = lib.skml_dense_encode_f32(ctx, C.c_void_p(xs[i % len(xs)].data_ptr()), n, C.byref(p),
+                                       C.c_void_p(pl.data_ptr()), nb)
         if st:
             raise RuntimeError("encode failed")
 
-    enc()
+    for i in range(5):
+        enc(i)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(reps):
-        enc()
+    for i in range(reps):
+        enc(i)
     torch.cuda.synchronize()
     t = (time.perf_counter() - t0) / reps
     lib.skml_ctx_set_timing(ctx, -1)
     lib.skml_ctx_reset_stats(ctx)
-    for _ in range(3):
-        enc()
+    for i in range(10):
+        enc(i)
     ks = kernel_stats(lib, ctx)
     lib.skml_ctx_set_timing(ctx, 0)
     hdr = _lib_header(lib, ctx, pl)
     alg = (8.0 + hdr.code_bits / 8.0) * n
-    res = {"workload": "2^28-float (1 GiB) dense gradient, 256 requested bins, encode", "ms": round(t * 1e3, 4),
+    res = {"workload": label, "ms": round(t * 1e3, 4),
            "gbps_fp32_in": round(4.0 * n / t / 1e9, 1), "roofline_frac_9B": round(alg / t / 1e9 / HBM_PEAK_GBS, 4),
            "bin_num_effective": hdr.bin_num,
            "kernels_us": {k: round(v["avg_us"], 2) for k, v in ks.items()}}
+    if "k_leaf" in ks:
+        res["k_leaf_gbps"] = round(4.0 * n / (ks["k_leaf"]["avg_us"] * 1e-6) / 1e9, 1)
     if "k_quantize" in ks:
         q = ks["k_quantize"]["avg_us"] * 1e-6
         res["k_quantize_gbps"] = round((4.0 + hdr.code_bits / 8.0) * n / q / 1e9, 1)
-    del x, pl
+    del pl
     return res
 
 
@@ -501,7 +520,9 @@ def _workload_label(args, world):
     npow = f"2^{n.bit_length() - 1}" if n & (n - 1) == 0 else str(n)
     tag = ""
     if (args.quant, args.dtype) == ("quantile", "f32"):
-        if n == 2**26 and bins == 256:
+        if n == 2**28 and bins == 256:
+            tag = "north star: "
+        elif n == 2**26 and bins == 256:
             tag = "C4: " if world > 1 else "C2: "
         elif n == 2**27 and bins == 4 and world > 1:
             tag = "C5 shard: "
@@ -566,18 +587,23 @@ def main():
 
     n, bins = args.n, args.bins
     nb = lib.skml_dense_payload_bytes(n, bins)
-    nbuf = max(1, args.buffers)
+    esize = 8 if args.dtype == "f64" else 4
+    # rotating buckets: at least 2, and at least 1 GiB in all, so no step starts on bytes the
+    # previous step left in the 256 MB Infinity Cache
+    nbuf = args.buffers if args.buffers > 0 else max(2, -(-(2**30) // (esize * n)))
     gen = torch.Generator(device=dev)
     xs = []
     for b in range(nbuf):
-        gen.manual_seed(4 + rank + 1000 * b)  # config 4: bucket r seeded 4 + r
+        # rank r's first bucket is seeded 6 + r (rank 0: the data of
+        # tests/test_gpu_configs.py::test_north_star_2p28_matches_oracle)
+        gen.manual_seed(6 + rank + 1000 * b)
         xs.append(torch.randn(n, device=dev, generator=gen,
                               dtype=torch.float64 if args.dtype == "f64" else torch.float32))
     payload = sk.alloc_aligned(nb, dev)
     params = _lib.Params()
     lib.skml_params_default(C.byref(params))
     params.bin_num = bins
-    params.seed = 2 + rank
+    params.seed = 6 + rank
 
     exch = None
     allp = None
@@ -602,7 +628,6 @@ def main():
                            ("quantile", "f64"): "skml_dense_encode_f64",
                            ("uniform", "f32"): "skml_dense_encode_uniform_f32",
                            ("uniform", "f64"): "skml_dense_encode_uniform_f64"}[(args.quant, args.dtype)])
-    esize = 8 if args.dtype == "f64" else 4
 
     def step(i):
         x = xs[i % nbuf]
@@ -677,7 +702,7 @@ def main():
                 "traffic": traffic[0] if traffic else None,
                 "traffic_source": traffic[1] if traffic else None,
                 "alg_bytes_per_launch": alg_bytes[dom]}
-    valu = sq_valu(dom) if (args.n == 2**26 and args.dtype == "f32" and args.quant == "quantile") else None
+    valu = sq_valu(dom, args.n) if (args.dtype == "f32" and args.quant == "quantile") else None
     if valu:
         # the sort-dominated leaf is bound by VALU issue, not HBM: its issue rate against the ceiling
         rate = valu[0] / (live["avg_us"] * 1e-6) / 1e9
@@ -750,8 +775,8 @@ def main():
         extras["sparse_exchange"] = sparse_exchange_step(sk, exch, dev, rank, world, barrier)
 
     if (rank == 0 and world == 1 and not args.no_extras and not args.no_configs and args.quant == "quantile"
-            and args.dtype == "f32" and args.n == 2**26):
-        extras["other_configs"] = other_configs(sk, lib, ctx, dev, xs)
+            and args.dtype == "f32" and args.n == 2**28):
+        extras["other_configs"] = other_configs(sk, lib, ctx, dev)
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline and args.quant == "quantile" and args.dtype == "f32":

@@ -112,6 +112,10 @@ int skml_ctx_reset_stats(skml_ctx* ctx);
  * 3 full): average device ms over `iters` launches on n values.  Not part of the codec. */
 int skml_debug_leaf_stage(skml_ctx* ctx, const float* x_dev, int64_t n, int stage, int iters,
                           double* avg_ms);
+/* Test hook: while `on` is non-zero, the sparse encode treats its two MinMax staging scratch
+ * buffers (the hashed cells and the per-(tile, bucket) reservations) as failed allocations, so
+ * the fallback path (key-carrying pairs, rehashing scatter) is exercised.  Not part of the codec. */
+int skml_debug_sparse_scratch_fail(int on);
 
 /* ---- Dense path: QuantileQuantizer.quantize + Quantizer.getBins/getValues ---- */
 
@@ -238,7 +242,8 @@ int skml_host_free(void* p);
  * previous one.  payload_host NULL: *written = an upper bound of the payload size.  Otherwise
  * *written = the bytes written (codes_offset + ceil(n * code_bits / 8)).  params->parallelism > 1
  * selects parallelQuantize (QuantileQuantizer.java:53-92) with that many slices, as on the sparse
- * path (params->dedup then applies as given).  Synchronising. */
+ * path (params->dedup then applies as given); params->quant_type = SKML_UNIFORM selects
+ * UniformQuantizer instead (skml_dense_encode_uniform_f32/_f64).  Synchronising. */
 int skml_dense_encode_host_f32(skml_ctx* ctx, const float* x_host, int64_t n, const skml_params* params,
                                void* payload_host, size_t payload_cap, size_t* written);
 /* The reference's own double[] input (QuantileQuantizer.quantize(double[]), no fp32 rounding):

@@ -23,6 +23,9 @@ final class HipCodec {
     static native byte[] encodeDenseF64(long ctx, double[] x, int binNum, boolean dedup, long seed,
                                         int parallelism);
 
+    // UniformQuantizer.quantize / parallelQuantize (the same computation) over double[]
+    static native byte[] encodeDenseUniformF64(long ctx, double[] x, int binNum);
+
     static native void decodeDense(long ctx, byte[] payload, float[] out);
 
     static native void decodeDenseF64(long ctx, byte[] payload, double[] out);

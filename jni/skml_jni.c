@@ -135,6 +135,34 @@ JNIEXPORT jbyteArray JNICALL Java_org_dma_sketchml_hip_HipCodec_encodeDenseF64(J
     return out;
 }
 
+/* byte[] encodeDenseUniformF64(long ctx, double[] x, int binNum): UniformQuantizer.quantize(double[])
+ * (quantization/UniformQuantizer.java:21-45) through the host entry point with
+ * params.quant_type = SKML_UNIFORM, i.e. skml_dense_encode_uniform_f64 on the device copy. */
+JNIEXPORT jbyteArray JNICALL Java_org_dma_sketchml_hip_HipCodec_encodeDenseUniformF64(JNIEnv* env, jclass cls,
+                                                                                    jlong ctx, jdoubleArray xs,
+                                                                                    jint bins) {
+    (void)cls;
+    skml_params p;
+    fill_params(&p, bins, JNI_FALSE, 0, 1);
+    p.quant_type = SKML_UNIFORM;
+    const jsize n = (*env)->GetArrayLength(env, xs);
+    size_t cap = 0, wrote = 0;
+    if (throw_status(env, skml_dense_encode_host_f64(CTX(ctx), NULL, n, &p, NULL, 0, &cap))) return NULL;
+    uint8_t* buf = (uint8_t*)malloc(cap ? cap : 1);
+    if (!buf) return NULL;
+    double* x = (double*)(*env)->GetPrimitiveArrayCritical(env, xs, NULL);
+    if (pin_failed(env, x, buf)) {
+        free(buf);
+        return NULL;
+    }
+    int st = skml_dense_encode_host_f64(CTX(ctx), x, n, &p, buf, cap, &wrote);
+    (*env)->ReleasePrimitiveArrayCritical(env, xs, x, JNI_ABORT);
+    jbyteArray out = st ? NULL : to_byte_array(env, buf, wrote);
+    free(buf);
+    throw_status(env, st);
+    return out;
+}
+
 /* void decodeDense(long ctx, byte[] payload, float[] out)  (DenseVectorCompressor.java:84-91) */
 JNIEXPORT void JNICALL Java_org_dma_sketchml_hip_HipCodec_decodeDense(JNIEnv* env, jclass cls, jlong ctx,
                                                                     jbyteArray payload, jfloatArray out) {

@@ -82,6 +82,10 @@ def lib():
         L.orc_parallel_quantize.argtypes = [dblp, C.c_int32, C.c_int32, C.c_int32, C.c_int64,
                                             C.POINTER(QuantHeader), i32p]
         L.orc_uniform_quantize.argtypes = [dblp, C.c_int32, C.c_int32, C.POINTER(QuantHeader), i32p]
+        L.orc_quantize_header_f32.argtypes = [C.POINTER(C.c_float), C.c_int64, C.c_int32, C.c_int64,
+                                              C.POINTER(QuantHeader)]
+        L.orc_index_of_many_f32.argtypes = [C.POINTER(QuantHeader), C.POINTER(C.c_float), C.c_int64, i32p]
+        L.orc_index_of_many_f32.restype = None
         L.orc_index_of.argtypes = [C.POINTER(QuantHeader), C.c_double]
         L.orc_index_of.restype = C.c_int32
         L.orc_get_values.argtypes = [C.POINTER(QuantHeader), dblp]
@@ -192,6 +196,27 @@ def quantize(values, bin_num=256, seed=0) -> OracleQuant:
     if st:
         raise OracleError(st, "quantize")
     return OracleQuant(hdr, bins[: len(v)])
+
+
+def quantize_header_f32(values, bin_num=256, seed=0) -> OracleQuant:
+    """QuantileQuantizer.quantize's header (sketch, getQuantiles, Maths.unique, findZeroIdx) of float
+    values widened to double, without the bins: the full-size tests take those slice by slice from
+    index_of_many_f32 (bins is None here)."""
+    v = np.ascontiguousarray(values, dtype=np.float32)
+    hdr = QuantHeader()
+    st = lib().orc_quantize_header_f32(v.ctypes.data_as(C.POINTER(C.c_float)), len(v), bin_num, seed, C.byref(hdr))
+    if st:
+        raise OracleError(st, "quantize_header_f32")
+    return OracleQuant(hdr, None)
+
+
+def index_of_many_f32(oq: OracleQuant, values) -> np.ndarray:
+    """Quantizer.quantizeToBins of a float slice against oq's header (ctypes releases the GIL, so
+    slices can run on a thread pool)."""
+    v = np.ascontiguousarray(values, dtype=np.float32)
+    out = np.empty(len(v), dtype=np.int32)
+    lib().orc_index_of_many_f32(C.byref(oq.hdr), v.ctypes.data_as(C.POINTER(C.c_float)), len(v), _p(out, i32p))
+    return out
 
 
 def uniform_quantize(values, bin_num=256) -> OracleQuant:

@@ -421,6 +421,33 @@ int orc_quantize(const double* values, int32_t n, int32_t bin_num, int64_t seed,
     return ORC_OK;
 }
 
+/* QuantileQuantizer.quantize (QuantileQuantizer.java:27-43) up to findZeroIdx on float input
+ * widened to double; n may exceed a Java int only in the sense that hdr->n is then meaningless
+ * (the tests stay at or below 2^30). */
+int orc_quantize_header_f32(const float* values, int64_t n, int32_t bin_num, int64_t seed, orc_quant_header* hdr) {
+    if (bin_num <= 1 || bin_num > 65536) return ORC_E_ARG;
+    orc_jrandom rng;
+    orc_jr_seed(&rng, seed);
+    qsk* q = (qsk*)malloc(sizeof(qsk));
+    if (!q) return ORC_E_OOM;
+    qsk_init(q, &rng);
+    for (int64_t i = 0; i < n; i++)
+        if (qsk_update(q, (double)values[i])) { free(q); return ORC_E_NAN; }
+    hdr->n = (int32_t)n;
+    hdr->min = q->minv;
+    hdr->max = q->maxv;
+    int st = qsk_quantiles(q, bin_num, hdr->splits);
+    free(q);
+    if (st) return st;
+    hdr->bin_num = java_unique(hdr->splits, bin_num - 1) + 1;
+    find_zero_idx(hdr);
+    return ORC_OK;
+}
+
+void orc_index_of_many_f32(const orc_quant_header* h, const float* x, int64_t n, int32_t* bins) {
+    for (int64_t i = 0; i < n; i++) bins[i] = orc_index_of(h, (double)x[i]);
+}
+
 int orc_parallel_quantize(const double* values, int32_t n, int32_t bin_num, int32_t threads,
                           int64_t seed, orc_quant_header* hdr, int32_t* bins) {
     if (bin_num <= 1 || bin_num > 65536 || threads < 1) return ORC_E_ARG;

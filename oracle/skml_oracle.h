@@ -78,8 +78,15 @@ int orc_parallel_quantize(const double* values, int32_t n, int32_t bin_num, int3
  * by indexOf.  bins may be NULL. */
 int orc_uniform_quantize(const double* values, int32_t n, int32_t bin_num, orc_quant_header* hdr,
                          int32_t* bins);
+/* The same on float values (each widened to double, exactly as a float[] copied into the
+ * reference's double[] would be): the header only, for the full-size parity tests, whose bins
+ * come from orc_index_of_many_f32 in slices.  No bins argument. */
+int orc_quantize_header_f32(const float* values, int64_t n, int32_t bin_num, int64_t seed, orc_quant_header* hdr);
 /* Quantizer.indexOf (Quantizer.java:49-72) */
 int32_t orc_index_of(const orc_quant_header* h, double x);
+/* Quantizer.quantizeToBins (Quantizer.java:94-101) over a slice of float values: bins[i] =
+ * indexOf((double) x[i]).  Elementwise, so callers may run slices on several threads. */
+void orc_index_of_many_f32(const orc_quant_header* h, const float* x, int64_t n, int32_t* bins);
 /* Quantizer.getValues (Quantizer.java:39-47) */
 void orc_get_values(const orc_quant_header* h, double* out);
 /* Quantizer.timesBy (Quantizer.java:119-124) */

@@ -28,6 +28,8 @@ SKML_E_OOM = 6
 SKML_E_STATE = 7
 UNIQUE_ID_BYTES = 128
 SKML_MAX_BINS = 65536
+SKML_QUANTILE = 0
+SKML_UNIFORM = 1
 
 vp = C.c_void_p
 i32 = C.c_int32
@@ -71,6 +73,7 @@ _SIGS = {
     "skml_ctx_kernel_stats": (C.c_int, [vp, C.c_int, i64p, C.POINTER(C.c_double)]),
     "skml_ctx_reset_stats": (C.c_int, [vp]),
     "skml_debug_leaf_stage": (C.c_int, [vp, vp, i64, C.c_int, C.c_int, C.POINTER(C.c_double)]),
+    "skml_debug_sparse_scratch_fail": (C.c_int, [C.c_int]),
     "skml_dense_payload_bytes": (C.c_size_t, [i64, i32]),
     "skml_dense_encode_f32": (C.c_int, [vp, vp, i64, C.POINTER(Params), vp, C.c_size_t]),
     "skml_dense_encode_with_splits_f32": (C.c_int, [vp, vp, i64, dblp, i32, C.c_double, C.c_double,

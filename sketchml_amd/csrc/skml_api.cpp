@@ -1673,13 +1673,15 @@ int decode_host(skml_ctx* c, const void* payload, size_t len, T* out, int64_t n,
 
 extern "C" {
 
-// params->parallelism > 1 selects QuantileQuantizer.parallelQuantize with that many slices (as
-// on the sparse path); otherwise quantize.
+// params->quant_type = SKML_UNIFORM selects UniformQuantizer (Quantizer.newQuantizer's switch,
+// base/Quantizer.java:126-136, as on the sparse path); otherwise params->parallelism > 1 selects
+// QuantileQuantizer.parallelQuantize with that many slices, else quantize.
 int skml_dense_encode_host_f32(skml_ctx* c, const float* x, int64_t n, const skml_params* p, void* payload,
                                size_t cap, size_t* written) {
     return encode_host<float>(c, x, n, p, payload, cap, written,
                               [](skml_ctx* c2, const float* xd, int64_t m, const skml_params* q, void* pl, size_t cp) {
-                                  return q->parallelism > 1
+                                  return q->quant_type == SKML_UNIFORM ? skml_dense_encode_uniform_f32(c2, xd, m, q, pl, cp)
+                                         : q->parallelism > 1
                                              ? skml_dense_encode_parallel_f32(c2, xd, m, q->parallelism, q, pl, cp)
                                              : skml_dense_encode_f32(c2, xd, m, q, pl, cp);
                               });
@@ -1689,7 +1691,8 @@ int skml_dense_encode_host_f64(skml_ctx* c, const double* x, int64_t n, const sk
                                size_t cap, size_t* written) {
     return encode_host<double>(c, x, n, p, payload, cap, written,
                                [](skml_ctx* c2, const double* xd, int64_t m, const skml_params* q, void* pl, size_t cp) {
-                                   return q->parallelism > 1
+                                   return q->quant_type == SKML_UNIFORM ? skml_dense_encode_uniform_f64(c2, xd, m, q, pl, cp)
+                                          : q->parallelism > 1
                                               ? skml_dense_encode_parallel_f64(c2, xd, m, q->parallelism, q, pl, cp)
                                               : skml_dense_encode_f64(c2, xd, m, q, pl, cp);
                                });

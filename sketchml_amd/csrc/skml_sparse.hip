@@ -914,7 +914,6 @@ constexpr int kMmSubCells = 1 << kMmSubBits;
 constexpr int kMmBucketCells = kMmCellsPerBucket;
 static_assert(kMmBucketCells == 1 << kMmBucketBits, "bucket size");
 constexpr int kMmLdsBuckets = 8192;  // per-workgroup bucket tables in LDS up to this many (96 KB in the scatter)
-constexpr int kMmChunk = (int)kMmChunkElems;
 constexpr int kMmThreads = 1024;  // count / scatter workgroups: big tiles, long per-bucket runs
 #ifndef SKML_MM_BATCH
 #define SKML_MM_BATCH 4
@@ -1070,7 +1069,7 @@ __global__ __launch_bounds__(kMmThreads, SKML_GP_WAVES) void k_group_prep(const 
                                                            uint32_t* __restrict__ err,
                                                            unsigned long long* __restrict__ bucket_count,
                                                            int nbuckets, int32_t* __restrict__ cells_out,
-                                                           uint32_t* __restrict__ tile_off) {
+                                                           uint32_t* __restrict__ tile_off, int64_t chunk) {
     if (gp->status) return;
     __shared__ int64_t S[kMaxGroups + 1];
     __shared__ uint32_t H[kMaxGroups * kDeltaHist];
@@ -1090,7 +1089,7 @@ __global__ __launch_bounds__(kMmThreads, SKML_GP_WAVES) void k_group_prep(const 
         for (int j = threadIdx.x; j < nbuckets; j += kMmThreads) BH[j] = 0;
     __syncthreads();
     uint32_t bad = 0;
-    const int64_t c0 = (int64_t)blockIdx.x * kMmChunk, c1 = std::min<int64_t>(n, c0 + kMmChunk);
+    const int64_t c0 = (int64_t)blockIdx.x * chunk, c1 = std::min<int64_t>(n, c0 + chunk);
     // kMmBatch elements per thread in flight: their keys and predecessors load together
     for (int64_t base = c0; base < c1; base += kMmBatch * kMmThreads) {
         int32_t key[kMmBatch], prv[kMmBatch];
@@ -1206,9 +1205,10 @@ hipError_t launch_group_prep(hipStream_t st, const int32_t* gkeys, int64_t n, co
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL(k_group_prep, dim3((unsigned)sp_tiles(n, kMmChunk)), dim3(kMmThreads), lds, st, gkeys, n, gp,
+    const int64_t chunk = mm_chunk(n);
+    hipLaunchKernelGGL(k_group_prep, dim3((unsigned)sp_tiles(n, chunk)), dim3(kMmThreads), lds, st, gkeys, n, gp,
                        need, hist, err, reinterpret_cast<unsigned long long*>(bucket_count), nbuckets, cells,
-                       nbuckets <= kMmLdsBuckets ? tile_off : nullptr);
+                       nbuckets <= kMmLdsBuckets ? tile_off : nullptr, chunk);
     return hipGetLastError();
 }
 
@@ -1224,7 +1224,7 @@ __global__ __launch_bounds__(kMmThreads) void k_mm_scatter(const int32_t* __rest
                                                            unsigned long long* __restrict__ cursor, int nbuckets,
                                                            uint64_t* __restrict__ pairs,
                                                            const int32_t* __restrict__ cells_in,
-                                                           const uint32_t* __restrict__ tile_off) {
+                                                           const uint32_t* __restrict__ tile_off, int64_t chunk) {
     if (gp->status) return;
     __shared__ int64_t S[kMaxGroups + 1];
     extern __shared__ uint64_t dyn64[];  // dst[nbuckets] (u64), cnt[nbuckets] (u32): dynamic, see launch
@@ -1236,7 +1236,7 @@ __global__ __launch_bounds__(kMmThreads) void k_mm_scatter(const int32_t* __rest
     if (lds_b)
         for (int j = threadIdx.x; j < nbuckets; j += kMmThreads) cnt[j] = 0;
     __syncthreads();
-    const int64_t c0 = (int64_t)blockIdx.x * kMmChunk, c1 = std::min<int64_t>(n, c0 + kMmChunk);
+    const int64_t c0 = (int64_t)blockIdx.x * chunk, c1 = std::min<int64_t>(n, c0 + chunk);
     // cell of (element i, row r): from k_group_prep's table when it kept one, else hashed again
     auto cell_of = [&](int g, int r, int64_t i, int32_t key) -> int64_t {
         return cells_in ? (int64_t)cells_in[(int64_t)r * n + i] : mm_cell(gp, g, r, key);
@@ -1353,7 +1353,7 @@ __device__ __forceinline__ void mm_scatter_staged_body(const int32_t* __restrict
                                                        const uint64_t* __restrict__ bucket_base, int nbuckets,
                                                        PAIR* __restrict__ pairs, const int32_t* __restrict__ cells_in,
                                                        const uint32_t* __restrict__ tile_off, uint64_t* dyn64,
-                                                       uint32_t* scan_sh) {
+                                                       uint32_t* scan_sh, int64_t chunk) {
     constexpr bool kNarrow = sizeof(PAIR) == 4;
     constexpr int kStage = 8 * T;
     // LDS: dstb[nb] u64 | stage[kStage] PAIR | lc[nb] u32 | lofs[nb + 1] u32 | sb[kStage] u16
@@ -1368,7 +1368,7 @@ __device__ __forceinline__ void mm_scatter_staged_body(const int32_t* __restrict
         dstb[j] = bucket_base[j] + row[j];
         lc[j] = 0;
     }
-    const int64_t c0 = (int64_t)blockIdx.x * kMmChunk, c1 = std::min<int64_t>(n, c0 + kMmChunk);
+    const int64_t c0 = (int64_t)blockIdx.x * chunk, c1 = std::min<int64_t>(n, c0 + chunk);
     const int et = 8 / rows;  // elements per thread per chunk: et * rows <= 8 pairs each
     const int np = et * rows;
     const int64_t step = (int64_t)et * T;
@@ -1464,16 +1464,16 @@ __global__ __launch_bounds__(T) void k_mm_scatter_staged(const int32_t* __restri
                                                          const uint64_t* __restrict__ bucket_base, int nbuckets,
                                                          void* __restrict__ pairs,
                                                          const int32_t* __restrict__ cells_in,
-                                                         const uint32_t* __restrict__ tile_off) {
+                                                         const uint32_t* __restrict__ tile_off, int64_t chunk) {
     if (gp->status) return;
     extern __shared__ uint64_t dyn64[];
     __shared__ uint32_t scan_sh[T / 64];
     if (gp->mm_narrow)
         mm_scatter_staged_body<T, uint32_t>(gkeys, gbins, n, gp, bucket_base, nbuckets,
-                                            static_cast<uint32_t*>(pairs), cells_in, tile_off, dyn64, scan_sh);
+                                            static_cast<uint32_t*>(pairs), cells_in, tile_off, dyn64, scan_sh, chunk);
     else
         mm_scatter_staged_body<T, uint64_t>(gkeys, gbins, n, gp, bucket_base, nbuckets,
-                                            static_cast<uint64_t*>(pairs), cells_in, tile_off, dyn64, scan_sh);
+                                            static_cast<uint64_t*>(pairs), cells_in, tile_off, dyn64, scan_sh, chunk);
 }
 #ifndef SKML_STAGE_THREADS
 #define SKML_STAGE_THREADS 512
@@ -1492,6 +1492,7 @@ hipError_t launch_mm_scatter(hipStream_t st, const int32_t* gkeys, const uint16_
                              void* pairs_v, const int32_t* cells, const uint32_t* tile_off) {
     uint64_t* pairs = static_cast<uint64_t*>(pairs_v);  // the unstaged scatter: key-carrying pairs only
     if (n <= 0) return hipSuccess;
+    const int64_t chunk = mm_chunk(n);
     if (mm_scatter_staged(cells != nullptr, tile_off != nullptr, nbuckets)) {
         static bool attr_s = false;
         if (!attr_s) {
@@ -1500,9 +1501,9 @@ hipError_t launch_mm_scatter(hipStream_t st, const int32_t* gkeys, const uint16_
             if (e != hipSuccess) return e;
             attr_s = true;
         }
-        hipLaunchKernelGGL(k_mm_scatter_staged<kStageThreads>, dim3((unsigned)sp_tiles(n, kMmChunk)),
+        hipLaunchKernelGGL(k_mm_scatter_staged<kStageThreads>, dim3((unsigned)sp_tiles(n, chunk)),
                            dim3(kStageThreads), staged_lds(nbuckets), st, gkeys, gbins, n, gp, bucket_base, nbuckets,
-                           pairs_v, cells, tile_off);
+                           pairs_v, cells, tile_off, chunk);
         return hipGetLastError();
     }
     constexpr size_t kPer = sizeof(uint64_t) + sizeof(uint32_t);
@@ -1514,9 +1515,9 @@ hipError_t launch_mm_scatter(hipStream_t st, const int32_t* gkeys, const uint16_
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL(k_mm_scatter, dim3((unsigned)sp_tiles(n, kMmChunk)), dim3(kMmThreads), lds, st, gkeys, gbins, n,
+    hipLaunchKernelGGL(k_mm_scatter, dim3((unsigned)sp_tiles(n, chunk)), dim3(kMmThreads), lds, st, gkeys, gbins, n,
                        gp, bucket_base, reinterpret_cast<unsigned long long*>(cursor), nbuckets, pairs, cells,
-                       nbuckets <= kMmLdsBuckets ? tile_off : nullptr);
+                       nbuckets <= kMmLdsBuckets ? tile_off : nullptr, chunk);
     return hipGetLastError();
 }
 

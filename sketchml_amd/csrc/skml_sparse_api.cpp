@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -417,6 +418,9 @@ int check_params(const skml_params* p) {
 // (k_sp_plan_*) -- and the host reads the quantizer header, splits and group table back once.
 // vals: nnz floats, or nnz doubles when f64 (the reference's own double[] values: the quantizer
 // sketches and bins the doubles themselves, QuantileQuantizer.quantize(double[])).
+// skml_debug_sparse_scratch_fail: simulate failed MinMax staging allocations (tests only)
+static std::atomic<int> g_fail_cellbuf{0};
+
 int encode_kv(skml_ctx* c, const int32_t* keys, const void* vals, bool f64, int64_t nnz, const skml_params* p,
               skml_sparse** out) {
     hipStream_t st = ctx_stream(c);
@@ -475,10 +479,19 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const void* vals, bool f64, int6
     SpInit init{};
     init.G = G;
     init.rows = rows;
-    // the staged scatter's conditions (cells kept, ranges reserved), known from the sizes alone
+    // The staged scatter needs the pairs' hashed cells (int32, under 2^31 cells) and the per-(tile,
+    // bucket) reservations (under 2^31 pairs).  Both scratch buffers are taken here, before
+    // k_sp_plan_edges chooses narrow pairs, so narrow_ok follows what was actually allocated: when
+    // either allocation fails the encode takes the rehashing, key-carrying scatter instead of failing.
     const int nbuckets = (int)((cells_max + kMmCellsPerBucket - 1) / kMmCellsPerBucket);
     const bool reserve = (uint64_t)rows * (uint64_t)nnz < (1ull << 31);
-    init.narrow_ok = mm_scatter_staged(cells_max < INT32_MAX, reserve, nbuckets) ? 1 : 0;
+    const int64_t mm_tiles = sp_tiles(nnz, mm_chunk(nnz));  // the tiles k_group_prep / the scatter use
+    const bool staging = !g_fail_cellbuf.load();
+    uint32_t* tile_off =
+        reserve && staging ? scratch<uint32_t>(c, kSlotTileOff, (size_t)mm_tiles * (size_t)nbuckets) : nullptr;
+    int32_t* cellbuf =
+        cells_max < INT32_MAX && staging ? scratch<int32_t>(c, kSlotCellIdx, (size_t)rows * (size_t)nnz) : nullptr;
+    init.narrow_ok = mm_scatter_staged(cellbuf != nullptr, tile_off != nullptr, nbuckets) ? 1 : 0;
     init.col_ratio = p->col_ratio;
     for (int g = 0; g < G; g++) pick_hashes(p->hash_seed + g, rows, init.hash_ids[g]);
     SP_TRY(launch_sp_plan_edges(st, s->qpayload, init, s->g_dev));
@@ -497,9 +510,6 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const void* vals, bool f64, int6
     int32_t* gk = scratch<int32_t>(c, kSlotGKeys, (size_t)nnz);
     uint16_t* gb = scratch<uint16_t>(c, kSlotGBins, (size_t)nnz);  // grouped bins (< 65536)
     uint8_t* need = scratch<uint8_t>(c, kSlotNeed, (size_t)nnz);
-    // per (tile, bucket) reserved offsets (u32: a bucket holds fewer than 2^32 pairs)
-    const int64_t mm_tiles = sp_tiles(nnz, kMmChunkElems);
-    uint32_t* tile_off = reserve ? scratch<uint32_t>(c, kSlotTileOff, (size_t)mm_tiles * (size_t)nbuckets) : nullptr;
     // reserved ranges are padded to 16 wide (u64) or 32 narrow (u32) pairs
     const size_t npairs = (size_t)rows * (size_t)nnz + (tile_off ? (size_t)15 * mm_tiles * nbuckets : 0);
     const size_t npairs32 = (size_t)rows * (size_t)nnz + (tile_off ? (size_t)31 * mm_tiles * nbuckets : 0);
@@ -509,12 +519,6 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const void* vals, bool f64, int6
     uint32_t* hist = small;
     uint32_t* err = small + kMaxGroups * kDeltaHist;
     SP_TRY(launch_part_scatter(st, keys, s->qpayload, nnz, s->g_dev, tc, gk, gb));
-    // the pairs' table cells, hashed once (int32 cells; without room or past 2^31 cells the scatter rehashes)
-    int32_t* cellbuf =
-        cells_max < INT32_MAX ? scratch<int32_t>(c, kSlotCellIdx, (size_t)rows * (size_t)nnz) : nullptr;
-    // k_sp_plan_edges chose narrow pairs on init.narrow_ok: the staged scatter must run
-    if (init.narrow_ok && !mm_scatter_staged(cellbuf != nullptr, tile_off != nullptr, nbuckets))
-        return bail(sfail(SKML_E_OOM, "sparse scratch (MinMax cells)"));
     SP_TRY(launch_group_prep(st, gk, nnz, s->g_dev, need, hist, err, bucket, nbuckets, cellbuf, tile_off));
     // ---- 4. DeltaAdaptive key streams on the side stream, beside the MinMax scatter and minima:
     // the VALU-bound stream writer runs while the scatter waits on memory.  The two chains touch
@@ -1890,6 +1894,11 @@ int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t
     unsigned bad = 0;
     if (int e = sync_to_host(c, &bad, err, sizeof(bad))) return e;
     if (bad) return sfail(SKML_E_ARG, "a payload holds a key outside [0, %lld) or a bin outside its values", (long long)dim);
+    return SKML_OK;
+}
+
+int skml_debug_sparse_scratch_fail(int on) {
+    g_fail_cellbuf.store(on ? 1 : 0);
     return SKML_OK;
 }
 

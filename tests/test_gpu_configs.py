@@ -220,6 +220,81 @@ def test_c2_full_size_matches_oracle(gpu):
     assert np.array_equal(dec.cpu().numpy().view(np.uint32), want.view(np.uint32))
 
 
+def _unpack_codes(codes, bits, count):
+    """Bins from a payload's packed codes (code_bits per element, LSB-first; include/skml.h)."""
+    if bits == 8:
+        return codes[:count].astype(np.int32)
+    if bits == 16:
+        return codes[: 2 * count].view(np.uint16).astype(np.int32)
+    per = 8 // bits
+    shifts = (np.arange(per, dtype=np.uint8) * bits)[None, :]
+    out = (codes[: (count + per - 1) // per, None] >> shifts) & np.uint8((1 << bits) - 1)
+    return out.reshape(-1)[:count].astype(np.int32)
+
+
+def _full_size_parity(gpu, n, bins, seed, want_bin_num, want_bits, slice_n=2**24):
+    """Encode n device-generated N(0,1) floats (torch generator `seed`, as bench.py makes them) and
+    compare with the oracle: header, splits, every bin (slice by slice from the packed codes) and
+    every decoded float's bits.  The oracle's sketch runs once over all n values (it is sequential
+    by nature: one Random stream); its quantizeToBins runs slice by slice on a thread pool."""
+    L = _lib()
+    ctx = gpu.get_context()
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    x = torch.randn(n, device="cuda", generator=g)
+    nb = L.lib.skml_dense_payload_bytes(n, bins)
+    pl = gpu.alloc_aligned(nb, "cuda")
+    assert L.lib.skml_dense_encode_f32(ctx.handle, C.c_void_p(x.data_ptr()), n, C.byref(_params(bins, seed)),
+                                       C.c_void_p(pl.data_ptr()), nb) == 0, L.last_error()
+    dec = torch.empty(n, dtype=torch.float32, device="cuda")
+    assert L.lib.skml_dense_decode_f32(ctx.handle, C.c_void_p(pl.data_ptr()), C.c_void_p(dec.data_ptr()), n) == 0
+    xh = x.cpu().numpy()
+    del x
+    st, h, sp = _header(gpu, pl)
+    assert st == 0 and h.code_bits == want_bits
+    codes = pl[h.codes_offset: h.codes_offset + (n * h.code_bits + 7) // 8].cpu().numpy()
+    del pl
+    oq = O.quantize_header_f32(xh, bins, seed)
+    assert oq.bin_num == want_bin_num
+    assert (h.bin_num, h.zero_idx, h.min, h.max, h.n) == (oq.bin_num, oq.zero_idx, oq.min, oq.max, n)
+    assert np.array_equal(sp, oq.splits)
+    vals32 = oq.values().astype(np.float32)
+
+    def check(s0):
+        s1 = min(n, s0 + slice_n)
+        ob = O.index_of_many_f32(oq, xh[s0:s1])
+        per = 8 // h.code_bits if h.code_bits < 8 else 1
+        lo = s0 // per * (h.code_bits // 8 if h.code_bits >= 8 else 1)
+        got = _unpack_codes(codes[lo:], h.code_bits, s1 - s0)
+        return bool(np.array_equal(got, ob)), ob
+
+    bad = []
+    with ThreadPoolExecutor(16) as ex:
+        for s0, (ok, ob) in zip(range(0, n, slice_n), ex.map(check, range(0, n, slice_n))):
+            if not ok:
+                bad.append(s0)
+                continue
+            d = dec[s0: s0 + len(ob)].cpu().numpy()
+            if not np.array_equal(d.view(np.uint32), vals32[ob].view(np.uint32)):
+                bad.append(s0)
+    assert not bad, f"slices differing from the oracle start at {bad[:8]}"
+
+
+@pytest.mark.timeout(300)
+def test_north_star_2p28_matches_oracle(gpu):
+    """The north-star configuration bench.py's headline times: a 2^28-float (1 GiB) bucket, 256
+    requested bins (129 effective, 8-bit codes), seed 6.  At this size the leaf runs 16,384 tiles
+    (4 waves per wave slot) and the merge tree reaches level 20: splits, header, every bin and every
+    decoded float against the oracle (QuantileQuantizer.java:27-50)."""
+    _full_size_parity(gpu, 2**28, 256, 6, 129, 8)
+
+
+@pytest.mark.timeout(600)
+def test_c5_whole_gradient_2p30_matches_oracle(gpu):
+    """C5's whole 1B-float (2^30) gradient on one GPU at B = 4 (2-bit codes), seed 5: 64 leaf tiles
+    per wave slot and a level-22 merge tree, against the oracle element by element."""
+    _full_size_parity(gpu, 2**30, 4, 5, 4, 2)
+
+
 def test_c1_app_loopback_l2_bound(gpu):
     """C1 (the reference's App.dense loopback, sample/App.java:33-63) at exactly 10^6 values:
     oracle parity, the half-bin-width bound per element (P2) and the loopback L2 error equal to

@@ -160,6 +160,46 @@ def test_encode_host_f64_and_host_helpers(gpu):
     assert np.array_equal(out, want)
 
 
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+def test_encode_host_uniform_quant_type(gpu, dtype):
+    """params.quant_type = SKML_UNIFORM on the host entry points (the JNI encodeDenseUniformF64 /
+    HipUniformQuantizer path): UniformQuantizer.quantize (quantization/UniformQuantizer.java:21-45)
+    against the oracle, and byte-equal to the device-resident skml_dense_encode_uniform_*."""
+    L = _L()
+    ctx = gpu.get_context()
+    n = 2**20 + 4321
+    x = np.random.default_rng(12).standard_normal(n)
+    if dtype == "f32":
+        x = x.astype(np.float32)
+    p = _params(256, 0)
+    p.quant_type = L.SKML_UNIFORM
+    enc_host = L.lib.skml_dense_encode_host_f32 if dtype == "f32" else L.lib.skml_dense_encode_host_f64
+    cap = C.c_size_t()
+    assert enc_host(ctx.handle, None, n, C.byref(p), None, 0, C.byref(cap)) == 0
+    pl = np.zeros(cap.value, dtype=np.uint8)
+    wrote = C.c_size_t()
+    assert enc_host(ctx.handle, x.ctypes.data_as(C.c_void_p), n, C.byref(p), pl.ctypes.data_as(C.c_void_p),
+                    pl.nbytes, C.byref(wrote)) == 0, L.last_error()
+    pl = pl[: wrote.value]
+    oq = O.uniform_quantize(x.astype(np.float64), 256)
+    h = L.DenseHeader()
+    sp = np.zeros(256, dtype=np.float64)
+    assert L.lib.skml_dense_info_host(pl.ctypes.data_as(C.c_void_p), len(pl), C.byref(h),
+                                      sp.ctypes.data_as(L.dblp), 256) == 0
+    assert (h.bin_num, h.zero_idx, h.min, h.max, h.n) == (oq.bin_num, oq.zero_idx, oq.min, oq.max, n)
+    assert np.array_equal(sp[: h.bin_num - 1], oq.splits)
+    bins = np.zeros(n, dtype=np.int32)
+    assert L.lib.skml_dense_bins_host(pl.ctypes.data_as(C.c_void_p), len(pl), bins.ctypes.data_as(C.c_void_p), n) == 0
+    assert np.array_equal(bins, oq.bins)
+    xd = torch.from_numpy(x).cuda()
+    nb = L.lib.skml_dense_payload_bytes(n, 256)
+    dpl = gpu.alloc_aligned(nb, "cuda")
+    enc_dev = L.lib.skml_dense_encode_uniform_f32 if dtype == "f32" else L.lib.skml_dense_encode_uniform_f64
+    assert enc_dev(ctx.handle, C.c_void_p(xd.data_ptr()), n, C.byref(p), C.c_void_p(dpl.data_ptr()), nb) == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(pl, dpl[: len(pl)].cpu().numpy())
+
+
 def test_sparse_and_delta_host_entries(gpu):
     L = _L()
     ctx = gpu.get_context()

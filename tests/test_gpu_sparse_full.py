@@ -40,23 +40,41 @@ def _compare_groups(pl, osp, groups):
 
 
 def test_c3_full_size_matches_oracle(gpu):
+    """Both C3 entry points at full size against one oracle result: to_sparse + encode_sparse, and
+    encode_dense_as_sparse (the call bench.py times: compaction into the context's scratch, then
+    encode_kv), whose keys the oracle's own toSparse (DenseDoubleGradient.scala:64-89) produces."""
     dim = 2**28
     g = torch.Generator(device="cuda").manual_seed(3)
     x = torch.randn(dim, device="cuda", generator=g)
     x[torch.rand(dim, device="cuda", generator=g) >= 0.1] = 0.0
+    pl_dense = gpu.encode_dense_as_sparse(x, 256, 8, 2, 0.3, 3, 3)
     keys, vals = gpu.to_sparse(x)
+    xh = x.cpu().numpy()
     del x
     pl = gpu.encode_sparse(keys, vals, 256, 8, 2, 0.3, 3, 3)
     kh, vh = keys.cpu().numpy(), vals.cpu().numpy()
     assert len(kh) > 26_000_000
-    osp = O.sparse_compress(kh, vh.astype(np.float64), 256, 8, 2, 0.3, 3, 3)
+    ok_keys, ok_vals = O.to_sparse(xh.astype(np.float64))
+    del xh
+    assert np.array_equal(kh, ok_keys) and np.array_equal(vh.astype(np.float64), ok_vals)
+    osp = O.sparse_compress(ok_keys, ok_vals, 256, 8, 2, 0.3, 3, 3)
+    del ok_keys, ok_vals
+    # the timed entry point first: header, every group, restore
+    hdr, splits = pl_dense.quant_header()
+    assert (hdr.bin_num, hdr.zero_idx, hdr.min, hdr.max) == (osp.q.bin_num, osp.q.zero_idx, osp.q.min, osp.q.max)
+    assert np.array_equal(splits, osp.q.splits)
+    _compare_groups(pl_dense, osp, 8)
+    rk, rb = pl_dense.restore_bins()
+    ok, ob = osp.restore()
+    assert np.array_equal(rk.cpu().numpy(), ok)
+    assert np.array_equal(rb.cpu().numpy(), ob)
+    del rk, rb, pl_dense
     hdr, splits = pl.quant_header()
     assert (hdr.bin_num, hdr.zero_idx, hdr.min, hdr.max) == (osp.q.bin_num, osp.q.zero_idx, osp.q.min, osp.q.max)
     assert np.array_equal(splits, osp.q.splits)
     assert int(osp.col_num.max()) > 900_000       # the large-modulus regime of the hash
     _compare_groups(pl, osp, 8)
     rk, rb = pl.restore_bins()
-    ok, ob = osp.restore()
     assert np.array_equal(rk.cpu().numpy(), ok)
     assert np.array_equal(rb.cpu().numpy(), ob)
     del rk, rb
@@ -214,6 +232,31 @@ def test_minmax_pair_width_paths(gpu, pos_frac, mixed, dim):
     osp = O.sparse_compress(keys, vals, 256, 8, 2, 0.3, 1, 2)
     assert _has_mixed_group(osp.q.zero_idx, osp.q.bin_num, 8) == mixed
     pl = gpu.encode_sparse(torch.from_numpy(keys).cuda(), torch.from_numpy(vals).cuda(), 256, 8, 2, 0.3, 1, 2)
+    _compare_groups(pl, osp, 8)
+    rk, rb = pl.restore_bins()
+    ok, ob = osp.restore()
+    assert np.array_equal(rk.cpu().numpy(), ok) and np.array_equal(rb.cpu().numpy(), ob)
+
+
+@pytest.mark.parametrize("pos_frac,mixed", [(0.5, False), (0.03, True)])
+def test_minmax_without_staging_scratch(gpu, pos_frac, mixed):
+    """When the MinMax staging scratch (hashed cells, per-(tile, bucket) reservations) cannot be
+    allocated, the encode falls back to key-carrying pairs and the rehashing scatter instead of
+    failing (skml_debug_sparse_scratch_fail simulates the failed allocations); the tables still
+    equal the oracle's."""
+    from sketchml_amd import _lib
+    rng = np.random.default_rng(17)
+    dim = 2000003
+    keys = np.nonzero(rng.random(dim) < 0.3)[0].astype(np.int32)
+    vals = -np.abs(rng.standard_normal(len(keys)))
+    vals[rng.random(len(keys)) < pos_frac] *= -1
+    osp = O.sparse_compress(keys, vals, 256, 8, 2, 0.3, 1, 2)
+    assert _has_mixed_group(osp.q.zero_idx, osp.q.bin_num, 8) == mixed
+    _lib.lib.skml_debug_sparse_scratch_fail(1)
+    try:
+        pl = gpu.encode_sparse(torch.from_numpy(keys).cuda(), torch.from_numpy(vals).cuda(), 256, 8, 2, 0.3, 1, 2)
+    finally:
+        _lib.lib.skml_debug_sparse_scratch_fail(0)
     _compare_groups(pl, osp, 8)
     rk, rb = pl.restore_bins()
     ok, ob = osp.restore()

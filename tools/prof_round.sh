@@ -14,7 +14,7 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-for
     -- python3 bench.py --no-cpu-baseline --no-extras --steps 10 > "$OUT/fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv \
     -- python3 bench.py --no-cpu-baseline --no-extras --steps 10 > "$OUT/write.log" 2>&1
-python3 tools/pmc_summary.py --fetch "$OUT/fetch" --write "$OUT/write" --n 67108864 --out "$OUT/pmc.json" > /dev/null
+python3 tools/pmc_summary.py --fetch "$OUT/fetch" --write "$OUT/write" --n 268435456 --out "$OUT/pmc.json" > /dev/null
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY \
     -d "$OUT/sq" -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-extras --steps 5 --warmup 2 > "$OUT/sq.log" 2>&1
 python3 - "$OUT" <<'PY'
@@ -27,7 +27,8 @@ for p in glob.glob(os.path.join(out, "sq", "**", "*counter_collection.csv"), rec
             continue
         per.setdefault(r["Kernel_Name"], {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
 res = {k: {c: statistics.mean(v) for c, v in d.items()} for k, d in per.items()}
-json.dump({"source": "rocprofv3 --pmc SQ_* (one pass), bench.py --steps 5, n=2^26", "per_launch_mean": res},
+json.dump({"source": "rocprofv3 --pmc SQ_* (one pass), bench.py --steps 5 (default: n=2^28)", "n": 268435456,
+           "per_launch_mean": res},
           open(os.path.join(out, "sq.json"), "w"), indent=1)
 PY
 find "$OUT" -name "*counter_collection.csv" -size +20M -delete
