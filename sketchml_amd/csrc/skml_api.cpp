@@ -1166,11 +1166,13 @@ int skml_dense_decode_sum_f32(skml_ctx* c, const void* payloads, int32_t P, size
             skml_dense_payload_bytes(n, h[p].req_bins) > stride)
             return fail(SKML_E_ARG, "payload %d: inconsistent header or larger than the stride %zu", p, stride);
     }
-    int common_bits = h[0].code_bits;
-    for (int p = 1; p < P; p++)
+    int common_bits = h[0].code_bits, max_bins = h[0].bin_num;
+    for (int p = 1; p < P; p++) {
         if (h[p].code_bits != common_bits) common_bits = 0;
+        max_bins = std::max(max_bins, (int)h[p].bin_num);
+    }
     KernelTimer kt(c, SKML_K_DECODE_SUM);
-    HIP_TRY(launch_decode_sum(c->stream, payloads, P, stride, out, n, scale, common_bits));
+    HIP_TRY(launch_decode_sum(c->stream, payloads, P, stride, out, n, scale, common_bits, max_bins));
     return SKML_OK;
 }
 

@@ -439,10 +439,115 @@ __global__ __launch_bounds__(256) void k_decode_sum(const uint8_t* __restrict__ 
     }
 }
 
+// Bank-replicated LUTs (payloads of at most 256 bins, one code width).  Every lookup of the sum
+// is a ds_read_b64 at a random entry; with one table per payload (k_decode_sum) the 64 lanes of a
+// wave land on 16 bank pairs at random and the read takes ~8-9 passes instead of the b64 minimum
+// of 4.  Here each payload's table holds R copies interleaved entry by entry (entry c of copy r
+// at double index c * R + r) and lane l reads copy l % R: with R = 16 an entry of copy r sits in
+// banks 2r and 2r + 1 whatever c is, so every bank serves exactly the 4 lanes of its copy.  The
+// tables of all P payloads (P * bins * R doubles, up to 160 KB) fill one workgroup of 1,024
+// threads per CU; R is the largest power of two <= 16 that fits.
+constexpr int kRepThreads = 1024;
+constexpr size_t kRepLdsMax = 160 * 1024 - 256;
+template <int BITS, int R>
+__global__ __launch_bounds__(kRepThreads) void k_decode_sum_rep(const uint8_t* __restrict__ payloads, int P,
+                                                                size_t stride, float* __restrict__ out, int64_t n,
+                                                                double scale, int tab) {
+    extern __shared__ double rl[];  // P tables of `tab` doubles (bins * R)
+    __shared__ const uint8_t* s_codes[kMaxSumPayloads];
+    for (int p = 0; p < P; p++) {
+        const uint8_t* pl = payloads + (size_t)p * stride;
+        const skml_dense_header* h = reinterpret_cast<const skml_dense_header*>(pl);
+        const double* sp = reinterpret_cast<const double*>(pl + kHeaderBytes);
+        if (threadIdx.x == 0) s_codes[p] = pl + h->codes_offset;
+        const int cells = h->bin_num * R;
+        for (int i = threadIdx.x; i < cells; i += kRepThreads) rl[(size_t)p * tab + i] = lut_value(h, sp, i / R);
+    }
+    __syncthreads();
+    const double* my = rl + (threadIdx.x & (R - 1));
+    const int64_t full = n / 16;
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    for (int64_t g = (int64_t)blockIdx.x * kRepThreads + threadIdx.x; g < full; g += (int64_t)gridDim.x * kRepThreads) {
+        const int64_t e0 = g * 16;
+        double acc[16];
+#pragma unroll
+        for (int e = 0; e < 16; e++) acc[e] = 0.0;
+        for (int p0 = 0; p0 < P; p0 += kSumChunk) {
+            uint32_t w[kSumChunk][8];
+#pragma unroll
+            for (int q = 0; q < kSumChunk; q++)
+                if (p0 + q < P) load_codes16(s_codes[p0 + q], e0, BITS, w[q]);
+#pragma unroll
+            for (int q = 0; q < kSumChunk; q++) {
+                if (p0 + q >= P) break;
+                const double* t = my + (size_t)(p0 + q) * tab;
+#pragma unroll
+                for (int e = 0; e < 16; e++) acc[e] += t[code16_at(w[q], e, BITS) * R];
+            }
+        }
+        f32x4* dst = reinterpret_cast<f32x4*>(out + e0);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const f32x4 o = {(float)(acc[4 * j] * scale), (float)(acc[4 * j + 1] * scale),
+                             (float)(acc[4 * j + 2] * scale), (float)(acc[4 * j + 3] * scale)};
+            __builtin_nontemporal_store(o, dst + j);
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x < 16) {  // the last n % 16 elements
+        const int64_t e = full * 16 + threadIdx.x;
+        if (e < n) {
+            double a = 0.0;
+            for (int p = 0; p < P; p++) a += my[(size_t)p * tab + read_code(s_codes[p], e, BITS) * R];
+            out[e] = (float)(a * scale);
+        }
+    }
+}
+
+template <int BITS, int R>
+hipError_t launch_rep(hipStream_t st, const uint8_t* pl, int P, size_t stride, float* out, int64_t n, double scale,
+                      int max_bins) {
+    static bool attr = false;
+    auto* fn = &k_decode_sum_rep<BITS, R>;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)kRepLdsMax);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    const int tab = max_bins * R;
+    const size_t lds = sizeof(double) * (size_t)tab * (size_t)P;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int64_t groups = n / 16;
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((groups + kRepThreads - 1) / kRepThreads, cus));
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(kRepThreads), lds, st, pl, P, stride, out, n, scale, tab);
+    return hipGetLastError();
+}
+
+template <int BITS>
+hipError_t launch_rep_bits(hipStream_t st, const uint8_t* pl, int P, size_t stride, float* out, int64_t n,
+                           double scale, int max_bins) {
+    const size_t per = sizeof(double) * (size_t)max_bins * (size_t)P;
+    if (per * 16 <= kRepLdsMax) return launch_rep<BITS, 16>(st, pl, P, stride, out, n, scale, max_bins);
+    if (per * 8 <= kRepLdsMax) return launch_rep<BITS, 8>(st, pl, P, stride, out, n, scale, max_bins);
+    if (per * 4 <= kRepLdsMax) return launch_rep<BITS, 4>(st, pl, P, stride, out, n, scale, max_bins);
+    return launch_rep<BITS, 2>(st, pl, P, stride, out, n, scale, max_bins);
+}
+
 hipError_t launch_decode_sum(hipStream_t st, const void* payloads, int P, size_t stride, float* out,
-                             int64_t n, double scale, int common_bits) {
+                             int64_t n, double scale, int common_bits, int max_bins) {
     if (n <= 0) return hipSuccess;
     if (P < 1 || P > kMaxSumPayloads) return hipErrorInvalidValue;
+    if (max_bins <= kSumLutBins && std::getenv("SKML_DECODE_SUM_PLAIN") == nullptr) {
+        const uint8_t* pl = reinterpret_cast<const uint8_t*>(payloads);
+        switch (common_bits) {
+            case 8: return launch_rep_bits<8>(st, pl, P, stride, out, n, scale, max_bins);
+            case 4: return launch_rep_bits<4>(st, pl, P, stride, out, n, scale, max_bins);
+            case 2: return launch_rep_bits<2>(st, pl, P, stride, out, n, scale, max_bins);
+            case 1: return launch_rep_bits<1>(st, pl, P, stride, out, n, scale, max_bins);
+            default: break;  // mixed widths: the per-payload kernel below
+        }
+    }
     const int64_t groups = n / 16;
     const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((groups + 255) / 256, 2048));
     const uint8_t* pl = reinterpret_cast<const uint8_t*>(payloads);

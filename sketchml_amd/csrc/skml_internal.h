@@ -166,7 +166,8 @@ hipError_t launch_quantize(hipStream_t st, const float* x, int64_t n, void* payl
                            int req_bins);
 hipError_t launch_decode(hipStream_t st, const void* payload, float* out, int64_t n);
 hipError_t launch_decode_sum(hipStream_t st, const void* payloads, int P, size_t stride, float* out,
-                             int64_t n, double scale, int common_bits);  // common_bits 0: mixed widths
+                             int64_t n, double scale, int common_bits,
+                             int max_bins);  // common_bits 0: mixed widths
 hipError_t launch_bins(hipStream_t st, const void* payload, int32_t* bins, int64_t n);
 hipError_t launch_ref_body(hipStream_t st, const void* payload, uint8_t* out, int64_t n, int width);
 hipError_t launch_times_by(hipStream_t st, void* payload, double x);

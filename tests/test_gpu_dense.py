@@ -375,6 +375,41 @@ def test_decode_sum(gpu):
     assert np.array_equal(out.cpu().numpy(), (want * (1.0 / P)).astype(np.float32))
 
 
+# (P, requested bins per payload, n), with the oracle's effective bin counts: 8-bit codes at R = 16
+# (8 x 136), R = 8 (8 x up to 221) and R = 4 (16 x up to 235; R = 2 is never needed at P <= 16);
+# 4-, 2- and 1-bit codes; a mixed-width set (the per-payload kernel); n = 15 (tail only).
+@pytest.mark.parametrize("P,bins,n", [(8, [256] * 8, 2**20 + 13), (8, [256] * 8, 40005),
+                                      (16, [512] * 16, 40000 + 5), (5, [16] * 5, 2**18 + 7), (4, [4] * 4, 99999),
+                                      (3, [2] * 3, 4097), (6, [256, 16, 4, 2, 256, 16], 50001), (1, [256], 15)])
+def test_decode_sum_replicated_tables(gpu, P, bins, n):
+    """k_decode_sum_rep (bank-replicated LUTs; R chosen from P and the largest bin count) and the
+    per-payload kernel for mixed widths: bit-exact against the oracle's decodes summed in double
+    in payload order, then x 1/P (Gradient.sum + timesBy, ml/gradient/Gradient.scala:44-49).
+    Requested bins 512 with Maths.unique give effective counts up to 256 (8-bit codes)."""
+    from sketchml_amd import _lib
+    ctx = gpu.get_context()
+    nb = max(_lib.lib.skml_dense_payload_bytes(n, b) for b in bins)
+    nb = (nb + 255) // 256 * 256
+    allp = gpu.alloc_aligned(nb * P, "cuda")
+    want = np.zeros(n, dtype=np.float64)
+    for p in range(P):
+        x = _data(n, 300 + p, "normal")
+        xt = torch.from_numpy(x).cuda()
+        pr = _lib.Params()
+        _lib.lib.skml_params_default(C.byref(pr))
+        pr.seed, pr.bin_num = p, bins[p]
+        assert _lib.lib.skml_dense_encode_f32(ctx.handle, C.c_void_p(xt.data_ptr()), n, C.byref(pr),
+                                              C.c_void_p(allp.data_ptr() + p * nb), nb) == 0
+        torch.cuda.synchronize()
+        oq = O.quantize(x.astype(np.float64), bins[p], p)
+        want += oq.values()[oq.bins]
+    out = torch.empty(n, dtype=torch.float32, device="cuda")
+    assert _lib.lib.skml_dense_decode_sum_f32(ctx.handle, C.c_void_p(allp.data_ptr()), P, nb,
+                                              C.c_void_p(out.data_ptr()), n, 1.0 / P) == 0, _lib.last_error()
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), (want * (1.0 / P)).astype(np.float32))
+
+
 def test_dense_vector_compressor_surface(gpu):
     x = torch.from_numpy(_data(12345, 1, "app")).cuda()
     comp = gpu.DenseVectorCompressor(gpu.QuantizationType.QUANTILE, 256, seed=9)
