@@ -401,7 +401,46 @@ __global__ __launch_bounds__(256) void k_decode_sum(const uint8_t* __restrict__ 
     };
     const int64_t full = n / 16;
     typedef float f32x4 __attribute__((ext_vector_type(4)));
-    for (int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x; g < full; g += (int64_t)gridDim.x * 256) {
+    const int64_t gstep = (int64_t)gridDim.x * 256;
+    if (BITS && P <= kSumChunk) {
+        // software-pipelined: the next step's code loads are issued before this step's lookups, so
+        // a wave waits on HBM once per kernel instead of once per step
+        uint32_t wn[kSumChunk][8];
+        int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+#pragma unroll
+        for (int q = 0; q < kSumChunk; q++)
+            if (q < P && g < full) load_codes16(s_codes[q], g * 16, BITS, wn[q]);
+        for (; g < full; g += gstep) {
+            constexpr int kW = BITS >= 2 ? BITS / 2 : 1;  // code words per payload per step
+            uint32_t w[kSumChunk][8];
+#pragma unroll
+            for (int q = 0; q < kSumChunk; q++)
+#pragma unroll
+                for (int k = 0; k < kW; k++) w[q][k] = wn[q][k];
+            if (g + gstep < full) {
+#pragma unroll
+                for (int q = 0; q < kSumChunk; q++)
+                    if (q < P) load_codes16(s_codes[q], (g + gstep) * 16, BITS, wn[q]);
+            }
+            double acc[16];
+#pragma unroll
+            for (int e = 0; e < 16; e++) acc[e] = 0.0;
+#pragma unroll
+            for (int q = 0; q < kSumChunk; q++) {
+                if (q >= P) break;
+#pragma unroll
+                for (int e = 0; e < 16; e++) acc[e] += value(q, code16_at(w[q], e, BITS));
+            }
+            f32x4* dst = reinterpret_cast<f32x4*>(out + g * 16);
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const f32x4 o = {(float)(acc[4 * j] * scale), (float)(acc[4 * j + 1] * scale),
+                                 (float)(acc[4 * j + 2] * scale), (float)(acc[4 * j + 3] * scale)};
+                __builtin_nontemporal_store(o, dst + j);
+            }
+        }
+    } else
+    for (int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x; g < full; g += gstep) {
         const int64_t e0 = g * 16;
         double acc[16];
 #pragma unroll
@@ -439,112 +478,137 @@ __global__ __launch_bounds__(256) void k_decode_sum(const uint8_t* __restrict__ 
     }
 }
 
-// Bank-replicated LUTs (payloads of at most 256 bins, one code width).  Every lookup of the sum
-// is a ds_read_b64 at a random entry; with one table per payload (k_decode_sum) the 64 lanes of a
-// wave land on 16 bank pairs at random and the read takes ~8-9 passes instead of the b64 minimum
-// of 4.  Here each payload's table holds R copies interleaved entry by entry (entry c of copy r
-// at double index c * R + r) and lane l reads copy l % R: with R = 16 an entry of copy r sits in
-// banks 2r and 2r + 1 whatever c is, so every bank serves exactly the 4 lanes of its copy.  The
-// tables of all P payloads (P * bins * R doubles, up to 160 KB) fill one workgroup of 1,024
-// threads per CU; R is the largest power of two <= 16 that fits.
-constexpr int kRepThreads = 1024;
-constexpr size_t kRepLdsMax = 160 * 1024 - 256;
-template <int BITS, int R>
-__global__ __launch_bounds__(kRepThreads) void k_decode_sum_rep(const uint8_t* __restrict__ payloads, int P,
-                                                                size_t stride, float* __restrict__ out, int64_t n,
-                                                                double scale, int tab) {
-    extern __shared__ double rl[];  // P tables of `tab` doubles (bins * R)
-    __shared__ const uint8_t* s_codes[kMaxSumPayloads];
+// Occupancy form (one code width, at most 8 payloads of at most 256 bins): each lookup is a random
+// ds_read_b64, and a wave keeps at most 15 LDS reads in flight (lgkmcnt), so the sum runs at the
+// rate the resident waves can keep lookups in flight (r04 counters: LDS array busy 22 % of the
+// time, VALU 14 %).  Bank-replicated tables (16 interleaved copies, one workgroup per CU) halved
+// the bank conflicts and ran slower (412 against 355 us at C4) for the same reason.  Here a lane
+// owns 8 elements (half the registers of k_decode_sum: 8 waves per SIMD), the tables take
+// P x bins doubles of dynamic LDS instead of a 32 KB array, and the next step's codes are loaded
+// before this step's lookups.
+constexpr int kOccPer = 8, kOccMaxP = 8;
+__device__ __forceinline__ void load_codes8(const uint8_t* codes, int64_t e0, int bits, uint32_t (&w)[4]) {
+    switch (bits) {
+        case 8: {
+            const uint2 v = *reinterpret_cast<const uint2*>(codes + e0);
+            w[0] = v.x; w[1] = v.y;
+            break;
+        }
+        case 16: {
+            const uint4 v = *reinterpret_cast<const uint4*>(codes + 2 * e0);
+            w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+            break;
+        }
+        case 4: w[0] = *reinterpret_cast<const uint32_t*>(codes + e0 / 2); break;
+        case 2: w[0] = *reinterpret_cast<const uint16_t*>(codes + e0 / 4); break;
+        default: w[0] = codes[e0 / 8]; break;
+    }
+}
+__device__ __forceinline__ uint32_t code8_at(const uint32_t (&w)[4], int e, int bits) {
+    switch (bits) {
+        case 8: return (w[e >> 2] >> (8 * (e & 3))) & 255u;
+        case 16: return (w[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
+        case 4: return (w[0] >> (4 * e)) & 15u;
+        case 2: return (w[0] >> (2 * e)) & 3u;
+        default: return (w[0] >> e) & 1u;
+    }
+}
+template <int BITS, bool PF>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PF ? 6 : 8))) void k_decode_sum_occ(
+    const uint8_t* __restrict__ payloads, int P, size_t stride, float* __restrict__ out, int64_t n, double scale,
+    int tab) {
+    extern __shared__ double lt[];  // P tables of `tab` doubles
+    __shared__ const uint8_t* s_codes[kOccMaxP];
     for (int p = 0; p < P; p++) {
         const uint8_t* pl = payloads + (size_t)p * stride;
         const skml_dense_header* h = reinterpret_cast<const skml_dense_header*>(pl);
         const double* sp = reinterpret_cast<const double*>(pl + kHeaderBytes);
         if (threadIdx.x == 0) s_codes[p] = pl + h->codes_offset;
-        const int cells = h->bin_num * R;
-        for (int i = threadIdx.x; i < cells; i += kRepThreads) rl[(size_t)p * tab + i] = lut_value(h, sp, i / R);
+        for (int b = threadIdx.x; b < h->bin_num; b += 256) lt[p * tab + b] = lut_value(h, sp, b);
     }
     __syncthreads();
-    const double* my = rl + (threadIdx.x & (R - 1));
-    const int64_t full = n / 16;
+    constexpr int kW = BITS >= 4 ? BITS / 4 : 1;  // code words per payload per step
+    const int64_t full = n / kOccPer, gstep = (int64_t)gridDim.x * 256;
+    int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    uint32_t wn[kOccMaxP][4];
+    if (PF) {
+#pragma unroll
+        for (int q = 0; q < kOccMaxP; q++)
+            if (q < P && g < full) load_codes8(s_codes[q], g * kOccPer, BITS, wn[q]);
+    }
     typedef float f32x4 __attribute__((ext_vector_type(4)));
-    for (int64_t g = (int64_t)blockIdx.x * kRepThreads + threadIdx.x; g < full; g += (int64_t)gridDim.x * kRepThreads) {
-        const int64_t e0 = g * 16;
-        double acc[16];
+    for (; g < full; g += gstep) {
+        uint32_t w[kOccMaxP][4];
+        if (PF) {
 #pragma unroll
-        for (int e = 0; e < 16; e++) acc[e] = 0.0;
-        for (int p0 = 0; p0 < P; p0 += kSumChunk) {
-            uint32_t w[kSumChunk][8];
+            for (int q = 0; q < kOccMaxP; q++)
 #pragma unroll
-            for (int q = 0; q < kSumChunk; q++)
-                if (p0 + q < P) load_codes16(s_codes[p0 + q], e0, BITS, w[q]);
+                for (int k = 0; k < kW; k++) w[q][k] = wn[q][k];
+            if (g + gstep < full) {
 #pragma unroll
-            for (int q = 0; q < kSumChunk; q++) {
-                if (p0 + q >= P) break;
-                const double* t = my + (size_t)(p0 + q) * tab;
-#pragma unroll
-                for (int e = 0; e < 16; e++) acc[e] += t[code16_at(w[q], e, BITS) * R];
+                for (int q = 0; q < kOccMaxP; q++)
+                    if (q < P) load_codes8(s_codes[q], (g + gstep) * kOccPer, BITS, wn[q]);
             }
-        }
-        f32x4* dst = reinterpret_cast<f32x4*>(out + e0);
+        } else {
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
+            for (int q = 0; q < kOccMaxP; q++)
+                if (q < P) load_codes8(s_codes[q], g * kOccPer, BITS, w[q]);
+        }
+        double acc[kOccPer];
+#pragma unroll
+        for (int e = 0; e < kOccPer; e++) acc[e] = 0.0;
+#pragma unroll
+        for (int q = 0; q < kOccMaxP; q++) {
+            if (q >= P) break;
+            const double* t = lt + q * tab;
+#pragma unroll
+            for (int e = 0; e < kOccPer; e++) acc[e] += t[code8_at(w[q], e, BITS)];
+        }
+        f32x4* dst = reinterpret_cast<f32x4*>(out + g * kOccPer);
+#pragma unroll
+        for (int j = 0; j < kOccPer / 4; j++) {
             const f32x4 o = {(float)(acc[4 * j] * scale), (float)(acc[4 * j + 1] * scale),
                              (float)(acc[4 * j + 2] * scale), (float)(acc[4 * j + 3] * scale)};
             __builtin_nontemporal_store(o, dst + j);
         }
     }
-    if (blockIdx.x == 0 && threadIdx.x < 16) {  // the last n % 16 elements
-        const int64_t e = full * 16 + threadIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x < kOccPer) {  // the last n % 8 elements
+        const int64_t e = full * kOccPer + threadIdx.x;
         if (e < n) {
             double a = 0.0;
-            for (int p = 0; p < P; p++) a += my[(size_t)p * tab + read_code(s_codes[p], e, BITS) * R];
+            for (int p = 0; p < P; p++) a += lt[p * tab + read_code(s_codes[p], e, BITS)];
             out[e] = (float)(a * scale);
         }
     }
 }
 
-template <int BITS, int R>
-hipError_t launch_rep(hipStream_t st, const uint8_t* pl, int P, size_t stride, float* out, int64_t n, double scale,
-                      int max_bins) {
-    static bool attr = false;
-    auto* fn = &k_decode_sum_rep<BITS, R>;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)kRepLdsMax);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
-    const int tab = max_bins * R;
-    const size_t lds = sizeof(double) * (size_t)tab * (size_t)P;
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const int64_t groups = n / 16;
-    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((groups + kRepThreads - 1) / kRepThreads, cus));
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(kRepThreads), lds, st, pl, P, stride, out, n, scale, tab);
-    return hipGetLastError();
-}
-
 template <int BITS>
-hipError_t launch_rep_bits(hipStream_t st, const uint8_t* pl, int P, size_t stride, float* out, int64_t n,
-                           double scale, int max_bins) {
-    const size_t per = sizeof(double) * (size_t)max_bins * (size_t)P;
-    if (per * 16 <= kRepLdsMax) return launch_rep<BITS, 16>(st, pl, P, stride, out, n, scale, max_bins);
-    if (per * 8 <= kRepLdsMax) return launch_rep<BITS, 8>(st, pl, P, stride, out, n, scale, max_bins);
-    if (per * 4 <= kRepLdsMax) return launch_rep<BITS, 4>(st, pl, P, stride, out, n, scale, max_bins);
-    return launch_rep<BITS, 2>(st, pl, P, stride, out, n, scale, max_bins);
+hipError_t launch_occ(hipStream_t st, const uint8_t* pl, int P, size_t stride, float* out, int64_t n, double scale,
+                      int max_bins) {
+    const size_t lds = sizeof(double) * (size_t)max_bins * (size_t)P;
+    const int64_t groups = n / kOccPer;
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((groups + 255) / 256, 4096));
+    const bool pf = std::getenv("SKML_DECODE_SUM_NOPF") == nullptr;  // A/B switch
+    if (pf)
+        hipLaunchKernelGGL((k_decode_sum_occ<BITS, true>), dim3(grid), dim3(256), lds, st, pl, P, stride, out, n, scale,
+                           max_bins);
+    else
+        hipLaunchKernelGGL((k_decode_sum_occ<BITS, false>), dim3(grid), dim3(256), lds, st, pl, P, stride, out, n, scale,
+                           max_bins);
+    return hipGetLastError();
 }
 
 hipError_t launch_decode_sum(hipStream_t st, const void* payloads, int P, size_t stride, float* out,
                              int64_t n, double scale, int common_bits, int max_bins) {
     if (n <= 0) return hipSuccess;
     if (P < 1 || P > kMaxSumPayloads) return hipErrorInvalidValue;
-    if (max_bins <= kSumLutBins && std::getenv("SKML_DECODE_SUM_PLAIN") == nullptr) {
+    if (max_bins <= kSumLutBins && P <= kOccMaxP && std::getenv("SKML_DECODE_SUM_PLAIN") == nullptr) {
         const uint8_t* pl = reinterpret_cast<const uint8_t*>(payloads);
         switch (common_bits) {
-            case 8: return launch_rep_bits<8>(st, pl, P, stride, out, n, scale, max_bins);
-            case 4: return launch_rep_bits<4>(st, pl, P, stride, out, n, scale, max_bins);
-            case 2: return launch_rep_bits<2>(st, pl, P, stride, out, n, scale, max_bins);
-            case 1: return launch_rep_bits<1>(st, pl, P, stride, out, n, scale, max_bins);
+            case 8: return launch_occ<8>(st, pl, P, stride, out, n, scale, max_bins);
+            case 4: return launch_occ<4>(st, pl, P, stride, out, n, scale, max_bins);
+            case 2: return launch_occ<2>(st, pl, P, stride, out, n, scale, max_bins);
+            case 1: return launch_occ<1>(st, pl, P, stride, out, n, scale, max_bins);
             default: break;  // mixed widths: the per-payload kernel below
         }
     }

@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "skml_internal.h"
 
 namespace skml {
@@ -24,9 +26,14 @@ __device__ __forceinline__ bool is_nan_bits(uint32_t b) { return (b & 0x7FFFFFFF
 // DPP quad_perm / row_mirror / row_half_mirror / row_ror:8 when the pattern stays inside a
 // 16-lane row, ds_swizzle (bit mode) inside 32 lanes, ds_bpermute otherwise.
 // ------------------------------------------------------------------------------------------
+// SKML_XLANE_SWIZZLE (A/B builds): every exchange inside 32 lanes through ds_swizzle, i.e. the
+// LDS pipe, instead of a DPP move on the VALU (the leaf is VALU-issue bound).
 template <int M>
 __device__ __forceinline__ uint32_t lane_xor(uint32_t v) {
     int x = (int)v;
+#ifdef SKML_XLANE_SWIZZLE
+    if constexpr (M < 32) return (uint32_t)__builtin_amdgcn_ds_swizzle(x, (M << 10) | 0x1F);
+#endif
     if constexpr (M == 1) return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, true);
     else if constexpr (M == 2) return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, true);
     else if constexpr (M == 3) return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0x1B, 0xF, 0xF, true);
@@ -168,6 +175,13 @@ struct OddEvenNet {
         return c;
     }
     static constexpr int kCount = count();
+    // the first n comparators all join registers of one aligned block of 4
+    static constexpr bool first_within_fours(int n) {
+        auto t = table();
+        for (int c = 0; c < n; c++)
+            if (t.a[c] / 4 != t.b[c] / 4) return false;
+        return true;
+    }
     struct Table {
         unsigned char a[kCount], b[kCount];
     };
@@ -187,12 +201,44 @@ struct OddEvenNet {
     }
 };
 
+// A 4-sorter of 8 VALU ops from gfx950's 3-input min / med3 / max (a comparator network needs 5
+// comparators = 10 ops): p = min(a,b), q = max(a,b); the smallest is min3(p,c,d), the largest
+// max3(q,c,d), the second smallest min(med3(p,c,d), q), the second largest max(med3(q,c,d), p).
+// v_min3 / v_med3 / v_max3_f32 order -0.0 before +0.0 like v_min / v_max (tools/ubench/min3_probe.hip
+// checks every operand order and every 4-tuple over {-inf,-2,-1,-0,+0,1,2,+inf}).
+__device__ __forceinline__ void sort4_3in(float& a, float& b, float& c, float& d) {
+    float p, q, lo, hi, m1, m2, o1, o2;
+    asm("v_min_f32 %0, %1, %2" : "=v"(p) : "v"(a), "v"(b));
+    asm("v_max_f32 %0, %1, %2" : "=v"(q) : "v"(a), "v"(b));
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(lo) : "v"(p), "v"(c), "v"(d));
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(hi) : "v"(q), "v"(c), "v"(d));
+    asm("v_med3_f32 %0, %1, %2, %3" : "=v"(m1) : "v"(p), "v"(c), "v"(d));
+    asm("v_med3_f32 %0, %1, %2, %3" : "=v"(m2) : "v"(q), "v"(c), "v"(d));
+    asm("v_min_f32 %0, %1, %2" : "=v"(o1) : "v"(m1), "v"(q));
+    asm("v_max_f32 %0, %1, %2" : "=v"(o2) : "v"(m2), "v"(p));
+    a = lo;
+    b = o1;
+    c = o2;
+    d = hi;
+}
+#ifndef SKML_SORT4_3IN
+#define SKML_SORT4_3IN 1
+#endif
+
 template <int R, typename T>
 __device__ __forceinline__ void sort_regs_oddeven(T (&v)[R]) {
     constexpr int C = OddEvenNet<R>::kCount;
     constexpr auto net = OddEvenNet<R>::table();
+    // Batcher's first two merge levels (5 R / 4 comparators) sort each block of 4 registers
+    constexpr bool k4 = SKML_SORT4_3IN && std::is_same<T, float>::value && R >= 8;
+    constexpr int c0 = k4 ? 5 * (R / 4) : 0;
+    static_assert(!k4 || OddEvenNet<R>::first_within_fours(c0), "network prefix is not the 4-sorters");
+    if constexpr (k4) {
 #pragma unroll
-    for (int c = 0; c < C; c++) {
+        for (int b = 0; b < R / 4; b++) sort4_3in(v[4 * b], v[4 * b + 1], v[4 * b + 2], v[4 * b + 3]);
+    }
+#pragma unroll
+    for (int c = c0; c < C; c++) {
         ce(v[net.a[c]], v[net.b[c]]);
         // 64 keys per lane: keep the scheduler from stretching live ranges past the register budget
         if (R >= 64 && (c & 31) == 31) __builtin_amdgcn_sched_barrier(0);
@@ -248,6 +294,12 @@ __device__ __forceinline__ double med3(double a, double b, double c) {
     return __double_as_longlong(c) > 0 ? hi : lo;
 }
 
+#ifndef SKML_FLIP_GROUP
+#define SKML_FLIP_GROUP 4  // pairs of a flip stage between scheduling barriers
+#endif
+#ifndef SKML_HALF_GROUP
+#define SKML_HALF_GROUP 8  // registers of a cross-lane half-clean stage between scheduling barriers
+#endif
 // Flip stage across a block of (M+1) lanes: element (lane, r) meets (lane^M, R-1-r).
 template <int R, int M, typename T>
 __device__ __forceinline__ void flip_lanes(T (&v)[R], int lane) {
@@ -259,7 +311,7 @@ __device__ __forceinline__ void flip_lanes(T (&v)[R], int lane) {
         v[r] = med3(v[r], pa, sel);
         v[R - 1 - r] = med3(v[R - 1 - r], pb, sel);
         // keep the scheduler from hoisting every exchange of the stage (register pressure)
-        if ((r & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+        if ((r & (SKML_FLIP_GROUP - 1)) == SKML_FLIP_GROUP - 1) __builtin_amdgcn_sched_barrier(0);
     }
 }
 
@@ -269,7 +321,7 @@ __device__ __forceinline__ void halfclean_lanes(T (&v)[R], int lane) {
 #pragma unroll
     for (int r = 0; r < R; r++) {
         v[r] = med3(v[r], lane_xor<D>(v[r]), sel);
-        if ((r & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+        if ((r & (SKML_HALF_GROUP - 1)) == SKML_HALF_GROUP - 1) __builtin_amdgcn_sched_barrier(0);
     }
 }
 

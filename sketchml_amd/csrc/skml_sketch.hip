@@ -568,6 +568,9 @@ constexpr int kL64Rounds = kLeafWaveChunks / kL64Chunks;
 #ifndef SKML_LEAF64_WAVES
 #define SKML_LEAF64_WAVES 4
 #endif
+#ifndef SKML_LEAF_MIN3DET
+#define SKML_LEAF_MIN3DET 1
+#endif
 #ifndef SKML_LEAF_SPLIT_BELOW
 #define SKML_LEAF_SPLIT_BELOW 3072  // full tiles under which k_leaf64<true> runs
 #endif
@@ -624,6 +627,20 @@ __global__ __launch_bounds__(256, SKML_LEAF64_WAVES) void k_leaf64(const float* 
                 float4 f[16];
 #pragma unroll
                 for (int j = 0; j < 16; j++) f[j] = src[j * kL64Lanes + (ln & 3)];
+#if SKML_LEAF_MIN3DET
+                // zero / NaN detector: v_minimum3_f32 over |x| two values per op (NaN propagates,
+                // min |x| is 0 iff a zero is present), two chains, one ballot per round
+                float za = __builtin_inff(), zb = __builtin_inff();
+#pragma unroll
+                for (int j = 0; j < 16; j++) {
+                    asm("v_minimum3_f32 %0, |%1|, |%2|, %3" : "=v"(za) : "v"(f[j].x), "v"(f[j].y), "v"(za));
+                    asm("v_minimum3_f32 %0, |%1|, |%2|, %3" : "=v"(zb) : "v"(f[j].z), "v"(f[j].w), "v"(zb));
+                    v[j * 4 + 0] = f[j].x, v[j * 4 + 1] = f[j].y, v[j * 4 + 2] = f[j].z, v[j * 4 + 3] = f[j].w;
+                }
+                float zm;
+                asm("v_minimum3_f32 %0, %1, %2, %2" : "=v"(zm) : "v"(za), "v"(zb));
+                zmask = __ballot(!(zm > 0.0f));  // -0.0 | +0.0 | NaN somewhere in the lane
+#else
 #pragma unroll
                 for (int j = 0; j < 16; j++) {
                     const float e4[4] = {f[j].x, f[j].y, f[j].z, f[j].w};
@@ -633,6 +650,7 @@ __global__ __launch_bounds__(256, SKML_LEAF64_WAVES) void k_leaf64(const float* 
                         v[j * 4 + e] = e4[e];
                     }
                 }
+#endif
             }
             uint32_t rfl = 0;
             if (zmask) {  // wave-uniform: which zero signs, and NaN

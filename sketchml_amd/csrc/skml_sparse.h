@@ -165,19 +165,22 @@ hipError_t launch_group_prefix(hipStream_t st, const uint32_t* delta, int64_t n,
 // null; gvals (optional) receives quantValues[bin] from qv[nq], a bin outside it sets *err
 hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, const SpGroups* gp, const SpGroups& gh,
                            const uint64_t* tile_base, const uint64_t* gpre, const int32_t* table, const void* tnar,
-                           int width, int32_t* gkeys, int32_t* gbins, const double* qv = nullptr, int nq = 0,
-                           double* gvals = nullptr, unsigned* err = nullptr);
+                           int width, int32_t* gkeys, int32_t* gbins, int nq = 0, void* gbn = nullptr,
+                           int bn_width = 0, unsigned* err = nullptr);
 // the narrow (width 8 or 16) image of int32 MinMax tables for k_dec_keys; t32 16-byte aligned
 hipError_t launch_narrow_table(hipStream_t st, const int32_t* t32, int64_t ncells, int width, void* tn);
 // live entries of a restored payload (skml_sparse_decode_sum_f64's toAuto choice)
-hipError_t launch_count_live(hipStream_t st, const double* vals, int64_t n, uint64_t* count);
+// live entries (|quantValues[bin]| > 1e-8) among n narrow bins (bw = 1 or 2 bytes each)
+hipError_t launch_count_live(hipStream_t st, const void* bins, int bw, int64_t n, const double* qv, uint64_t* count);
 // the tiled Gradient.sum: per-payload run bounds per dense tile, then the tiles built in LDS
 constexpr int kAggTile = 4096;  // dense keys per tile (32 KB of doubles in LDS)
 struct AggPayload {
     const int32_t* gk;      // restored keys, grouped order
-    const double* gv;       // their values, quantValues[bin]
+    const void* gb;         // their bins, bw bytes each (1: bin_num <= 256, else 2)
+    const double* qv;       // quantValues (timesBy applied), nq of them
     const int32_t* bounds;  // [G][ntiles + 1]
     int32_t G, dense_form;
+    int32_t bw, nq;
 };
 static_assert(sizeof(AggPayload) % 8 == 0, "copied as u64 words");
 hipError_t launch_agg_bounds(hipStream_t st, const int32_t* gk, int64_t n, const SpGroups* gp, int64_t ntiles,

@@ -2271,8 +2271,8 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_keys(const uint32_t* __rest
                                                           const uint64_t* __restrict__ gpre,
                                                           const int32_t* __restrict__ table, const TN* __restrict__ tnar,
                                                           int32_t* __restrict__ gkeys, int32_t* __restrict__ gbins,
-                                                          const double* __restrict__ qv, int nq,
-                                                          double* __restrict__ gvals, unsigned* __restrict__ err) {
+                                                          int nq, void* __restrict__ gbn, int bn_width,
+                                                          unsigned* __restrict__ err) {
     __shared__ int64_t S[kMaxGroups + 1];
     __shared__ uint64_t sh[kDecThreads / 64];
     load_starts(gp, S);
@@ -2336,23 +2336,33 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_keys(const uint32_t* __rest
             if ((int32_t)((uint32_t)mm_dist(tv[j], zero) - (uint32_t)mm_dist(res[j], zero)) > 0) res[j] = tv[j];
     }
     const bool full = i0 + 4 <= n;
-    if (gvals) {  // quantValues[bin] (Gradient.sum's restore): a bin outside the values is an error
+    if (gbn) {  // Gradient.sum's restore: narrow bins (the values come from quantValues in LDS later);
+                // a bin outside the values is an error
         bool bad = false;
-        double v[4];
+        uint32_t b[4];
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const bool ok = res[j] >= 0 && res[j] < nq;
             bad |= !ok && i0 + j < n;
-            v[j] = ok ? qv[res[j]] : 0.0;
+            b[j] = ok ? (uint32_t)res[j] : 0u;
         }
         if (bad) atomicOr(err, 1u);
-        if (full && (reinterpret_cast<uintptr_t>(gvals + i0) & 15) == 0) {
-            reinterpret_cast<double2*>(gvals + i0)[0] = make_double2(v[0], v[1]);
-            reinterpret_cast<double2*>(gvals + i0)[1] = make_double2(v[2], v[3]);
-        } else {
+        if (bn_width == 1) {
+            uint8_t* o = static_cast<uint8_t*>(gbn) + i0;
+            if (full && (reinterpret_cast<uintptr_t>(o) & 3) == 0)
+                *reinterpret_cast<uint32_t*>(o) = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
+            else
 #pragma unroll
-            for (int j = 0; j < 4; j++)
-                if (i0 + j < n) gvals[i0 + j] = v[j];
+                for (int j = 0; j < 4; j++)
+                    if (i0 + j < n) o[j] = (uint8_t)b[j];
+        } else {
+            uint16_t* o = static_cast<uint16_t*>(gbn) + i0;
+            if (full && (reinterpret_cast<uintptr_t>(o) & 7) == 0)
+                *reinterpret_cast<uint2*>(o) = make_uint2(b[0] | (b[1] << 16), b[2] | (b[3] << 16));
+            else
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if (i0 + j < n) o[j] = (uint16_t)b[j];
         }
     }
     if (full && (reinterpret_cast<uintptr_t>(gkeys + i0) & 15) == 0) {
@@ -2375,7 +2385,7 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_keys(const uint32_t* __rest
 
 hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, const SpGroups* gp, const SpGroups& gh,
                            const uint64_t* tile_base, const uint64_t* gpre, const int32_t* table, const void* tnar,
-                           int width, int32_t* gkeys, int32_t* gbins, const double* qv, int nq, double* gvals,
+                           int width, int32_t* gkeys, int32_t* gbins, int nq, void* gbn, int bn_width,
                            unsigned* err) {
     if (sp_tiles(n, kSpTile) <= 0) return hipSuccess;
     int64_t per[8] = {};  // tiles per XCD slot (dec_tile_of_block)
@@ -2388,13 +2398,13 @@ hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, con
     const unsigned grid = (unsigned)(8 * most);
     if (width == 8)
         hipLaunchKernelGGL(k_dec_keys<uint8_t>, dim3(grid), dim3(kDecThreads), 0, st, delta, n, gp, tile_base, gpre,
-                           table, static_cast<const uint8_t*>(tnar), gkeys, gbins, qv, nq, gvals, err);
+                           table, static_cast<const uint8_t*>(tnar), gkeys, gbins, nq, gbn, bn_width, err);
     else if (width == 16)
         hipLaunchKernelGGL(k_dec_keys<uint16_t>, dim3(grid), dim3(kDecThreads), 0, st, delta, n, gp, tile_base, gpre,
-                           table, static_cast<const uint16_t*>(tnar), gkeys, gbins, qv, nq, gvals, err);
+                           table, static_cast<const uint16_t*>(tnar), gkeys, gbins, nq, gbn, bn_width, err);
     else
         hipLaunchKernelGGL(k_dec_keys<int32_t>, dim3(grid), dim3(kDecThreads), 0, st, delta, n, gp, tile_base, gpre,
-                           table, static_cast<const int32_t*>(nullptr), gkeys, gbins, qv, nq, gvals, err);
+                           table, static_cast<const int32_t*>(nullptr), gkeys, gbins, nq, gbn, bn_width, err);
     return hipGetLastError();
 }
 
@@ -2458,7 +2468,7 @@ hipError_t launch_agg_bounds(hipStream_t st, const int32_t* gk, int64_t n, const
 // before any add, so a tile waits on a few load latencies instead of three per payload.  The adds
 // then run payload by payload (keys are unique within a payload; one barrier between payloads),
 // which keeps Gradient.sum's order for every key.
-constexpr int kAggPB = 8, kAggE = 8, kAggThreads = 512;
+constexpr int kAggPB = 8, kAggE = 8, kAggThreads = 512, kAggLdsValues = 256;
 __device__ __forceinline__ int agg_search(const int64_t* pre, int n, int64_t j) {  // largest i < n: pre[i] <= j
     int i = 0;
     for (int step = 32; step >= 1; step >>= 1)
@@ -2475,6 +2485,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_tiles(const AggPayload* __r
     __shared__ int64_t poff[kAggPB + 1];             // the batch's payloads concatenated
     __shared__ int32_t dform[kAggPB];
     __shared__ AggPayload pl_s[kAggPB];
+    __shared__ double qt[kAggPB][kAggLdsValues];  // the batch's quantValues (nq <= 256)
     const int64_t t = blockIdx.x;
     const int64_t k0 = t * kAggTile, nk = std::min<int64_t>(kAggTile, dim - k0);
     for (int x = threadIdx.x; x < kAggTile; x += kAggThreads) acc[x] = (from_out && x < nk) ? out[k0 + x] : 0.0;
@@ -2484,6 +2495,11 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_tiles(const AggPayload* __r
         __syncthreads();  // the previous batch is done with pre / base / poff / pl_s
         if (threadIdx.x < np * (int)(sizeof(AggPayload) / 8))
             reinterpret_cast<uint64_t*>(pl_s)[threadIdx.x] = reinterpret_cast<const uint64_t*>(pays + p0)[threadIdx.x];
+        for (int x = threadIdx.x; x < np * kAggLdsValues; x += kAggThreads) {
+            const AggPayload& a = pays[p0 + x / kAggLdsValues];
+            const int b = x % kAggLdsValues;
+            if (a.nq <= kAggLdsValues && b < a.nq) qt[x / kAggLdsValues][b] = a.qv[b];
+        }
         for (int pl = threadIdx.x >> 6; pl < np; pl += kAggThreads / 64) {  // a wave per payload, a lane per group
             const int g = threadIdx.x & 63;
             const AggPayload& a = pays[p0 + pl];
@@ -2530,8 +2546,10 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_tiles(const AggPayload* __r
                     const int64_t jl = j - poff[pl];
                     const int g = agg_search(pre[pl], kMaxGroups, jl);
                     const int64_t i = base[pl][g] + (jl - pre[pl][g]);
-                    kk[u] = pl_s[pl].gk[i];
-                    vv[u] = pl_s[pl].gv[i];
+                    const AggPayload& a = pl_s[pl];
+                    kk[u] = a.gk[i];
+                    const uint32_t b = a.bw == 1 ? static_cast<const uint8_t*>(a.gb)[i] : static_cast<const uint16_t*>(a.gb)[i];
+                    vv[u] = a.nq <= kAggLdsValues ? qt[pl][b] : a.qv[b];
                     pe[u] = (int8_t)pl;
                 }
             }
@@ -2573,21 +2591,27 @@ hipError_t launch_agg_tiles(hipStream_t st, const AggPayload* pays, int P, int64
 }
 
 // live entries (|quantValues[bin]| > 1e-8) of a restored payload, for toAuto's dense / sparse choice
-__global__ __launch_bounds__(kSpThreads) void k_count_live(const double* __restrict__ vals, int64_t n,
+template <typename B>
+__global__ __launch_bounds__(kSpThreads) void k_count_live(const B* __restrict__ bins, int64_t n,
+                                                           const double* __restrict__ qv,
                                                            unsigned long long* __restrict__ count) {
     uint64_t c = 0;
     for (int64_t i = (int64_t)blockIdx.x * kSpThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kSpThreads)
-        c += fabs(vals[i]) > 1e-8 ? 1u : 0u;
+        c += fabs(qv[bins[i]]) > 1e-8 ? 1u : 0u;
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) c += __shfl_xor(c, off, 64);
     if ((threadIdx.x & 63) == 0 && c) atomicAdd(count, (unsigned long long)c);
 }
-hipError_t launch_count_live(hipStream_t st, const double* vals, int64_t n, uint64_t* count) {
+hipError_t launch_count_live(hipStream_t st, const void* bins, int bw, int64_t n, const double* qv, uint64_t* count) {
     hipError_t e = hipMemsetAsync(count, 0, sizeof(uint64_t), st);
     if (e != hipSuccess || n <= 0) return e;
     const int64_t grid = std::min<int64_t>(sp_tiles(n, kSpThreads * 8), 4096);
-    hipLaunchKernelGGL(k_count_live, dim3((unsigned)grid), dim3(kSpThreads), 0, st, vals, n,
-                       reinterpret_cast<unsigned long long*>(count));
+    if (bw == 1)
+        hipLaunchKernelGGL(k_count_live<uint8_t>, dim3((unsigned)grid), dim3(kSpThreads), 0, st,
+                           static_cast<const uint8_t*>(bins), n, qv, reinterpret_cast<unsigned long long*>(count));
+    else
+        hipLaunchKernelGGL(k_count_live<uint16_t>, dim3((unsigned)grid), dim3(kSpThreads), 0, st,
+                           static_cast<const uint16_t*>(bins), n, qv, reinterpret_cast<unsigned long long*>(count));
     return hipGetLastError();
 }
 

@@ -37,11 +37,14 @@ class Quantizer:
         """deferred=True: quantize() only queues the encode on the stream and returns (no host
         synchronisation); the header is read, and a NaN input raises QuantileSketchException, at
         the first getter (getBins, getSplits, writeObject, ...) or at the next quantize(),
-        whichever comes first.  The next quantize() reads the previous header first (one
-        synchronisation) because QuantileQuantizer.java:42 carries the binNum that Maths.unique
-        reduced into the next encode.  Every encode gets a payload buffer of its own, so a
-        `payload` reference taken earlier keeps its bytes.  The default keeps the reference's
-        eager behaviour."""
+        whichever comes first.  The next quantize() of a QuantileQuantizer reads the previous
+        header first (one host synchronisation per call) because QuantileQuantizer.java:42 carries
+        the binNum that Maths.unique reduced into the next encode; back-to-back deferred quantile
+        encodes therefore synchronise once per call, and only the first encode of a series runs
+        with no synchronisation at all.  The UniformQuantizer never lowers binNum (no Maths.unique,
+        UniformQuantizer.java:21-45), so its deferred encodes skip that read and never
+        synchronise.  Every encode gets a payload buffer of its own, so a `payload` reference
+        taken earlier keeps its bytes.  The default keeps the reference's eager behaviour."""
         self.binNum = int(binNum)
         self.seed = int(seed)
         self._deferred = bool(deferred)
@@ -93,7 +96,7 @@ class Quantizer:
               (True, False): "skml_dense_encode_uniform_f32", (True, True): "skml_dense_encode_uniform_f64"}
 
     def _encode(self, values, dedup: bool, uniform: bool = False, threads: int = 1):
-        if self._deferred and self.payload is not None and self._hdr is None:
+        if self._deferred and self.payload is not None and self._hdr is None and not uniform:
             try:
                 self._load_header()  # the previous encode's effective binNum (and its NaN status)
             except QuantileSketchException:

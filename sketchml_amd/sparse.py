@@ -126,7 +126,10 @@ class SparsePayload:
         """GroupedMinMaxSketch.readObject of the stream serialize() writes; quant_values (the
         SparseVectorCompressor.quantValues doubles) make restore() return values as well."""
         dev = torch.cuda.current_device() if device is None else torch.device(device).index
-        arr = np.frombuffer(data, dtype=np.uint8)  # read only: the C call takes a const stream
+        try:
+            arr = np.frombuffer(data, dtype=np.uint8)  # zero copy for buffer objects (read only: a const stream)
+        except TypeError:
+            arr = np.frombuffer(bytes(data), dtype=np.uint8)  # any iterable of ints, as bytes() accepts
         qv = None if quant_values is None else np.ascontiguousarray(quant_values, dtype=np.float64)
         h = C.c_void_p()
         check(_lib.lib.skml_sparse_deserialize(

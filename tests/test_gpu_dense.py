@@ -375,18 +375,26 @@ def test_decode_sum(gpu):
     assert np.array_equal(out.cpu().numpy(), (want * (1.0 / P)).astype(np.float32))
 
 
-# (P, requested bins per payload, n), with the oracle's effective bin counts: 8-bit codes at R = 16
-# (8 x 136), R = 8 (8 x up to 221) and R = 4 (16 x up to 235; R = 2 is never needed at P <= 16);
-# 4-, 2- and 1-bit codes; a mixed-width set (the per-payload kernel); n = 15 (tail only).
+# (P, requested bins per payload, n), with the oracle's effective bin counts: 8-bit codes (8 x 136,
+# 8 x up to 221, and 16 x up to 235, which takes the per-payload kernel); 4-, 2- and 1-bit codes;
+# a mixed-width set (the per-payload kernel); n = 15 (tail only).
 @pytest.mark.parametrize("P,bins,n", [(8, [256] * 8, 2**20 + 13), (8, [256] * 8, 40005),
                                       (16, [512] * 16, 40000 + 5), (5, [16] * 5, 2**18 + 7), (4, [4] * 4, 99999),
                                       (3, [2] * 3, 4097), (6, [256, 16, 4, 2, 256, 16], 50001), (1, [256], 15)])
-def test_decode_sum_replicated_tables(gpu, P, bins, n):
-    """k_decode_sum_rep (bank-replicated LUTs; R chosen from P and the largest bin count) and the
-    per-payload kernel for mixed widths: bit-exact against the oracle's decodes summed in double
+@pytest.mark.parametrize("kernel", ["occ", "occ_nopf", "plain"])
+def test_decode_sum_replicated_tables(gpu, P, bins, n, kernel, monkeypatch):
+    """k_decode_sum_occ (8 elements per lane, P <= 8 tables of the largest bin count in LDS; with
+    and without the next step's code prefetch) and the per-payload kernel (P > 8, mixed widths,
+    > 256 bins): bit-exact against the oracle's decodes summed in double
     in payload order, then x 1/P (Gradient.sum + timesBy, ml/gradient/Gradient.scala:44-49).
-    Requested bins 512 with Maths.unique give effective counts up to 256 (8-bit codes)."""
+    Requested bins 512 with Maths.unique give effective counts up to 256 (8-bit codes).
+    kernel "plain": SKML_DECODE_SUM_PLAIN=1 selects the one-table-per-payload kernel (its
+    software-pipelined form when the width is common and P <= 8)."""
     from sketchml_amd import _lib
+    if kernel == "plain":
+        monkeypatch.setenv("SKML_DECODE_SUM_PLAIN", "1")
+    elif kernel == "occ_nopf":
+        monkeypatch.setenv("SKML_DECODE_SUM_NOPF", "1")
     ctx = gpu.get_context()
     nb = max(_lib.lib.skml_dense_payload_bytes(n, b) for b in bins)
     nb = (nb + 255) // 256 * 256
