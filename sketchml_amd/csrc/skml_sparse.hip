@@ -2272,7 +2272,7 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_keys(const uint32_t* __rest
                                                           const int32_t* __restrict__ table, const TN* __restrict__ tnar,
                                                           int32_t* __restrict__ gkeys, int32_t* __restrict__ gbins,
                                                           int nq, void* __restrict__ gbn, int bn_width,
-                                                          unsigned* __restrict__ err) {
+                                                          unsigned* __restrict__ err, int batch_rows) {
     __shared__ int64_t S[kMaxGroups + 1];
     __shared__ uint64_t sh[kDecThreads / 64];
     load_starts(gp, S);
@@ -2313,27 +2313,62 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_keys(const uint32_t* __rest
         res[j] = zero;
     }
     constexpr uint32_t kTop = sizeof(TN) == 4 ? 0u : (uint32_t)(TN)~(TN)0;
-    for (int r = 0; r < rows; r++) {
-        int64_t idx[4];
-        int32_t tv[4];
+    auto cell_of = [&](int j, int r) -> int64_t {
+        const int gj = grp[j];
+        const int32_t cols = gp->cols[gj];
+        return i0 + j < n ? gp->tab_off[gj] + (int64_t)r * cols +
+                                java_hash_fm(gp->hash_ids[gj][r], key[j], cols, gp->inv_cols[gj])
+                          : -1;
+    };
+    auto gather = [&](int64_t idx) -> int32_t {
+        if constexpr (sizeof(TN) == 4) return idx >= 0 ? table[idx] : zero;
+        else return idx >= 0 ? (int32_t)tnar[idx] : zero;
+    };
+    // MinMaxSketch.query: the strictly farther value wins, ties keep the earlier row
+    auto take = [&](int j, int32_t tv) {
+        if ((int32_t)((uint32_t)mm_dist(tv, zero) - (uint32_t)mm_dist(res[j], zero)) > 0) res[j] = tv;
+    };
+    if (rows == 2 && batch_rows) {
+        // the default shape: both rows' 8 cells hashed first, then all 8 gathers in flight at once
+        // (the query is bound by the gathers' L2 latency, not by the hash arithmetic)
+        int64_t idx[2][4];
+        int32_t tv[2][4];
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int gj = grp[j];
-            const int32_t cols = gp->cols[gj];
-            idx[j] = i0 + j < n ? gp->tab_off[gj] + (int64_t)r * cols +
-                                      java_hash_fm(gp->hash_ids[gj][r], key[j], cols, gp->inv_cols[gj])
-                                : -1;
-            if constexpr (sizeof(TN) == 4) tv[j] = idx[j] >= 0 ? table[idx[j]] : zero;
-            else tv[j] = idx[j] >= 0 ? (int32_t)tnar[idx[j]] : zero;
-        }
+        for (int r = 0; r < 2; r++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) idx[r][j] = cell_of(j, r);
+#pragma unroll
+        for (int r = 0; r < 2; r++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) tv[r][j] = gather(idx[r][j]);
         if constexpr (sizeof(TN) < 4) {
 #pragma unroll
-            for (int j = 0; j < 4; j++)  // the sentinel: the cell's int32 value
-                if (idx[j] >= 0 && (uint32_t)tv[j] == kTop) tv[j] = table[idx[j]];
+            for (int r = 0; r < 2; r++)
+#pragma unroll
+                for (int j = 0; j < 4; j++)  // the sentinel: the cell's int32 value
+                    if (idx[r][j] >= 0 && (uint32_t)tv[r][j] == kTop) tv[r][j] = table[idx[r][j]];
         }
 #pragma unroll
-        for (int j = 0; j < 4; j++)  // MinMaxSketch.query: the strictly farther value wins, ties keep the earlier row
-            if ((int32_t)((uint32_t)mm_dist(tv[j], zero) - (uint32_t)mm_dist(res[j], zero)) > 0) res[j] = tv[j];
+        for (int r = 0; r < 2; r++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) take(j, tv[r][j]);
+    } else {
+        for (int r = 0; r < rows; r++) {
+            int64_t idx[4];
+            int32_t tv[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                idx[j] = cell_of(j, r);
+                tv[j] = gather(idx[j]);
+            }
+            if constexpr (sizeof(TN) < 4) {
+#pragma unroll
+                for (int j = 0; j < 4; j++)  // the sentinel: the cell's int32 value
+                    if (idx[j] >= 0 && (uint32_t)tv[j] == kTop) tv[j] = table[idx[j]];
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) take(j, tv[j]);
+        }
     }
     const bool full = i0 + 4 <= n;
     if (gbn) {  // Gradient.sum's restore: narrow bins (the values come from quantValues in LDS later);
@@ -2396,15 +2431,16 @@ hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, con
     int64_t most = 0;
     for (int x = 0; x < 8; x++) most = std::max(most, per[x]);
     const unsigned grid = (unsigned)(8 * most);
+    const int batch_rows = std::getenv("SKML_DEC_ROWS_SERIAL") == nullptr ? 1 : 0;  // A/B switch
     if (width == 8)
         hipLaunchKernelGGL(k_dec_keys<uint8_t>, dim3(grid), dim3(kDecThreads), 0, st, delta, n, gp, tile_base, gpre,
-                           table, static_cast<const uint8_t*>(tnar), gkeys, gbins, nq, gbn, bn_width, err);
+                           table, static_cast<const uint8_t*>(tnar), gkeys, gbins, nq, gbn, bn_width, err, batch_rows);
     else if (width == 16)
         hipLaunchKernelGGL(k_dec_keys<uint16_t>, dim3(grid), dim3(kDecThreads), 0, st, delta, n, gp, tile_base, gpre,
-                           table, static_cast<const uint16_t*>(tnar), gkeys, gbins, nq, gbn, bn_width, err);
+                           table, static_cast<const uint16_t*>(tnar), gkeys, gbins, nq, gbn, bn_width, err, batch_rows);
     else
         hipLaunchKernelGGL(k_dec_keys<int32_t>, dim3(grid), dim3(kDecThreads), 0, st, delta, n, gp, tile_base, gpre,
-                           table, static_cast<const int32_t*>(nullptr), gkeys, gbins, nq, gbn, bn_width, err);
+                           table, static_cast<const int32_t*>(nullptr), gkeys, gbins, nq, gbn, bn_width, err, batch_rows);
     return hipGetLastError();
 }
 
@@ -2445,6 +2481,9 @@ __global__ __launch_bounds__(kSpThreads) void k_agg_bounds(const int32_t* __rest
             while (i >= S[g + 1]) g++;
             const int64_t lo = S[g], hi = S[g + 1];
             if (key[e] < 0 || (int64_t)key[e] >= dim) atomicOr(err, 1u);  // SparseDoubleGradient's bound check
+            // keys ascend strictly inside a group (the tiles add without atomics; a repeated key would
+            // race), as SparseDoubleGradient's constructor requires of the merged indices
+            if (i > lo && key[e] <= prev) atomicOr(err, 1u);
             const int64_t ti = tile_of(key[e]);
             const int64_t pt = i > lo ? tile_of(prev) : -1;
             int32_t* b = bounds + (int64_t)g * ld;

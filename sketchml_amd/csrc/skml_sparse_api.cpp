@@ -583,12 +583,12 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const void* vals, bool f64, int6
 }
 
 // DeltaAdaptive decode of all groups + MinMax query: grouped keys/bins into gk/gb.
-// DecodeValues: restore quantValues[bin] (qv on the device, nq of them) into gv instead of / beside
-// the bins (Gradient.sum's restore); a bin outside qv sets *err.
+// DecodeValues: Gradient.sum's restore writes narrow bins (bw bytes: 1 for bin_num <= 256, else 2)
+// into gb for the tiled sum, which looks quantValues up itself; a bin outside the nq values sets *err.
 struct DecodeValues {
-    const double* qv;
     int nq;
-    double* gv;
+    void* gb;
+    int bw;
     unsigned* err;
 };
 int decode_groups(skml_ctx* c, const skml_sparse* s, int32_t* gk, int32_t* gb, bool query,
@@ -630,8 +630,8 @@ int decode_groups(skml_ctx* c, const skml_sparse* s, int32_t* gk, int32_t* gb, b
         if (!tnar) return sfail(SKML_E_OOM, "decode scratch (table image)");
         SP_HIP(launch_narrow_table(st, tab, s->ncells, width, tnar));
     }
-    SP_HIP(launch_dec_keys(st, delta, n, s->g_dev, G, ts2, gpre, tab, tnar, width, gk, gb, dv ? dv->qv : nullptr,
-                           dv ? dv->nq : 0, dv ? dv->gv : nullptr, dv ? dv->err : nullptr));
+    SP_HIP(launch_dec_keys(st, delta, n, s->g_dev, G, ts2, gpre, tab, tnar, width, gk, gb, dv ? dv->nq : 0,
+                           dv ? dv->gb : nullptr, dv ? dv->bw : 0, dv ? dv->err : nullptr));
     return SKML_OK;
 }
 
@@ -1828,7 +1828,7 @@ int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t
     // batch starts the sum at +0.0, later ones continue from it, the last one applies the scale
     constexpr size_t kBudget = (size_t)3 << 30;
     auto need_of = [&](int p) {
-        return (size_t)views[(size_t)p].nnz * 12 + (size_t)views[(size_t)p].g.G * (size_t)(ntiles + 1) * 4 + 1024;
+        return (size_t)views[(size_t)p].nnz * 6 + (size_t)views[(size_t)p].g.G * (size_t)(ntiles + 1) * 4 + 1024;
     };
     std::vector<int> todo;
     for (int p = 0; p < P; p++)
@@ -1855,9 +1855,9 @@ int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t
             nb += (int64_t)views[(size_t)todo[q]].g.G * (ntiles + 1);
         }
         int32_t* gk = scratch<int32_t>(c, kSlotCKeys, (size_t)nk);
-        double* gv = scratch<double>(c, kSlotCVals, (size_t)nk);
+        uint16_t* gbn = scratch<uint16_t>(c, kSlotCVals, (size_t)nk);  // 1 or 2 bytes per bin, 16-byte aligned runs
         int32_t* bounds = scratch<int32_t>(c, kSlotCells, (size_t)nb);
-        if (!gk || !gv || !bounds) return sfail(SKML_E_OOM, "decode_sum scratch (%lld keys)", (long long)nk);
+        if (!gk || !gbn || !bounds) return sfail(SKML_E_OOM, "decode_sum scratch (%lld keys)", (long long)nk);
         SP_HIP(hipMemsetAsync(bounds, 0, sizeof(int32_t) * (size_t)nb, st));  // empty groups: every bound 0
         std::vector<AggPayload> pays;
         int64_t ko = 0, bo = 0;
@@ -1866,15 +1866,18 @@ int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t
             const skml_sparse& v = views[(size_t)p];
             AggPayload a{};
             a.gk = gk + ko;
-            a.gv = gv + ko;
+            a.nq = (int)v.qvalues.size();
+            a.bw = a.nq <= 256 ? 1 : 2;
+            a.gb = a.bw == 1 ? static_cast<const void*>(reinterpret_cast<uint8_t*>(gbn) + ko)
+                             : static_cast<const void*>(gbn + ko);
+            a.qv = reinterpret_cast<const double*>(static_cast<const uint8_t*>(blobs) + (size_t)p * stride +
+                                                   hs[(size_t)p].off_values);
             a.bounds = bounds + bo;
             a.G = v.g.G;
-            const DecodeValues dv{reinterpret_cast<const double*>(static_cast<const uint8_t*>(blobs) + (size_t)p * stride +
-                                                                  hs[(size_t)p].off_values),
-                                  (int)v.qvalues.size(), gv + ko, err};
+            const DecodeValues dv{a.nq, const_cast<void*>(a.gb), a.bw, err};
             if (int e = decode_groups(c, &v, gk + ko, nullptr, true, &dv)) return e;
             if (v.nnz > lim) {  // live <= nnz: only then can toAuto pick the dense form
-                SP_HIP(launch_count_live(st, a.gv, v.nnz, live));
+                SP_HIP(launch_count_live(st, a.gb, a.bw, v.nnz, a.qv, live));
                 uint64_t nlive = 0;
                 if (int e = sync_to_host(c, &nlive, live, sizeof(nlive))) return e;
                 a.dense_form = (int64_t)nlive > lim ? 1 : 0;

@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--aggregate", type=int, default=0,
                     help="also time Gradient.sum of this many payloads (skml_sparse_decode_sum_f64)")
+    ap.add_argument("--only-e2e", action="store_true",
+                    help="one warm-up and `reps` timed dense -> payload encodes only (the PMC passes' program)")
     a = ap.parse_args()
     import sketchml_amd as sk
     dev = torch.device("cuda", 0)
@@ -46,6 +48,10 @@ def main():
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / reps, out
 
+    if a.only_e2e:
+        t_e2e, _ = timed(lambda: sk.encode_dense_as_sparse(x, 256, 8, 2, 0.3, 3, 3), a.reps)
+        print(json.dumps({"dense_to_payload_ms": round(t_e2e * 1e3, 3)}))
+        return
     t_compact, (keys, vals) = timed(lambda: sk.to_sparse(x), a.reps)
     nnz = keys.numel()
     t_encode, pl = timed(lambda: sk.encode_sparse(keys, vals, 256, 8, 2, 0.3, 3, 3), a.reps)

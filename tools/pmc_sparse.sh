@@ -1,7 +1,15 @@
-# rocprofv3 PMC passes over the C3 sparse bench (GPU box): HBM bytes, L2 write requests, SQ instruction mix
+#!/bin/bash
+# rocprofv3 FETCH_SIZE / WRITE_SIZE passes (separate runs) over one C3 sparse encode (GPU box), folded
+# per kernel by tools/pmc_sparse_summary.py into gpurun_out/pmc_sp_TAG/sparse_pmc.json: HBM bytes per
+# launch of every kernel of dense -> payload, their sum and its ratio to the 6.2 B/element
+# algorithmic bytes of SURVEY §8(d).  usage (through gpurun): bash tools/pmc_sparse.sh TAG
 set -e
+TAG=${1:-cur}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-mkdir -p gpurun_out/pmc_sp
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex 'k_(compact|part|group_prep|mm_|delta)' -d gpurun_out/pmc_sp/fetch -o run --output-format csv -- python3 tools/bench_sparse.py --reps 1 > /dev/null
-timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE TCC_EA0_WRREQ_64B --kernel-include-regex 'k_(compact|part|group_prep|mm_|delta)' -d gpurun_out/pmc_sp/write -o run --output-format csv -- python3 tools/bench_sparse.py --reps 1 > /dev/null
-timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_SALU --kernel-include-regex 'k_(compact|part|group_prep|mm_|delta)' -d gpurun_out/pmc_sp/sq -o run --output-format csv -- python3 tools/bench_sparse.py --reps 1 > /dev/null
+OUT=gpurun_out/pmc_sp_$TAG
+mkdir -p $OUT
+timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/fetch -o run --output-format csv -- python3 tools/bench_sparse.py --reps 1 --only-e2e > $OUT/fetch.log 2>&1
+timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/write -o run --output-format csv -- python3 tools/bench_sparse.py --reps 1 --only-e2e > $OUT/write.log 2>&1
+python3 tools/pmc_sparse_summary.py --fetch $OUT/fetch --write $OUT/write --out $OUT/sparse_pmc.json
+find "$OUT" -name "*counter_collection.csv" -size +20M -delete
+find "$OUT" -name "*kernel_trace.csv" -size +20M -delete
