@@ -117,6 +117,12 @@ int skml_debug_leaf_stage(skml_ctx* ctx, const float* x_dev, int64_t n, int stag
  * the fallback path (key-carrying pairs, rehashing scatter) is exercised.  Not part of the codec. */
 int skml_debug_sparse_scratch_fail(int on);
 
+/* Test hook: how the calling thread's last restore / decode merged the groups' runs (Sort.merge):
+ * 0 none (fewer than two groups or no keys), 1 the one-pass key-range merge, 2 the pairwise merge
+ * rounds (forced by SKML_RS_ROUNDS), 3 the one-pass merge found the input irregular (a run that
+ * does not ascend, a repeated key, a key outside [0, INT32_MAX)) and the rounds ran instead. */
+int skml_debug_sparse_merge_path(void);
+
 /* ---- Dense path: QuantileQuantizer.quantize + Quantizer.getBins/getValues ---- */
 
 /* Bytes of a device payload able to hold n codes for `bin_num` requested bins. */

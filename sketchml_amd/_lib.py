@@ -74,6 +74,7 @@ _SIGS = {
     "skml_ctx_reset_stats": (C.c_int, [vp]),
     "skml_debug_leaf_stage": (C.c_int, [vp, vp, i64, C.c_int, C.c_int, C.POINTER(C.c_double)]),
     "skml_debug_sparse_scratch_fail": (C.c_int, [C.c_int]),
+    "skml_debug_sparse_merge_path": (C.c_int, []),
     "skml_dense_payload_bytes": (C.c_size_t, [i64, i32]),
     "skml_dense_encode_f32": (C.c_int, [vp, vp, i64, C.POINTER(Params), vp, C.c_size_t]),
     "skml_dense_encode_with_splits_f32": (C.c_int, [vp, vp, i64, dblp, i32, C.c_double, C.c_double,

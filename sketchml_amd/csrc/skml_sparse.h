@@ -159,14 +159,31 @@ hipError_t launch_dec_deltas(hipStream_t st, const uint64_t* delta_words, int64_
                              const uint64_t* tile_base, uint32_t* delta, uint64_t* tile_sums);
 hipError_t launch_group_prefix(hipStream_t st, const uint32_t* delta, int64_t n, const SpGroups* gp, int G,
                                const uint64_t* tile_base, uint64_t* gpre);
+// The stream passes without materialised lengths / deltas: pass 0 writes each kSpTile tile's sum of
+// delta bit lengths into bit_sums; pass 1 (bit_sums scanned) writes the tiles' delta sums into
+// delta_sums and every group's in-tile delta prefix at its first element into gpart[G].
+hipError_t launch_dec_sums(hipStream_t st, const uint64_t* flag_words, int64_t n_flag_words, const int64_t* end_pos,
+                           const uint64_t* delta_words, int64_t n_delta_words, int64_t n, const SpGroups* gp,
+                           uint64_t* bit_sums, int pass, uint64_t* delta_sums, uint64_t* gpart);
+// k_dec_keys's source of deltas when dw != nullptr: recomputed from the streams (bit_base = the
+// scanned bit_sums, gpart from launch_dec_sums pass 1; `delta` and `gpre` are then unused)
+struct DecStreams {
+    const uint64_t* fw = nullptr;
+    int64_t nfw = 0;
+    const int64_t* end_pos = nullptr;
+    const uint64_t* dw = nullptr;
+    int64_t ndw = 0;
+    const uint64_t* bit_base = nullptr;
+    const uint64_t* gpart = nullptr;
+};
 // keys and MinMax bins; gh: the host copy of *gp (the grid follows the group sizes).  width 8 / 16:
 // tnar is launch_narrow_table's image of `table` (int32 cells outside [0, 2^width - 1) read back
 // from `table`); width 32: `table` alone (nullptr with gp->rows == 0: keys only).  gbins may be
 // null; gvals (optional) receives quantValues[bin] from qv[nq], a bin outside it sets *err
 hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, const SpGroups* gp, const SpGroups& gh,
                            const uint64_t* tile_base, const uint64_t* gpre, const int32_t* table, const void* tnar,
-                           int width, int32_t* gkeys, int32_t* gbins, int nq = 0, void* gbn = nullptr,
-                           int bn_width = 0, unsigned* err = nullptr);
+                           int width, int32_t* gkeys, int32_t* gbins, int nq, void* gbn, int bn_width,
+                           unsigned* err, const DecStreams& ds);
 // the narrow (width 8 or 16) image of int32 MinMax tables for k_dec_keys; t32 16-byte aligned
 hipError_t launch_narrow_table(hipStream_t st, const int32_t* t32, int64_t ncells, int width, void* tn);
 // live entries of a restored payload (skml_sparse_decode_sum_f64's toAuto choice)
@@ -210,6 +227,20 @@ static_assert(sizeof(SpBlobHeader) <= 256, "blob header fits its 256-byte sectio
 // run_start: nruns + 1 device offsets; total = run_start[nruns].
 // run_start: nruns + 1 HOST offsets (passed to the kernels by value); split: (total / 2048 + 2)
 // int64 device scratch (the tile boundaries' merge-path split points)
+// Sort.merge in one pass (the regular case: runs ascend strictly, keys distinct and in [0, INT32_MAX)):
+// bounds = G x (kRsRanges + 1) int32 scratch; info->irregular != 0 after the launches means the
+// input was not regular and the caller must run the merge rounds instead.  vkind 0: out = int32
+// bins; 1: float quantValues[bin]; 2: double quantValues[bin] (qv: nq doubles).
+constexpr int kRsBits = 16, kRsRange = 1 << kRsBits, kRsWords = kRsRange / 32;
+constexpr int64_t kRsRanges = (int64_t)1 << (31 - kRsBits);  // key ranges of [0, 2^31)
+struct RsInfo {
+    unsigned irregular;          // 1: a run does not ascend / key out of range, 2: a repeated key or bad bin
+    int32_t tmax1;               // 1 + the last key range holding a key
+    int32_t tlast1[kMaxGroups];  // 1 + run g's last key range (0: empty run)
+};
+hipError_t launch_rs_merge(hipStream_t st, const int32_t* gk, const int32_t* gb, int64_t n, const SpGroups* gp,
+                           int32_t* bounds, RsInfo* info, int32_t* keys_out, void* out, int vkind, const double* qv,
+                           int nq);
 hipError_t launch_merge_round(hipStream_t st, const int32_t* kin, const int32_t* bin_in, int32_t* kout,
                               int32_t* bout, const int64_t* run_start, int nruns, int64_t total, int64_t* split);
 // values[bins[i]] from the double quantValues LUT (SparseVectorCompressor.java:118-126).

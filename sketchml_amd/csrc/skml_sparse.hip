@@ -15,6 +15,7 @@
 //                    resolved by selecting zero bits, delta offsets and keys by scans.
 //   k_merge_round    Sort.merge (util/Sort.java:362-379) as rounds of stable merge-path merges.
 #include <algorithm>
+#include <type_traits>
 
 #include "skml_device.hpp"
 #include "skml_sparse.h"
@@ -192,6 +193,17 @@ __device__ __forceinline__ int32_t java_hash_fm(int id, int32_t key, int32_t siz
     if (m < 0) m += size;
     else if (m >= size) m -= size;
     return (int32_t)m;
+}
+
+// 4 elements' cells of one MinMax row with the hash fixed at compile time, as 32-bit offsets
+// (row0: the row's first cell, relative): for a k_dec_keys tile inside one group, whose lanes all
+// use the same hash id, java_hash_mix folds to the one hash instead of computing every variant.
+template <int ID>
+__device__ __forceinline__ void dec_row_cells(const int32_t (&key)[4], int64_t i0, int64_t n, int64_t row0,
+                                              int32_t cols, double inv, uint32_t (&rel)[4]) {
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+        rel[j] = i0 + j < n ? (uint32_t)(row0 + java_hash_fm(ID, key[j], cols, inv)) : ~0u;
 }
 
 // |v - zero| with Java int wrap (MinMaxSketch.compare, MinMaxSketch.java:80-86)
@@ -2188,6 +2200,118 @@ hipError_t launch_dec_deltas(hipStream_t st, const uint64_t* delta_words, int64_
     return hipGetLastError();
 }
 
+// ---- the same stream passes without materialised lengths / deltas (the default) ----
+// k_dec_lsum: per 2,048-element tile, the sum of the delta bit lengths (reads the flag stream
+// only); k_dec_dsum: per tile, the deltas' sum and each group's in-tile delta prefix at its first
+// element (bit offsets from the scanned length sums); k_dec_keys then recomputes the lengths and
+// deltas of its own elements from the streams.  Neither the 1-byte lengths nor the 4-byte deltas
+// go through memory, and k_dec_lens / k_dec_deltas / k_group_prefix do not run.
+__device__ __forceinline__ int dec_len_of(const uint64_t* __restrict__ fw, int64_t nfw,
+                                          const int64_t* __restrict__ end_pos, const SpGroups* __restrict__ gp,
+                                          const DeltaShape& s, int g, int64_t i, int64_t sg) {
+    int iv;
+    if (!s.kind) {
+        iv = (int)get_bits(fw, nfw, gp->fb[g] + (i - sg) * s.nf, s.nf) + 1;
+    } else {
+        const int64_t start = i == sg ? gp->fb[g] : end_pos[i - 1] + 1;
+        iv = (int)(end_pos[i] - start);
+    }
+    return s.bpi * iv;
+}
+
+__global__ __launch_bounds__(kSpThreads) void k_dec_lsum(const uint64_t* __restrict__ fw, int64_t nfw,
+                                                         const int64_t* __restrict__ end_pos, int64_t n,
+                                                         const SpGroups* __restrict__ gp,
+                                                         uint64_t* __restrict__ tile_sums) {
+    __shared__ int64_t S[kMaxGroups + 1];
+    __shared__ uint64_t sh[4];
+    load_starts(gp, S);
+    __syncthreads();
+    const int64_t i0 = (int64_t)blockIdx.x * kSpTile + threadIdx.x * 8;
+    uint64_t sum = 0;
+    if (i0 < n) {
+        int g = group_of_elem(S, i0);
+        DeltaShape s = delta_shape(gp, g);
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int64_t i = i0 + j;
+            if (i >= n) break;
+            while (i >= S[g + 1]) s = delta_shape(gp, ++g);
+            sum += (uint64_t)dec_len_of(fw, nfw, end_pos, gp, s, g, i, S[g]);
+        }
+    }
+    uint64_t v[1] = {sum}, tot[1];
+    block_excl_scan<1>(v, tot, sh);
+    if (threadIdx.x == 0) tile_sums[blockIdx.x] = tot[0];
+}
+
+__global__ __launch_bounds__(kSpThreads) void k_dec_dsum(const uint64_t* __restrict__ fw, int64_t nfw,
+                                                         const int64_t* __restrict__ end_pos,
+                                                         const uint64_t* __restrict__ dw, int64_t ndw, int64_t n,
+                                                         const SpGroups* __restrict__ gp,
+                                                         const uint64_t* __restrict__ bit_base,
+                                                         uint64_t* __restrict__ tile_sums, uint64_t* __restrict__ gpart) {
+    __shared__ int64_t S[kMaxGroups + 1];
+    __shared__ uint64_t sh[4];
+    load_starts(gp, S);
+    __syncthreads();
+    const int64_t i0 = (int64_t)blockIdx.x * kSpTile + threadIdx.x * 8;
+    int l[8];
+    uint64_t sum = 0;
+    int g0 = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) l[j] = 0;
+    if (i0 < n) {
+        int g = g0 = group_of_elem(S, i0);
+        DeltaShape s = delta_shape(gp, g);
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int64_t i = i0 + j;
+            if (i >= n) break;
+            while (i >= S[g + 1]) s = delta_shape(gp, ++g);
+            l[j] = dec_len_of(fw, nfw, end_pos, gp, s, g, i, S[g]);
+            sum += (uint64_t)l[j];
+        }
+    }
+    uint64_t v[1] = {sum}, tot[1];
+    block_excl_scan<1>(v, tot, sh);
+    int64_t off = (int64_t)(bit_base[blockIdx.x] + v[0]);
+    uint32_t d[8];
+    uint64_t dsum = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        d[j] = i0 + j < n ? get_bits(dw, ndw, off, l[j]) : 0u;
+        dsum += d[j];
+        off += l[j];
+    }
+    uint64_t v2[1] = {dsum}, tot2[1];
+    block_excl_scan<1>(v2, tot2, sh);
+    if (threadIdx.x == 0) tile_sums[blockIdx.x] = tot2[0];
+    if (i0 < n) {  // groups whose first element is one of this thread's: their in-tile delta prefix
+        for (int g = g0; g < gp->G && S[g] < i0 + 8 && S[g] < n; g++) {
+            if (S[g] < i0) continue;
+            uint64_t part = v2[0];
+#pragma unroll
+            for (int j = 0; j < 8; j++) part += i0 + j < S[g] ? d[j] : 0u;
+            gpart[g] = part;
+        }
+    }
+}
+
+hipError_t launch_dec_sums(hipStream_t st, const uint64_t* flag_words, int64_t n_flag_words, const int64_t* end_pos,
+                           const uint64_t* delta_words, int64_t n_delta_words, int64_t n, const SpGroups* gp,
+                           uint64_t* bit_sums, int pass, uint64_t* delta_sums, uint64_t* gpart) {
+    const int64_t tiles = sp_tiles(n, kSpTile);
+    if (tiles <= 0) return hipSuccess;
+    if (pass == 0)
+        hipLaunchKernelGGL(k_dec_lsum, dim3((unsigned)tiles), dim3(kSpThreads), 0, st, flag_words, n_flag_words, end_pos,
+                           n, gp, bit_sums);
+    else
+        hipLaunchKernelGGL(k_dec_dsum, dim3((unsigned)tiles), dim3(kSpThreads), 0, st, flag_words, n_flag_words, end_pos,
+                           delta_words, n_delta_words, n, gp, bit_sums, delta_sums, gpart);
+    return hipGetLastError();
+}
+
 // Exclusive delta prefix at each group's first element: tile base + the in-tile partial sum.
 __global__ __launch_bounds__(kSpThreads) void k_group_prefix(const uint32_t* __restrict__ delta, int64_t n,
                                                              const SpGroups* __restrict__ gp,
@@ -2260,29 +2384,73 @@ __device__ __forceinline__ int64_t dec_tile_of_block(const int64_t* S, int G, in
 // keys: group-restarted prefix sums of the deltas (Java int wrap); bins: MinMaxSketch.query
 // (MinMaxSketch.java:64-73): the row value farthest from zero, the first row on ties.  TN: the
 // narrow table's cell type (int32_t: the int32 table itself).  512 threads per 2,048-element tile,
-// 4 consecutive elements per thread (16-byte delta loads and key stores; few registers, so 8
-// waves per SIMD hide the table gathers).
+// 4 consecutive elements per thread (16-byte key stores); the deltas come from `delta` or, by
+// default, from the streams themselves (DecStreams).  MODE 1 needs 65 VGPRs (3 workgroups per
+// CU), MODE 0 81.
 constexpr int kDecThreads = 512;
 static_assert(kDecThreads * 4 == kSpTile, "dec_keys tile");
-template <typename TN>
+// MODE 1: the default shape (2 rows), tiles inside one group only (a tile across a group edge
+// returns at once): both rows' hashes fixed at compile time by a switch on the group's hash ids,
+// 8 gathers in flight per thread, cells as 32-bit offsets.  MODE 0: any shape and any tile, one
+// row at a time with a per-lane hash id; it runs the whole grid for other shapes, or only the
+// edge tiles (`edges`, at most one per group edge) after a MODE 1 launch.  Keeping the two apart
+// keeps MODE 1's registers at what its own code needs.
+struct DecEdgeTiles {
+    int64_t t[kMaxGroups];
+    int n;  // 0: every tile (dec_tile_of_block)
+};
+template <typename TN, int MODE>
 __global__ __launch_bounds__(kDecThreads) void k_dec_keys(const uint32_t* __restrict__ delta, int64_t n,
                                                           const SpGroups* __restrict__ gp,
                                                           const uint64_t* __restrict__ tile_base,
-                                                          const uint64_t* __restrict__ gpre,
+                                                          const uint64_t* gpre,
                                                           const int32_t* __restrict__ table, const TN* __restrict__ tnar,
                                                           int32_t* __restrict__ gkeys, int32_t* __restrict__ gbins,
                                                           int nq, void* __restrict__ gbn, int bn_width,
-                                                          unsigned* __restrict__ err, int batch_rows) {
+                                                          unsigned* __restrict__ err, DecEdgeTiles edges, DecStreams ds) {
     __shared__ int64_t S[kMaxGroups + 1];
     __shared__ uint64_t sh[kDecThreads / 64];
+    __shared__ uint64_t GPRE[kMaxGroups];
     load_starts(gp, S);
     __syncthreads();
-    const int64_t tile = dec_tile_of_block(S, gp->G, blockIdx.x);
+    const int64_t tile = edges.n > 0 ? edges.t[blockIdx.x] : dec_tile_of_block(S, gp->G, blockIdx.x);
     if (tile < 0) return;  // workgroup-uniform
+    if constexpr (MODE == 1) {
+        const int64_t tf = tile * kSpTile, tl = std::min<int64_t>(n, tf + kSpTile) - 1;
+        if (group_of_elem(S, tf) != group_of_elem(S, tl)) return;  // an edge tile: the MODE 0 launch
+    }
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int64_t i0 = tile * kSpTile + t * 4;
     uint32_t d[4];
-    if (i0 + 4 <= n) {
+    if (ds.dw) {  // lengths from the flags, deltas from the delta stream (k_dec_lsum / k_dec_dsum)
+        if (t < gp->G) GPRE[t] = S[t] < n ? tile_base[S[t] / kSpTile] + ds.gpart[t] : 0ull;
+        int l[4] = {0, 0, 0, 0};
+        uint64_t lsum = 0;
+        if (i0 < n) {
+            int g = group_of_elem(S, i0);
+            DeltaShape s = delta_shape(gp, g);
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int64_t i = i0 + j;
+                if (i >= n) break;
+                while (i >= S[g + 1]) s = delta_shape(gp, ++g);
+                l[j] = dec_len_of(ds.fw, ds.nfw, ds.end_pos, gp, s, g, i, S[g]);
+                lsum += (uint64_t)l[j];
+            }
+        }
+        const uint64_t linc = wave_incl_u64(lsum, lane);
+        if (lane == 63) sh[w] = linc;
+        __syncthreads();
+        int64_t off = (int64_t)(ds.bit_base[tile] + linc - lsum);
+#pragma unroll
+        for (int j = 0; j < kDecThreads / 64; j++) off += j < w ? (int64_t)sh[j] : 0;
+        __syncthreads();  // sh is reused by the delta scan
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            d[j] = i0 + j < n ? get_bits(ds.dw, ds.ndw, off, l[j]) : 0u;
+            off += l[j];
+        }
+    } else if (i0 + 4 <= n) {
         const uint4 v = *reinterpret_cast<const uint4*>(delta + i0);
         d[0] = v.x, d[1] = v.y, d[2] = v.z, d[3] = v.w;
     } else {
@@ -2309,7 +2477,7 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_keys(const uint32_t* __rest
             while (i >= S[g + 1]) g++;
         p += d[j];
         grp[j] = g;
-        key[j] = (int32_t)(uint32_t)(p - gpre[g]);
+        key[j] = (int32_t)(uint32_t)(p - (ds.dw ? GPRE[g] : gpre[g]));
         res[j] = zero;
     }
     constexpr uint32_t kTop = sizeof(TN) == 4 ? 0u : (uint32_t)(TN)~(TN)0;
@@ -2328,25 +2496,44 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_keys(const uint32_t* __rest
     auto take = [&](int j, int32_t tv) {
         if ((int32_t)((uint32_t)mm_dist(tv, zero) - (uint32_t)mm_dist(res[j], zero)) > 0) res[j] = tv;
     };
-    if (rows == 2 && batch_rows) {
-        // the default shape: both rows' 8 cells hashed first, then all 8 gathers in flight at once
-        // (the query is bound by the gathers' L2 latency, not by the hash arithmetic)
-        int64_t idx[2][4];
+    if constexpr (MODE == 1) {
+        // both rows' 8 cells hashed, all 8 gathers in flight at once (the query is bound by the
+        // gathers' L2 latency); the host runs this form only while every cell index is below
+        // 2^32 - 1, and ~0u marks an element past n
+        const int g0 = grp[0];  // the tile's one group
+        const int64_t tb = gp->tab_off[g0];
+        const int32_t cols = gp->cols[g0];
+        const double inv = gp->inv_cols[g0];
+        const TN* tnb = tnar + tb;
+        const int32_t* t32b = table + tb;
+        uint32_t rel[2][4];
         int32_t tv[2][4];
 #pragma unroll
-        for (int r = 0; r < 2; r++)
+        for (int r = 0; r < 2; r++) {  // a row's 4 gathers leave before the next row is hashed
+            const int id = __builtin_amdgcn_readfirstlane(gp->hash_ids[g0][r]);
+            const int64_t row0 = (int64_t)r * cols;
+            switch (id) {
+                case 0: dec_row_cells<0>(key, i0, n, row0, cols, inv, rel[r]); break;
+                case 1: dec_row_cells<1>(key, i0, n, row0, cols, inv, rel[r]); break;
+                case 2: dec_row_cells<2>(key, i0, n, row0, cols, inv, rel[r]); break;
+                case 3: dec_row_cells<3>(key, i0, n, row0, cols, inv, rel[r]); break;
+                case 4: dec_row_cells<4>(key, i0, n, row0, cols, inv, rel[r]); break;
+                case 5: dec_row_cells<5>(key, i0, n, row0, cols, inv, rel[r]); break;
+                case 6: dec_row_cells<6>(key, i0, n, row0, cols, inv, rel[r]); break;
+                default: dec_row_cells<7>(key, i0, n, row0, cols, inv, rel[r]); break;
+            }
 #pragma unroll
-            for (int j = 0; j < 4; j++) idx[r][j] = cell_of(j, r);
-#pragma unroll
-        for (int r = 0; r < 2; r++)
-#pragma unroll
-            for (int j = 0; j < 4; j++) tv[r][j] = gather(idx[r][j]);
+            for (int j = 0; j < 4; j++) {
+                if constexpr (sizeof(TN) == 4) tv[r][j] = rel[r][j] != ~0u ? t32b[rel[r][j]] : zero;
+                else tv[r][j] = rel[r][j] != ~0u ? (int32_t)tnb[rel[r][j]] : zero;
+            }
+        }
         if constexpr (sizeof(TN) < 4) {
 #pragma unroll
             for (int r = 0; r < 2; r++)
 #pragma unroll
                 for (int j = 0; j < 4; j++)  // the sentinel: the cell's int32 value
-                    if (idx[r][j] >= 0 && (uint32_t)tv[r][j] == kTop) tv[r][j] = table[idx[r][j]];
+                    if (rel[r][j] != ~0u && (uint32_t)tv[r][j] == kTop) tv[r][j] = t32b[rel[r][j]];
         }
 #pragma unroll
         for (int r = 0; r < 2; r++)
@@ -2421,7 +2608,7 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_keys(const uint32_t* __rest
 hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, const SpGroups* gp, const SpGroups& gh,
                            const uint64_t* tile_base, const uint64_t* gpre, const int32_t* table, const void* tnar,
                            int width, int32_t* gkeys, int32_t* gbins, int nq, void* gbn, int bn_width,
-                           unsigned* err) {
+                           unsigned* err, const DecStreams& ds) {
     if (sp_tiles(n, kSpTile) <= 0) return hipSuccess;
     int64_t per[8] = {};  // tiles per XCD slot (dec_tile_of_block)
     for (int g = 0; g < gh.G; g++) {
@@ -2431,16 +2618,37 @@ hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, con
     int64_t most = 0;
     for (int x = 0; x < 8; x++) most = std::max(most, per[x]);
     const unsigned grid = (unsigned)(8 * most);
-    const int batch_rows = std::getenv("SKML_DEC_ROWS_SERIAL") == nullptr ? 1 : 0;  // A/B switch
-    if (width == 8)
-        hipLaunchKernelGGL(k_dec_keys<uint8_t>, dim3(grid), dim3(kDecThreads), 0, st, delta, n, gp, tile_base, gpre,
-                           table, static_cast<const uint8_t*>(tnar), gkeys, gbins, nq, gbn, bn_width, err, batch_rows);
-    else if (width == 16)
-        hipLaunchKernelGGL(k_dec_keys<uint16_t>, dim3(grid), dim3(kDecThreads), 0, st, delta, n, gp, tile_base, gpre,
-                           table, static_cast<const uint16_t*>(tnar), gkeys, gbins, nq, gbn, bn_width, err, batch_rows);
-    else
-        hipLaunchKernelGGL(k_dec_keys<int32_t>, dim3(grid), dim3(kDecThreads), 0, st, delta, n, gp, tile_base, gpre,
-                           table, static_cast<const int32_t*>(nullptr), gkeys, gbins, nq, gbn, bn_width, err, batch_rows);
+    // MODE 1 over every tile, then MODE 0 over the edge tiles; MODE 0 alone for other shapes, for
+    // tables past 2^32 - 1 cells, and under SKML_DEC_ROWS_SERIAL (the A/B switch)
+    const bool batched = gh.rows == 2 && table != nullptr && std::getenv("SKML_DEC_ROWS_SERIAL") == nullptr &&
+                         gh.ncells < (int64_t)0xFFFFFFFF;
+    DecEdgeTiles all{}, edges{};
+    all.n = 0;
+    if (batched) {  // tiles holding a group edge that is not a tile edge
+        for (int g = 1; g < gh.G; g++) {
+            const int64_t e = gh.gstart[g];
+            if (e <= 0 || e >= n || e % kSpTile == 0 || gh.gstart[g + 1] == e) continue;
+            const int64_t t = e / kSpTile;
+            if (edges.n == 0 || edges.t[edges.n - 1] != t) edges.t[edges.n++] = t;
+        }
+    }
+#define SKML_DEC_LAUNCH(TNT, MODE, GRID, TILES, TNPTR)                                                            \
+    hipLaunchKernelGGL((k_dec_keys<TNT, MODE>), dim3(GRID), dim3(kDecThreads), 0, st, delta, n, gp, tile_base, gpre, \
+                       table, TNPTR, gkeys, gbins, nq, gbn, bn_width, err, TILES, ds)
+#define SKML_DEC_WIDTH(TNT, TNPTR)                                                          \
+    do {                                                                                  \
+        if (batched) {                                                                    \
+            SKML_DEC_LAUNCH(TNT, 1, grid, all, TNPTR);                                    \
+            if (edges.n > 0) SKML_DEC_LAUNCH(TNT, 0, (unsigned)edges.n, edges, TNPTR);    \
+        } else {                                                                          \
+            SKML_DEC_LAUNCH(TNT, 0, grid, all, TNPTR);                                    \
+        }                                                                                 \
+    } while (0)
+    if (width == 8) SKML_DEC_WIDTH(uint8_t, static_cast<const uint8_t*>(tnar));
+    else if (width == 16) SKML_DEC_WIDTH(uint16_t, static_cast<const uint16_t*>(tnar));
+    else SKML_DEC_WIDTH(int32_t, static_cast<const int32_t*>(nullptr));
+#undef SKML_DEC_WIDTH
+#undef SKML_DEC_LAUNCH
     return hipGetLastError();
 }
 
@@ -2621,11 +2829,120 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_tiles(const AggPayload* __r
     __syncthreads();
     for (int x = threadIdx.x; x < nk; x += kAggThreads) out[k0 + x] = scale == 1.0 ? acc[x] : __dmul_rn(acc[x], scale);
 }
+// The same sum with one wave per payload of the batch (8 waves, 8 payloads): the wave walks its
+// payload's group runs in this tile (run bounds from k_agg_bounds), one lane per element, so no
+// element has to search for its payload and group (k_agg_tiles: two LDS binary searches per
+// element); every wave loads its elements' keys and bins first, then the waves add into the LDS
+// tile one after the other in payload order (one barrier per payload; keys are unique within a
+// payload).  Up to kAggWPer elements per lane are held in registers, a longer payload (a dense
+// form, or a tile far denser than the mean) adds the rest in further rounds of its turn.
+constexpr int kAggWPer = 16;
+__global__ __launch_bounds__(kAggThreads) void k_agg_tiles_w(const AggPayload* __restrict__ pays, int P,
+                                                            int64_t ntiles, int64_t dim, double* __restrict__ out,
+                                                            int from_out, double scale, unsigned* __restrict__ err) {
+    static_assert(kAggThreads / 64 == kAggPB, "one wave per payload of a batch");
+    __shared__ double acc[kAggTile];
+    __shared__ double qt[kAggPB][kAggLdsValues];
+    __shared__ int32_t rb[kAggPB][kMaxGroups + 1];  // run prefix (elements) per group, this tile
+    __shared__ int32_t rs[kAggPB][kMaxGroups];      // run start (element index in the payload)
+    const int64_t t = blockIdx.x;
+    const int64_t k0 = t * kAggTile, nk = std::min<int64_t>(kAggTile, dim - k0);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int x = threadIdx.x; x < kAggTile; x += kAggThreads) acc[x] = (from_out && x < nk) ? out[k0 + x] : 0.0;
+    unsigned bad = 0;
+    for (int p0 = 0; p0 < P; p0 += kAggPB) {
+        const int np = std::min(kAggPB, P - p0);
+        __syncthreads();  // the previous batch is done with qt / rb / rs
+        AggPayload a{};
+        const bool mine = wave < np;
+        if (mine) a = pays[p0 + wave];
+        if (mine) {
+            for (int b = lane; b < kAggLdsValues; b += 64)
+                if (a.nq <= kAggLdsValues && b < a.nq) qt[wave][b] = a.qv[b];
+            int32_t len = 0;
+            if (lane < a.G) {
+                const int32_t* bd = a.bounds + (int64_t)lane * (ntiles + 1);
+                const int32_t b0 = bd[t], b1 = bd[t + 1];
+                len = b1 > b0 ? b1 - b0 : 0;
+                rs[wave][lane] = b0;
+            }
+            int32_t x = len;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const int32_t y = __shfl_up(x, off, 64);
+                if (lane >= off) x += y;
+            }
+            if (lane < kMaxGroups) rb[wave][lane + 1] = x;
+            if (lane == 0) rb[wave][0] = 0;
+        }
+        __syncthreads();
+        // this wave's elements: compact index j = lane + 64 u over the concatenated runs; the run
+        // holding j by a walk over the (few) run prefixes
+        const int total = mine ? rb[wave][a.G] : 0;
+        const bool lds_q = a.nq <= kAggLdsValues;
+        int32_t kk[kAggWPer];
+        double vv[kAggWPer];
+#pragma unroll
+        for (int u = 0; u < kAggWPer; u++) {
+            const int j = lane + 64 * u;
+            kk[u] = 0;
+            vv[u] = 0.0;
+            if (j < total) {
+                int g = 0;
+                while (rb[wave][g + 1] <= j) g++;
+                const int64_t i = (int64_t)rs[wave][g] + (j - rb[wave][g]);
+                kk[u] = a.gk[i];
+                const uint32_t b = a.bw == 1 ? static_cast<const uint8_t*>(a.gb)[i] : static_cast<const uint16_t*>(a.gb)[i];
+                vv[u] = lds_q ? qt[wave][b] : a.qv[b];
+            }
+        }
+        for (int pl = 0; pl < np; pl++) {
+            if (wave == pl) {
+                const bool dform = a.dense_form != 0;
+                // a key outside this tile is an error (k_agg_bounds placed it here); the dense form
+                // keeps |v| > EPS only (SparseDoubleGradient.toDense)
+#define SKML_AGG_ADD(K, V)                                              \
+    do {                                                                \
+        const int32_t k_ = (K);                                         \
+        const double v_ = (V);                                          \
+        if (k_ < k0 || (int64_t)k_ >= k0 + nk) bad = 1;                 \
+        else if (!dform || fabs(v_) > 1e-8) acc[k_ - k0] += v_;         \
+    } while (0)
+#pragma unroll
+                for (int u = 0; u < kAggWPer; u++)
+                    if (lane + 64 * u < total) SKML_AGG_ADD(kk[u], vv[u]);
+                for (int j = lane + 64 * kAggWPer; j < total; j += 64) {  // the rest of a long payload
+                    int g = 0;
+                    while (rb[wave][g + 1] <= j) g++;
+                    const int64_t i = (int64_t)rs[wave][g] + (j - rb[wave][g]);
+                    const uint32_t b =
+                        a.bw == 1 ? static_cast<const uint8_t*>(a.gb)[i] : static_cast<const uint16_t*>(a.gb)[i];
+                    SKML_AGG_ADD(a.gk[i], lds_q ? qt[wave][b] : a.qv[b]);
+                }
+#undef SKML_AGG_ADD
+            }
+            __syncthreads();
+            if (pays[p0 + pl].dense_form) {  // the dense form adds +0.0 elsewhere: -0.0 sums become +0.0
+                for (int x = threadIdx.x; x < kAggTile; x += kAggThreads)
+                    if (__double_as_longlong(acc[x]) == (long long)0x8000000000000000ull) acc[x] = 0.0;
+                __syncthreads();
+            }
+        }
+    }
+    if (bad) atomicOr(err, 1u);
+    __syncthreads();
+    for (int x = threadIdx.x; x < nk; x += kAggThreads) out[k0 + x] = scale == 1.0 ? acc[x] : __dmul_rn(acc[x], scale);
+}
+
 hipError_t launch_agg_tiles(hipStream_t st, const AggPayload* pays, int P, int64_t ntiles, int64_t dim, double* out,
                             int from_out, double scale, unsigned* err) {
     if (ntiles <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_agg_tiles, dim3((unsigned)ntiles), dim3(kAggThreads), 0, st, pays, P, ntiles, dim, out, from_out,
-                       scale, err);
+    if (std::getenv("SKML_AGG_SEARCH") != nullptr)  // A/B switch: the per-element search form
+        hipLaunchKernelGGL(k_agg_tiles, dim3((unsigned)ntiles), dim3(kAggThreads), 0, st, pays, P, ntiles, dim, out,
+                           from_out, scale, err);
+    else
+        hipLaunchKernelGGL(k_agg_tiles_w, dim3((unsigned)ntiles), dim3(kAggThreads), 0, st, pays, P, ntiles, dim, out,
+                           from_out, scale, err);
     return hipGetLastError();
 }
 
@@ -2782,6 +3099,236 @@ hipError_t launch_merge_round(hipStream_t st, const int32_t* kin, const int32_t*
                        split);
     hipLaunchKernelGGL(k_merge_round, dim3((unsigned)tiles), dim3(kMergeThreads), 0, st, kin, bin_in, kout, bout, rs,
                        nruns, total, split);
+    return hipGetLastError();
+}
+
+// ---- Sort.merge in one pass over key ranges (the regular case) ----
+// Sort.merge (util/Sort.java:362-379) takes the smallest head of the G runs each step (ties to the
+// lower run).  When every run ascends strictly, no key repeats across runs and every key lies in
+// [0, INT32_MAX), that is the ascending order of all keys, so an element's output index is the
+// number of keys smaller than its own.  k_rs_bounds records where each run enters every range of
+// kRsRange keys (and flags a run that does not ascend or a key outside the range); k_rs_merge marks
+// one range's keys in an LDS bitmap, scans the bitmap's popcounts, and sends each element to the
+// range's base + its rank among the set bits, with its bin or quantValues[bin].  A repeated key
+// (a bit already set) flags the input too, and the host then runs the pairwise merge rounds,
+// which follow Sort.merge for any input.  Regular C3 payloads: one pass instead of three rounds.
+__global__ __launch_bounds__(kSpThreads) void k_rs_bounds(const int32_t* __restrict__ gk, int64_t n,
+                                                          const SpGroups* __restrict__ gp, int32_t* __restrict__ bounds,
+                                                          RsInfo* __restrict__ info) {
+    __shared__ int64_t S[kMaxGroups + 1];
+    load_starts(gp, S);
+    __syncthreads();
+    constexpr int64_t ld = kRsRanges + 1;
+    unsigned bad = 0;
+    const int64_t nq = (n + 3) / 4;
+    for (int64_t qd = (int64_t)blockIdx.x * kSpThreads + threadIdx.x; qd < nq; qd += (int64_t)gridDim.x * kSpThreads) {
+        const int64_t i0 = 4 * qd;
+        int32_t key[4];
+        if (i0 + 4 <= n && (reinterpret_cast<uintptr_t>(gk) & 15) == 0) {
+            const int4 v = *reinterpret_cast<const int4*>(gk + i0);
+            key[0] = v.x, key[1] = v.y, key[2] = v.z, key[3] = v.w;
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; e++) key[e] = i0 + e < n ? gk[i0 + e] : 0;
+        }
+        int32_t prev = i0 > 0 ? gk[i0 - 1] : 0;
+        int g = group_of_elem(S, i0);
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const int64_t i = i0 + e;
+            if (i >= n) break;
+            while (i >= S[g + 1]) g++;
+            const int32_t k = key[e];
+            const bool first = i == S[g];
+            if (k < 0 || k == INT32_MAX || (!first && k <= prev)) {
+                bad = 1;
+            } else {
+                const int64_t ti = k >> kRsBits;
+                const int64_t pt = first || prev < 0 ? -1 : prev >> kRsBits;
+                int32_t* b = bounds + (int64_t)g * ld;
+                for (int64_t t = pt + 1; t <= ti; t++) b[t] = (int32_t)i;
+                if (i == S[g + 1] - 1) {  // the run's last range ends at the run's end
+                    b[ti + 1] = (int32_t)S[g + 1];
+                    info->tlast1[g] = (int32_t)ti + 1;
+                    atomicMax(&info->tmax1, (int32_t)ti + 1);
+                }
+            }
+            prev = k;
+        }
+    }
+    if (bad) atomicOr(&info->irregular, 1u);
+}
+
+__device__ __forceinline__ int agg_search32(const int32_t* pre, int n, int j) {  // largest i < n: pre[i] <= j
+    int i = 0;
+    for (int step = 32; step >= 1; step >>= 1)
+        if (i + step < n && pre[i + step] <= j) i += step;
+    return i;
+}
+
+template <typename V>
+__device__ __forceinline__ V rs_value(int32_t b, const V* lut, const double* qv, int nq, bool lds, unsigned& bad) {
+    if constexpr (std::is_same<V, int32_t>::value) {
+        return b;
+    } else {
+        if (b < 0 || b >= nq) {
+            bad = 1;
+            return (V)0;
+        }
+        return lds ? lut[b] : (V)qv[b];
+    }
+}
+
+constexpr int kRsThreads = 256, kRsBatch = 4, kRsLut = 2048;
+static_assert(kRsWords % kRsThreads == 0, "bitmap words per thread");
+template <typename V>
+__global__ __launch_bounds__(kRsThreads) void k_rs_merge(const int32_t* __restrict__ gk, const int32_t* __restrict__ gb,
+                                                         const SpGroups* __restrict__ gp,
+                                                         const int32_t* __restrict__ bounds, RsInfo* __restrict__ info,
+                                                         int32_t* __restrict__ keys_out, V* __restrict__ out,
+                                                         const double* __restrict__ qv, int nq) {
+    constexpr int kWordsPer = kRsWords / kRsThreads;
+    constexpr int kLut = std::is_same<V, int32_t>::value ? 1 : kRsLut;
+    __shared__ uint32_t bm[kRsWords];
+    __shared__ uint32_t wp[kRsWords];
+    __shared__ int64_t S[kMaxGroups + 1];
+    __shared__ int64_t lo_s[kMaxGroups];
+    __shared__ int32_t pre[kMaxGroups + 1];
+    __shared__ int64_t obase;
+    __shared__ uint32_t wsum[kRsThreads / 64];
+    __shared__ V lut[kLut];
+    if (info->irregular) return;  // workgroup-uniform: the merge rounds run instead
+    const int tmax = info->tmax1 - 1;
+    const int G = gp->G, t_ = threadIdx.x, lane = t_ & 63, w = t_ >> 6;
+    load_starts(gp, S);
+    const bool lds = !std::is_same<V, int32_t>::value && nq <= kLut;
+    if (lds)
+        for (int b = t_; b < nq; b += kRsThreads) lut[b] = (V)qv[b];
+    constexpr int64_t ld = kRsRanges + 1;
+    unsigned bad = 0;
+    for (int64_t t = blockIdx.x; t <= tmax; t += gridDim.x) {
+        __syncthreads();  // S / lut loaded; the previous range is done with bm / wp / pre
+        if (w == 0) {  // lane g: run g's piece of this range
+            int64_t lo = 0, len = 0, before = 0;
+            if (lane < G) {
+                const int64_t s0 = S[lane], s1 = S[lane + 1];
+                const int tl = info->tlast1[lane] - 1;  // -1: an empty run
+                lo = s1;
+                int64_t hi = s1;
+                if (tl >= 0 && t <= tl) {
+                    lo = bounds[(int64_t)lane * ld + t];
+                    hi = bounds[(int64_t)lane * ld + t + 1];
+                }
+                before = lo - s0;
+                len = hi - lo;
+                lo_s[lane] = lo;
+            }
+            int64_t x = len;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const int64_t y = __shfl_up(x, off, 64);
+                if (lane >= off) x += y;
+            }
+            if (lane < kMaxGroups) pre[lane + 1] = (int32_t)x;
+            if (lane == 0) pre[0] = 0;
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) before += __shfl_xor(before, off, 64);
+            if (lane == 0) obase = before;
+        }
+        for (int j = t_; j < kRsWords; j += kRsThreads) bm[j] = 0;
+        __syncthreads();
+        const int cnt = pre[G];
+        if (cnt == 0) continue;  // workgroup-uniform
+        // pass 1: the range's keys into the bitmap (4 loads in flight per thread)
+        for (int j0 = 0; j0 < cnt; j0 += kRsThreads * kRsBatch) {
+            int32_t kk[kRsBatch];
+#pragma unroll
+            for (int u = 0; u < kRsBatch; u++) {
+                const int j = j0 + u * kRsThreads + t_;
+                kk[u] = -1;
+                if (j < cnt) {
+                    const int g = agg_search32(pre, G, j);
+                    kk[u] = gk[lo_s[g] + (j - pre[g])];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kRsBatch; u++) {
+                if (kk[u] < 0) continue;
+                const uint32_t off = (uint32_t)kk[u] & (kRsRange - 1), bit = 1u << (off & 31);
+                if (atomicOr(&bm[off >> 5], bit) & bit) bad = 1;  // a repeated key
+            }
+        }
+        __syncthreads();
+        // exclusive prefix of the words' popcounts: thread t_ owns words [t_ * kWordsPer, +kWordsPer)
+        uint32_t pc[kWordsPer], own = 0;
+#pragma unroll
+        for (int q = 0; q < kWordsPer; q++) {
+            pc[q] = __popc(bm[t_ * kWordsPer + q]);
+            own += pc[q];
+        }
+        uint32_t inc = own;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(inc, off, 64);
+            if (lane >= off) inc += y;
+        }
+        if (lane == 63) wsum[w] = inc;
+        __syncthreads();
+        uint32_t run = inc - own;
+        for (int q = 0; q < w; q++) run += wsum[q];
+#pragma unroll
+        for (int q = 0; q < kWordsPer; q++) {
+            wp[t_ * kWordsPer + q] = run;
+            run += pc[q];
+        }
+        __syncthreads();
+        // pass 2: each element to base + rank
+        const int64_t ob = obase;
+        for (int j0 = 0; j0 < cnt; j0 += kRsThreads * kRsBatch) {
+            int32_t kk[kRsBatch], bb[kRsBatch];
+#pragma unroll
+            for (int u = 0; u < kRsBatch; u++) {
+                const int j = j0 + u * kRsThreads + t_;
+                kk[u] = -1;
+                if (j < cnt) {
+                    const int g = agg_search32(pre, G, j);
+                    const int64_t i = lo_s[g] + (j - pre[g]);
+                    kk[u] = gk[i];
+                    bb[u] = gb[i];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kRsBatch; u++) {
+                if (kk[u] < 0) continue;
+                const uint32_t off = (uint32_t)kk[u] & (kRsRange - 1);
+                const uint32_t r = wp[off >> 5] + __popc(bm[off >> 5] & ((1u << (off & 31)) - 1u));
+                keys_out[ob + r] = kk[u];
+                out[ob + r] = rs_value<V>(bb[u], lut, qv, nq, lds, bad);
+            }
+        }
+    }
+    if (bad) atomicOr(&info->irregular, 2u);
+}
+
+hipError_t launch_rs_merge(hipStream_t st, const int32_t* gk, const int32_t* gb, int64_t n, const SpGroups* gp,
+                           int32_t* bounds, RsInfo* info, int32_t* keys_out, void* out, int vkind, const double* qv,
+                           int nq) {
+    if (n <= 0) return hipSuccess;
+    hipError_t e = hipMemsetAsync(info, 0, sizeof(RsInfo), st);
+    if (e != hipSuccess) return e;
+    const int64_t bgrid = std::min<int64_t>(sp_tiles((n + 3) / 4, kSpThreads), 8192);
+    hipLaunchKernelGGL(k_rs_bounds, dim3((unsigned)bgrid), dim3(kSpThreads), 0, st, gk, n, gp, bounds, info);
+    // persistent workgroups over the key ranges up to the largest key (read on the device)
+    const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(sp_tiles(n, 4096), 1), 2048);
+    if (vkind == 0)
+        hipLaunchKernelGGL(k_rs_merge<int32_t>, dim3(grid), dim3(kRsThreads), 0, st, gk, gb, gp, bounds, info, keys_out,
+                           static_cast<int32_t*>(out), qv, nq);
+    else if (vkind == 1)
+        hipLaunchKernelGGL(k_rs_merge<float>, dim3(grid), dim3(kRsThreads), 0, st, gk, gb, gp, bounds, info, keys_out,
+                           static_cast<float*>(out), qv, nq);
+    else
+        hipLaunchKernelGGL(k_rs_merge<double>, dim3(grid), dim3(kRsThreads), 0, st, gk, gb, gp, bounds, info, keys_out,
+                           static_cast<double*>(out), qv, nq);
     return hipGetLastError();
 }
 

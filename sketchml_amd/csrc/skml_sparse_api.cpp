@@ -62,6 +62,7 @@ enum {
     kSlotWire,      // readObject: the device copy of the field stream
     kSlotWireMeta,  // the wire kernels' section tables and small results
     kSlotNarrowTab, // the MinMax query's narrow table image
+    kSlotRsMerge,   // one-pass Sort.merge: RsInfo + the runs' key-range bounds
     kSlotCount_,
 };
 static_assert(kSlotCount_ <= kScratchSlots, "scratch slots");
@@ -609,17 +610,38 @@ int decode_groups(skml_ctx* c, const skml_sparse* s, int32_t* gk, int32_t* gb, b
         SP_HIP(launch_unary_select(st, s->flag_words, s->n_flag_words, s->g_dev, ts, end_pos));
     }
     const int64_t tiles = sp_tiles(n, kSpTile);
-    uint8_t* dlen = scratch<uint8_t>(c, kSlotNeed, (size_t)n);
-    uint32_t* delta = scratch<uint32_t>(c, kSlotDelta, (size_t)n);
     uint64_t* ts = scratch<uint64_t>(c, kSlotTiles, (size_t)(tiles + 1) * 2);
     uint64_t* gpre = scratch<uint64_t>(c, kSlotSmall, kMaxGroups + 8);
-    if (!dlen || !delta || !ts || !gpre) return sfail(SKML_E_OOM, "decode scratch");
+    if (!ts || !gpre) return sfail(SKML_E_OOM, "decode scratch");
     uint64_t* ts2 = ts + (tiles + 1);
-    SP_HIP(launch_dec_lens(st, s->flag_words, s->n_flag_words, end_pos, n, s->g_dev, dlen, ts));
-    if (int e = scan_tiles(c, ts, tiles, 1, nullptr)) return e;
-    SP_HIP(launch_dec_deltas(st, s->delta_words, s->n_delta_words, dlen, n, s->g_dev, ts, delta, ts2));
-    if (int e = scan_tiles(c, ts2, tiles, 1, nullptr)) return e;
-    SP_HIP(launch_group_prefix(st, delta, n, s->g_dev, G.G, ts2, gpre));
+    uint32_t* delta = nullptr;
+    DecStreams ds;
+    // A/B switch: SKML_DEC_MATERIALIZE keeps the lengths and deltas in memory (k_dec_lens,
+    // k_dec_deltas, k_group_prefix); by default k_dec_keys recomputes them from the streams
+    if (std::getenv("SKML_DEC_MATERIALIZE") != nullptr) {
+        uint8_t* dlen = scratch<uint8_t>(c, kSlotNeed, (size_t)n);
+        delta = scratch<uint32_t>(c, kSlotDelta, (size_t)n);
+        if (!dlen || !delta) return sfail(SKML_E_OOM, "decode scratch");
+        SP_HIP(launch_dec_lens(st, s->flag_words, s->n_flag_words, end_pos, n, s->g_dev, dlen, ts));
+        if (int e = scan_tiles(c, ts, tiles, 1, nullptr)) return e;
+        SP_HIP(launch_dec_deltas(st, s->delta_words, s->n_delta_words, dlen, n, s->g_dev, ts, delta, ts2));
+        if (int e = scan_tiles(c, ts2, tiles, 1, nullptr)) return e;
+        SP_HIP(launch_group_prefix(st, delta, n, s->g_dev, G.G, ts2, gpre));
+    } else {
+        SP_HIP(launch_dec_sums(st, s->flag_words, s->n_flag_words, end_pos, s->delta_words, s->n_delta_words, n,
+                               s->g_dev, ts, 0, nullptr, nullptr));
+        if (int e = scan_tiles(c, ts, tiles, 1, nullptr)) return e;
+        SP_HIP(launch_dec_sums(st, s->flag_words, s->n_flag_words, end_pos, s->delta_words, s->n_delta_words, n,
+                               s->g_dev, ts, 1, ts2, gpre));
+        if (int e = scan_tiles(c, ts2, tiles, 1, nullptr)) return e;
+        ds.fw = s->flag_words;
+        ds.nfw = s->n_flag_words;
+        ds.end_pos = end_pos;
+        ds.dw = s->delta_words;
+        ds.ndw = s->n_delta_words;
+        ds.bit_base = ts;
+        ds.gpart = gpre;
+    }
     // the query gathers from a byte (binNum <= 256) or 16-bit image of the tables
     const int32_t* tab = query ? s->tables : nullptr;
     int width = 32;
@@ -631,7 +653,7 @@ int decode_groups(skml_ctx* c, const skml_sparse* s, int32_t* gk, int32_t* gb, b
         SP_HIP(launch_narrow_table(st, tab, s->ncells, width, tnar));
     }
     SP_HIP(launch_dec_keys(st, delta, n, s->g_dev, G, ts2, gpre, tab, tnar, width, gk, gb, dv ? dv->nq : 0,
-                           dv ? dv->gb : nullptr, dv ? dv->bw : 0, dv ? dv->err : nullptr));
+                           dv ? dv->gb : nullptr, dv ? dv->bw : 0, dv ? dv->err : nullptr, ds));
     return SKML_OK;
 }
 
@@ -672,6 +694,30 @@ int merge_groups(skml_ctx* c, const skml_sparse* s, int32_t* gk, int32_t* gb, in
     if (!keys_done) SP_HIP(hipMemcpyAsync(keys_out, kin, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToDevice, st));
     if (!bins_done && bins_out && bins_out != bin)
         SP_HIP(hipMemcpyAsync(bins_out, bin, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToDevice, st));
+    return SKML_OK;
+}
+
+// Sort.merge's one-pass form (launch_rs_merge) into keys_out and out (vkind: 0 int32 bins, 1 float /
+// 2 double quantValues[bin]).  *pending: a pinned word that is non-zero after the stream
+// synchronises if the input was not regular and merge_groups must run instead; nullptr when the
+// one-pass form did not run (one run, or SKML_RS_ROUNDS set: the rounds' A/B switch).
+thread_local int t_merge_path = 0;  // skml_debug_sparse_merge_path
+
+int rs_merge_start(skml_ctx* c, const skml_sparse* s, const int32_t* gk, const int32_t* gb, int32_t* keys_out,
+                   void* out, int vkind, const double* qv, int nq, volatile unsigned** pending) {
+    *pending = nullptr;
+    if (s->g.G < 2 || std::getenv("SKML_RS_ROUNDS") != nullptr) return SKML_OK;
+    hipStream_t st = ctx_stream(c);
+    const size_t o_b = align_up(sizeof(RsInfo), 256);
+    char* blk = static_cast<char*>(
+        ctx_scratch(c, kSlotRsMerge, o_b + sizeof(int32_t) * (size_t)s->g.G * (size_t)(kRsRanges + 1)));
+    unsigned* pin = static_cast<unsigned*>(ctx_pinned(c, 64));
+    if (!blk || !pin) return sfail(SKML_E_OOM, "merge scratch");
+    RsInfo* info = reinterpret_cast<RsInfo*>(blk);
+    SP_HIP(launch_rs_merge(st, gk, gb, s->nnz, s->g_dev, reinterpret_cast<int32_t*>(blk + o_b), info, keys_out, out,
+                           vkind, qv, nq));
+    SP_HIP(hipMemcpyAsync(pin, &info->irregular, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    *pending = pin;
     return SKML_OK;
 }
 
@@ -780,14 +826,27 @@ int decode_values(skml_ctx* c, const skml_sparse* s, int32_t* keys_dev, T* vals_
     int32_t* b1 = scratch<int32_t>(c, kSlotB1, (size_t)n);
     if (!gk || !gb || !b1) return sfail(SKML_E_OOM, "decode scratch");
     if (int e = decode_groups(c, s, gk, gb, true)) return e;
-    if (int e = merge_groups(c, s, gk, gb, keys_dev, b1)) return e;
-    const int32_t* bin = b1;
+    const int nq = (int)s->qvalues.size();
     double* qv = reinterpret_cast<double*>(ctx_scratch(c, kSlotCells, sizeof(double) * s->qvalues.size()));
     if (!qv) return sfail(SKML_E_OOM, "value table");
     SP_HIP(hipMemcpyAsync(qv, s->qvalues.data(), sizeof(double) * s->qvalues.size(), hipMemcpyHostToDevice, st));
-    if constexpr (sizeof(T) == 8) SP_HIP(launch_bin_values64(st, bin, n, qv, (int)s->qvalues.size(), vals_dev));
-    else SP_HIP(launch_bin_values(st, bin, n, qv, (int)s->qvalues.size(), vals_dev));
+    auto rounds = [&]() -> int {  // pairwise merge rounds, then quantValues[bin]
+        if (int e = merge_groups(c, s, gk, gb, keys_dev, b1)) return e;
+        if constexpr (sizeof(T) == 8) SP_HIP(launch_bin_values64(st, b1, n, qv, nq, vals_dev));
+        else SP_HIP(launch_bin_values(st, b1, n, qv, nq, vals_dev));
+        return SKML_OK;
+    };
+    volatile unsigned* pending = nullptr;
+    if (int e = rs_merge_start(c, s, gk, gb, keys_dev, vals_dev, sizeof(T) == 8 ? 2 : 1, qv, nq, &pending)) return e;
+    if (!pending)
+        if (int e = rounds()) return e;
     SP_HIP(hipStreamSynchronize(st));
+    t_merge_path = s->g.G < 2 ? 0 : pending ? 1 : 2;
+    if (pending && *pending) {  // not regular (or a bin outside quantValues): the rounds decide
+        t_merge_path = 3;
+        if (int e = rounds()) return e;
+        SP_HIP(hipStreamSynchronize(st));
+    }
     return SKML_OK;
 }
 }  // namespace
@@ -1573,8 +1632,17 @@ int skml_sparse_restore_bins(skml_ctx* c, const skml_sparse* s, int32_t* keys_de
     int32_t* gb = scratch<int32_t>(c, kSlotGBins, (size_t)n);
     if (!gk || !gb) return sfail(SKML_E_OOM, "restore scratch");
     if (int e = decode_groups(c, s, gk, gb, true)) return e;
-    if (int e = merge_groups(c, s, gk, gb, keys_dev, bins_dev)) return e;
+    volatile unsigned* pending = nullptr;
+    if (int e = rs_merge_start(c, s, gk, gb, keys_dev, bins_dev, 0, nullptr, 0, &pending)) return e;
+    if (!pending)
+        if (int e = merge_groups(c, s, gk, gb, keys_dev, bins_dev)) return e;
     SP_HIP(hipStreamSynchronize(st));
+    t_merge_path = s->g.G < 2 ? 0 : pending ? 1 : 2;
+    if (pending && *pending) {  // not regular: the merge rounds decide
+        t_merge_path = 3;
+        if (int e = merge_groups(c, s, gk, gb, keys_dev, bins_dev)) return e;
+        SP_HIP(hipStreamSynchronize(st));
+    }
     return SKML_OK;
 }
 
@@ -1899,6 +1967,8 @@ int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t
     if (bad) return sfail(SKML_E_ARG, "a payload holds a key outside [0, %lld) or a bin outside its values", (long long)dim);
     return SKML_OK;
 }
+
+int skml_debug_sparse_merge_path(void) { return t_merge_path; }
 
 int skml_debug_sparse_scratch_fail(int on) {
     g_fail_cellbuf.store(on ? 1 : 0);

@@ -76,21 +76,74 @@ def test_sparse_edge_values(gpu, kind):
     _check_sparse(gpu, keys, vals, seed=5, hash_seed=1)
 
 
+@pytest.fixture(params=["one_pass", "rounds"])
+def merge_form(request, monkeypatch):
+    """restore both ways.  one_pass (the default): lengths and deltas recomputed inside the key
+    query (k_dec_lsum / k_dec_dsum / k_dec_keys), tiles of one group through the compile-time-hash
+    query and the edge tiles through the generic one, Sort.merge as the one-pass key-range merge.
+    rounds: the A/B switches back to the round-3 forms (materialised lengths and deltas, one
+    generic query per row, the pairwise merge rounds, which are also the fallback for irregular
+    input)."""
+    if request.param == "rounds":
+        monkeypatch.setenv("SKML_RS_ROUNDS", "1")
+        monkeypatch.setenv("SKML_DEC_MATERIALIZE", "1")
+        monkeypatch.setenv("SKML_DEC_ROWS_SERIAL", "1")
+    return request.param
+
+
+def _merge_path():
+    from sketchml_amd import _lib
+    return _lib.lib.skml_debug_sparse_merge_path()
+
+
 @pytest.mark.parametrize("groups,rows,ratio,bins", [(2, 1, 0.3, 256), (4, 3, 0.5, 64), (16, 8, 0.1, 1024),
                                                     (64, 2, 0.3, 4096), (8, 2, 1.7, 16), (3, 1, 0.3, 128),
                                                     (5, 2, 0.3, 256), (7, 3, 0.2, 512)])
-def test_sparse_shapes(gpu, groups, rows, ratio, bins):
+def test_sparse_shapes(gpu, groups, rows, ratio, bins, merge_form):
     """Odd group counts leave an unpaired run in restore's Sort.merge rounds."""
     keys, vals = _sparse_data(120000, 0.15, groups * 100 + rows, "normal")
     _check_sparse(gpu, keys, vals, bins, groups, rows, ratio, seed=7, hash_seed=groups)
+    assert _merge_path() == (1 if merge_form == "one_pass" else 2)
 
 
 @pytest.mark.parametrize("groups", [7, 8])
-def test_sparse_restore_many_merge_tiles(gpu, groups):
+def test_sparse_restore_many_merge_tiles(gpu, groups, merge_form):
     """~630 K keys: every Sort.merge round spans ~150 merge tiles of 4,096 outputs, with tile
-    boundaries inside and at the ends of the merged pairs (k_merge_splits)."""
+    boundaries inside and at the ends of the merged pairs (k_merge_splits); the one-pass merge
+    covers 33 key ranges of 65,536 keys, ~19.7 K keys each."""
     keys, vals = _sparse_data(2**21 + 3, 0.3, 40 + groups, "normal")
     _check_sparse(gpu, keys, vals, 256, groups, 2, 0.3, seed=11, hash_seed=groups)
+    assert _merge_path() == (1 if merge_form == "one_pass" else 2)
+
+
+@pytest.mark.parametrize("layout", ["range_edges", "full_ranges", "far_apart", "int_max"])
+def test_sparse_restore_key_ranges(gpu, layout, merge_form):
+    """Keys placed against the one-pass merge's 65,536-key ranges: on and next to range edges
+    (0, 65535, 65536, ...), whole ranges filled (every bitmap bit set, ranges of 65,536
+    elements), keys ranges apart up to 2^31 - 2 (empty ranges between, a run's bounds filled over
+    a gap), and a key of INT32_MAX, which Sort.merge never selects (its `< Integer.MAX_VALUE`
+    test): the one-pass form hands that input to the rounds (path 3), whose result the oracle
+    states."""
+    rng = np.random.default_rng(len(layout))
+    if layout == "range_edges":
+        e = np.arange(1, 40, dtype=np.int64) * 65536
+        keys = np.unique(np.concatenate([[0, 1, 65534, 65535], e - 1, e, e + 1]))
+    elif layout == "full_ranges":
+        keys = np.arange(3 * 65536 + 100, dtype=np.int64) + 65536
+    elif layout == "far_apart":
+        keys = np.unique(np.concatenate([rng.integers(0, 2**31 - 1, 3000), [2**31 - 2, 0, 65536 * 32767]]))
+    else:
+        keys = np.unique(np.concatenate([rng.integers(0, 2**20, 5000), [2**31 - 2, 2**31 - 1]]))
+    keys = keys.astype(np.int32)
+    vals = rng.standard_normal(len(keys)).astype(np.float32)
+    pl, osp = _check_sparse(gpu, keys, vals, 256, 8, 2, 0.3, seed=3, hash_seed=4)
+    rk, rb = pl.restore_bins()
+    ok, ob = osp.restore()
+    assert np.array_equal(rk.cpu().numpy(), ok) and np.array_equal(rb.cpu().numpy(), ob)
+    if merge_form == "rounds":
+        assert _merge_path() == 2
+    else:
+        assert _merge_path() == (3 if layout == "int_max" else 1)
 
 
 def test_sparse_key_gaps_choose_each_interval_kind(gpu):
@@ -125,12 +178,18 @@ def test_sparse_rejects_non_increasing_keys(gpu):
         gpu.encode_sparse(torch.from_numpy(keys).cuda(), torch.from_numpy(vals).cuda(), 4, 2)
 
 
-def test_sparse_duplicate_keys_across_groups_are_kept(gpu):
+def test_sparse_duplicate_keys_across_groups_are_kept(gpu, merge_form):
     """A key repeated in two different groups is legal for the reference (each group ascends);
-    Sort.merge then emits the lower group's copy first."""
+    Sort.merge then emits the lower group's copy first.  The one-pass merge sees the repeated bit
+    and hands the payload to the merge rounds (path 3)."""
     keys = np.array([5, 9, 9, 12, 40, 41], dtype=np.int32)
     vals = np.array([0.5, -1, 2, 0.25, -0.5, 1], dtype=np.float32)
-    _check_sparse(gpu, keys, vals, 4, 2, 1, 0.5, 1, 1)
+    pl, osp = _check_sparse(gpu, keys, vals, 4, 2, 1, 0.5, 1, 1)
+    assert _merge_path() == (3 if merge_form == "one_pass" else 2)
+    rk, rb = pl.restore_bins()
+    ok, ob = osp.restore()
+    assert np.array_equal(rk.cpu().numpy(), ok) and np.array_equal(rb.cpu().numpy(), ob)
+    assert _merge_path() == (3 if merge_form == "one_pass" else 2)
 
 
 def test_sparse_length_mismatch(gpu):

@@ -116,7 +116,19 @@ def test_corrupt_blobs_are_refused(gpu):
         gpu.decode_sum(blob, 1, blob.numel(), 1000)
 
 
-def test_decode_sum_eight_payloads_matches_oracle(gpu):
+# "wave": k_agg_tiles_w (a wave per payload) with the row-batched MinMax query (the defaults);
+# "search": k_agg_tiles (per-element run search) with the row-by-row query (the A/B switches)
+KERNELS = {"wave": {}, "search": {"SKML_AGG_SEARCH": "1", "SKML_DEC_ROWS_SERIAL": "1", "SKML_DEC_MATERIALIZE": "1"}}
+
+
+@pytest.fixture(params=sorted(KERNELS))
+def agg_kernel(request, monkeypatch):
+    for k, v in KERNELS[request.param].items():
+        monkeypatch.setenv(k, v)
+    return request.param
+
+
+def test_decode_sum_eight_payloads_matches_oracle(gpu, agg_kernel):
     dim = 2**20 + 5
     pls, osps = zip(*[_payload(gpu, dim, 0.1 + 0.02 * p, 10 + p) for p in range(8)])
     allb, stride = _gather_local(pls)
@@ -128,7 +140,7 @@ def test_decode_sum_eight_payloads_matches_oracle(gpu):
     assert np.array_equal(got_avg.view(np.uint64), (want * (1.0 / 8)).view(np.uint64))
 
 
-def test_decode_sum_dense_form_payloads(gpu):
+def test_decode_sum_dense_form_payloads(gpu, agg_kernel):
     """Payloads with more than dim * 2 / 3 live values reach plusBy in dense form: bucket values with
     |v| <= 1e-8 (the tiny cluster's midpoints) are not added."""
     dim = 30011
@@ -143,7 +155,7 @@ def test_decode_sum_dense_form_payloads(gpu):
     assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
 
 
-def test_decode_sum_skips_empty_payloads(gpu):
+def test_decode_sum_skips_empty_payloads(gpu, agg_kernel):
     dim = 4096
     empty = gpu.encode_sparse(torch.zeros(0, dtype=torch.int32).cuda(), torch.zeros(0, dtype=torch.float64).cuda())
     p1, o1 = _payload(gpu, dim, 0.2, 31)

@@ -7,7 +7,7 @@ tail -1 gpurun_out/r04f_dsum_tests.log
 timeout -k 10 400 python -u -m pytest tests/test_gpu_jni_harness.py tests/test_gpu_sparse_exchange.py tests/test_gpu_sparse.py tests/test_gpu_sparse_full.py -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/r04f_sparse_tests.log 2>&1
 tail -1 gpurun_out/r04f_sparse_tests.log
 for i in 1 2; do
-  SKML_DEC_ROWS_SERIAL=1 timeout -k 10 200 python tools/bench_sparse.py --reps 10 --aggregate 8 > gpurun_out/r04f_sparse_c3_serial_$i.json 2>&1
+  SKML_DEC_ROWS_SERIAL=1 SKML_AGG_SEARCH=1 SKML_RS_ROUNDS=1 SKML_DEC_MATERIALIZE=1 timeout -k 10 200 python tools/bench_sparse.py --reps 10 --aggregate 8 > gpurun_out/r04f_sparse_c3_serial_$i.json 2>&1
   timeout -k 10 200 python tools/bench_sparse.py --reps 10 --aggregate 8 > gpurun_out/r04f_sparse_c3_$i.json 2>&1
   python3 -c "
 import json

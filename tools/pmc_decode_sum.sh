@@ -8,7 +8,7 @@ cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/dsum_$TAG
 mkdir -p "$OUT"
-VARIANTS="occ:_ occ_nopf:SKML_DECODE_SUM_NOPF=1 plain:SKML_DECODE_SUM_PLAIN=1"
+VARIANTS="occ:SKML_AB_DEFAULT=1 occ_nopf:SKML_DECODE_SUM_NOPF=1 plain:SKML_DECODE_SUM_PLAIN=1"
 for i in 1 2 3; do
   for V in $VARIANTS; do
     env "${V#*:}" timeout -k 10 120 python3 tools/bench_decode_sum.py >> "$OUT/ab_${V%%:*}.jsonl"
