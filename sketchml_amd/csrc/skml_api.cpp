@@ -1878,6 +1878,7 @@ int ctx_side_fork(skml_ctx* c, hipStream_t* side, hipEvent_t* fork, hipEvent_t* 
     *join = c->ev_join2;
     return SKML_OK;
 }
+skml_ctx* ctx_side_ctx(skml_ctx* c) { return c->side; }
 int ctx_device(skml_ctx* c) { return c->device; }
 int set_error(int code, const char* msg) { return fail(code, "%s", msg); }
 bool ctx_timing(skml_ctx* c) { return c->timing != 0; }

@@ -159,23 +159,6 @@ hipError_t launch_dec_deltas(hipStream_t st, const uint64_t* delta_words, int64_
                              const uint64_t* tile_base, uint32_t* delta, uint64_t* tile_sums);
 hipError_t launch_group_prefix(hipStream_t st, const uint32_t* delta, int64_t n, const SpGroups* gp, int G,
                                const uint64_t* tile_base, uint64_t* gpre);
-// The stream passes without materialised lengths / deltas: pass 0 writes each kSpTile tile's sum of
-// delta bit lengths into bit_sums; pass 1 (bit_sums scanned) writes the tiles' delta sums into
-// delta_sums and every group's in-tile delta prefix at its first element into gpart[G].
-hipError_t launch_dec_sums(hipStream_t st, const uint64_t* flag_words, int64_t n_flag_words, const int64_t* end_pos,
-                           const uint64_t* delta_words, int64_t n_delta_words, int64_t n, const SpGroups* gp,
-                           uint64_t* bit_sums, int pass, uint64_t* delta_sums, uint64_t* gpart);
-// k_dec_keys's source of deltas when dw != nullptr: recomputed from the streams (bit_base = the
-// scanned bit_sums, gpart from launch_dec_sums pass 1; `delta` and `gpre` are then unused)
-struct DecStreams {
-    const uint64_t* fw = nullptr;
-    int64_t nfw = 0;
-    const int64_t* end_pos = nullptr;
-    const uint64_t* dw = nullptr;
-    int64_t ndw = 0;
-    const uint64_t* bit_base = nullptr;
-    const uint64_t* gpart = nullptr;
-};
 // keys and MinMax bins; gh: the host copy of *gp (the grid follows the group sizes).  width 8 / 16:
 // tnar is launch_narrow_table's image of `table` (int32 cells outside [0, 2^width - 1) read back
 // from `table`); width 32: `table` alone (nullptr with gp->rows == 0: keys only).  gbins may be
@@ -183,7 +166,7 @@ struct DecStreams {
 hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, const SpGroups* gp, const SpGroups& gh,
                            const uint64_t* tile_base, const uint64_t* gpre, const int32_t* table, const void* tnar,
                            int width, int32_t* gkeys, int32_t* gbins, int nq, void* gbn, int bn_width,
-                           unsigned* err, const DecStreams& ds);
+                           unsigned* err);
 // the narrow (width 8 or 16) image of int32 MinMax tables for k_dec_keys; t32 16-byte aligned
 hipError_t launch_narrow_table(hipStream_t st, const int32_t* t32, int64_t ncells, int width, void* tn);
 // live entries of a restored payload (skml_sparse_decode_sum_f64's toAuto choice)
@@ -231,7 +214,7 @@ static_assert(sizeof(SpBlobHeader) <= 256, "blob header fits its 256-byte sectio
 // bounds = G x (kRsRanges + 1) int32 scratch; info->irregular != 0 after the launches means the
 // input was not regular and the caller must run the merge rounds instead.  vkind 0: out = int32
 // bins; 1: float quantValues[bin]; 2: double quantValues[bin] (qv: nq doubles).
-constexpr int kRsBits = 16, kRsRange = 1 << kRsBits, kRsWords = kRsRange / 32;
+constexpr int kRsBits = 13, kRsRange = 1 << kRsBits, kRsWords = kRsRange / 32;
 constexpr int64_t kRsRanges = (int64_t)1 << (31 - kRsBits);  // key ranges of [0, 2^31)
 struct RsInfo {
     unsigned irregular;          // 1: a run does not ascend / key out of range, 2: a repeated key or bad bin
@@ -336,6 +319,8 @@ hipError_t launch_rd_words(hipStream_t st, const uint8_t* stream, const int64_t*
 hipStream_t ctx_stream(skml_ctx* c);
 // the context's side stream (a high-priority child context) and two events for a fork / join
 int ctx_side_fork(skml_ctx* c, hipStream_t* side, hipEvent_t* fork, hipEvent_t* join);
+// the side context itself (its stream is ctx_side_fork's `side`; nullptr before the first fork)
+skml_ctx* ctx_side_ctx(skml_ctx* c);
 int ctx_device(skml_ctx* c);
 // grow-only device scratch buffer `slot` (< kScratchSlots) of at least `bytes`; null on failure
 constexpr int kScratchSlots = 20;

@@ -2117,6 +2117,18 @@ __device__ __forceinline__ uint32_t get_bits(const uint64_t* words, int64_t nwor
     return __brev(field) >> (32 - nbits);
 }
 
+// The same read from two words already in registers: off in [0, 64) is relative to w0 and
+// off + nbits <= 128.
+__device__ __forceinline__ uint32_t bits_of_window(uint64_t w0, uint64_t w1, int off, int nbits) {
+    if (nbits <= 0) return 0;
+    const uint64_t v = off ? (w0 >> off) | (w1 << (64 - off)) : w0;
+    const uint32_t field = (uint32_t)(v & ((1ull << nbits) - 1ull));
+    return __brev(field) >> (32 - nbits);
+}
+__device__ __forceinline__ uint64_t word_or_zero(const uint64_t* __restrict__ words, int64_t nwords, int64_t w) {
+    return w < nwords ? words[w] : 0ull;
+}
+
 __global__ __launch_bounds__(kSpThreads) void k_dec_lens(const uint64_t* __restrict__ fw, int64_t nfw,
                                                          const int64_t* __restrict__ end_pos, int64_t n,
                                                          const SpGroups* __restrict__ gp, uint8_t* __restrict__ dlen,
@@ -2127,8 +2139,27 @@ __global__ __launch_bounds__(kSpThreads) void k_dec_lens(const uint64_t* __restr
     __syncthreads();
     const int64_t i0 = (int64_t)blockIdx.x * kSpTile + threadIdx.x * 8;
     uint64_t sum = 0;
-    if (i0 < n) {
-        int g = group_of_elem(S, i0);
+    int gf = i0 < n ? group_of_elem(S, i0) : 0;
+    if (i0 + 8 <= n && i0 + 8 <= S[gf + 1] && !gp->kind[gf]) {
+        // the common case: 8 fixed-width flags of one group, at most 40 contiguous bits: two word
+        // loads instead of one or two per element, one 8-byte store of the lengths
+        const DeltaShape s = delta_shape(gp, gf);
+        const int64_t b0 = gp->fb[gf] + (i0 - S[gf]) * s.nf;
+        const int64_t w = b0 >> 6;
+        const int sh = (int)(b0 & 63);
+        const uint64_t w0 = word_or_zero(fw, nfw, w), w1 = word_or_zero(fw, nfw, w + 1);
+        uint64_t packed = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int off = sh + j * s.nf;  // < 64 + 40
+            const uint32_t f = off < 64 ? bits_of_window(w0, w1, off, s.nf) : bits_of_window(w1, 0ull, off - 64, s.nf);
+            const int dl = s.bpi * ((int)f + 1);
+            packed |= (uint64_t)(uint8_t)dl << (8 * j);
+            sum += dl;
+        }
+        *reinterpret_cast<uint64_t*>(dlen + i0) = packed;
+    } else if (i0 < n) {
+        int g = gf;
         DeltaShape s = delta_shape(gp, g);
         for (int j = 0; j < 8; j++) {
             const int64_t i = i0 + j;
@@ -2169,20 +2200,49 @@ __global__ __launch_bounds__(kSpThreads) void k_dec_deltas(const uint64_t* __res
     const int64_t i0 = (int64_t)blockIdx.x * kSpTile + threadIdx.x * 8;
     uint8_t l[8];
     uint64_t sum = 0;
-    for (int j = 0; j < 8; j++) {
-        l[j] = i0 + j < n ? dlen[i0 + j] : 0;
-        sum += l[j];
+    const bool full = i0 + 8 <= n;
+    if (full) {  // one 8-byte load of the lengths
+        const uint64_t pk = *reinterpret_cast<const uint64_t*>(dlen + i0);
+#pragma unroll
+        for (int j = 0; j < 8; j++) l[j] = (uint8_t)(pk >> (8 * j));
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; j++) l[j] = i0 + j < n ? dlen[i0 + j] : 0;
     }
+#pragma unroll
+    for (int j = 0; j < 8; j++) sum += l[j];
     uint64_t v[1] = {sum}, tot[1];
     block_excl_scan<1>(v, tot, sh);
     int64_t off = (int64_t)(tile_base[blockIdx.x] + v[0]);
     uint64_t dsum = 0;
-    for (int j = 0; j < 8; j++) {
-        if (i0 + j >= n) break;
-        const uint32_t d = get_bits(dw, ndw, off, l[j]);
-        delta[i0 + j] = d;
-        dsum += d;
-        off += l[j];
+    if (full) {
+        // the thread's 8 deltas are contiguous, at most 256 bits: five words loaded up front, each
+        // field taken from the two words it straddles
+        const int64_t w = off >> 6;
+        uint64_t W[5];
+#pragma unroll
+        for (int q = 0; q < 5; q++) W[q] = word_or_zero(dw, ndw, w + q);
+        int r = (int)(off & 63);
+        uint32_t d[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int q = r >> 6, o = r & 63;
+            const uint64_t lo = q == 0 ? W[0] : q == 1 ? W[1] : q == 2 ? W[2] : q == 3 ? W[3] : W[4];
+            const uint64_t hi = q == 0 ? W[1] : q == 1 ? W[2] : q == 2 ? W[3] : q == 3 ? W[4] : 0ull;
+            d[j] = bits_of_window(lo, hi, o, l[j]);
+            dsum += d[j];
+            r += l[j];
+        }
+        *reinterpret_cast<uint4*>(delta + i0) = make_uint4(d[0], d[1], d[2], d[3]);
+        *reinterpret_cast<uint4*>(delta + i0 + 4) = make_uint4(d[4], d[5], d[6], d[7]);
+    } else {
+        for (int j = 0; j < 8; j++) {
+            if (i0 + j >= n) break;
+            const uint32_t d = get_bits(dw, ndw, off, l[j]);
+            delta[i0 + j] = d;
+            dsum += d;
+            off += l[j];
+        }
     }
     uint64_t v2[1] = {dsum}, tot2[1];
     block_excl_scan<1>(v2, tot2, sh);
@@ -2197,118 +2257,6 @@ hipError_t launch_dec_deltas(hipStream_t st, const uint64_t* delta_words, int64_
     if (tiles <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_dec_deltas, dim3((unsigned)tiles), dim3(kSpThreads), 0, st, delta_words, n_delta_words,
                        dlen, n, tile_base, delta, tile_sums);
-    return hipGetLastError();
-}
-
-// ---- the same stream passes without materialised lengths / deltas (the default) ----
-// k_dec_lsum: per 2,048-element tile, the sum of the delta bit lengths (reads the flag stream
-// only); k_dec_dsum: per tile, the deltas' sum and each group's in-tile delta prefix at its first
-// element (bit offsets from the scanned length sums); k_dec_keys then recomputes the lengths and
-// deltas of its own elements from the streams.  Neither the 1-byte lengths nor the 4-byte deltas
-// go through memory, and k_dec_lens / k_dec_deltas / k_group_prefix do not run.
-__device__ __forceinline__ int dec_len_of(const uint64_t* __restrict__ fw, int64_t nfw,
-                                          const int64_t* __restrict__ end_pos, const SpGroups* __restrict__ gp,
-                                          const DeltaShape& s, int g, int64_t i, int64_t sg) {
-    int iv;
-    if (!s.kind) {
-        iv = (int)get_bits(fw, nfw, gp->fb[g] + (i - sg) * s.nf, s.nf) + 1;
-    } else {
-        const int64_t start = i == sg ? gp->fb[g] : end_pos[i - 1] + 1;
-        iv = (int)(end_pos[i] - start);
-    }
-    return s.bpi * iv;
-}
-
-__global__ __launch_bounds__(kSpThreads) void k_dec_lsum(const uint64_t* __restrict__ fw, int64_t nfw,
-                                                         const int64_t* __restrict__ end_pos, int64_t n,
-                                                         const SpGroups* __restrict__ gp,
-                                                         uint64_t* __restrict__ tile_sums) {
-    __shared__ int64_t S[kMaxGroups + 1];
-    __shared__ uint64_t sh[4];
-    load_starts(gp, S);
-    __syncthreads();
-    const int64_t i0 = (int64_t)blockIdx.x * kSpTile + threadIdx.x * 8;
-    uint64_t sum = 0;
-    if (i0 < n) {
-        int g = group_of_elem(S, i0);
-        DeltaShape s = delta_shape(gp, g);
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const int64_t i = i0 + j;
-            if (i >= n) break;
-            while (i >= S[g + 1]) s = delta_shape(gp, ++g);
-            sum += (uint64_t)dec_len_of(fw, nfw, end_pos, gp, s, g, i, S[g]);
-        }
-    }
-    uint64_t v[1] = {sum}, tot[1];
-    block_excl_scan<1>(v, tot, sh);
-    if (threadIdx.x == 0) tile_sums[blockIdx.x] = tot[0];
-}
-
-__global__ __launch_bounds__(kSpThreads) void k_dec_dsum(const uint64_t* __restrict__ fw, int64_t nfw,
-                                                         const int64_t* __restrict__ end_pos,
-                                                         const uint64_t* __restrict__ dw, int64_t ndw, int64_t n,
-                                                         const SpGroups* __restrict__ gp,
-                                                         const uint64_t* __restrict__ bit_base,
-                                                         uint64_t* __restrict__ tile_sums, uint64_t* __restrict__ gpart) {
-    __shared__ int64_t S[kMaxGroups + 1];
-    __shared__ uint64_t sh[4];
-    load_starts(gp, S);
-    __syncthreads();
-    const int64_t i0 = (int64_t)blockIdx.x * kSpTile + threadIdx.x * 8;
-    int l[8];
-    uint64_t sum = 0;
-    int g0 = 0;
-#pragma unroll
-    for (int j = 0; j < 8; j++) l[j] = 0;
-    if (i0 < n) {
-        int g = g0 = group_of_elem(S, i0);
-        DeltaShape s = delta_shape(gp, g);
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const int64_t i = i0 + j;
-            if (i >= n) break;
-            while (i >= S[g + 1]) s = delta_shape(gp, ++g);
-            l[j] = dec_len_of(fw, nfw, end_pos, gp, s, g, i, S[g]);
-            sum += (uint64_t)l[j];
-        }
-    }
-    uint64_t v[1] = {sum}, tot[1];
-    block_excl_scan<1>(v, tot, sh);
-    int64_t off = (int64_t)(bit_base[blockIdx.x] + v[0]);
-    uint32_t d[8];
-    uint64_t dsum = 0;
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-        d[j] = i0 + j < n ? get_bits(dw, ndw, off, l[j]) : 0u;
-        dsum += d[j];
-        off += l[j];
-    }
-    uint64_t v2[1] = {dsum}, tot2[1];
-    block_excl_scan<1>(v2, tot2, sh);
-    if (threadIdx.x == 0) tile_sums[blockIdx.x] = tot2[0];
-    if (i0 < n) {  // groups whose first element is one of this thread's: their in-tile delta prefix
-        for (int g = g0; g < gp->G && S[g] < i0 + 8 && S[g] < n; g++) {
-            if (S[g] < i0) continue;
-            uint64_t part = v2[0];
-#pragma unroll
-            for (int j = 0; j < 8; j++) part += i0 + j < S[g] ? d[j] : 0u;
-            gpart[g] = part;
-        }
-    }
-}
-
-hipError_t launch_dec_sums(hipStream_t st, const uint64_t* flag_words, int64_t n_flag_words, const int64_t* end_pos,
-                           const uint64_t* delta_words, int64_t n_delta_words, int64_t n, const SpGroups* gp,
-                           uint64_t* bit_sums, int pass, uint64_t* delta_sums, uint64_t* gpart) {
-    const int64_t tiles = sp_tiles(n, kSpTile);
-    if (tiles <= 0) return hipSuccess;
-    if (pass == 0)
-        hipLaunchKernelGGL(k_dec_lsum, dim3((unsigned)tiles), dim3(kSpThreads), 0, st, flag_words, n_flag_words, end_pos,
-                           n, gp, bit_sums);
-    else
-        hipLaunchKernelGGL(k_dec_dsum, dim3((unsigned)tiles), dim3(kSpThreads), 0, st, flag_words, n_flag_words, end_pos,
-                           delta_words, n_delta_words, n, gp, bit_sums, delta_sums, gpart);
     return hipGetLastError();
 }
 
@@ -2384,9 +2332,7 @@ __device__ __forceinline__ int64_t dec_tile_of_block(const int64_t* S, int G, in
 // keys: group-restarted prefix sums of the deltas (Java int wrap); bins: MinMaxSketch.query
 // (MinMaxSketch.java:64-73): the row value farthest from zero, the first row on ties.  TN: the
 // narrow table's cell type (int32_t: the int32 table itself).  512 threads per 2,048-element tile,
-// 4 consecutive elements per thread (16-byte key stores); the deltas come from `delta` or, by
-// default, from the streams themselves (DecStreams).  MODE 1 needs 65 VGPRs (3 workgroups per
-// CU), MODE 0 81.
+// 4 consecutive elements per thread (16-byte delta loads and key stores).
 constexpr int kDecThreads = 512;
 static_assert(kDecThreads * 4 == kSpTile, "dec_keys tile");
 // MODE 1: the default shape (2 rows), tiles inside one group only (a tile across a group edge
@@ -2403,14 +2349,13 @@ template <typename TN, int MODE>
 __global__ __launch_bounds__(kDecThreads) void k_dec_keys(const uint32_t* __restrict__ delta, int64_t n,
                                                           const SpGroups* __restrict__ gp,
                                                           const uint64_t* __restrict__ tile_base,
-                                                          const uint64_t* gpre,
+                                                          const uint64_t* __restrict__ gpre,
                                                           const int32_t* __restrict__ table, const TN* __restrict__ tnar,
                                                           int32_t* __restrict__ gkeys, int32_t* __restrict__ gbins,
                                                           int nq, void* __restrict__ gbn, int bn_width,
-                                                          unsigned* __restrict__ err, DecEdgeTiles edges, DecStreams ds) {
+                                                          unsigned* __restrict__ err, DecEdgeTiles edges) {
     __shared__ int64_t S[kMaxGroups + 1];
     __shared__ uint64_t sh[kDecThreads / 64];
-    __shared__ uint64_t GPRE[kMaxGroups];
     load_starts(gp, S);
     __syncthreads();
     const int64_t tile = edges.n > 0 ? edges.t[blockIdx.x] : dec_tile_of_block(S, gp->G, blockIdx.x);
@@ -2422,35 +2367,7 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_keys(const uint32_t* __rest
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int64_t i0 = tile * kSpTile + t * 4;
     uint32_t d[4];
-    if (ds.dw) {  // lengths from the flags, deltas from the delta stream (k_dec_lsum / k_dec_dsum)
-        if (t < gp->G) GPRE[t] = S[t] < n ? tile_base[S[t] / kSpTile] + ds.gpart[t] : 0ull;
-        int l[4] = {0, 0, 0, 0};
-        uint64_t lsum = 0;
-        if (i0 < n) {
-            int g = group_of_elem(S, i0);
-            DeltaShape s = delta_shape(gp, g);
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const int64_t i = i0 + j;
-                if (i >= n) break;
-                while (i >= S[g + 1]) s = delta_shape(gp, ++g);
-                l[j] = dec_len_of(ds.fw, ds.nfw, ds.end_pos, gp, s, g, i, S[g]);
-                lsum += (uint64_t)l[j];
-            }
-        }
-        const uint64_t linc = wave_incl_u64(lsum, lane);
-        if (lane == 63) sh[w] = linc;
-        __syncthreads();
-        int64_t off = (int64_t)(ds.bit_base[tile] + linc - lsum);
-#pragma unroll
-        for (int j = 0; j < kDecThreads / 64; j++) off += j < w ? (int64_t)sh[j] : 0;
-        __syncthreads();  // sh is reused by the delta scan
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            d[j] = i0 + j < n ? get_bits(ds.dw, ds.ndw, off, l[j]) : 0u;
-            off += l[j];
-        }
-    } else if (i0 + 4 <= n) {
+    if (i0 + 4 <= n) {
         const uint4 v = *reinterpret_cast<const uint4*>(delta + i0);
         d[0] = v.x, d[1] = v.y, d[2] = v.z, d[3] = v.w;
     } else {
@@ -2477,7 +2394,7 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_keys(const uint32_t* __rest
             while (i >= S[g + 1]) g++;
         p += d[j];
         grp[j] = g;
-        key[j] = (int32_t)(uint32_t)(p - (ds.dw ? GPRE[g] : gpre[g]));
+        key[j] = (int32_t)(uint32_t)(p - gpre[g]);
         res[j] = zero;
     }
     constexpr uint32_t kTop = sizeof(TN) == 4 ? 0u : (uint32_t)(TN)~(TN)0;
@@ -2608,7 +2525,7 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_keys(const uint32_t* __rest
 hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, const SpGroups* gp, const SpGroups& gh,
                            const uint64_t* tile_base, const uint64_t* gpre, const int32_t* table, const void* tnar,
                            int width, int32_t* gkeys, int32_t* gbins, int nq, void* gbn, int bn_width,
-                           unsigned* err, const DecStreams& ds) {
+                           unsigned* err) {
     if (sp_tiles(n, kSpTile) <= 0) return hipSuccess;
     int64_t per[8] = {};  // tiles per XCD slot (dec_tile_of_block)
     for (int g = 0; g < gh.G; g++) {
@@ -2634,7 +2551,7 @@ hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, con
     }
 #define SKML_DEC_LAUNCH(TNT, MODE, GRID, TILES, TNPTR)                                                            \
     hipLaunchKernelGGL((k_dec_keys<TNT, MODE>), dim3(GRID), dim3(kDecThreads), 0, st, delta, n, gp, tile_base, gpre, \
-                       table, TNPTR, gkeys, gbins, nq, gbn, bn_width, err, TILES, ds)
+                       table, TNPTR, gkeys, gbins, nq, gbn, bn_width, err, TILES)
 #define SKML_DEC_WIDTH(TNT, TNPTR)                                                          \
     do {                                                                                  \
         if (batched) {                                                                    \
@@ -2836,7 +2753,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_tiles(const AggPayload* __r
 // tile one after the other in payload order (one barrier per payload; keys are unique within a
 // payload).  Up to kAggWPer elements per lane are held in registers, a longer payload (a dense
 // form, or a tile far denser than the mean) adds the rest in further rounds of its turn.
-constexpr int kAggWPer = 16;
+constexpr int kAggWPer = 8;
 __global__ __launch_bounds__(kAggThreads) void k_agg_tiles_w(const AggPayload* __restrict__ pays, int P,
                                                             int64_t ntiles, int64_t dim, double* __restrict__ out,
                                                             int from_out, double scale, unsigned* __restrict__ err) {
@@ -2845,62 +2762,75 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_tiles_w(const AggPayload* _
     __shared__ double qt[kAggPB][kAggLdsValues];
     __shared__ int32_t rb[kAggPB][kMaxGroups + 1];  // run prefix (elements) per group, this tile
     __shared__ int32_t rs[kAggPB][kMaxGroups];      // run start (element index in the payload)
-    const int64_t t = blockIdx.x;
-    const int64_t k0 = t * kAggTile, nk = std::min<int64_t>(kAggTile, dim - k0);
+    __shared__ int32_t dfs[kAggPB];                 // dense_form of the batch's payloads
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int x = threadIdx.x; x < kAggTile; x += kAggThreads) acc[x] = (from_out && x < nk) ? out[k0 + x] : 0.0;
-    unsigned bad = 0;
-    for (int p0 = 0; p0 < P; p0 += kAggPB) {
-        const int np = std::min(kAggPB, P - p0);
-        __syncthreads();  // the previous batch is done with qt / rb / rs
-        AggPayload a{};
-        const bool mine = wave < np;
-        if (mine) a = pays[p0 + wave];
-        if (mine) {
+    // a persistent grid: with one batch (P <= kAggPB) the payloads and their quantValues are read
+    // once per workgroup instead of once per tile
+    const bool one_batch = P <= kAggPB;
+    AggPayload a{};
+    auto load_batch = [&](int p0, int np) {
+        if (wave < np) {
+            a = pays[p0 + wave];
             for (int b = lane; b < kAggLdsValues; b += 64)
                 if (a.nq <= kAggLdsValues && b < a.nq) qt[wave][b] = a.qv[b];
-            int32_t len = 0;
-            if (lane < a.G) {
-                const int32_t* bd = a.bounds + (int64_t)lane * (ntiles + 1);
-                const int32_t b0 = bd[t], b1 = bd[t + 1];
-                len = b1 > b0 ? b1 - b0 : 0;
-                rs[wave][lane] = b0;
-            }
-            int32_t x = len;
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const int32_t y = __shfl_up(x, off, 64);
-                if (lane >= off) x += y;
-            }
-            if (lane < kMaxGroups) rb[wave][lane + 1] = x;
-            if (lane == 0) rb[wave][0] = 0;
+            if (lane == 0) dfs[wave] = a.dense_form;
         }
-        __syncthreads();
-        // this wave's elements: compact index j = lane + 64 u over the concatenated runs; the run
-        // holding j by a walk over the (few) run prefixes
-        const int total = mine ? rb[wave][a.G] : 0;
-        const bool lds_q = a.nq <= kAggLdsValues;
-        int32_t kk[kAggWPer];
-        double vv[kAggWPer];
+    };
+    if (one_batch) load_batch(0, P);
+    unsigned bad = 0;
+    for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int64_t k0 = t * kAggTile, nk = std::min<int64_t>(kAggTile, dim - k0);
+        __syncthreads();  // the previous tile's stores have read acc
+        for (int x = threadIdx.x; x < kAggTile; x += kAggThreads) acc[x] = (from_out && x < nk) ? out[k0 + x] : 0.0;
+        for (int p0 = 0; p0 < P; p0 += kAggPB) {
+            const int np = std::min(kAggPB, P - p0);
+            __syncthreads();  // the previous batch is done with qt / rb / rs
+            if (!one_batch) load_batch(p0, np);
+            const bool mine = wave < np;
+            if (mine) {
+                int32_t len = 0;
+                if (lane < a.G) {
+                    const int32_t* bd = a.bounds + (int64_t)lane * (ntiles + 1);
+                    const int32_t b0 = bd[t], b1 = bd[t + 1];
+                    len = b1 > b0 ? b1 - b0 : 0;
+                    rs[wave][lane] = b0;
+                }
+                int32_t x = len;
 #pragma unroll
-        for (int u = 0; u < kAggWPer; u++) {
-            const int j = lane + 64 * u;
-            kk[u] = 0;
-            vv[u] = 0.0;
-            if (j < total) {
-                int g = 0;
-                while (rb[wave][g + 1] <= j) g++;
-                const int64_t i = (int64_t)rs[wave][g] + (j - rb[wave][g]);
-                kk[u] = a.gk[i];
-                const uint32_t b = a.bw == 1 ? static_cast<const uint8_t*>(a.gb)[i] : static_cast<const uint16_t*>(a.gb)[i];
-                vv[u] = lds_q ? qt[wave][b] : a.qv[b];
+                for (int off = 1; off < 64; off <<= 1) {
+                    const int32_t y = __shfl_up(x, off, 64);
+                    if (lane >= off) x += y;
+                }
+                if (lane < kMaxGroups) rb[wave][lane + 1] = x;
+                if (lane == 0) rb[wave][0] = 0;
             }
-        }
-        for (int pl = 0; pl < np; pl++) {
-            if (wave == pl) {
-                const bool dform = a.dense_form != 0;
-                // a key outside this tile is an error (k_agg_bounds placed it here); the dense form
-                // keeps |v| > EPS only (SparseDoubleGradient.toDense)
+            __syncthreads();
+            // this wave's elements: compact index j = lane + 64 u over the concatenated runs; the run
+            // holding j by a walk over the (few) run prefixes
+            const int total = mine ? rb[wave][a.G] : 0;
+            const bool lds_q = a.nq <= kAggLdsValues;
+            int32_t kk[kAggWPer];
+            double vv[kAggWPer];
+#pragma unroll
+            for (int u = 0; u < kAggWPer; u++) {
+                const int j = lane + 64 * u;
+                kk[u] = 0;
+                vv[u] = 0.0;
+                if (j < total) {
+                    int g = 0;
+                    while (rb[wave][g + 1] <= j) g++;
+                    const int64_t i = (int64_t)rs[wave][g] + (j - rb[wave][g]);
+                    kk[u] = a.gk[i];
+                    const uint32_t b =
+                        a.bw == 1 ? static_cast<const uint8_t*>(a.gb)[i] : static_cast<const uint16_t*>(a.gb)[i];
+                    vv[u] = lds_q ? qt[wave][b] : a.qv[b];
+                }
+            }
+            for (int pl = 0; pl < np; pl++) {
+                if (wave == pl) {
+                    const bool dform = a.dense_form != 0;
+                    // a key outside this tile is an error (k_agg_bounds placed it here); the dense form
+                    // keeps |v| > EPS only (SparseDoubleGradient.toDense)
 #define SKML_AGG_ADD(K, V)                                              \
     do {                                                                \
         const int32_t k_ = (K);                                         \
@@ -2909,40 +2839,56 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_tiles_w(const AggPayload* _
         else if (!dform || fabs(v_) > 1e-8) acc[k_ - k0] += v_;         \
     } while (0)
 #pragma unroll
-                for (int u = 0; u < kAggWPer; u++)
-                    if (lane + 64 * u < total) SKML_AGG_ADD(kk[u], vv[u]);
-                for (int j = lane + 64 * kAggWPer; j < total; j += 64) {  // the rest of a long payload
-                    int g = 0;
-                    while (rb[wave][g + 1] <= j) g++;
-                    const int64_t i = (int64_t)rs[wave][g] + (j - rb[wave][g]);
-                    const uint32_t b =
-                        a.bw == 1 ? static_cast<const uint8_t*>(a.gb)[i] : static_cast<const uint16_t*>(a.gb)[i];
-                    SKML_AGG_ADD(a.gk[i], lds_q ? qt[wave][b] : a.qv[b]);
-                }
+                    for (int u = 0; u < kAggWPer; u++)
+                        if (lane + 64 * u < total) SKML_AGG_ADD(kk[u], vv[u]);
+                    for (int j = lane + 64 * kAggWPer; j < total; j += 64) {  // the rest of a long payload
+                        int g = 0;
+                        while (rb[wave][g + 1] <= j) g++;
+                        const int64_t i = (int64_t)rs[wave][g] + (j - rb[wave][g]);
+                        const uint32_t b =
+                            a.bw == 1 ? static_cast<const uint8_t*>(a.gb)[i] : static_cast<const uint16_t*>(a.gb)[i];
+                        SKML_AGG_ADD(a.gk[i], lds_q ? qt[wave][b] : a.qv[b]);
+                    }
 #undef SKML_AGG_ADD
-            }
-            __syncthreads();
-            if (pays[p0 + pl].dense_form) {  // the dense form adds +0.0 elsewhere: -0.0 sums become +0.0
-                for (int x = threadIdx.x; x < kAggTile; x += kAggThreads)
-                    if (__double_as_longlong(acc[x]) == (long long)0x8000000000000000ull) acc[x] = 0.0;
+                }
                 __syncthreads();
+                if (dfs[pl]) {  // the dense form adds +0.0 elsewhere: -0.0 sums become +0.0
+                    for (int x = threadIdx.x; x < kAggTile; x += kAggThreads)
+                        if (__double_as_longlong(acc[x]) == (long long)0x8000000000000000ull) acc[x] = 0.0;
+                    __syncthreads();
+                }
             }
         }
+        __syncthreads();
+        for (int x = threadIdx.x; x < nk; x += kAggThreads)
+            out[k0 + x] = scale == 1.0 ? acc[x] : __dmul_rn(acc[x], scale);
     }
     if (bad) atomicOr(err, 1u);
-    __syncthreads();
-    for (int x = threadIdx.x; x < nk; x += kAggThreads) out[k0 + x] = scale == 1.0 ? acc[x] : __dmul_rn(acc[x], scale);
 }
 
 hipError_t launch_agg_tiles(hipStream_t st, const AggPayload* pays, int P, int64_t ntiles, int64_t dim, double* out,
                             int from_out, double scale, unsigned* err) {
     if (ntiles <= 0) return hipSuccess;
-    if (std::getenv("SKML_AGG_SEARCH") != nullptr)  // A/B switch: the per-element search form
+    const char* form = std::getenv("SKML_AGG_FORM");  // A/B switch: "s" = the per-element search form
+    if (std::getenv("SKML_AGG_SEARCH") != nullptr || (form && form[0] == 's'))
         hipLaunchKernelGGL(k_agg_tiles, dim3((unsigned)ntiles), dim3(kAggThreads), 0, st, pays, P, ntiles, dim, out,
                            from_out, scale, err);
-    else
-        hipLaunchKernelGGL(k_agg_tiles_w, dim3((unsigned)ntiles), dim3(kAggThreads), 0, st, pays, P, ntiles, dim, out,
-                           from_out, scale, err);
+    else {  // persistent: as many workgroups as are resident at once
+        static int resident = 0;
+        if (!resident) {
+            int dev = 0, per_cu = 0;
+            hipDeviceProp_t prop;
+            if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess ||
+                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_agg_tiles_w, kAggThreads, 0) != hipSuccess)
+                return hipGetLastError();
+            resident = std::max(1, per_cu) * prop.multiProcessorCount;
+        }
+        // (A/B switch: SKML_AGG_GRID_ALL = one workgroup per tile)
+        const unsigned grid =
+            (unsigned)(std::getenv("SKML_AGG_GRID_ALL") != nullptr ? ntiles : std::min<int64_t>(ntiles, resident));
+        hipLaunchKernelGGL(k_agg_tiles_w, dim3(grid), dim3(kAggThreads), 0, st, pays, P, ntiles, dim, out, from_out,
+                           scale, err);
+    }
     return hipGetLastError();
 }
 
@@ -3179,18 +3125,17 @@ __device__ __forceinline__ V rs_value(int32_t b, const V* lut, const double* qv,
     }
 }
 
-constexpr int kRsThreads = 256, kRsBatch = 4, kRsLut = 2048;
-static_assert(kRsWords % kRsThreads == 0, "bitmap words per thread");
+constexpr int kRsThreads = 256, kRsBatch = 4, kRsLut = 1024;
+static_assert(kRsWords == kRsThreads, "one bitmap word per thread");
 template <typename V>
 __global__ __launch_bounds__(kRsThreads) void k_rs_merge(const int32_t* __restrict__ gk, const int32_t* __restrict__ gb,
                                                          const SpGroups* __restrict__ gp,
                                                          const int32_t* __restrict__ bounds, RsInfo* __restrict__ info,
                                                          int32_t* __restrict__ keys_out, V* __restrict__ out,
                                                          const double* __restrict__ qv, int nq) {
-    constexpr int kWordsPer = kRsWords / kRsThreads;
     constexpr int kLut = std::is_same<V, int32_t>::value ? 1 : kRsLut;
     __shared__ uint32_t bm[kRsWords];
-    __shared__ uint32_t wp[kRsWords];
+    __shared__ int32_t slot[kRsRange];  // the bin of the key at each offset of the range
     __shared__ int64_t S[kMaxGroups + 1];
     __shared__ int64_t lo_s[kMaxGroups];
     __shared__ int32_t pre[kMaxGroups + 1];
@@ -3207,7 +3152,7 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_merge(const int32_t* __restri
     constexpr int64_t ld = kRsRanges + 1;
     unsigned bad = 0;
     for (int64_t t = blockIdx.x; t <= tmax; t += gridDim.x) {
-        __syncthreads();  // S / lut loaded; the previous range is done with bm / wp / pre
+        __syncthreads();  // S / lut loaded; the previous range is done with bm / slot / pre
         if (w == 0) {  // lane g: run g's piece of this range
             int64_t lo = 0, len = 0, before = 0;
             if (lane < G) {
@@ -3235,55 +3180,12 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_merge(const int32_t* __restri
             for (int off = 32; off >= 1; off >>= 1) before += __shfl_xor(before, off, 64);
             if (lane == 0) obase = before;
         }
-        for (int j = t_; j < kRsWords; j += kRsThreads) bm[j] = 0;
+        bm[t_] = 0;
         __syncthreads();
         const int cnt = pre[G];
         if (cnt == 0) continue;  // workgroup-uniform
-        // pass 1: the range's keys into the bitmap (4 loads in flight per thread)
-        for (int j0 = 0; j0 < cnt; j0 += kRsThreads * kRsBatch) {
-            int32_t kk[kRsBatch];
-#pragma unroll
-            for (int u = 0; u < kRsBatch; u++) {
-                const int j = j0 + u * kRsThreads + t_;
-                kk[u] = -1;
-                if (j < cnt) {
-                    const int g = agg_search32(pre, G, j);
-                    kk[u] = gk[lo_s[g] + (j - pre[g])];
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < kRsBatch; u++) {
-                if (kk[u] < 0) continue;
-                const uint32_t off = (uint32_t)kk[u] & (kRsRange - 1), bit = 1u << (off & 31);
-                if (atomicOr(&bm[off >> 5], bit) & bit) bad = 1;  // a repeated key
-            }
-        }
-        __syncthreads();
-        // exclusive prefix of the words' popcounts: thread t_ owns words [t_ * kWordsPer, +kWordsPer)
-        uint32_t pc[kWordsPer], own = 0;
-#pragma unroll
-        for (int q = 0; q < kWordsPer; q++) {
-            pc[q] = __popc(bm[t_ * kWordsPer + q]);
-            own += pc[q];
-        }
-        uint32_t inc = own;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t y = __shfl_up(inc, off, 64);
-            if (lane >= off) inc += y;
-        }
-        if (lane == 63) wsum[w] = inc;
-        __syncthreads();
-        uint32_t run = inc - own;
-        for (int q = 0; q < w; q++) run += wsum[q];
-#pragma unroll
-        for (int q = 0; q < kWordsPer; q++) {
-            wp[t_ * kWordsPer + q] = run;
-            run += pc[q];
-        }
-        __syncthreads();
-        // pass 2: each element to base + rank
-        const int64_t ob = obase;
+        // pass 1: the range's keys into the bitmap, their bins into the offset slots (4 loads of
+        // each in flight per thread)
         for (int j0 = 0; j0 < cnt; j0 += kRsThreads * kRsBatch) {
             int32_t kk[kRsBatch], bb[kRsBatch];
 #pragma unroll
@@ -3300,11 +3202,32 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_merge(const int32_t* __restri
 #pragma unroll
             for (int u = 0; u < kRsBatch; u++) {
                 if (kk[u] < 0) continue;
-                const uint32_t off = (uint32_t)kk[u] & (kRsRange - 1);
-                const uint32_t r = wp[off >> 5] + __popc(bm[off >> 5] & ((1u << (off & 31)) - 1u));
-                keys_out[ob + r] = kk[u];
-                out[ob + r] = rs_value<V>(bb[u], lut, qv, nq, lds, bad);
+                const uint32_t off = (uint32_t)kk[u] & (kRsRange - 1), bit = 1u << (off & 31);
+                if (atomicOr(&bm[off >> 5], bit) & bit) bad = 1;  // a repeated key
+                slot[off] = bb[u];
             }
+        }
+        __syncthreads();
+        // pass 2: thread t_ owns bitmap word t_, i.e. the keys t * kRsRange + 32 t_ + [0, 32): its
+        // set bits go out in key order from its exclusive popcount prefix
+        const uint32_t word = bm[t_];
+        const uint32_t own = __popc(word);
+        uint32_t inc = own;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(inc, off, 64);
+            if (lane >= off) inc += y;
+        }
+        if (lane == 63) wsum[w] = inc;
+        __syncthreads();
+        uint32_t run = inc - own;
+        for (int q = 0; q < w; q++) run += wsum[q];
+        int64_t o = obase + run;
+        const int32_t kbase = (int32_t)(t * kRsRange) + 32 * t_;
+        for (uint32_t m = word; m; m &= m - 1, o++) {
+            const int b = __ffs(m) - 1;
+            keys_out[o] = kbase + b;
+            out[o] = rs_value<V>(slot[32 * t_ + b], lut, qv, nq, lds, bad);
         }
     }
     if (bad) atomicOr(&info->irregular, 2u);

@@ -614,34 +614,14 @@ int decode_groups(skml_ctx* c, const skml_sparse* s, int32_t* gk, int32_t* gb, b
     uint64_t* gpre = scratch<uint64_t>(c, kSlotSmall, kMaxGroups + 8);
     if (!ts || !gpre) return sfail(SKML_E_OOM, "decode scratch");
     uint64_t* ts2 = ts + (tiles + 1);
-    uint32_t* delta = nullptr;
-    DecStreams ds;
-    // A/B switch: SKML_DEC_MATERIALIZE keeps the lengths and deltas in memory (k_dec_lens,
-    // k_dec_deltas, k_group_prefix); by default k_dec_keys recomputes them from the streams
-    if (std::getenv("SKML_DEC_MATERIALIZE") != nullptr) {
-        uint8_t* dlen = scratch<uint8_t>(c, kSlotNeed, (size_t)n);
-        delta = scratch<uint32_t>(c, kSlotDelta, (size_t)n);
-        if (!dlen || !delta) return sfail(SKML_E_OOM, "decode scratch");
-        SP_HIP(launch_dec_lens(st, s->flag_words, s->n_flag_words, end_pos, n, s->g_dev, dlen, ts));
-        if (int e = scan_tiles(c, ts, tiles, 1, nullptr)) return e;
-        SP_HIP(launch_dec_deltas(st, s->delta_words, s->n_delta_words, dlen, n, s->g_dev, ts, delta, ts2));
-        if (int e = scan_tiles(c, ts2, tiles, 1, nullptr)) return e;
-        SP_HIP(launch_group_prefix(st, delta, n, s->g_dev, G.G, ts2, gpre));
-    } else {
-        SP_HIP(launch_dec_sums(st, s->flag_words, s->n_flag_words, end_pos, s->delta_words, s->n_delta_words, n,
-                               s->g_dev, ts, 0, nullptr, nullptr));
-        if (int e = scan_tiles(c, ts, tiles, 1, nullptr)) return e;
-        SP_HIP(launch_dec_sums(st, s->flag_words, s->n_flag_words, end_pos, s->delta_words, s->n_delta_words, n,
-                               s->g_dev, ts, 1, ts2, gpre));
-        if (int e = scan_tiles(c, ts2, tiles, 1, nullptr)) return e;
-        ds.fw = s->flag_words;
-        ds.nfw = s->n_flag_words;
-        ds.end_pos = end_pos;
-        ds.dw = s->delta_words;
-        ds.ndw = s->n_delta_words;
-        ds.bit_base = ts;
-        ds.gpart = gpre;
-    }
+    uint8_t* dlen = scratch<uint8_t>(c, kSlotNeed, (size_t)n);
+    uint32_t* delta = scratch<uint32_t>(c, kSlotDelta, (size_t)n);
+    if (!dlen || !delta) return sfail(SKML_E_OOM, "decode scratch");
+    SP_HIP(launch_dec_lens(st, s->flag_words, s->n_flag_words, end_pos, n, s->g_dev, dlen, ts));
+    if (int e = scan_tiles(c, ts, tiles, 1, nullptr)) return e;
+    SP_HIP(launch_dec_deltas(st, s->delta_words, s->n_delta_words, dlen, n, s->g_dev, ts, delta, ts2));
+    if (int e = scan_tiles(c, ts2, tiles, 1, nullptr)) return e;
+    SP_HIP(launch_group_prefix(st, delta, n, s->g_dev, G.G, ts2, gpre));
     // the query gathers from a byte (binNum <= 256) or 16-bit image of the tables
     const int32_t* tab = query ? s->tables : nullptr;
     int width = 32;
@@ -653,7 +633,7 @@ int decode_groups(skml_ctx* c, const skml_sparse* s, int32_t* gk, int32_t* gb, b
         SP_HIP(launch_narrow_table(st, tab, s->ncells, width, tnar));
     }
     SP_HIP(launch_dec_keys(st, delta, n, s->g_dev, G, ts2, gpre, tab, tnar, width, gk, gb, dv ? dv->nq : 0,
-                           dv ? dv->gb : nullptr, dv ? dv->bw : 0, dv ? dv->err : nullptr, ds));
+                           dv ? dv->gb : nullptr, dv ? dv->bw : 0, dv ? dv->err : nullptr));
     return SKML_OK;
 }
 
@@ -697,12 +677,12 @@ int merge_groups(skml_ctx* c, const skml_sparse* s, int32_t* gk, int32_t* gb, in
     return SKML_OK;
 }
 
+thread_local int t_merge_path = 0;  // skml_debug_sparse_merge_path
+
 // Sort.merge's one-pass form (launch_rs_merge) into keys_out and out (vkind: 0 int32 bins, 1 float /
 // 2 double quantValues[bin]).  *pending: a pinned word that is non-zero after the stream
 // synchronises if the input was not regular and merge_groups must run instead; nullptr when the
 // one-pass form did not run (one run, or SKML_RS_ROUNDS set: the rounds' A/B switch).
-thread_local int t_merge_path = 0;  // skml_debug_sparse_merge_path
-
 int rs_merge_start(skml_ctx* c, const skml_sparse* s, const int32_t* gk, const int32_t* gb, int32_t* keys_out,
                    void* out, int vkind, const double* qv, int nq, volatile unsigned** pending) {
     *pending = nullptr;
@@ -1927,10 +1907,26 @@ int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t
         int32_t* bounds = scratch<int32_t>(c, kSlotCells, (size_t)nb);
         if (!gk || !gbn || !bounds) return sfail(SKML_E_OOM, "decode_sum scratch (%lld keys)", (long long)nk);
         SP_HIP(hipMemsetAsync(bounds, 0, sizeof(int32_t) * (size_t)nb, st));  // empty groups: every bound 0
+        // two lanes: payloads alternate between the caller's stream and the side context's (each
+        // restore is a chain of small latency-bound kernels; two chains fill the chip better),
+        // joined before the tiles; SKML_SERIAL, SKML_AGG_ONE_LANE or a single payload keep one lane
+        skml_ctx* lanes[2] = {c, nullptr};
+        hipStream_t side_st = nullptr;
+        hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+        if (end - at > 1 && std::getenv("SKML_AGG_ONE_LANE") == nullptr &&  // (the A/B switch)
+            ctx_side_fork(c, &side_st, &ev_fork, &ev_join) == SKML_OK) {
+            lanes[1] = ctx_side_ctx(c);
+            SP_HIP(hipEventRecord(ev_fork, st));
+            SP_HIP(hipStreamWaitEvent(side_st, ev_fork, 0));
+        }
         std::vector<AggPayload> pays;
         int64_t ko = 0, bo = 0;
         for (size_t q = at; q < end; q++) {
             const int p = todo[q];
+            const int li = lanes[1] && ((q - at) & 1) ? 1 : 0;
+            skml_ctx* lc = lanes[li];
+            hipStream_t ls = ctx_stream(lc);
+            uint64_t* llive = live + li;
             const skml_sparse& v = views[(size_t)p];
             AggPayload a{};
             a.gk = gk + ko;
@@ -1943,17 +1939,31 @@ int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t
             a.bounds = bounds + bo;
             a.G = v.g.G;
             const DecodeValues dv{a.nq, const_cast<void*>(a.gb), a.bw, err};
-            if (int e = decode_groups(c, &v, gk + ko, nullptr, true, &dv)) return e;
+            auto join = [&](int e) {  // an error after the fork: the caller's stream still waits for the side
+                if (lanes[1]) {
+                    (void)hipEventRecord(ev_join, side_st);
+                    (void)hipStreamWaitEvent(st, ev_join, 0);
+                }
+                return e;
+            };
+            if (int e = decode_groups(lc, &v, gk + ko, nullptr, true, &dv)) return join(e);
             if (v.nnz > lim) {  // live <= nnz: only then can toAuto pick the dense form
-                SP_HIP(launch_count_live(st, a.gb, a.bw, v.nnz, a.qv, live));
+                if (launch_count_live(ls, a.gb, a.bw, v.nnz, a.qv, llive) != hipSuccess)
+                    return join(sfail(SKML_E_HIP, "count_live launch failed"));
                 uint64_t nlive = 0;
-                if (int e = sync_to_host(c, &nlive, live, sizeof(nlive))) return e;
+                if (int e = sync_to_host(lc, &nlive, llive, sizeof(nlive))) return join(e);
                 a.dense_form = (int64_t)nlive > lim ? 1 : 0;
             }
-            SP_HIP(launch_agg_bounds(st, a.gk, v.nnz, v.g_dev, ntiles, dim, const_cast<int32_t*>(a.bounds), err));
+            if (launch_agg_bounds(ls, a.gk, v.nnz, v.g_dev, ntiles, dim, const_cast<int32_t*>(a.bounds), err) !=
+                hipSuccess)
+                return join(sfail(SKML_E_HIP, "agg_bounds launch failed"));
             pays.push_back(a);
             ko += (v.nnz + 3) & ~int64_t{3};
             bo += (int64_t)v.g.G * (ntiles + 1);
+        }
+        if (lanes[1]) {
+            SP_HIP(hipEventRecord(ev_join, side_st));
+            SP_HIP(hipStreamWaitEvent(st, ev_join, 0));
         }
         const bool last = end == todo.size();
         SP_HIP(hipMemcpyAsync(d_pays, pays.data(), sizeof(AggPayload) * pays.size(), hipMemcpyHostToDevice, st));

@@ -382,7 +382,7 @@ def test_decode_sum(gpu):
                                       (16, [512] * 16, 40000 + 5), (5, [16] * 5, 2**18 + 7), (4, [4] * 4, 99999),
                                       (3, [2] * 3, 4097), (6, [256, 16, 4, 2, 256, 16], 50001), (1, [256], 15)])
 @pytest.mark.parametrize("kernel", ["occ", "occ_nopf", "plain"])
-def test_decode_sum_replicated_tables(gpu, P, bins, n, kernel, monkeypatch):
+def test_decode_sum_forms(gpu, P, bins, n, kernel, monkeypatch):
     """k_decode_sum_occ (8 elements per lane, P <= 8 tables of the largest bin count in LDS; with
     and without the next step's code prefetch) and the per-payload kernel (P > 8, mixed widths,
     > 256 bins): bit-exact against the oracle's decodes summed in double

@@ -78,15 +78,13 @@ def test_sparse_edge_values(gpu, kind):
 
 @pytest.fixture(params=["one_pass", "rounds"])
 def merge_form(request, monkeypatch):
-    """restore both ways.  one_pass (the default): lengths and deltas recomputed inside the key
-    query (k_dec_lsum / k_dec_dsum / k_dec_keys), tiles of one group through the compile-time-hash
-    query and the edge tiles through the generic one, Sort.merge as the one-pass key-range merge.
-    rounds: the A/B switches back to the round-3 forms (materialised lengths and deltas, one
-    generic query per row, the pairwise merge rounds, which are also the fallback for irregular
-    input)."""
+    """restore both ways.  one_pass (the default): tiles of one group through the compile-time-hash
+    query (k_dec_keys MODE 1) and the edge tiles through the generic one, Sort.merge as the
+    one-pass key-range merge.  rounds: the A/B switches back to the round-3 forms (one generic
+    query per row for every tile, the pairwise merge rounds, which are also the fallback for
+    irregular input)."""
     if request.param == "rounds":
         monkeypatch.setenv("SKML_RS_ROUNDS", "1")
-        monkeypatch.setenv("SKML_DEC_MATERIALIZE", "1")
         monkeypatch.setenv("SKML_DEC_ROWS_SERIAL", "1")
     return request.param
 
@@ -110,7 +108,7 @@ def test_sparse_shapes(gpu, groups, rows, ratio, bins, merge_form):
 def test_sparse_restore_many_merge_tiles(gpu, groups, merge_form):
     """~630 K keys: every Sort.merge round spans ~150 merge tiles of 4,096 outputs, with tile
     boundaries inside and at the ends of the merged pairs (k_merge_splits); the one-pass merge
-    covers 33 key ranges of 65,536 keys, ~19.7 K keys each."""
+    covers 257 key ranges of 8,192 keys, ~2.5 K keys each."""
     keys, vals = _sparse_data(2**21 + 3, 0.3, 40 + groups, "normal")
     _check_sparse(gpu, keys, vals, 256, groups, 2, 0.3, seed=11, hash_seed=groups)
     assert _merge_path() == (1 if merge_form == "one_pass" else 2)
@@ -118,20 +116,20 @@ def test_sparse_restore_many_merge_tiles(gpu, groups, merge_form):
 
 @pytest.mark.parametrize("layout", ["range_edges", "full_ranges", "far_apart", "int_max"])
 def test_sparse_restore_key_ranges(gpu, layout, merge_form):
-    """Keys placed against the one-pass merge's 65,536-key ranges: on and next to range edges
-    (0, 65535, 65536, ...), whole ranges filled (every bitmap bit set, ranges of 65,536
+    """Keys placed against the one-pass merge's 8,192-key ranges: on and next to range edges
+    (0, 8191, 8192, ...), whole ranges filled (every bitmap bit set, ranges of 8,192
     elements), keys ranges apart up to 2^31 - 2 (empty ranges between, a run's bounds filled over
     a gap), and a key of INT32_MAX, which Sort.merge never selects (its `< Integer.MAX_VALUE`
     test): the one-pass form hands that input to the rounds (path 3), whose result the oracle
     states."""
     rng = np.random.default_rng(len(layout))
     if layout == "range_edges":
-        e = np.arange(1, 40, dtype=np.int64) * 65536
-        keys = np.unique(np.concatenate([[0, 1, 65534, 65535], e - 1, e, e + 1]))
+        e = np.arange(1, 40, dtype=np.int64) * 8192
+        keys = np.unique(np.concatenate([[0, 1, 8190, 8191], e - 1, e, e + 1, 2**31 - 8192 + np.arange(-2, 3)]))
     elif layout == "full_ranges":
         keys = np.arange(3 * 65536 + 100, dtype=np.int64) + 65536
     elif layout == "far_apart":
-        keys = np.unique(np.concatenate([rng.integers(0, 2**31 - 1, 3000), [2**31 - 2, 0, 65536 * 32767]]))
+        keys = np.unique(np.concatenate([rng.integers(0, 2**31 - 1, 3000), [2**31 - 2, 0, 8192 * 262143]]))
     else:
         keys = np.unique(np.concatenate([rng.integers(0, 2**20, 5000), [2**31 - 2, 2**31 - 1]]))
     keys = keys.astype(np.int32)

@@ -118,7 +118,10 @@ def test_corrupt_blobs_are_refused(gpu):
 
 # "wave": k_agg_tiles_w (a wave per payload) with the row-batched MinMax query (the defaults);
 # "search": k_agg_tiles (per-element run search) with the row-by-row query (the A/B switches)
-KERNELS = {"wave": {}, "search": {"SKML_AGG_SEARCH": "1", "SKML_DEC_ROWS_SERIAL": "1", "SKML_DEC_MATERIALIZE": "1"}}
+# Gradient.sum's tile kernel: wave (default: one wave per payload adding into an LDS tile, restores
+# on two streams) and search (the round-3 per-element form, with the generic per-row MinMax query
+# and one stream)
+KERNELS = {"wave": {}, "search": {"SKML_AGG_FORM": "s", "SKML_DEC_ROWS_SERIAL": "1", "SKML_AGG_ONE_LANE": "1"}}
 
 
 @pytest.fixture(params=sorted(KERNELS))

@@ -1,0 +1,18 @@
+# r04j: persistent wave tiles for Gradient.sum (2 workgroups per CU, payloads read once per
+# workgroup) against one workgroup per tile; parity of the aggregate tests
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+set -e
+timeout -k 10 300 python -u -m pytest tests/test_gpu_sparse_exchange.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/r04j_tests.log 2>&1
+tail -1 gpurun_out/r04j_tests.log
+for i in 1 2; do
+  for V in pers:SKML_AB_DEFAULT=1 all:SKML_AGG_GRID_ALL=1 search:SKML_AGG_FORM=s; do
+    env "${V#*:}" timeout -k 10 200 python tools/bench_sparse.py --reps 5 --aggregate 8 > gpurun_out/r04j_${V%%:*}_$i.json 2>&1
+    python3 -c "
+import json
+d = json.loads(open('gpurun_out/r04j_${V%%:*}_$i.json').read().strip().splitlines()[-1])
+print('${V%%:*}', $i, {k: d['ms'][k] for k in ('encode_kv', 'decode', 'decode_sum')})"
+  done
+done
+SKML_AGG_ONE_LANE=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r04j_prof -o run --output-format csv -- python3 tools/bench_sparse.py --reps 2 --aggregate 8 > gpurun_out/r04j_prof.json 2>&1
+python3 tools/kstats_cmp.py gpurun_out/r04j_prof gpurun_out/r04j_prof k_ > gpurun_out/r04j_kstats.txt
+head -30 gpurun_out/r04j_kstats.txt
