@@ -333,9 +333,9 @@ def sparse_aggregate(sk, spl, dim, timed_median, P=8):
            "per_payload_ms": round((ts - t1) / (P - 1) * 1e3, 3),
            "alg_bytes": alg, "roofline_frac": round(alg / ts / 1e9 / HBM_PEAK_GBS, 4),
            "note": "median wall time of synchronised calls; one payload = DeltaAdaptive decode + MinMax query "
-                   "+ add into the double sum tile by tile (no Sort.merge: keys are unique); the fixed part is "
-                   "the 2 GiB write of the sum (the x 1/P scale is fused into it); alg_bytes = P blobs read + "
-                   "the sum written"}
+                   "(restores alternate between two streams) + add into the double sum tile by tile in payload "
+                   "order (persistent tiles; no Sort.merge: keys are unique); the fixed part is the 2 GiB write "
+                   "of the sum (the x 1/P scale is fused into it); alg_bytes = P blobs read + the sum written"}
     del allb, out
     return res
 
