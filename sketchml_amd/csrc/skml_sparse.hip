@@ -791,7 +791,8 @@ __global__ __launch_bounds__(kSpThreads) void k_part_scatter(const int32_t* __re
                                                              const uint8_t* __restrict__ qpayload, int64_t n,
                                                              const SpGroups* __restrict__ gp,
                                                              const uint64_t* __restrict__ tile_base,
-                                                             int32_t* __restrict__ gkeys, uint16_t* __restrict__ gbins) {
+                                                             int32_t* __restrict__ gkeys, uint16_t* __restrict__ gbins,
+                                                             int runs) {
     if (gp->status) return;
     constexpr int kWaves = kSpThreads / 64, kSteps = kSpTile / kSpThreads;
     __shared__ int32_t E[kMaxGroups];
@@ -807,6 +808,99 @@ __global__ __launch_bounds__(kSpThreads) void k_part_scatter(const int32_t* __re
     // the output base of group t's run in this tile, read before the counting (no round trip later)
     int64_t gbase = 0;
     if (t < G) gbase = gp->gstart[t] + (int64_t)tile_base[(int64_t)t * ((int64_t)gridDim.x + 1) + blockIdx.x];
+    if (few && runs) {
+        // Thread t owns the tile's elements [8t, 8t + 8): one 32-byte key load and one 8-byte code
+        // load per thread.  Stable ranks without ballots: the thread's per-group counts packed as
+        // 16-bit fields (groups 0,2,4,6 in lo, 1,3,5,7 in hi), a wave scan of the packed words,
+        // the waves' totals through LDS.
+        const FewEdges fe = few_edges(gp, G);
+        const int64_t i0 = (int64_t)blockIdx.x * kSpTile + 8 * t;
+        int32_t kk[8], bb[8], gg[8];
+        const bool full = i0 + 8 <= n;
+        if (full && (reinterpret_cast<uintptr_t>(keys + i0) & 15) == 0) {
+            const int4 a = *reinterpret_cast<const int4*>(keys + i0), b = *reinterpret_cast<const int4*>(keys + i0 + 4);
+            kk[0] = a.x, kk[1] = a.y, kk[2] = a.z, kk[3] = a.w, kk[4] = b.x, kk[5] = b.y, kk[6] = b.z, kk[7] = b.w;
+        } else {
+#pragma unroll
+            for (int s = 0; s < 8; s++) kk[s] = i0 + s < n ? keys[i0 + s] : 0;
+        }
+        if (full && bits == 8 && (reinterpret_cast<uintptr_t>(codes + i0) & 7) == 0) {
+            const uint64_t w8 = *reinterpret_cast<const uint64_t*>(codes + i0);
+#pragma unroll
+            for (int s = 0; s < 8; s++) bb[s] = (int32_t)((w8 >> (8 * s)) & 255u);
+        } else {
+#pragma unroll
+            for (int s = 0; s < 8; s++) bb[s] = i0 + s < n ? code_at(codes, i0 + s, bits) : 0;
+        }
+        uint64_t lo = 0, hi = 0;  // this thread's per-group counts
+#pragma unroll
+        for (int s = 0; s < 8; s++) {
+            gg[s] = i0 + s < n ? few_group(fe, bb[s]) : -1;
+            if (gg[s] >= 0) {
+                const uint64_t one = 1ull << (16 * (gg[s] >> 1));
+                if (gg[s] & 1) hi += one;
+                else lo += one;
+            }
+        }
+        uint64_t li = lo, hi_i = hi;  // inclusive wave scans
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint64_t yl = __shfl_up(li, off, 64), yh = __shfl_up(hi_i, off, 64);
+            if (lane >= off) {
+                li += yl;
+                hi_i += yh;
+            }
+        }
+        __shared__ uint64_t wt[kWaves][2];
+        __shared__ int32_t wbase[kWaves][kFewGroups];  // LDS slot of (wave, group)'s first element
+        if (lane == 63) {
+            wt[w][0] = li;
+            wt[w][1] = hi_i;
+        }
+        __syncthreads();
+        if (t < 64) {  // lane g < G: the tile's group g totals, the LDS layout in group order
+            uint32_t c = 0;
+            if (lane < G)
+                for (int j = 0; j < kWaves; j++) c += few_field(wt[j][0], wt[j][1], lane);
+            uint32_t x = c;  // inclusive scan over the groups
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t y = __shfl_up(x, off, 64);
+                if (lane >= off) x += y;
+            }
+            if (lane < G) {
+                uint32_t run = x - c;
+                gdst[lane] = gbase - (int64_t)run;
+                for (int j = 0; j < kWaves; j++) {
+                    wbase[j][lane] = (int32_t)run;
+                    run += few_field(wt[j][0], wt[j][1], lane);
+                }
+            }
+        }
+        __syncthreads();
+        const uint64_t le = li - lo, he = hi_i - hi;  // exclusive: earlier lanes of this wave
+        uint64_t seen_l = 0, seen_h = 0;              // this thread's earlier elements
+#pragma unroll
+        for (int s = 0; s < 8; s++) {
+            const int g = gg[s];
+            if (g < 0) continue;
+            const int pos = wbase[w][g] + (int)few_field(le, he, g) + (int)few_field(seen_l, seen_h, g);
+            sk[pos] = kk[s];
+            sb[pos] = bb[s];
+            sg[pos] = (uint8_t)g;
+            const uint64_t one = 1ull << (16 * (g >> 1));
+            if (g & 1) seen_h += one;
+            else seen_l += one;
+        }
+        __syncthreads();
+        const int tile_n = (int)std::min<int64_t>(kSpTile, n - (int64_t)blockIdx.x * kSpTile);
+        for (int q = t; q < tile_n; q += kSpThreads) {
+            const int64_t dst = gdst[sg[q]] + q;
+            gkeys[dst] = sk[q];
+            gbins[dst] = (uint16_t)sb[q];
+        }
+        return;
+    }
     if (!few) {
         load_edges(gp, E);
         for (int j = t; j < kWaves * kMaxGroups; j += kSpThreads) wb[j / kMaxGroups][j % kMaxGroups] = 0;
@@ -905,8 +999,9 @@ hipError_t launch_part_scatter(hipStream_t st, const int32_t* keys, const void* 
                                uint16_t* gbins) {
     const int64_t tiles = sp_tiles(n, kSpTile);
     if (tiles <= 0) return hipSuccess;
+    const int runs = std::getenv("SKML_PART_BALLOT") == nullptr ? 1 : 0;  // A/B switch: the ballot-ranked form
     hipLaunchKernelGGL(k_part_scatter, dim3((unsigned)tiles), dim3(kSpThreads), 0, st, keys,
-                       reinterpret_cast<const uint8_t*>(qpayload), n, gp, tile_base, gkeys, gbins);
+                       reinterpret_cast<const uint8_t*>(qpayload), n, gp, tile_base, gkeys, gbins, runs);
     return hipGetLastError();
 }
 
@@ -1357,8 +1452,20 @@ __device__ __forceinline__ uint32_t block_excl_scan_u32(uint32_t v, uint32_t* sh
     return before + inc - v;
 }
 
+// One element's two cells (rows 0 and 1) with the group's hash ids fixed at compile time, for the
+// rehashing staged scatter (cells_in == nullptr): rows 0 / 1 of element u go to nc[2u] / nc[2u + 1].
+template <int ID>
+__device__ __forceinline__ void mm_row_cells_rh(const int32_t (&key)[8], int r, int64_t row0, int32_t cols, double inv,
+                                                int32_t (&nc)[8]) {
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+        if (nc[2 * u + r] >= 0) nc[2 * u + r] = (int32_t)(row0 + java_hash_fm(ID, key[2 * u + r], cols, inv));
+}
+
 // PAIR: uint64_t (key-carrying pairs) or uint32_t (narrow pairs, SpGroups.mm_narrow).
-template <int T, typename PAIR>
+// cells_in == nullptr (two rows only): the cells are hashed again here instead of read back from
+// k_group_prep (which then writes none): 8 bytes per element less written and read, one more hash.
+template <int T, typename PAIR, bool REHASH>
 __device__ __forceinline__ void mm_scatter_staged_body(const int32_t* __restrict__ gkeys,
                                                        const uint16_t* __restrict__ gbins, int64_t n,
                                                        const SpGroups* __restrict__ gp,
@@ -1368,6 +1475,7 @@ __device__ __forceinline__ void mm_scatter_staged_body(const int32_t* __restrict
                                                        uint32_t* scan_sh, int64_t chunk) {
     constexpr bool kNarrow = sizeof(PAIR) == 4;
     constexpr int kStage = 8 * T;
+    __shared__ int64_t S[kMaxGroups + 1];
     // LDS: dstb[nb] u64 | stage[kStage] PAIR | lc[nb] u32 | lofs[nb + 1] u32 | sb[kStage] u16
     uint64_t* dstb = dyn64;
     PAIR* stage = reinterpret_cast<PAIR*>(dstb + nbuckets);
@@ -1375,11 +1483,13 @@ __device__ __forceinline__ void mm_scatter_staged_body(const int32_t* __restrict
     uint32_t* lofs = lc + nbuckets;
     uint16_t* sb = reinterpret_cast<uint16_t*>(lofs + nbuckets + 1);
     const int t = threadIdx.x, rows = gp->rows, zero = gp->zero;
+    constexpr bool rehash = REHASH;
     const uint32_t* row = tile_off + (int64_t)blockIdx.x * nbuckets;
     for (int j = t; j < nbuckets; j += T) {
         dstb[j] = bucket_base[j] + row[j];
         lc[j] = 0;
     }
+    if constexpr (REHASH) load_starts(gp, S);
     const int64_t c0 = (int64_t)blockIdx.x * chunk, c1 = std::min<int64_t>(n, c0 + chunk);
     const int et = 8 / rows;  // elements per thread per chunk: et * rows <= 8 pairs each
     const int np = et * rows;
@@ -1393,8 +1503,13 @@ __device__ __forceinline__ void mm_scatter_staged_body(const int32_t* __restrict
             const int64_t i = base + (int64_t)u * T + t;
             nc[k] = -1;
             if (k < np && i < c1) {
-                nc[k] = cells_in[(int64_t)r * n + i];
-                if constexpr (!kNarrow) nk[k] = gkeys[i];
+                if constexpr (REHASH) {  // rows == 2: element u's key in nk[2u] and nk[2u + 1], hashed below
+                    nc[k] = 0;
+                    nk[k] = gkeys[i];
+                } else {
+                    nc[k] = cells_in[(int64_t)r * n + i];
+                    if constexpr (!kNarrow) nk[k] = gkeys[i];
+                }
                 nbn[k] = gbins[i];
             }
         }
@@ -1405,6 +1520,38 @@ __device__ __forceinline__ void mm_scatter_staged_body(const int32_t* __restrict
         PAIR pv[8];
         int32_t bk[8];
         uint32_t rk[8];
+        if constexpr (REHASH) {
+            const int64_t last = std::min<int64_t>(c1, base + step) - 1;
+            const int g_lo = group_of_elem(S, base);
+            if (g_lo == group_of_elem(S, last)) {  // workgroup-uniform: one group, one hash per row
+                const int32_t cols = gp->cols[g_lo];
+                const double inv = gp->inv_cols[g_lo];
+#pragma unroll
+                for (int r = 0; r < 2; r++) {
+                    const int id = __builtin_amdgcn_readfirstlane(gp->hash_ids[g_lo][r]);
+                    const int64_t row0 = gp->tab_off[g_lo] + (int64_t)r * cols;
+                    switch (id) {
+                        case 0: mm_row_cells_rh<0>(nk, r, row0, cols, inv, nc); break;
+                        case 1: mm_row_cells_rh<1>(nk, r, row0, cols, inv, nc); break;
+                        case 2: mm_row_cells_rh<2>(nk, r, row0, cols, inv, nc); break;
+                        case 3: mm_row_cells_rh<3>(nk, r, row0, cols, inv, nc); break;
+                        case 4: mm_row_cells_rh<4>(nk, r, row0, cols, inv, nc); break;
+                        case 5: mm_row_cells_rh<5>(nk, r, row0, cols, inv, nc); break;
+                        case 6: mm_row_cells_rh<6>(nk, r, row0, cols, inv, nc); break;
+                        default: mm_row_cells_rh<7>(nk, r, row0, cols, inv, nc); break;
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int64_t i = base + (int64_t)u * T + t;
+                    if (nc[2 * u] < 0) continue;
+                    const int g = group_of_elem(S, i);
+                    nc[2 * u] = (int32_t)mm_cell(gp, g, 0, nk[2 * u]);
+                    nc[2 * u + 1] = (int32_t)mm_cell(gp, g, 1, nk[2 * u]);
+                }
+            }
+        }
 #pragma unroll
         for (int k = 0; k < 8; k++) {
             bk[k] = nc[k] >= 0 ? nc[k] >> kMmBucketBits : -1;
@@ -1469,7 +1616,7 @@ __device__ __forceinline__ void mm_scatter_staged_body(const int32_t* __restrict
     }
 }
 
-template <int T>
+template <int T, bool REHASH>
 __global__ __launch_bounds__(T) void k_mm_scatter_staged(const int32_t* __restrict__ gkeys,
                                                          const uint16_t* __restrict__ gbins, int64_t n,
                                                          const SpGroups* __restrict__ gp,
@@ -1481,10 +1628,10 @@ __global__ __launch_bounds__(T) void k_mm_scatter_staged(const int32_t* __restri
     extern __shared__ uint64_t dyn64[];
     __shared__ uint32_t scan_sh[T / 64];
     if (gp->mm_narrow)
-        mm_scatter_staged_body<T, uint32_t>(gkeys, gbins, n, gp, bucket_base, nbuckets,
+        mm_scatter_staged_body<T, uint32_t, REHASH>(gkeys, gbins, n, gp, bucket_base, nbuckets,
                                             static_cast<uint32_t*>(pairs), cells_in, tile_off, dyn64, scan_sh, chunk);
     else
-        mm_scatter_staged_body<T, uint64_t>(gkeys, gbins, n, gp, bucket_base, nbuckets,
+        mm_scatter_staged_body<T, uint64_t, REHASH>(gkeys, gbins, n, gp, bucket_base, nbuckets,
                                             static_cast<uint64_t*>(pairs), cells_in, tile_off, dyn64, scan_sh, chunk);
 }
 #ifndef SKML_STAGE_THREADS
@@ -1498,24 +1645,36 @@ inline size_t staged_lds(int nbuckets) {
 bool mm_scatter_staged(bool cells, bool reserved, int nbuckets) {
     return cells && reserved && nbuckets <= kStageBuckets;
 }
+bool mm_rehash_default() {  // A/B switch: SKML_MM_CELLS=1 keeps k_group_prep's cell array
+    return std::getenv("SKML_MM_CELLS") == nullptr;
+}
 
 hipError_t launch_mm_scatter(hipStream_t st, const int32_t* gkeys, const uint16_t* gbins, int64_t n,
                              const SpGroups* gp, const uint64_t* bucket_base, uint64_t* cursor, int nbuckets,
-                             void* pairs_v, const int32_t* cells, const uint32_t* tile_off) {
+                             void* pairs_v, const int32_t* cells, const uint32_t* tile_off, bool rehash) {
+    const bool gp_rows_two = rehash;  // the host asks for rehash only with two rows
     uint64_t* pairs = static_cast<uint64_t*>(pairs_v);  // the unstaged scatter: key-carrying pairs only
     if (n <= 0) return hipSuccess;
     const int64_t chunk = mm_chunk(n);
-    if (mm_scatter_staged(cells != nullptr, tile_off != nullptr, nbuckets)) {
+    if (mm_scatter_staged(cells != nullptr || rehash, tile_off != nullptr, nbuckets)) {
         static bool attr_s = false;
         if (!attr_s) {
-            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mm_scatter_staged<kStageThreads>),
+            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mm_scatter_staged<kStageThreads, false>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)staged_lds(kStageBuckets));
+            if (e == hipSuccess)
+                e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mm_scatter_staged<kStageThreads, true>),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)staged_lds(kStageBuckets));
             if (e != hipSuccess) return e;
             attr_s = true;
         }
-        hipLaunchKernelGGL(k_mm_scatter_staged<kStageThreads>, dim3((unsigned)sp_tiles(n, chunk)),
-                           dim3(kStageThreads), staged_lds(nbuckets), st, gkeys, gbins, n, gp, bucket_base, nbuckets,
-                           pairs_v, cells, tile_off, chunk);
+        if (rehash && gp_rows_two)
+            hipLaunchKernelGGL((k_mm_scatter_staged<kStageThreads, true>), dim3((unsigned)sp_tiles(n, chunk)),
+                               dim3(kStageThreads), staged_lds(nbuckets), st, gkeys, gbins, n, gp, bucket_base,
+                               nbuckets, pairs_v, nullptr, tile_off, chunk);
+        else
+            hipLaunchKernelGGL((k_mm_scatter_staged<kStageThreads, false>), dim3((unsigned)sp_tiles(n, chunk)),
+                               dim3(kStageThreads), staged_lds(nbuckets), st, gkeys, gbins, n, gp, bucket_base,
+                               nbuckets, pairs_v, cells, tile_off, chunk);
         return hipGetLastError();
     }
     constexpr size_t kPer = sizeof(uint64_t) + sizeof(uint32_t);
@@ -2874,18 +3033,21 @@ hipError_t launch_agg_tiles(hipStream_t st, const AggPayload* pays, int P, int64
         hipLaunchKernelGGL(k_agg_tiles, dim3((unsigned)ntiles), dim3(kAggThreads), 0, st, pays, P, ntiles, dim, out,
                            from_out, scale, err);
     else {  // persistent: as many workgroups as are resident at once
-        static int resident = 0;
+        static int resident = 0;  // 0 until known; -1: the occupancy query failed (one workgroup per tile)
         if (!resident) {
             int dev = 0, per_cu = 0;
             hipDeviceProp_t prop;
-            if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess ||
-                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_agg_tiles_w, kAggThreads, 0) != hipSuccess)
-                return hipGetLastError();
-            resident = std::max(1, per_cu) * prop.multiProcessorCount;
+            if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess &&
+                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_agg_tiles_w, kAggThreads, 0) == hipSuccess)
+                resident = std::max(1, per_cu) * prop.multiProcessorCount;
+            else
+                resident = -1;
+            (void)hipGetLastError();
         }
         // (A/B switch: SKML_AGG_GRID_ALL = one workgroup per tile)
         const unsigned grid =
-            (unsigned)(std::getenv("SKML_AGG_GRID_ALL") != nullptr ? ntiles : std::min<int64_t>(ntiles, resident));
+            (unsigned)(std::getenv("SKML_AGG_GRID_ALL") != nullptr || resident < 0 ? ntiles
+                                                                                  : std::min<int64_t>(ntiles, resident));
         hipLaunchKernelGGL(k_agg_tiles_w, dim3(grid), dim3(kAggThreads), 0, st, pays, P, ntiles, dim, out, from_out,
                            scale, err);
     }
