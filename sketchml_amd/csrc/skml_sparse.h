@@ -106,13 +106,10 @@ hipError_t launch_group_prep(hipStream_t st, const int32_t* gkeys, int64_t n, co
                              uint32_t* tile_off);
 // pairs in bucket order (bucket_base: exclusive scan of the counts; cursor: nbuckets u64, zeroed).
 // Pairs are u64, or u32 when gp->mm_narrow (only with the staged scatter: mm_scatter_staged).
-// rehash (two rows only, cells == nullptr): the staged scatter hashes each key again instead of
-// reading k_group_prep's cells; mm_rehash_default() is the build's choice (SKML_MM_CELLS=1: cells).
 bool mm_scatter_staged(bool cells, bool reserved, int nbuckets);
-bool mm_rehash_default();
 hipError_t launch_mm_scatter(hipStream_t st, const int32_t* gkeys, const uint16_t* gbins, int64_t n,
                              const SpGroups* gp, const uint64_t* bucket_base, uint64_t* cursor, int nbuckets,
-                             void* pairs, const int32_t* cells, const uint32_t* tile_off, bool rehash = false);
+                             void* pairs, const int32_t* cells, const uint32_t* tile_off);
 #ifndef SKML_MM_CHUNK
 #define SKML_MM_CHUNK 32768
 #endif

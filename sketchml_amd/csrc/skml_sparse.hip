@@ -1452,20 +1452,8 @@ __device__ __forceinline__ uint32_t block_excl_scan_u32(uint32_t v, uint32_t* sh
     return before + inc - v;
 }
 
-// One element's two cells (rows 0 and 1) with the group's hash ids fixed at compile time, for the
-// rehashing staged scatter (cells_in == nullptr): rows 0 / 1 of element u go to nc[2u] / nc[2u + 1].
-template <int ID>
-__device__ __forceinline__ void mm_row_cells_rh(const int32_t (&key)[8], int r, int64_t row0, int32_t cols, double inv,
-                                                int32_t (&nc)[8]) {
-#pragma unroll
-    for (int u = 0; u < 4; u++)
-        if (nc[2 * u + r] >= 0) nc[2 * u + r] = (int32_t)(row0 + java_hash_fm(ID, key[2 * u + r], cols, inv));
-}
-
 // PAIR: uint64_t (key-carrying pairs) or uint32_t (narrow pairs, SpGroups.mm_narrow).
-// cells_in == nullptr (two rows only): the cells are hashed again here instead of read back from
-// k_group_prep (which then writes none): 8 bytes per element less written and read, one more hash.
-template <int T, typename PAIR, bool REHASH>
+template <int T, typename PAIR>
 __device__ __forceinline__ void mm_scatter_staged_body(const int32_t* __restrict__ gkeys,
                                                        const uint16_t* __restrict__ gbins, int64_t n,
                                                        const SpGroups* __restrict__ gp,
@@ -1475,7 +1463,6 @@ __device__ __forceinline__ void mm_scatter_staged_body(const int32_t* __restrict
                                                        uint32_t* scan_sh, int64_t chunk) {
     constexpr bool kNarrow = sizeof(PAIR) == 4;
     constexpr int kStage = 8 * T;
-    __shared__ int64_t S[kMaxGroups + 1];
     // LDS: dstb[nb] u64 | stage[kStage] PAIR | lc[nb] u32 | lofs[nb + 1] u32 | sb[kStage] u16
     uint64_t* dstb = dyn64;
     PAIR* stage = reinterpret_cast<PAIR*>(dstb + nbuckets);
@@ -1483,13 +1470,11 @@ __device__ __forceinline__ void mm_scatter_staged_body(const int32_t* __restrict
     uint32_t* lofs = lc + nbuckets;
     uint16_t* sb = reinterpret_cast<uint16_t*>(lofs + nbuckets + 1);
     const int t = threadIdx.x, rows = gp->rows, zero = gp->zero;
-    constexpr bool rehash = REHASH;
     const uint32_t* row = tile_off + (int64_t)blockIdx.x * nbuckets;
     for (int j = t; j < nbuckets; j += T) {
         dstb[j] = bucket_base[j] + row[j];
         lc[j] = 0;
     }
-    if constexpr (REHASH) load_starts(gp, S);
     const int64_t c0 = (int64_t)blockIdx.x * chunk, c1 = std::min<int64_t>(n, c0 + chunk);
     const int et = 8 / rows;  // elements per thread per chunk: et * rows <= 8 pairs each
     const int np = et * rows;
@@ -1503,13 +1488,8 @@ __device__ __forceinline__ void mm_scatter_staged_body(const int32_t* __restrict
             const int64_t i = base + (int64_t)u * T + t;
             nc[k] = -1;
             if (k < np && i < c1) {
-                if constexpr (REHASH) {  // rows == 2: element u's key in nk[2u] and nk[2u + 1], hashed below
-                    nc[k] = 0;
-                    nk[k] = gkeys[i];
-                } else {
-                    nc[k] = cells_in[(int64_t)r * n + i];
-                    if constexpr (!kNarrow) nk[k] = gkeys[i];
-                }
+                nc[k] = cells_in[(int64_t)r * n + i];
+                if constexpr (!kNarrow) nk[k] = gkeys[i];
                 nbn[k] = gbins[i];
             }
         }
@@ -1520,38 +1500,6 @@ __device__ __forceinline__ void mm_scatter_staged_body(const int32_t* __restrict
         PAIR pv[8];
         int32_t bk[8];
         uint32_t rk[8];
-        if constexpr (REHASH) {
-            const int64_t last = std::min<int64_t>(c1, base + step) - 1;
-            const int g_lo = group_of_elem(S, base);
-            if (g_lo == group_of_elem(S, last)) {  // workgroup-uniform: one group, one hash per row
-                const int32_t cols = gp->cols[g_lo];
-                const double inv = gp->inv_cols[g_lo];
-#pragma unroll
-                for (int r = 0; r < 2; r++) {
-                    const int id = __builtin_amdgcn_readfirstlane(gp->hash_ids[g_lo][r]);
-                    const int64_t row0 = gp->tab_off[g_lo] + (int64_t)r * cols;
-                    switch (id) {
-                        case 0: mm_row_cells_rh<0>(nk, r, row0, cols, inv, nc); break;
-                        case 1: mm_row_cells_rh<1>(nk, r, row0, cols, inv, nc); break;
-                        case 2: mm_row_cells_rh<2>(nk, r, row0, cols, inv, nc); break;
-                        case 3: mm_row_cells_rh<3>(nk, r, row0, cols, inv, nc); break;
-                        case 4: mm_row_cells_rh<4>(nk, r, row0, cols, inv, nc); break;
-                        case 5: mm_row_cells_rh<5>(nk, r, row0, cols, inv, nc); break;
-                        case 6: mm_row_cells_rh<6>(nk, r, row0, cols, inv, nc); break;
-                        default: mm_row_cells_rh<7>(nk, r, row0, cols, inv, nc); break;
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const int64_t i = base + (int64_t)u * T + t;
-                    if (nc[2 * u] < 0) continue;
-                    const int g = group_of_elem(S, i);
-                    nc[2 * u] = (int32_t)mm_cell(gp, g, 0, nk[2 * u]);
-                    nc[2 * u + 1] = (int32_t)mm_cell(gp, g, 1, nk[2 * u]);
-                }
-            }
-        }
 #pragma unroll
         for (int k = 0; k < 8; k++) {
             bk[k] = nc[k] >= 0 ? nc[k] >> kMmBucketBits : -1;
@@ -1616,7 +1564,7 @@ __device__ __forceinline__ void mm_scatter_staged_body(const int32_t* __restrict
     }
 }
 
-template <int T, bool REHASH>
+template <int T>
 __global__ __launch_bounds__(T) void k_mm_scatter_staged(const int32_t* __restrict__ gkeys,
                                                          const uint16_t* __restrict__ gbins, int64_t n,
                                                          const SpGroups* __restrict__ gp,
@@ -1628,10 +1576,10 @@ __global__ __launch_bounds__(T) void k_mm_scatter_staged(const int32_t* __restri
     extern __shared__ uint64_t dyn64[];
     __shared__ uint32_t scan_sh[T / 64];
     if (gp->mm_narrow)
-        mm_scatter_staged_body<T, uint32_t, REHASH>(gkeys, gbins, n, gp, bucket_base, nbuckets,
+        mm_scatter_staged_body<T, uint32_t>(gkeys, gbins, n, gp, bucket_base, nbuckets,
                                             static_cast<uint32_t*>(pairs), cells_in, tile_off, dyn64, scan_sh, chunk);
     else
-        mm_scatter_staged_body<T, uint64_t, REHASH>(gkeys, gbins, n, gp, bucket_base, nbuckets,
+        mm_scatter_staged_body<T, uint64_t>(gkeys, gbins, n, gp, bucket_base, nbuckets,
                                             static_cast<uint64_t*>(pairs), cells_in, tile_off, dyn64, scan_sh, chunk);
 }
 #ifndef SKML_STAGE_THREADS
@@ -1645,36 +1593,24 @@ inline size_t staged_lds(int nbuckets) {
 bool mm_scatter_staged(bool cells, bool reserved, int nbuckets) {
     return cells && reserved && nbuckets <= kStageBuckets;
 }
-bool mm_rehash_default() {  // A/B switch: SKML_MM_CELLS=1 keeps k_group_prep's cell array
-    return std::getenv("SKML_MM_CELLS") == nullptr;
-}
 
 hipError_t launch_mm_scatter(hipStream_t st, const int32_t* gkeys, const uint16_t* gbins, int64_t n,
                              const SpGroups* gp, const uint64_t* bucket_base, uint64_t* cursor, int nbuckets,
-                             void* pairs_v, const int32_t* cells, const uint32_t* tile_off, bool rehash) {
-    const bool gp_rows_two = rehash;  // the host asks for rehash only with two rows
+                             void* pairs_v, const int32_t* cells, const uint32_t* tile_off) {
     uint64_t* pairs = static_cast<uint64_t*>(pairs_v);  // the unstaged scatter: key-carrying pairs only
     if (n <= 0) return hipSuccess;
     const int64_t chunk = mm_chunk(n);
-    if (mm_scatter_staged(cells != nullptr || rehash, tile_off != nullptr, nbuckets)) {
+    if (mm_scatter_staged(cells != nullptr, tile_off != nullptr, nbuckets)) {
         static bool attr_s = false;
         if (!attr_s) {
-            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mm_scatter_staged<kStageThreads, false>),
+            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mm_scatter_staged<kStageThreads>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)staged_lds(kStageBuckets));
-            if (e == hipSuccess)
-                e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mm_scatter_staged<kStageThreads, true>),
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)staged_lds(kStageBuckets));
             if (e != hipSuccess) return e;
             attr_s = true;
         }
-        if (rehash && gp_rows_two)
-            hipLaunchKernelGGL((k_mm_scatter_staged<kStageThreads, true>), dim3((unsigned)sp_tiles(n, chunk)),
-                               dim3(kStageThreads), staged_lds(nbuckets), st, gkeys, gbins, n, gp, bucket_base,
-                               nbuckets, pairs_v, nullptr, tile_off, chunk);
-        else
-            hipLaunchKernelGGL((k_mm_scatter_staged<kStageThreads, false>), dim3((unsigned)sp_tiles(n, chunk)),
-                               dim3(kStageThreads), staged_lds(nbuckets), st, gkeys, gbins, n, gp, bucket_base,
-                               nbuckets, pairs_v, cells, tile_off, chunk);
+        hipLaunchKernelGGL(k_mm_scatter_staged<kStageThreads>, dim3((unsigned)sp_tiles(n, chunk)),
+                           dim3(kStageThreads), staged_lds(nbuckets), st, gkeys, gbins, n, gp, bucket_base, nbuckets,
+                           pairs_v, cells, tile_off, chunk);
         return hipGetLastError();
     }
     constexpr size_t kPer = sizeof(uint64_t) + sizeof(uint32_t);

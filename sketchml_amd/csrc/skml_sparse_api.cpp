@@ -490,12 +490,9 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const void* vals, bool f64, int6
     const bool staging = !g_fail_cellbuf.load();
     uint32_t* tile_off =
         reserve && staging ? scratch<uint32_t>(c, kSlotTileOff, (size_t)mm_tiles * (size_t)nbuckets) : nullptr;
-    // two rows (the default shape): the scatter hashes the keys again instead of reading a cell array
-    const bool rehash = rows == 2 && cells_max < INT32_MAX && staging && mm_rehash_default();
-    int32_t* cellbuf = !rehash && cells_max < INT32_MAX && staging
-                           ? scratch<int32_t>(c, kSlotCellIdx, (size_t)rows * (size_t)nnz)
-                           : nullptr;
-    init.narrow_ok = mm_scatter_staged(cellbuf != nullptr || rehash, tile_off != nullptr, nbuckets) ? 1 : 0;
+    int32_t* cellbuf =
+        cells_max < INT32_MAX && staging ? scratch<int32_t>(c, kSlotCellIdx, (size_t)rows * (size_t)nnz) : nullptr;
+    init.narrow_ok = mm_scatter_staged(cellbuf != nullptr, tile_off != nullptr, nbuckets) ? 1 : 0;
     init.col_ratio = p->col_ratio;
     for (int g = 0; g < G; g++) pick_hashes(p->hash_seed + g, rows, init.hash_ids[g]);
     SP_TRY(launch_sp_plan_edges(st, s->qpayload, init, s->g_dev));
@@ -542,7 +539,7 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const void* vals, bool f64, int6
         return bail(e);
     if (side) SP_TRY(hipEventRecord(ev_join, side));
     SP_TRY(launch_scan_cols(st, bucket, nbuckets, 1));
-    SP_TRY(launch_mm_scatter(st, gk, gb, nnz, s->g_dev, bucket, cursor, nbuckets, pairs, cellbuf, tile_off, rehash));
+    SP_TRY(launch_mm_scatter(st, gk, gb, nnz, s->g_dev, bucket, cursor, nbuckets, pairs, cellbuf, tile_off));
     SP_TRY(launch_mm_bucket(st, pairs, bucket, nbuckets, s->g_dev, s->tables));
     if (side) SP_TRY(hipStreamWaitEvent(st, ev_join, 0));
     // ---- 5. the one read-back: quantizer header and splits, group table ----

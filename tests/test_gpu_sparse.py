@@ -106,19 +106,6 @@ def test_partition_scatter_forms(gpu, form, monkeypatch):
         _check_sparse(gpu, keys, vals, bins, groups, 2, 0.3, seed=groups, hash_seed=bins)
 
 
-@pytest.mark.parametrize("cells", ["rehash", "cells"])
-def test_minmax_scatter_cell_sources(gpu, cells, monkeypatch):
-    """Two-row payloads: the staged MinMax scatter hashes every key again (default) or reads the
-    cells k_group_prep kept (SKML_MM_CELLS=1); the tables equal the oracle's either way, including
-    tiles that span a group edge (the generic hash path)."""
-    if cells == "cells":
-        monkeypatch.setenv("SKML_MM_CELLS", "1")
-    keys, vals = _sparse_data(300000, 0.3, 91, "normal")
-    _check_sparse(gpu, keys, vals, 256, 8, 2, 0.3, seed=5, hash_seed=6)
-    keys, vals = _sparse_data(50000, 0.5, 92, "dups")
-    _check_sparse(gpu, keys, vals, 64, 4, 2, 0.7, seed=6, hash_seed=7)
-
-
 @pytest.mark.parametrize("groups,rows,ratio,bins", [(2, 1, 0.3, 256), (4, 3, 0.5, 64), (16, 8, 0.1, 1024),
                                                     (64, 2, 0.3, 4096), (8, 2, 1.7, 16), (3, 1, 0.3, 128),
                                                     (5, 2, 0.3, 256), (7, 3, 0.2, 512)])
