@@ -2872,21 +2872,44 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_tiles_w(const AggPayload* _
         }
     };
     if (one_batch) load_batch(0, P);
+    // with one batch, lane g of wave p holds the next tile's run bounds of payload p, group g:
+    // loaded one tile ahead, so a tile's element loads wait on one memory round trip, not two
+    int32_t nb0 = 0, nb1 = 0;
+    auto fetch_bounds = [&](int64_t tt) {
+        if (one_batch && wave < P && lane < a.G && tt < ntiles) {
+            const int32_t* bd = a.bounds + (int64_t)lane * (ntiles + 1);
+            nb0 = bd[tt];
+            nb1 = bd[tt + 1];
+        }
+    };
+    fetch_bounds(blockIdx.x);
     unsigned bad = 0;
+    // The store of tile t - 1 is deferred until tile t's element loads are in flight, and the
+    // zeroing of the LDS sum follows it, so both overlap those loads' latency.
+    int64_t prev_k0 = -1, prev_nk = 0;
+    auto store_prev = [&]() {
+        if (prev_k0 >= 0)
+            for (int x = threadIdx.x; x < prev_nk; x += kAggThreads)
+                out[prev_k0 + x] = scale == 1.0 ? acc[x] : __dmul_rn(acc[x], scale);
+    };
     for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const int64_t k0 = t * kAggTile, nk = std::min<int64_t>(kAggTile, dim - k0);
-        __syncthreads();  // the previous tile's stores have read acc
-        for (int x = threadIdx.x; x < kAggTile; x += kAggThreads) acc[x] = (from_out && x < nk) ? out[k0 + x] : 0.0;
+        const int32_t cb0 = nb0, cb1 = nb1;  // this tile's bounds (one batch)
+        fetch_bounds(t + gridDim.x);
         for (int p0 = 0; p0 < P; p0 += kAggPB) {
             const int np = std::min(kAggPB, P - p0);
-            __syncthreads();  // the previous batch is done with qt / rb / rs
+            __syncthreads();  // the previous batch / tile is done with qt / rb / rs / acc's adds
             if (!one_batch) load_batch(p0, np);
             const bool mine = wave < np;
             if (mine) {
                 int32_t len = 0;
                 if (lane < a.G) {
-                    const int32_t* bd = a.bounds + (int64_t)lane * (ntiles + 1);
-                    const int32_t b0 = bd[t], b1 = bd[t + 1];
+                    int32_t b0 = cb0, b1 = cb1;
+                    if (!one_batch) {
+                        const int32_t* bd = a.bounds + (int64_t)lane * (ntiles + 1);
+                        b0 = bd[t];
+                        b1 = bd[t + 1];
+                    }
                     len = b1 > b0 ? b1 - b0 : 0;
                     rs[wave][lane] = b0;
                 }
@@ -2921,6 +2944,15 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_tiles_w(const AggPayload* _
                     vv[u] = lds_q ? qt[wave][b] : a.qv[b];
                 }
             }
+            if (p0 == 0) {  // the previous tile leaves, this tile's sum starts (loads in flight)
+                store_prev();
+                __syncthreads();
+                for (int x = threadIdx.x; x < kAggTile; x += kAggThreads)
+                    acc[x] = (from_out && x < nk) ? out[k0 + x] : 0.0;
+                __syncthreads();
+                prev_k0 = k0;
+                prev_nk = nk;
+            }
             for (int pl = 0; pl < np; pl++) {
                 if (wave == pl) {
                     const bool dform = a.dense_form != 0;
@@ -2954,10 +2986,9 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_tiles_w(const AggPayload* _
                 }
             }
         }
-        __syncthreads();
-        for (int x = threadIdx.x; x < nk; x += kAggThreads)
-            out[k0 + x] = scale == 1.0 ? acc[x] : __dmul_rn(acc[x], scale);
     }
+    __syncthreads();
+    store_prev();
     if (bad) atomicOr(err, 1u);
 }
 
