@@ -2672,52 +2672,93 @@ hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, con
 // sum is read and written once instead of one random read-modify-write per restored key.
 // bounds[g * (ntiles + 1) + t] = first element (payload index) of group g's run with key >=
 // t * kAggTile; 0 throughout for an empty group.
+// Run bounds over 16 consecutive restored keys per thread (four 16-byte loads and the key before
+// them; the group's ends in registers): for each element, the ranges between its predecessor's
+// range and its own get the element's index, and a run's last element closes its run.
+// AGG: Gradient.sum's tiles of kAggTile keys (clamped to ntiles, tail filled to ntiles, keys
+// checked against [0, dim)); else Sort.merge's ranges of kRsRange keys (last range + 1 and the
+// range maxima into info, INT32_MAX and negative keys flagged irregular).  Both flag a key that
+// does not ascend inside its run.
+template <bool AGG>
+__device__ __forceinline__ void run_bounds16(const int32_t* __restrict__ gk, int64_t n, const int64_t* S,
+                                             int32_t* __restrict__ bounds, int64_t ld, int64_t ntiles, int64_t dim,
+                                             RsInfo* __restrict__ info, unsigned& bad) {
+    constexpr int kPer = 16;
+    const int64_t i0 = ((int64_t)blockIdx.x * kSpThreads + threadIdx.x) * kPer;
+    if (i0 >= n) return;
+    int32_t key[kPer];
+    if (i0 + kPer <= n && (reinterpret_cast<uintptr_t>(gk) & 15) == 0) {
+#pragma unroll
+        for (int q = 0; q < kPer / 4; q++) {
+            const int4 v = *reinterpret_cast<const int4*>(gk + i0 + 4 * q);
+            key[4 * q] = v.x, key[4 * q + 1] = v.y, key[4 * q + 2] = v.z, key[4 * q + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int e = 0; e < kPer; e++) key[e] = i0 + e < n ? gk[i0 + e] : 0;
+    }
+    int32_t prev = i0 > 0 ? gk[i0 - 1] : 0;
+    int g = group_of_elem(S, i0);
+    int64_t lo = S[g], hi = S[g + 1];
+    auto tile_of = [&](int32_t k) -> int64_t {
+        if constexpr (AGG) return k < 0 ? 0 : std::min<int64_t>((int64_t)(k >> 12), ntiles);
+        else return (int64_t)(k >> kRsBits);
+    };
+    static_assert(kAggTile == 1 << 12, "kAggTile");
+#pragma unroll
+    for (int e = 0; e < kPer; e++) {
+        const int64_t i = i0 + e;
+        if (i >= n) break;
+        while (i >= hi) {  // the next non-empty run (rare: at most G - 1 times over all threads)
+            g++;
+            lo = S[g];
+            hi = S[g + 1];
+        }
+        const int32_t k = key[e];
+        const bool first = i == lo;
+        bool ok;
+        if constexpr (AGG) {
+            if (k < 0 || (int64_t)k >= dim) bad = 1;  // SparseDoubleGradient's bound check
+            // keys ascend strictly inside a group (the tiles add without atomics)
+            if (!first && k <= prev) bad = 1;
+            ok = true;
+        } else {
+            ok = !(k < 0 || k == INT32_MAX || (!first && k <= prev));
+            if (!ok) bad = 1;
+        }
+        if (ok) {
+            const int64_t ti = tile_of(k);
+            const int64_t pt = first || (!AGG && prev < 0) ? -1 : tile_of(prev);
+            int32_t* b = bounds + (int64_t)g * ld;
+            for (int64_t t = pt + 1; t <= ti; t++) b[t] = (int32_t)i;
+            if (i == hi - 1) {
+                if constexpr (AGG) {
+                    for (int64_t t = ti + 1; t <= ntiles; t++) b[t] = (int32_t)hi;
+                } else {  // the run's last range ends at the run's end
+                    b[ti + 1] = (int32_t)hi;
+                    info->tlast1[g] = (int32_t)ti + 1;
+                    atomicMax(&info->tmax1, (int32_t)ti + 1);
+                }
+            }
+        }
+        prev = k;
+    }
+}
+
 __global__ __launch_bounds__(kSpThreads) void k_agg_bounds(const int32_t* __restrict__ gk, int64_t n,
                                                            const SpGroups* __restrict__ gp, int64_t ntiles, int64_t dim,
                                                            int32_t* __restrict__ bounds, unsigned* __restrict__ err) {
     __shared__ int64_t S[kMaxGroups + 1];
     load_starts(gp, S);
     __syncthreads();
-    const int64_t ld = ntiles + 1;
-    auto tile_of = [&](int32_t k) -> int64_t { return k < 0 ? 0 : std::min<int64_t>((int64_t)k / kAggTile, ntiles); };
-    // 4 consecutive elements per thread (one 16-byte load and the key before them)
-    const int64_t nq = (n + 3) / 4;
-    for (int64_t qd = (int64_t)blockIdx.x * kSpThreads + threadIdx.x; qd < nq; qd += (int64_t)gridDim.x * kSpThreads) {
-        const int64_t i0 = 4 * qd;
-        int32_t key[4];
-        if (i0 + 4 <= n && (reinterpret_cast<uintptr_t>(gk) & 15) == 0) {
-            const int4 v = *reinterpret_cast<const int4*>(gk + i0);
-            key[0] = v.x, key[1] = v.y, key[2] = v.z, key[3] = v.w;
-        } else {
-#pragma unroll
-            for (int e = 0; e < 4; e++) key[e] = i0 + e < n ? gk[i0 + e] : 0;
-        }
-        int32_t prev = i0 > 0 ? gk[i0 - 1] : 0;
-        int g = group_of_elem(S, i0);
-#pragma unroll
-        for (int e = 0; e < 4; e++) {
-            const int64_t i = i0 + e;
-            if (i >= n) break;
-            while (i >= S[g + 1]) g++;
-            const int64_t lo = S[g], hi = S[g + 1];
-            if (key[e] < 0 || (int64_t)key[e] >= dim) atomicOr(err, 1u);  // SparseDoubleGradient's bound check
-            // keys ascend strictly inside a group (the tiles add without atomics; a repeated key would
-            // race), as SparseDoubleGradient's constructor requires of the merged indices
-            if (i > lo && key[e] <= prev) atomicOr(err, 1u);
-            const int64_t ti = tile_of(key[e]);
-            const int64_t pt = i > lo ? tile_of(prev) : -1;
-            int32_t* b = bounds + (int64_t)g * ld;
-            for (int64_t t = pt + 1; t <= ti; t++) b[t] = (int32_t)i;
-            if (i == hi - 1)
-                for (int64_t t = ti + 1; t <= ntiles; t++) b[t] = (int32_t)hi;
-            prev = key[e];
-        }
-    }
+    unsigned bad = 0;
+    run_bounds16<true>(gk, n, S, bounds, ntiles + 1, ntiles, dim, nullptr, bad);
+    if (bad) atomicOr(err, 1u);
 }
 hipError_t launch_agg_bounds(hipStream_t st, const int32_t* gk, int64_t n, const SpGroups* gp, int64_t ntiles,
                              int64_t dim, int32_t* bounds, unsigned* err) {
     if (n <= 0) return hipSuccess;
-    const int64_t grid = std::min<int64_t>(sp_tiles((n + 3) / 4, kSpThreads), 8192);
+    const int64_t grid = sp_tiles(sp_tiles(n, 16), kSpThreads);  // 16 keys per thread
     hipLaunchKernelGGL(k_agg_bounds, dim3((unsigned)grid), dim3(kSpThreads), 0, st, gk, n, gp, ntiles, dim, bounds, err);
     return hipGetLastError();
 }
@@ -2734,6 +2775,13 @@ __device__ __forceinline__ int agg_search(const int64_t* pre, int n, int64_t j) 
         if (i + step < n && pre[i + step] <= j) i += step;
     return i;
 }
+__device__ __forceinline__ int agg_search32(const int32_t* pre, int n, int j) {  // largest i < n: pre[i] <= j
+    int i = 0;
+    for (int step = 32; step >= 1; step >>= 1)
+        if (i + step < n && pre[i + step] <= j) i += step;
+    return i;
+}
+
 __global__ __launch_bounds__(kAggThreads) void k_agg_tiles(const AggPayload* __restrict__ pays, int P, int64_t ntiles,
                                                           int64_t dim, double* __restrict__ out, int from_out,
                                                           double scale, unsigned* __restrict__ err) {
@@ -2927,6 +2975,21 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_tiles_w(const AggPayload* _
             // holding j by a walk over the (few) run prefixes
             const int total = mine ? rb[wave][a.G] : 0;
             const bool lds_q = a.nq <= kAggLdsValues;
+            // the run holding j: with at most 8 groups, a count of the run ends (held in registers)
+            // at or below j; else a binary search of the 65 prefix entries
+            int32_t re[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) re[q] = rb[wave][q + 1];
+            const bool few_g = a.G <= 8;
+            auto run_of = [&](int j) -> int {
+                if (few_g) {
+                    int g = 0;
+#pragma unroll
+                    for (int q = 0; q < 8; q++) g += re[q] <= j ? 1 : 0;
+                    return g;
+                }
+                return agg_search32(rb[wave], kMaxGroups + 1, j);
+            };
             int32_t kk[kAggWPer];
             double vv[kAggWPer];
 #pragma unroll
@@ -2935,8 +2998,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_tiles_w(const AggPayload* _
                 kk[u] = 0;
                 vv[u] = 0.0;
                 if (j < total) {
-                    int g = 0;
-                    while (rb[wave][g + 1] <= j) g++;
+                    const int g = run_of(j);
                     const int64_t i = (int64_t)rs[wave][g] + (j - rb[wave][g]);
                     kk[u] = a.gk[i];
                     const uint32_t b =
@@ -2969,8 +3031,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_tiles_w(const AggPayload* _
                     for (int u = 0; u < kAggWPer; u++)
                         if (lane + 64 * u < total) SKML_AGG_ADD(kk[u], vv[u]);
                     for (int j = lane + 64 * kAggWPer; j < total; j += 64) {  // the rest of a long payload
-                        int g = 0;
-                        while (rb[wave][g + 1] <= j) g++;
+                        const int g = run_of(j);
                         const int64_t i = (int64_t)rs[wave][g] + (j - rb[wave][g]);
                         const uint32_t b =
                             a.bw == 1 ? static_cast<const uint8_t*>(a.gb)[i] : static_cast<const uint16_t*>(a.gb)[i];
@@ -3193,52 +3254,9 @@ __global__ __launch_bounds__(kSpThreads) void k_rs_bounds(const int32_t* __restr
     __shared__ int64_t S[kMaxGroups + 1];
     load_starts(gp, S);
     __syncthreads();
-    constexpr int64_t ld = kRsRanges + 1;
     unsigned bad = 0;
-    const int64_t nq = (n + 3) / 4;
-    for (int64_t qd = (int64_t)blockIdx.x * kSpThreads + threadIdx.x; qd < nq; qd += (int64_t)gridDim.x * kSpThreads) {
-        const int64_t i0 = 4 * qd;
-        int32_t key[4];
-        if (i0 + 4 <= n && (reinterpret_cast<uintptr_t>(gk) & 15) == 0) {
-            const int4 v = *reinterpret_cast<const int4*>(gk + i0);
-            key[0] = v.x, key[1] = v.y, key[2] = v.z, key[3] = v.w;
-        } else {
-#pragma unroll
-            for (int e = 0; e < 4; e++) key[e] = i0 + e < n ? gk[i0 + e] : 0;
-        }
-        int32_t prev = i0 > 0 ? gk[i0 - 1] : 0;
-        int g = group_of_elem(S, i0);
-#pragma unroll
-        for (int e = 0; e < 4; e++) {
-            const int64_t i = i0 + e;
-            if (i >= n) break;
-            while (i >= S[g + 1]) g++;
-            const int32_t k = key[e];
-            const bool first = i == S[g];
-            if (k < 0 || k == INT32_MAX || (!first && k <= prev)) {
-                bad = 1;
-            } else {
-                const int64_t ti = k >> kRsBits;
-                const int64_t pt = first || prev < 0 ? -1 : prev >> kRsBits;
-                int32_t* b = bounds + (int64_t)g * ld;
-                for (int64_t t = pt + 1; t <= ti; t++) b[t] = (int32_t)i;
-                if (i == S[g + 1] - 1) {  // the run's last range ends at the run's end
-                    b[ti + 1] = (int32_t)S[g + 1];
-                    info->tlast1[g] = (int32_t)ti + 1;
-                    atomicMax(&info->tmax1, (int32_t)ti + 1);
-                }
-            }
-            prev = k;
-        }
-    }
+    run_bounds16<false>(gk, n, S, bounds, kRsRanges + 1, 0, 0, info, bad);
     if (bad) atomicOr(&info->irregular, 1u);
-}
-
-__device__ __forceinline__ int agg_search32(const int32_t* pre, int n, int j) {  // largest i < n: pre[i] <= j
-    int i = 0;
-    for (int step = 32; step >= 1; step >>= 1)
-        if (i + step < n && pre[i + step] <= j) i += step;
-    return i;
 }
 
 template <typename V>
@@ -3313,6 +3331,20 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_merge(const int32_t* __restri
         __syncthreads();
         const int cnt = pre[G];
         if (cnt == 0) continue;  // workgroup-uniform
+        // the run holding j: with at most 8 runs a count of the run ends (in registers) at or below
+        // j, else a binary search of the prefix
+        int32_t re[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) re[q] = q + 1 <= G ? pre[q + 1] : INT32_MAX;
+        auto run_of = [&](int j) -> int {
+            if (G <= 8) {
+                int g = 0;
+#pragma unroll
+                for (int q = 0; q < 8; q++) g += re[q] <= j ? 1 : 0;
+                return g;
+            }
+            return agg_search32(pre, G, j);
+        };
         // pass 1: the range's keys into the bitmap, their bins into the offset slots (4 loads of
         // each in flight per thread)
         for (int j0 = 0; j0 < cnt; j0 += kRsThreads * kRsBatch) {
@@ -3322,7 +3354,7 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_merge(const int32_t* __restri
                 const int j = j0 + u * kRsThreads + t_;
                 kk[u] = -1;
                 if (j < cnt) {
-                    const int g = agg_search32(pre, G, j);
+                    const int g = run_of(j);
                     const int64_t i = lo_s[g] + (j - pre[g]);
                     kk[u] = gk[i];
                     bb[u] = gb[i];
@@ -3368,7 +3400,7 @@ hipError_t launch_rs_merge(hipStream_t st, const int32_t* gk, const int32_t* gb,
     if (n <= 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(info, 0, sizeof(RsInfo), st);
     if (e != hipSuccess) return e;
-    const int64_t bgrid = std::min<int64_t>(sp_tiles((n + 3) / 4, kSpThreads), 8192);
+    const int64_t bgrid = sp_tiles(sp_tiles(n, 16), kSpThreads);
     hipLaunchKernelGGL(k_rs_bounds, dim3((unsigned)bgrid), dim3(kSpThreads), 0, st, gk, n, gp, bounds, info);
     // persistent workgroups over the key ranges up to the largest key (read on the device)
     const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(sp_tiles(n, 4096), 1), 2048);
