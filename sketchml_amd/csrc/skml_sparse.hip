@@ -3298,18 +3298,30 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_merge(const int32_t* __restri
         for (int b = t_; b < nq; b += kRsThreads) lut[b] = (V)qv[b];
     constexpr int64_t ld = kRsRanges + 1;
     unsigned bad = 0;
+    // wave 0, lane g < G: run g's last range, and the bounds of this workgroup's next range,
+    // loaded one range ahead so a range waits on one memory round trip (its elements), not two
+    const int tl = (w == 0 && lane < G) ? info->tlast1[lane] - 1 : -1;  // -1: an empty run
+    int32_t nlo = 0, nhi = 0;
+    auto fetch = [&](int64_t tt) {
+        if (tl >= 0 && tt <= tl) {
+            nlo = bounds[(int64_t)lane * ld + tt];
+            nhi = bounds[(int64_t)lane * ld + tt + 1];
+        }
+    };
+    if (w == 0 && lane < G) fetch(blockIdx.x);
     for (int64_t t = blockIdx.x; t <= tmax; t += gridDim.x) {
+        const int32_t clo = nlo, chi = nhi;
+        if (w == 0 && lane < G) fetch(t + gridDim.x);
         __syncthreads();  // S / lut loaded; the previous range is done with bm / slot / pre
         if (w == 0) {  // lane g: run g's piece of this range
             int64_t lo = 0, len = 0, before = 0;
             if (lane < G) {
                 const int64_t s0 = S[lane], s1 = S[lane + 1];
-                const int tl = info->tlast1[lane] - 1;  // -1: an empty run
                 lo = s1;
                 int64_t hi = s1;
                 if (tl >= 0 && t <= tl) {
-                    lo = bounds[(int64_t)lane * ld + t];
-                    hi = bounds[(int64_t)lane * ld + t + 1];
+                    lo = clo;
+                    hi = chi;
                 }
                 before = lo - s0;
                 len = hi - lo;
@@ -3402,8 +3414,9 @@ hipError_t launch_rs_merge(hipStream_t st, const int32_t* gk, const int32_t* gb,
     if (e != hipSuccess) return e;
     const int64_t bgrid = sp_tiles(sp_tiles(n, 16), kSpThreads);
     hipLaunchKernelGGL(k_rs_bounds, dim3((unsigned)bgrid), dim3(kSpThreads), 0, st, gk, n, gp, bounds, info);
-    // persistent workgroups over the key ranges up to the largest key (read on the device)
-    const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(sp_tiles(n, 4096), 1), 2048);
+    // persistent workgroups over the key ranges up to the largest key (read on the device): as many
+    // as are resident at once (4 per CU), fewer for small inputs
+    const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(sp_tiles(n, 4096), 1), 1024);
     if (vkind == 0)
         hipLaunchKernelGGL(k_rs_merge<int32_t>, dim3(grid), dim3(kRsThreads), 0, st, gk, gb, gp, bounds, info, keys_out,
                            static_cast<int32_t*>(out), qv, nq);
