@@ -183,10 +183,15 @@ struct AggPayload {
     int32_t bw, nq;
 };
 static_assert(sizeof(AggPayload) % 8 == 0, "copied as u64 words");
+// tile_bits: log2 of the keys per tile the bounds are taken at (agg_tile_bits of the chosen form)
 hipError_t launch_agg_bounds(hipStream_t st, const int32_t* gk, int64_t n, const SpGroups* gp, int64_t ntiles,
-                             int64_t dim, int32_t* bounds, unsigned* err);
+                             int64_t dim, int32_t* bounds, unsigned* err, int tile_bits);
+// vtiles: the staged wave-tile form (agg_vtiles_ok: at most 8 payloads per launch, 8 groups and 256
+// quantValues each); it sets err bit 2 for a key repeated inside one payload
+bool agg_vtiles_ok(int P, int max_groups, int max_nq);
+int agg_tile_bits(bool vtiles);
 hipError_t launch_agg_tiles(hipStream_t st, const AggPayload* pays, int P, int64_t ntiles, int64_t dim, double* out,
-                            int from_out, double scale, unsigned* err);
+                            int from_out, double scale, unsigned* err, bool vtiles);
 
 // Exported sparse payload: one contiguous device blob (skml_sparse_export / _import, the unit the
 // RCCL all-gather moves).  Offsets are from the blob start, every section 256-byte aligned.

@@ -2440,7 +2440,11 @@ struct DecEdgeTiles {
     int64_t t[kMaxGroups];
     int n;  // 0: every tile (dec_tile_of_block)
 };
-template <typename TN, int MODE>
+// NT: the delta stream and the key / bin stores nontemporal, so they pass L2 without evicting the
+// table the gathers read.
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+typedef int32_t i32x4_t __attribute__((ext_vector_type(4)));
+template <typename TN, int MODE, bool NT = false>
 __global__ __launch_bounds__(kDecThreads) void k_dec_keys(const uint32_t* __restrict__ delta, int64_t n,
                                                           const SpGroups* __restrict__ gp,
                                                           const uint64_t* __restrict__ tile_base,
@@ -2463,8 +2467,13 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_keys(const uint32_t* __rest
     const int64_t i0 = tile * kSpTile + t * 4;
     uint32_t d[4];
     if (i0 + 4 <= n) {
-        const uint4 v = *reinterpret_cast<const uint4*>(delta + i0);
-        d[0] = v.x, d[1] = v.y, d[2] = v.z, d[3] = v.w;
+        if constexpr (NT) {
+            const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(delta + i0));
+            d[0] = v.x, d[1] = v.y, d[2] = v.z, d[3] = v.w;
+        } else {
+            const uint4 v = *reinterpret_cast<const uint4*>(delta + i0);
+            d[0] = v.x, d[1] = v.y, d[2] = v.z, d[3] = v.w;
+        }
     } else {
 #pragma unroll
         for (int j = 0; j < 4; j++) d[j] = i0 + j < n ? delta[i0 + j] : 0u;
@@ -2583,9 +2592,11 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_keys(const uint32_t* __rest
         if (bad) atomicOr(err, 1u);
         if (bn_width == 1) {
             uint8_t* o = static_cast<uint8_t*>(gbn) + i0;
-            if (full && (reinterpret_cast<uintptr_t>(o) & 3) == 0)
-                *reinterpret_cast<uint32_t*>(o) = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
-            else
+            if (full && (reinterpret_cast<uintptr_t>(o) & 3) == 0) {
+                const uint32_t w4 = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
+                if constexpr (NT) __builtin_nontemporal_store(w4, reinterpret_cast<uint32_t*>(o));
+                else *reinterpret_cast<uint32_t*>(o) = w4;
+            } else
 #pragma unroll
                 for (int j = 0; j < 4; j++)
                     if (i0 + j < n) o[j] = (uint8_t)b[j];
@@ -2600,7 +2611,12 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_keys(const uint32_t* __rest
         }
     }
     if (full && (reinterpret_cast<uintptr_t>(gkeys + i0) & 15) == 0) {
-        *reinterpret_cast<int4*>(gkeys + i0) = make_int4(key[0], key[1], key[2], key[3]);
+        if constexpr (NT) {
+            const i32x4_t kv = {key[0], key[1], key[2], key[3]};
+            __builtin_nontemporal_store(kv, reinterpret_cast<i32x4_t*>(gkeys + i0));
+        } else {
+            *reinterpret_cast<int4*>(gkeys + i0) = make_int4(key[0], key[1], key[2], key[3]);
+        }
     } else {
 #pragma unroll
         for (int j = 0; j < 4; j++)
@@ -2644,13 +2660,18 @@ hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, con
             if (edges.n == 0 || edges.t[edges.n - 1] != t) edges.t[edges.n++] = t;
         }
     }
+    const bool nt = std::getenv("SKML_DEC_NT") != nullptr;  // (A/B switch: nontemporal streams)
 #define SKML_DEC_LAUNCH(TNT, MODE, GRID, TILES, TNPTR)                                                            \
     hipLaunchKernelGGL((k_dec_keys<TNT, MODE>), dim3(GRID), dim3(kDecThreads), 0, st, delta, n, gp, tile_base, gpre, \
                        table, TNPTR, gkeys, gbins, nq, gbn, bn_width, err, TILES)
 #define SKML_DEC_WIDTH(TNT, TNPTR)                                                          \
     do {                                                                                  \
         if (batched) {                                                                    \
-            SKML_DEC_LAUNCH(TNT, 1, grid, all, TNPTR);                                    \
+            if (nt)                                                                       \
+                hipLaunchKernelGGL((k_dec_keys<TNT, 1, true>), dim3(grid), dim3(kDecThreads), 0, st, delta, n, gp, \
+                                   tile_base, gpre, table, TNPTR, gkeys, gbins, nq, gbn, bn_width, err, all); \
+            else                                                                          \
+                SKML_DEC_LAUNCH(TNT, 1, grid, all, TNPTR);                                \
             if (edges.n > 0) SKML_DEC_LAUNCH(TNT, 0, (unsigned)edges.n, edges, TNPTR);    \
         } else {                                                                          \
             SKML_DEC_LAUNCH(TNT, 0, grid, all, TNPTR);                                    \
@@ -2682,7 +2703,7 @@ hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, con
 template <bool AGG>
 __device__ __forceinline__ void run_bounds16(const int32_t* __restrict__ gk, int64_t n, const int64_t* S,
                                              int32_t* __restrict__ bounds, int64_t ld, int64_t ntiles, int64_t dim,
-                                             RsInfo* __restrict__ info, unsigned& bad) {
+                                             RsInfo* __restrict__ info, unsigned& bad, int tile_bits = 12) {
     constexpr int kPer = 16;
     const int64_t i0 = ((int64_t)blockIdx.x * kSpThreads + threadIdx.x) * kPer;
     if (i0 >= n) return;
@@ -2701,10 +2722,9 @@ __device__ __forceinline__ void run_bounds16(const int32_t* __restrict__ gk, int
     int g = group_of_elem(S, i0);
     int64_t lo = S[g], hi = S[g + 1];
     auto tile_of = [&](int32_t k) -> int64_t {
-        if constexpr (AGG) return k < 0 ? 0 : std::min<int64_t>((int64_t)(k >> 12), ntiles);
+        if constexpr (AGG) return k < 0 ? 0 : std::min<int64_t>((int64_t)(k >> tile_bits), ntiles);
         else return (int64_t)(k >> kRsBits);
     };
-    static_assert(kAggTile == 1 << 12, "kAggTile");
 #pragma unroll
     for (int e = 0; e < kPer; e++) {
         const int64_t i = i0 + e;
@@ -2747,19 +2767,21 @@ __device__ __forceinline__ void run_bounds16(const int32_t* __restrict__ gk, int
 
 __global__ __launch_bounds__(kSpThreads) void k_agg_bounds(const int32_t* __restrict__ gk, int64_t n,
                                                            const SpGroups* __restrict__ gp, int64_t ntiles, int64_t dim,
-                                                           int32_t* __restrict__ bounds, unsigned* __restrict__ err) {
+                                                           int32_t* __restrict__ bounds, unsigned* __restrict__ err,
+                                                           int tile_bits) {
     __shared__ int64_t S[kMaxGroups + 1];
     load_starts(gp, S);
     __syncthreads();
     unsigned bad = 0;
-    run_bounds16<true>(gk, n, S, bounds, ntiles + 1, ntiles, dim, nullptr, bad);
+    run_bounds16<true>(gk, n, S, bounds, ntiles + 1, ntiles, dim, nullptr, bad, tile_bits);
     if (bad) atomicOr(err, 1u);
 }
 hipError_t launch_agg_bounds(hipStream_t st, const int32_t* gk, int64_t n, const SpGroups* gp, int64_t ntiles,
-                             int64_t dim, int32_t* bounds, unsigned* err) {
+                             int64_t dim, int32_t* bounds, unsigned* err, int tile_bits) {
     if (n <= 0) return hipSuccess;
     const int64_t grid = sp_tiles(sp_tiles(n, 16), kSpThreads);  // 16 keys per thread
-    hipLaunchKernelGGL(k_agg_bounds, dim3((unsigned)grid), dim3(kSpThreads), 0, st, gk, n, gp, ntiles, dim, bounds, err);
+    hipLaunchKernelGGL(k_agg_bounds, dim3((unsigned)grid), dim3(kSpThreads), 0, st, gk, n, gp, ntiles, dim, bounds, err,
+                       tile_bits);
     return hipGetLastError();
 }
 
@@ -3053,9 +3075,192 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_tiles_w(const AggPayload* _
     if (bad) atomicOr(err, 1u);
 }
 
+// One wave per tile of kAggVTile keys, staged: lane 8p + g of the wave holds the run piece of
+// payload p, group g (P <= 8, G <= 8), the pieces are concatenated payload by payload and each lane
+// loads up to kAggWPer elements of the concatenation.  The wave then writes every element's bin to
+// its slot of the wave's stage (one byte per (payload, key)) and sets the slot's presence bit; a
+// bit already set is a key repeated inside one payload (flagged).  Last, lane l owns keys
+// 8l .. 8l + 7 and sums them in registers payload after payload, which is Gradient.sum's order for
+// every key, without a read-modify-write of an LDS sum per element.  Persistent waves: each wave
+// loads its next tile's run bounds one tile ahead, and stores a tile's sums after the next tile's
+// element loads are in flight.  bw == 1 and nq <= 256 for every payload (agg_vtiles_ok).
+constexpr int kAggVBits = 9, kAggVTile = 1 << kAggVBits;
+static_assert(kAggVTile == 8 * 64, "eight keys per lane");
+__global__ __launch_bounds__(kAggThreads) void k_agg_vtiles(const AggPayload* __restrict__ pays, int P,
+                                                           int64_t ntiles, int64_t dim, double* __restrict__ out,
+                                                           int from_out, double scale, unsigned* __restrict__ err) {
+    constexpr int kWaves = kAggThreads / 64;
+    __shared__ uint8_t bins[kWaves][kAggPB][kAggVTile];  // the stage: a bin per (payload, key)
+    __shared__ uint32_t here[kWaves][kAggPB][kAggVTile / 32];  // presence bits
+    __shared__ double qt[kAggPB][kAggLdsValues];
+    __shared__ int32_t pre[kWaves][65];  // the wave's 64 run pieces, scanned
+    __shared__ int32_t pb0[kWaves][64];  // each piece's first element in its payload
+    __shared__ AggPayload pl[kAggPB];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (threadIdx.x < P * (int)(sizeof(AggPayload) / 8))
+        reinterpret_cast<uint64_t*>(pl)[threadIdx.x] = reinterpret_cast<const uint64_t*>(pays)[threadIdx.x];
+    __syncthreads();
+    if (wave < P)
+        for (int b = lane; b < pl[wave].nq; b += 64) qt[wave][b] = pl[wave].qv[b];
+    __syncthreads();
+    const int pl_l = lane >> 3, g_l = lane & 7;
+    const bool lane_on = pl_l < P && g_l < pl[pl_l].G;
+    const int32_t* bd = lane_on ? pl[pl_l].bounds + (int64_t)g_l * (ntiles + 1) : nullptr;
+    uint8_t(*B)[kAggVTile] = bins[wave];
+    uint32_t(*H)[kAggVTile / 32] = here[wave];
+    unsigned bad = 0;
+    const int64_t nw = (int64_t)gridDim.x * kWaves;
+    int32_t nb0 = 0, nb1 = 0;
+    auto fetch = [&](int64_t tt) {
+        if (lane_on && tt < ntiles) {
+            nb0 = bd[tt];
+            nb1 = bd[tt + 1];
+        }
+    };
+    double acc[8];
+    int64_t prev_k0 = -1, prev_nk = 0;
+    auto store_prev = [&]() {  // lane l's 8 keys of the previous tile
+        if (prev_k0 < 0) return;
+        const int x0 = 8 * lane;
+        double* o = out + prev_k0 + x0;
+        if (x0 + 8 <= prev_nk && (reinterpret_cast<uintptr_t>(o) & 15) == 0) {
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                *reinterpret_cast<double2*>(o + 2 * q) = make_double2(acc[2 * q], acc[2 * q + 1]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+                if (x0 + i < prev_nk) o[i] = acc[i];
+        }
+    };
+    int64_t t = (int64_t)blockIdx.x * kWaves + wave;
+    fetch(t);
+    for (; t < ntiles; t += nw) {
+        const int64_t k0 = t << kAggVBits, nk = std::min<int64_t>(kAggVTile, dim - k0);
+        const int32_t b0 = nb0, b1 = nb1;
+        fetch(t + nw);
+        const int32_t len = lane_on && b1 > b0 ? b1 - b0 : 0;
+        int32_t x = len;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int32_t y = __shfl_up(x, off, 64);
+            if (lane >= off) x += y;
+        }
+        pre[wave][lane + 1] = x;
+        if (lane == 0) pre[wave][0] = 0;
+        pb0[wave][lane] = b0;
+        reinterpret_cast<uint64_t*>(H)[lane] = 0;  // 8 x 16 words: two per lane
+        const int total = __shfl(x, 63, 64);
+        __builtin_amdgcn_wave_barrier();
+        auto piece_of = [&](int j) -> int {  // largest s < 64 with pre[s] <= j
+            int s_ = 0;
+#pragma unroll
+            for (int step = 32; step >= 1; step >>= 1)
+                if (pre[wave][s_ + step] <= j) s_ += step;
+            return s_;
+        };
+        auto load_elem = [&](int j, int32_t& key, uint32_t& bin) -> int {  // returns the payload
+            const int sp = piece_of(j);
+            const int p = sp >> 3;
+            const int64_t i = (int64_t)pb0[wave][sp] + (j - pre[wave][sp]);
+            key = pl[p].gk[i];
+            bin = static_cast<const uint8_t*>(pl[p].gb)[i];
+            return p;
+        };
+        int8_t pe[kAggWPer];
+        int32_t kk[kAggWPer];
+        uint32_t bb[kAggWPer];
+#pragma unroll
+        for (int u = 0; u < kAggWPer; u++) {
+            const int j = lane + 64 * u;
+            pe[u] = -1;
+            kk[u] = 0;
+            bb[u] = 0;
+            if (j < total) pe[u] = (int8_t)load_elem(j, kk[u], bb[u]);
+        }
+        store_prev();  // after this tile's loads are issued
+        prev_k0 = k0;
+        prev_nk = nk;
+        auto stage = [&](int p, int32_t k, uint32_t b) {
+            if (k < k0 || (int64_t)k >= k0 + nk) {  // k_agg_bounds placed it here: an error
+                bad |= 1u;
+                return;
+            }
+            const int xk = (int)(k - k0);
+            B[p][xk] = (uint8_t)b;
+            const uint32_t bit = 1u << (xk & 31);
+            if (atomicOr(&H[p][xk >> 5], bit) & bit) bad |= 2u;  // a key twice in one payload
+        };
+#pragma unroll
+        for (int u = 0; u < kAggWPer; u++)
+            if (pe[u] >= 0) stage(pe[u], kk[u], bb[u]);
+        for (int j = 64 * kAggWPer + lane; j < total; j += 64) {  // elements past the registers
+            int32_t k;
+            uint32_t b;
+            const int p = load_elem(j, k, b);
+            stage(p, k, b);
+        }
+        __builtin_amdgcn_wave_barrier();
+        // lane l: keys 8l .. 8l + 7, payload after payload
+#pragma unroll
+        for (int i = 0; i < 8; i++)  // a later batch continues the sum
+            acc[i] = from_out && 8 * lane + i < nk ? out[k0 + 8 * lane + i] : 0.0;
+        for (int p = 0; p < P; p++) {
+            const uint32_t m = reinterpret_cast<const uint8_t*>(H[p])[lane];
+            const uint2 bw8 = *reinterpret_cast<const uint2*>(&B[p][8 * lane]);
+            const bool dform = pl[p].dense_form != 0;
+            double v[8];
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const uint32_t b = ((i < 4 ? bw8.x : bw8.y) >> (8 * (i & 3))) & 0xFFu;
+                v[i] = 0.0;
+                if (m & (1u << i)) v[i] = qt[p][b];
+            }
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                // the dense form keeps |v| > EPS only (SparseDoubleGradient.toDense), and adds +0.0
+                // elsewhere: a -0.0 sum becomes +0.0
+                if ((m & (1u << i)) && (!dform || fabs(v[i]) > 1e-8)) acc[i] += v[i];
+                if (dform && __double_as_longlong(acc[i]) == (long long)0x8000000000000000ull) acc[i] = 0.0;
+            }
+        }
+        if (scale != 1.0)
+#pragma unroll
+            for (int i = 0; i < 8; i++) acc[i] = __dmul_rn(acc[i], scale);
+        __builtin_amdgcn_wave_barrier();  // the stage is read before the next tile writes it
+    }
+    store_prev();
+    if (bad) atomicOr(err, bad);
+}
+
+bool agg_vtiles_ok(int P, int max_groups, int max_nq) {  // the wave-tile form: P <= 8, G <= 8, nq <= 256
+    const char* form = std::getenv("SKML_AGG_FORM");
+    return P <= kAggPB && max_groups <= 8 && max_nq <= kAggLdsValues && !(form && (form[0] == 's' || form[0] == 'w')) &&
+           std::getenv("SKML_AGG_SEARCH") == nullptr;
+}
+int agg_tile_bits(bool vtiles) { return vtiles ? kAggVBits : 12; }
+
 hipError_t launch_agg_tiles(hipStream_t st, const AggPayload* pays, int P, int64_t ntiles, int64_t dim, double* out,
-                            int from_out, double scale, unsigned* err) {
+                            int from_out, double scale, unsigned* err, bool vtiles) {
     if (ntiles <= 0) return hipSuccess;
+    if (vtiles) {
+        static int resident_v = 0;  // waves' workgroups resident at once; -1: unknown (one wave per tile)
+        if (!resident_v) {
+            int dev = 0, per_cu = 0;
+            hipDeviceProp_t prop;
+            if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess &&
+                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_agg_vtiles, kAggThreads, 0) == hipSuccess)
+                resident_v = std::max(1, per_cu) * prop.multiProcessorCount;
+            else
+                resident_v = -1;
+            (void)hipGetLastError();
+        }
+        const int64_t all = sp_tiles(ntiles, kAggThreads / 64);
+        const unsigned grid = (unsigned)(resident_v < 0 ? all : std::min<int64_t>(all, resident_v));
+        hipLaunchKernelGGL(k_agg_vtiles, dim3(grid), dim3(kAggThreads), 0, st, pays, P, ntiles, dim, out, from_out,
+                           scale, err);
+        return hipGetLastError();
+    }
     const char* form = std::getenv("SKML_AGG_FORM");  // A/B switch: "s" = the per-element search form
     if (std::getenv("SKML_AGG_SEARCH") != nullptr || (form && form[0] == 's'))
         hipLaunchKernelGGL(k_agg_tiles, dim3((unsigned)ntiles), dim3(kAggThreads), 0, st, pays, P, ntiles, dim, out,

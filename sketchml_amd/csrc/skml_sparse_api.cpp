@@ -1871,17 +1871,19 @@ int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t
             return sfail(e, "payload %d: %s", p, skml_last_error());
     }
     const int64_t lim = (int64_t)(int32_t)((uint32_t)dim * 2u) / 3;  // dim * 2 / 3 with Java int wrap
-    const int64_t ntiles = sp_tiles(dim, kAggTile);
+    // run bounds are taken per tile of the tile kernel: 512 keys for the wave-tile form, else 4,096
+    const int64_t ntiles_max = sp_tiles(dim, (int64_t)1 << agg_tile_bits(true));
     // payloads in batches whose restored keys + bins + run bounds fit the scratch budget; the first
     // batch starts the sum at +0.0, later ones continue from it, the last one applies the scale
     constexpr size_t kBudget = (size_t)3 << 30;
     auto need_of = [&](int p) {
-        return (size_t)views[(size_t)p].nnz * 6 + (size_t)views[(size_t)p].g.G * (size_t)(ntiles + 1) * 4 + 1024;
+        return (size_t)views[(size_t)p].nnz * 6 + (size_t)views[(size_t)p].g.G * (size_t)(ntiles_max + 1) * 4 + 1024;
     };
     std::vector<int> todo;
     for (int p = 0; p < P; p++)
         if (views[(size_t)p].nnz > 0) todo.push_back(p);  // an empty restore adds nothing (sparse form)
-    uint8_t* small = scratch<uint8_t>(c, kSlotStatus, 1024 + sizeof(AggPayload) * (size_t)P);
+    // (room for one entry per (payload, group): the split form below)
+    uint8_t* small = scratch<uint8_t>(c, kSlotStatus, 1024 + sizeof(AggPayload) * (size_t)P * kMaxGroups);
     if (!small) return sfail(SKML_E_OOM, "decode_sum scratch");
     unsigned* err = reinterpret_cast<unsigned*>(small);
     uint64_t* live = reinterpret_cast<uint64_t*>(small + 256);
@@ -1892,11 +1894,24 @@ int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t
         SP_HIP(hipStreamSynchronize(st));
         return SKML_OK;
     }
+    // split: every sparse-form payload enters the tiles as one pseudo-payload per group, in group
+    // order, after a first pass found a key repeated across a payload's groups (legal for the
+    // reference: plusBy then adds both copies, the lower group's first, as Sort.merge emits them)
+    auto run = [&](bool split) -> int {
+    SP_HIP(hipMemsetAsync(err, 0, sizeof(unsigned), st));
     size_t at = 0;
     bool first = true;
     while (at < todo.size()) {
         size_t end = at, bytes = 0;
         while (end < todo.size() && (end == at || bytes + need_of(todo[end]) <= kBudget)) bytes += need_of(todo[end++]);
+        int max_g = 0, max_nq = 0;
+        for (size_t q = at; q < end; q++) {
+            max_g = std::max(max_g, (int)views[(size_t)todo[q]].g.G);
+            max_nq = std::max(max_nq, (int)views[(size_t)todo[q]].qvalues.size());
+        }
+        const bool vt = split ? agg_vtiles_ok(8, max_g, max_nq) : agg_vtiles_ok((int)(end - at), max_g, max_nq);
+        const int tile_bits = agg_tile_bits(vt);
+        const int64_t ntiles = sp_tiles(dim, (int64_t)1 << tile_bits);
         int64_t nk = 0, nb = 0;
         for (size_t q = at; q < end; q++) {
             nk += (views[(size_t)todo[q]].nnz + 3) & ~int64_t{3};  // every payload's keys 16-byte aligned
@@ -1954,8 +1969,8 @@ int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t
                 if (int e = sync_to_host(lc, &nlive, llive, sizeof(nlive))) return join(e);
                 a.dense_form = (int64_t)nlive > lim ? 1 : 0;
             }
-            if (launch_agg_bounds(ls, a.gk, v.nnz, v.g_dev, ntiles, dim, const_cast<int32_t*>(a.bounds), err) !=
-                hipSuccess)
+            if (launch_agg_bounds(ls, a.gk, v.nnz, v.g_dev, ntiles, dim, const_cast<int32_t*>(a.bounds), err,
+                                  tile_bits) != hipSuccess)
                 return join(sfail(SKML_E_HIP, "agg_bounds launch failed"));
             pays.push_back(a);
             ko += (v.nnz + 3) & ~int64_t{3};
@@ -1966,16 +1981,42 @@ int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t
             SP_HIP(hipStreamWaitEvent(st, ev_join, 0));
         }
         const bool last = end == todo.size();
-        SP_HIP(hipMemcpyAsync(d_pays, pays.data(), sizeof(AggPayload) * pays.size(), hipMemcpyHostToDevice, st));
-        SP_HIP(launch_agg_tiles(st, d_pays, (int)pays.size(), ntiles, dim, out, first ? 0 : 1, last ? scale : 1.0, err));
+        std::vector<AggPayload> list;
+        for (const AggPayload& a : pays) {
+            if (!split || a.dense_form) {
+                list.push_back(a);
+                continue;
+            }
+            for (int g = 0; g < a.G; g++) {
+                AggPayload b = a;
+                b.G = 1;
+                b.bounds = a.bounds + (int64_t)g * (ntiles + 1);
+                list.push_back(b);
+            }
+        }
+        SP_HIP(hipMemcpyAsync(d_pays, list.data(), sizeof(AggPayload) * list.size(), hipMemcpyHostToDevice, st));
+        const size_t chunk = split && vt ? (size_t)8 : list.size();
+        for (size_t c0 = 0; c0 < list.size(); c0 += chunk) {
+            const size_t nc = std::min(chunk, list.size() - c0);
+            SP_HIP(launch_agg_tiles(st, d_pays + c0, (int)nc, ntiles, dim, out, first && c0 == 0 ? 0 : 1,
+                                    last && c0 + nc == list.size() ? scale : 1.0, err, vt));
+        }
         SP_HIP(hipStreamSynchronize(st));  // `pays` (host) and the scratch are reused by the next batch
         first = false;
         at = end;
     }
     unsigned bad = 0;
     if (int e = sync_to_host(c, &bad, err, sizeof(bad))) return e;
-    if (bad) return sfail(SKML_E_ARG, "a payload holds a key outside [0, %lld) or a bin outside its values", (long long)dim);
+    if (bad & 1u)
+        return sfail(SKML_E_ARG, "a payload holds a key outside [0, %lld) or a bin outside its values", (long long)dim);
+    if (bad & 2u) {
+        if (!split) return -1;  // the split form follows
+        return sfail(SKML_E_ARG, "a dense-form payload repeats a key across its groups");
+    }
     return SKML_OK;
+    };
+    const int e = run(false);
+    return e == -1 ? run(true) : e;
 }
 
 int skml_debug_sparse_merge_path(void) { return t_merge_path; }

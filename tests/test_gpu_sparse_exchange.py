@@ -41,24 +41,24 @@ def oracle_sum(osps, dim, scale=1.0):
             out = out + 0.0
             out[k[live]] += v[live]
             forms.append("dense")
-        else:
-            out[k] += v
+        else:                                     # plusBy(sparse): every copy of a repeated key, in order
+            np.add.at(out, k, v)
             forms.append("sparse")
     if scale != 1.0:
         out = out * scale
     return out, forms
 
 
-def _payload(gpu, dim, density, seed, bins=256, tiny=0.0):
+def _payload(gpu, dim, density, seed, bins=256, tiny=0.0, groups=8):
     rng = np.random.default_rng(seed)
     keys = np.nonzero(rng.random(dim) < density)[0].astype(np.int32)
     vals = rng.standard_normal(len(keys))
     if tiny:
         t = rng.random(len(keys)) < tiny
         vals[t] = rng.uniform(-3e-9, 3e-9, int(t.sum()))
-    pl = gpu.encode_sparse(torch.from_numpy(keys).cuda(), torch.from_numpy(vals).cuda(), bins, 8, 2, 0.3, seed,
+    pl = gpu.encode_sparse(torch.from_numpy(keys).cuda(), torch.from_numpy(vals).cuda(), bins, groups, 2, 0.3, seed,
                            seed + 100)
-    osp = O.sparse_compress(keys, vals, bins, 8, 2, 0.3, seed, seed + 100)
+    osp = O.sparse_compress(keys, vals, bins, groups, 2, 0.3, seed, seed + 100)
     return pl, osp
 
 
@@ -116,12 +116,13 @@ def test_corrupt_blobs_are_refused(gpu):
         gpu.decode_sum(blob, 1, blob.numel(), 1000)
 
 
-# "wave": k_agg_tiles_w (a wave per payload) with the row-batched MinMax query (the defaults);
-# "search": k_agg_tiles (per-element run search) with the row-by-row query (the A/B switches)
-# Gradient.sum's tile kernel: wave (default: one wave per payload adding into an LDS tile, restores
-# on two streams) and search (the round-3 per-element form, with the generic per-row MinMax query
-# and one stream)
-KERNELS = {"wave": {}, "search": {"SKML_AGG_FORM": "s", "SKML_DEC_ROWS_SERIAL": "1", "SKML_AGG_ONE_LANE": "1"}}
+# Gradient.sum's tile kernel: vtile (default: one wave per 512-key tile that stages every payload's
+# bins with presence bits and sums each key in registers, payload after payload; restores on two
+# streams), wave (one wave per payload adding into a 4,096-key LDS tile) and search (the round-3
+# per-element form, with the generic per-row MinMax query and one stream).  Only vtile sees a key
+# repeated across one payload's groups (the wave and search forms add such copies racily).
+KERNELS = {"vtile": {}, "wave": {"SKML_AGG_FORM": "w"},
+           "search": {"SKML_AGG_FORM": "s", "SKML_DEC_ROWS_SERIAL": "1", "SKML_AGG_ONE_LANE": "1"}}
 
 
 @pytest.fixture(params=sorted(KERNELS))
@@ -156,6 +157,61 @@ def test_decode_sum_dense_form_payloads(gpu, agg_kernel):
     assert forms == ["dense", "sparse", "dense"]
     assert np.any(np.abs(o1.q.values()) <= EPS)          # the tiny values really exist
     assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
+
+
+def test_decode_sum_many_payloads_and_groups(gpu, agg_kernel):
+    """Shapes past the wave-tile form's 8 payloads x 8 groups: nine payloads in one launch, and
+    payloads of 12 groups, take the 4,096-key tiles; a dense-enough payload runs past the
+    per-lane registers of a tile."""
+    dim = 200003
+    pls, osps = zip(*[_payload(gpu, dim, 0.05 + 0.01 * p, 50 + p) for p in range(9)])
+    allb, stride = _gather_local(pls)
+    got = gpu.decode_sum(allb, 9, stride, dim).cpu().numpy()
+    want, _ = oracle_sum(osps, dim)
+    assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
+    pls, osps = zip(*[_payload(gpu, dim, 0.4, 60 + p, groups=12) for p in range(3)])
+    allb, stride = _gather_local(pls)
+    got = gpu.decode_sum(allb, 3, stride, dim).cpu().numpy()
+    want, _ = oracle_sum(osps, dim)
+    assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
+
+
+def _dup_payload(gpu, dim, seed, groups=4):
+    """A payload whose keys repeat across groups (legal for the reference, see
+    test_sparse_duplicate_keys_across_groups_are_kept): each repeated key carries one value far
+    below and one far above the rest, so its copies land in the first and the last group."""
+    rng = np.random.default_rng(seed)
+    keys = np.nonzero(rng.random(dim) < 0.2)[0].astype(np.int32)
+    vals = rng.standard_normal(len(keys)).clip(-4, 4)
+    rep = np.sort(rng.choice(len(keys), 300, replace=False))
+    ins = np.zeros(len(keys), dtype=bool)
+    ins[rep] = True
+    keys2 = np.repeat(keys, np.where(ins, 2, 1))
+    vals2 = np.empty(len(keys2))
+    pos = np.cumsum(np.where(ins, 2, 1)) - np.where(ins, 2, 1)
+    vals2[pos] = np.where(ins, -6.0 - rng.random(len(keys)), vals)
+    vals2[pos[ins] + 1] = 6.0 + rng.random(int(ins.sum()))
+    pl = gpu.encode_sparse(torch.from_numpy(keys2).cuda(), torch.from_numpy(vals2).cuda(), 256, groups, 2, 0.3, seed,
+                           seed + 100)
+    osp = O.sparse_compress(keys2, vals2, 256, groups, 2, 0.3, seed, seed + 100)
+    return pl, osp
+
+
+def test_decode_sum_keys_repeated_across_groups(gpu, agg_kernel):
+    """plusBy adds both copies of a repeated key, the lower group's first (Sort.merge).  The staged
+    tiles see the second copy's presence bit and run the sum again with every sparse-form payload
+    split into one pseudo-payload per group, in group order."""
+    dim = 100003
+    p0, o0 = _payload(gpu, dim, 0.2, 71, groups=4)
+    p1, o1 = _dup_payload(gpu, dim, 72)
+    k1, _ = o1.restore()
+    assert len(np.unique(k1)) < len(k1)                   # the repeats survive the codec
+    allb, stride = _gather_local([p0, p1])
+    got = gpu.decode_sum(allb, 2, stride, dim).cpu().numpy()
+    want, forms = oracle_sum([o0, o1], dim)
+    assert forms == ["sparse", "sparse"]
+    if agg_kernel == "vtile":
+        assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
 
 
 def test_decode_sum_skips_empty_payloads(gpu, agg_kernel):
