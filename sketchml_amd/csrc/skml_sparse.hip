@@ -2660,7 +2660,9 @@ hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, con
             if (edges.n == 0 || edges.t[edges.n - 1] != t) edges.t[edges.n++] = t;
         }
     }
-    const bool nt = std::getenv("SKML_DEC_NT") != nullptr;  // (A/B switch: nontemporal streams)
+    // nontemporal streams (decode 0.73 -> 0.71 ms, profiles/ab/r04_sparse_restore_aggregate.txt);
+    // SKML_DEC_TEMPORAL=1 is the A/B switch back
+    const bool nt = std::getenv("SKML_DEC_TEMPORAL") == nullptr;
 #define SKML_DEC_LAUNCH(TNT, MODE, GRID, TILES, TNPTR)                                                            \
     hipLaunchKernelGGL((k_dec_keys<TNT, MODE>), dim3(GRID), dim3(kDecThreads), 0, st, delta, n, gp, tile_base, gpre, \
                        table, TNPTR, gkeys, gbins, nq, gbn, bn_width, err, TILES)
@@ -2919,9 +2921,31 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_tiles(const AggPayload* __r
 // payload).  Up to kAggWPer elements per lane are held in registers, a longer payload (a dense
 // form, or a tile far denser than the mean) adds the rest in further rounds of its turn.
 constexpr int kAggWPer = 8;
+// How a persistent grid walks the tiles.  kWalkPlain (the default): unit u = b * units-per-
+// workgroup + sub takes tiles u, u + units, ..., so all units sweep the sum together (one write
+// front).  kWalkXcd: the units renumbered so that each XCD's workgroups (b % 8, the dispatcher's
+// round robin) take consecutive tiles in every round, keeping neighbouring tiles' lines in one L2
+// (measured equal: 1,826 against 1,822 us).  kWalkContig: each unit a contiguous share of the tiles
+// (measured slower, 5.87-5.92 -> 6.60-6.62 ms end to end: 4,096 separate write fronts).
+// profiles/ab/r04_sparse_aggregate_tiles.txt.
+constexpr int kWalkPlain = 0, kWalkContig = 1, kWalkXcd = 2;
+struct TileWalk {
+    int64_t t0, t1, step;
+};
+__device__ __forceinline__ TileWalk tile_walk(int64_t blk, int64_t nblk, int sub, int nsub, int64_t ntiles, int walk) {
+    const int64_t units = nblk * nsub;
+    if (walk == kWalkContig) {
+        const int64_t unit = blk * nsub + sub, per = (ntiles + units - 1) / units;
+        return {unit * per, std::min<int64_t>(ntiles, unit * per + per), 1};
+    }
+    int64_t unit = blk * nsub + sub;
+    if (walk == kWalkXcd && nblk % 8 == 0) unit = ((blk & 7) * (nblk >> 3) + (blk >> 3)) * nsub + sub;
+    return {unit, ntiles, units};
+}
 __global__ __launch_bounds__(kAggThreads) void k_agg_tiles_w(const AggPayload* __restrict__ pays, int P,
                                                             int64_t ntiles, int64_t dim, double* __restrict__ out,
-                                                            int from_out, double scale, unsigned* __restrict__ err) {
+                                                            int from_out, double scale, unsigned* __restrict__ err,
+                                                            int walk) {
     static_assert(kAggThreads / 64 == kAggPB, "one wave per payload of a batch");
     __shared__ double acc[kAggTile];
     __shared__ double qt[kAggPB][kAggLdsValues];
@@ -2952,7 +2976,8 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_tiles_w(const AggPayload* _
             nb1 = bd[tt + 1];
         }
     };
-    fetch_bounds(blockIdx.x);
+    const TileWalk tw = tile_walk(blockIdx.x, gridDim.x, 0, 1, ntiles, walk);
+    fetch_bounds(tw.t0);
     unsigned bad = 0;
     // The store of tile t - 1 is deferred until tile t's element loads are in flight, and the
     // zeroing of the LDS sum follows it, so both overlap those loads' latency.
@@ -2962,10 +2987,10 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_tiles_w(const AggPayload* _
             for (int x = threadIdx.x; x < prev_nk; x += kAggThreads)
                 out[prev_k0 + x] = scale == 1.0 ? acc[x] : __dmul_rn(acc[x], scale);
     };
-    for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    for (int64_t t = tw.t0; t < tw.t1; t += tw.step) {
         const int64_t k0 = t * kAggTile, nk = std::min<int64_t>(kAggTile, dim - k0);
         const int32_t cb0 = nb0, cb1 = nb1;  // this tile's bounds (one batch)
-        fetch_bounds(t + gridDim.x);
+        fetch_bounds(t + tw.step);
         for (int p0 = 0; p0 < P; p0 += kAggPB) {
             const int np = std::min(kAggPB, P - p0);
             __syncthreads();  // the previous batch / tile is done with qt / rb / rs / acc's adds
@@ -3088,15 +3113,18 @@ constexpr int kAggVBits = 9, kAggVTile = 1 << kAggVBits;
 static_assert(kAggVTile == 8 * 64, "eight keys per lane");
 __global__ __launch_bounds__(kAggThreads) void k_agg_vtiles(const AggPayload* __restrict__ pays, int P,
                                                            int64_t ntiles, int64_t dim, double* __restrict__ out,
-                                                           int from_out, double scale, unsigned* __restrict__ err) {
+                                                           int from_out, double scale, unsigned* __restrict__ err,
+                                                           int walk) {
     constexpr int kWaves = kAggThreads / 64;
-    __shared__ uint8_t bins[kWaves][kAggPB][kAggVTile];  // the stage: a bin per (payload, key)
+    // the stage: a bin per (payload, key); between tiles, the transpose of the stored sums
+    __shared__ __attribute__((aligned(16))) uint8_t bins[kWaves][kAggPB][kAggVTile];
+    static_assert(kAggPB * kAggVTile == kAggVTile * sizeof(double), "a tile of sums fits the stage");
     __shared__ uint32_t here[kWaves][kAggPB][kAggVTile / 32];  // presence bits
     __shared__ double qt[kAggPB][kAggLdsValues];
     __shared__ int32_t pre[kWaves][65];  // the wave's 64 run pieces, scanned
     __shared__ int32_t pb0[kWaves][64];  // each piece's first element in its payload
     __shared__ AggPayload pl[kAggPB];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (threadIdx.x < P * (int)(sizeof(AggPayload) / 8))
         reinterpret_cast<uint64_t*>(pl)[threadIdx.x] = reinterpret_cast<const uint64_t*>(pays)[threadIdx.x];
     __syncthreads();
@@ -3119,26 +3147,32 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_vtiles(const AggPayload* __
     };
     double acc[8];
     int64_t prev_k0 = -1, prev_nk = 0;
-    auto store_prev = [&]() {  // lane l's 8 keys of the previous tile
+    // a tile's sums (lane l: keys 8l .. 8l + 7) wait in the stage until the next tile's loads are
+    // in flight, and leave transposed, so each 16-byte store instruction covers 1 KB of the sum
+    double* T = reinterpret_cast<double*>(&B[0][0]);
+    auto store_prev = [&]() {
         if (prev_k0 < 0) return;
-        const int x0 = 8 * lane;
-        double* o = out + prev_k0 + x0;
-        if (x0 + 8 <= prev_nk && (reinterpret_cast<uintptr_t>(o) & 15) == 0) {
+        double* o = out + prev_k0;
+        const bool whole = prev_nk == kAggVTile && (reinterpret_cast<uintptr_t>(o) & 15) == 0;
 #pragma unroll
-            for (int q = 0; q < 4; q++)
-                *reinterpret_cast<double2*>(o + 2 * q) = make_double2(acc[2 * q], acc[2 * q + 1]);
-        } else {
-#pragma unroll
-            for (int i = 0; i < 8; i++)
-                if (x0 + i < prev_nk) o[i] = acc[i];
+        for (int q = 0; q < 4; q++) {
+            const int x = 128 * q + 2 * lane;
+            const double2 v = *reinterpret_cast<const double2*>(T + x);
+            if (whole) {
+                *reinterpret_cast<double2*>(o + x) = v;
+            } else {
+                if (x < prev_nk) o[x] = v.x;
+                if (x + 1 < prev_nk) o[x + 1] = v.y;
+            }
         }
+        __builtin_amdgcn_wave_barrier();
     };
-    int64_t t = (int64_t)blockIdx.x * kWaves + wave;
-    fetch(t);
-    for (; t < ntiles; t += nw) {
+    const TileWalk tw = tile_walk(blockIdx.x, gridDim.x, wave, kWaves, ntiles, walk);
+    fetch(tw.t0);
+    for (int64_t t = tw.t0; t < tw.t1; t += tw.step) {
         const int64_t k0 = t << kAggVBits, nk = std::min<int64_t>(kAggVTile, dim - k0);
         const int32_t b0 = nb0, b1 = nb1;
-        fetch(t + nw);
+        fetch(t + tw.step);
         const int32_t len = lane_on && b1 > b0 ? b1 - b0 : 0;
         int32_t x = len;
 #pragma unroll
@@ -3227,7 +3261,11 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_vtiles(const AggPayload* __
         if (scale != 1.0)
 #pragma unroll
             for (int i = 0; i < 8; i++) acc[i] = __dmul_rn(acc[i], scale);
-        __builtin_amdgcn_wave_barrier();  // the stage is read before the next tile writes it
+        __builtin_amdgcn_wave_barrier();  // the stage is read before the sums replace it
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            *reinterpret_cast<double2*>(T + 8 * lane + 2 * q) = make_double2(acc[2 * q], acc[2 * q + 1]);
+        __builtin_amdgcn_wave_barrier();
     }
     store_prev();
     if (bad) atomicOr(err, bad);
@@ -3243,6 +3281,9 @@ int agg_tile_bits(bool vtiles) { return vtiles ? kAggVBits : 12; }
 hipError_t launch_agg_tiles(hipStream_t st, const AggPayload* pays, int P, int64_t ntiles, int64_t dim, double* out,
                             int from_out, double scale, unsigned* err, bool vtiles) {
     if (ntiles <= 0) return hipSuccess;
+    // (A/B switches: SKML_AGG_WALK=xcd / contig)
+    const char* wk = std::getenv("SKML_AGG_WALK");
+    const int walk = !wk ? kWalkPlain : wk[0] == 'c' ? kWalkContig : wk[0] == 'x' ? kWalkXcd : kWalkPlain;
     if (vtiles) {
         static int resident_v = 0;  // waves' workgroups resident at once; -1: unknown (one wave per tile)
         if (!resident_v) {
@@ -3258,7 +3299,7 @@ hipError_t launch_agg_tiles(hipStream_t st, const AggPayload* pays, int P, int64
         const int64_t all = sp_tiles(ntiles, kAggThreads / 64);
         const unsigned grid = (unsigned)(resident_v < 0 ? all : std::min<int64_t>(all, resident_v));
         hipLaunchKernelGGL(k_agg_vtiles, dim3(grid), dim3(kAggThreads), 0, st, pays, P, ntiles, dim, out, from_out,
-                           scale, err);
+                           scale, err, walk);
         return hipGetLastError();
     }
     const char* form = std::getenv("SKML_AGG_FORM");  // A/B switch: "s" = the per-element search form
@@ -3282,7 +3323,7 @@ hipError_t launch_agg_tiles(hipStream_t st, const AggPayload* pays, int P, int64
             (unsigned)(std::getenv("SKML_AGG_GRID_ALL") != nullptr || resident < 0 ? ntiles
                                                                                   : std::min<int64_t>(ntiles, resident));
         hipLaunchKernelGGL(k_agg_tiles_w, dim3(grid), dim3(kAggThreads), 0, st, pays, P, ntiles, dim, out, from_out,
-                           scale, err);
+                           scale, err, walk);
     }
     return hipGetLastError();
 }

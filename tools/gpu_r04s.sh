@@ -1,8 +1,8 @@
-# r04s: k_dec_keys with nontemporal streams (SKML_DEC_NT) A/B, and its L2 hit / miss counters
+# r04s: k_dec_keys with nontemporal streams (SKML_DEC_NT) and k_rs_merge's per-word emission (SKML_RS_EMIT_BITS) A/B, and its L2 hit / miss counters
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/r04s
 set -e
 for i in 1 2 3; do
-  for V in base:SKML_AB_DEFAULT=1 nt:SKML_DEC_NT=1; do
+  for V in base:SKML_AB_DEFAULT=1 nt:SKML_DEC_NT=1 bits:SKML_RS_EMIT_BITS=1; do
     env "${V#*:}" timeout -k 10 200 python tools/bench_sparse.py --reps 5 --aggregate 8 > gpurun_out/r04s/${V%%:*}_$i.json 2>&1
     python3 -c "
 import json
