@@ -487,23 +487,31 @@ __global__ __launch_bounds__(256) void k_decode_sum(const uint8_t* __restrict__ 
 // P x bins doubles of dynamic LDS instead of a 32 KB array, and the next step's codes are loaded
 // before this step's lookups.
 constexpr int kOccPer = 8, kOccMaxP = 8;
-__device__ __forceinline__ void load_codes8(const uint8_t* codes, int64_t e0, int bits, uint32_t (&w)[4]) {
+// The code loads go through a global (address space 1) pointer: the payloads' code pointers sit in
+// LDS, and loads through a generic pointer would be flat loads, which count on lgkmcnt too, so the
+// table lookups' LDS waits would also wait for the next step's prefetched codes.
+#define SKML_G(T) const __attribute__((address_space(1))) T*
+__device__ __forceinline__ void load_codes8(const uint8_t* codes_any, int64_t e0, int bits, uint32_t (&w)[4]) {
+    SKML_G(uint8_t) codes = (SKML_G(uint8_t))codes_any;
     switch (bits) {
         case 8: {
-            const uint2 v = *reinterpret_cast<const uint2*>(codes + e0);
+            typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+            const u32x2_t v = *(SKML_G(u32x2_t))(codes + e0);
             w[0] = v.x; w[1] = v.y;
             break;
         }
         case 16: {
-            const uint4 v = *reinterpret_cast<const uint4*>(codes + 2 * e0);
+            typedef uint32_t u32x4_g __attribute__((ext_vector_type(4)));
+            const u32x4_g v = *(SKML_G(u32x4_g))(codes + 2 * e0);
             w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
             break;
         }
-        case 4: w[0] = *reinterpret_cast<const uint32_t*>(codes + e0 / 2); break;
-        case 2: w[0] = *reinterpret_cast<const uint16_t*>(codes + e0 / 4); break;
+        case 4: w[0] = *(SKML_G(uint32_t))(codes + e0 / 2); break;
+        case 2: w[0] = *(SKML_G(uint16_t))(codes + e0 / 4); break;
         default: w[0] = codes[e0 / 8]; break;
     }
 }
+#undef SKML_G
 __device__ __forceinline__ uint32_t code8_at(const uint32_t (&w)[4], int e, int bits) {
     switch (bits) {
         case 8: return (w[e >> 2] >> (8 * (e & 3))) & 255u;

@@ -1,0 +1,19 @@
+# r04w: wave-per-payload tiles as the default again (global payload loads, lane tags for keys
+# repeated across groups); vtile = SKML_AGG_FORM=v; prev = the r04zz library (sketchml_amd/lib_prev).
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/r04w
+set -e
+timeout -k 10 400 python -u -m pytest tests/test_gpu_sparse_exchange.py tests/test_gpu_sparse.py tests/test_gpu_dense.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/r04w/tests.log 2>&1
+tail -1 gpurun_out/r04w/tests.log
+for i in 1 2 3; do
+  for V in "wave:SKML_AB_DEFAULT=1" "vtile:SKML_AGG_FORM=v" "prev:SKML_LIB=sketchml_amd/lib_prev/libskml.so"; do
+    N=${V%%:*}
+    env ${V#*:} timeout -k 10 200 python tools/bench_sparse.py --reps 5 --aggregate 8 > gpurun_out/r04w/${N}_$i.json 2>&1
+    python3 -c "
+import json
+d = json.loads(open('gpurun_out/r04w/${N}_$i.json').read().strip().splitlines()[-1])
+print('$N', $i, {k: d['ms'][k] for k in ('decode', 'decode_sum')})"
+  done
+done
+SKML_AGG_ONE_LANE=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r04w/prof -o run --output-format csv -- python3 tools/bench_sparse.py --reps 2 --aggregate 8 > gpurun_out/r04w/prof.json 2>&1
+python3 tools/kstats_cmp.py gpurun_out/r04w/prof gpurun_out/r04w/prof k_agg k_dec k_rs > gpurun_out/r04w/kstats.txt
+cat gpurun_out/r04w/kstats.txt
