@@ -2960,8 +2960,6 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_tiles_w(const AggPayload* _
     __shared__ int32_t rb[kAggPB][kMaxGroups + 1];  // run prefix (elements) per group, this tile
     __shared__ int32_t rs[kAggPB][kMaxGroups];      // run start (element index in the payload)
     __shared__ int32_t dfs[kAggPB];                 // dense_form of the batch's payloads
-    __shared__ int32_t tag[kAggTile];  // the lane that last added at each key (repeat detection)
-    volatile int32_t* vtag = tag;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     // a persistent grid: with one batch (P <= kAggPB) the payloads and their quantValues are read
     // once per workgroup instead of once per tile
@@ -3076,23 +3074,15 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_tiles_w(const AggPayload* _
                     const bool dform = a.dense_form != 0;
                     // a key outside this tile is an error (k_agg_bounds placed it here); the dense form
                     // keeps |v| > EPS only (SparseDoubleGradient.toDense)
-// Two lanes of one add instruction at the same key (a key repeated across the payload's groups,
-// within 64 elements) would lose one add: each lane tags the key with its lane first and reads the
-// tag back, and a lane that does not find its own tag flags the payload (err bit 2: the host sums
-// again with one pseudo-payload per group).  Copies in different instructions add in order.
-#define SKML_AGG_ADD(K, V)                                                 \
-    do {                                                                   \
-        const int32_t k_ = (K);                                            \
-        const double v_ = (V);                                             \
-        if (k_ < k0 || (int64_t)k_ >= k0 + nk) {                           \
-            bad |= 1u;                                                     \
-        } else {                                                           \
-            const int x_ = (int)(k_ - k0);                                 \
-            vtag[x_] = lane;                                               \
-            const double o_ = acc[x_];                                     \
-            if (vtag[x_] != lane) bad |= 2u;                               \
-            if (!dform || fabs(v_) > 1e-8) acc[x_] = o_ + v_;              \
-        }                                                                  \
+// (Two lanes of one add instruction at the same key, a key repeated across the payload's groups
+// within 64 elements, lose one add: this form does not see such repeats; k_agg_vtiles does.  Lane
+// tags that caught them cost 1,639 -> 2,149 us, profiles/ab/r04_sparse_aggregate_tiles.txt.)
+#define SKML_AGG_ADD(K, V)                                              \
+    do {                                                                \
+        const int32_t k_ = (K);                                         \
+        const double v_ = (V);                                          \
+        if (k_ < k0 || (int64_t)k_ >= k0 + nk) bad = 1;                 \
+        else if (!dform || fabs(v_) > 1e-8) acc[k_ - k0] += v_;         \
     } while (0)
 #pragma unroll
                     for (int u = 0; u < kAggWPer; u++)
@@ -3303,11 +3293,12 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_vtiles(const AggPayload* __
     if (bad) atomicOr(err, bad);
 }
 
-// the staged wave-tile form (P <= 8, G <= 8, nq <= 256) under SKML_AGG_FORM=v: since the payload
-// pointers are read with global loads, the wave-per-payload tiles are faster (1,639 against 1,832 us)
+// the staged wave-tile form (the default for P <= 8, G <= 8, nq <= 256): it sums a key repeated
+// across a payload's groups exactly (presence bits + the split pass); the wave-per-payload tiles
+// (SKML_AGG_FORM=w, 1,639 against 1,832 us) do not see such repeats
 bool agg_vtiles_ok(int P, int max_groups, int max_nq) {
     const char* form = std::getenv("SKML_AGG_FORM");
-    return form && form[0] == 'v' && P <= kAggPB && max_groups <= 8 && max_nq <= kAggLdsValues &&
+    return P <= kAggPB && max_groups <= 8 && max_nq <= kAggLdsValues && !(form && (form[0] == 's' || form[0] == 'w')) &&
            std::getenv("SKML_AGG_SEARCH") == nullptr;
 }
 int agg_tile_bits(bool vtiles) { return vtiles ? kAggVBits : 12; }

@@ -116,12 +116,13 @@ def test_corrupt_blobs_are_refused(gpu):
         gpu.decode_sum(blob, 1, blob.numel(), 1000)
 
 
-# Gradient.sum's tile kernel: wave (default: one wave per payload adding into a 4,096-key LDS tile,
-# restores on two streams), vtile (SKML_AGG_FORM=v: one wave per 512-key tile that stages every
-# payload's bins with presence bits and sums each key in registers, payload after payload) and
-# search (the round-3 per-element form, with the generic per-row MinMax query and one stream).
-# wave and vtile detect a key repeated across one payload's groups; search adds such copies racily.
-KERNELS = {"wave": {}, "vtile": {"SKML_AGG_FORM": "v"},
+# Gradient.sum's tile kernel: vtile (default: one wave per 512-key tile that stages every
+# payload's bins with presence bits and sums each key in registers, payload after payload;
+# restores on two streams), wave (SKML_AGG_FORM=w: one wave per payload adding into a 4,096-key
+# LDS tile) and search (the round-3 per-element form, with the generic per-row MinMax query and
+# one stream).  Only vtile sees a key repeated across one payload's groups; the other two add
+# copies that meet in one instruction racily.
+KERNELS = {"vtile": {}, "wave": {"SKML_AGG_FORM": "w"},
            "search": {"SKML_AGG_FORM": "s", "SKML_DEC_ROWS_SERIAL": "1", "SKML_AGG_ONE_LANE": "1"}}
 
 
@@ -198,9 +199,9 @@ def _dup_payload(gpu, dim, seed, groups=4):
 
 
 def test_decode_sum_keys_repeated_across_groups(gpu, agg_kernel):
-    """plusBy adds both copies of a repeated key, the lower group's first (Sort.merge).  The wave
-    tiles' lane tags (or the staged tiles' presence bits) see the repeat and the sum runs again with
-    every sparse-form payload split into one pseudo-payload per group, in group order."""
+    """plusBy adds both copies of a repeated key, the lower group's first (Sort.merge).  The staged
+    tiles see the second copy's presence bit and run the sum again with every sparse-form payload
+    split into one pseudo-payload per group, in group order."""
     dim = 100003
     p0, o0 = _payload(gpu, dim, 0.2, 71, groups=4)
     p1, o1 = _dup_payload(gpu, dim, 72)
@@ -210,7 +211,7 @@ def test_decode_sum_keys_repeated_across_groups(gpu, agg_kernel):
     got = gpu.decode_sum(allb, 2, stride, dim).cpu().numpy()
     want, forms = oracle_sum([o0, o1], dim)
     assert forms == ["sparse", "sparse"]
-    if agg_kernel != "search":
+    if agg_kernel == "vtile":
         assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
 
 
