@@ -38,6 +38,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--warmup-ms", type=float, default=60.0,
+                    help="continue the warm-up until this much wall time has passed (the engine clock "
+                         "settles after ~25 ms of sustained encodes)")
     ap.add_argument("--n", type=int, default=2**28, help="floats per GPU bucket (default: the north-star 2^28)")
     ap.add_argument("--bins", type=int, default=256)
     ap.add_argument("--buffers", type=int, default=0,
@@ -293,9 +296,7 @@ def other_configs(sk, lib, ctx, dev):
     out["dense_decode_sum_c4"] = dense_decode_sum(sk, lib, ctx, dev, xs, n, p)
     del xs
     dim = 2**28
-    g = torch.Generator(device=dev).manual_seed(3)
-    d = torch.randn(dim, device=dev, generator=g)
-    d[torch.rand(dim, device=dev, generator=g) >= 0.1] = 0.0
+    d = c3_dense(dev, 3, dim)
     te, spl = timed_median(lambda: sk.encode_dense_as_sparse(d, 256, 8, 2, 0.3, 3, 3), 5)
     td, (rk, rv) = timed_median(lambda: spl.restore(), 5)
     nnz = int(rk.numel())
@@ -305,38 +306,53 @@ def other_configs(sk, lib, ctx, dev):
                         "roofline_frac": round(alg / te / 1e9 / HBM_PEAK_GBS, 4), "restore_ms": round(td * 1e3, 3),
                         "note": "median wall time of 5 synchronised calls (one nnz read after the compaction, one read-back at the end)"}
     del d, rk, rv
-    out["sparse_aggregate"] = sparse_aggregate(sk, spl, dim, timed_median)
+    out["sparse_aggregate"] = sparse_aggregate(sk, spl, dim, timed_median, dev)
     return out
 
 
-def sparse_aggregate(sk, spl, dim, timed_median, P=8):
+def c3_dense(dev, seed, dim=2**28):
+    """A C3-shaped dense gradient: N(0, 1), 10 % of the entries kept; rank r's is seed 3 + r."""
+    g = torch.Generator(device=dev).manual_seed(seed)
+    d = torch.randn(dim, device=dev, generator=g)
+    d[torch.rand(dim, device=dev, generator=g) >= 0.1] = 0.0
+    return d
+
+
+def sparse_aggregate(sk, spl, dim, timed_median, dev, P=8):
     """The ml path's DP step after the all-gather: P exported C3 payloads in
     stride-spaced slots -> Gradient.sum in double on the device (skml_sparse_decode_sum_f64), plus
-    the export itself.  The P slots hold copies of one C3 payload (every rank's payload has the
-    C3 shape; the cost per payload does not depend on its values)."""
+    the export itself.  The P payloads are distinct, as in the DP step: rank r's C3 gradient
+    (dense seed 3 + r, the sparse_exchange_step data) encoded with seeds 3 + r; their keys cover
+    ~57 % of the dims.  tests/test_gpu_sparse_exchange.py checks this exact sum against the oracle."""
     from sketchml_amd.distributed import blob_stride
-    nb = spl.export_bytes()
-    stride = blob_stride([nb])
-    allb = torch.empty(stride * P, dtype=torch.uint8, device="cuda")
+    pls = [spl]
+    for r in range(1, P):
+        d = c3_dense(dev, 3 + r, dim)
+        pls.append(sk.encode_dense_as_sparse(d, 256, 8, 2, 0.3, 3 + r, 3 + r))
+        del d
+    sizes = [p.export_bytes() for p in pls]
+    stride = blob_stride(sizes)
+    allb = torch.zeros(stride * P, dtype=torch.uint8, device="cuda")
     tx, _ = timed_median(lambda: spl.export(allb[:stride]), 5)
     for q in range(1, P):
-        allb[q * stride:(q + 1) * stride].copy_(allb[:stride])
+        pls[q].export(allb[q * stride:(q + 1) * stride])
     out = torch.empty(dim, dtype=torch.float64, device="cuda")
-    ts, _ = timed_median(lambda: sk.decode_sum(allb, P, stride, dim, 1.0 / P, out), 3)
-    t1, _ = timed_median(lambda: sk.decode_sum(allb, 1, stride, dim, 1.0, out), 3)
-    nnz = spl.nnz()
+    ts, _ = timed_median(lambda: sk.decode_sum(allb, P, stride, dim, 1.0 / P, out), 5)
+    t1, _ = timed_median(lambda: sk.decode_sum(allb, 1, stride, dim, 1.0, out), 5)
+    nnz = [p.nnz() for p in pls]
     # algorithmic bytes: every blob read once, the 2^28 double sum written once
-    alg = P * nb + 8.0 * dim
-    res = {"workload": f"Gradient.sum of {P} C3 sparse payloads (nnz {nnz} each) into a 2^28-dim double sum, x 1/{P}",
-           "blob_bytes": nb, "export_ms": round(tx * 1e3, 3), "decode_sum_ms": round(ts * 1e3, 3),
+    alg = float(sum(sizes)) + 8.0 * dim
+    res = {"workload": f"Gradient.sum of {P} distinct C3 sparse payloads (dense seeds 3..{2 + P}, nnz {min(nnz)}.."
+                       f"{max(nnz)}) into a 2^28-dim double sum, x 1/{P}",
+           "blob_bytes": sizes, "export_ms": round(tx * 1e3, 3), "decode_sum_ms": round(ts * 1e3, 3),
            "decode_sum_one_payload_ms": round(t1 * 1e3, 3),
            "per_payload_ms": round((ts - t1) / (P - 1) * 1e3, 3),
            "alg_bytes": alg, "roofline_frac": round(alg / ts / 1e9 / HBM_PEAK_GBS, 4),
-           "note": "median wall time of synchronised calls; one payload = DeltaAdaptive decode + MinMax query "
-                   "(restores alternate between two streams) + add into the double sum tile by tile in payload "
-                   "order (persistent tiles; no Sort.merge: keys are unique); the fixed part is the 2 GiB write "
-                   "of the sum (the x 1/P scale is fused into it); alg_bytes = P blobs read + the sum written"}
-    del allb, out
+           "note": "8 distinct payloads; median wall time of 5 synchronised calls; one payload = DeltaAdaptive "
+                   "decode + MinMax query (restores alternate between two streams) + add into the double sum tile "
+                   "by tile in payload order; the fixed part is the 2 GiB write of the sum (the x 1/P scale is fused "
+                   "into it); alg_bytes = P blobs read + the sum written"}
+    del allb, out, pls
     return res
 
 
@@ -425,9 +441,7 @@ def sparse_exchange_step(sk, exch, dev, rank, world, barrier, reps=3):
     computes Gradient.sum x 1/P in double.  Max over ranks of the median of `reps` steps."""
     from sketchml_amd import distributed as D
     dim = 2**28
-    g = torch.Generator(device=dev).manual_seed(3 + rank)
-    d = torch.randn(dim, device=dev, generator=g)
-    d[torch.rand(dim, device=dev, generator=g) >= 0.1] = 0.0
+    d = c3_dense(dev, 3 + rank, dim)
     spl = sk.encode_dense_as_sparse(d, 256, 8, 2, 0.3, 3 + rank, 3 + rank)
     del d
     nb = spl.export_bytes()
@@ -649,26 +663,49 @@ def main():
         if dist.is_initialized():
             dist.barrier()
 
-    for i in range(args.warmup):
+    # warm-up: W untimed steps, continued until --warmup-ms of wall time has passed.  The engine
+    # clock needs ~25 ms of sustained load to settle: in a kernel trace of the first 85 encodes
+    # (profiles/r05b_warmup_ramp.txt) the leaf runs 400-445 us for the first ten and settles at
+    # ~340 us after ~40; five steps (3 ms) leave the timed region inside that ramp.
+    # Every rank runs the same number of steps (each step may hold a collective).
+    t_w = time.perf_counter()
+    nwarm = max(1, args.warmup)
+    for i in range(nwarm):
         step(i)
     torch.cuda.synchronize()
-    # live HIP-event timing of the leaf kernel only (two events per step), on the codec stream
+    el_ms = (time.perf_counter() - t_w) * 1e3
+    extra = 0 if el_ms >= args.warmup_ms else int(np.ceil((args.warmup_ms - el_ms) / (el_ms / nwarm)))
+    if world > 1:
+        t = torch.tensor([extra], device=dev, dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        extra = int(t.item())
+    for i in range(extra):
+        step(nwarm + i)
+    nwarm += extra
+    torch.cuda.synchronize()
+
+    def timed_region(first):
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            step(first + i)
+        torch.cuda.synchronize()
+        barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
+
+    # the headline: K encodes, nothing else on the stream
+    elapsed = timed_region(nwarm)
+    # the same K encodes again with HIP events around the leaf launches only (on the codec
+    # stream): the live kernel time of the roofline, measured outside the headline's region
     lib.skml_ctx_set_timing(ctx, 1 << 0)
     lib.skml_ctx_reset_stats(ctx)
-
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(args.warmup + i)
-    torch.cuda.synchronize()
-    barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed_ev = timed_region(nwarm + args.steps)
     lib.skml_ctx_set_timing(ctx, 0)
     kstats = kernel_stats(lib, ctx)
     # per-kernel breakdown of the whole encode (every kernel timed) in a separate, untimed pass
@@ -716,7 +753,10 @@ def main():
               "kernels": {k: {"avg_us": round(v["avg_us"], 2), "launches": v["launches"]}
                           for k, v in allstats.items()},
               "kernel_breakdown_note": f"every kernel event-timed over {steps_b} extra encodes outside "
-                                       "the timed region; the timed region times only the dominant kernel",
+                                       "the timed region; the roofline's live time comes from a second region of "
+                                       "the same K encodes with events around the leaf only",
+              "ms_per_step_leaf_evented": round(1000.0 * elapsed_ev / args.steps, 4),
+              "warmup_steps_run": nwarm,
               "bin_num_effective": hdr.bin_num, "code_bits": code_bits}
 
     # ---- decode throughput + decode L2 error (rank-local) ----
@@ -791,6 +831,8 @@ def main():
             "metric": "device-resident grad encode GB/s (fp32 in) + decode L2 err, 1/2/4/8 GPU",
             "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "warmup_note": f"{nwarm} untimed encodes: --warmup {args.warmup}, extended to {args.warmup_ms:g} ms of "
+                           "sustained load so the engine clock has settled (profiles/r05b_warmup_ramp.txt)",
             "scaling": "weak", "vs_baseline": None, "dtype": args.dtype, "data": "synthetic N(0,1), torch generator",
             "config": {"workload": _workload_label(args, world),
                        "n_per_gpu": n, "bins": bins, "rotating_buffers": nbuf, "parallelism": f"dp{world}"},

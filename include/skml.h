@@ -119,9 +119,22 @@ int skml_debug_sparse_scratch_fail(int on);
 
 /* Test hook: how the calling thread's last restore / decode merged the groups' runs (Sort.merge):
  * 0 none (fewer than two groups or no keys), 1 the one-pass key-range merge, 2 the pairwise merge
- * rounds (forced by SKML_RS_ROUNDS), 3 the one-pass merge found the input irregular (a run that
- * does not ascend, a repeated key, a key outside [0, INT32_MAX)) and the rounds ran instead. */
+ * rounds (forced by SKML_FORM_RS_ROUNDS), 3 the one-pass merge found the input irregular (a run
+ * that does not ascend, a repeated key, a key outside [0, INT32_MAX)) and the rounds ran instead. */
 int skml_debug_sparse_merge_path(void);
+
+/* Test hook: force one of the library's alternative kernel forms, process-wide.  Every form gives
+ * the same results (the tests run each one against the oracle); 0 is the library's own choice.
+ * Returns the previous value, or -1 for an unknown id.  Not part of the codec. */
+#define SKML_FORM_LEAF_SPLIT 0      /* 1: one wave per 64-chunk tile always, 2: the split leaf always */
+#define SKML_FORM_DECODE_SUM 1      /* 1: the per-payload kernel, 2: the occupancy form without prefetch */
+#define SKML_FORM_PART_BALLOT 2     /* 1: the ballot-ranked partition scatter */
+#define SKML_FORM_RS_ROUNDS 3       /* 1: Sort.merge by the pairwise merge rounds always */
+#define SKML_FORM_DEC_ROWS_SERIAL 4 /* 1: the generic MinMax query (rows one by one) for every tile */
+#define SKML_FORM_AGG_TILES 5       /* 1: Gradient.sum with the 4,096-key wave-per-payload tiles */
+#define SKML_FORM_AGG_ONE_LANE 6    /* 1: Gradient.sum restores every payload on the caller's stream */
+#define SKML_FORM_COUNT 7
+int skml_debug_form(int id, int value);
 
 /* ---- Dense path: QuantileQuantizer.quantize + Quantizer.getBins/getValues ---- */
 

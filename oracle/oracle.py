@@ -391,6 +391,61 @@ def sparse_compress(keys, vals, bin_num=256, group_num=8, row_num=2, col_ratio=0
     return OracleSparse(s, bins[: len(k)])
 
 
+EPS = 1e-8  # Maths.EPS (ml/.../util/Maths.scala)
+
+
+def _java_int_two_thirds(dim):
+    """dim * 2 / 3 in Java int arithmetic (SparseDoubleGradient.scala:47)."""
+    v = (dim * 2) & 0xFFFFFFFF
+    v = v - (1 << 32) if v >= 1 << 31 else v
+    return int(v / 3)
+
+
+class GradientSumError(ValueError):
+    """The IllegalArgumentException of SparseDoubleGradient's constructor (a `require`)."""
+
+
+def gradient_sum(restored, dim, scale=1.0):
+    """Gradient.sum (ml/.../gradient/Gradient.scala:44-49) over SketchGradients of sparse form, each
+    given as its restored (keys, values) in Sort.merge order (values = quantValues[bins] after
+    timesBy).  Returns (sum, forms), forms[p] = "dense" | "sparse".
+
+    sum = new DenseDoubleGradient(dim) (+0.0 everywhere); for each payload in order
+    sum.plusBy(p.toAuto) (DenseDoubleGradient.scala:38): SketchGradient.toSparse
+    (SketchGradient.scala:62-68) builds SparseDoubleGradient(dim, keys, values), whose constructor
+    requires strictly increasing keys in [0, dim) (SparseDoubleGradient.scala:9-14; a repeated
+    key raises); toAuto (:45-48) takes toDense when countNNZ (|v| > EPS, :28-34) exceeds
+    dim * 2 / 3 in Java int arithmetic.  toDense (:36-42) writes the live values into zeros and
+    plusBy(dense) (DenseDoubleGradient.scala:10-14) adds every entry (so -0.0 sums become +0.0);
+    plusBy(sparse) (:16-22) adds each value at its key.  Then timesBy(scale) when scale != 1 (the
+    exchange's 1/P)."""
+    out = np.zeros(dim, dtype=np.float64)
+    forms = []
+    lim = _java_int_two_thirds(dim)
+    for k, v in restored:
+        k = np.asarray(k, dtype=np.int64)
+        v = np.asarray(v, dtype=np.float64)
+        if len(k) == 0:
+            raise GradientSumError("head of empty list (SparseDoubleGradient.scala:11)")
+        if k[0] < 0:
+            raise GradientSumError(f"requirement failed: Negative index: {k[0]}.")
+        if len(k) > 1 and not np.all(k[1:] > k[:-1]):
+            raise GradientSumError("requirement failed: Indices are not strictly increasing")
+        if k[-1] >= dim:
+            raise GradientSumError(f"requirement failed: Index {k[-1]} out of bounds for gradient of dimension {dim}")
+        live = np.abs(v) > EPS
+        if int(live.sum()) > lim:
+            out += 0.0
+            out[k[live]] += v[live]
+            forms.append("dense")
+        else:
+            out[k] += v
+            forms.append("sparse")
+    if scale != 1.0:
+        out *= scale
+    return out, forms
+
+
 def bench_dense_encode(x_f32, bin_num=256, seed=0, reps=1):
     x = np.ascontiguousarray(x_f32, dtype=np.float32)
     codes = np.zeros(len(x), dtype=np.uint8)

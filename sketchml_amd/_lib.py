@@ -6,6 +6,7 @@ package fails loudly.  The library is built in-tree by __graft_entry__.build()
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import os
 
@@ -75,6 +76,7 @@ _SIGS = {
     "skml_debug_leaf_stage": (C.c_int, [vp, vp, i64, C.c_int, C.c_int, C.POINTER(C.c_double)]),
     "skml_debug_sparse_scratch_fail": (C.c_int, [C.c_int]),
     "skml_debug_sparse_merge_path": (C.c_int, []),
+    "skml_debug_form": (C.c_int, [C.c_int, C.c_int]),
     "skml_dense_payload_bytes": (C.c_size_t, [i64, i32]),
     "skml_dense_encode_f32": (C.c_int, [vp, vp, i64, C.POINTER(Params), vp, C.c_size_t]),
     "skml_dense_encode_with_splits_f32": (C.c_int, [vp, vp, i64, dblp, i32, C.c_double, C.c_double,
@@ -162,6 +164,22 @@ def _load():
 
 
 lib = _load()
+
+# skml_debug_form ids (include/skml.h SKML_FORM_*): alternative kernel forms the tests force to run
+# each one against the oracle; every form gives the same results, 0 is the library's own choice.
+FORMS = {"leaf_split": 0, "decode_sum": 1, "part_ballot": 2, "rs_rounds": 3, "dec_rows_serial": 4,
+         "agg_tiles": 5, "agg_one_lane": 6}
+
+
+@contextlib.contextmanager
+def forced_forms(**values):
+    """with forced_forms(rs_rounds=1, ...): the named forms forced for the duration."""
+    prev = {k: lib.skml_debug_form(FORMS[k], int(v)) for k, v in values.items()}
+    try:
+        yield
+    finally:
+        for k, v in prev.items():
+            lib.skml_debug_form(FORMS[k], v)
 
 
 def last_error() -> str:

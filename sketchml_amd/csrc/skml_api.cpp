@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <cmath>
 #include <condition_variable>
 #include <cstdarg>
@@ -126,7 +127,16 @@ struct KernelTimer {
 };
 KernelTimer* make_timer(skml_ctx* c, int kid) { return new KernelTimer(c, kid); }
 void end_timer(KernelTimer* t) { delete t; }
+
+// skml_debug_form's process-wide selections (read once per launch decision, no environment)
+static std::atomic<int> g_form[SKML_FORM_COUNT];
+int form(int id) { return id >= 0 && id < SKML_FORM_COUNT ? g_form[id].load(std::memory_order_relaxed) : 0; }
 }  // namespace skml
+
+extern "C" int skml_debug_form(int id, int value) {
+    if (id < 0 || id >= SKML_FORM_COUNT) return -1;
+    return g_form[id].exchange(value);
+}
 
 namespace {
 

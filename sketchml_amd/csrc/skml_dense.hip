@@ -90,9 +90,16 @@ __device__ __forceinline__ uint32_t quant_bin(const QuantTables& q, float xv) {
     return xv == xv ? bin : q.nan_bin;
 }
 
+// 8-bit codes leave as one 16-byte write-through (sc1) store per lane: the wave's 1,024 codes of a
+// tile are transposed through 1 KB of LDS (lane l then holds codes 16 l .. 16 l + 15).  Write-through
+// stores leave no dirty lines in the XCD's L2, so the end of the pass has nothing to write back
+// before the next kernel starts: nontemporal 4-byte stores left ~10 us of idle time at that
+// boundary in every 2^28 encode (profiles/r05b_warmup_ramp.txt, tools/trace_gaps.py).
+constexpr int kQStageWords = 256;  // per wave: 1,024 one-byte codes
+
 template <int MODE>
 __device__ __forceinline__ void quant_tiles(const QuantTables& q, const float* __restrict__ x, int64_t n,
-                                            uint8_t* __restrict__ codes, int bits) {
+                                            uint8_t* __restrict__ codes, int bits, uint32_t* __restrict__ stage) {
     const int lane = threadIdx.x & 63;
     const int64_t nwaves_total = (int64_t)gridDim.x * (kQThreads / 64);
     const int64_t wave_id = (int64_t)blockIdx.x * (kQThreads / 64) + (threadIdx.x >> 6);
@@ -105,6 +112,10 @@ __device__ __forceinline__ void quant_tiles(const QuantTables& q, const float* _
 #pragma unroll
         for (int j = 0; j < 4; j++) f[j] = __builtin_nontemporal_load(src + j * 64 + lane);
     }
+    // codes are < 4 GB past `codes` (n < 2^31): one buffer descriptor, 32-bit offsets
+    const bool wt = bits == 8 && (reinterpret_cast<uintptr_t>(codes) & 15) == 0;
+    const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
+        codes, 0, (int)std::min<int64_t>(full_tiles * 1024, (int64_t)0x7FFFFC00), 0x00020000);
     for (int64_t tile = wave_id; tile < full_tiles; tile += nwaves_total) {
         f32x4 g[4];
         const int64_t next = tile + nwaves_total;
@@ -113,11 +124,26 @@ __device__ __forceinline__ void quant_tiles(const QuantTables& q, const float* _
 #pragma unroll
             for (int j = 0; j < 4; j++) g[j] = __builtin_nontemporal_load(src + j * 64 + lane);
         }
+        if (wt) {
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint32_t c0 = quant_bin<MODE>(q, f[j].x), c1 = quant_bin<MODE>(q, f[j].y);
-            const uint32_t c2 = quant_bin<MODE>(q, f[j].z), c3 = quant_bin<MODE>(q, f[j].w);
-            store_codes4(codes, tile * 1024 + j * 256 + lane * 4, c0, c1, c2, c3, bits, lane);
+            for (int j = 0; j < 4; j++) {
+                const uint32_t c0 = quant_bin<MODE>(q, f[j].x), c1 = quant_bin<MODE>(q, f[j].y);
+                const uint32_t c2 = quant_bin<MODE>(q, f[j].z), c3 = quant_bin<MODE>(q, f[j].w);
+                stage[j * 64 + lane] = c0 | (c1 << 8) | (c2 << 16) | (c3 << 24);
+            }
+            __builtin_amdgcn_wave_barrier();
+            const uint4 w = reinterpret_cast<const uint4*>(stage)[lane];
+            __builtin_amdgcn_wave_barrier();  // the stage is read before the next tile overwrites it
+            typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{w.x, w.y, w.z, w.w}, crs, (int)(tile * 1024 + lane * 16), 0,
+                                                   16 /* sc1: write-through */);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t c0 = quant_bin<MODE>(q, f[j].x), c1 = quant_bin<MODE>(q, f[j].y);
+                const uint32_t c2 = quant_bin<MODE>(q, f[j].z), c3 = quant_bin<MODE>(q, f[j].w);
+                store_codes4(codes, tile * 1024 + j * 256 + lane * 4, c0, c1, c2, c3, bits, lane);
+            }
         }
 #pragma unroll
         for (int j = 0; j < 4; j++) f[j] = g[j];
@@ -149,6 +175,7 @@ __global__ __launch_bounds__(kQThreads) __attribute__((amdgpu_waves_per_eu(8))) 
                                                         uint8_t* __restrict__ payload,
                                                         const QuantLut* __restrict__ lut, int lds_splits) {
     extern __shared__ __align__(16) uint8_t qsm[];
+    __shared__ __align__(16) uint32_t qstage[kQThreads / 64][kQStageWords];
     const skml_dense_header* hdr = reinterpret_cast<const skml_dense_header*>(payload);
     if (hdr->status != SKML_OK) return;
     const int bins = hdr->bin_num, bits = hdr->code_bits, nsplit = bins - 1;
@@ -194,14 +221,14 @@ __global__ __launch_bounds__(kQThreads) __attribute__((amdgpu_waves_per_eu(8))) 
     }
     __syncthreads();
     switch (mode) {
-        case 0: quant_tiles<0>(q, x, n, codes, bits); break;
-        case 1: quant_tiles<1>(q, x, n, codes, bits); break;
-        case 2: quant_tiles<2>(q, x, n, codes, bits); break;
-        case 3: quant_tiles<3>(q, x, n, codes, bits); break;
-        case 4: quant_tiles<4>(q, x, n, codes, bits); break;
-        case kModeEytz: quant_tiles<kModeEytz>(q, x, n, codes, bits); break;
-        case kModeJava: quant_tiles<kModeJava>(q, x, n, codes, bits); break;
-        default: quant_tiles<kModeGlobal>(q, x, n, codes, bits); break;
+        case 0: quant_tiles<0>(q, x, n, codes, bits, qstage[threadIdx.x >> 6]); break;
+        case 1: quant_tiles<1>(q, x, n, codes, bits, qstage[threadIdx.x >> 6]); break;
+        case 2: quant_tiles<2>(q, x, n, codes, bits, qstage[threadIdx.x >> 6]); break;
+        case 3: quant_tiles<3>(q, x, n, codes, bits, qstage[threadIdx.x >> 6]); break;
+        case 4: quant_tiles<4>(q, x, n, codes, bits, qstage[threadIdx.x >> 6]); break;
+        case kModeEytz: quant_tiles<kModeEytz>(q, x, n, codes, bits, qstage[threadIdx.x >> 6]); break;
+        case kModeJava: quant_tiles<kModeJava>(q, x, n, codes, bits, qstage[threadIdx.x >> 6]); break;
+        default: quant_tiles<kModeGlobal>(q, x, n, codes, bits, qstage[threadIdx.x >> 6]); break;
     }
 }
 
@@ -596,7 +623,7 @@ hipError_t launch_occ(hipStream_t st, const uint8_t* pl, int P, size_t stride, f
     const size_t lds = sizeof(double) * (size_t)max_bins * (size_t)P;
     const int64_t groups = n / kOccPer;
     const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((groups + 255) / 256, 4096));
-    const bool pf = std::getenv("SKML_DECODE_SUM_NOPF") == nullptr;  // A/B switch
+    const bool pf = form(SKML_FORM_DECODE_SUM) != 2;  // (2: without the next step's prefetch)
     if (pf)
         hipLaunchKernelGGL((k_decode_sum_occ<BITS, true>), dim3(grid), dim3(256), lds, st, pl, P, stride, out, n, scale,
                            max_bins);
@@ -610,7 +637,7 @@ hipError_t launch_decode_sum(hipStream_t st, const void* payloads, int P, size_t
                              int64_t n, double scale, int common_bits, int max_bins) {
     if (n <= 0) return hipSuccess;
     if (P < 1 || P > kMaxSumPayloads) return hipErrorInvalidValue;
-    if (max_bins <= kSumLutBins && P <= kOccMaxP && std::getenv("SKML_DECODE_SUM_PLAIN") == nullptr) {
+    if (max_bins <= kSumLutBins && P <= kOccMaxP && form(SKML_FORM_DECODE_SUM) != 1) {
         const uint8_t* pl = reinterpret_cast<const uint8_t*>(payloads);
         switch (common_bits) {
             case 8: return launch_occ<8>(st, pl, P, stride, out, n, scale, max_bins);

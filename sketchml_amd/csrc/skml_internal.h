@@ -8,6 +8,9 @@
 
 namespace skml {
 
+// The kernel form selected by skml_debug_form (SKML_FORM_*): 0 = the library's own choice.
+int form(int id);
+
 constexpr uint64_t kLcgMult = 0x5DEECE66DULL;  // java.util.Random
 constexpr uint64_t kLcgAdd = 0xBULL;
 constexpr uint64_t kLcgMask = (1ULL << 48) - 1;

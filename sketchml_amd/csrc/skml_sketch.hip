@@ -978,13 +978,10 @@ __global__ __launch_bounds__(512, MINW) void k_leaf(const float* __restrict__ x,
 }
 
 // One wave per tile fills the chip from 4,096 tiles (2^26 values) up; below that the split form
-// (four waves per tile) keeps more waves in flight.  SKML_LEAF_SPLIT=0/1 forces either (A/B runs).
+// (four waves per tile) keeps more waves in flight.  SKML_FORM_LEAF_SPLIT forces either (tests).
 static bool leaf_split(int64_t full_tiles) {
-    static const int force = [] {
-        const char* e = std::getenv("SKML_LEAF_SPLIT");
-        return e ? std::atoi(e) : -1;
-    }();
-    if (force >= 0) return force != 0;
+    const int force = form(SKML_FORM_LEAF_SPLIT);
+    if (force) return force == 2;
     return full_tiles < SKML_LEAF_SPLIT_BELOW;
 }
 

@@ -186,9 +186,11 @@ static_assert(sizeof(AggPayload) % 8 == 0, "copied as u64 words");
 // tile_bits: log2 of the keys per tile the bounds are taken at (agg_tile_bits of the chosen form)
 hipError_t launch_agg_bounds(hipStream_t st, const int32_t* gk, int64_t n, const SpGroups* gp, int64_t ntiles,
                              int64_t dim, int32_t* bounds, unsigned* err, int tile_bits);
-// vtiles: the staged wave-tile form (agg_vtiles_ok: at most 8 payloads per launch, 8 groups and 256
-// quantValues each); it sets err bit 2 for a key repeated inside one payload
-bool agg_vtiles_ok(int P, int max_groups, int max_nq);
+// vtiles: the staged wave-tile form (agg_vtiles_ok: payloads of at most 8 groups and 256
+// quantValues, launched 8 at a time); else the 4,096-key wave-per-payload tiles (any P, G, nq).
+// Both set err bit 1 for a key outside its tile and bit 2 for a key repeated inside one payload.
+constexpr int kAggVPayloads = 8;
+bool agg_vtiles_ok(int max_groups, int max_nq);
 int agg_tile_bits(bool vtiles);
 hipError_t launch_agg_tiles(hipStream_t st, const AggPayload* pays, int P, int64_t ntiles, int64_t dim, double* out,
                             int from_out, double scale, unsigned* err, bool vtiles);

@@ -999,7 +999,7 @@ hipError_t launch_part_scatter(hipStream_t st, const int32_t* keys, const void* 
                                uint16_t* gbins) {
     const int64_t tiles = sp_tiles(n, kSpTile);
     if (tiles <= 0) return hipSuccess;
-    const int runs = std::getenv("SKML_PART_BALLOT") == nullptr ? 1 : 0;  // A/B switch: the ballot-ranked form
+    const int runs = form(SKML_FORM_PART_BALLOT) == 1 ? 0 : 1;  // (0: the ballot-ranked form)
     hipLaunchKernelGGL(k_part_scatter, dim3((unsigned)tiles), dim3(kSpThreads), 0, st, keys,
                        reinterpret_cast<const uint8_t*>(qpayload), n, gp, tile_base, gkeys, gbins, runs);
     return hipGetLastError();
@@ -2647,8 +2647,8 @@ hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, con
     for (int x = 0; x < 8; x++) most = std::max(most, per[x]);
     const unsigned grid = (unsigned)(8 * most);
     // MODE 1 over every tile, then MODE 0 over the edge tiles; MODE 0 alone for other shapes, for
-    // tables past 2^32 - 1 cells, and under SKML_DEC_ROWS_SERIAL (the A/B switch)
-    const bool batched = gh.rows == 2 && table != nullptr && std::getenv("SKML_DEC_ROWS_SERIAL") == nullptr &&
+    // tables past 2^32 - 1 cells, and under SKML_FORM_DEC_ROWS_SERIAL (tests)
+    const bool batched = gh.rows == 2 && table != nullptr && form(SKML_FORM_DEC_ROWS_SERIAL) != 1 &&
                          gh.ncells < (int64_t)0xFFFFFFFF;
     DecEdgeTiles all{}, edges{};
     all.n = 0;
@@ -2660,20 +2660,15 @@ hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, con
             if (edges.n == 0 || edges.t[edges.n - 1] != t) edges.t[edges.n++] = t;
         }
     }
-    // nontemporal streams (decode 0.73 -> 0.71 ms, profiles/ab/r04_sparse_restore_aggregate.txt);
-    // SKML_DEC_TEMPORAL=1 is the A/B switch back
-    const bool nt = std::getenv("SKML_DEC_TEMPORAL") == nullptr;
+    // nontemporal streams (decode 0.73 -> 0.71 ms, profiles/ab/r04_sparse_restore_aggregate.txt)
 #define SKML_DEC_LAUNCH(TNT, MODE, GRID, TILES, TNPTR)                                                            \
     hipLaunchKernelGGL((k_dec_keys<TNT, MODE>), dim3(GRID), dim3(kDecThreads), 0, st, delta, n, gp, tile_base, gpre, \
                        table, TNPTR, gkeys, gbins, nq, gbn, bn_width, err, TILES)
 #define SKML_DEC_WIDTH(TNT, TNPTR)                                                          \
     do {                                                                                  \
         if (batched) {                                                                    \
-            if (nt)                                                                       \
-                hipLaunchKernelGGL((k_dec_keys<TNT, 1, true>), dim3(grid), dim3(kDecThreads), 0, st, delta, n, gp, \
-                                   tile_base, gpre, table, TNPTR, gkeys, gbins, nq, gbn, bn_width, err, all); \
-            else                                                                          \
-                SKML_DEC_LAUNCH(TNT, 1, grid, all, TNPTR);                                \
+            hipLaunchKernelGGL((k_dec_keys<TNT, 1, true>), dim3(grid), dim3(kDecThreads), 0, st, delta, n, gp,    \
+                               tile_base, gpre, table, TNPTR, gkeys, gbins, nq, gbn, bn_width, err, all);    \
             if (edges.n > 0) SKML_DEC_LAUNCH(TNT, 0, (unsigned)edges.n, edges, TNPTR);    \
         } else {                                                                          \
             SKML_DEC_LAUNCH(TNT, 0, grid, all, TNPTR);                                    \
@@ -2787,11 +2782,6 @@ hipError_t launch_agg_bounds(hipStream_t st, const int32_t* gk, int64_t n, const
     return hipGetLastError();
 }
 
-// Payloads are taken kAggPB at a time: one step loads every (payload, group) run bound of the
-// tile, and each batch of up to kAggE elements per thread issues all its key / bin / value loads
-// before any add, so a tile waits on a few load latencies instead of three per payload.  The adds
-// then run payload by payload (keys are unique within a payload; one barrier between payloads),
-// which keeps Gradient.sum's order for every key.
 // Loads through AggPayload's pointers as global (address space 1) loads.  The pointers come from
 // memory (the payload table, copied to LDS or registers), so the compiler would emit flat loads,
 // which count on lgkmcnt as well: every later LDS wait would then wait for them too, one memory
@@ -2800,13 +2790,8 @@ template <typename T>
 __device__ __forceinline__ T gload(const void* p, int64_t i) {
     return ((const __attribute__((address_space(1))) T*)p)[i];
 }
-constexpr int kAggPB = 8, kAggE = 8, kAggThreads = 512, kAggLdsValues = 256;
-__device__ __forceinline__ int agg_search(const int64_t* pre, int n, int64_t j) {  // largest i < n: pre[i] <= j
-    int i = 0;
-    for (int step = 32; step >= 1; step >>= 1)
-        if (i + step < n && pre[i + step] <= j) i += step;
-    return i;
-}
+constexpr int kAggPB = 8, kAggThreads = 512, kAggLdsValues = 256;
+static_assert(kAggPB == kAggVPayloads, "eight payloads per batch in both tile forms");
 __device__ __forceinline__ int agg_search32(const int32_t* pre, int n, int j) {  // largest i < n: pre[i] <= j
     int i = 0;
     for (int step = 32; step >= 1; step >>= 1)
@@ -2814,148 +2799,33 @@ __device__ __forceinline__ int agg_search32(const int32_t* pre, int n, int j) { 
     return i;
 }
 
-__global__ __launch_bounds__(kAggThreads) void k_agg_tiles(const AggPayload* __restrict__ pays, int P, int64_t ntiles,
-                                                          int64_t dim, double* __restrict__ out, int from_out,
-                                                          double scale, unsigned* __restrict__ err) {
-    static_assert(kMaxGroups == 64, "one lane per group");
-    __shared__ double acc[kAggTile];
-    __shared__ int64_t pre[kAggPB][kMaxGroups + 1];  // a payload's segments in this tile, scanned
-    __shared__ int64_t base[kAggPB][kMaxGroups];     // first element of each segment in its payload
-    __shared__ int64_t poff[kAggPB + 1];             // the batch's payloads concatenated
-    __shared__ int32_t dform[kAggPB];
-    __shared__ AggPayload pl_s[kAggPB];
-    __shared__ double qt[kAggPB][kAggLdsValues];  // the batch's quantValues (nq <= 256)
-    const int64_t t = blockIdx.x;
-    const int64_t k0 = t * kAggTile, nk = std::min<int64_t>(kAggTile, dim - k0);
-    for (int x = threadIdx.x; x < kAggTile; x += kAggThreads) acc[x] = (from_out && x < nk) ? out[k0 + x] : 0.0;
-    unsigned bad = 0;
-    for (int p0 = 0; p0 < P; p0 += kAggPB) {
-        const int np = std::min(kAggPB, P - p0);
-        __syncthreads();  // the previous batch is done with pre / base / poff / pl_s
-        if (threadIdx.x < np * (int)(sizeof(AggPayload) / 8))
-            reinterpret_cast<uint64_t*>(pl_s)[threadIdx.x] = reinterpret_cast<const uint64_t*>(pays + p0)[threadIdx.x];
-        for (int x = threadIdx.x; x < np * kAggLdsValues; x += kAggThreads) {
-            const AggPayload& a = pays[p0 + x / kAggLdsValues];
-            const int b = x % kAggLdsValues;
-            if (a.nq <= kAggLdsValues && b < a.nq) qt[x / kAggLdsValues][b] = gload<double>(a.qv, b);
-        }
-        for (int pl = threadIdx.x >> 6; pl < np; pl += kAggThreads / 64) {  // a wave per payload, a lane per group
-            const int g = threadIdx.x & 63;
-            const AggPayload& a = pays[p0 + pl];
-            int64_t len = 0;
-            if (g < a.G) {
-                const int32_t* bd = a.bounds + (int64_t)g * (ntiles + 1);
-                const int32_t b0 = gload<int32_t>(bd, t), b1 = gload<int32_t>(bd, t + 1);
-                len = b1 > b0 ? b1 - b0 : 0;
-                base[pl][g] = b0;
-            }
-            if (g == 0) dform[pl] = a.dense_form;
-            int64_t x = len;
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const int64_t y = __shfl_up(x, off, 64);
-                if (g >= off) x += y;
-            }
-            pre[pl][g + 1] = x;
-            if (g == 0) pre[pl][0] = 0;
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            int64_t o = 0;
-            for (int pl = 0; pl < np; pl++) {
-                poff[pl] = o;
-                o += pre[pl][kMaxGroups];
-            }
-            poff[np] = o;
-        }
-        __syncthreads();
-        const int64_t total = poff[np];
-        int next = 0;  // the first payload of the batch whose adds are not complete
-        for (int64_t e0 = 0; e0 < total || next < np; e0 += (int64_t)kAggThreads * kAggE) {
-            const int64_t e1 = std::min<int64_t>(total, e0 + (int64_t)kAggThreads * kAggE);
-            int8_t pe[kAggE];
-            int32_t kk[kAggE];
-            double vv[kAggE];
-#pragma unroll
-            for (int u = 0; u < kAggE; u++) {
-                const int64_t j = e0 + u * kAggThreads + threadIdx.x;
-                pe[u] = -1;
-                if (j < e1) {
-                    const int pl = agg_search(poff, np, j);
-                    const int64_t jl = j - poff[pl];
-                    const int g = agg_search(pre[pl], kMaxGroups, jl);
-                    const int64_t i = base[pl][g] + (jl - pre[pl][g]);
-                    const AggPayload& a = pl_s[pl];
-                    kk[u] = gload<int32_t>(a.gk, i);
-                    const uint32_t b = a.bw == 1 ? gload<uint8_t>(a.gb, i) : gload<uint16_t>(a.gb, i);
-                    vv[u] = a.nq <= kAggLdsValues ? qt[pl][b] : gload<double>(a.qv, b);
-                    pe[u] = (int8_t)pl;
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < kAggE; u++)
-                if (pe[u] >= 0 && (kk[u] < k0 || (int64_t)kk[u] >= k0 + nk)) {
-                    bad = 1;
-                    pe[u] = -1;
-                }
-#pragma unroll
-            for (int u = 0; u < kAggE; u++)  // SparseDoubleGradient.toDense keeps |v| > EPS
-                if (pe[u] >= 0 && dform[pe[u]] && !(fabs(vv[u]) > 1e-8)) pe[u] = -1;
-            // the payload holding element e1 - 1 (every remaining one in the last batch)
-            const int last = e1 >= total ? np - 1 : agg_search(poff, np, e1 - 1);
-            for (int pl = next; pl <= last; pl++) {
-#pragma unroll
-                for (int u = 0; u < kAggE; u++)
-                    if (pe[u] == pl) acc[kk[u] - k0] += vv[u];
-                __syncthreads();
-                if (poff[pl + 1] <= e1 && dform[pl]) {  // complete: the dense form adds +0.0 elsewhere
-                    for (int x = threadIdx.x; x < kAggTile; x += kAggThreads)
-                        if (__double_as_longlong(acc[x]) == (long long)0x8000000000000000ull) acc[x] = 0.0;
-                    __syncthreads();
-                }
-            }
-            next = poff[last + 1] <= e1 ? last + 1 : last;
-        }
-    }
-    if (bad) atomicOr(err, 1u);
-    __syncthreads();
-    for (int x = threadIdx.x; x < nk; x += kAggThreads) out[k0 + x] = scale == 1.0 ? acc[x] : __dmul_rn(acc[x], scale);
-}
-// The same sum with one wave per payload of the batch (8 waves, 8 payloads): the wave walks its
-// payload's group runs in this tile (run bounds from k_agg_bounds), one lane per element, so no
-// element has to search for its payload and group (k_agg_tiles: two LDS binary searches per
-// element); every wave loads its elements' keys and bins first, then the waves add into the LDS
-// tile one after the other in payload order (one barrier per payload; keys are unique within a
-// payload).  Up to kAggWPer elements per lane are held in registers, a longer payload (a dense
-// form, or a tile far denser than the mean) adds the rest in further rounds of its turn.
+// Gradient.sum over tiles of kAggTile keys, one wave per payload of a batch (8 waves, 8
+// payloads): the wave walks its payload's group runs in this tile (run bounds from k_agg_bounds),
+// one lane per element; every wave loads its elements' keys and bins first, then the waves add
+// into the LDS tile one after the other in payload order (one barrier per payload).  Up to
+// kAggWPer elements per lane are held in registers, a longer payload (a dense form, or a tile far
+// denser than the mean) adds the rest in further rounds of its turn.  Each wave marks its
+// payload's keys in a presence bitmap of the tile as it adds them (an LDS atomic OR with return):
+// a bit already set is a key repeated across the payload's groups, which the reference's
+// SparseDoubleGradient constructor rejects (err bit 2).  The general form: any P, G and nq.
 constexpr int kAggWPer = 8;
-// How a persistent grid walks the tiles.  kWalkPlain (the default): unit u = b * units-per-
-// workgroup + sub takes tiles u, u + units, ..., so all units sweep the sum together (one write
-// front).  kWalkXcd: the units renumbered so that each XCD's workgroups (b % 8, the dispatcher's
-// round robin) take consecutive tiles in every round, keeping neighbouring tiles' lines in one L2
-// (measured equal: 1,826 against 1,822 us).  kWalkContig: each unit a contiguous share of the tiles
-// (measured slower, 5.87-5.92 -> 6.60-6.62 ms end to end: 4,096 separate write fronts).
-// profiles/ab/r04_sparse_aggregate_tiles.txt.
-constexpr int kWalkPlain = 0, kWalkContig = 1, kWalkXcd = 2;
+// A persistent grid walks the tiles strided: unit u = b * units-per-workgroup + sub takes tiles
+// u, u + units, ..., so all units sweep the sum together (one write front).  Measured and dropped
+// (round 4, profiles/ab/r04_sparse_aggregate_tiles.txt): an XCD-aware renumbering (equal: 1,826
+// against 1,822 us) and a contiguous share per unit (5.87-5.92 -> 6.60-6.62 ms end to end: 4,096
+// separate write fronts).
 struct TileWalk {
     int64_t t0, t1, step;
 };
-__device__ __forceinline__ TileWalk tile_walk(int64_t blk, int64_t nblk, int sub, int nsub, int64_t ntiles, int walk) {
-    const int64_t units = nblk * nsub;
-    if (walk == kWalkContig) {
-        const int64_t unit = blk * nsub + sub, per = (ntiles + units - 1) / units;
-        return {unit * per, std::min<int64_t>(ntiles, unit * per + per), 1};
-    }
-    int64_t unit = blk * nsub + sub;
-    if (walk == kWalkXcd && nblk % 8 == 0) unit = ((blk & 7) * (nblk >> 3) + (blk >> 3)) * nsub + sub;
-    return {unit, ntiles, units};
+__device__ __forceinline__ TileWalk tile_walk(int64_t blk, int64_t nblk, int sub, int nsub, int64_t ntiles) {
+    return {blk * nsub + sub, ntiles, nblk * nsub};
 }
 __global__ __launch_bounds__(kAggThreads) void k_agg_tiles_w(const AggPayload* __restrict__ pays, int P,
                                                             int64_t ntiles, int64_t dim, double* __restrict__ out,
-                                                            int from_out, double scale, unsigned* __restrict__ err,
-                                                            int walk) {
+                                                            int from_out, double scale, unsigned* __restrict__ err) {
     static_assert(kAggThreads / 64 == kAggPB, "one wave per payload of a batch");
     __shared__ double acc[kAggTile];
+    __shared__ uint32_t here[kAggPB][kAggTile / 32];  // presence bits, one bitmap per wave
     __shared__ double qt[kAggPB][kAggLdsValues];
     __shared__ int32_t rb[kAggPB][kMaxGroups + 1];  // run prefix (elements) per group, this tile
     __shared__ int32_t rs[kAggPB][kMaxGroups];      // run start (element index in the payload)
@@ -2984,7 +2854,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_tiles_w(const AggPayload* _
             nb1 = gload<int32_t>(bd, tt + 1);
         }
     };
-    const TileWalk tw = tile_walk(blockIdx.x, gridDim.x, 0, 1, ntiles, walk);
+    const TileWalk tw = tile_walk(blockIdx.x, gridDim.x, 0, 1, ntiles);
     fetch_bounds(tw.t0);
     unsigned bad = 0;
     // The store of tile t - 1 is deferred until tile t's element loads are in flight, and the
@@ -3024,6 +2894,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_tiles_w(const AggPayload* _
                 }
                 if (lane < kMaxGroups) rb[wave][lane + 1] = x;
                 if (lane == 0) rb[wave][0] = 0;
+                reinterpret_cast<uint64_t*>(here[wave])[lane] = 0;  // 128 words: two per lane
             }
             __syncthreads();
             // this wave's elements: compact index j = lane + 64 u over the concatenated runs; the run
@@ -3072,17 +2943,22 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_tiles_w(const AggPayload* _
             for (int pl = 0; pl < np; pl++) {
                 if (wave == pl) {
                     const bool dform = a.dense_form != 0;
-                    // a key outside this tile is an error (k_agg_bounds placed it here); the dense form
-                    // keeps |v| > EPS only (SparseDoubleGradient.toDense)
-// (Two lanes of one add instruction at the same key, a key repeated across the payload's groups
-// within 64 elements, lose one add: this form does not see such repeats; k_agg_vtiles does.  Lane
-// tags that caught them cost 1,639 -> 2,149 us, profiles/ab/r04_sparse_aggregate_tiles.txt.)
-#define SKML_AGG_ADD(K, V)                                              \
-    do {                                                                \
-        const int32_t k_ = (K);                                         \
-        const double v_ = (V);                                          \
-        if (k_ < k0 || (int64_t)k_ >= k0 + nk) bad = 1;                 \
-        else if (!dform || fabs(v_) > 1e-8) acc[k_ - k0] += v_;         \
+                    // a key outside this tile is an error (k_agg_bounds placed it here), and so is a
+                    // key already marked in this payload's bitmap: then two lanes of one instruction
+                    // may have added it racily, but the sum is refused anyway.  The dense form keeps
+                    // |v| > EPS only (SparseDoubleGradient.toDense).
+#define SKML_AGG_ADD(K, V)                                                        \
+    do {                                                                          \
+        const int32_t k_ = (K);                                                   \
+        const double v_ = (V);                                                    \
+        if (k_ < k0 || (int64_t)k_ >= k0 + nk) {                                  \
+            bad |= 1u;                                                            \
+        } else {                                                                  \
+            const int x_ = (int)(k_ - k0);                                        \
+            const uint32_t bit_ = 1u << (x_ & 31);                                \
+            if (atomicOr(&here[wave][x_ >> 5], bit_) & bit_) bad |= 2u;           \
+            if (!dform || fabs(v_) > 1e-8) acc[x_] += v_;                         \
+        }                                                                         \
     } while (0)
 #pragma unroll
                     for (int u = 0; u < kAggWPer; u++)
@@ -3122,8 +2998,7 @@ constexpr int kAggVBits = 9, kAggVTile = 1 << kAggVBits;
 static_assert(kAggVTile == 8 * 64, "eight keys per lane");
 __global__ __launch_bounds__(kAggThreads) void k_agg_vtiles(const AggPayload* __restrict__ pays, int P,
                                                            int64_t ntiles, int64_t dim, double* __restrict__ out,
-                                                           int from_out, double scale, unsigned* __restrict__ err,
-                                                           int walk) {
+                                                           int from_out, double scale, unsigned* __restrict__ err) {
     constexpr int kWaves = kAggThreads / 64;
     // the stage: a bin per (payload, key); between tiles, the transpose of the stored sums
     __shared__ __attribute__((aligned(16))) uint8_t bins[kWaves][kAggPB][kAggVTile];
@@ -3146,7 +3021,6 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_vtiles(const AggPayload* __
     uint8_t(*B)[kAggVTile] = bins[wave];
     uint32_t(*H)[kAggVTile / 32] = here[wave];
     unsigned bad = 0;
-    const int64_t nw = (int64_t)gridDim.x * kWaves;
     int32_t nb0 = 0, nb1 = 0;
     auto fetch = [&](int64_t tt) {
         if (lane_on && tt < ntiles) {
@@ -3176,7 +3050,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_vtiles(const AggPayload* __
         }
         __builtin_amdgcn_wave_barrier();
     };
-    const TileWalk tw = tile_walk(blockIdx.x, gridDim.x, wave, kWaves, ntiles, walk);
+    const TileWalk tw = tile_walk(blockIdx.x, gridDim.x, wave, kWaves, ntiles);
     fetch(tw.t0);
     for (int64_t t = tw.t0; t < tw.t1; t += tw.step) {
         const int64_t k0 = t << kAggVBits, nk = std::min<int64_t>(kAggVTile, dim - k0);
@@ -3293,63 +3167,44 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_vtiles(const AggPayload* __
     if (bad) atomicOr(err, bad);
 }
 
-// the staged wave-tile form (the default for P <= 8, G <= 8, nq <= 256): it sums a key repeated
-// across a payload's groups exactly (presence bits + the split pass); the wave-per-payload tiles
-// (SKML_AGG_FORM=w, 1,639 against 1,832 us) do not see such repeats
-bool agg_vtiles_ok(int P, int max_groups, int max_nq) {
-    const char* form = std::getenv("SKML_AGG_FORM");
-    return P <= kAggPB && max_groups <= 8 && max_nq <= kAggLdsValues && !(form && (form[0] == 's' || form[0] == 'w')) &&
-           std::getenv("SKML_AGG_SEARCH") == nullptr;
+// The staged wave-tile form is the default for payloads of at most 8 groups and 256 quantValues
+// (the caller launches it 8 payloads at a time); the wave-per-payload tiles take every other shape
+// (SKML_FORM_AGG_TILES forces them for tests).
+bool agg_vtiles_ok(int max_groups, int max_nq) {
+    return max_groups <= 8 && max_nq <= kAggLdsValues && form(SKML_FORM_AGG_TILES) != 1;
 }
 int agg_tile_bits(bool vtiles) { return vtiles ? kAggVBits : 12; }
+
+// workgroups of `kern` resident at once on the device (0 if the query fails: one per tile)
+template <typename K>
+static int resident_workgroups(K kern) {
+    int dev = 0, per_cu = 0;
+    hipDeviceProp_t prop;
+    int r = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kAggThreads, 0) == hipSuccess)
+        r = std::max(1, per_cu) * prop.multiProcessorCount;
+    (void)hipGetLastError();
+    return r;
+}
 
 hipError_t launch_agg_tiles(hipStream_t st, const AggPayload* pays, int P, int64_t ntiles, int64_t dim, double* out,
                             int from_out, double scale, unsigned* err, bool vtiles) {
     if (ntiles <= 0) return hipSuccess;
-    // (A/B switches: SKML_AGG_WALK=xcd / contig)
-    const char* wk = std::getenv("SKML_AGG_WALK");
-    const int walk = !wk ? kWalkPlain : wk[0] == 'c' ? kWalkContig : wk[0] == 'x' ? kWalkXcd : kWalkPlain;
     if (vtiles) {
-        static int resident_v = 0;  // waves' workgroups resident at once; -1: unknown (one wave per tile)
-        if (!resident_v) {
-            int dev = 0, per_cu = 0;
-            hipDeviceProp_t prop;
-            if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess &&
-                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_agg_vtiles, kAggThreads, 0) == hipSuccess)
-                resident_v = std::max(1, per_cu) * prop.multiProcessorCount;
-            else
-                resident_v = -1;
-            (void)hipGetLastError();
-        }
+        if (P < 1 || P > kAggVPayloads) return hipErrorInvalidValue;  // one lane per (payload, group)
+        static const int resident_v = resident_workgroups(k_agg_vtiles);
         const int64_t all = sp_tiles(ntiles, kAggThreads / 64);
-        const unsigned grid = (unsigned)(resident_v < 0 ? all : std::min<int64_t>(all, resident_v));
+        const unsigned grid = (unsigned)(resident_v <= 0 ? all : std::min<int64_t>(all, resident_v));
         hipLaunchKernelGGL(k_agg_vtiles, dim3(grid), dim3(kAggThreads), 0, st, pays, P, ntiles, dim, out, from_out,
-                           scale, err, walk);
+                           scale, err);
         return hipGetLastError();
     }
-    const char* form = std::getenv("SKML_AGG_FORM");  // A/B switch: "s" = the per-element search form
-    if (std::getenv("SKML_AGG_SEARCH") != nullptr || (form && form[0] == 's'))
-        hipLaunchKernelGGL(k_agg_tiles, dim3((unsigned)ntiles), dim3(kAggThreads), 0, st, pays, P, ntiles, dim, out,
-                           from_out, scale, err);
-    else {  // persistent: as many workgroups as are resident at once
-        static int resident = 0;  // 0 until known; -1: the occupancy query failed (one workgroup per tile)
-        if (!resident) {
-            int dev = 0, per_cu = 0;
-            hipDeviceProp_t prop;
-            if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess &&
-                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_agg_tiles_w, kAggThreads, 0) == hipSuccess)
-                resident = std::max(1, per_cu) * prop.multiProcessorCount;
-            else
-                resident = -1;
-            (void)hipGetLastError();
-        }
-        // (A/B switch: SKML_AGG_GRID_ALL = one workgroup per tile)
-        const unsigned grid =
-            (unsigned)(std::getenv("SKML_AGG_GRID_ALL") != nullptr || resident < 0 ? ntiles
-                                                                                  : std::min<int64_t>(ntiles, resident));
-        hipLaunchKernelGGL(k_agg_tiles_w, dim3(grid), dim3(kAggThreads), 0, st, pays, P, ntiles, dim, out, from_out,
-                           scale, err, walk);
-    }
+    // persistent: as many workgroups as are resident at once
+    static const int resident = resident_workgroups(k_agg_tiles_w);
+    const unsigned grid = (unsigned)(resident <= 0 ? ntiles : std::min<int64_t>(ntiles, resident));
+    hipLaunchKernelGGL(k_agg_tiles_w, dim3(grid), dim3(kAggThreads), 0, st, pays, P, ntiles, dim, out, from_out, scale,
+                       err);
     return hipGetLastError();
 }
 

@@ -686,7 +686,7 @@ thread_local int t_merge_path = 0;  // skml_debug_sparse_merge_path
 int rs_merge_start(skml_ctx* c, const skml_sparse* s, const int32_t* gk, const int32_t* gb, int32_t* keys_out,
                    void* out, int vkind, const double* qv, int nq, volatile unsigned** pending) {
     *pending = nullptr;
-    if (s->g.G < 2 || std::getenv("SKML_RS_ROUNDS") != nullptr) return SKML_OK;
+    if (s->g.G < 2 || form(SKML_FORM_RS_ROUNDS) == 1) return SKML_OK;
     hipStream_t st = ctx_stream(c);
     const size_t o_b = align_up(sizeof(RsInfo), 256);
     char* blk = static_cast<char*>(
@@ -1856,7 +1856,10 @@ int skml_sparse_import(skml_ctx* c, const void* blob, size_t len, skml_sparse** 
 // (DenseDoubleGradient.scala:38; SketchGradient.toSparse -> SparseDoubleGradient.toAuto), then
 // out *= scale unless scale == 1.  A payload whose live count (|v| > 1e-8) exceeds dim * 2 / 3 (Java
 // int arithmetic) reaches plusBy in dense form: only its live values are added, and every entry
-// takes the dense form's + 0.0.
+// takes the dense form's + 0.0.  SketchGradient.toSparse builds a SparseDoubleGradient from the
+// restored keys, whose constructor requires them strictly increasing and inside [0, dim)
+// (SparseDoubleGradient.scala:9-14): a key repeated across a payload's groups, a run that does not
+// ascend or a key out of range fails the whole sum with SKML_E_ARG.
 int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t stride, int64_t dim, double scale,
                                double* out) {
     if (!c || !blobs || P < 1 || dim < 0 || dim > (int64_t)INT32_MAX || (dim > 0 && !out) || stride % 256)
@@ -1873,17 +1876,21 @@ int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t
     const int64_t lim = (int64_t)(int32_t)((uint32_t)dim * 2u) / 3;  // dim * 2 / 3 with Java int wrap
     // run bounds are taken per tile of the tile kernel: 512 keys for the wave-tile form, else 4,096
     const int64_t ntiles_max = sp_tiles(dim, (int64_t)1 << agg_tile_bits(true));
+    auto bin_width = [&](int p) { return views[(size_t)p].qvalues.size() <= 256 ? 1 : 2; };
+    // a payload's restored keys and bins, each 16-byte aligned in its scratch buffer
+    auto key_words = [&](int p) { return (views[(size_t)p].nnz + 3) & ~int64_t{3}; };
+    auto bin_bytes = [&](int p) { return (views[(size_t)p].nnz * bin_width(p) + 15) & ~int64_t{15}; };
     // payloads in batches whose restored keys + bins + run bounds fit the scratch budget; the first
     // batch starts the sum at +0.0, later ones continue from it, the last one applies the scale
     constexpr size_t kBudget = (size_t)3 << 30;
     auto need_of = [&](int p) {
-        return (size_t)views[(size_t)p].nnz * 6 + (size_t)views[(size_t)p].g.G * (size_t)(ntiles_max + 1) * 4 + 1024;
+        return (size_t)key_words(p) * 4 + (size_t)bin_bytes(p) +
+               (size_t)views[(size_t)p].g.G * (size_t)(ntiles_max + 1) * 4 + 1024;
     };
     std::vector<int> todo;
     for (int p = 0; p < P; p++)
         if (views[(size_t)p].nnz > 0) todo.push_back(p);  // an empty restore adds nothing (sparse form)
-    // (room for one entry per (payload, group): the split form below)
-    uint8_t* small = scratch<uint8_t>(c, kSlotStatus, 1024 + sizeof(AggPayload) * (size_t)P * kMaxGroups);
+    uint8_t* small = scratch<uint8_t>(c, kSlotStatus, 1024 + sizeof(AggPayload) * (size_t)P);
     if (!small) return sfail(SKML_E_OOM, "decode_sum scratch");
     unsigned* err = reinterpret_cast<unsigned*>(small);
     uint64_t* live = reinterpret_cast<uint64_t*>(small + 256);
@@ -1894,11 +1901,6 @@ int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t
         SP_HIP(hipStreamSynchronize(st));
         return SKML_OK;
     }
-    // split: every sparse-form payload enters the tiles as one pseudo-payload per group, in group
-    // order, after a first pass found a key repeated across a payload's groups (legal for the
-    // reference: plusBy then adds both copies, the lower group's first, as Sort.merge emits them)
-    auto run = [&](bool split) -> int {
-    SP_HIP(hipMemsetAsync(err, 0, sizeof(unsigned), st));
     size_t at = 0;
     bool first = true;
     while (at < todo.size()) {
@@ -1909,33 +1911,33 @@ int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t
             max_g = std::max(max_g, (int)views[(size_t)todo[q]].g.G);
             max_nq = std::max(max_nq, (int)views[(size_t)todo[q]].qvalues.size());
         }
-        const bool vt = split ? agg_vtiles_ok(8, max_g, max_nq) : agg_vtiles_ok((int)(end - at), max_g, max_nq);
+        const bool vt = agg_vtiles_ok(max_g, max_nq);
         const int tile_bits = agg_tile_bits(vt);
         const int64_t ntiles = sp_tiles(dim, (int64_t)1 << tile_bits);
-        int64_t nk = 0, nb = 0;
+        int64_t nk = 0, nbb = 0, nb = 0;
         for (size_t q = at; q < end; q++) {
-            nk += (views[(size_t)todo[q]].nnz + 3) & ~int64_t{3};  // every payload's keys 16-byte aligned
+            nk += key_words(todo[q]);
+            nbb += bin_bytes(todo[q]);
             nb += (int64_t)views[(size_t)todo[q]].g.G * (ntiles + 1);
         }
         int32_t* gk = scratch<int32_t>(c, kSlotCKeys, (size_t)nk);
-        uint16_t* gbn = scratch<uint16_t>(c, kSlotCVals, (size_t)nk);  // 1 or 2 bytes per bin, 16-byte aligned runs
+        uint8_t* gbn = scratch<uint8_t>(c, kSlotCVals, (size_t)nbb);  // 1 or 2 bytes per bin
         int32_t* bounds = scratch<int32_t>(c, kSlotCells, (size_t)nb);
         if (!gk || !gbn || !bounds) return sfail(SKML_E_OOM, "decode_sum scratch (%lld keys)", (long long)nk);
         SP_HIP(hipMemsetAsync(bounds, 0, sizeof(int32_t) * (size_t)nb, st));  // empty groups: every bound 0
         // two lanes: payloads alternate between the caller's stream and the side context's (each
         // restore is a chain of small latency-bound kernels; two chains fill the chip better),
-        // joined before the tiles; SKML_SERIAL, SKML_AGG_ONE_LANE or a single payload keep one lane
+        // joined before the tiles; SKML_SERIAL, SKML_FORM_AGG_ONE_LANE or a single payload keep one
         skml_ctx* lanes[2] = {c, nullptr};
         hipStream_t side_st = nullptr;
         hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-        if (end - at > 1 && std::getenv("SKML_AGG_ONE_LANE") == nullptr &&  // (the A/B switch)
-            ctx_side_fork(c, &side_st, &ev_fork, &ev_join) == SKML_OK) {
+        if (end - at > 1 && form(SKML_FORM_AGG_ONE_LANE) != 1 && ctx_side_fork(c, &side_st, &ev_fork, &ev_join) == SKML_OK) {
             lanes[1] = ctx_side_ctx(c);
             SP_HIP(hipEventRecord(ev_fork, st));
             SP_HIP(hipStreamWaitEvent(side_st, ev_fork, 0));
         }
         std::vector<AggPayload> pays;
-        int64_t ko = 0, bo = 0;
+        int64_t ko = 0, bbo = 0, bo = 0;
         for (size_t q = at; q < end; q++) {
             const int p = todo[q];
             const int li = lanes[1] && ((q - at) & 1) ? 1 : 0;
@@ -1946,9 +1948,8 @@ int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t
             AggPayload a{};
             a.gk = gk + ko;
             a.nq = (int)v.qvalues.size();
-            a.bw = a.nq <= 256 ? 1 : 2;
-            a.gb = a.bw == 1 ? static_cast<const void*>(reinterpret_cast<uint8_t*>(gbn) + ko)
-                             : static_cast<const void*>(gbn + ko);
+            a.bw = bin_width(p);
+            a.gb = gbn + bbo;
             a.qv = reinterpret_cast<const double*>(static_cast<const uint8_t*>(blobs) + (size_t)p * stride +
                                                    hs[(size_t)p].off_values);
             a.bounds = bounds + bo;
@@ -1973,7 +1974,8 @@ int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t
                                   tile_bits) != hipSuccess)
                 return join(sfail(SKML_E_HIP, "agg_bounds launch failed"));
             pays.push_back(a);
-            ko += (v.nnz + 3) & ~int64_t{3};
+            ko += key_words(p);
+            bbo += bin_bytes(p);
             bo += (int64_t)v.g.G * (ntiles + 1);
         }
         if (lanes[1]) {
@@ -1981,25 +1983,14 @@ int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t
             SP_HIP(hipStreamWaitEvent(st, ev_join, 0));
         }
         const bool last = end == todo.size();
-        std::vector<AggPayload> list;
-        for (const AggPayload& a : pays) {
-            if (!split || a.dense_form) {
-                list.push_back(a);
-                continue;
-            }
-            for (int g = 0; g < a.G; g++) {
-                AggPayload b = a;
-                b.G = 1;
-                b.bounds = a.bounds + (int64_t)g * (ntiles + 1);
-                list.push_back(b);
-            }
-        }
-        SP_HIP(hipMemcpyAsync(d_pays, list.data(), sizeof(AggPayload) * list.size(), hipMemcpyHostToDevice, st));
-        const size_t chunk = split && vt ? (size_t)8 : list.size();
-        for (size_t c0 = 0; c0 < list.size(); c0 += chunk) {
-            const size_t nc = std::min(chunk, list.size() - c0);
+        SP_HIP(hipMemcpyAsync(d_pays, pays.data(), sizeof(AggPayload) * pays.size(), hipMemcpyHostToDevice, st));
+        // the wave-tile form takes 8 payloads per launch (a lane per (payload, group)); later
+        // launches continue the sum in payload order
+        const size_t chunk = vt ? (size_t)kAggVPayloads : pays.size();
+        for (size_t c0 = 0; c0 < pays.size(); c0 += chunk) {
+            const size_t nc = std::min(chunk, pays.size() - c0);
             SP_HIP(launch_agg_tiles(st, d_pays + c0, (int)nc, ntiles, dim, out, first && c0 == 0 ? 0 : 1,
-                                    last && c0 + nc == list.size() ? scale : 1.0, err, vt));
+                                    last && c0 + nc == pays.size() ? scale : 1.0, err, vt));
         }
         SP_HIP(hipStreamSynchronize(st));  // `pays` (host) and the scratch are reused by the next batch
         first = false;
@@ -2008,15 +1999,12 @@ int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t
     unsigned bad = 0;
     if (int e = sync_to_host(c, &bad, err, sizeof(bad))) return e;
     if (bad & 1u)
-        return sfail(SKML_E_ARG, "a payload holds a key outside [0, %lld) or a bin outside its values", (long long)dim);
-    if (bad & 2u) {
-        if (!split) return -1;  // the split form follows
-        return sfail(SKML_E_ARG, "a dense-form payload repeats a key across its groups");
-    }
+        return sfail(SKML_E_ARG, "a payload holds a key outside [0, %lld), a non-ascending run or a bin outside its "
+                                 "values (SparseDoubleGradient requires ascending indices in range)", (long long)dim);
+    if (bad & 2u)
+        return sfail(SKML_E_ARG, "requirement failed: Indices are not strictly increasing (a key repeated across a "
+                                 "payload's groups; SparseDoubleGradient.scala:12)");
     return SKML_OK;
-    };
-    const int e = run(false);
-    return e == -1 ? run(true) : e;
 }
 
 int skml_debug_sparse_merge_path(void) { return t_merge_path; }

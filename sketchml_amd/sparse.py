@@ -184,7 +184,9 @@ def decode_sum(blobs: torch.Tensor, nblobs: int, stride: int, dim: int, scale: f
                out: torch.Tensor | None = None) -> torch.Tensor:
     """Gradient.sum (ml/gradient/Gradient.scala:44-49) of `nblobs` exported sparse payloads laid out
     `stride` bytes apart: a float64 dense sum of length dim, payloads added in order (then scaled
-    when scale != 1).  skml_sparse_decode_sum_f64."""
+    when scale != 1).  skml_sparse_decode_sum_f64.  Like SketchGradient.toSparse's
+    SparseDoubleGradient constructor, a payload whose restored keys repeat (a key in two groups)
+    or leave [0, dim) raises SketchMLException."""
     dev = blobs.device
     if out is None:
         out = torch.empty(max(int(dim), 1), dtype=torch.float64, device=dev)

@@ -134,6 +134,20 @@ def test_abi_exports_every_declared_symbol():
     assert sorted(_lib.EXPORTED) == declared
 
 
+def test_form_ids_match_header():
+    """sketchml_amd._lib.FORMS mirrors the SKML_FORM_* ids of include/skml.h; skml_debug_form
+    returns the previous value and -1 for an unknown id (host-only)."""
+    from sketchml_amd import _lib
+    with open(os.path.join(ROOT, "include", "skml.h")) as f:
+        ids = {m.group(1).lower(): int(m.group(2)) for m in re.finditer(r"#define SKML_FORM_([A-Z_]+) (\d+)", f.read())}
+    count = ids.pop("count")
+    assert ids == _lib.FORMS and count == len(ids)
+    assert _lib.lib.skml_debug_form(count, 1) == -1
+    with _lib.forced_forms(rs_rounds=1):
+        assert _lib.lib.skml_debug_form(_lib.FORMS["rs_rounds"], 1) == 1
+    assert _lib.lib.skml_debug_form(_lib.FORMS["rs_rounds"], 0) == 0
+
+
 def test_abi_host_only_calls():
     """Calls that touch no device: defaults, version, payload sizing, error reporting."""
     from sketchml_amd import _lib

@@ -382,19 +382,21 @@ def test_decode_sum(gpu):
                                       (16, [512] * 16, 40000 + 5), (5, [16] * 5, 2**18 + 7), (4, [4] * 4, 99999),
                                       (3, [2] * 3, 4097), (6, [256, 16, 4, 2, 256, 16], 50001), (1, [256], 15)])
 @pytest.mark.parametrize("kernel", ["occ", "occ_nopf", "plain"])
-def test_decode_sum_forms(gpu, P, bins, n, kernel, monkeypatch):
+def test_decode_sum_forms(gpu, P, bins, n, kernel):
     """k_decode_sum_occ (8 elements per lane, P <= 8 tables of the largest bin count in LDS; with
     and without the next step's code prefetch) and the per-payload kernel (P > 8, mixed widths,
     > 256 bins): bit-exact against the oracle's decodes summed in double
     in payload order, then x 1/P (Gradient.sum + timesBy, ml/gradient/Gradient.scala:44-49).
     Requested bins 512 with Maths.unique give effective counts up to 256 (8-bit codes).
-    kernel "plain": SKML_DECODE_SUM_PLAIN=1 selects the one-table-per-payload kernel (its
+    kernel "plain": SKML_FORM_DECODE_SUM = 1 selects the one-table-per-payload kernel (its
     software-pipelined form when the width is common and P <= 8)."""
     from sketchml_amd import _lib
-    if kernel == "plain":
-        monkeypatch.setenv("SKML_DECODE_SUM_PLAIN", "1")
-    elif kernel == "occ_nopf":
-        monkeypatch.setenv("SKML_DECODE_SUM_NOPF", "1")
+    with _lib.forced_forms(decode_sum={"occ": 0, "plain": 1, "occ_nopf": 2}[kernel]):
+        _decode_sum_case(gpu, P, bins, n)
+
+
+def _decode_sum_case(gpu, P, bins, n):
+    from sketchml_amd import _lib
     ctx = gpu.get_context()
     nb = max(_lib.lib.skml_dense_payload_bytes(n, b) for b in bins)
     nb = (nb + 255) // 256 * 256

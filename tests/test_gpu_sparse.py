@@ -77,16 +77,16 @@ def test_sparse_edge_values(gpu, kind):
 
 
 @pytest.fixture(params=["one_pass", "rounds"])
-def merge_form(request, monkeypatch):
+def merge_form(request):
     """restore both ways.  one_pass (the default): tiles of one group through the compile-time-hash
     query (k_dec_keys MODE 1) and the edge tiles through the generic one, Sort.merge as the
-    one-pass key-range merge.  rounds: the A/B switches back to the round-3 forms (one generic
-    query per row for every tile, the pairwise merge rounds, which are also the fallback for
-    irregular input)."""
-    if request.param == "rounds":
-        monkeypatch.setenv("SKML_RS_ROUNDS", "1")
-        monkeypatch.setenv("SKML_DEC_ROWS_SERIAL", "1")
-    return request.param
+    one-pass key-range merge.  rounds: the round-3 forms forced through skml_debug_form (one
+    generic query per row for every tile, the pairwise merge rounds, which are also the fallback
+    for irregular input)."""
+    from sketchml_amd import _lib
+    forms = {"rs_rounds": 1, "dec_rows_serial": 1} if request.param == "rounds" else {}
+    with _lib.forced_forms(**forms):
+        yield request.param
 
 
 def _merge_path():
@@ -95,15 +95,15 @@ def _merge_path():
 
 
 @pytest.mark.parametrize("form", ["runs", "ballot"])
-def test_partition_scatter_forms(gpu, form, monkeypatch):
+def test_partition_scatter_forms(gpu, form):
     """The partition scatter's few-groups forms: per-thread runs of 8 elements ranked from packed
-    per-group counts (default) and the ballot-ranked form (SKML_PART_BALLOT=1); ragged last tile,
-    2 to 8 groups, 8- and 16-bit codes."""
-    if form == "ballot":
-        monkeypatch.setenv("SKML_PART_BALLOT", "1")
-    for groups, bins, dim in ((8, 256, 200003), (2, 16, 70001), (5, 512, 99991)):
-        keys, vals = _sparse_data(dim, 0.2, groups + dim, "normal")
-        _check_sparse(gpu, keys, vals, bins, groups, 2, 0.3, seed=groups, hash_seed=bins)
+    per-group counts (default) and the ballot-ranked form (SKML_FORM_PART_BALLOT); ragged last
+    tile, 2 to 8 groups, 8- and 16-bit codes."""
+    from sketchml_amd import _lib
+    with _lib.forced_forms(part_ballot=1 if form == "ballot" else 0):
+        for groups, bins, dim in ((8, 256, 200003), (2, 16, 70001), (5, 512, 99991)):
+            keys, vals = _sparse_data(dim, 0.2, groups + dim, "normal")
+            _check_sparse(gpu, keys, vals, bins, groups, 2, 0.3, seed=groups, hash_seed=bins)
 
 
 @pytest.mark.parametrize("groups,rows,ratio,bins", [(2, 1, 0.3, 256), (4, 3, 0.5, 64), (16, 8, 0.1, 1024),

@@ -21,32 +21,10 @@ pytestmark = pytest.mark.gpu
 EPS = 1e-8
 
 
-def _java_lim(dim):
-    """dim * 2 / 3 in Java int arithmetic (DenseDoubleGradient / SparseDoubleGradient.toAuto)."""
-    v = (dim * 2) & 0xFFFFFFFF
-    v = v - (1 << 32) if v >= 1 << 31 else v
-    return int(v / 3)
-
-
 def oracle_sum(osps, dim, scale=1.0):
-    """Gradient.sum over the oracle's payloads: DenseDoubleGradient(dim), then plusBy(p.toAuto) in
-    order; returns (sum, forms) where forms[p] is 'dense' or 'sparse'."""
-    out = np.zeros(dim, dtype=np.float64)
-    forms = []
-    for osp in osps:
-        k, b = osp.restore()
-        v = osp.q.values()[b]
-        live = np.abs(v) > EPS
-        if int(live.sum()) > _java_lim(dim):      # SparseDoubleGradient.toDense: live values only
-            out = out + 0.0
-            out[k[live]] += v[live]
-            forms.append("dense")
-        else:                                     # plusBy(sparse): every copy of a repeated key, in order
-            np.add.at(out, k, v)
-            forms.append("sparse")
-    if scale != 1.0:
-        out = out * scale
-    return out, forms
+    """Gradient.sum over the oracle's payloads (oracle.gradient_sum: DenseDoubleGradient(dim), then
+    plusBy(p.toAuto) in order); returns (sum, forms)."""
+    return O.gradient_sum(((k, osp.q.values()[b]) for osp in osps for k, b in [osp.restore()]), dim, scale)
 
 
 def _payload(gpu, dim, density, seed, bins=256, tiny=0.0, groups=8):
@@ -116,21 +94,21 @@ def test_corrupt_blobs_are_refused(gpu):
         gpu.decode_sum(blob, 1, blob.numel(), 1000)
 
 
-# Gradient.sum's tile kernel: vtile (default: one wave per 512-key tile that stages every
-# payload's bins with presence bits and sums each key in registers, payload after payload;
-# restores on two streams), wave (SKML_AGG_FORM=w: one wave per payload adding into a 4,096-key
-# LDS tile) and search (the round-3 per-element form, with the generic per-row MinMax query and
-# one stream).  Only vtile sees a key repeated across one payload's groups; the other two add
-# copies that meet in one instruction racily.
-KERNELS = {"vtile": {}, "wave": {"SKML_AGG_FORM": "w"},
-           "search": {"SKML_AGG_FORM": "s", "SKML_DEC_ROWS_SERIAL": "1", "SKML_AGG_ONE_LANE": "1"}}
+# Gradient.sum's tile kernels: vtile (default for payloads of <= 8 groups and <= 256 quantValues:
+# one wave per 512-key tile stages every payload's bins with presence bits and sums each key in
+# registers, payload after payload, 8 payloads per launch; restores on two streams), wave
+# (SKML_FORM_AGG_TILES: one wave per payload adding into a 4,096-key LDS tile, the form for any
+# other shape) and wave_serial (the wave tiles with the generic per-row MinMax query and one
+# stream).  Every form is exact, and every form refuses a key repeated across a payload's groups.
+KERNELS = {"vtile": {}, "wave": {"agg_tiles": 1},
+           "wave_serial": {"agg_tiles": 1, "dec_rows_serial": 1, "agg_one_lane": 1}}
 
 
 @pytest.fixture(params=sorted(KERNELS))
-def agg_kernel(request, monkeypatch):
-    for k, v in KERNELS[request.param].items():
-        monkeypatch.setenv(k, v)
-    return request.param
+def agg_kernel(request):
+    from sketchml_amd import _lib
+    with _lib.forced_forms(**KERNELS[request.param]):
+        yield request.param
 
 
 def test_decode_sum_eight_payloads_matches_oracle(gpu, agg_kernel):
@@ -177,8 +155,8 @@ def test_decode_sum_many_payloads_and_groups(gpu, agg_kernel):
     assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
 
 
-def _dup_payload(gpu, dim, seed, groups=4):
-    """A payload whose keys repeat across groups (legal for the reference, see
+def _dup_payload(gpu, dim, seed, groups=4, bins=256):
+    """A payload whose keys repeat across groups (legal for the sketch module's restore, see
     test_sparse_duplicate_keys_across_groups_are_kept): each repeated key carries one value far
     below and one far above the rest, so its copies land in the first and the last group."""
     rng = np.random.default_rng(seed)
@@ -192,27 +170,55 @@ def _dup_payload(gpu, dim, seed, groups=4):
     pos = np.cumsum(np.where(ins, 2, 1)) - np.where(ins, 2, 1)
     vals2[pos] = np.where(ins, -6.0 - rng.random(len(keys)), vals)
     vals2[pos[ins] + 1] = 6.0 + rng.random(int(ins.sum()))
-    pl = gpu.encode_sparse(torch.from_numpy(keys2).cuda(), torch.from_numpy(vals2).cuda(), 256, groups, 2, 0.3, seed,
+    pl = gpu.encode_sparse(torch.from_numpy(keys2).cuda(), torch.from_numpy(vals2).cuda(), bins, groups, 2, 0.3, seed,
                            seed + 100)
-    osp = O.sparse_compress(keys2, vals2, 256, groups, 2, 0.3, seed, seed + 100)
+    osp = O.sparse_compress(keys2, vals2, bins, groups, 2, 0.3, seed, seed + 100)
     return pl, osp
 
 
-def test_decode_sum_keys_repeated_across_groups(gpu, agg_kernel):
-    """plusBy adds both copies of a repeated key, the lower group's first (Sort.merge).  The staged
-    tiles see the second copy's presence bit and run the sum again with every sparse-form payload
-    split into one pseudo-payload per group, in group order."""
+@pytest.mark.parametrize("shape", ["two", "nine_payloads", "twelve_groups", "bins_512"])
+def test_decode_sum_keys_repeated_across_groups(gpu, agg_kernel, shape):
+    """SketchGradient.toSparse builds a SparseDoubleGradient from the restored keys, whose
+    constructor requires them strictly increasing (SparseDoubleGradient.scala:12): a key repeated
+    across a payload's groups fails Gradient.sum.  Every tile form sees the repeat (presence
+    bits) and the call raises; shapes past the wave-tile form (9 payloads, 12 groups, 512 bins)
+    take the 4,096-key tiles."""
     dim = 100003
-    p0, o0 = _payload(gpu, dim, 0.2, 71, groups=4)
-    p1, o1 = _dup_payload(gpu, dim, 72)
+    groups = 12 if shape == "twelve_groups" else 4
+    bins = 512 if shape == "bins_512" else 256
+    npay = 9 if shape == "nine_payloads" else 2
+    good = [_payload(gpu, dim, 0.2, 71 + p, groups=groups, bins=bins) for p in range(npay - 1)]
+    p1, o1 = _dup_payload(gpu, dim, 72, groups=groups, bins=bins)
     k1, _ = o1.restore()
     assert len(np.unique(k1)) < len(k1)                   # the repeats survive the codec
-    allb, stride = _gather_local([p0, p1])
-    got = gpu.decode_sum(allb, 2, stride, dim).cpu().numpy()
-    want, forms = oracle_sum([o0, o1], dim)
-    assert forms == ["sparse", "sparse"]
-    if agg_kernel == "vtile":
-        assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
+    pls = [g[0] for g in good] + [p1]
+    osps = [g[1] for g in good] + [o1]
+    with pytest.raises(O.GradientSumError, match="strictly increasing"):
+        oracle_sum(osps, dim)
+    allb, stride = _gather_local(pls)
+    with pytest.raises(gpu.SketchMLException, match="strictly increasing"):
+        gpu.decode_sum(allb, npay, stride, dim)
+    # the payloads without the repeat still sum exactly (the error left no state behind)
+    allb, stride = _gather_local(pls[:-1])
+    got = gpu.decode_sum(allb, npay - 1, stride, dim).cpu().numpy()
+    want, _ = oracle_sum(osps[:-1], dim)
+    assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
+
+
+@pytest.mark.parametrize("order", ["wide_first", "narrow_first", "all_wide"])
+def test_decode_sum_mixed_bin_widths(gpu, agg_kernel, order):
+    """Payloads whose quantValues need 2-byte bins (bin_num > 256, requested 512) and 1-byte ones
+    (256) in one sum: each restore writes its bins at its own byte offset (a 2-byte
+    payload before a 1-byte one used to overlap it)."""
+    dim = 150001
+    spec = {"wide_first": [512, 256, 512, 256], "narrow_first": [256, 512, 256], "all_wide": [512, 1024, 512]}[order]
+    pls, osps = zip(*[_payload(gpu, dim, 0.12 + 0.03 * p, 90 + p, bins=b) for p, b in enumerate(spec)])
+    assert any(len(o.q.values()) > 256 for o in osps)
+    allb, stride = _gather_local(pls)
+    got = gpu.decode_sum(allb, len(spec), stride, dim, 0.25).cpu().numpy()
+    want, forms = oracle_sum(osps, dim, 0.25)
+    assert set(forms) == {"sparse"}
+    assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
 
 
 def test_decode_sum_skips_empty_payloads(gpu, agg_kernel):
@@ -247,3 +253,60 @@ def test_sparse_exchange_world1_rccl(gpu):
         assert np.array_equal(avg.cpu().numpy().view(np.uint64), want.view(np.uint64))
     finally:
         dist.destroy_process_group()
+
+
+def _c3_dense(seed, dim=2**28):
+    """A C3-shaped dense gradient as bench.py builds rank r's (seed 3 + r): N(0, 1), 10 % kept."""
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    x = torch.randn(dim, device="cuda", generator=g)
+    x[torch.rand(dim, device="cuda", generator=g) >= 0.1] = 0.0
+    return x
+
+
+def test_decode_sum_eight_distinct_c3_payloads_full_size(gpu):
+    """The sum bench.py times (extras.other_configs.sparse_aggregate) at its own size: 8 distinct
+    C3 payloads (2^28 dims, 10 % nnz, dense seeds 3 .. 10, the DP step's per-rank gradients) through
+    Gradient.sum x 1/8, bit-exact against the oracle's Gradient.sum of the oracle's own encodes
+    (toSparse, SparseVectorCompressor.compressSparse, restore).  The union of keys covers ~57 % of
+    the dims, so the 524,288 wave tiles see run pieces that do not line up across payloads.  Both
+    tile forms are checked against the one oracle sum."""
+    from concurrent.futures import ThreadPoolExecutor
+    from sketchml_amd import _lib
+    from sketchml_amd.distributed import blob_stride
+    dim, P = 2**28, 8
+    blobs, host = [], []
+    for p in range(P):
+        x = _c3_dense(3 + p, dim)
+        pl = gpu.encode_dense_as_sparse(x, 256, 8, 2, 0.3, 3 + p, 3 + p)
+        blobs.append(pl.export())
+        host.append(O.to_sparse(x.cpu().numpy().astype(np.float64)))
+        del x, pl
+    stride = blob_stride([b.numel() for b in blobs])
+    allb = torch.zeros(stride * P, dtype=torch.uint8, device="cuda")
+    for p, b in enumerate(blobs):
+        allb[p * stride:p * stride + b.numel()].copy_(b)
+    del blobs
+
+    def oracle_restore(p):  # the C oracle releases the GIL: the 8 encodes run side by side
+        k, v = host[p]
+        osp = O.sparse_compress(k, v, 256, 8, 2, 0.3, 3 + p, 3 + p)
+        rk, rb = osp.restore()
+        return rk, osp.q.values()[rb]
+
+    with ThreadPoolExecutor(8) as ex:
+        restored = list(ex.map(oracle_restore, range(P)))
+    del host
+    union = np.zeros(dim, dtype=bool)
+    for k, _ in restored:
+        union[k] = True
+    assert 0.5 < union.mean() < 0.6                     # distinct key sets, not copies
+    del union
+    want, forms = O.gradient_sum(restored, dim, 1.0 / P)
+    del restored
+    assert forms == ["sparse"] * P
+    for form in (0, 1):                                  # the staged wave tiles, then the 4,096-key tiles
+        with _lib.forced_forms(agg_tiles=form):
+            got = gpu.decode_sum(allb, P, stride, dim, 1.0 / P)
+            torch.cuda.synchronize()
+            assert np.array_equal(got.cpu().numpy().view(np.uint64), want.view(np.uint64)), form
+            del got

@@ -115,7 +115,14 @@ def main():
     }
     if a.aggregate:
         from sketchml_amd.distributed import blob_stride
-        pls = [sk.encode_sparse(keys, vals, 256, 8, 2, 0.3, 3 + p, 3 + p) for p in range(a.aggregate)]
+        # distinct payloads, as in the DP step: rank r's C3 gradient (dense seed 3 + r), bench.py's data
+        pls = [pl2]
+        for r in range(1, a.aggregate):
+            gr = torch.Generator(device=dev).manual_seed(3 + r)
+            xr = torch.randn(a.dim, device=dev, generator=gr)
+            xr[torch.rand(a.dim, device=dev, generator=gr) >= a.density] = 0.0
+            pls.append(sk.encode_dense_as_sparse(xr, 256, 8, 2, 0.3, 3 + r, 3 + r))
+            del xr
         stride = blob_stride([p.export_bytes() for p in pls])
         allb = torch.zeros(stride * len(pls), dtype=torch.uint8, device=dev)
         for i, p in enumerate(pls):
@@ -123,7 +130,7 @@ def main():
         del pls
         t_sum, _ = timed(lambda: sk.decode_sum(allb, a.aggregate, stride, a.dim, 1.0 / a.aggregate), a.reps)
         line["ms"]["decode_sum"] = round(t_sum * 1e3, 3)
-        line["aggregate"] = {"payloads": a.aggregate, "blob_stride": stride}
+        line["aggregate"] = {"payloads": a.aggregate, "blob_stride": stride, "distinct": True}
     print(json.dumps(line))
 
 
