@@ -603,6 +603,9 @@ __global__ __launch_bounds__(256, SKML_LEAF64_WAVES) void k_leaf64(const float* 
     const int64_t tile = SPLIT ? blk : blk * kLeaf2Waves + wave;
     const int64_t c_tile = tile * kLeafWaveChunks;
     if (c_tile >= chunks) return;  // workgroup-uniform under SPLIT, wave-uniform otherwise
+#ifdef SKML_PROF_LEAF
+    const unsigned long long prof_t0 = wall_clock64();
+#endif
     float* wfb = fb[wave];
     uint32_t mn = ~0u, mx = 0, fl = 0u;
     bool neg_any = false, pos_any = false;
@@ -810,6 +813,14 @@ __global__ __launch_bounds__(256, SKML_LEAF64_WAVES) void k_leaf64(const float* 
         p.flags = fl | ((mn < 0x007FFFFFu || mx > 0xFF800000u) ? 1u : 0u);
         p.pad = 0;
         part[tile] = p;
+#ifdef SKML_PROF_LEAF
+        if (!SPLIT && tile < 65536) {
+            g_leafprof[4 * tile] = prof_t0;
+            g_leafprof[4 * tile + 1] = wall_clock64();
+            g_leafprof[4 * tile + 2] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));   // HW_ID
+            g_leafprof[4 * tile + 3] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));  // XCC_ID
+        }
+#endif
     }
 }
 

@@ -379,6 +379,7 @@ def test_decode_sum(gpu):
 # 8 x up to 221, and 16 x up to 235, which takes the per-payload kernel); 4-, 2- and 1-bit codes;
 # a mixed-width set (the per-payload kernel); n = 15 (tail only).
 @pytest.mark.parametrize("P,bins,n", [(8, [256] * 8, 2**20 + 13), (8, [256] * 8, 40005),
+                                      (8, [512] * 8, 2**18 + 3), (4, [1024] * 4, 50001),
                                       (16, [512] * 16, 40000 + 5), (5, [16] * 5, 2**18 + 7), (4, [4] * 4, 99999),
                                       (3, [2] * 3, 4097), (6, [256, 16, 4, 2, 256, 16], 50001), (1, [256], 15)])
 @pytest.mark.parametrize("kernel", ["occ", "occ_nopf", "plain"])

@@ -26,6 +26,9 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     a = ap.parse_args()
     import sketchml_amd as sk
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import forms  # noqa: E402
+    forms.apply()  # SKML_TOOL_FORMS (tools/ab.sh)
     from sketchml_amd import _lib
     lib = _lib.lib
     dev = torch.device("cuda", 0)

@@ -33,6 +33,9 @@ def main():
                     help="one warm-up and `reps` timed dense -> payload encodes only (the PMC passes' program)")
     a = ap.parse_args()
     import sketchml_amd as sk
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import forms  # noqa: E402
+    forms.apply()  # SKML_TOOL_FORMS (tools/ab.sh)
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(3)
     x = torch.randn(a.dim, device=dev, generator=g)

@@ -13,3 +13,5 @@ timeout -k 10 200 rocprofv3 --kernel-trace -d gpurun_out/r05c/trace -o run --out
 python3 tools/trace_gaps.py gpurun_out/r05c/trace --skip 200 > gpurun_out/r05c/gaps.json
 cat gpurun_out/r05c/gaps.json
 find gpurun_out/r05c -name "*.csv" -size +20M -delete
+SKML_LIB=sketchml_amd/lib_prof/libskml.so timeout -k 10 120 python tools/prof_leaf_waves.py 268435456 > gpurun_out/r05c/leaf_waves.txt 2>&1
+cat gpurun_out/r05c/leaf_waves.txt

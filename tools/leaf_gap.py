@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--n", type=int, default=2**28)
     a = ap.parse_args()
     import sketchml_amd as sk
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import forms  # noqa: E402
+    forms.apply()  # SKML_TOOL_FORMS (tools/ab.sh)
     from sketchml_amd import _lib
     lib = _lib.lib
     dev = torch.device("cuda", 0)

@@ -9,7 +9,7 @@ OUT=gpurun_out/pmc_agg_$TAG
 mkdir -p "$OUT"
 for PASS in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_LDS"; do
   NAME=$(echo $PASS | cut -d' ' -f1)
-  SKML_AGG_ONE_LANE=1 timeout -s KILL 240 rocprofv3 --pmc $PASS --kernel-trace -d "$OUT/$NAME" -o run --output-format csv -- python3 tools/bench_sparse.py --reps 1 --aggregate 8 > "$OUT/$NAME.log" 2>&1
+  SKML_TOOL_FORMS=agg_one_lane:1 timeout -s KILL 240 rocprofv3 --pmc $PASS --kernel-trace -d "$OUT/$NAME" -o run --output-format csv -- python3 tools/bench_sparse.py --reps 1 --aggregate 8 > "$OUT/$NAME.log" 2>&1
 done
 python3 - "$OUT" <<'PY'
 import csv, glob, json, os, re, statistics, sys
@@ -25,7 +25,7 @@ summ = {k: {c: statistics.mean(v) for c, v in d.items()} for k, d in res.items()
 for k, d in summ.items():
     if "FETCH_SIZE" in d: d["read_bytes (2 x FETCH_SIZE KiB)"] = 2 * d["FETCH_SIZE"] * 1024
     if "WRITE_SIZE" in d: d["write_bytes"] = d["WRITE_SIZE"] * 1024
-json.dump({"source": "rocprofv3 --pmc, tools/bench_sparse.py --reps 1 --aggregate 8, SKML_AGG_ONE_LANE=1; per dispatch means",
+json.dump({"source": "rocprofv3 --pmc, tools/bench_sparse.py --reps 1 --aggregate 8, SKML_TOOL_FORMS=agg_one_lane:1; per dispatch means",
            "kernels": summ}, open(os.path.join(out, "summary.json"), "w"), indent=1)
 print(json.dumps(summ, indent=1))
 PY

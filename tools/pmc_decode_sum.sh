@@ -1,6 +1,6 @@
 #!/bin/bash
 # k_decode_sum at C4 (8 x 2^26 8-bit codes): time A/B of the occupancy kernel with and without the
-# next step's code prefetch and the 16-element per-payload kernel (SKML_DECODE_SUM_PLAIN=1), then
+# next step's code prefetch and the 16-element per-payload kernel (SKML_FORM_DECODE_SUM 1), then
 # one LDS / VALU counter pass of each.  usage (through gpurun): bash tools/pmc_decode_sum.sh TAG
 set -e
 TAG=${1:-cur}
@@ -8,7 +8,7 @@ cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/dsum_$TAG
 mkdir -p "$OUT"
-VARIANTS="occ:SKML_AB_DEFAULT=1 occ_nopf:SKML_DECODE_SUM_NOPF=1 plain:SKML_DECODE_SUM_PLAIN=1"
+VARIANTS="occ:SKML_TOOL_FORMS=decode_sum:0 occ_nopf:SKML_TOOL_FORMS=decode_sum:2 plain:SKML_TOOL_FORMS=decode_sum:1"
 for i in 1 2 3; do
   for V in $VARIANTS; do
     env "${V#*:}" timeout -k 10 120 python3 tools/bench_decode_sum.py >> "$OUT/ab_${V%%:*}.jsonl"

@@ -47,3 +47,12 @@ for it in range(3):
                       f"end max {en[m].max():.1f}")
         hist = np.histogram(dur, bins=10)
         print("   dur histogram:", list(hist[0]), [round(v, 1) for v in hist[1]])
+        # resident waves over time (1 us steps): how much of the span the chip runs short of waves
+        T = np.arange(0.0, en.max() + 1.0, 1.0)
+        conc = np.searchsorted(np.sort(st), T, side="right") - np.searchsorted(np.sort(en), T, side="right")
+        peak = conc.max()
+        used = dur.sum() / (peak * en.max())
+        t90 = T[np.nonzero(conc >= 0.9 * peak)[0][-1]]
+        t50 = T[np.nonzero(conc >= 0.5 * peak)[0][-1]]
+        print(f"   resident waves: peak {peak}, wave-slot use over the span {used:.3f}; "
+              f">= 90 % of peak until {t90:.0f} us, >= 50 % until {t50:.0f} us, span {en.max():.0f} us")
