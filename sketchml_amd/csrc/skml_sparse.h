@@ -181,6 +181,9 @@ struct AggPayload {
     const int32_t* bounds;  // [G][ntiles + 1]
     int32_t G, dense_form;
     int32_t bw, nq;
+    // gk - keys base and gb - bins base (elements / bytes) of launch_agg_tiles' bases: the staged
+    // tiles index both with 32-bit offsets from one base each
+    int32_t gk_off, gb_off;
 };
 static_assert(sizeof(AggPayload) % 8 == 0, "copied as u64 words");
 // tile_bits: log2 of the keys per tile the bounds are taken at (agg_tile_bits of the chosen form)
@@ -192,8 +195,10 @@ hipError_t launch_agg_bounds(hipStream_t st, const int32_t* gk, int64_t n, const
 constexpr int kAggVPayloads = 8;
 bool agg_vtiles_ok(int max_groups, int max_nq);
 int agg_tile_bits(bool vtiles);
+// kbase / bbase: the buffers every payload's gk / gb lie in (AggPayload::gk_off / gb_off)
 hipError_t launch_agg_tiles(hipStream_t st, const AggPayload* pays, int P, int64_t ntiles, int64_t dim, double* out,
-                            int from_out, double scale, unsigned* err, bool vtiles);
+                            int from_out, double scale, unsigned* err, bool vtiles, const int32_t* kbase,
+                            const uint8_t* bbase);
 
 // Exported sparse payload: one contiguous device blob (skml_sparse_export / _import, the unit the
 // RCCL all-gather moves).  Offsets are from the blob start, every section 256-byte aligned.

@@ -2987,26 +2987,32 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_tiles_w(const AggPayload* _
 
 // One wave per tile of kAggVTile keys, staged: lane 8p + g of the wave holds the run piece of
 // payload p, group g (P <= 8, G <= 8), the pieces are concatenated payload by payload and each lane
-// loads up to kAggWPer elements of the concatenation.  The wave then writes every element's bin to
-// its slot of the wave's stage (one byte per (payload, key)) and sets the slot's presence bit; a
-// bit already set is a key repeated inside one payload (flagged).  Last, lane l owns keys
+// loads up to kAggWPer * SUB elements of the concatenation.  The wave then writes every element's
+// bin to its slot of the wave's stage (one byte per (payload, key)) and sets the slot's presence
+// bit; a bit already set is a key repeated inside one payload (err bit 2).  Last, lane l owns keys
 // 8l .. 8l + 7 and sums them in registers payload after payload, which is Gradient.sum's order for
 // every key, without a read-modify-write of an LDS sum per element.  Persistent waves: each wave
 // loads its next tile's run bounds one tile ahead, and stores a tile's sums after the next tile's
 // element loads are in flight.  bw == 1 and nq <= 256 for every payload (agg_vtiles_ok).
+// SUB > 1: a wave takes SUB consecutive tiles at once (one bounds pair and one round of element
+// loads for all of them: run pieces SUB times longer, so fewer L2 requests per element), then
+// stages and sums them one tile after the other through the same 4 KB stage.
 constexpr int kAggVBits = 9, kAggVTile = 1 << kAggVBits;
 static_assert(kAggVTile == 8 * 64, "eight keys per lane");
-__global__ __launch_bounds__(kAggThreads) void k_agg_vtiles(const AggPayload* __restrict__ pays, int P,
-                                                           int64_t ntiles, int64_t dim, double* __restrict__ out,
-                                                           int from_out, double scale, unsigned* __restrict__ err) {
+template <int SUB>
+__global__ __launch_bounds__(kAggThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_agg_vtiles(
+    const AggPayload* __restrict__ pays, int P, int64_t ntiles, int64_t dim, double* __restrict__ out, int from_out,
+    double scale, unsigned* __restrict__ err, const int32_t* __restrict__ kbase, const uint8_t* __restrict__ bbase) {
     constexpr int kWaves = kAggThreads / 64;
+    constexpr int kPer = kAggWPer * SUB;  // elements per lane held in registers
     // the stage: a bin per (payload, key); between tiles, the transpose of the stored sums
     __shared__ __attribute__((aligned(16))) uint8_t bins[kWaves][kAggPB][kAggVTile];
     static_assert(kAggPB * kAggVTile == kAggVTile * sizeof(double), "a tile of sums fits the stage");
     __shared__ uint32_t here[kWaves][kAggPB][kAggVTile / 32];  // presence bits
     __shared__ double qt[kAggPB][kAggLdsValues];
     __shared__ int32_t pre[kWaves][65];  // the wave's 64 run pieces, scanned
-    __shared__ int32_t pb0[kWaves][64];  // each piece's first element in its payload
+    __shared__ int32_t pk0[kWaves][64];  // each piece's first key (index from kbase)
+    __shared__ int32_t pn0[kWaves][64];  // and its first bin (byte from bbase)
     __shared__ AggPayload pl[kAggPB];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (threadIdx.x < P * (int)(sizeof(AggPayload) / 8))
@@ -3021,25 +3027,26 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_vtiles(const AggPayload* __
     uint8_t(*B)[kAggVTile] = bins[wave];
     uint32_t(*H)[kAggVTile / 32] = here[wave];
     unsigned bad = 0;
+    const int64_t nsup = (ntiles + SUB - 1) / SUB;  // super-tiles of SUB tiles
     int32_t nb0 = 0, nb1 = 0;
     auto fetch = [&](int64_t tt) {
-        if (lane_on && tt < ntiles) {
-            nb0 = gload<int32_t>(bd, tt);
-            nb1 = gload<int32_t>(bd, tt + 1);
+        if (lane_on && tt < nsup) {
+            nb0 = gload<int32_t>(bd, tt * SUB);
+            nb1 = gload<int32_t>(bd, std::min<int64_t>(tt * SUB + SUB, ntiles));
         }
     };
-    double acc[8];
     int64_t prev_k0 = -1, prev_nk = 0;
-    // a tile's sums (lane l: keys 8l .. 8l + 7) wait in the stage until the next tile's loads are
-    // in flight, and leave transposed, so each 16-byte store instruction covers 1 KB of the sum
+    // a tile's sums (lane l: keys 8l .. 8l + 7) wait in the stage until the next loads are in
+    // flight (the last tile of a super-tile) or the next tile is staged, and leave transposed, so
+    // each 16-byte store instruction covers 1 KB of the sum
     double* T = reinterpret_cast<double*>(&B[0][0]);
-    auto store_prev = [&]() {
+    auto store_prev = [&](int l) {
         if (prev_k0 < 0) return;
         double* o = out + prev_k0;
         const bool whole = prev_nk == kAggVTile && (reinterpret_cast<uintptr_t>(o) & 15) == 0;
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            const int x = 128 * q + 2 * lane;
+            const int x = 128 * q + 2 * l;
             const double2 v = *reinterpret_cast<const double2*>(T + x);
             if (whole) {
                 *reinterpret_cast<double2*>(o + x) = v;
@@ -3049,25 +3056,25 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_vtiles(const AggPayload* __
             }
         }
         __builtin_amdgcn_wave_barrier();
+        prev_k0 = -1;
     };
-    const TileWalk tw = tile_walk(blockIdx.x, gridDim.x, wave, kWaves, ntiles);
+    const TileWalk tw = tile_walk(blockIdx.x, gridDim.x, wave, kWaves, nsup);
     fetch(tw.t0);
     for (int64_t t = tw.t0; t < tw.t1; t += tw.step) {
-        const int64_t k0 = t << kAggVBits, nk = std::min<int64_t>(kAggVTile, dim - k0);
+        // lane-derived values are recomputed each tile behind an empty asm barrier: hoisted out of
+        // the loop (32 element indices, shuffle addresses) they were spilled to scratch
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const int64_t K0 = t * SUB << kAggVBits, NK = std::min<int64_t>((int64_t)SUB << kAggVBits, dim - K0);
         const int32_t b0 = nb0, b1 = nb1;
         fetch(t + tw.step);
         const int32_t len = lane_on && b1 > b0 ? b1 - b0 : 0;
-        int32_t x = len;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int32_t y = __shfl_up(x, off, 64);
-            if (lane >= off) x += y;
-        }
-        pre[wave][lane + 1] = x;
-        if (lane == 0) pre[wave][0] = 0;
-        pb0[wave][lane] = b0;
-        reinterpret_cast<uint64_t*>(H)[lane] = 0;  // 8 x 16 words: two per lane
-        const int total = __shfl(x, 63, 64);
+        const int32_t x = (int32_t)wave_incl_scan_u32((uint32_t)len);  // DPP scan: no lane-id addresses
+        pre[wave][ln + 1] = x;
+        if (ln == 0) pre[wave][0] = 0;
+        pk0[wave][ln] = lane_on ? pl[pl_l].gk_off + b0 : 0;
+        pn0[wave][ln] = lane_on ? pl[pl_l].gb_off + b0 : 0;
+        const int total = __builtin_amdgcn_readlane(x, 63);
         __builtin_amdgcn_wave_barrier();
         auto piece_of = [&](int j) -> int {  // largest s < 64 with pre[s] <= j
             int s_ = 0;
@@ -3076,94 +3083,112 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_vtiles(const AggPayload* __
                 if (pre[wave][s_ + step] <= j) s_ += step;
             return s_;
         };
-        auto load_elem = [&](int j, int32_t& key, uint32_t& bin) -> int {  // returns the payload
-            const int sp = piece_of(j);
-            const int p = sp >> 3;
-            const int64_t i = (int64_t)pb0[wave][sp] + (j - pre[wave][sp]);
-            key = gload<int32_t>(pl[p].gk, i);
-            bin = gload<uint8_t>(pl[p].gb, i);
-            return p;
-        };
-        // every element's piece first (8 independent LDS searches), then every element's loads
-        int spc[kAggWPer];
+        // eight elements' pieces first (independent LDS searches), then their loads
+        int32_t kk[kPer];
+        uint32_t bb[kPer];
 #pragma unroll
-        for (int u = 0; u < kAggWPer; u++) {
-            const int j = lane + 64 * u;
-            spc[u] = piece_of(j < total ? j : 0);
-        }
-        int8_t pe[kAggWPer];
-        int32_t kk[kAggWPer];
-        uint32_t bb[kAggWPer];
+        for (int u0 = 0; u0 < kPer; u0 += kAggWPer) {
+            int spc[kAggWPer];
 #pragma unroll
-        for (int u = 0; u < kAggWPer; u++) {
-            const int j = lane + 64 * u;
-            pe[u] = -1;
-            kk[u] = 0;
-            bb[u] = 0;
-            if (j < total) {
-                const int sp = spc[u], p = sp >> 3;
-                const int64_t i = (int64_t)pb0[wave][sp] + (j - pre[wave][sp]);
-                kk[u] = gload<int32_t>(pl[p].gk, i);
-                bb[u] = gload<uint8_t>(pl[p].gb, i);
-                pe[u] = (int8_t)p;
-            }
-        }
-        store_prev();  // after this tile's loads are issued
-        prev_k0 = k0;
-        prev_nk = nk;
-        auto stage = [&](int p, int32_t k, uint32_t b) {
-            if (k < k0 || (int64_t)k >= k0 + nk) {  // k_agg_bounds placed it here: an error
-                bad |= 1u;
-                return;
-            }
-            const int xk = (int)(k - k0);
-            B[p][xk] = (uint8_t)b;
-            const uint32_t bit = 1u << (xk & 31);
-            if (atomicOr(&H[p][xk >> 5], bit) & bit) bad |= 2u;  // a key twice in one payload
-        };
-#pragma unroll
-        for (int u = 0; u < kAggWPer; u++)
-            if (pe[u] >= 0) stage(pe[u], kk[u], bb[u]);
-        for (int j = 64 * kAggWPer + lane; j < total; j += 64) {  // elements past the registers
-            int32_t k;
-            uint32_t b;
-            const int p = load_elem(j, k, b);
-            stage(p, k, b);
-        }
-        __builtin_amdgcn_wave_barrier();
-        // lane l: keys 8l .. 8l + 7, payload after payload
-#pragma unroll
-        for (int i = 0; i < 8; i++)  // a later batch continues the sum
-            acc[i] = from_out && 8 * lane + i < nk ? out[k0 + 8 * lane + i] : 0.0;
-        for (int p = 0; p < P; p++) {
-            const uint32_t m = reinterpret_cast<const uint8_t*>(H[p])[lane];
-            const uint2 bw8 = *reinterpret_cast<const uint2*>(&B[p][8 * lane]);
-            const bool dform = pl[p].dense_form != 0;
-            double v[8];
-#pragma unroll
-            for (int i = 0; i < 8; i++) {
-                const uint32_t b = ((i < 4 ? bw8.x : bw8.y) >> (8 * (i & 3))) & 0xFFu;
-                v[i] = 0.0;
-                if (m & (1u << i)) v[i] = qt[p][b];
+            for (int u = 0; u < kAggWPer; u++) {
+                const int j = ln + 64 * (u0 + u);
+                spc[u] = piece_of(j < total ? j : 0);
             }
 #pragma unroll
-            for (int i = 0; i < 8; i++) {
-                // the dense form keeps |v| > EPS only (SparseDoubleGradient.toDense), and adds +0.0
-                // elsewhere: a -0.0 sum becomes +0.0
-                if ((m & (1u << i)) && (!dform || fabs(v[i]) > 1e-8)) acc[i] += v[i];
-                if (dform && __double_as_longlong(acc[i]) == (long long)0x8000000000000000ull) acc[i] = 0.0;
+            for (int u = 0; u < kAggWPer; u++) {
+                const int j = ln + 64 * (u0 + u);
+                kk[u0 + u] = INT32_MIN;
+                bb[u0 + u] = 0;
+                if (j < total) {
+                    const int sp = spc[u], p = sp >> 3, d = j - pre[wave][sp];
+                    kk[u0 + u] = gload<int32_t>(kbase, (uint32_t)(pk0[wave][sp] + d));
+                    bb[u0 + u] = gload<uint8_t>(bbase, (uint32_t)(pn0[wave][sp] + d)) | ((uint32_t)p << 8);
+                }
             }
         }
-        if (scale != 1.0)
+        // one word per element: key offset in the super-tile (bits 0..12), bin (13..20), payload
+        // (21..23); ~0u: no element.  A key outside the super-tile is an error (k_agg_bounds placed
+        // it here).
+        uint32_t ew[kPer];
 #pragma unroll
-            for (int i = 0; i < 8; i++) acc[i] = __dmul_rn(acc[i], scale);
-        __builtin_amdgcn_wave_barrier();  // the stage is read before the sums replace it
+        for (int u = 0; u < kPer; u++) {
+            const int64_t off = (int64_t)kk[u] - K0;
+            ew[u] = ~0u;
+            if (ln + 64 * u < total) {
+                if (off < 0 || off >= NK) bad |= 1u;
+                else ew[u] = (uint32_t)off | ((bb[u] & 0xFFu) << 13) | ((bb[u] >> 8) << 21);
+            }
+        }
+        store_prev(ln);  // after this super-tile's loads are issued
+#pragma unroll 1
+        for (int sub = 0; sub < SUB; sub++) {
+            const int64_t k0 = K0 + ((int64_t)sub << kAggVBits);
+            const int64_t nk = std::min<int64_t>(kAggVTile, dim - k0);
+            if (nk <= 0) break;
+            int ls = ln;  // (rematerialised per tile, like ln)
+            asm volatile("" : "+v"(ls));
+            if (sub > 0) store_prev(ls);  // the previous tile's sums leave the stage before it is reused
+            reinterpret_cast<uint64_t*>(H)[ls] = 0;  // 8 x 16 words: two per ls
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t sub_lo = (uint32_t)sub << kAggVBits;
+            auto stage = [&](uint32_t w) {  // w: an element word of this tile
+                const int p = (int)(w >> 21), xk = (int)((w & 0x1FFFu) - sub_lo);
+                B[p][xk] = (uint8_t)(w >> 13);
+                const uint32_t bit = 1u << (xk & 31);
+                if (atomicOr(&H[p][xk >> 5], bit) & bit) bad |= 2u;  // a key twice in one payload
+            };
 #pragma unroll
-        for (int q = 0; q < 4; q++)
-            *reinterpret_cast<double2*>(T + 8 * lane + 2 * q) = make_double2(acc[2 * q], acc[2 * q + 1]);
-        __builtin_amdgcn_wave_barrier();
+            for (int u = 0; u < kPer; u++)
+                if (ew[u] != ~0u && ((ew[u] & 0x1FFFu) >> kAggVBits) == (uint32_t)sub) stage(ew[u]);
+            for (int j = 64 * kPer + ls; j < total; j += 64) {  // elements past the registers
+                const int sp = piece_of(j), p = sp >> 3, d = j - pre[wave][sp];
+                const int64_t off = (int64_t)gload<int32_t>(kbase, (uint32_t)(pk0[wave][sp] + d)) - K0;
+                if (off < 0 || off >= NK) {
+                    bad |= 1u;
+                    continue;
+                }
+                if ((off >> kAggVBits) == sub)
+                    stage((uint32_t)off | ((uint32_t)gload<uint8_t>(bbase, (uint32_t)(pn0[wave][sp] + d)) << 13) |
+                          ((uint32_t)p << 21));
+            }
+            __builtin_amdgcn_wave_barrier();
+            // ls l: keys 8l .. 8l + 7, payload after payload
+            double acc[8];
+#pragma unroll
+            for (int i = 0; i < 8; i++)  // a later batch continues the sum
+                acc[i] = from_out && 8 * ls + i < nk ? out[k0 + 8 * ls + i] : 0.0;
+            for (int p = 0; p < P; p++) {
+                const uint32_t m = reinterpret_cast<const uint8_t*>(H[p])[ls];
+                const uint2 bw8 = *reinterpret_cast<const uint2*>(&B[p][8 * ls]);
+                const bool dform = pl[p].dense_form != 0;
+                double v[8];
+#pragma unroll
+                for (int i = 0; i < 8; i++) {
+                    const uint32_t b = ((i < 4 ? bw8.x : bw8.y) >> (8 * (i & 3))) & 0xFFu;
+                    v[i] = 0.0;
+                    if (m & (1u << i)) v[i] = qt[p][b];
+                }
+#pragma unroll
+                for (int i = 0; i < 8; i++) {
+                    // the dense form keeps |v| > EPS only (SparseDoubleGradient.toDense), and adds +0.0
+                    // elsewhere: a -0.0 sum becomes +0.0
+                    if ((m & (1u << i)) && (!dform || fabs(v[i]) > 1e-8)) acc[i] += v[i];
+                    if (dform && __double_as_longlong(acc[i]) == (long long)0x8000000000000000ull) acc[i] = 0.0;
+                }
+            }
+            if (scale != 1.0)
+#pragma unroll
+                for (int i = 0; i < 8; i++) acc[i] = __dmul_rn(acc[i], scale);
+            __builtin_amdgcn_wave_barrier();  // the stage is read before the sums replace it
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                *reinterpret_cast<double2*>(T + 8 * ls + 2 * q) = make_double2(acc[2 * q], acc[2 * q + 1]);
+            __builtin_amdgcn_wave_barrier();
+            prev_k0 = k0;
+            prev_nk = nk;
+        }
     }
-    store_prev();
+    store_prev(lane);
     if (bad) atomicOr(err, bad);
 }
 
@@ -3189,15 +3214,33 @@ static int resident_workgroups(K kern) {
 }
 
 hipError_t launch_agg_tiles(hipStream_t st, const AggPayload* pays, int P, int64_t ntiles, int64_t dim, double* out,
-                            int from_out, double scale, unsigned* err, bool vtiles) {
+                            int from_out, double scale, unsigned* err, bool vtiles, const int32_t* kbase,
+                            const uint8_t* bbase) {
     if (ntiles <= 0) return hipSuccess;
     if (vtiles) {
         if (P < 1 || P > kAggVPayloads) return hipErrorInvalidValue;  // one lane per (payload, group)
-        static const int resident_v = resident_workgroups(k_agg_vtiles);
+        // SKML_FORM_AGG_TILES = 2 / 3: four / two tiles per wave round (A/B forms)
+        if (form(SKML_FORM_AGG_TILES) == 2) {
+            static const int resident4 = resident_workgroups(k_agg_vtiles<4>);
+            const int64_t all = sp_tiles(sp_tiles(ntiles, 4), kAggThreads / 64);
+            const unsigned grid = (unsigned)(resident4 <= 0 ? all : std::min<int64_t>(all, resident4));
+            hipLaunchKernelGGL(k_agg_vtiles<4>, dim3(grid), dim3(kAggThreads), 0, st, pays, P, ntiles, dim, out,
+                               from_out, scale, err, kbase, bbase);
+            return hipGetLastError();
+        }
+        if (form(SKML_FORM_AGG_TILES) == 3) {
+            static const int resident2 = resident_workgroups(k_agg_vtiles<2>);
+            const int64_t all = sp_tiles(sp_tiles(ntiles, 2), kAggThreads / 64);
+            const unsigned grid = (unsigned)(resident2 <= 0 ? all : std::min<int64_t>(all, resident2));
+            hipLaunchKernelGGL(k_agg_vtiles<2>, dim3(grid), dim3(kAggThreads), 0, st, pays, P, ntiles, dim, out,
+                               from_out, scale, err, kbase, bbase);
+            return hipGetLastError();
+        }
+        static const int resident_v = resident_workgroups(k_agg_vtiles<1>);
         const int64_t all = sp_tiles(ntiles, kAggThreads / 64);
         const unsigned grid = (unsigned)(resident_v <= 0 ? all : std::min<int64_t>(all, resident_v));
-        hipLaunchKernelGGL(k_agg_vtiles, dim3(grid), dim3(kAggThreads), 0, st, pays, P, ntiles, dim, out, from_out,
-                           scale, err);
+        hipLaunchKernelGGL(k_agg_vtiles<1>, dim3(grid), dim3(kAggThreads), 0, st, pays, P, ntiles, dim, out, from_out,
+                           scale, err, kbase, bbase);
         return hipGetLastError();
     }
     // persistent: as many workgroups as are resident at once

@@ -1954,6 +1954,8 @@ int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t
                                                    hs[(size_t)p].off_values);
             a.bounds = bounds + bo;
             a.G = v.g.G;
+            a.gk_off = (int32_t)ko;   // < 2^31: the batch's keys fit the 3 GB scratch budget
+            a.gb_off = (int32_t)bbo;
             const DecodeValues dv{a.nq, const_cast<void*>(a.gb), a.bw, err};
             auto join = [&](int e) {  // an error after the fork: the caller's stream still waits for the side
                 if (lanes[1]) {
@@ -1990,7 +1992,7 @@ int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t
         for (size_t c0 = 0; c0 < pays.size(); c0 += chunk) {
             const size_t nc = std::min(chunk, pays.size() - c0);
             SP_HIP(launch_agg_tiles(st, d_pays + c0, (int)nc, ntiles, dim, out, first && c0 == 0 ? 0 : 1,
-                                    last && c0 + nc == pays.size() ? scale : 1.0, err, vt));
+                                    last && c0 + nc == pays.size() ? scale : 1.0, err, vt, gk, gbn));
         }
         SP_HIP(hipStreamSynchronize(st));  // `pays` (host) and the scratch are reused by the next batch
         first = false;

@@ -15,3 +15,4 @@ cat gpurun_out/r05c/gaps.json
 find gpurun_out/r05c -name "*.csv" -size +20M -delete
 SKML_LIB=sketchml_amd/lib_prof/libskml.so timeout -k 10 120 python tools/prof_leaf_waves.py 268435456 > gpurun_out/r05c/leaf_waves.txt 2>&1
 cat gpurun_out/r05c/leaf_waves.txt
+bash tools/ab.sh agg 2 sparse v1= v2=form:agg_tiles:3 v4=form:agg_tiles:2 w=form:agg_tiles:1
