@@ -295,6 +295,13 @@ def other_configs(sk, lib, ctx, dev):
     del pls
     out["dense_decode_sum_c4"] = dense_decode_sum(sk, lib, ctx, dev, xs, n, p)
     del xs
+    # C5's consumer: 8 payloads of 2^27 floats at 4 requested bins (2-bit codes)
+    x27 = []
+    for b in range(2):
+        gen.manual_seed(27 + 1000 * b)
+        x27.append(torch.randn(2**27, device=dev, generator=gen))
+    out["dense_decode_sum_c5"] = dense_decode_sum(sk, lib, ctx, dev, x27, 2**27, _lib_params(4), bins=4)
+    del x27
     dim = 2**28
     d = c3_dense(dev, 3, dim)
     te, spl = timed_median(lambda: sk.encode_dense_as_sparse(d, 256, 8, 2, 0.3, 3, 3), 5)
@@ -356,11 +363,12 @@ def sparse_aggregate(sk, spl, dim, timed_median, dev, P=8):
     return res
 
 
-def dense_decode_sum(sk, lib, ctx, dev, xs, n, p, P=8):
+def dense_decode_sum(sk, lib, ctx, dev, xs, n, p, P=8, bins=256):
     """C4's consumer on one GPU: P = 8 gathered 2^26-value dense payloads -> fused decode + sum in
     double + x 1/P (skml_dense_decode_sum_f32), HIP-event timed on the codec stream.  Algorithmic
-    bytes = P * n * b / 8 (codes) + 4 n (fp32 out)."""
-    nb = lib.skml_dense_payload_bytes(n, 256)
+    bytes = P * n * b / 8 (codes) + 4 n (fp32 out).  With bins = 4 and n = 2^27: C5's consumer (each
+    rank sums the 8 gathered 2^27-float shards' 2-bit payloads)."""
+    nb = lib.skml_dense_payload_bytes(n, bins)
     stride = (nb + 255) // 256 * 256
     allp = sk.alloc_aligned(stride * P, dev)
     ptrs = (C.c_void_p * P)(*[xs[i % len(xs)].data_ptr() for i in range(P)])
@@ -384,7 +392,8 @@ def dense_decode_sum(sk, lib, ctx, dev, xs, n, p, P=8):
     us = ks["k_decode_sum"]["avg_us"]
     alg = P * n * hdr.code_bits / 8.0 + 4.0 * n
     del allp, out
-    return {"workload": f"{P} dense payloads of 2^26 codes ({hdr.code_bits}-bit) -> one fp32 sum x 1/{P}",
+    return {"workload": f"{P} dense payloads of 2^{n.bit_length() - 1} codes ({hdr.code_bits}-bit, {hdr.bin_num} bins) "
+                        f"-> one fp32 sum x 1/{P}",
             "k_decode_sum_us": round(us, 2), "alg_bytes": alg,
             "gbps": round(alg / (us * 1e-6) / 1e9, 1), "roofline_frac": round(alg / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
 

@@ -90,11 +90,15 @@ __device__ __forceinline__ uint32_t quant_bin(const QuantTables& q, float xv) {
     return xv == xv ? bin : q.nan_bin;
 }
 
-// 8-bit codes leave as one 16-byte write-through (sc1) store per lane: the wave's 1,024 codes of a
-// tile are transposed through 1 KB of LDS (lane l then holds codes 16 l .. 16 l + 15).  Write-through
-// stores leave no dirty lines in the XCD's L2, so the end of the pass has nothing to write back
-// before the next kernel starts: nontemporal 4-byte stores left ~10 us of idle time at that
-// boundary in every 2^28 encode (profiles/r05b_warmup_ramp.txt, tools/trace_gaps.py).
+// Code store forms for 8-bit codes (SKML_Q_STORE, A/B builds): 0 (default) a 4-byte nontemporal
+// store per lane and group of 4 codes; 1 / 2 the wave's 1,024 codes of a tile transposed through
+// 1 KB of LDS (lane l then holds codes 16 l .. 16 l + 15) and stored as one 16-byte nontemporal (1)
+// or write-through sc1 (2) store per lane.  Write-through leaves no dirty lines in the XCD's L2 for
+// the end-of-kernel write-back (the ~10 us idle gap before the next encode's leaf, tools/trace_gaps.py),
+// but the form measured 224 -> 246 us per 2^28 quantize (profiles/r05c_bench.json).
+#ifndef SKML_Q_STORE
+#define SKML_Q_STORE 0
+#endif
 constexpr int kQStageWords = 256;  // per wave: 1,024 one-byte codes
 
 template <int MODE>
@@ -113,7 +117,7 @@ __device__ __forceinline__ void quant_tiles(const QuantTables& q, const float* _
         for (int j = 0; j < 4; j++) f[j] = __builtin_nontemporal_load(src + j * 64 + lane);
     }
     // codes are < 4 GB past `codes` (n < 2^31): one buffer descriptor, 32-bit offsets
-    const bool wt = bits == 8 && (reinterpret_cast<uintptr_t>(codes) & 15) == 0;
+    const bool wt = SKML_Q_STORE != 0 && bits == 8 && (reinterpret_cast<uintptr_t>(codes) & 15) == 0;
     const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
         codes, 0, (int)std::min<int64_t>(full_tiles * 1024, (int64_t)0x7FFFFC00), 0x00020000);
     for (int64_t tile = wave_id; tile < full_tiles; tile += nwaves_total) {
@@ -136,7 +140,7 @@ __device__ __forceinline__ void quant_tiles(const QuantTables& q, const float* _
             __builtin_amdgcn_wave_barrier();  // the stage is read before the next tile overwrites it
             typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
             __builtin_amdgcn_raw_buffer_store_b128(u32x4{w.x, w.y, w.z, w.w}, crs, (int)(tile * 1024 + lane * 16), 0,
-                                                   16 /* sc1: write-through */);
+                                                   SKML_Q_STORE == 2 ? 16 /* sc1: write-through */ : 2 /* nt */);
         } else {
 #pragma unroll
             for (int j = 0; j < 4; j++) {

@@ -2545,6 +2545,10 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_keys(const uint32_t* __rest
             }
 #pragma unroll
             for (int j = 0; j < 4; j++) {
+#ifdef SKML_ABLATE_DEC_GATHER  // timing ablation only (wrong bins): the table gathers priced
+                tv[r][j] = (int32_t)(rel[r][j] & 0x3Fu);
+                continue;
+#endif
                 if constexpr (sizeof(TN) == 4) tv[r][j] = rel[r][j] != ~0u ? t32b[rel[r][j]] : zero;
                 else tv[r][j] = rel[r][j] != ~0u ? (int32_t)tnb[rel[r][j]] : zero;
             }
