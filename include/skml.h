@@ -126,7 +126,7 @@ int skml_debug_sparse_merge_path(void);
 /* Test hook: force one of the library's alternative kernel forms, process-wide.  Every form gives
  * the same results (the tests run each one against the oracle); 0 is the library's own choice.
  * Returns the previous value, or -1 for an unknown id.  Not part of the codec. */
-#define SKML_FORM_LEAF_SPLIT 0      /* 1: one wave per 64-chunk tile always, 2: the split leaf always */
+#define SKML_FORM_LEAF_SPLIT 0      /* 1: one wave per 64-chunk tile always, 2: the split leaf always, 3 / 4 / 5: the last 25 / 12.5 / 50 % split */
 #define SKML_FORM_DECODE_SUM 1      /* 1: the per-payload kernel, 2: the occupancy form without prefetch */
 #define SKML_FORM_PART_BALLOT 2     /* 1: the ballot-ranked partition scatter */
 #define SKML_FORM_RS_ROUNDS 3       /* 1: Sort.merge by the pairwise merge rounds always */

@@ -572,7 +572,7 @@ constexpr int kL64Rounds = kLeafWaveChunks / kL64Chunks;
 #define SKML_LEAF_MIN3DET 1
 #endif
 #ifndef SKML_LEAF_SPLIT_BELOW
-#define SKML_LEAF_SPLIT_BELOW 3072  // full tiles under which k_leaf64<true> runs
+#define SKML_LEAF_SPLIT_BELOW 3072  // full tiles under which the split leaf runs alone
 #endif
 // `chunks` counts the full tiles' chunks; when total_chunks holds a partial tile as well, that
 // tile's small trees (k_leaf2's PARTIAL path, one wave) run in workgroup 0, which is dispatched
@@ -581,26 +581,20 @@ constexpr int kL64Rounds = kLeafWaveChunks / kL64Chunks;
 // tile, wave w running round w to its level-4 node; waves 1 and 3 merge the pairs to level 5 and
 // wave 3 the level-6 node (exact merges there when the waves' zero signs differ), so a small
 // bucket runs 4x the waves with the same outputs.
+struct Leaf64Shared {
+    float fb[kLeaf2Waves][kWaveFb];
+    float2 stk[kLeaf2Waves][2][64];  // the carry stack (levels 4, 5) in LDS, not registers
+    uint32_t wpart[kLeaf2Waves][4];  // SPLIT: each wave's min / max / flags / zero signs
+};
 template <bool SPLIT>
-__global__ __launch_bounds__(256, SKML_LEAF64_WAVES) void k_leaf64(const float* __restrict__ x, int64_t chunks, uint64_t s0,
-                                                   const uint64_t* __restrict__ tab, LeafPartial* __restrict__ part,
-                                                   float* __restrict__ nodes6, float* __restrict__ roots,
-                                                   uint8_t* __restrict__ ubits, int64_t total_chunks) {
-    __shared__ float fb[kLeaf2Waves][kWaveFb];
-    __shared__ float2 stk[kLeaf2Waves][2][64];  // the carry stack (levels 4, 5) in LDS, not registers
-    __shared__ uint32_t wpart[kLeaf2Waves][4];  // SPLIT: each wave's min / max / flags / zero signs
+__device__ __forceinline__ void leaf64_tile(const float* __restrict__ x, int64_t chunks, uint64_t s0,
+                                            const uint64_t* __restrict__ tab, LeafPartial* __restrict__ part,
+                                            float* __restrict__ nodes6, float* __restrict__ roots,
+                                            uint8_t* __restrict__ ubits, int64_t tile, Leaf64Shared& L) {
+    auto& fb = L.fb;
+    auto& stk = L.stk;
+    auto& wpart = L.wpart;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    int64_t blk = blockIdx.x;
-    if (total_chunks > chunks) {
-        if (blk == 0) {
-            if (wave == 0)
-                leaf2_wave<3, true, float>(x, total_chunks, s0, tab, part, nodes6, roots, chunks / kLeafWaveChunks,
-                                           nullptr, fb[0]);
-            return;
-        }
-        blk -= 1;
-    }
-    const int64_t tile = SPLIT ? blk : blk * kLeaf2Waves + wave;
     const int64_t c_tile = tile * kLeafWaveChunks;
     if (c_tile >= chunks) return;  // workgroup-uniform under SPLIT, wave-uniform otherwise
 #ifdef SKML_PROF_LEAF
@@ -824,6 +818,40 @@ __global__ __launch_bounds__(256, SKML_LEAF64_WAVES) void k_leaf64(const float* 
     }
 }
 
+// MODE 0: one wave per 64-chunk tile; MODE 1: the split form (four waves per tile); MODE 2: tiles
+// below split_from one per wave, the rest split.  The split tiles come last in dispatch order, so
+// the end of a large bucket runs in quarter-size units: one wave per tile left a tail in which
+// the chip ran short of waves (2^28: wave-slot use 0.82 over the span, tools/prof_leaf_waves.py,
+// profiles/r05d_leaf_waves.txt).
+template <int MODE>
+__global__ __launch_bounds__(256, SKML_LEAF64_WAVES) void k_leaf64(const float* __restrict__ x, int64_t chunks, uint64_t s0,
+                                                   const uint64_t* __restrict__ tab, LeafPartial* __restrict__ part,
+                                                   float* __restrict__ nodes6, float* __restrict__ roots,
+                                                   uint8_t* __restrict__ ubits, int64_t total_chunks,
+                                                   int64_t split_from) {
+    __shared__ Leaf64Shared L;
+    const int wave = threadIdx.x >> 6;
+    int64_t blk = blockIdx.x;
+    if (total_chunks > chunks) {
+        if (blk == 0) {
+            if (wave == 0)
+                leaf2_wave<3, true, float>(x, total_chunks, s0, tab, part, nodes6, roots, chunks / kLeafWaveChunks,
+                                           nullptr, L.fb[0]);
+            return;
+        }
+        blk -= 1;
+    }
+    if constexpr (MODE == 0) {
+        leaf64_tile<false>(x, chunks, s0, tab, part, nodes6, roots, ubits, blk * kLeaf2Waves + wave, L);
+    } else if constexpr (MODE == 1) {
+        leaf64_tile<true>(x, chunks, s0, tab, part, nodes6, roots, ubits, blk, L);
+    } else {
+        const int64_t nwg = split_from / kLeaf2Waves;  // split_from: a multiple of 4
+        if (blk < nwg) leaf64_tile<false>(x, chunks, s0, tab, part, nodes6, roots, ubits, blk * kLeaf2Waves + wave, L);
+        else leaf64_tile<true>(x, chunks, s0, tab, part, nodes6, roots, ubits, split_from + (blk - nwg), L);
+    }
+}
+
 template <int STAGE, int MINW = 1>
 __global__ __launch_bounds__(512, MINW) void k_leaf(const float* __restrict__ x, int64_t chunks,
                                               uint64_t s0, const uint64_t* __restrict__ tab,
@@ -989,11 +1017,28 @@ __global__ __launch_bounds__(512, MINW) void k_leaf(const float* __restrict__ x,
 }
 
 // One wave per tile fills the chip from 4,096 tiles (2^26 values) up; below that the split form
-// (four waves per tile) keeps more waves in flight.  SKML_FORM_LEAF_SPLIT forces either (tests).
-static bool leaf_split(int64_t full_tiles) {
-    const int force = form(SKML_FORM_LEAF_SPLIT);
-    if (force) return force == 2;
-    return full_tiles < SKML_LEAF_SPLIT_BELOW;
+// (four waves per tile) keeps more waves in flight.  Larger buckets end with split tiles (the
+// hybrid MODE 2), so the last wave generation runs in quarter-size units.  Returns the first
+// split tile (0: all split, full: none).  SKML_FORM_LEAF_SPLIT forces a form (tests, A/B):
+// 1 none, 2 all, 3 / 4 / 5 the last 25 / 12.5 / 50 % of the tiles.
+#ifndef SKML_LEAF_SPLIT_TAIL_PCT
+#define SKML_LEAF_SPLIT_TAIL_PCT 25
+#endif
+static int64_t leaf_split_from(int64_t full_tiles) {
+    auto tail = [&](int pct_x2) {  // the first split tile for the last pct_x2 / 2 % of the tiles
+        const int64_t s = full_tiles - full_tiles * pct_x2 / 200;
+        return std::max<int64_t>(0, s / kLeaf2Waves * kLeaf2Waves);
+    };
+    switch (form(SKML_FORM_LEAF_SPLIT)) {
+        case 1: return full_tiles;
+        case 2: return 0;
+        case 3: return tail(50);
+        case 4: return tail(25);
+        case 5: return tail(100);
+        default: break;
+    }
+    if (full_tiles < SKML_LEAF_SPLIT_BELOW) return 0;
+    return tail(2 * SKML_LEAF_SPLIT_TAIL_PCT);
 }
 
 hipError_t launch_leaf(hipStream_t st, const float* x, int64_t chunks, uint64_t s0,
@@ -1004,14 +1049,21 @@ hipError_t launch_leaf(hipStream_t st, const float* x, int64_t chunks, uint64_t 
 #endif
     if (full > 0 && SKML_LEAF64) {  // the partial tile, if any, rides in the same launch
         const int extra = chunks % kLeafWaveChunks ? 1 : 0;
-        if (leaf_split(full)) {
-            hipLaunchKernelGGL(k_leaf64<true>, dim3((unsigned)(full + extra)), dim3(64 * kLeaf2Waves), 0, st, x,
-                               full * kLeafWaveChunks, s0, jump_tab, part, nodes6, roots, ubits, chunks);
+        const int64_t split_from = leaf_split_from(full);
+        if (split_from == 0) {
+            hipLaunchKernelGGL(k_leaf64<1>, dim3((unsigned)(full + extra)), dim3(64 * kLeaf2Waves), 0, st, x,
+                               full * kLeafWaveChunks, s0, jump_tab, part, nodes6, roots, ubits, chunks, (int64_t)0);
             return hipGetLastError();
         }
-        const unsigned grid = (unsigned)((full + kLeaf2Waves - 1) / kLeaf2Waves + extra);
-        hipLaunchKernelGGL(k_leaf64<false>, dim3(grid), dim3(64 * kLeaf2Waves), 0, st, x, full * kLeafWaveChunks, s0,
-                           jump_tab, part, nodes6, roots, ubits, chunks);
+        if (split_from >= full) {
+            const unsigned grid = (unsigned)((full + kLeaf2Waves - 1) / kLeaf2Waves + extra);
+            hipLaunchKernelGGL(k_leaf64<0>, dim3(grid), dim3(64 * kLeaf2Waves), 0, st, x, full * kLeafWaveChunks, s0,
+                               jump_tab, part, nodes6, roots, ubits, chunks, full);
+            return hipGetLastError();
+        }
+        const unsigned grid = (unsigned)(split_from / kLeaf2Waves + (full - split_from) + extra);
+        hipLaunchKernelGGL(k_leaf64<2>, dim3(grid), dim3(64 * kLeaf2Waves), 0, st, x, full * kLeafWaveChunks, s0,
+                           jump_tab, part, nodes6, roots, ubits, chunks, split_from);
         return hipGetLastError();
     } else if (full > 0)
         hipLaunchKernelGGL((k_leaf2<3, false>), dim3((unsigned)((full + kLeaf2Waves - 1) / kLeaf2Waves)),

@@ -86,6 +86,24 @@ def test_quantize_edge_data(gpu, kind, n):
     _check(gq, oq, x)
 
 
+@pytest.mark.parametrize("kind", ["normal", "signed_zero"])
+def test_leaf_forms_match_oracle(gpu, kind):
+    """The sketch leaf's forms give the oracle's sketch: one wave per 64-chunk tile, the split leaf
+    (four waves per tile), and the hybrid that ends a large bucket with split tiles (the default
+    from 3,072 tiles; the last 12.5 / 25 / 50 % split), on 4,096 full tiles plus a partial one.
+    signed_zero sends rounds through the exact (count-based) merge path in both forms."""
+    from sketchml_amd import _lib
+    n = 4096 * 64 * 256 + 12345
+    x = _data(n, 91, kind)
+    oq = O.quantize(x.astype(np.float64), 256, 91)
+    xt = torch.from_numpy(x).cuda()
+    for form in (0, 1, 2, 3, 4, 5):
+        with _lib.forced_forms(leaf_split=form):
+            gq = gpu.QuantileQuantizer(256, seed=91)
+            gq.quantize(xt)
+            _check(gq, oq, x)
+
+
 def test_deferred_quantize(gpu):
     """deferred=True queues the encode without a host synchronisation and reuses the payload;
     results equal the eager path, and NaN surfaces at the first getter."""

@@ -15,6 +15,11 @@ import torch  # noqa: E402
 import sketchml_amd as sk  # noqa: E402
 from sketchml_amd import _lib  # noqa: E402
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import forms  # noqa: E402
+
+forms.apply()  # SKML_TOOL_FORMS: e.g. leaf_split:1 (only one-wave-per-tile waves carry stamps)
+
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 2**26
 tiles = min(65536, n // 256 // 64)
 x = torch.randn(n, device="cuda")
@@ -54,5 +59,13 @@ for it in range(3):
         used = dur.sum() / (peak * en.max())
         t90 = T[np.nonzero(conc >= 0.9 * peak)[0][-1]]
         t50 = T[np.nonzero(conc >= 0.5 * peak)[0][-1]]
+        # duration by start time (when in the kernel a wave starts decides whom it shares its SIMD with)
+        order = np.argsort(st)
+        for q in range(10):
+            sel = order[q * len(order) // 10:(q + 1) * len(order) // 10]
+            print(f"   start decile {q}: start {st[sel].min():6.1f}..{st[sel].max():6.1f} us  dur p10 "
+                  f"{np.percentile(dur[sel], 10):6.1f} p50 {np.percentile(dur[sel], 50):6.1f} p90 {np.percentile(dur[sel], 90):6.1f}")
+        os.makedirs("gpurun_out", exist_ok=True)
+        np.savez_compressed("gpurun_out/leaf_waves.npz", st=st, en=en, hw=hw, xcc=xcc)
         print(f"   resident waves: peak {peak}, wave-slot use over the span {used:.3f}; "
               f">= 90 % of peak until {t90:.0f} us, >= 50 % until {t50:.0f} us, span {en.max():.0f} us")
