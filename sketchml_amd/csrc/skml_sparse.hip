@@ -198,12 +198,25 @@ __device__ __forceinline__ int32_t java_hash_fm(int id, int32_t key, int32_t siz
 // 4 elements' cells of one MinMax row with the hash fixed at compile time, as 32-bit offsets
 // (row0: the row's first cell, relative): for a k_dec_keys tile inside one group, whose lanes all
 // use the same hash id, java_hash_mix folds to the one hash instead of computing every variant.
-template <int ID>
+// SKML_DEC_INTMOD (A/B builds): 1 = the modulus by a 32-bit magic-number division (java_mod, as the
+// encode's MinMax insert does) instead of the double-precision quotient.
+#ifndef SKML_DEC_INTMOD
+#define SKML_DEC_INTMOD 0
+#endif
+template <int ID, typename DV>
 __device__ __forceinline__ void dec_row_cells(const int32_t (&key)[4], int64_t i0, int64_t n, int64_t row0,
-                                              int32_t cols, double inv, uint32_t (&rel)[4]) {
+                                              int32_t cols, double inv, const DV& dv, uint32_t (&rel)[4]) {
 #pragma unroll
-    for (int j = 0; j < 4; j++)
-        rel[j] = i0 + j < n ? (uint32_t)(row0 + java_hash_fm(ID, key[j], cols, inv)) : ~0u;
+    for (int j = 0; j < 4; j++) {
+#ifdef SKML_ABLATE_DEC_HASH  // timing ablation only (wrong cells): the hashes priced
+        rel[j] = i0 + j < n ? (uint32_t)(row0 + ((uint32_t)key[j] & 0xFFFFu)) : ~0u;
+        continue;
+#endif
+        if constexpr (SKML_DEC_INTMOD)
+            rel[j] = i0 + j < n ? (uint32_t)(row0 + dv(java_hash_mix(ID, key[j]))) : ~0u;
+        else
+            rel[j] = i0 + j < n ? (uint32_t)(row0 + java_hash_fm(ID, key[j], cols, inv)) : ~0u;
+    }
 }
 
 // |v - zero| with Java int wrap (MinMaxSketch.compare, MinMaxSketch.java:80-86)
@@ -2525,6 +2538,8 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_keys(const uint32_t* __rest
         const int64_t tb = gp->tab_off[g0];
         const int32_t cols = gp->cols[g0];
         const double inv = gp->inv_cols[g0];
+        const DivU32 dvc = divu32_make((uint32_t)cols);
+        const auto dv = [&](uint32_t h) { return java_mod((int32_t)h, cols, dvc); };
         const TN* tnb = tnar + tb;
         const int32_t* t32b = table + tb;
         uint32_t rel[2][4];
@@ -2534,14 +2549,14 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_keys(const uint32_t* __rest
             const int id = __builtin_amdgcn_readfirstlane(gp->hash_ids[g0][r]);
             const int64_t row0 = (int64_t)r * cols;
             switch (id) {
-                case 0: dec_row_cells<0>(key, i0, n, row0, cols, inv, rel[r]); break;
-                case 1: dec_row_cells<1>(key, i0, n, row0, cols, inv, rel[r]); break;
-                case 2: dec_row_cells<2>(key, i0, n, row0, cols, inv, rel[r]); break;
-                case 3: dec_row_cells<3>(key, i0, n, row0, cols, inv, rel[r]); break;
-                case 4: dec_row_cells<4>(key, i0, n, row0, cols, inv, rel[r]); break;
-                case 5: dec_row_cells<5>(key, i0, n, row0, cols, inv, rel[r]); break;
-                case 6: dec_row_cells<6>(key, i0, n, row0, cols, inv, rel[r]); break;
-                default: dec_row_cells<7>(key, i0, n, row0, cols, inv, rel[r]); break;
+                case 0: dec_row_cells<0>(key, i0, n, row0, cols, inv, dv, rel[r]); break;
+                case 1: dec_row_cells<1>(key, i0, n, row0, cols, inv, dv, rel[r]); break;
+                case 2: dec_row_cells<2>(key, i0, n, row0, cols, inv, dv, rel[r]); break;
+                case 3: dec_row_cells<3>(key, i0, n, row0, cols, inv, dv, rel[r]); break;
+                case 4: dec_row_cells<4>(key, i0, n, row0, cols, inv, dv, rel[r]); break;
+                case 5: dec_row_cells<5>(key, i0, n, row0, cols, inv, dv, rel[r]); break;
+                case 6: dec_row_cells<6>(key, i0, n, row0, cols, inv, dv, rel[r]); break;
+                default: dec_row_cells<7>(key, i0, n, row0, cols, inv, dv, rel[r]); break;
             }
 #pragma unroll
             for (int j = 0; j < 4; j++) {
@@ -3196,6 +3211,184 @@ __global__ __launch_bounds__(kAggThreads) __attribute__((amdgpu_waves_per_eu(4))
     if (bad) atomicOr(err, bad);
 }
 
+// The staged tiles with the next tile's element loads in flight while this tile is staged and
+// summed (software pipelined: run bounds two tiles ahead, elements one tile ahead, the piece tables
+// double-buffered in LDS).  Same sums as k_agg_vtiles<1>.
+__global__ __launch_bounds__(kAggThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_agg_vtiles_pf(
+    const AggPayload* __restrict__ pays, int P, int64_t ntiles, int64_t dim, double* __restrict__ out, int from_out,
+    double scale, unsigned* __restrict__ err, const int32_t* __restrict__ kbase, const uint8_t* __restrict__ bbase) {
+    constexpr int kWaves = kAggThreads / 64;
+    __shared__ __attribute__((aligned(16))) uint8_t bins[kWaves][kAggPB][kAggVTile];
+    __shared__ uint32_t here[kWaves][kAggPB][kAggVTile / 32];
+    __shared__ double qt[kAggPB][kAggLdsValues];
+    __shared__ int32_t pre[2][kWaves][65];
+    __shared__ int32_t pk0[2][kWaves][64];
+    __shared__ int32_t pn0[2][kWaves][64];
+    __shared__ AggPayload pl[kAggPB];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (threadIdx.x < P * (int)(sizeof(AggPayload) / 8))
+        reinterpret_cast<uint64_t*>(pl)[threadIdx.x] = reinterpret_cast<const uint64_t*>(pays)[threadIdx.x];
+    __syncthreads();
+    if (wave < P)
+        for (int b = lane; b < pl[wave].nq; b += 64) qt[wave][b] = gload<double>(pl[wave].qv, b);
+    __syncthreads();
+    const int pl_l = lane >> 3, g_l = lane & 7;
+    const bool lane_on = pl_l < P && g_l < pl[pl_l].G;
+    const int32_t* bd = lane_on ? pl[pl_l].bounds + (int64_t)g_l * (ntiles + 1) : nullptr;
+    const int32_t gk_off = lane_on ? pl[pl_l].gk_off : 0, gb_off = lane_on ? pl[pl_l].gb_off : 0;
+    uint8_t(*B)[kAggVTile] = bins[wave];
+    uint32_t(*H)[kAggVTile / 32] = here[wave];
+    unsigned bad = 0;
+    int32_t nb0 = 0, nb1 = 0;
+    auto fetch = [&](int64_t tt) {
+        if (lane_on && tt < ntiles) {
+            nb0 = gload<int32_t>(bd, tt);
+            nb1 = gload<int32_t>(bd, tt + 1);
+        }
+    };
+    // a tile's piece tables into buffer `buf`; returns its element count
+    auto plan = [&](int buf, int32_t b0, int32_t b1, int ln) -> int {
+        const int32_t len = lane_on && b1 > b0 ? b1 - b0 : 0;
+        const int32_t x = (int32_t)wave_incl_scan_u32((uint32_t)len);
+        pre[buf][wave][ln + 1] = x;
+        if (ln == 0) pre[buf][wave][0] = 0;
+        pk0[buf][wave][ln] = gk_off + b0;
+        pn0[buf][wave][ln] = gb_off + b0;
+        __builtin_amdgcn_wave_barrier();
+        return __builtin_amdgcn_readlane(x, 63);
+    };
+    auto piece_of = [&](int buf, int j) -> int {  // largest s < 64 with pre[s] <= j
+        int s_ = 0;
+#pragma unroll
+        for (int step = 32; step >= 1; step >>= 1)
+            if (pre[buf][wave][s_ + step] <= j) s_ += step;
+        return s_;
+    };
+    auto load = [&](int buf, int total, int ln, int32_t (&kk)[kAggWPer], uint32_t (&bb)[kAggWPer]) {
+        int spc[kAggWPer];
+#pragma unroll
+        for (int u = 0; u < kAggWPer; u++) {
+            const int j = ln + 64 * u;
+            spc[u] = piece_of(buf, j < total ? j : 0);
+        }
+#pragma unroll
+        for (int u = 0; u < kAggWPer; u++) {
+            const int j = ln + 64 * u;
+            kk[u] = INT32_MIN;
+            bb[u] = 0;
+            if (j < total) {
+                const int sp = spc[u], d = j - pre[buf][wave][sp];
+                kk[u] = gload<int32_t>(kbase, (uint32_t)(pk0[buf][wave][sp] + d));
+                bb[u] = gload<uint8_t>(bbase, (uint32_t)(pn0[buf][wave][sp] + d)) | ((uint32_t)(sp >> 3) << 8);
+            }
+        }
+    };
+    int64_t prev_k0 = -1, prev_nk = 0;
+    double* T = reinterpret_cast<double*>(&B[0][0]);
+    auto store_prev = [&](int l) {
+        if (prev_k0 < 0) return;
+        double* o = out + prev_k0;
+        const bool whole = prev_nk == kAggVTile && (reinterpret_cast<uintptr_t>(o) & 15) == 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int x = 128 * q + 2 * l;
+            const double2 v = *reinterpret_cast<const double2*>(T + x);
+            if (whole) {
+                *reinterpret_cast<double2*>(o + x) = v;
+            } else {
+                if (x < prev_nk) o[x] = v.x;
+                if (x + 1 < prev_nk) o[x + 1] = v.y;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        prev_k0 = -1;
+    };
+    const TileWalk tw = tile_walk(blockIdx.x, gridDim.x, wave, kWaves, ntiles);
+    int buf = 0, total = 0;
+    int32_t kk[kAggWPer], kn[kAggWPer];
+    uint32_t bb[kAggWPer], bn[kAggWPer];
+    if (tw.t0 < tw.t1) {
+        fetch(tw.t0);
+        total = plan(0, nb0, nb1, lane);
+        load(0, total, lane, kk, bb);
+        fetch(tw.t0 + tw.step);
+    }
+    for (int64_t t = tw.t0; t < tw.t1; t += tw.step) {
+        int ln = lane;  // lane-derived values rematerialised per tile (hoisted, they spill)
+        asm volatile("" : "+v"(ln));
+        const int64_t k0 = t << kAggVBits, nk = std::min<int64_t>(kAggVTile, dim - k0);
+        // the next tile: its piece tables and its element loads, in flight while this one is summed
+        int total_n = 0;
+        const bool more = t + tw.step < tw.t1;
+        if (more) {
+            total_n = plan(buf ^ 1, nb0, nb1, ln);
+            load(buf ^ 1, total_n, ln, kn, bn);
+            fetch(t + 2 * tw.step);
+        }
+        store_prev(ln);
+        reinterpret_cast<uint64_t*>(H)[ln] = 0;
+        __builtin_amdgcn_wave_barrier();
+        auto stage = [&](int p, int32_t k, uint32_t b) {
+            if (k < k0 || (int64_t)k >= k0 + nk) {  // k_agg_bounds placed it here: an error
+                bad |= 1u;
+                return;
+            }
+            const int xk = (int)(k - k0);
+            B[p][xk] = (uint8_t)b;
+            const uint32_t bit = 1u << (xk & 31);
+            if (atomicOr(&H[p][xk >> 5], bit) & bit) bad |= 2u;  // a key twice in one payload
+        };
+#pragma unroll
+        for (int u = 0; u < kAggWPer; u++)
+            if (ln + 64 * u < total) stage((int)(bb[u] >> 8), kk[u], bb[u] & 0xFFu);
+        for (int j = 64 * kAggWPer + ln; j < total; j += 64) {  // elements past the registers
+            const int sp = piece_of(buf, j), d = j - pre[buf][wave][sp];
+            stage(sp >> 3, gload<int32_t>(kbase, (uint32_t)(pk0[buf][wave][sp] + d)),
+                  gload<uint8_t>(bbase, (uint32_t)(pn0[buf][wave][sp] + d)));
+        }
+        __builtin_amdgcn_wave_barrier();
+        double acc[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) acc[i] = from_out && 8 * ln + i < nk ? out[k0 + 8 * ln + i] : 0.0;
+        for (int p = 0; p < P; p++) {
+            const uint32_t m = reinterpret_cast<const uint8_t*>(H[p])[ln];
+            const uint2 bw8 = *reinterpret_cast<const uint2*>(&B[p][8 * ln]);
+            const bool dform = pl[p].dense_form != 0;
+            double v[8];
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const uint32_t b = ((i < 4 ? bw8.x : bw8.y) >> (8 * (i & 3))) & 0xFFu;
+                v[i] = 0.0;
+                if (m & (1u << i)) v[i] = qt[p][b];
+            }
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                if ((m & (1u << i)) && (!dform || fabs(v[i]) > 1e-8)) acc[i] += v[i];
+                if (dform && __double_as_longlong(acc[i]) == (long long)0x8000000000000000ull) acc[i] = 0.0;
+            }
+        }
+        if (scale != 1.0)
+#pragma unroll
+            for (int i = 0; i < 8; i++) acc[i] = __dmul_rn(acc[i], scale);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            *reinterpret_cast<double2*>(T + 8 * ln + 2 * q) = make_double2(acc[2 * q], acc[2 * q + 1]);
+        __builtin_amdgcn_wave_barrier();
+        prev_k0 = k0;
+        prev_nk = nk;
+        buf ^= 1;
+        total = total_n;
+#pragma unroll
+        for (int u = 0; u < kAggWPer; u++) {
+            kk[u] = kn[u];
+            bb[u] = bn[u];
+        }
+    }
+    store_prev(lane);
+    if (bad) atomicOr(err, bad);
+}
+
 // The staged wave-tile form is the default for payloads of at most 8 groups and 256 quantValues
 // (the caller launches it 8 payloads at a time); the wave-per-payload tiles take every other shape
 // (SKML_FORM_AGG_TILES forces them for tests).
@@ -3229,6 +3422,14 @@ hipError_t launch_agg_tiles(hipStream_t st, const AggPayload* pays, int P, int64
             const int64_t all = sp_tiles(sp_tiles(ntiles, 4), kAggThreads / 64);
             const unsigned grid = (unsigned)(resident4 <= 0 ? all : std::min<int64_t>(all, resident4));
             hipLaunchKernelGGL(k_agg_vtiles<4>, dim3(grid), dim3(kAggThreads), 0, st, pays, P, ntiles, dim, out,
+                               from_out, scale, err, kbase, bbase);
+            return hipGetLastError();
+        }
+        if (form(SKML_FORM_AGG_TILES) == 4) {
+            static const int resident_pf = resident_workgroups(k_agg_vtiles_pf);
+            const int64_t all = sp_tiles(ntiles, kAggThreads / 64);
+            const unsigned grid = (unsigned)(resident_pf <= 0 ? all : std::min<int64_t>(all, resident_pf));
+            hipLaunchKernelGGL(k_agg_vtiles_pf, dim3(grid), dim3(kAggThreads), 0, st, pays, P, ntiles, dim, out,
                                from_out, scale, err, kbase, bbase);
             return hipGetLastError();
         }

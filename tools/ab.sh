@@ -4,7 +4,8 @@
 # KIND: dense  -> bench.py encode only (--steps 100, no extras)
 #       sparse -> tools/bench_sparse.py --reps 10 --aggregate 8 (8 distinct C3 payloads)
 #       dsum   -> tools/bench_decode_sum.py
-#       gap    -> tools/leaf_gap.py --steps 20 --reps 2
+#       gap    -> tools/leaf_gap.py --steps 20 --reps 2 (gap26 / gap24: at 2^26 / 2^24 floats)
+#       restore -> tools/bench_sparse.py --only-decode (restore of one C3 payload)
 # VARIANT: name=SETTINGS, SETTINGS a comma list of
 #       lib:DIR          another in-tree build (SKML_LIB=sketchml_amd/DIR/libskml.so)
 #       form:NAME:VALUE  a skml_debug_form setting, applied by the tool (tools/forms.py)
@@ -20,6 +21,9 @@ case $KIND in
   sparse) CMD="python tools/bench_sparse.py --reps 10 --aggregate 8" ;;
   dsum)   CMD="python tools/bench_decode_sum.py" ;;
   gap)    CMD="python tools/leaf_gap.py --steps 20 --reps 2" ;;
+  gap26)  CMD="python tools/leaf_gap.py --steps 40 --reps 2 --n 67108864" ;;
+  gap24)  CMD="python tools/leaf_gap.py --steps 80 --reps 2 --n 16777216" ;;
+  restore) CMD="python tools/bench_sparse.py --reps 20 --only-decode" ;;
   *) echo "unknown kind $KIND"; exit 2 ;;
 esac
 for i in $(seq 1 "$REPS"); do

@@ -10,7 +10,7 @@ if kind == "dense":
     out = {"ms_per_step": d["ms_per_step"], "kernels_us": {k: v["avg_us"] for k, v in d["extras"]["kernels"].items()}}
 elif kind == "sparse":
     out = d["ms"]
-elif kind == "gap":
+elif kind in ("gap", "gap26", "gap24"):
     out = d.get("summary", d)
 else:
     out = d

@@ -31,6 +31,8 @@ def main():
                     help="also time Gradient.sum of this many payloads (skml_sparse_decode_sum_f64)")
     ap.add_argument("--only-e2e", action="store_true",
                     help="one warm-up and `reps` timed dense -> payload encodes only (the PMC passes' program)")
+    ap.add_argument("--only-decode", action="store_true",
+                    help="one encode, then one warm-up and `reps` timed restores (decompressSparse) only")
     a = ap.parse_args()
     import sketchml_amd as sk
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -51,6 +53,11 @@ def main():
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / reps, out
 
+    if a.only_decode:
+        pl0 = sk.encode_dense_as_sparse(x, 256, 8, 2, 0.3, 3, 3)
+        t_dec, _ = timed(lambda: pl0.restore(), a.reps)
+        print(json.dumps({"decode_ms": round(t_dec * 1e3, 3)}))
+        return
     if a.only_e2e:
         t_e2e, _ = timed(lambda: sk.encode_dense_as_sparse(x, 256, 8, 2, 0.3, 3, 3), a.reps)
         print(json.dumps({"dense_to_payload_ms": round(t_e2e * 1e3, 3)}))

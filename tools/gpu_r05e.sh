@@ -7,3 +7,6 @@ cat gpurun_out/r05e/leaf_waves.txt
 bash tools/ab.sh hybrid 3 gap normal=form:leaf_split:1 h25= h12=form:leaf_split:4 h50=form:leaf_split:5
 timeout -k 10 300 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_dense.py -k "leaf_forms or large or quantize_matches" > gpurun_out/r05e/tests.log 2>&1
 tail -3 gpurun_out/r05e/tests.log
+bash tools/ab.sh decq 2 sparse base= dm1=lib:lib_dm1 gat=lib:lib_abl hash=lib:lib_abl2
+SKML_LIB=sketchml_amd/lib_dm1/libskml.so timeout -k 10 300 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_sparse.py tests/test_gpu_sparse_full.py -k "restore or shapes or c3_full or edge or f64" > gpurun_out/r05e/dm1_tests.log 2>&1
+tail -2 gpurun_out/r05e/dm1_tests.log
