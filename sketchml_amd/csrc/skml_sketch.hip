@@ -1021,8 +1021,12 @@ __global__ __launch_bounds__(512, MINW) void k_leaf(const float* __restrict__ x,
 // hybrid MODE 2), so the last wave generation runs in quarter-size units.  Returns the first
 // split tile (0: all split, full: none).  SKML_FORM_LEAF_SPLIT forces a form (tests, A/B):
 // 1 none, 2 all, 3 / 4 / 5 the last 25 / 12.5 / 50 % of the tiles.
+// The split leaf runs every size by default: at 2^28 it takes 326 us against 342 us for one wave
+// per tile (the tail: wave-slot use 0.80 over the span, profiles/r05e_leaf_waves_normal_form.txt),
+// at 2^26 the two are level (0.1618 / 0.1625 ms per encode), at 2^24 it is faster (0.069 / 0.079),
+// and the hybrid tails measured between (profiles/ab/r05_split*.txt, r05_hybrid.txt).
 #ifndef SKML_LEAF_SPLIT_TAIL_PCT
-#define SKML_LEAF_SPLIT_TAIL_PCT 25
+#define SKML_LEAF_SPLIT_TAIL_PCT 100
 #endif
 static int64_t leaf_split_from(int64_t full_tiles) {
     auto tail = [&](int pct_x2) {  // the first split tile for the last pct_x2 / 2 % of the tiles
@@ -1037,8 +1041,12 @@ static int64_t leaf_split_from(int64_t full_tiles) {
         case 5: return tail(100);
         default: break;
     }
+#if SKML_LEAF_SPLIT_TAIL_PCT >= 100
+    return 0;
+#else
     if (full_tiles < SKML_LEAF_SPLIT_BELOW) return 0;
     return tail(2 * SKML_LEAF_SPLIT_TAIL_PCT);
+#endif
 }
 
 hipError_t launch_leaf(hipStream_t st, const float* x, int64_t chunks, uint64_t s0,

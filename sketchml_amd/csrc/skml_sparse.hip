@@ -3416,7 +3416,9 @@ hipError_t launch_agg_tiles(hipStream_t st, const AggPayload* pays, int P, int64
     if (ntiles <= 0) return hipSuccess;
     if (vtiles) {
         if (P < 1 || P > kAggVPayloads) return hipErrorInvalidValue;  // one lane per (payload, group)
-        // SKML_FORM_AGG_TILES = 2 / 3: four / two tiles per wave round (A/B forms)
+        // the default: the prefetching form (5.57-5.64 against 5.63-5.66 ms for 8 C3 payloads,
+        // profiles/ab/r05_pf.txt); SKML_FORM_AGG_TILES = 5 / 2 / 3: the plain staged tiles, four /
+        // two tiles per wave round (A/B forms)
         if (form(SKML_FORM_AGG_TILES) == 2) {
             static const int resident4 = resident_workgroups(k_agg_vtiles<4>);
             const int64_t all = sp_tiles(sp_tiles(ntiles, 4), kAggThreads / 64);
@@ -3425,7 +3427,7 @@ hipError_t launch_agg_tiles(hipStream_t st, const AggPayload* pays, int P, int64
                                from_out, scale, err, kbase, bbase);
             return hipGetLastError();
         }
-        if (form(SKML_FORM_AGG_TILES) == 4) {
+        if (form(SKML_FORM_AGG_TILES) == 0 || form(SKML_FORM_AGG_TILES) == 4) {
             static const int resident_pf = resident_workgroups(k_agg_vtiles_pf);
             const int64_t all = sp_tiles(ntiles, kAggThreads / 64);
             const unsigned grid = (unsigned)(resident_pf <= 0 ? all : std::min<int64_t>(all, resident_pf));

@@ -94,14 +94,15 @@ def test_corrupt_blobs_are_refused(gpu):
         gpu.decode_sum(blob, 1, blob.numel(), 1000)
 
 
-# Gradient.sum's tile kernels: vtile (default for payloads of <= 8 groups and <= 256 quantValues:
+# Gradient.sum's tile kernels: vtile_pf (the default for payloads of <= 8 groups and <= 256
+# quantValues: vtile with the next tile's element loads in flight), vtile (
 # one wave per 512-key tile stages every payload's bins with presence bits and sums each key in
 # registers, payload after payload, 8 payloads per launch; restores on two streams), wave
 # (SKML_FORM_AGG_TILES: one wave per payload adding into a 4,096-key LDS tile, the form for any
 # other shape) and wave_serial (the wave tiles with the generic per-row MinMax query and one
 # stream); vtile2 / vtile4 take two / four staged tiles per wave round (one round of element
 # loads); vtile_pf loads the next tile's elements while a tile is summed.  Every form is exact, and every form refuses a key repeated across a payload's groups.
-KERNELS = {"vtile": {}, "vtile2": {"agg_tiles": 3}, "vtile4": {"agg_tiles": 2}, "vtile_pf": {"agg_tiles": 4},
+KERNELS = {"vtile_pf": {}, "vtile": {"agg_tiles": 5}, "vtile2": {"agg_tiles": 3}, "vtile4": {"agg_tiles": 2},
            "wave": {"agg_tiles": 1},
            "wave_serial": {"agg_tiles": 1, "dec_rows_serial": 1, "agg_one_lane": 1}}
 
@@ -306,7 +307,7 @@ def test_decode_sum_eight_distinct_c3_payloads_full_size(gpu):
     want, forms = O.gradient_sum(restored, dim, 1.0 / P)
     del restored
     assert forms == ["sparse"] * P
-    for form in (0, 4, 3, 2, 1):                         # staged tiles (1, prefetching, 2, 4 per round), 4,096-key tiles
+    for form in (0, 5, 3, 2, 1):                         # staged tiles (prefetching, 1, 2, 4 per round), 4,096-key tiles
         with _lib.forced_forms(agg_tiles=form):
             got = gpu.decode_sum(allb, P, stride, dim, 1.0 / P)
             torch.cuda.synchronize()
