@@ -2457,46 +2457,24 @@ struct DecEdgeTiles {
 // table the gathers read.
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 typedef int32_t i32x4_t __attribute__((ext_vector_type(4)));
-template <typename TN, int MODE, bool NT = false>
-__global__ __launch_bounds__(kDecThreads) void k_dec_keys(const uint32_t* __restrict__ delta, int64_t n,
-                                                          const SpGroups* __restrict__ gp,
-                                                          const uint64_t* __restrict__ tile_base,
-                                                          const uint64_t* __restrict__ gpre,
-                                                          const int32_t* __restrict__ table, const TN* __restrict__ tnar,
-                                                          int32_t* __restrict__ gkeys, int32_t* __restrict__ gbins,
-                                                          int nq, void* __restrict__ gbn, int bn_width,
-                                                          unsigned* __restrict__ err, DecEdgeTiles edges) {
-    __shared__ int64_t S[kMaxGroups + 1];
-    __shared__ uint64_t sh[kDecThreads / 64];
-    load_starts(gp, S);
-    __syncthreads();
-    const int64_t tile = edges.n > 0 ? edges.t[blockIdx.x] : dec_tile_of_block(S, gp->G, blockIdx.x);
-    if (tile < 0) return;  // workgroup-uniform
-    if constexpr (MODE == 1) {
-        const int64_t tf = tile * kSpTile, tl = std::min<int64_t>(n, tf + kSpTile) - 1;
-        if (group_of_elem(S, tf) != group_of_elem(S, tl)) return;  // an edge tile: the MODE 0 launch
-    }
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+// One tile of k_dec_keys from its preloaded deltas `d` and base `tb` (tile_base[tile]).  sh: one
+// u64 per wave of LDS (the cross-wave prefix); a persistent caller alternates two of them.
+template <typename TN, int MODE, bool NT>
+__device__ __forceinline__ void dec_keys_tile(int64_t n, const SpGroups* __restrict__ gp,
+                                              const uint64_t* __restrict__ gpre, const int32_t* __restrict__ table,
+                                              const TN* __restrict__ tnar, int32_t* __restrict__ gkeys,
+                                              int32_t* __restrict__ gbins, int nq, void* __restrict__ gbn,
+                                              int bn_width, unsigned* __restrict__ err, const int64_t* S,
+                                              uint64_t* sh, int64_t tile, const uint32_t (&d)[4], uint64_t tb,
+                                              int tid) {
+    const int t = tid, lane = t & 63, w = t >> 6;
     const int64_t i0 = tile * kSpTile + t * 4;
-    uint32_t d[4];
-    if (i0 + 4 <= n) {
-        if constexpr (NT) {
-            const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(delta + i0));
-            d[0] = v.x, d[1] = v.y, d[2] = v.z, d[3] = v.w;
-        } else {
-            const uint4 v = *reinterpret_cast<const uint4*>(delta + i0);
-            d[0] = v.x, d[1] = v.y, d[2] = v.z, d[3] = v.w;
-        }
-    } else {
-#pragma unroll
-        for (int j = 0; j < 4; j++) d[j] = i0 + j < n ? delta[i0 + j] : 0u;
-    }
     // the tile's exclusive prefix of the deltas (64-bit: a tile's deltas may pass 2^32)
     const uint64_t own = (uint64_t)d[0] + d[1] + d[2] + d[3];
     const uint64_t inc = wave_incl_u64(own, lane);
     if (lane == 63) sh[w] = inc;
     __syncthreads();
-    uint64_t p = tile_base[tile] + inc - own;
+    uint64_t p = tb + inc - own;
 #pragma unroll
     for (int j = 0; j < kDecThreads / 64; j++) p += j < w ? sh[j] : 0ull;
     if (i0 >= n) return;
@@ -2652,6 +2630,121 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_keys(const uint32_t* __rest
     }
 }
 
+
+template <typename TN, int MODE, bool NT = false>
+__global__ __launch_bounds__(kDecThreads) void k_dec_keys(const uint32_t* __restrict__ delta, int64_t n,
+                                                          const SpGroups* __restrict__ gp,
+                                                          const uint64_t* __restrict__ tile_base,
+                                                          const uint64_t* __restrict__ gpre,
+                                                          const int32_t* __restrict__ table, const TN* __restrict__ tnar,
+                                                          int32_t* __restrict__ gkeys, int32_t* __restrict__ gbins,
+                                                          int nq, void* __restrict__ gbn, int bn_width,
+                                                          unsigned* __restrict__ err, DecEdgeTiles edges) {
+    __shared__ int64_t S[kMaxGroups + 1];
+    __shared__ uint64_t sh[kDecThreads / 64];
+    load_starts(gp, S);
+    __syncthreads();
+    const int64_t tile = edges.n > 0 ? edges.t[blockIdx.x] : dec_tile_of_block(S, gp->G, blockIdx.x);
+    if (tile < 0) return;  // workgroup-uniform
+    if constexpr (MODE == 1) {
+        const int64_t tf = tile * kSpTile, tl = std::min<int64_t>(n, tf + kSpTile) - 1;
+        if (group_of_elem(S, tf) != group_of_elem(S, tl)) return;  // an edge tile: the MODE 0 launch
+    }
+    const int t = threadIdx.x;
+    const int64_t i0 = tile * kSpTile + t * 4;
+    uint32_t d[4];
+    if (i0 + 4 <= n) {
+        if constexpr (NT) {
+            const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(delta + i0));
+            d[0] = v.x, d[1] = v.y, d[2] = v.z, d[3] = v.w;
+        } else {
+            const uint4 v = *reinterpret_cast<const uint4*>(delta + i0);
+            d[0] = v.x, d[1] = v.y, d[2] = v.z, d[3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; j++) d[j] = i0 + j < n ? delta[i0 + j] : 0u;
+    }
+    dec_keys_tile<TN, MODE, NT>(n, gp, gpre, table, tnar, gkeys, gbins, nq, gbn, bn_width, err, S, sh, tile, d,
+                                tile_base[tile], (int)threadIdx.x);
+}
+
+// MODE 1 over every inner tile with persistent workgroups: workgroup b walks the tiles that
+// dec_tile_of_block deals to its XCD slot (b % 8), and loads the next tile's deltas and base
+// while it hashes, gathers and stores the current one.  Same output as k_dec_keys<TN, 1, NT>.
+template <typename TN, bool NT>
+__global__ __launch_bounds__(kDecThreads) void k_dec_keys_p(const uint32_t* __restrict__ delta, int64_t n,
+                                                            const SpGroups* __restrict__ gp,
+                                                            const uint64_t* __restrict__ tile_base,
+                                                            const uint64_t* __restrict__ gpre,
+                                                            const int32_t* __restrict__ table,
+                                                            const TN* __restrict__ tnar, int32_t* __restrict__ gkeys,
+                                                            int32_t* __restrict__ gbins, int nq, void* __restrict__ gbn,
+                                                            int bn_width, unsigned* __restrict__ err, int64_t per_slot) {
+    __shared__ int64_t S[kMaxGroups + 1];
+    __shared__ uint64_t sh[2][kDecThreads / 64];
+    load_starts(gp, S);
+    __syncthreads();
+    const int64_t slot = blockIdx.x & 7, stride = gridDim.x >> 3;  // gridDim.x: a multiple of 8
+    // the j-th tile of this XCD slot's list (-1: past it); edge tiles are skipped (the MODE 0 launch)
+    auto tile_at = [&](int64_t j) -> int64_t {
+        while (j < per_slot) {
+            const int64_t tt = dec_tile_of_block(S, gp->G, j * 8 + slot);
+            if (tt < 0) return -1;
+            const int64_t tf = tt * kSpTile, tl = std::min<int64_t>(n, tf + kSpTile) - 1;
+            if (group_of_elem(S, tf) == group_of_elem(S, tl)) return tt;
+            j += stride;  // an edge tile: the next one of this workgroup's walk
+        }
+        return -1;
+    };
+    auto load = [&](int64_t tt, uint32_t (&d)[4], uint64_t& tb) {
+        const int64_t i0 = tt * kSpTile + threadIdx.x * 4;
+        if (i0 + 4 <= n) {
+            const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(delta + i0));
+            d[0] = v.x, d[1] = v.y, d[2] = v.z, d[3] = v.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; j++) d[j] = i0 + j < n ? delta[i0 + j] : 0u;
+        }
+        tb = tile_base[tt];
+    };
+    int64_t j = blockIdx.x >> 3;
+    int64_t tile = tile_at(j);
+    uint32_t d[4] = {0, 0, 0, 0}, dn[4] = {0, 0, 0, 0};
+    uint64_t tb = 0, tbn = 0;
+    if (tile >= 0) load(tile, d, tb);
+    int par = 0;
+    while (tile >= 0) {
+        j += stride;
+        const int64_t next = tile_at(j);
+        if (next >= 0) load(next, dn, tbn);  // in flight while this tile is decoded
+        int tid = threadIdx.x;  // thread-derived values rematerialised per tile (hoisted, they cost registers)
+        asm volatile("" : "+v"(tid));
+        dec_keys_tile<TN, 1, NT>(n, gp, gpre, table, tnar, gkeys, gbins, nq, gbn, bn_width, err, S, sh[par], tile, d,
+                                 tb, tid);
+        // (dec_keys_tile returns early past n, after its barrier; every thread of the workgroup
+        // still runs the same iterations)
+        tile = next;
+        par ^= 1;
+#pragma unroll
+        for (int q = 0; q < 4; q++) d[q] = dn[q];
+        tb = tbn;
+    }
+}
+
+// workgroups of `kern` (`threads` each) resident at once on the device; 0 if the query fails
+template <typename K>
+static int resident_blocks(K kern, int threads) {
+    int dev = 0, per_cu = 0;
+    hipDeviceProp_t prop;
+    int r = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, 0) == hipSuccess)
+        r = std::max(1, per_cu) * prop.multiProcessorCount;
+    (void)hipGetLastError();
+    return r;
+}
+
 hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, const SpGroups* gp, const SpGroups& gh,
                            const uint64_t* tile_base, const uint64_t* gpre, const int32_t* table, const void* tnar,
                            int width, int32_t* gkeys, int32_t* gbins, int nq, void* gbn, int bn_width,
@@ -2683,9 +2776,18 @@ hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, con
 #define SKML_DEC_LAUNCH(TNT, MODE, GRID, TILES, TNPTR)                                                            \
     hipLaunchKernelGGL((k_dec_keys<TNT, MODE>), dim3(GRID), dim3(kDecThreads), 0, st, delta, n, gp, tile_base, gpre, \
                        table, TNPTR, gkeys, gbins, nq, gbn, bn_width, err, TILES)
+    // MODE 1 with persistent workgroups (the next tile's deltas in flight) unless
+    // SKML_FORM_DEC_ROWS_SERIAL = 2 asks for one workgroup per tile
+    const bool persistent = form(SKML_FORM_DEC_ROWS_SERIAL) != 2;
 #define SKML_DEC_WIDTH(TNT, TNPTR)                                                          \
     do {                                                                                  \
-        if (batched) {                                                                    \
+        if (batched && persistent) {                                                      \
+            static const int res = resident_blocks(k_dec_keys_p<TNT, true>, kDecThreads); \
+            const int64_t ps = res > 0 ? std::max<int64_t>(1, std::min<int64_t>(most, res / 8)) : most; \
+            hipLaunchKernelGGL((k_dec_keys_p<TNT, true>), dim3((unsigned)(8 * ps)), dim3(kDecThreads), 0, st, delta, \
+                               n, gp, tile_base, gpre, table, TNPTR, gkeys, gbins, nq, gbn, bn_width, err, most); \
+            if (edges.n > 0) SKML_DEC_LAUNCH(TNT, 0, (unsigned)edges.n, edges, TNPTR);    \
+        } else if (batched) {                                                             \
             hipLaunchKernelGGL((k_dec_keys<TNT, 1, true>), dim3(grid), dim3(kDecThreads), 0, st, delta, n, gp,    \
                                tile_base, gpre, table, TNPTR, gkeys, gbins, nq, gbn, bn_width, err, all);    \
             if (edges.n > 0) SKML_DEC_LAUNCH(TNT, 0, (unsigned)edges.n, edges, TNPTR);    \
@@ -3782,6 +3884,167 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_merge(const int32_t* __restri
     if (bad) atomicOr(&info->irregular, 2u);
 }
 
+// Sort.merge in one pass, software pipelined: while range t is marked, scanned and emitted, the
+// element loads of the workgroup's next range are in flight (its piece table computed one range
+// ahead into the other half of a double buffer, its run bounds fetched two ranges ahead).  Same
+// output and the same irregular-input flags as k_rs_merge.
+template <typename V>
+__global__ __launch_bounds__(kRsThreads) void k_rs_merge_pf(const int32_t* __restrict__ gk,
+                                                            const int32_t* __restrict__ gb,
+                                                            const SpGroups* __restrict__ gp,
+                                                            const int32_t* __restrict__ bounds,
+                                                            RsInfo* __restrict__ info, int32_t* __restrict__ keys_out,
+                                                            V* __restrict__ out, const double* __restrict__ qv, int nq) {
+    constexpr int kLut = std::is_same<V, int32_t>::value ? 1 : kRsLut;
+    __shared__ uint32_t bm[kRsWords];
+    __shared__ int32_t slot[kRsRange];
+    __shared__ int64_t S[kMaxGroups + 1];
+    __shared__ int64_t lo_s[3][kMaxGroups];
+    __shared__ int32_t pre[3][kMaxGroups + 1];
+    __shared__ int64_t obase[3];
+    __shared__ uint32_t wsum[kRsThreads / 64];
+    __shared__ V lut[kLut];
+    if (info->irregular) return;  // workgroup-uniform: the merge rounds run instead
+    const int tmax = info->tmax1 - 1;
+    const int G = gp->G, t_ = threadIdx.x, lane = t_ & 63, w = t_ >> 6;
+    load_starts(gp, S);
+    const bool lds = !std::is_same<V, int32_t>::value && nq <= kLut;
+    if (lds)
+        for (int b = t_; b < nq; b += kRsThreads) lut[b] = (V)qv[b];
+    constexpr int64_t ld = kRsRanges + 1;
+    unsigned bad = 0;
+    const int tl = (w == 0 && lane < G) ? info->tlast1[lane] - 1 : -1;  // -1: an empty run
+    int32_t nlo = 0, nhi = 0;
+    auto fetch = [&](int64_t tt) {
+        if (tl >= 0 && tt <= tl) {
+            nlo = bounds[(int64_t)lane * ld + tt];
+            nhi = bounds[(int64_t)lane * ld + tt + 1];
+        }
+    };
+    // wave 0: range tt's run pieces into buffer b (lane g < G: run g), from bounds (clo, chi)
+    auto plan = [&](int b, int64_t tt, int32_t clo, int32_t chi) {
+        int64_t lo = 0, len = 0, before = 0;
+        if (lane < G) {
+            const int64_t s0 = S[lane], s1 = S[lane + 1];
+            lo = s1;
+            int64_t hi = s1;
+            if (tl >= 0 && tt <= tl) {
+                lo = clo;
+                hi = chi;
+            }
+            before = lo - s0;
+            len = hi - lo;
+            lo_s[b][lane] = lo;
+        }
+        int64_t x = len;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int64_t y = __shfl_up(x, off, 64);
+            if (lane >= off) x += y;
+        }
+        if (lane < kMaxGroups) pre[b][lane + 1] = (int32_t)x;
+        if (lane == 0) pre[b][0] = 0;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) before += __shfl_xor(before, off, 64);
+        if (lane == 0) obase[b] = before;
+    };
+    auto run_of = [&](int b, int j) -> int {
+        if (G <= 8) {
+            int g = 0;
+#pragma unroll
+            for (int q = 0; q < 8; q++) g += (q + 1 <= G && pre[b][q + 1] <= j) ? 1 : 0;
+            return g;
+        }
+        return agg_search32(pre[b], G, j);
+    };
+    auto load = [&](int b, int32_t (&kk)[kRsBatch], int32_t (&bb)[kRsBatch]) {
+        const int cnt = pre[b][G];
+#pragma unroll
+        for (int u = 0; u < kRsBatch; u++) {
+            const int j = u * kRsThreads + t_;
+            kk[u] = -1;
+            bb[u] = 0;
+            if (j < cnt) {
+                const int g = run_of(b, j);
+                const int64_t i = lo_s[b][g] + (j - pre[b][g]);
+                kk[u] = gk[i];
+                bb[u] = gb[i];
+            }
+        }
+    };
+    int32_t kc[kRsBatch], bc[kRsBatch], kn[kRsBatch], bn[kRsBatch];
+    int buf = 0;
+    const int64_t t0 = blockIdx.x;
+    if (t0 <= tmax) {
+        if (w == 0) {
+            fetch(t0);
+            plan(0, t0, nlo, nhi);
+            fetch(t0 + gridDim.x);
+        }
+        __syncthreads();
+        load(0, kc, bc);
+    }
+    for (int64_t t = t0; t <= tmax; t += gridDim.x) {
+        const bool more = t + gridDim.x <= tmax;
+        const int nbuf = buf == 2 ? 0 : buf + 1;
+        if (w == 0 && more) {  // the next range's piece table, from the bounds fetched one range ago
+            plan(nbuf, t + gridDim.x, nlo, nhi);
+            fetch(t + 2 * (int64_t)gridDim.x);
+        }
+        bm[t_] = 0;
+        __syncthreads();  // bm zeroed, the next plan visible, the previous emit done with bm / slot
+        if (more) load(nbuf, kn, bn);  // in flight while this range is marked and emitted
+        const int cnt = pre[buf][G];
+        // pass 1: this range's keys into the bitmap, their bins into the offset slots
+#pragma unroll
+        for (int u = 0; u < kRsBatch; u++) {
+            if (kc[u] < 0) continue;
+            const uint32_t off = (uint32_t)kc[u] & (kRsRange - 1), bit = 1u << (off & 31);
+            if (atomicOr(&bm[off >> 5], bit) & bit) bad = 1;  // a repeated key
+            slot[off] = bc[u];
+        }
+        for (int j = kRsThreads * kRsBatch + t_; j < cnt; j += kRsThreads) {  // past the registers
+            const int g = run_of(buf, j);
+            const int64_t i = lo_s[buf][g] + (j - pre[buf][g]);
+            const int32_t k = gk[i];
+            const uint32_t off = (uint32_t)k & (kRsRange - 1), bit = 1u << (off & 31);
+            if (atomicOr(&bm[off >> 5], bit) & bit) bad = 1;
+            slot[off] = gb[i];
+        }
+        __syncthreads();
+        if (cnt > 0) {  // workgroup-uniform
+            // pass 2: thread t_ owns bitmap word t_: its set bits go out in key order from its
+            // exclusive popcount prefix
+            const uint32_t word = bm[t_];
+            const uint32_t own = __popc(word);
+            uint32_t inc = own;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t y = __shfl_up(inc, off, 64);
+                if (lane >= off) inc += y;
+            }
+            if (lane == 63) wsum[w] = inc;
+            __syncthreads();
+            uint32_t run = inc - own;
+            for (int q = 0; q < w; q++) run += wsum[q];
+            int64_t o = obase[buf] + run;
+            const int32_t kbase = (int32_t)(t * kRsRange) + 32 * t_;
+            for (uint32_t m = word; m; m &= m - 1, o++) {
+                const int b = __ffs(m) - 1;
+                keys_out[o] = kbase + b;
+                out[o] = rs_value<V>(slot[32 * t_ + b], lut, qv, nq, lds, bad);
+            }
+        }
+        buf = nbuf;
+#pragma unroll
+        for (int u = 0; u < kRsBatch; u++) {
+            kc[u] = kn[u];
+            bc[u] = bn[u];
+        }
+    }
+    if (bad) atomicOr(&info->irregular, 2u);
+}
+
 hipError_t launch_rs_merge(hipStream_t st, const int32_t* gk, const int32_t* gb, int64_t n, const SpGroups* gp,
                            int32_t* bounds, RsInfo* info, int32_t* keys_out, void* out, int vkind, const double* qv,
                            int nq) {
@@ -3793,15 +4056,22 @@ hipError_t launch_rs_merge(hipStream_t st, const int32_t* gk, const int32_t* gb,
     // persistent workgroups over the key ranges up to the largest key (read on the device): as many
     // as are resident at once (4 per CU), fewer for small inputs
     const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(sp_tiles(n, 4096), 1), 1024);
-    if (vkind == 0)
-        hipLaunchKernelGGL(k_rs_merge<int32_t>, dim3(grid), dim3(kRsThreads), 0, st, gk, gb, gp, bounds, info, keys_out,
-                           static_cast<int32_t*>(out), qv, nq);
-    else if (vkind == 1)
-        hipLaunchKernelGGL(k_rs_merge<float>, dim3(grid), dim3(kRsThreads), 0, st, gk, gb, gp, bounds, info, keys_out,
-                           static_cast<float*>(out), qv, nq);
-    else
-        hipLaunchKernelGGL(k_rs_merge<double>, dim3(grid), dim3(kRsThreads), 0, st, gk, gb, gp, bounds, info, keys_out,
-                           static_cast<double*>(out), qv, nq);
+    // the pipelined form unless SKML_FORM_RS_ROUNDS = 2 asks for the plain one-pass kernel
+#define SKML_RS_LAUNCH(K)                                                                                         \
+    do {                                                                                                          \
+        if (vkind == 0)                                                                                           \
+            hipLaunchKernelGGL(K<int32_t>, dim3(grid), dim3(kRsThreads), 0, st, gk, gb, gp, bounds, info, keys_out, \
+                               static_cast<int32_t*>(out), qv, nq);                                              \
+        else if (vkind == 1)                                                                                      \
+            hipLaunchKernelGGL(K<float>, dim3(grid), dim3(kRsThreads), 0, st, gk, gb, gp, bounds, info, keys_out,  \
+                               static_cast<float*>(out), qv, nq);                                                \
+        else                                                                                                      \
+            hipLaunchKernelGGL(K<double>, dim3(grid), dim3(kRsThreads), 0, st, gk, gb, gp, bounds, info, keys_out, \
+                               static_cast<double*>(out), qv, nq);                                               \
+    } while (0)
+    if (form(SKML_FORM_RS_ROUNDS) == 2) SKML_RS_LAUNCH(k_rs_merge);
+    else SKML_RS_LAUNCH(k_rs_merge_pf);
+#undef SKML_RS_LAUNCH
     return hipGetLastError();
 }
 

@@ -76,15 +76,17 @@ def test_sparse_edge_values(gpu, kind):
     _check_sparse(gpu, keys, vals, seed=5, hash_seed=1)
 
 
-@pytest.fixture(params=["one_pass", "rounds"])
+@pytest.fixture(params=["one_pass", "one_pass_plain", "rounds"])
 def merge_form(request):
-    """restore both ways.  one_pass (the default): tiles of one group through the compile-time-hash
+    """restore three ways.  one_pass (the default): tiles of one group through the compile-time-hash
     query (k_dec_keys MODE 1) and the edge tiles through the generic one, Sort.merge as the
-    one-pass key-range merge.  rounds: the round-3 forms forced through skml_debug_form (one
-    generic query per row for every tile, the pairwise merge rounds, which are also the fallback
-    for irregular input)."""
+    one-pass key-range merge with the next range's loads in flight.  one_pass_plain: the same merge
+    without that prefetch.  rounds: the round-3 forms forced through skml_debug_form (one generic
+    query per row for every tile, the pairwise merge rounds, which are also the fallback for
+    irregular input)."""
     from sketchml_amd import _lib
-    forms = {"rs_rounds": 1, "dec_rows_serial": 1} if request.param == "rounds" else {}
+    forms = {"rs_rounds": 1, "dec_rows_serial": 1} if request.param == "rounds" else \
+        {"rs_rounds": 2} if request.param == "one_pass_plain" else {}
     with _lib.forced_forms(**forms):
         yield request.param
 
@@ -113,7 +115,7 @@ def test_sparse_shapes(gpu, groups, rows, ratio, bins, merge_form):
     """Odd group counts leave an unpaired run in restore's Sort.merge rounds."""
     keys, vals = _sparse_data(120000, 0.15, groups * 100 + rows, "normal")
     _check_sparse(gpu, keys, vals, bins, groups, rows, ratio, seed=7, hash_seed=groups)
-    assert _merge_path() == (1 if merge_form == "one_pass" else 2)
+    assert _merge_path() == (2 if merge_form == "rounds" else 1)
 
 
 @pytest.mark.parametrize("groups", [7, 8])
@@ -123,7 +125,7 @@ def test_sparse_restore_many_merge_tiles(gpu, groups, merge_form):
     covers 257 key ranges of 8,192 keys, ~2.5 K keys each."""
     keys, vals = _sparse_data(2**21 + 3, 0.3, 40 + groups, "normal")
     _check_sparse(gpu, keys, vals, 256, groups, 2, 0.3, seed=11, hash_seed=groups)
-    assert _merge_path() == (1 if merge_form == "one_pass" else 2)
+    assert _merge_path() == (2 if merge_form == "rounds" else 1)
 
 
 @pytest.mark.parametrize("layout", ["range_edges", "full_ranges", "far_apart", "int_max"])
@@ -195,11 +197,11 @@ def test_sparse_duplicate_keys_across_groups_are_kept(gpu, merge_form):
     keys = np.array([5, 9, 9, 12, 40, 41], dtype=np.int32)
     vals = np.array([0.5, -1, 2, 0.25, -0.5, 1], dtype=np.float32)
     pl, osp = _check_sparse(gpu, keys, vals, 4, 2, 1, 0.5, 1, 1)
-    assert _merge_path() == (3 if merge_form == "one_pass" else 2)
+    assert _merge_path() == (2 if merge_form == "rounds" else 3)
     rk, rb = pl.restore_bins()
     ok, ob = osp.restore()
     assert np.array_equal(rk.cpu().numpy(), ok) and np.array_equal(rb.cpu().numpy(), ob)
-    assert _merge_path() == (3 if merge_form == "one_pass" else 2)
+    assert _merge_path() == (2 if merge_form == "rounds" else 3)
 
 
 def test_sparse_length_mismatch(gpu):
