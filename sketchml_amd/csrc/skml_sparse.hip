@@ -2776,9 +2776,10 @@ hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, con
 #define SKML_DEC_LAUNCH(TNT, MODE, GRID, TILES, TNPTR)                                                            \
     hipLaunchKernelGGL((k_dec_keys<TNT, MODE>), dim3(GRID), dim3(kDecThreads), 0, st, delta, n, gp, tile_base, gpre, \
                        table, TNPTR, gkeys, gbins, nq, gbn, bn_width, err, TILES)
-    // MODE 1 with persistent workgroups (the next tile's deltas in flight) unless
-    // SKML_FORM_DEC_ROWS_SERIAL = 2 asks for one workgroup per tile
-    const bool persistent = form(SKML_FORM_DEC_ROWS_SERIAL) != 2;
+    // MODE 1 with one workgroup per tile; SKML_FORM_DEC_ROWS_SERIAL = 2 selects persistent
+    // workgroups with the next tile's deltas in flight (measured slower at 2^28: restore 0.767
+    // vs 0.707 ms, profiles/ab/r05_decp.txt; kept as an A/B form)
+    const bool persistent = form(SKML_FORM_DEC_ROWS_SERIAL) == 2;
 #define SKML_DEC_WIDTH(TNT, TNPTR)                                                          \
     do {                                                                                  \
         if (batched && persistent) {                                                      \
