@@ -115,25 +115,31 @@ __device__ __forceinline__ void load_starts(const SpGroups* gp, int64_t* S) {
 __device__ __forceinline__ uint32_t sar(uint32_t c, int s) { return (uint32_t)((int32_t)c >> s); }
 
 // BKDRHash's digit loop over a non-negative key, three decimal digits per step: a full chunk r
-// (digits d0 d1 d2, d0 the lowest) advances the code to code * s^3 + d0 s^2 + d1 s + d2, the last
-// chunk by as many digits as it has.  Divisions by 1000 / 100 / 10 as multiply-shifts, exact for
-// every 31-bit key and every r < 1000 (checked exhaustively against the digit loop on the host).
+// (digits d0 d1 d2, d0 the lowest) advances the code to code * s^3 + (d0 s + d1) s + d2, the last
+// chunk by as many digits as it has.  Every product but code * s^k has both operands below 2^24
+// (r < 1000, d < 10, s <= 13131, k / 1000 < 2^23, (d0 s + d1) s < 2^31), so it is a full-rate
+// 24-bit multiply instead of a quarter-rate 32-bit one; k / 1000 as the truncated double product
+// with RN(1/1000), which lies above 1/1000: never below the quotient, and below the next integer
+// by more than the product's rounding for every 32-bit k.  Checked exhaustively against the digit
+// loop on the host (tests/test_hash_arith.py).
+__device__ __forceinline__ uint32_t div1000(uint32_t k) { return (uint32_t)((double)k * 0.001); }
+__device__ __forceinline__ uint32_t bkdr3(uint32_t seed, uint32_t r) {  // r < 1000: d0 s^2 + d1 s + d2
+    const uint32_t t = __umul24(r, 205u) >> 11, h = __umul24(r, 41u) >> 12;  // r / 10, r / 100
+    return __umul24(__umul24(r - 10u * t, seed) + (t - 10u * h), seed) + h;
+}
 __device__ __forceinline__ uint32_t bkdr_chunks(uint32_t seed, uint32_t k) {
     const uint32_t s2 = seed * seed, s3 = s2 * seed;
     uint32_t c = 0;
     while (k >= 1000u) {
-        const uint32_t q = __umulhi(k, 0x10624DD3u) >> 6;  // k / 1000
-        const uint32_t r = k - 1000u * q;
-        const uint32_t t = (r * 205u) >> 11, h = (r * 41u) >> 12;  // r / 10, r / 100
-        c = c * s3 + (r - 10u * t) * s2 + (t - 10u * h) * seed + h;
+        const uint32_t q = div1000(k);
+        c = c * s3 + bkdr3(seed, k - __umul24(q, 1000u));
         k = q;
     }
     if (k >= 100u) {
-        const uint32_t t = (k * 205u) >> 11, h = (k * 41u) >> 12;
-        c = c * s3 + (k - 10u * t) * s2 + (t - 10u * h) * seed + h;
+        c = c * s3 + bkdr3(seed, k);
     } else if (k >= 10u) {
-        const uint32_t t = (k * 205u) >> 11;
-        c = c * s2 + (k - 10u * t) * seed + t;
+        const uint32_t t = __umul24(k, 205u) >> 11;
+        c = c * s2 + __umul24(k - 10u * t, seed) + t;
     } else if (k) {
         c = c * seed + k;
     }
@@ -186,7 +192,18 @@ __device__ __forceinline__ int32_t java_hash(int id, int32_t key, int32_t size) 
 // The same with `% size` folded non-negative as r - floor(r * (1/size)) * size: the double
 // product is within one of the true quotient and one correction step makes the result exact (an
 // integer division by a run-time divisor is a long instruction sequence on the GPU).
+// For size <= 2^30, in 32 bits: the quotient is off by at most one, so the uncorrected remainder
+// lies in [-size, 2 size) (tests/test_hash_arith.py).
+__device__ __forceinline__ int32_t java_hash_fm32(int id, int32_t key, int32_t size, double inv) {
+    const int32_t r = (int32_t)java_hash_mix(id, key);
+    const int32_t q = (int32_t)floor((double)r * inv);
+    int32_t m = (int32_t)((uint32_t)r - (uint32_t)q * (uint32_t)size);
+    if (m < 0) m += size;
+    else if (m >= size) m -= size;
+    return m;
+}
 __device__ __forceinline__ int32_t java_hash_fm(int id, int32_t key, int32_t size, double inv) {
+    if (size <= 0x40000000) return java_hash_fm32(id, key, size, inv);
     const int32_t r = (int32_t)java_hash_mix(id, key);
     const int64_t q = (int64_t)floor((double)r * inv);
     int64_t m = (int64_t)r - q * (int64_t)size;
@@ -215,7 +232,7 @@ __device__ __forceinline__ void dec_row_cells(const int32_t (&key)[4], int64_t i
         if constexpr (SKML_DEC_INTMOD)
             rel[j] = i0 + j < n ? (uint32_t)(row0 + dv(java_hash_mix(ID, key[j]))) : ~0u;
         else
-            rel[j] = i0 + j < n ? (uint32_t)(row0 + java_hash_fm(ID, key[j], cols, inv)) : ~0u;
+            rel[j] = i0 + j < n ? (uint32_t)(row0 + java_hash_fm32(ID, key[j], cols, inv)) : ~0u;
     }
 }
 
@@ -2481,16 +2498,28 @@ __device__ __forceinline__ void dec_keys_tile(int64_t n, const SpGroups* __restr
     const int zero = gp->zero, rows = gp->rows;
     int32_t key[4], res[4];
     int grp[4];
-    int g = group_of_elem(S, i0);
+    if constexpr (MODE == 1) {  // the tile's one group, workgroup-uniform
+        const int g = __builtin_amdgcn_readfirstlane(group_of_elem(S, tile * kSpTile));
+        const uint64_t gb = gpre[g];
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const int64_t i = i0 + j;
-        if (i < n)
-            while (i >= S[g + 1]) g++;
-        p += d[j];
-        grp[j] = g;
-        key[j] = (int32_t)(uint32_t)(p - gpre[g]);
-        res[j] = zero;
+        for (int j = 0; j < 4; j++) {
+            p += d[j];
+            grp[j] = g;
+            key[j] = (int32_t)(uint32_t)(p - gb);
+            res[j] = zero;
+        }
+    } else {
+        int g = group_of_elem(S, i0);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int64_t i = i0 + j;
+            if (i < n)
+                while (i >= S[g + 1]) g++;
+            p += d[j];
+            grp[j] = g;
+            key[j] = (int32_t)(uint32_t)(p - gpre[g]);
+            res[j] = zero;
+        }
     }
     constexpr uint32_t kTop = sizeof(TN) == 4 ? 0u : (uint32_t)(TN)~(TN)0;
     auto cell_of = [&](int j, int r) -> int64_t {
@@ -2759,9 +2788,10 @@ hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, con
     for (int x = 0; x < 8; x++) most = std::max(most, per[x]);
     const unsigned grid = (unsigned)(8 * most);
     // MODE 1 over every tile, then MODE 0 over the edge tiles; MODE 0 alone for other shapes, for
-    // tables past 2^32 - 1 cells, and under SKML_FORM_DEC_ROWS_SERIAL (tests)
+    // tables past 2^31 cells (MODE 1's cells are 32-bit offsets and its modulus takes cols <=
+    // 2^30), and under SKML_FORM_DEC_ROWS_SERIAL (tests)
     const bool batched = gh.rows == 2 && table != nullptr && form(SKML_FORM_DEC_ROWS_SERIAL) != 1 &&
-                         gh.ncells < (int64_t)0xFFFFFFFF;
+                         gh.ncells <= ((int64_t)1 << 31);
     DecEdgeTiles all{}, edges{};
     all.n = 0;
     if (batched) {  // tiles holding a group edge that is not a tile edge
