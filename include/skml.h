@@ -319,7 +319,8 @@ int skml_sparse_encode_f64(skml_ctx* ctx, const double* dense_dev, int64_t dim,
                            const skml_params* params, skml_sparse** out);
 /* GroupedMinMaxSketch.restore + Sort.merge (GroupedMinMaxSketch.java:123-146,
  * util/Sort.java:362-379) and SparseVectorCompressor.decompressSparse's value lookup
- * (SparseVectorCompressor.java:118-126).  keys/vals device buffers of nnz capacity. */
+ * (SparseVectorCompressor.java:118-126).  keys/vals device buffers of nnz capacity.  A restored
+ * bin outside quantValues returns SKML_E_ARG (Java: ArrayIndexOutOfBoundsException). */
 int skml_sparse_decode_f32(skml_ctx* ctx, const skml_sparse* s, int32_t* keys_dev,
                            float* vals_dev);
 /* The same with the values as the reference's doubles (quantValues[bin], no fp32 rounding). */

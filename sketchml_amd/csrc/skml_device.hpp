@@ -27,13 +27,19 @@ __device__ __forceinline__ bool is_nan_bits(uint32_t b) { return (b & 0x7FFFFFFF
 // 16-lane row, ds_swizzle (bit mode) inside 32 lanes, ds_bpermute otherwise.
 // ------------------------------------------------------------------------------------------
 // SKML_XLANE_SWIZZLE (A/B builds): every exchange inside 32 lanes through ds_swizzle, i.e. the
-// LDS pipe, instead of a DPP move on the VALU (the leaf is VALU-issue bound).
+// LDS pipe, instead of a DPP move on the VALU (the leaf is VALU-issue bound); SKML_XLANE_SWZ: the
+// same for the masks M whose bit is set (bit M), DPP for the rest.
+#ifdef SKML_XLANE_SWIZZLE
+#define SKML_XLANE_SWZ 0xFFFFFFFFu
+#endif
+#ifndef SKML_XLANE_SWZ
+#define SKML_XLANE_SWZ 0u
+#endif
 template <int M>
 __device__ __forceinline__ uint32_t lane_xor(uint32_t v) {
     int x = (int)v;
-#ifdef SKML_XLANE_SWIZZLE
-    if constexpr (M < 32) return (uint32_t)__builtin_amdgcn_ds_swizzle(x, (M << 10) | 0x1F);
-#endif
+    if constexpr (M < 32 && ((SKML_XLANE_SWZ >> M) & 1u))
+        return (uint32_t)__builtin_amdgcn_ds_swizzle(x, (M << 10) | 0x1F);
     if constexpr (M == 1) return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, true);
     else if constexpr (M == 2) return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, true);
     else if constexpr (M == 3) return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0x1B, 0xF, 0xF, true);

@@ -238,11 +238,12 @@ hipError_t launch_rs_merge(hipStream_t st, const int32_t* gk, const int32_t* gb,
                            int nq);
 hipError_t launch_merge_round(hipStream_t st, const int32_t* kin, const int32_t* bin_in, int32_t* kout,
                               int32_t* bout, const int64_t* run_start, int nruns, int64_t total, int64_t* split);
-// values[bins[i]] from the double quantValues LUT (SparseVectorCompressor.java:118-126).
+// values[bins[i]] from the double quantValues LUT (SparseVectorCompressor.java:118-126); a bin
+// outside [0, B) writes 0 and sets *err.
 hipError_t launch_bin_values(hipStream_t st, const int32_t* bins, int64_t n, const double* qvalues, int B,
-                             float* vals);
+                             float* vals, unsigned* err);
 hipError_t launch_bin_values64(hipStream_t st, const int32_t* bins, int64_t n, const double* qvalues, int B,
-                               double* vals);
+                               double* vals, unsigned* err);
 
 // HuffmanEncoder of the MinMaxSketch tables (serialisation): per-group histograms [G][B+1]
 // (symbol B = the fill value), code lengths per tile, and the MSB-first code stream writer

@@ -4111,33 +4111,38 @@ hipError_t launch_rs_merge(hipStream_t st, const int32_t* gk, const int32_t* gb,
 template <typename T>
 __global__ __launch_bounds__(kSpThreads) void k_bin_values(const int32_t* __restrict__ bins, int64_t n,
                                                            const double* __restrict__ qv, int B,
-                                                           T* __restrict__ vals) {
+                                                           T* __restrict__ vals, unsigned* __restrict__ err) {
     __shared__ T lut[4096];
     const bool lds = B <= 4096;
     if (lds) {
         for (int b = threadIdx.x; b < B; b += kSpThreads) lut[b] = (T)qv[b];
         __syncthreads();
     }
+    bool bad = false;
     for (int64_t i = (int64_t)blockIdx.x * kSpThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kSpThreads) {
         const int b = bins[i];
-        vals[i] = lds ? lut[b] : (T)qv[b];
+        const bool ok = b >= 0 && b < B;  // Java: quantValues[bin] out of bounds throws
+        bad |= !ok;
+        vals[i] = !ok ? (T)0 : lds ? lut[b] : (T)qv[b];
     }
+    if (bad) atomicOr(err, 1u);
 }
 
 template <typename T>
-hipError_t launch_bin_values_t(hipStream_t st, const int32_t* bins, int64_t n, const double* qvalues, int B, T* vals) {
+hipError_t launch_bin_values_t(hipStream_t st, const int32_t* bins, int64_t n, const double* qvalues, int B, T* vals,
+                               unsigned* err) {
     if (n <= 0) return hipSuccess;
     const int64_t grid = std::min<int64_t>(sp_tiles(n, kSpThreads * 4), 4096);
-    hipLaunchKernelGGL(k_bin_values<T>, dim3((unsigned)grid), dim3(kSpThreads), 0, st, bins, n, qvalues, B, vals);
+    hipLaunchKernelGGL(k_bin_values<T>, dim3((unsigned)grid), dim3(kSpThreads), 0, st, bins, n, qvalues, B, vals, err);
     return hipGetLastError();
 }
 hipError_t launch_bin_values(hipStream_t st, const int32_t* bins, int64_t n, const double* qvalues, int B,
-                             float* vals) {
-    return launch_bin_values_t<float>(st, bins, n, qvalues, B, vals);
+                             float* vals, unsigned* err) {
+    return launch_bin_values_t<float>(st, bins, n, qvalues, B, vals, err);
 }
 hipError_t launch_bin_values64(hipStream_t st, const int32_t* bins, int64_t n, const double* qvalues, int B,
-                               double* vals) {
-    return launch_bin_values_t<double>(st, bins, n, qvalues, B, vals);
+                               double* vals, unsigned* err) {
+    return launch_bin_values_t<double>(st, bins, n, qvalues, B, vals, err);
 }
 
 // =============================================================================================

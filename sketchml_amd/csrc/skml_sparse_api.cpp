@@ -681,8 +681,9 @@ thread_local int t_merge_path = 0;  // skml_debug_sparse_merge_path
 
 // Sort.merge's one-pass form (launch_rs_merge) into keys_out and out (vkind: 0 int32 bins, 1 float /
 // 2 double quantValues[bin]).  *pending: a pinned word that is non-zero after the stream
-// synchronises if the input was not regular and merge_groups must run instead; nullptr when the
-// one-pass form did not run (one run, or SKML_RS_ROUNDS set: the rounds' A/B switch).
+// synchronises if the input was not regular (or held a bin outside quantValues) and merge_groups
+// must run instead; nullptr when the one-pass form did not run (one run, or the rounds forced
+// through skml_debug_form).
 int rs_merge_start(skml_ctx* c, const skml_sparse* s, const int32_t* gk, const int32_t* gb, int32_t* keys_out,
                    void* out, int vkind, const double* qv, int nq, volatile unsigned** pending) {
     *pending = nullptr;
@@ -810,22 +811,30 @@ int decode_values(skml_ctx* c, const skml_sparse* s, int32_t* keys_dev, T* vals_
     double* qv = reinterpret_cast<double*>(ctx_scratch(c, kSlotCells, sizeof(double) * s->qvalues.size()));
     if (!qv) return sfail(SKML_E_OOM, "value table");
     SP_HIP(hipMemcpyAsync(qv, s->qvalues.data(), sizeof(double) * s->qvalues.size(), hipMemcpyHostToDevice, st));
-    auto rounds = [&]() -> int {  // pairwise merge rounds, then quantValues[bin]
+    // pairwise merge rounds, then quantValues[bin]; a bin outside the nq values (Java: index out
+    // of bounds) fails the decode (the one-pass merge sends such input here too)
+    auto rounds = [&]() -> int {
+        unsigned* err = scratch<unsigned>(c, kSlotStatus, 64);
+        if (!err) return sfail(SKML_E_OOM, "decode scratch");
+        SP_HIP(hipMemsetAsync(err, 0, sizeof(unsigned), st));
         if (int e = merge_groups(c, s, gk, gb, keys_dev, b1)) return e;
-        if constexpr (sizeof(T) == 8) SP_HIP(launch_bin_values64(st, b1, n, qv, nq, vals_dev));
-        else SP_HIP(launch_bin_values(st, b1, n, qv, nq, vals_dev));
-        return SKML_OK;
+        if constexpr (sizeof(T) == 8) SP_HIP(launch_bin_values64(st, b1, n, qv, nq, vals_dev, err));
+        else SP_HIP(launch_bin_values(st, b1, n, qv, nq, vals_dev, err));
+        unsigned bad = 0;
+        if (int e = sync_to_host(c, &bad, err, sizeof(bad))) return e;
+        return bad ? sfail(SKML_E_ARG, "a restored bin lies outside the %d quantValues", nq) : SKML_OK;
     };
     volatile unsigned* pending = nullptr;
     if (int e = rs_merge_start(c, s, gk, gb, keys_dev, vals_dev, sizeof(T) == 8 ? 2 : 1, qv, nq, &pending)) return e;
-    if (!pending)
-        if (int e = rounds()) return e;
+    if (!pending) {
+        t_merge_path = s->g.G < 2 ? 0 : 2;
+        return rounds();
+    }
     SP_HIP(hipStreamSynchronize(st));
-    t_merge_path = s->g.G < 2 ? 0 : pending ? 1 : 2;
-    if (pending && *pending) {  // not regular (or a bin outside quantValues): the rounds decide
+    t_merge_path = 1;
+    if (*pending) {  // not regular, or a bin outside quantValues: the rounds decide
         t_merge_path = 3;
-        if (int e = rounds()) return e;
-        SP_HIP(hipStreamSynchronize(st));
+        return rounds();
     }
     return SKML_OK;
 }

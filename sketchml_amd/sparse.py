@@ -90,7 +90,8 @@ class SparsePayload:
     def restore(self, dtype=torch.float32):
         """GroupedMinMaxSketch.restore + SparseVectorCompressor.decompressSparse: device keys
         (int32) and values quantValues[bin] (fp32 of the doubles, or the doubles themselves with
-        dtype=torch.float64, as the reference returns them)."""
+        dtype=torch.float64, as the reference returns them).  A restored bin outside quantValues
+        raises SketchMLException, as the reference's array lookup throws."""
         n = self.nnz()
         dev = torch.device("cuda", self.device)
         wide = dtype == torch.float64

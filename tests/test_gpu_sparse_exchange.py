@@ -94,6 +94,33 @@ def test_corrupt_blobs_are_refused(gpu):
         gpu.decode_sum(blob, 1, blob.numel(), 1000)
 
 
+
+@pytest.mark.parametrize("bins,forms", [(256, {}), (1000, {}), (256, {"rs_rounds": 1}), (256, {"rs_rounds": 2})])
+def test_restore_values_refuse_bins_outside_quant_values(gpu, bins, forms):
+    """quantValues[bin] with a bin past the values (SparseVectorCompressor.java:118-126 throws
+    ArrayIndexOutOfBoundsException): every MinMax cell of an imported blob overwritten with binNum
+    + 5.  restore() of the values refuses it through the pipelined one-pass merge (256 and 1,000
+    values), the plain one-pass kernel and the merge rounds alike; restore_bins() returns the raw
+    cells as MinMaxSketch.query does."""
+    from sketchml_amd import _lib
+    pl, _ = _payload(gpu, 60000, 0.2, 4, bins=bins)
+    blob = pl.export().clone()
+    hdr = blob[:256].cpu().numpy()
+    ncells = int(hdr[24:32].view(np.int64)[0])
+    off_tab = int(hdr[96:104].view(np.int64)[0])
+    cells = torch.full((ncells,), bins + 5, dtype=torch.int32, device="cuda")
+    blob[off_tab:off_tab + 4 * ncells] = cells.view(torch.uint8)
+    bad = gpu.SparsePayload.from_blob(blob)
+    with _lib.forced_forms(**forms):
+        _, b = bad.restore_bins()
+        assert int(b.min()) == bins + 5 and int(b.max()) == bins + 5
+        for dt in (torch.float32, torch.float64):
+            with pytest.raises(gpu.SketchMLException, match="outside"):
+                bad.restore(dt)
+        _, v = pl.restore(torch.float64)             # the context recovers for a good payload
+        assert torch.isfinite(v).all()
+
+
 # Gradient.sum's tile kernels: vtile_pf (the default for payloads of <= 8 groups and <= 256
 # quantValues: vtile with the next tile's element loads in flight), vtile (
 # one wave per 512-key tile stages every payload's bins with presence bits and sums each key in
