@@ -225,7 +225,8 @@ static_assert(sizeof(SpBlobHeader) <= 256, "blob header fits its 256-byte sectio
 // Sort.merge in one pass (the regular case: runs ascend strictly, keys distinct and in [0, INT32_MAX)):
 // bounds = G x (kRsRanges + 1) int32 scratch; info->irregular != 0 after the launches means the
 // input was not regular and the caller must run the merge rounds instead.  vkind 0: out = int32
-// bins; 1: float quantValues[bin]; 2: double quantValues[bin] (qv: nq doubles).
+// bins; 1: float quantValues[bin]; 2: double quantValues[bin] (qv: nq doubles).  *info must be
+// zeroed by the caller before the launch.
 constexpr int kRsBits = 13, kRsRange = 1 << kRsBits, kRsWords = kRsRange / 32;
 constexpr int64_t kRsRanges = (int64_t)1 << (31 - kRsBits);  // key ranges of [0, 2^31)
 struct RsInfo {

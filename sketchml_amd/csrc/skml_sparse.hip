@@ -3917,8 +3917,12 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_merge(const int32_t* __restri
 
 // Sort.merge in one pass, software pipelined: while range t is marked, scanned and emitted, the
 // element loads of the workgroup's next range are in flight (its piece table computed one range
-// ahead into the other half of a double buffer, its run bounds fetched two ranges ahead).  Same
-// output and the same irregular-input flags as k_rs_merge.
+// ahead into the other half of a double buffer, its run bounds fetched two ranges ahead).  The
+// emission is coalesced: each thread lists its word's set offsets at their ranks in `ord`, and
+// output j of the range is written by thread j % 256 (the per-bit stores of k_rs_merge write 64
+// scattered words per instruction).  Values restores hold the bins as 16-bit slots (checked
+// against nq on load: a bin outside quantValues flags the input, as rs_value does), so `ord` fits
+// in the LDS the int32 slots took.  Same output and irregular-input flags as k_rs_merge.
 template <typename V>
 __global__ __launch_bounds__(kRsThreads) void k_rs_merge_pf(const int32_t* __restrict__ gk,
                                                             const int32_t* __restrict__ gb,
@@ -3926,9 +3930,12 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_merge_pf(const int32_t* __res
                                                             const int32_t* __restrict__ bounds,
                                                             RsInfo* __restrict__ info, int32_t* __restrict__ keys_out,
                                                             V* __restrict__ out, const double* __restrict__ qv, int nq) {
-    constexpr int kLut = std::is_same<V, int32_t>::value ? 1 : kRsLut;
+    constexpr bool kBins = std::is_same<V, int32_t>::value;  // int32 bins out: any table value
+    constexpr int kLut = kBins ? 1 : kRsLut;
+    using ST = typename std::conditional<kBins, int32_t, uint16_t>::type;
     __shared__ uint32_t bm[kRsWords];
-    __shared__ int32_t slot[kRsRange];
+    __shared__ ST slot[kRsRange];
+    __shared__ uint16_t ord[kRsRange];  // the range's set offsets in key order
     __shared__ int64_t S[kMaxGroups + 1];
     __shared__ int64_t lo_s[3][kMaxGroups];
     __shared__ int32_t pre[3][kMaxGroups + 1];
@@ -4027,12 +4034,23 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_merge_pf(const int32_t* __res
         if (more) load(nbuf, kn, bn);  // in flight while this range is marked and emitted
         const int cnt = pre[buf][G];
         // pass 1: this range's keys into the bitmap, their bins into the offset slots
+        auto to_slot = [&](int32_t b) -> ST {
+            if constexpr (kBins) {
+                return b;
+            } else {
+                if (b < 0 || b >= nq) {  // quantValues[bin] out of bounds: the rounds report it
+                    bad = 1;
+                    return 0;
+                }
+                return (ST)b;
+            }
+        };
 #pragma unroll
         for (int u = 0; u < kRsBatch; u++) {
             if (kc[u] < 0) continue;
             const uint32_t off = (uint32_t)kc[u] & (kRsRange - 1), bit = 1u << (off & 31);
             if (atomicOr(&bm[off >> 5], bit) & bit) bad = 1;  // a repeated key
-            slot[off] = bc[u];
+            slot[off] = to_slot(bc[u]);
         }
         for (int j = kRsThreads * kRsBatch + t_; j < cnt; j += kRsThreads) {  // past the registers
             const int g = run_of(buf, j);
@@ -4040,7 +4058,7 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_merge_pf(const int32_t* __res
             const int32_t k = gk[i];
             const uint32_t off = (uint32_t)k & (kRsRange - 1), bit = 1u << (off & 31);
             if (atomicOr(&bm[off >> 5], bit) & bit) bad = 1;
-            slot[off] = gb[i];
+            slot[off] = to_slot(gb[i]);
         }
         __syncthreads();
         if (cnt > 0) {  // workgroup-uniform
@@ -4058,12 +4076,14 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_merge_pf(const int32_t* __res
             __syncthreads();
             uint32_t run = inc - own;
             for (int q = 0; q < w; q++) run += wsum[q];
-            int64_t o = obase[buf] + run;
-            const int32_t kbase = (int32_t)(t * kRsRange) + 32 * t_;
-            for (uint32_t m = word; m; m &= m - 1, o++) {
-                const int b = __ffs(m) - 1;
-                keys_out[o] = kbase + b;
-                out[o] = rs_value<V>(slot[32 * t_ + b], lut, qv, nq, lds, bad);
+            for (uint32_t m = word; m; m &= m - 1, run++) ord[run] = (uint16_t)(32 * t_ + __ffs(m) - 1);
+            __syncthreads();
+            const int64_t ob = obase[buf];
+            const int32_t kbase = (int32_t)(t * kRsRange);
+            for (int j = t_; j < cnt; j += kRsThreads) {
+                const int off = ord[j];
+                keys_out[ob + j] = kbase + off;
+                out[ob + j] = rs_value<V>((int32_t)slot[off], lut, qv, nq, lds, bad);
             }
         }
         buf = nbuf;
@@ -4080,8 +4100,6 @@ hipError_t launch_rs_merge(hipStream_t st, const int32_t* gk, const int32_t* gb,
                            int32_t* bounds, RsInfo* info, int32_t* keys_out, void* out, int vkind, const double* qv,
                            int nq) {
     if (n <= 0) return hipSuccess;
-    hipError_t e = hipMemsetAsync(info, 0, sizeof(RsInfo), st);
-    if (e != hipSuccess) return e;
     const int64_t bgrid = sp_tiles(sp_tiles(n, 16), kSpThreads);
     hipLaunchKernelGGL(k_rs_bounds, dim3((unsigned)bgrid), dim3(kSpThreads), 0, st, gk, n, gp, bounds, info);
     // persistent workgroups over the key ranges up to the largest key (read on the device): as many

@@ -679,25 +679,39 @@ int merge_groups(skml_ctx* c, const skml_sparse* s, int32_t* gk, int32_t* gb, in
 
 thread_local int t_merge_path = 0;  // skml_debug_sparse_merge_path
 
-// Sort.merge's one-pass form (launch_rs_merge) into keys_out and out (vkind: 0 int32 bins, 1 float /
-// 2 double quantValues[bin]).  *pending: a pinned word that is non-zero after the stream
-// synchronises if the input was not regular (or held a bin outside quantValues) and merge_groups
-// must run instead; nullptr when the one-pass form did not run (one run, or the rounds forced
-// through skml_debug_form).
-int rs_merge_start(skml_ctx* c, const skml_sparse* s, const int32_t* gk, const int32_t* gb, int32_t* keys_out,
-                   void* out, int vkind, const double* qv, int nq, volatile unsigned** pending) {
-    *pending = nullptr;
+// Sort.merge's one-pass form: its scratch (RsInfo + the runs' key-range bounds) taken and RsInfo
+// zeroed up front, so the fill runs while the restore's first kernels are still being queued;
+// m->info stays nullptr when the one-pass form will not run (one run, or the rounds forced through
+// skml_debug_form).
+struct RsMerge {
+    RsInfo* info = nullptr;
+    int32_t* bounds = nullptr;
+};
+int rs_merge_prepare(skml_ctx* c, const skml_sparse* s, RsMerge* m) {
+    *m = RsMerge{};
     if (s->g.G < 2 || form(SKML_FORM_RS_ROUNDS) == 1) return SKML_OK;
-    hipStream_t st = ctx_stream(c);
     const size_t o_b = align_up(sizeof(RsInfo), 256);
     char* blk = static_cast<char*>(
         ctx_scratch(c, kSlotRsMerge, o_b + sizeof(int32_t) * (size_t)s->g.G * (size_t)(kRsRanges + 1)));
+    if (!blk) return sfail(SKML_E_OOM, "merge scratch");
+    SP_HIP(hipMemsetAsync(blk, 0, o_b, ctx_stream(c)));  // whole 256-byte units: one fill
+    m->info = reinterpret_cast<RsInfo*>(blk);
+    m->bounds = reinterpret_cast<int32_t*>(blk + o_b);
+    return SKML_OK;
+}
+// The one-pass merge (launch_rs_merge) into keys_out and out (vkind: 0 int32 bins, 1 float / 2
+// double quantValues[bin]).  *pending: a pinned word that is non-zero after the stream
+// synchronises if the input was not regular (or held a bin outside quantValues) and merge_groups
+// must run instead; nullptr when the one-pass form did not run.
+int rs_merge_start(skml_ctx* c, const skml_sparse* s, const RsMerge& m, const int32_t* gk, const int32_t* gb,
+                   int32_t* keys_out, void* out, int vkind, const double* qv, int nq, volatile unsigned** pending) {
+    *pending = nullptr;
+    if (!m.info) return SKML_OK;
+    hipStream_t st = ctx_stream(c);
     unsigned* pin = static_cast<unsigned*>(ctx_pinned(c, 64));
-    if (!blk || !pin) return sfail(SKML_E_OOM, "merge scratch");
-    RsInfo* info = reinterpret_cast<RsInfo*>(blk);
-    SP_HIP(launch_rs_merge(st, gk, gb, s->nnz, s->g_dev, reinterpret_cast<int32_t*>(blk + o_b), info, keys_out, out,
-                           vkind, qv, nq));
-    SP_HIP(hipMemcpyAsync(pin, &info->irregular, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    if (!pin) return sfail(SKML_E_OOM, "merge scratch");
+    SP_HIP(launch_rs_merge(st, gk, gb, s->nnz, s->g_dev, m.bounds, m.info, keys_out, out, vkind, qv, nq));
+    SP_HIP(hipMemcpyAsync(pin, &m.info->irregular, sizeof(unsigned), hipMemcpyDeviceToHost, st));
     *pending = pin;
     return SKML_OK;
 }
@@ -806,11 +820,15 @@ int decode_values(skml_ctx* c, const skml_sparse* s, int32_t* keys_dev, T* vals_
     int32_t* gb = scratch<int32_t>(c, kSlotGBins, (size_t)n);
     int32_t* b1 = scratch<int32_t>(c, kSlotB1, (size_t)n);
     if (!gk || !gb || !b1) return sfail(SKML_E_OOM, "decode scratch");
-    if (int e = decode_groups(c, s, gk, gb, true)) return e;
+    // the value table's upload and the merge's RsInfo fill go first: the GPU runs them while the
+    // decode's kernels are still being queued
     const int nq = (int)s->qvalues.size();
     double* qv = reinterpret_cast<double*>(ctx_scratch(c, kSlotCells, sizeof(double) * s->qvalues.size()));
     if (!qv) return sfail(SKML_E_OOM, "value table");
     SP_HIP(hipMemcpyAsync(qv, s->qvalues.data(), sizeof(double) * s->qvalues.size(), hipMemcpyHostToDevice, st));
+    RsMerge rm;
+    if (int e = rs_merge_prepare(c, s, &rm)) return e;
+    if (int e = decode_groups(c, s, gk, gb, true)) return e;
     // pairwise merge rounds, then quantValues[bin]; a bin outside the nq values (Java: index out
     // of bounds) fails the decode (the one-pass merge sends such input here too)
     auto rounds = [&]() -> int {
@@ -825,7 +843,8 @@ int decode_values(skml_ctx* c, const skml_sparse* s, int32_t* keys_dev, T* vals_
         return bad ? sfail(SKML_E_ARG, "a restored bin lies outside the %d quantValues", nq) : SKML_OK;
     };
     volatile unsigned* pending = nullptr;
-    if (int e = rs_merge_start(c, s, gk, gb, keys_dev, vals_dev, sizeof(T) == 8 ? 2 : 1, qv, nq, &pending)) return e;
+    if (int e = rs_merge_start(c, s, rm, gk, gb, keys_dev, vals_dev, sizeof(T) == 8 ? 2 : 1, qv, nq, &pending))
+        return e;
     if (!pending) {
         t_merge_path = s->g.G < 2 ? 0 : 2;
         return rounds();
@@ -1620,9 +1639,11 @@ int skml_sparse_restore_bins(skml_ctx* c, const skml_sparse* s, int32_t* keys_de
     int32_t* gk = scratch<int32_t>(c, kSlotGKeys, (size_t)n);
     int32_t* gb = scratch<int32_t>(c, kSlotGBins, (size_t)n);
     if (!gk || !gb) return sfail(SKML_E_OOM, "restore scratch");
+    RsMerge rm;
+    if (int e = rs_merge_prepare(c, s, &rm)) return e;
     if (int e = decode_groups(c, s, gk, gb, true)) return e;
     volatile unsigned* pending = nullptr;
-    if (int e = rs_merge_start(c, s, gk, gb, keys_dev, bins_dev, 0, nullptr, 0, &pending)) return e;
+    if (int e = rs_merge_start(c, s, rm, gk, gb, keys_dev, bins_dev, 0, nullptr, 0, &pending)) return e;
     if (!pending)
         if (int e = merge_groups(c, s, gk, gb, keys_dev, bins_dev)) return e;
     SP_HIP(hipStreamSynchronize(st));
