@@ -195,10 +195,11 @@ hipError_t launch_agg_bounds(hipStream_t st, const int32_t* gk, int64_t n, const
 constexpr int kAggVPayloads = 8;
 bool agg_vtiles_ok(int max_groups, int max_nq);
 int agg_tile_bits(bool vtiles);
-// kbase / bbase: the buffers every payload's gk / gb lie in (AggPayload::gk_off / gb_off)
+// kbase / bbase: the buffers every payload's gk / gb lie in (AggPayload::gk_off / gb_off);
+// any_dense: a payload of the launch takes the dense form (AggPayload::dense_form)
 hipError_t launch_agg_tiles(hipStream_t st, const AggPayload* pays, int P, int64_t ntiles, int64_t dim, double* out,
                             int from_out, double scale, unsigned* err, bool vtiles, const int32_t* kbase,
-                            const uint8_t* bbase);
+                            const uint8_t* bbase, bool any_dense);
 
 // Exported sparse payload: one contiguous device blob (skml_sparse_export / _import, the unit the
 // RCCL all-gather moves).  Offsets are from the blob start, every section 256-byte aligned.

@@ -3522,6 +3522,193 @@ __global__ __launch_bounds__(kAggThreads) __attribute__((amdgpu_waves_per_eu(4))
     if (bad) atomicOr(err, bad);
 }
 
+// The sum tile itself in LDS: the same waves, tiles, run pieces and prefetch as k_agg_vtiles_pf,
+// but each element is added straight into the wave's 512 doubles of the tile (read, add, write
+// back) instead of being staged as a bin and summed by a sweep over every (payload, key) slot,
+// which looked up quantValues 64 times per lane and tile for ~6 present elements.  The elements of
+// a tile are concatenated payload by payload, so each element row (one load instruction) holds
+// ascending payloads by lane and later rows never hold an earlier payload; a row is added payload
+// by payload (one masked pass per payload present in it, usually one or two), and since a payload
+// holds a key at most once, no two lanes of a pass touch the same slot and every key receives its
+// payloads' values in payload order -- Gradient.sum's order, with the same roundings as the
+// staged form.  A key repeated inside a payload (presence bit already set) is not added and sets
+// err bit 2.  Dense-form payloads (a -0.0 sum turned into +0.0 at every key) keep the staged form.
+__global__ __launch_bounds__(kAggThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_agg_vtiles_rmw(
+    const AggPayload* __restrict__ pays, int P, int64_t ntiles, int64_t dim, double* __restrict__ out, int from_out,
+    double scale, unsigned* __restrict__ err, const int32_t* __restrict__ kbase, const uint8_t* __restrict__ bbase) {
+    constexpr int kWaves = kAggThreads / 64;
+    __shared__ __attribute__((aligned(16))) double tsum[kWaves][kAggVTile];
+    __shared__ uint32_t here[kWaves][kAggPB][kAggVTile / 32];
+    __shared__ double qt[kAggPB][kAggLdsValues];
+    __shared__ int32_t pre[2][kWaves][65];
+    __shared__ int32_t pk0[2][kWaves][64];
+    __shared__ int32_t pn0[2][kWaves][64];
+    __shared__ AggPayload pl[kAggPB];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (threadIdx.x < P * (int)(sizeof(AggPayload) / 8))
+        reinterpret_cast<uint64_t*>(pl)[threadIdx.x] = reinterpret_cast<const uint64_t*>(pays)[threadIdx.x];
+    __syncthreads();
+    if (wave < P)
+        for (int b = lane; b < pl[wave].nq; b += 64) qt[wave][b] = gload<double>(pl[wave].qv, b);
+    __syncthreads();
+    const int pl_l = lane >> 3, g_l = lane & 7;
+    const bool lane_on = pl_l < P && g_l < pl[pl_l].G;
+    const int32_t* bd = lane_on ? pl[pl_l].bounds + (int64_t)g_l * (ntiles + 1) : nullptr;
+    const int32_t gk_off = lane_on ? pl[pl_l].gk_off : 0, gb_off = lane_on ? pl[pl_l].gb_off : 0;
+    double* T = tsum[wave];
+    uint32_t(*H)[kAggVTile / 32] = here[wave];
+    unsigned bad = 0;
+    int32_t nb0 = 0, nb1 = 0;
+    auto fetch = [&](int64_t tt) {
+        if (lane_on && tt < ntiles) {
+            nb0 = gload<int32_t>(bd, tt);
+            nb1 = gload<int32_t>(bd, tt + 1);
+        }
+    };
+    auto plan = [&](int buf, int32_t b0, int32_t b1, int ln) -> int {
+        const int32_t len = lane_on && b1 > b0 ? b1 - b0 : 0;
+        const int32_t x = (int32_t)wave_incl_scan_u32((uint32_t)len);
+        pre[buf][wave][ln + 1] = x;
+        if (ln == 0) pre[buf][wave][0] = 0;
+        pk0[buf][wave][ln] = gk_off + b0;
+        pn0[buf][wave][ln] = gb_off + b0;
+        __builtin_amdgcn_wave_barrier();
+        return __builtin_amdgcn_readlane(x, 63);
+    };
+    auto piece_of = [&](int buf, int j) -> int {  // largest s < 64 with pre[s] <= j
+        int s_ = 0;
+#pragma unroll
+        for (int step = 32; step >= 1; step >>= 1)
+            if (pre[buf][wave][s_ + step] <= j) s_ += step;
+        return s_;
+    };
+    auto load = [&](int buf, int total, int ln, int32_t (&kk)[kAggWPer], uint32_t (&bb)[kAggWPer]) {
+        int spc[kAggWPer];
+#pragma unroll
+        for (int u = 0; u < kAggWPer; u++) {
+            const int j = ln + 64 * u;
+            spc[u] = piece_of(buf, j < total ? j : 0);
+        }
+#pragma unroll
+        for (int u = 0; u < kAggWPer; u++) {
+            const int j = ln + 64 * u;
+            kk[u] = INT32_MIN;
+            bb[u] = 0;
+            if (j < total) {
+                const int sp = spc[u], d = j - pre[buf][wave][sp];
+                kk[u] = gload<int32_t>(kbase, (uint32_t)(pk0[buf][wave][sp] + d));
+                bb[u] = gload<uint8_t>(bbase, (uint32_t)(pn0[buf][wave][sp] + d)) | ((uint32_t)(sp >> 3) << 8);
+            }
+        }
+    };
+    int64_t prev_k0 = -1, prev_nk = 0;
+    auto store_prev = [&](int l) {  // the previous tile's sums, x scale, 1 KB per store instruction
+        if (prev_k0 < 0) return;
+        double* o = out + prev_k0;
+        const bool whole = prev_nk == kAggVTile && (reinterpret_cast<uintptr_t>(o) & 15) == 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int x = 128 * q + 2 * l;
+            double2 v = *reinterpret_cast<const double2*>(T + x);
+            if (scale != 1.0) {
+                v.x = __dmul_rn(v.x, scale);
+                v.y = __dmul_rn(v.y, scale);
+            }
+            if (whole) {
+                *reinterpret_cast<double2*>(o + x) = v;
+            } else {
+                if (x < prev_nk) o[x] = v.x;
+                if (x + 1 < prev_nk) o[x + 1] = v.y;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        prev_k0 = -1;
+    };
+    const TileWalk tw = tile_walk(blockIdx.x, gridDim.x, wave, kWaves, ntiles);
+    int buf = 0, total = 0;
+    int32_t kk[kAggWPer], kn[kAggWPer];
+    uint32_t bb[kAggWPer], bn[kAggWPer];
+    if (tw.t0 < tw.t1) {
+        fetch(tw.t0);
+        total = plan(0, nb0, nb1, lane);
+        load(0, total, lane, kk, bb);
+        fetch(tw.t0 + tw.step);
+    }
+    for (int64_t t = tw.t0; t < tw.t1; t += tw.step) {
+        int ln = lane;  // lane-derived values rematerialised per tile (hoisted, they spill)
+        asm volatile("" : "+v"(ln));
+        const int64_t k0 = t << kAggVBits, nk = std::min<int64_t>(kAggVTile, dim - k0);
+        int total_n = 0;
+        const bool more = t + tw.step < tw.t1;
+        if (more) {
+            total_n = plan(buf ^ 1, nb0, nb1, ln);
+            load(buf ^ 1, total_n, ln, kn, bn);
+            fetch(t + 2 * tw.step);
+        }
+        store_prev(ln);
+        // the tile's starting sums (a later batch of payloads continues them) and presence bits
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            double2 v = make_double2(0.0, 0.0);
+            if (from_out) {
+                const int x = 8 * ln + 2 * q;
+                if (x < nk) v.x = out[k0 + x];
+                if (x + 1 < nk) v.y = out[k0 + x + 1];
+            }
+            *reinterpret_cast<double2*>(T + 8 * ln + 2 * q) = v;
+        }
+        reinterpret_cast<uint64_t*>(H)[ln] = 0;
+        __builtin_amdgcn_wave_barrier();
+        // one row of elements (lane l: element j = l + 64 u), payload by payload
+        auto add_row = [&](bool act, int p_el, int32_t k, uint32_t b) {
+            uint64_t rem = __ballot(act);
+            while (rem) {
+                const int first = __ffsll((unsigned long long)rem) - 1;
+                const int pcur = __builtin_amdgcn_readlane(p_el, first);
+                const bool mine = act && p_el == pcur;
+                if (mine) {
+                    if (k < k0 || (int64_t)k >= k0 + nk) {  // k_agg_bounds placed it here: an error
+                        bad |= 1u;
+                    } else {
+                        const int xk = (int)(k - k0);
+                        const uint32_t bit = 1u << (xk & 31);
+                        if (atomicOr(&H[pcur][xk >> 5], bit) & bit) bad |= 2u;  // a key twice in one payload
+                        else T[xk] = T[xk] + qt[pcur][b];
+                    }
+                }
+                rem &= ~__ballot(mine);
+            }
+        };
+#pragma unroll
+        for (int u = 0; u < kAggWPer; u++)
+            add_row(ln + 64 * u < total, (int)(bb[u] >> 8), kk[u], bb[u] & 0xFFu);
+        for (int j0 = 64 * kAggWPer; j0 < total; j0 += 64) {  // rows past the registers
+            const int j = j0 + ln;
+            const bool act = j < total;
+            int sp = 0, d = 0;
+            if (act) {
+                sp = piece_of(buf, j);
+                d = j - pre[buf][wave][sp];
+            }
+            const int32_t k = act ? gload<int32_t>(kbase, (uint32_t)(pk0[buf][wave][sp] + d)) : 0;
+            const uint32_t b = act ? gload<uint8_t>(bbase, (uint32_t)(pn0[buf][wave][sp] + d)) : 0u;
+            add_row(act, sp >> 3, k, b);
+        }
+        __builtin_amdgcn_wave_barrier();
+        prev_k0 = k0;
+        prev_nk = nk;
+        buf ^= 1;
+        total = total_n;
+#pragma unroll
+        for (int u = 0; u < kAggWPer; u++) {
+            kk[u] = kn[u];
+            bb[u] = bn[u];
+        }
+    }
+    store_prev(lane);
+    if (bad) atomicOr(err, bad);
+}
+
 // The staged wave-tile form is the default for payloads of at most 8 groups and 256 quantValues
 // (the caller launches it 8 payloads at a time); the wave-per-payload tiles take every other shape
 // (SKML_FORM_AGG_TILES forces them for tests).
@@ -3545,13 +3732,22 @@ static int resident_workgroups(K kern) {
 
 hipError_t launch_agg_tiles(hipStream_t st, const AggPayload* pays, int P, int64_t ntiles, int64_t dim, double* out,
                             int from_out, double scale, unsigned* err, bool vtiles, const int32_t* kbase,
-                            const uint8_t* bbase) {
+                            const uint8_t* bbase, bool any_dense) {
     if (ntiles <= 0) return hipSuccess;
     if (vtiles) {
         if (P < 1 || P > kAggVPayloads) return hipErrorInvalidValue;  // one lane per (payload, group)
-        // the default: the prefetching form (5.57-5.64 against 5.63-5.66 ms for 8 C3 payloads,
-        // profiles/ab/r05_pf.txt); SKML_FORM_AGG_TILES = 5 / 2 / 3: the plain staged tiles, four /
-        // two tiles per wave round (A/B forms)
+        // the default: the sum tile in LDS (k_agg_vtiles_rmw) unless a payload takes the dense
+        // form; then the prefetching staged form (5.57-5.64 against 5.63-5.66 ms for 8 C3
+        // payloads, profiles/ab/r05_pf.txt); SKML_FORM_AGG_TILES = 4 / 5 / 2 / 3: the prefetching
+        // staged form, the plain staged tiles, four / two tiles per wave round (A/B forms)
+        if (form(SKML_FORM_AGG_TILES) == 0 && !any_dense) {
+            static const int resident_rmw = resident_workgroups(k_agg_vtiles_rmw);
+            const int64_t all = sp_tiles(ntiles, kAggThreads / 64);
+            const unsigned grid = (unsigned)(resident_rmw <= 0 ? all : std::min<int64_t>(all, resident_rmw));
+            hipLaunchKernelGGL(k_agg_vtiles_rmw, dim3(grid), dim3(kAggThreads), 0, st, pays, P, ntiles, dim, out,
+                               from_out, scale, err, kbase, bbase);
+            return hipGetLastError();
+        }
         if (form(SKML_FORM_AGG_TILES) == 2) {
             static const int resident4 = resident_workgroups(k_agg_vtiles<4>);
             const int64_t all = sp_tiles(sp_tiles(ntiles, 4), kAggThreads / 64);

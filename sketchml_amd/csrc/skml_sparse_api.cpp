@@ -2021,8 +2021,10 @@ int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t
         const size_t chunk = vt ? (size_t)kAggVPayloads : pays.size();
         for (size_t c0 = 0; c0 < pays.size(); c0 += chunk) {
             const size_t nc = std::min(chunk, pays.size() - c0);
+            bool any_dense = false;
+            for (size_t q = c0; q < c0 + nc; q++) any_dense |= pays[q].dense_form != 0;
             SP_HIP(launch_agg_tiles(st, d_pays + c0, (int)nc, ntiles, dim, out, first && c0 == 0 ? 0 : 1,
-                                    last && c0 + nc == pays.size() ? scale : 1.0, err, vt, gk, gbn));
+                                    last && c0 + nc == pays.size() ? scale : 1.0, err, vt, gk, gbn, any_dense));
         }
         SP_HIP(hipStreamSynchronize(st));  // `pays` (host) and the scratch are reused by the next batch
         first = false;

@@ -121,15 +121,17 @@ def test_restore_values_refuse_bins_outside_quant_values(gpu, bins, forms):
         assert torch.isfinite(v).all()
 
 
-# Gradient.sum's tile kernels: vtile_pf (the default for payloads of <= 8 groups and <= 256
-# quantValues: vtile with the next tile's element loads in flight), vtile (
+# Gradient.sum's tile kernels: vtile_rmw (the default for payloads of <= 8 groups and <= 256
+# quantValues: the 512-key sum tile in LDS, each element added into it row by row, payload by
+# payload, with the next tile's element loads in flight; dense-form payloads take vtile_pf),
+# vtile_pf (vtile with the next tile's element loads in flight), vtile (
 # one wave per 512-key tile stages every payload's bins with presence bits and sums each key in
 # registers, payload after payload, 8 payloads per launch; restores on two streams), wave
 # (SKML_FORM_AGG_TILES: one wave per payload adding into a 4,096-key LDS tile, the form for any
 # other shape) and wave_serial (the wave tiles with the generic per-row MinMax query and one
 # stream); vtile2 / vtile4 take two / four staged tiles per wave round (one round of element
 # loads); vtile_pf loads the next tile's elements while a tile is summed.  Every form is exact, and every form refuses a key repeated across a payload's groups.
-KERNELS = {"vtile_pf": {}, "vtile": {"agg_tiles": 5}, "vtile2": {"agg_tiles": 3}, "vtile4": {"agg_tiles": 2},
+KERNELS = {"vtile_rmw": {}, "vtile_pf": {"agg_tiles": 4}, "vtile": {"agg_tiles": 5}, "vtile2": {"agg_tiles": 3}, "vtile4": {"agg_tiles": 2},
            "wave": {"agg_tiles": 1},
            "wave_serial": {"agg_tiles": 1, "dec_rows_serial": 1, "agg_one_lane": 1}}
 
@@ -334,7 +336,7 @@ def test_decode_sum_eight_distinct_c3_payloads_full_size(gpu):
     want, forms = O.gradient_sum(restored, dim, 1.0 / P)
     del restored
     assert forms == ["sparse"] * P
-    for form in (0, 5, 3, 2, 1):                         # staged tiles (prefetching, 1, 2, 4 per round), 4,096-key tiles
+    for form in (0, 4, 5, 3, 2, 1):                      # sum tile in LDS, staged tiles (prefetching, 1, 2, 4 per round), 4,096-key tiles
         with _lib.forced_forms(agg_tiles=form):
             got = gpu.decode_sum(allb, P, stride, dim, 1.0 / P)
             torch.cuda.synchronize()
