@@ -2972,6 +2972,16 @@ struct TileWalk {
 __device__ __forceinline__ TileWalk tile_walk(int64_t blk, int64_t nblk, int sub, int nsub, int64_t ntiles) {
     return {blk * nsub + sub, ntiles, nblk * nsub};
 }
+// The same sweep with each round's tiles dealt to the XCDs in contiguous segments: workgroup b runs
+// on XCD b % 8, so within a round XCD x takes tiles [x, x + 1) * (nblk / 8) * nsub and its
+// workgroups take consecutive nsub-tile groups of that segment.  Neighbouring tiles share the
+// cache lines of the payloads' run pieces (a 128-byte line of keys spans ~5 tiles of a C3 piece,
+// of bins ~20): dealt round-robin, each line was fetched into several XCDs' L2 (k_agg_vtiles_rmw
+// read 3.96 GB per 1.1 GB of elements, profiles/r05m_agg_pmc.json).  One write front per XCD.
+__device__ __forceinline__ TileWalk tile_walk_xcd(int64_t blk, int64_t nblk, int sub, int nsub, int64_t ntiles) {
+    if (nblk % 8 != 0) return tile_walk(blk, nblk, sub, nsub, ntiles);
+    return {(blk % 8) * (nblk / 8) * nsub + (blk / 8) * nsub + sub, ntiles, nblk * nsub};
+}
 __global__ __launch_bounds__(kAggThreads) void k_agg_tiles_w(const AggPayload* __restrict__ pays, int P,
                                                             int64_t ntiles, int64_t dim, double* __restrict__ out,
                                                             int from_out, double scale, unsigned* __restrict__ err) {
@@ -3543,6 +3553,7 @@ __global__ __launch_bounds__(kAggThreads) __attribute__((amdgpu_waves_per_eu(4))
     __shared__ int32_t pre[2][kWaves][65];
     __shared__ int32_t pk0[2][kWaves][64];
     __shared__ int32_t pn0[2][kWaves][64];
+    __shared__ __attribute__((aligned(8))) uint8_t pcs[kWaves][64 * kAggWPer];  // piece of element j
     __shared__ AggPayload pl[kAggPB];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (threadIdx.x < P * (int)(sizeof(AggPayload) / 8))
@@ -3582,12 +3593,32 @@ __global__ __launch_bounds__(kAggThreads) __attribute__((amdgpu_waves_per_eu(4))
             if (pre[buf][wave][s_ + step] <= j) s_ += step;
         return s_;
     };
+    // the pieces of the elements held in registers: lane l searches the piece of j = 8 l and walks
+    // on through j = 8 l + 7 (a piece holds ~6 elements of a C3 tile), into pcs; the loads then
+    // read the piece of j = l + 64 u back (one search per lane instead of one per element)
     auto load = [&](int buf, int total, int ln, int32_t (&kk)[kAggWPer], uint32_t (&bb)[kAggWPer]) {
+        {
+            const int j0 = kAggWPer * ln;
+            if (j0 < total) {
+                int s_ = piece_of(buf, j0);
+                uint32_t w0 = 0, w1 = 0;
+#pragma unroll
+                for (int u = 0; u < kAggWPer; u++) {
+                    const int j = j0 + u;
+                    if (j < total)
+                        while (pre[buf][wave][s_ + 1] <= j) s_++;
+                    if (u < 4) w0 |= (uint32_t)s_ << (8 * u);
+                    else w1 |= (uint32_t)s_ << (8 * (u - 4));
+                }
+                *reinterpret_cast<uint2*>(&pcs[wave][j0]) = make_uint2(w0, w1);
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
         int spc[kAggWPer];
 #pragma unroll
         for (int u = 0; u < kAggWPer; u++) {
             const int j = ln + 64 * u;
-            spc[u] = piece_of(buf, j < total ? j : 0);
+            spc[u] = j < total ? (int)pcs[wave][j] : 0;
         }
 #pragma unroll
         for (int u = 0; u < kAggWPer; u++) {
@@ -3624,7 +3655,8 @@ __global__ __launch_bounds__(kAggThreads) __attribute__((amdgpu_waves_per_eu(4))
         __builtin_amdgcn_wave_barrier();
         prev_k0 = -1;
     };
-    const TileWalk tw = tile_walk(blockIdx.x, gridDim.x, wave, kWaves, ntiles);
+    // (elements prefetched two tiles ahead measured level: profiles/ab/r05_agg_prefetch2.txt)
+    const TileWalk tw = tile_walk_xcd(blockIdx.x, gridDim.x, wave, kWaves, ntiles);
     int buf = 0, total = 0;
     int32_t kk[kAggWPer], kn[kAggWPer];
     uint32_t bb[kAggWPer], bn[kAggWPer];
