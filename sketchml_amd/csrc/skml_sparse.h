@@ -163,10 +163,19 @@ hipError_t launch_group_prefix(hipStream_t st, const uint32_t* delta, int64_t n,
 // tnar is launch_narrow_table's image of `table` (int32 cells outside [0, 2^width - 1) read back
 // from `table`); width 32: `table` alone (nullptr with gp->rows == 0: keys only).  gbins may be
 // null; gvals (optional) receives quantValues[bin] from qv[nq], a bin outside it sets *err
+// Gradient.sum's run bounds written by the key query itself (k_agg_bounds' job): bounds[g *
+// (ntiles + 1) + t] = the first element of run g with key >= t << tile_bits (the run's end past
+// its last key); a key outside [0, dim) or not ascending inside its run sets *err bit 0.
+// bounds == nullptr: not written.
+struct RunBoundsOut {
+    int32_t* bounds;
+    int64_t ntiles, dim;
+    int tile_bits;
+};
 hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, const SpGroups* gp, const SpGroups& gh,
                            const uint64_t* tile_base, const uint64_t* gpre, const int32_t* table, const void* tnar,
                            int width, int32_t* gkeys, int32_t* gbins, int nq, void* gbn, int bn_width,
-                           unsigned* err);
+                           unsigned* err, RunBoundsOut rb = RunBoundsOut{nullptr, 0, 0, 0});
 // the narrow (width 8 or 16) image of int32 MinMax tables for k_dec_keys; t32 16-byte aligned
 hipError_t launch_narrow_table(hipStream_t st, const int32_t* t32, int64_t ncells, int width, void* tn);
 // live entries of a restored payload (skml_sparse_decode_sum_f64's toAuto choice)

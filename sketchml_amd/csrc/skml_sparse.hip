@@ -2483,7 +2483,7 @@ __device__ __forceinline__ void dec_keys_tile(int64_t n, const SpGroups* __restr
                                               int32_t* __restrict__ gbins, int nq, void* __restrict__ gbn,
                                               int bn_width, unsigned* __restrict__ err, const int64_t* S,
                                               uint64_t* sh, int64_t tile, const uint32_t (&d)[4], uint64_t tb,
-                                              int tid) {
+                                              int tid, const RunBoundsOut& rb) {
     const int t = tid, lane = t & 63, w = t >> 6;
     const int64_t i0 = tile * kSpTile + t * 4;
     // the tile's exclusive prefix of the deltas (64-bit: a tile's deltas may pass 2^32)
@@ -2495,6 +2495,7 @@ __device__ __forceinline__ void dec_keys_tile(int64_t n, const SpGroups* __restr
 #pragma unroll
     for (int j = 0; j < kDecThreads / 64; j++) p += j < w ? sh[j] : 0ull;
     if (i0 >= n) return;
+    const uint64_t p_before = p;  // the deltas' prefix through element i0 - 1
     const int zero = gp->zero, rows = gp->rows;
     int32_t key[4], res[4];
     int grp[4];
@@ -2520,6 +2521,31 @@ __device__ __forceinline__ void dec_keys_tile(int64_t n, const SpGroups* __restr
             key[j] = (int32_t)(uint32_t)(p - gpre[g]);
             res[j] = zero;
         }
+    }
+    if (rb.bounds) {  // Gradient.sum's run bounds (run_bounds16<true>'s rule), from the keys in hand
+        bool bad = false;
+        auto tile_of = [&](int32_t k) -> int64_t {
+            return k < 0 ? 0 : std::min<int64_t>((int64_t)(k >> rb.tile_bits), rb.ntiles);
+        };
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int64_t i = i0 + j;
+            if (i >= n) break;
+            const int g = grp[j];
+            const int64_t lo = S[g], hi = S[g + 1];
+            const int32_t k = key[j];
+            const bool first = i == lo;
+            // the element before, inside the same run when this one is not its first
+            const int32_t prev = j > 0 ? key[j - 1] : (int32_t)(uint32_t)(p_before - gpre[g]);
+            if (k < 0 || (int64_t)k >= rb.dim) bad = true;  // SparseDoubleGradient's bound check
+            if (!first && k <= prev) bad = true;            // keys ascend strictly inside a run
+            const int64_t ti = tile_of(k), pt = first ? -1 : tile_of(prev);
+            int32_t* b = rb.bounds + (int64_t)g * (rb.ntiles + 1);
+            for (int64_t t = pt + 1; t <= ti; t++) b[t] = (int32_t)i;
+            if (i == hi - 1)
+                for (int64_t t = ti + 1; t <= rb.ntiles; t++) b[t] = (int32_t)hi;
+        }
+        if (bad) atomicOr(err, 1u);
     }
     constexpr uint32_t kTop = sizeof(TN) == 4 ? 0u : (uint32_t)(TN)~(TN)0;
     auto cell_of = [&](int j, int r) -> int64_t {
@@ -2668,7 +2694,8 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_keys(const uint32_t* __rest
                                                           const int32_t* __restrict__ table, const TN* __restrict__ tnar,
                                                           int32_t* __restrict__ gkeys, int32_t* __restrict__ gbins,
                                                           int nq, void* __restrict__ gbn, int bn_width,
-                                                          unsigned* __restrict__ err, DecEdgeTiles edges) {
+                                                          unsigned* __restrict__ err, DecEdgeTiles edges,
+                                                          RunBoundsOut rb) {
     __shared__ int64_t S[kMaxGroups + 1];
     __shared__ uint64_t sh[kDecThreads / 64];
     load_starts(gp, S);
@@ -2695,7 +2722,7 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_keys(const uint32_t* __rest
         for (int j = 0; j < 4; j++) d[j] = i0 + j < n ? delta[i0 + j] : 0u;
     }
     dec_keys_tile<TN, MODE, NT>(n, gp, gpre, table, tnar, gkeys, gbins, nq, gbn, bn_width, err, S, sh, tile, d,
-                                tile_base[tile], (int)threadIdx.x);
+                                tile_base[tile], (int)threadIdx.x, rb);
 }
 
 // MODE 1 over every inner tile with persistent workgroups: workgroup b walks the tiles that
@@ -2709,7 +2736,8 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_keys_p(const uint32_t* __re
                                                             const int32_t* __restrict__ table,
                                                             const TN* __restrict__ tnar, int32_t* __restrict__ gkeys,
                                                             int32_t* __restrict__ gbins, int nq, void* __restrict__ gbn,
-                                                            int bn_width, unsigned* __restrict__ err, int64_t per_slot) {
+                                                            int bn_width, unsigned* __restrict__ err, int64_t per_slot,
+                                                            RunBoundsOut rb) {
     __shared__ int64_t S[kMaxGroups + 1];
     __shared__ uint64_t sh[2][kDecThreads / 64];
     load_starts(gp, S);
@@ -2750,7 +2778,7 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_keys_p(const uint32_t* __re
         int tid = threadIdx.x;  // thread-derived values rematerialised per tile (hoisted, they cost registers)
         asm volatile("" : "+v"(tid));
         dec_keys_tile<TN, 1, NT>(n, gp, gpre, table, tnar, gkeys, gbins, nq, gbn, bn_width, err, S, sh[par], tile, d,
-                                 tb, tid);
+                                 tb, tid, rb);
         // (dec_keys_tile returns early past n, after its barrier; every thread of the workgroup
         // still runs the same iterations)
         tile = next;
@@ -2777,7 +2805,7 @@ static int resident_blocks(K kern, int threads) {
 hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, const SpGroups* gp, const SpGroups& gh,
                            const uint64_t* tile_base, const uint64_t* gpre, const int32_t* table, const void* tnar,
                            int width, int32_t* gkeys, int32_t* gbins, int nq, void* gbn, int bn_width,
-                           unsigned* err) {
+                           unsigned* err, RunBoundsOut rb) {
     if (sp_tiles(n, kSpTile) <= 0) return hipSuccess;
     int64_t per[8] = {};  // tiles per XCD slot (dec_tile_of_block)
     for (int g = 0; g < gh.G; g++) {
@@ -2805,7 +2833,7 @@ hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, con
     // nontemporal streams (decode 0.73 -> 0.71 ms, profiles/ab/r04_sparse_restore_aggregate.txt)
 #define SKML_DEC_LAUNCH(TNT, MODE, GRID, TILES, TNPTR)                                                            \
     hipLaunchKernelGGL((k_dec_keys<TNT, MODE>), dim3(GRID), dim3(kDecThreads), 0, st, delta, n, gp, tile_base, gpre, \
-                       table, TNPTR, gkeys, gbins, nq, gbn, bn_width, err, TILES)
+                       table, TNPTR, gkeys, gbins, nq, gbn, bn_width, err, TILES, rb)
     // MODE 1 with one workgroup per tile; SKML_FORM_DEC_ROWS_SERIAL = 2 selects persistent
     // workgroups with the next tile's deltas in flight (measured slower at 2^28: restore 0.767
     // vs 0.707 ms, profiles/ab/r05_decp.txt; kept as an A/B form)
@@ -2816,11 +2844,11 @@ hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, con
             static const int res = resident_blocks(k_dec_keys_p<TNT, true>, kDecThreads); \
             const int64_t ps = res > 0 ? std::max<int64_t>(1, std::min<int64_t>(most, res / 8)) : most; \
             hipLaunchKernelGGL((k_dec_keys_p<TNT, true>), dim3((unsigned)(8 * ps)), dim3(kDecThreads), 0, st, delta, \
-                               n, gp, tile_base, gpre, table, TNPTR, gkeys, gbins, nq, gbn, bn_width, err, most); \
+                               n, gp, tile_base, gpre, table, TNPTR, gkeys, gbins, nq, gbn, bn_width, err, most, rb); \
             if (edges.n > 0) SKML_DEC_LAUNCH(TNT, 0, (unsigned)edges.n, edges, TNPTR);    \
         } else if (batched) {                                                             \
             hipLaunchKernelGGL((k_dec_keys<TNT, 1, true>), dim3(grid), dim3(kDecThreads), 0, st, delta, n, gp,    \
-                               tile_base, gpre, table, TNPTR, gkeys, gbins, nq, gbn, bn_width, err, all);    \
+                               tile_base, gpre, table, TNPTR, gkeys, gbins, nq, gbn, bn_width, err, all, rb); \
             if (edges.n > 0) SKML_DEC_LAUNCH(TNT, 0, (unsigned)edges.n, edges, TNPTR);    \
         } else {                                                                          \
             SKML_DEC_LAUNCH(TNT, 0, grid, all, TNPTR);                                    \

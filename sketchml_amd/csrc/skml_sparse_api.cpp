@@ -586,11 +586,13 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const void* vals, bool f64, int6
 // DeltaAdaptive decode of all groups + MinMax query: grouped keys/bins into gk/gb.
 // DecodeValues: Gradient.sum's restore writes narrow bins (bw bytes: 1 for bin_num <= 256, else 2)
 // into gb for the tiled sum, which looks quantValues up itself; a bin outside the nq values sets *err.
+// rb: the tiles' run bounds, written by the query too (rb.bounds nullptr: not).
 struct DecodeValues {
     int nq;
     void* gb;
     int bw;
     unsigned* err;
+    RunBoundsOut rb;
 };
 int decode_groups(skml_ctx* c, const skml_sparse* s, int32_t* gk, int32_t* gb, bool query,
                   const DecodeValues* dv = nullptr) {
@@ -633,7 +635,8 @@ int decode_groups(skml_ctx* c, const skml_sparse* s, int32_t* gk, int32_t* gb, b
         SP_HIP(launch_narrow_table(st, tab, s->ncells, width, tnar));
     }
     SP_HIP(launch_dec_keys(st, delta, n, s->g_dev, G, ts2, gpre, tab, tnar, width, gk, gb, dv ? dv->nq : 0,
-                           dv ? dv->gb : nullptr, dv ? dv->bw : 0, dv ? dv->err : nullptr));
+                           dv ? dv->gb : nullptr, dv ? dv->bw : 0, dv ? dv->err : nullptr,
+                           dv ? dv->rb : RunBoundsOut{nullptr, 0, 0, 0}));
     return SKML_OK;
 }
 
@@ -1986,7 +1989,12 @@ int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t
             a.G = v.g.G;
             a.gk_off = (int32_t)ko;   // < 2^31: the batch's keys fit the 3 GB scratch budget
             a.gb_off = (int32_t)bbo;
-            const DecodeValues dv{a.nq, const_cast<void*>(a.gb), a.bw, err};
+            // the run bounds come from the key query unless SKML_FORM_AGG_BOUNDS = 1 asks for the
+            // separate k_agg_bounds pass (A/B)
+            const bool own_pass = form(SKML_FORM_AGG_BOUNDS) == 1;
+            const DecodeValues dv{a.nq, const_cast<void*>(a.gb), a.bw, err,
+                                  own_pass ? RunBoundsOut{nullptr, 0, 0, 0}
+                                           : RunBoundsOut{const_cast<int32_t*>(a.bounds), ntiles, dim, tile_bits}};
             auto join = [&](int e) {  // an error after the fork: the caller's stream still waits for the side
                 if (lanes[1]) {
                     (void)hipEventRecord(ev_join, side_st);
@@ -2002,8 +2010,8 @@ int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t
                 if (int e = sync_to_host(lc, &nlive, llive, sizeof(nlive))) return join(e);
                 a.dense_form = (int64_t)nlive > lim ? 1 : 0;
             }
-            if (launch_agg_bounds(ls, a.gk, v.nnz, v.g_dev, ntiles, dim, const_cast<int32_t*>(a.bounds), err,
-                                  tile_bits) != hipSuccess)
+            if (own_pass && launch_agg_bounds(ls, a.gk, v.nnz, v.g_dev, ntiles, dim, const_cast<int32_t*>(a.bounds), err,
+                                              tile_bits) != hipSuccess)
                 return join(sfail(SKML_E_HIP, "agg_bounds launch failed"));
             pays.push_back(a);
             ko += key_words(p);
