@@ -163,14 +163,18 @@ hipError_t launch_group_prefix(hipStream_t st, const uint32_t* delta, int64_t n,
 // tnar is launch_narrow_table's image of `table` (int32 cells outside [0, 2^width - 1) read back
 // from `table`); width 32: `table` alone (nullptr with gp->rows == 0: keys only).  gbins may be
 // null; gvals (optional) receives quantValues[bin] from qv[nq], a bin outside it sets *err
-// Gradient.sum's run bounds written by the key query itself (k_agg_bounds' job): bounds[g *
-// (ntiles + 1) + t] = the first element of run g with key >= t << tile_bits (the run's end past
-// its last key); a key outside [0, dim) or not ascending inside its run sets *err bit 0.
+// The runs' bounds written by the key query itself.  info == nullptr: Gradient.sum's tiles
+// (k_agg_bounds' job): bounds[g * (ntiles + 1) + t] = the first element of run g with key >= t <<
+// tile_bits (the run's end past its last key); a key outside [0, dim) or not ascending inside its
+// run sets *err bit 0.  info != nullptr: the one-pass Sort.merge's key ranges (k_rs_bounds' job,
+// kRsRanges + 1 per run, RsInfo's last ranges and irregular flag; *info zeroed before).
 // bounds == nullptr: not written.
+struct RsInfo;
 struct RunBoundsOut {
     int32_t* bounds;
     int64_t ntiles, dim;
     int tile_bits;
+    RsInfo* info = nullptr;
 };
 hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, const SpGroups* gp, const SpGroups& gh,
                            const uint64_t* tile_base, const uint64_t* gpre, const int32_t* table, const void* tnar,
@@ -246,7 +250,7 @@ struct RsInfo {
 };
 hipError_t launch_rs_merge(hipStream_t st, const int32_t* gk, const int32_t* gb, int64_t n, const SpGroups* gp,
                            int32_t* bounds, RsInfo* info, int32_t* keys_out, void* out, int vkind, const double* qv,
-                           int nq);
+                           int nq, bool bounds_ready);  // bounds_ready: the key query wrote bounds and *info
 hipError_t launch_merge_round(hipStream_t st, const int32_t* kin, const int32_t* bin_in, int32_t* kout,
                               int32_t* bout, const int64_t* run_start, int nruns, int64_t total, int64_t* split);
 // values[bins[i]] from the double quantValues LUT (SparseVectorCompressor.java:118-126); a bin

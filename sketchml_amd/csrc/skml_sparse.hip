@@ -2522,9 +2522,12 @@ __device__ __forceinline__ void dec_keys_tile(int64_t n, const SpGroups* __restr
             res[j] = zero;
         }
     }
-    if (rb.bounds) {  // Gradient.sum's run bounds (run_bounds16<true>'s rule), from the keys in hand
+    if (rb.bounds) {  // the runs' bounds (run_bounds16's rules), from the keys in hand
+        const bool rs = rb.info != nullptr;  // Sort.merge's key ranges, else Gradient.sum's tiles
+        const int64_t ld = rs ? kRsRanges + 1 : rb.ntiles + 1;
         bool bad = false;
         auto tile_of = [&](int32_t k) -> int64_t {
+            if (rs) return (int64_t)(k >> kRsBits);
             return k < 0 ? 0 : std::min<int64_t>((int64_t)(k >> rb.tile_bits), rb.ntiles);
         };
 #pragma unroll
@@ -2537,15 +2540,30 @@ __device__ __forceinline__ void dec_keys_tile(int64_t n, const SpGroups* __restr
             const bool first = i == lo;
             // the element before, inside the same run when this one is not its first
             const int32_t prev = j > 0 ? key[j - 1] : (int32_t)(uint32_t)(p_before - gpre[g]);
-            if (k < 0 || (int64_t)k >= rb.dim) bad = true;  // SparseDoubleGradient's bound check
-            if (!first && k <= prev) bad = true;            // keys ascend strictly inside a run
-            const int64_t ti = tile_of(k), pt = first ? -1 : tile_of(prev);
-            int32_t* b = rb.bounds + (int64_t)g * (rb.ntiles + 1);
-            for (int64_t t = pt + 1; t <= ti; t++) b[t] = (int32_t)i;
-            if (i == hi - 1)
-                for (int64_t t = ti + 1; t <= rb.ntiles; t++) b[t] = (int32_t)hi;
+            bool ok = true;
+            if (rs) {  // the one-pass merge's regular input (else the merge rounds run)
+                ok = !(k < 0 || k == INT32_MAX || (!first && k <= prev));
+                bad |= !ok;
+            } else {
+                if (k < 0 || (int64_t)k >= rb.dim) bad = true;  // SparseDoubleGradient's bound check
+                if (!first && k <= prev) bad = true;            // keys ascend strictly inside a run
+            }
+            if (ok) {
+                const int64_t ti = tile_of(k), pt = first || (rs && prev < 0) ? -1 : tile_of(prev);
+                int32_t* b = rb.bounds + (int64_t)g * ld;
+                for (int64_t t = pt + 1; t <= ti; t++) b[t] = (int32_t)i;
+                if (i == hi - 1) {
+                    if (rs) {  // the run's last range ends at the run's end
+                        b[ti + 1] = (int32_t)hi;
+                        rb.info->tlast1[g] = (int32_t)ti + 1;
+                        atomicMax(&rb.info->tmax1, (int32_t)ti + 1);
+                    } else {
+                        for (int64_t t = ti + 1; t <= rb.ntiles; t++) b[t] = (int32_t)hi;
+                    }
+                }
+            }
         }
-        if (bad) atomicOr(err, 1u);
+        if (bad) atomicOr(rs ? &rb.info->irregular : err, 1u);
     }
     constexpr uint32_t kTop = sizeof(TN) == 4 ? 0u : (uint32_t)(TN)~(TN)0;
     auto cell_of = [&](int j, int r) -> int64_t {
@@ -4354,10 +4372,11 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_merge_pf(const int32_t* __res
 
 hipError_t launch_rs_merge(hipStream_t st, const int32_t* gk, const int32_t* gb, int64_t n, const SpGroups* gp,
                            int32_t* bounds, RsInfo* info, int32_t* keys_out, void* out, int vkind, const double* qv,
-                           int nq) {
+                           int nq, bool bounds_ready) {
     if (n <= 0) return hipSuccess;
     const int64_t bgrid = sp_tiles(sp_tiles(n, 16), kSpThreads);
-    hipLaunchKernelGGL(k_rs_bounds, dim3((unsigned)bgrid), dim3(kSpThreads), 0, st, gk, n, gp, bounds, info);
+    if (!bounds_ready)
+        hipLaunchKernelGGL(k_rs_bounds, dim3((unsigned)bgrid), dim3(kSpThreads), 0, st, gk, n, gp, bounds, info);
     // persistent workgroups over the key ranges up to the largest key (read on the device): as many
     // as are resident at once (4 per CU), fewer for small inputs
     const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(sp_tiles(n, 4096), 1), 1024);

@@ -595,7 +595,7 @@ struct DecodeValues {
     RunBoundsOut rb;
 };
 int decode_groups(skml_ctx* c, const skml_sparse* s, int32_t* gk, int32_t* gb, bool query,
-                  const DecodeValues* dv = nullptr) {
+                  const DecodeValues* dv = nullptr, const RunBoundsOut* rbo = nullptr) {
     hipStream_t st = ctx_stream(c);
     const SpGroups& G = s->g;
     const int64_t n = s->nnz;
@@ -636,7 +636,7 @@ int decode_groups(skml_ctx* c, const skml_sparse* s, int32_t* gk, int32_t* gb, b
     }
     SP_HIP(launch_dec_keys(st, delta, n, s->g_dev, G, ts2, gpre, tab, tnar, width, gk, gb, dv ? dv->nq : 0,
                            dv ? dv->gb : nullptr, dv ? dv->bw : 0, dv ? dv->err : nullptr,
-                           dv ? dv->rb : RunBoundsOut{nullptr, 0, 0, 0}));
+                           dv ? dv->rb : rbo ? *rbo : RunBoundsOut{nullptr, 0, 0, 0}));
     return SKML_OK;
 }
 
@@ -689,6 +689,11 @@ thread_local int t_merge_path = 0;  // skml_debug_sparse_merge_path
 struct RsMerge {
     RsInfo* info = nullptr;
     int32_t* bounds = nullptr;
+    bool by_query = false;  // the key query writes the bounds (query_bounds); else k_rs_bounds
+    RunBoundsOut query_bounds() {
+        by_query = info && form(SKML_FORM_RUN_BOUNDS) != 1;
+        return RunBoundsOut{by_query ? bounds : nullptr, 0, 0, kRsBits, info};
+    }
 };
 int rs_merge_prepare(skml_ctx* c, const skml_sparse* s, RsMerge* m) {
     *m = RsMerge{};
@@ -713,7 +718,7 @@ int rs_merge_start(skml_ctx* c, const skml_sparse* s, const RsMerge& m, const in
     hipStream_t st = ctx_stream(c);
     unsigned* pin = static_cast<unsigned*>(ctx_pinned(c, 64));
     if (!pin) return sfail(SKML_E_OOM, "merge scratch");
-    SP_HIP(launch_rs_merge(st, gk, gb, s->nnz, s->g_dev, m.bounds, m.info, keys_out, out, vkind, qv, nq));
+    SP_HIP(launch_rs_merge(st, gk, gb, s->nnz, s->g_dev, m.bounds, m.info, keys_out, out, vkind, qv, nq, m.by_query));
     SP_HIP(hipMemcpyAsync(pin, &m.info->irregular, sizeof(unsigned), hipMemcpyDeviceToHost, st));
     *pending = pin;
     return SKML_OK;
@@ -831,7 +836,8 @@ int decode_values(skml_ctx* c, const skml_sparse* s, int32_t* keys_dev, T* vals_
     SP_HIP(hipMemcpyAsync(qv, s->qvalues.data(), sizeof(double) * s->qvalues.size(), hipMemcpyHostToDevice, st));
     RsMerge rm;
     if (int e = rs_merge_prepare(c, s, &rm)) return e;
-    if (int e = decode_groups(c, s, gk, gb, true)) return e;
+    const RunBoundsOut rbo = rm.query_bounds();  // the merge's key-range bounds from the query
+    if (int e = decode_groups(c, s, gk, gb, true, nullptr, &rbo)) return e;
     // pairwise merge rounds, then quantValues[bin]; a bin outside the nq values (Java: index out
     // of bounds) fails the decode (the one-pass merge sends such input here too)
     auto rounds = [&]() -> int {
@@ -1644,7 +1650,8 @@ int skml_sparse_restore_bins(skml_ctx* c, const skml_sparse* s, int32_t* keys_de
     if (!gk || !gb) return sfail(SKML_E_OOM, "restore scratch");
     RsMerge rm;
     if (int e = rs_merge_prepare(c, s, &rm)) return e;
-    if (int e = decode_groups(c, s, gk, gb, true)) return e;
+    const RunBoundsOut rbo = rm.query_bounds();  // the merge's key-range bounds from the query
+    if (int e = decode_groups(c, s, gk, gb, true, nullptr, &rbo)) return e;
     volatile unsigned* pending = nullptr;
     if (int e = rs_merge_start(c, s, rm, gk, gb, keys_dev, bins_dev, 0, nullptr, 0, &pending)) return e;
     if (!pending)
@@ -1989,9 +1996,9 @@ int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t
             a.G = v.g.G;
             a.gk_off = (int32_t)ko;   // < 2^31: the batch's keys fit the 3 GB scratch budget
             a.gb_off = (int32_t)bbo;
-            // the run bounds come from the key query unless SKML_FORM_AGG_BOUNDS = 1 asks for the
+            // the run bounds come from the key query unless SKML_FORM_RUN_BOUNDS = 1 asks for the
             // separate k_agg_bounds pass (A/B)
-            const bool own_pass = form(SKML_FORM_AGG_BOUNDS) == 1;
+            const bool own_pass = form(SKML_FORM_RUN_BOUNDS) == 1;
             const DecodeValues dv{a.nq, const_cast<void*>(a.gb), a.bw, err,
                                   own_pass ? RunBoundsOut{nullptr, 0, 0, 0}
                                            : RunBoundsOut{const_cast<int32_t*>(a.bounds), ntiles, dim, tile_bits}};

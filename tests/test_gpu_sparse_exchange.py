@@ -132,7 +132,7 @@ def test_restore_values_refuse_bins_outside_quant_values(gpu, bins, forms):
 # other shape) and wave_serial (the wave tiles with the generic per-row MinMax query and one
 # stream); vtile2 / vtile4 take two / four staged tiles per wave round (one round of element
 # loads); vtile_pf loads the next tile's elements while a tile is summed.  Every form is exact, and every form refuses a key repeated across a payload's groups.
-KERNELS = {"vtile_rmw": {}, "vtile_rmw_bounds_pass": {"agg_bounds": 1}, "vtile_pf": {"agg_tiles": 4},
+KERNELS = {"vtile_rmw": {}, "vtile_rmw_bounds_pass": {"run_bounds": 1}, "vtile_pf": {"agg_tiles": 4},
            "vtile": {"agg_tiles": 5}, "vtile2": {"agg_tiles": 3}, "vtile4": {"agg_tiles": 2},
            "wave": {"agg_tiles": 1},
            "wave_serial": {"agg_tiles": 1, "dec_rows_serial": 1, "agg_one_lane": 1}}
