@@ -151,9 +151,17 @@ hipError_t launch_unary_count(hipStream_t st, const uint64_t* flag_words, int64_
                               const SpGroups* gp, uint64_t* tile_sums);
 hipError_t launch_unary_select(hipStream_t st, const uint64_t* flag_words, int64_t nwords,
                                const SpGroups* gp, const uint64_t* tile_base, int64_t* end_pos);
+// the narrow table image k_dec_keys gathers from (launch_narrow_table's job), built by extra blocks
+// of the k_dec_lens launch beside the lengths; tn == nullptr: none
+struct NarrowJob {
+    const int32_t* t32;
+    int64_t ncells;
+    void* tn;
+    int width;
+};
 hipError_t launch_dec_lens(hipStream_t st, const uint64_t* flag_words, int64_t n_flag_words,
                            const int64_t* end_pos, int64_t n, const SpGroups* gp, uint8_t* dlen,
-                           uint64_t* tile_sums);
+                           uint64_t* tile_sums, NarrowJob nj = NarrowJob{nullptr, 0, nullptr, 0});
 hipError_t launch_dec_deltas(hipStream_t st, const uint64_t* delta_words, int64_t n_delta_words,
                              const uint8_t* dlen, int64_t n, const SpGroups* gp,
                              const uint64_t* tile_base, uint32_t* delta, uint64_t* tile_sums);

@@ -2254,10 +2254,31 @@ __device__ __forceinline__ uint64_t word_or_zero(const uint64_t* __restrict__ wo
     return w < nwords ? words[w] : 0ull;
 }
 
+template <typename TN>
+__device__ __forceinline__ void narrow_cells(const int32_t* __restrict__ t32, int64_t ncells, TN* __restrict__ tn,
+                                             int64_t blk) {
+    constexpr uint32_t kTop = (uint32_t)(TN)~(TN)0;
+    const int64_t i0 = (blk * kSpThreads + threadIdx.x) * 4;
+    if (i0 + 4 <= ncells) {
+        const int4 v = *reinterpret_cast<const int4*>(t32 + i0);
+        const int32_t e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; j++) tn[i0 + j] = (TN)((uint32_t)e[j] < kTop ? (uint32_t)e[j] : kTop);
+    } else {
+        for (int64_t i = i0; i < ncells; i++) tn[i] = (TN)((uint32_t)t32[i] < kTop ? (uint32_t)t32[i] : kTop);
+    }
+}
 __global__ __launch_bounds__(kSpThreads) void k_dec_lens(const uint64_t* __restrict__ fw, int64_t nfw,
                                                          const int64_t* __restrict__ end_pos, int64_t n,
                                                          const SpGroups* __restrict__ gp, uint8_t* __restrict__ dlen,
-                                                         uint64_t* __restrict__ tile_sums) {
+                                                         uint64_t* __restrict__ tile_sums, int64_t nlens,
+                                                         NarrowJob nj) {
+    if ((int64_t)blockIdx.x >= nlens) {  // the blocks past the lengths' tiles build the narrow table
+        const int64_t b = (int64_t)blockIdx.x - nlens;
+        if (nj.width == 8) narrow_cells<uint8_t>(nj.t32, nj.ncells, static_cast<uint8_t*>(nj.tn), b);
+        else narrow_cells<uint16_t>(nj.t32, nj.ncells, static_cast<uint16_t*>(nj.tn), b);
+        return;
+    }
     __shared__ int64_t S[kMaxGroups + 1];
     __shared__ uint64_t sh[4];
     load_starts(gp, S);
@@ -2309,11 +2330,13 @@ __global__ __launch_bounds__(kSpThreads) void k_dec_lens(const uint64_t* __restr
 
 hipError_t launch_dec_lens(hipStream_t st, const uint64_t* flag_words, int64_t n_flag_words,
                            const int64_t* end_pos, int64_t n, const SpGroups* gp, uint8_t* dlen,
-                           uint64_t* tile_sums) {
+                           uint64_t* tile_sums, NarrowJob nj) {
     const int64_t tiles = sp_tiles(n, kSpTile);
-    if (tiles <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_dec_lens, dim3((unsigned)tiles), dim3(kSpThreads), 0, st, flag_words, n_flag_words,
-                       end_pos, n, gp, dlen, tile_sums);
+    if (tiles <= 0) return nj.tn ? launch_narrow_table(st, nj.t32, nj.ncells, nj.width, nj.tn) : hipSuccess;
+    if (nj.tn && (reinterpret_cast<uintptr_t>(nj.t32) & 15) != 0) return hipErrorInvalidValue;
+    const int64_t nn = nj.tn && nj.ncells > 0 ? sp_tiles(nj.ncells, (int64_t)kSpThreads * 4) : 0;
+    hipLaunchKernelGGL(k_dec_lens, dim3((unsigned)(tiles + nn)), dim3(kSpThreads), 0, st, flag_words, n_flag_words,
+                       end_pos, n, gp, dlen, tile_sums, tiles, nj);
     return hipGetLastError();
 }
 
@@ -2415,16 +2438,7 @@ hipError_t launch_group_prefix(hipStream_t st, const uint32_t* delta, int64_t n,
 template <typename TN>
 __global__ __launch_bounds__(kSpThreads) void k_narrow_table(const int32_t* __restrict__ t32, int64_t ncells,
                                                              TN* __restrict__ tn) {
-    constexpr uint32_t kTop = (uint32_t)(TN)~(TN)0;
-    const int64_t i0 = ((int64_t)blockIdx.x * kSpThreads + threadIdx.x) * 4;
-    if (i0 + 4 <= ncells) {
-        const int4 v = *reinterpret_cast<const int4*>(t32 + i0);
-        const int32_t e[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int j = 0; j < 4; j++) tn[i0 + j] = (TN)((uint32_t)e[j] < kTop ? (uint32_t)e[j] : kTop);
-    } else {
-        for (int64_t i = i0; i < ncells; i++) tn[i] = (TN)((uint32_t)t32[i] < kTop ? (uint32_t)t32[i] : kTop);
-    }
+    narrow_cells<TN>(t32, ncells, tn, blockIdx.x);
 }
 
 hipError_t launch_narrow_table(hipStream_t st, const int32_t* t32, int64_t ncells, int width, void* tn) {

@@ -619,12 +619,8 @@ int decode_groups(skml_ctx* c, const skml_sparse* s, int32_t* gk, int32_t* gb, b
     uint8_t* dlen = scratch<uint8_t>(c, kSlotNeed, (size_t)n);
     uint32_t* delta = scratch<uint32_t>(c, kSlotDelta, (size_t)n);
     if (!dlen || !delta) return sfail(SKML_E_OOM, "decode scratch");
-    SP_HIP(launch_dec_lens(st, s->flag_words, s->n_flag_words, end_pos, n, s->g_dev, dlen, ts));
-    if (int e = scan_tiles(c, ts, tiles, 1, nullptr)) return e;
-    SP_HIP(launch_dec_deltas(st, s->delta_words, s->n_delta_words, dlen, n, s->g_dev, ts, delta, ts2));
-    if (int e = scan_tiles(c, ts2, tiles, 1, nullptr)) return e;
-    SP_HIP(launch_group_prefix(st, delta, n, s->g_dev, G.G, ts2, gpre));
-    // the query gathers from a byte (binNum <= 256) or 16-bit image of the tables
+    // the query gathers from a byte (binNum <= 256) or 16-bit image of the tables, built by extra
+    // blocks of the lengths' launch
     const int32_t* tab = query ? s->tables : nullptr;
     int width = 32;
     void* tnar = nullptr;
@@ -632,8 +628,13 @@ int decode_groups(skml_ctx* c, const skml_sparse* s, int32_t* gk, int32_t* gb, b
         width = G.bin_num <= 256 ? 8 : 16;  // any width gives the same bins (the sentinel reads back)
         tnar = ctx_scratch(c, kSlotNarrowTab, (size_t)s->ncells * (size_t)(width / 8));
         if (!tnar) return sfail(SKML_E_OOM, "decode scratch (table image)");
-        SP_HIP(launch_narrow_table(st, tab, s->ncells, width, tnar));
     }
+    SP_HIP(launch_dec_lens(st, s->flag_words, s->n_flag_words, end_pos, n, s->g_dev, dlen, ts,
+                           NarrowJob{tab, s->ncells, tnar, width}));
+    if (int e = scan_tiles(c, ts, tiles, 1, nullptr)) return e;
+    SP_HIP(launch_dec_deltas(st, s->delta_words, s->n_delta_words, dlen, n, s->g_dev, ts, delta, ts2));
+    if (int e = scan_tiles(c, ts2, tiles, 1, nullptr)) return e;
+    SP_HIP(launch_group_prefix(st, delta, n, s->g_dev, G.G, ts2, gpre));
     SP_HIP(launch_dec_keys(st, delta, n, s->g_dev, G, ts2, gpre, tab, tnar, width, gk, gb, dv ? dv->nq : 0,
                            dv ? dv->gb : nullptr, dv ? dv->bw : 0, dv ? dv->err : nullptr,
                            dv ? dv->rb : rbo ? *rbo : RunBoundsOut{nullptr, 0, 0, 0}));
