@@ -3608,7 +3608,9 @@ __global__ __launch_bounds__(kAggThreads) __attribute__((amdgpu_waves_per_eu(4))
     double scale, unsigned* __restrict__ err, const int32_t* __restrict__ kbase, const uint8_t* __restrict__ bbase) {
     constexpr int kWaves = kAggThreads / 64;
     __shared__ __attribute__((aligned(16))) double tsum[kWaves][kAggVTile];
-    __shared__ uint32_t here[kWaves][kAggPB][kAggVTile / 32];
+    // presence bits of the payload being added: key x at word x % 64, bit x / 64 (a pass's 64
+    // random keys spread over 64 words: few lanes share a word's atomic), cleared at each payload
+    __shared__ uint32_t here[kWaves][64];
     __shared__ double qt[kAggPB][kAggLdsValues];
     __shared__ int32_t pre[2][kWaves][65];
     __shared__ int32_t pk0[2][kWaves][64];
@@ -3627,7 +3629,7 @@ __global__ __launch_bounds__(kAggThreads) __attribute__((amdgpu_waves_per_eu(4))
     const int32_t* bd = lane_on ? pl[pl_l].bounds + (int64_t)g_l * (ntiles + 1) : nullptr;
     const int32_t gk_off = lane_on ? pl[pl_l].gk_off : 0, gb_off = lane_on ? pl[pl_l].gb_off : 0;
     double* T = tsum[wave];
-    uint32_t(*H)[kAggVTile / 32] = here[wave];
+    uint32_t* H = here[wave];
     unsigned bad = 0;
     int32_t nb0 = 0, nb1 = 0;
     auto fetch = [&](int64_t tt) {
@@ -3705,6 +3707,10 @@ __global__ __launch_bounds__(kAggThreads) __attribute__((amdgpu_waves_per_eu(4))
                 v.x = __dmul_rn(v.x, scale);
                 v.y = __dmul_rn(v.y, scale);
             }
+#ifdef SKML_ABLATE_AGG_STORE  // timing ablation only (no sums written): the sum's stores priced
+            if (v.x == 12345.678) o[x] = v.y;
+            continue;
+#endif
             if (whole) {
                 *reinterpret_cast<double2*>(o + x) = v;
             } else {
@@ -3749,22 +3755,32 @@ __global__ __launch_bounds__(kAggThreads) __attribute__((amdgpu_waves_per_eu(4))
             }
             *reinterpret_cast<double2*>(T + 8 * ln + 2 * q) = v;
         }
-        reinterpret_cast<uint64_t*>(H)[ln] = 0;
-        __builtin_amdgcn_wave_barrier();
+        int p_last = -1;  // the payload whose presence bits H holds (wave-uniform)
+        const int32_t k0i = (int32_t)k0;  // dim <= 2^31: tile starts fit int32
         // one row of elements (lane l: element j = l + 64 u), payload by payload
         auto add_row = [&](bool act, int p_el, int32_t k, uint32_t b) {
             uint64_t rem = __ballot(act);
             while (rem) {
                 const int first = __ffsll((unsigned long long)rem) - 1;
                 const int pcur = __builtin_amdgcn_readlane(p_el, first);
+                if (pcur != p_last) {  // a new payload: its own presence bits
+                    H[ln] = 0u;
+                    __builtin_amdgcn_wave_barrier();
+                    p_last = pcur;
+                }
                 const bool mine = act && p_el == pcur;
+#ifdef SKML_ABLATE_AGG_RMW  // timing ablation only (wrong sums): the adds into the tile priced
+                if (mine && k == INT32_MIN) bad |= 4u;
+                rem &= ~__ballot(mine);
+                continue;
+#endif
                 if (mine) {
-                    if (k < k0 || (int64_t)k >= k0 + nk) {  // k_agg_bounds placed it here: an error
+                    const int32_t xk = k - k0i;
+                    if ((uint32_t)xk >= (uint32_t)nk) {  // k_agg_bounds' placement says otherwise: an error
                         bad |= 1u;
                     } else {
-                        const int xk = (int)(k - k0);
-                        const uint32_t bit = 1u << (xk & 31);
-                        if (atomicOr(&H[pcur][xk >> 5], bit) & bit) bad |= 2u;  // a key twice in one payload
+                        const uint32_t bit = 1u << (xk >> 6);
+                        if (atomicOr(&H[xk & 63], bit) & bit) bad |= 2u;  // a key twice in one payload
                         else T[xk] = T[xk] + qt[pcur][b];
                     }
                 }
