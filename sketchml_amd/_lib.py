@@ -168,7 +168,7 @@ lib = _load()
 # skml_debug_form ids (include/skml.h SKML_FORM_*): alternative kernel forms the tests force to run
 # each one against the oracle; every form gives the same results, 0 is the library's own choice.
 FORMS = {"leaf_split": 0, "decode_sum": 1, "part_ballot": 2, "rs_rounds": 3, "dec_rows_serial": 4,
-         "agg_tiles": 5, "agg_one_lane": 6, "run_bounds": 7}
+         "agg_tiles": 5, "agg_one_lane": 6, "run_bounds": 7, "dec_lookback": 8}
 
 
 @contextlib.contextmanager

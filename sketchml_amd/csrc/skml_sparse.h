@@ -165,6 +165,14 @@ hipError_t launch_dec_lens(hipStream_t st, const uint64_t* flag_words, int64_t n
 hipError_t launch_dec_deltas(hipStream_t st, const uint64_t* delta_words, int64_t n_delta_words,
                              const uint8_t* dlen, int64_t n, const SpGroups* gp,
                              const uint64_t* tile_base, uint32_t* delta, uint64_t* tile_sums);
+// lengths and deltas in one pass (decoupled look-back over the tiles' bit totals; status: 2 tiles
+// + 2 u64 of scratch, zeroed by the launch); tile_sums: the tiles' delta sums as launch_dec_deltas
+// writes them, or with scan_sums their exclusive scan and total (a second look-back), as
+// scan_tiles leaves them
+hipError_t launch_dec_lens_deltas(hipStream_t st, const uint64_t* flag_words, int64_t n_flag_words,
+                                  const int64_t* end_pos, int64_t n, const SpGroups* gp,
+                                  const uint64_t* delta_words, int64_t n_delta_words, uint32_t* delta,
+                                  uint64_t* tile_sums, uint64_t* status, NarrowJob nj, bool scan_sums);
 hipError_t launch_group_prefix(hipStream_t st, const uint32_t* delta, int64_t n, const SpGroups* gp, int G,
                                const uint64_t* tile_base, uint64_t* gpre);
 // keys and MinMax bins; gh: the host copy of *gp (the grid follows the group sizes).  width 8 / 16:
@@ -359,7 +367,7 @@ int ctx_side_fork(skml_ctx* c, hipStream_t* side, hipEvent_t* fork, hipEvent_t* 
 skml_ctx* ctx_side_ctx(skml_ctx* c);
 int ctx_device(skml_ctx* c);
 // grow-only device scratch buffer `slot` (< kScratchSlots) of at least `bytes`; null on failure
-constexpr int kScratchSlots = 20;
+constexpr int kScratchSlots = 24;
 void* ctx_scratch(skml_ctx* c, int slot, size_t bytes);
 // pinned host staging of at least `bytes`
 void* ctx_pinned(skml_ctx* c, size_t bytes);

@@ -2268,6 +2268,54 @@ __device__ __forceinline__ void narrow_cells(const int32_t* __restrict__ t32, in
         for (int64_t i = i0; i < ncells; i++) tn[i] = (TN)((uint32_t)t32[i] < kTop ? (uint32_t)t32[i] : kTop);
     }
 }
+// The DeltaAdaptive bit lengths of elements i0 .. i0 + 7 (flag stream -> interval -> bits per
+// delta) into l[], 0 past n; returns their sum.
+__device__ __forceinline__ uint64_t dec_lens8(const uint64_t* __restrict__ fw, int64_t nfw,
+                                              const int64_t* __restrict__ end_pos, int64_t n,
+                                              const SpGroups* __restrict__ gp, const int64_t* S, int64_t i0,
+                                              uint8_t (&l)[8]) {
+    uint64_t sum = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) l[j] = 0;
+    int gf = i0 < n ? group_of_elem(S, i0) : 0;
+    if (i0 + 8 <= n && i0 + 8 <= S[gf + 1] && !gp->kind[gf]) {
+        // the common case: 8 fixed-width flags of one group, at most 40 contiguous bits: two word
+        // loads instead of one or two per element
+        const DeltaShape s = delta_shape(gp, gf);
+        const int64_t b0 = gp->fb[gf] + (i0 - S[gf]) * s.nf;
+        const int64_t w = b0 >> 6;
+        const int sh = (int)(b0 & 63);
+        const uint64_t w0 = word_or_zero(fw, nfw, w), w1 = word_or_zero(fw, nfw, w + 1);
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int off = sh + j * s.nf;  // < 64 + 40
+            const uint32_t f = off < 64 ? bits_of_window(w0, w1, off, s.nf) : bits_of_window(w1, 0ull, off - 64, s.nf);
+            const int dl = s.bpi * ((int)f + 1);
+            l[j] = (uint8_t)dl;
+            sum += dl;
+        }
+    } else if (i0 < n) {
+        int g = gf;
+        DeltaShape s = delta_shape(gp, g);
+        for (int j = 0; j < 8; j++) {
+            const int64_t i = i0 + j;
+            if (i >= n) break;
+            while (i >= S[g + 1]) s = delta_shape(gp, ++g);
+            int iv;
+            if (!s.kind) {
+                iv = (int)get_bits(fw, nfw, gp->fb[g] + (i - S[g]) * s.nf, s.nf) + 1;
+            } else {
+                const int64_t start = i == S[g] ? gp->fb[g] : end_pos[i - 1] + 1;
+                iv = (int)(end_pos[i] - start);
+            }
+            const int dl = s.bpi * iv;
+            l[j] = (uint8_t)dl;
+            sum += dl;
+        }
+    }
+    return sum;
+}
+
 __global__ __launch_bounds__(kSpThreads) void k_dec_lens(const uint64_t* __restrict__ fw, int64_t nfw,
                                                          const int64_t* __restrict__ end_pos, int64_t n,
                                                          const SpGroups* __restrict__ gp, uint8_t* __restrict__ dlen,
@@ -2284,44 +2332,17 @@ __global__ __launch_bounds__(kSpThreads) void k_dec_lens(const uint64_t* __restr
     load_starts(gp, S);
     __syncthreads();
     const int64_t i0 = (int64_t)blockIdx.x * kSpTile + threadIdx.x * 8;
-    uint64_t sum = 0;
-    int gf = i0 < n ? group_of_elem(S, i0) : 0;
-    if (i0 + 8 <= n && i0 + 8 <= S[gf + 1] && !gp->kind[gf]) {
-        // the common case: 8 fixed-width flags of one group, at most 40 contiguous bits: two word
-        // loads instead of one or two per element, one 8-byte store of the lengths
-        const DeltaShape s = delta_shape(gp, gf);
-        const int64_t b0 = gp->fb[gf] + (i0 - S[gf]) * s.nf;
-        const int64_t w = b0 >> 6;
-        const int sh = (int)(b0 & 63);
-        const uint64_t w0 = word_or_zero(fw, nfw, w), w1 = word_or_zero(fw, nfw, w + 1);
+    uint8_t l[8];
+    const uint64_t sum = dec_lens8(fw, nfw, end_pos, n, gp, S, i0, l);
+    if (i0 + 8 <= n) {  // one 8-byte store of the lengths
         uint64_t packed = 0;
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const int off = sh + j * s.nf;  // < 64 + 40
-            const uint32_t f = off < 64 ? bits_of_window(w0, w1, off, s.nf) : bits_of_window(w1, 0ull, off - 64, s.nf);
-            const int dl = s.bpi * ((int)f + 1);
-            packed |= (uint64_t)(uint8_t)dl << (8 * j);
-            sum += dl;
-        }
+        for (int j = 0; j < 8; j++) packed |= (uint64_t)l[j] << (8 * j);
         *reinterpret_cast<uint64_t*>(dlen + i0) = packed;
-    } else if (i0 < n) {
-        int g = gf;
-        DeltaShape s = delta_shape(gp, g);
-        for (int j = 0; j < 8; j++) {
-            const int64_t i = i0 + j;
-            if (i >= n) break;
-            while (i >= S[g + 1]) s = delta_shape(gp, ++g);
-            int iv;
-            if (!s.kind) {
-                iv = (int)get_bits(fw, nfw, gp->fb[g] + (i - S[g]) * s.nf, s.nf) + 1;
-            } else {
-                const int64_t start = i == S[g] ? gp->fb[g] : end_pos[i - 1] + 1;
-                iv = (int)(end_pos[i] - start);
-            }
-            const int dl = s.bpi * iv;
-            dlen[i] = (uint8_t)dl;
-            sum += dl;
-        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+            if (i0 + j < n) dlen[i0 + j] = l[j];
     }
     uint64_t v[1] = {sum}, tot[1];
     block_excl_scan<1>(v, tot, sh);
@@ -2340,30 +2361,12 @@ hipError_t launch_dec_lens(hipStream_t st, const uint64_t* flag_words, int64_t n
     return hipGetLastError();
 }
 
-__global__ __launch_bounds__(kSpThreads) void k_dec_deltas(const uint64_t* __restrict__ dw, int64_t ndw,
-                                                           const uint8_t* __restrict__ dlen, int64_t n,
-                                                           const uint64_t* __restrict__ tile_base,
-                                                           uint32_t* __restrict__ delta, uint64_t* __restrict__ tile_sums) {
-    __shared__ uint64_t sh[4];
-    const int64_t i0 = (int64_t)blockIdx.x * kSpTile + threadIdx.x * 8;
-    uint8_t l[8];
-    uint64_t sum = 0;
-    const bool full = i0 + 8 <= n;
-    if (full) {  // one 8-byte load of the lengths
-        const uint64_t pk = *reinterpret_cast<const uint64_t*>(dlen + i0);
-#pragma unroll
-        for (int j = 0; j < 8; j++) l[j] = (uint8_t)(pk >> (8 * j));
-    } else {
-#pragma unroll
-        for (int j = 0; j < 8; j++) l[j] = i0 + j < n ? dlen[i0 + j] : 0;
-    }
-#pragma unroll
-    for (int j = 0; j < 8; j++) sum += l[j];
-    uint64_t v[1] = {sum}, tot[1];
-    block_excl_scan<1>(v, tot, sh);
-    int64_t off = (int64_t)(tile_base[blockIdx.x] + v[0]);
+// The deltas of elements i0 .. i0 + 7 from their lengths l[] and the first one's bit offset
+// `off` in the delta stream, stored to delta[]; returns their sum.
+__device__ __forceinline__ uint64_t dec_deltas8(const uint64_t* __restrict__ dw, int64_t ndw, int64_t n, int64_t i0,
+                                                int64_t off, const uint8_t (&l)[8], uint32_t* __restrict__ delta) {
     uint64_t dsum = 0;
-    if (full) {
+    if (i0 + 8 <= n) {
         // the thread's 8 deltas are contiguous, at most 256 bits: five words loaded up front, each
         // field taken from the two words it straddles
         const int64_t w = off >> 6;
@@ -2392,9 +2395,130 @@ __global__ __launch_bounds__(kSpThreads) void k_dec_deltas(const uint64_t* __res
             off += l[j];
         }
     }
+    return dsum;
+}
+
+__global__ __launch_bounds__(kSpThreads) void k_dec_deltas(const uint64_t* __restrict__ dw, int64_t ndw,
+                                                           const uint8_t* __restrict__ dlen, int64_t n,
+                                                           const uint64_t* __restrict__ tile_base,
+                                                           uint32_t* __restrict__ delta, uint64_t* __restrict__ tile_sums) {
+    __shared__ uint64_t sh[4];
+    const int64_t i0 = (int64_t)blockIdx.x * kSpTile + threadIdx.x * 8;
+    uint8_t l[8];
+    uint64_t sum = 0;
+    if (i0 + 8 <= n) {  // one 8-byte load of the lengths
+        const uint64_t pk = *reinterpret_cast<const uint64_t*>(dlen + i0);
+#pragma unroll
+        for (int j = 0; j < 8; j++) l[j] = (uint8_t)(pk >> (8 * j));
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; j++) l[j] = i0 + j < n ? dlen[i0 + j] : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j++) sum += l[j];
+    uint64_t v[1] = {sum}, tot[1];
+    block_excl_scan<1>(v, tot, sh);
+    const uint64_t dsum = dec_deltas8(dw, ndw, n, i0, (int64_t)(tile_base[blockIdx.x] + v[0]), l, delta);
     uint64_t v2[1] = {dsum}, tot2[1];
     block_excl_scan<1>(v2, tot2, sh);
     if (threadIdx.x == 0) tile_sums[blockIdx.x] = tot2[0];
+}
+
+// Lengths and deltas in one pass: each tile (taken in ticket order) computes its lengths in
+// registers, takes its first bit offset in the delta stream by a decoupled look-back over the
+// tiles' bit totals (the compaction's scheme), and extracts its deltas -- no length array written
+// and read back, no tile scan in between.  Extra blocks past the tiles build the narrow table.
+__device__ __forceinline__ uint64_t lookback_excl(uint64_t* status, int64_t tile, uint64_t total, int lane) {
+    uint64_t excl = 0;
+    if (tile == 0) {
+        if (lane == 0) st_status(&status[0], kStPre | total);
+        return 0;
+    }
+    if (lane == 0) st_status(&status[tile], kStAgg | total);
+    int64_t p = tile - 1;
+    while (true) {
+        const int64_t idx = p - lane;
+        uint64_t sv = idx >= 0 ? ld_status(&status[idx]) : kStPre;  // before tile 0: prefix 0
+        while (__ballot((sv & ~kStMask) == 0)) {
+            __builtin_amdgcn_s_sleep(1);
+            if ((sv & ~kStMask) == 0) sv = ld_status(&status[idx]);
+        }
+        const uint64_t pre = __ballot((sv & ~kStMask) == kStPre);
+        const int stop = pre ? __ffsll((unsigned long long)pre) - 1 : 63;  // nearest prefix
+        uint64_t contrib = lane <= stop ? (sv & kStMask) : 0;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) contrib += __shfl_xor(contrib, off, 64);
+        excl += contrib;
+        if (pre) break;
+        p -= 64;
+    }
+    if (lane == 0) st_status(&status[tile], kStPre | (excl + total));
+    return excl;
+}
+__global__ __launch_bounds__(kSpThreads) void k_dec_lens_deltas(const uint64_t* __restrict__ fw, int64_t nfw,
+                                                                const int64_t* __restrict__ end_pos, int64_t n,
+                                                                const SpGroups* __restrict__ gp,
+                                                                const uint64_t* __restrict__ dw, int64_t ndw,
+                                                                uint32_t* __restrict__ delta,
+                                                                uint64_t* __restrict__ tile_sums, uint64_t* status,
+                                                                uint64_t* status2, unsigned* ticket, int64_t nlens,
+                                                                NarrowJob nj) {
+    if ((int64_t)blockIdx.x >= nlens) {  // the blocks past the tiles build the narrow table
+        const int64_t b = (int64_t)blockIdx.x - nlens;
+        if (nj.width == 8) narrow_cells<uint8_t>(nj.t32, nj.ncells, static_cast<uint8_t*>(nj.tn), b);
+        else narrow_cells<uint16_t>(nj.t32, nj.ncells, static_cast<uint16_t*>(nj.tn), b);
+        return;
+    }
+    __shared__ int64_t S[kMaxGroups + 1];
+    __shared__ uint64_t sh[4];
+    __shared__ int64_t s_tile;
+    __shared__ uint64_t s_excl;
+    load_starts(gp, S);
+    if (threadIdx.x == 0) s_tile = (int64_t)atomicAdd(ticket, 1u);  // tiles in arrival order
+    __syncthreads();
+    const int64_t tile = s_tile;
+    const int64_t i0 = tile * kSpTile + threadIdx.x * 8;
+    uint8_t l[8];
+    const uint64_t sum = dec_lens8(fw, nfw, end_pos, n, gp, S, i0, l);
+    uint64_t v[1] = {sum}, tot[1];
+    block_excl_scan<1>(v, tot, sh);
+    if (threadIdx.x < 64) {
+        const uint64_t excl = lookback_excl(status, tile, tot[0], (int)threadIdx.x);
+        if (threadIdx.x == 0) s_excl = excl;
+    }
+    __syncthreads();
+    const uint64_t dsum = dec_deltas8(dw, ndw, n, i0, (int64_t)(s_excl + v[0]), l, delta);
+    uint64_t v2[1] = {dsum}, tot2[1];
+    block_excl_scan<1>(v2, tot2, sh);
+    if (status2) {  // the tiles' delta prefixes too (a second look-back): tile_sums = the exclusive scan
+        if (threadIdx.x < 64) {
+            const uint64_t excl2 = lookback_excl(status2, tile, tot2[0], (int)threadIdx.x);
+            if (threadIdx.x == 0) {
+                tile_sums[tile] = excl2;
+                if (tile == nlens - 1) tile_sums[nlens] = excl2 + tot2[0];
+            }
+        }
+    } else if (threadIdx.x == 0) {
+        tile_sums[tile] = tot2[0];
+    }
+}
+
+hipError_t launch_dec_lens_deltas(hipStream_t st, const uint64_t* flag_words, int64_t n_flag_words,
+                                  const int64_t* end_pos, int64_t n, const SpGroups* gp,
+                                  const uint64_t* delta_words, int64_t n_delta_words, uint32_t* delta,
+                                  uint64_t* tile_sums, uint64_t* status, NarrowJob nj, bool scan_sums) {
+    const int64_t tiles = sp_tiles(n, kSpTile);
+    if (tiles <= 0) return nj.tn ? launch_narrow_table(st, nj.t32, nj.ncells, nj.width, nj.tn) : hipSuccess;
+    if (nj.tn && (reinterpret_cast<uintptr_t>(nj.t32) & 15) != 0) return hipErrorInvalidValue;
+    // statuses of the bit offsets, the ticket, statuses of the delta prefixes
+    hipError_t e = hipMemsetAsync(status, 0, sizeof(uint64_t) * (size_t)(2 * tiles + 2), st);
+    if (e != hipSuccess) return e;
+    const int64_t nn = nj.tn && nj.ncells > 0 ? sp_tiles(nj.ncells, (int64_t)kSpThreads * 4) : 0;
+    hipLaunchKernelGGL(k_dec_lens_deltas, dim3((unsigned)(tiles + nn)), dim3(kSpThreads), 0, st, flag_words,
+                       n_flag_words, end_pos, n, gp, delta_words, n_delta_words, delta, tile_sums, status,
+                       scan_sums ? status + tiles + 2 : nullptr, reinterpret_cast<unsigned*>(status + tiles), tiles,
+                       nj);
+    return hipGetLastError();
 }
 
 hipError_t launch_dec_deltas(hipStream_t st, const uint64_t* delta_words, int64_t n_delta_words,

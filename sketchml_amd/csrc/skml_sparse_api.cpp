@@ -63,6 +63,7 @@ enum {
     kSlotWireMeta,  // the wire kernels' section tables and small results
     kSlotNarrowTab, // the MinMax query's narrow table image
     kSlotRsMerge,   // one-pass Sort.merge: RsInfo + the runs' key-range bounds
+    kSlotLookback,  // the restore's look-back statuses (lengths + deltas in one pass)
     kSlotCount_,
 };
 static_assert(kSlotCount_ <= kScratchSlots, "scratch slots");
@@ -629,11 +630,26 @@ int decode_groups(skml_ctx* c, const skml_sparse* s, int32_t* gk, int32_t* gb, b
         tnar = ctx_scratch(c, kSlotNarrowTab, (size_t)s->ncells * (size_t)(width / 8));
         if (!tnar) return sfail(SKML_E_OOM, "decode scratch (table image)");
     }
-    SP_HIP(launch_dec_lens(st, s->flag_words, s->n_flag_words, end_pos, n, s->g_dev, dlen, ts,
-                           NarrowJob{tab, s->ncells, tnar, width}));
-    if (int e = scan_tiles(c, ts, tiles, 1, nullptr)) return e;
-    SP_HIP(launch_dec_deltas(st, s->delta_words, s->n_delta_words, dlen, n, s->g_dev, ts, delta, ts2));
-    if (int e = scan_tiles(c, ts2, tiles, 1, nullptr)) return e;
+    // three passes (lengths, their tile scan, deltas); SKML_FORM_DEC_LOOKBACK = 1: one pass with
+    // decoupled look-backs for the bit offsets and the deltas' prefixes, 2: the same pass with the
+    // deltas' tile scan after it (A/B forms, measured slower: the look-back chain across 13 K tiles
+    // ran 230 us against 107 us for the three passes, profiles/ab/r05_dec_lookback.txt)
+    const int lb = form(SKML_FORM_DEC_LOOKBACK);
+    const int split = lb == 1 ? 0 : lb == 2 ? 2 : 1;
+    if (split == 1) {
+        SP_HIP(launch_dec_lens(st, s->flag_words, s->n_flag_words, end_pos, n, s->g_dev, dlen, ts,
+                               NarrowJob{tab, s->ncells, tnar, width}));
+        if (int e = scan_tiles(c, ts, tiles, 1, nullptr)) return e;
+        SP_HIP(launch_dec_deltas(st, s->delta_words, s->n_delta_words, dlen, n, s->g_dev, ts, delta, ts2));
+    } else {
+        uint64_t* status = scratch<uint64_t>(c, kSlotLookback, 2 * (size_t)tiles + 8);
+        if (!status) return sfail(SKML_E_OOM, "decode scratch (look-back)");
+        SP_HIP(launch_dec_lens_deltas(st, s->flag_words, s->n_flag_words, end_pos, n, s->g_dev, s->delta_words,
+                                      s->n_delta_words, delta, ts2, status, NarrowJob{tab, s->ncells, tnar, width},
+                                      split == 0));
+    }
+    if (split != 0)
+        if (int e = scan_tiles(c, ts2, tiles, 1, nullptr)) return e;
     SP_HIP(launch_group_prefix(st, delta, n, s->g_dev, G.G, ts2, gpre));
     SP_HIP(launch_dec_keys(st, delta, n, s->g_dev, G, ts2, gpre, tab, tnar, width, gk, gb, dv ? dv->nq : 0,
                            dv ? dv->gb : nullptr, dv ? dv->bw : 0, dv ? dv->err : nullptr,

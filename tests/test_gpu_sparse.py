@@ -76,21 +76,25 @@ def test_sparse_edge_values(gpu, kind):
     _check_sparse(gpu, keys, vals, seed=5, hash_seed=1)
 
 
-@pytest.fixture(params=["one_pass", "one_pass_plain", "persistent_query", "bounds_pass", "rounds"])
+@pytest.fixture(params=["one_pass", "one_pass_plain", "persistent_query", "bounds_pass", "dec_lookback", "dec_lookback_scan", "rounds"])
 def merge_form(request):
     """restore three ways.  one_pass (the default): tiles of one group through the compile-time-hash
     query (k_dec_keys MODE 1) and the edge tiles through the generic one, Sort.merge as the
     one-pass key-range merge with the next range's loads in flight.  one_pass_plain: the same merge
     without that prefetch.  persistent_query: the compile-time-hash query in persistent workgroups
     (A/B form, slower at 2^28).  bounds_pass: the key ranges' bounds from k_rs_bounds instead of the
-    key query.  rounds: the round-3 forms forced through skml_debug_form (one generic
+    key query.  dec_lookback: the bit lengths and deltas in one pass with decoupled look-backs (A/B
+    form, slower); dec_lookback_scan: the same with the deltas' tile prefixes from a scan after it.
+    rounds: the round-3 forms forced through skml_debug_form (one generic
     query per row for every tile, the pairwise merge rounds, which are also the fallback for
     irregular input)."""
     from sketchml_amd import _lib
     forms = {"rs_rounds": 1, "dec_rows_serial": 1} if request.param == "rounds" else \
         {"rs_rounds": 2} if request.param == "one_pass_plain" else \
         {"dec_rows_serial": 2} if request.param == "persistent_query" else \
-        {"run_bounds": 1} if request.param == "bounds_pass" else {}
+        {"run_bounds": 1} if request.param == "bounds_pass" else \
+        {"dec_lookback": 1} if request.param == "dec_lookback" else \
+        {"dec_lookback": 2} if request.param == "dec_lookback_scan" else {}
     with _lib.forced_forms(**forms):
         yield request.param
 
