@@ -753,7 +753,11 @@ def main():
         # the sort-dominated leaf is bound by VALU issue, not HBM: its issue rate against the ceiling
         rate = valu[0] / (live["avg_us"] * 1e-6) / 1e9
         roofline["valu"] = {"insts_per_launch": valu[0], "source": valu[1], "issue_ginst_s": round(rate, 1),
-                            "peak_ginst_s": round(VALU_PEAK_GINST, 1), "frac": round(rate / VALU_PEAK_GINST, 4)}
+                            "peak_ginst_s": round(VALU_PEAK_GINST, 1), "frac": round(rate / VALU_PEAK_GINST, 4),
+                            "peak_note": "one wave-instruction per clock per CU at 2.4 GHz: the rate of the "
+                                         "network's min / max / med3 / DPP ops; the adds, ands and shifts "
+                                         "around them issue at the SIMD-32 rate, so the mix can reach 1.0 "
+                                         "(and the engine clock may run above 2.4 GHz)"}
     encode_device_us = sum(v["avg_us"] * v["launches"] for k, v in allstats.items()
                            if k in alg_bytes) / steps_b
     extras = {"encode_device_us": round(encode_device_us, 2),
