@@ -131,7 +131,7 @@ int skml_debug_sparse_merge_path(void);
 #define SKML_FORM_PART_BALLOT 2     /* 1: the ballot-ranked partition scatter */
 #define SKML_FORM_RS_ROUNDS 3       /* 1: Sort.merge by the pairwise merge rounds always, 2: the one-pass merge without prefetch */
 #define SKML_FORM_DEC_ROWS_SERIAL 4 /* 1: the generic MinMax query (rows one by one) for every tile, 2: persistent workgroups (A/B) */
-#define SKML_FORM_AGG_TILES 5       /* 0: Gradient.sum's sum tile in LDS (the default; staged and prefetched for dense-form payloads), 1: the 4,096-key wave-per-payload tiles, 2 / 3: staged tiles four / two per round, 4: staged tiles with the next tile prefetched, 5: staged tiles without */
+#define SKML_FORM_AGG_TILES 5       /* 0: Gradient.sum's sum tile in LDS (the default), 1: the 4,096-key wave-per-payload tiles, 2 / 3: staged tiles four / two per round, 4: staged tiles with the next tile prefetched, 5: staged tiles without */
 #define SKML_FORM_AGG_ONE_LANE 6    /* 1: Gradient.sum restores every payload on the caller's stream */
 #define SKML_FORM_RUN_BOUNDS 7      /* 1: the runs' tile / key-range bounds (Gradient.sum, the one-pass Sort.merge) in passes of their own (k_agg_bounds, k_rs_bounds) instead of by the key query */
 #define SKML_FORM_DEC_LOOKBACK 8    /* 1: the restore's bit lengths and deltas in one pass with decoupled look-backs for the bit offsets and the deltas' prefixes (A/B: slower), 2: the same pass with the deltas' tile scan after it */

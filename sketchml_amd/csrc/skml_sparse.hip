@@ -3160,7 +3160,7 @@ __device__ __forceinline__ TileWalk tile_walk(int64_t blk, int64_t nblk, int sub
 // on XCD b % 8, so within a round XCD x takes tiles [x, x + 1) * (nblk / 8) * nsub and its
 // workgroups take consecutive nsub-tile groups of that segment.  Neighbouring tiles share the
 // cache lines of the payloads' run pieces (a 128-byte line of keys spans ~5 tiles of a C3 piece,
-// of bins ~20): dealt round-robin, each line was fetched into several XCDs' L2 (k_agg_vtiles_rmw
+// of bins ~20): dealt round-robin, each line was fetched into several XCDs' L2 (the sum-tile kernel
 // read 3.96 GB per 1.1 GB of elements, profiles/r05m_agg_pmc.json).  One write front per XCD.
 __device__ __forceinline__ TileWalk tile_walk_xcd(int64_t blk, int64_t nblk, int sub, int nsub, int64_t ntiles) {
     if (nblk % 8 != 0) return tile_walk(blk, nblk, sub, nsub, ntiles);
@@ -3716,38 +3716,51 @@ __global__ __launch_bounds__(kAggThreads) __attribute__((amdgpu_waves_per_eu(4))
     if (bad) atomicOr(err, bad);
 }
 
-// The sum tile itself in LDS: the same waves, tiles, run pieces and prefetch as k_agg_vtiles_pf,
-// but each element is added straight into the wave's 512 doubles of the tile (read, add, write
-// back) instead of being staged as a bin and summed by a sweep over every (payload, key) slot,
-// which looked up quantValues 64 times per lane and tile for ~6 present elements.  The elements of
-// a tile are concatenated payload by payload, so each element row (one load instruction) holds
-// ascending payloads by lane and later rows never hold an earlier payload; a row is added payload
-// by payload (one masked pass per payload present in it, usually one or two), and since a payload
-// holds a key at most once, no two lanes of a pass touch the same slot and every key receives its
-// payloads' values in payload order -- Gradient.sum's order, with the same roundings as the
-// staged form.  A key repeated inside a payload (presence bit already set) is not added and sets
-// err bit 2.  Dense-form payloads (a -0.0 sum turned into +0.0 at every key) keep the staged form.
-__global__ __launch_bounds__(kAggThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_agg_vtiles_rmw(
+// The sum tile itself in LDS: the waves, run pieces and prefetch of k_agg_vtiles_pf, but each
+// element is added straight into the wave's tile of doubles (read, add, write back) instead of
+// being staged as a bin and summed by a sweep over every (payload, key) slot, which looked up
+// quantValues once per (payload, key) for ~10 % present.  The elements of a tile are concatenated
+// payload by payload, so each element row (one load instruction) holds ascending payloads by lane
+// and later rows never hold an earlier payload; a row is added payload by payload (one masked pass
+// per payload present in it, usually one or two), and since a payload holds a key at most once, no
+// two lanes of a pass touch the same slot and every key receives its payloads' values in payload
+// order -- Gradient.sum's order, with the staged form's roundings.  A key repeated inside a
+// payload (presence bit already set) is not added and sets err bit 2.  Dense-form payloads
+// (DenseDoubleGradient.plusBy: only |v| > 1e-8 added, and every key's -0.0 sum turned into +0.0)
+// sweep the tile once their payload is complete, before any later payload's add.
+// BITS: 2^BITS keys per tile (512; 1,024-key tiles on four waves per workgroup, with run pieces
+// twice as long, ran 5.7 against 5.0 ms for 8 C3 payloads: 247 VGPRs and half the waves per CU,
+// profiles/ab/r05_agg_rmw1k.txt), PER: elements per lane held in registers (a longer tile takes
+// the rest row by row).  DENSE: some payload of the launch takes the dense form.
+template <int BITS, int WAVES, int PER, bool DENSE>
+__global__ __launch_bounds__(64 * WAVES) void k_agg_rmw(
     const AggPayload* __restrict__ pays, int P, int64_t ntiles, int64_t dim, double* __restrict__ out, int from_out,
     double scale, unsigned* __restrict__ err, const int32_t* __restrict__ kbase, const uint8_t* __restrict__ bbase) {
-    constexpr int kWaves = kAggThreads / 64;
-    __shared__ __attribute__((aligned(16))) double tsum[kWaves][kAggVTile];
-    // presence bits of the payload being added: key x at word x % 64, bit x / 64 (a pass's 64
-    // random keys spread over 64 words: few lanes share a word's atomic), cleared at each payload
-    __shared__ uint32_t here[kWaves][64];
+    constexpr int kTile = 1 << BITS, kKeys = kTile / 64;  // keys per lane in the stores
+    static_assert(PER == 8 || PER == 16, "piece bytes written as 8 or 16");
+    static_assert(kTile / 64 <= 16, "presence bits: 64 words of 16 bits at most");
+    __shared__ __attribute__((aligned(16))) double tsum[WAVES][kTile];
+    // presence bits of the payload being added: key x at word x % 64, bit x / 64, cleared at each
+    // payload (a pass's random keys spread over 64 words: few lanes share a word's atomic)
+    __shared__ uint32_t here[WAVES][64];
     __shared__ double qt[kAggPB][kAggLdsValues];
-    __shared__ int32_t pre[2][kWaves][65];
-    __shared__ int32_t pk0[2][kWaves][64];
-    __shared__ int32_t pn0[2][kWaves][64];
-    __shared__ __attribute__((aligned(8))) uint8_t pcs[kWaves][64 * kAggWPer];  // piece of element j
+    __shared__ int32_t pre[2][WAVES][65];
+    __shared__ int32_t pk0[2][WAVES][64];
+    __shared__ int32_t pn0[2][WAVES][64];
+    __shared__ __attribute__((aligned(16))) uint8_t pcs[WAVES][64 * PER];  // piece of element j
     __shared__ AggPayload pl[kAggPB];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (threadIdx.x < P * (int)(sizeof(AggPayload) / 8))
         reinterpret_cast<uint64_t*>(pl)[threadIdx.x] = reinterpret_cast<const uint64_t*>(pays)[threadIdx.x];
     __syncthreads();
-    if (wave < P)
-        for (int b = lane; b < pl[wave].nq; b += 64) qt[wave][b] = gload<double>(pl[wave].qv, b);
+    for (int q = wave; q < P; q += WAVES)
+        for (int b = lane; b < pl[q].nq; b += 64) qt[q][b] = gload<double>(pl[q].qv, b);
     __syncthreads();
+    uint32_t dmask = 0;  // dense-form payloads
+    if constexpr (DENSE) {
+        for (int q = 0; q < P; q++) dmask |= pl[q].dense_form ? 1u << q : 0u;
+        dmask = __builtin_amdgcn_readfirstlane(dmask);
+    }
     const int pl_l = lane >> 3, g_l = lane & 7;
     const bool lane_on = pl_l < P && g_l < pl[pl_l].G;
     const int32_t* bd = lane_on ? pl[pl_l].bounds + (int64_t)g_l * (ntiles + 1) : nullptr;
@@ -3779,35 +3792,35 @@ __global__ __launch_bounds__(kAggThreads) __attribute__((amdgpu_waves_per_eu(4))
             if (pre[buf][wave][s_ + step] <= j) s_ += step;
         return s_;
     };
-    // the pieces of the elements held in registers: lane l searches the piece of j = 8 l and walks
-    // on through j = 8 l + 7 (a piece holds ~6 elements of a C3 tile), into pcs; the loads then
-    // read the piece of j = l + 64 u back (one search per lane instead of one per element)
-    auto load = [&](int buf, int total, int ln, int32_t (&kk)[kAggWPer], uint32_t (&bb)[kAggWPer]) {
+    // the pieces of the elements held in registers: lane l searches the piece of j = PER l and
+    // walks on through PER l + PER - 1 (a piece holds ~6-13 elements of a C3 tile), into pcs; the
+    // loads then read the piece of j = l + 64 u back (one search per lane instead of per element)
+    auto load = [&](int buf, int total, int ln, int32_t (&kk)[PER], uint32_t (&bb)[PER]) {
         {
-            const int j0 = kAggWPer * ln;
+            const int j0 = PER * ln;
             if (j0 < total) {
                 int s_ = piece_of(buf, j0);
-                uint32_t w0 = 0, w1 = 0;
+                uint32_t w[PER / 4] = {};
 #pragma unroll
-                for (int u = 0; u < kAggWPer; u++) {
+                for (int u = 0; u < PER; u++) {
                     const int j = j0 + u;
                     if (j < total)
                         while (pre[buf][wave][s_ + 1] <= j) s_++;
-                    if (u < 4) w0 |= (uint32_t)s_ << (8 * u);
-                    else w1 |= (uint32_t)s_ << (8 * (u - 4));
+                    w[u >> 2] |= (uint32_t)s_ << (8 * (u & 3));
                 }
-                *reinterpret_cast<uint2*>(&pcs[wave][j0]) = make_uint2(w0, w1);
+                if constexpr (PER == 8) *reinterpret_cast<uint2*>(&pcs[wave][j0]) = make_uint2(w[0], w[1]);
+                else *reinterpret_cast<uint4*>(&pcs[wave][j0]) = make_uint4(w[0], w[1], w[2], w[3]);
             }
             __builtin_amdgcn_wave_barrier();
         }
-        int spc[kAggWPer];
+        int spc[PER];
 #pragma unroll
-        for (int u = 0; u < kAggWPer; u++) {
+        for (int u = 0; u < PER; u++) {
             const int j = ln + 64 * u;
             spc[u] = j < total ? (int)pcs[wave][j] : 0;
         }
 #pragma unroll
-        for (int u = 0; u < kAggWPer; u++) {
+        for (int u = 0; u < PER; u++) {
             const int j = ln + 64 * u;
             kk[u] = INT32_MIN;
             bb[u] = 0;
@@ -3822,9 +3835,9 @@ __global__ __launch_bounds__(kAggThreads) __attribute__((amdgpu_waves_per_eu(4))
     auto store_prev = [&](int l) {  // the previous tile's sums, x scale, 1 KB per store instruction
         if (prev_k0 < 0) return;
         double* o = out + prev_k0;
-        const bool whole = prev_nk == kAggVTile && (reinterpret_cast<uintptr_t>(o) & 15) == 0;
+        const bool whole = prev_nk == kTile && (reinterpret_cast<uintptr_t>(o) & 15) == 0;
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
+        for (int q = 0; q < kTile / 128; q++) {
             const int x = 128 * q + 2 * l;
             double2 v = *reinterpret_cast<const double2*>(T + x);
             if (scale != 1.0) {
@@ -3845,11 +3858,22 @@ __global__ __launch_bounds__(kAggThreads) __attribute__((amdgpu_waves_per_eu(4))
         __builtin_amdgcn_wave_barrier();
         prev_k0 = -1;
     };
-    // (elements prefetched two tiles ahead measured level: profiles/ab/r05_agg_prefetch2.txt)
-    const TileWalk tw = tile_walk_xcd(blockIdx.x, gridDim.x, wave, kWaves, ntiles);
+    // payloads [a, b) complete: a dense-form one among them turns every -0.0 sum of the tile into +0.0
+    auto finish = [&](int a, int b, int ln) {
+        if constexpr (!DENSE) return;
+        if (b <= a || !((dmask >> a) & ((1u << (b - a)) - 1u))) return;  // wave-uniform
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int i = 0; i < kKeys; i++) {
+            double& t = T[kKeys * ln + i];
+            if (__double_as_longlong(t) == (long long)0x8000000000000000ull) t = 0.0;
+        }
+        __builtin_amdgcn_wave_barrier();
+    };
+    const TileWalk tw = tile_walk_xcd(blockIdx.x, gridDim.x, wave, WAVES, ntiles);
     int buf = 0, total = 0;
-    int32_t kk[kAggWPer], kn[kAggWPer];
-    uint32_t bb[kAggWPer], bn[kAggWPer];
+    int32_t kk[PER], kn[PER];
+    uint32_t bb[PER], bn[PER];
     if (tw.t0 < tw.t1) {
         fetch(tw.t0);
         total = plan(0, nb0, nb1, lane);
@@ -3859,7 +3883,7 @@ __global__ __launch_bounds__(kAggThreads) __attribute__((amdgpu_waves_per_eu(4))
     for (int64_t t = tw.t0; t < tw.t1; t += tw.step) {
         int ln = lane;  // lane-derived values rematerialised per tile (hoisted, they spill)
         asm volatile("" : "+v"(ln));
-        const int64_t k0 = t << kAggVBits, nk = std::min<int64_t>(kAggVTile, dim - k0);
+        const int64_t k0 = t << BITS, nk = std::min<int64_t>(kTile, dim - k0);
         int total_n = 0;
         const bool more = t + tw.step < tw.t1;
         if (more) {
@@ -3868,18 +3892,19 @@ __global__ __launch_bounds__(kAggThreads) __attribute__((amdgpu_waves_per_eu(4))
             fetch(t + 2 * tw.step);
         }
         store_prev(ln);
-        // the tile's starting sums (a later batch of payloads continues them) and presence bits
+        // the tile's starting sums (a later batch of payloads continues them)
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
+        for (int q = 0; q < kKeys / 2; q++) {
             double2 v = make_double2(0.0, 0.0);
             if (from_out) {
-                const int x = 8 * ln + 2 * q;
+                const int x = kKeys * ln + 2 * q;
                 if (x < nk) v.x = out[k0 + x];
                 if (x + 1 < nk) v.y = out[k0 + x + 1];
             }
-            *reinterpret_cast<double2*>(T + 8 * ln + 2 * q) = v;
+            *reinterpret_cast<double2*>(T + kKeys * ln + 2 * q) = v;
         }
-        int p_last = -1;  // the payload whose presence bits H holds (wave-uniform)
+        __builtin_amdgcn_wave_barrier();
+        int h_for = -1, p_act = 0;  // H's payload; payloads below p_act are complete (wave-uniform)
         const int32_t k0i = (int32_t)k0;  // dim <= 2^31: tile starts fit int32
         // one row of elements (lane l: element j = l + 64 u), payload by payload
         auto add_row = [&](bool act, int p_el, int32_t k, uint32_t b) {
@@ -3887,10 +3912,12 @@ __global__ __launch_bounds__(kAggThreads) __attribute__((amdgpu_waves_per_eu(4))
             while (rem) {
                 const int first = __ffsll((unsigned long long)rem) - 1;
                 const int pcur = __builtin_amdgcn_readlane(p_el, first);
-                if (pcur != p_last) {  // a new payload: its own presence bits
+                if (pcur != h_for) {  // a new payload: the ones before it are complete
+                    finish(p_act, pcur, ln);
+                    p_act = pcur;
                     H[ln] = 0u;
                     __builtin_amdgcn_wave_barrier();
-                    p_last = pcur;
+                    h_for = pcur;
                 }
                 const bool mine = act && p_el == pcur;
 #ifdef SKML_ABLATE_AGG_RMW  // timing ablation only (wrong sums): the adds into the tile priced
@@ -3900,21 +3927,25 @@ __global__ __launch_bounds__(kAggThreads) __attribute__((amdgpu_waves_per_eu(4))
 #endif
                 if (mine) {
                     const int32_t xk = k - k0i;
-                    if ((uint32_t)xk >= (uint32_t)nk) {  // k_agg_bounds' placement says otherwise: an error
+                    if ((uint32_t)xk >= (uint32_t)nk) {  // outside the tile its bounds placed it in: an error
                         bad |= 1u;
                     } else {
                         const uint32_t bit = 1u << (xk >> 6);
-                        if (atomicOr(&H[xk & 63], bit) & bit) bad |= 2u;  // a key twice in one payload
-                        else T[xk] = T[xk] + qt[pcur][b];
+                        if (atomicOr(&H[xk & 63], bit) & bit) {
+                            bad |= 2u;  // a key twice in one payload
+                        } else {
+                            const double v = qt[pcur][b];
+                            if (!DENSE || !((dmask >> pcur) & 1u) || fabs(v) > 1e-8) T[xk] = T[xk] + v;
+                        }
                     }
                 }
                 rem &= ~__ballot(mine);
             }
         };
 #pragma unroll
-        for (int u = 0; u < kAggWPer; u++)
+        for (int u = 0; u < PER; u++)
             add_row(ln + 64 * u < total, (int)(bb[u] >> 8), kk[u], bb[u] & 0xFFu);
-        for (int j0 = 64 * kAggWPer; j0 < total; j0 += 64) {  // rows past the registers
+        for (int j0 = 64 * PER; j0 < total; j0 += 64) {  // rows past the registers
             const int j = j0 + ln;
             const bool act = j < total;
             int sp = 0, d = 0;
@@ -3926,13 +3957,14 @@ __global__ __launch_bounds__(kAggThreads) __attribute__((amdgpu_waves_per_eu(4))
             const uint32_t b = act ? gload<uint8_t>(bbase, (uint32_t)(pn0[buf][wave][sp] + d)) : 0u;
             add_row(act, sp >> 3, k, b);
         }
+        finish(p_act, P, ln);  // the payloads from the last one seen on
         __builtin_amdgcn_wave_barrier();
         prev_k0 = k0;
         prev_nk = nk;
         buf ^= 1;
         total = total_n;
 #pragma unroll
-        for (int u = 0; u < kAggWPer; u++) {
+        for (int u = 0; u < PER; u++) {
             kk[u] = kn[u];
             bb[u] = bn[u];
         }
@@ -3968,16 +4000,22 @@ hipError_t launch_agg_tiles(hipStream_t st, const AggPayload* pays, int P, int64
     if (ntiles <= 0) return hipSuccess;
     if (vtiles) {
         if (P < 1 || P > kAggVPayloads) return hipErrorInvalidValue;  // one lane per (payload, group)
-        // the default: the sum tile in LDS (k_agg_vtiles_rmw) unless a payload takes the dense
-        // form; then the prefetching staged form (5.57-5.64 against 5.63-5.66 ms for 8 C3
-        // payloads, profiles/ab/r05_pf.txt); SKML_FORM_AGG_TILES = 4 / 5 / 2 / 3: the prefetching
-        // staged form, the plain staged tiles, four / two tiles per wave round (A/B forms)
-        if (form(SKML_FORM_AGG_TILES) == 0 && !any_dense) {
-            static const int resident_rmw = resident_workgroups(k_agg_vtiles_rmw);
-            const int64_t all = sp_tiles(ntiles, kAggThreads / 64);
-            const unsigned grid = (unsigned)(resident_rmw <= 0 ? all : std::min<int64_t>(all, resident_rmw));
-            hipLaunchKernelGGL(k_agg_vtiles_rmw, dim3(grid), dim3(kAggThreads), 0, st, pays, P, ntiles, dim, out,
-                               from_out, scale, err, kbase, bbase);
+        // the default: the sum tile in LDS (k_agg_rmw); SKML_FORM_AGG_TILES = 6: its 512-key form,
+        // 4 / 5 / 2 / 3: the prefetching staged form (5.57-5.64 against 5.63-5.66 ms for 8 C3
+        // payloads, profiles/ab/r05_pf.txt), the plain staged tiles, four / two tiles per wave
+        // round (A/B forms)
+        if (form(SKML_FORM_AGG_TILES) == 0) {  // the sum tile in LDS (dense-form payloads swept)
+#define SKML_RMW_LAUNCH(DENSE)                                                                                   \
+    do {                                                                                                         \
+        static const int res = resident_blocks(k_agg_rmw<kAggVBits, 8, 8, DENSE>, kAggThreads);                   \
+        const int64_t all = sp_tiles(ntiles, 8);                                                                 \
+        const unsigned grid = (unsigned)(res <= 0 ? all : std::min<int64_t>(all, res));                          \
+        hipLaunchKernelGGL((k_agg_rmw<kAggVBits, 8, 8, DENSE>), dim3(grid), dim3(kAggThreads), 0, st, pays, P,   \
+                           ntiles, dim, out, from_out, scale, err, kbase, bbase);                                \
+    } while (0)
+            if (any_dense) SKML_RMW_LAUNCH(true);
+            else SKML_RMW_LAUNCH(false);
+#undef SKML_RMW_LAUNCH
             return hipGetLastError();
         }
         if (form(SKML_FORM_AGG_TILES) == 2) {

@@ -122,9 +122,10 @@ def test_restore_values_refuse_bins_outside_quant_values(gpu, bins, forms):
 
 
 # Gradient.sum's tile kernels: vtile_rmw (the default for payloads of <= 8 groups and <= 256
-# quantValues: the 512-key sum tile in LDS, each element added into it row by row, payload by
-# payload, with the next tile's element loads in flight; dense-form payloads take vtile_pf; the
-# run bounds come from the key query, vtile_rmw_bounds_pass: from their own k_agg_bounds pass),
+# quantValues: a 512-key sum tile in LDS per wave, each element added into it row by row,
+# payload by payload, with the next tile's element loads in flight, dense-form payloads swept at
+# their end; the run bounds come from the key query,
+# vtile_rmw_bounds_pass: from their own k_agg_bounds pass),
 # vtile_pf (vtile with the next tile's element loads in flight), vtile (
 # one wave per 512-key tile stages every payload's bins with presence bits and sums each key in
 # registers, payload after payload, 8 payloads per launch; restores on two streams), wave
@@ -132,7 +133,8 @@ def test_restore_values_refuse_bins_outside_quant_values(gpu, bins, forms):
 # other shape) and wave_serial (the wave tiles with the generic per-row MinMax query and one
 # stream); vtile2 / vtile4 take two / four staged tiles per wave round (one round of element
 # loads); vtile_pf loads the next tile's elements while a tile is summed.  Every form is exact, and every form refuses a key repeated across a payload's groups.
-KERNELS = {"vtile_rmw": {}, "vtile_rmw_bounds_pass": {"run_bounds": 1}, "vtile_pf": {"agg_tiles": 4},
+KERNELS = {"vtile_rmw": {}, "vtile_rmw_bounds_pass": {"run_bounds": 1},
+           "vtile_pf": {"agg_tiles": 4},
            "vtile": {"agg_tiles": 5}, "vtile2": {"agg_tiles": 3}, "vtile4": {"agg_tiles": 2},
            "wave": {"agg_tiles": 1},
            "wave_serial": {"agg_tiles": 1, "dec_rows_serial": 1, "agg_one_lane": 1}}
