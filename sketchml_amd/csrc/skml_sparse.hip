@@ -226,13 +226,17 @@ __device__ __forceinline__ void dec_row_cells(const int32_t (&key)[4], int64_t i
 #pragma unroll
     for (int j = 0; j < 4; j++) {
 #ifdef SKML_ABLATE_DEC_HASH  // timing ablation only (wrong cells): the hashes priced
-        rel[j] = i0 + j < n ? (uint32_t)(row0 + ((uint32_t)key[j] & 0xFFFFu)) : ~0u;
+        rel[j] = (uint32_t)(row0 + ((uint32_t)key[j] & 0xFFFFu));
         continue;
 #endif
+        // every element is hashed, those past n too (their keys are whatever the prefix left and
+        // their cells lie inside the row; nothing of theirs is stored): no exec-mask branches
+        // around the digit loops and the gathers
+        (void)i0, (void)n;
         if constexpr (SKML_DEC_INTMOD)
-            rel[j] = i0 + j < n ? (uint32_t)(row0 + dv(java_hash_mix(ID, key[j]))) : ~0u;
+            rel[j] = (uint32_t)(row0 + dv(java_hash_mix(ID, key[j])));
         else
-            rel[j] = i0 + j < n ? (uint32_t)(row0 + java_hash_fm32(ID, key[j], cols, inv)) : ~0u;
+            rel[j] = (uint32_t)(row0 + java_hash_fm32(ID, key[j], cols, inv));
     }
 }
 
@@ -2722,7 +2726,7 @@ __device__ __forceinline__ void dec_keys_tile(int64_t n, const SpGroups* __restr
     if constexpr (MODE == 1) {
         // both rows' 8 cells hashed, all 8 gathers in flight at once (the query is bound by the
         // gathers' L2 latency); the host runs this form only while every cell index is below
-        // 2^32 - 1, and ~0u marks an element past n
+        // 2^32 - 1
         const int g0 = grp[0];  // the tile's one group
         const int64_t tb = gp->tab_off[g0];
         const int32_t cols = gp->cols[g0];
@@ -2753,8 +2757,8 @@ __device__ __forceinline__ void dec_keys_tile(int64_t n, const SpGroups* __restr
                 tv[r][j] = (int32_t)(rel[r][j] & 0x3Fu);
                 continue;
 #endif
-                if constexpr (sizeof(TN) == 4) tv[r][j] = rel[r][j] != ~0u ? t32b[rel[r][j]] : zero;
-                else tv[r][j] = rel[r][j] != ~0u ? (int32_t)tnb[rel[r][j]] : zero;
+                if constexpr (sizeof(TN) == 4) tv[r][j] = t32b[rel[r][j]];
+                else tv[r][j] = (int32_t)tnb[rel[r][j]];
             }
         }
         if constexpr (sizeof(TN) < 4) {
@@ -2762,8 +2766,14 @@ __device__ __forceinline__ void dec_keys_tile(int64_t n, const SpGroups* __restr
             for (int r = 0; r < 2; r++)
 #pragma unroll
                 for (int j = 0; j < 4; j++)  // the sentinel: the cell's int32 value
-                    if (rel[r][j] != ~0u && (uint32_t)tv[r][j] == kTop) tv[r][j] = t32b[rel[r][j]];
+                    if ((uint32_t)tv[r][j] == kTop) tv[r][j] = t32b[rel[r][j]];
         }
+#ifdef SKML_ABLATE_DEC_HASH  // (the wrong cells may be empty ones: keep the bins inside quantValues)
+#pragma unroll
+        for (int r = 0; r < 2; r++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) tv[r][j] &= 0x3F;
+#endif
 #pragma unroll
         for (int r = 0; r < 2; r++)
 #pragma unroll

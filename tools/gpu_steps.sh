@@ -15,7 +15,8 @@
 #   timeline:KIND[:N]         rocprofv3 --kernel-trace --memory-copy-trace over tools/bench_sparse.py
 #                             (KIND: restore = --only-decode, encode = --only-e2e, aggregate =
 #                             --aggregate 8), the last N operations -> TAG/KIND_timeline.txt
-#   kstats:KIND               rocprofv3 --kernel-trace --stats over the same -> TAG/KIND_kernel_stats.csv
+#   kstats:KIND[:LIB]         rocprofv3 --kernel-trace --stats over the same (with sketchml_amd/LIB/libskml.so
+#                             if given) -> TAG/KIND[_LIB]_kernel_stats.csv
 #   hiptrace                  HIP API + kernel trace of the C3 encode -> TAG/hiptrace/
 #   leafgap                   tools/leaf_gap.py (clean / evented / synchronised encode blocks)
 #   leafwaves[:LIB]           tools/prof_leaf_waves.py at 2^28 (a SKML_PROF_LEAF build in LIB)
@@ -65,10 +66,14 @@ for STEP in "$@"; do
       head -"${N:-20}" "$OUT/${KIND}_timeline.txt"
       find "$OUT" -name "*.csv" -size +20M -delete ;;
     kstats:*)
-      KIND=${STEP#kstats:}
-      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/${KIND}_stats" -o run --output-format csv \
-        -- python3 tools/bench_sparse.py $(sparse_args "$KIND") > "$OUT/${KIND}_stats.log" 2>&1
-      cp "$(find "$OUT/${KIND}_stats" -name '*kernel_stats.csv' | head -1)" "$OUT/${KIND}_kernel_stats.csv"
+      IFS=':' read -r _ KIND LIB <<< "$STEP"
+      NAME=${KIND}${LIB:+_$LIB}
+      (
+        if [ -n "$LIB" ]; then export SKML_LIB=sketchml_amd/$LIB/libskml.so; fi
+        timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/${NAME}_stats" -o run --output-format csv \
+          -- python3 tools/bench_sparse.py $(sparse_args "$KIND") > "$OUT/${NAME}_stats.log" 2>&1
+      )
+      cp "$(find "$OUT/${NAME}_stats" -name '*kernel_stats.csv' | head -1)" "$OUT/${NAME}_kernel_stats.csv"
       find "$OUT" -name "*kernel_trace.csv" -size +20M -delete ;;
     hiptrace)
       timeout -k 10 300 rocprofv3 --hip-trace --kernel-trace --memory-copy-trace -d "$OUT/hiptrace" -o run \
