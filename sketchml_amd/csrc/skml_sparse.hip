@@ -1187,8 +1187,12 @@ __device__ __forceinline__ void mm_cells(const int32_t (&key)[kMmBatch], int64_t
         const int64_t i = base + u * kMmThreads + threadIdx.x;
         if (i >= c1) continue;
         uint32_t h;
+#ifdef SKML_ABLATE_GP_HASH  // timing ablation only (wrong cells): the insert's hashes priced
+        h = (uint32_t)key[u] * 2654435761u;
+#else
         if constexpr (ID >= 3) h = key[u] >= 0 ? bkdr_fast<ID>((uint32_t)key[u], BK) : java_hash_mix(ID, key[u]);
         else h = java_hash_mix(ID, key[u]);
+#endif
         const int64_t cell = row0 + java_mod((int32_t)h, cols, dv);
         if (cells_out) cells_out[(int64_t)r * n + i] = (int32_t)cell;  // hashed once, reused by the scatter
         const int b = (int)(cell >> kMmBucketBits);
