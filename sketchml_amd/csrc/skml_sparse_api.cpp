@@ -1733,14 +1733,9 @@ int check_blob_groups(const SpBlobHeader& h, const SpGroups& G) {
     return SKML_OK;
 }
 
-// The host meta of a blob at `dev` (header, group table, quantizer header + splits, values), read
-// with one device-to-host copy, and a non-owning skml_sparse view of its device sections.
-int blob_meta(skml_ctx* c, const uint8_t* dev, size_t len, SpBlobHeader* h, skml_sparse* view) {
-    if (!dev || len < 256 || (reinterpret_cast<uintptr_t>(dev) & 255))
-        return sfail(SKML_E_ARG, "sparse blob: NULL, shorter than its header or not 256-byte aligned");
-    if (int e = sync_to_host(c, h, dev, sizeof(*h))) return e;
+// A blob's header, checked against the `len` bytes it may span.
+int blob_check_header(const SpBlobHeader* h, size_t len) {
     if (h->magic != kSpBlobMagic || h->version != 1) return sfail(SKML_E_STATE, "not a sparse blob");
-    const size_t meta_end = (size_t)h->off_tables;
     if (h->total_bytes < 256 || (size_t)h->total_bytes > len || h->nnz < 0 || h->nnz > INT32_MAX || h->ncells < 0 ||
         h->nvalues < 1 || h->nvalues > SKML_MAX_BINS || h->quant_bytes < kHeaderBytes ||
         h->off_groups != 256 || h->off_quant < h->off_groups + (int64_t)sizeof(SpGroups) ||
@@ -1748,29 +1743,77 @@ int blob_meta(skml_ctx* c, const uint8_t* dev, size_t len, SpBlobHeader* h, skml
         h->off_flags < h->off_tables + 4 * h->ncells || h->off_deltas < h->off_flags + 8 * h->n_flag_words ||
         h->total_bytes < h->off_deltas + 8 * h->n_delta_words || (h->off_tables | h->off_flags | h->off_deltas) & 255)
         return sfail(SKML_E_ARG, "sparse blob: inconsistent section offsets");
-    std::vector<uint8_t> meta(meta_end);
-    if (int e = sync_to_host(c, meta.data(), dev, meta_end)) return e;
-    std::memcpy(&view->g, meta.data() + h->off_groups, sizeof(SpGroups));
-    if (int e = check_blob_groups(*h, view->g)) return e;
-    std::memcpy(&view->hdr, meta.data() + h->off_quant, sizeof(skml_dense_header));
-    const double* sp = reinterpret_cast<const double*>(meta.data() + h->off_quant + kHeaderBytes);
-    const int ns = (h->quant_bytes - kHeaderBytes) / 8;
-    view->splits.assign(sp, sp + ns);
-    const double* qv = reinterpret_cast<const double*>(meta.data() + h->off_values);
-    view->qvalues.assign(qv, qv + h->nvalues);
-    view->device = ctx_device(c);
-    view->nnz = h->nnz;
-    view->params = h->params;
-    view->ncells = h->ncells;
-    view->flag_bits = h->flag_bits;
-    view->delta_bits = h->delta_bits;
-    view->n_flag_words = h->n_flag_words;
-    view->n_delta_words = h->n_delta_words;
-    view->g_dev = reinterpret_cast<SpGroups*>(const_cast<uint8_t*>(dev) + h->off_groups);
-    view->tables = reinterpret_cast<int32_t*>(const_cast<uint8_t*>(dev) + h->off_tables);
-    view->flag_words = reinterpret_cast<uint64_t*>(const_cast<uint8_t*>(dev) + h->off_flags);
-    view->delta_words = reinterpret_cast<uint64_t*>(const_cast<uint8_t*>(dev) + h->off_deltas);
     return SKML_OK;
+}
+
+// A non-owning skml_sparse view of the blob at `dev`, from its host meta `meta` (header, group
+// table, quantizer header + splits, values: the blob's bytes up to off_tables).
+int blob_view(skml_ctx* c, const uint8_t* dev, const SpBlobHeader& h, const uint8_t* meta, skml_sparse* view) {
+    std::memcpy(&view->g, meta + h.off_groups, sizeof(SpGroups));
+    if (int e = check_blob_groups(h, view->g)) return e;
+    std::memcpy(&view->hdr, meta + h.off_quant, sizeof(skml_dense_header));
+    const double* sp = reinterpret_cast<const double*>(meta + h.off_quant + kHeaderBytes);
+    const int ns = (h.quant_bytes - kHeaderBytes) / 8;
+    view->splits.assign(sp, sp + ns);
+    const double* qv = reinterpret_cast<const double*>(meta + h.off_values);
+    view->qvalues.assign(qv, qv + h.nvalues);
+    view->device = ctx_device(c);
+    view->nnz = h.nnz;
+    view->params = h.params;
+    view->ncells = h.ncells;
+    view->flag_bits = h.flag_bits;
+    view->delta_bits = h.delta_bits;
+    view->n_flag_words = h.n_flag_words;
+    view->n_delta_words = h.n_delta_words;
+    view->g_dev = reinterpret_cast<SpGroups*>(const_cast<uint8_t*>(dev) + h.off_groups);
+    view->tables = reinterpret_cast<int32_t*>(const_cast<uint8_t*>(dev) + h.off_tables);
+    view->flag_words = reinterpret_cast<uint64_t*>(const_cast<uint8_t*>(dev) + h.off_flags);
+    view->delta_words = reinterpret_cast<uint64_t*>(const_cast<uint8_t*>(dev) + h.off_deltas);
+    return SKML_OK;
+}
+
+// The host meta of P blobs at `dev` + p * stride and their views: the first 16 KB of every blob
+// (header, group table, quantizer and values of up to ~1,000 bins) in one strided device-to-host
+// copy, and only if some blob's meta runs past that, every blob's meta in a second (a read-back
+// per blob and section cost ~20 us of host round trip each, 16 of them for 8 payloads).
+int blob_metas(skml_ctx* c, const uint8_t* dev, int P, size_t stride, SpBlobHeader* hs, skml_sparse* views) {
+    if (!dev || P < 1 || stride < 256 || (stride & 255) || (reinterpret_cast<uintptr_t>(dev) & 255))
+        return sfail(SKML_E_ARG, "sparse blob: NULL, shorter than its header or not 256-byte aligned");
+    hipStream_t st = ctx_stream(c);
+    size_t w = std::min<size_t>(stride, 16384);
+    uint8_t* pin = static_cast<uint8_t*>(ctx_pinned(c, w * (size_t)P));
+    if (!pin) return sfail(SKML_E_OOM, "pinned staging of %zu bytes", w * (size_t)P);
+    SP_HIP(hipMemcpy2DAsync(pin, w, dev, stride, w, (size_t)P, hipMemcpyDeviceToHost, st));
+    SP_HIP(hipStreamSynchronize(st));
+    size_t meta_max = 0;
+    for (int p = 0; p < P; p++) {
+        std::memcpy(&hs[p], pin + (size_t)p * w, sizeof(SpBlobHeader));
+        if (int e = blob_check_header(&hs[p], stride)) return sfail(e, "payload %d: %s", p, skml_last_error());
+        meta_max = std::max(meta_max, (size_t)hs[p].off_tables);
+    }
+    if (meta_max > w) {  // off_tables is a multiple of 256 below total_bytes <= stride
+        w = meta_max;
+        pin = static_cast<uint8_t*>(ctx_pinned(c, w * (size_t)P));
+        if (!pin) return sfail(SKML_E_OOM, "pinned staging of %zu bytes", w * (size_t)P);
+        SP_HIP(hipMemcpy2DAsync(pin, w, dev, stride, w, (size_t)P, hipMemcpyDeviceToHost, st));
+        SP_HIP(hipStreamSynchronize(st));
+    }
+    for (int p = 0; p < P; p++)
+        if (int e = blob_view(c, dev + (size_t)p * stride, hs[p], pin + (size_t)p * w, &views[p]))
+            return sfail(e, "payload %d: %s", p, skml_last_error());
+    return SKML_OK;
+}
+
+// The host meta of a blob at `dev` (header, group table, quantizer header + splits, values) and a
+// non-owning skml_sparse view of its device sections.
+int blob_meta(skml_ctx* c, const uint8_t* dev, size_t len, SpBlobHeader* h, skml_sparse* view) {
+    if (!dev || len < 256 || (reinterpret_cast<uintptr_t>(dev) & 255))
+        return sfail(SKML_E_ARG, "sparse blob: NULL, shorter than its header or not 256-byte aligned");
+    if (int e = sync_to_host(c, h, dev, sizeof(*h))) return e;
+    if (int e = blob_check_header(h, len)) return e;
+    std::vector<uint8_t> meta((size_t)h->off_tables);
+    if (int e = sync_to_host(c, meta.data(), dev, meta.size())) return e;
+    return blob_view(c, dev, *h, meta.data(), view);
 }
 
 // a view points into memory it does not own: cleared before it goes out of scope, so no later
@@ -1925,11 +1968,7 @@ int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t
     hipStream_t st = ctx_stream(c);
     std::vector<SpBlobHeader> hs((size_t)P);
     std::vector<skml_sparse> views((size_t)P);  // non-owning: skml_sparse frees nothing on destruction
-    for (int p = 0; p < P; p++) {
-        if (int e = blob_meta(c, static_cast<const uint8_t*>(blobs) + (size_t)p * stride, stride, &hs[(size_t)p],
-                              &views[(size_t)p]))
-            return sfail(e, "payload %d: %s", p, skml_last_error());
-    }
+    if (int e = blob_metas(c, static_cast<const uint8_t*>(blobs), P, stride, hs.data(), views.data())) return e;
     const int64_t lim = (int64_t)(int32_t)((uint32_t)dim * 2u) / 3;  // dim * 2 / 3 with Java int wrap
     // run bounds are taken per tile of the tile kernel: 512 keys for the wave-tile form, else 4,096
     const int64_t ntiles_max = sp_tiles(dim, (int64_t)1 << agg_tile_bits(true));

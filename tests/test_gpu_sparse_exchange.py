@@ -95,6 +95,38 @@ def test_corrupt_blobs_are_refused(gpu):
 
 
 
+def test_decode_sum_refuses_a_corrupt_payload_among_several(gpu):
+    """Gradient.sum reads every payload's header and meta in two strided copies: a payload with a
+    bad magic, one whose sections run past the stride and one with inconsistent offsets are each
+    refused by index, and the intact set still sums exactly."""
+    dim = 40009
+    pls, osps = zip(*[_payload(gpu, dim, 0.2, 30 + p) for p in range(3)])
+    allb, stride = _gather_local(pls)
+    bad = allb.clone()
+    bad[stride] ^= 0xFF                           # payload 1's magic
+    with pytest.raises(gpu.SketchMLException, match="payload 1"):
+        gpu.decode_sum(bad, 3, stride, dim)
+    bad = allb.clone()
+    total = np.array([stride + 256], dtype=np.int64).view(np.uint8)
+    bad[2 * stride + 8:2 * stride + 16] = torch.from_numpy(total).cuda()  # payload 2 claims more than its slot
+    with pytest.raises(gpu.SketchMLException, match="payload 2"):
+        gpu.decode_sum(bad, 3, stride, dim)
+    got = gpu.decode_sum(allb, 3, stride, dim).cpu().numpy()
+    want, _ = oracle_sum(osps, dim)
+    assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
+
+
+def test_decode_sum_payload_meta_past_the_first_read(gpu):
+    """A payload of 3,000 bins carries ~48 KB of splits and values, past the 16 KB that the first
+    strided read-back takes of every blob: the metas are read again whole, and the sum is exact."""
+    dim = 50021
+    pls, osps = zip(*[_payload(gpu, dim, 0.3, 40, bins=256), _payload(gpu, dim, 0.3, 41, bins=3000)])
+    allb, stride = _gather_local(pls)
+    got = gpu.decode_sum(allb, 2, stride, dim).cpu().numpy()
+    want, _ = oracle_sum(osps, dim)
+    assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
+
+
 @pytest.mark.parametrize("bins,forms", [(256, {}), (1000, {}), (256, {"rs_rounds": 1}), (256, {"rs_rounds": 2})])
 def test_restore_values_refuse_bins_outside_quant_values(gpu, bins, forms):
     """quantValues[bin] with a bin past the values (SparseVectorCompressor.java:118-126 throws
