@@ -17,7 +17,7 @@
 #                             --aggregate 8), the last N operations -> TAG/KIND_timeline.txt
 #   kstats:KIND[:LIB]         rocprofv3 --kernel-trace --stats over the same (with sketchml_amd/LIB/libskml.so
 #                             if given) -> TAG/KIND[_LIB]_kernel_stats.csv
-#   hiptrace                  HIP API + kernel trace of the C3 encode -> TAG/hiptrace/
+#   hiptrace[:KIND]           HIP API + kernel trace of the C3 encode (or KIND as in timeline) -> TAG/hiptrace/
 #   leafgap                   tools/leaf_gap.py (clean / evented / synchronised encode blocks)
 #   leafwaves[:LIB]           tools/prof_leaf_waves.py at 2^28 (a SKML_PROF_LEAF build in LIB)
 #   mergephases[:LIB]         tools/prof_merge.py at 2^28 (a SKML_PROF_SUMMARY build in LIB)
@@ -75,9 +75,11 @@ for STEP in "$@"; do
       )
       cp "$(find "$OUT/${NAME}_stats" -name '*kernel_stats.csv' | head -1)" "$OUT/${NAME}_kernel_stats.csv"
       find "$OUT" -name "*kernel_trace.csv" -size +20M -delete ;;
-    hiptrace)
+    hiptrace*)
+      KIND=${STEP#hiptrace}; KIND=${KIND#:}
+      if [ -n "$KIND" ]; then ARGS=$(sparse_args "$KIND"); else ARGS="--reps 3 --only-e2e"; fi
       timeout -k 10 300 rocprofv3 --hip-trace --kernel-trace --memory-copy-trace -d "$OUT/hiptrace" -o run \
-        --output-format csv -- python3 tools/bench_sparse.py --reps 3 --only-e2e > "$OUT/hiptrace.log" 2>&1
+        --output-format csv -- python3 tools/bench_sparse.py $ARGS > "$OUT/hiptrace.log" 2>&1
       find "$OUT" -name "*.csv" -size +30M -delete ;;
     leafgap)
       timeout -k 10 200 python tools/leaf_gap.py --steps 20 --reps 3 > "$OUT/leaf_gap.jsonl" 2>&1
