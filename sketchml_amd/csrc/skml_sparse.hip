@@ -4477,13 +4477,23 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_merge_pf(const int32_t* __res
     };
     auto load = [&](int b, int32_t (&kk)[kRsBatch], int32_t (&bb)[kRsBatch]) {
         const int cnt = pre[b][G];
+        // the run ends in registers once per range (at most 8 runs), not one LDS read per run and element
+        int32_t re[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) re[q] = q + 1 <= G ? pre[b][q + 1] : INT32_MAX;
 #pragma unroll
         for (int u = 0; u < kRsBatch; u++) {
             const int j = u * kRsThreads + t_;
             kk[u] = -1;
             bb[u] = 0;
             if (j < cnt) {
-                const int g = run_of(b, j);
+                int g = 0;
+                if (G <= 8) {
+#pragma unroll
+                    for (int q = 0; q < 8; q++) g += re[q] <= j ? 1 : 0;
+                } else {
+                    g = run_of(b, j);
+                }
                 const int64_t i = lo_s[b][g] + (j - pre[b][g]);
                 kk[u] = gk[i];
                 bb[u] = gb[i];
