@@ -3759,8 +3759,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_agg_rmw(
     __shared__ uint32_t here[WAVES][64];
     __shared__ double qt[kAggPB][kAggLdsValues];
     __shared__ int32_t pre[2][WAVES][65];
-    __shared__ int32_t pk0[2][WAVES][64];
-    __shared__ int32_t pn0[2][WAVES][64];
+    __shared__ int2 pkn[2][WAVES][64];  // piece s's key / bin element bases minus its first index pre[s]
     __shared__ __attribute__((aligned(16))) uint8_t pcs[WAVES][64 * PER];  // piece of element j
     __shared__ AggPayload pl[kAggPB];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -3794,8 +3793,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_agg_rmw(
         const int32_t x = (int32_t)wave_incl_scan_u32((uint32_t)len);
         pre[buf][wave][ln + 1] = x;
         if (ln == 0) pre[buf][wave][0] = 0;
-        pk0[buf][wave][ln] = gk_off + b0;
-        pn0[buf][wave][ln] = gb_off + b0;
+        pkn[buf][wave][ln] = make_int2(gk_off + b0 - (x - len), gb_off + b0 - (x - len));
         __builtin_amdgcn_wave_barrier();
         return __builtin_amdgcn_readlane(x, 63);
     };
@@ -3806,25 +3804,13 @@ __global__ __launch_bounds__(64 * WAVES) void k_agg_rmw(
             if (pre[buf][wave][s_ + step] <= j) s_ += step;
         return s_;
     };
-    // the pieces of the elements held in registers: lane l searches the piece of j = PER l and
-    // walks on through PER l + PER - 1 (a piece holds ~6-13 elements of a C3 tile), into pcs; the
-    // loads then read the piece of j = l + 64 u back (one search per lane instead of per element)
+    // the pieces of the elements held in registers: lane l writes its own piece's number over the
+    // piece's elements in pcs (a piece holds ~6-13 elements of a C3 tile: stores, no dependent
+    // LDS reads); the loads then read the piece of j = l + 64 u back
     auto load = [&](int buf, int total, int ln, int32_t (&kk)[PER], uint32_t (&bb)[PER]) {
         {
-            const int j0 = PER * ln;
-            if (j0 < total) {
-                int s_ = piece_of(buf, j0);
-                uint32_t w[PER / 4] = {};
-#pragma unroll
-                for (int u = 0; u < PER; u++) {
-                    const int j = j0 + u;
-                    if (j < total)
-                        while (pre[buf][wave][s_ + 1] <= j) s_++;
-                    w[u >> 2] |= (uint32_t)s_ << (8 * (u & 3));
-                }
-                if constexpr (PER == 8) *reinterpret_cast<uint2*>(&pcs[wave][j0]) = make_uint2(w[0], w[1]);
-                else *reinterpret_cast<uint4*>(&pcs[wave][j0]) = make_uint4(w[0], w[1], w[2], w[3]);
-            }
+            const int e0 = pre[buf][wave][ln], e1 = min(pre[buf][wave][ln + 1], 64 * PER);
+            for (int e = e0; e < e1; e++) pcs[wave][e] = (uint8_t)ln;
             __builtin_amdgcn_wave_barrier();
         }
         int spc[PER];
@@ -3839,9 +3825,10 @@ __global__ __launch_bounds__(64 * WAVES) void k_agg_rmw(
             kk[u] = INT32_MIN;
             bb[u] = 0;
             if (j < total) {
-                const int sp = spc[u], d = j - pre[buf][wave][sp];
-                kk[u] = gload<int32_t>(kbase, (uint32_t)(pk0[buf][wave][sp] + d));
-                bb[u] = gload<uint8_t>(bbase, (uint32_t)(pn0[buf][wave][sp] + d)) | ((uint32_t)(sp >> 3) << 8);
+                const int sp = spc[u];
+                const int2 kb = pkn[buf][wave][sp];
+                kk[u] = gload<int32_t>(kbase, (uint32_t)(kb.x + j));
+                bb[u] = gload<uint8_t>(bbase, (uint32_t)(kb.y + j)) | ((uint32_t)(sp >> 3) << 8);
             }
         }
     };
@@ -3962,13 +3949,14 @@ __global__ __launch_bounds__(64 * WAVES) void k_agg_rmw(
         for (int j0 = 64 * PER; j0 < total; j0 += 64) {  // rows past the registers
             const int j = j0 + ln;
             const bool act = j < total;
-            int sp = 0, d = 0;
+            int sp = 0;
+            int2 kb = make_int2(0, 0);
             if (act) {
                 sp = piece_of(buf, j);
-                d = j - pre[buf][wave][sp];
+                kb = pkn[buf][wave][sp];
             }
-            const int32_t k = act ? gload<int32_t>(kbase, (uint32_t)(pk0[buf][wave][sp] + d)) : 0;
-            const uint32_t b = act ? gload<uint8_t>(bbase, (uint32_t)(pn0[buf][wave][sp] + d)) : 0u;
+            const int32_t k = act ? gload<int32_t>(kbase, (uint32_t)(kb.x + j)) : 0;
+            const uint32_t b = act ? gload<uint8_t>(bbase, (uint32_t)(kb.y + j)) : 0u;
             add_row(act, sp >> 3, k, b);
         }
         finish(p_act, P, ln);  // the payloads from the last one seen on
