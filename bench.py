@@ -247,6 +247,7 @@ def other_configs(sk, lib, ctx, dev):
         xs.append(torch.randn(2**26, device=dev, generator=gen))
     out["dense_c2"] = dense_bucket(sk, lib, ctx, dev, xs, "C2: 2^26-float dense gradient bucket, 256 requested bins, "
                                    "encode (4 rotating buckets)")
+    out["dense_c2"]["parity_test"] = "tests/test_gpu_configs.py::test_c2_full_size_matches_oracle"
 
     def timed(fn, reps):
         fn()
@@ -270,16 +271,17 @@ def other_configs(sk, lib, ctx, dev):
             ts.append(time.perf_counter() - t0)
         return statistics.median(ts), r
 
-    x32 = xs[0]
-    n = x32.numel()
-    x64 = x32.double()
+    n = xs[0].numel()
+    gen.manual_seed(4)
+    x64 = torch.randn(n, dtype=torch.float64, device=dev, generator=gen)
     nb = lib.skml_dense_payload_bytes(n, 256)
     pl = sk.alloc_aligned(nb, dev)
     p = _lib_params(256)
     t64, _ = timed(lambda: lib.skml_dense_encode_f64(ctx, C.c_void_p(x64.data_ptr()), n, C.byref(p),
                                                       C.c_void_p(pl.data_ptr()), nb), 20)
-    out["fp64_encode"] = {"workload": "C2 bucket as fp64 (2^26 doubles), 256 bins", "ms": round(t64 * 1e3, 4),
-                          "gbps_fp64_in": round(8.0 * n / t64 / 1e9, 1)}
+    out["fp64_encode"] = {"workload": "C2 shape in fp64: 2^26 N(0,1) doubles (generator seed 4), 256 bins",
+                          "ms": round(t64 * 1e3, 4), "gbps_fp64_in": round(8.0 * n / t64 / 1e9, 1),
+                          "parity_test": "tests/test_gpu_f64_uniform.py::test_f64_bench_workload_2p26_matches_oracle"}
     del x64, pl
     # several independent buckets per call (skml_dense_encode_batch_f32: two streams, so one
     # bucket's VALU-bound sketch overlaps the previous bucket's HBM-bound quantize)
@@ -291,17 +293,19 @@ def other_configs(sk, lib, ctx, dev):
     caps = (C.c_size_t * nbk)(*([nb] * nbk))
     tb, _ = timed(lambda: lib.skml_dense_encode_batch_f32(ctx, nbk, ptrs, ns, C.byref(p), pptr, caps), 10)
     out["batched_buckets"] = {"workload": f"{nbk} independent 2^26-float buckets per call, 256 bins",
-                              "ms_per_bucket": round(tb / nbk * 1e3, 4), "gbps": round(4.0 * n * nbk / tb / 1e9, 1)}
-    del pls
-    out["dense_decode_sum_c4"] = dense_decode_sum(sk, lib, ctx, dev, xs, n, p)
-    del xs
-    # C5's consumer: 8 payloads of 2^27 floats at 4 requested bins (2-bit codes)
-    x27 = []
-    for b in range(2):
-        gen.manual_seed(27 + 1000 * b)
-        x27.append(torch.randn(2**27, device=dev, generator=gen))
-    out["dense_decode_sum_c5"] = dense_decode_sum(sk, lib, ctx, dev, x27, 2**27, _lib_params(4), bins=4)
-    del x27
+                              "ms_per_bucket": round(tb / nbk * 1e3, 4), "gbps": round(4.0 * n * nbk / tb / 1e9, 1),
+                              "parity_test": "tests/test_gpu_dense.py::test_quantize_buckets_matches_single_encodes, "
+                                             "tests/test_gpu_configs.py::test_c4_consumer_decode_sum_8x2p26_matches_oracle "
+                                             "(8 x 2^26 through the batched encode)"}
+    del pls, xs
+    # the consumers: C4's 8 gathered 2^26-float buckets (bucket r drawn with seed 4 + r, 8-bit codes)
+    # and C5's 8 gathered 2^27-float shards (seed 5 + r, 4 requested bins = 2-bit codes)
+    out["dense_decode_sum_c4"] = dense_decode_sum(sk, lib, ctx, dev, 2**26, 256, 4)
+    out["dense_decode_sum_c4"]["parity_test"] = \
+        "tests/test_gpu_configs.py::test_c4_consumer_decode_sum_8x2p26_matches_oracle"
+    out["dense_decode_sum_c5"] = dense_decode_sum(sk, lib, ctx, dev, 2**27, 4, 5)
+    out["dense_decode_sum_c5"]["parity_test"] = \
+        "tests/test_gpu_configs.py::test_c5_consumer_decode_sum_8x2p27_matches_oracle"
     dim = 2**28
     d = c3_dense(dev, 3, dim)
     te, spl = timed_median(lambda: sk.encode_dense_as_sparse(d, 256, 8, 2, 0.3, 3, 3), 5)
@@ -311,9 +315,12 @@ def other_configs(sk, lib, ctx, dev):
     out["sparse_c3"] = {"workload": "C3: 2^28-dim dense fp32, 10 % nnz, 256 bins, 8 groups, 2 rows, colRatio 0.3",
                         "nnz": nnz, "encode_ms": round(te * 1e3, 3), "gbps_dense_in": round(4.0 * dim / te / 1e9, 1),
                         "roofline_frac": round(alg / te / 1e9 / HBM_PEAK_GBS, 4), "restore_ms": round(td * 1e3, 3),
-                        "note": "median wall time of 5 synchronised calls (one nnz read after the compaction, one read-back at the end)"}
+                        "note": "median wall time of 5 synchronised calls (one nnz read after the compaction, one read-back at the end)",
+                        "parity_test": "tests/test_gpu_sparse_full.py::test_c3_full_size_matches_oracle"}
     del d, rk, rv
     out["sparse_aggregate"] = sparse_aggregate(sk, spl, dim, timed_median, dev)
+    out["sparse_aggregate"]["parity_test"] = \
+        "tests/test_gpu_sparse_exchange.py::test_decode_sum_eight_distinct_c3_payloads_full_size"
     return out
 
 
@@ -363,11 +370,19 @@ def sparse_aggregate(sk, spl, dim, timed_median, dev, P=8):
     return res
 
 
-def dense_decode_sum(sk, lib, ctx, dev, xs, n, p, P=8, bins=256):
-    """C4's consumer on one GPU: P = 8 gathered 2^26-value dense payloads -> fused decode + sum in
-    double + x 1/P (skml_dense_decode_sum_f32), HIP-event timed on the codec stream.  Algorithmic
-    bytes = P * n * b / 8 (codes) + 4 n (fp32 out).  With bins = 4 and n = 2^27: C5's consumer (each
-    rank sums the 8 gathered 2^27-float shards' 2-bit payloads)."""
+def dense_decode_sum(sk, lib, ctx, dev, n, bins, seed0, P=8):
+    """C4's consumer on one GPU: P = 8 gathered 2^26-value dense payloads (bucket r drawn with
+    generator seed seed0 + r, encoded with params seed seed0) -> fused decode + sum in double +
+    x 1/P (skml_dense_decode_sum_f32), HIP-event timed on the codec stream.  Algorithmic bytes =
+    P * n * b / 8 (codes) + 4 n (fp32 out).  With bins = 4 and n = 2^27: C5's consumer (each rank
+    sums the 8 gathered 2^27-float shards' 2-bit payloads)."""
+    gen = torch.Generator(device=dev)
+    xs = []
+    for r in range(P):
+        gen.manual_seed(seed0 + r)
+        xs.append(torch.randn(n, device=dev, generator=gen))
+    p = _lib_params(bins)
+    p.seed = seed0
     nb = lib.skml_dense_payload_bytes(n, bins)
     stride = (nb + 255) // 256 * 256
     allp = sk.alloc_aligned(stride * P, dev)
@@ -377,6 +392,8 @@ def dense_decode_sum(sk, lib, ctx, dev, xs, n, p, P=8, bins=256):
     caps = (C.c_size_t * P)(*([stride] * P))
     if lib.skml_dense_encode_batch_f32(ctx, P, ptrs, ns, C.byref(p), pptr, caps):
         raise RuntimeError("batch encode failed")
+    torch.cuda.synchronize()
+    del xs
     out = torch.empty(n, dtype=torch.float32, device=dev)
     run = lambda: lib.skml_dense_decode_sum_f32(ctx, C.c_void_p(allp.data_ptr()), P, stride,  # noqa: E731
                                                  C.c_void_p(out.data_ptr()), n, 1.0 / P)

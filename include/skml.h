@@ -386,10 +386,9 @@ int skml_sparse_import(skml_ctx* ctx, const void* blob_dev, size_t len, skml_spa
  * key adds quantValues[bin] in double (the live values only, plus the dense form's +0.0, when the
  * payload's live count exceeds dim * 2 / 3: SparseDoubleGradient.toAuto); then out *= scale when
  * scale != 1 (the 1/P average, one double multiply per element).  A key outside [0, dim) fails
- * with SKML_E_ARG (SparseDoubleGradient's bound check).  A key repeated across one payload's groups
- * adds every copy, the lower group's first (Sort.merge order), when the launch takes the staged
- * tiles (<= 8 payloads of <= 8 groups and <= 256 quantValues); a dense-form payload with such a
- * repeat fails with SKML_E_ARG.  Synchronising. */
+ * with SKML_E_ARG (SparseDoubleGradient's bound check), and so do a key repeated across one
+ * payload's groups (its constructor requires strictly increasing keys) and a payload that restores
+ * no keys (its constructor reads indices.head).  Synchronising. */
 int skml_sparse_decode_sum_f64(skml_ctx* ctx, const void* blobs_dev, int32_t P, size_t stride, int64_t dim,
                                double scale, double* out_dev);
 /* Host-memory forms of encode_kv / decode (int[] keys and float[] values in JVM arrays). */

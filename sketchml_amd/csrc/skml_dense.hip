@@ -518,7 +518,9 @@ __global__ __launch_bounds__(256) void k_decode_sum(const uint8_t* __restrict__ 
 // P x bins doubles of dynamic LDS instead of a 32 KB array, and the next step's codes are loaded
 // before this step's lookups.
 constexpr int kOccPer = 8, kOccMaxP = 8;
-constexpr size_t kOccLdsMax = 64 * 1024;  // dynamic LDS of the P tables
+// dynamic LDS of the P tables: what is left of the 64 KB a launch may take without opting in
+// after the kernel's static array of code pointers
+constexpr size_t kOccLdsMax = 64 * 1024 - sizeof(const uint8_t*) * kOccMaxP;
 // The code loads go through a global (address space 1) pointer: the payloads' code pointers sit in
 // LDS, and loads through a generic pointer would be flat loads, which count on lgkmcnt too, so the
 // table lookups' LDS waits would also wait for the next step's prefetched codes.
@@ -642,8 +644,8 @@ hipError_t launch_decode_sum(hipStream_t st, const void* payloads, int P, size_t
                              int64_t n, double scale, int common_bits, int max_bins) {
     if (n <= 0) return hipSuccess;
     if (P < 1 || P > kMaxSumPayloads) return hipErrorInvalidValue;
-    // the occupancy form whenever the P tables fit 64 KB of LDS: every 1..8-bit shape (<= 256 bins),
-    // and 16-bit codes up to 8 payloads x 1,024 bins
+    // the occupancy form whenever the P tables fit beside its static LDS: every 1..8-bit shape
+    // (<= 256 bins), and 16-bit codes up to 8 x 1,023 or 7 x 1,024 bins (8 x 1,024 take k_decode_sum)
     if ((size_t)max_bins * (size_t)P * sizeof(double) <= kOccLdsMax && P <= kOccMaxP && form(SKML_FORM_DECODE_SUM) != 1) {
         const uint8_t* pl = reinterpret_cast<const uint8_t*>(payloads);
         switch (common_bits) {

@@ -1983,20 +1983,19 @@ int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t
         return (size_t)key_words(p) * 4 + (size_t)bin_bytes(p) +
                (size_t)views[(size_t)p].g.G * (size_t)(ntiles_max + 1) * 4 + 1024;
     };
-    std::vector<int> todo;
+    // SketchGradient.toSparse of an empty restore builds SparseDoubleGradient(dim, [], []), whose
+    // constructor reads indices.head (SparseDoubleGradient.scala:11) and throws: so does the sum
     for (int p = 0; p < P; p++)
-        if (views[(size_t)p].nnz > 0) todo.push_back(p);  // an empty restore adds nothing (sparse form)
+        if (views[(size_t)p].nnz == 0)
+            return sfail(SKML_E_ARG, "payload %d restores no keys: head of empty list (SparseDoubleGradient.scala:11)", p);
+    std::vector<int> todo;
+    for (int p = 0; p < P; p++) todo.push_back(p);
     uint8_t* small = scratch<uint8_t>(c, kSlotStatus, 1024 + sizeof(AggPayload) * (size_t)P);
     if (!small) return sfail(SKML_E_OOM, "decode_sum scratch");
     unsigned* err = reinterpret_cast<unsigned*>(small);
     uint64_t* live = reinterpret_cast<uint64_t*>(small + 256);
     AggPayload* d_pays = reinterpret_cast<AggPayload*>(small + 1024);
     SP_HIP(hipMemsetAsync(err, 0, sizeof(unsigned), st));
-    if (todo.empty()) {
-        if (dim > 0) SP_HIP(hipMemsetAsync(out, 0, sizeof(double) * (size_t)dim, st));
-        SP_HIP(hipStreamSynchronize(st));
-        return SKML_OK;
-    }
     size_t at = 0;
     bool first = true;
     while (at < todo.size()) {

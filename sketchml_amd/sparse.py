@@ -187,7 +187,8 @@ def decode_sum(blobs: torch.Tensor, nblobs: int, stride: int, dim: int, scale: f
     `stride` bytes apart: a float64 dense sum of length dim, payloads added in order (then scaled
     when scale != 1).  skml_sparse_decode_sum_f64.  Like SketchGradient.toSparse's
     SparseDoubleGradient constructor, a payload whose restored keys repeat (a key in two groups)
-    or leave [0, dim) raises SketchMLException."""
+    or leave [0, dim), or that restores no keys at all (the constructor reads indices.head),
+    raises SketchMLException."""
     dev = blobs.device
     if out is None:
         out = torch.empty(max(int(dim), 1), dtype=torch.float64, device=dev)

@@ -295,6 +295,75 @@ def test_c5_whole_gradient_2p30_matches_oracle(gpu):
     _full_size_parity(gpu, 2**30, 4, 5, 4, 2)
 
 
+def _decode_sum_bench_workload(gpu, P, n, bins, seed0, param_seed, slice_n=2**24):
+    """bench.py's dense_decode_sum workload at its timed size: P device buckets of n N(0,1) floats
+    (torch generator seed seed0 + r for bucket r), one batched encode (bins, params seed
+    param_seed), then the fused decode + double sum + x 1/P (skml_dense_decode_sum_f32).  Every
+    payload's header and splits against the oracle, then the sum against the oracle's per-payload
+    getValues()[indexOf(x)] summed in double in payload order, x 1/P, rounded once to fp32
+    (Gradient.sum + timesBy, ml/gradient/Gradient.scala:44-49), bit for bit."""
+    L = _lib()
+    ctx = gpu.get_context()
+    xs = []
+    for r in range(P):
+        g = torch.Generator(device="cuda").manual_seed(seed0 + r)
+        xs.append(torch.randn(n, device="cuda", generator=g))
+    nb = L.lib.skml_dense_payload_bytes(n, bins)
+    stride = (nb + 255) // 256 * 256
+    allp = gpu.alloc_aligned(stride * P, "cuda")
+    p = _params(bins, param_seed)
+    ptrs = (C.c_void_p * P)(*[x.data_ptr() for x in xs])
+    pptr = (C.c_void_p * P)(*[allp.data_ptr() + r * stride for r in range(P)])
+    ns = (C.c_int64 * P)(*([n] * P))
+    caps = (C.c_size_t * P)(*([stride] * P))
+    assert L.lib.skml_dense_encode_batch_f32(ctx.handle, P, ptrs, ns, C.byref(p), pptr, caps) == 0, L.last_error()
+    out = torch.empty(n, dtype=torch.float32, device="cuda")
+    assert L.lib.skml_dense_decode_sum_f32(ctx.handle, C.c_void_p(allp.data_ptr()), P, stride,
+                                           C.c_void_p(out.data_ptr()), n, 1.0 / P) == 0, L.last_error()
+    torch.cuda.synchronize()
+    hosts = [x.cpu().numpy() for x in xs]
+    del xs
+    with ThreadPoolExecutor(P) as ex:
+        oqs = list(ex.map(lambda a: O.quantize_header_f32(a, bins, param_seed), hosts))
+    for r, oq in enumerate(oqs):
+        st, h, sp = _header(gpu, allp[r * stride:])
+        assert st == 0
+        assert (h.bin_num, h.zero_idx, h.min, h.max, h.n) == (oq.bin_num, oq.zero_idx, oq.min, oq.max, n), r
+        assert np.array_equal(sp, oq.splits), r
+    got = out.cpu().numpy()
+    del out, allp
+
+    def check(s0):
+        s1 = min(n, s0 + slice_n)
+        acc = np.zeros(s1 - s0, dtype=np.float64)
+        for oq, xh in zip(oqs, hosts):
+            acc += oq.values()[O.index_of_many_f32(oq, xh[s0:s1])]
+        return bool(np.array_equal(got[s0:s1].view(np.uint32), (acc * (1.0 / P)).astype(np.float32).view(np.uint32)))
+
+    with ThreadPoolExecutor(16) as ex:
+        bad = [s0 for s0, ok in zip(range(0, n, slice_n), ex.map(check, range(0, n, slice_n))) if not ok]
+    assert not bad, f"slices differing from the oracle start at {bad[:8]}"
+    return oqs
+
+
+@pytest.mark.timeout(300)
+def test_c5_consumer_decode_sum_8x2p27_matches_oracle(gpu):
+    """C5's consumer as bench.py times it (extras.other_configs.dense_decode_sum_c5): the 8 gathered
+    2^27-float shards of the 2^30-float gradient (shard r drawn with seed 5 + r), 4 requested bins
+    = 2-bit codes, summed by the occupancy decode-sum kernel, bit-exact."""
+    oqs = _decode_sum_bench_workload(gpu, 8, 2**27, 4, 5, 5)
+    assert all(oq.bin_num == 4 for oq in oqs)
+
+
+@pytest.mark.timeout(300)
+def test_c4_consumer_decode_sum_8x2p26_matches_oracle(gpu):
+    """C4's consumer as bench.py times it (extras.other_configs.dense_decode_sum_c4): 8 buckets of
+    2^26 floats (bucket r drawn with seed 4 + r), 256 requested bins (129 effective, 8-bit codes),
+    bit-exact."""
+    oqs = _decode_sum_bench_workload(gpu, 8, 2**26, 256, 4, 4)
+    assert all(oq.bin_num == 129 for oq in oqs)
+
+
 def test_c1_app_loopback_l2_bound(gpu):
     """C1 (the reference's App.dense loopback, sample/App.java:33-63) at exactly 10^6 values:
     oracle parity, the half-bin-width bound per element (P2) and the loopback L2 error equal to

@@ -439,6 +439,46 @@ def _decode_sum_case(gpu, P, bins, n):
     assert np.array_equal(out.cpu().numpy(), (want * (1.0 / P)).astype(np.float32))
 
 
+@pytest.mark.parametrize("P,bins", [(8, 1024), (8, 1023), (7, 1024), (2, 4096)])
+def test_decode_sum_lds_boundary(gpu, P, bins):
+    """16-bit codes at the edge of the occupancy form's LDS: P tables of `bins` doubles plus the
+    kernel's static code-pointer array must fit 64 KB, so 8 x 1,024 bins (exactly 64 KB of tables)
+    take the per-payload kernel and 8 x 1,023 / 7 x 1,024 the occupancy form.  A sketch cannot
+    keep 1,024 distinct splits, so the payloads come from the split-injected encode; the expected
+    sum is every payload's Quantizer.getValues()[indexOf(x)] (Quantizer.java:39-72) in double in
+    payload order, x 1/P."""
+    from sketchml_amd import _lib
+    ctx = gpu.get_context()
+    n = 70001
+    nb = (_lib.lib.skml_dense_payload_bytes(n, bins) + 255) // 256 * 256
+    allp = gpu.alloc_aligned(nb * P, "cuda")
+    want = np.zeros(n, dtype=np.float64)
+    rng = np.random.default_rng(P * 10007 + bins)
+    for p in range(P):
+        splits = np.sort(rng.choice(np.arange(-4 * bins, 4 * bins), bins - 1, replace=False)) / 1024.0
+        mn, mx = -8.0, 8.0
+        x = np.clip(rng.standard_normal(n) * 2.0, mn, mx).astype(np.float32)
+        sp = np.ascontiguousarray(splits, dtype=np.float64)
+        xt = torch.from_numpy(x).cuda()
+        assert _lib.lib.skml_dense_encode_with_splits_f32(ctx.handle, C.c_void_p(xt.data_ptr()), n,
+                                                          sp.ctypes.data_as(_lib.dblp), len(sp), mn, mx,
+                                                          C.c_void_p(allp.data_ptr() + p * nb), nb) == 0
+        torch.cuda.synchronize()
+        h = O.QuantHeader()
+        h.bin_num, h.n, h.min, h.max = bins, n, mn, mx
+        for i, s in enumerate(sp):
+            h.splits[i] = float(s)
+        h.zero_idx = int(np.sum(sp < 0.0))
+        vals = np.zeros(bins, dtype=np.float64)
+        O.lib().orc_get_values(C.byref(h), vals.ctypes.data_as(O.dblp))
+        want += vals[np.searchsorted(sp, x.astype(np.float64), side="right")]
+    out = torch.empty(n, dtype=torch.float32, device="cuda")
+    assert _lib.lib.skml_dense_decode_sum_f32(ctx.handle, C.c_void_p(allp.data_ptr()), P, nb,
+                                              C.c_void_p(out.data_ptr()), n, 1.0 / P) == 0, _lib.last_error()
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), (want * (1.0 / P)).astype(np.float32))
+
+
 def test_dense_vector_compressor_surface(gpu):
     x = torch.from_numpy(_data(12345, 1, "app")).cuda()
     comp = gpu.DenseVectorCompressor(gpu.QuantizationType.QUANTILE, 256, seed=9)

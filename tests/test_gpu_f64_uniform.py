@@ -93,6 +93,46 @@ def test_f64_large_pow2(gpu):
     _check(gq, O.quantize(x, 256, 12), x)
 
 
+@pytest.mark.timeout(300)
+def test_f64_bench_workload_2p26_matches_oracle(gpu):
+    """bench.py's extras.other_configs.fp64_encode workload at its timed size: 2^26 doubles drawn on
+    the device by torch.randn(float64) under generator seed 4, 256 requested bins, the default
+    params (seed 0).  Header, splits, every bin and every decoded double against the oracle's
+    QuantileQuantizer.quantize(double[]) (QuantileQuantizer.java:27-50) over the same values."""
+    import ctypes as C
+    from sketchml_amd import _lib as L
+    ctx = gpu.get_context()
+    n = 2**26
+    g = torch.Generator(device="cuda").manual_seed(4)
+    x = torch.randn(n, dtype=torch.float64, device="cuda", generator=g)
+    p = L.Params()
+    L.lib.skml_params_default(C.byref(p))
+    p.bin_num = 256
+    nb = L.lib.skml_dense_payload_bytes(n, 256)
+    pl = gpu.alloc_aligned(nb, "cuda")
+    assert L.lib.skml_dense_encode_f64(ctx.handle, C.c_void_p(x.data_ptr()), n, C.byref(p),
+                                       C.c_void_p(pl.data_ptr()), nb) == 0, L.last_error()
+    dec = torch.empty(n, dtype=torch.float64, device="cuda")
+    assert L.lib.skml_dense_decode_f64(ctx.handle, C.c_void_p(pl.data_ptr()), C.c_void_p(dec.data_ptr()), n) == 0
+    bins = torch.empty(n, dtype=torch.int32, device="cuda")
+    assert L.lib.skml_dense_bins_i32(ctx.handle, C.c_void_p(pl.data_ptr()), C.c_void_p(bins.data_ptr()), n) == 0
+    h = L.DenseHeader()
+    sp = np.zeros(65536, dtype=np.float64)
+    assert L.lib.skml_dense_info(ctx.handle, C.c_void_p(pl.data_ptr()), C.byref(h), sp.ctypes.data_as(L.dblp),
+                                 65536) == 0
+    xh = x.cpu().numpy()
+    del x
+    oq = O.quantize(xh, 256, int(p.seed))
+    assert oq.bin_num == h.bin_num and oq.bin_num > 100
+    assert (h.zero_idx, h.n) == (oq.zero_idx, n)
+    assert np.float64(h.min).tobytes() == np.float64(oq.min).tobytes()
+    assert np.float64(h.max).tobytes() == np.float64(oq.max).tobytes()
+    assert np.array_equal(sp[: oq.bin_num - 1], oq.splits)
+    gb = bins.cpu().numpy()
+    assert np.array_equal(gb, oq.bins)
+    assert np.array_equal(dec.cpu().numpy().view(np.uint64), oq.values()[oq.bins].view(np.uint64))
+
+
 def test_f64_of_f32_values_equals_f32_path(gpu):
     """fp32 values widened to fp64 give the fp32 path's splits and bins (the reference converts
     every value to double anyway)."""

@@ -289,12 +289,22 @@ def test_decode_sum_mixed_bin_widths(gpu, agg_kernel, order):
     assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
 
 
-def test_decode_sum_skips_empty_payloads(gpu, agg_kernel):
+def test_decode_sum_refuses_empty_payloads(gpu, agg_kernel):
+    """An empty restore cannot reach Gradient.sum in the reference: SketchGradient.toSparse builds
+    SparseDoubleGradient(dim, [], []), whose constructor reads indices.head and throws
+    (SparseDoubleGradient.scala:11).  The oracle raises there, and so does the library, whichever
+    position the empty payload holds."""
     dim = 4096
     empty = gpu.encode_sparse(torch.zeros(0, dtype=torch.int32).cuda(), torch.zeros(0, dtype=torch.float64).cuda())
     p1, o1 = _payload(gpu, dim, 0.2, 31)
-    allb, stride = _gather_local([empty, p1])
-    got = gpu.decode_sum(allb, 2, stride, dim).cpu().numpy()
+    with pytest.raises(O.GradientSumError):
+        O.gradient_sum([(np.zeros(0, np.int32), np.zeros(0)), (o1.restore()[0], o1.q.values()[o1.restore()[1]])], dim)
+    for order in ([empty, p1], [p1, empty]):
+        allb, stride = _gather_local(order)
+        with pytest.raises(gpu.SketchMLException, match="head of empty list"):
+            gpu.decode_sum(allb, 2, stride, dim)
+    allb, stride = _gather_local([p1])  # the context stays usable
+    got = gpu.decode_sum(allb, 1, stride, dim).cpu().numpy()
     want, _ = oracle_sum([o1], dim)
     assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
 

@@ -21,6 +21,7 @@
 #   leafgap                   tools/leaf_gap.py (clean / evented / synchronised encode blocks)
 #   leafwaves[:LIB]           tools/prof_leaf_waves.py at 2^28 (a SKML_PROF_LEAF build in LIB)
 #   mergephases[:LIB]         tools/prof_merge.py at 2^28 (a SKML_PROF_SUMMARY build in LIB)
+#   ubench:NAME               tools/ubench/bin/NAME (built here: hipcc --offload-arch=gfx950 -O3 -o tools/ubench/bin/NAME tools/ubench/NAME.hip)
 # Per-variant libraries and kernel forms go through ab.sh's variants (lib:DIR, form:NAME:VALUE).
 set -e
 TAG=$1
@@ -94,6 +95,10 @@ for STEP in "$@"; do
       SKML_LIB=sketchml_amd/${LIB:-lib_profs}/libskml.so timeout -k 10 120 python tools/prof_merge.py 268435456 \
         > "$OUT/merge_phases.txt" 2>&1
       tail -3 "$OUT/merge_phases.txt" ;;
+    ubench:*)
+      NAME=${STEP#ubench:}
+      timeout -k 10 300 tools/ubench/bin/"$NAME" > "$OUT/ubench_$NAME.txt" 2>&1
+      tail -4 "$OUT/ubench_$NAME.txt" ;;
     *) echo "unknown step $STEP"; exit 2 ;;
   esac
 done

@@ -54,6 +54,7 @@ __global__ __launch_bounds__(256) void kern(float* out, Stamp* st, float seed) {
             else if constexpr (KIND == 26) { asm volatile("v_permlane32_swap_b32 %0, %1" : "+v"(a) : "v"(b)); r = a; }
             else if constexpr (KIND == 27) { asm volatile("v_max_f32_dpp %0, -%1, %2 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(b), "v"(a)); }
             else if constexpr (KIND == 28) { asm volatile("v_max_f32_dpp %0, -%1, %2 row_mirror row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(b), "v"(a)); }
+            else if constexpr (KIND == 30) { asm volatile("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); }
             else if constexpr (KIND == 29) {  // two values per instruction: count as 2 per pair
                 typedef float f2v __attribute__((ext_vector_type(2)));
                 f2v p = {a, b}, q = {sel, sel};
@@ -74,7 +75,7 @@ __global__ __launch_bounds__(256) void kern(float* out, Stamp* st, float seed) {
 
 template <int K>
 void run(const char* name, float* d, Stamp* st, Stamp* hst, int cus) {
-    for (int wps = 4; wps <= 8; wps *= 2) {
+    for (int wps = 1; wps <= 8; wps *= 2) {
         const int blocks = cus * wps;
         const size_t lds = (160 * 1024) / wps - 1024;
         hipFuncSetAttribute((const void*)kern<K>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -118,6 +119,7 @@ int main(int argc, char** argv) {
     hst = (Stamp*)malloc(sizeof(Stamp) * cus * 8 * 4);
     printf("CUs %d\n", cus);
     run<0>("v_min_f32", d, st, hst, cus);
+    run<30>("v_max_f32", d, st, hst, cus);
     run<1>("v_med3_f32", d, st, hst, cus);
     run<2>("v_min_u32", d, st, hst, cus);
     run<3>("v_med3_u32", d, st, hst, cus);
