@@ -125,18 +125,23 @@ int skml_debug_sparse_merge_path(void);
 
 /* Test hook: force one of the library's alternative kernel forms, process-wide.  Every form gives
  * the same results (the tests run each one against the oracle); 0 is the library's own choice.
- * Returns the previous value, or -1 for an unknown id.  Not part of the codec. */
-#define SKML_FORM_LEAF_SPLIT 0      /* 1: one wave per 64-chunk tile always, 2: the split leaf always, 3 / 4 / 5: the last 25 / 12.5 / 50 % split */
-#define SKML_FORM_DECODE_SUM 1      /* 1: the per-payload kernel, 2: the occupancy form without prefetch */
+ * Returns the previous value, -1 for an unknown id, or -2 (nothing changed) for a form whose
+ * kernels only the A/B build carries (built with -DSKML_AB into sketchml_amd/lib_ab/: the forms
+ * measured slower than the default, kept for A/B runs).  Not part of the codec. */
+#define SKML_FORM_LEAF_SPLIT 0      /* 2: the split leaf always (the default at every size); A/B build: 1 one wave per 64-chunk tile, 3 / 4 / 5 the last 25 / 12.5 / 50 % split */
+#define SKML_FORM_DECODE_SUM 1      /* 1: the per-payload kernel (the form for > 8 payloads, mixed widths or wide tables); A/B build: 2 the occupancy form without prefetch */
 #define SKML_FORM_PART_BALLOT 2     /* 1: the ballot-ranked partition scatter */
-#define SKML_FORM_RS_ROUNDS 3       /* 1: Sort.merge by the pairwise merge rounds always, 2: the one-pass merge without prefetch */
-#define SKML_FORM_DEC_ROWS_SERIAL 4 /* 1: the generic MinMax query (rows one by one) for every tile, 2: persistent workgroups (A/B) */
-#define SKML_FORM_AGG_TILES 5       /* 0: Gradient.sum's sum tile in LDS (the default), 1: the 4,096-key wave-per-payload tiles, 2 / 3: staged tiles four / two per round, 4: staged tiles with the next tile prefetched, 5: staged tiles without */
+#define SKML_FORM_RS_ROUNDS 3       /* 1: Sort.merge by the pairwise merge rounds always (the fallback for irregular runs); A/B build: 2 the one-pass merge without prefetch */
+#define SKML_FORM_DEC_ROWS_SERIAL 4 /* 1: the generic MinMax query (rows one by one; the form for edge tiles and rows != 2) for every tile; A/B build: 2 persistent workgroups */
+#define SKML_FORM_AGG_TILES 5       /* 0: Gradient.sum's sum tile in LDS (the default), 1: the 4,096-key wave-per-payload tiles (the form for > 8 groups or > 256 quantValues); A/B build: 2 / 3 staged tiles four / two per round, 4 staged tiles with the next tile prefetched, 5 staged tiles without */
 #define SKML_FORM_AGG_ONE_LANE 6    /* 1: Gradient.sum restores every payload on the caller's stream */
-#define SKML_FORM_RUN_BOUNDS 7      /* 1: the runs' tile / key-range bounds (Gradient.sum, the one-pass Sort.merge) in passes of their own (k_agg_bounds, k_rs_bounds) instead of by the key query */
-#define SKML_FORM_DEC_LOOKBACK 8    /* 1: the restore's bit lengths and deltas in one pass with decoupled look-backs for the bit offsets and the deltas' prefixes (A/B: slower), 2: the same pass with the deltas' tile scan after it */
+#define SKML_FORM_RUN_BOUNDS 7      /* A/B build: 1 the runs' tile / key-range bounds (Gradient.sum, the one-pass Sort.merge) in passes of their own (k_agg_bounds, k_rs_bounds) instead of by the key query */
+#define SKML_FORM_DEC_LOOKBACK 8    /* A/B build: 1 the restore's bit lengths and deltas in one pass with decoupled look-backs for the bit offsets and the deltas' prefixes, 2 the same pass with the deltas' tile scan after it */
 #define SKML_FORM_COUNT 9
 int skml_debug_form(int id, int value);
+/* Build flags of the loaded library: SKML_BUILD_AB when it carries the A/B-only forms. */
+#define SKML_BUILD_AB 1
+int skml_build_flags(void);
 
 /* ---- Dense path: QuantileQuantizer.quantize + Quantizer.getBins/getValues ---- */
 

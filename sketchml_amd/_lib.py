@@ -77,6 +77,7 @@ _SIGS = {
     "skml_debug_sparse_scratch_fail": (C.c_int, [C.c_int]),
     "skml_debug_sparse_merge_path": (C.c_int, []),
     "skml_debug_form": (C.c_int, [C.c_int, C.c_int]),
+    "skml_build_flags": (C.c_int, []),
     "skml_dense_payload_bytes": (C.c_size_t, [i64, i32]),
     "skml_dense_encode_f32": (C.c_int, [vp, vp, i64, C.POINTER(Params), vp, C.c_size_t]),
     "skml_dense_encode_with_splits_f32": (C.c_int, [vp, vp, i64, dblp, i32, C.c_double, C.c_double,
@@ -171,11 +172,28 @@ FORMS = {"leaf_split": 0, "decode_sum": 1, "part_ballot": 2, "rs_rounds": 3, "de
          "agg_tiles": 5, "agg_one_lane": 6, "run_bounds": 7, "dec_lookback": 8}
 
 
+# SKML_BUILD_AB: the loaded library is the A/B build (sketchml_amd/lib_ab, `make -C
+# sketchml_amd/csrc ab`), which also carries the forms measured slower than the default
+AB_BUILD = bool(lib.skml_build_flags() & 1)
+
+
+class FormNotBuilt(RuntimeError):
+    """A kernel form only the A/B build carries (skml_debug_form returned -2)."""
+
+
 @contextlib.contextmanager
 def forced_forms(**values):
-    """with forced_forms(rs_rounds=1, ...): the named forms forced for the duration."""
-    prev = {k: lib.skml_debug_form(FORMS[k], int(v)) for k, v in values.items()}
+    """with forced_forms(rs_rounds=1, ...): the named forms forced for the duration.  Raises
+    FormNotBuilt (forcing nothing) for a form this build does not carry."""
+    prev = {}
     try:
+        for k, v in values.items():
+            r = lib.skml_debug_form(FORMS[k], int(v))
+            if r == -2:
+                raise FormNotBuilt(f"form {k}={v} is built only with -DSKML_AB (SKML_LIB=sketchml_amd/lib_ab/libskml.so)")
+            if r < 0:
+                raise ValueError(f"unknown form {k}")
+            prev[k] = r
         yield
     finally:
         for k, v in prev.items():

@@ -133,9 +133,37 @@ static std::atomic<int> g_form[SKML_FORM_COUNT];
 int form(int id) { return id >= 0 && id < SKML_FORM_COUNT ? g_form[id].load(std::memory_order_relaxed) : 0; }
 }  // namespace skml
 
+// The forms whose kernels only the A/B build (-DSKML_AB, sketchml_amd/lib_ab) carries: measured
+// slower than the default, kept for the A/B tools and the tests that load that build.
+static bool ab_only_form(int id, int v) {
+    switch (id) {
+        case SKML_FORM_LEAF_SPLIT: return v == 1 || v >= 3;
+        case SKML_FORM_DECODE_SUM: return v == 2;
+        case SKML_FORM_RS_ROUNDS: return v == 2;
+        case SKML_FORM_DEC_ROWS_SERIAL: return v == 2;
+        case SKML_FORM_AGG_TILES: return v >= 2;
+        case SKML_FORM_RUN_BOUNDS: return v != 0;
+        case SKML_FORM_DEC_LOOKBACK: return v != 0;
+        default: return false;
+    }
+}
+
 extern "C" int skml_debug_form(int id, int value) {
     if (id < 0 || id >= SKML_FORM_COUNT) return -1;
+#ifndef SKML_AB
+    if (ab_only_form(id, value)) return -2;
+#else
+    (void)ab_only_form;
+#endif
     return g_form[id].exchange(value);
+}
+
+extern "C" int skml_build_flags(void) {
+#ifdef SKML_AB
+    return SKML_BUILD_AB;
+#else
+    return 0;
+#endif
 }
 
 namespace {

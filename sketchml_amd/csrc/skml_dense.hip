@@ -630,13 +630,15 @@ hipError_t launch_occ(hipStream_t st, const uint8_t* pl, int P, size_t stride, f
     const size_t lds = sizeof(double) * (size_t)max_bins * (size_t)P;
     const int64_t groups = n / kOccPer;
     const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((groups + 255) / 256, 4096));
-    const bool pf = form(SKML_FORM_DECODE_SUM) != 2;  // (2: without the next step's prefetch)
-    if (pf)
-        hipLaunchKernelGGL((k_decode_sum_occ<BITS, true>), dim3(grid), dim3(256), lds, st, pl, P, stride, out, n, scale,
-                           max_bins);
-    else
+#ifdef SKML_AB
+    if (form(SKML_FORM_DECODE_SUM) == 2) {  // A/B: without the next step's prefetch (slower)
         hipLaunchKernelGGL((k_decode_sum_occ<BITS, false>), dim3(grid), dim3(256), lds, st, pl, P, stride, out, n, scale,
                            max_bins);
+        return hipGetLastError();
+    }
+#endif
+    hipLaunchKernelGGL((k_decode_sum_occ<BITS, true>), dim3(grid), dim3(256), lds, st, pl, P, stride, out, n, scale,
+                       max_bins);
     return hipGetLastError();
 }
 

@@ -1033,6 +1033,7 @@ static int64_t leaf_split_from(int64_t full_tiles) {
         const int64_t s = full_tiles - full_tiles * pct_x2 / 200;
         return std::max<int64_t>(0, s / kLeaf2Waves * kLeaf2Waves);
     };
+#ifdef SKML_AB  // one wave per tile (1) and the hybrid tails (3 / 4 / 5): measured slower at 2^28
     switch (form(SKML_FORM_LEAF_SPLIT)) {
         case 1: return full_tiles;
         case 2: return 0;
@@ -1041,6 +1042,7 @@ static int64_t leaf_split_from(int64_t full_tiles) {
         case 5: return tail(100);
         default: break;
     }
+#endif
 #if SKML_LEAF_SPLIT_TAIL_PCT >= 100
     return 0;
 #else
@@ -1063,6 +1065,7 @@ hipError_t launch_leaf(hipStream_t st, const float* x, int64_t chunks, uint64_t 
                                full * kLeafWaveChunks, s0, jump_tab, part, nodes6, roots, ubits, chunks, (int64_t)0);
             return hipGetLastError();
         }
+#if defined(SKML_AB) || SKML_LEAF_SPLIT_TAIL_PCT < 100
         if (split_from >= full) {
             const unsigned grid = (unsigned)((full + kLeaf2Waves - 1) / kLeaf2Waves + extra);
             hipLaunchKernelGGL(k_leaf64<0>, dim3(grid), dim3(64 * kLeaf2Waves), 0, st, x, full * kLeafWaveChunks, s0,
@@ -1073,6 +1076,9 @@ hipError_t launch_leaf(hipStream_t st, const float* x, int64_t chunks, uint64_t 
         hipLaunchKernelGGL(k_leaf64<2>, dim3(grid), dim3(64 * kLeaf2Waves), 0, st, x, full * kLeafWaveChunks, s0,
                            jump_tab, part, nodes6, roots, ubits, chunks, split_from);
         return hipGetLastError();
+#else
+        return hipErrorInvalidValue;  // (unreachable: split_from is 0)
+#endif
     } else if (full > 0)
         hipLaunchKernelGGL((k_leaf2<3, false>), dim3((unsigned)((full + kLeaf2Waves - 1) / kLeaf2Waves)),
                            dim3(64 * kLeaf2Waves), 0, st, x, full * kLeafWaveChunks, s0, jump_tab, part,

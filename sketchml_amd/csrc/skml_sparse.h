@@ -169,10 +169,12 @@ hipError_t launch_dec_deltas(hipStream_t st, const uint64_t* delta_words, int64_
 // + 2 u64 of scratch, zeroed by the launch); tile_sums: the tiles' delta sums as launch_dec_deltas
 // writes them, or with scan_sums their exclusive scan and total (a second look-back), as
 // scan_tiles leaves them
+#ifdef SKML_AB
 hipError_t launch_dec_lens_deltas(hipStream_t st, const uint64_t* flag_words, int64_t n_flag_words,
                                   const int64_t* end_pos, int64_t n, const SpGroups* gp,
                                   const uint64_t* delta_words, int64_t n_delta_words, uint32_t* delta,
                                   uint64_t* tile_sums, uint64_t* status, NarrowJob nj, bool scan_sums);
+#endif
 hipError_t launch_group_prefix(hipStream_t st, const uint32_t* delta, int64_t n, const SpGroups* gp, int G,
                                const uint64_t* tile_base, uint64_t* gpre);
 // keys and MinMax bins; gh: the host copy of *gp (the grid follows the group sizes).  width 8 / 16:
@@ -216,8 +218,10 @@ struct AggPayload {
 };
 static_assert(sizeof(AggPayload) % 8 == 0, "copied as u64 words");
 // tile_bits: log2 of the keys per tile the bounds are taken at (agg_tile_bits of the chosen form)
+#ifdef SKML_AB
 hipError_t launch_agg_bounds(hipStream_t st, const int32_t* gk, int64_t n, const SpGroups* gp, int64_t ntiles,
                              int64_t dim, int32_t* bounds, unsigned* err, int tile_bits);
+#endif
 // vtiles: the staged wave-tile form (agg_vtiles_ok: payloads of at most 8 groups and 256
 // quantValues, launched 8 at a time); else the 4,096-key wave-per-payload tiles (any P, G, nq).
 // Both set err bit 1 for a key outside its tile and bit 2 for a key repeated inside one payload.

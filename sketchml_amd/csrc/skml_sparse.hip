@@ -2432,6 +2432,7 @@ __global__ __launch_bounds__(kSpThreads) void k_dec_deltas(const uint64_t* __res
     if (threadIdx.x == 0) tile_sums[blockIdx.x] = tot2[0];
 }
 
+#ifdef SKML_AB  // A/B form, measured slower (profiles/ab/r05_dec_lookback.txt)
 // Lengths and deltas in one pass: each tile (taken in ticket order) computes its lengths in
 // registers, takes its first bit offset in the delta stream by a decoupled look-back over the
 // tiles' bit totals (the compaction's scheme), and extracts its deltas -- no length array written
@@ -2528,6 +2529,8 @@ hipError_t launch_dec_lens_deltas(hipStream_t st, const uint64_t* flag_words, in
                        nj);
     return hipGetLastError();
 }
+#endif  // SKML_AB
+
 
 hipError_t launch_dec_deltas(hipStream_t st, const uint64_t* delta_words, int64_t n_delta_words,
                              const uint8_t* dlen, int64_t n, const SpGroups* gp,
@@ -2895,6 +2898,7 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_keys(const uint32_t* __rest
                                 tile_base[tile], (int)threadIdx.x, rb);
 }
 
+#ifdef SKML_AB  // A/B form, measured slower (profiles/ab/r05_decp.txt)
 // MODE 1 over every inner tile with persistent workgroups: workgroup b walks the tiles that
 // dec_tile_of_block deals to its XCD slot (b % 8), and loads the next tile's deltas and base
 // while it hashes, gathers and stores the current one.  Same output as k_dec_keys<TN, 1, NT>.
@@ -2958,6 +2962,8 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_keys_p(const uint32_t* __re
         tb = tbn;
     }
 }
+#endif  // SKML_AB
+
 
 // workgroups of `kern` (`threads` each) resident at once on the device; 0 if the query fails
 template <typename K>
@@ -3007,16 +3013,23 @@ hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, con
     // MODE 1 with one workgroup per tile; SKML_FORM_DEC_ROWS_SERIAL = 2 selects persistent
     // workgroups with the next tile's deltas in flight (measured slower at 2^28: restore 0.767
     // vs 0.707 ms, profiles/ab/r05_decp.txt; kept as an A/B form)
+#ifdef SKML_AB
     const bool persistent = form(SKML_FORM_DEC_ROWS_SERIAL) == 2;
-#define SKML_DEC_WIDTH(TNT, TNPTR)                                                          \
-    do {                                                                                  \
+#define SKML_DEC_PERSISTENT(TNT, TNPTR)                                                          \
         if (batched && persistent) {                                                      \
             static const int res = resident_blocks(k_dec_keys_p<TNT, true>, kDecThreads); \
             const int64_t ps = res > 0 ? std::max<int64_t>(1, std::min<int64_t>(most, res / 8)) : most; \
             hipLaunchKernelGGL((k_dec_keys_p<TNT, true>), dim3((unsigned)(8 * ps)), dim3(kDecThreads), 0, st, delta, \
                                n, gp, tile_base, gpre, table, TNPTR, gkeys, gbins, nq, gbn, bn_width, err, most, rb); \
             if (edges.n > 0) SKML_DEC_LAUNCH(TNT, 0, (unsigned)edges.n, edges, TNPTR);    \
-        } else if (batched) {                                                             \
+        } else
+#else
+#define SKML_DEC_PERSISTENT(TNT, TNPTR)
+#endif
+#define SKML_DEC_WIDTH(TNT, TNPTR)                                                          \
+    do {                                                                                  \
+        SKML_DEC_PERSISTENT(TNT, TNPTR)                                                   \
+        if (batched) {                                                                    \
             hipLaunchKernelGGL((k_dec_keys<TNT, 1, true>), dim3(grid), dim3(kDecThreads), 0, st, delta, n, gp,    \
                                tile_base, gpre, table, TNPTR, gkeys, gbins, nq, gbn, bn_width, err, all, rb); \
             if (edges.n > 0) SKML_DEC_LAUNCH(TNT, 0, (unsigned)edges.n, edges, TNPTR);    \
@@ -3028,6 +3041,7 @@ hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, con
     else if (width == 16) SKML_DEC_WIDTH(uint16_t, static_cast<const uint16_t*>(tnar));
     else SKML_DEC_WIDTH(int32_t, static_cast<const int32_t*>(nullptr));
 #undef SKML_DEC_WIDTH
+#undef SKML_DEC_PERSISTENT
 #undef SKML_DEC_LAUNCH
     return hipGetLastError();
 }
@@ -3040,6 +3054,7 @@ hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, con
 // sum is read and written once instead of one random read-modify-write per restored key.
 // bounds[g * (ntiles + 1) + t] = first element (payload index) of group g's run with key >=
 // t * kAggTile; 0 throughout for an empty group.
+#ifdef SKML_AB  // the runs' bounds in passes of their own (SKML_FORM_RUN_BOUNDS = 1); the key query writes them
 // Run bounds over 16 consecutive restored keys per thread (four 16-byte loads and the key before
 // them; the group's ends in registers): for each element, the ranges between its predecessor's
 // range and its own get the element's index, and a run's last element closes its run.
@@ -3131,6 +3146,7 @@ hipError_t launch_agg_bounds(hipStream_t st, const int32_t* gk, int64_t n, const
                        tile_bits);
     return hipGetLastError();
 }
+#endif  // SKML_AB
 
 // Loads through AggPayload's pointers as global (address space 1) loads.  The pointers come from
 // memory (the payload table, copied to LDS or registers), so the compiler would emit flat loads,
@@ -3359,6 +3375,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_tiles_w(const AggPayload* _
 // stages and sums them one tile after the other through the same 4 KB stage.
 constexpr int kAggVBits = 9, kAggVTile = 1 << kAggVBits;
 static_assert(kAggVTile == 8 * 64, "eight keys per lane");
+#ifdef SKML_AB  // A/B forms of the sum tile (SKML_FORM_AGG_TILES 2..5), measured slower than k_agg_rmw
 template <int SUB>
 __global__ __launch_bounds__(kAggThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_agg_vtiles(
     const AggPayload* __restrict__ pays, int P, int64_t ntiles, int64_t dim, double* __restrict__ out, int from_out,
@@ -3730,6 +3747,8 @@ __global__ __launch_bounds__(kAggThreads) __attribute__((amdgpu_waves_per_eu(4))
     if (bad) atomicOr(err, bad);
 }
 
+#endif  // SKML_AB
+
 // The sum tile itself in LDS: the waves, run pieces and prefetch of k_agg_vtiles_pf, but each
 // element is added straight into the wave's tile of doubles (read, add, write back) instead of
 // being staged as a bin and summed by a sweep over every (payload, key) slot, which looked up
@@ -4002,11 +4021,36 @@ hipError_t launch_agg_tiles(hipStream_t st, const AggPayload* pays, int P, int64
     if (ntiles <= 0) return hipSuccess;
     if (vtiles) {
         if (P < 1 || P > kAggVPayloads) return hipErrorInvalidValue;  // one lane per (payload, group)
-        // the default: the sum tile in LDS (k_agg_rmw); SKML_FORM_AGG_TILES = 6: its 512-key form,
-        // 4 / 5 / 2 / 3: the prefetching staged form (5.57-5.64 against 5.63-5.66 ms for 8 C3
-        // payloads, profiles/ab/r05_pf.txt), the plain staged tiles, four / two tiles per wave
-        // round (A/B forms)
-        if (form(SKML_FORM_AGG_TILES) == 0) {  // the sum tile in LDS (dense-form payloads swept)
+        // the default: the sum tile in LDS (k_agg_rmw); the A/B build adds SKML_FORM_AGG_TILES 4 / 5
+        // (the staged tiles with and without the next tile's prefetch; 5.57-5.64 against 5.63-5.66
+        // ms for 8 C3 payloads, profiles/ab/r05_pf.txt, both slower than k_agg_rmw) and 2 / 3 (four /
+        // two staged tiles per wave round)
+#ifdef SKML_AB
+        const int f = form(SKML_FORM_AGG_TILES);
+        if (f >= 2 && f <= 5) {
+            if (f == 4) {
+                static const int resident_pf = resident_workgroups(k_agg_vtiles_pf);
+                const int64_t all = sp_tiles(ntiles, kAggThreads / 64);
+                const unsigned grid = (unsigned)(resident_pf <= 0 ? all : std::min<int64_t>(all, resident_pf));
+                hipLaunchKernelGGL(k_agg_vtiles_pf, dim3(grid), dim3(kAggThreads), 0, st, pays, P, ntiles, dim, out,
+                                   from_out, scale, err, kbase, bbase);
+                return hipGetLastError();
+            }
+#define SKML_VT_LAUNCH(SUB)                                                                                  \
+    do {                                                                                                     \
+        static const int res = resident_workgroups(k_agg_vtiles<SUB>);                                        \
+        const int64_t all = sp_tiles(sp_tiles(ntiles, SUB), kAggThreads / 64);                               \
+        const unsigned grid = (unsigned)(res <= 0 ? all : std::min<int64_t>(all, res));                      \
+        hipLaunchKernelGGL(k_agg_vtiles<SUB>, dim3(grid), dim3(kAggThreads), 0, st, pays, P, ntiles, dim, out, \
+                           from_out, scale, err, kbase, bbase);                                              \
+    } while (0)
+            if (f == 2) SKML_VT_LAUNCH(4);
+            else if (f == 3) SKML_VT_LAUNCH(2);
+            else SKML_VT_LAUNCH(1);
+#undef SKML_VT_LAUNCH
+            return hipGetLastError();
+        }
+#endif
 #define SKML_RMW_LAUNCH(DENSE)                                                                                   \
     do {                                                                                                         \
         static const int res = resident_blocks(k_agg_rmw<kAggVBits, 8, 8, DENSE>, kAggThreads);                   \
@@ -4015,40 +4059,9 @@ hipError_t launch_agg_tiles(hipStream_t st, const AggPayload* pays, int P, int64
         hipLaunchKernelGGL((k_agg_rmw<kAggVBits, 8, 8, DENSE>), dim3(grid), dim3(kAggThreads), 0, st, pays, P,   \
                            ntiles, dim, out, from_out, scale, err, kbase, bbase);                                \
     } while (0)
-            if (any_dense) SKML_RMW_LAUNCH(true);
-            else SKML_RMW_LAUNCH(false);
+        if (any_dense) SKML_RMW_LAUNCH(true);
+        else SKML_RMW_LAUNCH(false);
 #undef SKML_RMW_LAUNCH
-            return hipGetLastError();
-        }
-        if (form(SKML_FORM_AGG_TILES) == 2) {
-            static const int resident4 = resident_workgroups(k_agg_vtiles<4>);
-            const int64_t all = sp_tiles(sp_tiles(ntiles, 4), kAggThreads / 64);
-            const unsigned grid = (unsigned)(resident4 <= 0 ? all : std::min<int64_t>(all, resident4));
-            hipLaunchKernelGGL(k_agg_vtiles<4>, dim3(grid), dim3(kAggThreads), 0, st, pays, P, ntiles, dim, out,
-                               from_out, scale, err, kbase, bbase);
-            return hipGetLastError();
-        }
-        if (form(SKML_FORM_AGG_TILES) == 0 || form(SKML_FORM_AGG_TILES) == 4) {
-            static const int resident_pf = resident_workgroups(k_agg_vtiles_pf);
-            const int64_t all = sp_tiles(ntiles, kAggThreads / 64);
-            const unsigned grid = (unsigned)(resident_pf <= 0 ? all : std::min<int64_t>(all, resident_pf));
-            hipLaunchKernelGGL(k_agg_vtiles_pf, dim3(grid), dim3(kAggThreads), 0, st, pays, P, ntiles, dim, out,
-                               from_out, scale, err, kbase, bbase);
-            return hipGetLastError();
-        }
-        if (form(SKML_FORM_AGG_TILES) == 3) {
-            static const int resident2 = resident_workgroups(k_agg_vtiles<2>);
-            const int64_t all = sp_tiles(sp_tiles(ntiles, 2), kAggThreads / 64);
-            const unsigned grid = (unsigned)(resident2 <= 0 ? all : std::min<int64_t>(all, resident2));
-            hipLaunchKernelGGL(k_agg_vtiles<2>, dim3(grid), dim3(kAggThreads), 0, st, pays, P, ntiles, dim, out,
-                               from_out, scale, err, kbase, bbase);
-            return hipGetLastError();
-        }
-        static const int resident_v = resident_workgroups(k_agg_vtiles<1>);
-        const int64_t all = sp_tiles(ntiles, kAggThreads / 64);
-        const unsigned grid = (unsigned)(resident_v <= 0 ? all : std::min<int64_t>(all, resident_v));
-        hipLaunchKernelGGL(k_agg_vtiles<1>, dim3(grid), dim3(kAggThreads), 0, st, pays, P, ntiles, dim, out, from_out,
-                           scale, err, kbase, bbase);
         return hipGetLastError();
     }
     // persistent: as many workgroups as are resident at once
@@ -4225,6 +4238,7 @@ hipError_t launch_merge_round(hipStream_t st, const int32_t* kin, const int32_t*
 // range's base + its rank among the set bits, with its bin or quantValues[bin].  A repeated key
 // (a bit already set) flags the input too, and the host then runs the pairwise merge rounds,
 // which follow Sort.merge for any input.  Regular C3 payloads: one pass instead of three rounds.
+#ifdef SKML_AB  // the ranges' bounds in a pass of their own (SKML_FORM_RUN_BOUNDS = 1); the key query writes them
 __global__ __launch_bounds__(kSpThreads) void k_rs_bounds(const int32_t* __restrict__ gk, int64_t n,
                                                           const SpGroups* __restrict__ gp, int32_t* __restrict__ bounds,
                                                           RsInfo* __restrict__ info) {
@@ -4235,6 +4249,8 @@ __global__ __launch_bounds__(kSpThreads) void k_rs_bounds(const int32_t* __restr
     run_bounds16<false>(gk, n, S, bounds, kRsRanges + 1, 0, 0, info, bad);
     if (bad) atomicOr(&info->irregular, 1u);
 }
+
+#endif  // SKML_AB
 
 template <typename V>
 __device__ __forceinline__ V rs_value(int32_t b, const V* lut, const double* qv, int nq, bool lds, unsigned& bad) {
@@ -4251,6 +4267,7 @@ __device__ __forceinline__ V rs_value(int32_t b, const V* lut, const double* qv,
 
 constexpr int kRsThreads = 256, kRsBatch = 4, kRsLut = 1024;
 static_assert(kRsWords == kRsThreads, "one bitmap word per thread");
+#ifdef SKML_AB  // the one-pass merge without the pipelining (SKML_FORM_RS_ROUNDS = 2), measured slower
 template <typename V>
 __global__ __launch_bounds__(kRsThreads) void k_rs_merge(const int32_t* __restrict__ gk, const int32_t* __restrict__ gb,
                                                          const SpGroups* __restrict__ gp,
@@ -4382,6 +4399,8 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_merge(const int32_t* __restri
     }
     if (bad) atomicOr(&info->irregular, 2u);
 }
+
+#endif  // SKML_AB
 
 // Sort.merge in one pass, software pipelined: while range t is marked, scanned and emitted, the
 // element loads of the workgroup's next range are in flight (its piece table computed one range
@@ -4579,8 +4598,13 @@ hipError_t launch_rs_merge(hipStream_t st, const int32_t* gk, const int32_t* gb,
                            int nq, bool bounds_ready) {
     if (n <= 0) return hipSuccess;
     const int64_t bgrid = sp_tiles(sp_tiles(n, 16), kSpThreads);
+#ifdef SKML_AB
     if (!bounds_ready)
         hipLaunchKernelGGL(k_rs_bounds, dim3((unsigned)bgrid), dim3(kSpThreads), 0, st, gk, n, gp, bounds, info);
+#else
+    (void)bgrid;
+    if (!bounds_ready) return hipErrorInvalidValue;  // the key query writes the ranges' bounds
+#endif
     // persistent workgroups over the key ranges up to the largest key (read on the device): as many
     // as are resident at once (4 per CU), fewer for small inputs
     const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(sp_tiles(n, 4096), 1), 1024);
@@ -4597,8 +4621,11 @@ hipError_t launch_rs_merge(hipStream_t st, const int32_t* gk, const int32_t* gb,
             hipLaunchKernelGGL(K<double>, dim3(grid), dim3(kRsThreads), 0, st, gk, gb, gp, bounds, info, keys_out, \
                                static_cast<double*>(out), qv, nq);                                               \
     } while (0)
+#ifdef SKML_AB
     if (form(SKML_FORM_RS_ROUNDS) == 2) SKML_RS_LAUNCH(k_rs_merge);
-    else SKML_RS_LAUNCH(k_rs_merge_pf);
+    else
+#endif
+    SKML_RS_LAUNCH(k_rs_merge_pf);
 #undef SKML_RS_LAUNCH
     return hipGetLastError();
 }

@@ -634,19 +634,25 @@ int decode_groups(skml_ctx* c, const skml_sparse* s, int32_t* gk, int32_t* gb, b
     // decoupled look-backs for the bit offsets and the deltas' prefixes, 2: the same pass with the
     // deltas' tile scan after it (A/B forms, measured slower: the look-back chain across 13 K tiles
     // ran 230 us against 107 us for the three passes, profiles/ab/r05_dec_lookback.txt)
+#ifdef SKML_AB
     const int lb = form(SKML_FORM_DEC_LOOKBACK);
     const int split = lb == 1 ? 0 : lb == 2 ? 2 : 1;
+#else
+    constexpr int split = 1;
+#endif
     if (split == 1) {
         SP_HIP(launch_dec_lens(st, s->flag_words, s->n_flag_words, end_pos, n, s->g_dev, dlen, ts,
                                NarrowJob{tab, s->ncells, tnar, width}));
         if (int e = scan_tiles(c, ts, tiles, 1, nullptr)) return e;
         SP_HIP(launch_dec_deltas(st, s->delta_words, s->n_delta_words, dlen, n, s->g_dev, ts, delta, ts2));
     } else {
+#ifdef SKML_AB
         uint64_t* status = scratch<uint64_t>(c, kSlotLookback, 2 * (size_t)tiles + 8);
         if (!status) return sfail(SKML_E_OOM, "decode scratch (look-back)");
         SP_HIP(launch_dec_lens_deltas(st, s->flag_words, s->n_flag_words, end_pos, n, s->g_dev, s->delta_words,
                                       s->n_delta_words, delta, ts2, status, NarrowJob{tab, s->ncells, tnar, width},
                                       split == 0));
+#endif
     }
     if (split != 0)
         if (int e = scan_tiles(c, ts2, tiles, 1, nullptr)) return e;
@@ -2053,7 +2059,11 @@ int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t
             a.gb_off = (int32_t)bbo;
             // the run bounds come from the key query unless SKML_FORM_RUN_BOUNDS = 1 asks for the
             // separate k_agg_bounds pass (A/B)
+#ifdef SKML_AB
             const bool own_pass = form(SKML_FORM_RUN_BOUNDS) == 1;
+#else
+            constexpr bool own_pass = false;
+#endif
             const DecodeValues dv{a.nq, const_cast<void*>(a.gb), a.bw, err,
                                   own_pass ? RunBoundsOut{nullptr, 0, 0, 0}
                                            : RunBoundsOut{const_cast<int32_t*>(a.bounds), ntiles, dim, tile_bits}};
@@ -2072,9 +2082,11 @@ int skml_sparse_decode_sum_f64(skml_ctx* c, const void* blobs, int32_t P, size_t
                 if (int e = sync_to_host(lc, &nlive, llive, sizeof(nlive))) return join(e);
                 a.dense_form = (int64_t)nlive > lim ? 1 : 0;
             }
+#ifdef SKML_AB
             if (own_pass && launch_agg_bounds(ls, a.gk, v.nnz, v.g_dev, ntiles, dim, const_cast<int32_t*>(a.bounds), err,
                                               tile_bits) != hipSuccess)
                 return join(sfail(SKML_E_HIP, "agg_bounds launch failed"));
+#endif
             pays.push_back(a);
             ko += key_words(p);
             bbo += bin_bytes(p);

@@ -146,6 +146,21 @@ def test_form_ids_match_header():
     with _lib.forced_forms(rs_rounds=1):
         assert _lib.lib.skml_debug_form(_lib.FORMS["rs_rounds"], 1) == 1
     assert _lib.lib.skml_debug_form(_lib.FORMS["rs_rounds"], 0) == 0
+    # the product library refuses the forms only the A/B build carries, and changes nothing
+    ab_only = [("leaf_split", 1), ("leaf_split", 4), ("decode_sum", 2), ("rs_rounds", 2), ("dec_rows_serial", 2),
+               ("agg_tiles", 2), ("agg_tiles", 5), ("run_bounds", 1), ("dec_lookback", 1), ("dec_lookback", 2)]
+    for name, v in ab_only:
+        if _lib.AB_BUILD:
+            assert _lib.lib.skml_debug_form(_lib.FORMS[name], v) == 0
+            assert _lib.lib.skml_debug_form(_lib.FORMS[name], 0) == v
+        else:
+            assert _lib.lib.skml_debug_form(_lib.FORMS[name], v) == -2
+            assert _lib.lib.skml_debug_form(_lib.FORMS[name], 0) == 0
+            other = "part_ballot" if name == "rs_rounds" else "rs_rounds"
+            with pytest.raises(_lib.FormNotBuilt):
+                with _lib.forced_forms(**{other: 1, name: v}):
+                    pass
+            assert _lib.lib.skml_debug_form(_lib.FORMS[other], 0) == 0  # restored on the way out
 
 
 def test_abi_host_only_calls():

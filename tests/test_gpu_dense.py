@@ -86,18 +86,20 @@ def test_quantize_edge_data(gpu, kind, n):
     _check(gq, oq, x)
 
 
+@pytest.mark.parametrize("forms", [(0, 2), pytest.param((1, 3, 4, 5), marks=pytest.mark.ab)], ids=["shipped", "ab"])
 @pytest.mark.parametrize("kind", ["normal", "signed_zero"])
-def test_leaf_forms_match_oracle(gpu, kind):
-    """The sketch leaf's forms give the oracle's sketch: one wave per 64-chunk tile, the split leaf
-    (four waves per tile), and the hybrid that ends a large bucket with split tiles (the default
-    from 3,072 tiles; the last 12.5 / 25 / 50 % split), on 4,096 full tiles plus a partial one.
-    signed_zero sends rounds through the exact (count-based) merge path in both forms."""
+def test_leaf_forms_match_oracle(gpu, kind, forms):
+    """The sketch leaf's forms give the oracle's sketch, on 4,096 full tiles plus a partial one:
+    the split leaf (four waves per 64-chunk tile; the default at every size, 0 and 2), and in the
+    A/B build one wave per tile (1) and the hybrids that end a large bucket with split tiles (the
+    last 12.5 / 25 / 50 % split).  signed_zero sends rounds through the exact (count-based) merge
+    path in every form."""
     from sketchml_amd import _lib
     n = 4096 * 64 * 256 + 12345
     x = _data(n, 91, kind)
     oq = O.quantize(x.astype(np.float64), 256, 91)
     xt = torch.from_numpy(x).cuda()
-    for form in (0, 1, 2, 3, 4, 5):
+    for form in forms:
         with _lib.forced_forms(leaf_split=form):
             gq = gpu.QuantileQuantizer(256, seed=91)
             gq.quantize(xt)
@@ -400,7 +402,7 @@ def test_decode_sum(gpu):
                                       (8, [512] * 8, 2**18 + 3), (4, [1024] * 4, 50001),
                                       (16, [512] * 16, 40000 + 5), (5, [16] * 5, 2**18 + 7), (4, [4] * 4, 99999),
                                       (3, [2] * 3, 4097), (6, [256, 16, 4, 2, 256, 16], 50001), (1, [256], 15)])
-@pytest.mark.parametrize("kernel", ["occ", "occ_nopf", "plain"])
+@pytest.mark.parametrize("kernel", ["occ", pytest.param("occ_nopf", marks=pytest.mark.ab), "plain"])
 def test_decode_sum_forms(gpu, P, bins, n, kernel):
     """k_decode_sum_occ (8 elements per lane, P <= 8 tables of the largest bin count in LDS; with
     and without the next step's code prefetch) and the per-payload kernel (P > 8, mixed widths,

@@ -76,9 +76,13 @@ def test_sparse_edge_values(gpu, kind):
     _check_sparse(gpu, keys, vals, seed=5, hash_seed=1)
 
 
-@pytest.fixture(params=["one_pass", "one_pass_plain", "persistent_query", "bounds_pass", "dec_lookback", "dec_lookback_scan", "rounds"])
+@pytest.fixture(params=["one_pass", pytest.param("one_pass_plain", marks=pytest.mark.ab),
+                        pytest.param("persistent_query", marks=pytest.mark.ab),
+                        pytest.param("bounds_pass", marks=pytest.mark.ab),
+                        pytest.param("dec_lookback", marks=pytest.mark.ab),
+                        pytest.param("dec_lookback_scan", marks=pytest.mark.ab), "rounds"])
 def merge_form(request):
-    """restore three ways.  one_pass (the default): tiles of one group through the compile-time-hash
+    """restore in every form (the A/B-build-only ones marked `ab`).  one_pass (the default): tiles of one group through the compile-time-hash
     query (k_dec_keys MODE 1) and the edge tiles through the generic one, Sort.merge as the
     one-pass key-range merge with the next range's loads in flight.  one_pass_plain: the same merge
     without that prefetch.  persistent_query: the compile-time-hash query in persistent workgroups

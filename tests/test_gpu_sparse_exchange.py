@@ -127,7 +127,8 @@ def test_decode_sum_payload_meta_past_the_first_read(gpu):
     assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
 
 
-@pytest.mark.parametrize("bins,forms", [(256, {}), (1000, {}), (256, {"rs_rounds": 1}), (256, {"rs_rounds": 2})])
+@pytest.mark.parametrize("bins,forms", [(256, {}), (1000, {}), (256, {"rs_rounds": 1}),
+                                        pytest.param(256, {"rs_rounds": 2}, marks=pytest.mark.ab)])
 def test_restore_values_refuse_bins_outside_quant_values(gpu, bins, forms):
     """quantValues[bin] with a bin past the values (SparseVectorCompressor.java:118-126 throws
     ArrayIndexOutOfBoundsException): every MinMax cell of an imported blob overwritten with binNum
@@ -172,7 +173,10 @@ KERNELS = {"vtile_rmw": {}, "vtile_rmw_bounds_pass": {"run_bounds": 1},
            "wave_serial": {"agg_tiles": 1, "dec_rows_serial": 1, "agg_one_lane": 1}}
 
 
-@pytest.fixture(params=sorted(KERNELS))
+AB_KERNELS = {"vtile_rmw_bounds_pass", "vtile_pf", "vtile", "vtile2", "vtile4"}  # only in the A/B build
+
+
+@pytest.fixture(params=[pytest.param(k, marks=pytest.mark.ab) if k in AB_KERNELS else k for k in sorted(KERNELS)])
 def agg_kernel(request):
     from sketchml_amd import _lib
     with _lib.forced_forms(**KERNELS[request.param]):
@@ -382,7 +386,8 @@ def test_decode_sum_eight_distinct_c3_payloads_full_size(gpu):
     want, forms = O.gradient_sum(restored, dim, 1.0 / P)
     del restored
     assert forms == ["sparse"] * P
-    for form in (0, 4, 5, 3, 2, 1):                      # sum tile in LDS, staged tiles (prefetching, 1, 2, 4 per round), 4,096-key tiles
+    # sum tile in LDS, 4,096-key tiles; the A/B build: staged tiles (prefetching, 1, 2, 4 per round)
+    for form in (0, 1) + ((4, 5, 3, 2) if _lib.AB_BUILD else ()):
         with _lib.forced_forms(agg_tiles=form):
             got = gpu.decode_sum(allb, P, stride, dim, 1.0 / P)
             torch.cuda.synchronize()

@@ -9,6 +9,7 @@
 # STEP:
 #   tests:FILE[+FILE...][@K]  pytest -m gpu on tests/FILE.py ... (-k K if given) -> TAG/tests.log
 #   suite                     the whole GPU suite and smoke() (tools/final_evidence.sh TAG tests-only)
+#   abtests                   the tests of the A/B-only kernel forms against sketchml_amd/lib_ab (make -C sketchml_amd/csrc ab)
 #   bench                     python bench.py --gpus 1 --steps 20 --warmup 5 -> TAG/bench.json
 #   ab:NAME:REPS:KIND:VARIANT[+VARIANT...]   tools/ab.sh NAME REPS KIND VARIANT ... (see ab.sh)
 #   pmc:agg | pmc:restore | pmc:sparse       the counter passes (tools/pmc_*.sh TAG)
@@ -50,6 +51,10 @@ for STEP in "$@"; do
       tail -2 "$OUT/tests.log" ;;
     suite)
       bash tools/final_evidence.sh "$TAG" tests-only ;;
+    abtests)
+      SKML_LIB=sketchml_amd/lib_ab/libskml.so timeout -k 10 600 python -u -m pytest tests -x -q --timeout 300 \
+        --timeout-method thread -m "gpu and ab" > "$OUT/ab_tests.log" 2>&1
+      tail -2 "$OUT/ab_tests.log" ;;
     bench)
       timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err"
       tail -c 300 "$OUT/bench.json" ;;
