@@ -155,14 +155,28 @@ def pmc_traffic(kernel, n, dtype="f32", quant="quantile"):
     return best
 
 
-# VALU issue ceiling of the sketch's instruction classes (wave-instructions / s, whole chip).
-# tools/ubench/issue.hip measured on gfx950, 8 waves per SIMD of independent chains: v_min/v_max/
-# v_med3/v_min3 (f32 and u32), every DPP move or DPP-fused op, v_cndmask_e64 and v_perm take
-# ~4.4 SIMD cycles per wave-instruction (the 4-cycle "quarter-wave" rate: one wave-instruction per
-# clock per CU), while v_add/v_sub/v_and/v_xor/v_lshr/v_mul_f32/v_fma_f32 take ~2.6 (the SIMD-32
-# rate).  A sorting network is almost all of the former, so the denominator is 1 wave-instruction
-# per clock per CU at the 2.4 GHz peak engine clock on 256 CUs.
-VALU_PEAK_GINST = 2.4e9 * 256 / 1e9
+# VALU issue ceiling of the leaf (wave-instructions / s, whole chip).  tools/ubench/issue.hip on
+# gfx950 (profiles/r06_ubench_issue.txt, 8 waves per SIMD of independent chains): v_min/v_max/
+# v_med3/v_min3 (f32 and u32), every DPP move or DPP-fused op, v_cmp/v_cndmask_e64, v_bfi/v_perm
+# take ~4.4 SIMD cycles per wave-instruction (the 4-cycle rate: one wave-instruction per clock per
+# CU), while v_add/v_sub/v_and/v_xor/v_lshr/v_mul_f32/v_fma_f32 take ~2.6 (the SIMD-32 rate, 2
+# cycles).  The leaf's code is 7.8 % 2-cycle instructions (tools/valu_mix.py ->
+# profiles/r06_leaf_valu_mix.json), so its ceiling is the 4-cycle rate x 4 / (4 - 2 x 0.078) at the
+# 2.4 GHz peak engine clock on 256 CUs.
+VALU_CLASS_PEAK_GINST = 2.4e9 * 256 / 1e9
+
+
+def _valu_mix_factor():
+    try:
+        with open(os.path.join(ROOT, "profiles", "r06_leaf_valu_mix.json")) as f:
+            d = json.load(f)
+        return float(d["ceiling_factor"]), "profiles/r06_leaf_valu_mix.json"
+    except Exception:
+        return 1.0, None
+
+
+VALU_MIX_FACTOR, VALU_MIX_SOURCE = _valu_mix_factor()
+VALU_PEAK_GINST = VALU_CLASS_PEAK_GINST * VALU_MIX_FACTOR
 
 
 def sq_valu(kernel, n):
@@ -771,10 +785,11 @@ def main():
         rate = valu[0] / (live["avg_us"] * 1e-6) / 1e9
         roofline["valu"] = {"insts_per_launch": valu[0], "source": valu[1], "issue_ginst_s": round(rate, 1),
                             "peak_ginst_s": round(VALU_PEAK_GINST, 1), "frac": round(rate / VALU_PEAK_GINST, 4),
-                            "peak_note": "one wave-instruction per clock per CU at 2.4 GHz: the rate of the "
-                                         "network's min / max / med3 / DPP ops; the adds, ands and shifts "
-                                         "around them issue at the SIMD-32 rate, so the mix can reach 1.0 "
-                                         "(and the engine clock may run above 2.4 GHz)"}
+                            "peak_source": ["profiles/r06_ubench_issue.txt", VALU_MIX_SOURCE],
+                            "peak_note": f"one wave-instruction per clock per CU at 2.4 GHz (the measured rate "
+                                         f"of the network's min / max / med3 / DPP ops: 4 SIMD cycles each) x "
+                                         f"{VALU_MIX_FACTOR} for the leaf's share of 2-cycle adds, ands and "
+                                         f"shifts (SIMD-32 rate)"}
     encode_device_us = sum(v["avg_us"] * v["launches"] for k, v in allstats.items()
                            if k in alg_bytes) / steps_b
     extras = {"encode_device_us": round(encode_device_us, 2),
@@ -860,7 +875,8 @@ def main():
         line = {
             "metric": "device-resident grad encode GB/s (fp32 in) + decode L2 err, 1/2/4/8 GPU",
             "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "warmup": args.warmup, "warmup_steps_run": nwarm, "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
             "warmup_note": f"{nwarm} untimed encodes: --warmup {args.warmup}, extended to {args.warmup_ms:g} ms of "
                            "sustained load so the engine clock has settled (profiles/r05b_warmup_ramp.txt)",
             "scaling": "weak", "vs_baseline": None, "dtype": args.dtype, "data": "synthetic N(0,1), torch generator",

@@ -48,6 +48,17 @@ class Params(C.Structure):
                 ("hash_seed", C.c_int64), ("quant_type", C.c_int32), ("parallelism", C.c_int32)]
 
 
+class SparseBlobHeader(C.Structure):
+    """The 256-byte header of an exported sparse payload (SpBlobHeader, csrc/skml_sparse.h)."""
+    _fields_ = [("magic", C.c_uint32), ("version", C.c_int32), ("total_bytes", C.c_int64), ("nnz", C.c_int64),
+                ("ncells", C.c_int64), ("n_flag_words", C.c_int64), ("n_delta_words", C.c_int64),
+                ("flag_bits", C.c_int64), ("delta_bits", C.c_int64), ("nvalues", C.c_int32),
+                ("quant_bytes", C.c_int32), ("off_groups", C.c_int64), ("off_quant", C.c_int64),
+                ("off_values", C.c_int64), ("off_tables", C.c_int64), ("off_flags", C.c_int64),
+                ("off_deltas", C.c_int64), ("params", Params), ("table_width", C.c_int32), ("pad0", C.c_int32),
+                ("reserved", C.c_int64 * 7)]
+
+
 class DenseHeader(C.Structure):
     _fields_ = [("magic", C.c_uint32), ("status", C.c_int32), ("n", C.c_int64),
                 ("bin_num", C.c_int32), ("zero_idx", C.c_int32), ("code_bits", C.c_int32),

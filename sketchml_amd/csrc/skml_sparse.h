@@ -136,10 +136,20 @@ inline int64_t mm_chunk(int64_t n) {
     }
     return best;
 }
-// per-bucket minimum -> int32 MinMaxSketch tables (empty cells get the fill value); nbuckets may
+// The exact narrow image of MinMax tables whose cells hold bins in [0, bin_num) or the fill: a bin
+// in 8 bits when bin_num <= 255, in 16 bits when bin_num <= 65,535 (0: no narrow image), the fill
+// as the top code 2^W - 1.  The encoder writes it beside the int32 cells, the restore gathers from
+// it, and the exchange blob carries it instead of the int32 cells.
+__host__ __device__ inline int tnar_width_for(int32_t bin_num) {
+    return bin_num <= 255 ? 8 : bin_num <= 65535 ? 16 : 0;
+}
+// per-bucket minimum -> int32 MinMaxSketch tables (empty cells get the fill value) and, when tnar is
+// not nullptr, their exact narrow image (tnar_width_for(gp->bin_num) bits a cell); nbuckets may
 // exceed the table's (gp->ncells) buckets: the extra workgroups exit
 hipError_t launch_mm_bucket(hipStream_t st, const void* pairs, const uint64_t* bucket_base, int nbuckets,
-                            const SpGroups* gp, int32_t* table);
+                            const SpGroups* gp, int32_t* table, void* tnar);
+// int32 cells from an exact narrow image of tw (8 or 16) bits: the top code becomes `fill`
+hipError_t launch_widen_cells(hipStream_t st, const void* tn, int tw, int64_t ncells, int32_t fill, int32_t* t32);
 // DeltaAdaptiveEncoder bit streams: tile sums of (flag bits, delta bits), then the writer.
 hipError_t launch_delta_lens(hipStream_t st, const uint8_t* need, int64_t n, const SpGroups* gp,
                              uint64_t* tile_sums);
@@ -179,7 +189,8 @@ hipError_t launch_group_prefix(hipStream_t st, const uint32_t* delta, int64_t n,
                                const uint64_t* tile_base, uint64_t* gpre);
 // keys and MinMax bins; gh: the host copy of *gp (the grid follows the group sizes).  width 8 / 16:
 // tnar is launch_narrow_table's image of `table` (int32 cells outside [0, 2^width - 1) read back
-// from `table`); width 32: `table` alone (nullptr with gp->rows == 0: keys only).  gbins may be
+// from `table`), or with table == nullptr an exact image (tnar_width_for: the top code is the
+// fill); width 32: `table` alone (nullptr with gp->rows == 0: keys only).  gbins may be
 // null; gvals (optional) receives quantValues[bin] from qv[nq], a bin outside it sets *err
 // The runs' bounds written by the key query itself.  info == nullptr: Gradient.sum's tiles
 // (k_agg_bounds' job): bounds[g * (ntiles + 1) + t] = the first element of run g with key >= t <<
@@ -249,7 +260,9 @@ struct SpBlobHeader {
     int32_t quant_bytes;                  // dense header + splits
     int64_t off_groups, off_quant, off_values, off_tables, off_flags, off_deltas;
     skml_params params;
-    int64_t reserved[8];
+    int32_t table_width;                  // version 2: bits a MinMax cell (8 / 16: the exact narrow
+    int32_t pad0;                         // image, tnar_width_for; 32: int32 cells); version 1: 32
+    int64_t reserved[7];
 };
 static_assert(sizeof(SpBlobHeader) <= 256, "blob header fits its 256-byte section");
 // One round of pairwise stable merges of sorted runs (Sort.merge order: lower run first on ties).

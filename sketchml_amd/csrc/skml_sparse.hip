@@ -1670,10 +1670,14 @@ hipError_t launch_mm_scatter(hipStream_t st, const int32_t* gkeys, const uint16_
 // Narrow pairs (SpGroups.mm_narrow) take 32-bit LDS minima over (distance, sign) for the whole
 // bucket; key-carrying pairs take 64-bit minima, one 8192-cell sub-range after the other (each
 // sub-range re-reads the bucket's pairs; this path only runs for groups on both sides of zeroIdx).
+// tnar (may be nullptr): the exact narrow image of the table as well -- a cell's bin in 8 bits when
+// the group table's bin_num <= 255, else in 16 bits when <= 65,535, the fill as the top code
+// (2^W - 1); the payload's restore gathers from it and the exchange blob carries it
+// (tnar_width_for).
 __global__ __launch_bounds__(kMmThreads) void k_mm_bucket(const void* __restrict__ pairs_v,
                                                           const uint64_t* __restrict__ bucket_base,
                                                           const SpGroups* __restrict__ gp,
-                                                          int32_t* __restrict__ table) {
+                                                          int32_t* __restrict__ table, void* __restrict__ tnar) {
     constexpr int kWords = kMmBucketCells / 2 > kMmSubCells ? kMmBucketCells / 2 : kMmSubCells;
     __shared__ unsigned long long cm64[kWords];  // u32 minima of the bucket, or u64 of a sub-range
     uint32_t* cm = reinterpret_cast<uint32_t*>(cm64);
@@ -1683,6 +1687,12 @@ __global__ __launch_bounds__(kMmThreads) void k_mm_bucket(const void* __restrict
     const int32_t zero = gp->zero, fill = gp->fill;
     const uint64_t p0 = bucket_base[b], p1 = bucket_base[b + 1];
     const int64_t cell0 = (int64_t)b << kMmBucketBits;
+    const int tw = tnar ? tnar_width_for(gp->bin_num) : 0;
+    auto put = [&](int64_t cell, int32_t out) {
+        table[cell] = out;
+        if (tw == 8) static_cast<uint8_t*>(tnar)[cell] = out == fill ? (uint8_t)0xFF : (uint8_t)out;
+        else if (tw == 16) static_cast<uint16_t*>(tnar)[cell] = out == fill ? (uint16_t)0xFFFF : (uint16_t)out;
+    };
     if (gp->mm_narrow) {
         const uint32_t* pairs = static_cast<const uint32_t*>(pairs_v);
         for (int j = threadIdx.x; j < kMmBucketCells; j += kMmThreads) cm[j] = ~0u;
@@ -1705,7 +1715,7 @@ __global__ __launch_bounds__(kMmThreads) void k_mm_bucket(const void* __restrict
                 const int32_t dist = (int32_t)(v >> 1);
                 out = (v & 1u) ? zero - dist : zero + dist;
             }
-            table[cell0 + j] = out;
+            put(cell0 + j, out);
         }
         return;
     }
@@ -1735,16 +1745,33 @@ __global__ __launch_bounds__(kMmThreads) void k_mm_bucket(const void* __restrict
                 const int32_t dist = (int32_t)(v >> 48);
                 out = ((v >> 16) & 1u) ? zero - dist : zero + dist;
             }
-            table[s0 + j] = out;
+            put(s0 + j, out);
         }
     }
 }
 
 hipError_t launch_mm_bucket(hipStream_t st, const void* pairs, const uint64_t* bucket_base, int nbuckets,
-                            const SpGroups* gp, int32_t* table) {
+                            const SpGroups* gp, int32_t* table, void* tnar) {
     if (nbuckets <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_mm_bucket, dim3((unsigned)nbuckets), dim3(kMmThreads), 0, st, pairs, bucket_base, gp,
-                       table);
+                       table, tnar);
+    return hipGetLastError();
+}
+
+// int32 cells from an exact narrow image (tnar_width_for): the top code back to the fill
+__global__ __launch_bounds__(256) void k_widen_cells(const void* __restrict__ tn, int tw, int64_t ncells, int32_t fill,
+                                                     int32_t* __restrict__ t32) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < ncells; i += (int64_t)gridDim.x * 256) {
+        const uint32_t v = tw == 8 ? static_cast<const uint8_t*>(tn)[i] : static_cast<const uint16_t*>(tn)[i];
+        t32[i] = v == (tw == 8 ? 0xFFu : 0xFFFFu) ? fill : (int32_t)v;
+    }
+}
+
+hipError_t launch_widen_cells(hipStream_t st, const void* tn, int tw, int64_t ncells, int32_t fill, int32_t* t32) {
+    if (ncells <= 0) return hipSuccess;
+    if (tw != 8 && tw != 16) return hipErrorInvalidValue;
+    const unsigned grid = (unsigned)std::min<int64_t>(sp_tiles(ncells, 256 * 4), 4096);
+    hipLaunchKernelGGL(k_widen_cells, dim3(grid), dim3(256), 0, st, tn, tw, ncells, fill, t32);
     return hipGetLastError();
 }
 
@@ -2741,7 +2768,7 @@ __device__ __forceinline__ void dec_keys_tile(int64_t n, const SpGroups* __restr
         const DivU32 dvc = divu32_make((uint32_t)cols);
         const auto dv = [&](uint32_t h) { return java_mod((int32_t)h, cols, dvc); };
         const TN* tnb = tnar + tb;
-        const int32_t* t32b = table + tb;
+        const int32_t* t32b = table ? table + tb : nullptr;  // nullptr: tnar is exact (top code = fill)
         uint32_t rel[2][4];
         int32_t tv[2][4];
 #pragma unroll
@@ -2772,8 +2799,8 @@ __device__ __forceinline__ void dec_keys_tile(int64_t n, const SpGroups* __restr
 #pragma unroll
             for (int r = 0; r < 2; r++)
 #pragma unroll
-                for (int j = 0; j < 4; j++)  // the sentinel: the cell's int32 value
-                    if ((uint32_t)tv[r][j] == kTop) tv[r][j] = t32b[rel[r][j]];
+                for (int j = 0; j < 4; j++)  // the top code: the cell's int32 value, or the fill
+                    if ((uint32_t)tv[r][j] == kTop) tv[r][j] = t32b ? t32b[rel[r][j]] : gp->fill;
         }
 #ifdef SKML_ABLATE_DEC_HASH  // (the wrong cells may be empty ones: keep the bins inside quantValues)
 #pragma unroll
@@ -2796,8 +2823,8 @@ __device__ __forceinline__ void dec_keys_tile(int64_t n, const SpGroups* __restr
             }
             if constexpr (sizeof(TN) < 4) {
 #pragma unroll
-                for (int j = 0; j < 4; j++)  // the sentinel: the cell's int32 value
-                    if (idx[j] >= 0 && (uint32_t)tv[j] == kTop) tv[j] = table[idx[j]];
+                for (int j = 0; j < 4; j++)  // the top code: the cell's int32 value, or the fill
+                    if (idx[j] >= 0 && (uint32_t)tv[j] == kTop) tv[j] = table ? table[idx[j]] : gp->fill;
             }
 #pragma unroll
             for (int j = 0; j < 4; j++) take(j, tv[j]);
@@ -2994,7 +3021,8 @@ hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, con
     // MODE 1 over every tile, then MODE 0 over the edge tiles; MODE 0 alone for other shapes, for
     // tables past 2^31 cells (MODE 1's cells are 32-bit offsets and its modulus takes cols <=
     // 2^30), and under SKML_FORM_DEC_ROWS_SERIAL (tests)
-    const bool batched = gh.rows == 2 && table != nullptr && form(SKML_FORM_DEC_ROWS_SERIAL) != 1 &&
+    const bool batched = gh.rows == 2 && (table != nullptr || (tnar != nullptr && width < 32)) &&
+                         form(SKML_FORM_DEC_ROWS_SERIAL) != 1 &&
                          gh.ncells <= ((int64_t)1 << 31);
     DecEdgeTiles all{}, edges{};
     all.n = 0;

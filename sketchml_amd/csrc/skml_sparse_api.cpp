@@ -239,6 +239,8 @@ struct skml_sparse {
     SpGroups* g_dev = nullptr;  // device copy
     int32_t* tables = nullptr;  // all groups' MinMaxSketch tables, rows x cols each
     int64_t ncells = 0;
+    void* tnar = nullptr;       // their exact narrow image (tnar_width_for), or nullptr; in the block
+    int tnar_width = 0;         // 8 or 16 bits a cell
     uint64_t* flag_words = nullptr;  // concatenated DeltaAdaptive flag streams
     uint64_t* delta_words = nullptr;
     int64_t flag_bits = 0, delta_bits = 0;
@@ -451,7 +453,11 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const void* vals, bool f64, int6
     s->qbytes = skml_dense_payload_bytes(nnz, p->bin_num);
     const size_t o_g = align_up(s->qbytes, 256);
     const size_t o_tab = o_g + align_up(sizeof(SpGroups), 256);
-    const size_t o_fw = o_tab + align_up(sizeof(int32_t) * (size_t)std::max<int64_t>(cells_max, 1), 256);
+    // the tables' exact narrow image: 16 bits a cell reserved (the effective bin count, which picks
+    // 8 or 16, is known on the device only)
+    const bool want_tn = tnar_width_for(p->bin_num) != 0;
+    const size_t o_tn = o_tab + align_up(sizeof(int32_t) * (size_t)std::max<int64_t>(cells_max, 1), 256);
+    const size_t o_fw = o_tn + (want_tn ? align_up(sizeof(uint16_t) * (size_t)std::max<int64_t>(cells_max, 1), 256) : 0);
     const size_t o_dw = o_fw + align_up(sizeof(uint64_t) * (size_t)fwn, 256);
     const size_t total = o_dw + sizeof(uint64_t) * (size_t)dwn;
     char* blk = static_cast<char*>(block_get(s->device, total, &s->block_cap));
@@ -460,6 +466,7 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const void* vals, bool f64, int6
     s->qpayload = blk;
     s->g_dev = reinterpret_cast<SpGroups*>(blk + o_g);
     s->tables = reinterpret_cast<int32_t*>(blk + o_tab);
+    s->tnar = want_tn ? blk + o_tn : nullptr;
     s->flag_words = reinterpret_cast<uint64_t*>(blk + o_fw);
     s->delta_words = reinterpret_cast<uint64_t*>(blk + o_dw);
     // ---- 1. the values' quantizer (Quantizer.newQuantizer(quantType), SparseVectorCompressor.java:60-62) ----
@@ -541,7 +548,7 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const void* vals, bool f64, int6
     if (side) SP_TRY(hipEventRecord(ev_join, side));
     SP_TRY(launch_scan_cols(st, bucket, nbuckets, 1));
     SP_TRY(launch_mm_scatter(st, gk, gb, nnz, s->g_dev, bucket, cursor, nbuckets, pairs, cellbuf, tile_off));
-    SP_TRY(launch_mm_bucket(st, pairs, bucket, nbuckets, s->g_dev, s->tables));
+    SP_TRY(launch_mm_bucket(st, pairs, bucket, nbuckets, s->g_dev, s->tables, s->tnar));
     if (side) SP_TRY(hipStreamWaitEvent(st, ev_join, 0));
     // ---- 5. the one read-back: quantizer header and splits, group table ----
     const size_t qh = kHeaderBytes + sizeof(double) * (size_t)(p->bin_num - 1);
@@ -576,6 +583,8 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const void* vals, bool f64, int6
         }
     }
     s->ncells = s->g.ncells;
+    s->tnar_width = s->tnar ? tnar_width_for(s->g.bin_num) : 0;
+    if (!s->tnar_width) s->tnar = nullptr;
     s->flag_bits = s->g.fb[G];
     s->delta_bits = s->g.db[G];
     s->n_flag_words = (s->flag_bits + 63) / 64 + 1;
@@ -625,7 +634,11 @@ int decode_groups(skml_ctx* c, const skml_sparse* s, int32_t* gk, int32_t* gb, b
     const int32_t* tab = query ? s->tables : nullptr;
     int width = 32;
     void* tnar = nullptr;
-    if (tab && s->ncells > 0 && (reinterpret_cast<uintptr_t>(tab) & 15) == 0) {
+    if (query && s->tnar && s->ncells > 0) {  // the payload's exact image (encoder or blob): gathered as is
+        tab = nullptr;
+        width = s->tnar_width;
+        tnar = s->tnar;
+    } else if (tab && s->ncells > 0 && (reinterpret_cast<uintptr_t>(tab) & 15) == 0) {
         width = G.bin_num <= 256 ? 8 : 16;  // any width gives the same bins (the sentinel reads back)
         tnar = ctx_scratch(c, kSlotNarrowTab, (size_t)s->ncells * (size_t)(width / 8));
         if (!tnar) return sfail(SKML_E_OOM, "decode scratch (table image)");
@@ -642,7 +655,7 @@ int decode_groups(skml_ctx* c, const skml_sparse* s, int32_t* gk, int32_t* gb, b
 #endif
     if (split == 1) {
         SP_HIP(launch_dec_lens(st, s->flag_words, s->n_flag_words, end_pos, n, s->g_dev, dlen, ts,
-                               NarrowJob{tab, s->ncells, tnar, width}));
+                               NarrowJob{tab, s->ncells, tab ? tnar : nullptr, width}));
         if (int e = scan_tiles(c, ts, tiles, 1, nullptr)) return e;
         SP_HIP(launch_dec_deltas(st, s->delta_words, s->n_delta_words, dlen, n, s->g_dev, ts, delta, ts2));
     } else {
@@ -650,7 +663,7 @@ int decode_groups(skml_ctx* c, const skml_sparse* s, int32_t* gk, int32_t* gb, b
         uint64_t* status = scratch<uint64_t>(c, kSlotLookback, 2 * (size_t)tiles + 8);
         if (!status) return sfail(SKML_E_OOM, "decode scratch (look-back)");
         SP_HIP(launch_dec_lens_deltas(st, s->flag_words, s->n_flag_words, end_pos, n, s->g_dev, s->delta_words,
-                                      s->n_delta_words, delta, ts2, status, NarrowJob{tab, s->ncells, tnar, width},
+                                      s->n_delta_words, delta, ts2, status, NarrowJob{tab, s->ncells, tab ? tnar : nullptr, width},
                                       split == 0));
 #endif
     }
@@ -1511,6 +1524,7 @@ int skml_sparse_deserialize(skml_ctx* c, const uint8_t* buf, size_t len, const d
     G.db[G.G] = dbits;
     s->nnz = n;
     s->ncells = cells;
+    G.ncells = cells;  // the group table's total as the encoder's plan leaves it (exported blobs check it)
     s->flag_bits = fbits;
     s->delta_bits = dbits;
     s->n_flag_words = (fbits + 63) / 64 + 1;
@@ -1696,15 +1710,17 @@ namespace {
 struct BlobLayout {
     size_t off_groups, off_quant, off_values, off_tables, off_flags, off_deltas, total;
     int32_t quant_bytes;
+    int table_width;  // the MinMax cells: the payload's exact narrow image (8 / 16 bits) when it has one
 };
 BlobLayout blob_layout(const skml_sparse* s) {
     BlobLayout L;
     L.quant_bytes = (int32_t)(kHeaderBytes + sizeof(double) * (size_t)std::max(s->hdr.bin_num - 1, 0));
+    L.table_width = s->tnar ? s->tnar_width : 32;
     L.off_groups = 256;
     L.off_quant = L.off_groups + align_up(sizeof(SpGroups), 256);
     L.off_values = L.off_quant + align_up((size_t)L.quant_bytes, 256);
     L.off_tables = L.off_values + align_up(sizeof(double) * std::max<size_t>(s->qvalues.size(), 1), 256);
-    L.off_flags = L.off_tables + align_up(sizeof(int32_t) * (size_t)std::max<int64_t>(s->ncells, 1), 256);
+    L.off_flags = L.off_tables + align_up((size_t)L.table_width / 8 * (size_t)std::max<int64_t>(s->ncells, 1), 256);
     L.off_deltas = L.off_flags + align_up(sizeof(uint64_t) * (size_t)s->n_flag_words, 256);
     L.total = L.off_deltas + align_up(sizeof(uint64_t) * (size_t)s->n_delta_words, 256);
     return L;
@@ -1716,6 +1732,7 @@ int check_blob_groups(const SpBlobHeader& h, const SpGroups& G) {
     auto bad = [](const char* what) { return sfail(SKML_E_ARG, "sparse blob: inconsistent %s", what); };
     if (G.G < 1 || G.G > kMaxGroups || G.rows < 0 || G.rows > kMaxRows) return bad("group / row count");
     if (G.bin_num < 1 || G.bin_num > h.nvalues || G.zero < 0 || G.zero >= G.bin_num) return bad("bins");
+    if (h.version >= 2 && h.table_width != 32 && h.table_width != tnar_width_for(G.bin_num)) return bad("cell width");
     if (G.gstart[0] != 0 || G.gstart[G.G] != h.nnz || G.fb[0] != 0 || G.db[0] != 0) return bad("stream starts");
     if (G.fb[G.G] != h.flag_bits || G.db[G.G] != h.delta_bits || G.ncells != h.ncells) return bad("stream totals");
     if (h.n_flag_words < (h.flag_bits + 63) / 64 + 1 || h.n_delta_words < (h.delta_bits + 63) / 64 + 1)
@@ -1740,13 +1757,16 @@ int check_blob_groups(const SpBlobHeader& h, const SpGroups& G) {
 }
 
 // A blob's header, checked against the `len` bytes it may span.
+int blob_table_width(const SpBlobHeader* h) { return h->version >= 2 ? h->table_width : 32; }
 int blob_check_header(const SpBlobHeader* h, size_t len) {
-    if (h->magic != kSpBlobMagic || h->version != 1) return sfail(SKML_E_STATE, "not a sparse blob");
+    if (h->magic != kSpBlobMagic || h->version < 1 || h->version > 2) return sfail(SKML_E_STATE, "not a sparse blob");
+    const int tw = blob_table_width(h);
+    if (tw != 8 && tw != 16 && tw != 32) return sfail(SKML_E_ARG, "sparse blob: cell width %d", tw);
     if (h->total_bytes < 256 || (size_t)h->total_bytes > len || h->nnz < 0 || h->nnz > INT32_MAX || h->ncells < 0 ||
         h->nvalues < 1 || h->nvalues > SKML_MAX_BINS || h->quant_bytes < kHeaderBytes ||
         h->off_groups != 256 || h->off_quant < h->off_groups + (int64_t)sizeof(SpGroups) ||
         h->off_values < h->off_quant + h->quant_bytes || h->off_tables < h->off_values + 8 * (int64_t)h->nvalues ||
-        h->off_flags < h->off_tables + 4 * h->ncells || h->off_deltas < h->off_flags + 8 * h->n_flag_words ||
+        h->off_flags < h->off_tables + tw / 8 * h->ncells || h->off_deltas < h->off_flags + 8 * h->n_flag_words ||
         h->total_bytes < h->off_deltas + 8 * h->n_delta_words || (h->off_tables | h->off_flags | h->off_deltas) & 255)
         return sfail(SKML_E_ARG, "sparse blob: inconsistent section offsets");
     return SKML_OK;
@@ -1772,7 +1792,11 @@ int blob_view(skml_ctx* c, const uint8_t* dev, const SpBlobHeader& h, const uint
     view->n_flag_words = h.n_flag_words;
     view->n_delta_words = h.n_delta_words;
     view->g_dev = reinterpret_cast<SpGroups*>(const_cast<uint8_t*>(dev) + h.off_groups);
-    view->tables = reinterpret_cast<int32_t*>(const_cast<uint8_t*>(dev) + h.off_tables);
+    uint8_t* tab = const_cast<uint8_t*>(dev) + h.off_tables;
+    const int tw = blob_table_width(&h);
+    view->tables = tw == 32 ? reinterpret_cast<int32_t*>(tab) : nullptr;
+    view->tnar = tw == 32 ? nullptr : tab;
+    view->tnar_width = tw == 32 ? 0 : tw;
     view->flag_words = reinterpret_cast<uint64_t*>(const_cast<uint8_t*>(dev) + h.off_flags);
     view->delta_words = reinterpret_cast<uint64_t*>(const_cast<uint8_t*>(dev) + h.off_deltas);
     return SKML_OK;
@@ -1829,6 +1853,7 @@ struct ViewGuard {
     ~ViewGuard() {
         v->g_dev = nullptr;
         v->tables = nullptr;
+        v->tnar = nullptr;
         v->flag_words = v->delta_words = nullptr;
         v->qpayload = nullptr;
     }
@@ -1857,7 +1882,8 @@ int skml_sparse_export(skml_ctx* c, const skml_sparse* s, void* dst, size_t cap)
     std::memset(pin, 0, host_bytes);
     SpBlobHeader h{};
     h.magic = kSpBlobMagic;
-    h.version = 1;
+    h.version = 2;
+    h.table_width = L.table_width;
     h.total_bytes = (int64_t)L.total;
     h.nnz = s->nnz;
     h.ncells = s->ncells;
@@ -1884,8 +1910,9 @@ int skml_sparse_export(skml_ctx* c, const skml_sparse* s, void* dst, size_t cap)
     if (!s->qvalues.empty()) std::memcpy(pin + L.off_values, s->qvalues.data(), sizeof(double) * s->qvalues.size());
     uint8_t* d = static_cast<uint8_t*>(dst);
     SP_HIP(hipMemcpyAsync(d, pin, host_bytes, hipMemcpyHostToDevice, st));
-    if (s->ncells > 0)
-        SP_HIP(hipMemcpyAsync(d + L.off_tables, s->tables, sizeof(int32_t) * (size_t)s->ncells, hipMemcpyDeviceToDevice, st));
+    if (s->ncells > 0)  // the exact narrow image when the payload has one, else the int32 cells
+        SP_HIP(hipMemcpyAsync(d + L.off_tables, s->tnar ? s->tnar : static_cast<const void*>(s->tables),
+                              (size_t)L.table_width / 8 * (size_t)s->ncells, hipMemcpyDeviceToDevice, st));
     if (s->n_flag_words > 0)
         SP_HIP(hipMemcpyAsync(d + L.off_flags, s->flag_words, sizeof(uint64_t) * (size_t)s->n_flag_words,
                               hipMemcpyDeviceToDevice, st));
@@ -1918,8 +1945,12 @@ int skml_sparse_import(skml_ctx* c, const void* blob, size_t len, skml_sparse** 
     s->delta_bits = view.delta_bits;
     s->n_flag_words = view.n_flag_words;
     s->n_delta_words = view.n_delta_words;
+    // a narrow blob keeps its exact image (the restore gathers from it) and gets its int32 cells
+    // back (serialisation, group info)
+    const int tw = view.tnar ? view.tnar_width : 0;
     const size_t o_tab = align_up(sizeof(SpGroups), 256);
-    const size_t o_fw = o_tab + align_up(sizeof(int32_t) * (size_t)std::max<int64_t>(s->ncells, 1), 256);
+    const size_t o_tn = o_tab + align_up(sizeof(int32_t) * (size_t)std::max<int64_t>(s->ncells, 1), 256);
+    const size_t o_fw = o_tn + (tw ? align_up((size_t)tw / 8 * (size_t)std::max<int64_t>(s->ncells, 1), 256) : 0);
     const size_t o_dw = o_fw + align_up(sizeof(uint64_t) * (size_t)s->n_flag_words, 256);
     const size_t total = o_dw + sizeof(uint64_t) * (size_t)s->n_delta_words;
     char* blk = static_cast<char*>(block_get(s->device, total, &s->block_cap));
@@ -1930,6 +1961,8 @@ int skml_sparse_import(skml_ctx* c, const void* blob, size_t len, skml_sparse** 
     s->block = blk;
     s->g_dev = reinterpret_cast<SpGroups*>(blk);
     s->tables = reinterpret_cast<int32_t*>(blk + o_tab);
+    s->tnar = tw ? blk + o_tn : nullptr;
+    s->tnar_width = tw;
     s->flag_words = reinterpret_cast<uint64_t*>(blk + o_fw);
     s->delta_words = reinterpret_cast<uint64_t*>(blk + o_dw);
     auto fail_rel = [&](int e) {
@@ -1943,8 +1976,12 @@ int skml_sparse_import(skml_ctx* c, const void* blob, size_t len, skml_sparse** 
         if (e_ != hipSuccess) return fail_rel(sfail(SKML_E_HIP, "%s failed: %s", #expr, hipGetErrorString(e_))); \
     } while (0)
     IMP_HIP(hipMemcpyAsync(s->g_dev, view.g_dev, sizeof(SpGroups), hipMemcpyDeviceToDevice, st));
-    if (s->ncells > 0)
+    if (s->ncells > 0 && tw) {
+        IMP_HIP(hipMemcpyAsync(s->tnar, view.tnar, (size_t)tw / 8 * (size_t)s->ncells, hipMemcpyDeviceToDevice, st));
+        IMP_HIP(launch_widen_cells(st, s->tnar, tw, s->ncells, s->g.fill, s->tables));
+    } else if (s->ncells > 0) {
         IMP_HIP(hipMemcpyAsync(s->tables, view.tables, sizeof(int32_t) * (size_t)s->ncells, hipMemcpyDeviceToDevice, st));
+    }
     if (s->n_flag_words > 0)
         IMP_HIP(hipMemcpyAsync(s->flag_words, view.flag_words, sizeof(uint64_t) * (size_t)s->n_flag_words,
                                hipMemcpyDeviceToDevice, st));

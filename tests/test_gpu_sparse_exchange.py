@@ -74,6 +74,55 @@ def test_export_import_round_trip(gpu):
     assert np.array_equal(v2.cpu().numpy(), (osp.q.values() * 0.5)[ob])
 
 
+def _blob_header(blob):
+    from sketchml_amd import _lib
+    return _lib.SparseBlobHeader.from_buffer_copy(blob[:256].cpu().numpy().tobytes())
+
+
+def _blob_cells(blob):
+    """The MinMax cells of a blob as int32: the exact narrow image widened (top code -> the fill)."""
+    h = _blob_header(blob)
+    raw = blob[h.off_tables:h.off_tables + h.ncells * h.table_width // 8].cpu().numpy()
+    if h.table_width == 32:
+        return raw.view(np.int32)
+    cells = raw.view(np.uint8 if h.table_width == 8 else np.uint16).astype(np.int64)
+    fill = int(blob[256 + 16:256 + 20].cpu().numpy().view(np.int32)[0])  # SpGroups.fill
+    cells[cells == (1 << h.table_width) - 1] = fill
+    return cells.astype(np.int32)
+
+
+@pytest.mark.parametrize("bins,width", [(256, 8), (3000, 16)])
+def test_blob_carries_exact_narrow_tables(gpu, bins, width):
+    """The exchange blob carries the MinMax tables as the encoder's exact narrow image: 8 bits a
+    cell for at most 255 effective bins, 16 bits up to 65,535, the fill as the top code.  Widened,
+    the cells equal the int32 table the payload serialises (MinMaxSketch.writeObject's table,
+    MinMaxSketch.java:88-97) -- the same payload read back by readObject has no narrow image and
+    exports int32 cells -- and a Gradient.sum over blobs of all three widths is exact."""
+    dim = 120011
+    pl, osp = _payload(gpu, dim, 0.3, 55, bins=bins)
+    assert (osp.q.bin_num <= 255) == (width == 8)
+    blob = pl.export()
+    h = _blob_header(blob)
+    assert (h.version, h.table_width) == (2, width)
+    wide = gpu.SparsePayload.deserialize(pl.serialize(), quant_values=pl.values())
+    blob32 = wide.export()
+    assert _blob_header(blob32).table_width == 32
+    assert blob.numel() < blob32.numel()
+    assert np.array_equal(_blob_cells(blob), _blob_cells(blob32))
+    tables = np.concatenate([pl.group(g)["table"] for g in range(8) if pl.group(g)["size"] > 0])
+    assert np.array_equal(np.sort(_blob_cells(blob)), np.sort(tables))
+    back = gpu.SparsePayload.from_blob(blob)          # the imported payload: cells widened again
+    assert back.serialize() == pl.serialize()
+    k0, b0 = pl.restore_bins()
+    k1, b1 = back.restore_bins()
+    assert torch.equal(k0, k1) and torch.equal(b0, b1)
+    p8, o8 = _payload(gpu, dim, 0.2, 56, bins=256)
+    allb, stride = _gather_local([pl, wide, p8, back])
+    got = gpu.decode_sum(allb, 4, stride, dim, 0.25).cpu().numpy()
+    want, _ = oracle_sum([osp, osp, o8, osp], dim, 0.25)
+    assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
+
+
 def test_corrupt_blobs_are_refused(gpu):
     pl, _ = _payload(gpu, 50000, 0.2, 2)
     blob = pl.export()
@@ -89,6 +138,13 @@ def test_corrupt_blobs_are_refused(gpu):
         gpu.SparsePayload.from_blob(bad)
     with pytest.raises(gpu.SketchMLException):    # shorter than the blob says
         gpu.SparsePayload.from_blob(blob, 1024)
+    from sketchml_amd import _lib
+    woff = _lib.SparseBlobHeader.table_width.offset
+    for w in (12, 16):                            # not a cell width; not this bin count's narrow width
+        bad = blob.clone()
+        bad[woff:woff + 4] = torch.from_numpy(np.array([w], dtype=np.int32).view(np.uint8)).cuda()
+        with pytest.raises(gpu.SketchMLException):
+            gpu.SparsePayload.from_blob(bad)
     # a key beyond the sum's dimension (SparseDoubleGradient's bound check)
     with pytest.raises(gpu.SketchMLException, match="outside"):
         gpu.decode_sum(blob, 1, blob.numel(), 1000)
@@ -136,17 +192,21 @@ def test_restore_values_refuse_bins_outside_quant_values(gpu, bins, forms):
     values), the plain one-pass kernel and the merge rounds alike; restore_bins() returns the raw
     cells as MinMaxSketch.query does."""
     from sketchml_amd import _lib
-    pl, _ = _payload(gpu, 60000, 0.2, 4, bins=bins)
+    pl, osp = _payload(gpu, 60000, 0.2, 4, bins=bins)
     blob = pl.export().clone()
-    hdr = blob[:256].cpu().numpy()
-    ncells = int(hdr[24:32].view(np.int64)[0])
-    off_tab = int(hdr[96:104].view(np.int64)[0])
-    cells = torch.full((ncells,), bins + 5, dtype=torch.int32, device="cuda")
-    blob[off_tab:off_tab + 4 * ncells] = cells.view(torch.uint8)
+    h = _lib.SparseBlobHeader.from_buffer_copy(blob[:256].cpu().numpy().tobytes())
+    beff = osp.q.bin_num
+    # the cells in the blob's width (the exact narrow image: the top code is the fill)
+    dt = {8: np.uint8, 16: np.uint16, 32: np.int32}[h.table_width]
+    assert h.table_width == (8 if beff <= 255 else 16)
+    value = min(beff + 5, (1 << h.table_width) - 2)  # outside quantValues, below the top code
+    assert value >= beff
+    cells = torch.from_numpy(np.full(h.ncells, value, dtype=dt).view(np.uint8)).cuda()
+    blob[h.off_tables:h.off_tables + cells.numel()] = cells
     bad = gpu.SparsePayload.from_blob(blob)
     with _lib.forced_forms(**forms):
         _, b = bad.restore_bins()
-        assert int(b.min()) == bins + 5 and int(b.max()) == bins + 5
+        assert int(b.min()) == value and int(b.max()) == value
         for dt in (torch.float32, torch.float64):
             with pytest.raises(gpu.SketchMLException, match="outside"):
                 bad.restore(dt)

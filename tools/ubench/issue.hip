@@ -4,6 +4,7 @@
 // s_memtime / s_memrealtime) and the kernel's wall time.
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <cstring>
 
 #define N_ITER 4096
 #define NV 32
@@ -55,6 +56,33 @@ __global__ __launch_bounds__(256) void kern(float* out, Stamp* st, float seed) {
             else if constexpr (KIND == 27) { asm volatile("v_max_f32_dpp %0, -%1, %2 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(b), "v"(a)); }
             else if constexpr (KIND == 28) { asm volatile("v_max_f32_dpp %0, -%1, %2 row_mirror row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(b), "v"(a)); }
             else if constexpr (KIND == 30) { asm volatile("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); }
+            else if constexpr (KIND == 31) { asm volatile("v_cmp_lt_f32_e32 vcc, %1, %2" : "=v"(r) : "v"(a), "v"(b) : "vcc"); }
+            else if constexpr (KIND == 32) { asm volatile("v_cndmask_b32_e32 %0, %1, %2, vcc" : "=v"(r) : "v"(a), "v"(b)); }
+            else if constexpr (KIND == 33) { asm volatile("v_min_i16_e32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); }
+            else if constexpr (KIND == 34) { asm volatile("v_max_u16_e32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); }
+            else if constexpr (KIND == 35) { asm volatile("v_sub_f32_e32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); }
+            else if constexpr (KIND == 36) { asm volatile("v_mov_b32_e32 %0, %1" : "=v"(r) : "v"(b)); }
+            else if constexpr (KIND == 37) { asm volatile("v_min_f32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:DWORD" : "=v"(r) : "v"(a), "v"(b)); }
+            else if constexpr (KIND == 38) {  // compare-exchange as v_cmp_e32 + 2 x v_cndmask_e32 (3 instructions per 2 values)
+                if (i & 1) { r = a; }
+                else {
+                    float lo, hi;
+                    asm volatile("v_cmp_lt_f32_e32 vcc, %2, %3\n\tv_cndmask_b32_e32 %0, %3, %2, vcc\n\tv_cndmask_b32_e32 %1, %2, %3, vcc"
+                                 : "=&v"(lo), "=&v"(hi) : "v"(a), "v"(b) : "vcc");
+                    r = lo;
+                    v[(i + 1) & (NV - 1)] = hi;
+                }
+            }
+            else if constexpr (KIND == 39) {  // compare-exchange as v_min_f32 + v_max_f32 (2 instructions per 2 values)
+                if (i & 1) { r = a; }
+                else {
+                    float lo, hi;
+                    asm volatile("v_min_f32 %0, %2, %3\n\tv_max_f32 %1, %2, %3" : "=&v"(lo), "=&v"(hi) : "v"(a), "v"(b));
+                    r = lo;
+                    v[(i + 1) & (NV - 1)] = hi;
+                }
+            }
+            else if constexpr (KIND == 40) { asm volatile("v_cmp_gt_u32_e32 vcc, %1, %2" : "=v"(r) : "v"(a), "v"(b) : "vcc"); }
             else if constexpr (KIND == 29) {  // two values per instruction: count as 2 per pair
                 typedef float f2v __attribute__((ext_vector_type(2)));
                 f2v p = {a, b}, q = {sel, sel};
@@ -73,8 +101,10 @@ __global__ __launch_bounds__(256) void kern(float* out, Stamp* st, float seed) {
     if (acc == 12345.f) pad[threadIdx.x] = acc;
 }
 
+static const char* g_filter = nullptr;
 template <int K>
 void run(const char* name, float* d, Stamp* st, Stamp* hst, int cus) {
+    if (g_filter && !strstr(name, g_filter)) return;
     for (int wps = 1; wps <= 8; wps *= 2) {
         const int blocks = cus * wps;
         const size_t lds = (160 * 1024) / wps - 1024;
@@ -100,7 +130,8 @@ void run(const char* name, float* d, Stamp* st, Stamp* hst, int cus) {
         cyc /= blocks * 4;
         real /= blocks * 4;
         const double ghz = cyc / real * 0.1;  // s_memrealtime runs at 100 MHz
-        const double instr = (double)N_ITER * NV;  // per wave
+        // per wave (the compare-exchange kinds: instructions per 2 values x NV / 2 per iteration)
+        const double instr = (double)N_ITER * (K == 38 ? NV / 2 * 3 : K == 39 ? NV : NV);
         // per SIMD: wps waves, each `instr` instructions, over `cyc` cycles
         printf("%-28s waves/SIMD %d  %6.2f cyc/instr/SIMD (in-wave)  %6.2f (wall)  clk %.2f GHz  %.3f ms\n", name,
                wps, cyc / (instr * wps), ms * 1e-3 * ghz * 1e9 / (instr * wps), ghz, ms);
@@ -117,6 +148,7 @@ int main(int argc, char** argv) {
     hipMalloc(&d, sizeof(float) * 256 * cus * 8);
     hipMalloc(&st, sizeof(Stamp) * cus * 8 * 4);
     hst = (Stamp*)malloc(sizeof(Stamp) * cus * 8 * 4);
+    if (argc > 1) g_filter = argv[1];
     printf("CUs %d\n", cus);
     run<0>("v_min_f32", d, st, hst, cus);
     run<30>("v_max_f32", d, st, hst, cus);
@@ -149,5 +181,15 @@ int main(int argc, char** argv) {
     run<27>("v_max_f32_dpp_neg_quad", d, st, hst, cus);
     run<28>("v_max_f32_dpp_neg_mirror", d, st, hst, cus);
     run<29>("v_pk_mul_f32/v_mul_f32 alt", d, st, hst, cus);
+    run<31>("v_cmp_lt_f32_e32", d, st, hst, cus);
+    run<32>("v_cndmask_b32_e32", d, st, hst, cus);
+    run<33>("v_min_i16_e32", d, st, hst, cus);
+    run<34>("v_max_u16_e32", d, st, hst, cus);
+    run<35>("v_sub_f32_e32", d, st, hst, cus);
+    run<36>("v_mov_b32_e32", d, st, hst, cus);
+    run<37>("v_min_f32_sdwa", d, st, hst, cus);
+    run<38>("CE cmp_e32+2xcndmask_e32", d, st, hst, cus);
+    run<39>("CE v_min_f32+v_max_f32", d, st, hst, cus);
+    run<40>("v_cmp_gt_u32_e32", d, st, hst, cus);
     return 0;
 }
