@@ -148,6 +148,8 @@ __host__ __device__ inline int tnar_width_for(int32_t bin_num) {
 // exceed the table's (gp->ncells) buckets: the extra workgroups exit
 hipError_t launch_mm_bucket(hipStream_t st, const void* pairs, const uint64_t* bucket_base, int nbuckets,
                             const SpGroups* gp, int32_t* table, void* tnar);
+// quantValues (Quantizer.getValues) of a dense quantizer payload into qv[bin_num] on the device
+hipError_t launch_sp_qvalues(hipStream_t st, const void* qpayload, double* qv);
 // int32 cells from an exact narrow image of tw (8 or 16) bits: the top code becomes `fill`
 hipError_t launch_widen_cells(hipStream_t st, const void* tn, int tw, int64_t ncells, int32_t fill, int32_t* t32);
 // DeltaAdaptiveEncoder bit streams: tile sums of (flag bits, delta bits), then the writer.

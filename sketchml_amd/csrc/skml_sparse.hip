@@ -660,7 +660,11 @@ hipError_t launch_compact64(hipStream_t st, const double* x, int64_t dim, int32_
 // =============================================================================================
 // Column scan of [tiles][K] u64 tile sums (one workgroup per column)
 // =============================================================================================
-constexpr int kScanThreads = 1024, kScanPer = 8;  // one workgroup per column, 8K entries per pass
+// One workgroup per column, 16K entries per pass (C3's 13,107 tiles: one pass).  256 threads, not
+// 1,024: a 1,024-thread workgroup needs 16 wave slots of one CU at once and, queued beside the
+// other restore's k_dec_keys in Gradient.sum, waited 150-250 us for a CU to drain
+// (profiles/r06c_aggregate_timeline.txt).
+constexpr int kScanThreads = 256, kScanPer = 64;
 // Entry (i, k) at sums[k * ld + i * es]: [tiles][K] row-major (ld 1, es K) or one column of
 // tiles + 1 entries per k (ld tiles + 1, es 1: contiguous column reads).
 __global__ __launch_bounds__(kScanThreads) void k_scan_cols(uint64_t* sums, int64_t tiles, int64_t ld, int64_t es) {
@@ -669,12 +673,25 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_cols(uint64_t* sums, int6
     uint64_t carry = 0;
     for (int64_t c0 = 0; c0 < tiles; c0 += kScanThreads * kScanPer) {
         uint64_t loc[kScanPer], s = 0;
+        const int64_t i0 = c0 + t * kScanPer;
+        if (es == 1 && i0 + kScanPer <= tiles && ((k * ld + i0) & 1) == 0) {  // 16-byte loads
+            typedef uint64_t u64x2_t __attribute__((ext_vector_type(2)));
+            const u64x2_t* src = reinterpret_cast<const u64x2_t*>(sums + k * ld + i0);
 #pragma unroll
-        for (int j = 0; j < kScanPer; j++) {
-            const int64_t i = c0 + t * kScanPer + j;
-            loc[j] = i < tiles ? sums[k * ld + i * es] : 0;
-            s += loc[j];
+            for (int j = 0; j < kScanPer / 2; j++) {
+                const u64x2_t v = src[j];
+                loc[2 * j] = v.x;
+                loc[2 * j + 1] = v.y;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < kScanPer; j++) {
+                const int64_t i = i0 + j;
+                loc[j] = i < tiles ? sums[k * ld + i * es] : 0;
+            }
         }
+#pragma unroll
+        for (int j = 0; j < kScanPer; j++) s += loc[j];
         const uint64_t inc = wave_incl_u64(s, lane);
         if (lane == 63) sh[w] = inc;
         __syncthreads();
@@ -1755,6 +1772,28 @@ hipError_t launch_mm_bucket(hipStream_t st, const void* pairs, const uint64_t* b
     if (nbuckets <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_mm_bucket, dim3((unsigned)nbuckets), dim3(kMmThreads), 0, st, pairs, bucket_base, gp,
                        table, tnar);
+    return hipGetLastError();
+}
+
+// SparseVectorCompressor.quantValues = Quantizer.getValues() (base/Quantizer.java:39-47) of the
+// values' quantizer payload, on the device: the same double expressions the host evaluates after
+// the encode's read-back, so the restore needs no upload of the table.
+__global__ __launch_bounds__(256) void k_sp_qvalues(const uint8_t* __restrict__ qpayload, double* __restrict__ qv) {
+    const skml_dense_header* h = reinterpret_cast<const skml_dense_header*>(qpayload);
+    if (h->status != SKML_OK) return;
+    const double* sp = reinterpret_cast<const double*>(qpayload + kHeaderBytes);
+    const int B = h->bin_num, ns = B - 1;
+    for (int b = (int)threadIdx.x; b < B && ns > 0; b += 256) {
+        double v;
+        if (b == 0) v = 0.5 * (h->min + sp[0]);
+        else if (b == ns) v = 0.5 * (sp[ns - 1] + h->max);
+        else v = 0.5 * (sp[b - 1] + sp[b]);
+        qv[b] = v;
+    }
+}
+
+hipError_t launch_sp_qvalues(hipStream_t st, const void* qpayload, double* qv) {
+    hipLaunchKernelGGL(k_sp_qvalues, dim3(1), dim3(256), 0, st, static_cast<const uint8_t*>(qpayload), qv);
     return hipGetLastError();
 }
 

@@ -241,6 +241,8 @@ struct skml_sparse {
     int64_t ncells = 0;
     void* tnar = nullptr;       // their exact narrow image (tnar_width_for), or nullptr; in the block
     int tnar_width = 0;         // 8 or 16 bits a cell
+    double* qv_dev = nullptr;   // quantValues on the device (in the block), valid while qv_dev_ok:
+    bool qv_dev_ok = false;     // written by the encode / import, stale after timesBy until re-uploaded
     uint64_t* flag_words = nullptr;  // concatenated DeltaAdaptive flag streams
     uint64_t* delta_words = nullptr;
     int64_t flag_bits = 0, delta_bits = 0;
@@ -459,11 +461,13 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const void* vals, bool f64, int6
     const size_t o_tn = o_tab + align_up(sizeof(int32_t) * (size_t)std::max<int64_t>(cells_max, 1), 256);
     const size_t o_fw = o_tn + (want_tn ? align_up(sizeof(uint16_t) * (size_t)std::max<int64_t>(cells_max, 1), 256) : 0);
     const size_t o_dw = o_fw + align_up(sizeof(uint64_t) * (size_t)fwn, 256);
-    const size_t total = o_dw + sizeof(uint64_t) * (size_t)dwn;
+    const size_t o_qv = o_dw + align_up(sizeof(uint64_t) * (size_t)dwn, 256);
+    const size_t total = o_qv + sizeof(double) * (size_t)p->bin_num;
     char* blk = static_cast<char*>(block_get(s->device, total, &s->block_cap));
     if (!blk) return bail(sfail(SKML_E_OOM, "sparse payload of %zu bytes", total));
     s->block = blk;
     s->qpayload = blk;
+    s->qv_dev = reinterpret_cast<double*>(blk + o_qv);
     s->g_dev = reinterpret_cast<SpGroups*>(blk + o_g);
     s->tables = reinterpret_cast<int32_t*>(blk + o_tab);
     s->tnar = want_tn ? blk + o_tn : nullptr;
@@ -504,6 +508,7 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const void* vals, bool f64, int6
     init.col_ratio = p->col_ratio;
     for (int g = 0; g < G; g++) pick_hashes(p->hash_seed + g, rows, init.hash_ids[g]);
     SP_TRY(launch_sp_plan_edges(st, s->qpayload, init, s->g_dev));
+    SP_TRY(launch_sp_qvalues(st, s->qpayload, s->qv_dev));
     const int64_t tiles = sp_tiles(nnz, kSpTile);
     uint64_t* tc = scratch<uint64_t>(c, kSlotTiles, (size_t)(tiles + 1) * G);
     if (!tc) return bail(sfail(SKML_E_OOM, "tile counts"));
@@ -582,6 +587,7 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const void* vals, bool f64, int6
             s->qvalues[(size_t)b] = v;
         }
     }
+    s->qv_dev_ok = true;
     s->ncells = s->g.ncells;
     s->tnar_width = s->tnar ? tnar_width_for(s->g.bin_num) : 0;
     if (!s->tnar_width) s->tnar = nullptr;
@@ -867,9 +873,13 @@ int decode_values(skml_ctx* c, const skml_sparse* s, int32_t* keys_dev, T* vals_
     // the value table's upload and the merge's RsInfo fill go first: the GPU runs them while the
     // decode's kernels are still being queued
     const int nq = (int)s->qvalues.size();
-    double* qv = reinterpret_cast<double*>(ctx_scratch(c, kSlotCells, sizeof(double) * s->qvalues.size()));
-    if (!qv) return sfail(SKML_E_OOM, "value table");
-    SP_HIP(hipMemcpyAsync(qv, s->qvalues.data(), sizeof(double) * s->qvalues.size(), hipMemcpyHostToDevice, st));
+    double* qv = s->qv_dev;  // the payload's device copy (encode / import), or the host table uploaded
+    if (!qv || !s->qv_dev_ok) {
+        if (!qv) qv = reinterpret_cast<double*>(ctx_scratch(c, kSlotCells, sizeof(double) * s->qvalues.size()));
+        if (!qv) return sfail(SKML_E_OOM, "value table");
+        SP_HIP(hipMemcpyAsync(qv, s->qvalues.data(), sizeof(double) * s->qvalues.size(), hipMemcpyHostToDevice, st));
+        if (qv == s->qv_dev) const_cast<skml_sparse*>(s)->qv_dev_ok = true;  // ordered before later restores
+    }
     RsMerge rm;
     if (int e = rs_merge_prepare(c, s, &rm)) return e;
     const RunBoundsOut rbo = rm.query_bounds();  // the merge's key-range bounds from the query
@@ -917,6 +927,7 @@ int skml_sparse_decode_f64(skml_ctx* c, const skml_sparse* s, int32_t* keys_dev,
 int skml_sparse_times_by(skml_sparse* s, double x) {
     if (!s) return sfail(SKML_E_ARG, "NULL argument");
     for (double& v : s->qvalues) v *= x;  // SparseVectorCompressor.timesBy (:128-134)
+    s->qv_dev_ok = false;  // the device copy is re-uploaded by the next restore
     return SKML_OK;
 }
 
@@ -1952,12 +1963,14 @@ int skml_sparse_import(skml_ctx* c, const void* blob, size_t len, skml_sparse** 
     const size_t o_tn = o_tab + align_up(sizeof(int32_t) * (size_t)std::max<int64_t>(s->ncells, 1), 256);
     const size_t o_fw = o_tn + (tw ? align_up((size_t)tw / 8 * (size_t)std::max<int64_t>(s->ncells, 1), 256) : 0);
     const size_t o_dw = o_fw + align_up(sizeof(uint64_t) * (size_t)s->n_flag_words, 256);
-    const size_t total = o_dw + sizeof(uint64_t) * (size_t)s->n_delta_words;
+    const size_t o_qv = o_dw + align_up(sizeof(uint64_t) * (size_t)s->n_delta_words, 256);
+    const size_t total = o_qv + sizeof(double) * std::max<size_t>(s->qvalues.size(), 1);
     char* blk = static_cast<char*>(block_get(s->device, total, &s->block_cap));
     if (!blk) {
         sparse_release(s);
         return sfail(SKML_E_OOM, "imported sparse payload of %zu bytes", total);
     }
+    s->qv_dev = reinterpret_cast<double*>(blk + o_qv);
     s->block = blk;
     s->g_dev = reinterpret_cast<SpGroups*>(blk);
     s->tables = reinterpret_cast<int32_t*>(blk + o_tab);
@@ -1976,6 +1989,10 @@ int skml_sparse_import(skml_ctx* c, const void* blob, size_t len, skml_sparse** 
         if (e_ != hipSuccess) return fail_rel(sfail(SKML_E_HIP, "%s failed: %s", #expr, hipGetErrorString(e_))); \
     } while (0)
     IMP_HIP(hipMemcpyAsync(s->g_dev, view.g_dev, sizeof(SpGroups), hipMemcpyDeviceToDevice, st));
+    if (!s->qvalues.empty())  // the blob's values section: the device copy of quantValues
+        IMP_HIP(hipMemcpyAsync(s->qv_dev, static_cast<const uint8_t*>(blob) + h.off_values,
+                               sizeof(double) * s->qvalues.size(), hipMemcpyDeviceToDevice, st));
+    s->qv_dev_ok = !s->qvalues.empty();
     if (s->ncells > 0 && tw) {
         IMP_HIP(hipMemcpyAsync(s->tnar, view.tnar, (size_t)tw / 8 * (size_t)s->ncells, hipMemcpyDeviceToDevice, st));
         IMP_HIP(launch_widen_cells(st, s->tnar, tw, s->ncells, s->g.fill, s->tables));

@@ -22,6 +22,7 @@
 #   leafgap                   tools/leaf_gap.py (clean / evented / synchronised encode blocks)
 #   leafwaves[:LIB]           tools/prof_leaf_waves.py at 2^28 (a SKML_PROF_LEAF build in LIB)
 #   mergephases[:LIB]         tools/prof_merge.py at 2^28 (a SKML_PROF_SUMMARY build in LIB)
+#   batchtrace[:ARGS]         rocprofv3 --kernel-trace over tools/batch_probe.py ARGS -> TAG/batch_timeline.txt
 #   ubench:NAME               tools/ubench/bin/NAME (built here: hipcc --offload-arch=gfx950 -O3 -o tools/ubench/bin/NAME tools/ubench/NAME.hip)
 # Per-variant libraries and kernel forms go through ab.sh's variants (lib:DIR, form:NAME:VALUE).
 set -e
@@ -100,6 +101,13 @@ for STEP in "$@"; do
       SKML_LIB=sketchml_amd/${LIB:-lib_profs}/libskml.so timeout -k 10 120 python tools/prof_merge.py 268435456 \
         > "$OUT/merge_phases.txt" 2>&1
       tail -3 "$OUT/merge_phases.txt" ;;
+    batchtrace*)
+      ARGS=${STEP#batchtrace}; ARGS=${ARGS#:}
+      timeout -k 10 300 rocprofv3 --kernel-trace -d "$OUT/batch_trace" -o run --output-format csv \
+        -- python3 tools/batch_probe.py $ARGS > "$OUT/batch_trace.log" 2>&1
+      python3 tools/trace_gaps.py "$OUT/batch_trace" --timeline 60 > "$OUT/batch_timeline.txt"
+      tail -1 "$OUT/batch_trace.log"
+      find "$OUT" -name "*.csv" -size +20M -delete ;;
     ubench:*)
       NAME=${STEP#ubench:}
       timeout -k 10 300 tools/ubench/bin/"$NAME" > "$OUT/ubench_$NAME.txt" 2>&1
