@@ -517,6 +517,9 @@ __global__ __launch_bounds__(256) void k_decode_sum(const uint8_t* __restrict__ 
 // owns 8 elements (half the registers of k_decode_sum: 8 waves per SIMD), the tables take
 // P x bins doubles of dynamic LDS instead of a 32 KB array, and the next step's codes are loaded
 // before this step's lookups.
+#ifndef SKML_OCC_WAVES
+#define SKML_OCC_WAVES 6  // waves per SIMD of the prefetching form (A/B builds vary it)
+#endif
 constexpr int kOccPer = 8, kOccMaxP = 8;
 // dynamic LDS of the P tables: what is left of the 64 KB a launch may take without opting in
 // after the kernel's static array of code pointers
@@ -556,7 +559,7 @@ __device__ __forceinline__ uint32_t code8_at(const uint32_t (&w)[4], int e, int 
     }
 }
 template <int BITS, bool PF>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PF ? 6 : 8))) void k_decode_sum_occ(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PF ? SKML_OCC_WAVES : 8))) void k_decode_sum_occ(
     const uint8_t* __restrict__ payloads, int P, size_t stride, float* __restrict__ out, int64_t n, double scale,
     int tab) {
     extern __shared__ double lt[];  // P tables of `tab` doubles
