@@ -683,9 +683,16 @@ def main():
                            ("uniform", "f32"): "skml_dense_encode_uniform_f32",
                            ("uniform", "f64"): "skml_dense_encode_uniform_f64"}[(args.quant, args.dtype)])
 
+    skip_exchange = [False]  # the N > 1 encode-only region (extras.encode_only)
+
     def step(i):
         x = xs[i % nbuf]
         b = i % len(payloads)
+        if skip_exchange[0]:
+            st = encode(ctx, C.c_void_p(x.data_ptr()), n, C.byref(params), C.c_void_p(payloads[b].data_ptr()), nb)
+            if st:
+                raise RuntimeError(_lib.last_error())
+            return
         if exch is not None and ex_used[b]:
             main_stream.wait_event(ev_ex[b])  # the previous all-gather of this buffer has read it
         p = payloads[b]
@@ -830,6 +837,16 @@ def main():
             extras["host_path"] = host_path_rates(lib, ctx, x, n, params)
             extras["h2d_d2h_inclusive_gbps"] = extras["host_path"]["pageable"]["gbps_fp32_in"]
 
+    # ---- N > 1: the same K encodes without the exchange (every rank's encode alone, at the max
+    # over ranks), so the scaling line shows the encode's own weak scaling beside `value` ----
+    if exch is not None:
+        skip_exchange[0] = True
+        el_enc = timed_region(nwarm + 2 * args.steps)
+        skip_exchange[0] = False
+        extras["encode_only"] = {"ms_per_step": round(1000.0 * el_enc / args.steps, 4),
+                                 "value_gbps": round(world * esize * n * args.steps / el_enc / 1e9, 2),
+                                 "note": "the same K steps with the payload all-gather left out; `value` keeps it "
+                                         "(each step's all-gather overlaps the next step's encode)"}
     # ---- N > 1: the exchange step alone, and a check of the gathered payloads ----
     if exch is not None and not args.no_extras:
         from sketchml_amd.distributed import decode_sum

@@ -288,18 +288,9 @@ int ensure_ranks(skml_ctx* ctx, int64_t n, int bins) {
         HIP_TRY(hipMalloc(&ctx->ranks, sizeof(int64_t) * (cnt + 1)));
         ctx->ranks_cap = cnt;
     }
-    std::vector<int64_t> r(cnt + 1, 0);
-    volatile double frac = 1.0 / bins;  // volatile: keep the JVM's sequential double rounding
-    const double step = 1.0 / bins;
-    for (size_t i = 0; i < cnt; i++) {
-        int64_t rank = (int64_t)((double)n * frac);
-        if (rank > n - 1) rank = n - 1;
-        r[i] = rank;
-        frac = frac + step;
-    }
-    HIP_TRY(hipMemcpyAsync(ctx->ranks, r.data(), sizeof(int64_t) * cnt, hipMemcpyHostToDevice,
-                           ctx->stream));
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    // written on the stream ahead of the sketch (no host table, no synchronisation); the kernels
+    // reading it follow on the same stream
+    HIP_TRY(launch_set_ranks(ctx->stream, n, bins, ctx->ranks));
     ctx->ranks_n = n;
     ctx->ranks_bins = bins;
     return SKML_OK;

@@ -161,6 +161,8 @@ hipError_t launch_merge_pass(hipStream_t st, const MergePass& pass, const MergeP
 hipError_t launch_summary(hipStream_t st, const float* x, int64_t n, const LeafPartial* part,
                           int64_t nparts, const float* roots, const int64_t* ranks, int req_bins,
                           int dedup, void* payload, double* scratch_raw, QuantLut* lut);
+// getQuantiles' rank table for (n, bins) written on the device (bins - 1 int64)
+hipError_t launch_set_ranks(hipStream_t st, int64_t n, int bins, int64_t* ranks);
 hipError_t launch_set_splits(hipStream_t st, void* payload, int64_t n, const double* splits_dev,
                              int nsplits, double mn, double mx, int req_bins, QuantLut* lut);
 // ---- kernel launchers (skml_dense.hip) ----

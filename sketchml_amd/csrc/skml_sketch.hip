@@ -1029,7 +1029,7 @@ __global__ __launch_bounds__(512, MINW) void k_leaf(const float* __restrict__ x,
 #define SKML_LEAF_SPLIT_TAIL_PCT 100
 #endif
 static int64_t leaf_split_from(int64_t full_tiles) {
-    auto tail = [&](int pct_x2) {  // the first split tile for the last pct_x2 / 2 % of the tiles
+    [[maybe_unused]] auto tail = [&](int pct_x2) {  // the first split tile for the last pct_x2 / 2 % of the tiles
         const int64_t s = full_tiles - full_tiles * pct_x2 / 200;
         return std::max<int64_t>(0, s / kLeaf2Waves * kLeaf2Waves);
     };
@@ -1810,6 +1810,27 @@ __global__ __launch_bounds__(256) void k_set_splits(uint8_t* payload, int64_t n,
         hdr->codes_offset = (int64_t)dense_codes_offset(req_bins);
         hdr->reserved = 0;
     }
+}
+
+// HeapQuantileSketch.getQuantiles' ranks (HeapQuantileSketch.java:305-320): rank_i = min((long)(n *
+// curFrac), n - 1) with curFrac += 1/bins accumulated in double, in order -- one thread, the same
+// IEEE double sequence as the JVM (built with -ffp-contract=off).  On the device so that a new n
+// (every sparse payload's nnz) costs no host upload and no synchronisation.
+__global__ __launch_bounds__(64) void k_set_ranks(int64_t n, int bins, int64_t* __restrict__ ranks) {
+    if (threadIdx.x != 0) return;
+    const double step = 1.0 / bins;
+    double frac = step;
+    for (int i = 0; i < bins - 1; i++) {
+        int64_t r = (int64_t)((double)n * frac);
+        if (r > n - 1) r = n - 1;
+        ranks[i] = r;
+        frac = frac + step;
+    }
+}
+
+hipError_t launch_set_ranks(hipStream_t st, int64_t n, int bins, int64_t* ranks) {
+    hipLaunchKernelGGL(k_set_ranks, dim3(1), dim3(64), 0, st, n, bins, ranks);
+    return hipGetLastError();
 }
 
 hipError_t launch_set_splits(hipStream_t st, void* payload, int64_t n, const double* splits_dev,
