@@ -73,6 +73,47 @@ __device__ __forceinline__ void st_status(uint64_t* p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+#ifndef SKML_LOOKBACK_ROWS
+#define SKML_LOOKBACK_ROWS 16  // predecessors per look-back step = 64 x this (A/B builds vary it)
+#endif
+// Decoupled look-back of one wave: the sum of the counts of the tiles before `tile` (every lane
+// gets it).  One step loads 64 x K predecessors' status words at once (K per lane, all in flight),
+// then walks them nearest first, in rows of 64, to the nearest inclusive prefix.  The tiles in
+// flight finish at about the same time, so the nearest prefix sits several hundred tiles back: at
+// 64 per step that took a dozen dependent L2 round trips per tile.
+template <int K>
+__device__ __forceinline__ uint64_t lookback_excl(const uint64_t* status, int64_t tile, int lane) {
+    uint64_t acc = 0;
+    int64_t p = tile - 1;
+    bool done = false;
+    while (!done) {
+        uint64_t sv[K];
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const int64_t idx = p - (int64_t)(k * 64 + lane);
+            sv[k] = idx >= 0 ? ld_status(&status[idx]) : kStPre;  // before tile 0: prefix 0
+        }
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            if (!done) {  // (no break: sv stays in registers only while every index is static)
+                const int64_t idx = p - (int64_t)(k * 64 + lane);
+                while (__ballot((sv[k] & ~kStMask) == 0)) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if ((sv[k] & ~kStMask) == 0) sv[k] = ld_status(&status[idx]);
+                }
+                const uint64_t pre = __ballot((sv[k] & ~kStMask) == kStPre);
+                const int stop = pre ? __ffsll((unsigned long long)pre) - 1 : 63;
+                acc += lane <= stop ? (sv[k] & kStMask) : 0;
+                done = pre != 0;
+            }
+        }
+        p -= 64 * K;
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    return acc;
+}
+
 // packed code of element e (LSB-first codes, code_bits in {1,2,4,8,16})
 __device__ __forceinline__ int32_t code_at(const uint8_t* codes, int64_t e, int bits) {
     switch (bits) {
@@ -365,29 +406,13 @@ __global__ __launch_bounds__(kSpThreads) void k_compact(const T* __restrict__ x,
         slab_pre[j] = tile_total + before;
         tile_total += tot;
     }
-    if (t < 64) {  // wave 0: publish the aggregate, then look back 64 predecessors per step
+    if (t < 64) {  // wave 0: publish the aggregate, then look back
         uint64_t excl = 0;
         if (tile == 0) {
             if (lane == 0) st_status(&status[0], kStPre | tile_total);
         } else {
             if (lane == 0) st_status(&status[tile], kStAgg | tile_total);
-            int64_t p = tile - 1;
-            while (true) {
-                const int64_t idx = p - lane;
-                uint64_t sv = idx >= 0 ? ld_status(&status[idx]) : kStPre;  // before tile 0: prefix 0
-                while (__ballot((sv & ~kStMask) == 0)) {
-                    __builtin_amdgcn_s_sleep(1);
-                    if ((sv & ~kStMask) == 0) sv = ld_status(&status[idx]);
-                }
-                const uint64_t pre = __ballot((sv & ~kStMask) == kStPre);
-                const int stop = pre ? __ffsll((unsigned long long)pre) - 1 : 63;  // nearest prefix
-                uint64_t contrib = lane <= stop ? (sv & kStMask) : 0;
-#pragma unroll
-                for (int off = 32; off >= 1; off >>= 1) contrib += __shfl_xor(contrib, off, 64);
-                excl += contrib;
-                if (pre) break;
-                p -= 64;
-            }
+            excl = lookback_excl<sizeof(T) == 8 ? 1 : 4>(status, tile, lane);  // rows the register budget allows
             if (lane == 0) st_status(&status[tile], kStPre | (excl + tile_total));
         }
         if (lane == 0) {
@@ -569,30 +594,14 @@ __global__ __launch_bounds__(kSpThreads) __attribute__((amdgpu_waves_per_eu(3)))
             for (int e = 0; e < 4; e++) f[j][e] = g[j][e];
     }
     const uint32_t tile_total = run;
-    if (t < 64) {  // wave 0: publish the aggregate, then look back 64 predecessors per step
+    if (t < 64) {  // wave 0: publish the aggregate, then look back
         const int lane = t;
         uint64_t excl = 0;
         if (tile == 0) {
             if (lane == 0) st_status(&status[0], kStPre | tile_total);
         } else {
             if (lane == 0) st_status(&status[tile], kStAgg | tile_total);
-            int64_t p = tile - 1;
-            while (true) {
-                const int64_t idx = p - lane;
-                uint64_t sv = idx >= 0 ? ld_status(&status[idx]) : kStPre;
-                while (__ballot((sv & ~kStMask) == 0)) {
-                    __builtin_amdgcn_s_sleep(1);
-                    if ((sv & ~kStMask) == 0) sv = ld_status(&status[idx]);
-                }
-                const uint64_t pre = __ballot((sv & ~kStMask) == kStPre);
-                const int stop = pre ? __ffsll((unsigned long long)pre) - 1 : 63;
-                uint64_t contrib = lane <= stop ? (sv & kStMask) : 0;
-#pragma unroll
-                for (int off = 32; off >= 1; off >>= 1) contrib += __shfl_xor(contrib, off, 64);
-                excl += contrib;
-                if (pre) break;
-                p -= 64;
-            }
+            excl = lookback_excl<SKML_LOOKBACK_ROWS>(status, tile, lane);
             if (lane == 0) st_status(&status[tile], kStPre | (excl + tile_total));
         }
         if (lane == 0) {

@@ -7,6 +7,7 @@
 #       gap    -> tools/leaf_gap.py --steps 20 --reps 2 (gap26 / gap24: at 2^26 / 2^24 floats)
 #       restore -> tools/bench_sparse.py --only-decode (restore of one C3 payload)
 #       batch  -> tools/batch_probe.py (skml_dense_encode_batch_f32, 8 x 2^26 floats)
+#       sparse_enc -> tools/bench_sparse.py --only-e2e (C3 dense -> payload)
 # VARIANT: name=SETTINGS, SETTINGS a comma list of
 #       lib:DIR          another in-tree build (SKML_LIB=sketchml_amd/DIR/libskml.so)
 #       form:NAME:VALUE  a skml_debug_form setting, applied by the tool (tools/forms.py)
@@ -25,6 +26,7 @@ case $KIND in
   gap26)  CMD="python tools/leaf_gap.py --steps 40 --reps 2 --n 67108864" ;;
   gap24)  CMD="python tools/leaf_gap.py --steps 80 --reps 2 --n 16777216" ;;
   restore) CMD="python tools/bench_sparse.py --reps 20 --only-decode" ;;
+  sparse_enc) CMD="python tools/bench_sparse.py --reps 20 --only-e2e" ;;
   batch)  CMD="python tools/batch_probe.py --reps 7" ;;
   *) echo "unknown kind $KIND"; exit 2 ;;
 esac

@@ -8,8 +8,8 @@ lines = [ln for ln in open(path).read().splitlines() if ln.startswith("{")]
 d = json.loads(lines[-1])
 if kind == "dense":
     out = {"ms_per_step": d["ms_per_step"], "kernels_us": {k: v["avg_us"] for k, v in d["extras"]["kernels"].items()}}
-elif kind == "sparse":
-    out = d["ms"]
+elif kind in ("sparse", "sparse_enc"):
+    out = d.get("ms", d)
 elif kind in ("gap", "gap26", "gap24"):
     out = d.get("summary", d)
 else:
