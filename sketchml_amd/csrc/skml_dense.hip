@@ -101,16 +101,6 @@ __device__ __forceinline__ uint32_t quant_bin(const QuantTables& q, float xv) {
 #endif
 constexpr int kQStageWords = 256;  // per wave: 1,024 one-byte codes
 
-// Tile order of the quantize pass: SKML_Q_REVERSE 1 walks the bucket from its end, so the first
-// waves read what the sketch's leaf pass read last (its tiles go in ascending order), while that
-// is still in the memory-side cache (256 MB on MI355X); 0 is ascending (A/B builds).
-#ifndef SKML_Q_REVERSE
-#define SKML_Q_REVERSE 1
-#endif
-__device__ __forceinline__ int64_t q_tile_at(int64_t i, int64_t full_tiles) {
-    return SKML_Q_REVERSE ? full_tiles - 1 - i : i;
-}
-
 template <int MODE>
 __device__ __forceinline__ void quant_tiles(const QuantTables& q, const float* __restrict__ x, int64_t n,
                                             uint8_t* __restrict__ codes, int bits, uint32_t* __restrict__ stage) {
@@ -122,7 +112,7 @@ __device__ __forceinline__ void quant_tiles(const QuantTables& q, const float* _
     // software-pipelined: the next tile's 4 KiB is in flight while this one is binned
     f32x4 f[4];
     if (wave_id < full_tiles) {
-        const f32x4* src = reinterpret_cast<const f32x4*>(x + q_tile_at(wave_id, full_tiles) * 1024);
+        const f32x4* src = reinterpret_cast<const f32x4*>(x + wave_id * 1024);
 #pragma unroll
         for (int j = 0; j < 4; j++) f[j] = __builtin_nontemporal_load(src + j * 64 + lane);
     }
@@ -130,12 +120,11 @@ __device__ __forceinline__ void quant_tiles(const QuantTables& q, const float* _
     const bool wt = SKML_Q_STORE != 0 && bits == 8 && (reinterpret_cast<uintptr_t>(codes) & 15) == 0;
     const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
         codes, 0, (int)std::min<int64_t>(full_tiles * 1024, (int64_t)0x7FFFFC00), 0x00020000);
-    for (int64_t it = wave_id; it < full_tiles; it += nwaves_total) {
-        const int64_t tile = q_tile_at(it, full_tiles);
+    for (int64_t tile = wave_id; tile < full_tiles; tile += nwaves_total) {
         f32x4 g[4];
-        const int64_t next = it + nwaves_total;
+        const int64_t next = tile + nwaves_total;
         if (next < full_tiles) {
-            const f32x4* src = reinterpret_cast<const f32x4*>(x + q_tile_at(next, full_tiles) * 1024);
+            const f32x4* src = reinterpret_cast<const f32x4*>(x + next * 1024);
 #pragma unroll
             for (int j = 0; j < 4; j++) g[j] = __builtin_nontemporal_load(src + j * 64 + lane);
         }
@@ -529,7 +518,7 @@ __global__ __launch_bounds__(256) void k_decode_sum(const uint8_t* __restrict__ 
 // P x bins doubles of dynamic LDS instead of a 32 KB array, and the next step's codes are loaded
 // before this step's lookups.
 #ifndef SKML_OCC_WAVES
-#define SKML_OCC_WAVES 6  // waves per SIMD of the prefetching form (A/B builds vary it)
+#define SKML_OCC_WAVES 4  // waves per SIMD of the prefetching form (4 against 6 and 8: profiles/ab/r06_occ_waves.txt)
 #endif
 constexpr int kOccPer = 8, kOccMaxP = 8;
 // dynamic LDS of the P tables: what is left of the 64 KB a launch may take without opting in

@@ -74,7 +74,7 @@ __device__ __forceinline__ void st_status(uint64_t* p, uint64_t v) {
 }
 
 #ifndef SKML_LOOKBACK_ROWS
-#define SKML_LOOKBACK_ROWS 16  // predecessors per look-back step = 64 x this (A/B builds vary it)
+#define SKML_LOOKBACK_ROWS 1  // predecessors per look-back step = 64 x this (A/B builds vary it)
 #endif
 // Decoupled look-back of one wave: the sum of the counts of the tiles before `tile` (every lane
 // gets it).  One step loads 64 x K predecessors' status words at once (K per lane, all in flight),
@@ -547,6 +547,27 @@ __device__ __forceinline__ void cb_load(const float* __restrict__ x, int64_t bas
     }
 }
 
+// workgroups of `kern` (`threads` each) resident at once on the device; 0 if the query fails
+template <typename K>
+static int resident_blocks(K kern, int threads) {
+    int dev = 0, per_cu = 0;
+    hipDeviceProp_t prop;
+    int r = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, 0) == hipSuccess)
+        r = std::max(1, per_cu) * prop.multiProcessorCount;
+    (void)hipGetLastError();
+    return r;
+}
+
+#ifndef SKML_COMPACT_PERSIST
+#define SKML_COMPACT_PERSIST 1  // 0: one tile per workgroup (A/B builds)
+#endif
+// Persistent form: a workgroup takes the next tile's ticket before its look-back and loads that
+// tile's first sub-tile while its stores drain, so no workgroup start, first-load latency or store
+// phase leaves the CU without loads in flight; the grid is what the CUs hold at once.  Tickets are
+// taken in order by running workgroups, and a workgroup waits only on lower tickets, so the
+// look-back always progresses.
 __global__ __launch_bounds__(kSpThreads) __attribute__((amdgpu_waves_per_eu(3))) void k_compact_big(const float* __restrict__ x, int64_t dim,
                                                             int32_t* __restrict__ keys, float* __restrict__ vals,
                                                             uint64_t* status, unsigned* ticket, int64_t ntiles,
@@ -558,88 +579,100 @@ __global__ __launch_bounds__(kSpThreads) __attribute__((amdgpu_waves_per_eu(3)))
     __shared__ int64_t s_tile;
     __shared__ uint64_t s_excl;
     const int t = threadIdx.x;
+    if ((reinterpret_cast<uintptr_t>(x) & 15) != 0) __builtin_trap();  // the launcher checks alignment
     if (t == 0) s_tile = (int64_t)atomicAdd(ticket, 1u);
     __syncthreads();
-    const int64_t tile = s_tile;
-    const int64_t base = tile * kCbTile;
-    if ((reinterpret_cast<uintptr_t>(x) & 15) != 0) __builtin_trap();  // the launcher checks alignment
+    int64_t tile = s_tile;
+    if (tile >= ntiles) return;  // workgroup-uniform
     float f[kCbSlabs][4], g[kCbSlabs][4];
-    uint32_t run = 0;
-    cb_load(x, base, dim, f);
+    cb_load(x, tile * kCbTile, dim, f);
 #pragma unroll 1
-    for (int sb = 0; sb < kCbSub; sb++) {
-        float (&cur)[kCbSlabs][4] = f;
-        if (sb + 1 < kCbSub) cb_load(x, base + (int64_t)(sb + 1) * kCbSubElems, dim, g);
-        CbRanks R;
-        cb_rank(cur, wtot, R);
-        if (t == 0) sub_pre[sb] = run;
-        if (run + R.total <= (uint32_t)kCbCap) {
+    while (true) {
+        const int64_t base = tile * kCbTile;
+        uint32_t run = 0;
+#pragma unroll 1
+        for (int sb = 0; sb < kCbSub; sb++) {
+            float (&cur)[kCbSlabs][4] = f;
+            if (sb + 1 < kCbSub) cb_load(x, base + (int64_t)(sb + 1) * kCbSubElems, dim, g);
+            CbRanks R;
+            cb_rank(cur, wtot, R);
+            if (t == 0) sub_pre[sb] = run;
+            if (run + R.total <= (uint32_t)kCbCap) {
 #pragma unroll
-            for (int j = 0; j < kCbSlabs; j++) {
-                uint32_t pos = run + R.slab_pre[j];
-                const int off0 = 4 * (j * kSpThreads + t);
+                for (int j = 0; j < kCbSlabs; j++) {
+                    uint32_t pos = run + R.slab_pre[j];
+                    const int off0 = 4 * (j * kSpThreads + t);
 #pragma unroll
-                for (int e = 0; e < 4; e++)
-                    if ((R.keep >> (4 * j + e)) & 1u) {
-                        st_v[pos] = cur[j][e];
-                        st_k[pos] = (uint16_t)(off0 + e);
-                        pos++;
-                    }
+                    for (int e = 0; e < 4; e++)
+                        if ((R.keep >> (4 * j + e)) & 1u) {
+                            st_v[pos] = cur[j][e];
+                            st_k[pos] = (uint16_t)(off0 + e);
+                            pos++;
+                        }
+                }
+            }
+            run += R.total;
+#pragma unroll
+            for (int j = 0; j < kCbSlabs; j++)
+#pragma unroll
+                for (int e = 0; e < 4; e++) f[j][e] = g[j][e];
+        }
+        const uint32_t tile_total = run;
+        // every thread read s_tile before cb_rank's barriers: the next ticket may land there now
+        if (SKML_COMPACT_PERSIST && t == 0) s_tile = (int64_t)atomicAdd(ticket, 1u);
+        if (t < 64) {  // wave 0: publish the aggregate, then look back
+            const int lane = t;
+            uint64_t excl = 0;
+            if (tile == 0) {
+                if (lane == 0) st_status(&status[0], kStPre | tile_total);
+            } else {
+                if (lane == 0) st_status(&status[tile], kStAgg | tile_total);
+                excl = lookback_excl<SKML_LOOKBACK_ROWS>(status, tile, lane);
+                if (lane == 0) st_status(&status[tile], kStPre | (excl + tile_total));
+            }
+            if (lane == 0) {
+                s_excl = excl;
+                sub_pre[kCbSub] = tile_total;
+                if (tile == ntiles - 1) *nnz_out = (int64_t)(excl + tile_total);
             }
         }
-        run += R.total;
+        __syncthreads();
+        const int64_t out0 = (int64_t)s_excl;
+        const int64_t next = SKML_COMPACT_PERSIST ? s_tile : ntiles;
+        if (tile_total <= (uint32_t)kCbCap) {
+            if (next < ntiles) cb_load(x, next * kCbTile, dim, f);  // in flight while this tile's stores drain
+            for (uint32_t q = t; q < tile_total; q += kSpThreads) {
+                int sb = 0;
 #pragma unroll
-        for (int j = 0; j < kCbSlabs; j++)
-#pragma unroll
-            for (int e = 0; e < 4; e++) f[j][e] = g[j][e];
-    }
-    const uint32_t tile_total = run;
-    if (t < 64) {  // wave 0: publish the aggregate, then look back
-        const int lane = t;
-        uint64_t excl = 0;
-        if (tile == 0) {
-            if (lane == 0) st_status(&status[0], kStPre | tile_total);
+                for (int k = 1; k < kCbSub; k++) sb += q >= sub_pre[k] ? 1 : 0;
+                keys[out0 + q] = (int32_t)(base + (int64_t)sb * kCbSubElems + st_k[q]);
+                vals[out0 + q] = st_v[q];
+            }
         } else {
-            if (lane == 0) st_status(&status[tile], kStAgg | tile_total);
-            excl = lookback_excl<SKML_LOOKBACK_ROWS>(status, tile, lane);
-            if (lane == 0) st_status(&status[tile], kStPre | (excl + tile_total));
-        }
-        if (lane == 0) {
-            s_excl = excl;
-            sub_pre[kCbSub] = tile_total;
-            if (tile == ntiles - 1) *nnz_out = (int64_t)(excl + tile_total);
-        }
-    }
-    __syncthreads();
-    const int64_t out0 = (int64_t)s_excl;
-    if (tile_total <= (uint32_t)kCbCap) {
-        for (uint32_t q = t; q < tile_total; q += kSpThreads) {
-            int sb = 0;
+            // more kept values than the stage holds: read each sub-tile again and store directly
+            for (int sb = 0; sb < kCbSub; sb++) {
+                const int64_t sbase = base + (int64_t)sb * kCbSubElems;
+                cb_load(x, sbase, dim, f);
+                CbRanks R;
+                cb_rank(f, wtot, R);
 #pragma unroll
-            for (int k = 1; k < kCbSub; k++) sb += q >= sub_pre[k] ? 1 : 0;
-            keys[out0 + q] = (int32_t)(base + (int64_t)sb * kCbSubElems + st_k[q]);
-            vals[out0 + q] = st_v[q];
-        }
-        return;
-    }
-    // more kept values than the stage holds: read each sub-tile again and store directly
-    for (int sb = 0; sb < kCbSub; sb++) {
-        const int64_t sbase = base + (int64_t)sb * kCbSubElems;
-        cb_load(x, sbase, dim, f);
-        CbRanks R;
-        cb_rank(f, wtot, R);
+                for (int j = 0; j < kCbSlabs; j++) {
+                    int64_t pos = out0 + sub_pre[sb] + R.slab_pre[j];
+                    const int64_t e0 = sbase + 4 * ((int64_t)j * kSpThreads + t);
 #pragma unroll
-        for (int j = 0; j < kCbSlabs; j++) {
-            int64_t pos = out0 + sub_pre[sb] + R.slab_pre[j];
-            const int64_t e0 = sbase + 4 * ((int64_t)j * kSpThreads + t);
-#pragma unroll
-            for (int e = 0; e < 4; e++)
-                if ((R.keep >> (4 * j + e)) & 1u) {
-                    keys[pos] = (int32_t)(e0 + e);
-                    vals[pos] = f[j][e];
-                    pos++;
+                    for (int e = 0; e < 4; e++)
+                        if ((R.keep >> (4 * j + e)) & 1u) {
+                            keys[pos] = (int32_t)(e0 + e);
+                            vals[pos] = f[j][e];
+                            pos++;
+                        }
                 }
+            }
+            if (next < ntiles) cb_load(x, next * kCbTile, dim, f);
         }
+        if (next >= ntiles) break;
+        __syncthreads();  // the stage, sub_pre and s_excl are the next tile's
+        tile = next;
     }
 }
 
@@ -657,7 +690,12 @@ hipError_t launch_compact(hipStream_t st, const float* x, int64_t dim, int32_t* 
     if ((reinterpret_cast<uintptr_t>(x) & 15) != 0 || dim < kCbTile)  // small or unaligned: the one-tile kernel
         return launch_compact_t<float>(st, x, dim, keys, vals, status, ticket, nnz_out);
     const int64_t tiles = sp_tiles(dim, kCbTile);
-    hipLaunchKernelGGL(k_compact_big, dim3((unsigned)tiles), dim3(kSpThreads), 0, st, x, dim, keys, vals, status,
+    int64_t grid = tiles;
+    if (SKML_COMPACT_PERSIST) {  // the workgroups the CUs hold at once
+        static const int resident = resident_blocks(k_compact_big, kSpThreads);
+        if (resident > 0) grid = std::min<int64_t>(tiles, resident);
+    }
+    hipLaunchKernelGGL(k_compact_big, dim3((unsigned)grid), dim3(kSpThreads), 0, st, x, dim, keys, vals, status,
                        ticket, tiles, nnz_out);
     return hipGetLastError();
 }
@@ -669,11 +707,19 @@ hipError_t launch_compact64(hipStream_t st, const double* x, int64_t dim, int32_
 // =============================================================================================
 // Column scan of [tiles][K] u64 tile sums (one workgroup per column)
 // =============================================================================================
-// One workgroup per column, 16K entries per pass (C3's 13,107 tiles: one pass).  256 threads, not
-// 1,024: a 1,024-thread workgroup needs 16 wave slots of one CU at once and, queued beside the
-// other restore's k_dec_keys in Gradient.sum, waited 150-250 us for a CU to drain
-// (profiles/r06c_aggregate_timeline.txt).
-constexpr int kScanThreads = 256, kScanPer = 64;
+// One workgroup of 1,024 threads per column, 8K entries per pass.  A 1,024-thread workgroup needs
+// 16 wave slots of one CU at once, and in Gradient.sum it waits for a CU beside the other
+// restore's k_dec_keys (profiles/r06c_aggregate_timeline.txt); 256-thread one-pass scans remove
+// that wait but ran slower end to end (restore +13 us, Gradient.sum +80 us: the two restores'
+// key queries then overlap each other, profiles/ab/r06_scan_threads.txt).
+#ifndef SKML_SCAN_THREADS
+#define SKML_SCAN_THREADS 1024  // A/B builds: 256 (with SKML_SCAN_PER 64)
+#endif
+#ifndef SKML_SCAN_PER
+#define SKML_SCAN_PER 8
+#endif
+constexpr int kScanThreads = SKML_SCAN_THREADS, kScanPer = SKML_SCAN_PER;
+static_assert(kScanPer % 2 == 0, "16-byte loads of two entries");
 // Entry (i, k) at sums[k * ld + i * es]: [tiles][K] row-major (ld 1, es K) or one column of
 // tiles + 1 entries per k (ld tiles + 1, es 1: contiguous column reads).
 __global__ __launch_bounds__(kScanThreads) void k_scan_cols(uint64_t* sums, int64_t tiles, int64_t ld, int64_t es) {
@@ -3039,19 +3085,6 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_keys_p(const uint32_t* __re
 }
 #endif  // SKML_AB
 
-
-// workgroups of `kern` (`threads` each) resident at once on the device; 0 if the query fails
-template <typename K>
-static int resident_blocks(K kern, int threads) {
-    int dev = 0, per_cu = 0;
-    hipDeviceProp_t prop;
-    int r = 0;
-    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess &&
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, 0) == hipSuccess)
-        r = std::max(1, per_cu) * prop.multiProcessorCount;
-    (void)hipGetLastError();
-    return r;
-}
 
 hipError_t launch_dec_keys(hipStream_t st, const uint32_t* delta, int64_t n, const SpGroups* gp, const SpGroups& gh,
                            const uint64_t* tile_base, const uint64_t* gpre, const int32_t* table, const void* tnar,

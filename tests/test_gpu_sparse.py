@@ -244,9 +244,9 @@ def test_compaction_exact(gpu):
 def test_compaction_big_tiles(gpu, dim, density):
     """The 65,536-value tiles of k_compact_big: kept values staged in LDS up to 8,192 per tile (a
     tile above that re-reads its input), partial last tiles, all-zero input.  At 2^26 + 9 there
-    are more tiles (1,025) than resident workgroups (3 per CU), so later tiles look back across
-    workgroups dispatched in a second wave; at densities around and above 1/8 some or all tiles
-    take the re-read path."""
+    are more tiles (1,025) than resident workgroups (3 per CU), so each persistent workgroup takes
+    a second tile (prefetched during its first tile's stores) and looks back across tiles held by
+    other workgroups; at densities around and above 1/8 some or all tiles take the re-read path."""
     rng = np.random.default_rng(dim)
     x = np.where(rng.random(dim) < density, rng.standard_normal(dim), 0.0).astype(np.float32)
     x[rng.random(dim) < 0.001] = np.float32(1e-8)
