@@ -520,43 +520,49 @@ __global__ __launch_bounds__(256) void k_decode_sum(const uint8_t* __restrict__ 
 #ifndef SKML_OCC_WAVES
 #define SKML_OCC_WAVES 4  // waves per SIMD of the prefetching form (4 against 6 and 8: profiles/ab/r06_occ_waves.txt)
 #endif
-constexpr int kOccPer = 8, kOccMaxP = 8;
+#ifndef SKML_OCC_PER
+#define SKML_OCC_PER 8  // elements per lane and step (A/B builds: 16)
+#endif
+constexpr int kOccPer = SKML_OCC_PER, kOccMaxP = 8;
+static_assert(kOccPer == 8 || kOccPer == 16, "8 or 16 elements per lane");
 // dynamic LDS of the P tables: what is left of the 64 KB a launch may take without opting in
 // after the kernel's static array of code pointers
 constexpr size_t kOccLdsMax = 64 * 1024 - sizeof(const uint8_t*) * kOccMaxP;
+// code words one lane holds per payload and step
+template <int BITS>
+constexpr int occ_words() { return kOccPer * BITS >= 32 ? kOccPer * BITS / 32 : 1; }
 // The code loads go through a global (address space 1) pointer: the payloads' code pointers sit in
 // LDS, and loads through a generic pointer would be flat loads, which count on lgkmcnt too, so the
 // table lookups' LDS waits would also wait for the next step's prefetched codes.
 #define SKML_G(T) const __attribute__((address_space(1))) T*
-__device__ __forceinline__ void load_codes8(const uint8_t* codes_any, int64_t e0, int bits, uint32_t (&w)[4]) {
+template <int BITS>
+__device__ __forceinline__ void load_codes_occ(const uint8_t* codes_any, int64_t e0, uint32_t (&w)[occ_words<BITS>()]) {
     SKML_G(uint8_t) codes = (SKML_G(uint8_t))codes_any;
-    switch (bits) {
-        case 8: {
-            typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
-            const u32x2_t v = *(SKML_G(u32x2_t))(codes + e0);
-            w[0] = v.x; w[1] = v.y;
-            break;
+    constexpr int kBytes = kOccPer * BITS / 8;  // e0 is a multiple of kOccPer: aligned to kBytes
+    const int64_t b0 = e0 * BITS / 8;
+    typedef uint32_t u32x4_g __attribute__((ext_vector_type(4)));
+    typedef uint32_t u32x2_g __attribute__((ext_vector_type(2)));
+    if constexpr (kBytes >= 16) {
+#pragma unroll
+        for (int q = 0; q < kBytes / 16; q++) {
+            const u32x4_g v = *(SKML_G(u32x4_g))(codes + b0 + 16 * q);
+            w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
         }
-        case 16: {
-            typedef uint32_t u32x4_g __attribute__((ext_vector_type(4)));
-            const u32x4_g v = *(SKML_G(u32x4_g))(codes + 2 * e0);
-            w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
-            break;
-        }
-        case 4: w[0] = *(SKML_G(uint32_t))(codes + e0 / 2); break;
-        case 2: w[0] = *(SKML_G(uint16_t))(codes + e0 / 4); break;
-        default: w[0] = codes[e0 / 8]; break;
+    } else if constexpr (kBytes == 8) {
+        const u32x2_g v = *(SKML_G(u32x2_g))(codes + b0);
+        w[0] = v.x; w[1] = v.y;
+    } else if constexpr (kBytes == 4) {
+        w[0] = *(SKML_G(uint32_t))(codes + b0);
+    } else if constexpr (kBytes == 2) {
+        w[0] = *(SKML_G(uint16_t))(codes + b0);
+    } else {
+        w[0] = codes[b0];
     }
 }
 #undef SKML_G
-__device__ __forceinline__ uint32_t code8_at(const uint32_t (&w)[4], int e, int bits) {
-    switch (bits) {
-        case 8: return (w[e >> 2] >> (8 * (e & 3))) & 255u;
-        case 16: return (w[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
-        case 4: return (w[0] >> (4 * e)) & 15u;
-        case 2: return (w[0] >> (2 * e)) & 3u;
-        default: return (w[0] >> e) & 1u;
-    }
+template <int BITS>
+__device__ __forceinline__ uint32_t code_occ_at(const uint32_t (&w)[occ_words<BITS>()], int e) {
+    return (w[(e * BITS) >> 5] >> ((e * BITS) & 31)) & ((1u << BITS) - 1u);
 }
 template <int BITS, bool PF>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PF ? SKML_OCC_WAVES : 8))) void k_decode_sum_occ(
@@ -572,18 +578,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PF ? SKML_O
         for (int b = threadIdx.x; b < h->bin_num; b += 256) lt[p * tab + b] = lut_value(h, sp, b);
     }
     __syncthreads();
-    constexpr int kW = BITS >= 4 ? BITS / 4 : 1;  // code words per payload per step
+    constexpr int kW = occ_words<BITS>();  // code words per payload per step
     const int64_t full = n / kOccPer, gstep = (int64_t)gridDim.x * 256;
     int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    uint32_t wn[kOccMaxP][4];
+    uint32_t wn[kOccMaxP][kW];
     if (PF) {
 #pragma unroll
         for (int q = 0; q < kOccMaxP; q++)
-            if (q < P && g < full) load_codes8(s_codes[q], g * kOccPer, BITS, wn[q]);
+            if (q < P && g < full) load_codes_occ<BITS>(s_codes[q], g * kOccPer, wn[q]);
     }
     typedef float f32x4 __attribute__((ext_vector_type(4)));
     for (; g < full; g += gstep) {
-        uint32_t w[kOccMaxP][4];
+        uint32_t w[kOccMaxP][kW];
         if (PF) {
 #pragma unroll
             for (int q = 0; q < kOccMaxP; q++)
@@ -592,12 +598,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PF ? SKML_O
             if (g + gstep < full) {
 #pragma unroll
                 for (int q = 0; q < kOccMaxP; q++)
-                    if (q < P) load_codes8(s_codes[q], (g + gstep) * kOccPer, BITS, wn[q]);
+                    if (q < P) load_codes_occ<BITS>(s_codes[q], (g + gstep) * kOccPer, wn[q]);
             }
         } else {
 #pragma unroll
             for (int q = 0; q < kOccMaxP; q++)
-                if (q < P) load_codes8(s_codes[q], g * kOccPer, BITS, w[q]);
+                if (q < P) load_codes_occ<BITS>(s_codes[q], g * kOccPer, w[q]);
         }
         double acc[kOccPer];
 #pragma unroll
@@ -607,7 +613,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PF ? SKML_O
             if (q >= P) break;
             const double* t = lt + q * tab;
 #pragma unroll
-            for (int e = 0; e < kOccPer; e++) acc[e] += t[code8_at(w[q], e, BITS)];
+            for (int e = 0; e < kOccPer; e++) acc[e] += t[code_occ_at<BITS>(w[q], e)];
         }
         f32x4* dst = reinterpret_cast<f32x4*>(out + g * kOccPer);
 #pragma unroll
@@ -617,7 +623,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PF ? SKML_O
             __builtin_nontemporal_store(o, dst + j);
         }
     }
-    if (blockIdx.x == 0 && threadIdx.x < kOccPer) {  // the last n % 8 elements
+    if (blockIdx.x == 0 && threadIdx.x < kOccPer) {  // the last n % kOccPer elements
         const int64_t e = full * kOccPer + threadIdx.x;
         if (e < n) {
             double a = 0.0;
