@@ -1813,18 +1813,31 @@ __global__ __launch_bounds__(256) void k_set_splits(uint8_t* payload, int64_t n,
 }
 
 // HeapQuantileSketch.getQuantiles' ranks (HeapQuantileSketch.java:305-320): rank_i = min((long)(n *
-// curFrac), n - 1) with curFrac += 1/bins accumulated in double, in order -- one thread, the same
+// curFrac), n - 1) with curFrac += 1/bins accumulated in double, in order (one lane), the same
 // IEEE double sequence as the JVM (built with -ffp-contract=off).  On the device so that a new n
 // (every sparse payload's nnz) costs no host upload and no synchronisation.
 __global__ __launch_bounds__(64) void k_set_ranks(int64_t n, int bins, int64_t* __restrict__ ranks) {
-    if (threadIdx.x != 0) return;
+    // lane 0 runs the dependent chain of additions (one v_add_f64 each) into LDS, 1,024 at a time;
+    // the wave then converts them in parallel (the double -> int64 conversion is the long part)
+    constexpr int kChunk = 1024;
+    __shared__ double fr[kChunk];
+    const int lane = threadIdx.x;
     const double step = 1.0 / bins;
     double frac = step;
-    for (int i = 0; i < bins - 1; i++) {
-        int64_t r = (int64_t)((double)n * frac);
-        if (r > n - 1) r = n - 1;
-        ranks[i] = r;
-        frac = frac + step;
+    for (int i0 = 0; i0 < bins - 1; i0 += kChunk) {
+        const int m = min(kChunk, bins - 1 - i0);
+        if (lane == 0)
+            for (int j = 0; j < m; j++) {
+                fr[j] = frac;
+                frac = frac + step;
+            }
+        __syncthreads();
+        for (int j = lane; j < m; j += 64) {
+            int64_t r = (int64_t)((double)n * fr[j]);
+            if (r > n - 1) r = n - 1;
+            ranks[i0 + j] = r;
+        }
+        __syncthreads();
     }
 }
 

@@ -561,13 +561,13 @@ static int resident_blocks(K kern, int threads) {
 }
 
 #ifndef SKML_COMPACT_PERSIST
-#define SKML_COMPACT_PERSIST 1  // 0: one tile per workgroup (A/B builds)
+#define SKML_COMPACT_PERSIST 0  // 1: the persistent form (A/B builds)
 #endif
-// Persistent form: a workgroup takes the next tile's ticket before its look-back and loads that
-// tile's first sub-tile while its stores drain, so no workgroup start, first-load latency or store
-// phase leaves the CU without loads in flight; the grid is what the CUs hold at once.  Tickets are
-// taken in order by running workgroups, and a workgroup waits only on lower tickets, so the
-// look-back always progresses.
+// One tile per workgroup.  The persistent form (SKML_COMPACT_PERSIST 1, A/B builds) takes the next
+// tile's ticket before its look-back and loads that tile's first sub-tile while its stores drain,
+// with the grid at what the CUs hold at once (tickets are taken in order by running workgroups and
+// a workgroup waits only on lower tickets, so the look-back always progresses); it measured 10-20
+// us slower per C3 encode (profiles/ab/r06_compact_persist.txt).
 __global__ __launch_bounds__(kSpThreads) __attribute__((amdgpu_waves_per_eu(3))) void k_compact_big(const float* __restrict__ x, int64_t dim,
                                                             int32_t* __restrict__ keys, float* __restrict__ vals,
                                                             uint64_t* status, unsigned* ticket, int64_t ntiles,
