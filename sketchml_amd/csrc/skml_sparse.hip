@@ -72,6 +72,12 @@ __device__ __forceinline__ uint64_t ld_status(const uint64_t* p) {
 __device__ __forceinline__ void st_status(uint64_t* p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// A count the host may be polling in coherent host memory (ctx_host_word): a system-scope store,
+// so it is not held in L2.  No release: the host only reads the value, and everything that reads
+// the compaction's output runs later on the same stream.
+__device__ __forceinline__ void put_count(int64_t* p, int64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 #ifndef SKML_LOOKBACK_ROWS
 #define SKML_LOOKBACK_ROWS 1  // predecessors per look-back step = 64 x this (A/B builds vary it)
@@ -417,7 +423,7 @@ __global__ __launch_bounds__(kSpThreads) void k_compact(const T* __restrict__ x,
         }
         if (lane == 0) {
             s_excl = excl;
-            if (tile == ntiles - 1) *nnz_out = (int64_t)(excl + tile_total);
+            if (tile == ntiles - 1) put_count(nnz_out, (int64_t)(excl + tile_total));
         }
     }
     __syncthreads();
@@ -633,7 +639,7 @@ __global__ __launch_bounds__(kSpThreads) __attribute__((amdgpu_waves_per_eu(3)))
             if (lane == 0) {
                 s_excl = excl;
                 sub_pre[kCbSub] = tile_total;
-                if (tile == ntiles - 1) *nnz_out = (int64_t)(excl + tile_total);
+                if (tile == ntiles - 1) put_count(nnz_out, (int64_t)(excl + tile_total));
             }
         }
         __syncthreads();
@@ -722,7 +728,11 @@ constexpr int kScanThreads = SKML_SCAN_THREADS, kScanPer = SKML_SCAN_PER;
 static_assert(kScanPer % 2 == 0, "16-byte loads of two entries");
 // Entry (i, k) at sums[k * ld + i * es]: [tiles][K] row-major (ld 1, es K) or one column of
 // tiles + 1 entries per k (ld tiles + 1, es 1: contiguous column reads).
+// PER entries per thread and pass: 2 x kScanPer when that covers a column in one pass (C3's
+// 13,108 partition tiles), else kScanPer.
+template <int PER>
 __global__ __launch_bounds__(kScanThreads) void k_scan_cols(uint64_t* sums, int64_t tiles, int64_t ld, int64_t es) {
+    constexpr int kScanPer = PER;
     __shared__ uint64_t sh[kScanThreads / 64];
     const int k = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
     uint64_t carry = 0;
@@ -770,12 +780,18 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_cols(uint64_t* sums, int6
     if (t == 0) sums[k * ld + tiles * es] = carry;
 }
 
+static void scan_cols_launch(hipStream_t st, uint64_t* sums, int64_t tiles, int K, int64_t ld, int64_t es) {
+    if (tiles > (int64_t)kScanThreads * kScanPer && tiles <= (int64_t)kScanThreads * kScanPer * 2)
+        hipLaunchKernelGGL(k_scan_cols<2 * kScanPer>, dim3(K), dim3(kScanThreads), 0, st, sums, tiles, ld, es);
+    else
+        hipLaunchKernelGGL(k_scan_cols<kScanPer>, dim3(K), dim3(kScanThreads), 0, st, sums, tiles, ld, es);
+}
 hipError_t launch_scan_cols(hipStream_t st, uint64_t* sums, int64_t tiles, int K) {
-    hipLaunchKernelGGL(k_scan_cols, dim3(K), dim3(kScanThreads), 0, st, sums, tiles, (int64_t)1, (int64_t)K);
+    scan_cols_launch(st, sums, tiles, K, (int64_t)1, (int64_t)K);
     return hipGetLastError();
 }
 hipError_t launch_scan_cols_major(hipStream_t st, uint64_t* sums, int64_t tiles, int K) {
-    hipLaunchKernelGGL(k_scan_cols, dim3(K), dim3(kScanThreads), 0, st, sums, tiles, tiles + 1, (int64_t)1);
+    scan_cols_launch(st, sums, tiles, K, tiles + 1, (int64_t)1);
     return hipGetLastError();
 }
 
@@ -815,6 +831,9 @@ __device__ __forceinline__ uint32_t few_field(uint64_t lo, uint64_t hi, int g) {
     return (uint32_t)(((g & 1) ? hi : lo) >> (16 * (g >> 1))) & 0xFFFFu;
 }
 
+// kPartTiles consecutive tiles per workgroup, their code loads issued together (one tile per
+// workgroup left the 2 KB-per-workgroup pass bound by workgroup dispatch: 26 us at C3).
+constexpr int kPartTiles = 4;
 __global__ __launch_bounds__(kSpThreads) void k_part_count(const uint8_t* __restrict__ qpayload, int64_t n,
                                                            const SpGroups* __restrict__ gp,
                                                            uint64_t* __restrict__ tile_counts,
@@ -827,51 +846,68 @@ __global__ __launch_bounds__(kSpThreads) void k_part_count(const uint8_t* __rest
     }
     if (gp->status) return;
     __shared__ int32_t E[kMaxGroups];
-    __shared__ uint32_t cnt[kMaxGroups];
-    __shared__ uint64_t wsum[kSpThreads / 64][2];
+    __shared__ uint32_t cnt[kPartTiles][kMaxGroups];
+    __shared__ uint64_t wsum[kPartTiles][kSpThreads / 64][2];
     const skml_dense_header* h = reinterpret_cast<const skml_dense_header*>(qpayload);
     const uint8_t* codes = qpayload + h->codes_offset;
     const int bits = h->code_bits, G = gp->G;
-    const int64_t base = (int64_t)blockIdx.x * kSpTile;
+    const int64_t tiles = (n + kSpTile - 1) / kSpTile;
+    const int64_t tile0 = (int64_t)blockIdx.x * kPartTiles;
+    const int t = threadIdx.x;
     if (G <= kFewGroups) {  // 8 consecutive elements per lane, counted in registers
         static_assert(kSpTile == 8 * kSpThreads, "one 8-element run per lane");
         const FewEdges fe = few_edges(gp, G);
-        const int t = threadIdx.x;
-        const int64_t i0 = base + 8 * t;
-        uint64_t acc = 0;
-        if (bits == 8 && i0 + 8 <= n && ((reinterpret_cast<uintptr_t>(codes) & 7) == 0)) {
-            const uint64_t w8 = *reinterpret_cast<const uint64_t*>(codes + i0);
+        const bool fast = bits == 8 && ((reinterpret_cast<uintptr_t>(codes) & 7) == 0);
+        uint64_t w8[kPartTiles];
 #pragma unroll
-            for (int k = 0; k < 8; k++) acc += 1ull << (8 * few_group(fe, (int32_t)((w8 >> (8 * k)) & 255u)));
-        } else {
-#pragma unroll
-            for (int k = 0; k < 8; k++)
-                if (i0 + k < n) acc += 1ull << (8 * few_group(fe, code_at(codes, i0 + k, bits)));
+        for (int k = 0; k < kPartTiles; k++) {
+            const int64_t i0 = (tile0 + k) * kSpTile + 8 * t;
+            w8[k] = fast && i0 + 8 <= n ? *reinterpret_cast<const uint64_t*>(codes + i0) : 0ull;
         }
-        uint64_t lo, hi;
-        few_wave_sum(acc, lo, hi);
-        if ((t & 63) == 0) {
-            wsum[t >> 6][0] = lo;
-            wsum[t >> 6][1] = hi;
+#pragma unroll
+        for (int k = 0; k < kPartTiles; k++) {
+            const int64_t i0 = (tile0 + k) * kSpTile + 8 * t;
+            uint64_t acc = 0;
+            if (fast && i0 + 8 <= n) {
+#pragma unroll
+                for (int e = 0; e < 8; e++) acc += 1ull << (8 * few_group(fe, (int32_t)((w8[k] >> (8 * e)) & 255u)));
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; e++)
+                    if (i0 + e < n) acc += 1ull << (8 * few_group(fe, code_at(codes, i0 + e, bits)));
+            }
+            uint64_t lo, hi;
+            few_wave_sum(acc, lo, hi);
+            if ((t & 63) == 0) {
+                wsum[k][t >> 6][0] = lo;
+                wsum[k][t >> 6][1] = hi;
+            }
         }
         __syncthreads();
-        if (t < G) {
-            uint32_t c = 0;
+        if (t < kPartTiles * G) {
+            const int k = t / G, g = t - k * G;
+            if (tile0 + k < tiles) {
+                uint32_t c = 0;
 #pragma unroll
-            for (int w = 0; w < kSpThreads / 64; w++) c += few_field(wsum[w][0], wsum[w][1], t);
-            tile_counts[(int64_t)t * (gridDim.x + 1) + blockIdx.x] = c;
+                for (int w = 0; w < kSpThreads / 64; w++) c += few_field(wsum[k][w][0], wsum[k][w][1], g);
+                tile_counts[(int64_t)g * (tiles + 1) + tile0 + k] = c;
+            }
         }
         return;
     }
     load_edges(gp, E);
-    for (int j = threadIdx.x; j < kMaxGroups; j += kSpThreads) cnt[j] = 0;
+    for (int j = t; j < kPartTiles * kMaxGroups; j += kSpThreads) cnt[j / kMaxGroups][j % kMaxGroups] = 0;
     __syncthreads();
-    for (int j = threadIdx.x; j < kSpTile; j += kSpThreads) {
-        const int64_t i = base + j;
-        if (i < n) atomicAdd(&cnt[group_of_bin(E, code_at(codes, i, bits))], 1u);
+    for (int k = 0; k < kPartTiles; k++)
+        for (int j = t; j < kSpTile; j += kSpThreads) {
+            const int64_t i = (tile0 + k) * kSpTile + j;
+            if (i < n) atomicAdd(&cnt[k][group_of_bin(E, code_at(codes, i, bits))], 1u);
+        }
+    __syncthreads();
+    for (int j = t; j < kPartTiles * G; j += kSpThreads) {
+        const int k = j / G, g = j - k * G;
+        if (tile0 + k < tiles) tile_counts[(int64_t)g * (tiles + 1) + tile0 + k] = cnt[k][g];
     }
-    __syncthreads();
-    for (int g = threadIdx.x; g < G; g += kSpThreads) tile_counts[(int64_t)g * (gridDim.x + 1) + blockIdx.x] = cnt[g];
 }
 
 hipError_t launch_part_count(hipStream_t st, const void* qpayload, int64_t n, const SpGroups* gp,
@@ -884,7 +920,7 @@ hipError_t launch_part_count(hipStream_t st, const void* qpayload, int64_t n, co
         }
         return n64 > 0 ? hipMemsetAsync(z64, 0, sizeof(uint64_t) * (size_t)n64, st) : hipSuccess;
     }
-    hipLaunchKernelGGL(k_part_count, dim3((unsigned)tiles), dim3(kSpThreads), 0, st,
+    hipLaunchKernelGGL(k_part_count, dim3((unsigned)((tiles + kPartTiles - 1) / kPartTiles)), dim3(kSpThreads), 0, st,
                        reinterpret_cast<const uint8_t*>(qpayload), n, gp, tile_counts, z32, n32, z64, n64);
     return hipGetLastError();
 }
@@ -1136,6 +1172,9 @@ constexpr int kMmBatch = SKML_MM_BATCH;  // elements per thread in flight (count
 #define SKML_BUCKET_BATCH 8
 #endif
 constexpr int kBucketBatch = SKML_BUCKET_BATCH;  // pairs per thread in flight in the bucket minima
+#ifndef SKML_BUCKET_VEC
+#define SKML_BUCKET_VEC 8  // narrow pairs: 16-byte loads per thread in flight (0: one pair per load)
+#endif
 
 // a group's MinMaxSketch shape, staged in LDS by the count pass
 // Unsigned division by a run-time d through a multiplier (the round-up method: exact for every
@@ -1770,6 +1809,25 @@ __global__ __launch_bounds__(kMmThreads) void k_mm_bucket(const void* __restrict
         for (int j = threadIdx.x; j < kMmBucketCells; j += kMmThreads) cm[j] = ~0u;
         __syncthreads();
         constexpr uint32_t kLo = (uint32_t)(kMmBucketCells - 1);
+#if SKML_BUCKET_VEC
+        // 16-byte loads: a bucket's range [p0, p1) is whole 32-pair lines (bucket_base is the scan
+        // of mm_pad(count, true) per (tile, bucket)), so four pairs per load stay in range
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4* pv = reinterpret_cast<const u32x4*>(pairs + p0);
+        const uint64_t nv = (p1 - p0) / 4;
+        constexpr int kV = SKML_BUCKET_VEC;  // 16-byte loads per thread in flight
+        for (uint64_t q = threadIdx.x; q < nv; q += kV * kMmThreads) {
+            u32x4 v[kV];
+#pragma unroll
+            for (int u = 0; u < kV; u++)
+                v[u] = q + u * kMmThreads < nv ? pv[q + u * kMmThreads] : u32x4{kMmNoPair32, kMmNoPair32, kMmNoPair32, kMmNoPair32};
+#pragma unroll
+            for (int u = 0; u < kV; u++)
+#pragma unroll
+                for (int e = 0; e < 4; e++)
+                    if (v[u][e] != kMmNoPair32) atomicMin(&cm[v[u][e] & kLo], v[u][e] >> kMmBucketBits);
+        }
+#else
         constexpr int kB = 2 * kBucketBatch;  // half the bytes per pair: twice the pairs in flight
         for (uint64_t p = p0 + threadIdx.x; p < p1; p += kB * kMmThreads) {
             uint32_t v[kB];
@@ -1779,6 +1837,7 @@ __global__ __launch_bounds__(kMmThreads) void k_mm_bucket(const void* __restrict
             for (int u = 0; u < kB; u++)
                 if (v[u] != kMmNoPair32) atomicMin(&cm[v[u] & kLo], v[u] >> kMmBucketBits);
         }
+#endif
         __syncthreads();
         for (int j = threadIdx.x; j < kMmBucketCells && cell0 + j < ncells; j += kMmThreads) {
             const uint32_t v = cm[j];
@@ -2246,6 +2305,30 @@ __global__ __launch_bounds__(64) void k_sp_finalize(SpGroups* __restrict__ gp, c
             gp->fb[g] = gp->fb[g + 1];
             gp->db[g] = gp->db[g + 1];
         }
+}
+
+// The encode's one read-back, written by the device into the context's coherent host buffer: the
+// quantizer's header and splits (qh bytes) at 0, the group table at o_pg, then `seq` at `flag`
+// once every byte before it is visible (the host polls the flag instead of two copies and a
+// stream synchronisation).  One wave: its stores complete before the system-scope release.
+__global__ __launch_bounds__(64) void k_sp_publish(const uint64_t* __restrict__ qpayload, int64_t qh_words,
+                                                   const uint64_t* __restrict__ gp, int64_t gp_words,
+                                                   uint64_t* __restrict__ host, int64_t o_pg_words,
+                                                   int64_t* __restrict__ flag, int64_t seq) {
+    const int lane = threadIdx.x;
+    for (int64_t i = lane; i < qh_words; i += 64)
+        __hip_atomic_store(host + i, qpayload[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    for (int64_t i = lane; i < gp_words; i += 64)
+        __hip_atomic_store(host + o_pg_words + i, gp[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    if (lane == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+hipError_t launch_sp_publish(hipStream_t st, const void* qpayload, size_t qh, const SpGroups* gp, void* host,
+                             size_t o_pg, int64_t* flag, int64_t seq) {
+    hipLaunchKernelGGL(k_sp_publish, dim3(1), dim3(64), 0, st, static_cast<const uint64_t*>(qpayload),
+                       (int64_t)(qh / 8), reinterpret_cast<const uint64_t*>(gp), (int64_t)(sizeof(SpGroups) / 8),
+                       static_cast<uint64_t*>(host), (int64_t)(o_pg / 8), flag, seq);
+    return hipGetLastError();
 }
 
 hipError_t launch_sp_plan_edges(hipStream_t st, const void* qpayload, const SpInit& init, SpGroups* gp) {
