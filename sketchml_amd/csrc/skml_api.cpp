@@ -84,9 +84,6 @@ struct skml_ctx {
     // one coherent, device-mapped host word: a kernel publishes a count there (the compaction's
     // nnz) and the host polls it instead of a copy + stream synchronisation
     int64_t* hword = nullptr;
-    void* hpub = nullptr;  // the sparse encode's read-back (k_sp_publish), grow-only
-    size_t hpub_cap = 0;
-    int64_t pub_seq = 0;
     // host-memory entry points (skml_dense_encode_host_f32 / _decode_host_f32): device copies of
     // the input / payload, two pinned staging buffers and a pool of host copy threads
     void* hx = nullptr;
@@ -411,7 +408,6 @@ int skml_ctx_destroy(skml_ctx* c) {
         if (c->scratch[i]) (void)hipFree(c->scratch[i]);
     if (c->pinned) (void)hipHostFree(c->pinned);
     if (c->hword) (void)hipHostFree(c->hword);
-    if (c->hpub) (void)hipHostFree(c->hpub);
     destroy_host_path(c);
     if (c->own_stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -1946,24 +1942,6 @@ int64_t* ctx_host_word(skml_ctx* c) {
     }
     return c->hword;
 }
-void* ctx_host_pub(skml_ctx* c, size_t bytes) {
-    if (bytes > c->hpub_cap) {
-        if (c->hpub) {
-            (void)hipStreamSynchronize(c->stream);
-            (void)hipHostFree(c->hpub);
-        }
-        c->hpub = nullptr;
-        c->hpub_cap = 0;
-        const size_t cap = align_up(bytes + 4096, 4096);
-        if (hipHostMalloc(&c->hpub, cap, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
-            (void)hipGetLastError();
-            return nullptr;
-        }
-        c->hpub_cap = cap;
-    }
-    return c->hpub;
-}
-int64_t ctx_next_seq(skml_ctx* c) { return ++c->pub_seq; }
 void* ctx_pinned(skml_ctx* c, size_t bytes) {
     if (bytes > c->pinned_cap) {
         if (c->pinned) {

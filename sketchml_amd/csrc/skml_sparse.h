@@ -67,9 +67,6 @@ hipError_t launch_sp_plan_edges(hipStream_t st, const void* qpayload, const SpIn
 hipError_t launch_sp_plan_groups(hipStream_t st, SpGroups* gp, const uint64_t* sizes, int64_t stride);
 hipError_t launch_sp_plan_delta(hipStream_t st, SpGroups* gp, const uint32_t* hist, const uint32_t* err);
 hipError_t launch_sp_finalize(hipStream_t st, SpGroups* gp, const uint64_t* tot);
-// qpayload[0, qh) and *gp into coherent host memory at 0 and o_pg (multiples of 8), then seq at flag
-hipError_t launch_sp_publish(hipStream_t st, const void* qpayload, size_t qh, const SpGroups* gp, void* host,
-                             size_t o_pg, int64_t* flag, int64_t seq);
 // Zero the stream words the writer ORs into (every tile's first and last word, and the word
 // after the end) from the scanned [tiles + 1][2] tile sums.
 hipError_t launch_sp_zero_edges(hipStream_t st, const uint64_t* tile_base, int64_t tiles, const SpGroups* gp,
@@ -82,6 +79,8 @@ hipError_t launch_compact64(hipStream_t st, const double* x, int64_t dim, int32_
                             uint64_t* status, unsigned* ticket, int64_t* nnz_out);
 // Exclusive scan, in place, of each of K columns of a [tiles][K] u64 table; totals -> row `tiles`.
 hipError_t launch_scan_cols(hipStream_t st, uint64_t* sums, int64_t tiles, int K);
+// launch_scan_cols on 256-thread workgroups (a kernel queued beside a full chip)
+hipError_t launch_scan_cols_small(hipStream_t st, uint64_t* sums, int64_t tiles, int K);
 // The same over K columns of tiles + 1 entries each, column k at sums + k * (tiles + 1).
 hipError_t launch_scan_cols_major(hipStream_t st, uint64_t* sums, int64_t tiles, int K);
 // FSketchUtils.partition: per-tile group counts (column-major: group g's column of tiles + 1 at
@@ -395,10 +394,6 @@ void* ctx_scratch(skml_ctx* c, int slot, size_t bytes);
 void* ctx_pinned(skml_ctx* c, size_t bytes);
 // the context's coherent, device-mapped host word (nullptr if it cannot be allocated)
 int64_t* ctx_host_word(skml_ctx* c);
-// grow-only coherent, device-mapped host buffer of at least `bytes` (nullptr on failure), and the
-// context's next publication sequence number (> 0)
-void* ctx_host_pub(skml_ctx* c, size_t bytes);
-int64_t ctx_next_seq(skml_ctx* c);
 int set_error(int code, const char* msg);
 bool ctx_timing(skml_ctx* c);
 

@@ -728,11 +728,11 @@ constexpr int kScanThreads = SKML_SCAN_THREADS, kScanPer = SKML_SCAN_PER;
 static_assert(kScanPer % 2 == 0, "16-byte loads of two entries");
 // Entry (i, k) at sums[k * ld + i * es]: [tiles][K] row-major (ld 1, es K) or one column of
 // tiles + 1 entries per k (ld tiles + 1, es 1: contiguous column reads).
-// PER entries per thread and pass: 2 x kScanPer when that covers a column in one pass (C3's
-// 13,108 partition tiles), else kScanPer.
-template <int PER>
-__global__ __launch_bounds__(kScanThreads) void k_scan_cols(uint64_t* sums, int64_t tiles, int64_t ld, int64_t es) {
-    constexpr int kScanPer = PER;
+// THREADS x PER entries per pass (kScanThreads x kScanPer by default; the sparse encode's side
+// chain takes 256-thread workgroups, launch_scan_cols_small)
+template <int THREADS = kScanThreads, int PER = kScanPer>
+__global__ __launch_bounds__(THREADS) void k_scan_cols(uint64_t* sums, int64_t tiles, int64_t ld, int64_t es) {
+    constexpr int kScanThreads = THREADS, kScanPer = PER;
     __shared__ uint64_t sh[kScanThreads / 64];
     const int k = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
     uint64_t carry = 0;
@@ -780,18 +780,19 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_cols(uint64_t* sums, int6
     if (t == 0) sums[k * ld + tiles * es] = carry;
 }
 
-static void scan_cols_launch(hipStream_t st, uint64_t* sums, int64_t tiles, int K, int64_t ld, int64_t es) {
-    if (tiles > (int64_t)kScanThreads * kScanPer && tiles <= (int64_t)kScanThreads * kScanPer * 2)
-        hipLaunchKernelGGL(k_scan_cols<2 * kScanPer>, dim3(K), dim3(kScanThreads), 0, st, sums, tiles, ld, es);
-    else
-        hipLaunchKernelGGL(k_scan_cols<kScanPer>, dim3(K), dim3(kScanThreads), 0, st, sums, tiles, ld, es);
-}
 hipError_t launch_scan_cols(hipStream_t st, uint64_t* sums, int64_t tiles, int K) {
-    scan_cols_launch(st, sums, tiles, K, (int64_t)1, (int64_t)K);
+    hipLaunchKernelGGL(k_scan_cols<>, dim3(K), dim3(kScanThreads), 0, st, sums, tiles, (int64_t)1, (int64_t)K);
     return hipGetLastError();
 }
 hipError_t launch_scan_cols_major(hipStream_t st, uint64_t* sums, int64_t tiles, int K) {
-    scan_cols_launch(st, sums, tiles, K, tiles + 1, (int64_t)1);
+    hipLaunchKernelGGL(k_scan_cols<>, dim3(K), dim3(kScanThreads), 0, st, sums, tiles, tiles + 1, (int64_t)1);
+    return hipGetLastError();
+}
+// The same scan on 256-thread workgroups: in the sparse encode's side chain a 1,024-thread
+// workgroup waits for a whole CU's wave slots beside the MinMax scatter (4-5 us alone, 57-70 us
+// there), which pushed the DeltaAdaptive writer onto the bucket minima.
+hipError_t launch_scan_cols_small(hipStream_t st, uint64_t* sums, int64_t tiles, int K) {
+    hipLaunchKernelGGL((k_scan_cols<256, 32>), dim3(K), dim3(256), 0, st, sums, tiles, (int64_t)1, (int64_t)K);
     return hipGetLastError();
 }
 
@@ -1172,9 +1173,6 @@ constexpr int kMmBatch = SKML_MM_BATCH;  // elements per thread in flight (count
 #define SKML_BUCKET_BATCH 8
 #endif
 constexpr int kBucketBatch = SKML_BUCKET_BATCH;  // pairs per thread in flight in the bucket minima
-#ifndef SKML_BUCKET_VEC
-#define SKML_BUCKET_VEC 8  // narrow pairs: 16-byte loads per thread in flight (0: one pair per load)
-#endif
 
 // a group's MinMaxSketch shape, staged in LDS by the count pass
 // Unsigned division by a run-time d through a multiplier (the round-up method: exact for every
@@ -1735,8 +1733,12 @@ __global__ __launch_bounds__(T) void k_mm_scatter_staged(const int32_t* __restri
 #define SKML_STAGE_THREADS 512
 #endif
 constexpr int kStageThreads = SKML_STAGE_THREADS;
+#ifndef SKML_STAGE_LDS_MIN
+#define SKML_STAGE_LDS_MIN 0  // A/B builds: a larger LDS request, i.e. fewer scatter workgroups per CU
+#endif
 inline size_t staged_lds(int nbuckets) {
-    return (sizeof(uint64_t) + sizeof(uint16_t)) * 8 * kStageThreads + 16 * (size_t)nbuckets + 4;
+    const size_t need = (sizeof(uint64_t) + sizeof(uint16_t)) * 8 * kStageThreads + 16 * (size_t)nbuckets + 4;
+    return need > (size_t)SKML_STAGE_LDS_MIN ? need : (size_t)SKML_STAGE_LDS_MIN;
 }
 
 bool mm_scatter_staged(bool cells, bool reserved, int nbuckets) {
@@ -1809,25 +1811,6 @@ __global__ __launch_bounds__(kMmThreads) void k_mm_bucket(const void* __restrict
         for (int j = threadIdx.x; j < kMmBucketCells; j += kMmThreads) cm[j] = ~0u;
         __syncthreads();
         constexpr uint32_t kLo = (uint32_t)(kMmBucketCells - 1);
-#if SKML_BUCKET_VEC
-        // 16-byte loads: a bucket's range [p0, p1) is whole 32-pair lines (bucket_base is the scan
-        // of mm_pad(count, true) per (tile, bucket)), so four pairs per load stay in range
-        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-        const u32x4* pv = reinterpret_cast<const u32x4*>(pairs + p0);
-        const uint64_t nv = (p1 - p0) / 4;
-        constexpr int kV = SKML_BUCKET_VEC;  // 16-byte loads per thread in flight
-        for (uint64_t q = threadIdx.x; q < nv; q += kV * kMmThreads) {
-            u32x4 v[kV];
-#pragma unroll
-            for (int u = 0; u < kV; u++)
-                v[u] = q + u * kMmThreads < nv ? pv[q + u * kMmThreads] : u32x4{kMmNoPair32, kMmNoPair32, kMmNoPair32, kMmNoPair32};
-#pragma unroll
-            for (int u = 0; u < kV; u++)
-#pragma unroll
-                for (int e = 0; e < 4; e++)
-                    if (v[u][e] != kMmNoPair32) atomicMin(&cm[v[u][e] & kLo], v[u][e] >> kMmBucketBits);
-        }
-#else
         constexpr int kB = 2 * kBucketBatch;  // half the bytes per pair: twice the pairs in flight
         for (uint64_t p = p0 + threadIdx.x; p < p1; p += kB * kMmThreads) {
             uint32_t v[kB];
@@ -1837,7 +1820,6 @@ __global__ __launch_bounds__(kMmThreads) void k_mm_bucket(const void* __restrict
             for (int u = 0; u < kB; u++)
                 if (v[u] != kMmNoPair32) atomicMin(&cm[v[u] & kLo], v[u] >> kMmBucketBits);
         }
-#endif
         __syncthreads();
         for (int j = threadIdx.x; j < kMmBucketCells && cell0 + j < ncells; j += kMmThreads) {
             const uint32_t v = cm[j];
@@ -2305,30 +2287,6 @@ __global__ __launch_bounds__(64) void k_sp_finalize(SpGroups* __restrict__ gp, c
             gp->fb[g] = gp->fb[g + 1];
             gp->db[g] = gp->db[g + 1];
         }
-}
-
-// The encode's one read-back, written by the device into the context's coherent host buffer: the
-// quantizer's header and splits (qh bytes) at 0, the group table at o_pg, then `seq` at `flag`
-// once every byte before it is visible (the host polls the flag instead of two copies and a
-// stream synchronisation).  One wave: its stores complete before the system-scope release.
-__global__ __launch_bounds__(64) void k_sp_publish(const uint64_t* __restrict__ qpayload, int64_t qh_words,
-                                                   const uint64_t* __restrict__ gp, int64_t gp_words,
-                                                   uint64_t* __restrict__ host, int64_t o_pg_words,
-                                                   int64_t* __restrict__ flag, int64_t seq) {
-    const int lane = threadIdx.x;
-    for (int64_t i = lane; i < qh_words; i += 64)
-        __hip_atomic_store(host + i, qpayload[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    for (int64_t i = lane; i < gp_words; i += 64)
-        __hip_atomic_store(host + o_pg_words + i, gp[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    if (lane == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-hipError_t launch_sp_publish(hipStream_t st, const void* qpayload, size_t qh, const SpGroups* gp, void* host,
-                             size_t o_pg, int64_t* flag, int64_t seq) {
-    hipLaunchKernelGGL(k_sp_publish, dim3(1), dim3(64), 0, st, static_cast<const uint64_t*>(qpayload),
-                       (int64_t)(qh / 8), reinterpret_cast<const uint64_t*>(gp), (int64_t)(sizeof(SpGroups) / 8),
-                       static_cast<uint64_t*>(host), (int64_t)(o_pg / 8), flag, seq);
-    return hipGetLastError();
 }
 
 hipError_t launch_sp_plan_edges(hipStream_t st, const void* qpayload, const SpInit& init, SpGroups* gp) {

@@ -373,28 +373,23 @@ int sync_to_host(skml_ctx* c, void* dst, const void* src, size_t bytes) {
     return SKML_OK;
 }
 
-// Exclusive column scans of a [tiles][K] table; column totals copied to `totals` (host).
-// Spin on a word in the context's coherent host memory until a kernel of this stream publishes
-// it: want >= 0 waits for that value, want < 0 for any value >= 0 (*out gets it).  The stream is
-// checked every few thousand polls, so a failed launch cannot hang the caller.
-int wait_host_word(skml_ctx* c, const int64_t* word, int64_t want, int64_t* out) {
+// Spin on the context's coherent host word until a kernel of this stream publishes a count >= 0
+// there.  The stream is checked every few thousand polls, so a failed launch cannot hang the caller.
+int wait_host_count(skml_ctx* c, const int64_t* word, int64_t* out) {
     const volatile int64_t* w = word;
     hipStream_t st = ctx_stream(c);
-    auto ready = [&](int64_t v) { return want >= 0 ? v == want : v >= 0; };
     for (uint64_t k = 1;; k++) {
         const int64_t v = *w;
-        if (ready(v)) {
-            std::atomic_thread_fence(std::memory_order_acquire);  // the published bytes after the flag
-            if (out) *out = v;
+        if (v >= 0) {
+            *out = v;
             return SKML_OK;
         }
         if ((k & 4095) == 0) {
             const hipError_t e = hipStreamQuery(st);
             if (e == hipSuccess) {  // the stream has drained: the publishing store is visible now
                 const int64_t v2 = *w;
-                if (!ready(v2)) return sfail(SKML_E_HIP, "a kernel did not publish its result");
-                std::atomic_thread_fence(std::memory_order_acquire);
-                if (out) *out = v2;
+                if (v2 < 0) return sfail(SKML_E_HIP, "the compaction did not publish its count");
+                *out = v2;
                 return SKML_OK;
             }
             if (e != hipErrorNotReady) return sfail(SKML_E_HIP, "stream failed: %s", hipGetErrorString(e));
@@ -403,6 +398,7 @@ int wait_host_word(skml_ctx* c, const int64_t* word, int64_t want, int64_t* out)
     }
 }
 
+// Exclusive column scans of a [tiles][K] table; column totals copied to `totals` (host).
 int scan_tiles(skml_ctx* c, uint64_t* sums, int64_t tiles, int K, uint64_t* totals) {
     SP_HIP(launch_scan_cols(ctx_stream(c), sums, tiles, K));
     if (totals) return sync_to_host(c, totals, sums + tiles * K, sizeof(uint64_t) * (size_t)K);
@@ -424,7 +420,7 @@ int encode_delta_device(skml_ctx* c, hipStream_t st, SpGroups* g_dev, const int3
     if (!ts) return sfail(SKML_E_OOM, "tile sums");
     SP_HIP(launch_sp_plan_delta(st, g_dev, hist, err));
     SP_HIP(launch_delta_lens(st, need, n, g_dev, ts));
-    SP_HIP(launch_scan_cols(st, ts, tiles, 2));
+    SP_HIP(launch_scan_cols_small(st, ts, tiles, 2));
     SP_HIP(launch_sp_zero_edges(st, ts, tiles, g_dev, fw, dw));
     SP_HIP(launch_delta_write(st, gk, need, n, g_dev, ts, fw, dw));
     SP_HIP(launch_sp_finalize(st, g_dev, ts + tiles * 2));
@@ -568,43 +564,30 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const void* vals, bool f64, int6
     // disjoint fields of the group table and disjoint buffers; the main stream joins before the
     // read-back.  (Forking before the count pass instead, with the deltas and histogram computed
     // on the side, overlapped the two VALU-bound passes and was slower.) ----
-    // The MinMax chain is queued before the side chain's launches, so the caller's stream never
-    // waits on the host while those are issued (a 7 us gap after k_group_prep when it came second).
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     hipStream_t ds = st;
     if (nnz > 0 && ctx_side_fork(c, &side, &ev_fork, &ev_join) == SKML_OK) {
         SP_TRY(hipEventRecord(ev_fork, st));
+        SP_TRY(hipStreamWaitEvent(side, ev_fork, 0));
         ds = side;
     } else {
         side = nullptr;
     }
+    if (int e = encode_delta_device(c, ds, s->g_dev, gk, need, nnz, hist, err, s->flag_words, s->delta_words))
+        return bail(e);
+    if (side) SP_TRY(hipEventRecord(ev_join, side));
     SP_TRY(launch_scan_cols(st, bucket, nbuckets, 1));
     SP_TRY(launch_mm_scatter(st, gk, gb, nnz, s->g_dev, bucket, cursor, nbuckets, pairs, cellbuf, tile_off));
     SP_TRY(launch_mm_bucket(st, pairs, bucket, nbuckets, s->g_dev, s->tables, s->tnar));
-    if (side) SP_TRY(hipStreamWaitEvent(side, ev_fork, 0));
-    if (int e = encode_delta_device(c, ds, s->g_dev, gk, need, nnz, hist, err, s->flag_words, s->delta_words))
-        return bail(e);
-    if (side) {
-        SP_TRY(hipEventRecord(ev_join, side));
-        SP_TRY(hipStreamWaitEvent(st, ev_join, 0));
-    }
+    if (side) SP_TRY(hipStreamWaitEvent(st, ev_join, 0));
     // ---- 5. the one read-back: quantizer header and splits, group table ----
-    // (k_sp_publish writes both into coherent host memory and raises a flag; the host spins on it)
     const size_t qh = kHeaderBytes + sizeof(double) * (size_t)(p->bin_num - 1);
-    const size_t o_pg = align_up(qh, 256), o_flag = align_up(o_pg + sizeof(SpGroups), 256);
-    uint8_t* pin = static_cast<uint8_t*>(ctx_host_pub(c, o_flag + 64));
-    if (pin) {
-        int64_t* flag = reinterpret_cast<int64_t*>(pin + o_flag);
-        const int64_t seq = ctx_next_seq(c);
-        SP_TRY(launch_sp_publish(st, s->qpayload, qh, s->g_dev, pin, o_pg, flag, seq));
-        if (int e = wait_host_word(c, flag, seq, nullptr)) return bail(e);
-    } else {  // no coherent host buffer: copies into pinned staging and a synchronisation
-        pin = static_cast<uint8_t*>(ctx_pinned(c, o_pg + sizeof(SpGroups)));
-        if (!pin) return bail(sfail(SKML_E_OOM, "pinned staging"));
-        SP_TRY(hipMemcpyAsync(pin, s->qpayload, qh, hipMemcpyDeviceToHost, st));
-        SP_TRY(hipMemcpyAsync(pin + o_pg, s->g_dev, sizeof(SpGroups), hipMemcpyDeviceToHost, st));
-        SP_TRY(hipStreamSynchronize(st));
-    }
+    const size_t o_pg = align_up(qh, 256);
+    uint8_t* pin = static_cast<uint8_t*>(ctx_pinned(c, o_pg + sizeof(SpGroups)));
+    if (!pin) return bail(sfail(SKML_E_OOM, "pinned staging"));
+    SP_TRY(hipMemcpyAsync(pin, s->qpayload, qh, hipMemcpyDeviceToHost, st));
+    SP_TRY(hipMemcpyAsync(pin + o_pg, s->g_dev, sizeof(SpGroups), hipMemcpyDeviceToHost, st));
+    SP_TRY(hipStreamSynchronize(st));
 #undef SP_TRY
     std::memcpy(&s->hdr, pin, sizeof(skml_dense_header));
     std::memcpy(&s->g, pin + o_pg, sizeof(SpGroups));
@@ -837,7 +820,7 @@ int compact_any(skml_ctx* c, const T* dense, int64_t dim, int32_t* keys, T* vals
     int64_t* dst = hw ? hw : nnz_dev;
     if constexpr (sizeof(T) == 8) SP_HIP(launch_compact64(st, dense, dim, keys, vals, status, ticket, dst));
     else SP_HIP(launch_compact(st, dense, dim, keys, vals, status, ticket, dst));
-    if (hw) return wait_host_word(c, hw, -1, nnz_out);
+    if (hw) return wait_host_count(c, hw, nnz_out);
     return sync_to_host(c, nnz_out, nnz_dev, sizeof(int64_t));
 }
 }  // namespace
