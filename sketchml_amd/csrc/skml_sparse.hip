@@ -1733,12 +1733,8 @@ __global__ __launch_bounds__(T) void k_mm_scatter_staged(const int32_t* __restri
 #define SKML_STAGE_THREADS 512
 #endif
 constexpr int kStageThreads = SKML_STAGE_THREADS;
-#ifndef SKML_STAGE_LDS_MIN
-#define SKML_STAGE_LDS_MIN 0  // A/B builds: a larger LDS request, i.e. fewer scatter workgroups per CU
-#endif
 inline size_t staged_lds(int nbuckets) {
-    const size_t need = (sizeof(uint64_t) + sizeof(uint16_t)) * 8 * kStageThreads + 16 * (size_t)nbuckets + 4;
-    return need > (size_t)SKML_STAGE_LDS_MIN ? need : (size_t)SKML_STAGE_LDS_MIN;
+    return (sizeof(uint64_t) + sizeof(uint16_t)) * 8 * kStageThreads + 16 * (size_t)nbuckets + 4;
 }
 
 bool mm_scatter_staged(bool cells, bool reserved, int nbuckets) {
