@@ -1184,10 +1184,15 @@ int skml_dense_decode_sum_f32(skml_ctx* c, const void* payloads, int32_t P, size
     HIP_TRY(hipSetDevice(c->device));
     // Gradient.sum adds gradients of one dimension (ml/gradient/Gradient.scala:44-49): every
     // payload must be a finished dense payload of exactly n codes that fits its stride.
+    // (into the context's pinned staging: a strided copy into pageable host memory returned a wrong
+    // second row on some boxes, profiles/r06z_gpu_tests_first.log)
     skml_dense_header h[16];
-    HIP_TRY(hipMemcpy2DAsync(h, sizeof(skml_dense_header), payloads, stride, sizeof(skml_dense_header), (size_t)P,
+    auto* hp = static_cast<skml_dense_header*>(ctx_pinned(c, sizeof(skml_dense_header) * (size_t)P));
+    if (!hp) return fail(SKML_E_OOM, "pinned staging");
+    HIP_TRY(hipMemcpy2DAsync(hp, sizeof(skml_dense_header), payloads, stride, sizeof(skml_dense_header), (size_t)P,
                              hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    std::memcpy(h, hp, sizeof(skml_dense_header) * (size_t)P);
     for (int p = 0; p < P; p++) {
         if (h[p].magic != SKML_DENSE_MAGIC) return fail(SKML_E_STATE, "payload %d is not a dense payload", p);
         if (h[p].status == SKML_E_NAN) return fail(SKML_E_NAN, "payload %d: Encounter NaN value", p);
