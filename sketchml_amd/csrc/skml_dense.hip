@@ -518,7 +518,12 @@ __global__ __launch_bounds__(256) void k_decode_sum(const uint8_t* __restrict__ 
 // P x bins doubles of dynamic LDS instead of a 32 KB array, and the next step's codes are loaded
 // before this step's lookups.
 #ifndef SKML_OCC_WAVES
-#define SKML_OCC_WAVES 4  // waves per SIMD of the prefetching form (4 against 6 and 8: profiles/ab/r06_occ_waves.txt)
+#define SKML_OCC_WAVES 4  // waves per SIMD of the prefetching form, 8- and 16-bit codes (4 against 6 and 8: profiles/ab/r06_occ_waves.txt)
+#endif
+#ifndef SKML_OCC_WAVES_NARROW
+// the same for 1-, 2- and 4-bit codes: a step then loads 1-4 bytes per payload and lane, so the
+// codes need more waves in flight (C5's 2-bit sum ran 154 us at 6 and 253 us at 4, profiles/ab/r06_occ_narrow.txt)
+#define SKML_OCC_WAVES_NARROW 6
 #endif
 #ifndef SKML_OCC_PER
 #define SKML_OCC_PER 8  // elements per lane and step (A/B builds: 16)
@@ -565,7 +570,7 @@ __device__ __forceinline__ uint32_t code_occ_at(const uint32_t (&w)[occ_words<BI
     return (w[(e * BITS) >> 5] >> ((e * BITS) & 31)) & ((1u << BITS) - 1u);
 }
 template <int BITS, bool PF>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PF ? SKML_OCC_WAVES : 8))) void k_decode_sum_occ(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PF ? (BITS >= 8 ? SKML_OCC_WAVES : SKML_OCC_WAVES_NARROW) : 8))) void k_decode_sum_occ(
     const uint8_t* __restrict__ payloads, int P, size_t stride, float* __restrict__ out, int64_t n, double scale,
     int tab) {
     extern __shared__ double lt[];  // P tables of `tab` doubles
