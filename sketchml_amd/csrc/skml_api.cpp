@@ -220,7 +220,11 @@ int ensure_ws(skml_ctx* ctx, int64_t chunks, Workspace* w) {
         ctx->ws = nullptr;
         size_t cap = need + need / 4;
         HIP_TRY(hipMalloc(&ctx->ws, cap));
-        HIP_TRY(hipMemset(ctx->ws, 0, 256));
+        // the fused summary's arrival counter starts at 0; zeroed on the context's own stream: a
+        // hipMemset goes to the null stream, which a non-blocking stream (the batch encode's side
+        // lane) does not wait for, so a fresh side workspace could be counted on before it was
+        // zeroed and the summary skipped (a payload without a header, tests/test_gpu_configs.py C4)
+        HIP_TRY(hipMemsetAsync(ctx->ws, 0, 256, ctx->stream));
         ctx->ws_cap = cap;
     }
     ws_layout(chunks, w, (char*)ctx->ws);
@@ -1184,15 +1188,10 @@ int skml_dense_decode_sum_f32(skml_ctx* c, const void* payloads, int32_t P, size
     HIP_TRY(hipSetDevice(c->device));
     // Gradient.sum adds gradients of one dimension (ml/gradient/Gradient.scala:44-49): every
     // payload must be a finished dense payload of exactly n codes that fits its stride.
-    // (into the context's pinned staging: a strided copy into pageable host memory returned a wrong
-    // second row on some boxes, profiles/r06z_gpu_tests_first.log)
     skml_dense_header h[16];
-    auto* hp = static_cast<skml_dense_header*>(ctx_pinned(c, sizeof(skml_dense_header) * (size_t)P));
-    if (!hp) return fail(SKML_E_OOM, "pinned staging");
-    HIP_TRY(hipMemcpy2DAsync(hp, sizeof(skml_dense_header), payloads, stride, sizeof(skml_dense_header), (size_t)P,
+    HIP_TRY(hipMemcpy2DAsync(h, sizeof(skml_dense_header), payloads, stride, sizeof(skml_dense_header), (size_t)P,
                              hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    std::memcpy(h, hp, sizeof(skml_dense_header) * (size_t)P);
     for (int p = 0; p < P; p++) {
         if (h[p].magic != SKML_DENSE_MAGIC) return fail(SKML_E_STATE, "payload %d is not a dense payload", p);
         if (h[p].status == SKML_E_NAN) return fail(SKML_E_NAN, "payload %d: Encounter NaN value", p);

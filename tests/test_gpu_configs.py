@@ -167,6 +167,14 @@ def test_c4_eight_buckets_batch_rccl_decode_sum(gpu):
     finally:
         comm.close()
     del xs
+    # the gathered layout first: every rank's slot a byte-identical copy of its payload
+    for r in range(P):
+        src, dst = pls[r][:nb], allp[r * nb:(r + 1) * nb]
+        if not torch.equal(src, dst):
+            magic_src = int(src[:4].cpu().view(torch.int32)[0])
+            magic_dst = int(dst[:4].cpu().view(torch.int32)[0])
+            raise AssertionError(f"slot {r} differs from payload {r} after the all-gather "
+                                 f"(payload magic {magic_src:#x}, slot magic {magic_dst:#x})")
     out = torch.empty(n, dtype=torch.float32, device="cuda")
     assert L.lib.skml_dense_decode_sum_f32(ctx.handle, C.c_void_p(allp.data_ptr()), P, nb,
                                            C.c_void_p(out.data_ptr()), n, 1.0 / P) == 0, L.last_error()
