@@ -4556,7 +4556,9 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_merge(const int32_t* __restri
 // scattered words per instruction).  Values restores hold the bins as 16-bit slots (checked
 // against nq on load: a bin outside quantValues flags the input, as rs_value does), so `ord` fits
 // in the LDS the int32 slots took.  Same output and irregular-input flags as k_rs_merge.
-template <typename V>
+// NARROW (values restores with at most 256 quantValues): byte slots and a 256-entry table, 26-27 KB
+// of LDS instead of 37-41 KB, so 5-6 workgroups per CU hold ranges in flight instead of 3-4.
+template <typename V, bool NARROW = false>
 __global__ __launch_bounds__(kRsThreads) void k_rs_merge_pf(const int32_t* __restrict__ gk,
                                                             const int32_t* __restrict__ gb,
                                                             const SpGroups* __restrict__ gp,
@@ -4564,8 +4566,9 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_merge_pf(const int32_t* __res
                                                             RsInfo* __restrict__ info, int32_t* __restrict__ keys_out,
                                                             V* __restrict__ out, const double* __restrict__ qv, int nq) {
     constexpr bool kBins = std::is_same<V, int32_t>::value;  // int32 bins out: any table value
-    constexpr int kLut = kBins ? 1 : kRsLut;
-    using ST = typename std::conditional<kBins, int32_t, uint16_t>::type;
+    static_assert(!(kBins && NARROW), "narrow slots hold quantValues indices only");
+    constexpr int kLut = kBins ? 1 : NARROW ? 256 : kRsLut;
+    using ST = typename std::conditional<kBins, int32_t, typename std::conditional<NARROW, uint8_t, uint16_t>::type>::type;
     __shared__ uint32_t bm[kRsWords];
     __shared__ ST slot[kRsRange];
     __shared__ uint16_t ord[kRsRange];  // the range's set offsets in key order
@@ -4771,7 +4774,24 @@ hipError_t launch_rs_merge(hipStream_t st, const int32_t* gk, const int32_t* gb,
     if (form(SKML_FORM_RS_ROUNDS) == 2) SKML_RS_LAUNCH(k_rs_merge);
     else
 #endif
-    SKML_RS_LAUNCH(k_rs_merge_pf);
+#ifndef SKML_RS_NARROW
+#define SKML_RS_NARROW 1  // A/B builds: 0 keeps 16-bit slots for every values restore
+#endif
+    if (SKML_RS_NARROW && vkind != 0 && nq >= 1 && nq <= 256) {
+        // the grid is what the CUs hold of the narrow form (5-6 per CU), fewer for small inputs
+        static const int res_f = resident_blocks(k_rs_merge_pf<float, true>, kRsThreads);
+        static const int res_d = resident_blocks(k_rs_merge_pf<double, true>, kRsThreads);
+        const int res = vkind == 1 ? res_f : res_d;
+        const unsigned g2 = (unsigned)std::min<int64_t>(std::max<int64_t>(sp_tiles(n, 4096), 1), res > 0 ? res : 1024);
+        if (vkind == 1)
+            hipLaunchKernelGGL((k_rs_merge_pf<float, true>), dim3(g2), dim3(kRsThreads), 0, st, gk, gb, gp, bounds, info,
+                               keys_out, static_cast<float*>(out), qv, nq);
+        else
+            hipLaunchKernelGGL((k_rs_merge_pf<double, true>), dim3(g2), dim3(kRsThreads), 0, st, gk, gb, gp, bounds, info,
+                               keys_out, static_cast<double*>(out), qv, nq);
+    } else {
+        SKML_RS_LAUNCH(k_rs_merge_pf);
+    }
 #undef SKML_RS_LAUNCH
     return hipGetLastError();
 }
