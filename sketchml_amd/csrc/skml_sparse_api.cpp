@@ -533,7 +533,6 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const void* vals, bool f64, int6
     init.col_ratio = p->col_ratio;
     for (int g = 0; g < G; g++) pick_hashes(p->hash_seed + g, rows, init.hash_ids[g]);
     SP_TRY(launch_sp_plan_edges(st, s->qpayload, init, s->g_dev));
-    SP_TRY(launch_sp_qvalues(st, s->qpayload, s->qv_dev));
     const int64_t tiles = sp_tiles(nnz, kSpTile);
     uint64_t* tc = scratch<uint64_t>(c, kSlotTiles, (size_t)(tiles + 1) * G);
     if (!tc) return bail(sfail(SKML_E_OOM, "tile counts"));
@@ -575,6 +574,8 @@ int encode_kv(skml_ctx* c, const int32_t* keys, const void* vals, bool f64, int6
     }
     if (int e = encode_delta_device(c, ds, s->g_dev, gk, need, nnz, hist, err, s->flag_words, s->delta_words))
         return bail(e);
+    // quantValues on the device (only restores read them): on the side chain, off the critical path
+    SP_TRY(launch_sp_qvalues(ds, s->qpayload, s->qv_dev));
     if (side) SP_TRY(hipEventRecord(ev_join, side));
     SP_TRY(launch_scan_cols(st, bucket, nbuckets, 1));
     SP_TRY(launch_mm_scatter(st, gk, gb, nnz, s->g_dev, bucket, cursor, nbuckets, pairs, cellbuf, tile_off));
