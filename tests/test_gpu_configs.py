@@ -189,6 +189,50 @@ def test_c4_eight_buckets_batch_rccl_decode_sum(gpu):
     assert np.array_equal(out.cpu().numpy(), (want * (1.0 / P)).astype(np.float32))
 
 
+def test_batch_encode_fresh_side_lane_on_recycled_memory(gpu):
+    """Regression for the batched encode's side lane: a fresh context's workspace (its fused
+    summary's arrival counter) must be zeroed on its own stream -- zeroed on the null stream, which
+    the side lane's non-blocking stream does not wait for, the summary could be skipped and a
+    payload left without a header.  Device memory is filled with 0xFF and released to HIP first, so
+    the new workspaces are likely to reuse it; every batched payload must carry a finished header
+    and equal the same bucket encoded alone on the shared context, byte for byte.  The race is
+    timing-dependent: a build with the null-stream zeroing also passed this test on one box
+    (DESIGN.md §0); it failed 3 of 5 full-suite runs through the C4 test above."""
+    from sketchml_amd.context import Context
+    L = _lib()
+    P, n = 4, 2**20 + 512
+    xs = [torch.from_numpy(_normal(n, 30 + r)).cuda() for r in range(P)]
+    nb = L.lib.skml_dense_payload_bytes(n, 256)
+    p = _params(256, 6)
+    shared = gpu.get_context()
+    want = []
+    for r in range(P):
+        pl = gpu.alloc_aligned(nb, "cuda")
+        pl.zero_()  # the payload's alignment padding is not written: zero it on both sides
+        assert L.lib.skml_dense_encode_f32(shared.handle, C.c_void_p(xs[r].data_ptr()), n, C.byref(p),
+                                           C.c_void_p(pl.data_ptr()), nb) == 0, L.last_error()
+        want.append(pl)
+    torch.cuda.synchronize()
+    for _ in range(3):
+        junk = torch.full((256 << 20,), 0xFF, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        del junk
+        torch.cuda.empty_cache()
+        ctx = Context(0)
+        pls = [gpu.alloc_aligned(nb, "cuda").zero_() for _ in range(P)]
+        ptrs = (C.c_void_p * P)(*[x.data_ptr() for x in xs])
+        pptr = (C.c_void_p * P)(*[q.data_ptr() for q in pls])
+        ns = (C.c_int64 * P)(*([n] * P))
+        caps = (C.c_size_t * P)(*([nb] * P))
+        assert L.lib.skml_dense_encode_batch_f32(ctx.handle, P, ptrs, ns, C.byref(p), pptr, caps) == 0, L.last_error()
+        torch.cuda.synchronize()
+        for r in range(P):
+            st, h, _ = _header(gpu, pls[r])
+            assert st == 0 and h.n == n, f"bucket {r} of a fresh context's batch has no finished header"
+            assert torch.equal(pls[r], want[r]), f"bucket {r} of a fresh context's batch differs"
+        del ctx
+
+
 def test_c5_shard_two_bit_codes(gpu):
     """One C5 shard: 2^27 values (seed 5), B = 4 -> 2-bit codes, against the oracle."""
     L = _lib()
